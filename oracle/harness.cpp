@@ -1,0 +1,478 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY (see raft_ref.h header comment).
+// Lockstep multi-group harness: node.go step order + quiesce.go + a
+// deterministic network (DESIGN.md §Round semantics).
+#include "harness.h"
+
+#include <algorithm>
+#include <cstring>
+#include <thread>
+
+namespace orc {
+
+// ------------------------------------------------------------ workload / faults
+// Restated independently on device (dragonboat_amd/csrc/workload.h).
+u64 wl_payload_lo(u64 seed, u64 cid, u64 round) {
+  return splitmix64(seed ^ (cid * 0xD1B54A32D192ED03ULL) ^ (round << 1));
+}
+
+bool wl_group_active(const HarnessConfig& c, u64 cid) {
+  if (c.wl_active_mod <= 1) return true;
+  return splitmix64(c.seed ^ 0xA5A5A5A5A5A5A5A5ULL ^ (cid * 0x9E3779B97F4A7C15ULL)) %
+             c.wl_active_mod == 0;
+}
+
+int wl_input(const HarnessConfig& c, u64 cid, u32 round) {
+  if (!c.wl_enabled) return 0;
+  if (round < c.wl_start_round) return 0;
+  if (c.wl_stop_round != 0 && round >= c.wl_stop_round) return 0;
+  if (!wl_group_active(c, cid)) return 0;
+  if (c.wl_read_permille == 0) return 1;
+  u64 u = splitmix64(c.seed ^ (cid * 0xC2B2AE3D27D4EB4FULL) ^ ((u64)round << 20)) % 1000;
+  return u < c.wl_read_permille ? 2 : 1;
+}
+
+bool iso_selected(const HarnessConfig& c, u64 cid, u32 epoch) {
+  if (c.iso_mod <= 1) return true;
+  return splitmix64(c.seed ^ (cid * 0x94D049BB133111EBULL) ^ ((u64)epoch << 40)) %
+             c.iso_mod == 0;
+}
+
+// ------------------------------------------------------------ quiesce.go
+struct QuiesceManager {  // quiesce.go:23-33
+  u64 tick = 0, electionTick = 0, quiescedSince = 0, noActivitySince = 0,
+      exitQuiesceTick = 0;
+  bool enabled = false;
+  bool newFlag = false;
+
+  bool newQuiesceState() {  // quiesce.go:39-41
+    bool v = newFlag;
+    newFlag = false;
+    return v;
+  }
+  u64 threshold() const { return electionTick * 10; }  // quiesce.go:84-86
+  bool quiesced() const { return enabled && quiescedSince > 0; }  // quiesce.go:57-62
+  bool newToQuiesce() const {  // quiesce.go:88-93
+    if (!quiesced()) return false;
+    return tick - quiescedSince < electionTick;
+  }
+  bool justExitedQuiesce() const {  // quiesce.go:95-100
+    if (quiesced()) return false;
+    return tick - exitQuiesceTick < threshold();
+  }
+  void enterQuiesce() {  // quiesce.go:112-117
+    quiescedSince = tick;
+    noActivitySince = tick;
+    newFlag = true;
+  }
+  void exitQuiesce() {  // quiesce.go:119-122
+    quiescedSince = 0;
+    exitQuiesceTick = tick;
+  }
+  u64 increaseQuiesceTick() {  // quiesce.go:43-55
+    if (!enabled) return 0;
+    u64 th = threshold();
+    tick++;
+    if (!quiesced()) {
+      if (tick - noActivitySince > th) enterQuiesce();
+    }
+    return tick;
+  }
+  void recordActivity(int t) {  // quiesce.go:64-82
+    if (!enabled) return;
+    if (t == Heartbeat || t == HeartbeatResp) {
+      if (!quiesced()) return;
+      if (newToQuiesce()) return;
+    }
+    noActivitySince = tick;
+    if (quiesced()) exitQuiesce();
+  }
+  void tryEnterQuiesce() {  // quiesce.go:102-110
+    if (justExitedQuiesce()) return;
+    if (!quiesced()) enterQuiesce();
+  }
+};
+
+// ------------------------------------------------------------ node
+struct Node {
+  TestLogDB db;
+  Peer* peer = nullptr;
+  QuiesceManager q;
+  u64 confirmedIndex = 0;
+  u64 smAppliedIndex = 0;
+  u64 tickCount = 0;
+  u64 digest = 0;
+  std::vector<Message> in[8];   // this round's inbox, per sender slot (stream order)
+  std::vector<Message> nxt[8];  // next round's inbox
+  ~Node() { delete peer; }
+};
+
+struct Group {
+  u64 cid = 0;
+  std::vector<Node*> nodes;
+  u32 iso_mask = 0;
+  u32 iso_until = 0;
+  ~Group() {
+    for (auto* n : nodes) delete n;
+  }
+};
+
+struct Harness {
+  HarnessConfig cfg;
+  std::vector<Group*> groups;
+  u32 round = 0;
+  u64 counters[HC_NUM] = {0};
+  ~Harness() {
+    for (auto* g : groups) delete g;
+  }
+};
+
+static u64 cmd_word(const std::string& s, int w) {
+  u64 x = 0;
+  for (int i = 0; i < 8; i++) {
+    size_t p = (size_t)w * 8 + i;
+    if (p < s.size()) x |= (u64)(uint8_t)s[p] << (8 * i);
+  }
+  return x;
+}
+
+static u64 hash_entry(u64 h, const Entry& e) {
+  h = hfold(h, e.index);
+  h = hfold(h, e.term);
+  h = hfold(h, (u64)e.type | ((u64)e.cmd.size() << 32));
+  h = hfold(h, cmd_word(e.cmd, 0));
+  h = hfold(h, cmd_word(e.cmd, 1));
+  return h;
+}
+
+static u64 hash_message(u64 h, const Message& m) {
+  h = hfold(h, (u64)m.type | ((u64)(m.reject ? 1 : 0) << 8) | ((u64)m.entries.size() << 16));
+  h = hfold(h, m.to);
+  h = hfold(h, m.from);
+  h = hfold(h, m.term);
+  h = hfold(h, m.log_term);
+  h = hfold(h, m.log_index);
+  h = hfold(h, m.commit);
+  h = hfold(h, m.hint);
+  h = hfold(h, m.hint_high);
+  for (auto& e : m.entries) h = hash_entry(h, e);
+  return h;
+}
+
+static std::string payload_cmd(u64 seed, u64 cid, u64 round) {
+  u64 lo = wl_payload_lo(seed, cid, round);
+  u64 hi = splitmix64(lo);
+  std::string s(16, '\0');
+  for (int i = 0; i < 8; i++) {
+    s[i] = (char)((lo >> (8 * i)) & 0xff);
+    s[8 + i] = (char)((hi >> (8 * i)) & 0xff);
+  }
+  return s;
+}
+
+Harness* harness_create(const HarnessConfig& cfg) {
+  if (cfg.n_replicas < 1 || cfg.n_replicas > 8) panicf("n_replicas must be 1..8");
+  Harness* h = new Harness();
+  h->cfg = cfg;
+  std::vector<std::pair<u64, std::string>> addrs;
+  for (u32 k = 0; k < cfg.n_replicas; k++)
+    addrs.push_back({k + 1, "node-" + std::to_string(k + 1)});
+  for (u64 g = 0; g < cfg.n_groups; g++) {
+    Group* gr = new Group();
+    gr->cid = cfg.cid_base + g;
+    for (u32 k = 0; k < cfg.n_replicas; k++) {
+      Node* n = new Node();
+      Config c;
+      c.nodeID = k + 1;
+      c.clusterID = gr->cid;
+      c.electionRTT = cfg.election_rtt;
+      c.heartbeatRTT = cfg.heartbeat_rtt;
+      c.checkQuorum = cfg.check_quorum;
+      c.quiesce = cfg.quiesce;
+      c.rngSeed = cfg.seed;
+      c.maxEntrySize = cfg.max_entry_size;
+      n->peer = Peer::Launch(c, &n->db, addrs, true, true);  // node.go:280-292
+      n->q.enabled = cfg.quiesce;
+      n->q.electionTick = cfg.election_rtt * 2;  // node.go:165
+      gr->nodes.push_back(n);
+    }
+    h->groups.push_back(gr);
+  }
+  return h;
+}
+
+void harness_destroy(Harness* h) { delete h; }
+
+// One stepNode + update processing for replica k of group gr in round r.
+static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, u64* ctr) {
+  Node* nd = gr->nodes[k];
+  Peer* p = nd->peer;
+  Raft* R = p->raft;
+  const u32 n = cfg.n_replicas;
+  ctr[HC_STEPS]++;
+  // handleEvents: updateBatchedLastApplied (node.go:1002-1006, 1032)
+  p->NotifyRaftLastApplied(nd->smAppliedIndex);
+  // client input of this round goes to replicas that lead at round start
+  int inp = R->state == Leader ? wl_input(cfg, gr->cid, r) : 0;
+  const u64 committed0 = R->log.committed;
+  const u64 campaigns0 = R->events.campaignLaunched;
+  // handleReadIndexRequests (node.go:1108-1118)
+  u64 readReq = 0;
+  if (inp == 2) {
+    nd->q.recordActivity(ReadIndex);
+    readReq = 1;
+    ctr[HC_READS]++;
+  }
+  // handleReceivedMessages (node.go:1171-1205); one LocalTick per round
+  u64 ltCount = 1;
+  for (u32 s = 0; s < n; s++) {
+    for (auto& m : nd->in[s]) {
+      ctr[HC_MSG_IN]++;
+      ctr[HC_ENT_IN] += m.entries.size();
+      if (m.type == Quiesce) {  // handleMessage, node.go:1207-1220
+        nd->q.tryEnterQuiesce();
+        continue;
+      }
+      // tryRecordNodeActivity, node.go:1161-1169
+      if ((m.type == Heartbeat || m.type == HeartbeatResp) && m.hint > 0)
+        nd->q.recordActivity(ReadIndex);
+      else
+        nd->q.recordActivity(m.type);
+      p->Handle(m);
+    }
+    nd->in[s].clear();
+  }
+  if (readReq > 0) {  // batchedReadIndex, node.go:1379-1382
+    SystemCtx ctx;
+    ctx.low = ((u64)(r + 1) << 32) | (u64)(k + 1);
+    ctx.high = gr->cid + 1;
+    p->ReadIndex(ctx);
+  }
+  // handleLocalTickMessage (node.go:1152-1159) → node.tick (1384-1399)
+  if (ltCount > cfg.election_rtt) ltCount = cfg.election_rtt;
+  for (u64 i = 0; i < ltCount; i++) {
+    nd->tickCount++;
+    nd->q.increaseQuiesceTick();
+    if (nd->q.quiesced()) {
+      p->QuiescedTick();
+      ctr[HC_QUIESCED_TICKS]++;
+    } else {
+      p->Tick();
+      ctr[HC_ACTIVE_TICKS]++;
+    }
+  }
+  // handleProposals (node.go:1091-1106)
+  if (inp == 1) {
+    std::vector<Entry> ents(1);
+    ents[0].type = ApplicationEntry;
+    ents[0].cmd = payload_cmd(cfg.seed, gr->cid, r);
+    p->ProposeEntries(ents);
+    ctr[HC_PROPOSALS]++;
+  }
+  // stepNode: quiesce state (node.go:1021-1023)
+  const bool sendQ = nd->q.newQuiesceState();
+  // getUpdate (node.go:907-923)
+  u64 msgHash = 0, nMsgs = 0, rtrHash = 0, applyHash = 0, dropHash = 0;
+  auto deliver = [&](const Message& m) {
+    if (m.to < 1 || m.to > n) return;  // not a member of this lockstep group
+    u32 d = (u32)(m.to - 1);
+    if (((gr->iso_mask >> k) & 1) || ((gr->iso_mask >> d) & 1)) {
+      ctr[HC_MSG_DROPPED]++;
+      return;
+    }
+    ctr[HC_MSG_OUT]++;
+    ctr[HC_ENT_OUT] += m.entries.size();
+    gr->nodes[d]->nxt[k].push_back(m);
+  };
+  if (sendQ) {  // sendEnterQuiesceMessages, node.go:873-886
+    for (u32 d = 0; d < n; d++) {
+      if (d == k) continue;
+      Message m;
+      m.type = Quiesce;
+      m.from = k + 1;
+      m.to = d + 1;
+      m.cluster_id = gr->cid;
+      deliver(m);
+    }
+  }
+  if (p->HasUpdate(true) || nd->confirmedIndex != nd->smAppliedIndex) {
+    Update ud = p->GetUpdate(true, nd->smAppliedIndex);
+    nd->confirmedIndex = nd->smAppliedIndex;
+    for (auto& m : ud.messages) {
+      msgHash = hash_message(msgHash, m);
+      nMsgs++;
+    }
+    // applyRaftUpdates: the harness state machine applies immediately
+    for (auto& e : ud.committed_entries) applyHash = hash_entry(applyHash, e);
+    ctr[HC_ENT_APPLIED] += ud.committed_entries.size();
+    if (!ud.committed_entries.empty()) nd->smAppliedIndex = ud.committed_entries.back().index;
+    // sendReplicateMessages (node.go:897-905) then, after persistence,
+    // sendMessages (node.go:888-895)
+    for (auto& m : ud.messages)
+      if (m.type == Replicate) deliver(m);
+    // processReadyToRead
+    for (auto& rr : ud.ready_to_reads) {
+      rtrHash = hfold(rtrHash, rr.index);
+      rtrHash = hfold(rtrHash, rr.ctx.low);
+      rtrHash = hfold(rtrHash, rr.ctx.high);
+    }
+    ctr[HC_READS_CONFIRMED] += ud.ready_to_reads.size();
+    for (auto& e : ud.dropped_entries) dropHash = hash_entry(dropHash, e);
+    for (auto& c : ud.dropped_read_indexes) {
+      dropHash = hfold(dropHash, c.low);
+      dropHash = hfold(dropHash, c.high);
+    }
+    ctr[HC_DROPPED_PROPOSALS] += ud.dropped_entries.size();
+    ctr[HC_DROPPED_READS] += ud.dropped_read_indexes.size();
+    // SaveRaftState → logreader.Append (node.go:975-977)
+    nd->db.Append(ud.entries_to_save);
+    if (!isEmptyState(ud.state)) nd->db.SetState(ud.state);
+    ctr[HC_ENT_SAVED] += ud.entries_to_save.size();
+    for (auto& m : ud.messages)
+      if (m.type != Replicate) deliver(m);
+    p->Commit(ud);  // commitRaftUpdate
+  }
+  ctr[HC_CAMPAIGNS] += R->events.campaignLaunched - campaigns0;
+  if (R->state == Leader) {
+    ctr[HC_COMMITTED] += R->log.committed - committed0;
+    ctr[HC_LEADER_STEPS]++;
+  }
+  if (cfg.trace) {
+    u64 d = nd->digest;
+    d = hfold(d, r);
+    d = hfold(d, (u64)R->state | ((u64)(nd->q.quiesced() ? 1 : 0) << 8) |
+                     ((u64)(sendQ ? 1 : 0) << 9) | ((u64)(R->quiesce ? 1 : 0) << 10));
+    d = hfold(d, R->term);
+    d = hfold(d, R->vote);
+    d = hfold(d, R->leaderID);
+    d = hfold(d, R->log.committed);
+    d = hfold(d, R->log.lastIndex());
+    d = hfold(d, R->log.processed);
+    d = hfold(d, R->electionTick | (R->heartbeatTick << 32));
+    d = hfold(d, R->randomizedElectionTimeout);
+    d = hfold(d, msgHash);
+    d = hfold(d, nMsgs);
+    d = hfold(d, rtrHash);
+    d = hfold(d, applyHash);
+    d = hfold(d, dropHash);
+    nd->digest = d;
+  }
+}
+
+static void run_group_round(const HarnessConfig& cfg, Group* gr, u32 r, u64* ctr) {
+  // fault schedule: isolation decided from round-start roles
+  if (gr->iso_mask && r >= gr->iso_until) gr->iso_mask = 0;
+  if (cfg.iso_period && r > 0 && r % cfg.iso_period == 0 &&
+      iso_selected(cfg, gr->cid, r / cfg.iso_period)) {
+    u32 mask = 0;
+    for (u32 k = 0; k < cfg.n_replicas; k++)
+      if (gr->nodes[k]->peer->raft->state == Leader) mask |= 1u << k;
+    if (mask) {
+      gr->iso_mask = mask;
+      gr->iso_until = r + cfg.iso_len;
+    }
+  }
+  for (u32 k = 0; k < cfg.n_replicas; k++) step_replica(cfg, gr, k, r, ctr);
+  for (u32 k = 0; k < cfg.n_replicas; k++) {
+    Node* nd = gr->nodes[k];
+    for (u32 s = 0; s < cfg.n_replicas; s++) {
+      nd->in[s].swap(nd->nxt[s]);
+      nd->nxt[s].clear();
+    }
+  }
+}
+
+void harness_run(Harness* h, u32 rounds) {
+  const u32 T = std::max<u32>(1, h->cfg.threads);
+  const u32 r0 = h->round;
+  std::vector<std::vector<u64>> ctrs(T, std::vector<u64>(HC_NUM, 0));
+  auto worker = [&](u32 t) {
+    for (u32 r = r0; r < r0 + rounds; r++)
+      for (u64 g = t; g < h->groups.size(); g += T)
+        run_group_round(h->cfg, h->groups[g], r, ctrs[t].data());
+  };
+  if (T == 1) {
+    worker(0);
+  } else {
+    std::vector<std::thread> th;
+    std::vector<std::exception_ptr> errs(T);
+    for (u32 t = 0; t < T; t++)
+      th.emplace_back([&, t]() {
+        try {
+          worker(t);
+        } catch (...) {
+          errs[t] = std::current_exception();
+        }
+      });
+    for (auto& x : th) x.join();
+    for (auto& e : errs)
+      if (e) std::rethrow_exception(e);
+  }
+  for (u32 t = 0; t < T; t++)
+    for (int i = 0; i < HC_NUM; i++) h->counters[i] += ctrs[t][i];
+  h->round += rounds;
+}
+
+u32 harness_round(const Harness* h) { return h->round; }
+
+void harness_views(const Harness* h, ReplicaView* out) {
+  const u32 n = h->cfg.n_replicas;
+  for (u64 g = 0; g < h->groups.size(); g++) {
+    for (u32 k = 0; k < n; k++) {
+      const Node* nd = h->groups[g]->nodes[k];
+      const Raft* R = nd->peer->raft;
+      ReplicaView& v = out[g * n + k];
+      std::memset(&v, 0, sizeof(v));
+      v.term = R->term;
+      v.vote = R->vote;
+      v.leader_id = R->leaderID;
+      v.committed = R->log.committed;
+      v.last_index = R->log.lastIndex();
+      v.processed = R->log.processed;
+      v.saved_to = R->log.inmem.savedTo;
+      v.digest = nd->digest;
+      v.role = (u32)R->state;
+      v.election_tick = (u32)R->electionTick;
+      v.heartbeat_tick = (u32)R->heartbeatTick;
+      v.rand_election_timeout = (u32)R->randomizedElectionTimeout;
+      v.q_tick = (u32)nd->q.tick;
+      v.q_quiesced_since = (u32)nd->q.quiescedSince;
+      v.q_no_activity_since = (u32)nd->q.noActivitySince;
+      v.q_exit_quiesce_tick = (u32)nd->q.exitQuiesceTick;
+      v.raft_quiesce = R->quiesce ? 1 : 0;
+      v.rq_count = (u32)R->readIndex.queue.size();
+      u32 resp = 0, granted = 0;
+      for (auto& kv : R->votes) {
+        if (kv.first >= 1 && kv.first <= 8) {
+          resp |= 1u << (kv.first - 1);
+          if (kv.second) granted |= 1u << (kv.first - 1);
+        }
+      }
+      v.votes_resp = resp;
+      v.votes_granted = granted;
+      if (R->state == Leader) {
+        for (auto& kv : R->remotes) {
+          if (kv.first >= 1 && kv.first <= 8) {
+            u32 s = (u32)(kv.first - 1);
+            v.match[s] = kv.second.match;
+            v.next[s] = kv.second.next;
+            v.rstate[s] = (u32)kv.second.state;
+            v.ractive[s] = kv.second.active ? 1 : 0;
+          }
+        }
+      }
+    }
+  }
+}
+
+void harness_counters(const Harness* h, u64* out) {
+  for (int i = 0; i < HC_NUM; i++) out[i] = h->counters[i];
+}
+
+u64 harness_log_term(const Harness* h, u64 g, u32 k, u64 index) {
+  const Raft* R = h->groups[g]->nodes[k]->peer->raft;
+  u64 t = 0;
+  if (R->log.term(index, &t) != ErrOK) return 0;
+  return t;
+}
+
+}  // namespace orc

@@ -1,0 +1,91 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY (see raft_ref.h header comment).
+//
+// Deterministic lockstep harness around the raft restatement: it runs the
+// dragonboat node step loop (node.go:1016-1067 stepNode/handleEvents,
+// 1171-1205 handleReceivedMessages, 1384-1399 tick, quiesce.go) for many
+// independent groups, delivering every message emitted in round r at round
+// r+1, exactly as node_test.go:270-401 (step/stepNodes) drive a cluster.
+// The MI355X engine implements the same round semantics on device; both are
+// specified in DESIGN.md §Round semantics and must agree bit for bit.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "raft_ref.h"
+
+namespace orc {
+
+// Counter slots, shared numbering with the engine (include/rbe.h RBE_CTR_*).
+enum HarnessCounter {
+  HC_STEPS = 0,           // replica-steps with >=1 input (every replica ticks every round)
+  HC_COMMITTED = 1,       // leader commit advances (entries committed, once per group)
+  HC_MSG_IN = 2,          // messages handled from the inbox (incl. Quiesce)
+  HC_MSG_OUT = 3,         // messages delivered to the network (after drops)
+  HC_ENT_IN = 4,          // entries carried by handled messages
+  HC_ENT_OUT = 5,         // entries carried by delivered messages
+  HC_READS_CONFIRMED = 6, // ReadyToRead records produced
+  HC_PROPOSALS = 7,       // proposals injected by the workload
+  HC_READS = 8,           // ReadIndex requests injected by the workload
+  HC_QUIESCED_TICKS = 9,  // QuiescedTick calls
+  HC_ACTIVE_TICKS = 10,   // Tick calls
+  HC_CAMPAIGNS = 11,      // campaign() calls
+  HC_ENT_SAVED = 12,      // entries in EntriesToSave
+  HC_ENT_APPLIED = 13,    // entries in CommittedEntries
+  HC_MSG_DROPPED = 14,    // messages dropped by the fault schedule
+  HC_DROPPED_PROPOSALS = 15,
+  HC_DROPPED_READS = 16,
+  HC_LEADER_STEPS = 17,   // replica-steps that end as leader
+  HC_NUM = 24
+};
+
+struct HarnessConfig {
+  u64 n_groups = 1;
+  u32 n_replicas = 3;
+  u64 cid_base = 1;            // cluster id of group g is cid_base + g
+  u64 election_rtt = 10;
+  u64 heartbeat_rtt = 1;
+  bool check_quorum = false;
+  bool quiesce = false;
+  u64 seed = 0x5EEDD8A6ULL;
+  u64 max_entry_size = DefaultMaxEntrySize;
+  // workload
+  u32 wl_start_round = 0;      // no client input before this round
+  u32 wl_stop_round = 0;       // no client input from this round on (0 = never stop)
+  u32 wl_active_mod = 1;       // group active iff mix(seed,cid) % mod == 0
+  u32 wl_read_permille = 0;    // per active group per round: read w.p. p/1000 else propose
+  u32 wl_enabled = 0;          // 0: no client input at all
+  // fault schedule: isolate the leader(s) of selected groups
+  u32 iso_period = 0;          // 0 = no faults
+  u32 iso_len = 0;
+  u32 iso_mod = 10;
+  // tracing
+  u32 trace = 1;               // compute per-replica digests
+  u32 threads = 1;             // worker threads (groups partitioned cid % T)
+};
+
+struct ReplicaView {  // mirrors rbe_replica_view in include/rbe.h
+  u64 term, vote, leader_id, committed, last_index, processed, saved_to, digest;
+  u32 role, election_tick, heartbeat_tick, rand_election_timeout;
+  u32 q_tick, q_quiesced_since, q_no_activity_since, q_exit_quiesce_tick;
+  u32 raft_quiesce, rq_count, votes_resp, votes_granted;
+  u64 match[8], next[8];
+  u32 rstate[8], ractive[8];
+};
+
+struct Harness;
+Harness* harness_create(const HarnessConfig& cfg);
+void harness_destroy(Harness* h);
+void harness_run(Harness* h, u32 rounds);
+u32 harness_round(const Harness* h);
+void harness_views(const Harness* h, ReplicaView* out);  // n_groups*n_replicas views
+void harness_counters(const Harness* h, u64* out);       // HC_NUM counters
+u64 harness_log_term(const Harness* h, u64 g, u32 k, u64 index);  // term of entry (0 if absent)
+
+// shared helpers (restated independently in the engine)
+u64 wl_payload_lo(u64 seed, u64 cid, u64 round);
+bool wl_group_active(const HarnessConfig& c, u64 cid);
+int wl_input(const HarnessConfig& c, u64 cid, u32 round);  // 0 none, 1 propose, 2 read
+bool iso_selected(const HarnessConfig& c, u64 cid, u32 epoch);
+inline u64 hfold(u64 h, u64 x) { return splitmix64(h ^ x); }
+
+}  // namespace orc
