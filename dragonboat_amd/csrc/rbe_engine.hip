@@ -1,0 +1,637 @@
+// MI355X batched Raft step engine: kernels, device memory, C ABI (include/rbe.h).
+//
+// Round pipeline on one HIP stream:
+//   [k_isolate  — only on fault-schedule epoch rounds, one lane per group]
+//   k_step<N>   — one lane per replica: inbox → protocol → outbox + Update
+// Per-lane event counters are reduced across the 64-lane wavefront with
+// cross-lane shuffles and added to 64-bit device counters by one lane.
+// rbe_run replays a captured HIP graph of K step launches plus a round
+// advance when no per-round host work is needed.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/rbe.h"
+#include "rbe_step.h"
+
+using namespace rbe;
+
+#define HIP_IGNORE(x) ((void)(x))
+#define HIP_OK(x)                                                      \
+  do {                                                                 \
+    hipError_t err__ = (x);                                            \
+    if (err__ != hipSuccess) {                                         \
+      fprintf(stderr, "rbe: %s failed: %s\n", #x, hipGetErrorString(err__)); \
+      return RBE_E_HIP;                                                \
+    }                                                                  \
+  } while (0)
+
+static constexpr int kBlock = 256;
+
+// ------------------------------------------------------------------ kernels
+__device__ __forceinline__ u32 wave_sum(u32 v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_step(Planes P, Params C, const u32* round_ptr,
+                                                 u32 round_add) {
+  const u32 round = (round_ptr ? *round_ptr : 0u) + round_add;
+  const u64 r = (u64)blockIdx.x * kBlock + threadIdx.x;
+  StepCounters c;
+#pragma unroll
+  for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
+  if (r < C.n_rep) step_replica<N>(P, C, r, round, c);
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < C_NUM; i++) {
+    // skip the reduction when no lane of the wave saw the event
+    if (__ballot(c.v[i] != 0) == 0ull) continue;
+    const u32 s = wave_sum(c.v[i]);
+    if (lane == 0) atomicAdd((unsigned long long*)&P.counters[i], (unsigned long long)s);
+  }
+}
+
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_launch(Planes P, Params C) {
+  const u64 r = (u64)blockIdx.x * kBlock + threadIdx.x;
+  if (r < C.n_rep) launch_replica<N>(P, C, r);
+}
+
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_isolate(Planes P, Params C, u32 round) {
+  const u64 g = (u64)blockIdx.x * kBlock + threadIdx.x;
+  if (g < C.n_groups) iso_group<N>(P, C, g, round);
+}
+
+__global__ void k_advance(u32* round_ptr, u32 k) { *round_ptr += k; }
+
+// ------------------------------------------------------------------ engine
+struct rbe_engine {
+  rbe_config cfg;
+  Params C;
+  Planes P;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  u32 round = 0;
+  u32* d_round = nullptr;
+  std::vector<void*> allocs;
+  hipGraphExec_t graph = nullptr;
+  u32 graph_rounds = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+static u64 bytes_of(const Params& C, u64* parts) {
+  const u64 N = C.n, G = C.n_groups, R = C.n_rep;
+  u64 p[16] = {
+      R * sizeof(Hot),
+      R * sizeof(Core),
+      R * N * sizeof(RemoteMN),
+      R * N,
+      R * C.rq_cap * sizeof(ReadReq),
+      (u64)C.ring * R * sizeof(u64),
+      (u64)C.ring * R * sizeof(Body),
+      2 * G * N * N * sizeof(u16),
+      2 * G * N * N * C.maxm * sizeof(Msg),
+      2 * R * C.ecap * sizeof(Ent),
+      G * sizeof(u8),
+      G * sizeof(u32),
+      R * sizeof(Upd),
+      R * C.rtr_cap * sizeof(RTR),
+      R * C.dri_cap * sizeof(DropRI),
+      R * sizeof(ExtIn),
+  };
+  u64 t = 0;
+  for (int i = 0; i < 16; i++) {
+    if (parts) parts[i] = p[i];
+    t += (p[i] + 255) & ~255ull;
+  }
+  return t + 256;
+}
+
+static int make_params(const rbe_config* cfg, Params* out) {
+  if (!cfg || cfg->abi_version != RBE_ABI_VERSION) return RBE_E_INVALID;
+  Params C;
+  memset(&C, 0, sizeof(C));
+  C.n = cfg->n_replicas;
+  if (C.n != 1 && C.n != 3 && C.n != 5) return RBE_E_INVALID;
+  if (cfg->n_groups == 0) return RBE_E_INVALID;
+  C.n_groups = cfg->n_groups;
+  C.n_rep = cfg->n_groups * C.n;
+  C.cid_base = cfg->cid_base ? cfg->cid_base : 1;
+  C.cid_stride = cfg->cid_stride ? cfg->cid_stride : 1;
+  C.seed = cfg->seed;
+  C.max_entry_size = cfg->max_entry_size ? cfg->max_entry_size : (64ull << 20);
+  C.ring = cfg->ring ? cfg->ring : 64;
+  if (C.ring & (C.ring - 1)) return RBE_E_INVALID;
+  if (C.ring < 8) return RBE_E_INVALID;
+  C.rq_cap = cfg->rq_cap ? cfg->rq_cap : 8;
+  if (C.rq_cap > 255) return RBE_E_INVALID;
+  C.maxm = cfg->maxm ? cfg->maxm : 12;
+  if (C.maxm > 127) return RBE_E_INVALID;
+  C.ecap = cfg->ecap ? cfg->ecap : 2 * C.ring;
+  C.rtr_cap = cfg->rtr_cap ? cfg->rtr_cap : 8;
+  C.dri_cap = cfg->dri_cap ? cfg->dri_cap : 8;
+  C.election_rtt = cfg->election_rtt;
+  C.heartbeat_rtt = cfg->heartbeat_rtt;
+  // config.Validate (config/config.go:173-208)
+  if (C.heartbeat_rtt == 0 || C.election_rtt == 0 || C.election_rtt <= 2 * C.heartbeat_rtt)
+    return RBE_E_INVALID;
+  if (C.election_rtt > 30000) return RBE_E_INVALID;  // randomized timeout kept in u16
+  C.check_quorum = cfg->check_quorum;
+  C.quiesce = cfg->quiesce;
+  C.trace = cfg->trace;
+  C.wl_enabled = cfg->wl_enabled;
+  C.wl_start_round = cfg->wl_start_round;
+  C.wl_stop_round = cfg->wl_stop_round;
+  C.wl_active_mod = cfg->wl_active_mod;
+  C.wl_read_permille = cfg->wl_read_permille;
+  C.ext_inputs = cfg->ext_inputs;
+  C.iso_period = cfg->iso_period;
+  C.iso_len = cfg->iso_len;
+  C.iso_mod = cfg->iso_mod;
+  *out = C;
+  return RBE_OK;
+}
+
+template <typename F>
+static int dispatch_n(u32 n, F&& f) {
+  switch (n) {
+    case 1: return f(std::integral_constant<int, 1>());
+    case 3: return f(std::integral_constant<int, 3>());
+    case 5: return f(std::integral_constant<int, 5>());
+    default: return RBE_E_INVALID;
+  }
+}
+
+template <typename T>
+static int d2h(rbe_engine* e, T* dst, const T* src, u64 n) {
+  HIP_OK(hipMemcpyAsync(dst, src, n * sizeof(T), hipMemcpyDeviceToHost, e->stream));
+  return RBE_OK;
+}
+
+static unsigned grid_for(u64 n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+static int launch_step(rbe_engine* e, const u32* round_ptr, u32 round_add) {
+  return dispatch_n(e->C.n, [&](auto NN) {
+    constexpr int N = decltype(NN)::value;
+    hipLaunchKernelGGL(k_step<N>, dim3(grid_for(e->C.n_rep)), dim3(kBlock), 0, e->stream, e->P,
+                       e->C, round_ptr, round_add);
+    HIP_OK(hipGetLastError());
+    return RBE_OK;
+  });
+}
+
+extern "C" {
+
+int rbe_abi_version(void) { return RBE_ABI_VERSION; }
+
+int rbe_footprint(const rbe_config* cfg, uint64_t* bytes) {
+  Params C;
+  int rc = make_params(cfg, &C);
+  if (rc) return rc;
+  *bytes = bytes_of(C, nullptr);
+  return RBE_OK;
+}
+
+int rbe_destroy(rbe_engine* e) {
+  if (!e) return RBE_OK;
+  HIP_IGNORE(hipSetDevice(e->device));
+  if (e->stream) HIP_IGNORE(hipStreamSynchronize(e->stream));
+  if (e->graph) HIP_IGNORE(hipGraphExecDestroy(e->graph));
+  for (void* p : e->allocs) HIP_IGNORE(hipFree(p));
+  if (e->d_round) HIP_IGNORE(hipFree(e->d_round));
+  if (e->ev0) HIP_IGNORE(hipEventDestroy(e->ev0));
+  if (e->ev1) HIP_IGNORE(hipEventDestroy(e->ev1));
+  if (e->stream) HIP_IGNORE(hipStreamDestroy(e->stream));
+  delete e;
+  return RBE_OK;
+}
+
+int rbe_create(const rbe_config* cfg, rbe_engine** out) {
+  if (!out) return RBE_E_INVALID;
+  *out = nullptr;
+  Params C;
+  int rc = make_params(cfg, &C);
+  if (rc) return rc;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RBE_E_NODEV;
+  if (cfg->device < 0 || cfg->device >= ndev) return RBE_E_NODEV;
+  HIP_OK(hipSetDevice(cfg->device));
+  rbe_engine* e = new (std::nothrow) rbe_engine();
+  if (!e) return RBE_E_NOMEM;
+  e->cfg = *cfg;
+  e->C = C;
+  e->device = cfg->device;
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    rbe_destroy(e);
+    return RBE_E_HIP;
+  }
+  HIP_IGNORE(hipEventCreate(&e->ev0));
+  HIP_IGNORE(hipEventCreate(&e->ev1));
+  u64 parts[16];
+  bytes_of(C, parts);
+  void* ptrs[16];
+  for (int i = 0; i < 16; i++) {
+    u64 b = parts[i] ? parts[i] : 16;
+    if (hipMalloc(&ptrs[i], b) != hipSuccess) {
+      for (int j = 0; j < i; j++) e->allocs.push_back(ptrs[j]);
+      rbe_destroy(e);
+      return RBE_E_NOMEM;
+    }
+    e->allocs.push_back(ptrs[i]);
+    if (hipMemsetAsync(ptrs[i], 0, b, e->stream) != hipSuccess) {
+      rbe_destroy(e);
+      return RBE_E_HIP;
+    }
+  }
+  Planes& P = e->P;
+  P.hot = (Hot*)ptrs[0];
+  P.core = (Core*)ptrs[1];
+  P.rem = (RemoteMN*)ptrs[2];
+  P.rem_st = (u8*)ptrs[3];
+  P.rq = (ReadReq*)ptrs[4];
+  P.term_ring = (u64*)ptrs[5];
+  P.pay_ring = (Body*)ptrs[6];
+  u64 cnt_half = C.n_groups * C.n * C.n;
+  P.cnt[0] = (u16*)ptrs[7];
+  P.cnt[1] = P.cnt[0] + cnt_half;
+  u64 msg_half = C.n_groups * C.n * C.n * C.maxm;
+  P.msgs[0] = (Msg*)ptrs[8];
+  P.msgs[1] = P.msgs[0] + msg_half;
+  u64 ar_half = C.n_rep * C.ecap;
+  P.arena[0] = (Ent*)ptrs[9];
+  P.arena[1] = P.arena[0] + ar_half;
+  P.iso_mask = (u8*)ptrs[10];
+  P.iso_until = (u32*)ptrs[11];
+  P.upd = (Upd*)ptrs[12];
+  P.rtr = (RTR*)ptrs[13];
+  P.dri = (DropRI*)ptrs[14];
+  P.ext = (ExtIn*)ptrs[15];
+  if (hipMalloc(&P.counters, C_NUM * sizeof(u64)) != hipSuccess) {
+    rbe_destroy(e);
+    return RBE_E_NOMEM;
+  }
+  e->allocs.push_back(P.counters);
+  HIP_IGNORE(hipMemsetAsync(P.counters, 0, C_NUM * sizeof(u64), e->stream));
+  if (hipMalloc(&e->d_round, sizeof(u32)) != hipSuccess) {
+    rbe_destroy(e);
+    return RBE_E_NOMEM;
+  }
+  HIP_IGNORE(hipMemsetAsync(e->d_round, 0, sizeof(u32), e->stream));
+  rc = dispatch_n(C.n, [&](auto NN) {
+    constexpr int N = decltype(NN)::value;
+    hipLaunchKernelGGL(k_launch<N>, dim3(grid_for(C.n_rep)), dim3(kBlock), 0, e->stream, e->P,
+                       e->C);
+    HIP_OK(hipGetLastError());
+    return RBE_OK;
+  });
+  if (rc || hipStreamSynchronize(e->stream) != hipSuccess) {
+    rbe_destroy(e);
+    return rc ? rc : RBE_E_HIP;
+  }
+  *out = e;
+  return RBE_OK;
+}
+
+static int step_one(rbe_engine* e) {
+  const Params& C = e->C;
+  if (C.iso_period && e->round > 0 && e->round % C.iso_period == 0) {
+    int rc = dispatch_n(C.n, [&](auto NN) {
+      constexpr int N = decltype(NN)::value;
+      hipLaunchKernelGGL(k_isolate<N>, dim3(grid_for(C.n_groups)), dim3(kBlock), 0, e->stream,
+                         e->P, e->C, e->round);
+      HIP_OK(hipGetLastError());
+      return RBE_OK;
+    });
+    if (rc) return rc;
+  }
+  int rc = launch_step(e, nullptr, e->round);
+  if (rc) return rc;
+  e->round++;
+  return RBE_OK;
+}
+
+int rbe_step(rbe_engine* e) {
+  if (!e) return RBE_E_INVALID;
+  HIP_OK(hipSetDevice(e->device));
+  return step_one(e);
+}
+
+// K rounds as one graph: K step launches reading the round from device memory,
+// then one advance of that counter.
+static int run_graph(rbe_engine* e, u32 rounds) {
+  if (e->graph && e->graph_rounds != rounds) {
+    HIP_IGNORE(hipGraphExecDestroy(e->graph));
+    e->graph = nullptr;
+  }
+  if (!e->graph) {
+    HIP_OK(hipMemcpyAsync(e->d_round, &e->round, sizeof(u32), hipMemcpyHostToDevice, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    hipGraph_t g;
+    HIP_OK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+    for (u32 i = 0; i < rounds; i++) {
+      int rc = launch_step(e, e->d_round, i);
+      if (rc) {
+        HIP_IGNORE(hipStreamEndCapture(e->stream, &g));
+        return rc;
+      }
+    }
+    hipLaunchKernelGGL(k_advance, dim3(1), dim3(1), 0, e->stream, e->d_round, rounds);
+    HIP_OK(hipStreamEndCapture(e->stream, &g));
+    HIP_OK(hipGraphInstantiate(&e->graph, g, nullptr, nullptr, 0));
+    HIP_IGNORE(hipGraphDestroy(g));
+    e->graph_rounds = rounds;
+  } else {
+    HIP_OK(hipMemcpyAsync(e->d_round, &e->round, sizeof(u32), hipMemcpyHostToDevice, e->stream));
+  }
+  HIP_OK(hipGraphLaunch(e->graph, e->stream));
+  e->round += rounds;
+  return RBE_OK;
+}
+
+int rbe_run(rbe_engine* e, uint32_t rounds) {
+  if (!e) return RBE_E_INVALID;
+  if (rounds == 0) return RBE_OK;
+  HIP_OK(hipSetDevice(e->device));
+  const bool graphable = e->C.iso_period == 0 && !e->C.ext_inputs && rounds >= 2;
+  if (graphable && getenv("RBE_NO_GRAPH") == nullptr) return run_graph(e, rounds);
+  for (u32 i = 0; i < rounds; i++) {
+    int rc = step_one(e);
+    if (rc) return rc;
+  }
+  return RBE_OK;
+}
+
+int rbe_run_timed(rbe_engine* e, uint32_t rounds, float* ms) {
+  if (!e || !ms) return RBE_E_INVALID;
+  HIP_OK(hipSetDevice(e->device));
+  HIP_OK(hipEventRecord(e->ev0, e->stream));
+  int rc = rbe_run(e, rounds);
+  if (rc) return rc;
+  HIP_OK(hipEventRecord(e->ev1, e->stream));
+  HIP_OK(hipEventSynchronize(e->ev1));
+  HIP_OK(hipEventElapsedTime(ms, e->ev0, e->ev1));
+  return RBE_OK;
+}
+
+int rbe_sync(rbe_engine* e) {
+  if (!e) return RBE_E_INVALID;
+  HIP_OK(hipSetDevice(e->device));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return RBE_OK;
+}
+
+int rbe_round(const rbe_engine* e, uint32_t* round) {
+  if (!e || !round) return RBE_E_INVALID;
+  *round = e->round;
+  return RBE_OK;
+}
+
+int rbe_push_proposals(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint8_t* cmd16,
+                       const uint32_t* cmd_len) {
+  if (!e || !e->C.ext_inputs) return RBE_E_STATE;
+  HIP_OK(hipSetDevice(e->device));
+  for (u64 i = 0; i < n; i++) {
+    if (replica[i] >= e->C.n_rep || cmd_len[i] > 16) return RBE_E_INVALID;
+    ExtIn x;
+    memset(&x, 0, sizeof(x));
+    x.kind = 1;
+    x.len = cmd_len[i];
+    memcpy(&x.lo, cmd16 + 16 * i, 8);
+    memcpy(&x.hi, cmd16 + 16 * i + 8, 8);
+    HIP_OK(hipMemcpyAsync(&e->P.ext[replica[i]], &x, sizeof(x), hipMemcpyHostToDevice, e->stream));
+  }
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return RBE_OK;
+}
+
+int rbe_push_read_index(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint64_t* lo,
+                        const uint64_t* hi) {
+  if (!e || !e->C.ext_inputs) return RBE_E_STATE;
+  HIP_OK(hipSetDevice(e->device));
+  for (u64 i = 0; i < n; i++) {
+    if (replica[i] >= e->C.n_rep || lo[i] == 0) return RBE_E_INVALID;  // requests.go:726
+    ExtIn x;
+    memset(&x, 0, sizeof(x));
+    x.kind = 2;
+    x.ctx_low = lo[i];
+    x.ctx_high = hi[i];
+    HIP_OK(hipMemcpyAsync(&e->P.ext[replica[i]], &x, sizeof(x), hipMemcpyHostToDevice, e->stream));
+  }
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return RBE_OK;
+}
+
+int rbe_get_counters(rbe_engine* e, uint64_t* out) {
+  if (!e || !out) return RBE_E_INVALID;
+  HIP_OK(hipSetDevice(e->device));
+  HIP_OK(hipMemcpyAsync(out, e->P.counters, C_NUM * sizeof(u64), hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return RBE_OK;
+}
+
+int rbe_reset_counters(rbe_engine* e) {
+  if (!e) return RBE_E_INVALID;
+  HIP_OK(hipSetDevice(e->device));
+  HIP_OK(hipMemsetAsync(e->P.counters, 0, C_NUM * sizeof(u64), e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return RBE_OK;
+}
+
+int rbe_get_views(rbe_engine* e, uint64_t first, uint64_t count, rbe_replica_view* out) {
+  if (!e || !out || first + count > e->C.n_rep) return RBE_E_INVALID;
+  HIP_OK(hipSetDevice(e->device));
+  const u32 N = e->C.n;
+  std::vector<Hot> hot(count);
+  std::vector<Core> core(count);
+  std::vector<RemoteMN> rem(count * N);
+  std::vector<u8> rst(count * N);
+  std::vector<Upd> upd(count);
+  if (d2h(e, hot.data(), e->P.hot + first, count) || d2h(e, core.data(), e->P.core + first, count) ||
+      d2h(e, rem.data(), e->P.rem + first * N, count * N) ||
+      d2h(e, rst.data(), e->P.rem_st + first * N, count * N) ||
+      d2h(e, upd.data(), e->P.upd + first, count))
+    return RBE_E_HIP;
+  HIP_OK(hipStreamSynchronize(e->stream));
+  for (u64 i = 0; i < count; i++) {
+    rbe_replica_view& v = out[i];
+    memset(&v, 0, sizeof(v));
+    const Hot& h = hot[i];
+    const Core& c = core[i];
+    v.term = c.term;
+    v.vote = c.vote;
+    v.leader_id = c.leader;
+    v.committed = c.committed;
+    v.last_index = c.last_index;
+    v.processed = c.processed;
+    v.saved_to = c.saved_to;
+    v.digest = upd[i].digest;
+    v.role = h.role;
+    v.election_tick = h.election_tick;
+    v.heartbeat_tick = h.heartbeat_tick;
+    v.rand_election_timeout = h.rand_et;
+    v.q_tick = h.q_tick;
+    v.q_quiesced_since = h.q_quiesced_since;
+    v.q_no_activity_since = h.q_no_activity_since;
+    v.q_exit_quiesce_tick = h.q_exit_quiesce_tick;
+    v.raft_quiesce = (h.flags & HF_RAFT_QUIESCE) ? 1 : 0;
+    v.rq_count = c.rq_count;
+    v.votes_resp = h.votes_resp;
+    v.votes_granted = h.votes_granted;
+    if (h.role == R_Leader) {
+      for (u32 s = 0; s < N && s < 8; s++) {
+        v.match[s] = rem[i * N + s].match;
+        v.next[s] = rem[i * N + s].next;
+        v.rstate[s] = rst[i * N + s] & 3;
+        v.ractive[s] = (rst[i * N + s] >> 2) & 1;
+      }
+    }
+  }
+  return RBE_OK;
+}
+
+int rbe_get_updates(rbe_engine* e, uint64_t first, uint64_t count, rbe_update* out) {
+  if (!e || !out || first + count > e->C.n_rep) return RBE_E_INVALID;
+  HIP_OK(hipSetDevice(e->device));
+  std::vector<Upd> upd(count);
+  std::vector<Core> core(count);
+  std::vector<Hot> hot(count);
+  if (d2h(e, upd.data(), e->P.upd + first, count) || d2h(e, core.data(), e->P.core + first, count) ||
+      d2h(e, hot.data(), e->P.hot + first, count))
+    return RBE_E_HIP;
+  HIP_OK(hipStreamSynchronize(e->stream));
+  for (u64 i = 0; i < count; i++) {
+    rbe_update& u = out[i];
+    memset(&u, 0, sizeof(u));
+    u.term = core[i].term;
+    u.vote = core[i].vote;
+    u.commit = core[i].committed;
+    u.save_lo = upd[i].save_lo;
+    u.save_hi = upd[i].save_hi;
+    u.apply_lo = upd[i].apply_lo;
+    u.apply_hi = upd[i].apply_hi;
+    u.digest = upd[i].digest;
+    u.n_messages = upd[i].n_msgs;
+    u.n_ready_to_read = upd[i].n_rtr;
+    u.n_dropped_entries = upd[i].n_drop_ent;
+    u.n_dropped_read_indexes = upd[i].n_drop_ri;
+    u.fault = upd[i].fault;
+    u.flags = upd[i].flags;
+    u.role = hot[i].role;
+    u.leader_id = core[i].leader;
+  }
+  return RBE_OK;
+}
+
+int rbe_get_messages(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t cap,
+                     uint32_t* n_out) {
+  if (!e || !n_out || replica >= e->C.n_rep || e->round == 0) return RBE_E_INVALID;
+  HIP_OK(hipSetDevice(e->device));
+  const u32 N = e->C.n, par = (e->round - 1) & 1u;
+  const u64 g = replica / N;
+  const u32 k = (u32)(replica % N);
+  std::vector<u16> cnt(N);
+  HIP_OK(hipMemcpyAsync(cnt.data(), e->P.cnt[par] + g * N * N + k * N, N * sizeof(u16),
+                        hipMemcpyDeviceToHost, e->stream));
+  std::vector<Msg> lst((size_t)N * e->C.maxm);
+  HIP_OK(hipMemcpyAsync(lst.data(), e->P.msgs[par] + (g * N + k) * N * (u64)e->C.maxm,
+                        lst.size() * sizeof(Msg), hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  u32 n = 0;
+  for (u32 d = 0; d < N; d++) {
+    const u32 pc = cnt[d], na = pc & 0x7F, nb = (pc >> 7) & 0x7F;
+    for (u32 i = 0; i < na + nb; i++) {
+      const Msg& m = i < na ? lst[d * e->C.maxm + i] : lst[d * e->C.maxm + e->C.maxm - 1 - (i - na)];
+      if (n < cap && out) {
+        rbe_message& o = out[n];
+        memset(&o, 0, sizeof(o));
+        o.type = m.type;
+        o.reject = m.reject;
+        o.to = m.to;
+        o.from = m.from;
+        o.cluster_id = e->C.cid_base + g * e->C.cid_stride;
+        o.term = m.term;
+        o.log_term = m.log_term;
+        o.log_index = m.log_index;
+        o.commit = m.commit;
+        o.hint = m.hint;
+        o.hint_high = m.hint_high;
+        o.n_entries = m.n_ent;
+      }
+      n++;
+    }
+  }
+  *n_out = n;
+  return RBE_OK;
+}
+
+int rbe_get_ready_to_reads(rbe_engine* e, uint64_t replica, rbe_ready_to_read* out, uint32_t cap,
+                           uint32_t* n_out) {
+  if (!e || !n_out || replica >= e->C.n_rep) return RBE_E_INVALID;
+  HIP_OK(hipSetDevice(e->device));
+  Upd u;
+  HIP_OK(hipMemcpyAsync(&u, e->P.upd + replica, sizeof(u), hipMemcpyDeviceToHost, e->stream));
+  std::vector<RTR> v(e->C.rtr_cap);
+  HIP_OK(hipMemcpyAsync(v.data(), e->P.rtr + replica * e->C.rtr_cap, v.size() * sizeof(RTR),
+                        hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  u32 n = u.n_rtr < e->C.rtr_cap ? u.n_rtr : e->C.rtr_cap;
+  for (u32 i = 0; i < n && i < cap && out; i++) {
+    out[i].index = v[i].index;
+    out[i].ctx_low = v[i].low;
+    out[i].ctx_high = v[i].high;
+  }
+  *n_out = n;
+  return RBE_OK;
+}
+
+int rbe_get_entries(rbe_engine* e, uint64_t replica, uint64_t lo, uint64_t hi, rbe_entry* out) {
+  if (!e || !out || replica >= e->C.n_rep || lo == 0 || hi < lo) return RBE_E_INVALID;
+  HIP_OK(hipSetDevice(e->device));
+  Core c;
+  HIP_OK(hipMemcpy(&c, e->P.core + replica, sizeof(c), hipMemcpyDeviceToHost));
+  if (hi > c.last_index || c.last_index - lo >= e->C.ring) return RBE_E_INVALID;
+  for (u64 i = lo; i <= hi; i++) {
+    u64 slot = (i & (u64)(e->C.ring - 1)) * e->C.n_rep + replica;
+    u64 t;
+    Body b;
+    HIP_OK(hipMemcpy(&t, e->P.term_ring + slot, sizeof(t), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(&b, e->P.pay_ring + slot, sizeof(b), hipMemcpyDeviceToHost));
+    rbe_entry& o = out[i - lo];
+    memset(&o, 0, sizeof(o));
+    o.index = i;
+    o.term = t;
+    o.type = b.type;
+    o.cmd_len = b.len;
+    memcpy(o.cmd, &b.lo, 8);
+    memcpy(o.cmd + 8, &b.hi, 8);
+  }
+  return RBE_OK;
+}
+
+int rbe_fault_summary(rbe_engine* e, uint64_t* n_faulty, uint32_t* fault_or) {
+  if (!e || !n_faulty || !fault_or) return RBE_E_INVALID;
+  HIP_OK(hipSetDevice(e->device));
+  const u64 R = e->C.n_rep;
+  std::vector<Upd> upd(R);
+  HIP_OK(hipMemcpyAsync(upd.data(), e->P.upd, R * sizeof(Upd), hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  u64 n = 0;
+  u32 o = 0;
+  for (u64 i = 0; i < R; i++) {
+    if (upd[i].fault) n++;
+    o |= upd[i].fault;
+  }
+  *n_faulty = n;
+  *fault_or = o;
+  return RBE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,1405 @@
+// MI355X batched Raft step engine — the per-replica step.
+//
+// One lane steps one replica through one lockstep round: the dragonboat node
+// step (node.go:1016-1067 stepNode/handleEvents, 1171-1205
+// handleReceivedMessages, 1384-1399 tick, quiesce.go) driving the raft
+// protocol (internal/raft/raft.go) on struct-of-arrays state in HBM.
+// Inbound messages are read from the senders' previous-round outbox lists,
+// outbound messages are written to this round's lists; nothing a lane writes
+// is read by another lane in the same launch (DESIGN.md §Round semantics).
+//
+// Kernel groups of the north star map onto this file as:
+//   (1) ReplicateResp → tryCommit: on_replicate_resp / try_commit / kth_match
+//   (2) log matching: on_replicate / match_term / try_append
+//   (3) vote tally: campaign / on_vote_resp / on_request_vote
+//   (4) ReadIndex quorum: on_leader_read_index / rq_confirm / on_heartbeat_resp
+//   (5) tick / quiesce: node_tick / raft_tick / quiesce manager
+#pragma once
+#include "rbe_types.h"
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define RBE_HD __host__ __device__ __forceinline__
+#else
+#define RBE_HD inline
+#endif
+
+namespace rbe {
+
+RBE_HD u64 mix64(u64 x) {  // splitmix64 finalizer (same constants as the oracle)
+  x += 0x9E3779B97F4A7C15ULL;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+  return x ^ (x >> 31);
+}
+RBE_HD u64 hfold(u64 h, u64 x) { return mix64(h ^ x); }
+RBE_HD u64 umin64(u64 a, u64 b) { return a < b ? a : b; }
+RBE_HD u64 umax64(u64 a, u64 b) { return a > b ? a : b; }
+RBE_HD u32 popc8(u32 x) {
+  x = x - ((x >> 1) & 0x55u);
+  x = (x & 0x33u) + ((x >> 2) & 0x33u);
+  return (x + (x >> 4)) & 0x0Fu;
+}
+
+// ----------------------------------------------------------------- workload
+// DESIGN.md §Workload; restated independently in oracle/harness.cpp.
+RBE_HD u64 wl_payload_lo(u64 seed, u64 cid, u64 round) {
+  return mix64(seed ^ (cid * 0xD1B54A32D192ED03ULL) ^ (round << 1));
+}
+RBE_HD bool wl_group_active(const Params& C, u64 cid) {
+  if (C.wl_active_mod <= 1) return true;
+  return mix64(C.seed ^ 0xA5A5A5A5A5A5A5A5ULL ^ (cid * 0x9E3779B97F4A7C15ULL)) %
+             C.wl_active_mod == 0;
+}
+RBE_HD u32 wl_input(const Params& C, u64 cid, u32 round) {
+  if (!C.wl_enabled) return 0;
+  if (round < C.wl_start_round) return 0;
+  if (C.wl_stop_round != 0 && round >= C.wl_stop_round) return 0;
+  if (!wl_group_active(C, cid)) return 0;
+  if (C.wl_read_permille == 0) return 1;
+  u64 u = mix64(C.seed ^ (cid * 0xC2B2AE3D27D4EB4FULL) ^ ((u64)round << 20)) % 1000;
+  return u < C.wl_read_permille ? 2u : 1u;
+}
+RBE_HD bool iso_selected(const Params& C, u64 cid, u32 epoch) {
+  if (C.iso_mod <= 1) return true;
+  return mix64(C.seed ^ (cid * 0x94D049BB133111EBULL) ^ ((u64)epoch << 40)) % C.iso_mod == 0;
+}
+// injected replacement for random.LockGuardedRand (raft.go:632)
+RBE_HD u64 rto_rand(u64 seed, u64 cid, u64 nid, u64 count) {
+  return mix64(seed ^ (cid * 0x9E3779B97F4A7C15ULL) ^ (nid << 32) ^ count);
+}
+
+RBE_HD bool is_leader_message(u32 t) {  // raft.go:1382-1385
+  return t == M_Replicate || t == M_InstallSnapshot || t == M_Heartbeat || t == M_TimeoutNow ||
+         t == M_ReadIndexResp;
+}
+
+// per-lane step result handed back to the kernel wrapper for wave reduction
+struct StepCounters {
+  u32 v[C_NUM];
+};
+
+// ----------------------------------------------------------------- the lane
+template <int N>
+struct Lane {
+  const Planes& P;
+  const Params& C;
+  const u64 r;      // global replica index
+  const u64 g;      // group
+  const u32 k;      // slot; node id = k + 1
+  const u32 round;
+  const u32 par;    // round & 1: outbox buffer written this round
+  const u64 cid;
+  const u8 self;    // node id
+
+  // registers: hot + core
+  u8 role, flags, vresp, vgrant;
+  u32 etick, htick, ret;
+  u32 q_tick, q_qs, q_nas, q_eqt, rngc;
+  bool q_new;
+  u64 term, committed, last, processed, saved_to;
+  u8 vote, leader, ltt, rq_head, rq_count;
+  u8 iso;  // isolation mask of this group for this round
+
+  // per-step outputs
+  u64 pc_lo, pc_hi;  // per destination 16-bit A | B << 7 | quiesce << 15 (registers)
+  u32 arena_used;
+  u64 seg_lo;
+  u32 seg_off, seg_len;
+  u64 msg_hash, rtr_hash, drop_hash;
+  u32 n_msgs, n_rtr, n_drop_ent, n_drop_ri;
+  u32 fault;
+  StepCounters& ctr;
+
+  RBE_HD Lane(const Planes& P_, const Params& C_, u64 r_, u32 round_, StepCounters& c_)
+      : P(P_), C(C_), r(r_), g(r_ / N), k((u32)(r_ % N)), round(round_), par(round_ & 1u),
+        cid(C_.cid_base + (r_ / N) * C_.cid_stride), self((u8)(r_ % N + 1)), ctr(c_) {}
+
+  // ------------------------------------------------------------- faults
+  RBE_HD void set_fault(u32 f) {
+    if (!(fault & f)) ctr.v[C_FAULTS]++;
+    fault |= f;
+  }
+
+  // ------------------------------------------------------------- log (term ring)
+  RBE_HD u64 ring_slot(u64 idx) const { return (idx & (u64)(C.ring - 1)) * C.n_rep + r; }
+  // entryLog.term (logentry.go:142-161): 0 with no error outside
+  // [firstIndex-1, lastIndex]; firstIndex is 1 (no compaction on device).
+  RBE_HD u64 log_term(u64 idx) {
+    if (idx > last || idx == 0) return 0;
+    if (last - idx >= C.ring) {
+      set_fault(F_WINDOW);
+      return 0;
+    }
+    ctr.v[C_RING_ACCESS]++;
+    return P.term_ring[ring_slot(idx)];
+  }
+  RBE_HD bool match_term(u64 idx, u64 t) { return log_term(idx) == t; }  // logentry.go:357-363
+  RBE_HD bool up_to_date(u64 idx, u64 t) {  // logentry.go:365-377
+    u64 lt = log_term(last);
+    if (t >= lt) {
+      if (t > lt) return true;
+      return idx >= last;
+    }
+    return false;
+  }
+  RBE_HD void commit_to(u64 idx) {  // logentry.go:324-333
+    if (idx <= committed) return;
+    if (idx > last) {
+      set_fault(F_PANIC);
+      return;
+    }
+    committed = idx;
+  }
+  RBE_HD bool log_try_commit(u64 idx, u64 t) {  // logentry.go:379-394
+    if (idx <= committed) return false;
+    u64 lt = log_term(idx);
+    if (lt == t) {
+      commit_to(idx);
+      return true;
+    }
+    return false;
+  }
+  RBE_HD void ring_put(u64 idx, u64 t, u32 type, u32 len, u64 lo, u64 hi) {
+    u64 s = ring_slot(idx);
+    P.term_ring[s] = t;
+    Body b;
+    b.type = type;
+    b.len = len;
+    b.lo = lo;
+    b.hi = hi;
+    P.pay_ring[s] = b;
+    ctr.v[C_RING_ACCESS]++;
+  }
+  // limitSize (entryutils.go:52-64) over [lo, hi] with sizes 128 + len
+  RBE_HD u64 limit_count(u64 lo, u64 hi) {
+    u64 n = hi - lo + 1;
+    if (n * (128 + 16) <= C.max_entry_size) return n;
+    u64 total = 128 + P.pay_ring[ring_slot(lo)].len;
+    u64 inc = 1;
+    for (; inc < n; inc++) {
+      total += 128 + P.pay_ring[ring_slot(lo + inc)].len;
+      if (total > C.max_entry_size) break;
+    }
+    return inc;
+  }
+
+  // ------------------------------------------------------------- remotes
+  RBE_HD RemoteMN* rem(u32 slot) const { return &P.rem[r * N + slot]; }
+  RBE_HD u8 rst(u32 slot) const { return P.rem_st[r * N + slot]; }
+  RBE_HD void set_rst(u32 slot, u8 v) { P.rem_st[r * N + slot] = v; }
+  RBE_HD u8 rstate(u32 slot) const { return rst(slot) & 3; }
+  RBE_HD void set_rstate(u32 slot, u8 s) { set_rst(slot, (u8)((rst(slot) & ~3) | s)); }
+  RBE_HD bool ractive(u32 slot) const { return (rst(slot) >> 2) & 1; }
+  RBE_HD void set_active(u32 slot, bool a) { set_rst(slot, (u8)((rst(slot) & 3) | (a ? 4 : 0))); }
+  RBE_HD bool is_paused(u32 slot) const {  // remote.go:173-186
+    u8 s = rstate(slot);
+    return s == RS_Wait || s == RS_Snapshot;
+  }
+  RBE_HD void wait_to_retry(u32 slot) {  // remote.go:94-98
+    if (rstate(slot) == RS_Wait) set_rstate(slot, RS_Retry);
+  }
+  RBE_HD void become_retry(u32 slot) {  // remote.go:75-83 (snapshotIndex is 0 on device)
+    RemoteMN* x = rem(slot);
+    x->next = x->match + 1;
+    set_rstate(slot, RS_Retry);
+  }
+  RBE_HD void become_replicate(u32 slot) {  // remote.go:102-106
+    RemoteMN* x = rem(slot);
+    x->next = x->match + 1;
+    set_rstate(slot, RS_Replicate);
+  }
+  RBE_HD bool try_update(u32 slot, u64 idx) {  // remote.go:123-133
+    RemoteMN* x = rem(slot);
+    ctr.v[C_REMOTE_TOUCH]++;
+    if (x->next < idx + 1) x->next = idx + 1;
+    if (x->match < idx) {
+      wait_to_retry(slot);
+      x->match = idx;
+      return true;
+    }
+    return false;
+  }
+  RBE_HD void progress(u32 slot, u64 li) {  // remote.go:135-143
+    u8 s = rstate(slot);
+    if (s == RS_Replicate) rem(slot)->next = li + 1;
+    else if (s == RS_Retry) set_rstate(slot, RS_Wait);
+    else set_fault(F_PANIC);
+  }
+  RBE_HD void responded_to(u32 slot) {  // remote.go:145-153
+    u8 s = rstate(slot);
+    if (s == RS_Retry) become_replicate(slot);
+    else if (s == RS_Snapshot) {
+      if (rem(slot)->match >= 0) become_retry(slot);  // snapshotIndex == 0 on device
+    }
+  }
+  RBE_HD bool decrease_to(u32 slot, u64 rejected, u64 lst) {  // remote.go:155-171
+    RemoteMN* x = rem(slot);
+    if (rstate(slot) == RS_Replicate) {
+      if (rejected <= x->match) return false;
+      x->next = x->match + 1;
+      return true;
+    }
+    if (x->next - 1 != rejected) return false;
+    wait_to_retry(slot);
+    x->next = umax64(1, umin64(rejected, lst + 1));
+    return true;
+  }
+
+  // ------------------------------------------------------------- emission
+  RBE_HD u32 get_pc(u32 d) const {
+    return d < 4 ? (u32)((pc_lo >> (16 * d)) & 0xFFFFu) : (u32)((pc_hi >> (16 * (d - 4))) & 0xFFFFu);
+  }
+  RBE_HD void add_pc(u32 d, u32 v) {
+    if (d < 4) pc_lo += (u64)v << (16 * d);
+    else pc_hi += (u64)v << (16 * (d - 4));
+  }
+  RBE_HD u64 msg_slot_base(u32 sender, u32 dest) const {
+    return ((g * N + sender) * N + dest) * (u64)C.maxm;
+  }
+  // raft.send + finalizeMessageTerm (raft.go:640-658) + the network: the
+  // message joins Update.Messages (hashed here, in emission order) and is
+  // written to the (self → dest) list, Replicate messages in front (node.go
+  // sends them before persistence, 897-905) and the rest behind (888-895).
+  RBE_HD void send(Msg& m) {
+    m.from = self;
+    if (m.type != M_RequestVote) {
+      if (m.type == M_Propose || m.type == M_ReadIndex) m.term = 0;
+      else m.term = term;
+    }
+    n_msgs++;
+    if (C.trace) {
+      u64 h = msg_hash;
+      h = hfold(h, (u64)m.type | ((u64)m.reject << 8) | ((u64)m.n_ent << 16));
+      h = hfold(h, m.to);
+      h = hfold(h, m.from);
+      h = hfold(h, m.term);
+      h = hfold(h, m.log_term);
+      h = hfold(h, m.log_index);
+      h = hfold(h, m.commit);
+      h = hfold(h, m.hint);
+      h = hfold(h, m.hint_high);
+      if (m.n_ent) {
+        const Ent* a = &P.arena[par][r * C.ecap + m.ent_off];
+        for (u32 i = 0; i < m.n_ent; i++) {
+          Ent e = a[i];
+          u64 idx = m.type == M_Replicate ? m.log_index + 1 + i : 0;
+          h = hfold(h, idx);
+          h = hfold(h, e.term);
+          h = hfold(h, (u64)e.type | ((u64)e.len << 32));
+          h = hfold(h, e.lo);
+          h = hfold(h, e.hi);
+        }
+      }
+      msg_hash = h;
+    }
+    if (m.to < 1 || m.to > N) return;
+    u32 d = m.to - 1u;
+    if (((iso >> k) & 1u) || ((iso >> d) & 1u)) {
+      ctr.v[C_MSG_DROPPED]++;
+      return;
+    }
+    const u32 pc = get_pc(d);
+    u32 a = pc & 0x7Fu, b = (pc >> 7) & 0x7Fu;
+    if (a + b >= C.maxm) {
+      set_fault(F_OUTBOX);
+      return;
+    }
+    u32 slot;
+    if (m.type == M_Replicate) {
+      slot = a;
+      add_pc(d, 1u);
+    } else {
+      slot = C.maxm - 1u - b;
+      add_pc(d, 1u << 7);
+    }
+    P.msgs[par][msg_slot_base(k, d) + slot] = m;
+    ctr.v[C_MSG_OUT]++;
+    ctr.v[C_ENT_OUT] += m.n_ent;
+  }
+  RBE_HD Msg mk(u32 type, u8 to) const {
+    Msg m;
+    m.type = (u8)type;
+    m.from = 0;
+    m.to = to;
+    m.reject = 0;
+    m.n_ent = 0;
+    m.pad0 = 0;
+    m.ent_off = 0;
+    m.pad1 = 0;
+    m.term = m.log_term = m.log_index = m.commit = m.hint = m.hint_high = 0;
+    return m;
+  }
+  // copy log entries [lo, lo+cnt) into this round's arena (reusing the last
+  // copied segment when it already covers them); returns the arena offset
+  RBE_HD bool arena_log_range(u64 lo, u32 cnt, u32* off) {
+    if (seg_len && lo >= seg_lo && lo + cnt <= seg_lo + seg_len) {
+      *off = seg_off + (u32)(lo - seg_lo);
+      return true;
+    }
+    Ent* a = &P.arena[par][r * C.ecap];
+    if (seg_len && lo >= seg_lo && lo <= seg_lo + seg_len && seg_off + seg_len == arena_used) {
+      u64 have_hi = seg_lo + seg_len;  // exclusive
+      u32 extra = (u32)(lo + cnt - have_hi);
+      if (arena_used + extra > C.ecap) {
+        set_fault(F_ARENA);
+        return false;
+      }
+      for (u32 i = 0; i < extra; i++) {
+        u64 idx = have_hi + i;
+        if (last - idx >= C.ring) set_fault(F_WINDOW);
+        u64 s = ring_slot(idx);
+        Body b = P.pay_ring[s];
+        Ent e;
+        e.term = P.term_ring[s];
+        e.type = b.type;
+        e.len = b.len;
+        e.lo = b.lo;
+        e.hi = b.hi;
+        a[arena_used + i] = e;
+      }
+      ctr.v[C_RING_ACCESS] += extra;
+      arena_used += extra;
+      seg_len += extra;
+      *off = seg_off + (u32)(lo - seg_lo);
+      return true;
+    }
+    if (arena_used + cnt > C.ecap) {
+      set_fault(F_ARENA);
+      return false;
+    }
+    for (u32 i = 0; i < cnt; i++) {
+      u64 idx = lo + i;
+      if (last - idx >= C.ring) set_fault(F_WINDOW);
+      u64 s = ring_slot(idx);
+      Body b = P.pay_ring[s];
+      Ent e;
+      e.term = P.term_ring[s];
+      e.type = b.type;
+      e.len = b.len;
+      e.lo = b.lo;
+      e.hi = b.hi;
+      a[arena_used + i] = e;
+    }
+    ctr.v[C_RING_ACCESS] += cnt;
+    seg_lo = lo;
+    seg_off = arena_used;
+    seg_len = cnt;
+    *off = arena_used;
+    arena_used += cnt;
+    return true;
+  }
+  RBE_HD bool arena_put(const Ent* src, u32 cnt, u32* off) {
+    if (arena_used + cnt > C.ecap) {
+      set_fault(F_ARENA);
+      return false;
+    }
+    Ent* a = &P.arena[par][r * C.ecap];
+    for (u32 i = 0; i < cnt; i++) a[arena_used + i] = src[i];
+    *off = arena_used;
+    arena_used += cnt;
+    return true;
+  }
+
+  // ------------------------------------------------------------- outputs
+  RBE_HD void add_ready_to_read(u64 index, u64 low, u64 high) {  // raft.go:1624-1630
+    if (n_rtr >= C.rtr_cap) {
+      set_fault(F_RTR);
+      return;
+    }
+    RTR x;
+    x.index = index;
+    x.low = low;
+    x.high = high;
+    P.rtr[r * C.rtr_cap + n_rtr] = x;
+    n_rtr++;
+    if (C.trace) {
+      rtr_hash = hfold(rtr_hash, index);
+      rtr_hash = hfold(rtr_hash, low);
+      rtr_hash = hfold(rtr_hash, high);
+    }
+  }
+  RBE_HD void add_dropped_ri(u64 low, u64 high) {
+    if (n_drop_ri >= C.dri_cap) {
+      set_fault(F_DROPLIST);
+      return;
+    }
+    DropRI x;
+    x.low = low;
+    x.high = high;
+    P.dri[r * C.dri_cap + n_drop_ri] = x;
+    n_drop_ri++;
+  }
+  RBE_HD void report_dropped_read_index(u64 low, u64 high) {  // raft.go:1999-2012
+    add_dropped_ri(low, high);
+  }
+  RBE_HD void report_dropped_proposal(const Ent* e, u32 cnt) {  // raft.go:1987-1997
+    for (u32 i = 0; i < cnt; i++) {
+      n_drop_ent++;
+      if (C.trace) {
+        drop_hash = hfold(drop_hash, 0);
+        drop_hash = hfold(drop_hash, e[i].term);
+        drop_hash = hfold(drop_hash, (u64)e[i].type | ((u64)e[i].len << 32));
+        drop_hash = hfold(drop_hash, e[i].lo);
+        drop_hash = hfold(drop_hash, e[i].hi);
+      }
+    }
+  }
+
+  // ------------------------------------------------------------- state transitions
+  RBE_HD void set_randomized_election_timeout() {  // raft.go:631-634
+    u64 x = rto_rand(C.seed, cid, self, rngc++) % C.election_rtt;
+    ret = (u32)(C.election_rtt + x);
+  }
+  RBE_HD void reset_remotes() {  // raft.go:1023-1032
+    for (u32 s = 0; s < N; s++) {
+      RemoteMN x;
+      x.match = s == k ? last : 0;
+      x.next = last + 1;
+      *rem(s) = x;
+      set_rst(s, 0);
+    }
+    ctr.v[C_REMOTE_TOUCH] += N;
+  }
+  RBE_HD void reset(u64 t) {  // raft.go:989-1008
+    if (term != t) {
+      term = t;
+      vote = 0;
+    }
+    vresp = vgrant = 0;
+    etick = 0;
+    htick = 0;
+    set_randomized_election_timeout();
+    rq_head = rq_count = 0;
+    flags &= (u8)~HF_PENDING_CC;
+    ltt = 0;
+    reset_remotes();
+    seg_len = 0;
+  }
+  RBE_HD void become_follower(u64 t, u8 lid) {  // raft.go:947-955
+    role = R_Follower;
+    reset(t);
+    leader = lid;
+  }
+  RBE_HD void become_candidate() {  // raft.go:957-973
+    role = R_Candidate;
+    reset(term + 1);
+    leader = 0;
+    vote = self;
+  }
+  RBE_HD void become_leader() {  // raft.go:975-987
+    role = R_Leader;
+    reset(term);
+    leader = self;
+    // preLeaderPromotionHandleConfigChange (raft.go:1010-1018): count config
+    // change entries in (committed, last]
+    u32 ncc = 0;
+    for (u64 i = committed + 1; i <= last; i++) {
+      if (last - i >= C.ring) {
+        set_fault(F_WINDOW);
+        break;
+      }
+      if (P.pay_ring[ring_slot(i)].type == E_ConfigChange) ncc++;
+    }
+    if (ncc > 1) set_fault(F_PANIC);
+    else if (ncc == 1) flags |= HF_PENDING_CC;
+    // p72 of the raft thesis: an empty entry at the new term
+    append_entry(E_Application, 0, 0, 0);
+  }
+  // appendEntries (raft.go:909-920) for one entry
+  RBE_HD void append_entry(u32 type, u32 len, u64 lo, u64 hi) {
+    u64 idx = last + 1;
+    ring_put(idx, term, type, len, lo, hi);
+    last = idx;
+    try_update(k, last);
+    if (N / 2 + 1 == 1) try_commit();
+  }
+
+  // ------------------------------------------------------------- commit (kernel 1)
+  // tryCommit (raft.go:886-907): q = matched[n - quorum] of the sorted match
+  // values = the quorum-th largest; a register-resident selection over N.
+  RBE_HD u64 kth_match() {
+    u64 m[N];
+    for (u32 s = 0; s < N; s++) m[s] = rem(s)->match;
+    // odd-even transposition sort (fully unrolled for a compile-time N)
+    for (u32 pass = 0; pass < N; pass++) {
+      for (u32 i = pass & 1u; i + 1 < N; i += 2) {
+        u64 a = m[i], b = m[i + 1];
+        m[i] = a < b ? a : b;
+        m[i + 1] = a < b ? b : a;
+      }
+    }
+    ctr.v[C_REMOTE_TOUCH] += N;
+    return m[N - (N / 2 + 1)];
+  }
+  RBE_HD bool try_commit() { return log_try_commit(kth_match(), term); }
+
+  // ------------------------------------------------------------- replication
+  RBE_HD void send_replicate(u32 slot) {  // raft.go:758-792
+    if (is_paused(slot)) return;
+    u64 next = rem(slot)->next;
+    // makeReplicateMessage (raft.go:709-740)
+    u64 lt = log_term(next - 1);
+    Msg m = mk(M_Replicate, (u8)(slot + 1));
+    m.log_index = next - 1;
+    m.log_term = lt;
+    m.commit = committed;
+    if (next <= last) {
+      u64 cnt = limit_count(next, last);
+      u32 off = 0;
+      if (arena_log_range(next, (u32)cnt, &off)) {
+        m.n_ent = (u16)cnt;
+        m.ent_off = off;
+      }
+      progress(slot, next + cnt - 1);
+    }
+    send(m);
+  }
+  RBE_HD void broadcast_replicate() {  // raft.go:794-808
+    for (u32 s = 0; s < N; s++)
+      if (s != k) send_replicate(s);
+  }
+  RBE_HD void send_heartbeat(u32 slot, u64 low, u64 high) {  // raft.go:810-820
+    Msg m = mk(M_Heartbeat, (u8)(slot + 1));
+    m.commit = umin64(rem(slot)->match, committed);
+    m.hint = low;
+    m.hint_high = high;
+    send(m);
+  }
+  RBE_HD void broadcast_heartbeat_with_hint(u64 low, u64 high) {  // raft.go:834-846
+    for (u32 s = 0; s < N; s++)
+      if (s != k) send_heartbeat(s, low, high);
+    ctr.v[C_REMOTE_TOUCH] += N - 1;
+  }
+  RBE_HD void broadcast_heartbeat() {  // raft.go:824-832
+    if (rq_count > 0) {
+      const ReadReq& q = P.rq[r * C.rq_cap + (u32)((rq_head + rq_count - 1) % C.rq_cap)];
+      broadcast_heartbeat_with_hint(q.low, q.high);
+    } else {
+      broadcast_heartbeat_with_hint(0, 0);
+    }
+  }
+
+  // ------------------------------------------------------------- readIndex (kernel 4)
+  RBE_HD ReadReq* rq_at(u32 i) { return &P.rq[r * C.rq_cap + (u32)((rq_head + i) % C.rq_cap)]; }
+  RBE_HD void rq_add(u64 index, u64 low, u64 high, u8 from) {  // readindex.go:43-67
+    for (u32 i = 0; i < rq_count; i++) {
+      ReadReq* q = rq_at(i);
+      if (q->low == low && q->high == high) return;
+    }
+    if (rq_count > 0 && index < rq_at(rq_count - 1)->index) set_fault(F_PANIC);
+    if (rq_count >= C.rq_cap) {
+      set_fault(F_READQ);
+      return;
+    }
+    ReadReq q;
+    q.low = low;
+    q.high = high;
+    q.index = index;
+    q.from = from;
+    q.confirmed = 0;
+    for (int i = 0; i < 6; i++) q.pad[i] = 0;
+    *rq_at(rq_count) = q;
+    rq_count++;
+    ctr.v[C_RQ_TOUCH]++;
+  }
+  // readIndex.confirm (readindex.go:77-116) + handleReadIndexLeaderConfirmation
+  // (raft.go:1736-1756)
+  RBE_HD void rq_confirm(u64 low, u64 high, u8 from, u64 m_hint, u64 m_hint_high) {
+    int pos = -1;
+    for (u32 i = 0; i < rq_count; i++) {
+      ReadReq* q = rq_at(i);
+      if (q->low == low && q->high == high) {
+        pos = (int)i;
+        break;
+      }
+    }
+    if (pos < 0) return;
+    ReadReq* p = rq_at((u32)pos);
+    p->confirmed |= (u8)(1u << (from - 1));
+    ctr.v[C_RQ_TOUCH]++;
+    if ((int)popc8(p->confirmed) + 1 < (int)(N / 2 + 1)) return;
+    u64 sindex = p->index;
+    u32 done = (u32)pos + 1;
+    for (u32 i = 0; i < done; i++) {
+      ReadReq q = *rq_at(i);
+      if (q.index > sindex) set_fault(F_PANIC);
+      if (q.from == 0 || q.from == self) {
+        add_ready_to_read(sindex, q.low, q.high);
+      } else {
+        Msg m = mk(M_ReadIndexResp, q.from);
+        m.log_index = sindex;
+        m.hint = m_hint;
+        m.hint_high = m_hint_high;
+        send(m);
+      }
+    }
+    ctr.v[C_RQ_TOUCH] += done;
+    rq_head = (u8)((rq_head + done) % C.rq_cap);
+    rq_count = (u8)(rq_count - done);
+  }
+
+  // ------------------------------------------------------------- leader handlers
+  RBE_HD void on_leader_propose(const Ent* ents, u32 cnt) {  // raft.go:1587-1606
+    if (ltt != 0) {  // leaderTransfering
+      report_dropped_proposal(ents, cnt);
+      return;
+    }
+    for (u32 i = 0; i < cnt; i++) {
+      if (ents[i].type == E_ConfigChange) {
+        set_fault(F_UNSUPPORTED);  // config change proposals are host slow path
+        return;
+      }
+    }
+    for (u32 i = 0; i < cnt; i++) {
+      u64 idx = last + 1;
+      ring_put(idx, term, ents[i].type, ents[i].len, ents[i].lo, ents[i].hi);
+      last = idx;
+    }
+    try_update(k, last);
+    if (N / 2 + 1 == 1) try_commit();
+    broadcast_replicate();
+  }
+  RBE_HD void on_leader_read_index(u64 low, u64 high, u8 from) {  // raft.go:1633-1665
+    if (N / 2 + 1 != 1) {
+      // hasCommittedEntryAtCurrentTerm (raft.go:1609-1618)
+      if (log_term(committed) != term) {
+        report_dropped_read_index(low, high);
+        return;
+      }
+      rq_add(committed, low, high, from);
+      broadcast_heartbeat_with_hint(low, high);
+    } else {
+      add_ready_to_read(committed, low, high);
+    }
+  }
+  RBE_HD void on_replicate_resp(const Msg& m, u32 slot) {  // raft.go:1667-1696
+    set_active(slot, true);
+    if (!m.reject) {
+      bool paused = is_paused(slot);
+      if (try_update(slot, m.log_index)) {
+        responded_to(slot);
+        if (try_commit()) broadcast_replicate();
+        else if (paused) send_replicate(slot);
+        if (ltt != 0 && role == R_Leader && m.from == ltt && last == rem(slot)->match) {
+          Msg t = mk(M_TimeoutNow, ltt);
+          send(t);
+        }
+      }
+    } else {
+      if (decrease_to(slot, m.log_index, m.hint)) {
+        if (rstate(slot) == RS_Replicate) become_retry(slot);  // enterRetryState
+        send_replicate(slot);
+      }
+    }
+  }
+  RBE_HD void on_heartbeat_resp(const Msg& m, u32 slot) {  // raft.go:1698-1710
+    set_active(slot, true);
+    wait_to_retry(slot);
+    ctr.v[C_REMOTE_TOUCH]++;
+    if (rem(slot)->match < last) send_replicate(slot);
+    if (m.hint != 0) rq_confirm(m.hint, m.hint_high, m.from, m.hint, m.hint_high);
+  }
+  RBE_HD void on_leader_transfer(const Msg& m, u32 slot) {  // raft.go:1712-1734
+    u64 target = m.hint;
+    if (target == 0) {
+      set_fault(F_PANIC);
+      return;
+    }
+    if (ltt != 0) return;
+    if (self == target) return;
+    ltt = (u8)target;
+    etick = 0;
+    if (rem(slot)->match == last) {
+      Msg t = mk(M_TimeoutNow, (u8)target);
+      send(t);
+    }
+  }
+  RBE_HD bool leader_has_quorum() {  // raft.go:378-388
+    u32 c = 0;
+    for (u32 s = 0; s < N; s++) {
+      if (s == k || ractive(s)) {
+        c++;
+        set_active(s, false);
+      }
+    }
+    return c >= N / 2 + 1;
+  }
+
+  // ------------------------------------------------------------- follower side (kernel 2)
+  RBE_HD void on_replicate(const Msg& m, const Ent* ents) {  // raft.go:1339-1372
+    Msg resp = mk(M_ReplicateResp, m.from);
+    if (m.log_index < committed) {
+      resp.log_index = committed;
+      send(resp);
+      return;
+    }
+    if (match_term(m.log_index, m.log_term)) {
+      // tryAppend (logentry.go:291-302) / getConflictIndex (315-322)
+      u64 conflict = 0;
+      u32 ci = 0;
+      for (u32 i = 0; i < m.n_ent; i++) {
+        u64 idx = m.log_index + 1 + i;
+        if (!match_term(idx, ents[i].term)) {
+          conflict = idx;
+          ci = i;
+          break;
+        }
+      }
+      if (conflict != 0) {
+        if (conflict <= committed) {
+          set_fault(F_PANIC);
+        } else {
+          // inMemory.merge (inmemory.go:201-234): checkEntriesToAppend then
+          // truncate-and-append; savedTo = min(savedTo, first-1)
+          if (conflict - 1 >= 1 && conflict - 1 <= last && log_term(conflict - 1) > ents[ci].term)
+            set_fault(F_PANIC);
+          for (u32 i = ci; i < m.n_ent; i++)
+            ring_put(m.log_index + 1 + i, ents[i].term, ents[i].type, ents[i].len, ents[i].lo,
+                     ents[i].hi);
+          last = m.log_index + m.n_ent;
+          saved_to = umin64(saved_to, conflict - 1);
+          seg_len = 0;
+        }
+      }
+      u64 last_idx = m.log_index + m.n_ent;
+      commit_to(umin64(last_idx, m.commit));
+      resp.log_index = last_idx;
+    } else {
+      resp.reject = 1;
+      resp.log_index = m.log_index;
+      resp.hint = last;
+    }
+    send(resp);
+  }
+  RBE_HD void on_heartbeat(const Msg& m) {  // raft.go:1301-1309
+    commit_to(m.commit);
+    Msg resp = mk(M_HeartbeatResp, m.from);
+    resp.hint = m.hint;
+    resp.hint_high = m.hint_high;
+    send(resp);
+  }
+
+  // ------------------------------------------------------------- elections (kernel 3)
+  RBE_HD void campaign() {  // raft.go:1080-1116
+    become_candidate();
+    ctr.v[C_CAMPAIGNS]++;
+    // handleVoteResp(self, false)
+    vresp |= (u8)(1u << k);
+    vgrant |= (u8)(1u << k);
+    if (N / 2 + 1 == 1) {
+      become_leader();
+      return;
+    }
+    u64 hint = 0;
+    if (flags & HF_IS_LTT) {
+      hint = self;
+      flags &= (u8)~HF_IS_LTT;
+    }
+    u64 lt = log_term(last);
+    for (u32 s = 0; s < N; s++) {
+      if (s == k) continue;
+      Msg m = mk(M_RequestVote, (u8)(s + 1));
+      m.term = term;
+      m.log_index = last;
+      m.log_term = lt;
+      m.hint = hint;
+      send(m);
+    }
+  }
+  RBE_HD void on_election() {  // handleNodeElection, raft.go:1482-1512
+    if (role != R_Leader) {
+      if (committed > processed) return;  // hasConfigChangeToApply: committed > applied
+      campaign();
+    }
+  }
+  RBE_HD void on_request_vote(const Msg& m) {  // raft.go:1514-1535
+    Msg resp = mk(M_RequestVoteResp, m.from);
+    bool can_grant = vote == 0 || vote == m.from || m.term > term;
+    bool utd = up_to_date(m.log_index, m.log_term);
+    if (can_grant && utd) {
+      etick = 0;
+      vote = m.from;
+    } else {
+      resp.reject = 1;
+    }
+    send(resp);
+  }
+  RBE_HD void on_vote_resp(const Msg& m) {  // raft.go:1964-1981, 1060-1078
+    u8 bit = (u8)(1u << (m.from - 1));
+    if (!(vresp & bit)) {
+      vresp |= bit;
+      if (!m.reject) vgrant |= bit;
+    }
+    u32 count = popc8(vgrant);
+    u32 q = N / 2 + 1;
+    if (count == q) {
+      become_leader();
+      broadcast_replicate();
+    } else if (popc8(vresp) - count == q) {
+      become_follower(term, 0);
+    }
+  }
+
+  // ------------------------------------------------------------- ticks (kernel 5)
+  RBE_HD void raft_tick();
+  RBE_HD void non_leader_tick() {  // raft.go:566-590
+    etick++;
+    if (etick >= ret) {  // !selfRemoved() && timeForElection()
+      etick = 0;
+      on_election();  // Handle(Election): term 0 passes the gate; handled in any role
+    }
+  }
+  RBE_HD void leader_tick() {  // raft.go:592-621
+    etick++;
+    bool abort_lt = ltt != 0 && role == R_Leader && etick >= C.election_rtt;
+    if (etick >= C.election_rtt) {
+      etick = 0;
+      if (C.check_quorum) {
+        // Handle(CheckQuorum): dispatched by role; leader only
+        if (role == R_Leader) {
+          if (!leader_has_quorum()) become_follower(term, 0);
+        }
+      }
+    }
+    if (abort_lt) ltt = 0;
+    htick++;
+    if (htick >= C.heartbeat_rtt) {
+      htick = 0;
+      if (role == R_Leader) broadcast_heartbeat();  // Handle(LeaderHeartbeat)
+    }
+  }
+  RBE_HD void quiesced_tick() {  // raft.go:623-629
+    if (!(flags & HF_RAFT_QUIESCE)) flags |= HF_RAFT_QUIESCE;
+    etick++;
+  }
+  RBE_HD void on_timeout_now() {  // raft.go:1906-1916
+    etick = ret;
+    flags |= HF_IS_LTT;
+    raft_tick();
+    flags &= (u8)~HF_IS_LTT;
+  }
+
+  // ------------------------------------------------------------- quiesce manager
+  RBE_HD u32 q_threshold() const { return C.election_rtt * 2 * 10; }
+  RBE_HD bool q_quiesced() const { return C.quiesce && q_qs > 0; }
+  RBE_HD bool q_new_to_quiesce() const {
+    if (!q_quiesced()) return false;
+    return q_tick - q_qs < C.election_rtt * 2;
+  }
+  RBE_HD bool q_just_exited() const {
+    if (q_quiesced()) return false;
+    return q_tick - q_eqt < q_threshold();
+  }
+  RBE_HD void q_enter() {
+    q_qs = q_tick;
+    q_nas = q_tick;
+    q_new = true;
+  }
+  RBE_HD void q_exit() {
+    q_qs = 0;
+    q_eqt = q_tick;
+  }
+  RBE_HD void q_increase_tick() {  // quiesce.go:43-55
+    if (!C.quiesce) return;
+    q_tick++;
+    if (!q_quiesced()) {
+      if (q_tick - q_nas > q_threshold()) q_enter();
+    }
+  }
+  RBE_HD void q_record_activity(u32 t) {  // quiesce.go:64-82
+    if (!C.quiesce) return;
+    if (t == M_Heartbeat || t == M_HeartbeatResp) {
+      if (!q_quiesced()) return;
+      if (q_new_to_quiesce()) return;
+    }
+    q_nas = q_tick;
+    if (q_quiesced()) q_exit();
+  }
+  RBE_HD void q_try_enter() {  // quiesce.go:102-110
+    if (q_just_exited()) return;
+    if (!q_quiesced()) q_enter();
+  }
+
+  // ------------------------------------------------------------- Handle
+  // raft.Handle (raft.go:1451-1458): term gate then the (role, type) table
+  // of initializeHandlerMap (raft.go:2037-2098).
+  RBE_HD void handle(const Msg& m, const Ent* ents) {
+    // onMessageTermNotMatched (raft.go:1415-1449)
+    if (m.term != 0 && m.term != term) {
+      // dropRequestVoteFromHighTermNode (raft.go:1387-1409)
+      if (m.type == M_RequestVote && C.check_quorum && m.term > term) {
+        if (m.hint != m.from) {
+          if (role == R_Leader && !(flags & HF_RAFT_QUIESCE) && etick >= C.election_rtt)
+            set_fault(F_PANIC);
+          if (leader != 0 && etick < C.election_rtt) return;
+        }
+      }
+      if (m.term > term) {
+        u8 lid = is_leader_message(m.type) ? m.from : (u8)0;
+        become_follower(m.term, lid);
+      } else {
+        if (is_leader_message(m.type) && C.check_quorum) {
+          Msg x = mk(M_NoOP, m.from);
+          send(x);
+        }
+        return;
+      }
+    }
+    switch (role) {
+      case R_Follower:
+        switch (m.type) {
+          case M_Propose:  // raft.go:1841-1853
+            if (leader == 0) {
+              report_dropped_proposal(ents, m.n_ent);
+            } else {
+              Msg f = m;
+              f.to = leader;
+              u32 off = 0;
+              if (m.n_ent && arena_put(ents, m.n_ent, &off)) f.ent_off = off;
+              send(f);
+            }
+            return;
+          case M_Replicate:  // raft.go:1859-1863
+            etick = 0;
+            leader = m.from;
+            on_replicate(m, ents);
+            return;
+          case M_Heartbeat:  // raft.go:1865-1869
+            etick = 0;
+            leader = m.from;
+            on_heartbeat(m);
+            return;
+          case M_ReadIndex:  // raft.go:1871-1879
+            if (leader == 0) {
+              report_dropped_read_index(m.hint, m.hint_high);
+            } else {
+              Msg f = m;
+              f.to = leader;
+              send(f);
+            }
+            return;
+          case M_LeaderTransfer:  // raft.go:1881-1888
+            if (leader != 0) {
+              Msg f = m;
+              f.to = leader;
+              send(f);
+            }
+            return;
+          case M_ReadIndexResp:  // raft.go:1890-1898
+            etick = 0;
+            leader = m.from;
+            add_ready_to_read(m.log_index, m.hint, m.hint_high);
+            return;
+          case M_Election: on_election(); return;
+          case M_RequestVote: on_request_vote(m); return;
+          case M_TimeoutNow: on_timeout_now(); return;
+          case M_InstallSnapshot:
+          case M_ConfigChangeEvent:
+          case M_SnapshotReceived: set_fault(F_UNSUPPORTED); return;
+          default: return;
+        }
+      case R_Candidate:
+        switch (m.type) {
+          case M_Heartbeat:  // raft.go:1959-1962
+            become_follower(term, m.from);
+            on_heartbeat(m);
+            return;
+          case M_Propose: report_dropped_proposal(ents, m.n_ent); return;  // 1928-1931
+          case M_ReadIndex:  // raft.go:1933-1941 (reported twice, as in the reference)
+            report_dropped_read_index(m.hint, m.hint_high);
+            add_dropped_ri(m.hint, m.hint_high);
+            return;
+          case M_Replicate:  // raft.go:1949-1952
+            become_follower(term, m.from);
+            on_replicate(m, ents);
+            return;
+          case M_RequestVoteResp: on_vote_resp(m); return;
+          case M_Election: on_election(); return;
+          case M_RequestVote: on_request_vote(m); return;
+          case M_InstallSnapshot:
+          case M_ConfigChangeEvent:
+          case M_SnapshotReceived: set_fault(F_UNSUPPORTED); return;
+          default: return;
+        }
+      case R_Leader:
+        switch (m.type) {
+          case M_Propose: on_leader_propose(ents, m.n_ent); return;
+          case M_ReadIndex: on_leader_read_index(m.hint, m.hint_high, m.from); return;
+          case M_ReplicateResp:
+            if (m.from >= 1 && m.from <= N) on_replicate_resp(m, m.from - 1u);
+            return;
+          case M_HeartbeatResp:
+            if (m.from >= 1 && m.from <= N) on_heartbeat_resp(m, m.from - 1u);
+            return;
+          case M_LeaderTransfer:
+            if (m.from >= 1 && m.from <= N) on_leader_transfer(m, m.from - 1u);
+            return;
+          case M_Unreachable:  // raft.go:1773-1777
+            if (m.from >= 1 && m.from <= N && rstate(m.from - 1u) == RS_Replicate)
+              become_retry(m.from - 1u);
+            return;
+          case M_SnapshotStatus: return;  // no remote is ever in Snapshot state on device
+          case M_Election: return;        // leader ignores Election
+          case M_RequestVote: on_request_vote(m); return;
+          case M_ConfigChangeEvent:
+          case M_SnapshotReceived: set_fault(F_UNSUPPORTED); return;
+          default: return;  // RateLimit: limiter disabled → dropped
+        }
+      default:
+        set_fault(F_UNSUPPORTED);
+        return;
+    }
+  }
+
+  // ------------------------------------------------------------- the step
+  RBE_HD void load() {
+    Hot h = P.hot[r];
+    role = h.role;
+    flags = h.flags;
+    vresp = h.votes_resp;
+    vgrant = h.votes_granted;
+    etick = h.election_tick;
+    htick = h.heartbeat_tick;
+    ret = h.rand_et;
+    q_tick = h.q_tick;
+    q_qs = h.q_quiesced_since;
+    q_nas = h.q_no_activity_since;
+    q_eqt = h.q_exit_quiesce_tick;
+    rngc = h.rng_count;
+    Core c = P.core[r];
+    term = c.term;
+    committed = c.committed;
+    last = c.last_index;
+    processed = c.processed;
+    saved_to = c.saved_to;
+    vote = c.vote;
+    leader = c.leader;
+    ltt = c.ltt;
+    rq_head = c.rq_head;
+    rq_count = c.rq_count;
+  }
+  RBE_HD void store() {
+    Hot h;
+    h.role = role;
+    h.flags = flags;
+    h.votes_resp = vresp;
+    h.votes_granted = vgrant;
+    h.election_tick = etick;
+    h.heartbeat_tick = (u16)htick;
+    h.rand_et = (u16)ret;
+    h.q_tick = q_tick;
+    h.q_quiesced_since = q_qs;
+    h.q_no_activity_since = q_nas;
+    h.q_exit_quiesce_tick = q_eqt;
+    h.rng_count = rngc;
+    P.hot[r] = h;
+    Core c;
+    c.term = term;
+    c.committed = committed;
+    c.last_index = last;
+    c.processed = processed;
+    c.saved_to = saved_to;
+    c.vote = vote;
+    c.leader = leader;
+    c.ltt = ltt;
+    c.rq_head = rq_head;
+    c.rq_count = rq_count;
+    c.pad[0] = c.pad[1] = c.pad[2] = 0;
+    c.pad2[0] = c.pad2[1] = 0;
+    P.core[r] = c;
+  }
+
+  RBE_HD void run() {
+    load();
+    fault = P.upd[r].fault;
+    const u64 digest0 = P.upd[r].digest;
+    pc_lo = pc_hi = 0;
+    arena_used = 0;
+    seg_lo = 0;
+    seg_off = seg_len = 0;
+    msg_hash = rtr_hash = drop_hash = 0;
+    n_msgs = n_rtr = n_drop_ent = n_drop_ri = 0;
+    q_new = false;
+    {
+      const u32 until = P.iso_until[g];
+      iso = round < until ? P.iso_mask[g] : (u8)0;
+    }
+    ctr.v[C_STEPS]++;
+    const u64 committed0 = committed;
+    const u64 term0 = term, vote0 = vote;
+    // client input of this round goes to replicas that lead at round start
+    u32 inp = role == R_Leader ? wl_input(C, cid, round) : 0u;
+    ExtIn ext;
+    ext.kind = 0;
+    ext.len = 0;
+    ext.lo = ext.hi = ext.ctx_low = ext.ctx_high = ext.pad = 0;
+    if (C.ext_inputs) {
+      ext = P.ext[r];
+      if (ext.kind) {
+        ExtIn z;
+        z.kind = 0;
+        z.len = 0;
+        z.lo = z.hi = z.ctx_low = z.ctx_high = z.pad = 0;
+        P.ext[r] = z;
+        inp = ext.kind;
+      }
+    }
+    // handleReadIndexRequests (node.go:1108-1118)
+    if (inp == 2) {
+      q_record_activity(M_ReadIndex);
+      ctr.v[C_READS]++;
+    }
+    // handleReceivedMessages (node.go:1171-1205): inbox in (sender, stream) order
+    const u32 ppar = par ^ 1u;
+    if (round > 0) {
+      const u16* cnt = &P.cnt[ppar][g * N * N];
+      for (u32 s = 0; s < N; s++) {
+        if (s == k) continue;
+        const u32 pc = cnt[s * N + k];
+        if (pc == 0) continue;
+        const u32 na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
+        if (pc & 0x8000u) {  // Quiesce (node.go:1207-1210)
+          ctr.v[C_MSG_IN]++;
+          q_try_enter();
+        }
+        const Msg* lst = &P.msgs[ppar][msg_slot_base(s, k)];
+        const Ent* sarena = &P.arena[ppar][(g * N + s) * (u64)C.ecap];
+        for (u32 i = 0; i < na + nb; i++) {
+          const Msg m = i < na ? lst[i] : lst[C.maxm - 1u - (i - na)];
+          ctr.v[C_MSG_IN]++;
+          ctr.v[C_ENT_IN] += m.n_ent;
+          // tryRecordNodeActivity (node.go:1161-1169)
+          if ((m.type == M_Heartbeat || m.type == M_HeartbeatResp) && m.hint > 0)
+            q_record_activity(M_ReadIndex);
+          else
+            q_record_activity(m.type);
+          handle(m, m.n_ent ? sarena + m.ent_off : (const Ent*)0);
+        }
+      }
+    }
+    if (inp == 2) {  // batchedReadIndex (node.go:1379-1382) → Peer.ReadIndex
+      Msg m = mk(M_ReadIndex, 0);
+      if (C.ext_inputs && ext.kind == 2) {
+        m.hint = ext.ctx_low;
+        m.hint_high = ext.ctx_high;
+      } else {
+        m.hint = ((u64)(round + 1) << 32) | (u64)self;
+        m.hint_high = cid + 1;
+      }
+      handle(m, (const Ent*)0);
+    }
+    // handleLocalTickMessage → node.tick (node.go:1384-1399): one tick per round
+    q_increase_tick();
+    if (q_quiesced()) {
+      quiesced_tick();
+      ctr.v[C_QUIESCED_TICKS]++;
+    } else {
+      flags &= (u8)~HF_RAFT_QUIESCE;  // raft.tick: r.quiesce = false
+      raft_tick();
+      ctr.v[C_ACTIVE_TICKS]++;
+    }
+    // handleProposals (node.go:1091-1106) → Peer.ProposeEntries
+    if (inp == 1) {
+      Ent e;
+      e.term = 0;
+      e.type = E_Application;
+      if (C.ext_inputs && ext.kind == 1) {
+        e.len = ext.len;
+        e.lo = ext.lo;
+        e.hi = ext.hi;
+      } else {
+        e.len = 16;
+        e.lo = wl_payload_lo(C.seed, cid, round);
+        e.hi = mix64(e.lo);
+      }
+      Msg m = mk(M_Propose, 0);
+      m.from = self;  // Peer.ProposeEntries (peer.go:117-123)
+      m.n_ent = 1;
+      handle(m, &e);
+      ctr.v[C_PROPOSALS]++;
+    }
+    // stepNode: newQuiesceState → sendEnterQuiesceMessages (node.go:873-886)
+    const bool send_q = q_new;
+    if (send_q) {
+      for (u32 d = 0; d < N; d++) {
+        if (d == k) continue;
+        if (((iso >> k) & 1u) || ((iso >> d) & 1u)) {
+          ctr.v[C_MSG_DROPPED]++;
+          continue;
+        }
+        add_pc(d, 0x8000u);
+        ctr.v[C_MSG_OUT]++;
+      }
+    }
+    // getUpdate / Commit (peer.go:201-293): the harness persists and applies
+    // everything at once, so savedTo := lastIndex and processed := committed.
+    Upd u;
+    u.save_lo = saved_to + 1;
+    u.save_hi = last;
+    u.apply_lo = processed + 1;
+    u.apply_hi = committed;
+    if (committed > processed) {
+      u64 cnt = limit_count(processed + 1, committed);
+      u.apply_hi = processed + cnt;
+    }
+    u64 apply_hash = 0;
+    if (C.trace && u.apply_hi >= u.apply_lo) {
+      for (u64 i = u.apply_lo; i <= u.apply_hi; i++) {
+        if (last - i >= C.ring) {
+          set_fault(F_WINDOW);
+          break;
+        }
+        u64 s = ring_slot(i);
+        Body b = P.pay_ring[s];
+        apply_hash = hfold(apply_hash, i);
+        apply_hash = hfold(apply_hash, P.term_ring[s]);
+        apply_hash = hfold(apply_hash, (u64)b.type | ((u64)b.len << 32));
+        apply_hash = hfold(apply_hash, b.lo);
+        apply_hash = hfold(apply_hash, b.hi);
+      }
+    }
+    if (u.apply_hi >= u.apply_lo) ctr.v[C_ENT_APPLIED] += (u32)(u.apply_hi - u.apply_lo + 1);
+    if (u.save_hi >= u.save_lo) ctr.v[C_ENT_SAVED] += (u32)(u.save_hi - u.save_lo + 1);
+    if (n_rtr) ctr.v[C_READS_CONFIRMED] += n_rtr;
+    ctr.v[C_DROPPED_PROPOSALS] += n_drop_ent;
+    ctr.v[C_DROPPED_READS] += n_drop_ri;
+    if (u.apply_hi >= u.apply_lo) processed = u.apply_hi;
+    saved_to = last;
+    if (role == R_Leader) {
+      ctr.v[C_COMMITTED] += (u32)(committed - committed0);
+      ctr.v[C_LEADER_STEPS]++;
+    }
+    u64 d = digest0;
+    if (C.trace) {
+      u64 dh = drop_hash;
+      for (u32 i = 0; i < n_drop_ri; i++) {
+        DropRI x = P.dri[r * C.dri_cap + i];
+        dh = hfold(dh, x.low);
+        dh = hfold(dh, x.high);
+      }
+      d = hfold(d, round);
+      d = hfold(d, (u64)role | ((u64)(q_quiesced() ? 1 : 0) << 8) | ((u64)(send_q ? 1 : 0) << 9) |
+                       ((u64)((flags & HF_RAFT_QUIESCE) ? 1 : 0) << 10));
+      d = hfold(d, term);
+      d = hfold(d, vote);
+      d = hfold(d, leader);
+      d = hfold(d, committed);
+      d = hfold(d, last);
+      d = hfold(d, processed);
+      d = hfold(d, (u64)etick | ((u64)htick << 32));
+      d = hfold(d, ret);
+      d = hfold(d, msg_hash);
+      d = hfold(d, n_msgs);
+      d = hfold(d, rtr_hash);
+      d = hfold(d, apply_hash);
+      d = hfold(d, dh);
+    }
+    u.digest = d;
+    u.n_msgs = n_msgs;
+    u.n_rtr = n_rtr;
+    u.n_drop_ent = n_drop_ent;
+    u.n_drop_ri = n_drop_ri;
+    u.fault = fault;
+    u.flags = (term != term0 || vote != vote0 || committed != committed0 ? UF_STATE_CHANGED : 0u) |
+              (send_q ? UF_SENT_QUIESCE : 0u);
+    P.upd[r] = u;
+    // this round's outbox counts for every destination (zeros included)
+    u16* cnt = &P.cnt[par][g * N * N + k * N];
+    for (u32 dd = 0; dd < N; dd++) cnt[dd] = (u16)get_pc(dd);
+    store();
+  }
+};
+
+template <int N>
+RBE_HD void Lane<N>::raft_tick() {  // raft.go:551-564
+  flags &= (u8)~HF_RAFT_QUIESCE;
+  if (role == R_Leader) leader_tick();
+  else non_leader_tick();
+}
+
+template <int N>
+RBE_HD void step_replica(const Planes& P, const Params& C, u64 r, u32 round, StepCounters& ctr) {
+  Lane<N> lane(P, C, r, round, ctr);
+  lane.run();
+}
+
+// ------------------------------------------------------------------ launch
+// Launch (peer.go:64-86) + bootstrap (peer.go:378-408) for one replica:
+// newRaft → becomeFollower(0) draws a timeout, Launch → becomeFollower(1)
+// draws another; N config-change entries at term 1, committed; remotes
+// {match 0, next N+1}.
+template <int N>
+RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
+  const u32 k = (u32)(r % N);
+  const u64 cid = C.cid_base + (r / N) * C.cid_stride;
+  const u64 self = k + 1;
+  Hot h;
+  h.role = R_Follower;
+  h.flags = 0;
+  h.votes_resp = h.votes_granted = 0;
+  h.election_tick = 0;
+  h.heartbeat_tick = 0;
+  u64 rt = rto_rand(C.seed, cid, self, 1) % C.election_rtt;  // the second draw wins
+  h.rand_et = (u16)(C.election_rtt + rt);
+  h.q_tick = h.q_quiesced_since = h.q_no_activity_since = h.q_exit_quiesce_tick = 0;
+  h.rng_count = 2;
+  P.hot[r] = h;
+  Core c;
+  c.term = 1;
+  c.committed = N;
+  c.last_index = N;
+  c.processed = 0;
+  c.saved_to = 0;
+  c.vote = 0;
+  c.leader = 0;
+  c.ltt = 0;
+  c.rq_head = c.rq_count = 0;
+  c.pad[0] = c.pad[1] = c.pad[2] = 0;
+  c.pad2[0] = c.pad2[1] = 0;
+  P.core[r] = c;
+  for (u32 s = 0; s < N; s++) {
+    RemoteMN x;
+    x.match = 0;
+    x.next = N + 1;
+    P.rem[r * N + s] = x;
+    P.rem_st[r * N + s] = 0;
+  }
+  for (u32 i = 1; i <= N; i++) {
+    u64 slot = (i & (u64)(C.ring - 1)) * C.n_rep + r;
+    P.term_ring[slot] = 1;
+    Body b;
+    b.type = E_ConfigChange;
+    b.len = 8;
+    b.lo = 0xCC00000000000000ULL | (u64)i;
+    b.hi = 0;
+    P.pay_ring[slot] = b;
+  }
+  Upd u;
+  u.digest = 0;
+  u.save_lo = 1;
+  u.save_hi = 0;
+  u.apply_lo = 1;
+  u.apply_hi = 0;
+  u.n_msgs = u.n_rtr = u.n_drop_ent = u.n_drop_ri = 0;
+  u.fault = 0;
+  u.flags = 0;
+  P.upd[r] = u;
+}
+
+// fault schedule: at epoch rounds, isolate the replicas of
+// selected groups that lead at round start; one lane per group.
+template <int N>
+RBE_HD void iso_group(const Planes& P, const Params& C, u64 g, u32 round) {
+  const u64 cid = C.cid_base + g * C.cid_stride;
+  if (!iso_selected(C, cid, round / C.iso_period)) return;
+  u32 mask = 0;
+  for (u32 k = 0; k < N; k++)
+    if (P.hot[g * N + k].role == R_Leader) mask |= 1u << k;
+  if (mask) {
+    P.iso_mask[g] = (u8)mask;
+    P.iso_until[g] = round + C.iso_len;
+  }
+}
+
+}  // namespace rbe

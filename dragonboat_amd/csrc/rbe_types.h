@@ -1,0 +1,218 @@
+// MI355X batched Raft step engine — struct-of-arrays layout in HBM.
+//
+// The per-group protocol state that dragonboat's internal/raft keeps in Go
+// structs and maps (raft.go:197-232 raft, remote.go:62-69 remote,
+// readindex.go:31-34 readIndex, inmemory.go:36-44 inMemory) lives here as
+// planes indexed by the global replica index r = g * N + k (group g, replica
+// slot k, node ID k + 1).  See DESIGN.md §Data layout for the byte budget.
+#pragma once
+#include <stdint.h>
+
+namespace rbe {
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+typedef uint16_t u16;
+typedef uint8_t u8;
+
+// raftpb MessageType, raft.pb.go:23-51
+enum : u32 {
+  M_LocalTick = 0, M_Election = 1, M_LeaderHeartbeat = 2, M_ConfigChangeEvent = 3,
+  M_NoOP = 4, M_Ping = 5, M_Pong = 6, M_Propose = 7, M_SnapshotStatus = 8,
+  M_Unreachable = 9, M_CheckQuorum = 10, M_BatchedReadIndex = 11, M_Replicate = 12,
+  M_ReplicateResp = 13, M_RequestVote = 14, M_RequestVoteResp = 15,
+  M_InstallSnapshot = 16, M_Heartbeat = 17, M_HeartbeatResp = 18, M_ReadIndex = 19,
+  M_ReadIndexResp = 20, M_Quiesce = 21, M_SnapshotReceived = 22,
+  M_LeaderTransfer = 23, M_TimeoutNow = 24, M_RateLimit = 25
+};
+
+// raft State, raft.go:63-70 (observer/witness are host slow path)
+enum : u8 { R_Follower = 0, R_Candidate = 1, R_Leader = 2, R_Observer = 3, R_Witness = 4 };
+// remote flow-control states, remote.go:27-32
+enum : u8 { RS_Retry = 0, RS_Wait = 1, RS_Replicate = 2, RS_Snapshot = 3 };
+// entry types, raft.pb.go:138-141
+enum : u32 { E_Application = 0, E_ConfigChange = 1, E_Encoded = 2, E_Metadata = 3 };
+
+// sticky per-replica fault bits (the engine-side analog of plog.Panicf: the
+// replica stops being trustworthy, the engine keeps running, the host sees it)
+enum : u32 {
+  F_WINDOW = 1u << 0,       // term/payload ring miss (entry older than the ring window)
+  F_OUTBOX = 1u << 1,       // more than maxm messages to one destination in a round
+  F_ARENA = 1u << 2,        // per-round entry arena full
+  F_READQ = 1u << 3,        // readIndex queue full
+  F_RTR = 1u << 4,          // ReadyToRead output list full
+  F_PANIC = 1u << 5,        // a reference panic condition (e.g. commitTo > lastIndex)
+  F_UNSUPPORTED = 1u << 6,  // a slow-path message/entry type reached the device
+  F_DROPLIST = 1u << 7,     // dropped-ReadIndex output list full
+};
+
+// hot plane: everything a quiesced tick touches (32 B per replica)
+struct alignas(16) Hot {
+  u8 role;
+  u8 flags;          // HF_* below
+  u8 votes_resp;     // bit (id-1): a RequestVoteResp was counted from id (raft.votes keys)
+  u8 votes_granted;  // bit (id-1): that response granted the vote (raft.votes values)
+  u32 election_tick;
+  u16 heartbeat_tick;
+  u16 rand_et;       // randomizedElectionTimeout
+  u32 q_tick;        // quiesceManager (quiesce.go:23-33)
+  u32 q_quiesced_since;
+  u32 q_no_activity_since;
+  u32 q_exit_quiesce_tick;
+  u32 rng_count;     // randomized timeouts drawn so far (injected PRNG counter)
+};
+enum : u8 {
+  HF_RAFT_QUIESCE = 1,  // raft.quiesce
+  HF_PENDING_CC = 2,    // raft.pendingConfigChange
+  HF_IS_LTT = 4,        // raft.isLeaderTransferTarget
+};
+
+// core plane (64 B per replica)
+struct alignas(16) Core {
+  u64 term;
+  u64 committed;   // entryLog.committed
+  u64 last_index;  // entryLog.lastIndex()
+  u64 processed;   // entryLog.processed == node smAppliedIndex after each step
+  u64 saved_to;    // inMemory.savedTo
+  u8 vote;         // node IDs are slot+1; 0 = NoNode
+  u8 leader;
+  u8 ltt;          // leaderTransferTarget
+  u8 rq_head;      // readIndex queue ring head
+  u8 rq_count;
+  u8 pad[3];
+  u64 pad2[2];
+};
+
+// remote slot (remote.go:62-69): match/next; state|active<<2 lives in a u8 plane
+struct alignas(16) RemoteMN {
+  u64 match;
+  u64 next;
+};
+
+// readIndex queue entry (readindex.go:24-29): 32 B
+struct alignas(16) ReadReq {
+  u64 low, high;   // SystemCtx
+  u64 index;
+  u8 from;         // node id (0 = local)
+  u8 confirmed;    // bit (id-1) per confirming node
+  u8 pad[6];
+};
+
+// payload ring body (24 B): the entry fields besides Index/Term
+struct Body {
+  u32 type;
+  u32 len;   // Cmd length, <= 16
+  u64 lo, hi;  // Cmd bytes, little endian
+};
+
+// message record in a per-(sender,dest) outbox list: 64 B
+struct alignas(16) Msg {
+  u8 type, from, to, reject;
+  u16 n_ent;
+  u16 pad0;
+  u32 ent_off;  // offset of the first entry in the sender's per-round arena
+  u32 pad1;
+  u64 term, log_term, log_index, commit, hint, hint_high;
+};
+
+// arena entry: 32 B (index implicit: log_index + 1 + i for Replicate)
+struct alignas(16) Ent {
+  u64 term;
+  u32 type;
+  u32 len;
+  u64 lo, hi;
+};
+
+// per-replica step output record (Update summary)
+struct alignas(16) Upd {
+  u64 digest;       // running trace digest (trace mode)
+  u64 save_lo;      // EntriesToSave = [save_lo, save_hi] (empty if lo > hi)
+  u64 save_hi;
+  u64 apply_lo;     // CommittedEntries = [apply_lo, apply_hi]
+  u64 apply_hi;
+  u32 n_msgs;       // messages emitted this step (Update.Messages)
+  u32 n_rtr;        // ReadyToReads
+  u32 n_drop_ent;   // DroppedEntries
+  u32 n_drop_ri;    // DroppedReadIndexes
+  u32 fault;        // sticky F_* bits
+  u32 flags;        // UF_* bits
+};
+enum : u32 { UF_STATE_CHANGED = 1, UF_SENT_QUIESCE = 2, UF_HAS_UPDATE = 4 };
+
+struct RTR {  // ReadyToRead, raftpb/raft.go:52-56
+  u64 index, low, high;
+};
+struct DropRI {  // SystemCtx
+  u64 low, high;
+};
+
+// external (host-pushed) client input for one replica, consumed by the next
+// step (rbe_push_proposals / rbe_push_read_index)
+struct alignas(16) ExtIn {
+  u32 kind;  // 0 none, 1 propose, 2 read index
+  u32 len;
+  u64 lo, hi;       // proposal Cmd
+  u64 ctx_low, ctx_high;
+  u64 pad;
+};
+
+// counters (shared numbering with oracle/harness.h HC_*)
+enum : int {
+  C_STEPS = 0, C_COMMITTED = 1, C_MSG_IN = 2, C_MSG_OUT = 3, C_ENT_IN = 4, C_ENT_OUT = 5,
+  C_READS_CONFIRMED = 6, C_PROPOSALS = 7, C_READS = 8, C_QUIESCED_TICKS = 9,
+  C_ACTIVE_TICKS = 10, C_CAMPAIGNS = 11, C_ENT_SAVED = 12, C_ENT_APPLIED = 13,
+  C_MSG_DROPPED = 14, C_DROPPED_PROPOSALS = 15, C_DROPPED_READS = 16, C_LEADER_STEPS = 17,
+  C_REMOTE_TOUCH = 18, C_RING_ACCESS = 19, C_FAULTS = 20, C_RQ_TOUCH = 21,
+  C_NUM = 24
+};
+
+// engine parameters (immutable for a handle)
+struct Params {
+  u64 n_groups;
+  u64 n_rep;          // N * n_groups
+  u64 cid_base;       // cluster id of group g is cid_base + g * cid_stride
+  u64 cid_stride;
+  u64 seed;
+  u64 max_entry_size;
+  u32 n;              // replicas per group (N)
+  u32 ring;           // term/payload ring entries (power of two)
+  u32 rq_cap;         // readIndex queue capacity
+  u32 maxm;           // message slots per (sender, dest) per round
+  u32 ecap;           // arena entries per sender per round
+  u32 rtr_cap;        // ReadyToRead slots per replica per round
+  u32 dri_cap;        // dropped ReadIndex slots per replica per round
+  u32 election_rtt;
+  u32 heartbeat_rtt;
+  u32 check_quorum;
+  u32 quiesce;
+  u32 trace;
+  // workload
+  u32 wl_enabled, wl_start_round, wl_stop_round, wl_active_mod, wl_read_permille;
+  u32 ext_inputs;     // consume host-pushed ExtIn records
+  // faults
+  u32 iso_period, iso_len, iso_mod;
+  u32 pad;
+};
+
+// device pointers of every plane
+struct Planes {
+  Hot* hot;
+  Core* core;
+  RemoteMN* rem;      // [n_rep * N]
+  u8* rem_st;         // [n_rep * N]  state | active << 2
+  ReadReq* rq;        // [n_rep * rq_cap]
+  u64* term_ring;     // [ring][n_rep]
+  Body* pay_ring;     // [ring][n_rep]
+  u16* cnt[2];        // [n_groups * N * N]  A | B << 7 | quiesce << 15
+  Msg* msgs[2];       // [n_groups * N * N * maxm]
+  Ent* arena[2];      // [n_rep * ecap]
+  u8* iso_mask;       // [n_groups]
+  u32* iso_until;     // [n_groups]
+  Upd* upd;           // [n_rep]
+  RTR* rtr;           // [n_rep * rtr_cap]
+  DropRI* dri;        // [n_rep * dri_cap]
+  ExtIn* ext;         // [n_rep]
+  u64* counters;      // [C_NUM]
+};
+
+}  // namespace rbe

@@ -1,0 +1,294 @@
+"""ctypes binding to libdragonboat_amd.so (include/rbe.h).
+
+This is the product path: every call goes to the HIP engine on an MI355X.
+There is no CPU fallback; if the library or a gfx950 device is missing,
+`Engine(...)` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Dict, List, Optional
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libdragonboat_amd.so")
+RBE_ABI_VERSION = 1
+
+COUNTER_NAMES = ["steps", "committed", "msg_in", "msg_out", "ent_in", "ent_out",
+                 "reads_confirmed", "proposals", "reads", "quiesced_ticks", "active_ticks",
+                 "campaigns", "ent_saved", "ent_applied", "msg_dropped", "dropped_proposals",
+                 "dropped_reads", "leader_steps", "remote_touch", "ring_access", "faults",
+                 "rq_touch"]
+CTR_NUM = 24
+
+FAULT_NAMES = {0x01: "WINDOW", 0x02: "OUTBOX", 0x04: "ARENA", 0x08: "READQ", 0x10: "RTR",
+               0x20: "PANIC", 0x40: "UNSUPPORTED", 0x80: "DROPLIST"}
+
+
+class RbeConfig(C.Structure):
+    _fields_ = [("abi_version", C.c_uint32), ("device", C.c_int32), ("n_groups", C.c_uint64),
+                ("n_replicas", C.c_uint32), ("election_rtt", C.c_uint32),
+                ("heartbeat_rtt", C.c_uint32), ("check_quorum", C.c_uint32),
+                ("quiesce", C.c_uint32), ("ring", C.c_uint32), ("rq_cap", C.c_uint32),
+                ("maxm", C.c_uint32), ("ecap", C.c_uint32), ("rtr_cap", C.c_uint32),
+                ("dri_cap", C.c_uint32), ("trace", C.c_uint32), ("cid_base", C.c_uint64),
+                ("cid_stride", C.c_uint64), ("seed", C.c_uint64),
+                ("max_entry_size", C.c_uint64), ("wl_enabled", C.c_uint32),
+                ("wl_start_round", C.c_uint32), ("wl_stop_round", C.c_uint32),
+                ("wl_active_mod", C.c_uint32), ("wl_read_permille", C.c_uint32),
+                ("ext_inputs", C.c_uint32), ("iso_period", C.c_uint32),
+                ("iso_len", C.c_uint32), ("iso_mod", C.c_uint32),
+                ("reserved", C.c_uint32 * 7)]
+
+
+class RbeReplicaView(C.Structure):
+    _fields_ = [("term", C.c_uint64), ("vote", C.c_uint64), ("leader_id", C.c_uint64),
+                ("committed", C.c_uint64), ("last_index", C.c_uint64),
+                ("processed", C.c_uint64), ("saved_to", C.c_uint64), ("digest", C.c_uint64),
+                ("role", C.c_uint32), ("election_tick", C.c_uint32),
+                ("heartbeat_tick", C.c_uint32), ("rand_election_timeout", C.c_uint32),
+                ("q_tick", C.c_uint32), ("q_quiesced_since", C.c_uint32),
+                ("q_no_activity_since", C.c_uint32), ("q_exit_quiesce_tick", C.c_uint32),
+                ("raft_quiesce", C.c_uint32), ("rq_count", C.c_uint32),
+                ("votes_resp", C.c_uint32), ("votes_granted", C.c_uint32),
+                ("match", C.c_uint64 * 8), ("next", C.c_uint64 * 8),
+                ("rstate", C.c_uint32 * 8), ("ractive", C.c_uint32 * 8)]
+
+
+class RbeUpdate(C.Structure):
+    _fields_ = [("term", C.c_uint64), ("vote", C.c_uint64), ("commit", C.c_uint64),
+                ("save_lo", C.c_uint64), ("save_hi", C.c_uint64), ("apply_lo", C.c_uint64),
+                ("apply_hi", C.c_uint64), ("digest", C.c_uint64),
+                ("n_messages", C.c_uint32), ("n_ready_to_read", C.c_uint32),
+                ("n_dropped_entries", C.c_uint32), ("n_dropped_read_indexes", C.c_uint32),
+                ("fault", C.c_uint32), ("flags", C.c_uint32), ("role", C.c_uint32),
+                ("leader_id", C.c_uint32)]
+
+
+class RbeMessage(C.Structure):
+    _fields_ = [("type", C.c_uint32), ("reject", C.c_uint32), ("to", C.c_uint64),
+                ("from_", C.c_uint64), ("cluster_id", C.c_uint64), ("term", C.c_uint64),
+                ("log_term", C.c_uint64), ("log_index", C.c_uint64), ("commit", C.c_uint64),
+                ("hint", C.c_uint64), ("hint_high", C.c_uint64), ("n_entries", C.c_uint32),
+                ("reserved", C.c_uint32)]
+
+
+class RbeEntry(C.Structure):
+    _fields_ = [("index", C.c_uint64), ("term", C.c_uint64), ("type", C.c_uint32),
+                ("cmd_len", C.c_uint32), ("cmd", C.c_uint8 * 16)]
+
+
+class RbeReadyToRead(C.Structure):
+    _fields_ = [("index", C.c_uint64), ("ctx_low", C.c_uint64), ("ctx_high", C.c_uint64)]
+
+
+# exported symbols of include/rbe.h (checked by tests/test_capi.py)
+EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_step", "rbe_run", "rbe_sync",
+           "rbe_round", "rbe_run_timed", "rbe_push_proposals", "rbe_push_read_index",
+           "rbe_get_updates", "rbe_get_messages", "rbe_get_ready_to_reads", "rbe_get_entries",
+           "rbe_get_views", "rbe_get_counters", "rbe_reset_counters", "rbe_fault_summary",
+           "rbe_footprint"]
+
+_lib = None
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def load_library(path: Optional[str] = None):
+    """Load libdragonboat_amd.so; raise if it is missing (no fallback)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise EngineError(
+            f"{p} is missing: the HIP engine is the only implementation; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(p)
+    P = C.POINTER
+    vp, u64, u32, i32 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
+    sig = {
+        "rbe_create": (i32, [P(RbeConfig), P(vp)]),
+        "rbe_destroy": (i32, [vp]),
+        "rbe_abi_version": (i32, []),
+        "rbe_step": (i32, [vp]),
+        "rbe_run": (i32, [vp, u32]),
+        "rbe_sync": (i32, [vp]),
+        "rbe_round": (i32, [vp, P(u32)]),
+        "rbe_run_timed": (i32, [vp, u32, P(C.c_float)]),
+        "rbe_push_proposals": (i32, [vp, u64, P(u64), P(C.c_uint8), P(u32)]),
+        "rbe_push_read_index": (i32, [vp, u64, P(u64), P(u64), P(u64)]),
+        "rbe_get_updates": (i32, [vp, u64, u64, P(RbeUpdate)]),
+        "rbe_get_messages": (i32, [vp, u64, P(RbeMessage), u32, P(u32)]),
+        "rbe_get_ready_to_reads": (i32, [vp, u64, P(RbeReadyToRead), u32, P(u32)]),
+        "rbe_get_entries": (i32, [vp, u64, u64, u64, P(RbeEntry)]),
+        "rbe_get_views": (i32, [vp, u64, u64, P(RbeReplicaView)]),
+        "rbe_get_counters": (i32, [vp, P(u64)]),
+        "rbe_reset_counters": (i32, [vp]),
+        "rbe_fault_summary": (i32, [vp, P(u64), P(u32)]),
+        "rbe_footprint": (i32, [P(RbeConfig), P(u64)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    if L.rbe_abi_version() != RBE_ABI_VERSION:
+        raise EngineError("ABI version mismatch")
+    if path is None:
+        _lib = L
+    return L
+
+
+def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rtt: int = 10,
+                heartbeat_rtt: int = 1, check_quorum: bool = False, quiesce: bool = False,
+                ring: int = 0, rq_cap: int = 0, maxm: int = 0, ecap: int = 0, rtr_cap: int = 0,
+                dri_cap: int = 0, trace: bool = False, cid_base: int = 1, cid_stride: int = 1,
+                seed: int = 0x5EEDD8A6, max_entry_size: int = 0, wl_enabled: bool = False,
+                wl_start_round: int = 0, wl_stop_round: int = 0, wl_active_mod: int = 1,
+                wl_read_permille: int = 0, ext_inputs: bool = False, iso_period: int = 0,
+                iso_len: int = 0, iso_mod: int = 10) -> RbeConfig:
+    return RbeConfig(abi_version=RBE_ABI_VERSION, device=device, n_groups=n_groups,
+                     n_replicas=n_replicas, election_rtt=election_rtt,
+                     heartbeat_rtt=heartbeat_rtt, check_quorum=int(check_quorum),
+                     quiesce=int(quiesce), ring=ring, rq_cap=rq_cap, maxm=maxm, ecap=ecap,
+                     rtr_cap=rtr_cap, dri_cap=dri_cap, trace=int(trace), cid_base=cid_base,
+                     cid_stride=cid_stride, seed=seed, max_entry_size=max_entry_size,
+                     wl_enabled=int(wl_enabled), wl_start_round=wl_start_round,
+                     wl_stop_round=wl_stop_round, wl_active_mod=wl_active_mod,
+                     wl_read_permille=wl_read_permille, ext_inputs=int(ext_inputs),
+                     iso_period=iso_period, iso_len=iso_len, iso_mod=iso_mod)
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        raise EngineError(f"{what} failed with rc={rc}")
+
+
+class Engine:
+    """One batched Raft step engine on one GPU (one rbe_engine handle)."""
+
+    def __init__(self, cfg: Optional[RbeConfig] = None, **kw):
+        self.lib = load_library()
+        self.cfg = cfg if cfg is not None else make_config(**kw)
+        h = C.c_void_p()
+        _check(self.lib.rbe_create(C.byref(self.cfg), C.byref(h)), "rbe_create")
+        self.h = h
+        self.n_groups = self.cfg.n_groups
+        self.n_replicas = self.cfg.n_replicas
+        self.n_rep = self.n_groups * self.n_replicas
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.rbe_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # rounds
+    def step(self):
+        _check(self.lib.rbe_step(self.h), "rbe_step")
+
+    def run(self, rounds: int):
+        _check(self.lib.rbe_run(self.h, rounds), "rbe_run")
+
+    def run_timed(self, rounds: int) -> float:
+        ms = C.c_float()
+        _check(self.lib.rbe_run_timed(self.h, rounds, C.byref(ms)), "rbe_run_timed")
+        return ms.value
+
+    def sync(self):
+        _check(self.lib.rbe_sync(self.h), "rbe_sync")
+
+    @property
+    def round(self) -> int:
+        r = C.c_uint32()
+        _check(self.lib.rbe_round(self.h, C.byref(r)), "rbe_round")
+        return r.value
+
+    # inputs
+    def push_proposals(self, replicas, cmds: List[bytes]):
+        n = len(replicas)
+        rep = (C.c_uint64 * n)(*replicas)
+        buf = (C.c_uint8 * (16 * n))()
+        lens = (C.c_uint32 * n)()
+        for i, c in enumerate(cmds):
+            for j, b in enumerate(c[:16]):
+                buf[16 * i + j] = b
+            lens[i] = min(16, len(c))
+        _check(self.lib.rbe_push_proposals(self.h, n, rep, buf, lens), "rbe_push_proposals")
+
+    def push_read_index(self, replicas, ctxs):
+        n = len(replicas)
+        rep = (C.c_uint64 * n)(*replicas)
+        lo = (C.c_uint64 * n)(*[c[0] for c in ctxs])
+        hi = (C.c_uint64 * n)(*[c[1] for c in ctxs])
+        _check(self.lib.rbe_push_read_index(self.h, n, rep, lo, hi), "rbe_push_read_index")
+
+    # outputs
+    def counters(self) -> Dict[str, int]:
+        o = (C.c_uint64 * CTR_NUM)()
+        _check(self.lib.rbe_get_counters(self.h, o), "rbe_get_counters")
+        return {n: o[i] for i, n in enumerate(COUNTER_NAMES)}
+
+    def reset_counters(self):
+        _check(self.lib.rbe_reset_counters(self.h), "rbe_reset_counters")
+
+    def views(self, first: int = 0, count: Optional[int] = None):
+        count = self.n_rep - first if count is None else count
+        arr = (RbeReplicaView * count)()
+        _check(self.lib.rbe_get_views(self.h, first, count, arr), "rbe_get_views")
+        return arr
+
+    def updates(self, first: int = 0, count: Optional[int] = None):
+        count = self.n_rep - first if count is None else count
+        arr = (RbeUpdate * count)()
+        _check(self.lib.rbe_get_updates(self.h, first, count, arr), "rbe_get_updates")
+        return arr
+
+    def digests(self) -> np.ndarray:
+        u = self.updates()
+        return np.array([x.digest for x in u], dtype=np.uint64)
+
+    def messages(self, replica: int):
+        cap = 256
+        arr = (RbeMessage * cap)()
+        n = C.c_uint32()
+        _check(self.lib.rbe_get_messages(self.h, replica, arr, cap, C.byref(n)),
+               "rbe_get_messages")
+        return [arr[i] for i in range(min(n.value, cap))]
+
+    def ready_to_reads(self, replica: int):
+        cap = 64
+        arr = (RbeReadyToRead * cap)()
+        n = C.c_uint32()
+        _check(self.lib.rbe_get_ready_to_reads(self.h, replica, arr, cap, C.byref(n)),
+               "rbe_get_ready_to_reads")
+        return [(arr[i].index, arr[i].ctx_low, arr[i].ctx_high) for i in range(n.value)]
+
+    def entries(self, replica: int, lo: int, hi: int):
+        arr = (RbeEntry * (hi - lo + 1))()
+        _check(self.lib.rbe_get_entries(self.h, replica, lo, hi, arr), "rbe_get_entries")
+        return [(e.index, e.term, e.type, bytes(e.cmd[:e.cmd_len])) for e in arr]
+
+    def fault_summary(self):
+        n = C.c_uint64()
+        o = C.c_uint32()
+        _check(self.lib.rbe_fault_summary(self.h, C.byref(n), C.byref(o)), "rbe_fault_summary")
+        return n.value, o.value
+
+
+def footprint(cfg: RbeConfig) -> int:
+    b = C.c_uint64()
+    _check(load_library().rbe_footprint(C.byref(cfg), C.byref(b)), "rbe_footprint")
+    return b.value

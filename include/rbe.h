@@ -1,0 +1,218 @@
+/*
+ * rbe.h — C ABI of the MI355X batched Raft step engine (libdragonboat_amd.so).
+ *
+ * Drop-in boundary for dragonboat's step path.  Today the node layer drives
+ * one *raft.Peer per group under raftMu (node.go:79-80, 290) and
+ * execEngine.execNodes calls node.stepNode() for every ready cluster
+ * (execengine.go:494-503).  The engine replaces that per-group loop with one
+ * batched device step over every group a GPU owns.  Each entry point below
+ * names the reference interface it replaces.  The binding a Go maintainer
+ * would add (cgo) is in INTEGRATION.md.
+ *
+ * Conventions (mirroring binding/include/dragonboat/binding.h:107-113):
+ *   - every function returns int: 0 = ok, < 0 = RBE_E_* error;
+ *   - plain pointers and sizes only; host buffers are caller-owned;
+ *   - one handle per GPU, single-threaded per handle (Peer is not
+ *     thread-safe either, node.go:1017-1018);
+ *   - protocol invariant violations (plog.Panicf in the reference) do not
+ *     abort the process: they set a sticky per-replica fault word
+ *     (RBE_FAULT_*) that rbe_get_updates/rbe_get_views report.
+ *
+ * Node IDs inside a group are 1..n (slot + 1); the group of cluster id c is
+ * the engine-local index g with c = cid_base + g * cid_stride, which is
+ * dragonboat's FixedPartitioner rule (internal/server/partition.go:38-40)
+ * when cid_stride = number of GPUs and cid_base = 1 + rank.
+ */
+#ifndef DRAGONBOAT_AMD_RBE_H_
+#define DRAGONBOAT_AMD_RBE_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RBE_ABI_VERSION 1
+
+/* error codes */
+#define RBE_OK 0
+#define RBE_E_INVALID (-1)   /* bad argument / configuration */
+#define RBE_E_HIP (-2)       /* a HIP runtime call failed */
+#define RBE_E_NOMEM (-3)     /* device allocation failed */
+#define RBE_E_NODEV (-4)     /* no usable gfx950 device */
+#define RBE_E_STATE (-5)     /* call not valid in the current state */
+
+/* sticky per-replica fault bits (see dragonboat_amd/csrc/rbe_types.h) */
+#define RBE_FAULT_WINDOW 0x01u
+#define RBE_FAULT_OUTBOX 0x02u
+#define RBE_FAULT_ARENA 0x04u
+#define RBE_FAULT_READQ 0x08u
+#define RBE_FAULT_RTR 0x10u
+#define RBE_FAULT_PANIC 0x20u
+#define RBE_FAULT_UNSUPPORTED 0x40u
+#define RBE_FAULT_DROPLIST 0x80u
+
+/* counter slots (rbe_get_counters) */
+enum rbe_counter {
+  RBE_CTR_STEPS = 0,           /* replica-steps (group-steps metric) */
+  RBE_CTR_COMMITTED = 1,       /* entries committed, counted once per group at its leader */
+  RBE_CTR_MSG_IN = 2,
+  RBE_CTR_MSG_OUT = 3,
+  RBE_CTR_ENT_IN = 4,
+  RBE_CTR_ENT_OUT = 5,
+  RBE_CTR_READS_CONFIRMED = 6, /* ReadyToRead records (ReadIndex confirmations) */
+  RBE_CTR_PROPOSALS = 7,
+  RBE_CTR_READS = 8,
+  RBE_CTR_QUIESCED_TICKS = 9,
+  RBE_CTR_ACTIVE_TICKS = 10,
+  RBE_CTR_CAMPAIGNS = 11,
+  RBE_CTR_ENT_SAVED = 12,
+  RBE_CTR_ENT_APPLIED = 13,
+  RBE_CTR_MSG_DROPPED = 14,
+  RBE_CTR_DROPPED_PROPOSALS = 15,
+  RBE_CTR_DROPPED_READS = 16,
+  RBE_CTR_LEADER_STEPS = 17,
+  RBE_CTR_REMOTE_TOUCH = 18,
+  RBE_CTR_RING_ACCESS = 19,
+  RBE_CTR_FAULTS = 20,
+  RBE_CTR_RQ_TOUCH = 21,
+  RBE_CTR_NUM = 24
+};
+
+/*
+ * Engine configuration.  Protocol fields mirror config.Config
+ * (config/config.go:60-171): ElectionRTT, HeartbeatRTT, CheckQuorum, Quiesce;
+ * MaxInMemLogSize is 0 (rate limiter off).  max_entry_size mirrors
+ * settings.Soft.MaxEntrySize (soft.go:226).
+ */
+typedef struct rbe_config {
+  uint32_t abi_version;      /* RBE_ABI_VERSION */
+  int32_t device;            /* HIP device ordinal */
+  uint64_t n_groups;         /* groups owned by this engine */
+  uint32_t n_replicas;       /* voting replicas per group: 1, 3 or 5 */
+  uint32_t election_rtt;     /* ticks, config.ElectionRTT */
+  uint32_t heartbeat_rtt;    /* ticks, config.HeartbeatRTT */
+  uint32_t check_quorum;     /* config.CheckQuorum */
+  uint32_t quiesce;          /* config.Quiesce */
+  uint32_t ring;             /* in-memory entry window per replica (power of 2), 0 = 64 */
+  uint32_t rq_cap;           /* pending ReadIndex requests per leader, 0 = 8 */
+  uint32_t maxm;             /* message slots per (sender, destination) per round, 0 = 12 */
+  uint32_t ecap;             /* entry slots per sender per round, 0 = 2 * ring */
+  uint32_t rtr_cap;          /* ReadyToRead slots per replica per round, 0 = 8 */
+  uint32_t dri_cap;          /* dropped ReadIndex slots per replica per round, 0 = 8 */
+  uint32_t trace;            /* maintain per-replica trace digests */
+  uint64_t cid_base;         /* cluster id of group g = cid_base + g * cid_stride */
+  uint64_t cid_stride;       /* 0 = 1 */
+  uint64_t seed;             /* injected PRNG seed (election timeouts, workload) */
+  uint64_t max_entry_size;   /* bytes, 0 = 64 MiB */
+  /* synthetic client workload; wl_enabled = 0 disables */
+  uint32_t wl_enabled;
+  uint32_t wl_start_round;
+  uint32_t wl_stop_round;    /* 0 = never stop */
+  uint32_t wl_active_mod;    /* group active iff mix(seed, cid) % mod == 0 (1 = all) */
+  uint32_t wl_read_permille; /* read with probability p/1000, else propose */
+  uint32_t ext_inputs;       /* accept rbe_push_proposals / rbe_push_read_index */
+  /* fault schedule (network.isolate of the current leader), 0 = off */
+  uint32_t iso_period;
+  uint32_t iso_len;
+  uint32_t iso_mod;
+  uint32_t reserved[7];
+} rbe_config;
+
+/* Snapshot of one replica (tests, debugging, rbe_get_views). */
+typedef struct rbe_replica_view {
+  uint64_t term, vote, leader_id, committed, last_index, processed, saved_to, digest;
+  uint32_t role, election_tick, heartbeat_tick, rand_election_timeout;
+  uint32_t q_tick, q_quiesced_since, q_no_activity_since, q_exit_quiesce_tick;
+  uint32_t raft_quiesce, rq_count, votes_resp, votes_granted;
+  uint64_t match[8], next[8];
+  uint32_t rstate[8], ractive[8];
+} rbe_replica_view;
+
+/* Per-replica step result: the Update of peer.go:201-207 / raftpb Update
+ * (raftpb/raft.go:74-110) in range form.  Entries stay in the engine's ring
+ * and are fetched with rbe_get_entries. */
+typedef struct rbe_update {
+  uint64_t term, vote, commit;  /* pb.State (valid when flags & RBE_UF_STATE_CHANGED) */
+  uint64_t save_lo, save_hi;    /* EntriesToSave = [save_lo, save_hi] */
+  uint64_t apply_lo, apply_hi;  /* CommittedEntries = [apply_lo, apply_hi] */
+  uint64_t digest;              /* trace digest */
+  uint32_t n_messages, n_ready_to_read, n_dropped_entries, n_dropped_read_indexes;
+  uint32_t fault, flags;
+  uint32_t role, leader_id;
+} rbe_update;
+#define RBE_UF_STATE_CHANGED 1u
+#define RBE_UF_SENT_QUIESCE 2u
+
+/* raftpb Message (raft.pb.go:1019-1033) as emitted by the engine. */
+typedef struct rbe_message {
+  uint32_t type, reject;
+  uint64_t to, from, cluster_id, term, log_term, log_index, commit, hint, hint_high;
+  uint32_t n_entries, reserved;
+} rbe_message;
+
+/* raftpb Entry (raft.pb.go:589-598): Index/Term/Type + up to 16 Cmd bytes. */
+typedef struct rbe_entry {
+  uint64_t index, term;
+  uint32_t type, cmd_len;
+  uint8_t cmd[16];
+} rbe_entry;
+
+typedef struct rbe_ready_to_read {  /* raftpb ReadyToRead, raftpb/raft.go:52-56 */
+  uint64_t index, ctx_low, ctx_high;
+} rbe_ready_to_read;
+
+typedef struct rbe_engine rbe_engine;
+
+/* Lifecycle.  Replaces the per-group raft.Launch / newRaft (peer.go:64-86,
+ * raft.go:234-289): creates every group's replicas and bootstraps them with
+ * peer.go:378-408 semantics (initial = true, newNode = true). */
+int rbe_create(const rbe_config* cfg, rbe_engine** out);
+int rbe_destroy(rbe_engine* e);
+int rbe_abi_version(void);
+
+/* One lockstep round for every replica: the stepNode/handleEvents/getUpdate/
+ * Commit sequence of node.go:1016-1067, 907-994 driven by execEngine.execNodes
+ * (execengine.go:474-560), with messages of round r delivered in round r+1
+ * (DESIGN.md §Round semantics).  rbe_run runs `rounds` rounds back to back
+ * (HIP-graph replay when the configuration allows). */
+int rbe_step(rbe_engine* e);
+int rbe_run(rbe_engine* e, uint32_t rounds);
+int rbe_sync(rbe_engine* e);
+int rbe_round(const rbe_engine* e, uint32_t* round);
+
+/* Time `rounds` rounds with HIP events on the engine stream; *ms = elapsed. */
+int rbe_run_timed(rbe_engine* e, uint32_t rounds, float* ms);
+
+/* Client input for the next round.  Replaces Peer.ProposeEntries (peer.go:117)
+ * and Peer.ReadIndex (peer.go:297); requires cfg.ext_inputs.  replica =
+ * g * n_replicas + (node_id - 1). */
+int rbe_push_proposals(rbe_engine* e, uint64_t n, const uint64_t* replica,
+                       const uint8_t* cmd16, const uint32_t* cmd_len);
+int rbe_push_read_index(rbe_engine* e, uint64_t n, const uint64_t* replica,
+                        const uint64_t* ctx_low, const uint64_t* ctx_high);
+
+/* Results of the last round.  Replaces Peer.GetUpdate (peer.go:201-207);
+ * Peer.Commit (peer.go:282-293) is implicit (the harness persists and
+ * applies every round). */
+int rbe_get_updates(rbe_engine* e, uint64_t first, uint64_t count, rbe_update* out);
+int rbe_get_messages(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t cap,
+                     uint32_t* n_out);
+int rbe_get_ready_to_reads(rbe_engine* e, uint64_t replica, rbe_ready_to_read* out,
+                           uint32_t cap, uint32_t* n_out);
+int rbe_get_entries(rbe_engine* e, uint64_t replica, uint64_t lo, uint64_t hi,
+                    rbe_entry* out);
+int rbe_get_views(rbe_engine* e, uint64_t first, uint64_t count, rbe_replica_view* out);
+int rbe_get_counters(rbe_engine* e, uint64_t* out /* RBE_CTR_NUM */);
+int rbe_reset_counters(rbe_engine* e);
+/* number of replicas whose sticky fault word is non-zero, and the OR of all */
+int rbe_fault_summary(rbe_engine* e, uint64_t* n_faulty, uint32_t* fault_or);
+
+/* Device memory footprint (bytes) of a configuration, without allocating. */
+int rbe_footprint(const rbe_config* cfg, uint64_t* bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DRAGONBOAT_AMD_RBE_H_ */

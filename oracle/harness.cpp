@@ -178,7 +178,7 @@ Harness* harness_create(const HarnessConfig& cfg) {
     addrs.push_back({k + 1, "node-" + std::to_string(k + 1)});
   for (u64 g = 0; g < cfg.n_groups; g++) {
     Group* gr = new Group();
-    gr->cid = cfg.cid_base + g;
+    gr->cid = cfg.cid_base + g * cfg.cid_stride;
     for (u32 k = 0; k < cfg.n_replicas; k++) {
       Node* n = new Node();
       Config c;

@@ -41,7 +41,8 @@ enum HarnessCounter {
 struct HarnessConfig {
   u64 n_groups = 1;
   u32 n_replicas = 3;
-  u64 cid_base = 1;            // cluster id of group g is cid_base + g
+  u64 cid_base = 1;            // cluster id of group g is cid_base + g * cid_stride
+  u64 cid_stride = 1;
   u64 election_rtt = 10;
   u64 heartbeat_rtt = 1;
   bool check_quorum = false;

@@ -76,7 +76,8 @@ class OrcHarnessConfig(C.Structure):
                 ("wl_start_round", C.c_uint32), ("wl_stop_round", C.c_uint32),
                 ("wl_active_mod", C.c_uint32), ("wl_read_permille", C.c_uint32),
                 ("iso_period", C.c_uint32), ("iso_len", C.c_uint32), ("iso_mod", C.c_uint32),
-                ("trace", C.c_uint32), ("threads", C.c_uint32), ("pad", C.c_uint32)]
+                ("trace", C.c_uint32), ("threads", C.c_uint32), ("pad", C.c_uint32),
+                ("cid_stride", C.c_uint64)]
 
 
 class ReplicaView(C.Structure):
@@ -842,7 +843,7 @@ class Harness:
                  check_quorum=False, quiesce=False, seed=0x5EEDD8A6, max_entry_size=0,
                  wl_enabled=False, wl_start_round=0, wl_stop_round=0, wl_active_mod=1,
                  wl_read_permille=0, iso_period=0, iso_len=0, iso_mod=10, trace=True,
-                 threads=1):
+                 threads=1, cid_stride=1):
         c = OrcHarnessConfig(
             n_groups=n_groups, n_replicas=n_replicas, check_quorum=int(check_quorum),
             cid_base=cid_base, election_rtt=election_rtt, heartbeat_rtt=heartbeat_rtt,
@@ -850,7 +851,7 @@ class Harness:
             wl_enabled=int(wl_enabled), wl_start_round=wl_start_round,
             wl_stop_round=wl_stop_round, wl_active_mod=wl_active_mod,
             wl_read_permille=wl_read_permille, iso_period=iso_period, iso_len=iso_len,
-            iso_mod=iso_mod, trace=int(trace), threads=threads)
+            iso_mod=iso_mod, trace=int(trace), threads=threads, cid_stride=cid_stride)
         self.n_groups, self.n_replicas = n_groups, n_replicas
         self.h = lib().orc_harness_create(C.byref(c))
         if not self.h:

@@ -44,6 +44,7 @@ typedef struct {
   uint32_t quiesce, wl_enabled, wl_start_round, wl_stop_round;
   uint32_t wl_active_mod, wl_read_permille, iso_period, iso_len;
   uint32_t iso_mod, trace, threads, pad;
+  uint64_t cid_stride;
 } orc_harness_config;
 
 static thread_local std::string g_err;
@@ -739,6 +740,7 @@ void* orc_harness_create(const orc_harness_config* c) {
   h.n_groups = c->n_groups;
   h.n_replicas = c->n_replicas;
   h.cid_base = c->cid_base;
+  h.cid_stride = c->cid_stride ? c->cid_stride : 1;
   h.election_rtt = c->election_rtt;
   h.heartbeat_rtt = c->heartbeat_rtt;
   h.check_quorum = c->check_quorum != 0;

@@ -1,0 +1,62 @@
+"""TEST-ONLY wrapper of libsoa_cpu.so (host build of the device step function).
+
+Never imported by the dragonboat_amd package; see soa_cpu.cpp.
+"""
+import ctypes as C
+import os
+
+from dragonboat_amd.engine import CTR_NUM, COUNTER_NAMES, RbeReplicaView, make_config
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        p = os.path.join(_HERE, "libsoa_cpu.so")
+        if not os.path.exists(p):
+            raise RuntimeError(f"{p} missing: run __graft_entry__.build()")
+        L = C.CDLL(p)
+        L.soa_create.restype = C.c_void_p
+        L.soa_create.argtypes = [C.c_void_p]
+        L.soa_destroy.argtypes = [C.c_void_p]
+        L.soa_run.argtypes = [C.c_void_p, C.c_uint32]
+        L.soa_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+        L.soa_views.argtypes = [C.c_void_p, C.c_void_p]
+        L.soa_faults.restype = C.c_uint32
+        L.soa_faults.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+        _lib = L
+    return _lib
+
+
+class SoaCpu:
+    def __init__(self, **kw):
+        self.cfg = make_config(**kw)
+        self.n_rep = self.cfg.n_groups * self.cfg.n_replicas
+        self.h = lib().soa_create(C.byref(self.cfg))
+        if not self.h:
+            raise RuntimeError("soa_create failed")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().soa_destroy(self.h)
+            self.h = None
+
+    def run(self, rounds=1):
+        lib().soa_run(self.h, rounds)
+
+    def views(self):
+        arr = (RbeReplicaView * self.n_rep)()
+        lib().soa_views(self.h, C.cast(arr, C.c_void_p))
+        return arr
+
+    def counters(self):
+        o = (C.c_uint64 * CTR_NUM)()
+        lib().soa_counters(self.h, o)
+        return {n: o[i] for i, n in enumerate(COUNTER_NAMES)}
+
+    def faults(self):
+        n = C.c_uint64()
+        o = lib().soa_faults(self.h, C.byref(n))
+        return n.value, o

@@ -1,0 +1,176 @@
+// TEST-ONLY host build of the device step function (dragonboat_amd/csrc/rbe_step.h).
+//
+// The CPU test tier has no GPU, so the SoA protocol logic that k_step<N> runs
+// on MI355X is compiled here for the host and diffed against the oracle
+// harness round by round (tests/test_soa_cpu_parity.py).  This library is
+// never loaded by the dragonboat_amd package or by any -m gpu test: the GPU
+// parity tests call libdragonboat_amd.so through the C ABI.
+#include <cstring>
+#include <vector>
+
+#include "../../dragonboat_amd/csrc/rbe_step.h"
+#include "../../include/rbe.h"
+
+using namespace rbe;
+
+struct SoaEngine {
+  Params C;
+  Planes P;
+  std::vector<std::vector<uint8_t>> bufs;
+  u32 round = 0;
+  u64 counters[C_NUM] = {0};
+};
+
+template <typename T>
+static T* alloc(SoaEngine* e, u64 n) {
+  e->bufs.emplace_back(n * sizeof(T) + 64, 0);
+  return (T*)e->bufs.back().data();
+}
+
+template <int N>
+static void run_round(SoaEngine* e) {
+  if (e->C.iso_period && e->round > 0 && e->round % e->C.iso_period == 0)
+    for (u64 g = 0; g < e->C.n_groups; g++) iso_group<N>(e->P, e->C, g, e->round);
+  StepCounters c;
+  for (u64 r = 0; r < e->C.n_rep; r++) {
+    memset(&c, 0, sizeof(c));
+    step_replica<N>(e->P, e->C, r, e->round, c);
+    for (int i = 0; i < C_NUM; i++) e->counters[i] += c.v[i];
+  }
+  e->round++;
+}
+
+extern "C" {
+
+void* soa_create(const rbe_config* cfg) {
+  SoaEngine* e = new SoaEngine();
+  Params& C = e->C;
+  memset(&C, 0, sizeof(C));
+  C.n = cfg->n_replicas;
+  C.n_groups = cfg->n_groups;
+  C.n_rep = C.n_groups * C.n;
+  C.cid_base = cfg->cid_base ? cfg->cid_base : 1;
+  C.cid_stride = cfg->cid_stride ? cfg->cid_stride : 1;
+  C.seed = cfg->seed;
+  C.max_entry_size = cfg->max_entry_size ? cfg->max_entry_size : (64ull << 20);
+  C.ring = cfg->ring ? cfg->ring : 64;
+  C.rq_cap = cfg->rq_cap ? cfg->rq_cap : 8;
+  C.maxm = cfg->maxm ? cfg->maxm : 12;
+  C.ecap = cfg->ecap ? cfg->ecap : 2 * C.ring;
+  C.rtr_cap = cfg->rtr_cap ? cfg->rtr_cap : 8;
+  C.dri_cap = cfg->dri_cap ? cfg->dri_cap : 8;
+  C.election_rtt = cfg->election_rtt;
+  C.heartbeat_rtt = cfg->heartbeat_rtt;
+  C.check_quorum = cfg->check_quorum;
+  C.quiesce = cfg->quiesce;
+  C.trace = cfg->trace;
+  C.wl_enabled = cfg->wl_enabled;
+  C.wl_start_round = cfg->wl_start_round;
+  C.wl_stop_round = cfg->wl_stop_round;
+  C.wl_active_mod = cfg->wl_active_mod;
+  C.wl_read_permille = cfg->wl_read_permille;
+  C.ext_inputs = 0;
+  C.iso_period = cfg->iso_period;
+  C.iso_len = cfg->iso_len;
+  C.iso_mod = cfg->iso_mod;
+  if (C.n != 1 && C.n != 3 && C.n != 5) {
+    delete e;
+    return nullptr;
+  }
+  const u64 N = C.n, G = C.n_groups, R = C.n_rep;
+  Planes& P = e->P;
+  P.hot = alloc<Hot>(e, R);
+  P.core = alloc<Core>(e, R);
+  P.rem = alloc<RemoteMN>(e, R * N);
+  P.rem_st = alloc<u8>(e, R * N);
+  P.rq = alloc<ReadReq>(e, R * C.rq_cap);
+  P.term_ring = alloc<u64>(e, (u64)C.ring * R);
+  P.pay_ring = alloc<Body>(e, (u64)C.ring * R);
+  for (int p = 0; p < 2; p++) {
+    P.cnt[p] = alloc<u16>(e, G * N * N);
+    P.msgs[p] = alloc<Msg>(e, G * N * N * C.maxm);
+    P.arena[p] = alloc<Ent>(e, R * C.ecap);
+  }
+  P.iso_mask = alloc<u8>(e, G);
+  P.iso_until = alloc<u32>(e, G);
+  P.upd = alloc<Upd>(e, R);
+  P.rtr = alloc<RTR>(e, R * C.rtr_cap);
+  P.dri = alloc<DropRI>(e, R * C.dri_cap);
+  P.ext = alloc<ExtIn>(e, R);
+  P.counters = nullptr;
+  for (u64 r = 0; r < R; r++) {
+    if (N == 1) launch_replica<1>(P, C, r);
+    else if (N == 3) launch_replica<3>(P, C, r);
+    else launch_replica<5>(P, C, r);
+  }
+  return e;
+}
+
+void soa_destroy(void* h) { delete (SoaEngine*)h; }
+
+void soa_run(void* h, uint32_t rounds) {
+  SoaEngine* e = (SoaEngine*)h;
+  for (u32 i = 0; i < rounds; i++) {
+    if (e->C.n == 1) run_round<1>(e);
+    else if (e->C.n == 3) run_round<3>(e);
+    else run_round<5>(e);
+  }
+}
+
+void soa_counters(void* h, uint64_t* out) {
+  SoaEngine* e = (SoaEngine*)h;
+  for (int i = 0; i < C_NUM; i++) out[i] = e->counters[i];
+}
+
+void soa_views(void* h, rbe_replica_view* out) {
+  SoaEngine* e = (SoaEngine*)h;
+  const u32 N = e->C.n;
+  for (u64 i = 0; i < e->C.n_rep; i++) {
+    rbe_replica_view& v = out[i];
+    memset(&v, 0, sizeof(v));
+    const Hot& hh = e->P.hot[i];
+    const Core& c = e->P.core[i];
+    v.term = c.term;
+    v.vote = c.vote;
+    v.leader_id = c.leader;
+    v.committed = c.committed;
+    v.last_index = c.last_index;
+    v.processed = c.processed;
+    v.saved_to = c.saved_to;
+    v.digest = e->P.upd[i].digest;
+    v.role = hh.role;
+    v.election_tick = hh.election_tick;
+    v.heartbeat_tick = hh.heartbeat_tick;
+    v.rand_election_timeout = hh.rand_et;
+    v.q_tick = hh.q_tick;
+    v.q_quiesced_since = hh.q_quiesced_since;
+    v.q_no_activity_since = hh.q_no_activity_since;
+    v.q_exit_quiesce_tick = hh.q_exit_quiesce_tick;
+    v.raft_quiesce = (hh.flags & HF_RAFT_QUIESCE) ? 1 : 0;
+    v.rq_count = c.rq_count;
+    v.votes_resp = hh.votes_resp;
+    v.votes_granted = hh.votes_granted;
+    if (hh.role == R_Leader) {
+      for (u32 s = 0; s < N && s < 8; s++) {
+        v.match[s] = e->P.rem[i * N + s].match;
+        v.next[s] = e->P.rem[i * N + s].next;
+        v.rstate[s] = e->P.rem_st[i * N + s] & 3;
+        v.ractive[s] = (e->P.rem_st[i * N + s] >> 2) & 1;
+      }
+    }
+  }
+}
+
+uint32_t soa_faults(void* h, uint64_t* n_faulty) {
+  SoaEngine* e = (SoaEngine*)h;
+  uint32_t o = 0;
+  uint64_t n = 0;
+  for (u64 i = 0; i < e->C.n_rep; i++) {
+    if (e->P.upd[i].fault) n++;
+    o |= e->P.upd[i].fault;
+  }
+  *n_faulty = n;
+  return o;
+}
+
+}  // extern "C"
