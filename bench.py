@@ -1,0 +1,236 @@
+#!/usr/bin/env python3
+"""Benchmark: Raft group-steps/s + committed entries/s on MI355X.
+
+Workload (BASELINE.json `metric`, configs[3] "C4"): per GPU 1M Raft groups x 3
+replicas, Quiesce on, 90% of groups idle (quiesced after 200 ticks), 10%
+active with a 9:1 ReadIndex:propose mix, 16-byte proposals, ElectionRTT=10,
+HeartbeatRTT=1.  A "step" is one lockstep round of every replica of every
+group (one k_step launch): inbox → raft protocol → outbox + Update.
+
+Multi-GPU (torchrun, one process per GPU): groups shard by cluster id
+(cid % N == rank, dragonboat's FixedPartitioner); no data-path collective;
+per-GPU work is fixed (weak scaling).  `value` = group-steps of all ranks ÷
+the max-over-ranks timed-region wall time.
+
+Outputs ONE JSON line on rank 0 (see DESIGN.md §Measurement for the byte model).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Raft group-steps/sec + committed entries/sec (1M groups×3), 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+# SURVEY.md §8(d) algorithmic bytes per event
+BYTES = {
+    "active_ticks": 128,     # core state read 64 B + write 64 B per active step
+    "quiesced_ticks": 12,    # quiesced tick: 8 B read + 4 B written
+    "msg_in": 64, "msg_out": 64,  # fixed message record
+    "ent_in": 16, "ent_out": 16,  # payload per carried entry
+    "remote_touch": 17,      # match 8 + next 8 + state 1
+    "ring_access": 8,        # term-ring access
+    "ent_saved": 16,         # payload append
+    "rq_touch": 40,          # readIndex queue slot
+}
+
+WORKLOADS = {
+    # name: (engine kwargs, settle rounds, description)
+    "c4": (dict(n_groups=1_000_000, n_replicas=3, quiesce=True, wl_enabled=True,
+                wl_start_round=30, wl_active_mod=10, wl_read_permille=900, ring=64),
+           260, "C4: 1M groups x 3 replicas per GPU, Quiesce on, 90% idle (quiesced), "
+                "10% active with 9:1 ReadIndex:propose, 16 B proposals"),
+    "c2": (dict(n_groups=10_000, n_replicas=3, wl_enabled=True, wl_start_round=30, ring=64),
+           60, "C2: 10k groups x 3 replicas, 1 proposal per group per round"),
+    "c2m": (dict(n_groups=1_000_000, n_replicas=3, wl_enabled=True, wl_start_round=30,
+                 ring=64), 60, "C2 at 1M groups x 3: 1 proposal per group per round"),
+    "c3": (dict(n_groups=100_000, n_replicas=5, check_quorum=True, wl_enabled=True,
+                wl_start_round=40, iso_period=50, iso_len=30, iso_mod=10, ring=128),
+           100, "C3: 100k groups x 5, CheckQuorum, leader isolation 30/50 rounds for 10%"),
+}
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def cpu_baseline(name, groups, settle, rounds, threads):
+    """The oracle (C++ restatement of internal/raft, test infrastructure) on a
+    bounded sample of the same workload, timed on this host's cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    kw, _, _ = WORKLOADS[name]
+    kw = dict(kw)
+    kw.pop("ring", None)
+    kw["n_groups"] = groups
+    h = O.Harness(**kw, trace=False, threads=threads)
+    h.run(settle)
+    c0 = h.counters()
+    t0 = time.perf_counter()
+    h.run(rounds)
+    dt = time.perf_counter() - t0
+    c1 = h.counters()
+    steps = c1["steps"] - c0["steps"]
+    return {
+        "value": steps / dt,
+        "unit": "group-steps/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"{groups} groups x {kw['n_replicas']} replicas of the same workload, "
+                   f"{rounds} timed rounds after a {settle}-round settle; C++ restatement "
+                   f"of internal/raft (oracle/), not Go; {threads} threads, groups "
+                   f"partitioned cid % threads"),
+        "committed_entries_per_s": (c1["committed"] - c0["committed"]) / dt,
+        "seconds": dt,
+    }
+
+
+def load_traffic(name):
+    """HBM bytes per k_step launch from the committed PMC summary, if any."""
+    p = os.path.join(ROOT, "profiles", f"traffic_{name}.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            return json.load(f).get("bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
+    ap.add_argument("--groups", type=int, default=0, help="override groups per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-groups", type=int, default=30000)
+    ap.add_argument("--cpu-rounds", type=int, default=100)
+    ap.add_argument("--cpu-threads", type=int,
+                    default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    import torch
+    import torch.distributed as dist
+    use_dist = ws > 1
+    if use_dist:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+
+    from dragonboat_amd.engine import Engine, footprint, make_config
+
+    kw, settle, desc = WORKLOADS[args.workload]
+    kw = dict(kw)
+    if args.groups:
+        kw["n_groups"] = args.groups
+    # group-per-GPU sharding: cid = 1 + rank + g * world  (cid % world == rank)
+    cfg = make_config(device=local, cid_base=1 + rank, cid_stride=ws, trace=False, **kw)
+    eng = Engine(cfg)
+
+    def barrier():
+        if use_dist:
+            dist.barrier()
+        eng.sync()
+
+    # settle to steady state (elections done, idle groups quiesced), then warm up
+    eng.run(settle)
+    eng.run(max(1, args.warmup))
+    eng.sync()
+    eng.reset_counters()
+
+    barrier()
+    t0 = time.perf_counter()
+    ev_ms = eng.run_timed(args.steps)  # HIP events on the engine stream around K launches
+    barrier()
+    wall = time.perf_counter() - t0
+
+    c = eng.counters()
+    nf, fo = eng.fault_summary()
+    local_vals = torch.tensor([wall, float(c["steps"]), float(c["committed"]),
+                               float(c["reads_confirmed"]), float(nf)], dtype=torch.float64)
+    if use_dist:
+        t = local_vals.to(dev) if dist.get_backend() == "nccl" else local_vals
+        wall_t = t[0:1].clone()
+        sums = t[1:].clone()
+        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+        wall_max = float(wall_t.item())
+        steps, committed, reads, faulty = [float(x) for x in sums.cpu().tolist()]
+    else:
+        wall_max = wall
+        steps, committed, reads, faulty = [float(x) for x in local_vals[1:].tolist()]
+
+    # roofline of the dominant kernel (k_step) on this rank
+    alg_bytes = sum(BYTES[k] * c[k] for k in BYTES)
+    per_launch = alg_bytes / args.steps
+    avg_launch_s = (ev_ms / 1e3) / args.steps
+    achieved = per_launch / avg_launch_s / 1e9
+    traffic = load_traffic(args.workload)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": steps / wall_max,
+            "unit": "group-steps/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": wall_max * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic",
+            "config": {
+                "workload": desc,
+                "groups_per_gpu": int(kw["n_groups"]),
+                "replicas_per_group": int(kw["n_replicas"]),
+                "total_groups": int(kw["n_groups"]) * ws,
+                "parallelism": f"group-per-GPU x{ws} (cid % {ws})",
+                "election_rtt": 10, "heartbeat_rtt": 1,
+                "settle_rounds": settle,
+                "device_bytes_per_gpu": footprint(cfg),
+            },
+            "committed_entries_per_s": committed / wall_max,
+            "read_confirmations_per_s": reads / wall_max,
+            "faulty_replicas": int(faulty),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "k_step<3>",
+                "alg_bytes_per_launch": per_launch,
+                "avg_launch_us": avg_launch_s * 1e6,
+            },
+        }
+        if not args.no_cpu_baseline and ws == 1:
+            try:
+                out["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_groups,
+                                                   settle, args.cpu_rounds, args.cpu_threads)
+            except Exception as ex:  # the baseline must not hide the GPU number
+                out["cpu_baseline"] = {"error": repr(ex)}
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if use_dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -39,15 +39,7 @@ __device__ __forceinline__ u32 wave_sum(u32 v) {
   return v;
 }
 
-template <int N>
-__global__ __launch_bounds__(kBlock) void k_step(Planes P, Params C, const u32* round_ptr,
-                                                 u32 round_add) {
-  const u32 round = (round_ptr ? *round_ptr : 0u) + round_add;
-  const u64 r = (u64)blockIdx.x * kBlock + threadIdx.x;
-  StepCounters c;
-#pragma unroll
-  for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
-  if (r < C.n_rep) step_replica<N>(P, C, r, round, c);
+__device__ __forceinline__ void flush_counters(const Planes& P, const StepCounters& c) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) {
@@ -56,6 +48,98 @@ __global__ __launch_bounds__(kBlock) void k_step(Planes P, Params C, const u32* 
     const u32 s = wave_sum(c.v[i]);
     if (lane == 0) atomicAdd((unsigned long long*)&P.counters[i], (unsigned long long)s);
   }
+}
+
+// The whole handler table over every replica (reference mode, RBE_MODE=full).
+template <int N, bool TRACE>
+__global__ __launch_bounds__(kBlock) void k_step(Planes P, Params C, const u32* round_ptr,
+                                                 u32 round_add) {
+  const u32 round = (round_ptr ? *round_ptr : 0u) + round_add;
+  const u64 r = (u64)blockIdx.x * kBlock + threadIdx.x;
+  StepCounters c;
+#pragma unroll
+  for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
+  if (r < C.n_rep) step_replica<N, TRACE>(P, C, r, round, c);
+  flush_counters(P, c);
+}
+
+// Work lists of a round: 0 = steady-state leaders, 1 = steady-state followers,
+// 2 = full handler table.  Entry counts live in counts[list * 2 + parity].
+struct Lists {
+  u32* idx;     // [3][cap] replica indices
+  u32* counts;  // [3][2]
+  u64 cap;
+};
+
+// wave-aggregated append: one atomic per wave and list
+__device__ __forceinline__ void list_push(const Lists& L, u32 list, u32 par, bool want, u32 r) {
+  const u64 mask = __ballot(want);
+  if (!mask) return;
+  const int lane = threadIdx.x & 63;
+  const int first = __ffsll((unsigned long long)mask) - 1;
+  u32 base = 0;
+  if (lane == first) base = atomicAdd(&L.counts[list * 2 + par], (u32)__popcll(mask));
+  base = __shfl(base, first, 64);
+  if (want) L.idx[list * L.cap + base + __popcll(mask & ((1ull << lane) - 1ull))] = r;
+}
+
+// Pass 1 over every replica: idle rounds complete here; the rest is listed.
+template <int N, bool TRACE>
+__global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, const u32* round_ptr,
+                                                   u32 round_add, Lists L) {
+  const u32 round = (round_ptr ? *round_ptr : 0u) + round_add;
+  const u32 par = round & 1u;
+  if (blockIdx.x == 0 && threadIdx.x < 3) L.counts[threadIdx.x * 2 + (par ^ 1u)] = 0;
+  const u64 r = (u64)blockIdx.x * kBlock + threadIdx.x;
+  StepCounters c;
+#pragma unroll
+  for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
+  u32 cls = T_DONE;
+  if (r < C.n_rep) cls = triage_replica<N, TRACE>(P, C, r, round, c);
+  list_push(L, 0, par, cls == T_LEAD, (u32)r);
+  list_push(L, 1, par, cls == T_FOLL, (u32)r);
+  list_push(L, 2, par, cls == T_FULL, (u32)r);
+  flush_counters(P, c);
+}
+
+// Pass 2: the steady-state subset for one role over its list (persistent,
+// grid-stride); rounds outside the subset are moved to the full list.
+template <int N, bool TRACE, int MODE>
+__global__ __launch_bounds__(kBlock) void k_fast_list(Planes P, Params C, const u32* round_ptr,
+                                                      u32 round_add, Lists L) {
+  const u32 round = (round_ptr ? *round_ptr : 0u) + round_add;
+  const u32 par = round & 1u;
+  const u32 li = MODE == MODE_LEAD ? 0u : 1u;
+  const u32 n = L.counts[li * 2 + par];
+  StepCounters c;
+#pragma unroll
+  for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
+  const u64 stride = (u64)gridDim.x * kBlock;
+  for (u64 i0 = (u64)blockIdx.x * kBlock; i0 < n; i0 += stride) {
+    const u64 i = i0 + threadIdx.x;
+    bool slow = false;
+    u32 r = 0;
+    if (i < n) {
+      r = L.idx[li * L.cap + i];
+      slow = !step_replica_fast<N, TRACE, MODE>(P, C, r, round, c);
+    }
+    list_push(L, 2, par, slow, r);
+  }
+  flush_counters(P, c);
+}
+
+// Pass 3: the whole handler table over the full list (persistent, grid-stride).
+template <int N, bool TRACE>
+__global__ __launch_bounds__(kBlock) void k_full_list(Planes P, Params C, const u32* round_ptr,
+                                                      u32 round_add, Lists L) {
+  const u32 round = (round_ptr ? *round_ptr : 0u) + round_add;
+  const u32 n = L.counts[2 * 2 + (round & 1u)];
+  StepCounters c;
+#pragma unroll
+  for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
+  for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock)
+    step_replica<N, TRACE>(P, C, L.idx[2 * L.cap + i], round, c);
+  flush_counters(P, c);
 }
 
 template <int N>
@@ -85,7 +169,12 @@ struct rbe_engine {
   hipGraphExec_t graph = nullptr;
   u32 graph_rounds = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool full_mode = false;    // RBE_MODE=full: the whole handler table for every replica
+  Lists L;                   // per-round work lists (triage → fast → full)
 };
+
+static constexpr unsigned kFastGrid = 2048;  // persistent grid of k_fast_list
+static constexpr unsigned kFullGrid = 1024;  // persistent grid of k_full_list
 
 static u64 bytes_of(const Params& C, u64* parts) {
   const u64 N = C.n, G = C.n_groups, R = C.n_rep;
@@ -135,7 +224,7 @@ static int make_params(const rbe_config* cfg, Params* out) {
   if (C.rq_cap > 255) return RBE_E_INVALID;
   C.maxm = cfg->maxm ? cfg->maxm : 12;
   if (C.maxm > 127) return RBE_E_INVALID;
-  C.ecap = cfg->ecap ? cfg->ecap : 2 * C.ring;
+  C.ecap = cfg->ecap ? cfg->ecap : 32;
   C.rtr_cap = cfg->rtr_cap ? cfg->rtr_cap : 8;
   C.dri_cap = cfg->dri_cap ? cfg->dri_cap : 8;
   C.election_rtt = cfg->election_rtt;
@@ -178,13 +267,33 @@ static int d2h(rbe_engine* e, T* dst, const T* src, u64 n) {
 
 static unsigned grid_for(u64 n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
+template <int N, bool TRACE>
+static int launch_step_t(rbe_engine* e, const u32* round_ptr, u32 round_add) {
+  const unsigned g = grid_for(e->C.n_rep);
+  if (e->full_mode) {
+    hipLaunchKernelGGL((k_step<N, TRACE>), dim3(g), dim3(kBlock), 0, e->stream, e->P, e->C,
+                       round_ptr, round_add);
+  } else {
+    hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(g), dim3(kBlock), 0, e->stream, e->P, e->C,
+                       round_ptr, round_add, e->L);
+    const unsigned gf = g < kFastGrid ? g : kFastGrid;
+    hipLaunchKernelGGL((k_fast_list<N, TRACE, MODE_LEAD>), dim3(gf), dim3(kBlock), 0, e->stream,
+                       e->P, e->C, round_ptr, round_add, e->L);
+    hipLaunchKernelGGL((k_fast_list<N, TRACE, MODE_FOLL>), dim3(gf), dim3(kBlock), 0, e->stream,
+                       e->P, e->C, round_ptr, round_add, e->L);
+    const unsigned gs = g < kFullGrid ? g : kFullGrid;
+    hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kBlock), 0, e->stream, e->P, e->C,
+                       round_ptr, round_add, e->L);
+  }
+  HIP_OK(hipGetLastError());
+  return RBE_OK;
+}
+
 static int launch_step(rbe_engine* e, const u32* round_ptr, u32 round_add) {
   return dispatch_n(e->C.n, [&](auto NN) {
     constexpr int N = decltype(NN)::value;
-    hipLaunchKernelGGL(k_step<N>, dim3(grid_for(e->C.n_rep)), dim3(kBlock), 0, e->stream, e->P,
-                       e->C, round_ptr, round_add);
-    HIP_OK(hipGetLastError());
-    return RBE_OK;
+    return e->C.trace ? launch_step_t<N, true>(e, round_ptr, round_add)
+                      : launch_step_t<N, false>(e, round_ptr, round_add);
   });
 }
 
@@ -285,6 +394,21 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
     return RBE_E_NOMEM;
   }
   HIP_IGNORE(hipMemsetAsync(e->d_round, 0, sizeof(u32), e->stream));
+  const char* mode = getenv("RBE_MODE");
+  e->full_mode = mode && strcmp(mode, "full") == 0;
+  if (C.n_rep >= (1ull << 32)) {
+    rbe_destroy(e);
+    return RBE_E_INVALID;  // list entries are 32-bit replica indices
+  }
+  e->L.cap = C.n_rep;
+  if (hipMalloc(&e->L.idx, 3 * C.n_rep * sizeof(u32)) != hipSuccess ||
+      hipMalloc(&e->L.counts, 6 * sizeof(u32)) != hipSuccess) {
+    rbe_destroy(e);
+    return RBE_E_NOMEM;
+  }
+  e->allocs.push_back(e->L.idx);
+  e->allocs.push_back(e->L.counts);
+  HIP_IGNORE(hipMemsetAsync(e->L.counts, 0, 6 * sizeof(u32), e->stream));
   rc = dispatch_n(C.n, [&](auto NN) {
     constexpr int N = decltype(NN)::value;
     hipLaunchKernelGGL(k_launch<N>, dim3(grid_for(C.n_rep)), dim3(kBlock), 0, e->stream, e->P,
@@ -513,17 +637,22 @@ int rbe_get_updates(rbe_engine* e, uint64_t first, uint64_t count, rbe_update* o
     u.term = core[i].term;
     u.vote = core[i].vote;
     u.commit = core[i].committed;
-    u.save_lo = upd[i].save_lo;
-    u.save_hi = upd[i].save_hi;
-    u.apply_lo = upd[i].apply_lo;
-    u.apply_hi = upd[i].apply_hi;
     u.digest = upd[i].digest;
-    u.n_messages = upd[i].n_msgs;
-    u.n_ready_to_read = upd[i].n_rtr;
-    u.n_dropped_entries = upd[i].n_drop_ent;
-    u.n_dropped_read_indexes = upd[i].n_drop_ri;
     u.fault = upd[i].fault;
-    u.flags = upd[i].flags;
+    if (e->round > 0 && upd[i].round == e->round - 1) {
+      u.save_lo = upd[i].save_lo;
+      u.save_hi = upd[i].save_hi;
+      u.apply_lo = upd[i].apply_lo;
+      u.apply_hi = upd[i].apply_hi;
+      u.n_messages = upd[i].n_msgs;
+      u.n_ready_to_read = upd[i].n_rtr;
+      u.n_dropped_entries = upd[i].n_drop_ent;
+      u.n_dropped_read_indexes = upd[i].n_drop_ri;
+      u.flags = upd[i].flags;
+    } else {  // an idle round (triage) left the record untouched: empty Update
+      u.save_lo = u.apply_lo = 1;
+      u.save_hi = u.apply_hi = 0;
+    }
     u.role = hot[i].role;
     u.leader_id = core[i].leader;
   }
@@ -583,6 +712,7 @@ int rbe_get_ready_to_reads(rbe_engine* e, uint64_t replica, rbe_ready_to_read* o
                         hipMemcpyDeviceToHost, e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
   u32 n = u.n_rtr < e->C.rtr_cap ? u.n_rtr : e->C.rtr_cap;
+  if (e->round == 0 || u.round != e->round - 1) n = 0;
   for (u32 i = 0; i < n && i < cap && out; i++) {
     out[i].index = v[i].index;
     out[i].ctx_low = v[i].low;

@@ -46,10 +46,12 @@ RBE_HD u32 popc8(u32 x) {
 RBE_HD u64 wl_payload_lo(u64 seed, u64 cid, u64 round) {
   return mix64(seed ^ (cid * 0xD1B54A32D192ED03ULL) ^ (round << 1));
 }
+// uniform draw in [0, m) from the high 32 bits of x (multiply-shift, no division)
+RBE_HD u32 below(u64 x, u32 m) { return (u32)(((x >> 32) * (u64)m) >> 32); }
 RBE_HD bool wl_group_active(const Params& C, u64 cid) {
   if (C.wl_active_mod <= 1) return true;
-  return mix64(C.seed ^ 0xA5A5A5A5A5A5A5A5ULL ^ (cid * 0x9E3779B97F4A7C15ULL)) %
-             C.wl_active_mod == 0;
+  return below(mix64(C.seed ^ 0xA5A5A5A5A5A5A5A5ULL ^ (cid * 0x9E3779B97F4A7C15ULL)),
+               C.wl_active_mod) == 0;
 }
 RBE_HD u32 wl_input(const Params& C, u64 cid, u32 round) {
   if (!C.wl_enabled) return 0;
@@ -57,12 +59,13 @@ RBE_HD u32 wl_input(const Params& C, u64 cid, u32 round) {
   if (C.wl_stop_round != 0 && round >= C.wl_stop_round) return 0;
   if (!wl_group_active(C, cid)) return 0;
   if (C.wl_read_permille == 0) return 1;
-  u64 u = mix64(C.seed ^ (cid * 0xC2B2AE3D27D4EB4FULL) ^ ((u64)round << 20)) % 1000;
+  u32 u = below(mix64(C.seed ^ (cid * 0xC2B2AE3D27D4EB4FULL) ^ ((u64)round << 20)), 1000);
   return u < C.wl_read_permille ? 2u : 1u;
 }
 RBE_HD bool iso_selected(const Params& C, u64 cid, u32 epoch) {
   if (C.iso_mod <= 1) return true;
-  return mix64(C.seed ^ (cid * 0x94D049BB133111EBULL) ^ ((u64)epoch << 40)) % C.iso_mod == 0;
+  return below(mix64(C.seed ^ (cid * 0x94D049BB133111EBULL) ^ ((u64)epoch << 40)), C.iso_mod) ==
+         0;
 }
 // injected replacement for random.LockGuardedRand (raft.go:632)
 RBE_HD u64 rto_rand(u64 seed, u64 cid, u64 nid, u64 count) {
@@ -80,8 +83,13 @@ struct StepCounters {
 };
 
 // ----------------------------------------------------------------- the lane
-template <int N>
+enum : int { MODE_FULL = 0, MODE_LEAD = 1, MODE_FOLL = 2 };
+
+template <int N, bool TRACE, int MODE>
 struct Lane {
+  static constexpr bool FULL = MODE == MODE_FULL;  // the whole handler table
+  static constexpr bool LEAD = MODE == MODE_LEAD;  // steady-state leader subset
+  static constexpr bool FOLL = MODE == MODE_FOLL;  // steady-state follower subset
   const Planes& P;
   const Params& C;
   const u64 r;      // global replica index
@@ -98,7 +106,10 @@ struct Lane {
   u32 q_tick, q_qs, q_nas, q_eqt, rngc;
   bool q_new;
   u64 term, committed, last, processed, saved_to;
+  u64 t_last;  // term of entry `last` (log-tail cache, kept in Core)
   u8 vote, leader, ltt, rq_head, rq_count;
+  u64 c_match[N], c_next[N];  // LEAD: remote slots held in registers
+  u32 c_st[N];
   u8 iso;  // isolation mask of this group for this round
 
   // per-step outputs
@@ -109,6 +120,14 @@ struct Lane {
   u64 msg_hash, rtr_hash, drop_hash;
   u32 n_msgs, n_rtr, n_drop_ent, n_drop_ri;
   u32 fault;
+  // deferred fan-out actions, executed in this order after each event
+  u32 rep_mask;      // slots to sendReplicateMessage to
+  u8 tn_to;          // TimeoutNow target
+  bool hb_pending;   // broadcastHeartbeatMessageWithHint(hb_lo, hb_hi)
+  bool rq_pending;   // handleReadIndexLeaderConfirmation(rq_m)
+  u64 hb_lo, hb_hi;
+  u64 rq_lo, rq_hi;
+  u8 rq_from;
   StepCounters& ctr;
 
   RBE_HD Lane(const Planes& P_, const Params& C_, u64 r_, u32 round_, StepCounters& c_)
@@ -127,6 +146,7 @@ struct Lane {
   // [firstIndex-1, lastIndex]; firstIndex is 1 (no compaction on device).
   RBE_HD u64 log_term(u64 idx) {
     if (idx > last || idx == 0) return 0;
+    if (idx == last) return t_last;
     if (last - idx >= C.ring) {
       set_fault(F_WINDOW);
       return 0;
@@ -185,64 +205,113 @@ struct Lane {
   }
 
   // ------------------------------------------------------------- remotes
-  RBE_HD RemoteMN* rem(u32 slot) const { return &P.rem[r * N + slot]; }
-  RBE_HD u8 rst(u32 slot) const { return P.rem_st[r * N + slot]; }
-  RBE_HD void set_rst(u32 slot, u8 v) { P.rem_st[r * N + slot] = v; }
-  RBE_HD u8 rstate(u32 slot) const { return rst(slot) & 3; }
-  RBE_HD void set_rstate(u32 slot, u8 s) { set_rst(slot, (u8)((rst(slot) & ~3) | s)); }
-  RBE_HD bool ractive(u32 slot) const { return (rst(slot) >> 2) & 1; }
-  RBE_HD void set_active(u32 slot, bool a) { set_rst(slot, (u8)((rst(slot) & 3) | (a ? 4 : 0))); }
+  // Value accessors.  The leader-specialized fast mode keeps the N remote
+  // slots in registers for the whole round (loaded by load(), written back by
+  // store()); the selects over a compile-time N keep them out of scratch.
+  // The other modes read and write the SoA planes directly.
+  RBE_HD u64 rmatch(u32 s) const {
+    if constexpr (LEAD) {
+      u64 v = 0;
+      for (u32 i = 0; i < N; i++)
+        if (i == s) v = c_match[i];
+      return v;
+    } else {
+      return P.rem[r * N + s].match;
+    }
+  }
+  RBE_HD u64 rnext(u32 s) const {
+    if constexpr (LEAD) {
+      u64 v = 0;
+      for (u32 i = 0; i < N; i++)
+        if (i == s) v = c_next[i];
+      return v;
+    } else {
+      return P.rem[r * N + s].next;
+    }
+  }
+  RBE_HD u32 rst(u32 s) const {
+    if constexpr (LEAD) {
+      u32 v = 0;
+      for (u32 i = 0; i < N; i++)
+        if (i == s) v = c_st[i];
+      return v;
+    } else {
+      return P.rem_st[r * N + s];
+    }
+  }
+  RBE_HD void set_rmatch(u32 s, u64 v) {
+    if constexpr (LEAD) {
+      for (u32 i = 0; i < N; i++)
+        if (i == s) c_match[i] = v;
+    } else {
+      P.rem[r * N + s].match = v;
+    }
+  }
+  RBE_HD void set_rnext(u32 s, u64 v) {
+    if constexpr (LEAD) {
+      for (u32 i = 0; i < N; i++)
+        if (i == s) c_next[i] = v;
+    } else {
+      P.rem[r * N + s].next = v;
+    }
+  }
+  RBE_HD void set_rst(u32 s, u32 v) {
+    if constexpr (LEAD) {
+      for (u32 i = 0; i < N; i++)
+        if (i == s) c_st[i] = v;
+    } else {
+      P.rem_st[r * N + s] = (u8)v;
+    }
+  }
+  RBE_HD u32 rstate(u32 slot) const { return rst(slot) & 3u; }
+  RBE_HD void set_rstate(u32 slot, u32 s) { set_rst(slot, (rst(slot) & ~3u) | s); }
+  RBE_HD bool ractive(u32 slot) const { return (rst(slot) >> 2) & 1u; }
+  RBE_HD void set_active(u32 slot, bool a) { set_rst(slot, (rst(slot) & 3u) | (a ? 4u : 0u)); }
   RBE_HD bool is_paused(u32 slot) const {  // remote.go:173-186
-    u8 s = rstate(slot);
+    u32 s = rstate(slot);
     return s == RS_Wait || s == RS_Snapshot;
   }
   RBE_HD void wait_to_retry(u32 slot) {  // remote.go:94-98
     if (rstate(slot) == RS_Wait) set_rstate(slot, RS_Retry);
   }
   RBE_HD void become_retry(u32 slot) {  // remote.go:75-83 (snapshotIndex is 0 on device)
-    RemoteMN* x = rem(slot);
-    x->next = x->match + 1;
+    set_rnext(slot, rmatch(slot) + 1);
     set_rstate(slot, RS_Retry);
   }
   RBE_HD void become_replicate(u32 slot) {  // remote.go:102-106
-    RemoteMN* x = rem(slot);
-    x->next = x->match + 1;
+    set_rnext(slot, rmatch(slot) + 1);
     set_rstate(slot, RS_Replicate);
   }
   RBE_HD bool try_update(u32 slot, u64 idx) {  // remote.go:123-133
-    RemoteMN* x = rem(slot);
     ctr.v[C_REMOTE_TOUCH]++;
-    if (x->next < idx + 1) x->next = idx + 1;
-    if (x->match < idx) {
+    if (rnext(slot) < idx + 1) set_rnext(slot, idx + 1);
+    if (rmatch(slot) < idx) {
       wait_to_retry(slot);
-      x->match = idx;
+      set_rmatch(slot, idx);
       return true;
     }
     return false;
   }
   RBE_HD void progress(u32 slot, u64 li) {  // remote.go:135-143
-    u8 s = rstate(slot);
-    if (s == RS_Replicate) rem(slot)->next = li + 1;
+    u32 s = rstate(slot);
+    if (s == RS_Replicate) set_rnext(slot, li + 1);
     else if (s == RS_Retry) set_rstate(slot, RS_Wait);
     else set_fault(F_PANIC);
   }
   RBE_HD void responded_to(u32 slot) {  // remote.go:145-153
-    u8 s = rstate(slot);
+    u32 s = rstate(slot);
     if (s == RS_Retry) become_replicate(slot);
-    else if (s == RS_Snapshot) {
-      if (rem(slot)->match >= 0) become_retry(slot);  // snapshotIndex == 0 on device
-    }
+    else if (s == RS_Snapshot) become_retry(slot);  // match >= snapshotIndex (0 on device)
   }
   RBE_HD bool decrease_to(u32 slot, u64 rejected, u64 lst) {  // remote.go:155-171
-    RemoteMN* x = rem(slot);
     if (rstate(slot) == RS_Replicate) {
-      if (rejected <= x->match) return false;
-      x->next = x->match + 1;
+      if (rejected <= rmatch(slot)) return false;
+      set_rnext(slot, rmatch(slot) + 1);
       return true;
     }
-    if (x->next - 1 != rejected) return false;
+    if (rnext(slot) - 1 != rejected) return false;
     wait_to_retry(slot);
-    x->next = umax64(1, umin64(rejected, lst + 1));
+    set_rnext(slot, umax64(1, umin64(rejected, lst + 1)));
     return true;
   }
 
@@ -268,7 +337,7 @@ struct Lane {
       else m.term = term;
     }
     n_msgs++;
-    if (C.trace) {
+    if (TRACE) {
       u64 h = msg_hash;
       h = hfold(h, (u64)m.type | ((u64)m.reject << 8) | ((u64)m.n_ent << 16));
       h = hfold(h, m.to);
@@ -413,7 +482,7 @@ struct Lane {
     x.high = high;
     P.rtr[r * C.rtr_cap + n_rtr] = x;
     n_rtr++;
-    if (C.trace) {
+    if (TRACE) {
       rtr_hash = hfold(rtr_hash, index);
       rtr_hash = hfold(rtr_hash, low);
       rtr_hash = hfold(rtr_hash, high);
@@ -436,7 +505,7 @@ struct Lane {
   RBE_HD void report_dropped_proposal(const Ent* e, u32 cnt) {  // raft.go:1987-1997
     for (u32 i = 0; i < cnt; i++) {
       n_drop_ent++;
-      if (C.trace) {
+      if (TRACE) {
         drop_hash = hfold(drop_hash, 0);
         drop_hash = hfold(drop_hash, e[i].term);
         drop_hash = hfold(drop_hash, (u64)e[i].type | ((u64)e[i].len << 32));
@@ -448,15 +517,13 @@ struct Lane {
 
   // ------------------------------------------------------------- state transitions
   RBE_HD void set_randomized_election_timeout() {  // raft.go:631-634
-    u64 x = rto_rand(C.seed, cid, self, rngc++) % C.election_rtt;
+    u64 x = below(rto_rand(C.seed, cid, self, rngc++), C.election_rtt);
     ret = (u32)(C.election_rtt + x);
   }
   RBE_HD void reset_remotes() {  // raft.go:1023-1032
     for (u32 s = 0; s < N; s++) {
-      RemoteMN x;
-      x.match = s == k ? last : 0;
-      x.next = last + 1;
-      *rem(s) = x;
+      set_rmatch(s, s == k ? last : 0);
+      set_rnext(s, last + 1);
       set_rst(s, 0);
     }
     ctr.v[C_REMOTE_TOUCH] += N;
@@ -511,6 +578,7 @@ struct Lane {
     u64 idx = last + 1;
     ring_put(idx, term, type, len, lo, hi);
     last = idx;
+    t_last = term;
     try_update(k, last);
     if (N / 2 + 1 == 1) try_commit();
   }
@@ -520,7 +588,7 @@ struct Lane {
   // values = the quorum-th largest; a register-resident selection over N.
   RBE_HD u64 kth_match() {
     u64 m[N];
-    for (u32 s = 0; s < N; s++) m[s] = rem(s)->match;
+    for (u32 s = 0; s < N; s++) m[s] = rmatch(s);
     // odd-even transposition sort (fully unrolled for a compile-time N)
     for (u32 pass = 0; pass < N; pass++) {
       for (u32 i = pass & 1u; i + 1 < N; i += 2) {
@@ -537,7 +605,7 @@ struct Lane {
   // ------------------------------------------------------------- replication
   RBE_HD void send_replicate(u32 slot) {  // raft.go:758-792
     if (is_paused(slot)) return;
-    u64 next = rem(slot)->next;
+    u64 next = rnext(slot);
     // makeReplicateMessage (raft.go:709-740)
     u64 lt = log_term(next - 1);
     Msg m = mk(M_Replicate, (u8)(slot + 1));
@@ -555,25 +623,27 @@ struct Lane {
     }
     send(m);
   }
+  // Fan-out sends are deferred to the single post-event site in run() (same
+  // emission order: every handler requests them as its last action).
   RBE_HD void broadcast_replicate() {  // raft.go:794-808
-    for (u32 s = 0; s < N; s++)
-      if (s != k) send_replicate(s);
+    rep_mask |= ((1u << N) - 1u) & ~(1u << k);
   }
+  RBE_HD void request_replicate(u32 slot) { rep_mask |= 1u << slot; }  // sendReplicateMessage
   RBE_HD void send_heartbeat(u32 slot, u64 low, u64 high) {  // raft.go:810-820
     Msg m = mk(M_Heartbeat, (u8)(slot + 1));
-    m.commit = umin64(rem(slot)->match, committed);
+    m.commit = umin64(rmatch(slot), committed);
     m.hint = low;
     m.hint_high = high;
     send(m);
   }
   RBE_HD void broadcast_heartbeat_with_hint(u64 low, u64 high) {  // raft.go:834-846
-    for (u32 s = 0; s < N; s++)
-      if (s != k) send_heartbeat(s, low, high);
-    ctr.v[C_REMOTE_TOUCH] += N - 1;
+    hb_pending = true;
+    hb_lo = low;
+    hb_hi = high;
   }
   RBE_HD void broadcast_heartbeat() {  // raft.go:824-832
     if (rq_count > 0) {
-      const ReadReq& q = P.rq[r * C.rq_cap + (u32)((rq_head + rq_count - 1) % C.rq_cap)];
+      const ReadReq& q = *rq_at(rq_count - 1u);
       broadcast_heartbeat_with_hint(q.low, q.high);
     } else {
       broadcast_heartbeat_with_hint(0, 0);
@@ -581,7 +651,8 @@ struct Lane {
   }
 
   // ------------------------------------------------------------- readIndex (kernel 4)
-  RBE_HD ReadReq* rq_at(u32 i) { return &P.rq[r * C.rq_cap + (u32)((rq_head + i) % C.rq_cap)]; }
+  RBE_HD u32 rq_wrap(u32 x) const { return x >= C.rq_cap ? x - C.rq_cap : x; }  // x < 2*cap
+  RBE_HD ReadReq* rq_at(u32 i) { return &P.rq[r * C.rq_cap + rq_wrap((u32)rq_head + i)]; }
   RBE_HD void rq_add(u64 index, u64 low, u64 high, u8 from) {  // readindex.go:43-67
     for (u32 i = 0; i < rq_count; i++) {
       ReadReq* q = rq_at(i);
@@ -635,7 +706,7 @@ struct Lane {
       }
     }
     ctr.v[C_RQ_TOUCH] += done;
-    rq_head = (u8)((rq_head + done) % C.rq_cap);
+    rq_head = (u8)rq_wrap((u32)rq_head + done);
     rq_count = (u8)(rq_count - done);
   }
 
@@ -655,6 +726,7 @@ struct Lane {
       u64 idx = last + 1;
       ring_put(idx, term, ents[i].type, ents[i].len, ents[i].lo, ents[i].hi);
       last = idx;
+      t_last = term;
     }
     try_update(k, last);
     if (N / 2 + 1 == 1) try_commit();
@@ -680,16 +752,16 @@ struct Lane {
       if (try_update(slot, m.log_index)) {
         responded_to(slot);
         if (try_commit()) broadcast_replicate();
-        else if (paused) send_replicate(slot);
-        if (ltt != 0 && role == R_Leader && m.from == ltt && last == rem(slot)->match) {
-          Msg t = mk(M_TimeoutNow, ltt);
-          send(t);
-        }
+        else if (paused) request_replicate(slot);
+        // sendReplicateMessage never changes match/lastIndex/ltt, so the
+        // TimeoutNow condition is evaluated here and the send deferred after
+        // the replicate fan-out, as in the reference
+        if (ltt != 0 && role == R_Leader && m.from == ltt && last == rmatch(slot)) tn_to = ltt;
       }
     } else {
       if (decrease_to(slot, m.log_index, m.hint)) {
         if (rstate(slot) == RS_Replicate) become_retry(slot);  // enterRetryState
-        send_replicate(slot);
+        request_replicate(slot);
       }
     }
   }
@@ -697,8 +769,13 @@ struct Lane {
     set_active(slot, true);
     wait_to_retry(slot);
     ctr.v[C_REMOTE_TOUCH]++;
-    if (rem(slot)->match < last) send_replicate(slot);
-    if (m.hint != 0) rq_confirm(m.hint, m.hint_high, m.from, m.hint, m.hint_high);
+    if (rmatch(slot) < last) request_replicate(slot);
+    if (m.hint != 0) {  // handleReadIndexLeaderConfirmation, after the replicate
+      rq_pending = true;
+      rq_lo = m.hint;
+      rq_hi = m.hint_high;
+      rq_from = m.from;
+    }
   }
   RBE_HD void on_leader_transfer(const Msg& m, u32 slot) {  // raft.go:1712-1734
     u64 target = m.hint;
@@ -710,7 +787,7 @@ struct Lane {
     if (self == target) return;
     ltt = (u8)target;
     etick = 0;
-    if (rem(slot)->match == last) {
+    if (rmatch(slot) == last) {
       Msg t = mk(M_TimeoutNow, (u8)target);
       send(t);
     }
@@ -758,6 +835,7 @@ struct Lane {
             ring_put(m.log_index + 1 + i, ents[i].term, ents[i].type, ents[i].len, ents[i].lo,
                      ents[i].hi);
           last = m.log_index + m.n_ent;
+          t_last = ents[m.n_ent - 1].term;
           saved_to = umin64(saved_to, conflict - 1);
           seg_len = 0;
         }
@@ -847,7 +925,9 @@ struct Lane {
     etick++;
     if (etick >= ret) {  // !selfRemoved() && timeForElection()
       etick = 0;
-      on_election();  // Handle(Election): term 0 passes the gate; handled in any role
+      // Handle(Election): term 0 passes the gate; handled in any role
+      if constexpr (FULL) on_election();
+      else set_fault(F_UNSUPPORTED);  // excluded by fast_eligible()
     }
   }
   RBE_HD void leader_tick() {  // raft.go:592-621
@@ -857,8 +937,12 @@ struct Lane {
       etick = 0;
       if (C.check_quorum) {
         // Handle(CheckQuorum): dispatched by role; leader only
-        if (role == R_Leader) {
-          if (!leader_has_quorum()) become_follower(term, 0);
+        if constexpr (FULL) {
+          if (role == R_Leader) {
+            if (!leader_has_quorum()) become_follower(term, 0);
+          }
+        } else {
+          set_fault(F_UNSUPPORTED);  // excluded by fast_eligible()
         }
       }
     }
@@ -925,6 +1009,10 @@ struct Lane {
   // raft.Handle (raft.go:1451-1458): term gate then the (role, type) table
   // of initializeHandlerMap (raft.go:2037-2098).
   RBE_HD void handle(const Msg& m, const Ent* ents) {
+    if constexpr (!FULL) {
+      handle_fast(m, ents);
+      return;
+    }
     // onMessageTermNotMatched (raft.go:1415-1449)
     if (m.term != 0 && m.term != term) {
       // dropRequestVoteFromHighTermNode (raft.go:1387-1409)
@@ -1052,6 +1140,104 @@ struct Lane {
     }
   }
 
+  // ------------------------------------------------------------- fast path
+  // The steady-state subset of the handler table.  fast_eligible() admits a
+  // replica's round to the fast kernel only when every event of the round is
+  // in this subset (same term, no role change, no election, no check-quorum
+  // boundary, no leader transfer); the result is then identical to handle().
+  RBE_HD void handle_fast(const Msg& m, const Ent* ents) {
+    if (m.term != 0 && m.term != term) {
+      set_fault(F_UNSUPPORTED);
+      return;
+    }
+    if constexpr (FOLL) {
+      switch (m.type) {
+        case M_Replicate:  // raft.go:1859-1863
+          etick = 0;
+          leader = m.from;
+          on_replicate(m, ents);
+          return;
+        case M_Heartbeat:  // raft.go:1865-1869
+          etick = 0;
+          leader = m.from;
+          on_heartbeat(m);
+          return;
+        case M_ReadIndexResp:  // raft.go:1890-1898
+          etick = 0;
+          leader = m.from;
+          add_ready_to_read(m.log_index, m.hint, m.hint_high);
+          return;
+        default: set_fault(F_UNSUPPORTED); return;
+      }
+    }
+    if constexpr (LEAD) {
+      switch (m.type) {
+        case M_Propose: on_leader_propose(ents, m.n_ent); return;
+        case M_ReadIndex: on_leader_read_index(m.hint, m.hint_high, m.from); return;
+        case M_ReplicateResp: on_replicate_resp(m, m.from - 1u); return;
+        case M_HeartbeatResp: on_heartbeat_resp(m, m.from - 1u); return;
+        default: set_fault(F_UNSUPPORTED); return;
+      }
+    }
+  }
+  // Called after load() and before any state is written.  Reads only the
+  // 24-byte message headers of the inbox.
+  RBE_HD bool fast_eligible(u32 inp) const {
+    if (role != (LEAD ? R_Leader : R_Follower)) return false;
+    if (flags & HF_APPLY_PENDING) return false;
+    if (ltt != 0 || (flags & HF_IS_LTT)) return false;
+    if (role == R_Follower && inp) return false;
+    if (C.ext_inputs && P.ext[r].kind) return false;
+    bool from_leader = false;
+    u32 n_in = 0;
+    if (round > 0) {
+      const u32 ppar = par ^ 1u;
+      const u16* icnt = &P.cnt[ppar][g * N * N];
+      for (u32 s = 0; s < N; s++) {
+        if (s == k) continue;
+        const u32 pc = icnt[s * N + k];
+        const u32 na = pc & 0x7Fu, n = na + ((pc >> 7) & 0x7Fu);
+        n_in += n;
+        const Msg* lst = &P.msgs[ppar][msg_slot_base(s, k)];
+        for (u32 i = 0; i < n; i++) {
+          const Msg* mp = i < na ? &lst[i] : &lst[C.maxm - 1u - (i - na)];
+          const u32 t = mp->type;
+          const u64 mt = mp->term;
+          if (role == R_Follower) {
+            if (mt != term || mp->from != leader || leader == 0) return false;
+            if (t != M_Replicate && t != M_Heartbeat && t != M_ReadIndexResp) return false;
+            from_leader = true;
+          } else {
+            if (t == M_ReplicateResp || t == M_HeartbeatResp) {
+              if (mt != term) return false;
+            } else if (t == M_Propose || t == M_ReadIndex) {
+              if (mt != 0) return false;
+              if (t == M_Propose && ((const Ent*)&P.arena[ppar][(g * N + s) * (u64)C.ecap +
+                                                              mp->ent_off])->type ==
+                                        E_ConfigChange)
+                return false;
+            } else {
+              return false;
+            }
+          }
+        }
+      }
+    }
+    // With no message and no client input nothing can exit quiesce before the
+    // tick, so whether the tick is a QuiescedTick is known exactly.
+    const bool idle = n_in == 0 && inp == 0;
+    const bool q_at_tick =
+        idle && C.quiesce && (q_qs > 0 || (q_tick + 1u - q_nas > q_threshold()));
+    if (role == R_Follower) {
+      // the tick must not reach the election timeout (non_leader_tick)
+      if (!from_leader && !q_at_tick && etick + 1u >= ret) return false;
+    } else {
+      // the tick must not reach the check-quorum boundary (leader_tick)
+      if (C.check_quorum && !q_at_tick && etick + 1u >= C.election_rtt) return false;
+    }
+    return true;
+  }
+
   // ------------------------------------------------------------- the step
   RBE_HD void load() {
     Hot h = P.hot[r];
@@ -1073,6 +1259,7 @@ struct Lane {
     last = c.last_index;
     processed = c.processed;
     saved_to = c.saved_to;
+    t_last = c.t_last;
     vote = c.vote;
     leader = c.leader;
     ltt = c.ltt;
@@ -1106,12 +1293,36 @@ struct Lane {
     c.rq_head = rq_head;
     c.rq_count = rq_count;
     c.pad[0] = c.pad[1] = c.pad[2] = 0;
-    c.pad2[0] = c.pad2[1] = 0;
+    c.t_last = t_last;
+    c.pad2 = 0;
     P.core[r] = c;
+    if constexpr (LEAD) {
+      for (u32 s = 0; s < N; s++) {
+        RemoteMN x;
+        x.match = c_match[s];
+        x.next = c_next[s];
+        P.rem[r * N + s] = x;
+        P.rem_st[r * N + s] = (u8)c_st[s];
+      }
+    }
   }
 
-  RBE_HD void run() {
+  // Steps the replica through one round.  The fast variant (FULL = false)
+  // returns false without writing anything when the round needs the full
+  // handler table; the caller then queues the replica for k_full.
+  RBE_HD bool run() {
     load();
+    if constexpr (!FULL) {
+      if (!fast_eligible(role == R_Leader ? wl_input(C, cid, round) : 0u)) return false;
+    }
+    if constexpr (LEAD) {
+      for (u32 s = 0; s < N; s++) {
+        RemoteMN x = P.rem[r * N + s];
+        c_match[s] = x.match;
+        c_next[s] = x.next;
+        c_st[s] = P.rem_st[r * N + s];
+      }
+    }
     fault = P.upd[r].fault;
     const u64 digest0 = P.upd[r].digest;
     pc_lo = pc_hi = 0;
@@ -1150,23 +1361,118 @@ struct Lane {
       q_record_activity(M_ReadIndex);
       ctr.v[C_READS]++;
     }
-    // handleReceivedMessages (node.go:1171-1205): inbox in (sender, stream) order
+    // One event loop, one handle() site.  Events in node order:
+    //   handleReceivedMessages (node.go:1171-1205): inbox in (sender, stream) order
+    //   batchedReadIndex (node.go:1379-1382) → Peer.ReadIndex
+    //   handleLocalTickMessage → node.tick (node.go:1384-1399): one tick per round
+    //   handleProposals (node.go:1091-1106) → Peer.ProposeEntries
     const u32 ppar = par ^ 1u;
-    if (round > 0) {
-      const u16* cnt = &P.cnt[ppar][g * N * N];
-      for (u32 s = 0; s < N; s++) {
-        if (s == k) continue;
-        const u32 pc = cnt[s * N + k];
-        if (pc == 0) continue;
-        const u32 na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
-        if (pc & 0x8000u) {  // Quiesce (node.go:1207-1210)
-          ctr.v[C_MSG_IN]++;
-          q_try_enter();
+    const u16* icnt = &P.cnt[ppar][g * N * N];
+    u32 cs = 0, ci = 0, cn = 0, cna = 0;  // inbox cursor: sender, index, count, #A
+    bool copen = false;
+    u32 phase = round > 0 ? 0u : 1u;
+    rep_mask = 0;
+    tn_to = 0;
+    hb_pending = rq_pending = false;
+    hb_lo = hb_hi = rq_lo = rq_hi = 0;
+    rq_from = 0;
+#pragma unroll 1
+    for (;;) {
+      u32 kind = 0;  // 0 none, 1 inbox message, 2 local message, 3 tick
+      Msg m;
+      u64 ents_off = 0;  // entries of m: P.arena[ents_par] + ents_off
+      u32 ents_par = ppar;
+      if (phase == 0) {
+#pragma unroll 1
+        while (cs < N) {
+          if (!copen) {
+            if (cs == k) {
+              cs++;
+              continue;
+            }
+            const u32 pc = icnt[cs * N + k];
+            if (pc & 0x8000u) {  // Quiesce first in the sender's stream (node.go:1207-1210)
+              ctr.v[C_MSG_IN]++;
+              q_try_enter();
+            }
+            cna = pc & 0x7Fu;
+            cn = cna + ((pc >> 7) & 0x7Fu);
+            ci = 0;
+            copen = true;
+          }
+          if (ci < cn) {
+            const Msg* lst = &P.msgs[ppar][msg_slot_base(cs, k)];
+            m = ci < cna ? lst[ci] : lst[C.maxm - 1u - (ci - cna)];
+            ents_off = (g * N + cs) * (u64)C.ecap + m.ent_off;
+            ci++;
+            kind = 1;
+            break;
+          }
+          cs++;
+          copen = false;
         }
-        const Msg* lst = &P.msgs[ppar][msg_slot_base(s, k)];
-        const Ent* sarena = &P.arena[ppar][(g * N + s) * (u64)C.ecap];
-        for (u32 i = 0; i < na + nb; i++) {
-          const Msg m = i < na ? lst[i] : lst[C.maxm - 1u - (i - na)];
+        if (kind == 0) phase = 1;
+      }
+      if (kind == 0 && phase == 1) {
+        phase = 2;
+        if (inp == 2) {
+          m = mk(M_ReadIndex, 0);
+          if (C.ext_inputs && ext.kind == 2) {
+            m.hint = ext.ctx_low;
+            m.hint_high = ext.ctx_high;
+          } else {
+            m.hint = ((u64)(round + 1) << 32) | (u64)self;
+            m.hint_high = cid + 1;
+          }
+          kind = 2;
+        }
+      }
+      if (kind == 0 && phase == 2) {
+        phase = 3;
+        kind = 3;
+      }
+      if (kind == 0 && phase == 3) {
+        phase = 4;
+        if (inp == 1) {
+          Ent e;
+          e.term = 0;
+          e.type = E_Application;
+          if (C.ext_inputs && ext.kind == 1) {
+            e.len = ext.len;
+            e.lo = ext.lo;
+            e.hi = ext.hi;
+          } else {
+            e.len = 16;
+            e.lo = wl_payload_lo(C.seed, cid, round);
+            e.hi = mix64(e.lo);
+          }
+          // the proposed entry is staged in this round's arena so every
+          // handler reads entries from global memory
+          u32 off = 0;
+          if (arena_put(&e, 1, &off)) {
+            m = mk(M_Propose, 0);
+            m.from = self;  // Peer.ProposeEntries (peer.go:117-123)
+            m.n_ent = 1;
+            ents_par = par;
+            ents_off = r * (u64)C.ecap + off;
+            kind = 2;
+          }
+          ctr.v[C_PROPOSALS]++;
+        }
+      }
+      if (kind == 0) break;
+      if (kind == 3) {
+        q_increase_tick();
+        if (q_quiesced()) {
+          quiesced_tick();
+          ctr.v[C_QUIESCED_TICKS]++;
+        } else {
+          flags &= (u8)~HF_RAFT_QUIESCE;  // raft.tick: r.quiesce = false
+          raft_tick();
+          ctr.v[C_ACTIVE_TICKS]++;
+        }
+      } else {
+        if (kind == 1) {
           ctr.v[C_MSG_IN]++;
           ctr.v[C_ENT_IN] += m.n_ent;
           // tryRecordNodeActivity (node.go:1161-1169)
@@ -1174,50 +1480,32 @@ struct Lane {
             q_record_activity(M_ReadIndex);
           else
             q_record_activity(m.type);
-          handle(m, m.n_ent ? sarena + m.ent_off : (const Ent*)0);
         }
+        handle(m, &P.arena[ents_par][ents_off]);
       }
-    }
-    if (inp == 2) {  // batchedReadIndex (node.go:1379-1382) → Peer.ReadIndex
-      Msg m = mk(M_ReadIndex, 0);
-      if (C.ext_inputs && ext.kind == 2) {
-        m.hint = ext.ctx_low;
-        m.hint_high = ext.ctx_high;
-      } else {
-        m.hint = ((u64)(round + 1) << 32) | (u64)self;
-        m.hint_high = cid + 1;
+      // deferred fan-out, in the reference's emission order
+#pragma unroll 1
+      while (rep_mask) {
+        const u32 s = (u32)__builtin_ctz(rep_mask);
+        rep_mask &= rep_mask - 1u;
+        send_replicate(s);
       }
-      handle(m, (const Ent*)0);
-    }
-    // handleLocalTickMessage → node.tick (node.go:1384-1399): one tick per round
-    q_increase_tick();
-    if (q_quiesced()) {
-      quiesced_tick();
-      ctr.v[C_QUIESCED_TICKS]++;
-    } else {
-      flags &= (u8)~HF_RAFT_QUIESCE;  // raft.tick: r.quiesce = false
-      raft_tick();
-      ctr.v[C_ACTIVE_TICKS]++;
-    }
-    // handleProposals (node.go:1091-1106) → Peer.ProposeEntries
-    if (inp == 1) {
-      Ent e;
-      e.term = 0;
-      e.type = E_Application;
-      if (C.ext_inputs && ext.kind == 1) {
-        e.len = ext.len;
-        e.lo = ext.lo;
-        e.hi = ext.hi;
-      } else {
-        e.len = 16;
-        e.lo = wl_payload_lo(C.seed, cid, round);
-        e.hi = mix64(e.lo);
+      if (tn_to) {
+        Msg t = mk(M_TimeoutNow, tn_to);
+        tn_to = 0;
+        send(t);
       }
-      Msg m = mk(M_Propose, 0);
-      m.from = self;  // Peer.ProposeEntries (peer.go:117-123)
-      m.n_ent = 1;
-      handle(m, &e);
-      ctr.v[C_PROPOSALS]++;
+      if (hb_pending) {
+        hb_pending = false;
+#pragma unroll 1
+        for (u32 s = 0; s < N; s++)
+          if (s != k) send_heartbeat(s, hb_lo, hb_hi);
+        ctr.v[C_REMOTE_TOUCH] += N - 1;
+      }
+      if (rq_pending) {
+        rq_pending = false;
+        rq_confirm(rq_lo, rq_hi, rq_from, rq_lo, rq_hi);
+      }
     }
     // stepNode: newQuiesceState → sendEnterQuiesceMessages (node.go:873-886)
     const bool send_q = q_new;
@@ -1266,12 +1554,14 @@ struct Lane {
     ctr.v[C_DROPPED_READS] += n_drop_ri;
     if (u.apply_hi >= u.apply_lo) processed = u.apply_hi;
     saved_to = last;
+    if (processed < committed) flags |= HF_APPLY_PENDING;
+    else flags &= (u8)~HF_APPLY_PENDING;
     if (role == R_Leader) {
       ctr.v[C_COMMITTED] += (u32)(committed - committed0);
       ctr.v[C_LEADER_STEPS]++;
     }
     u64 d = digest0;
-    if (C.trace) {
+    if (TRACE) {
       u64 dh = drop_hash;
       for (u32 i = 0; i < n_drop_ri; i++) {
         DropRI x = P.dri[r * C.dri_cap + i];
@@ -1296,32 +1586,46 @@ struct Lane {
       d = hfold(d, dh);
     }
     u.digest = d;
-    u.n_msgs = n_msgs;
-    u.n_rtr = n_rtr;
-    u.n_drop_ent = n_drop_ent;
-    u.n_drop_ri = n_drop_ri;
+    u.n_msgs = (u16)n_msgs;
+    u.n_rtr = (u16)n_rtr;
+    u.n_drop_ent = (u16)n_drop_ent;
+    u.n_drop_ri = (u16)n_drop_ri;
     u.fault = fault;
-    u.flags = (term != term0 || vote != vote0 || committed != committed0 ? UF_STATE_CHANGED : 0u) |
-              (send_q ? UF_SENT_QUIESCE : 0u);
+    u.flags = (u16)((term != term0 || vote != vote0 || committed != committed0 ? UF_STATE_CHANGED
+                                                                                : 0u) |
+                    (send_q ? UF_SENT_QUIESCE : 0u));
+    u.pad = 0;
+    u.round = round;
+    u.pad2 = 0;
     P.upd[r] = u;
     // this round's outbox counts for every destination (zeros included)
     u16* cnt = &P.cnt[par][g * N * N + k * N];
     for (u32 dd = 0; dd < N; dd++) cnt[dd] = (u16)get_pc(dd);
     store();
+    return true;
   }
 };
 
-template <int N>
-RBE_HD void Lane<N>::raft_tick() {  // raft.go:551-564
+template <int N, bool TRACE, int MODE>
+RBE_HD void Lane<N, TRACE, MODE>::raft_tick() {  // raft.go:551-564
   flags &= (u8)~HF_RAFT_QUIESCE;
   if (role == R_Leader) leader_tick();
   else non_leader_tick();
 }
 
-template <int N>
+// the full handler table: always completes the round
+template <int N, bool TRACE>
 RBE_HD void step_replica(const Planes& P, const Params& C, u64 r, u32 round, StepCounters& ctr) {
-  Lane<N> lane(P, C, r, round, ctr);
+  Lane<N, TRACE, MODE_FULL> lane(P, C, r, round, ctr);
   lane.run();
+}
+// the steady-state subset: returns false (nothing written) when the round
+// needs the full table
+template <int N, bool TRACE, int MODE>
+RBE_HD bool step_replica_fast(const Planes& P, const Params& C, u64 r, u32 round,
+                              StepCounters& ctr) {
+  Lane<N, TRACE, MODE> lane(P, C, r, round, ctr);
+  return lane.run();
 }
 
 // ------------------------------------------------------------------ launch
@@ -1336,11 +1640,11 @@ RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   const u64 self = k + 1;
   Hot h;
   h.role = R_Follower;
-  h.flags = 0;
+  h.flags = HF_APPLY_PENDING;  // the bootstrap entries are saved and applied in round 0
   h.votes_resp = h.votes_granted = 0;
   h.election_tick = 0;
   h.heartbeat_tick = 0;
-  u64 rt = rto_rand(C.seed, cid, self, 1) % C.election_rtt;  // the second draw wins
+  u64 rt = below(rto_rand(C.seed, cid, self, 1), C.election_rtt);  // the second draw wins
   h.rand_et = (u16)(C.election_rtt + rt);
   h.q_tick = h.q_quiesced_since = h.q_no_activity_since = h.q_exit_quiesce_tick = 0;
   h.rng_count = 2;
@@ -1356,7 +1660,8 @@ RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   c.ltt = 0;
   c.rq_head = c.rq_count = 0;
   c.pad[0] = c.pad[1] = c.pad[2] = 0;
-  c.pad2[0] = c.pad2[1] = 0;
+  c.t_last = 1;  // bootstrap entries are at term 1
+  c.pad2 = 0;
   P.core[r] = c;
   for (u32 s = 0; s < N; s++) {
     RemoteMN x;
@@ -1384,7 +1689,139 @@ RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   u.n_msgs = u.n_rtr = u.n_drop_ent = u.n_drop_ri = 0;
   u.fault = 0;
   u.flags = 0;
+  u.pad = 0;
+  u.round = ~0u;
+  u.pad2 = 0;
   P.upd[r] = u;
+}
+
+// ------------------------------------------------------------------ triage
+// First pass of every round over every replica.  A round with no inbound
+// message (Quiesce notices aside), no client input and a tick that neither
+// elects nor heartbeats is executed completely here, in registers, touching
+// only the hot plane and the outbox-count row: handleReceivedMessages sees
+// only Quiesce (node.go:1207-1210 → quiesce.go:102-110), node.tick
+// (node.go:1384-1399) runs increaseQuiesceTick + QuiescedTick, or Tick with
+// electionTick++ below the randomized timeout (raft.go:566-590, 623-629).
+// Everything else is routed to the leader / follower / full lists.
+enum : u32 { T_DONE = 0, T_LEAD = 1, T_FOLL = 2, T_FULL = 3 };
+
+template <int N, bool TRACE>
+RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, u32 round,
+                          StepCounters& ctr) {
+  const u64 g = r / N;
+  const u32 k = (u32)(r % N);
+  const u32 par = round & 1u;
+  const Hot h = P.hot[r];
+  u32 nmsg = 0, qbits = 0;
+  if (round > 0) {
+    const u16* icnt = &P.cnt[par ^ 1u][g * N * N];
+    for (u32 s = 0; s < N; s++) {
+      if (s == k) continue;
+      const u32 pc = icnt[s * N + k];
+      nmsg += (pc & 0x7Fu) + ((pc >> 7) & 0x7Fu);
+      if (pc & 0x8000u) qbits |= 1u << s;
+    }
+  }
+  const u64 cid = C.cid_base + g * C.cid_stride;
+  const u32 cls = h.role == R_Leader ? T_LEAD : (h.role == R_Follower ? T_FOLL : T_FULL);
+  if (nmsg || (h.flags & HF_APPLY_PENDING)) return cls;
+  if (h.role == R_Leader && wl_input(C, cid, round)) return cls;
+  if (C.ext_inputs && P.ext[r].kind) return cls;
+  // quiesceManager (quiesce.go) on registers
+  const u32 et2 = C.election_rtt * 2, thr = et2 * 10;
+  u32 qt = h.q_tick, qs = h.q_quiesced_since, qn = h.q_no_activity_since, qe = h.q_exit_quiesce_tick;
+  bool qnew = false;
+  for (u32 s = 0; s < N; s++) {
+    if (!((qbits >> s) & 1u)) continue;
+    // tryEnterQuiesce: not right after an exit, not already quiesced
+    const bool quiesced = C.quiesce && qs > 0;
+    const bool just_exited = !quiesced && qt - qe < thr;
+    if (!just_exited && !quiesced) {
+      qs = qt;
+      qn = qt;
+      qnew = true;
+    }
+  }
+  if (C.quiesce) {  // increaseQuiesceTick
+    qt++;
+    if (!(qs > 0) && qt - qn > thr) {
+      qs = qt;
+      qn = qt;
+      qnew = true;
+    }
+  }
+  const bool quiesced = C.quiesce && qs > 0;
+  u32 etick = h.election_tick;
+  u8 flags = h.flags;
+  if (quiesced) {
+    flags |= HF_RAFT_QUIESCE;  // quiescedTick
+    etick++;
+  } else {
+    if (h.role == R_Leader) return cls;          // leaderTick broadcasts heartbeats
+    if (etick + 1u >= h.rand_et) return cls;     // nonLeaderTick would elect
+    flags &= (u8)~HF_RAFT_QUIESCE;
+    etick++;
+  }
+  // commit the idle round
+  ctr.v[C_STEPS]++;
+  ctr.v[C_MSG_IN] += popc8(qbits);
+  if (quiesced) ctr.v[C_QUIESCED_TICKS]++;
+  else ctr.v[C_ACTIVE_TICKS]++;
+  if (h.role == R_Leader) ctr.v[C_LEADER_STEPS]++;
+  u8 iso = 0;
+  if (qnew) {
+    const u32 until = P.iso_until[g];
+    iso = round < until ? P.iso_mask[g] : (u8)0;
+  }
+  u16* cnt = &P.cnt[par][g * N * N + k * N];
+  for (u32 d = 0; d < N; d++) {
+    u16 v = 0;
+    if (qnew && d != k) {  // sendEnterQuiesceMessages (node.go:873-886)
+      if (((iso >> k) & 1u) || ((iso >> d) & 1u)) {
+        ctr.v[C_MSG_DROPPED]++;
+      } else {
+        v = 0x8000u;
+        ctr.v[C_MSG_OUT]++;
+      }
+    }
+    cnt[d] = v;
+  }
+  Hot o = h;
+  o.flags = flags;
+  o.election_tick = etick;
+  o.q_tick = qt;
+  o.q_quiesced_since = qs;
+  o.q_no_activity_since = qn;
+  o.q_exit_quiesce_tick = qe;
+  P.hot[r] = o;
+  if (TRACE) {
+    const Core c = P.core[r];
+    Upd u = P.upd[r];
+    u64 d = u.digest;
+    d = hfold(d, round);
+    d = hfold(d, (u64)h.role | ((u64)(quiesced ? 1 : 0) << 8) | ((u64)(qnew ? 1 : 0) << 9) |
+                     ((u64)((flags & HF_RAFT_QUIESCE) ? 1 : 0) << 10));
+    d = hfold(d, c.term);
+    d = hfold(d, c.vote);
+    d = hfold(d, c.leader);
+    d = hfold(d, c.committed);
+    d = hfold(d, c.last_index);
+    d = hfold(d, c.processed);
+    d = hfold(d, (u64)etick | ((u64)h.heartbeat_tick << 32));
+    d = hfold(d, h.rand_et);
+    for (int i = 0; i < 5; i++) d = hfold(d, 0);  // no messages, reads, applies, drops
+    u.digest = d;
+    u.save_lo = c.saved_to + 1;
+    u.save_hi = c.last_index;
+    u.apply_lo = c.processed + 1;
+    u.apply_hi = c.committed;
+    u.n_msgs = u.n_rtr = u.n_drop_ent = u.n_drop_ri = 0;
+    u.flags = (u16)(qnew ? UF_SENT_QUIESCE : 0u);
+    u.round = round;
+    P.upd[r] = u;
+  }
+  return T_DONE;
 }
 
 // fault schedule: at epoch rounds, isolate the replicas of

@@ -65,6 +65,7 @@ enum : u8 {
   HF_RAFT_QUIESCE = 1,  // raft.quiesce
   HF_PENDING_CC = 2,    // raft.pendingConfigChange
   HF_IS_LTT = 4,        // raft.isLeaderTransferTarget
+  HF_APPLY_PENDING = 8, // processed < committed after the step (apply limited by size)
 };
 
 // core plane (64 B per replica)
@@ -80,7 +81,8 @@ struct alignas(16) Core {
   u8 rq_head;      // readIndex queue ring head
   u8 rq_count;
   u8 pad[3];
-  u64 pad2[2];
+  u64 t_last;      // term of entry last_index (log-tail cache)
+  u64 pad2;
 };
 
 // remote slot (remote.go:62-69): match/next; state|active<<2 lives in a u8 plane
@@ -130,12 +132,15 @@ struct alignas(16) Upd {
   u64 save_hi;
   u64 apply_lo;     // CommittedEntries = [apply_lo, apply_hi]
   u64 apply_hi;
-  u32 n_msgs;       // messages emitted this step (Update.Messages)
-  u32 n_rtr;        // ReadyToReads
-  u32 n_drop_ent;   // DroppedEntries
-  u32 n_drop_ri;    // DroppedReadIndexes
+  u16 n_msgs;       // messages emitted this step (Update.Messages)
+  u16 n_rtr;        // ReadyToReads
+  u16 n_drop_ent;   // DroppedEntries
+  u16 n_drop_ri;    // DroppedReadIndexes
   u32 fault;        // sticky F_* bits
-  u32 flags;        // UF_* bits
+  u16 flags;        // UF_* bits
+  u16 pad;
+  u32 round;        // round this record was written in (idle rounds leave it stale)
+  u32 pad2;
 };
 enum : u32 { UF_STATE_CHANGED = 1, UF_SENT_QUIESCE = 2, UF_HAS_UPDATE = 4 };
 

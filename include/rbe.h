@@ -97,7 +97,7 @@ typedef struct rbe_config {
   uint32_t ring;             /* in-memory entry window per replica (power of 2), 0 = 64 */
   uint32_t rq_cap;           /* pending ReadIndex requests per leader, 0 = 8 */
   uint32_t maxm;             /* message slots per (sender, destination) per round, 0 = 12 */
-  uint32_t ecap;             /* entry slots per sender per round, 0 = 2 * ring */
+  uint32_t ecap;             /* entry slots per sender per round, 0 = 32 */
   uint32_t rtr_cap;          /* ReadyToRead slots per replica per round, 0 = 8 */
   uint32_t dri_cap;          /* dropped ReadIndex slots per replica per round, 0 = 8 */
   uint32_t trace;            /* maintain per-replica trace digests */

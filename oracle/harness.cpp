@@ -17,8 +17,8 @@ u64 wl_payload_lo(u64 seed, u64 cid, u64 round) {
 
 bool wl_group_active(const HarnessConfig& c, u64 cid) {
   if (c.wl_active_mod <= 1) return true;
-  return splitmix64(c.seed ^ 0xA5A5A5A5A5A5A5A5ULL ^ (cid * 0x9E3779B97F4A7C15ULL)) %
-             c.wl_active_mod == 0;
+  return below(splitmix64(c.seed ^ 0xA5A5A5A5A5A5A5A5ULL ^ (cid * 0x9E3779B97F4A7C15ULL)),
+               c.wl_active_mod) == 0;
 }
 
 int wl_input(const HarnessConfig& c, u64 cid, u32 round) {
@@ -27,14 +27,14 @@ int wl_input(const HarnessConfig& c, u64 cid, u32 round) {
   if (c.wl_stop_round != 0 && round >= c.wl_stop_round) return 0;
   if (!wl_group_active(c, cid)) return 0;
   if (c.wl_read_permille == 0) return 1;
-  u64 u = splitmix64(c.seed ^ (cid * 0xC2B2AE3D27D4EB4FULL) ^ ((u64)round << 20)) % 1000;
+  u64 u = below(splitmix64(c.seed ^ (cid * 0xC2B2AE3D27D4EB4FULL) ^ ((u64)round << 20)), 1000);
   return u < c.wl_read_permille ? 2 : 1;
 }
 
 bool iso_selected(const HarnessConfig& c, u64 cid, u32 epoch) {
   if (c.iso_mod <= 1) return true;
-  return splitmix64(c.seed ^ (cid * 0x94D049BB133111EBULL) ^ ((u64)epoch << 40)) %
-             c.iso_mod == 0;
+  return below(splitmix64(c.seed ^ (cid * 0x94D049BB133111EBULL) ^ ((u64)epoch << 40)),
+               c.iso_mod) == 0;
 }
 
 // ------------------------------------------------------------ quiesce.go

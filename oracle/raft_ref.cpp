@@ -810,7 +810,7 @@ void Raft::quiescedTick() {  // raft.go:623-629
 }
 
 void Raft::setRandomizedElectionTimeout() {  // raft.go:631-634
-  u64 randTime = rto_rand(rngSeed, clusterID, nodeID, rngCount++) % electionTimeout;
+  u64 randTime = below(rto_rand(rngSeed, clusterID, nodeID, rngCount++), electionTimeout);
   randomizedElectionTimeout = electionTimeout + randTime;
 }
 

@@ -79,6 +79,10 @@ inline u64 splitmix64(u64 x) {
   x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
   return x ^ (x >> 31);
 }
+// Uniform draw in [0, m) from the high 32 bits of x (multiply-shift).  The
+// reference computes Uint64() % electionTimeout; the injected source is ours
+// to define, and this form needs no 64-bit division on device.
+inline u64 below(u64 x, u64 m) { return ((x >> 32) * (m & 0xFFFFFFFFULL)) >> 32; }
 // Injected replacement for random.LockGuardedRand.Uint64() at raft.go:632.
 inline u64 rto_rand(u64 seed, u64 cid, u64 nid, u64 count) {
   return splitmix64(seed ^ (cid * 0x9E3779B97F4A7C15ULL) ^ (nid << 32) ^ count);

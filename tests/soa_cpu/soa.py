@@ -24,6 +24,9 @@ def lib():
         L.soa_run.argtypes = [C.c_void_p, C.c_uint32]
         L.soa_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         L.soa_views.argtypes = [C.c_void_p, C.c_void_p]
+        L.soa_set_full_only.argtypes = [C.c_void_p, C.c_int]
+        L.soa_slow_total.restype = C.c_uint64
+        L.soa_slow_total.argtypes = [C.c_void_p]
         L.soa_faults.restype = C.c_uint32
         L.soa_faults.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         _lib = L
@@ -31,12 +34,16 @@ def lib():
 
 
 class SoaCpu:
-    def __init__(self, **kw):
+    def __init__(self, full_only=False, **kw):
         self.cfg = make_config(**kw)
         self.n_rep = self.cfg.n_groups * self.cfg.n_replicas
         self.h = lib().soa_create(C.byref(self.cfg))
         if not self.h:
             raise RuntimeError("soa_create failed")
+        lib().soa_set_full_only(self.h, int(full_only))
+
+    def slow_total(self):
+        return lib().soa_slow_total(self.h)
 
     def __del__(self):
         if getattr(self, "h", None):

@@ -19,6 +19,8 @@ struct SoaEngine {
   std::vector<std::vector<uint8_t>> bufs;
   u32 round = 0;
   u64 counters[C_NUM] = {0};
+  bool full_only = false;
+  u64 slow_total = 0;
 };
 
 template <typename T>
@@ -31,12 +33,41 @@ template <int N>
 static void run_round(SoaEngine* e) {
   if (e->C.iso_period && e->round > 0 && e->round % e->C.iso_period == 0)
     for (u64 g = 0; g < e->C.n_groups; g++) iso_group<N>(e->P, e->C, g, e->round);
+  // the GPU pipeline, sequentially: triage → leader fast list → follower fast
+  // list → full list (k_triage / k_fast_list / k_full_list)
   StepCounters c;
+  std::vector<u64> lists[3];
   for (u64 r = 0; r < e->C.n_rep; r++) {
     memset(&c, 0, sizeof(c));
-    step_replica<N>(e->P, e->C, r, e->round, c);
+    u32 cls = T_FULL;
+    if (!e->full_only)
+      cls = e->C.trace ? triage_replica<N, true>(e->P, e->C, r, e->round, c)
+                       : triage_replica<N, false>(e->P, e->C, r, e->round, c);
+    if (cls != T_DONE) lists[cls - 1].push_back(r);
     for (int i = 0; i < C_NUM; i++) e->counters[i] += c.v[i];
   }
+  for (int li = 0; li < 2; li++) {
+    for (u64 r : lists[li]) {
+      memset(&c, 0, sizeof(c));
+      bool ok;
+      if (li == 0)
+        ok = e->C.trace ? step_replica_fast<N, true, MODE_LEAD>(e->P, e->C, r, e->round, c)
+                        : step_replica_fast<N, false, MODE_LEAD>(e->P, e->C, r, e->round, c);
+      else
+        ok = e->C.trace ? step_replica_fast<N, true, MODE_FOLL>(e->P, e->C, r, e->round, c)
+                        : step_replica_fast<N, false, MODE_FOLL>(e->P, e->C, r, e->round, c);
+      if (!ok) lists[2].push_back(r);
+      for (int i = 0; i < C_NUM; i++) e->counters[i] += c.v[i];
+    }
+  }
+  std::vector<u64>& slow = lists[2];
+  for (u64 r : slow) {
+    memset(&c, 0, sizeof(c));
+    if (e->C.trace) step_replica<N, true>(e->P, e->C, r, e->round, c);
+    else step_replica<N, false>(e->P, e->C, r, e->round, c);
+    for (int i = 0; i < C_NUM; i++) e->counters[i] += c.v[i];
+  }
+  e->slow_total += slow.size();
   e->round++;
 }
 
@@ -56,7 +87,7 @@ void* soa_create(const rbe_config* cfg) {
   C.ring = cfg->ring ? cfg->ring : 64;
   C.rq_cap = cfg->rq_cap ? cfg->rq_cap : 8;
   C.maxm = cfg->maxm ? cfg->maxm : 12;
-  C.ecap = cfg->ecap ? cfg->ecap : 2 * C.ring;
+  C.ecap = cfg->ecap ? cfg->ecap : 32;
   C.rtr_cap = cfg->rtr_cap ? cfg->rtr_cap : 8;
   C.dri_cap = cfg->dri_cap ? cfg->dri_cap : 8;
   C.election_rtt = cfg->election_rtt;
@@ -107,6 +138,8 @@ void* soa_create(const rbe_config* cfg) {
 }
 
 void soa_destroy(void* h) { delete (SoaEngine*)h; }
+void soa_set_full_only(void* h, int v) { ((SoaEngine*)h)->full_only = v != 0; }
+uint64_t soa_slow_total(void* h) { return ((SoaEngine*)h)->slow_total; }
 
 void soa_run(void* h, uint32_t rounds) {
   SoaEngine* e = (SoaEngine*)h;
