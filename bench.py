@@ -94,15 +94,21 @@ def cpu_baseline(name, groups, settle, rounds, threads):
     }
 
 
-def load_traffic(name):
-    """HBM bytes per k_step launch from the committed PMC summary, if any."""
+def alg_bytes(c):
+    """SURVEY.md §8(d) algorithmic bytes of a counter set."""
+    return sum(BYTES[k] * c[k] for k in BYTES)
+
+
+def load_traffic(name, kernel):
+    """Measured HBM bytes per launch of `kernel` from the committed PMC summary
+    (profiles/traffic_<workload>.json, written by scripts/pmc_traffic.py), if any."""
     p = os.path.join(ROOT, "profiles", f"traffic_{name}.json")
     if not os.path.exists(p):
         return None
     try:
         with open(p) as f:
-            return json.load(f).get("bytes_per_launch")
-    except Exception:
+            return json.load(f).get("bytes_per_launch", {}).get(kernel)
+    except (OSError, ValueError, AttributeError):
         return None
 
 
@@ -114,6 +120,8 @@ def main():
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
     ap.add_argument("--groups", type=int, default=0, help="override groups per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--prof-rounds", type=int, default=50,
+                    help="rounds profiled per kernel with HIP events after the timed region")
     ap.add_argument("--cpu-groups", type=int, default=30000)
     ap.add_argument("--cpu-rounds", type=int, default=100)
     ap.add_argument("--cpu-threads", type=int,
@@ -131,7 +139,7 @@ def main():
         dist.init_process_group(backend=backend)
     dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
 
-    from dragonboat_amd.engine import Engine, footprint, make_config
+    from dragonboat_amd.engine import KERNEL_NAMES, Engine, footprint, make_config
 
     kw, settle, desc = WORKLOADS[args.workload]
     kw = dict(kw)
@@ -174,12 +182,25 @@ def main():
         wall_max = wall
         steps, committed, reads, faulty = [float(x) for x in local_vals[1:].tolist()]
 
-    # roofline of the dominant kernel (k_step) on this rank
-    alg_bytes = sum(BYTES[k] * c[k] for k in BYTES)
-    per_launch = alg_bytes / args.steps
-    avg_launch_s = (ev_ms / 1e3) / args.steps
-    achieved = per_launch / avg_launch_s / 1e9
-    traffic = load_traffic(args.workload)
+    # whole-round algorithmic bandwidth over the timed region (all kernels)
+    round_bytes = alg_bytes(c) / args.steps
+    round_gbs = round_bytes / ((ev_ms / 1e3) / args.steps) / 1e9
+
+    # per-kernel split: a further `prof_rounds` rounds, one at a time, with
+    # HIP events between the pipeline kernels on the engine stream and each
+    # kernel's own counters -> the dominant kernel's roofline
+    prof_rounds = max(1, min(args.steps, args.prof_rounds))
+    eng.reset_counters()
+    kms = eng.profile_rounds(prof_rounds)
+    kernels = []
+    for ki, name in enumerate(KERNEL_NAMES):
+        kc = eng.kernel_counters(ki)
+        b = alg_bytes(kc) / prof_rounds
+        us = kms[ki] * 1e3 / prof_rounds
+        kernels.append({"kernel": name, "avg_us": us, "alg_bytes_per_launch": b,
+                        "achieved_gbs": (b / (us * 1e-6) / 1e9) if us > 0 else 0.0})
+    dom = max(kernels, key=lambda k: k["avg_us"])
+    traffic = load_traffic(args.workload, dom["kernel"])
 
     if rank == 0:
         out = {
@@ -210,14 +231,22 @@ def main():
             "faulty_replicas": int(faulty),
             "roofline": {
                 "bound": "hbm",
-                "achieved": achieved,
+                "achieved": dom["achieved_gbs"],
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
+                "frac": dom["achieved_gbs"] / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "k_step<3>",
-                "alg_bytes_per_launch": per_launch,
-                "avg_launch_us": avg_launch_s * 1e6,
+                "kernel": dom["kernel"],
+                "alg_bytes_per_launch": dom["alg_bytes_per_launch"],
+                "avg_launch_us": dom["avg_us"],
+                "profiled_rounds": prof_rounds,
+            },
+            "round": {
+                "alg_bytes_per_round": round_bytes,
+                "achieved_gbs": round_gbs,
+                "frac": round_gbs / HBM_PEAK_GBS,
+                "event_ms_per_round": ev_ms / args.steps,
+                "kernels": kernels,
             },
         }
         if not args.no_cpu_baseline and ws == 1:

@@ -31,6 +31,11 @@ using namespace rbe;
   } while (0)
 
 static constexpr int kBlock = 256;
+static constexpr u32 kTriChunk = 2048;   // replicas per k_triage block (8 per lane)
+static constexpr int kCtrStripes = 64;   // counter stripes per kernel slot (flush_counters)
+// counter sections, one per pipeline kernel (rbe_get_kernel_counters)
+enum : int { KS_TRIAGE = 0, KS_FAST_LEAD = 1, KS_FAST_FOLL = 2, KS_FULL = 3, KS_NUM = 4 };
+static constexpr u64 kCtrWords = (u64)KS_NUM * kCtrStripes * C_NUM;
 
 // ------------------------------------------------------------------ kernels
 __device__ __forceinline__ u32 wave_sum(u32 v) {
@@ -39,14 +44,31 @@ __device__ __forceinline__ u32 wave_sum(u32 v) {
   return v;
 }
 
+// Event counters live in kCtrStripes stripes of C_NUM u64 (192 B apart, so
+// each stripe is its own L2 line).  A block reduces its lanes' counters through
+// shuffles and LDS and adds each non-zero total with ONE atomic into stripe
+// blockIdx % kCtrStripes: same-address atomics serialise in one L2 channel, so
+// one-atomic-per-wave into a single line was the round's bottleneck (r01 profile).
+// Every thread of the block must call this (it synchronises the block).
+template <int KS>
 __device__ __forceinline__ void flush_counters(const Planes& P, const StepCounters& c) {
-  const int lane = threadIdx.x & 63;
+  __shared__ u32 s_ctr[kBlock / 64][C_NUM];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) {
-    // skip the reduction when no lane of the wave saw the event
-    if (__ballot(c.v[i] != 0) == 0ull) continue;
-    const u32 s = wave_sum(c.v[i]);
-    if (lane == 0) atomicAdd((unsigned long long*)&P.counters[i], (unsigned long long)s);
+    u32 s = 0;
+    if (__ballot(c.v[i] != 0) != 0ull) s = wave_sum(c.v[i]);
+    if (lane == 0) s_ctr[w][i] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < C_NUM) {
+    u32 t = 0;
+#pragma unroll
+    for (int j = 0; j < kBlock / 64; j++) t += s_ctr[j][threadIdx.x];
+    if (t)
+      atomicAdd((unsigned long long*)&P.counters[((u64)KS * kCtrStripes + blockIdx.x % kCtrStripes) *
+                                                     C_NUM + threadIdx.x],
+                (unsigned long long)t);
   }
 }
 
@@ -60,7 +82,7 @@ __global__ __launch_bounds__(kBlock) void k_step(Planes P, Params C, const u32* 
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
   if (r < C.n_rep) step_replica<N, TRACE>(P, C, r, round, c);
-  flush_counters(P, c);
+  flush_counters<KS_FULL>(P, c);
 }
 
 // Work lists of a round: 0 = steady-state leaders, 1 = steady-state followers,
@@ -84,22 +106,52 @@ __device__ __forceinline__ void list_push(const Lists& L, u32 list, u32 par, boo
 }
 
 // Pass 1 over every replica: idle rounds complete here; the rest is listed.
+// A block owns kTriChunk consecutive replicas (coalesced Hot loads, 8 per
+// lane), compacts its three work lists in LDS with wave-aggregated LDS
+// atomics, then reserves space in each global list with ONE atomic per list
+// and copies its entries out coalesced.
 template <int N, bool TRACE>
 __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, const u32* round_ptr,
                                                    u32 round_add, Lists L) {
+  __shared__ u32 s_idx[3][kTriChunk];
+  __shared__ u32 s_n[3], s_base[3];
   const u32 round = (round_ptr ? *round_ptr : 0u) + round_add;
   const u32 par = round & 1u;
   if (blockIdx.x == 0 && threadIdx.x < 3) L.counts[threadIdx.x * 2 + (par ^ 1u)] = 0;
-  const u64 r = (u64)blockIdx.x * kBlock + threadIdx.x;
+  if (threadIdx.x < 3) s_n[threadIdx.x] = 0;
+  __syncthreads();
   StepCounters c;
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
-  u32 cls = T_DONE;
-  if (r < C.n_rep) cls = triage_replica<N, TRACE>(P, C, r, round, c);
-  list_push(L, 0, par, cls == T_LEAD, (u32)r);
-  list_push(L, 1, par, cls == T_FOLL, (u32)r);
-  list_push(L, 2, par, cls == T_FULL, (u32)r);
-  flush_counters(P, c);
+  const int lane = threadIdx.x & 63;
+  const u64 lo = (u64)blockIdx.x * kTriChunk;
+  for (u32 j = threadIdx.x; j < kTriChunk; j += kBlock) {
+    const u64 r = lo + j;
+    u32 cls = T_DONE;
+    if (r < C.n_rep) cls = triage_replica<N, TRACE>(P, C, r, round, c);
+#pragma unroll
+    for (u32 li = 0; li < 3; li++) {
+      const bool want = cls == li + 1;
+      const u64 mask = __ballot(want);
+      if (!mask) continue;
+      const int first = __ffsll((unsigned long long)mask) - 1;
+      u32 base = 0;
+      if (lane == first) base = atomicAdd(&s_n[li], (u32)__popcll(mask));
+      base = __shfl(base, first, 64);
+      if (want) s_idx[li][base + __popcll(mask & ((1ull << lane) - 1ull))] = (u32)r;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 3)
+    s_base[threadIdx.x] = s_n[threadIdx.x] ? atomicAdd(&L.counts[threadIdx.x * 2 + par],
+                                                       s_n[threadIdx.x])
+                                           : 0u;
+  __syncthreads();
+#pragma unroll
+  for (u32 li = 0; li < 3; li++)
+    for (u32 j = threadIdx.x; j < s_n[li]; j += kBlock)
+      L.idx[li * L.cap + s_base[li] + j] = s_idx[li][j];
+  flush_counters<KS_TRIAGE>(P, c);
 }
 
 // Pass 2: the steady-state subset for one role over its list (persistent,
@@ -125,7 +177,7 @@ __global__ __launch_bounds__(kBlock) void k_fast_list(Planes P, Params C, const 
     }
     list_push(L, 2, par, slow, r);
   }
-  flush_counters(P, c);
+  flush_counters<MODE == MODE_LEAD ? KS_FAST_LEAD : KS_FAST_FOLL>(P, c);
 }
 
 // Pass 3: the whole handler table over the full list (persistent, grid-stride).
@@ -139,7 +191,7 @@ __global__ __launch_bounds__(kBlock) void k_full_list(Planes P, Params C, const 
   for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
   for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock)
     step_replica<N, TRACE>(P, C, L.idx[2 * L.cap + i], round, c);
-  flush_counters(P, c);
+  flush_counters<KS_FULL>(P, c);
 }
 
 template <int N>
@@ -267,34 +319,68 @@ static int d2h(rbe_engine* e, T* dst, const T* src, u64 n) {
 
 static unsigned grid_for(u64 n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
+// One round's launches.  With `ev` (KS_NUM + 1 events) an event is recorded
+// on the engine stream before the first and after every pipeline kernel, so
+// ev[i]..ev[i+1] brackets kernel section i (rbe_profile_rounds).
 template <int N, bool TRACE>
-static int launch_step_t(rbe_engine* e, const u32* round_ptr, u32 round_add) {
+static int launch_step_t(rbe_engine* e, const u32* round_ptr, u32 round_add,
+                         hipEvent_t* ev = nullptr) {
   const unsigned g = grid_for(e->C.n_rep);
+  auto mark = [&](int i) {
+    if (ev) HIP_IGNORE(hipEventRecord(ev[i], e->stream));
+  };
   if (e->full_mode) {
+    mark(0);
+    mark(1);
+    mark(2);
+    mark(3);
     hipLaunchKernelGGL((k_step<N, TRACE>), dim3(g), dim3(kBlock), 0, e->stream, e->P, e->C,
                        round_ptr, round_add);
+    mark(4);
   } else {
-    hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(g), dim3(kBlock), 0, e->stream, e->P, e->C,
+    const unsigned gt = (unsigned)((e->C.n_rep + kTriChunk - 1) / kTriChunk);
+    mark(0);
+    hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(gt), dim3(kBlock), 0, e->stream, e->P, e->C,
                        round_ptr, round_add, e->L);
+    mark(1);
     const unsigned gf = g < kFastGrid ? g : kFastGrid;
     hipLaunchKernelGGL((k_fast_list<N, TRACE, MODE_LEAD>), dim3(gf), dim3(kBlock), 0, e->stream,
                        e->P, e->C, round_ptr, round_add, e->L);
+    mark(2);
     hipLaunchKernelGGL((k_fast_list<N, TRACE, MODE_FOLL>), dim3(gf), dim3(kBlock), 0, e->stream,
                        e->P, e->C, round_ptr, round_add, e->L);
+    mark(3);
     const unsigned gs = g < kFullGrid ? g : kFullGrid;
     hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kBlock), 0, e->stream, e->P, e->C,
                        round_ptr, round_add, e->L);
+    mark(4);
   }
   HIP_OK(hipGetLastError());
   return RBE_OK;
 }
 
-static int launch_step(rbe_engine* e, const u32* round_ptr, u32 round_add) {
+static int launch_step(rbe_engine* e, const u32* round_ptr, u32 round_add,
+                       hipEvent_t* ev = nullptr) {
   return dispatch_n(e->C.n, [&](auto NN) {
     constexpr int N = decltype(NN)::value;
-    return e->C.trace ? launch_step_t<N, true>(e, round_ptr, round_add)
-                      : launch_step_t<N, false>(e, round_ptr, round_add);
+    return e->C.trace ? launch_step_t<N, true>(e, round_ptr, round_add, ev)
+                      : launch_step_t<N, false>(e, round_ptr, round_add, ev);
   });
+}
+
+// Sum the counter stripes of one kernel section (ks >= 0) or of all (ks < 0).
+static int read_counters(rbe_engine* e, int ks, u64* out) {
+  std::vector<u64> st(kCtrWords);
+  HIP_OK(hipMemcpyAsync(st.data(), e->P.counters, st.size() * sizeof(u64), hipMemcpyDeviceToHost,
+                        e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  for (int i = 0; i < C_NUM; i++) out[i] = 0;
+  for (int k = 0; k < KS_NUM; k++) {
+    if (ks >= 0 && k != ks) continue;
+    for (int j = 0; j < kCtrStripes; j++)
+      for (int i = 0; i < C_NUM; i++) out[i] += st[((size_t)k * kCtrStripes + j) * C_NUM + i];
+  }
+  return RBE_OK;
 }
 
 extern "C" {
@@ -383,12 +469,12 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   P.rtr = (RTR*)ptrs[13];
   P.dri = (DropRI*)ptrs[14];
   P.ext = (ExtIn*)ptrs[15];
-  if (hipMalloc(&P.counters, C_NUM * sizeof(u64)) != hipSuccess) {
+  if (hipMalloc(&P.counters, kCtrWords * sizeof(u64)) != hipSuccess) {
     rbe_destroy(e);
     return RBE_E_NOMEM;
   }
   e->allocs.push_back(P.counters);
-  HIP_IGNORE(hipMemsetAsync(P.counters, 0, C_NUM * sizeof(u64), e->stream));
+  HIP_IGNORE(hipMemsetAsync(P.counters, 0, kCtrWords * sizeof(u64), e->stream));
   if (hipMalloc(&e->d_round, sizeof(u32)) != hipSuccess) {
     rbe_destroy(e);
     return RBE_E_NOMEM;
@@ -424,19 +510,23 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   return RBE_OK;
 }
 
-static int step_one(rbe_engine* e) {
+// fault-schedule epoch rounds: isolate the selected groups' leaders first
+static int launch_iso(rbe_engine* e) {
   const Params& C = e->C;
-  if (C.iso_period && e->round > 0 && e->round % C.iso_period == 0) {
-    int rc = dispatch_n(C.n, [&](auto NN) {
-      constexpr int N = decltype(NN)::value;
-      hipLaunchKernelGGL(k_isolate<N>, dim3(grid_for(C.n_groups)), dim3(kBlock), 0, e->stream,
-                         e->P, e->C, e->round);
-      HIP_OK(hipGetLastError());
-      return RBE_OK;
-    });
-    if (rc) return rc;
-  }
-  int rc = launch_step(e, nullptr, e->round);
+  if (!(C.iso_period && e->round > 0 && e->round % C.iso_period == 0)) return RBE_OK;
+  return dispatch_n(C.n, [&](auto NN) {
+    constexpr int N = decltype(NN)::value;
+    hipLaunchKernelGGL(k_isolate<N>, dim3(grid_for(C.n_groups)), dim3(kBlock), 0, e->stream,
+                       e->P, e->C, e->round);
+    HIP_OK(hipGetLastError());
+    return RBE_OK;
+  });
+}
+
+static int step_one(rbe_engine* e) {
+  int rc = launch_iso(e);
+  if (rc) return rc;
+  rc = launch_step(e, nullptr, e->round);
   if (rc) return rc;
   e->round++;
   return RBE_OK;
@@ -505,6 +595,32 @@ int rbe_run_timed(rbe_engine* e, uint32_t rounds, float* ms) {
   return RBE_OK;
 }
 
+int rbe_profile_rounds(rbe_engine* e, uint32_t rounds, float* ms_per_kernel) {
+  if (!e || !ms_per_kernel || rounds == 0) return RBE_E_INVALID;
+  HIP_OK(hipSetDevice(e->device));
+  hipEvent_t ev[KS_NUM + 1];
+  for (int i = 0; i <= KS_NUM; i++) HIP_OK(hipEventCreate(&ev[i]));
+  for (int i = 0; i < KS_NUM; i++) ms_per_kernel[i] = 0.f;
+  int rc = RBE_OK;
+  for (u32 k = 0; k < rounds && rc == RBE_OK; k++) {
+    rc = launch_iso(e);
+    if (rc) break;
+    rc = launch_step(e, nullptr, e->round, ev);
+    if (rc) break;
+    e->round++;
+    if (hipEventSynchronize(ev[KS_NUM]) != hipSuccess) {
+      rc = RBE_E_HIP;
+      break;
+    }
+    for (int i = 0; i < KS_NUM; i++) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, ev[i], ev[i + 1]) == hipSuccess) ms_per_kernel[i] += ms;
+    }
+  }
+  for (int i = 0; i <= KS_NUM; i++) HIP_IGNORE(hipEventDestroy(ev[i]));
+  return rc;
+}
+
 int rbe_sync(rbe_engine* e) {
   if (!e) return RBE_E_INVALID;
   HIP_OK(hipSetDevice(e->device));
@@ -553,18 +669,22 @@ int rbe_push_read_index(rbe_engine* e, uint64_t n, const uint64_t* replica, cons
   return RBE_OK;
 }
 
+int rbe_get_kernel_counters(rbe_engine* e, int32_t kernel, uint64_t* out) {
+  if (!e || !out || kernel < 0 || kernel >= KS_NUM) return RBE_E_INVALID;
+  HIP_OK(hipSetDevice(e->device));
+  return read_counters(e, kernel, out);
+}
+
 int rbe_get_counters(rbe_engine* e, uint64_t* out) {
   if (!e || !out) return RBE_E_INVALID;
   HIP_OK(hipSetDevice(e->device));
-  HIP_OK(hipMemcpyAsync(out, e->P.counters, C_NUM * sizeof(u64), hipMemcpyDeviceToHost, e->stream));
-  HIP_OK(hipStreamSynchronize(e->stream));
-  return RBE_OK;
+  return read_counters(e, -1, out);
 }
 
 int rbe_reset_counters(rbe_engine* e) {
   if (!e) return RBE_E_INVALID;
   HIP_OK(hipSetDevice(e->device));
-  HIP_OK(hipMemsetAsync(e->P.counters, 0, C_NUM * sizeof(u64), e->stream));
+  HIP_OK(hipMemsetAsync(e->P.counters, 0, kCtrWords * sizeof(u64), e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
   return RBE_OK;
 }

@@ -89,7 +89,8 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_step", "rbe_run"
            "rbe_round", "rbe_run_timed", "rbe_push_proposals", "rbe_push_read_index",
            "rbe_get_updates", "rbe_get_messages", "rbe_get_ready_to_reads", "rbe_get_entries",
            "rbe_get_views", "rbe_get_counters", "rbe_reset_counters", "rbe_fault_summary",
-           "rbe_footprint"]
+           "rbe_footprint", "rbe_profile_rounds", "rbe_get_kernel_counters"]
+KERNEL_NAMES = ["k_triage", "k_fast_list<LEAD>", "k_fast_list<FOLL>", "k_full_list"]
 
 _lib = None
 
@@ -131,6 +132,8 @@ def load_library(path: Optional[str] = None):
         "rbe_reset_counters": (i32, [vp]),
         "rbe_fault_summary": (i32, [vp, P(u64), P(u32)]),
         "rbe_footprint": (i32, [P(RbeConfig), P(u64)]),
+        "rbe_profile_rounds": (i32, [vp, u32, P(C.c_float)]),
+        "rbe_get_kernel_counters": (i32, [vp, C.c_int32, P(u64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -240,6 +243,19 @@ class Engine:
         o = (C.c_uint64 * CTR_NUM)()
         _check(self.lib.rbe_get_counters(self.h, o), "rbe_get_counters")
         return {n: o[i] for i, n in enumerate(COUNTER_NAMES)}
+
+    def kernel_counters(self, kernel: int) -> Dict[str, int]:
+        """Counters contributed by one pipeline kernel (KERNEL_NAMES index)."""
+        o = (C.c_uint64 * CTR_NUM)()
+        _check(self.lib.rbe_get_kernel_counters(self.h, kernel, o), "rbe_get_kernel_counters")
+        return {n: o[i] for i, n in enumerate(COUNTER_NAMES)}
+
+    def profile_rounds(self, rounds: int) -> List[float]:
+        """Run `rounds` rounds with HIP events between the pipeline kernels;
+        returns each kernel's total milliseconds (KERNEL_NAMES order)."""
+        ms = (C.c_float * len(KERNEL_NAMES))()
+        _check(self.lib.rbe_profile_rounds(self.h, rounds, ms), "rbe_profile_rounds")
+        return list(ms)
 
     def reset_counters(self):
         _check(self.lib.rbe_reset_counters(self.h), "rbe_reset_counters")

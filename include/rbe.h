@@ -184,6 +184,19 @@ int rbe_round(const rbe_engine* e, uint32_t* round);
 /* Time `rounds` rounds with HIP events on the engine stream; *ms = elapsed. */
 int rbe_run_timed(rbe_engine* e, uint32_t rounds, float* ms);
 
+/* Round-pipeline kernels, in launch order (rbe_profile_rounds,
+ * rbe_get_kernel_counters). */
+#define RBE_KERNEL_TRIAGE 0    /* k_triage: every replica; idle rounds finish here */
+#define RBE_KERNEL_FAST_LEAD 1 /* k_fast_list<LEAD>: steady-state leaders */
+#define RBE_KERNEL_FAST_FOLL 2 /* k_fast_list<FOLL>: steady-state followers */
+#define RBE_KERNEL_FULL 3      /* k_full_list: the whole handler table (elections, ...) */
+#define RBE_KERNEL_NUM 4
+
+/* Run `rounds` rounds one at a time with HIP events between the pipeline
+ * kernels on the engine stream; ms_per_kernel[RBE_KERNEL_NUM] receives each
+ * kernel's total elapsed time. */
+int rbe_profile_rounds(rbe_engine* e, uint32_t rounds, float* ms_per_kernel);
+
 /* Client input for the next round.  Replaces Peer.ProposeEntries (peer.go:117)
  * and Peer.ReadIndex (peer.go:297); requires cfg.ext_inputs.  replica =
  * g * n_replicas + (node_id - 1). */
@@ -204,6 +217,8 @@ int rbe_get_entries(rbe_engine* e, uint64_t replica, uint64_t lo, uint64_t hi,
                     rbe_entry* out);
 int rbe_get_views(rbe_engine* e, uint64_t first, uint64_t count, rbe_replica_view* out);
 int rbe_get_counters(rbe_engine* e, uint64_t* out /* RBE_CTR_NUM */);
+/* the counters one pipeline kernel (RBE_KERNEL_*) contributed */
+int rbe_get_kernel_counters(rbe_engine* e, int32_t kernel, uint64_t* out /* RBE_CTR_NUM */);
 int rbe_reset_counters(rbe_engine* e);
 /* number of replicas whose sticky fault word is non-zero, and the OR of all */
 int rbe_fault_summary(rbe_engine* e, uint64_t* n_faulty, uint32_t* fault_or);

@@ -128,6 +128,7 @@ def lib():
             "orc_raft_get": (u64, [vp, i32]), "orc_raft_set": (i32, [vp, i32, u64]),
             "orc_raft_call": (C.c_int64, [vp, i32, u64, u64]),
             "orc_raft_remote_get": (i32, [vp, i32, u64, P(u64)]),
+            "orc_remote_op": (C.c_int64, [P(u64), i32, u64, u64]),
             "orc_raft_remote_set": (None, [vp, i32, u64, u64, u64, u64, u64, u64]),
             "orc_raft_remote_del": (None, [vp, i32, u64]),
             "orc_raft_remote_clear": (None, [vp, i32]),
@@ -615,6 +616,31 @@ class Raft:
         s = ss.to_c()
         if lib().orc_raft_log_restore(self.h, C.byref(s)) < 0:
             raise _err()
+
+
+REMOTE_OPS = ["become_retry", "retry_to_wait", "wait_to_retry", "become_wait",
+              "become_replicate", "become_snapshot", "try_update", "progress", "responded_to",
+              "decrease_to", "is_paused", "clear_pending_snapshot", "set_active",
+              "set_not_active", "is_active"]
+
+
+class Remote:
+    """A free-standing `remote` (remote.go:62-69) for the remote_test.go tables."""
+
+    def __init__(self, match=0, next=0, snapshot_index=0, state=REMOTE_RETRY, active=False):
+        self.st = (C.c_uint64 * 5)(match, next, snapshot_index, state, int(active))
+
+    match = property(lambda self: self.st[0])
+    next = property(lambda self: self.st[1])
+    snapshot_index = property(lambda self: self.st[2])
+    state = property(lambda self: self.st[3])
+    active = property(lambda self: bool(self.st[4]))
+
+    def op(self, name, a=0, b=0):
+        v = lib().orc_remote_op(self.st, REMOTE_OPS.index(name), a, b)
+        if v <= -999:
+            raise _err()
+        return v
 
 
 class BlackHole:

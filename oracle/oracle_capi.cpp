@@ -384,6 +384,49 @@ int64_t orc_raft_call(void* rp, int fn, uint64_t a, uint64_t b) {
   GUARD_END(-999)
 }
 
+// A free-standing remote (remote.go:62-69) for the remote_test.go tables.
+// st = {match, next, snapshotIndex, state, active}; returns the op's bool
+// result (0/1), 0 for void ops, -999 when the reference would panic.
+enum { RO_BECOME_RETRY = 0, RO_RETRY_TO_WAIT, RO_WAIT_TO_RETRY, RO_BECOME_WAIT,
+       RO_BECOME_REPLICATE, RO_BECOME_SNAPSHOT, RO_TRY_UPDATE, RO_PROGRESS, RO_RESPONDED_TO,
+       RO_DECREASE_TO, RO_IS_PAUSED, RO_CLEAR_PENDING_SNAPSHOT, RO_SET_ACTIVE,
+       RO_SET_NOT_ACTIVE, RO_IS_ACTIVE };
+int64_t orc_remote_op(uint64_t* st, int op, uint64_t a, uint64_t b) {
+  GUARD_BEGIN
+  Remote x;
+  x.match = st[0];
+  x.next = st[1];
+  x.snapshotIndex = st[2];
+  x.state = (int)st[3];
+  x.active = st[4] != 0;
+  int64_t ret = 0;
+  switch (op) {
+    case RO_BECOME_RETRY: x.becomeRetry(); break;
+    case RO_RETRY_TO_WAIT: x.retryToWait(); break;
+    case RO_WAIT_TO_RETRY: x.waitToRetry(); break;
+    case RO_BECOME_WAIT: x.becomeWait(); break;
+    case RO_BECOME_REPLICATE: x.becomeReplicate(); break;
+    case RO_BECOME_SNAPSHOT: x.becomeSnapshot(a); break;
+    case RO_TRY_UPDATE: ret = x.tryUpdate(a) ? 1 : 0; break;
+    case RO_PROGRESS: x.progress(a); break;
+    case RO_RESPONDED_TO: x.respondedTo(); break;
+    case RO_DECREASE_TO: ret = x.decreaseTo(a, b) ? 1 : 0; break;
+    case RO_IS_PAUSED: ret = x.isPaused() ? 1 : 0; break;
+    case RO_CLEAR_PENDING_SNAPSHOT: x.clearPendingSnapshot(); break;
+    case RO_SET_ACTIVE: x.setActive(); break;
+    case RO_SET_NOT_ACTIVE: x.setNotActive(); break;
+    case RO_IS_ACTIVE: ret = x.isActive() ? 1 : 0; break;
+    default: g_err = "unknown remote op"; return -999;
+  }
+  st[0] = x.match;
+  st[1] = x.next;
+  st[2] = x.snapshotIndex;
+  st[3] = (uint64_t)x.state;
+  st[4] = x.active ? 1 : 0;
+  return ret;
+  GUARD_END(-999)
+}
+
 // remotes: kind 0 remotes, 1 observers, 2 witnesses
 static std::map<u64, Remote>& remote_map(Raft* r, int kind) {
   return kind == 0 ? r->remotes : (kind == 1 ? r->observers : r->witnesses);

@@ -1,0 +1,71 @@
+"""Fold rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into per-kernel HBM bytes
+per launch (profiles/traffic_<workload>.json, read by bench.py).
+
+Per /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE
+are in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide coalesced
+streaming reads, so the corrected read figure is 2 x FETCH_SIZE.  Both the raw
+and the corrected values are recorded.  Only the last LAST dispatches of each
+kernel are used (the bench's per-kernel profiled rounds, in steady state).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+LAST = 10
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def kernel_key(name):
+    if "k_triage" in name:
+        return "k_triage"
+    if "k_fast_list" in name:
+        # template args <N, TRACE, MODE>: MODE 1 = LEAD, 2 = FOLL
+        mode = name.split("k_fast_list<", 1)[1].split(">", 1)[0].split(",")[-1].strip()
+        return "k_fast_list<LEAD>" if mode == "1" else "k_fast_list<FOLL>"
+    if "k_full_list" in name:
+        return "k_full_list"
+    if "k_step" in name:
+        return "k_step"
+    return None
+
+
+def per_kernel(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    vals = defaultdict(list)
+    for f in files:
+        for row in csv.DictReader(open(f)):
+            if row.get("Counter_Name") != counter:
+                continue
+            k = kernel_key(row.get("Kernel_Name", ""))
+            if k:
+                vals[k].append((int(row.get("Dispatch_Id", 0)), float(row["Counter_Value"])))
+    out = {}
+    for k, v in vals.items():
+        v.sort()
+        last = [x for _, x in v[-LAST:]]
+        out[k] = sum(last) / len(last) * 1024.0  # KiB -> bytes
+    return out
+
+
+def main():
+    w, fdir, wdir = sys.argv[1:4]
+    fetch = per_kernel(fdir, "FETCH_SIZE")
+    write = per_kernel(wdir, "WRITE_SIZE")
+    res = {"workload": w, "unit": "bytes per launch", "dispatches_averaged": LAST,
+           "fetch_raw": fetch, "write": write, "bytes_per_launch": {}}
+    for k in set(fetch) | set(write):
+        res["bytes_per_launch"][k] = 2.0 * fetch.get(k, 0.0) + write.get(k, 0.0)
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    out = os.path.join(ROOT, "gpurun_out", f"traffic_{w}.json")
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    for k, v in sorted(res["bytes_per_launch"].items()):
+        print(f"{w} {k:20s} traffic {v / 1e6:9.2f} MB/launch (fetch raw {fetch.get(k, 0) / 1e6:.2f}"
+              f" MB, write {write.get(k, 0) / 1e6:.2f} MB)")
+
+
+if __name__ == "__main__":
+    main()
