@@ -140,13 +140,16 @@ def main():
     dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
 
     from dragonboat_amd.engine import KERNEL_NAMES, Engine, footprint, make_config
+    from dragonboat_amd.shard import reduce_results, shard_params
 
     kw, settle, desc = WORKLOADS[args.workload]
     kw = dict(kw)
     if args.groups:
         kw["n_groups"] = args.groups
-    # group-per-GPU sharding: cid = 1 + rank + g * world  (cid % world == rank)
-    cfg = make_config(device=local, cid_base=1 + rank, cid_stride=ws, trace=False, **kw)
+    # group-per-GPU sharding (dragonboat_amd/shard.py): rank r steps the
+    # clusters with (cid - 1) % world == r, dragonboat's FixedPartitioner rule
+    cid_base, cid_stride = shard_params(rank, ws)
+    cfg = make_config(device=local, cid_base=cid_base, cid_stride=cid_stride, trace=False, **kw)
     eng = Engine(cfg)
 
     def barrier():
@@ -168,19 +171,10 @@ def main():
 
     c = eng.counters()
     nf, fo = eng.fault_summary()
-    local_vals = torch.tensor([wall, float(c["steps"]), float(c["committed"]),
-                               float(c["reads_confirmed"]), float(nf)], dtype=torch.float64)
-    if use_dist:
-        t = local_vals.to(dev) if dist.get_backend() == "nccl" else local_vals
-        wall_t = t[0:1].clone()
-        sums = t[1:].clone()
-        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
-        wall_max = float(wall_t.item())
-        steps, committed, reads, faulty = [float(x) for x in sums.cpu().tolist()]
-    else:
-        wall_max = wall
-        steps, committed, reads, faulty = [float(x) for x in local_vals[1:].tolist()]
+    red_dev = dev if (use_dist and dist.get_backend() == "nccl") else None
+    wall_max, (steps, committed, reads, faulty) = reduce_results(
+        dist if use_dist else None, wall,
+        [c["steps"], c["committed"], c["reads_confirmed"], nf], device=red_dev)
 
     # whole-round algorithmic bandwidth over the timed region (all kernels)
     round_bytes = alg_bytes(c) / args.steps

@@ -129,6 +129,7 @@ def lib():
             "orc_raft_call": (C.c_int64, [vp, i32, u64, u64]),
             "orc_raft_remote_get": (i32, [vp, i32, u64, P(u64)]),
             "orc_remote_op": (C.c_int64, [P(u64), i32, u64, u64]),
+            "orc_raft_handle_direct": (i32, [vp, i32, P(OrcMsg)]),
             "orc_raft_remote_set": (None, [vp, i32, u64, u64, u64, u64, u64, u64]),
             "orc_raft_remote_del": (None, [vp, i32, u64]),
             "orc_raft_remote_clear": (None, [vp, i32]),
@@ -451,6 +452,13 @@ class Raft:
     def handle(self, m: Message):
         cm, keep = m.to_c()
         if lib().orc_raft_handle(self.h, C.byref(cm)) != 0:
+            raise _err()
+
+    def handle_direct(self, which: str, m: Message):
+        """Call one handler without Handle's term gate (as the Go tests do)."""
+        cm, keep = m.to_c()
+        idx = ["replicate", "heartbeat", "request_vote"].index(which)
+        if lib().orc_raft_handle_direct(self.h, idx, C.byref(cm)) != 0:
             raise _err()
 
     def read_messages(self) -> List[Message]:

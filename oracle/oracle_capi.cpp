@@ -220,6 +220,21 @@ int orc_raft_handle(void* r, const orc_msg* m) {
   GUARD_END(-1)
 }
 
+// Direct handler entry for tests that bypass Handle's term gate, as the
+// reference's tests do (e.g. raft_etcd_test.go:1260 sm.handleReplicateMessage).
+int orc_raft_handle_direct(void* r, int which, const orc_msg* m) {
+  GUARD_BEGIN
+  Raft* x = (Raft*)r;
+  Message msg = to_msg(m);
+  switch (which) {
+    case 0: x->handleReplicateMessage(msg); return 0;
+    case 1: x->handleHeartbeatMessage(msg); return 0;
+    case 2: x->handleNodeRequestVote(msg); return 0;
+    default: g_err = "bad handler"; return -1;
+  }
+  GUARD_END(-1)
+}
+
 int orc_raft_num_messages(void* r) { return (int)((Raft*)r)->msgs.size(); }
 int orc_raft_num_message_entries(void* r) {
   int n = 0;

@@ -87,3 +87,15 @@ def test_ext_inputs_path(gpu_available):
     eng.step()
     eng.step()
     assert eng.counters()["reads_confirmed"] == 4
+
+
+@pytest.mark.parametrize("name", ["C1_10k", "C2", "C3", "C3_HOT", "C4", "C4_DENSE", "SINGLE",
+                                  "MIXED"])
+def test_engine_reproduces_trace_fixture(gpu_available, name):
+    """The HIP engine against the committed round-trace fixtures."""
+    from dragonboat_amd.engine import Engine
+    from trace_util import check_against_fixture
+    eng = check_against_fixture(
+        name, lambda kw, extra: Engine(device=0, trace=True, **kw, **extra))
+    assert eng.fault_summary()[0] == 0
+    eng.close()
