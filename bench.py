@@ -223,6 +223,7 @@ def main():
             "committed_entries_per_s": committed / wall_max,
             "read_confirmations_per_s": reads / wall_max,
             "faulty_replicas": int(faulty),
+            "fault_bits_rank0": fo,
             "roofline": {
                 "bound": "hbm",
                 "achieved": dom["achieved_gbs"],
