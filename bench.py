@@ -139,7 +139,7 @@ def main():
         dist.init_process_group(backend=backend)
     dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
 
-    from dragonboat_amd.engine import KERNEL_NAMES, Engine, footprint, make_config
+    from dragonboat_amd.engine import Engine, footprint, make_config
     from dragonboat_amd.shard import reduce_results, shard_params
 
     kw, settle, desc = WORKLOADS[args.workload]
@@ -187,7 +187,9 @@ def main():
     eng.reset_counters()
     kms = eng.profile_rounds(prof_rounds)
     kernels = []
-    for ki, name in enumerate(KERNEL_NAMES):
+    for ki, name in enumerate(eng.kernel_names()):
+        if not name:
+            continue
         kc = eng.kernel_counters(ki)
         b = alg_bytes(kc) / prof_rounds
         us = kms[ki] * 1e3 / prof_rounds

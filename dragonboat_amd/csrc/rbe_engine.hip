@@ -16,7 +16,7 @@
 #include <vector>
 
 #include "../../include/rbe.h"
-#include "rbe_step.h"
+#include "rbe_fast.h"
 
 using namespace rbe;
 
@@ -31,6 +31,11 @@ using namespace rbe;
   } while (0)
 
 static constexpr int kBlock = 256;
+// minimum waves per SIMD requested for the fast-step kernels (caps their VGPRs:
+// 2 -> 256, 3 -> 168, 4 -> 128; beyond the cap the compiler spills to scratch)
+#ifndef RBE_FAST_WAVES
+#define RBE_FAST_WAVES 2
+#endif
 static constexpr u32 kTriChunk = 2048;   // replicas per k_triage block (8 per lane)
 static constexpr int kCtrStripes = 64;   // counter stripes per kernel slot (flush_counters)
 // counter sections, one per pipeline kernel (rbe_get_kernel_counters)
@@ -154,10 +159,68 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, const u32
   flush_counters<KS_TRIAGE>(P, c);
 }
 
+// The fused round (default pipeline): a block triages kTriChunk consecutive
+// replicas exactly like k_triage, but keeps its steady-state leaders (from the
+// front) and followers (from the back) in one LDS list and steps them itself
+// right away; only rounds that need the whole handler table go to the global
+// full list.  One launch replaces triage + two fast-list launches, the work
+// lists never touch HBM, and the latency-bound protocol work of some blocks
+// overlaps the streaming triage of others.
+template <int N, bool TRACE>
+__global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_round(Planes P, Params C, const u32* round_ptr,
+                                                  u32 round_add, Lists L) {
+  __shared__ u32 s_idx[kTriChunk];
+  __shared__ u32 s_nl, s_nf;
+  const u32 round = (round_ptr ? *round_ptr : 0u) + round_add;
+  const u32 par = round & 1u;
+  if (blockIdx.x == 0 && threadIdx.x == 0) L.counts[2 * 2 + (par ^ 1u)] = 0;
+  if (threadIdx.x == 0) s_nl = s_nf = 0;
+  __syncthreads();
+  StepCounters c;
+#pragma unroll
+  for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
+  const int lane = threadIdx.x & 63;
+  const u64 lo = (u64)blockIdx.x * kTriChunk;
+  for (u32 j = threadIdx.x; j < kTriChunk; j += kBlock) {
+    const u64 r = lo + j;
+    u32 cls = T_DONE;
+    if (r < C.n_rep) cls = triage_replica<N, TRACE>(P, C, r, round, c);
+#pragma unroll
+    for (u32 li = 0; li < 2; li++) {
+      const bool want = cls == li + 1;
+      const u64 mask = __ballot(want);
+      if (!mask) continue;
+      const int first = __ffsll((unsigned long long)mask) - 1;
+      u32 base = 0;
+      if (lane == first) base = atomicAdd(li == 0 ? &s_nl : &s_nf, (u32)__popcll(mask));
+      base = __shfl(base, first, 64);
+      const u32 pos = base + __popcll(mask & ((1ull << lane) - 1ull));
+      if (want) s_idx[li == 0 ? pos : kTriChunk - 1u - pos] = (u32)r;
+    }
+    list_push(L, 2, par, cls == T_FULL, (u32)r);
+  }
+  __syncthreads();
+  const u32 nl = s_nl, nt = s_nl + s_nf;
+  for (u32 i0 = 0; i0 < nt; i0 += kBlock) {
+    const u32 i = i0 + threadIdx.x;
+    bool slow = false;
+    u32 r = 0;
+    if (i < nl) {
+      r = s_idx[i];
+      slow = !step_fast<N, TRACE, MODE_LEAD>(P, C, r, round, c);
+    } else if (i < nt) {
+      r = s_idx[kTriChunk - 1u - (i - nl)];
+      slow = !step_fast<N, TRACE, MODE_FOLL>(P, C, r, round, c);
+    }
+    list_push(L, 2, par, slow, r);
+  }
+  flush_counters<KS_TRIAGE>(P, c);
+}
+
 // Pass 2: the steady-state subset for one role over its list (persistent,
 // grid-stride); rounds outside the subset are moved to the full list.
 template <int N, bool TRACE, int MODE>
-__global__ __launch_bounds__(kBlock) void k_fast_list(Planes P, Params C, const u32* round_ptr,
+__global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_list(Planes P, Params C, const u32* round_ptr,
                                                       u32 round_add, Lists L) {
   const u32 round = (round_ptr ? *round_ptr : 0u) + round_add;
   const u32 par = round & 1u;
@@ -173,7 +236,7 @@ __global__ __launch_bounds__(kBlock) void k_fast_list(Planes P, Params C, const 
     u32 r = 0;
     if (i < n) {
       r = L.idx[li * L.cap + i];
-      slow = !step_replica_fast<N, TRACE, MODE>(P, C, r, round, c);
+      slow = !step_fast<N, TRACE, MODE>(P, C, r, round, c);
     }
     list_push(L, 2, par, slow, r);
   }
@@ -221,7 +284,7 @@ struct rbe_engine {
   hipGraphExec_t graph = nullptr;
   u32 graph_rounds = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool full_mode = false;    // RBE_MODE=full: the whole handler table for every replica
+  int mode = 0;              // RBE_MODE: 0 fused (default), 1 split (triage + 2 fast lists), 2 full
   Lists L;                   // per-round work lists (triage → fast → full)
 };
 
@@ -329,7 +392,9 @@ static int launch_step_t(rbe_engine* e, const u32* round_ptr, u32 round_add,
   auto mark = [&](int i) {
     if (ev) HIP_IGNORE(hipEventRecord(ev[i], e->stream));
   };
-  if (e->full_mode) {
+  const unsigned gt = (unsigned)((e->C.n_rep + kTriChunk - 1) / kTriChunk);
+  const unsigned gs = g < kFullGrid ? g : kFullGrid;
+  if (e->mode == 2) {
     mark(0);
     mark(1);
     mark(2);
@@ -337,8 +402,17 @@ static int launch_step_t(rbe_engine* e, const u32* round_ptr, u32 round_add,
     hipLaunchKernelGGL((k_step<N, TRACE>), dim3(g), dim3(kBlock), 0, e->stream, e->P, e->C,
                        round_ptr, round_add);
     mark(4);
+  } else if (e->mode == 0) {
+    mark(0);
+    hipLaunchKernelGGL((k_round<N, TRACE>), dim3(gt), dim3(kBlock), 0, e->stream, e->P, e->C,
+                       round_ptr, round_add, e->L);
+    mark(1);
+    mark(2);
+    mark(3);
+    hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kBlock), 0, e->stream, e->P, e->C,
+                       round_ptr, round_add, e->L);
+    mark(4);
   } else {
-    const unsigned gt = (unsigned)((e->C.n_rep + kTriChunk - 1) / kTriChunk);
     mark(0);
     hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(gt), dim3(kBlock), 0, e->stream, e->P, e->C,
                        round_ptr, round_add, e->L);
@@ -350,7 +424,6 @@ static int launch_step_t(rbe_engine* e, const u32* round_ptr, u32 round_add,
     hipLaunchKernelGGL((k_fast_list<N, TRACE, MODE_FOLL>), dim3(gf), dim3(kBlock), 0, e->stream,
                        e->P, e->C, round_ptr, round_add, e->L);
     mark(3);
-    const unsigned gs = g < kFullGrid ? g : kFullGrid;
     hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kBlock), 0, e->stream, e->P, e->C,
                        round_ptr, round_add, e->L);
     mark(4);
@@ -481,7 +554,7 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   }
   HIP_IGNORE(hipMemsetAsync(e->d_round, 0, sizeof(u32), e->stream));
   const char* mode = getenv("RBE_MODE");
-  e->full_mode = mode && strcmp(mode, "full") == 0;
+  e->mode = !mode ? 0 : (strcmp(mode, "full") == 0 ? 2 : (strcmp(mode, "split") == 0 ? 1 : 0));
   if (C.n_rep >= (1ull << 32)) {
     rbe_destroy(e);
     return RBE_E_INVALID;  // list entries are 32-bit replica indices
@@ -666,6 +739,30 @@ int rbe_push_read_index(rbe_engine* e, uint64_t n, const uint64_t* replica, cons
     HIP_OK(hipMemcpyAsync(&e->P.ext[replica[i]], &x, sizeof(x), hipMemcpyHostToDevice, e->stream));
   }
   HIP_OK(hipStreamSynchronize(e->stream));
+  return RBE_OK;
+}
+
+#ifdef RBE_PHASE_TIMING
+// diagnostic build: read and clear the per-phase stamp sums (rbe_fast.h)
+int rbe_debug_phases(uint64_t* out16) {
+  unsigned long long h[16];
+  HIP_OK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)));
+  for (int i = 0; i < 16; i++) out16[i] = h[i];
+  memset(h, 0, sizeof(h));
+  HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), h, sizeof(h)));
+  return RBE_OK;
+}
+#endif
+
+int rbe_kernel_name(const rbe_engine* e, int32_t kernel, char* buf, uint32_t cap) {
+  if (!e || !buf || cap == 0 || kernel < 0 || kernel >= KS_NUM) return RBE_E_INVALID;
+  static const char* names[3][KS_NUM] = {
+      {"k_round", "", "", "k_full_list"},
+      {"k_triage", "k_fast_list<LEAD>", "k_fast_list<FOLL>", "k_full_list"},
+      {"", "", "", "k_step"}};
+  const char* n = names[e->mode][kernel];
+  strncpy(buf, n, cap - 1);
+  buf[cap - 1] = 0;
   return RBE_OK;
 }
 

@@ -1,0 +1,1289 @@
+// MI355X batched Raft step engine: the steady-state fast paths.
+//
+// k_round (rbe_engine.hip) steps most replica-rounds with these two
+// functions instead of the general Lane (rbe_step.h):
+//   lead_fast<N, TRACE>: a leader whose inbox holds only ReplicateResp /
+//     HeartbeatResp of its own term, with an optional local ReadIndex or
+//     proposal and a tick that is not a check-quorum boundary;
+//   foll_fast<N, TRACE>: a follower whose inbox holds only Replicate /
+//     Heartbeat / ReadIndexResp from its known leader, and whose tick does not
+//     start an election.
+// Both produce bit-for-bit the state, messages, outputs, counters and trace
+// digest that Lane<N, TRACE, MODE_FULL>::run() produces for the same round
+// (tests/test_soa_cpu_parity.py and the -m gpu tests diff them against the
+// oracle every round).  A round outside the subset returns false before
+// anything is written, and the caller queues the replica for k_full_list.
+//
+// The general Lane reads memory on demand inside a long, divergent handler
+// chain; its kernels need ~250 VGPRs and its critical path is dozens of
+// dependent loads.  Here the round is gather → compute → scatter:
+//   1. every independent load is issued up front: Hot, Core, the remote slots,
+//      the Update record, the isolation word and the inbound count words;
+//   2. the inbound message headers (and the leader's readIndex queue head)
+//      are the second level; nothing else waits on memory unless the round
+//      needs an entry older than the cached log tail (rare in steady state);
+//   3. all per-slot state lives in registers (every slot loop is unrolled, so
+//      every array index is a compile-time constant and nothing spills);
+//   4. results are written once at the end.
+#pragma once
+#include "rbe_step.h"
+
+namespace rbe {
+
+// Diagnostic build only (-DRBE_PHASE_TIMING, scripts/phase_timing.sh): per-wave
+// s_memtime stamps between the phases of the fast steps, summed per phase.
+#if defined(RBE_PHASE_TIMING) && (defined(__HIPCC__) || defined(__HIP__))
+__device__ unsigned long long g_phase[2][8];
+#endif
+#if defined(RBE_PHASE_TIMING) && defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ unsigned long long rbe_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define RBE_STAMP(var) const unsigned long long var = rbe_stamp()
+#define RBE_PHASE_ADD(role, i, a, b)                                                   \
+  do {                                                                                 \
+    if ((threadIdx.x & 63) == (u32)(__ffsll((unsigned long long)__ballot(1)) - 1))     \
+      atomicAdd(&g_phase[role][i], (unsigned long long)((b) - (a)));                   \
+  } while (0)
+#else
+#define RBE_STAMP(var)
+#define RBE_PHASE_ADD(role, i, a, b)
+#endif
+
+// Wait until every outstanding load of the lane has returned (a no-op on the
+// host build).  Placed between the gather and the first store of a fast step.
+RBE_HD void rbe_wait_all_loads() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_s_waitcnt(0);
+#endif
+}
+
+// max inbound messages per sender held in registers
+template <int N>
+struct FastCaps {
+  static constexpr u32 MAXM = N <= 3 ? 4 : 5;  // leader: per follower
+  static constexpr u32 FMAXM = 6;              // follower: from its leader
+  static constexpr u32 RQ = 3;                 // readIndex queue entries in registers
+};
+
+// one inbound message, the fields a steady-state handler reads
+struct InMsg {
+  u32 type, reject, n_ent, ent_off;
+  u64 term, log_term, log_index, commit, hint, hint_high;
+};
+
+RBE_HD InMsg load_in(const Msg* p) {
+  const Msg m = *p;
+  InMsg x;
+  x.type = m.type;
+  x.reject = m.reject;
+  x.n_ent = m.n_ent;
+  x.ent_off = m.ent_off;
+  x.term = m.term;
+  x.log_term = m.log_term;
+  x.log_index = m.log_index;
+  x.commit = m.commit;
+  x.hint = m.hint;
+  x.hint_high = m.hint_high;
+  return x;
+}
+
+// the fields a steady-state leader reads from a ReplicateResp / HeartbeatResp
+struct LeadMsg {
+  u32 w;  // type, from, to, reject (raw; decoded where used, outside the load's branch)
+  u64 term, log_index, hint, hint_high;
+};
+RBE_HD LeadMsg load_lead(const Msg* p) {
+  LeadMsg x;
+  x.w = *(const u32*)p;
+  x.term = p->term;
+  x.log_index = p->log_index;
+  x.hint = p->hint;
+  x.hint_high = p->hint_high;
+  return x;
+}
+
+// Output side shared by both roles: message emission (raft.send +
+// finalizeMessageTerm, raft.go:640-658, then the network list), ReadyToRead,
+// counters, the running trace hashes.  Mirrors Lane::send exactly.
+template <int N, bool TRACE>
+struct FastOut {
+  u64 r, g;
+  u32 k, par, self, round_;
+  u8 iso;
+  u64 pc;  // per destination 16 bits: A | B << 7 | quiesce << 15 (N <= 4 fits; N = 5 uses pc_hi)
+  u64 pc_hi;
+  u32 fault, n_msgs, n_rtr, n_drop_ri;
+  u64 msg_hash, rtr_hash, drop_hash;
+  u64 term;
+
+  RBE_HD u32 get_pc(u32 d) const {
+    return d < 4 ? (u32)((pc >> (16 * d)) & 0xFFFFu) : (u32)((pc_hi >> (16 * (d - 4))) & 0xFFFFu);
+  }
+  RBE_HD void add_pc(u32 d, u32 v) {
+    if (d < 4) pc += (u64)v << (16 * d);
+    else pc_hi += (u64)v << (16 * (d - 4));
+  }
+  RBE_HD void set_fault(StepCounters& ctr, u32 f) {
+    if (!(fault & f)) ctr.v[C_FAULTS]++;
+    fault |= f;
+  }
+  // `ent` points at the message's entries in this round's arena (may be null
+  // when n_ent == 0).
+  RBE_HD void send(const Planes& P, const Params& C, StepCounters& ctr, Msg& m, const Ent* ent) {
+    m.from = (u8)self;
+    if (m.type != M_RequestVote) {
+      if (m.type == M_Propose || m.type == M_ReadIndex) m.term = 0;
+      else m.term = term;
+    }
+    n_msgs++;
+    if (TRACE) {
+      u64 h = msg_hash;
+      h = hfold(h, (u64)m.type | ((u64)m.reject << 8) | ((u64)m.n_ent << 16));
+      h = hfold(h, m.to);
+      h = hfold(h, m.from);
+      h = hfold(h, m.term);
+      h = hfold(h, m.log_term);
+      h = hfold(h, m.log_index);
+      h = hfold(h, m.commit);
+      h = hfold(h, m.hint);
+      h = hfold(h, m.hint_high);
+      for (u32 i = 0; i < m.n_ent; i++) {
+        const Ent e = ent[i];
+        h = hfold(h, m.type == M_Replicate ? m.log_index + 1 + i : 0);
+        h = hfold(h, e.term);
+        h = hfold(h, (u64)e.type | ((u64)e.len << 32));
+        h = hfold(h, e.lo);
+        h = hfold(h, e.hi);
+      }
+      msg_hash = h;
+    }
+    if (m.to < 1 || m.to > N) return;
+    const u32 d = m.to - 1u;
+    if (((iso >> k) & 1u) || ((iso >> d) & 1u)) {
+      ctr.v[C_MSG_DROPPED]++;
+      return;
+    }
+    const u32 c = get_pc(d);
+    const u32 a = c & 0x7Fu, b = (c >> 7) & 0x7Fu;
+    if (a + b >= C.maxm) {
+      set_fault(ctr, F_OUTBOX);
+      return;
+    }
+    u32 slot;
+    if (m.type == M_Replicate) {
+      slot = a;
+      add_pc(d, 1u);
+    } else {
+      slot = C.maxm - 1u - b;
+      add_pc(d, 1u << 7);
+    }
+    P.msgs[par][((g * N + k) * N + d) * (u64)C.maxm + slot] = m;
+    ctr.v[C_MSG_OUT]++;
+    ctr.v[C_ENT_OUT] += m.n_ent;
+  }
+  RBE_HD void dropped_read_index(const Planes& P, const Params& C, StepCounters& ctr, u64 low,
+                                 u64 high) {  // raft.go:1999-2012
+    if (n_drop_ri >= C.dri_cap) {
+      set_fault(ctr, F_DROPLIST);
+      return;
+    }
+    DropRI x;
+    x.low = low;
+    x.high = high;
+    P.dri[r * C.dri_cap + n_drop_ri] = x;
+    n_drop_ri++;
+    if (TRACE) {
+      drop_hash = hfold(drop_hash, low);
+      drop_hash = hfold(drop_hash, high);
+    }
+  }
+  RBE_HD void ready_to_read(const Planes& P, const Params& C, StepCounters& ctr, u64 index,
+                            u64 low, u64 high) {  // raft.go:1624-1630
+    if (n_rtr >= C.rtr_cap) {
+      set_fault(ctr, F_RTR);
+      return;
+    }
+    RTR x;
+    x.index = index;
+    x.low = low;
+    x.high = high;
+    P.rtr[r * C.rtr_cap + n_rtr] = x;
+    n_rtr++;
+    if (TRACE) {
+      rtr_hash = hfold(rtr_hash, index);
+      rtr_hash = hfold(rtr_hash, low);
+      rtr_hash = hfold(rtr_hash, high);
+    }
+  }
+};
+
+RBE_HD Msg mk_msg(u32 type, u32 to) {
+  Msg m;
+  m.type = (u8)type;
+  m.from = 0;
+  m.to = (u8)to;
+  m.reject = 0;
+  m.n_ent = 0;
+  m.pad0 = 0;
+  m.ent_off = 0;
+  m.pad1 = 0;
+  m.term = m.log_term = m.log_index = m.commit = m.hint = m.hint_high = 0;
+  return m;
+}
+
+// quiesceManager on registers (quiesce.go; Lane::q_*)
+struct FastQ {
+  u32 tick, qs, nas, eqt;
+  bool qnew;
+  RBE_HD bool quiesced(const Params& C) const { return C.quiesce && qs > 0; }
+  RBE_HD bool new_to_quiesce(const Params& C) const {
+    return quiesced(C) && tick - qs < C.election_rtt * 2;
+  }
+  RBE_HD bool just_exited(const Params& C) const {
+    return !quiesced(C) && tick - eqt < C.election_rtt * 20;
+  }
+  RBE_HD void enter() {
+    qs = tick;
+    nas = tick;
+    qnew = true;
+  }
+  RBE_HD void increase_tick(const Params& C) {  // quiesce.go:43-55
+    if (!C.quiesce) return;
+    tick++;
+    if (!quiesced(C) && tick - nas > C.election_rtt * 20) enter();
+  }
+  RBE_HD void record_activity(const Params& C, u32 t) {  // quiesce.go:64-82
+    if (!C.quiesce) return;
+    if (t == M_Heartbeat || t == M_HeartbeatResp) {
+      if (!quiesced(C)) return;
+      if (new_to_quiesce(C)) return;
+    }
+    nas = tick;
+    if (quiesced(C)) {
+      qs = 0;
+      eqt = tick;
+    }
+  }
+  RBE_HD void try_enter(const Params& C) {  // quiesce.go:102-110
+    if (just_exited(C)) return;
+    if (!quiesced(C)) enter();
+  }
+};
+
+// Common epilogue: stepNode's quiesce send, getUpdate/Commit, the trace digest,
+// the Update record, this round's outbox counts, Hot/Core write-back.
+// Mirrors the tail of Lane::run().
+template <int N, bool TRACE>
+RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, FastOut<N, TRACE>& o,
+                        FastQ& q, u8 role, u8 flags, Hot h, Core c, u32 etick, u32 htick,
+                        u64 committed0, u64 digest0) {
+  const u64 r = o.r;
+  // stepNode: sendEnterQuiesceMessages (node.go:873-886)
+  const bool send_q = q.qnew;
+  if (send_q) {
+#pragma unroll
+    for (u32 d = 0; d < N; d++) {
+      if (d == o.k) continue;
+      if (((o.iso >> o.k) & 1u) || ((o.iso >> d) & 1u)) {
+        ctr.v[C_MSG_DROPPED]++;
+        continue;
+      }
+      o.add_pc(d, 0x8000u);
+      ctr.v[C_MSG_OUT]++;
+    }
+  }
+  Upd u;
+  u.save_lo = c.saved_to + 1;
+  u.save_hi = c.last_index;
+  u.apply_lo = c.processed + 1;
+  u.apply_hi = c.committed;
+  if (c.committed > c.processed) {
+    // limitSize (entryutils.go:52-64) with sizes 128 + len
+    const u64 lo = c.processed + 1, hi = c.committed;
+    u64 n = hi - lo + 1;
+    if (n * (128 + 16) > C.max_entry_size) {
+      u64 total = 128 + P.pay_ring[(lo & (u64)(C.ring - 1)) * C.n_rep + r].len;
+      u64 inc = 1;
+      for (; inc < n; inc++) {
+        total += 128 + P.pay_ring[((lo + inc) & (u64)(C.ring - 1)) * C.n_rep + r].len;
+        if (total > C.max_entry_size) break;
+      }
+      n = inc;
+    }
+    u.apply_hi = c.processed + n;
+  }
+  u64 apply_hash = 0;
+  if (TRACE && u.apply_hi >= u.apply_lo) {
+    for (u64 i = u.apply_lo; i <= u.apply_hi; i++) {
+      if (c.last_index - i >= C.ring) {
+        o.set_fault(ctr, F_WINDOW);
+        break;
+      }
+      const u64 s = (i & (u64)(C.ring - 1)) * C.n_rep + r;
+      const Body b = P.pay_ring[s];
+      apply_hash = hfold(apply_hash, i);
+      apply_hash = hfold(apply_hash, P.term_ring[s]);
+      apply_hash = hfold(apply_hash, (u64)b.type | ((u64)b.len << 32));
+      apply_hash = hfold(apply_hash, b.lo);
+      apply_hash = hfold(apply_hash, b.hi);
+    }
+  }
+  if (u.apply_hi >= u.apply_lo) ctr.v[C_ENT_APPLIED] += (u32)(u.apply_hi - u.apply_lo + 1);
+  if (u.save_hi >= u.save_lo) ctr.v[C_ENT_SAVED] += (u32)(u.save_hi - u.save_lo + 1);
+  if (o.n_rtr) ctr.v[C_READS_CONFIRMED] += o.n_rtr;
+  ctr.v[C_DROPPED_READS] += o.n_drop_ri;
+  if (u.apply_hi >= u.apply_lo) c.processed = u.apply_hi;
+  c.saved_to = c.last_index;
+  if (c.processed < c.committed) flags |= HF_APPLY_PENDING;
+  else flags &= (u8)~HF_APPLY_PENDING;
+  if (role == R_Leader) {
+    ctr.v[C_COMMITTED] += (u32)(c.committed - committed0);
+    ctr.v[C_LEADER_STEPS]++;
+  }
+  u64 d = digest0;
+  if (TRACE) {
+    d = hfold(d, o.round_);
+    d = hfold(d, (u64)role | ((u64)(q.quiesced(C) ? 1 : 0) << 8) | ((u64)(send_q ? 1 : 0) << 9) |
+                     ((u64)((flags & HF_RAFT_QUIESCE) ? 1 : 0) << 10));
+    d = hfold(d, c.term);
+    d = hfold(d, c.vote);
+    d = hfold(d, c.leader);
+    d = hfold(d, c.committed);
+    d = hfold(d, c.last_index);
+    d = hfold(d, c.processed);
+    d = hfold(d, (u64)etick | ((u64)htick << 32));
+    d = hfold(d, h.rand_et);
+    d = hfold(d, o.msg_hash);
+    d = hfold(d, o.n_msgs);
+    d = hfold(d, o.rtr_hash);
+    d = hfold(d, apply_hash);
+    d = hfold(d, o.drop_hash);  // dropped ReadIndexes (no dropped proposals here)
+  }
+  u.digest = d;
+  u.n_msgs = (u16)o.n_msgs;
+  u.n_rtr = (u16)o.n_rtr;
+  u.n_drop_ent = 0;
+  u.n_drop_ri = (u16)o.n_drop_ri;
+  u.fault = o.fault;
+  u.flags = (u16)((c.committed != committed0 ? UF_STATE_CHANGED : 0u) |
+                  (send_q ? UF_SENT_QUIESCE : 0u));
+  u.pad = 0;
+  u.round = o.round_;
+  u.pad2 = 0;
+  P.upd[r] = u;
+  u16* cnt = &P.cnt[o.par][o.g * N * N + o.k * N];
+#pragma unroll
+  for (u32 dd = 0; dd < N; dd++) cnt[dd] = (u16)o.get_pc(dd);
+  h.flags = flags;
+  h.election_tick = etick;
+  h.heartbeat_tick = (u16)htick;
+  h.q_tick = q.tick;
+  h.q_quiesced_since = q.qs;
+  h.q_no_activity_since = q.nas;
+  h.q_exit_quiesce_tick = q.eqt;
+  P.hot[r] = h;
+  P.core[r] = c;
+}
+
+// ---------------------------------------------------------------- leader
+// One steady-state leader round (see the file comment for the subset).
+// Mirrors Lane<N, TRACE, MODE_FULL>::run() event by event:
+//   inbox (ascending sender; Quiesce marker, then the sender's messages) →
+//   local ReadIndex → tick → proposal, each followed by the deferred fan-out
+//   (Replicate sends in ascending slot order, heartbeats, readIndex confirm).
+template <int N, bool TRACE>
+RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCounters& ctr) {
+  using Cap = FastCaps<N>;
+  constexpr u32 Q = N / 2 + 1;
+  if constexpr (N < 3) {
+    return false;
+  } else {
+  const u64 g = r / N;
+  const u32 k = (u32)(r % N);
+  const u32 par = round & 1u, ppar = par ^ 1u;
+  const u64 cid = C.cid_base + g * C.cid_stride;
+  // ---- gather, level 1: independent loads
+  RBE_STAMP(t0);
+  Hot h = P.hot[r];
+  Core c = P.core[r];
+  u64 match[N], next[N];
+  u32 st[N];
+#pragma unroll
+  for (u32 s = 0; s < N; s++) {
+    const RemoteMN x = P.rem[r * N + s];
+    match[s] = x.match;
+    next[s] = x.next;
+    st[s] = P.rem_st[r * N + s];
+  }
+  u32 pcin[N];
+#pragma unroll
+  for (u32 s = 0; s < N; s++)
+    pcin[s] = (round > 0 && s != k) ? (u32)P.cnt[ppar][g * N * N + s * N + k] : 0u;
+  const u32 until = P.iso_until[g];
+  const u8 isom = P.iso_mask[g];
+  const u64 digest0 = P.upd[r].digest;
+  const u32 fault0 = P.upd[r].fault;
+  // ---- eligibility on level-1 data
+  if (h.role != R_Leader) return false;
+  if (h.flags & (HF_APPLY_PENDING | HF_IS_LTT)) return false;
+  if (c.ltt != 0) return false;
+  if (C.ext_inputs && P.ext[r].kind) return false;
+  if (c.rq_count >= Cap::RQ) return false;
+  u32 n_in = 0;
+#pragma unroll
+  for (u32 s = 0; s < N; s++) {
+    if (s == k) continue;
+    const u32 na = pcin[s] & 0x7Fu, nb = (pcin[s] >> 7) & 0x7Fu;
+    if (na != 0 || nb > Cap::MAXM) return false;
+    n_in += nb;
+  }
+  const u32 inp = wl_input(C, cid, round);
+  // ---- gather, level 2: inbound message headers, readIndex queue
+  RBE_STAMP(t1);
+  // Loads only inside the branches; every use comes after the join, so no
+  // branch waits for its own loads (a wait inside each conditional block
+  // would serialise the message loads).
+  LeadMsg in[N][Cap::MAXM];
+  u32 nbs[N];
+#pragma unroll
+  for (u32 s = 0; s < N; s++) {
+    nbs[s] = s == k ? 0u : ((pcin[s] >> 7) & 0x7Fu);
+    const Msg* lst = &P.msgs[ppar][((g * N + s) * N + k) * (u64)C.maxm];
+#pragma unroll
+    for (u32 i = 0; i < Cap::MAXM; i++) {
+      in[s][i].w = 0xFFu;
+      in[s][i].term = in[s][i].log_index = in[s][i].hint = in[s][i].hint_high = 0;
+      if (i < nbs[s]) in[s][i] = load_lead(&lst[C.maxm - 1u - i]);
+    }
+  }
+  u64 rq_lo[Cap::RQ], rq_hi[Cap::RQ], rq_ix[Cap::RQ];
+  u32 rq_fr[Cap::RQ], rq_cf[Cap::RQ];
+  u32 rq_n = c.rq_count, rq_h = c.rq_head;
+  auto rq_slot = [&](u32 i) -> u64 {
+    u32 x = rq_h + i;
+    if (x >= C.rq_cap) x -= C.rq_cap;
+    return r * C.rq_cap + x;
+  };
+  u32 rq_w[Cap::RQ];  // from | confirmed << 8 (raw bytes 24..27 of the record)
+#pragma unroll
+  for (u32 i = 0; i < Cap::RQ; i++) {
+    rq_lo[i] = rq_hi[i] = rq_ix[i] = 0;
+    rq_w[i] = 0;
+    if (i < rq_n) {
+      const ReadReq* qp = &P.rq[rq_slot(i)];
+      rq_lo[i] = qp->low;
+      rq_hi[i] = qp->high;
+      rq_ix[i] = qp->index;
+      rq_w[i] = *(const u32*)&qp->from;
+    }
+  }
+#pragma unroll
+  for (u32 i = 0; i < Cap::RQ; i++) {
+    rq_fr[i] = rq_w[i] & 0xFFu;
+    rq_cf[i] = (rq_w[i] >> 8) & 0xFFu;
+  }
+  bool rq_dirty = false;
+#pragma unroll
+  for (u32 s = 0; s < N; s++) {
+    if (s == k) continue;
+#pragma unroll
+    for (u32 i = 0; i < Cap::MAXM; i++) {
+      if (i >= nbs[s]) continue;
+      const u32 t = in[s][i].w & 0xFFu;
+      if (t != M_ReplicateResp && t != M_HeartbeatResp) return false;
+      if (in[s][i].term != c.term) return false;
+      if (t == M_ReplicateResp && (in[s][i].w >> 24)) return false;  // rejection: decreaseTo
+    }
+    // every entry a Replicate of this round can carry is the one proposed
+    // this round (so no ring read is needed after the first store)
+    if (next[s] <= c.last_index) return false;
+  }
+  FastQ q;
+  q.tick = h.q_tick;
+  q.qs = h.q_quiesced_since;
+  q.nas = h.q_no_activity_since;
+  q.eqt = h.q_exit_quiesce_tick;
+  q.qnew = false;
+  {
+    const bool idle = n_in == 0 && inp == 0;
+    const bool q_at_tick = idle && C.quiesce &&
+                           (q.qs > 0 || (q.tick + 1u - q.nas > C.election_rtt * 20));
+    if (C.check_quorum && !q_at_tick && h.election_tick + 1u >= C.election_rtt) return false;
+  }
+  // ---- compute.  Every load above has completed before the first store
+  // below: vmcnt counts loads and stores in order, so a wait for a load still
+  // in flight after a store (the compiler is conservative inside the rolled
+  // message loop) would also wait for that store's acknowledgement.
+  asm volatile("" ::: "memory");
+  rbe_wait_all_loads();
+  RBE_STAMP(t2);
+  FastOut<N, TRACE> o;
+  o.r = r;
+  o.g = g;
+  o.k = k;
+  o.par = par;
+  o.self = k + 1;
+  o.round_ = round;
+  o.iso = round < until ? isom : (u8)0;
+  o.pc = o.pc_hi = 0;
+  o.fault = fault0;
+  o.n_msgs = o.n_rtr = o.n_drop_ri = 0;
+  o.msg_hash = o.rtr_hash = o.drop_hash = 0;
+  o.term = c.term;
+  u8 flags = h.flags;
+  u32 etick = h.election_tick, htick = h.heartbeat_tick;
+  const u64 committed0 = c.committed;
+  const u64 last0 = c.last_index;
+  ctr.v[C_STEPS]++;
+  // arena of this round (Lane::arena_put / arena_log_range)
+  Ent* arena = &P.arena[par][r * C.ecap];
+  u32 arena_used = 0, seg_off = 0, seg_len = 0;
+  u64 seg_lo = 0;
+  // the entry proposed this round (index prop_idx), still in registers
+  u64 prop_idx = 0, prop_lo = 0, prop_hi = 0;
+
+  // entryLog.term (logentry.go:142-161) without touching memory: a leader's
+  // entries [lead_start, last] are of its term and earlier ones of a lower
+  // term.  Every lookup here is either compared with the current term
+  // (tryCommit, hasCommittedEntryAtCurrentTerm) or, by the eligibility rule
+  // next[s] > last0, at an index >= lead_start (makeReplicateMessage), so
+  // "lower" (0) is exact for every use.  The ring read the general Lane
+  // performs is still counted and window-checked.
+  auto log_term = [&](u64 idx) -> u64 {
+    if (idx > c.last_index || idx == 0) return 0;
+    if (idx == c.last_index) return c.t_last;
+    if (c.last_index - idx >= C.ring) {
+      o.set_fault(ctr, F_WINDOW);
+      return 0;
+    }
+    ctr.v[C_RING_ACCESS]++;
+    return idx >= c.lead_start ? c.term : 0;
+  };
+  auto ent_at = [&](u64 idx) -> Ent {  // ring entry idx (registers when just proposed)
+    Ent e;
+    if (idx == prop_idx && prop_idx != 0) {
+      e.term = c.term;
+      e.type = E_Application;
+      e.len = 16;
+      e.lo = prop_lo;
+      e.hi = prop_hi;
+    } else {  // excluded by the eligibility rule next[s] > last0
+      o.set_fault(ctr, F_UNSUPPORTED);
+      e.term = 0;
+      e.type = E_Application;
+      e.len = 0;
+      e.lo = e.hi = 0;
+    }
+    return e;
+  };
+  auto limit_count = [&](u64 lo, u64 hi) -> u64 {  // limitSize, entryutils.go:52-64
+    const u64 n = hi - lo + 1;
+    if (n * (128 + 16) <= C.max_entry_size) return n;
+    u64 total = 128 + ent_at(lo).len;
+    u64 inc = 1;
+    for (; inc < n; inc++) {
+      total += 128 + ent_at(lo + inc).len;
+      if (total > C.max_entry_size) break;
+    }
+    return inc;
+  };
+  auto arena_log_range = [&](u64 lo, u32 cnt, u32* off) -> bool {  // Lane::arena_log_range
+    if (seg_len && lo >= seg_lo && lo + cnt <= seg_lo + seg_len) {
+      *off = seg_off + (u32)(lo - seg_lo);
+      return true;
+    }
+    if (seg_len && lo >= seg_lo && lo <= seg_lo + seg_len && seg_off + seg_len == arena_used) {
+      const u64 have_hi = seg_lo + seg_len;
+      const u32 extra = (u32)(lo + cnt - have_hi);
+      if (arena_used + extra > C.ecap) {
+        o.set_fault(ctr, F_ARENA);
+        return false;
+      }
+      for (u32 i = 0; i < extra; i++) {
+        const u64 idx = have_hi + i;
+        if (c.last_index - idx >= C.ring) o.set_fault(ctr, F_WINDOW);
+        arena[arena_used + i] = ent_at(idx);
+      }
+      ctr.v[C_RING_ACCESS] += extra;
+      arena_used += extra;
+      seg_len += extra;
+      *off = seg_off + (u32)(lo - seg_lo);
+      return true;
+    }
+    if (arena_used + cnt > C.ecap) {
+      o.set_fault(ctr, F_ARENA);
+      return false;
+    }
+    for (u32 i = 0; i < cnt; i++) {
+      const u64 idx = lo + i;
+      if (c.last_index - idx >= C.ring) o.set_fault(ctr, F_WINDOW);
+      arena[arena_used + i] = ent_at(idx);
+    }
+    ctr.v[C_RING_ACCESS] += cnt;
+    seg_lo = lo;
+    seg_off = arena_used;
+    seg_len = cnt;
+    *off = arena_used;
+    arena_used += cnt;
+    return true;
+  };
+  auto try_update = [&](u64& mt, u64& nx, u32& sw, u64 idx) -> bool {  // remote.go:123-133
+    ctr.v[C_REMOTE_TOUCH]++;
+    if (nx < idx + 1) nx = idx + 1;
+    if (mt < idx) {
+      if ((sw & 3u) == RS_Wait) sw = (sw & ~3u) | RS_Retry;
+      mt = idx;
+      return true;
+    }
+    return false;
+  };
+  auto try_commit = [&]() -> bool {  // raft.go:886-907 + logentry.go:379-394
+    u64 m[N];
+#pragma unroll
+    for (u32 s = 0; s < N; s++) m[s] = match[s];
+#pragma unroll
+    for (u32 pass = 0; pass < N; pass++) {
+#pragma unroll
+      for (u32 i = pass & 1u; i + 1 < N; i += 2) {
+        const u64 a = m[i], b = m[i + 1];
+        m[i] = a < b ? a : b;
+        m[i + 1] = a < b ? b : a;
+      }
+    }
+    ctr.v[C_REMOTE_TOUCH] += N;
+    const u64 qv = m[N - Q];
+    if (qv <= c.committed) return false;
+    if (log_term(qv) != c.term) return false;
+    if (qv > c.last_index) {  // commitTo panics (logentry.go:324-333)
+      o.set_fault(ctr, F_PANIC);
+      return true;
+    }
+    c.committed = qv;
+    return true;
+  };
+  // deferred fan-out state (Lane::rep_mask / hb_pending / rq_pending)
+  u32 rep_mask = 0;
+  bool hb_pending = false, rq_pending = false;
+  u64 hb_lo = 0, hb_hi = 0, rq_plo = 0, rq_phi = 0;
+  u32 rq_from = 0;
+  auto send_replicate = [&](u32 s) {  // raft.go:758-792
+    const u32 rs = st[s] & 3u;
+    if (rs == RS_Wait || rs == RS_Snapshot) return;
+    const u64 nx = next[s];
+    Msg m = mk_msg(M_Replicate, s + 1);
+    m.log_index = nx - 1;
+    m.log_term = log_term(nx - 1);
+    m.commit = c.committed;
+    if (nx <= c.last_index) {
+      const u64 cnt = limit_count(nx, c.last_index);
+      u32 off = 0;
+      if (arena_log_range(nx, (u32)cnt, &off)) {
+        m.n_ent = (u16)cnt;
+        m.ent_off = off;
+      }
+      // progress (remote.go:135-143)
+      if (rs == RS_Replicate) next[s] = nx + cnt;
+      else if (rs == RS_Retry) st[s] = (st[s] & ~3u) | RS_Wait;
+      else o.set_fault(ctr, F_PANIC);
+    }
+    o.send(P, C, ctr, m, arena + m.ent_off);
+  };
+  auto rq_confirm = [&](u64 low, u64 high, u32 from) {  // readindex.go:77-116
+    int pos = -1;
+#pragma unroll
+    for (u32 i = 0; i < Cap::RQ; i++)
+      if (pos < 0 && i < rq_n && rq_lo[i] == low && rq_hi[i] == high) pos = (int)i;
+    if (pos < 0) return;
+    u64 sindex = 0;
+    u32 conf = 0;
+#pragma unroll
+    for (u32 i = 0; i < Cap::RQ; i++)
+      if ((int)i == pos) {
+        rq_cf[i] |= 1u << (from - 1u);
+        conf = rq_cf[i];
+        sindex = rq_ix[i];
+      }
+    rq_dirty = true;
+    ctr.v[C_RQ_TOUCH]++;
+    if ((int)popc8(conf) + 1 < (int)Q) return;
+    const u32 done = (u32)pos + 1;
+#pragma unroll
+    for (u32 i = 0; i < Cap::RQ; i++) {
+      if (i >= done) continue;
+      if (rq_ix[i] > sindex) o.set_fault(ctr, F_PANIC);
+      if (rq_fr[i] == 0 || rq_fr[i] == o.self) {
+        o.ready_to_read(P, C, ctr, sindex, rq_lo[i], rq_hi[i]);
+      } else {
+        Msg m = mk_msg(M_ReadIndexResp, rq_fr[i]);
+        m.log_index = sindex;
+        m.hint = low;
+        m.hint_high = high;
+        o.send(P, C, ctr, m, nullptr);
+      }
+    }
+    ctr.v[C_RQ_TOUCH] += done;
+    // pop `done` entries: shift the register queue down
+#pragma unroll
+    for (u32 i = 0; i < Cap::RQ; i++) {
+      u64 a = 0, b = 0, x = 0;
+      u32 f = 0, cf = 0;
+#pragma unroll
+      for (u32 j = 0; j < Cap::RQ; j++)
+        if (j == i + done) {
+          a = rq_lo[j];
+          b = rq_hi[j];
+          x = rq_ix[j];
+          f = rq_fr[j];
+          cf = rq_cf[j];
+        }
+      rq_lo[i] = a;
+      rq_hi[i] = b;
+      rq_ix[i] = x;
+      rq_fr[i] = f;
+      rq_cf[i] = cf;
+    }
+    rq_h += done;
+    if (rq_h >= C.rq_cap) rq_h -= C.rq_cap;
+    rq_n -= done;
+  };
+  auto fan_out = [&]() {
+#pragma unroll
+    for (u32 s = 0; s < N; s++)
+      if (rep_mask & (1u << s)) send_replicate(s);
+    rep_mask = 0;
+    if (hb_pending) {
+      hb_pending = false;
+#pragma unroll
+      for (u32 s = 0; s < N; s++) {
+        if (s == k) continue;
+        Msg m = mk_msg(M_Heartbeat, s + 1);  // raft.go:810-820
+        m.commit = umin64(match[s], c.committed);
+        m.hint = hb_lo;
+        m.hint_high = hb_hi;
+        o.send(P, C, ctr, m, nullptr);
+      }
+      ctr.v[C_REMOTE_TOUCH] += N - 1;
+    }
+    if (rq_pending) {
+      rq_pending = false;
+      rq_confirm(rq_plo, rq_phi, rq_from);
+    }
+  };
+
+  // handleReadIndexRequests (node.go:1108-1118)
+  if (inp == 2) {
+    q.record_activity(C, M_ReadIndex);
+    ctr.v[C_READS]++;
+  }
+  // handleReceivedMessages: senders in ascending order
+#pragma unroll
+  for (u32 s = 0; s < N; s++) {
+    if (s == k) continue;
+    if (pcin[s] & 0x8000u) {  // Quiesce first in the sender's stream
+      ctr.v[C_MSG_IN]++;
+      q.try_enter(C);
+    }
+    // a rolled loop (the handler + fan-out body is too large to replicate
+    // per message) reading the prefetched headers through a select chain,
+    // so the register array is never indexed dynamically
+    const u32 nb = (pcin[s] >> 7) & 0x7Fu;
+#pragma unroll 1
+    for (u32 i = 0; i < nb; i++) {
+      LeadMsg m = in[s][0];
+#pragma unroll
+      for (u32 j = 1; j < Cap::MAXM; j++)
+        if (i == j) m = in[s][j];
+      ctr.v[C_MSG_IN]++;
+      const u32 mtype = m.w & 0xFFu;
+      if (mtype == M_HeartbeatResp && m.hint > 0) q.record_activity(C, M_ReadIndex);
+      else q.record_activity(C, mtype);
+      st[s] |= 4u;  // setActive
+      if (mtype == M_ReplicateResp) {  // raft.go:1667-1696
+        if (!(m.w >> 24)) {
+          const u32 rs = st[s] & 3u;
+          const bool paused = rs == RS_Wait || rs == RS_Snapshot;
+          if (try_update(match[s], next[s], st[s], m.log_index)) {
+            // respondedTo (remote.go:145-153); snapshotIndex is 0 on device
+            const u32 rs2 = st[s] & 3u;
+            if (rs2 == RS_Retry) {
+              next[s] = match[s] + 1;
+              st[s] = (st[s] & ~3u) | RS_Replicate;
+            } else if (rs2 == RS_Snapshot) {
+              next[s] = match[s] + 1;
+              st[s] = (st[s] & ~3u) | RS_Retry;
+            }
+            if (try_commit()) rep_mask |= ((1u << N) - 1u) & ~(1u << k);
+            else if (paused) rep_mask |= 1u << s;
+          }
+        } else {
+          // decreaseTo (remote.go:155-171)
+          bool dec = false;
+          if ((st[s] & 3u) == RS_Replicate) {
+            if (m.log_index > match[s]) {
+              next[s] = match[s] + 1;
+              dec = true;
+            }
+          } else if (next[s] - 1 == m.log_index) {
+            if ((st[s] & 3u) == RS_Wait) st[s] = (st[s] & ~3u) | RS_Retry;
+            next[s] = umax64(1, umin64(m.log_index, m.hint + 1));
+            dec = true;
+          }
+          if (dec) {
+            if ((st[s] & 3u) == RS_Replicate) {  // enterRetryState → becomeRetry
+              next[s] = match[s] + 1;
+              st[s] = (st[s] & ~3u) | RS_Retry;
+            }
+            rep_mask |= 1u << s;
+          }
+        }
+      } else {  // HeartbeatResp, raft.go:1698-1710
+        if ((st[s] & 3u) == RS_Wait) st[s] = (st[s] & ~3u) | RS_Retry;
+        ctr.v[C_REMOTE_TOUCH]++;
+        if (match[s] < c.last_index) rep_mask |= 1u << s;
+        if (m.hint != 0) {
+          rq_pending = true;
+          rq_plo = m.hint;
+          rq_phi = m.hint_high;
+          rq_from = s + 1;
+        }
+      }
+      fan_out();
+    }
+  }
+  // batchedReadIndex → Peer.ReadIndex → handleLeaderReadIndex (raft.go:1633-1665)
+  if (inp == 2) {
+    const u64 low = ((u64)(round + 1) << 32) | (u64)o.self, high = cid + 1;
+    if (log_term(c.committed) != c.term) {
+      o.dropped_read_index(P, C, ctr, low, high);
+    } else {
+      // readIndex.addRequest (readindex.go:43-67)
+      bool dup = false;
+#pragma unroll
+      for (u32 i = 0; i < Cap::RQ; i++)
+        if (i < rq_n && rq_lo[i] == low && rq_hi[i] == high) dup = true;
+      if (!dup) {
+        u64 back_ix = 0;
+#pragma unroll
+        for (u32 i = 0; i < Cap::RQ; i++)
+          if (i + 1 == rq_n) back_ix = rq_ix[i];
+        if (rq_n > 0 && c.committed < back_ix) o.set_fault(ctr, F_PANIC);
+        if (rq_n >= C.rq_cap) {
+          o.set_fault(ctr, F_READQ);
+        } else {
+#pragma unroll
+          for (u32 i = 0; i < Cap::RQ; i++)
+            if (i == rq_n) {
+              rq_lo[i] = low;
+              rq_hi[i] = high;
+              rq_ix[i] = c.committed;
+              rq_fr[i] = 0;
+              rq_cf[i] = 0;
+            }
+          rq_n++;
+          rq_dirty = true;
+          ctr.v[C_RQ_TOUCH]++;
+        }
+      }
+      hb_pending = true;
+      hb_lo = low;
+      hb_hi = high;
+    }
+    fan_out();
+  }
+  // the tick (node.go:1384-1399 → raft.go:551-564, 592-629)
+  RBE_STAMP(t3);
+  q.increase_tick(C);
+  if (q.quiesced(C)) {
+    flags |= HF_RAFT_QUIESCE;
+    etick++;
+    ctr.v[C_QUIESCED_TICKS]++;
+  } else {
+    flags &= (u8)~HF_RAFT_QUIESCE;
+    etick++;  // leaderTick
+    if (etick >= C.election_rtt) etick = 0;  // check-quorum boundary excluded above
+    htick++;
+    if (htick >= C.heartbeat_rtt) {
+      htick = 0;
+      // broadcastHeartbeatMessage (raft.go:824-832)
+      u64 lo = 0, hi = 0;
+#pragma unroll
+      for (u32 i = 0; i < Cap::RQ; i++)
+        if (i + 1 == rq_n) {
+          lo = rq_lo[i];
+          hi = rq_hi[i];
+        }
+      hb_pending = true;
+      hb_lo = lo;
+      hb_hi = hi;
+    }
+    ctr.v[C_ACTIVE_TICKS]++;
+  }
+  fan_out();
+  // the proposal (handleProposals → Peer.ProposeEntries → handleLeaderPropose)
+  if (inp == 1) {
+    const u64 lo = wl_payload_lo(C.seed, cid, round), hi = mix64(lo);
+    ctr.v[C_PROPOSALS]++;
+    if (arena_used + 1 > C.ecap) {
+      o.set_fault(ctr, F_ARENA);
+    } else {
+      Ent e;  // staged in the arena as the Propose message carries it (term 0)
+      e.term = 0;
+      e.type = E_Application;
+      e.len = 16;
+      e.lo = lo;
+      e.hi = hi;
+      arena[arena_used] = e;
+      arena_used++;
+      // appendEntries (raft.go:909-920)
+      const u64 idx = c.last_index + 1;
+      const u64 sl = (idx & (u64)(C.ring - 1)) * C.n_rep + r;
+      P.term_ring[sl] = c.term;
+      Body b;
+      b.type = E_Application;
+      b.len = 16;
+      b.lo = lo;
+      b.hi = hi;
+      P.pay_ring[sl] = b;
+      ctr.v[C_RING_ACCESS]++;
+      c.last_index = idx;
+      c.t_last = c.term;
+      prop_idx = idx;
+      prop_lo = lo;
+      prop_hi = hi;
+#pragma unroll
+      for (u32 s = 0; s < N; s++)
+        if (s == k) try_update(match[s], next[s], st[s], c.last_index);
+      rep_mask |= ((1u << N) - 1u) & ~(1u << k);
+      fan_out();
+    }
+  }
+  (void)last0;
+  // ---- scatter
+  RBE_STAMP(t4);
+#pragma unroll
+  for (u32 s = 0; s < N; s++) {
+    RemoteMN x;
+    x.match = match[s];
+    x.next = next[s];
+    P.rem[r * N + s] = x;
+    P.rem_st[r * N + s] = (u8)st[s];
+  }
+  if (rq_dirty) {
+#pragma unroll
+    for (u32 i = 0; i < Cap::RQ; i++) {
+      if (i < rq_n) {
+        ReadReq x;
+        x.low = rq_lo[i];
+        x.high = rq_hi[i];
+        x.index = rq_ix[i];
+        x.from = (u8)rq_fr[i];
+        x.confirmed = (u8)rq_cf[i];
+        for (int j = 0; j < 6; j++) x.pad[j] = 0;
+        P.rq[rq_slot(i)] = x;
+      }
+    }
+  }
+  c.rq_head = (u8)rq_h;
+  c.rq_count = (u8)rq_n;
+  fast_finish<N, TRACE>(P, C, ctr, o, q, R_Leader, flags, h, c, etick, htick, committed0, digest0);
+  RBE_STAMP(t5);
+  RBE_PHASE_ADD(0, 0, t0, t1);
+  RBE_PHASE_ADD(0, 1, t1, t2);
+  RBE_PHASE_ADD(0, 2, t2, t3);
+  RBE_PHASE_ADD(0, 3, t3, t4);
+  RBE_PHASE_ADD(0, 4, t4, t5);
+  RBE_PHASE_ADD(0, 7, 0, 1);
+  return true;
+  }
+}
+
+// ---------------------------------------------------------------- follower
+// One steady-state follower round: inbox from the known leader only
+// (Replicate / Heartbeat / ReadIndexResp of the current term), no client
+// input, a tick that does not start an election.
+template <int N, bool TRACE>
+RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCounters& ctr) {
+  using Cap = FastCaps<N>;
+  if constexpr (N < 3) {
+    return false;
+  } else {
+  const u64 g = r / N;
+  const u32 k = (u32)(r % N);
+  const u32 par = round & 1u, ppar = par ^ 1u;
+  // ---- gather, level 1
+  RBE_STAMP(t0);
+  Hot h = P.hot[r];
+  Core c = P.core[r];
+  u32 pcin[N];
+#pragma unroll
+  for (u32 s = 0; s < N; s++)
+    pcin[s] = (round > 0 && s != k) ? (u32)P.cnt[ppar][g * N * N + s * N + k] : 0u;
+  const u32 until = P.iso_until[g];
+  const u8 isom = P.iso_mask[g];
+  const u64 digest0 = P.upd[r].digest;
+  const u32 fault0 = P.upd[r].fault;
+  if (h.role != R_Follower) return false;
+  if (h.flags & (HF_APPLY_PENDING | HF_IS_LTT)) return false;
+  if (c.ltt != 0) return false;
+  if (C.ext_inputs && P.ext[r].kind) return false;
+  const u32 ls = (u32)c.leader - 1u;  // leader slot (0xFFFFFFFF when no leader)
+  u32 n_in = 0;
+#pragma unroll
+  for (u32 s = 0; s < N; s++) {
+    if (s == k) continue;
+    const u32 n = (pcin[s] & 0x7Fu) + ((pcin[s] >> 7) & 0x7Fu);
+    if (n && s != ls) return false;
+    n_in += n;
+  }
+  if (n_in > Cap::FMAXM) return false;
+  // ---- gather, level 2: the leader's messages (Replicate first, then the rest)
+  RBE_STAMP(t1);
+  InMsg in[Cap::FMAXM];
+  u32 na = 0;
+  const Msg* lst = &P.msgs[ppar][((g * N + (ls < N ? ls : 0)) * N + k) * (u64)C.maxm];
+#pragma unroll
+  for (u32 s = 0; s < N; s++)
+    if (s == ls && s != k) na = pcin[s] & 0x7Fu;
+  // loads only inside the branches, decoded after the join (see lead_fast)
+  Msg raw[Cap::FMAXM];
+#pragma unroll
+  for (u32 i = 0; i < Cap::FMAXM; i++) {
+    if (i < n_in) raw[i] = lst[i < na ? i : C.maxm - 1u - (i - na)];
+  }
+#pragma unroll
+  for (u32 i = 0; i < Cap::FMAXM; i++) {
+    if (i < n_in) in[i] = load_in(&raw[i]);
+    else in[i].type = 0xFFu;
+  }
+#pragma unroll
+  for (u32 i = 0; i < Cap::FMAXM; i++) {
+    if (in[i].type == 0xFFu) continue;
+    const u32 t = in[i].type;
+    if (in[i].term != c.term) return false;
+    if (t != M_Replicate && t != M_Heartbeat && t != M_ReadIndexResp) return false;
+  }
+  FastQ q;
+  q.tick = h.q_tick;
+  q.qs = h.q_quiesced_since;
+  q.nas = h.q_no_activity_since;
+  q.eqt = h.q_exit_quiesce_tick;
+  q.qnew = false;
+  {
+    const bool idle = n_in == 0;
+    const bool q_at_tick = idle && C.quiesce &&
+                           (q.qs > 0 || (q.tick + 1u - q.nas > C.election_rtt * 20));
+    if (n_in == 0 && !q_at_tick && h.election_tick + 1u >= h.rand_et) return false;
+  }
+  // ---- gather, level 3: the first entry of the first four Replicate messages
+  // (a steady-state round carries up to three: commit broadcasts and resends
+  // without entries, then the new proposal)
+  Ent pre0, pre1, pre2, pre3;
+  pre0.term = pre0.lo = pre0.hi = 0;
+  pre0.type = pre0.len = 0;
+  pre1 = pre2 = pre3 = pre0;
+  {
+    const Ent* ab = &P.arena[ppar][(g * N + (ls < N ? ls : 0)) * (u64)C.ecap];
+    if (na > 0 && n_in > 0 && in[0].n_ent > 0) pre0 = ab[in[0].ent_off];
+    if (na > 1 && n_in > 1 && in[1].n_ent > 0) pre1 = ab[in[1].ent_off];
+    if (na > 2 && n_in > 2 && in[2].n_ent > 0) pre2 = ab[in[2].ent_off];
+    if (na > 3 && n_in > 3 && in[3].n_ent > 0) pre3 = ab[in[3].ent_off];
+  }
+  // Simulate the round's Replicate handling (handleReplicateMessage,
+  // raft.go:1339-1372) on the log tail: admit the round only if every log
+  // lookup hits t_last or lies past the tail and every appended entry is one
+  // of the two prefetched, so nothing is read after the first store below.
+  {
+    u64 L = c.last_index, Cm = c.committed, T = c.t_last;
+#pragma unroll
+    for (u32 i = 0; i < Cap::FMAXM; i++) {
+      if (in[i].type == 0xFFu) continue;
+      const InMsg& m = in[i];
+      if (m.type == M_Replicate) {
+        if (m.log_index < Cm) continue;          // answered with committed
+        if (m.log_index != L) return false;      // a ring lookup (or past the tail)
+        if (m.log_term != T) continue;           // rejected: no lookups, no change
+        if (m.n_ent > 1 || (m.n_ent == 1 && i >= 4)) return false;
+        if (m.n_ent == 1) {                      // conflict at L + 1: append
+          T = i == 0 ? pre0.term : (i == 1 ? pre1.term : (i == 2 ? pre2.term : pre3.term));
+          L = L + 1;
+        }
+        const u64 li = m.log_index + m.n_ent;
+        const u64 x = li < m.commit ? li : m.commit;
+        if (x > Cm && x <= L) Cm = x;
+      } else if (m.type == M_Heartbeat) {
+        if (m.commit > Cm && m.commit <= L) Cm = m.commit;
+      }
+    }
+  }
+  // ---- compute.  Every load above has completed before the first store
+  // below (vmcnt counts loads and stores in order; see lead_fast).
+  asm volatile("" ::: "memory");
+  rbe_wait_all_loads();
+  RBE_STAMP(t2);
+  FastOut<N, TRACE> o;
+  o.r = r;
+  o.g = g;
+  o.k = k;
+  o.par = par;
+  o.self = k + 1;
+  o.round_ = round;
+  o.iso = round < until ? isom : (u8)0;
+  o.pc = o.pc_hi = 0;
+  o.fault = fault0;
+  o.n_msgs = o.n_rtr = o.n_drop_ri = 0;
+  o.msg_hash = o.rtr_hash = o.drop_hash = 0;
+  o.term = c.term;
+  u8 flags = h.flags;
+  u32 etick = h.election_tick;
+  const u32 htick = h.heartbeat_tick;
+  const u64 committed0 = c.committed;
+  ctr.v[C_STEPS]++;
+  // entryLog.term (logentry.go:142-161) without touching memory: the
+  // eligibility simulation above admits only rounds whose lookups hit the
+  // log tail (t_last) or lie past it.
+  auto log_term = [&](u64 idx) -> u64 {
+    if (idx > c.last_index || idx == 0) return 0;
+    if (idx == c.last_index) return c.t_last;
+    if (c.last_index - idx >= C.ring) {
+      o.set_fault(ctr, F_WINDOW);
+      return 0;
+    }
+    ctr.v[C_RING_ACCESS]++;
+    o.set_fault(ctr, F_UNSUPPORTED);  // excluded by the eligibility simulation
+    return 0;
+  };
+  auto commit_to = [&](u64 idx) {  // logentry.go:324-333
+    if (idx <= c.committed) return;
+    if (idx > c.last_index) {
+      o.set_fault(ctr, F_PANIC);
+      return;
+    }
+    c.committed = idx;
+  };
+  const u32 lid = ls + 1;
+#pragma unroll
+  for (u32 s = 0; s < N; s++) {
+    if (s == k) continue;
+    if (pcin[s] & 0x8000u) {  // Quiesce first in the sender's stream
+      ctr.v[C_MSG_IN]++;
+      q.try_enter(C);
+    }
+    if (s != ls) continue;
+#pragma unroll
+    for (u32 i = 0; i < Cap::FMAXM; i++) {
+      if (in[i].type == 0xFFu) continue;
+      const InMsg& m = in[i];
+      ctr.v[C_MSG_IN]++;
+      ctr.v[C_ENT_IN] += m.n_ent;
+      if (m.type == M_Heartbeat && m.hint > 0) q.record_activity(C, M_ReadIndex);
+      else q.record_activity(C, m.type);
+      etick = 0;  // handleFollower{Replicate,Heartbeat,ReadIndexResp}: leader = from
+      if (m.type == M_Replicate) {  // handleReplicateMessage, raft.go:1339-1372
+        const Ent* ents = &P.arena[ppar][(g * N + s) * (u64)C.ecap + m.ent_off];
+        (void)ents;
+        auto ent = [&](u32 e) -> Ent {  // the eligibility simulation admits n_ent <= 1
+          if (i == 1) return pre1;
+          if (i == 2) return pre2;
+          if (i == 3) return pre3;
+          return pre0;
+        };
+        Msg resp = mk_msg(M_ReplicateResp, lid);
+        if (m.log_index < c.committed) {
+          resp.log_index = c.committed;
+        } else if (log_term(m.log_index) == m.log_term) {
+          // tryAppend / getConflictIndex (logentry.go:291-322)
+          u64 conflict = 0;
+          u32 ci = 0;
+          for (u32 e = 0; e < m.n_ent; e++) {
+            const u64 idx = m.log_index + 1 + e;
+            if (log_term(idx) != ent(e).term) {
+              conflict = idx;
+              ci = e;
+              break;
+            }
+          }
+          if (conflict != 0) {
+            if (conflict <= c.committed) {
+              o.set_fault(ctr, F_PANIC);
+            } else {
+              if (conflict - 1 >= 1 && conflict - 1 <= c.last_index &&
+                  log_term(conflict - 1) > ent(ci).term)
+                o.set_fault(ctr, F_PANIC);
+              u64 tl = c.t_last;
+              for (u32 e = ci; e < m.n_ent; e++) {
+                const Ent x = ent(e);
+                const u64 sl = ((m.log_index + 1 + e) & (u64)(C.ring - 1)) * C.n_rep + r;
+                P.term_ring[sl] = x.term;
+                Body b;
+                b.type = x.type;
+                b.len = x.len;
+                b.lo = x.lo;
+                b.hi = x.hi;
+                P.pay_ring[sl] = b;
+                ctr.v[C_RING_ACCESS]++;
+                tl = x.term;
+              }
+              c.last_index = m.log_index + m.n_ent;
+              c.t_last = tl;
+              c.saved_to = umin64(c.saved_to, conflict - 1);
+            }
+          }
+          const u64 last_idx = m.log_index + m.n_ent;
+          commit_to(umin64(last_idx, m.commit));
+          resp.log_index = last_idx;
+        } else {
+          resp.reject = 1;
+          resp.log_index = m.log_index;
+          resp.hint = c.last_index;
+        }
+        o.send(P, C, ctr, resp, nullptr);
+      } else if (m.type == M_Heartbeat) {  // handleHeartbeatMessage, raft.go:1301-1309
+        commit_to(m.commit);
+        Msg resp = mk_msg(M_HeartbeatResp, lid);
+        resp.hint = m.hint;
+        resp.hint_high = m.hint_high;
+        o.send(P, C, ctr, resp, nullptr);
+      } else {  // ReadIndexResp, raft.go:1890-1898
+        o.ready_to_read(P, C, ctr, m.log_index, m.hint, m.hint_high);
+      }
+    }
+  }
+  // the tick (raft.go:566-590, 623-629)
+  RBE_STAMP(t3);
+  q.increase_tick(C);
+  if (q.quiesced(C)) {
+    flags |= HF_RAFT_QUIESCE;
+    etick++;
+    ctr.v[C_QUIESCED_TICKS]++;
+  } else {
+    flags &= (u8)~HF_RAFT_QUIESCE;
+    etick++;  // nonLeaderTick; reaching the timeout is excluded above
+    if (etick >= h.rand_et) o.set_fault(ctr, F_UNSUPPORTED);
+    ctr.v[C_ACTIVE_TICKS]++;
+  }
+  c.leader = n_in ? (u8)lid : c.leader;
+  fast_finish<N, TRACE>(P, C, ctr, o, q, R_Follower, flags, h, c, etick, htick, committed0,
+                        digest0);
+  RBE_STAMP(t5);
+  RBE_PHASE_ADD(1, 0, t0, t1);
+  RBE_PHASE_ADD(1, 1, t1, t2);
+  RBE_PHASE_ADD(1, 2, t2, t3);
+  RBE_PHASE_ADD(1, 4, t3, t5);
+  RBE_PHASE_ADD(1, 7, 0, 1);
+  return true;
+  }
+}
+
+// the fast step of one role (k_round, k_fast_list)
+template <int N, bool TRACE, int MODE>
+RBE_HD bool step_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCounters& ctr) {
+  if constexpr (MODE == MODE_LEAD) return lead_fast<N, TRACE>(P, C, r, round, ctr);
+  else return foll_fast<N, TRACE>(P, C, r, round, ctr);
+}
+
+}  // namespace rbe

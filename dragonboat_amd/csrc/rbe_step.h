@@ -107,6 +107,7 @@ struct Lane {
   bool q_new;
   u64 term, committed, last, processed, saved_to;
   u64 t_last;  // term of entry `last` (log-tail cache, kept in Core)
+  u64 lead_start;  // leader: index of its no-op (Core::lead_start)
   u8 vote, leader, ltt, rq_head, rq_count;
   u64 c_match[N], c_next[N];  // LEAD: remote slots held in registers
   u32 c_st[N];
@@ -572,6 +573,7 @@ struct Lane {
     else if (ncc == 1) flags |= HF_PENDING_CC;
     // p72 of the raft thesis: an empty entry at the new term
     append_entry(E_Application, 0, 0, 0);
+    lead_start = last;
   }
   // appendEntries (raft.go:909-920) for one entry
   RBE_HD void append_entry(u32 type, u32 len, u64 lo, u64 hi) {
@@ -1260,6 +1262,7 @@ struct Lane {
     processed = c.processed;
     saved_to = c.saved_to;
     t_last = c.t_last;
+    lead_start = c.lead_start;
     vote = c.vote;
     leader = c.leader;
     ltt = c.ltt;
@@ -1294,7 +1297,7 @@ struct Lane {
     c.rq_count = rq_count;
     c.pad[0] = c.pad[1] = c.pad[2] = 0;
     c.t_last = t_last;
-    c.pad2 = 0;
+    c.lead_start = lead_start;
     P.core[r] = c;
     if constexpr (LEAD) {
       for (u32 s = 0; s < N; s++) {
@@ -1661,7 +1664,7 @@ RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   c.rq_head = c.rq_count = 0;
   c.pad[0] = c.pad[1] = c.pad[2] = 0;
   c.t_last = 1;  // bootstrap entries are at term 1
-  c.pad2 = 0;
+  c.lead_start = 0;
   P.core[r] = c;
   for (u32 s = 0; s < N; s++) {
     RemoteMN x;

@@ -82,7 +82,8 @@ struct alignas(16) Core {
   u8 rq_count;
   u8 pad[3];
   u64 t_last;      // term of entry last_index (log-tail cache)
-  u64 pad2;
+  u64 lead_start;  // leader: index of its no-op, the first entry of its term (raft.go:985);
+                   // entries [lead_start, last_index] have term == term, earlier ones less
 };
 
 // remote slot (remote.go:62-69): match/next; state|active<<2 lives in a u8 plane

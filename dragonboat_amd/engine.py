@@ -89,8 +89,8 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_step", "rbe_run"
            "rbe_round", "rbe_run_timed", "rbe_push_proposals", "rbe_push_read_index",
            "rbe_get_updates", "rbe_get_messages", "rbe_get_ready_to_reads", "rbe_get_entries",
            "rbe_get_views", "rbe_get_counters", "rbe_reset_counters", "rbe_fault_summary",
-           "rbe_footprint", "rbe_profile_rounds", "rbe_get_kernel_counters"]
-KERNEL_NAMES = ["k_triage", "k_fast_list<LEAD>", "k_fast_list<FOLL>", "k_full_list"]
+           "rbe_footprint", "rbe_profile_rounds", "rbe_get_kernel_counters", "rbe_kernel_name"]
+KERNEL_SLOTS = 4
 
 _lib = None
 
@@ -104,7 +104,8 @@ def load_library(path: Optional[str] = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    # RBE_LIB: an alternative build of the same ABI (A/B experiments, diagnostics)
+    p = path or os.environ.get("RBE_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise EngineError(
             f"{p} is missing: the HIP engine is the only implementation; build it with "
@@ -134,6 +135,7 @@ def load_library(path: Optional[str] = None):
         "rbe_footprint": (i32, [P(RbeConfig), P(u64)]),
         "rbe_profile_rounds": (i32, [vp, u32, P(C.c_float)]),
         "rbe_get_kernel_counters": (i32, [vp, C.c_int32, P(u64)]),
+        "rbe_kernel_name": (i32, [vp, C.c_int32, C.c_char_p, u32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -245,15 +247,24 @@ class Engine:
         return {n: o[i] for i, n in enumerate(COUNTER_NAMES)}
 
     def kernel_counters(self, kernel: int) -> Dict[str, int]:
-        """Counters contributed by one pipeline kernel (KERNEL_NAMES index)."""
+        """Counters contributed by the kernel in one pipeline slot."""
         o = (C.c_uint64 * CTR_NUM)()
         _check(self.lib.rbe_get_kernel_counters(self.h, kernel, o), "rbe_get_kernel_counters")
         return {n: o[i] for i, n in enumerate(COUNTER_NAMES)}
 
+    def kernel_names(self) -> List[str]:
+        """Kernel in each pipeline slot ("" for an unused slot)."""
+        out = []
+        for i in range(KERNEL_SLOTS):
+            buf = C.create_string_buffer(64)
+            _check(self.lib.rbe_kernel_name(self.h, i, buf, 64), "rbe_kernel_name")
+            out.append(buf.value.decode())
+        return out
+
     def profile_rounds(self, rounds: int) -> List[float]:
         """Run `rounds` rounds with HIP events between the pipeline kernels;
-        returns each kernel's total milliseconds (KERNEL_NAMES order)."""
-        ms = (C.c_float * len(KERNEL_NAMES))()
+        returns each slot's total milliseconds (kernel_names() order)."""
+        ms = (C.c_float * KERNEL_SLOTS)()
         _check(self.lib.rbe_profile_rounds(self.h, rounds, ms), "rbe_profile_rounds")
         return list(ms)
 

@@ -184,13 +184,16 @@ int rbe_round(const rbe_engine* e, uint32_t* round);
 /* Time `rounds` rounds with HIP events on the engine stream; *ms = elapsed. */
 int rbe_run_timed(rbe_engine* e, uint32_t rounds, float* ms);
 
-/* Round-pipeline kernels, in launch order (rbe_profile_rounds,
- * rbe_get_kernel_counters). */
-#define RBE_KERNEL_TRIAGE 0    /* k_triage: every replica; idle rounds finish here */
-#define RBE_KERNEL_FAST_LEAD 1 /* k_fast_list<LEAD>: steady-state leaders */
-#define RBE_KERNEL_FAST_FOLL 2 /* k_fast_list<FOLL>: steady-state followers */
-#define RBE_KERNEL_FULL 3      /* k_full_list: the whole handler table (elections, ...) */
+/* Round-pipeline kernel slots (rbe_profile_rounds, rbe_get_kernel_counters,
+ * rbe_kernel_name).  The default pipeline is k_round (triage +
+ * steady-state leader/follower steps, fused) in slot 0 and k_full_list in
+ * slot 3; RBE_MODE=split runs k_triage / k_fast_list<LEAD> / k_fast_list<FOLL>
+ * / k_full_list in slots 0-3; RBE_MODE=full runs k_step in slot 3.  Unused
+ * slots have an empty name and zero time. */
 #define RBE_KERNEL_NUM 4
+
+/* Name of the kernel in `slot` for this engine's pipeline ("" if unused). */
+int rbe_kernel_name(const rbe_engine* e, int32_t slot, char* buf, uint32_t cap);
 
 /* Run `rounds` rounds one at a time with HIP events between the pipeline
  * kernels on the engine stream; ms_per_kernel[RBE_KERNEL_NUM] receives each

@@ -1,0 +1,38 @@
+"""Diagnostic: per-phase wave time of the fast steps (s_memtime stamps) from
+the RBE_PHASE_TIMING build (build/libdragonboat_amd_phase.so).
+
+    hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DRBE_PHASE_TIMING \
+        -o build/libdragonboat_amd_phase.so dragonboat_amd/csrc/rbe_engine.hip
+    RBE_MODE=split python scripts/phase_timing.py c4
+"""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from dragonboat_amd import engine as E  # noqa: E402
+
+lib = E.load_library(os.path.join(ROOT, "build", "libdragonboat_amd_phase.so"))
+E._lib = lib
+lib.rbe_debug_phases.argtypes = [C.POINTER(C.c_uint64)]
+w = sys.argv[1] if len(sys.argv) > 1 else "c4"
+kw, settle, _ = bench.WORKLOADS[w]
+eng = E.Engine(**kw)
+eng.run(settle)
+eng.sync()
+o = (C.c_uint64 * 16)()
+lib.rbe_debug_phases(o)
+rounds = 20
+ms = eng.profile_rounds(rounds)
+lib.rbe_debug_phases(o)
+names = {0: ["gather1", "gather2", "inbox+read", "tick+propose", "scatter+finish"],
+         1: ["gather1", "gather2", "inbox", "-", "tick+finish"]}
+for role, rn in ((0, "leader"), (1, "follower")):
+    n = o[role * 8 + 7]
+    if not n:
+        continue
+    parts = [f"{names[role][i]}={o[role * 8 + i] / n:.0f}" for i in range(5) if names[role][i] != "-"]
+    print(f"{w} {rn}: waves={n / rounds:.0f}/round cycles/wave: " + " ".join(parts))
+print("kernel ms per round:", [round(x / rounds, 4) for x in ms], eng.kernel_names())

@@ -19,6 +19,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def kernel_key(name):
+    if "k_round" in name:
+        return "k_round"
     if "k_triage" in name:
         return "k_triage"
     if "k_fast_list" in name:

@@ -8,7 +8,7 @@
 #include <cstring>
 #include <vector>
 
-#include "../../dragonboat_amd/csrc/rbe_step.h"
+#include "../../dragonboat_amd/csrc/rbe_fast.h"
 #include "../../include/rbe.h"
 
 using namespace rbe;
@@ -51,11 +51,11 @@ static void run_round(SoaEngine* e) {
       memset(&c, 0, sizeof(c));
       bool ok;
       if (li == 0)
-        ok = e->C.trace ? step_replica_fast<N, true, MODE_LEAD>(e->P, e->C, r, e->round, c)
-                        : step_replica_fast<N, false, MODE_LEAD>(e->P, e->C, r, e->round, c);
+        ok = e->C.trace ? step_fast<N, true, MODE_LEAD>(e->P, e->C, r, e->round, c)
+                        : step_fast<N, false, MODE_LEAD>(e->P, e->C, r, e->round, c);
       else
-        ok = e->C.trace ? step_replica_fast<N, true, MODE_FOLL>(e->P, e->C, r, e->round, c)
-                        : step_replica_fast<N, false, MODE_FOLL>(e->P, e->C, r, e->round, c);
+        ok = e->C.trace ? step_fast<N, true, MODE_FOLL>(e->P, e->C, r, e->round, c)
+                        : step_fast<N, false, MODE_FOLL>(e->P, e->C, r, e->round, c);
       if (!ok) lists[2].push_back(r);
       for (int i = 0; i < C_NUM; i++) e->counters[i] += c.v[i];
     }
