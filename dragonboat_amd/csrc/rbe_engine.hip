@@ -129,11 +129,39 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, const u32
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
   const int lane = threadIdx.x & 63;
-  const u64 lo = (u64)blockIdx.x * kTriChunk;
-  for (u32 j = threadIdx.x; j < kTriChunk; j += kBlock) {
-    const u64 r = lo + j;
+  // The idle bytes and inbound count words of all kPer replicas a lane owns
+  // (strided by the block size, so each load is coalesced across the wave and
+  // the work lists come out in replica order) are loaded before any of them
+  // is processed; most rounds are then decided without reading Hot: a lazy
+  // quiesced tick completes here, a replica with inbound messages is listed
+  // by the role its idle byte carries.
+  constexpr u32 kPer = kTriChunk / kBlock;
+  const u64 lo = (u64)blockIdx.x * kTriChunk + threadIdx.x;
+  u8 ibs[kPer];
+  u32 inb[kPer];
+#pragma unroll
+  for (u32 i = 0; i < kPer; i++) {
+    const u64 r = lo + (u64)i * kBlock;
+    ibs[i] = r < C.n_rep ? P.idle[r] : (u8)0;
+  }
+#pragma unroll
+  for (u32 i = 0; i < kPer; i++) {
+    const u64 r = lo + (u64)i * kBlock;
+    inb[i] = r < C.n_rep ? inbound_bits<N>(P, r, round) : 0u;
+  }
+  const bool shortcut = !TRACE && C.quiesce;
+#pragma unroll
+  for (u32 i = 0; i < kPer; i++) {
+    const u64 r = lo + (u64)i * kBlock;
     u32 cls = T_DONE;
-    if (r < C.n_rep) cls = triage_replica<N, TRACE>(P, C, r, round, c);
+    if (r < C.n_rep) {
+      if (shortcut && triage_lazy<N>(P, C, r, round, ibs[i], inb[i] & 1u, c))
+        cls = T_DONE;
+      else if (inb[i] & 2u)
+        cls = class_of_role(idle_role(ibs[i]));
+      else
+        cls = triage_replica<N, TRACE>(P, C, r, round, c);
+    }
 #pragma unroll
     for (u32 li = 0; li < 3; li++) {
       const bool want = cls == li + 1;
@@ -284,7 +312,7 @@ struct rbe_engine {
   hipGraphExec_t graph = nullptr;
   u32 graph_rounds = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  int mode = 0;              // RBE_MODE: 0 fused (default), 1 split (triage + 2 fast lists), 2 full
+  int mode = 1;              // RBE_MODE: 0 fused, 1 split (default: triage + 2 fast lists), 2 full
   Lists L;                   // per-round work lists (triage → fast → full)
 };
 
@@ -293,7 +321,7 @@ static constexpr unsigned kFullGrid = 1024;  // persistent grid of k_full_list
 
 static u64 bytes_of(const Params& C, u64* parts) {
   const u64 N = C.n, G = C.n_groups, R = C.n_rep;
-  u64 p[16] = {
+  u64 p[17] = {
       R * sizeof(Hot),
       R * sizeof(Core),
       R * N * sizeof(RemoteMN),
@@ -310,9 +338,10 @@ static u64 bytes_of(const Params& C, u64* parts) {
       R * C.rtr_cap * sizeof(RTR),
       R * C.dri_cap * sizeof(DropRI),
       R * sizeof(ExtIn),
+      R * sizeof(u8),
   };
   u64 t = 0;
-  for (int i = 0; i < 16; i++) {
+  for (int i = 0; i < 17; i++) {
     if (parts) parts[i] = p[i];
     t += (p[i] + 255) & ~255ull;
   }
@@ -503,10 +532,10 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   }
   HIP_IGNORE(hipEventCreate(&e->ev0));
   HIP_IGNORE(hipEventCreate(&e->ev1));
-  u64 parts[16];
+  u64 parts[17];
   bytes_of(C, parts);
-  void* ptrs[16];
-  for (int i = 0; i < 16; i++) {
+  void* ptrs[17];
+  for (int i = 0; i < 17; i++) {
     u64 b = parts[i] ? parts[i] : 16;
     if (hipMalloc(&ptrs[i], b) != hipSuccess) {
       for (int j = 0; j < i; j++) e->allocs.push_back(ptrs[j]);
@@ -542,6 +571,7 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   P.rtr = (RTR*)ptrs[13];
   P.dri = (DropRI*)ptrs[14];
   P.ext = (ExtIn*)ptrs[15];
+  P.idle = (u8*)ptrs[16];
   if (hipMalloc(&P.counters, kCtrWords * sizeof(u64)) != hipSuccess) {
     rbe_destroy(e);
     return RBE_E_NOMEM;
@@ -554,7 +584,9 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   }
   HIP_IGNORE(hipMemsetAsync(e->d_round, 0, sizeof(u32), e->stream));
   const char* mode = getenv("RBE_MODE");
-  e->mode = !mode ? 0 : (strcmp(mode, "full") == 0 ? 2 : (strcmp(mode, "split") == 0 ? 1 : 0));
+  // default: the split pipeline (k_triage → k_fast_list<LEAD> → k_fast_list<FOLL>
+  // → k_full_list); RBE_MODE=fused runs k_round + k_full_list, RBE_MODE=full k_step
+  e->mode = !mode ? 1 : (strcmp(mode, "full") == 0 ? 2 : (strcmp(mode, "fused") == 0 ? 0 : 1));
   if (C.n_rep >= (1ull << 32)) {
     rbe_destroy(e);
     return RBE_E_INVALID;  // list entries are 32-bit replica indices
@@ -804,7 +836,7 @@ int rbe_get_views(rbe_engine* e, uint64_t first, uint64_t count, rbe_replica_vie
   for (u64 i = 0; i < count; i++) {
     rbe_replica_view& v = out[i];
     memset(&v, 0, sizeof(v));
-    const Hot& h = hot[i];
+    const Hot h = materialize_hot(hot[i], e->C, e->round);
     const Core& c = core[i];
     v.term = c.term;
     v.vote = c.vote;

@@ -182,7 +182,9 @@ struct FastOut {
       slot = C.maxm - 1u - b;
       add_pc(d, 1u << 7);
     }
+#ifndef RBE_DIAG_NO_MSG_STORES
     P.msgs[par][((g * N + k) * N + d) * (u64)C.maxm + slot] = m;
+#endif
     ctr.v[C_MSG_OUT]++;
     ctr.v[C_ENT_OUT] += m.n_ent;
   }
@@ -375,6 +377,7 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
   u.pad = 0;
   u.round = o.round_;
   u.pad2 = 0;
+#ifndef RBE_DIAG_NO_STATE_STORES
   P.upd[r] = u;
   u16* cnt = &P.cnt[o.par][o.g * N * N + o.k * N];
 #pragma unroll
@@ -388,6 +391,8 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
   h.q_exit_quiesce_tick = q.eqt;
   P.hot[r] = h;
   P.core[r] = c;
+  P.idle[r] = idle_byte(C, role, flags, q.qs);
+#endif
 }
 
 // ---------------------------------------------------------------- leader
@@ -409,7 +414,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   const u64 cid = C.cid_base + g * C.cid_stride;
   // ---- gather, level 1: independent loads
   RBE_STAMP(t0);
-  Hot h = P.hot[r];
+  Hot h = load_hot(P, C, r, round);
   Core c = P.core[r];
   u64 match[N], next[N];
   u32 st[N];
@@ -1017,7 +1022,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   const u32 par = round & 1u, ppar = par ^ 1u;
   // ---- gather, level 1
   RBE_STAMP(t0);
-  Hot h = P.hot[r];
+  Hot h = load_hot(P, C, r, round);
   Core c = P.core[r];
   u32 pcin[N];
 #pragma unroll

@@ -72,6 +72,39 @@ RBE_HD u64 rto_rand(u64 seed, u64 cid, u64 nid, u64 count) {
   return mix64(seed ^ (cid * 0x9E3779B97F4A7C15ULL) ^ (nid << 32) ^ count);
 }
 
+// Lazy quiesced ticks.  With Quiesce on, every round advances the quiesce
+// tick of every replica by exactly one, so at the start of round `round` a
+// replica's q_tick equals `round`.  k_triage skips the Hot write of a round
+// that is nothing but a QuiescedTick (electionTick++ and tick++, raft.go:
+// 623-629, quiesce.go:43-55), so a stored record may lag; every reader
+// applies the missed ticks here.  Without Quiesce nothing is skipped.
+RBE_HD Hot materialize_hot(Hot h, const Params& C, u32 round) {
+  if (C.quiesce) {
+    const u32 lag = round - h.q_tick;
+    h.election_tick += lag;
+    h.q_tick = round;
+  }
+  return h;
+}
+RBE_HD Hot load_hot(const Planes& P, const Params& C, u64 r, u32 round) {
+  return materialize_hot(P.hot[r], C, round);
+}
+
+// The idle byte of a replica (Planes::idle), rewritten with every Hot write:
+//   IB_LAZY  the next round is a pure QuiescedTick unless an input arrives
+//            (Quiesce on, quiesced, RAFT_QUIESCE already set, nothing to apply);
+//   IB_LEAD  the replica leads (only a leader takes client input);
+//   IB_H1/H2 history: the last / second-last round was skipped lazily, so the
+//            outbox-count words of this round's parity are known to be zero;
+//   bits 4-6 the role, so a replica with inbound messages is classified
+//            without reading Hot.
+enum : u8 { IB_LAZY = 1, IB_LEAD = 2, IB_H1 = 4, IB_H2 = 8, IB_ROLE_SHIFT = 4 };
+RBE_HD u8 idle_byte(const Params& C, u8 role, u8 flags, u32 qs) {
+  const bool lazy = C.quiesce && qs > 0 && (flags & HF_RAFT_QUIESCE) && !(flags & HF_APPLY_PENDING);
+  return (u8)((lazy ? IB_LAZY : 0) | (role == R_Leader ? IB_LEAD : 0) | ((role & 7u) << IB_ROLE_SHIFT));
+}
+RBE_HD u32 idle_role(u8 ib) { return (ib >> IB_ROLE_SHIFT) & 7u; }
+
 RBE_HD bool is_leader_message(u32 t) {  // raft.go:1382-1385
   return t == M_Replicate || t == M_InstallSnapshot || t == M_Heartbeat || t == M_TimeoutNow ||
          t == M_ReadIndexResp;
@@ -1242,7 +1275,7 @@ struct Lane {
 
   // ------------------------------------------------------------- the step
   RBE_HD void load() {
-    Hot h = P.hot[r];
+    Hot h = load_hot(P, C, r, round);
     role = h.role;
     flags = h.flags;
     vresp = h.votes_resp;
@@ -1284,6 +1317,7 @@ struct Lane {
     h.q_exit_quiesce_tick = q_eqt;
     h.rng_count = rngc;
     P.hot[r] = h;
+    P.idle[r] = idle_byte(C, role, flags, q_qs);
     Core c;
     c.term = term;
     c.committed = committed;
@@ -1652,6 +1686,7 @@ RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   h.q_tick = h.q_quiesced_since = h.q_no_activity_since = h.q_exit_quiesce_tick = 0;
   h.rng_count = 2;
   P.hot[r] = h;
+  P.idle[r] = idle_byte(C, h.role, h.flags, 0);
   Core c;
   c.term = 1;
   c.committed = N;
@@ -1709,13 +1744,59 @@ RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
 // Everything else is routed to the leader / follower / full lists.
 enum : u32 { T_DONE = 0, T_LEAD = 1, T_FOLL = 2, T_FULL = 3 };
 
+// The lazy-idle shortcut (bench configuration: no trace, Quiesce on).  A
+// replica whose idle byte says IB_LAZY, with no inbound message or Quiesce
+// notice (`inbound` = any non-zero inbound count word) and no client input,
+// runs a round that is one QuiescedTick: it is applied lazily
+// (materialize_hot), so neither Hot nor the outbox counts are touched.  The
+// caller has loaded `ib` and `inbound` (k_triage prefetches them for all the
+// replicas a lane owns).  Returns true when the round is complete.
+template <int N>
+RBE_HD bool triage_lazy(const Planes& P, const Params& C, u64 r, u32 round, u8 ib, bool inbound,
+                        StepCounters& ctr) {
+  if (!(ib & IB_LAZY) || inbound) return false;
+  const u64 g = r / N;
+  if ((ib & IB_LEAD) && wl_input(C, C.cid_base + g * C.cid_stride, round)) return false;
+  if (C.ext_inputs && P.ext[r].kind) return false;
+  ctr.v[C_STEPS]++;
+  ctr.v[C_QUIESCED_TICKS]++;
+  if (ib & IB_LEAD) ctr.v[C_LEADER_STEPS]++;
+  if (!(ib & IB_H2)) {  // this parity's outbox counts may still be non-zero
+    u16* cnt = &P.cnt[round & 1u][g * N * N + (u32)(r % N) * N];
+    for (u32 d = 0; d < N; d++) cnt[d] = 0;
+  }
+  const u8 nb = (u8)((ib & ~(IB_H1 | IB_H2)) | IB_H1 | ((ib & IB_H1) ? IB_H2 : 0));
+  if (nb != ib) P.idle[r] = nb;
+  return true;
+}
+// the inbound count words of replica r in this round: bit 0 = any non-zero
+// word, bit 1 = any message (a Quiesce notice alone leaves it clear)
+template <int N>
+RBE_HD u32 inbound_bits(const Planes& P, u64 r, u32 round) {
+  if (round == 0) return 0;
+  const u64 g = r / N;
+  const u32 k = (u32)(r % N);
+  const u16* icnt = &P.cnt[(round & 1u) ^ 1u][g * N * N];
+  u32 any = 0;
+  for (u32 s = 0; s < N; s++) {
+    if (s == k) continue;
+    const u32 pc = icnt[s * N + k];
+    if (pc) any |= 1u;
+    if (pc & 0x3FFFu) any |= 2u;
+  }
+  return any;
+}
+RBE_HD u32 class_of_role(u32 role) {
+  return role == R_Leader ? 1u /*T_LEAD*/ : (role == R_Follower ? 2u /*T_FOLL*/ : 3u /*T_FULL*/);
+}
+
 template <int N, bool TRACE>
 RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, u32 round,
                           StepCounters& ctr) {
   const u64 g = r / N;
   const u32 k = (u32)(r % N);
   const u32 par = round & 1u;
-  const Hot h = P.hot[r];
+  const Hot h = load_hot(P, C, r, round);
   u32 nmsg = 0, qbits = 0;
   if (round > 0) {
     const u16* icnt = &P.cnt[par ^ 1u][g * N * N];
@@ -1777,27 +1858,39 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, u32 round,
     const u32 until = P.iso_until[g];
     iso = round < until ? P.iso_mask[g] : (u8)0;
   }
+  // A round that is only a QuiescedTick of an already-flagged replica writes
+  // nothing (lazy ticks, materialize_hot); its outbox counts are written only
+  // if the buffer of this parity still holds a non-zero word.
+  const bool lazy = !TRACE && quiesced && !qnew && qbits == 0 && (h.flags & HF_RAFT_QUIESCE);
   u16* cnt = &P.cnt[par][g * N * N + k * N];
-  for (u32 d = 0; d < N; d++) {
-    u16 v = 0;
-    if (qnew && d != k) {  // sendEnterQuiesceMessages (node.go:873-886)
-      if (((iso >> k) & 1u) || ((iso >> d) & 1u)) {
-        ctr.v[C_MSG_DROPPED]++;
-      } else {
-        v = 0x8000u;
-        ctr.v[C_MSG_OUT]++;
+  bool dirty = !lazy;
+  if (lazy)
+    for (u32 d = 0; d < N; d++) dirty |= cnt[d] != 0;
+  if (dirty) {
+    for (u32 d = 0; d < N; d++) {
+      u16 v = 0;
+      if (qnew && d != k) {  // sendEnterQuiesceMessages (node.go:873-886)
+        if (((iso >> k) & 1u) || ((iso >> d) & 1u)) {
+          ctr.v[C_MSG_DROPPED]++;
+        } else {
+          v = 0x8000u;
+          ctr.v[C_MSG_OUT]++;
+        }
       }
+      cnt[d] = v;
     }
-    cnt[d] = v;
   }
-  Hot o = h;
-  o.flags = flags;
-  o.election_tick = etick;
-  o.q_tick = qt;
-  o.q_quiesced_since = qs;
-  o.q_no_activity_since = qn;
-  o.q_exit_quiesce_tick = qe;
-  P.hot[r] = o;
+  if (!lazy) {
+    Hot o = h;
+    o.flags = flags;
+    o.election_tick = etick;
+    o.q_tick = qt;
+    o.q_quiesced_since = qs;
+    o.q_no_activity_since = qn;
+    o.q_exit_quiesce_tick = qe;
+    P.hot[r] = o;
+    P.idle[r] = idle_byte(C, h.role, flags, qs);
+  }
   if (TRACE) {
     const Core c = P.core[r];
     Upd u = P.upd[r];

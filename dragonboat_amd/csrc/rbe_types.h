@@ -213,6 +213,8 @@ struct Planes {
   Msg* msgs[2];       // [n_groups * N * N * maxm]
   Ent* arena[2];      // [n_rep * ecap]
   u8* iso_mask;       // [n_groups]
+  u8* idle;           // [n_rep] IB_* bits: lets k_triage finish a lazily quiesced round
+                      // without reading Hot (rbe_step.h, idle_byte)
   u32* iso_until;     // [n_groups]
   Upd* upd;           // [n_rep]
   RTR* rtr;           // [n_rep * rtr_cap]

@@ -185,11 +185,11 @@ int rbe_round(const rbe_engine* e, uint32_t* round);
 int rbe_run_timed(rbe_engine* e, uint32_t rounds, float* ms);
 
 /* Round-pipeline kernel slots (rbe_profile_rounds, rbe_get_kernel_counters,
- * rbe_kernel_name).  The default pipeline is k_round (triage +
- * steady-state leader/follower steps, fused) in slot 0 and k_full_list in
- * slot 3; RBE_MODE=split runs k_triage / k_fast_list<LEAD> / k_fast_list<FOLL>
- * / k_full_list in slots 0-3; RBE_MODE=full runs k_step in slot 3.  Unused
- * slots have an empty name and zero time. */
+ * rbe_kernel_name).  The default pipeline runs k_triage /
+ * k_fast_list<LEAD> / k_fast_list<FOLL> / k_full_list in slots 0-3;
+ * RBE_MODE=fused runs k_round (triage + steady-state steps in one kernel) in
+ * slot 0 and k_full_list in slot 3; RBE_MODE=full runs k_step in slot 3.
+ * Unused slots have an empty name and zero time. */
 #define RBE_KERNEL_NUM 4
 
 /* Name of the kernel in `slot` for this engine's pipeline ("" if unused). */

@@ -40,9 +40,17 @@ static void run_round(SoaEngine* e) {
   for (u64 r = 0; r < e->C.n_rep; r++) {
     memset(&c, 0, sizeof(c));
     u32 cls = T_FULL;
-    if (!e->full_only)
-      cls = e->C.trace ? triage_replica<N, true>(e->P, e->C, r, e->round, c)
-                       : triage_replica<N, false>(e->P, e->C, r, e->round, c);
+    if (!e->full_only) {
+      const u8 ib = e->P.idle[r];
+      const u32 inb = inbound_bits<N>(e->P, r, e->round);
+      if (!e->C.trace && e->C.quiesce && triage_lazy<N>(e->P, e->C, r, e->round, ib, inb & 1u, c))
+        cls = T_DONE;
+      else if (inb & 2u)  // messages: the role decides the list (as triage_replica would)
+        cls = class_of_role(idle_role(ib));
+      else
+        cls = e->C.trace ? triage_replica<N, true>(e->P, e->C, r, e->round, c)
+                         : triage_replica<N, false>(e->P, e->C, r, e->round, c);
+    }
     if (cls != T_DONE) lists[cls - 1].push_back(r);
     for (int i = 0; i < C_NUM; i++) e->counters[i] += c.v[i];
   }
@@ -123,6 +131,7 @@ void* soa_create(const rbe_config* cfg) {
     P.arena[p] = alloc<Ent>(e, R * C.ecap);
   }
   P.iso_mask = alloc<u8>(e, G);
+  P.idle = alloc<u8>(e, R);
   P.iso_until = alloc<u32>(e, G);
   P.upd = alloc<Upd>(e, R);
   P.rtr = alloc<RTR>(e, R * C.rtr_cap);
@@ -161,7 +170,7 @@ void soa_views(void* h, rbe_replica_view* out) {
   for (u64 i = 0; i < e->C.n_rep; i++) {
     rbe_replica_view& v = out[i];
     memset(&v, 0, sizeof(v));
-    const Hot& hh = e->P.hot[i];
+    const Hot hh = materialize_hot(e->P.hot[i], e->C, e->round);
     const Core& c = e->P.core[i];
     v.term = c.term;
     v.vote = c.vote;

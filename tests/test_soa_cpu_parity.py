@@ -36,3 +36,17 @@ def test_pipeline_takes_fast_paths():
     eng = SoaCpu(trace=True, **C2)
     eng.run(200)
     assert eng.slow_total() < 0.2 * eng.counters()["steps"]
+
+
+@pytest.mark.parametrize("name", ["C4", "C4_DENSE", "MIXED", "C2"])
+def test_soa_cpu_untraced_state_parity(name):
+    """Without trace the engine takes the bench paths (lazy quiesced ticks in
+    triage, no digest); every protocol field must still match the oracle."""
+    kw, rounds = CASES[name]
+    eng = SoaCpu(trace=False, **kw, **ENGINE_EXTRA.get(name, {}))
+    ref = O.Harness(**kw)
+    d = run_lockstep(eng, ref, rounds, every=1, skip=("digest",))
+    assert d is None, f"{name}: first divergence {d}"
+    assert eng.faults()[0] == 0
+    bad = counters_match(eng.counters(), ref.counters())
+    assert not bad, f"{name}: counters differ {bad}"
