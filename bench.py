@@ -53,6 +53,11 @@ WORKLOADS = {
     "c3": (dict(n_groups=100_000, n_replicas=5, check_quorum=True, wl_enabled=True,
                 wl_start_round=40, iso_period=50, iso_len=30, iso_mod=10, ring=128),
            100, "C3: 100k groups x 5, CheckQuorum, leader isolation 30/50 rounds for 10%"),
+    # groups per GPU; every rank holds the planes of all N x 500k groups and
+    # steps the replicas it owns
+    "c5": (dict(n_groups=500_000, n_replicas=3, wl_enabled=True, wl_start_round=30, ring=64),
+           60, "C5: 500k groups x 3 per GPU, replica-per-GPU (replica k of group g on rank "
+               "(g+k) % N), steady replication, cross-rank messages by all-to-all each round"),
 }
 
 
@@ -112,6 +117,113 @@ def load_traffic(name, kernel):
         return None
 
 
+def run_replica_mode(args, ws, rank, local, dist, dev, gloo_staged):
+    """C5: replica-per-GPU.  Every round = one engine round over the owned
+    replicas + one exchange (pack → counts all-to-all → records
+    all_to_all_single → unpack, dragonboat_amd/replica.py).  The timed region
+    holds both; the exchange share is reported beside it."""
+    from dragonboat_amd.engine import Engine, footprint, make_config
+    from dragonboat_amd.replica import ReplicaExchange
+    from dragonboat_amd.shard import reduce_results
+
+    kw, settle, desc = WORKLOADS["c5"]
+    kw = dict(kw)
+    per_gpu = args.groups or kw["n_groups"]
+    kw["n_groups"] = per_gpu * ws
+    cfg = make_config(device=0 if gloo_staged else local, trace=False,
+                      rep_world=ws if ws > 1 else 0, rep_rank=rank, **kw)
+    eng = Engine(cfg)
+    xch = None
+    if ws > 1:
+        xch = ReplicaExchange(eng, buf_device=dev, comm_device="cpu" if gloo_staged else dev)
+
+    def rounds(k, timed_xchg=None):
+        for _ in range(k):
+            eng.step()
+            if xch is not None:
+                if timed_xchg is not None:
+                    eng.sync()
+                    t = time.perf_counter()
+                    xch.exchange()
+                    timed_xchg[0] += time.perf_counter() - t
+                else:
+                    xch.exchange()
+
+    def barrier():
+        if ws > 1:
+            dist.barrier()
+        eng.sync()
+
+    rounds(settle)
+    rounds(max(1, args.warmup))
+    eng.sync()
+    eng.reset_counters()
+    b0 = xch.bytes_sent if xch else 0
+    barrier()
+    t0 = time.perf_counter()
+    rounds(args.steps)
+    barrier()
+    wall = time.perf_counter() - t0
+    c = eng.counters()
+    nf, fo = eng.fault_summary()
+    sent = (xch.bytes_sent - b0) if xch else 0
+    # exchange share, on separate rounds (the sync before each exchange would
+    # otherwise perturb the timed region)
+    xt = [0.0]
+    rounds(min(args.steps, 20), timed_xchg=xt)
+    xchg_ms = xt[0] * 1e3 / min(args.steps, 20)
+    red_dev = None if gloo_staged or ws == 1 else dev
+    wall_max, (steps, committed, reads, faulty, sent_all, xms_sum) = reduce_results(
+        dist if ws > 1 else None, wall, [c["steps"], c["committed"], c["reads_confirmed"], nf,
+                                         sent, xchg_ms], device=red_dev)
+    xms_mean = xms_sum / ws
+    # kernel split: single profiled rounds, each followed by its exchange
+    prof_rounds = max(1, min(args.steps, args.prof_rounds))
+    eng.reset_counters()
+    kms = [0.0] * 4
+    for _ in range(prof_rounds):
+        for i, v in enumerate(eng.profile_rounds(1)):
+            kms[i] += v
+        if xch is not None:
+            xch.exchange()
+    kernels = []
+    for ki, name in enumerate(eng.kernel_names()):
+        if not name:
+            continue
+        b = alg_bytes(eng.kernel_counters(ki)) / prof_rounds
+        us = kms[ki] * 1e3 / prof_rounds
+        kernels.append({"kernel": name, "avg_us": us, "alg_bytes_per_launch": b,
+                        "achieved_gbs": (b / (us * 1e-6) / 1e9) if us > 0 else 0.0})
+    dom = max(kernels, key=lambda k: k["avg_us"])
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": steps / wall_max, "unit": "group-steps/s",
+            "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": wall_max * 1e3 / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": desc, "groups_per_gpu": per_gpu, "replicas_per_group": 3,
+                       "total_groups": kw["n_groups"],
+                       "parallelism": f"replica-per-GPU x{ws} ((g+k) % {ws})",
+                       "exchange": ("gloo, host-staged (rehearsal)" if gloo_staged else
+                                    "RCCL all_to_all_single") if ws > 1 else "none (1 rank)",
+                       "election_rtt": 10, "heartbeat_rtt": 1, "settle_rounds": settle,
+                       "device_bytes_per_gpu": footprint(cfg)},
+            "committed_entries_per_s": committed / wall_max,
+            "read_confirmations_per_s": reads / wall_max,
+            "faulty_replicas": int(faulty), "fault_bits_rank0": fo,
+            "exchange": {"bytes_per_round_all_ranks": sent_all / args.steps,
+                         "ms_per_round_mean_rank": xms_mean},
+            "roofline": {"bound": "hbm", "achieved": dom["achieved_gbs"], "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": dom["achieved_gbs"] / HBM_PEAK_GBS,
+                         "traffic": None, "kernel": dom["kernel"],
+                         "alg_bytes_per_launch": dom["alg_bytes_per_launch"],
+                         "avg_launch_us": dom["avg_us"], "profiled_rounds": prof_rounds},
+            "round": {"kernels": kernels},
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -126,18 +238,28 @@ def main():
     ap.add_argument("--cpu-rounds", type=int, default=100)
     ap.add_argument("--cpu-threads", type=int,
                     default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    ap.add_argument("--xchg-gloo", action="store_true",
+                    help="c5 rehearsal: all ranks on cuda:0, exchange over gloo via host memory")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
     import torch
     import torch.distributed as dist
     use_dist = ws > 1
+    gloo_staged = args.workload == "c5" and args.xchg_gloo
+    if gloo_staged:
+        local = 0
     if use_dist:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = "nccl" if torch.cuda.is_available() and not gloo_staged else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
     dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+    if args.workload == "c5":
+        run_replica_mode(args, ws, rank, local, dist, dev, gloo_staged)
+        if use_dist:
+            dist.destroy_process_group()
+        return
 
     from dragonboat_amd.engine import Engine, footprint, make_config
     from dragonboat_amd.shard import reduce_results, shard_params

@@ -17,6 +17,7 @@
 
 #include "../../include/rbe.h"
 #include "rbe_fast.h"
+#include "rbe_xchg.h"
 
 using namespace rbe;
 
@@ -86,7 +87,7 @@ __global__ __launch_bounds__(kBlock) void k_step(Planes P, Params C, const u32* 
   StepCounters c;
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
-  if (r < C.n_rep) step_replica<N, TRACE>(P, C, r, round, c);
+  if (r < C.n_rep && owned<N>(C, r)) step_replica<N, TRACE>(P, C, r, round, c);
   flush_counters<KS_FULL>(P, c);
 }
 
@@ -154,7 +155,7 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, const u32
   for (u32 i = 0; i < kPer; i++) {
     const u64 r = lo + (u64)i * kBlock;
     u32 cls = T_DONE;
-    if (r < C.n_rep) {
+    if (r < C.n_rep && owned<N>(C, r)) {
       if (shortcut && triage_lazy<N>(P, C, r, round, ibs[i], inb[i] & 1u, c))
         cls = T_DONE;
       else if (inb[i] & 2u)
@@ -212,7 +213,7 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_round(Planes P, Para
   for (u32 j = threadIdx.x; j < kTriChunk; j += kBlock) {
     const u64 r = lo + j;
     u32 cls = T_DONE;
-    if (r < C.n_rep) cls = triage_replica<N, TRACE>(P, C, r, round, c);
+    if (r < C.n_rep && owned<N>(C, r)) cls = triage_replica<N, TRACE>(P, C, r, round, c);
 #pragma unroll
     for (u32 li = 0; li < 2; li++) {
       const bool want = cls == li + 1;
@@ -299,6 +300,60 @@ __global__ __launch_bounds__(kBlock) void k_isolate(Planes P, Params C, u32 roun
 
 __global__ void k_advance(u32* round_ptr, u32 k) { *round_ptr += k; }
 
+// ---- replica-per-GPU exchange (rbe_xchg.h)
+struct XchgCaps {
+  u64 cap[XS_NUM];
+};
+// Pack: one lane per replica; each block reserves its records' slots with one
+// global atomic per (peer, stream) after an LDS reduction of its lanes' counts.
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_xchg_pack(Planes P, Params C, u32 par, u8* buf,
+                                                      XchgCaps caps, u32* gcount) {
+  __shared__ u32 s_cnt[kXchgMaxWorld * XS_NUM];
+  __shared__ u32 s_base[kXchgMaxWorld * XS_NUM];
+  const u32 nc = C.rep_world * XS_NUM;
+  for (u32 i = threadIdx.x; i < nc; i += kBlock) s_cnt[i] = 0;
+  __syncthreads();
+  const u64 r = (u64)blockIdx.x * kBlock + threadIdx.x;
+  const bool mine = r < C.n_rep && owned<N>(C, r);
+  u32 cnt[kXchgMaxWorld * XS_NUM];
+  u32 base[kXchgMaxWorld * XS_NUM];
+  for (u32 i = 0; i < nc; i++) cnt[i] = 0;
+  if (mine) xchg_sender<N, false>(P, C, r, par, cnt, nullptr, nullptr, caps.cap);
+  for (u32 i = 0; i < nc; i++) base[i] = cnt[i] ? atomicAdd(&s_cnt[i], cnt[i]) : 0u;
+  __syncthreads();
+  for (u32 i = threadIdx.x; i < nc; i += kBlock)
+    s_base[i] = s_cnt[i] ? atomicAdd(&gcount[i], s_cnt[i]) : 0u;
+  __syncthreads();
+  if (mine) {
+    for (u32 i = 0; i < nc; i++) {
+      base[i] += s_base[i];
+      cnt[i] = 0;
+    }
+    xchg_sender<N, true>(P, C, r, par, cnt, base, buf, caps.cap);
+  }
+}
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_xchg_clear(Planes P, Params C, u32 par) {
+  const u64 r = (u64)blockIdx.x * kBlock + threadIdx.x;
+  if (r < C.n_rep && owned<N>(C, r)) xchg_clear<N>(P, C, r, par);
+}
+__global__ __launch_bounds__(kBlock) void k_xchg_put_cnt(Planes P, Params C, u32 par,
+                                                         const XCnt* x, u64 n) {
+  const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) xchg_put_cnt(P, C, par, x[i]);
+}
+__global__ __launch_bounds__(kBlock) void k_xchg_put_msg(Planes P, Params C, u32 par,
+                                                         const XMsg* x, u64 n) {
+  const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) xchg_put_msg(P, C, par, x[i]);
+}
+__global__ __launch_bounds__(kBlock) void k_xchg_put_ent(Planes P, Params C, u32 par,
+                                                         const XEnt* x, u64 n) {
+  const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) xchg_put_ent(P, C, par, x[i]);
+}
+
 // ------------------------------------------------------------------ engine
 struct rbe_engine {
   rbe_config cfg;
@@ -314,6 +369,7 @@ struct rbe_engine {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   int mode = 1;              // RBE_MODE: 0 fused, 1 split (default: triage + 2 fast lists), 2 full
   Lists L;                   // per-round work lists (triage → fast → full)
+  u32* xcount = nullptr;     // replica-per-GPU pack counters [rep_world * XS_NUM]
 };
 
 static constexpr unsigned kFastGrid = 2048;  // persistent grid of k_fast_list
@@ -389,6 +445,12 @@ static int make_params(const rbe_config* cfg, Params* out) {
   C.iso_period = cfg->iso_period;
   C.iso_len = cfg->iso_len;
   C.iso_mod = cfg->iso_mod;
+  C.rep_world = cfg->rep_world > 1 ? cfg->rep_world : 1;
+  C.rep_rank = cfg->rep_rank;
+  if (C.rep_world > kXchgMaxWorld || C.rep_rank >= C.rep_world) return RBE_E_INVALID;
+  // replica-per-GPU mode: the fault schedule needs every replica's role and
+  // host-pushed inputs are per replica; both stay group-per-GPU features
+  if (C.rep_world > 1 && (C.iso_period || C.ext_inputs)) return RBE_E_INVALID;
   *out = C;
   return RBE_OK;
 }
@@ -599,6 +661,11 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   }
   e->allocs.push_back(e->L.idx);
   e->allocs.push_back(e->L.counts);
+  if (hipMalloc(&e->xcount, kXchgMaxWorld * XS_NUM * sizeof(u32)) != hipSuccess) {
+    rbe_destroy(e);
+    return RBE_E_NOMEM;
+  }
+  e->allocs.push_back(e->xcount);
   HIP_IGNORE(hipMemsetAsync(e->L.counts, 0, 6 * sizeof(u32), e->stream));
   rc = dispatch_n(C.n, [&](auto NN) {
     constexpr int N = decltype(NN)::value;
@@ -785,6 +852,63 @@ int rbe_debug_phases(uint64_t* out16) {
   return RBE_OK;
 }
 #endif
+
+int rbe_xchg_record_bytes(uint64_t* out3) {
+  if (!out3) return RBE_E_INVALID;
+  for (u32 t = 0; t < XS_NUM; t++) out3[t] = kXRecBytes[t];
+  return RBE_OK;
+}
+
+int rbe_xchg_pack(rbe_engine* e, void* buf, const uint64_t* cap3, uint32_t* counts) {
+  if (!e || !buf || !cap3 || !counts || e->round == 0) return RBE_E_INVALID;
+  if (e->C.rep_world <= 1) return RBE_E_STATE;
+  HIP_OK(hipSetDevice(e->device));
+  XchgCaps caps;
+  for (u32 t = 0; t < XS_NUM; t++) caps.cap[t] = cap3[t];
+  const u32 par = (e->round - 1) & 1u, nc = e->C.rep_world * XS_NUM;
+  HIP_OK(hipMemsetAsync(e->xcount, 0, nc * sizeof(u32), e->stream));
+  int rc = dispatch_n(e->C.n, [&](auto NN) {
+    constexpr int N = decltype(NN)::value;
+    hipLaunchKernelGGL(k_xchg_pack<N>, dim3(grid_for(e->C.n_rep)), dim3(kBlock), 0, e->stream,
+                       e->P, e->C, par, (u8*)buf, caps, e->xcount);
+    HIP_OK(hipGetLastError());
+    return RBE_OK;
+  });
+  if (rc) return rc;
+  HIP_OK(hipMemcpyAsync(counts, e->xcount, nc * sizeof(u32), hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  for (u32 i = 0; i < nc; i++)
+    if (counts[i] > cap3[i % XS_NUM]) return RBE_E_NOMEM;  // a region overflowed
+  return RBE_OK;
+}
+
+int rbe_xchg_unpack(rbe_engine* e, const void* cnt, uint64_t n_cnt, const void* msg, uint64_t n_msg,
+                    const void* ent, uint64_t n_ent) {
+  if (!e || e->round == 0) return RBE_E_INVALID;
+  if (e->C.rep_world <= 1) return RBE_E_STATE;
+  HIP_OK(hipSetDevice(e->device));
+  const u32 par = (e->round - 1) & 1u;
+  int rc = dispatch_n(e->C.n, [&](auto NN) {
+    constexpr int N = decltype(NN)::value;
+    hipLaunchKernelGGL(k_xchg_clear<N>, dim3(grid_for(e->C.n_rep)), dim3(kBlock), 0, e->stream,
+                       e->P, e->C, par);
+    HIP_OK(hipGetLastError());
+    return RBE_OK;
+  });
+  if (rc) return rc;
+  if (n_cnt)
+    hipLaunchKernelGGL(k_xchg_put_cnt, dim3(grid_for(n_cnt)), dim3(kBlock), 0, e->stream, e->P,
+                       e->C, par, (const XCnt*)cnt, n_cnt);
+  if (n_msg)
+    hipLaunchKernelGGL(k_xchg_put_msg, dim3(grid_for(n_msg)), dim3(kBlock), 0, e->stream, e->P,
+                       e->C, par, (const XMsg*)msg, n_msg);
+  if (n_ent)
+    hipLaunchKernelGGL(k_xchg_put_ent, dim3(grid_for(n_ent)), dim3(kBlock), 0, e->stream, e->P,
+                       e->C, par, (const XEnt*)ent, n_ent);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return RBE_OK;
+}
 
 int rbe_kernel_name(const rbe_engine* e, int32_t kernel, char* buf, uint32_t cap) {
   if (!e || !buf || cap == 0 || kernel < 0 || kernel >= KS_NUM) return RBE_E_INVALID;

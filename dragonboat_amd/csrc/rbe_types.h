@@ -197,6 +197,8 @@ struct Params {
   u32 ext_inputs;     // consume host-pushed ExtIn records
   // faults
   u32 iso_period, iso_len, iso_mod;
+  u32 rep_world;      // replica-per-GPU mode when > 1 (rbe_xchg.h)
+  u32 rep_rank;
   u32 pad;
 };
 

@@ -40,7 +40,8 @@ class RbeConfig(C.Structure):
                 ("wl_active_mod", C.c_uint32), ("wl_read_permille", C.c_uint32),
                 ("ext_inputs", C.c_uint32), ("iso_period", C.c_uint32),
                 ("iso_len", C.c_uint32), ("iso_mod", C.c_uint32),
-                ("reserved", C.c_uint32 * 7)]
+                ("rep_world", C.c_uint32), ("rep_rank", C.c_uint32),
+                ("reserved", C.c_uint32 * 5)]
 
 
 class RbeReplicaView(C.Structure):
@@ -89,10 +90,14 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_step", "rbe_run"
            "rbe_round", "rbe_run_timed", "rbe_push_proposals", "rbe_push_read_index",
            "rbe_get_updates", "rbe_get_messages", "rbe_get_ready_to_reads", "rbe_get_entries",
            "rbe_get_views", "rbe_get_counters", "rbe_reset_counters", "rbe_fault_summary",
-           "rbe_footprint", "rbe_profile_rounds", "rbe_get_kernel_counters", "rbe_kernel_name"]
+           "rbe_footprint", "rbe_profile_rounds", "rbe_get_kernel_counters", "rbe_kernel_name",
+           "rbe_xchg_record_bytes", "rbe_xchg_pack", "rbe_xchg_unpack"]
 KERNEL_SLOTS = 4
 
 _lib = None
+
+
+RBE_E_NOMEM = -3
 
 
 class EngineError(RuntimeError):
@@ -136,6 +141,9 @@ def load_library(path: Optional[str] = None):
         "rbe_profile_rounds": (i32, [vp, u32, P(C.c_float)]),
         "rbe_get_kernel_counters": (i32, [vp, C.c_int32, P(u64)]),
         "rbe_kernel_name": (i32, [vp, C.c_int32, C.c_char_p, u32]),
+        "rbe_xchg_record_bytes": (i32, [P(u64)]),
+        "rbe_xchg_pack": (i32, [vp, vp, P(u64), P(u32)]),
+        "rbe_xchg_unpack": (i32, [vp, vp, u64, vp, u64, vp, u64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -155,7 +163,8 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                 seed: int = 0x5EEDD8A6, max_entry_size: int = 0, wl_enabled: bool = False,
                 wl_start_round: int = 0, wl_stop_round: int = 0, wl_active_mod: int = 1,
                 wl_read_permille: int = 0, ext_inputs: bool = False, iso_period: int = 0,
-                iso_len: int = 0, iso_mod: int = 10) -> RbeConfig:
+                iso_len: int = 0, iso_mod: int = 10, rep_world: int = 0,
+                rep_rank: int = 0) -> RbeConfig:
     return RbeConfig(abi_version=RBE_ABI_VERSION, device=device, n_groups=n_groups,
                      n_replicas=n_replicas, election_rtt=election_rtt,
                      heartbeat_rtt=heartbeat_rtt, check_quorum=int(check_quorum),
@@ -165,7 +174,8 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                      wl_enabled=int(wl_enabled), wl_start_round=wl_start_round,
                      wl_stop_round=wl_stop_round, wl_active_mod=wl_active_mod,
                      wl_read_permille=wl_read_permille, ext_inputs=int(ext_inputs),
-                     iso_period=iso_period, iso_len=iso_len, iso_mod=iso_mod)
+                     iso_period=iso_period, iso_len=iso_len, iso_mod=iso_mod,
+                     rep_world=rep_world, rep_rank=rep_rank)
 
 
 def _check(rc: int, what: str):
@@ -268,6 +278,30 @@ class Engine:
         _check(self.lib.rbe_profile_rounds(self.h, rounds, ms), "rbe_profile_rounds")
         return list(ms)
 
+    # replica-per-GPU exchange (dragonboat_amd/replica.py drives these)
+    def xchg_pack(self, buf_ptr: int, caps):
+        """Pack the last round's cross-rank records into the device buffer at
+        `buf_ptr`; returns (fits, counts[peer * 3 + stream]).  When a region
+        overflowed (fits False) the counts are still exact: grow and re-pack."""
+        world = max(1, self.cfg.rep_world)
+        cap = (C.c_uint64 * 3)(*caps)
+        out = (C.c_uint32 * (3 * world))()
+        rc = self.lib.rbe_xchg_pack(self.h, C.c_void_p(buf_ptr), cap, out)
+        if rc not in (0, RBE_E_NOMEM):
+            _check(rc, "rbe_xchg_pack")
+        return rc == 0, list(out)
+
+    def xchg_unpack(self, cnt_ptr: int, n_cnt: int, msg_ptr: int, n_msg: int, ent_ptr: int,
+                    n_ent: int):
+        _check(self.lib.rbe_xchg_unpack(self.h, C.c_void_p(cnt_ptr), n_cnt, C.c_void_p(msg_ptr),
+                                        n_msg, C.c_void_p(ent_ptr), n_ent), "rbe_xchg_unpack")
+
+    def owned(self, replica: int) -> bool:
+        """Replica-per-GPU ownership: replica k of group g lives on rank (g + k) % world."""
+        w = max(1, self.cfg.rep_world)
+        return w == 1 or (replica // self.n_replicas + replica % self.n_replicas) % w == \
+            self.cfg.rep_rank
+
     def reset_counters(self):
         _check(self.lib.rbe_reset_counters(self.h), "rbe_reset_counters")
 
@@ -313,6 +347,12 @@ class Engine:
         o = C.c_uint32()
         _check(self.lib.rbe_fault_summary(self.h, C.byref(n), C.byref(o)), "rbe_fault_summary")
         return n.value, o.value
+
+
+def xchg_record_bytes() -> List[int]:
+    o = (C.c_uint64 * 3)()
+    _check(load_library().rbe_xchg_record_bytes(o), "rbe_xchg_record_bytes")
+    return list(o)
 
 
 def footprint(cfg: RbeConfig) -> int:

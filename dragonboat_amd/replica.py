@@ -1,0 +1,154 @@
+"""Replica-per-GPU mode: the host side of the
+cross-rank message exchange.
+
+With `rep_world = W > 1`, replica k of group g is stepped on rank (g + k) % W,
+so the messages a Raft round produces between replicas of one group cross
+ranks.  In dragonboat they would leave through the transport
+(node.go:888-905 `sendMessages` → nodehost.go:1724 `sendMessage` →
+transport.go:392-557); here one round's cross-rank traffic moves as one
+all-to-all after the round:
+
+  1. `rbe_xchg_pack` (device): every owned sender packs the count words,
+     messages and Replicate entries it produced for replicas owned elsewhere
+     into fixed-size records, bucketed per destination rank and stream;
+  2. the per-(peer, stream) record counts go out with one small all-to-all;
+  3. the records go out with one `all_to_all_single` (RCCL over xGMI with the
+     nccl backend; gloo in the CPU tests and the one-GPU two-process test,
+     staged through host memory);
+  4. `rbe_xchg_unpack` (device): clears the remote senders' count words of the
+     round and scatters the received records into the same plane positions.
+
+Records name their destination slot, so order within a stream is free and
+the round that follows is bit-identical to a single-rank run of all replicas
+(tests/test_replica_gloo.py, tests/test_gpu_parity.py).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+from .engine import xchg_record_bytes
+
+STREAMS = 3  # count words, messages, entries
+
+
+def initial_caps(n_rep: int, n: int, world: int) -> List[int]:
+    """Per-(peer, stream) record capacities to start with.  The count stream
+    is bounded by the lists from owned senders to one peer; messages and
+    entries start at one per list and grow on demand (ReplicaExchange.grow)."""
+    lists = -(-n_rep * max(n - 1, 1) // world) + 64
+    return [lists, lists, lists // 2 + 64]
+
+
+class ReplicaExchange:
+    """Drives the exchange of one engine (the HIP `Engine`, or the host build
+    used by the CPU tests — anything with `xchg_pack`/`xchg_unpack`).
+
+    `buf_device` is where the pack buffer lives (the engine's GPU, or "cpu"
+    for the host build); `comm_device` is where the collectives run ("cuda:i"
+    for RCCL, "cpu" for gloo).  When they differ, records are staged through
+    the comm device."""
+
+    def __init__(self, engine, group=None, buf_device="cpu", comm_device="cpu",
+                 caps: Optional[Sequence[int]] = None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.eng = engine
+        self.group = group
+        self.world = int(engine.cfg.rep_world)
+        self.rank = int(engine.cfg.rep_rank)
+        if self.world < 2:
+            raise ValueError("replica exchange needs rep_world >= 2")
+        if dist.get_world_size(group) != self.world or dist.get_rank(group) != self.rank:
+            raise ValueError(f"process group (rank {dist.get_rank(group)} of "
+                             f"{dist.get_world_size(group)}) does not match the engine's "
+                             f"rep_rank {self.rank} of rep_world {self.world}")
+        self.rec = xchg_record_bytes()
+        n = int(engine.cfg.n_replicas)
+        self.caps = list(caps) if caps else initial_caps(int(engine.cfg.n_groups) * n, n,
+                                                         self.world)
+        self.buf_device = torch.device(buf_device)
+        self.comm_device = torch.device(comm_device)
+        self.bytes_sent = 0
+        self.records_sent = [0] * STREAMS
+        self._alloc()
+
+    # --- layout: per peer p, streams t = 0..2, cap[t] records each (rbe_xchg.h xchg_region)
+    def _per_peer(self) -> int:
+        return sum(c * b for c, b in zip(self.caps, self.rec))
+
+    def _region(self, p: int, t: int) -> int:
+        return p * self._per_peer() + sum(self.caps[i] * self.rec[i] for i in range(t))
+
+    def _alloc(self):
+        self.buf = self.torch.empty(self.world * self._per_peer(), dtype=self.torch.uint8,
+                                    device=self.buf_device)
+
+    def grow(self, counts: Sequence[int]):
+        need = [max(counts[p * STREAMS + t] for p in range(self.world)) for t in range(STREAMS)]
+        self.caps = [max(c, n + n // 4 + 64) for c, n in zip(self.caps, need)]
+        self._alloc()
+
+    def exchange(self):
+        """Move the last round's cross-rank records (call after every round)."""
+        torch, dist = self.torch, self.dist
+        fits, counts = self.eng.xchg_pack(self.buf.data_ptr(), self.caps)
+        if not fits:
+            self.grow(counts)
+            fits, counts = self.eng.xchg_pack(self.buf.data_ptr(), self.caps)
+            if not fits:
+                raise RuntimeError("replica exchange: pack overflow after growing")
+        W, S = self.world, STREAMS
+        send_cnt = torch.tensor(counts, dtype=torch.int64, device=self.comm_device)
+        recv_cnt = torch.empty_like(send_cnt)
+        dist.all_to_all_single(recv_cnt, send_cnt, group=self.group)
+        rc = recv_cnt.tolist()
+        # compact the populated prefix of every (peer, stream) region
+        parts, out_split = [], []
+        for p in range(W):
+            nbytes = 0
+            for t in range(S):
+                b = counts[p * S + t] * self.rec[t]
+                if b:
+                    o = self._region(p, t)
+                    parts.append(self.buf[o:o + b])
+                    nbytes += b
+            out_split.append(nbytes)
+        send = torch.cat(parts) if parts else torch.empty(0, dtype=torch.uint8,
+                                                          device=self.buf_device)
+        if send.device != self.comm_device:
+            send = send.to(self.comm_device)
+        in_split = [sum(rc[p * S + t] * self.rec[t] for t in range(S)) for p in range(W)]
+        recv = torch.empty(sum(in_split), dtype=torch.uint8, device=self.comm_device)
+        dist.all_to_all_single(recv, send, output_split_sizes=in_split,
+                               input_split_sizes=out_split, group=self.group)
+        self.bytes_sent += sum(out_split)
+        for t in range(S):
+            self.records_sent[t] += sum(counts[p * S + t] for p in range(W))
+        # per stream: the records of every source rank, back to back
+        streams: List[List] = [[] for _ in range(S)]
+        at = 0
+        for p in range(W):
+            for t in range(S):
+                b = rc[p * S + t] * self.rec[t]
+                if b:
+                    streams[t].append(recv[at:at + b])
+                at += b
+        cat = []
+        for t in range(S):
+            x = torch.cat(streams[t]) if streams[t] else torch.empty(0, dtype=torch.uint8,
+                                                                     device=self.comm_device)
+            if x.device != self.buf_device:
+                x = x.to(self.buf_device)
+            cat.append(x)
+        if self.buf_device.type == "cuda":
+            torch.cuda.current_stream(self.buf_device).synchronize()
+        n = [cat[t].numel() // self.rec[t] for t in range(S)]
+        self.eng.xchg_unpack(cat[0].data_ptr(), n[0], cat[1].data_ptr(), n[1],
+                             cat[2].data_ptr(), n[2])
+
+    def run(self, rounds: int):
+        """`rounds` lockstep rounds of the owned replicas, exchanging after each."""
+        for _ in range(rounds):
+            self.eng.step()
+            self.exchange()

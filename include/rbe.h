@@ -116,7 +116,12 @@ typedef struct rbe_config {
   uint32_t iso_period;
   uint32_t iso_len;
   uint32_t iso_mod;
-  uint32_t reserved[7];
+  /* replica-per-GPU mode: rep_world > 1 engines each step the
+   * replicas k of groups g with (g + k) % rep_world == rep_rank and exchange
+   * cross-GPU messages between rounds (rbe_xchg_*); 0/1 = off */
+  uint32_t rep_world;
+  uint32_t rep_rank;
+  uint32_t reserved[5];
 } rbe_config;
 
 /* Snapshot of one replica (tests, debugging, rbe_get_views). */
@@ -225,6 +230,23 @@ int rbe_get_kernel_counters(rbe_engine* e, int32_t kernel, uint64_t* out /* RBE_
 int rbe_reset_counters(rbe_engine* e);
 /* number of replicas whose sticky fault word is non-zero, and the OR of all */
 int rbe_fault_summary(rbe_engine* e, uint64_t* n_faulty, uint32_t* fault_or);
+
+/* Replica-per-GPU mode (cfg.rep_world > 1).  The engine steps
+ * only its own replicas; between rounds the host moves the messages of the
+ * last round across ranks (the north star's RCCL all-to-all over xGMI):
+ *   rbe_xchg_pack: packs the last round's records for every peer into the
+ *     device buffer `buf`, laid out per peer p as stream 0 (count words),
+ *     stream 1 (messages), stream 2 (Replicate entries) with cap3[t] records
+ *     per stream; counts[p * 3 + t] receives the record counts
+ *     (RBE_E_NOMEM if a capacity was exceeded);
+ *   rbe_xchg_unpack: clears the engine's remote-sender count words of that
+ *     round and scatters the received records (device pointers).
+ * Record sizes come from rbe_xchg_record_bytes.  Replaces, for replicas on
+ * other GPUs, the transport hop of node.go:888-905 → nodehost.go:1724. */
+int rbe_xchg_record_bytes(uint64_t* out3);
+int rbe_xchg_pack(rbe_engine* e, void* buf, const uint64_t* cap3, uint32_t* counts);
+int rbe_xchg_unpack(rbe_engine* e, const void* cnt_recs, uint64_t n_cnt, const void* msg_recs,
+                    uint64_t n_msg, const void* ent_recs, uint64_t n_ent);
 
 /* Device memory footprint (bytes) of a configuration, without allocating. */
 int rbe_footprint(const rbe_config* cfg, uint64_t* bytes);

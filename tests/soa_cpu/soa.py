@@ -29,6 +29,11 @@ def lib():
         L.soa_slow_total.argtypes = [C.c_void_p]
         L.soa_faults.restype = C.c_uint32
         L.soa_faults.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+        L.soa_xchg_pack.restype = C.c_int
+        L.soa_xchg_pack.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64),
+                                    C.POINTER(C.c_uint32)]
+        L.soa_xchg_unpack.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+                                      C.c_uint64, C.c_void_p, C.c_uint64]
         _lib = L
     return _lib
 
@@ -52,6 +57,21 @@ class SoaCpu:
 
     def run(self, rounds=1):
         lib().soa_run(self.h, rounds)
+
+    def step(self):
+        lib().soa_run(self.h, 1)
+
+    # replica-per-GPU exchange, same contract as Engine.xchg_pack / xchg_unpack
+    def xchg_pack(self, buf_ptr, caps):
+        world = max(1, self.cfg.rep_world)
+        cap = (C.c_uint64 * 3)(*caps)
+        out = (C.c_uint32 * (3 * world))()
+        rc = lib().soa_xchg_pack(self.h, C.c_void_p(buf_ptr), cap, out)
+        return rc == 0, list(out)
+
+    def xchg_unpack(self, cnt_ptr, n_cnt, msg_ptr, n_msg, ent_ptr, n_ent):
+        lib().soa_xchg_unpack(self.h, C.c_void_p(cnt_ptr), n_cnt, C.c_void_p(msg_ptr), n_msg,
+                              C.c_void_p(ent_ptr), n_ent)
 
     def views(self):
         arr = (RbeReplicaView * self.n_rep)()

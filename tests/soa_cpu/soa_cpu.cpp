@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../dragonboat_amd/csrc/rbe_fast.h"
+#include "../../dragonboat_amd/csrc/rbe_xchg.h"
 #include "../../include/rbe.h"
 
 using namespace rbe;
@@ -38,6 +39,7 @@ static void run_round(SoaEngine* e) {
   StepCounters c;
   std::vector<u64> lists[3];
   for (u64 r = 0; r < e->C.n_rep; r++) {
+    if (!owned<N>(e->C, r)) continue;
     memset(&c, 0, sizeof(c));
     u32 cls = T_FULL;
     if (!e->full_only) {
@@ -112,6 +114,8 @@ void* soa_create(const rbe_config* cfg) {
   C.iso_period = cfg->iso_period;
   C.iso_len = cfg->iso_len;
   C.iso_mod = cfg->iso_mod;
+  C.rep_world = cfg->rep_world > 1 ? cfg->rep_world : 1;
+  C.rep_rank = cfg->rep_rank;
   if (C.n != 1 && C.n != 3 && C.n != 5) {
     delete e;
     return nullptr;
@@ -216,3 +220,49 @@ uint32_t soa_faults(void* h, uint64_t* n_faulty) {
 }
 
 }  // extern "C"
+
+// replica-per-GPU exchange on the host build (same record format and the same
+// rbe_xchg.h functions as the device kernels)
+template <int N>
+static int soa_xchg_pack_t(SoaEngine* e, uint8_t* buf, const uint64_t* cap, uint32_t* counts) {
+  const u32 par = (e->round - 1) & 1u, nc = e->C.rep_world * XS_NUM;
+  for (u32 i = 0; i < nc; i++) counts[i] = 0;
+  std::vector<u32> cnt(nc), base(nc);
+  for (u64 r = 0; r < e->C.n_rep; r++) {
+    if (!owned<N>(e->C, r)) continue;
+    for (u32 i = 0; i < nc; i++) cnt[i] = 0;
+    xchg_sender<N, false>(e->P, e->C, r, par, cnt.data(), nullptr, nullptr, cap);
+    for (u32 i = 0; i < nc; i++) {
+      base[i] = counts[i];
+      counts[i] += cnt[i];
+      cnt[i] = 0;
+    }
+    xchg_sender<N, true>(e->P, e->C, r, par, cnt.data(), base.data(), buf, cap);
+  }
+  for (u32 i = 0; i < nc; i++)
+    if (counts[i] > cap[i % XS_NUM]) return -3;
+  return 0;
+}
+template <int N>
+static void soa_xchg_unpack_t(SoaEngine* e, const XCnt* c, uint64_t nc, const XMsg* m, uint64_t nm,
+                              const XEnt* x, uint64_t ne) {
+  const u32 par = (e->round - 1) & 1u;
+  for (u64 r = 0; r < e->C.n_rep; r++)
+    if (owned<N>(e->C, r)) xchg_clear<N>(e->P, e->C, r, par);
+  for (u64 i = 0; i < nc; i++) xchg_put_cnt(e->P, e->C, par, c[i]);
+  for (u64 i = 0; i < nm; i++) xchg_put_msg(e->P, e->C, par, m[i]);
+  for (u64 i = 0; i < ne; i++) xchg_put_ent(e->P, e->C, par, x[i]);
+}
+extern "C" int soa_xchg_pack(void* h, uint8_t* buf, const uint64_t* cap, uint32_t* counts) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (e->C.n == 3) return soa_xchg_pack_t<3>(e, buf, cap, counts);
+  if (e->C.n == 5) return soa_xchg_pack_t<5>(e, buf, cap, counts);
+  return soa_xchg_pack_t<1>(e, buf, cap, counts);
+}
+extern "C" void soa_xchg_unpack(void* h, const void* c, uint64_t nc, const void* m, uint64_t nm,
+                                const void* x, uint64_t ne) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (e->C.n == 3) soa_xchg_unpack_t<3>(e, (const XCnt*)c, nc, (const XMsg*)m, nm, (const XEnt*)x, ne);
+  else if (e->C.n == 5) soa_xchg_unpack_t<5>(e, (const XCnt*)c, nc, (const XMsg*)m, nm, (const XEnt*)x, ne);
+  else soa_xchg_unpack_t<1>(e, (const XCnt*)c, nc, (const XMsg*)m, nm, (const XEnt*)x, ne);
+}

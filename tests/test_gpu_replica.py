@@ -1,0 +1,19 @@
+"""Replica-per-GPU mode (C5) through the HIP engine: W processes share
+cuda:0, each stepping only the replicas it owns with libdragonboat_amd.so
+(rbe_step + rbe_xchg_pack/unpack), exchanging records over gloo staged
+through host memory.  Bar: every owned replica equals the oracle stepping
+all replicas in one process (test_replica_gloo.run_case)."""
+import pytest
+
+from test_replica_gloo import run_case
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", ["C2_w2", "C4_w3", "N5_w4"])
+def test_gpu_replica_per_rank_matches_oracle(gpu_available, name):
+    run_case(name, gpu=True)
+
+
+def test_gpu_replica_per_rank_untraced(gpu_available):
+    run_case("C4_w3", gpu=True, trace=False)

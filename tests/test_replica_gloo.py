@@ -1,0 +1,128 @@
+"""Replica-per-GPU mode (C5) on CPU: W processes (gloo), each stepping the
+replicas it owns with the host build of the device step (tests/soa_cpu) and
+moving cross-rank messages with dragonboat_amd.replica.ReplicaExchange — the
+same record format, pack/clear/scatter functions (rbe_xchg.h) and collective
+sequence the GPU path uses.  Every owned replica must equal, field by field
+and round by round at the checkpoints, the oracle harness stepping all
+replicas in one process; the counters summed over ranks must equal the
+oracle's."""
+import os
+import socket
+import sys
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+CASES = {
+    # steady replication, 3 replicas over 2 ranks (two replicas share a rank)
+    "C2_w2": (dict(n_groups=24, n_replicas=3, wl_enabled=True, wl_start_round=30), 2, 200, {}),
+    # quiesce + 9:1 reads, every replica of a group on its own rank
+    "C4_w3": (dict(n_groups=30, n_replicas=3, quiesce=True, wl_enabled=True, wl_start_round=30,
+                   wl_active_mod=2, wl_read_permille=900), 3, 300, {}),
+    # 5 replicas, check-quorum, elections from scratch, over 4 ranks
+    "N5_w4": (dict(n_groups=16, n_replicas=5, check_quorum=True, quiesce=True, wl_enabled=True,
+                   wl_start_round=25, wl_active_mod=2, wl_read_permille=500, seed=777), 4, 300,
+              dict(ring=128, rq_cap=64, maxm=24)),
+}
+CHECK_EVERY = 50
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, name, gpu, trace, q):
+    sys.path.insert(0, HERE)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from parity_util import FIELDS
+        from dragonboat_amd.replica import ReplicaExchange
+        kw, _, rounds, extra = CASES[name]
+        if gpu:  # the HIP engine, records staged through host memory for gloo
+            from dragonboat_amd.engine import Engine
+            eng = Engine(device=0, trace=trace, rep_world=world, rep_rank=rank, **kw, **extra)
+            xch = ReplicaExchange(eng, buf_device="cuda:0", comm_device="cpu", caps=[8, 8, 8])
+        else:
+            from soa_cpu.soa import SoaCpu
+            eng = SoaCpu(trace=trace, rep_world=world, rep_rank=rank, **kw, **extra)
+            xch = ReplicaExchange(eng, caps=[8, 8, 8])  # tiny caps: exercises grow()
+        snaps = []
+        for done in range(CHECK_EVERY, rounds + 1, CHECK_EVERY):
+            xch.run(CHECK_EVERY)
+            vs = eng.views()
+            n = kw["n_replicas"]
+            own = {i: tuple(tuple(getattr(vs[i], f)) if hasattr(getattr(vs[i], f), "__len__")
+                            else getattr(vs[i], f) for f in FIELDS)
+                   for i in range(len(vs)) if (i // n + i % n) % world == rank}
+            snaps.append((done, own))
+        nf = eng.fault_summary()[0] if gpu else eng.faults()[0]
+        q.put((rank, snaps, eng.counters(), nf, xch.records_sent))
+    except Exception as ex:  # surface worker failures in the parent
+        q.put((rank, repr(ex), None, None, None))
+        raise
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run_case(name, gpu=False, trace=True):
+    import oracle as O
+    from parity_util import FIELDS
+    kw, world, rounds, _ = CASES[name]
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, gpu, trace, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for rank, snaps, _, _, _ in res:
+        assert not isinstance(snaps, str), f"rank {rank}: {snaps}"
+    assert all(p.exitcode == 0 for p in procs)
+
+    ref = O.Harness(**kw)
+    n_rep = kw["n_groups"] * kw["n_replicas"]
+    covered = set()
+    for k, done in enumerate(range(CHECK_EVERY, rounds + 1, CHECK_EVERY)):
+        ref.run(CHECK_EVERY)
+        hv = ref.views()
+        for rank, snaps, _, _, _ in res:
+            assert snaps[k][0] == done
+            for i, got in snaps[k][1].items():
+                covered.add(i)
+                want = tuple(tuple(getattr(hv[i], f)) if hasattr(getattr(hv[i], f), "__len__")
+                             else getattr(hv[i], f) for f in FIELDS)
+                bad = [(f, a, b) for f, a, b in zip(FIELDS, got, want)
+                       if a != b and (trace or f != "digest")]
+                if bad:
+                    pytest.fail(f"{name}: round {done} replica {i} (rank {rank}) differs: "
+                                f"{bad[:3]}")
+    assert covered == set(range(n_rep))
+    hc = ref.counters()
+    for key, v in hc.items():
+        assert sum(r[2][key] for r in res) == v, key
+    assert all(r[3] == 0 for r in res), "faults"
+    # cross-rank traffic actually flowed: count words, messages and entries
+    sent = [sum(r[4][t] for r in res) for t in range(3)]
+    assert all(s > 0 for s in sent), sent
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_replica_per_rank_matches_oracle(name):
+    run_case(name)
+
+
+def test_replica_per_rank_untraced():
+    """Without trace (the bench paths: lazy quiesced ticks, no digest)."""
+    run_case("C4_w3", trace=False)
