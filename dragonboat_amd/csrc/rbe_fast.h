@@ -43,7 +43,15 @@ __device__ __forceinline__ unsigned long long rbe_stamp() {
   __builtin_amdgcn_sched_barrier(0);
   return t;
 }
+__device__ __forceinline__ unsigned long long rbe_rstamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
 #define RBE_STAMP(var) const unsigned long long var = rbe_stamp()
+#define RBE_RSTAMP(var) const unsigned long long var = rbe_rstamp()
 #define RBE_PHASE_ADD(role, i, a, b)                                                   \
   do {                                                                                 \
     if ((threadIdx.x & 63) == (u32)(__ffsll((unsigned long long)__ballot(1)) - 1))     \
@@ -51,6 +59,7 @@ __device__ __forceinline__ unsigned long long rbe_stamp() {
   } while (0)
 #else
 #define RBE_STAMP(var)
+#define RBE_RSTAMP(var)
 #define RBE_PHASE_ADD(role, i, a, b)
 #endif
 
@@ -120,6 +129,12 @@ struct FastOut {
   u32 fault, n_msgs, n_rtr, n_drop_ri;
   u64 msg_hash, rtr_hash, drop_hash;
   u64 term;
+  // event counts added to the lane's counters once, in fast_finish: every
+  // increment here is unconditional (a 0/1 value), because two branches
+  // that bump different counters get merged into one dynamically indexed
+  // bump, which puts the counter array in scratch memory — and a scratch
+  // reload after the lane's first store waits for every store before it
+  u32 fault0, n_out, n_drop_msg, n_ent_out;
 
   RBE_HD u32 get_pc(u32 d) const {
     return d < 4 ? (u32)((pc >> (16 * d)) & 0xFFFFu) : (u32)((pc_hi >> (16 * (d - 4))) & 0xFFFFu);
@@ -129,7 +144,7 @@ struct FastOut {
     else pc_hi += (u64)v << (16 * (d - 4));
   }
   RBE_HD void set_fault(StepCounters& ctr, u32 f) {
-    if (!(fault & f)) ctr.v[C_FAULTS]++;
+    (void)ctr;  // counted in fast_finish (new bits of the sticky word)
     fault |= f;
   }
   // `ent` points at the message's entries in this round's arena (may be null
@@ -164,16 +179,16 @@ struct FastOut {
     }
     if (m.to < 1 || m.to > N) return;
     const u32 d = m.to - 1u;
-    if (((iso >> k) & 1u) || ((iso >> d) & 1u)) {
-      ctr.v[C_MSG_DROPPED]++;
-      return;
-    }
+    const u32 drop = ((iso >> k) & 1u) | ((iso >> d) & 1u);
     const u32 c = get_pc(d);
     const u32 a = c & 0x7Fu, b = (c >> 7) & 0x7Fu;
-    if (a + b >= C.maxm) {
-      set_fault(ctr, F_OUTBOX);
-      return;
-    }
+    const u32 full = drop ? 0u : (a + b >= C.maxm ? 1u : 0u);
+    if (full) fault |= F_OUTBOX;
+    const u32 ok = 1u - drop - full;
+    n_drop_msg += drop;
+    n_out += ok;
+    n_ent_out += ok ? (u32)m.n_ent : 0u;
+    if (!ok) return;
     u32 slot;
     if (m.type == M_Replicate) {
       slot = a;
@@ -185,8 +200,6 @@ struct FastOut {
 #ifndef RBE_DIAG_NO_MSG_STORES
     P.msgs[par][((g * N + k) * N + d) * (u64)C.maxm + slot] = m;
 #endif
-    ctr.v[C_MSG_OUT]++;
-    ctr.v[C_ENT_OUT] += m.n_ent;
   }
   RBE_HD void dropped_read_index(const Planes& P, const Params& C, StepCounters& ctr, u64 low,
                                  u64 high) {  // raft.go:1999-2012
@@ -291,14 +304,15 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
 #pragma unroll
     for (u32 d = 0; d < N; d++) {
       if (d == o.k) continue;
-      if (((o.iso >> o.k) & 1u) || ((o.iso >> d) & 1u)) {
-        ctr.v[C_MSG_DROPPED]++;
-        continue;
-      }
-      o.add_pc(d, 0x8000u);
-      ctr.v[C_MSG_OUT]++;
+      const u32 drop = ((o.iso >> o.k) & 1u) | ((o.iso >> d) & 1u);
+      o.n_drop_msg += drop;
+      o.n_out += 1u - drop;
+      if (!drop) o.add_pc(d, 0x8000u);
     }
   }
+  ctr.v[C_MSG_OUT] += o.n_out;
+  ctr.v[C_MSG_DROPPED] += o.n_drop_msg;
+  ctr.v[C_ENT_OUT] += o.n_ent_out;
   Upd u;
   u.save_lo = c.saved_to + 1;
   u.save_hi = c.last_index;
@@ -372,6 +386,7 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
   u.n_drop_ent = 0;
   u.n_drop_ri = (u16)o.n_drop_ri;
   u.fault = o.fault;
+  ctr.v[C_FAULTS] += popc8(o.fault & ~o.fault0 & 0xFFu);
   u.flags = (u16)((c.committed != committed0 ? UF_STATE_CHANGED : 0u) |
                   (send_q ? UF_SENT_QUIESCE : 0u));
   u.pad = 0;
@@ -382,7 +397,7 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
   u16* cnt = &P.cnt[o.par][o.g * N * N + o.k * N];
 #pragma unroll
   for (u32 dd = 0; dd < N; dd++) cnt[dd] = (u16)o.get_pc(dd);
-  h.flags = flags;
+  h.flags = o.fault ? (u8)(flags | HF_FAULTED) : flags;
   h.election_tick = etick;
   h.heartbeat_tick = (u16)htick;
   h.q_tick = q.tick;
@@ -413,6 +428,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   const u32 par = round & 1u, ppar = par ^ 1u;
   const u64 cid = C.cid_base + g * C.cid_stride;
   // ---- gather, level 1: independent loads
+  RBE_RSTAMP(rt0);
   RBE_STAMP(t0);
   Hot h = load_hot(P, C, r, round);
   Core c = P.core[r];
@@ -429,10 +445,11 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
 #pragma unroll
   for (u32 s = 0; s < N; s++)
     pcin[s] = (round > 0 && s != k) ? (u32)P.cnt[ppar][g * N * N + s * N + k] : 0u;
-  const u32 until = P.iso_until[g];
-  const u8 isom = P.iso_mask[g];
-  const u64 digest0 = P.upd[r].digest;
-  const u32 fault0 = P.upd[r].fault;
+  // the isolation schedule and the Update record are read only when in use:
+  // two of the lane's scattered lines saved in the steady state
+  const u32 until = C.iso_period ? P.iso_until[g] : 0u;
+  const u8 isom = C.iso_period ? P.iso_mask[g] : (u8)0;
+  const u64 digest0 = TRACE ? P.upd[r].digest : 0;
   // ---- eligibility on level-1 data
   if (h.role != R_Leader) return false;
   if (h.flags & (HF_APPLY_PENDING | HF_IS_LTT)) return false;
@@ -453,17 +470,23 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   // Loads only inside the branches; every use comes after the join, so no
   // branch waits for its own loads (a wait inside each conditional block
   // would serialise the message loads).
-  LeadMsg in[N][Cap::MAXM];
-  u32 nbs[N];
+  // one row per other sender (row j is sender j + (j >= k)): no registers
+  // for the lane's own slot, which is what keeps the step out of scratch
+  LeadMsg in[N - 1][Cap::MAXM];
 #pragma unroll
-  for (u32 s = 0; s < N; s++) {
-    nbs[s] = s == k ? 0u : ((pcin[s] >> 7) & 0x7Fu);
-    const Msg* lst = &P.msgs[ppar][((g * N + s) * N + k) * (u64)C.maxm];
+  for (u32 j = 0; j + 1 < N; j++) {
+    const u32 sj = j + (j >= k ? 1u : 0u);
+    u32 pj = 0;
+#pragma unroll
+    for (u32 t = 0; t < N; t++)
+      if (t == sj) pj = pcin[t];
+    const u32 nbj = (pj >> 7) & 0x7Fu;
+    const Msg* lst = &P.msgs[ppar][((g * N + sj) * N + k) * (u64)C.maxm];
 #pragma unroll
     for (u32 i = 0; i < Cap::MAXM; i++) {
-      in[s][i].w = 0xFFu;
-      in[s][i].term = in[s][i].log_index = in[s][i].hint = in[s][i].hint_high = 0;
-      if (i < nbs[s]) in[s][i] = load_lead(&lst[C.maxm - 1u - i]);
+      in[j][i].w = 0xFFu;
+      in[j][i].term = in[j][i].log_index = in[j][i].hint = in[j][i].hint_high = 0;
+      if (i < nbj) in[j][i] = load_lead(&lst[C.maxm - 1u - i]);
     }
   }
   u64 rq_lo[Cap::RQ], rq_hi[Cap::RQ], rq_ix[Cap::RQ];
@@ -494,19 +517,21 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   }
   bool rq_dirty = false;
 #pragma unroll
-  for (u32 s = 0; s < N; s++) {
-    if (s == k) continue;
+  for (u32 j = 0; j + 1 < N; j++) {
 #pragma unroll
     for (u32 i = 0; i < Cap::MAXM; i++) {
-      if (i >= nbs[s]) continue;
-      const u32 t = in[s][i].w & 0xFFu;
+      const u32 t = in[j][i].w & 0xFFu;
+      if (t == 0xFFu) continue;  // no message in this slot
       if (t != M_ReplicateResp && t != M_HeartbeatResp) return false;
-      if (in[s][i].term != c.term) return false;
-      if (t == M_ReplicateResp && (in[s][i].w >> 24)) return false;  // rejection: decreaseTo
+      if (in[j][i].term != c.term) return false;
+      if (t == M_ReplicateResp && (in[j][i].w >> 24)) return false;  // rejection: decreaseTo
     }
+  }
+#pragma unroll
+  for (u32 s = 0; s < N; s++) {
     // every entry a Replicate of this round can carry is the one proposed
     // this round (so no ring read is needed after the first store)
-    if (next[s] <= c.last_index) return false;
+    if (s != k && next[s] <= c.last_index) return false;
   }
   FastQ q;
   q.tick = h.q_tick;
@@ -536,8 +561,10 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   o.round_ = round;
   o.iso = round < until ? isom : (u8)0;
   o.pc = o.pc_hi = 0;
-  o.fault = fault0;
+  o.fault = (h.flags & HF_FAULTED) ? P.upd[r].fault : 0u;  // rare: after the first fault
   o.n_msgs = o.n_rtr = o.n_drop_ri = 0;
+  o.n_out = o.n_drop_msg = o.n_ent_out = 0;
+  o.fault0 = o.fault;
   o.msg_hash = o.rtr_hash = o.drop_hash = 0;
   o.term = c.term;
   u8 flags = h.flags;
@@ -797,12 +824,16 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
     // per message) reading the prefetched headers through a select chain,
     // so the register array is never indexed dynamically
     const u32 nb = (pcin[s] >> 7) & 0x7Fu;
+    // this sender's row: s - 1 when s > k, else s (both compile-time here)
+    const u32 jlo = s == 0 ? 0u : s - 1u;
+    const u32 jhi = s + 1 >= N ? N - 2u : s;
+    const bool use_lo = s > k;
 #pragma unroll 1
     for (u32 i = 0; i < nb; i++) {
-      LeadMsg m = in[s][0];
+      LeadMsg m = use_lo ? in[jlo][0] : in[jhi][0];
 #pragma unroll
       for (u32 j = 1; j < Cap::MAXM; j++)
-        if (i == j) m = in[s][j];
+        if (i == j) m = use_lo ? in[jlo][j] : in[jhi][j];
       ctr.v[C_MSG_IN]++;
       const u32 mtype = m.w & 0xFFu;
       if (mtype == M_HeartbeatResp && m.hint > 0) q.record_activity(C, M_ReadIndex);
@@ -903,10 +934,12 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   // the tick (node.go:1384-1399 → raft.go:551-564, 592-629)
   RBE_STAMP(t3);
   q.increase_tick(C);
-  if (q.quiesced(C)) {
+  const u32 qd = q.quiesced(C) ? 1u : 0u;
+  ctr.v[C_QUIESCED_TICKS] += qd;
+  ctr.v[C_ACTIVE_TICKS] += 1u - qd;
+  if (qd) {
     flags |= HF_RAFT_QUIESCE;
     etick++;
-    ctr.v[C_QUIESCED_TICKS]++;
   } else {
     flags &= (u8)~HF_RAFT_QUIESCE;
     etick++;  // leaderTick
@@ -926,7 +959,6 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
       hb_lo = lo;
       hb_hi = hi;
     }
-    ctr.v[C_ACTIVE_TICKS]++;
   }
   fan_out();
   // the proposal (handleProposals → Peer.ProposeEntries → handleLeaderPropose)
@@ -997,6 +1029,9 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   c.rq_count = (u8)rq_n;
   fast_finish<N, TRACE>(P, C, ctr, o, q, R_Leader, flags, h, c, etick, htick, committed0, digest0);
   RBE_STAMP(t5);
+  RBE_RSTAMP(rt5);
+  RBE_PHASE_ADD(0, 5, rt0, rt5);
+  RBE_PHASE_ADD(0, 6, t0, t5);
   RBE_PHASE_ADD(0, 0, t0, t1);
   RBE_PHASE_ADD(0, 1, t1, t2);
   RBE_PHASE_ADD(0, 2, t2, t3);
@@ -1021,6 +1056,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   const u32 k = (u32)(r % N);
   const u32 par = round & 1u, ppar = par ^ 1u;
   // ---- gather, level 1
+  RBE_RSTAMP(rt0);
   RBE_STAMP(t0);
   Hot h = load_hot(P, C, r, round);
   Core c = P.core[r];
@@ -1028,10 +1064,11 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
 #pragma unroll
   for (u32 s = 0; s < N; s++)
     pcin[s] = (round > 0 && s != k) ? (u32)P.cnt[ppar][g * N * N + s * N + k] : 0u;
-  const u32 until = P.iso_until[g];
-  const u8 isom = P.iso_mask[g];
-  const u64 digest0 = P.upd[r].digest;
-  const u32 fault0 = P.upd[r].fault;
+  // the isolation schedule and the Update record are read only when in use:
+  // two of the lane's scattered lines saved in the steady state
+  const u32 until = C.iso_period ? P.iso_until[g] : 0u;
+  const u8 isom = C.iso_period ? P.iso_mask[g] : (u8)0;
+  const u64 digest0 = TRACE ? P.upd[r].digest : 0;
   if (h.role != R_Follower) return false;
   if (h.flags & (HF_APPLY_PENDING | HF_IS_LTT)) return false;
   if (c.ltt != 0) return false;
@@ -1139,8 +1176,10 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   o.round_ = round;
   o.iso = round < until ? isom : (u8)0;
   o.pc = o.pc_hi = 0;
-  o.fault = fault0;
+  o.fault = (h.flags & HF_FAULTED) ? P.upd[r].fault : 0u;  // rare: after the first fault
   o.n_msgs = o.n_rtr = o.n_drop_ri = 0;
+  o.n_out = o.n_drop_msg = o.n_ent_out = 0;
+  o.fault0 = o.fault;
   o.msg_hash = o.rtr_hash = o.drop_hash = 0;
   o.term = c.term;
   u8 flags = h.flags;
@@ -1261,20 +1300,24 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   // the tick (raft.go:566-590, 623-629)
   RBE_STAMP(t3);
   q.increase_tick(C);
-  if (q.quiesced(C)) {
+  const u32 qd = q.quiesced(C) ? 1u : 0u;
+  ctr.v[C_QUIESCED_TICKS] += qd;
+  ctr.v[C_ACTIVE_TICKS] += 1u - qd;
+  if (qd) {
     flags |= HF_RAFT_QUIESCE;
     etick++;
-    ctr.v[C_QUIESCED_TICKS]++;
   } else {
     flags &= (u8)~HF_RAFT_QUIESCE;
     etick++;  // nonLeaderTick; reaching the timeout is excluded above
     if (etick >= h.rand_et) o.set_fault(ctr, F_UNSUPPORTED);
-    ctr.v[C_ACTIVE_TICKS]++;
   }
   c.leader = n_in ? (u8)lid : c.leader;
   fast_finish<N, TRACE>(P, C, ctr, o, q, R_Follower, flags, h, c, etick, htick, committed0,
                         digest0);
   RBE_STAMP(t5);
+  RBE_RSTAMP(rt5);
+  RBE_PHASE_ADD(1, 5, rt0, rt5);
+  RBE_PHASE_ADD(1, 6, t0, t5);
   RBE_PHASE_ADD(1, 0, t0, t1);
   RBE_PHASE_ADD(1, 1, t1, t2);
   RBE_PHASE_ADD(1, 2, t2, t3);

@@ -1360,8 +1360,8 @@ struct Lane {
         c_st[s] = P.rem_st[r * N + s];
       }
     }
-    fault = P.upd[r].fault;
-    const u64 digest0 = P.upd[r].digest;
+    fault = (flags & HF_FAULTED) ? P.upd[r].fault : 0u;
+    const u64 digest0 = TRACE ? P.upd[r].digest : 0;
     pc_lo = pc_hi = 0;
     arena_used = 0;
     seg_lo = 0;
@@ -1369,9 +1369,11 @@ struct Lane {
     msg_hash = rtr_hash = drop_hash = 0;
     n_msgs = n_rtr = n_drop_ent = n_drop_ri = 0;
     q_new = false;
-    {
+    if (C.iso_period) {
       const u32 until = P.iso_until[g];
       iso = round < until ? P.iso_mask[g] : (u8)0;
+    } else {
+      iso = 0;
     }
     ctr.v[C_STEPS]++;
     const u64 committed0 = committed;
@@ -1593,6 +1595,7 @@ struct Lane {
     saved_to = last;
     if (processed < committed) flags |= HF_APPLY_PENDING;
     else flags &= (u8)~HF_APPLY_PENDING;
+    if (fault) flags |= HF_FAULTED;
     if (role == R_Leader) {
       ctr.v[C_COMMITTED] += (u32)(committed - committed0);
       ctr.v[C_LEADER_STEPS]++;
@@ -1854,7 +1857,7 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, u32 round,
   else ctr.v[C_ACTIVE_TICKS]++;
   if (h.role == R_Leader) ctr.v[C_LEADER_STEPS]++;
   u8 iso = 0;
-  if (qnew) {
+  if (qnew && C.iso_period) {
     const u32 until = P.iso_until[g];
     iso = round < until ? P.iso_mask[g] : (u8)0;
   }

@@ -66,6 +66,7 @@ enum : u8 {
   HF_PENDING_CC = 2,    // raft.pendingConfigChange
   HF_IS_LTT = 4,        // raft.isLeaderTransferTarget
   HF_APPLY_PENDING = 8, // processed < committed after the step (apply limited by size)
+  HF_FAULTED = 16,      // Upd.fault != 0 (the sticky fault word is read only then)
 };
 
 // core plane (64 B per replica)

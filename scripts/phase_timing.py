@@ -19,6 +19,9 @@ E._lib = lib
 lib.rbe_debug_phases.argtypes = [C.POINTER(C.c_uint64)]
 w = sys.argv[1] if len(sys.argv) > 1 else "c4"
 kw, settle, _ = bench.WORKLOADS[w]
+kw = dict(kw)
+if len(sys.argv) > 2:
+    kw["n_groups"] = int(sys.argv[2])
 eng = E.Engine(**kw)
 eng.run(settle)
 eng.sync()
@@ -35,4 +38,8 @@ for role, rn in ((0, "leader"), (1, "follower")):
         continue
     parts = [f"{names[role][i]}={o[role * 8 + i] / n:.0f}" for i in range(5) if names[role][i] != "-"]
     print(f"{w} {rn}: waves={n / rounds:.0f}/round cycles/wave: " + " ".join(parts))
+    tot, rt = o[role * 8 + 6] / n, o[role * 8 + 5] / n
+    if rt:
+        print(f"    wave t0->t5: {tot:.0f} cycles, {rt * 0.01:.2f} us realtime, "
+              f"clock {tot / (rt * 0.01) / 1e3:.2f} GHz")
 print("kernel ms per round:", [round(x / rounds, 4) for x in ms], eng.kernel_names())
