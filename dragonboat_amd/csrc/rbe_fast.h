@@ -101,6 +101,12 @@ RBE_HD InMsg load_in(const Msg* p) {
   return x;
 }
 
+// the fields a steady-state leader keeps of an accepted ReplicateResp
+// (a = LogIndex) or HeartbeatResp (a = Hint, b = HintHigh) after the gather
+struct LeadIn {
+  u32 w;  // type, from, to, reject (raw)
+  u64 a, b;
+};
 // the fields a steady-state leader reads from a ReplicateResp / HeartbeatResp
 struct LeadMsg {
   u32 w;  // type, from, to, reject (raw; decoded where used, outside the load's branch)
@@ -516,11 +522,16 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
     rq_cf[i] = (rq_w[i] >> 8) & 0xFFu;
   }
   bool rq_dirty = false;
+  // eligibility of the inbox, then only the fields the handlers read stay live
+  LeadIn inc[N - 1][Cap::MAXM];
 #pragma unroll
   for (u32 j = 0; j + 1 < N; j++) {
 #pragma unroll
     for (u32 i = 0; i < Cap::MAXM; i++) {
       const u32 t = in[j][i].w & 0xFFu;
+      inc[j][i].w = in[j][i].w;
+      inc[j][i].a = t == M_ReplicateResp ? in[j][i].log_index : in[j][i].hint;
+      inc[j][i].b = in[j][i].hint_high;
       if (t == 0xFFu) continue;  // no message in this slot
       if (t != M_ReplicateResp && t != M_HeartbeatResp) return false;
       if (in[j][i].term != c.term) return false;
@@ -830,20 +841,20 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
     const bool use_lo = s > k;
 #pragma unroll 1
     for (u32 i = 0; i < nb; i++) {
-      LeadMsg m = use_lo ? in[jlo][0] : in[jhi][0];
+      LeadIn m = use_lo ? inc[jlo][0] : inc[jhi][0];
 #pragma unroll
       for (u32 j = 1; j < Cap::MAXM; j++)
-        if (i == j) m = use_lo ? in[jlo][j] : in[jhi][j];
+        if (i == j) m = use_lo ? inc[jlo][j] : inc[jhi][j];
       ctr.v[C_MSG_IN]++;
       const u32 mtype = m.w & 0xFFu;
-      if (mtype == M_HeartbeatResp && m.hint > 0) q.record_activity(C, M_ReadIndex);
+      if (mtype == M_HeartbeatResp && m.a > 0) q.record_activity(C, M_ReadIndex);
       else q.record_activity(C, mtype);
       st[s] |= 4u;  // setActive
-      if (mtype == M_ReplicateResp) {  // raft.go:1667-1696
-        if (!(m.w >> 24)) {
+      if (mtype == M_ReplicateResp) {  // raft.go:1667-1696 (accepted: rejections
+        {                              // take the full table, see the gather)
           const u32 rs = st[s] & 3u;
           const bool paused = rs == RS_Wait || rs == RS_Snapshot;
-          if (try_update(match[s], next[s], st[s], m.log_index)) {
+          if (try_update(match[s], next[s], st[s], m.a)) {
             // respondedTo (remote.go:145-153); snapshotIndex is 0 on device
             const u32 rs2 = st[s] & 3u;
             if (rs2 == RS_Retry) {
@@ -856,35 +867,15 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
             if (try_commit()) rep_mask |= ((1u << N) - 1u) & ~(1u << k);
             else if (paused) rep_mask |= 1u << s;
           }
-        } else {
-          // decreaseTo (remote.go:155-171)
-          bool dec = false;
-          if ((st[s] & 3u) == RS_Replicate) {
-            if (m.log_index > match[s]) {
-              next[s] = match[s] + 1;
-              dec = true;
-            }
-          } else if (next[s] - 1 == m.log_index) {
-            if ((st[s] & 3u) == RS_Wait) st[s] = (st[s] & ~3u) | RS_Retry;
-            next[s] = umax64(1, umin64(m.log_index, m.hint + 1));
-            dec = true;
-          }
-          if (dec) {
-            if ((st[s] & 3u) == RS_Replicate) {  // enterRetryState → becomeRetry
-              next[s] = match[s] + 1;
-              st[s] = (st[s] & ~3u) | RS_Retry;
-            }
-            rep_mask |= 1u << s;
-          }
         }
       } else {  // HeartbeatResp, raft.go:1698-1710
         if ((st[s] & 3u) == RS_Wait) st[s] = (st[s] & ~3u) | RS_Retry;
         ctr.v[C_REMOTE_TOUCH]++;
         if (match[s] < c.last_index) rep_mask |= 1u << s;
-        if (m.hint != 0) {
+        if (m.a != 0) {
           rq_pending = true;
-          rq_plo = m.hint;
-          rq_phi = m.hint_high;
+          rq_plo = m.a;
+          rq_phi = m.b;
           rq_from = s + 1;
         }
       }

@@ -1763,7 +1763,7 @@ RBE_HD bool triage_lazy(const Planes& P, const Params& C, u64 r, u32 round, u8 i
   if (C.ext_inputs && P.ext[r].kind) return false;
   ctr.v[C_STEPS]++;
   ctr.v[C_QUIESCED_TICKS]++;
-  if (ib & IB_LEAD) ctr.v[C_LEADER_STEPS]++;
+  ctr.v[C_LEADER_STEPS] += (ib & IB_LEAD) ? 1u : 0u;
   if (!(ib & IB_H2)) {  // this parity's outbox counts may still be non-zero
     u16* cnt = &P.cnt[round & 1u][g * N * N + (u32)(r % N) * N];
     for (u32 d = 0; d < N; d++) cnt[d] = 0;
@@ -1853,9 +1853,11 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, u32 round,
   // commit the idle round
   ctr.v[C_STEPS]++;
   ctr.v[C_MSG_IN] += popc8(qbits);
-  if (quiesced) ctr.v[C_QUIESCED_TICKS]++;
-  else ctr.v[C_ACTIVE_TICKS]++;
-  if (h.role == R_Leader) ctr.v[C_LEADER_STEPS]++;
+  // branch-free bumps (see FastOut in rbe_fast.h: sibling branches bumping
+  // different counters become one indexed bump and the counters go to scratch)
+  ctr.v[C_QUIESCED_TICKS] += quiesced ? 1u : 0u;
+  ctr.v[C_ACTIVE_TICKS] += quiesced ? 0u : 1u;
+  ctr.v[C_LEADER_STEPS] += h.role == R_Leader ? 1u : 0u;
   u8 iso = 0;
   if (qnew && C.iso_period) {
     const u32 until = P.iso_until[g];
@@ -1873,12 +1875,10 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, u32 round,
     for (u32 d = 0; d < N; d++) {
       u16 v = 0;
       if (qnew && d != k) {  // sendEnterQuiesceMessages (node.go:873-886)
-        if (((iso >> k) & 1u) || ((iso >> d) & 1u)) {
-          ctr.v[C_MSG_DROPPED]++;
-        } else {
-          v = 0x8000u;
-          ctr.v[C_MSG_OUT]++;
-        }
+        const u32 drop = ((iso >> k) & 1u) | ((iso >> d) & 1u);
+        ctr.v[C_MSG_DROPPED] += drop;
+        ctr.v[C_MSG_OUT] += 1u - drop;
+        v = drop ? (u16)0 : (u16)0x8000u;
       }
       cnt[d] = v;
     }
