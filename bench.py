@@ -234,7 +234,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--prof-rounds", type=int, default=50,
                     help="rounds profiled per kernel with HIP events after the timed region")
-    ap.add_argument("--cpu-groups", type=int, default=30000)
+    ap.add_argument("--cpu-groups", type=int, default=300000)
     ap.add_argument("--cpu-rounds", type=int, default=100)
     ap.add_argument("--cpu-threads", type=int,
                     default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))

@@ -272,6 +272,36 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_list(Planes P, 
   flush_counters<MODE == MODE_LEAD ? KS_FAST_LEAD : KS_FAST_FOLL>(P, c);
 }
 
+// Pass 2, merged (RBE_MODE=both): the round's steady-state leaders and
+// followers in one launch, so the two roles' waves share the SIMDs instead of
+// running back to back; item i < n_lead is a leader, the rest followers.
+template <int N, bool TRACE>
+__global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, Params C,
+                                                                     const u32* round_ptr,
+                                                                     u32 round_add, Lists L) {
+  const u32 round = (round_ptr ? *round_ptr : 0u) + round_add;
+  const u32 par = round & 1u;
+  const u32 nl = L.counts[0 * 2 + par], n = nl + L.counts[1 * 2 + par];
+  StepCounters c;
+#pragma unroll
+  for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
+  const u64 stride = (u64)gridDim.x * kBlock;
+  for (u64 i0 = (u64)blockIdx.x * kBlock; i0 < n; i0 += stride) {
+    const u64 i = i0 + threadIdx.x;
+    bool slow = false;
+    u32 r = 0;
+    if (i < nl) {
+      r = L.idx[i];
+      slow = !step_fast<N, TRACE, MODE_LEAD>(P, C, r, round, c);
+    } else if (i < n) {
+      r = L.idx[L.cap + (i - nl)];
+      slow = !step_fast<N, TRACE, MODE_FOLL>(P, C, r, round, c);
+    }
+    list_push(L, 2, par, slow, r);
+  }
+  flush_counters<KS_FAST_LEAD>(P, c);
+}
+
 // Pass 3: the whole handler table over the full list (persistent, grid-stride).
 template <int N, bool TRACE>
 __global__ __launch_bounds__(kBlock) void k_full_list(Planes P, Params C, const u32* round_ptr,
@@ -367,7 +397,8 @@ struct rbe_engine {
   hipGraphExec_t graph = nullptr;
   u32 graph_rounds = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  int mode = 1;              // RBE_MODE: 0 fused, 1 split (default: triage + 2 fast lists), 2 full
+  int mode = 3;              // RBE_MODE: 0 fused, 1 split (triage + 2 fast lists), 2 full,
+                             // 3 both (default: triage + one merged fast launch)
   Lists L;                   // per-round work lists (triage → fast → full)
   u32* xcount = nullptr;     // replica-per-GPU pack counters [rep_world * XS_NUM]
 };
@@ -498,6 +529,19 @@ static int launch_step_t(rbe_engine* e, const u32* round_ptr, u32 round_add,
     hipLaunchKernelGGL((k_round<N, TRACE>), dim3(gt), dim3(kBlock), 0, e->stream, e->P, e->C,
                        round_ptr, round_add, e->L);
     mark(1);
+    mark(2);
+    mark(3);
+    hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kBlock), 0, e->stream, e->P, e->C,
+                       round_ptr, round_add, e->L);
+    mark(4);
+  } else if (e->mode == 3) {
+    mark(0);
+    hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(gt), dim3(kBlock), 0, e->stream, e->P, e->C,
+                       round_ptr, round_add, e->L);
+    mark(1);
+    const unsigned gf = g < kFastGrid ? g : kFastGrid;
+    hipLaunchKernelGGL((k_fast_both<N, TRACE>), dim3(gf), dim3(kBlock), 0, e->stream, e->P, e->C,
+                       round_ptr, round_add, e->L);
     mark(2);
     mark(3);
     hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kBlock), 0, e->stream, e->P, e->C,
@@ -646,9 +690,14 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   }
   HIP_IGNORE(hipMemsetAsync(e->d_round, 0, sizeof(u32), e->stream));
   const char* mode = getenv("RBE_MODE");
-  // default: the split pipeline (k_triage → k_fast_list<LEAD> → k_fast_list<FOLL>
-  // → k_full_list); RBE_MODE=fused runs k_round + k_full_list, RBE_MODE=full k_step
-  e->mode = !mode ? 1 : (strcmp(mode, "full") == 0 ? 2 : (strcmp(mode, "fused") == 0 ? 0 : 1));
+  // default: k_triage → k_fast_both → k_full_list; RBE_MODE=split runs the two
+  // roles as separate launches, RBE_MODE=fused k_round + k_full_list,
+  // RBE_MODE=full k_step alone
+  e->mode = !mode ? 3
+                  : (strcmp(mode, "full") == 0    ? 2
+                     : strcmp(mode, "fused") == 0 ? 0
+                     : strcmp(mode, "split") == 0 ? 1
+                                                  : 3);
   if (C.n_rep >= (1ull << 32)) {
     rbe_destroy(e);
     return RBE_E_INVALID;  // list entries are 32-bit replica indices
@@ -912,10 +961,11 @@ int rbe_xchg_unpack(rbe_engine* e, const void* cnt, uint64_t n_cnt, const void* 
 
 int rbe_kernel_name(const rbe_engine* e, int32_t kernel, char* buf, uint32_t cap) {
   if (!e || !buf || cap == 0 || kernel < 0 || kernel >= KS_NUM) return RBE_E_INVALID;
-  static const char* names[3][KS_NUM] = {
+  static const char* names[4][KS_NUM] = {
       {"k_round", "", "", "k_full_list"},
       {"k_triage", "k_fast_list<LEAD>", "k_fast_list<FOLL>", "k_full_list"},
-      {"", "", "", "k_step"}};
+      {"", "", "", "k_step"},
+      {"k_triage", "k_fast_both", "", "k_full_list"}};
   const char* n = names[e->mode][kernel];
   strncpy(buf, n, cap - 1);
   buf[cap - 1] = 0;

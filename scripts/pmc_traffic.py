@@ -23,6 +23,8 @@ def kernel_key(name):
         return "k_round"
     if "k_triage" in name:
         return "k_triage"
+    if "k_fast_both" in name:
+        return "k_fast_both"
     if "k_fast_list" in name:
         # template args <N, TRACE, MODE>: MODE 1 = LEAD, 2 = FOLL
         mode = name.split("k_fast_list<", 1)[1].split(">", 1)[0].split(",")[-1].strip()

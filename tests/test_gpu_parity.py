@@ -115,3 +115,20 @@ def test_engine_untraced_state_parity(gpu_available, name):
     bad = counters_match(eng.counters(), ref.counters())
     assert not bad, f"{name}: counters differ {bad}"
     eng.close()
+
+
+@pytest.mark.parametrize("mode", ["split", "fused", "full"])
+@pytest.mark.parametrize("name", ["C2", "C4_DENSE", "MIXED"])
+def test_pipeline_modes_parity(gpu_available, monkeypatch, name, mode):
+    """Every pipeline (RBE_MODE) is bit-exact with the oracle, not only the
+    default one (triage → merged fast launch → full list)."""
+    monkeypatch.setenv("RBE_MODE", mode)
+    kw, rounds = CASES[name]
+    eng = _engine(kw, name)
+    ref = O.Harness(**kw)
+    d = run_lockstep(eng, ref, min(rounds, 300), every=1)
+    assert d is None, f"{name}/{mode}: first divergence {d}"
+    assert eng.fault_summary()[0] == 0
+    bad = counters_match(eng.counters(), ref.counters())
+    assert not bad, f"{name}/{mode}: counters differ {bad}"
+    eng.close()
