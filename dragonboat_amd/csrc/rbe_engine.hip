@@ -92,12 +92,28 @@ __global__ __launch_bounds__(kBlock) void k_step(Planes P, Params C, const u32* 
 }
 
 // Work lists of a round: 0 = steady-state leaders, 1 = steady-state followers,
-// 2 = full handler table.  Entry counts live in counts[list * 2 + parity].
+// 2 = full handler table.  Lists 0 and 1 fill from both ends: the front holds
+// the common case (a leader without a proposal this round, a follower without
+// a Replicate), the back the rest, so the waves of the fast launch are mostly
+// homogeneous and skip the code paths none of their lanes take.  Front counts
+// live in counts[list * 2 + parity], back counts in counts[6 + list * 2 + parity];
+// the back of list l occupies idx[l * cap + cap - 1 - j].
 struct Lists {
   u32* idx;     // [3][cap] replica indices
-  u32* counts;  // [3][2]
+  u32* counts;  // [3][2] front, then [2][2] back
   u64 cap;
 };
+static constexpr u32 kListCounts = 10;
+// length of list li (front + back) and its i-th entry (front first)
+__device__ __forceinline__ u32 list_front(const Lists& L, u32 li, u32 par) {
+  return L.counts[li * 2 + par];
+}
+__device__ __forceinline__ u32 list_back(const Lists& L, u32 li, u32 par) {
+  return li < 2 ? L.counts[6 + li * 2 + par] : 0u;
+}
+__device__ __forceinline__ u32 list_at(const Lists& L, u32 li, u32 nfront, u64 i) {
+  return i < nfront ? L.idx[li * L.cap + i] : L.idx[li * L.cap + L.cap - 1 - (i - nfront)];
+}
 
 // wave-aggregated append: one atomic per wave and list
 __device__ __forceinline__ void list_push(const Lists& L, u32 list, u32 par, bool want, u32 r) {
@@ -120,11 +136,12 @@ template <int N, bool TRACE>
 __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, const u32* round_ptr,
                                                    u32 round_add, Lists L) {
   __shared__ u32 s_idx[3][kTriChunk];
-  __shared__ u32 s_n[3], s_base[3];
+  __shared__ u32 s_n[5], s_base[5];  // fronts of lists 0..2, backs of lists 0..1
   const u32 round = (round_ptr ? *round_ptr : 0u) + round_add;
   const u32 par = round & 1u;
-  if (blockIdx.x == 0 && threadIdx.x < 3) L.counts[threadIdx.x * 2 + (par ^ 1u)] = 0;
-  if (threadIdx.x < 3) s_n[threadIdx.x] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < 5)
+    L.counts[(threadIdx.x < 3 ? threadIdx.x * 2 : 6 + (threadIdx.x - 3) * 2) + (par ^ 1u)] = 0;
+  if (threadIdx.x < 5) s_n[threadIdx.x] = 0;
   __syncthreads();
   StepCounters c;
 #pragma unroll
@@ -163,28 +180,41 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, const u32
       else
         cls = triage_replica<N, TRACE>(P, C, r, round, c);
     }
+    // the back of the list: a leader proposing this round, a follower
+    // receiving a Replicate
+    bool back = false;
+    if (cls == T_LEAD)
+      back = wl_input(C, C.cid_base + (r / N) * C.cid_stride, round) == 1u;
+    else if (cls == T_FOLL)
+      back = (inb[i] & 4u) != 0;
 #pragma unroll
-    for (u32 li = 0; li < 3; li++) {
-      const bool want = cls == li + 1;
+    for (u32 sl = 0; sl < 5; sl++) {  // slots: fronts 0..2, backs of lists 0..1
+      const u32 li = sl < 3 ? sl : sl - 3;
+      const bool want = cls == li + 1 && back == (sl >= 3);
       const u64 mask = __ballot(want);
       if (!mask) continue;
       const int first = __ffsll((unsigned long long)mask) - 1;
       u32 base = 0;
-      if (lane == first) base = atomicAdd(&s_n[li], (u32)__popcll(mask));
+      if (lane == first) base = atomicAdd(&s_n[sl], (u32)__popcll(mask));
       base = __shfl(base, first, 64);
-      if (want) s_idx[li][base + __popcll(mask & ((1ull << lane) - 1ull))] = (u32)r;
+      const u32 pos = base + __popcll(mask & ((1ull << lane) - 1ull));
+      if (want) s_idx[li][sl < 3 ? pos : kTriChunk - 1u - pos] = (u32)r;
     }
   }
   __syncthreads();
-  if (threadIdx.x < 3)
-    s_base[threadIdx.x] = s_n[threadIdx.x] ? atomicAdd(&L.counts[threadIdx.x * 2 + par],
-                                                       s_n[threadIdx.x])
-                                           : 0u;
+  if (threadIdx.x < 5) {
+    const u32 at = threadIdx.x < 3 ? threadIdx.x * 2 + par : 6 + (threadIdx.x - 3) * 2 + par;
+    s_base[threadIdx.x] = s_n[threadIdx.x] ? atomicAdd(&L.counts[at], s_n[threadIdx.x]) : 0u;
+  }
   __syncthreads();
 #pragma unroll
   for (u32 li = 0; li < 3; li++)
     for (u32 j = threadIdx.x; j < s_n[li]; j += kBlock)
       L.idx[li * L.cap + s_base[li] + j] = s_idx[li][j];
+#pragma unroll
+  for (u32 li = 0; li < 2; li++)
+    for (u32 j = threadIdx.x; j < s_n[3 + li]; j += kBlock)
+      L.idx[li * L.cap + L.cap - 1 - (s_base[3 + li] + j)] = s_idx[li][kTriChunk - 1u - j];
   flush_counters<KS_TRIAGE>(P, c);
 }
 
@@ -254,7 +284,7 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_list(Planes P, 
   const u32 round = (round_ptr ? *round_ptr : 0u) + round_add;
   const u32 par = round & 1u;
   const u32 li = MODE == MODE_LEAD ? 0u : 1u;
-  const u32 n = L.counts[li * 2 + par];
+  const u32 nfront = list_front(L, li, par), n = nfront + list_back(L, li, par);
   StepCounters c;
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
@@ -264,7 +294,7 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_list(Planes P, 
     bool slow = false;
     u32 r = 0;
     if (i < n) {
-      r = L.idx[li * L.cap + i];
+      r = list_at(L, li, nfront, i);
       slow = !step_fast<N, TRACE, MODE>(P, C, r, round, c);
     }
     list_push(L, 2, par, slow, r);
@@ -281,7 +311,8 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, 
                                                                      u32 round_add, Lists L) {
   const u32 round = (round_ptr ? *round_ptr : 0u) + round_add;
   const u32 par = round & 1u;
-  const u32 nl = L.counts[0 * 2 + par], n = nl + L.counts[1 * 2 + par];
+  const u32 nlf = list_front(L, 0, par), nl = nlf + list_back(L, 0, par);
+  const u32 nff = list_front(L, 1, par), n = nl + nff + list_back(L, 1, par);
   StepCounters c;
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
@@ -291,10 +322,10 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, 
     bool slow = false;
     u32 r = 0;
     if (i < nl) {
-      r = L.idx[i];
+      r = list_at(L, 0, nlf, i);
       slow = !step_fast<N, TRACE, MODE_LEAD>(P, C, r, round, c);
     } else if (i < n) {
-      r = L.idx[L.cap + (i - nl)];
+      r = list_at(L, 1, nff, i - nl);
       slow = !step_fast<N, TRACE, MODE_FOLL>(P, C, r, round, c);
     }
     list_push(L, 2, par, slow, r);
@@ -704,7 +735,7 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   }
   e->L.cap = C.n_rep;
   if (hipMalloc(&e->L.idx, 3 * C.n_rep * sizeof(u32)) != hipSuccess ||
-      hipMalloc(&e->L.counts, 6 * sizeof(u32)) != hipSuccess) {
+      hipMalloc(&e->L.counts, kListCounts * sizeof(u32)) != hipSuccess) {
     rbe_destroy(e);
     return RBE_E_NOMEM;
   }
@@ -715,7 +746,7 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
     return RBE_E_NOMEM;
   }
   e->allocs.push_back(e->xcount);
-  HIP_IGNORE(hipMemsetAsync(e->L.counts, 0, 6 * sizeof(u32), e->stream));
+  HIP_IGNORE(hipMemsetAsync(e->L.counts, 0, kListCounts * sizeof(u32), e->stream));
   rc = dispatch_n(C.n, [&](auto NN) {
     constexpr int N = decltype(NN)::value;
     hipLaunchKernelGGL(k_launch<N>, dim3(grid_for(C.n_rep)), dim3(kBlock), 0, e->stream, e->P,

@@ -1773,7 +1773,8 @@ RBE_HD bool triage_lazy(const Planes& P, const Params& C, u64 r, u32 round, u8 i
   return true;
 }
 // the inbound count words of replica r in this round: bit 0 = any non-zero
-// word, bit 1 = any message (a Quiesce notice alone leaves it clear)
+// word, bit 1 = any message (a Quiesce notice alone leaves it clear), bit 2 =
+// any Replicate
 template <int N>
 RBE_HD u32 inbound_bits(const Planes& P, u64 r, u32 round) {
   if (round == 0) return 0;
@@ -1786,6 +1787,7 @@ RBE_HD u32 inbound_bits(const Planes& P, u64 r, u32 round) {
     const u32 pc = icnt[s * N + k];
     if (pc) any |= 1u;
     if (pc & 0x3FFFu) any |= 2u;
+    if (pc & 0x7Fu) any |= 4u;
   }
   return any;
 }
