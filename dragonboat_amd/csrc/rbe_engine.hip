@@ -37,7 +37,17 @@ static constexpr int kBlock = 256;
 #ifndef RBE_FAST_WAVES
 #define RBE_FAST_WAVES 2
 #endif
-static constexpr u32 kTriChunk = 2048;   // replicas per k_triage block (8 per lane)
+#ifndef RBE_TRI_CHUNK
+#define RBE_TRI_CHUNK 2048
+#endif
+// which fast steps work on wave-staged rows (k_fast_both, stage_in_wave)
+#ifndef RBE_STAGE_LEAD
+#define RBE_STAGE_LEAD 0
+#endif
+#ifndef RBE_STAGE_FOLL
+#define RBE_STAGE_FOLL 0
+#endif
+static constexpr u32 kTriChunk = RBE_TRI_CHUNK;   // replicas per k_triage block (8 per lane)
 static constexpr int kCtrStripes = 64;   // counter stripes per kernel slot (flush_counters)
 // counter sections, one per pipeline kernel (rbe_get_kernel_counters)
 enum : int { KS_TRIAGE = 0, KS_FAST_LEAD = 1, KS_FAST_FOLL = 2, KS_FULL = 3, KS_NUM = 4 };
@@ -155,17 +165,29 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, const u32
   // by the role its idle byte carries.
   constexpr u32 kPer = kTriChunk / kBlock;
   const u64 lo = (u64)blockIdx.x * kTriChunk + threadIdx.x;
+  // Every load is unconditional (a replica past the end reads replica 0 and
+  // is masked afterwards) and u32 index math: no load waits behind a branch
+  // or a 64-bit division, so all 8 * (N + 1) loads of a lane are in flight
+  // before the first wait.
   u8 ibs[kPer];
   u32 inb[kPer];
+  u16 wv[kPer][N];
+  u32 kk[kPer];
 #pragma unroll
   for (u32 i = 0; i < kPer; i++) {
     const u64 r = lo + (u64)i * kBlock;
-    ibs[i] = r < C.n_rep ? P.idle[r] : (u8)0;
+    const u32 rc = r < C.n_rep ? (u32)r : 0u;
+    ibs[i] = P.idle[rc];
+    const u32 g = rc / (u32)N;
+    kk[i] = rc - g * (u32)N;
+    inbound_load<N>(P, g, kk[i], round, wv[i]);
   }
 #pragma unroll
   for (u32 i = 0; i < kPer; i++) {
     const u64 r = lo + (u64)i * kBlock;
-    inb[i] = r < C.n_rep ? inbound_bits<N>(P, r, round) : 0u;
+    const bool in = r < C.n_rep;
+    ibs[i] = in ? ibs[i] : (u8)0;
+    inb[i] = in ? inbound_fold<N>(wv[i], kk[i], round) : 0u;
   }
   const bool shortcut = !TRACE && C.quiesce;
 #pragma unroll
@@ -184,7 +206,7 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, const u32
     // receiving a Replicate
     bool back = false;
     if (cls == T_LEAD)
-      back = wl_input(C, C.cid_base + (r / N) * C.cid_stride, round) == 1u;
+      back = wl_input(C, C.cid_base + (u64)((u32)r / (u32)N) * C.cid_stride, round) == 1u;
     else if (cls == T_FOLL)
       back = (inb[i] & 4u) != 0;
 #pragma unroll
@@ -302,13 +324,113 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_list(Planes P, 
   flush_counters<MODE == MODE_LEAD ? KS_FAST_LEAD : KS_FAST_FOLL>(P, c);
 }
 
-// Pass 2, merged (RBE_MODE=both): the round's steady-state leaders and
-// followers in one launch, so the two roles' waves share the SIMDs instead of
-// running back to back; item i < n_lead is a leader, the rest followers.
+// Orders a wave's LDS accesses around a cross-lane hand-off: the wave's DS
+// instructions execute in issue order, so a compiler barrier is all it takes.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Wave-cooperative row moves for the staged fast steps (StageRow, rbe_fast.h).
+// Load `it` of a plane with CH 16-B chunks per row serves chunk idx % CH of
+// row idx / CH, idx = it * 64 + lane: CH consecutive lanes cover one row, so a
+// wave instruction touches 64 / CH rows.  Row j belongs to lane j (its replica
+// index comes over by shuffle); bit j of `m` says whether lane j takes part.
+template <int N>
+__device__ __forceinline__ void stage_in_wave(const Planes& P, StageRow<N>* rows, u32 r,
+                                              u64 m_any, u64 m_lead) {
+  const int lane = threadIdx.x & 63;
+  constexpr int CC = sizeof(Core) / 16, CH = sizeof(Hot) / 16;
+  uint4 vc[CC], vh[CH], vr[N];
+#pragma unroll
+  for (int it = 0; it < CC; it++) {
+    const int idx = it * 64 + lane, j = idx / CC, q = idx % CC;
+    const u32 rj = __shfl(r, j, 64);
+    if ((m_any >> j) & 1ull) vc[it] = reinterpret_cast<const uint4*>(P.core + rj)[q];
+  }
+#pragma unroll
+  for (int it = 0; it < CH; it++) {
+    const int idx = it * 64 + lane, j = idx / CH, q = idx % CH;
+    const u32 rj = __shfl(r, j, 64);
+    if ((m_any >> j) & 1ull) vh[it] = reinterpret_cast<const uint4*>(P.hot + rj)[q];
+  }
+  if (m_lead) {
+#pragma unroll
+    for (int it = 0; it < N; it++) {
+      const int idx = it * 64 + lane, j = idx / N, q = idx % N;
+      const u32 rj = __shfl(r, j, 64);
+      if ((m_lead >> j) & 1ull) vr[it] = reinterpret_cast<const uint4*>(P.rem + (u64)rj * N)[q];
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < CC; it++) {
+    const int idx = it * 64 + lane, j = idx / CC, q = idx % CC;
+    if ((m_any >> j) & 1ull) reinterpret_cast<uint4*>(&rows[j].core)[q] = vc[it];
+  }
+#pragma unroll
+  for (int it = 0; it < CH; it++) {
+    const int idx = it * 64 + lane, j = idx / CH, q = idx % CH;
+    if ((m_any >> j) & 1ull) reinterpret_cast<uint4*>(&rows[j].hot)[q] = vh[it];
+  }
+  if (m_lead) {
+#pragma unroll
+    for (int it = 0; it < N; it++) {
+      const int idx = it * 64 + lane, j = idx / N, q = idx % N;
+      if ((m_lead >> j) & 1ull) reinterpret_cast<uint4*>(&rows[j].rem[0])[q] = vr[it];
+    }
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void stage_out_wave(const Planes& P, const StageRow<N>* rows, u32 r,
+                                               u64 m_done, u64 m_lead) {
+  const int lane = threadIdx.x & 63;
+  constexpr int CC = sizeof(Core) / 16, CU = sizeof(Upd) / 16, CH = sizeof(Hot) / 16;
+#pragma unroll
+  for (int it = 0; it < CC; it++) {
+    const int idx = it * 64 + lane, j = idx / CC, q = idx % CC;
+    const u32 rj = __shfl(r, j, 64);
+    if ((m_done >> j) & 1ull)
+      reinterpret_cast<uint4*>(P.core + rj)[q] = reinterpret_cast<const uint4*>(&rows[j].core)[q];
+  }
+#pragma unroll
+  for (int it = 0; it < CU; it++) {
+    const int idx = it * 64 + lane, j = idx / CU, q = idx % CU;
+    const u32 rj = __shfl(r, j, 64);
+    if ((m_done >> j) & 1ull)
+      reinterpret_cast<uint4*>(P.upd + rj)[q] = reinterpret_cast<const uint4*>(&rows[j].upd)[q];
+  }
+#pragma unroll
+  for (int it = 0; it < CH; it++) {
+    const int idx = it * 64 + lane, j = idx / CH, q = idx % CH;
+    const u32 rj = __shfl(r, j, 64);
+    if ((m_done >> j) & 1ull)
+      reinterpret_cast<uint4*>(P.hot + rj)[q] = reinterpret_cast<const uint4*>(&rows[j].hot)[q];
+  }
+  if (m_lead) {
+#pragma unroll
+    for (int it = 0; it < N; it++) {
+      const int idx = it * 64 + lane, j = idx / N, q = idx % N;
+      const u32 rj = __shfl(r, j, 64);
+      if ((m_lead >> j) & 1ull)
+        reinterpret_cast<uint4*>(P.rem + (u64)rj * N)[q] =
+            reinterpret_cast<const uint4*>(&rows[j].rem[0])[q];
+    }
+  }
+}
+
+// Pass 2, merged (RBE_MODE=both, the default): the round's steady-state
+// leaders and followers in one launch, so the two roles' waves share the SIMDs
+// instead of running back to back; item i < n_lead is a leader, the rest
+// followers.  The rows a step reads and rewrites whole (Hot, Core, Upd, the
+// leader's remote slots) move between HBM and LDS wave-cooperatively
+// (stage_in_wave / stage_out_wave); the step works on its LDS row.
 template <int N, bool TRACE>
 __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, Params C,
                                                                      const u32* round_ptr,
                                                                      u32 round_add, Lists L) {
+  __shared__ StageRow<N> s_rows[kBlock];
   const u32 round = (round_ptr ? *round_ptr : 0u) + round_add;
   const u32 par = round & 1u;
   const u32 nlf = list_front(L, 0, par), nl = nlf + list_back(L, 0, par);
@@ -316,19 +438,34 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, 
   StepCounters c;
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
+  StageRow<N>* wrows = &s_rows[threadIdx.x & ~63u];
+  StageRow<N>* mine = &s_rows[threadIdx.x];
   const u64 stride = (u64)gridDim.x * kBlock;
   for (u64 i0 = (u64)blockIdx.x * kBlock; i0 < n; i0 += stride) {
     const u64 i = i0 + threadIdx.x;
-    bool slow = false;
+    const bool lead = i < nl, any = i < n;
     u32 r = 0;
-    if (i < nl) {
-      r = list_at(L, 0, nlf, i);
-      slow = !step_fast<N, TRACE, MODE_LEAD>(P, C, r, round, c);
-    } else if (i < n) {
-      r = list_at(L, 1, nff, i - nl);
-      slow = !step_fast<N, TRACE, MODE_FOLL>(P, C, r, round, c);
+    if (lead) r = list_at(L, 0, nlf, i);
+    else if (any) r = list_at(L, 1, nff, i - nl);
+    const u64 m_any = __ballot(any), m_lead = __ballot(lead);
+    bool ok = false;
+    if (m_any) {
+      constexpr bool SL = RBE_STAGE_LEAD != 0, SF = RBE_STAGE_FOLL != 0;
+      const u64 m_st = (SL ? m_lead : 0ull) | (SF ? m_any & ~m_lead : 0ull);
+      if (SL || SF) {
+        stage_in_wave<N>(P, wrows, r, m_st, SL ? m_lead : 0ull);
+        wave_lds_sync();
+      }
+      if (lead) ok = step_fast<N, TRACE, MODE_LEAD, SL>(P, C, r, round, c, mine);
+      else if (any) ok = step_fast<N, TRACE, MODE_FOLL, SF>(P, C, r, round, c, mine);
+      if (SL || SF) {
+        wave_lds_sync();
+        const u64 m_ok = __ballot(ok) & m_st;
+        stage_out_wave<N>(P, wrows, r, m_ok, SL ? m_ok & m_lead : 0ull);
+        wave_lds_sync();
+      }
     }
-    list_push(L, 2, par, slow, r);
+    list_push(L, 2, par, any && !ok, r);
   }
   flush_counters<KS_FAST_LEAD>(P, c);
 }
@@ -435,7 +572,7 @@ struct rbe_engine {
 };
 
 static constexpr unsigned kFastGrid = 2048;  // persistent grid of k_fast_list
-static constexpr unsigned kFullGrid = 1024;  // persistent grid of k_full_list
+static constexpr unsigned kFullGrid = 256;  // persistent grid of k_full_list: one block per CU (its kernels run 1 wave per SIMD)
 
 static u64 bytes_of(const Params& C, u64* parts) {
   const u64 N = C.n, G = C.n_groups, R = C.n_rep;

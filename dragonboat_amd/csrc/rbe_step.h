@@ -1758,14 +1758,14 @@ template <int N>
 RBE_HD bool triage_lazy(const Planes& P, const Params& C, u64 r, u32 round, u8 ib, bool inbound,
                         StepCounters& ctr) {
   if (!(ib & IB_LAZY) || inbound) return false;
-  const u64 g = r / N;
-  if ((ib & IB_LEAD) && wl_input(C, C.cid_base + g * C.cid_stride, round)) return false;
+  const u32 g = (u32)r / (u32)N;  // replica indices fit u32 (work lists hold u32)
+  if ((ib & IB_LEAD) && wl_input(C, C.cid_base + (u64)g * C.cid_stride, round)) return false;
   if (C.ext_inputs && P.ext[r].kind) return false;
   ctr.v[C_STEPS]++;
   ctr.v[C_QUIESCED_TICKS]++;
   ctr.v[C_LEADER_STEPS] += (ib & IB_LEAD) ? 1u : 0u;
   if (!(ib & IB_H2)) {  // this parity's outbox counts may still be non-zero
-    u16* cnt = &P.cnt[round & 1u][g * N * N + (u32)(r % N) * N];
+    u16* cnt = &P.cnt[round & 1u][(u64)g * (N * N) + ((u32)r - g * (u32)N) * N];
     for (u32 d = 0; d < N; d++) cnt[d] = 0;
   }
   const u8 nb = (u8)((ib & ~(IB_H1 | IB_H2)) | IB_H1 | ((ib & IB_H1) ? IB_H2 : 0));
@@ -1774,22 +1774,30 @@ RBE_HD bool triage_lazy(const Planes& P, const Params& C, u64 r, u32 round, u8 i
 }
 // the inbound count words of replica r in this round: bit 0 = any non-zero
 // word, bit 1 = any message (a Quiesce notice alone leaves it clear), bit 2 =
-// any Replicate
+// any Replicate.  Split in a load phase and a fold so k_triage can issue the
+// words of all its replicas before it waits for any: every word of the
+// replica's column (its own slot included) is loaded unconditionally and the
+// own slot is masked in the fold, so no load sits behind a branch.
 template <int N>
-RBE_HD u32 inbound_bits(const Planes& P, u64 r, u32 round) {
-  if (round == 0) return 0;
-  const u64 g = r / N;
-  const u32 k = (u32)(r % N);
-  const u16* icnt = &P.cnt[(round & 1u) ^ 1u][g * N * N];
+RBE_HD void inbound_load(const Planes& P, u32 g, u32 k, u32 round, u16 (&w)[N]) {
+  const u16* icnt = &P.cnt[(round & 1u) ^ 1u][(u64)g * (N * N) + k];
+  for (u32 s = 0; s < N; s++) w[s] = icnt[s * N];
+}
+template <int N>
+RBE_HD u32 inbound_fold(const u16 (&w)[N], u32 k, u32 round) {
   u32 any = 0;
   for (u32 s = 0; s < N; s++) {
-    if (s == k) continue;
-    const u32 pc = icnt[s * N + k];
-    if (pc) any |= 1u;
-    if (pc & 0x3FFFu) any |= 2u;
-    if (pc & 0x7Fu) any |= 4u;
+    const u32 pc = s == k ? 0u : (u32)w[s];
+    any |= (pc != 0 ? 1u : 0u) | ((pc & 0x3FFFu) != 0 ? 2u : 0u) | ((pc & 0x7Fu) != 0 ? 4u : 0u);
   }
-  return any;
+  return round == 0 ? 0u : any;
+}
+template <int N>
+RBE_HD u32 inbound_bits(const Planes& P, u64 r, u32 round) {
+  const u32 g = (u32)(r / N), k = (u32)(r % N);
+  u16 w[N];
+  inbound_load<N>(P, g, k, round, w);
+  return inbound_fold<N>(w, k, round);
 }
 RBE_HD u32 class_of_role(u32 role) {
   return role == R_Leader ? 1u /*T_LEAD*/ : (role == R_Follower ? 2u /*T_FOLL*/ : 3u /*T_FULL*/);

@@ -1,0 +1,43 @@
+"""Per-kernel VGPRs / scratch / LDS of a built engine library, read from the
+gfx950 code object's metadata notes (no rebuild; scripts/kernel_resources.sh
+is the full --save-temps variant).   python3 scripts/so_resources.py lib.so [filter]"""
+import re
+import subprocess
+import sys
+import tempfile
+
+lib = sys.argv[1]
+flt = sys.argv[2] if len(sys.argv) > 2 else ""
+blob = open(lib, "rb").read()
+i = blob.find(b"__CLANG_OFFLOAD_BUNDLE__")
+if i < 0:
+    sys.exit("no offload bundle in " + lib)
+with tempfile.TemporaryDirectory() as d:
+    fb = f"{d}/fat.bin"
+    open(fb, "wb").write(blob[i:])
+    co = f"{d}/co.o"
+    subprocess.run(["/opt/rocm/lib/llvm/bin/clang-offload-bundler", "--type=o", "--unbundle",
+                    f"--input={fb}", f"--output={co}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950"], check=True)
+    notes = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", co],
+                           capture_output=True, text=True).stdout
+cur = {}
+rows = []
+for line in notes.splitlines():
+    line = line.strip()
+    m = re.match(r"- \.agpr_count:\s+(\d+)", line) or re.match(r"\.agpr_count:\s+(\d+)", line)
+    for key in ("agpr_count", "group_segment_fixed_size", "private_segment_fixed_size",
+                "vgpr_count", "sgpr_count", "name"):
+        mm = re.match(r"-?\s*\." + key + r":\s+(\S+)", line)
+        if mm:
+            if key == "agpr_count" and cur:
+                rows.append(cur)
+                cur = {}
+            cur[key] = mm.group(1)
+if cur:
+    rows.append(cur)
+for r in rows:
+    n = r.get("name", "?")
+    if flt in n:
+        print(f"vgpr {r.get('vgpr_count'):>4} agpr {r.get('agpr_count'):>3} scratch "
+              f"{r.get('private_segment_fixed_size'):>5} lds {r.get('group_segment_fixed_size'):>6}  {n}")

@@ -25,6 +25,7 @@ def lib():
         L.soa_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         L.soa_views.argtypes = [C.c_void_p, C.c_void_p]
         L.soa_set_full_only.argtypes = [C.c_void_p, C.c_int]
+        L.soa_set_staged.argtypes = [C.c_void_p, C.c_int]
         L.soa_slow_total.restype = C.c_uint64
         L.soa_slow_total.argtypes = [C.c_void_p]
         L.soa_faults.restype = C.c_uint32
@@ -39,13 +40,14 @@ def lib():
 
 
 class SoaCpu:
-    def __init__(self, full_only=False, **kw):
+    def __init__(self, full_only=False, staged=False, **kw):
         self.cfg = make_config(**kw)
         self.n_rep = self.cfg.n_groups * self.cfg.n_replicas
         self.h = lib().soa_create(C.byref(self.cfg))
         if not self.h:
             raise RuntimeError("soa_create failed")
         lib().soa_set_full_only(self.h, int(full_only))
+        lib().soa_set_staged(self.h, int(staged))
 
     def slow_total(self):
         return lib().soa_slow_total(self.h)

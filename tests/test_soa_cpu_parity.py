@@ -16,11 +16,14 @@ CASES = {"C1": (C1, 400), "C2": (C2, 300), "C3": (C3, 400), "C3_HOT": (C3_HOT, 4
          "MIXED": (MIXED, 600)}
 
 
-@pytest.mark.parametrize("full_only", [False, True], ids=["pipeline", "full_table"])
+@pytest.mark.parametrize("mode", ["pipeline", "full_table", "staged"])
 @pytest.mark.parametrize("name", list(CASES))
-def test_soa_cpu_lockstep_parity(name, full_only):
+def test_soa_cpu_lockstep_parity(name, mode):
+    """`staged`: the fast steps read and write a staged row (StageRow), as
+    k_fast_both runs them when built with RBE_STAGE_LEAD / RBE_STAGE_FOLL."""
     kw, rounds = CASES[name]
-    eng = SoaCpu(full_only=full_only, trace=True, **kw, **ENGINE_EXTRA.get(name, {}))
+    eng = SoaCpu(full_only=mode == "full_table", staged=mode == "staged", trace=True, **kw,
+                 **ENGINE_EXTRA.get(name, {}))
     ref = O.Harness(**kw)
     d = run_lockstep(eng, ref, rounds, every=1)
     assert d is None, f"{name}: first divergence {d}"
