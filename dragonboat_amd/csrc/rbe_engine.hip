@@ -40,12 +40,13 @@ static constexpr int kBlock = 256;
 #ifndef RBE_TRI_CHUNK
 #define RBE_TRI_CHUNK 2048
 #endif
-// which fast steps work on wave-staged rows (k_fast_both, stage_in_wave)
+// how the fast steps of k_fast_both use wave-staged rows (StageRow, rbe_fast.h):
+// 0 = direct, 1 = STG_OUT (row writes staged), 3 = STG_OUT | STG_IN
 #ifndef RBE_STAGE_LEAD
-#define RBE_STAGE_LEAD 0
+#define RBE_STAGE_LEAD 1
 #endif
 #ifndef RBE_STAGE_FOLL
-#define RBE_STAGE_FOLL 0
+#define RBE_STAGE_FOLL 1
 #endif
 static constexpr u32 kTriChunk = RBE_TRI_CHUNK;   // replicas per k_triage block (8 per lane)
 static constexpr int kCtrStripes = 64;   // counter stripes per kernel slot (flush_counters)
@@ -170,7 +171,6 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, const u32
   // or a 64-bit division, so all 8 * (N + 1) loads of a lane are in flight
   // before the first wait.
   u8 ibs[kPer];
-  u32 inb[kPer];
   u16 wv[kPer][N];
   u32 kk[kPer];
 #pragma unroll
@@ -182,23 +182,30 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, const u32
     kk[i] = rc - g * (u32)N;
     inbound_load<N>(P, g, kk[i], round, wv[i]);
   }
+  // the per-replica bytes packed into two registers, so the classification
+  // loop below runs rolled (one copy of triage_lazy / triage_replica in the
+  // instruction stream instead of kPer) without indexing a register array
+  u64 ibp = 0;
+  u32 inbp = 0;
 #pragma unroll
   for (u32 i = 0; i < kPer; i++) {
     const u64 r = lo + (u64)i * kBlock;
     const bool in = r < C.n_rep;
-    ibs[i] = in ? ibs[i] : (u8)0;
-    inb[i] = in ? inbound_fold<N>(wv[i], kk[i], round) : 0u;
+    ibp |= (u64)(in ? ibs[i] : (u8)0) << (8 * i);
+    inbp |= (in ? inbound_fold<N>(wv[i], kk[i], round) : 0u) << (3 * i);
   }
   const bool shortcut = !TRACE && C.quiesce;
-#pragma unroll
+#pragma unroll 1
   for (u32 i = 0; i < kPer; i++) {
     const u64 r = lo + (u64)i * kBlock;
+    const u8 ib = (u8)(ibp >> (8 * i));
+    const u32 inb = (inbp >> (3 * i)) & 7u;
     u32 cls = T_DONE;
     if (r < C.n_rep && owned<N>(C, r)) {
-      if (shortcut && triage_lazy<N>(P, C, r, round, ibs[i], inb[i] & 1u, c))
+      if (shortcut && triage_lazy<N>(P, C, r, round, ib, inb & 1u, c))
         cls = T_DONE;
-      else if (inb[i] & 2u)
-        cls = class_of_role(idle_role(ibs[i]));
+      else if (inb & 2u)
+        cls = class_of_role(idle_role(ib));
       else
         cls = triage_replica<N, TRACE>(P, C, r, round, c);
     }
@@ -208,7 +215,7 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, const u32
     if (cls == T_LEAD)
       back = wl_input(C, C.cid_base + (u64)((u32)r / (u32)N) * C.cid_stride, round) == 1u;
     else if (cls == T_FOLL)
-      back = (inb[i] & 4u) != 0;
+      back = (inb & 4u) != 0;
 #pragma unroll
     for (u32 sl = 0; sl < 5; sl++) {  // slots: fronts 0..2, backs of lists 0..1
       const u32 li = sl < 3 ? sl : sl - 3;
@@ -450,17 +457,18 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, 
     const u64 m_any = __ballot(any), m_lead = __ballot(lead);
     bool ok = false;
     if (m_any) {
-      constexpr bool SL = RBE_STAGE_LEAD != 0, SF = RBE_STAGE_FOLL != 0;
-      const u64 m_st = (SL ? m_lead : 0ull) | (SF ? m_any & ~m_lead : 0ull);
-      if (SL || SF) {
-        stage_in_wave<N>(P, wrows, r, m_st, SL ? m_lead : 0ull);
+      constexpr int SL = RBE_STAGE_LEAD, SF = RBE_STAGE_FOLL;
+      const u64 m_in = ((SL & STG_IN) ? m_lead : 0ull) | ((SF & STG_IN) ? m_any & ~m_lead : 0ull);
+      const u64 m_out = (SL ? m_lead : 0ull) | (SF ? m_any & ~m_lead : 0ull);
+      if ((SL | SF) & STG_IN) {
+        stage_in_wave<N>(P, wrows, r, m_in, (SL & STG_IN) ? m_lead : 0ull);
         wave_lds_sync();
       }
       if (lead) ok = step_fast<N, TRACE, MODE_LEAD, SL>(P, C, r, round, c, mine);
       else if (any) ok = step_fast<N, TRACE, MODE_FOLL, SF>(P, C, r, round, c, mine);
       if (SL || SF) {
         wave_lds_sync();
-        const u64 m_ok = __ballot(ok) & m_st;
+        const u64 m_ok = __ballot(ok) & m_out;
         stage_out_wave<N>(P, wrows, r, m_ok, SL ? m_ok & m_lead : 0ull);
         wave_lds_sync();
       }
@@ -572,7 +580,7 @@ struct rbe_engine {
 };
 
 static constexpr unsigned kFastGrid = 2048;  // persistent grid of k_fast_list
-static constexpr unsigned kFullGrid = 256;  // persistent grid of k_full_list: one block per CU (its kernels run 1 wave per SIMD)
+static constexpr unsigned kFullGrid = 512;  // persistent grid of k_full_list: 2 waves per SIMD, its kernels' occupancy cap
 
 static u64 bytes_of(const Params& C, u64* parts) {
   const u64 N = C.n, G = C.n_groups, R = C.n_rep;

@@ -80,13 +80,16 @@ struct FastCaps {
 };
 
 // Wave-cooperative staging of a lane's state rows (k_fast_both).
-// The whole wave moves the rows a fast step reads and rewrites whole between
-// HBM and LDS: four lanes per 64-B row, so a wave instruction touches 16 rows
-// instead of 64 scattered ones (a quarter of the TA work and of the L2 write
-// requests).  A STAGED step reads its Hot/Core/remote slots from the row and
-// writes Hot/Core/Upd/remote slots back to it; k_fast_both writes the rows of
-// the lanes whose step completed.  The host build stages one row at a time
+// Every lane writes its Hot/Core/Upd/remote rows whole at the end of a fast
+// step, each with 2-4 scattered 16-B stores, i.e. one L2 write request per
+// store and lane.  With STG_OUT the step writes those rows into its LDS row
+// instead and the whole wave writes them out afterwards, four lanes per 64-B
+// row (stage_out_wave), so one wave instruction makes 16 full-row requests
+// instead of 64 partial ones.  STG_IN also takes the step's Hot/Core/remote
+// reads from the row, loaded the same way before the step (measured slower:
+// it adds a dependent load level).  The host build stages one row at a time
 // (stage_row_in/out) so the CPU tier runs the same step code.
+enum : int { STG_OUT = 1, STG_IN = 2 };  // which side of a fast step uses the staged row
 template <int N>
 struct alignas(16) StageRow {
   Core core;
@@ -330,7 +333,7 @@ struct FastQ {
 // Common epilogue: stepNode's quiesce send, getUpdate/Commit, the trace digest,
 // the Update record, this round's outbox counts, Hot/Core write-back.
 // Mirrors the tail of Lane::run().
-template <int N, bool TRACE, bool STAGED = false>
+template <int N, bool TRACE, int STG = 0>
 RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, FastOut<N, TRACE>& o,
                         FastQ& q, u8 role, u8 flags, Hot h, Core c, u32 etick, u32 htick,
                         u64 committed0, u64 digest0, StageRow<N>* sr = nullptr) {
@@ -430,7 +433,7 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
   u.round = o.round_;
   u.pad2 = 0;
 #ifndef RBE_DIAG_NO_STATE_STORES
-  if constexpr (STAGED) sr->upd = u;
+  if constexpr ((STG & STG_OUT) != 0) sr->upd = u;
   else P.upd[r] = u;
   u16* cnt = &P.cnt[o.par][o.g * N * N + o.k * N];
 #pragma unroll
@@ -442,7 +445,7 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
   h.q_quiesced_since = q.qs;
   h.q_no_activity_since = q.nas;
   h.q_exit_quiesce_tick = q.eqt;
-  if constexpr (STAGED) {
+  if constexpr ((STG & STG_OUT) != 0) {
     sr->hot = h;
     sr->core = c;
   } else {
@@ -459,7 +462,7 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
 //   inbox (ascending sender; Quiesce marker, then the sender's messages) →
 //   local ReadIndex → tick → proposal, each followed by the deferred fan-out
 //   (Replicate sends in ascending slot order, heartbeats, readIndex confirm).
-template <int N, bool TRACE, bool STAGED = false>
+template <int N, bool TRACE, int STG = 0>
 RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCounters& ctr,
                       StageRow<N>* sr = nullptr) {
   using Cap = FastCaps<N>;
@@ -476,7 +479,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   RBE_STAMP(t0);
   Hot h;
   Core c;
-  if constexpr (STAGED) {
+  if constexpr ((STG & STG_IN) != 0) {
     h = materialize_hot(sr->hot, C, round);
     c = sr->core;
   } else {
@@ -488,7 +491,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
 #pragma unroll
   for (u32 s = 0; s < N; s++) {
     RemoteMN x;
-    if constexpr (STAGED) x = sr->rem[s];
+    if constexpr ((STG & STG_IN) != 0) x = sr->rem[s];
     else x = P.rem[r * N + s];
     match[s] = x.match;
     next[s] = x.next;
@@ -1045,7 +1048,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
     RemoteMN x;
     x.match = match[s];
     x.next = next[s];
-    if constexpr (STAGED) sr->rem[s] = x;
+    if constexpr ((STG & STG_OUT) != 0) sr->rem[s] = x;
     else P.rem[r * N + s] = x;
     P.rem_st[r * N + s] = (u8)st[s];
   }
@@ -1066,7 +1069,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   }
   c.rq_head = (u8)rq_h;
   c.rq_count = (u8)rq_n;
-  fast_finish<N, TRACE, STAGED>(P, C, ctr, o, q, R_Leader, flags, h, c, etick, htick, committed0,
+  fast_finish<N, TRACE, STG>(P, C, ctr, o, q, R_Leader, flags, h, c, etick, htick, committed0,
                                 digest0, sr);
   RBE_STAMP(t5);
   RBE_RSTAMP(rt5);
@@ -1086,7 +1089,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
 // One steady-state follower round: inbox from the known leader only
 // (Replicate / Heartbeat / ReadIndexResp of the current term), no client
 // input, a tick that does not start an election.
-template <int N, bool TRACE, bool STAGED = false>
+template <int N, bool TRACE, int STG = 0>
 RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCounters& ctr,
                       StageRow<N>* sr = nullptr) {
   using Cap = FastCaps<N>;
@@ -1101,7 +1104,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   RBE_STAMP(t0);
   Hot h;
   Core c;
-  if constexpr (STAGED) {
+  if constexpr ((STG & STG_IN) != 0) {
     h = materialize_hot(sr->hot, C, round);
     c = sr->core;
   } else {
@@ -1360,7 +1363,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
     if (etick >= h.rand_et) o.set_fault(ctr, F_UNSUPPORTED);
   }
   c.leader = n_in ? (u8)lid : c.leader;
-  fast_finish<N, TRACE, STAGED>(P, C, ctr, o, q, R_Follower, flags, h, c, etick, htick, committed0,
+  fast_finish<N, TRACE, STG>(P, C, ctr, o, q, R_Follower, flags, h, c, etick, htick, committed0,
                         digest0, sr);
   RBE_STAMP(t5);
   RBE_RSTAMP(rt5);
@@ -1376,11 +1379,11 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
 }
 
 // the fast step of one role (k_round, k_fast_list)
-template <int N, bool TRACE, int MODE, bool STAGED = false>
+template <int N, bool TRACE, int MODE, int STG = 0>
 RBE_HD bool step_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCounters& ctr,
                       StageRow<N>* sr = nullptr) {
-  if constexpr (MODE == MODE_LEAD) return lead_fast<N, TRACE, STAGED>(P, C, r, round, ctr, sr);
-  else return foll_fast<N, TRACE, STAGED>(P, C, r, round, ctr, sr);
+  if constexpr (MODE == MODE_LEAD) return lead_fast<N, TRACE, STG>(P, C, r, round, ctr, sr);
+  else return foll_fast<N, TRACE, STG>(P, C, r, round, ctr, sr);
 }
 
 }  // namespace rbe

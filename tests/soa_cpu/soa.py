@@ -40,7 +40,7 @@ def lib():
 
 
 class SoaCpu:
-    def __init__(self, full_only=False, staged=False, **kw):
+    def __init__(self, full_only=False, staged=0, **kw):
         self.cfg = make_config(**kw)
         self.n_rep = self.cfg.n_groups * self.cfg.n_replicas
         self.h = lib().soa_create(C.byref(self.cfg))

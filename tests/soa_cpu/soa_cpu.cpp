@@ -21,7 +21,7 @@ struct SoaEngine {
   u32 round = 0;
   u64 counters[C_NUM] = {0};
   bool full_only = false;
-  bool staged = false;  // fast steps on a staged row (StageRow, as k_fast_both may run them)
+  int staged = 0;  // STG_* bits: fast steps on a staged row (StageRow), as k_fast_both runs them
   u64 slow_total = 0;
 };
 
@@ -61,16 +61,26 @@ static void run_round(SoaEngine* e) {
     for (u64 r : lists[li]) {
       memset(&c, 0, sizeof(c));
       bool ok;
-      if (e->staged) {
+      if (e->staged == (STG_OUT | STG_IN)) {
         StageRow<N> row;
         memset(&row, 0xA5, sizeof(row));  // nothing the step reads may come from here unset
         stage_row_in<N>(e->P, r, li == 0, row);
         if (li == 0)
-          ok = e->C.trace ? step_fast<N, true, MODE_LEAD, true>(e->P, e->C, r, e->round, c, &row)
-                          : step_fast<N, false, MODE_LEAD, true>(e->P, e->C, r, e->round, c, &row);
+          ok = e->C.trace ? step_fast<N, true, MODE_LEAD, 3>(e->P, e->C, r, e->round, c, &row)
+                          : step_fast<N, false, MODE_LEAD, 3>(e->P, e->C, r, e->round, c, &row);
         else
-          ok = e->C.trace ? step_fast<N, true, MODE_FOLL, true>(e->P, e->C, r, e->round, c, &row)
-                          : step_fast<N, false, MODE_FOLL, true>(e->P, e->C, r, e->round, c, &row);
+          ok = e->C.trace ? step_fast<N, true, MODE_FOLL, 3>(e->P, e->C, r, e->round, c, &row)
+                          : step_fast<N, false, MODE_FOLL, 3>(e->P, e->C, r, e->round, c, &row);
+        if (ok) stage_row_out<N>(e->P, r, li == 0, row);
+      } else if (e->staged == STG_OUT) {
+        StageRow<N> row;
+        memset(&row, 0xA5, sizeof(row));
+        if (li == 0)
+          ok = e->C.trace ? step_fast<N, true, MODE_LEAD, 1>(e->P, e->C, r, e->round, c, &row)
+                          : step_fast<N, false, MODE_LEAD, 1>(e->P, e->C, r, e->round, c, &row);
+        else
+          ok = e->C.trace ? step_fast<N, true, MODE_FOLL, 1>(e->P, e->C, r, e->round, c, &row)
+                          : step_fast<N, false, MODE_FOLL, 1>(e->P, e->C, r, e->round, c, &row);
         if (ok) stage_row_out<N>(e->P, r, li == 0, row);
       } else if (li == 0) {
         ok = e->C.trace ? step_fast<N, true, MODE_LEAD>(e->P, e->C, r, e->round, c)
@@ -165,7 +175,7 @@ void* soa_create(const rbe_config* cfg) {
 
 void soa_destroy(void* h) { delete (SoaEngine*)h; }
 void soa_set_full_only(void* h, int v) { ((SoaEngine*)h)->full_only = v != 0; }
-void soa_set_staged(void* h, int v) { ((SoaEngine*)h)->staged = v != 0; }
+void soa_set_staged(void* h, int v) { ((SoaEngine*)h)->staged = v; }
 uint64_t soa_slow_total(void* h) { return ((SoaEngine*)h)->slow_total; }
 
 void soa_run(void* h, uint32_t rounds) {
