@@ -43,10 +43,10 @@ static constexpr int kBlock = 256;
 // how the fast steps of k_fast_both use wave-staged rows (StageRow, rbe_fast.h):
 // 0 = direct, 1 = STG_OUT (row writes staged), 3 = STG_OUT | STG_IN
 #ifndef RBE_STAGE_LEAD
-#define RBE_STAGE_LEAD 1
+#define RBE_STAGE_LEAD 0
 #endif
 #ifndef RBE_STAGE_FOLL
-#define RBE_STAGE_FOLL 1
+#define RBE_STAGE_FOLL 0
 #endif
 static constexpr u32 kTriChunk = RBE_TRI_CHUNK;   // replicas per k_triage block (8 per lane)
 static constexpr int kCtrStripes = 64;   // counter stripes per kernel slot (flush_counters)
@@ -466,7 +466,7 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, 
       }
       if (lead) ok = step_fast<N, TRACE, MODE_LEAD, SL>(P, C, r, round, c, mine);
       else if (any) ok = step_fast<N, TRACE, MODE_FOLL, SF>(P, C, r, round, c, mine);
-      if (SL || SF) {
+      if constexpr ((SL | SF) != 0) {
         wave_lds_sync();
         const u64 m_ok = __ballot(ok) & m_out;
         stage_out_wave<N>(P, wrows, r, m_ok, SL ? m_ok & m_lead : 0ull);
@@ -1107,11 +1107,10 @@ int rbe_xchg_pack(rbe_engine* e, void* buf, const uint64_t* cap3, uint32_t* coun
   return RBE_OK;
 }
 
-int rbe_xchg_unpack(rbe_engine* e, const void* cnt, uint64_t n_cnt, const void* msg, uint64_t n_msg,
-                    const void* ent, uint64_t n_ent) {
-  if (!e || e->round == 0) return RBE_E_INVALID;
-  if (e->C.rep_world <= 1) return RBE_E_STATE;
-  HIP_OK(hipSetDevice(e->device));
+// clear the remote senders' count words of the last round's parity, then
+// scatter exchange records (device pointers) into the planes
+static int xchg_scatter(rbe_engine* e, const void* cnt, uint64_t n_cnt, const void* msg,
+                        uint64_t n_msg, const void* ent, uint64_t n_ent) {
   const u32 par = (e->round - 1) & 1u;
   int rc = dispatch_n(e->C.n, [&](auto NN) {
     constexpr int N = decltype(NN)::value;
@@ -1133,6 +1132,66 @@ int rbe_xchg_unpack(rbe_engine* e, const void* cnt, uint64_t n_cnt, const void* 
   HIP_OK(hipGetLastError());
   HIP_OK(hipStreamSynchronize(e->stream));
   return RBE_OK;
+}
+
+int rbe_xchg_unpack(rbe_engine* e, const void* cnt, uint64_t n_cnt, const void* msg, uint64_t n_msg,
+                    const void* ent, uint64_t n_ent) {
+  if (!e || e->round == 0) return RBE_E_INVALID;
+  if (e->C.rep_world <= 1) return RBE_E_STATE;
+  HIP_OK(hipSetDevice(e->device));
+  return xchg_scatter(e, cnt, n_cnt, msg, n_msg, ent, n_ent);
+}
+
+int rbe_get_outbox(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t cap,
+                   uint32_t* n_out, rbe_entry* ents, uint32_t ent_cap, uint32_t* n_ents) {
+  if (!e || !n_out || !n_ents || replica >= e->C.n_rep || e->round == 0) return RBE_E_INVALID;
+  HIP_OK(hipSetDevice(e->device));
+  const u32 N = e->C.n, par = (e->round - 1) & 1u;
+  const u64 g = replica / N;
+  const u32 k = (u32)(replica % N);
+  std::vector<u16> cnt(N);
+  std::vector<Msg> lst((size_t)N * e->C.maxm);
+  std::vector<Ent> arena(e->C.ecap);
+  HIP_OK(hipMemcpyAsync(cnt.data(), e->P.cnt[par] + g * N * N + k * N, N * sizeof(u16),
+                        hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipMemcpyAsync(lst.data(), e->P.msgs[par] + (g * N + k) * N * (u64)e->C.maxm,
+                        lst.size() * sizeof(Msg), hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipMemcpyAsync(arena.data(), e->P.arena[par] + replica * e->C.ecap,
+                        arena.size() * sizeof(Ent), hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return dispatch_n(N, [&](auto NN) {
+    constexpr int NC = decltype(NN)::value;
+    outbox_messages<NC>(e->C, g, k, cnt.data(), lst.data(), arena.data(), out, cap, ents, ent_cap,
+                        n_out, n_ents);
+    return RBE_OK;
+  });
+}
+
+int rbe_push_messages(rbe_engine* e, uint64_t n, const uint64_t* group, const rbe_message* msgs,
+                      const rbe_entry* ents) {
+  if (!e || e->round == 0 || (n && (!group || !msgs))) return RBE_E_INVALID;
+  if (e->C.rep_world <= 1) return RBE_E_STATE;  // every sender is stepped here
+  HIP_OK(hipSetDevice(e->device));
+  std::vector<XCnt> c;
+  std::vector<XMsg> m;
+  std::vector<XEnt> x;
+  int rc = dispatch_n(e->C.n, [&](auto NN) {
+    constexpr int N = decltype(NN)::value;
+    return messages_to_records<N>(e->C, n, group, msgs, ents, c, m, x);
+  });
+  if (rc) return rc;
+  const size_t bytes = c.size() * sizeof(XCnt) + m.size() * sizeof(XMsg) + x.size() * sizeof(XEnt);
+  u8* d = nullptr;
+  if (bytes) HIP_OK(hipMalloc(&d, bytes));
+  const size_t om = c.size() * sizeof(XCnt), ox = om + m.size() * sizeof(XMsg);
+  if (!c.empty()) HIP_OK(hipMemcpyAsync(d, c.data(), om, hipMemcpyHostToDevice, e->stream));
+  if (!m.empty())
+    HIP_OK(hipMemcpyAsync(d + om, m.data(), ox - om, hipMemcpyHostToDevice, e->stream));
+  if (!x.empty())
+    HIP_OK(hipMemcpyAsync(d + ox, x.data(), bytes - ox, hipMemcpyHostToDevice, e->stream));
+  rc = xchg_scatter(e, d, c.size(), d + om, m.size(), d + ox, x.size());
+  if (d) HIP_IGNORE(hipFree(d));
+  return rc;
 }
 
 int rbe_kernel_name(const rbe_engine* e, int32_t kernel, char* buf, uint32_t cap) {

@@ -12,7 +12,10 @@
 // (no record) reads as an empty list.  Record order is irrelevant: every
 // record names its destination slot.
 #pragma once
-#include "rbe_step.h"
+#include "rbe_fast.h"
+#include "../../include/rbe.h"
+#include <unordered_map>
+#include <vector>
 
 namespace rbe {
 
@@ -133,6 +136,172 @@ RBE_HD void xchg_put_msg(const Planes& P, const Params& C, u32 par, const XMsg& 
 }
 RBE_HD void xchg_put_ent(const Planes& P, const Params& C, u32 par, const XEnt& x) {
   P.arena[par][x.key * C.ecap + x.off] = x.e;
+}
+
+// ------------------------------------------------ transport boundary (host)
+// rbe_get_outbox / rbe_push_messages: the messages of one round in raftpb
+// shape (rbe_message + rbe_entry), for replicas whose peers are stepped by
+// another engine (another rank, or another host behind dragonboat's own
+// transport).  Both directions reuse the exchange records above, so a pushed
+// message lands in exactly the plane slot the sender's own step would have
+// written.
+
+// Sender replica r = g * N + k's messages of parity `par` as the transport
+// sees them, destination by destination in ascending node id, each stream in
+// the order the receiving step handles it (node.go:1030-1067 with the
+// lockstep ordering of DESIGN.md §2): the Quiesce notice (node.go:873-886),
+// Replicate messages (sent before persistence, node.go:897-905), the rest.
+// A Replicate's entries follow in `ents` (rbe_message.n_entries of them,
+// Index = LogIndex + 1 + i).  cnt_row = the N count words of (g, k, *),
+// lst = the N * maxm message slots of (g, k, *), arena = the sender's ecap
+// arena entries, all host copies.  Counts beyond the capacities are reported
+// in *n_msg / *n_ent and not written.
+template <int N>
+void outbox_messages(const Params& C, u64 g, u32 k, const u16* cnt_row, const Msg* lst,
+                     const Ent* arena, rbe_message* out, u32 cap, rbe_entry* ents, u32 ent_cap,
+                     u32* n_msg, u32* n_ent) {
+  const u64 cid = C.cid_base + g * C.cid_stride;
+  u32 n = 0, ne = 0;
+  auto emit = [&](const Msg& m, u32 type, u32 to) {
+    if (n < cap && out) {
+      rbe_message& o = out[n];
+      o = rbe_message{};
+      o.type = type;
+      o.reject = m.reject;
+      o.to = to;
+      o.from = k + 1;
+      o.cluster_id = cid;
+      o.term = m.term;
+      o.log_term = m.log_term;
+      o.log_index = m.log_index;
+      o.commit = m.commit;
+      o.hint = m.hint;
+      o.hint_high = m.hint_high;
+      o.n_entries = type == M_Replicate ? m.n_ent : 0u;
+    }
+    n++;
+  };
+  for (u32 d = 0; d < N; d++) {
+    const u32 pc = cnt_row[d], na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
+    if (pc & 0x8000u) {
+      Msg q = mk_msg(M_Quiesce, d + 1);
+      emit(q, M_Quiesce, d + 1);
+    }
+    for (u32 i = 0; i < na + nb; i++) {
+      const Msg& m = i < na ? lst[d * C.maxm + i] : lst[d * C.maxm + C.maxm - 1u - (i - na)];
+      emit(m, m.type, d + 1);
+      if (m.type != M_Replicate) continue;
+      for (u32 j = 0; j < m.n_ent; j++) {
+        if (ents && ne < ent_cap && m.ent_off + j < C.ecap) {
+          const Ent& x = arena[m.ent_off + j];
+          rbe_entry& e = ents[ne];
+          e = rbe_entry{};
+          e.index = m.log_index + 1 + j;
+          e.term = x.term;
+          e.type = x.type;
+          e.cmd_len = x.len;
+          for (u32 b = 0; b < 8; b++) {
+            e.cmd[b] = (u8)(x.lo >> (8 * b));
+            e.cmd[8 + b] = (u8)(x.hi >> (8 * b));
+          }
+        }
+        ne++;
+      }
+    }
+  }
+  *n_msg = n;
+  *n_ent = ne;
+}
+
+// The inverse for one round's inbound batch: message i of group group[i]
+// from node msgs[i].from (a replica this engine does not step) to node
+// msgs[i].to (one it does), carrying msgs[i].n_entries entries taken in order
+// from `ents`.  Per (sender, destination) the Replicate messages keep their
+// order in the A list, the others in the B list, and a Quiesce message sets
+// the notice bit, exactly the layout a local sender's step writes.  The
+// records cover every list named; lists not named stay empty after the
+// unpack's clear.  Returns RBE_OK, RBE_E_INVALID (ids, ownership, entry
+// indexes) or RBE_E_NOMEM (more than maxm messages in one list, or more
+// than ecap entries from one sender).
+template <int N>
+int messages_to_records(const Params& C, u64 n, const u64* group, const rbe_message* msgs,
+                        const rbe_entry* ents, std::vector<XCnt>& oc, std::vector<XMsg>& om,
+                        std::vector<XEnt>& oe) {
+  std::unordered_map<u64, u32> words;  // list key → count word
+  std::vector<u64> order;              // list keys in first-use order
+  std::unordered_map<u64, u32> used;   // sender replica → arena entries used
+  u64 ei = 0;
+  for (u64 i = 0; i < n; i++) {
+    const rbe_message& m = msgs[i];
+    const u64 g = group[i];
+    if (g >= C.n_groups || m.from < 1 || m.from > N || m.to < 1 || m.to > N || m.from == m.to)
+      return RBE_E_INVALID;
+    const u32 s = (u32)m.from - 1u, d = (u32)m.to - 1u;
+    if (owner_of<N>(C, g, s) == C.rep_rank || owner_of<N>(C, g, d) != C.rep_rank)
+      return RBE_E_INVALID;
+    const u64 key = (g * N + s) * N + d;
+    auto it = words.find(key);
+    if (it == words.end()) {
+      it = words.emplace(key, 0u).first;
+      order.push_back(key);
+    }
+    u32& w = it->second;
+    if (m.type == M_Quiesce) {
+      w |= 0x8000u;
+      continue;
+    }
+    if (m.type >= 26 || (m.n_entries && m.type != M_Replicate)) return RBE_E_INVALID;
+    const u32 na = w & 0x7Fu, nb = (w >> 7) & 0x7Fu;
+    if (na + nb >= C.maxm) return RBE_E_NOMEM;
+    XMsg x;
+    x.key = key;
+    x.m = mk_msg(m.type, m.to);
+    x.m.from = (u8)m.from;
+    x.m.reject = (u8)(m.reject ? 1 : 0);
+    x.m.term = m.term;
+    x.m.log_term = m.log_term;
+    x.m.log_index = m.log_index;
+    x.m.commit = m.commit;
+    x.m.hint = m.hint;
+    x.m.hint_high = m.hint_high;
+    if (m.type == M_Replicate) {
+      x.slot = na;
+      w += 1u;
+      const u64 sr = g * N + s;
+      u32& off = used[sr];
+      if (m.n_entries > 0xFFFFu || off + m.n_entries > C.ecap) return RBE_E_NOMEM;
+      x.m.n_ent = (u16)m.n_entries;
+      x.m.ent_off = off;
+      for (u32 j = 0; j < m.n_entries; j++, ei++) {
+        const rbe_entry& e = ents[ei];
+        if (e.index != m.log_index + 1 + j || e.cmd_len > 16) return RBE_E_INVALID;
+        XEnt y;
+        y.key = sr;
+        y.off = off + j;
+        y.e.term = e.term;
+        y.e.type = e.type;
+        y.e.len = e.cmd_len;
+        y.e.lo = y.e.hi = 0;
+        for (u32 b = 0; b < 8; b++) {
+          y.e.lo |= (u64)e.cmd[b] << (8 * b);
+          y.e.hi |= (u64)e.cmd[8 + b] << (8 * b);
+        }
+        oe.push_back(y);
+      }
+      off += m.n_entries;
+    } else {
+      x.slot = C.maxm - 1u - nb;
+      w += 1u << 7;
+    }
+    om.push_back(x);
+  }
+  for (u64 key : order) {
+    XCnt c;
+    c.key = key;
+    c.word = words[key];
+    oc.push_back(c);
+  }
+  return RBE_OK;
 }
 
 }  // namespace rbe

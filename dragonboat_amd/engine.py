@@ -91,7 +91,8 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_step", "rbe_run"
            "rbe_get_updates", "rbe_get_messages", "rbe_get_ready_to_reads", "rbe_get_entries",
            "rbe_get_views", "rbe_get_counters", "rbe_reset_counters", "rbe_fault_summary",
            "rbe_footprint", "rbe_profile_rounds", "rbe_get_kernel_counters", "rbe_kernel_name",
-           "rbe_xchg_record_bytes", "rbe_xchg_pack", "rbe_xchg_unpack"]
+           "rbe_xchg_record_bytes", "rbe_xchg_pack", "rbe_xchg_unpack", "rbe_get_outbox",
+           "rbe_push_messages"]
 KERNEL_SLOTS = 4
 
 _lib = None
@@ -131,6 +132,8 @@ def load_library(path: Optional[str] = None):
         "rbe_push_read_index": (i32, [vp, u64, P(u64), P(u64), P(u64)]),
         "rbe_get_updates": (i32, [vp, u64, u64, P(RbeUpdate)]),
         "rbe_get_messages": (i32, [vp, u64, P(RbeMessage), u32, P(u32)]),
+        "rbe_get_outbox": (i32, [vp, u64, P(RbeMessage), u32, P(u32), P(RbeEntry), u32, P(u32)]),
+        "rbe_push_messages": (i32, [vp, u64, P(u64), P(RbeMessage), P(RbeEntry)]),
         "rbe_get_ready_to_reads": (i32, [vp, u64, P(RbeReadyToRead), u32, P(u32)]),
         "rbe_get_entries": (i32, [vp, u64, u64, u64, P(RbeEntry)]),
         "rbe_get_views": (i32, [vp, u64, u64, P(RbeReplicaView)]),
@@ -328,6 +331,26 @@ class Engine:
         _check(self.lib.rbe_get_messages(self.h, replica, arr, cap, C.byref(n)),
                "rbe_get_messages")
         return [arr[i] for i in range(min(n.value, cap))]
+
+    def outbox(self, replica: int, cap: int = 256, ent_cap: int = 1024):
+        """The last round's messages of `replica` in transport order, with the
+        entries of its Replicate messages (rbe_get_outbox)."""
+        arr = (RbeMessage * cap)()
+        ents = (RbeEntry * ent_cap)()
+        n, ne = C.c_uint32(), C.c_uint32()
+        _check(self.lib.rbe_get_outbox(self.h, replica, arr, cap, C.byref(n), ents, ent_cap,
+                                       C.byref(ne)), "rbe_get_outbox")
+        if n.value > cap or ne.value > ent_cap:
+            raise EngineError(f"outbox of {replica}: {n.value} messages / {ne.value} entries")
+        return [arr[i] for i in range(n.value)], [ents[i] for i in range(ne.value)]
+
+    def push_messages(self, groups, msgs, ents):
+        """Deliver one round's inbound batch from remote senders (rbe_push_messages)."""
+        n = len(msgs)
+        g = (C.c_uint64 * max(1, n))(*groups)
+        m = (RbeMessage * max(1, n))(*msgs)
+        e = (RbeEntry * max(1, len(ents)))(*ents)
+        _check(self.lib.rbe_push_messages(self.h, n, g, m, e), "rbe_push_messages")
 
     def ready_to_reads(self, replica: int):
         cap = 64

@@ -248,6 +248,27 @@ int rbe_xchg_pack(rbe_engine* e, void* buf, const uint64_t* cap3, uint32_t* coun
 int rbe_xchg_unpack(rbe_engine* e, const void* cnt_recs, uint64_t n_cnt, const void* msg_recs,
                     uint64_t n_msg, const void* ent_recs, uint64_t n_ent);
 
+/* Transport boundary for replicas whose peers another engine steps (cfg.rep_world > 1:
+ * the replicas of other ranks, or of other hosts behind dragonboat's transport).
+ *   rbe_get_outbox: sender `replica`'s messages of the last round in raftpb form,
+ *     per destination in ascending node id: the Quiesce notice (node.go:873-886),
+ *     Replicate messages, the rest; each Replicate's entries follow in `ents`
+ *     (n_entries of them).  Replaces reading Update.Messages for the transport
+ *     (node.go:888-905 → nodehost.go:1724 sendMessages).
+ *   rbe_push_messages: the round's inbound batch for the replicas this engine
+ *     steps, delivered to the next rbe_step.  Replaces Peer.Handle (peer.go:186-198)
+ *     as called by node.handleReceivedMessages (node.go:1030-1067): message i is
+ *     for group group[i], from node msgs[i].from (not stepped here) to node
+ *     msgs[i].to (stepped here), with msgs[i].n_entries entries taken in order from
+ *     `ents` (Index = LogIndex + 1 + j).  One call per round carries every remote
+ *     message of that round; lists it does not name are empty.  RBE_E_STATE when
+ *     rep_world <= 1 (every sender is local), RBE_E_NOMEM when one (sender,
+ *     destination) list exceeds cfg.maxm or one sender's entries cfg.ecap. */
+int rbe_get_outbox(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t cap,
+                   uint32_t* n_out, rbe_entry* ents, uint32_t ent_cap, uint32_t* n_ents);
+int rbe_push_messages(rbe_engine* e, uint64_t n, const uint64_t* group, const rbe_message* msgs,
+                      const rbe_entry* ents);
+
 /* Device memory footprint (bytes) of a configuration, without allocating. */
 int rbe_footprint(const rbe_config* cfg, uint64_t* bytes);
 

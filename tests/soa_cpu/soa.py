@@ -5,7 +5,8 @@ Never imported by the dragonboat_amd package; see soa_cpu.cpp.
 import ctypes as C
 import os
 
-from dragonboat_amd.engine import CTR_NUM, COUNTER_NAMES, RbeReplicaView, make_config
+from dragonboat_amd.engine import (CTR_NUM, COUNTER_NAMES, RbeEntry, RbeMessage, RbeReplicaView,
+                                   make_config)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _lib = None
@@ -28,6 +29,11 @@ def lib():
         L.soa_set_staged.argtypes = [C.c_void_p, C.c_int]
         L.soa_slow_total.restype = C.c_uint64
         L.soa_slow_total.argtypes = [C.c_void_p]
+        P = C.POINTER
+        L.soa_get_outbox.argtypes = [C.c_void_p, C.c_uint64, P(RbeMessage), C.c_uint32,
+                                     P(C.c_uint32), P(RbeEntry), C.c_uint32, P(C.c_uint32)]
+        L.soa_push_messages.argtypes = [C.c_void_p, C.c_uint64, P(C.c_uint64), P(RbeMessage),
+                                        P(RbeEntry)]
         L.soa_faults.restype = C.c_uint32
         L.soa_faults.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         L.soa_xchg_pack.restype = C.c_int
@@ -74,6 +80,25 @@ class SoaCpu:
     def xchg_unpack(self, cnt_ptr, n_cnt, msg_ptr, n_msg, ent_ptr, n_ent):
         lib().soa_xchg_unpack(self.h, C.c_void_p(cnt_ptr), n_cnt, C.c_void_p(msg_ptr), n_msg,
                               C.c_void_p(ent_ptr), n_ent)
+
+    # transport boundary, same contract as Engine.outbox / Engine.push_messages
+    def outbox(self, replica, cap=256, ent_cap=1024):
+        arr = (RbeMessage * cap)()
+        ents = (RbeEntry * ent_cap)()
+        n, ne = C.c_uint32(), C.c_uint32()
+        rc = lib().soa_get_outbox(self.h, replica, arr, cap, C.byref(n), ents, ent_cap,
+                                  C.byref(ne))
+        assert rc == 0 and n.value <= cap and ne.value <= ent_cap, (rc, n.value, ne.value)
+        return [arr[i] for i in range(n.value)], [ents[i] for i in range(ne.value)]
+
+    def push_messages(self, groups, msgs, ents):
+        n = len(msgs)
+        g = (C.c_uint64 * max(1, n))(*groups)
+        m = (RbeMessage * max(1, n))(*msgs)
+        e = (RbeEntry * max(1, len(ents)))(*ents)
+        rc = lib().soa_push_messages(self.h, n, g, m, e)
+        if rc != 0:
+            raise RuntimeError(f"soa_push_messages rc={rc}")
 
     def views(self):
         arr = (RbeReplicaView * self.n_rep)()

@@ -290,3 +290,41 @@ extern "C" void soa_xchg_unpack(void* h, const void* c, uint64_t nc, const void*
   else if (e->C.n == 5) soa_xchg_unpack_t<5>(e, (const XCnt*)c, nc, (const XMsg*)m, nm, (const XEnt*)x, ne);
   else soa_xchg_unpack_t<1>(e, (const XCnt*)c, nc, (const XMsg*)m, nm, (const XEnt*)x, ne);
 }
+
+// transport boundary on the host build (rbe_get_outbox / rbe_push_messages)
+extern "C" int soa_get_outbox(void* h, uint64_t replica, rbe_message* out, uint32_t cap,
+                              uint32_t* n_out, rbe_entry* ents, uint32_t ent_cap,
+                              uint32_t* n_ents) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (replica >= e->C.n_rep || e->round == 0) return RBE_E_INVALID;
+  const u32 N = e->C.n, par = (e->round - 1) & 1u;
+  const u64 g = replica / N;
+  const u32 k = (u32)(replica % N);
+  const u16* cnt = e->P.cnt[par] + g * N * N + k * N;
+  const Msg* lst = e->P.msgs[par] + (g * N + k) * N * (u64)e->C.maxm;
+  const Ent* arena = e->P.arena[par] + replica * e->C.ecap;
+  if (N == 3) outbox_messages<3>(e->C, g, k, cnt, lst, arena, out, cap, ents, ent_cap, n_out, n_ents);
+  else if (N == 5) outbox_messages<5>(e->C, g, k, cnt, lst, arena, out, cap, ents, ent_cap, n_out, n_ents);
+  else outbox_messages<1>(e->C, g, k, cnt, lst, arena, out, cap, ents, ent_cap, n_out, n_ents);
+  return RBE_OK;
+}
+template <int N>
+static int soa_push_t(SoaEngine* e, uint64_t n, const uint64_t* group, const rbe_message* msgs,
+                      const rbe_entry* ents) {
+  std::vector<XCnt> c;
+  std::vector<XMsg> m;
+  std::vector<XEnt> x;
+  const int rc = messages_to_records<N>(e->C, n, group, msgs, ents, c, m, x);
+  if (rc) return rc;
+  soa_xchg_unpack_t<N>(e, c.data(), c.size(), m.data(), m.size(), x.data(), x.size());
+  return RBE_OK;
+}
+extern "C" int soa_push_messages(void* h, uint64_t n, const uint64_t* group,
+                                 const rbe_message* msgs, const rbe_entry* ents) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (e->round == 0) return RBE_E_INVALID;
+  if (e->C.rep_world <= 1) return RBE_E_STATE;
+  if (e->C.n == 3) return soa_push_t<3>(e, n, group, msgs, ents);
+  if (e->C.n == 5) return soa_push_t<5>(e, n, group, msgs, ents);
+  return soa_push_t<1>(e, n, group, msgs, ents);
+}

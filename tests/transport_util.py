@@ -1,0 +1,66 @@
+"""Host transport loop over the Peer.Handle boundary (rbe_get_outbox /
+rbe_push_messages): W engines in one process, each stepping the replicas it
+owns (replica k of group g on engine (g + k) % W, rep_world = W); after every
+round each engine's outbound messages to replicas stepped elsewhere are read
+in raftpb form and delivered to the owning engine as its next round's inbound
+batch, as dragonboat's transport would carry them between NodeHosts
+(node.go:888-905 → nodehost.go:1724 → node.handleReceivedMessages)."""
+from parity_util import view_diff
+
+
+def owner(g, k, world):
+    return (g + k) % world
+
+
+def deliver(engs, n, n_rep):
+    """One transport hop: every engine's owned senders → the owners of the
+    destinations.  Returns the number of messages moved."""
+    world = len(engs)
+    batches = [([], [], []) for _ in range(world)]
+    moved = 0
+    for rank, e in enumerate(engs):
+        for r in range(n_rep):
+            g, k = divmod(r, n)
+            if owner(g, k, world) != rank:
+                continue
+            msgs, ents = e.outbox(r)
+            ei = 0
+            for m in msgs:
+                ne = m.n_entries
+                dst = owner(g, m.to - 1, world)
+                if dst != rank:
+                    gs, ms, es = batches[dst]
+                    gs.append(g)
+                    ms.append(m)
+                    es.extend(ents[ei:ei + ne])
+                    moved += 1
+                ei += ne
+            assert ei == len(ents)
+    for rank, e in enumerate(engs):
+        gs, ms, es = batches[rank]
+        e.push_messages(gs, ms, es)
+    return moved
+
+
+def run_transport(engs, ref, n, rounds, every=25):
+    """Step W engines and the oracle in lockstep with a transport hop after
+    each round; compare every owned replica with the oracle every `every`
+    rounds.  Returns (first divergence or None, messages moved)."""
+    world = len(engs)
+    n_rep = len(ref.views())
+    moved = 0
+    for done in range(1, rounds + 1):
+        for e in engs:
+            e.step()
+        ref.run(1)
+        moved += deliver(engs, n, n_rep)
+        if done % every and done != rounds:
+            continue
+        hv = ref.views()
+        evs = [e.views() for e in engs]
+        for r in range(n_rep):
+            g, k = divmod(r, n)
+            d = view_diff(evs[owner(g, k, world)][r], hv[r])
+            if d is not None:
+                return (done, r) + d, moved
+    return None, moved
