@@ -40,6 +40,10 @@ static constexpr int kBlock = 256;
 #ifndef RBE_TRI_CHUNK
 #define RBE_TRI_CHUNK 2048
 #endif
+// work-list entries carry the inbound summary word (kListAux); 0 = A/B baseline
+#ifndef RBE_LIST_AUX
+#define RBE_LIST_AUX 1
+#endif
 // how the fast steps of k_fast_both use wave-staged rows (StageRow, rbe_fast.h):
 // 0 = direct, 1 = STG_OUT (row writes staged), 3 = STG_OUT | STG_IN
 #ifndef RBE_STAGE_LEAD
@@ -111,9 +115,14 @@ __global__ __launch_bounds__(kBlock) void k_step(Planes P, Params C, const u32* 
 // the back of list l occupies idx[l * cap + cap - 1 - j].
 struct Lists {
   u32* idx;     // [3][cap] replica indices
+  u32* aux;     // [2][cap] inbound summary words of the leader / follower entries (inbound_aux)
   u32* counts;  // [3][2] front, then [2][2] back
   u64 cap;
 };
+// work-list entries carry their inbound summary word for N = 3 (14 bits; the
+// LDS compaction packs it with the 11-bit block position in one u32)
+template <int N>
+constexpr bool kListAux = N == 3 && RBE_TRI_CHUNK <= 2048 && RBE_LIST_AUX;
 static constexpr u32 kListCounts = 10;
 // length of list li (front + back) and its i-th entry (front first)
 __device__ __forceinline__ u32 list_front(const Lists& L, u32 li, u32 par) {
@@ -124,6 +133,9 @@ __device__ __forceinline__ u32 list_back(const Lists& L, u32 li, u32 par) {
 }
 __device__ __forceinline__ u32 list_at(const Lists& L, u32 li, u32 nfront, u64 i) {
   return i < nfront ? L.idx[li * L.cap + i] : L.idx[li * L.cap + L.cap - 1 - (i - nfront)];
+}
+__device__ __forceinline__ u32 list_aux_at(const Lists& L, u32 li, u32 nfront, u64 i) {
+  return i < nfront ? L.aux[li * L.cap + i] : L.aux[li * L.cap + L.cap - 1 - (i - nfront)];
 }
 
 // wave-aggregated append: one atomic per wave and list
@@ -187,12 +199,15 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, const u32
   // instruction stream instead of kPer) without indexing a register array
   u64 ibp = 0;
   u32 inbp = 0;
+  u64 auxp[2] = {0, 0};  // kListAux: 14-bit summary words, replicas 0-3 and 4-7
 #pragma unroll
   for (u32 i = 0; i < kPer; i++) {
     const u64 r = lo + (u64)i * kBlock;
     const bool in = r < C.n_rep;
     ibp |= (u64)(in ? ibs[i] : (u8)0) << (8 * i);
     inbp |= (in ? inbound_fold<N>(wv[i], kk[i], round) : 0u) << (3 * i);
+    if constexpr (kListAux<N>)
+      auxp[i / 4] |= (u64)(inbound_aux<N>(wv[i], kk[i], round) & 0x3FFFu) << (14 * (i % 4));
   }
   const bool shortcut = !TRACE && C.quiesce;
 #pragma unroll 1
@@ -227,7 +242,12 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, const u32
       if (lane == first) base = atomicAdd(&s_n[sl], (u32)__popcll(mask));
       base = __shfl(base, first, 64);
       const u32 pos = base + __popcll(mask & ((1ull << lane) - 1ull));
-      if (want) s_idx[li][sl < 3 ? pos : kTriChunk - 1u - pos] = (u32)r;
+      // fast lists with kListAux: block position | summary word << 11
+      u32 ent = (u32)r;
+      if (kListAux<N> && li < 2)
+        ent = (u32)(r - (u64)blockIdx.x * kTriChunk) |
+              ((u32)((auxp[i / 4] >> (14 * (i % 4))) & 0x3FFFu) << 11);
+      if (want) s_idx[li][sl < 3 ? pos : kTriChunk - 1u - pos] = ent;
     }
   }
   __syncthreads();
@@ -236,14 +256,22 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, const u32
     s_base[threadIdx.x] = s_n[threadIdx.x] ? atomicAdd(&L.counts[at], s_n[threadIdx.x]) : 0u;
   }
   __syncthreads();
+  const u32 rb = blockIdx.x * kTriChunk;
+  auto put = [&](u32 li, u64 at, u32 ent) {
+    if (kListAux<N> && li < 2) {
+      L.idx[li * L.cap + at] = rb + (ent & 0x7FFu);
+      L.aux[li * L.cap + at] = ent >> 11;
+    } else {
+      L.idx[li * L.cap + at] = ent;
+    }
+  };
 #pragma unroll
   for (u32 li = 0; li < 3; li++)
-    for (u32 j = threadIdx.x; j < s_n[li]; j += kBlock)
-      L.idx[li * L.cap + s_base[li] + j] = s_idx[li][j];
+    for (u32 j = threadIdx.x; j < s_n[li]; j += kBlock) put(li, s_base[li] + j, s_idx[li][j]);
 #pragma unroll
   for (u32 li = 0; li < 2; li++)
     for (u32 j = threadIdx.x; j < s_n[3 + li]; j += kBlock)
-      L.idx[li * L.cap + L.cap - 1 - (s_base[3 + li] + j)] = s_idx[li][kTriChunk - 1u - j];
+      put(li, L.cap - 1 - (s_base[3 + li] + j), s_idx[li][kTriChunk - 1u - j]);
   flush_counters<KS_TRIAGE>(P, c);
 }
 
@@ -451,9 +479,14 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, 
   for (u64 i0 = (u64)blockIdx.x * kBlock; i0 < n; i0 += stride) {
     const u64 i = i0 + threadIdx.x;
     const bool lead = i < nl, any = i < n;
-    u32 r = 0;
-    if (lead) r = list_at(L, 0, nlf, i);
-    else if (any) r = list_at(L, 1, nff, i - nl);
+    u32 r = 0, aux = 0;
+    if (lead) {
+      r = list_at(L, 0, nlf, i);
+      if constexpr (kListAux<N>) aux = list_aux_at(L, 0, nlf, i);
+    } else if (any) {
+      r = list_at(L, 1, nff, i - nl);
+      if constexpr (kListAux<N>) aux = list_aux_at(L, 1, nff, i - nl);
+    }
     const u64 m_any = __ballot(any), m_lead = __ballot(lead);
     bool ok = false;
     if (m_any) {
@@ -464,8 +497,10 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, 
         stage_in_wave<N>(P, wrows, r, m_in, (SL & STG_IN) ? m_lead : 0ull);
         wave_lds_sync();
       }
-      if (lead) ok = step_fast<N, TRACE, MODE_LEAD, SL>(P, C, r, round, c, mine);
-      else if (any) ok = step_fast<N, TRACE, MODE_FOLL, SF>(P, C, r, round, c, mine);
+      if (lead)
+        ok = step_fast<N, TRACE, MODE_LEAD, SL, kListAux<N>>(P, C, r, round, c, mine, aux);
+      else if (any)
+        ok = step_fast<N, TRACE, MODE_FOLL, SF, kListAux<N>>(P, C, r, round, c, mine, aux);
       if constexpr ((SL | SF) != 0) {
         wave_lds_sync();
         const u64 m_ok = __ballot(ok) & m_out;
@@ -880,11 +915,13 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   }
   e->L.cap = C.n_rep;
   if (hipMalloc(&e->L.idx, 3 * C.n_rep * sizeof(u32)) != hipSuccess ||
+      hipMalloc(&e->L.aux, 2 * C.n_rep * sizeof(u32)) != hipSuccess ||
       hipMalloc(&e->L.counts, kListCounts * sizeof(u32)) != hipSuccess) {
     rbe_destroy(e);
     return RBE_E_NOMEM;
   }
   e->allocs.push_back(e->L.idx);
+  e->allocs.push_back(e->L.aux);
   e->allocs.push_back(e->L.counts);
   if (hipMalloc(&e->xcount, kXchgMaxWorld * XS_NUM * sizeof(u32)) != hipSuccess) {
     rbe_destroy(e);

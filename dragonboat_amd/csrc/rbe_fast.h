@@ -462,9 +462,9 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
 //   inbox (ascending sender; Quiesce marker, then the sender's messages) →
 //   local ReadIndex → tick → proposal, each followed by the deferred fan-out
 //   (Replicate sends in ascending slot order, heartbeats, readIndex confirm).
-template <int N, bool TRACE, int STG = 0>
+template <int N, bool TRACE, int STG = 0, bool AUX = false>
 RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCounters& ctr,
-                      StageRow<N>* sr = nullptr) {
+                      StageRow<N>* sr = nullptr, u32 aux = 0) {
   using Cap = FastCaps<N>;
   constexpr u32 Q = N / 2 + 1;
   if constexpr (N < 3) {
@@ -498,9 +498,38 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
     st[s] = P.rem_st[r * N + s];
   }
   u32 pcin[N];
+  if constexpr (AUX) {  // the count words came with the work-list entry (inbound_aux)
 #pragma unroll
-  for (u32 s = 0; s < N; s++)
-    pcin[s] = (round > 0 && s != k) ? (u32)P.cnt[ppar][g * N * N + s * N + k] : 0u;
+    for (u32 s = 0; s < N; s++) pcin[s] = s == k ? 0u : aux_count_word<N>(aux, k, s);
+  } else {
+#pragma unroll
+    for (u32 s = 0; s < N; s++)
+      pcin[s] = (round > 0 && s != k) ? (u32)P.cnt[ppar][g * N * N + s * N + k] : 0u;
+  }
+  // one row per other sender (row j is sender j + (j >= k)): no registers
+  // for the lane's own slot, which is what keeps the step out of scratch.
+  // With AUX the counts are known before any load, so the inbound messages
+  // are part of the first gather level; otherwise they wait for the counts.
+  LeadMsg in[N - 1][Cap::MAXM];
+  auto load_inbox = [&]() {
+#pragma unroll
+    for (u32 j = 0; j + 1 < N; j++) {
+      const u32 sj = j + (j >= k ? 1u : 0u);
+      u32 pj = 0;
+#pragma unroll
+      for (u32 t = 0; t < N; t++)
+        if (t == sj) pj = pcin[t];
+      const u32 nbj = (pj >> 7) & 0x7Fu;
+      const Msg* lst = &P.msgs[ppar][((g * N + sj) * N + k) * (u64)C.maxm];
+#pragma unroll
+      for (u32 i = 0; i < Cap::MAXM; i++) {
+        in[j][i].w = 0xFFu;
+        in[j][i].term = in[j][i].log_index = in[j][i].hint = in[j][i].hint_high = 0;
+        if (i < nbj) in[j][i] = load_lead(&lst[C.maxm - 1u - i]);
+      }
+    }
+  };
+  if constexpr (AUX) load_inbox();
   // the isolation schedule and the Update record are read only when in use:
   // two of the lane's scattered lines saved in the steady state
   const u32 until = C.iso_period ? P.iso_until[g] : 0u;
@@ -526,25 +555,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   // Loads only inside the branches; every use comes after the join, so no
   // branch waits for its own loads (a wait inside each conditional block
   // would serialise the message loads).
-  // one row per other sender (row j is sender j + (j >= k)): no registers
-  // for the lane's own slot, which is what keeps the step out of scratch
-  LeadMsg in[N - 1][Cap::MAXM];
-#pragma unroll
-  for (u32 j = 0; j + 1 < N; j++) {
-    const u32 sj = j + (j >= k ? 1u : 0u);
-    u32 pj = 0;
-#pragma unroll
-    for (u32 t = 0; t < N; t++)
-      if (t == sj) pj = pcin[t];
-    const u32 nbj = (pj >> 7) & 0x7Fu;
-    const Msg* lst = &P.msgs[ppar][((g * N + sj) * N + k) * (u64)C.maxm];
-#pragma unroll
-    for (u32 i = 0; i < Cap::MAXM; i++) {
-      in[j][i].w = 0xFFu;
-      in[j][i].term = in[j][i].log_index = in[j][i].hint = in[j][i].hint_high = 0;
-      if (i < nbj) in[j][i] = load_lead(&lst[C.maxm - 1u - i]);
-    }
-  }
+  if constexpr (!AUX) load_inbox();
   u64 rq_lo[Cap::RQ], rq_hi[Cap::RQ], rq_ix[Cap::RQ];
   u32 rq_fr[Cap::RQ], rq_cf[Cap::RQ];
   u32 rq_n = c.rq_count, rq_h = c.rq_head;
@@ -1089,9 +1100,9 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
 // One steady-state follower round: inbox from the known leader only
 // (Replicate / Heartbeat / ReadIndexResp of the current term), no client
 // input, a tick that does not start an election.
-template <int N, bool TRACE, int STG = 0>
+template <int N, bool TRACE, int STG = 0, bool AUX = false>
 RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCounters& ctr,
-                      StageRow<N>* sr = nullptr) {
+                      StageRow<N>* sr = nullptr, u32 aux = 0) {
   using Cap = FastCaps<N>;
   if constexpr (N < 3) {
     return false;
@@ -1112,9 +1123,38 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
     c = P.core[r];
   }
   u32 pcin[N];
+  // With AUX the count words came with the work-list entry (inbound_aux):
+  // the messages of the one sender that has any (the leader, checked below)
+  // and the first entry of its arena are loaded in this first gather level.
+  Msg raw[Cap::FMAXM];
+  Ent spec0;
+  u32 ls_a = 0xFFFFFFFFu;
+  if constexpr (AUX) {
 #pragma unroll
-  for (u32 s = 0; s < N; s++)
-    pcin[s] = (round > 0 && s != k) ? (u32)P.cnt[ppar][g * N * N + s * N + k] : 0u;
+    for (u32 s = 0; s < N; s++) pcin[s] = s == k ? 0u : aux_count_word<N>(aux, k, s);
+    u32 na_a = 0, n_a = 0;
+#pragma unroll
+    for (u32 s = N; s-- > 0;) {
+      const u32 n = (pcin[s] & 0x7Fu) + ((pcin[s] >> 7) & 0x7Fu);
+      if (s != k && n) {
+        ls_a = s;
+        na_a = pcin[s] & 0x7Fu;
+        n_a = n;
+      }
+    }
+    const u32 sa = ls_a < N ? ls_a : 0u;
+    const Msg* la = &P.msgs[ppar][((g * N + sa) * N + k) * (u64)C.maxm];
+#pragma unroll
+    for (u32 i = 0; i < Cap::FMAXM; i++)
+      if (i < n_a) raw[i] = la[i < na_a ? i : C.maxm - 1u - (i - na_a)];
+    spec0.term = spec0.lo = spec0.hi = 0;
+    spec0.type = spec0.len = 0;
+    if (na_a > 0) spec0 = P.arena[ppar][(g * N + sa) * (u64)C.ecap];
+  } else {
+#pragma unroll
+    for (u32 s = 0; s < N; s++)
+      pcin[s] = (round > 0 && s != k) ? (u32)P.cnt[ppar][g * N * N + s * N + k] : 0u;
+  }
   // the isolation schedule and the Update record are read only when in use:
   // two of the lane's scattered lines saved in the steady state
   const u32 until = C.iso_period ? P.iso_until[g] : 0u;
@@ -1142,11 +1182,16 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
 #pragma unroll
   for (u32 s = 0; s < N; s++)
     if (s == ls && s != k) na = pcin[s] & 0x7Fu;
-  // loads only inside the branches, decoded after the join (see lead_fast)
-  Msg raw[Cap::FMAXM];
+  // loads only inside the branches, decoded after the join (see lead_fast);
+  // with AUX they were issued in the first level from the same list (every
+  // message came from ls, so ls_a == ls whenever n_in > 0)
+  if constexpr (!AUX) {
 #pragma unroll
-  for (u32 i = 0; i < Cap::FMAXM; i++) {
-    if (i < n_in) raw[i] = lst[i < na ? i : C.maxm - 1u - (i - na)];
+    for (u32 i = 0; i < Cap::FMAXM; i++) {
+      if (i < n_in) raw[i] = lst[i < na ? i : C.maxm - 1u - (i - na)];
+    }
+  } else {
+    (void)ls_a;
   }
 #pragma unroll
   for (u32 i = 0; i < Cap::FMAXM; i++) {
@@ -1181,7 +1226,12 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   pre1 = pre2 = pre3 = pre0;
   {
     const Ent* ab = &P.arena[ppar][(g * N + (ls < N ? ls : 0)) * (u64)C.ecap];
-    if (na > 0 && n_in > 0 && in[0].n_ent > 0) pre0 = ab[in[0].ent_off];
+    if constexpr (AUX) {  // the shared segment of a broadcast starts at offset 0
+      if (na > 0 && n_in > 0 && in[0].n_ent > 0)
+        pre0 = in[0].ent_off == 0 ? spec0 : ab[in[0].ent_off];
+    } else {
+      if (na > 0 && n_in > 0 && in[0].n_ent > 0) pre0 = ab[in[0].ent_off];
+    }
     if (na > 1 && n_in > 1 && in[1].n_ent > 0) pre1 = ab[in[1].ent_off];
     if (na > 2 && n_in > 2 && in[2].n_ent > 0) pre2 = ab[in[2].ent_off];
     if (na > 3 && n_in > 3 && in[3].n_ent > 0) pre3 = ab[in[3].ent_off];
@@ -1379,11 +1429,12 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
 }
 
 // the fast step of one role (k_round, k_fast_list)
-template <int N, bool TRACE, int MODE, int STG = 0>
+template <int N, bool TRACE, int MODE, int STG = 0, bool AUX = false>
 RBE_HD bool step_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCounters& ctr,
-                      StageRow<N>* sr = nullptr) {
-  if constexpr (MODE == MODE_LEAD) return lead_fast<N, TRACE, STG>(P, C, r, round, ctr, sr);
-  else return foll_fast<N, TRACE, STG>(P, C, r, round, ctr, sr);
+                      StageRow<N>* sr = nullptr, u32 aux = 0) {
+  if constexpr (MODE == MODE_LEAD)
+    return lead_fast<N, TRACE, STG, AUX>(P, C, r, round, ctr, sr, aux);
+  else return foll_fast<N, TRACE, STG, AUX>(P, C, r, round, ctr, sr, aux);
 }
 
 }  // namespace rbe

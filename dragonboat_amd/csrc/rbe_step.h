@@ -1799,6 +1799,36 @@ RBE_HD u32 inbound_bits(const Planes& P, u64 r, u32 round) {
   inbound_load<N>(P, g, k, round, w);
   return inbound_fold<N>(w, k, round);
 }
+// The inbound summary word a work-list entry carries to the fast kernel
+// (Lists::aux): for the j-th other sender (sender j + (j >= k)), 7 bits =
+// min(A, 7) | min(B, 7) << 3 | quiesce << 6 of its count word this round.
+// The fast steps rebuild their count words from it (aux_count_word) without
+// loading them, so their message loads issue in the first gather level.  The
+// clamp keeps every decision the fast steps take on the words: a leader
+// declines A > 0 or B > MAXM (< 7), a follower more than FMAXM (< 7) inbound
+// messages, and every count that is used is below 7.
+template <int N>
+RBE_HD u32 inbound_aux(const u16 (&w)[N], u32 k, u32 round) {
+  u32 aux = 0;
+  for (u32 j = 0; j + 1 < N; j++) {
+    const u32 s = j + (j >= k ? 1u : 0u);
+    u32 pc = 0;
+    for (u32 t = 0; t < N; t++)
+      if (t == s) pc = w[t];
+    const u32 a = pc & 0x7Fu, b = (pc >> 7) & 0x7Fu;
+    const u32 f = (a < 7u ? a : 7u) | ((b < 7u ? b : 7u) << 3) | (((pc >> 15) & 1u) << 6);
+    aux |= f << (7 * j);
+  }
+  return round == 0 ? 0u : aux;
+}
+// count word of sender slot s (!= k) rebuilt from an inbound summary word
+template <int N>
+RBE_HD u32 aux_count_word(u32 aux, u32 k, u32 s) {
+  const u32 j = s - (s > k ? 1u : 0u);
+  const u32 f = (aux >> (7 * j)) & 0x7Fu;
+  return (f & 7u) | (((f >> 3) & 7u) << 7) | (((f >> 6) & 1u) << 15);
+}
+
 RBE_HD u32 class_of_role(u32 role) {
   return role == R_Leader ? 1u /*T_LEAD*/ : (role == R_Follower ? 2u /*T_FOLL*/ : 3u /*T_FULL*/);
 }

@@ -21,7 +21,7 @@ struct SoaEngine {
   u32 round = 0;
   u64 counters[C_NUM] = {0};
   bool full_only = false;
-  int staged = 0;  // STG_* bits: fast steps on a staged row (StageRow), as k_fast_both runs them
+  int staged = 0;  // STG_* bits: fast steps on a staged row (StageRow); 4: counts from inbound_aux
   u64 slow_total = 0;
 };
 
@@ -61,7 +61,20 @@ static void run_round(SoaEngine* e) {
     for (u64 r : lists[li]) {
       memset(&c, 0, sizeof(c));
       bool ok;
-      if (e->staged == (STG_OUT | STG_IN)) {
+      if (e->staged == 4) {  // counts from the work-list summary word (k_fast_both)
+        const u32 g = (u32)(r / N), k = (u32)(r % N);
+        u16 w[N];
+        inbound_load<N>(e->P, g, k, e->round, w);
+        const u32 aux = inbound_aux<N>(w, k, e->round);
+        if (li == 0)
+          ok = e->C.trace
+                   ? step_fast<N, true, MODE_LEAD, 0, true>(e->P, e->C, r, e->round, c, nullptr, aux)
+                   : step_fast<N, false, MODE_LEAD, 0, true>(e->P, e->C, r, e->round, c, nullptr, aux);
+        else
+          ok = e->C.trace
+                   ? step_fast<N, true, MODE_FOLL, 0, true>(e->P, e->C, r, e->round, c, nullptr, aux)
+                   : step_fast<N, false, MODE_FOLL, 0, true>(e->P, e->C, r, e->round, c, nullptr, aux);
+      } else if (e->staged == (STG_OUT | STG_IN)) {
         StageRow<N> row;
         memset(&row, 0xA5, sizeof(row));  // nothing the step reads may come from here unset
         stage_row_in<N>(e->P, r, li == 0, row);
