@@ -17,6 +17,7 @@
 
 #include "../../include/rbe.h"
 #include "rbe_fast.h"
+#include "rbe_snap.h"
 #include "rbe_xchg.h"
 
 using namespace rbe;
@@ -805,6 +806,68 @@ static int read_counters(rbe_engine* e, int ks, u64* out) {
 extern "C" {
 
 int rbe_abi_version(void) { return RBE_ABI_VERSION; }
+
+// Group-range snapshots (rbe_snap.h): one 2-D copy per plane on the engine
+// stream, ordered after every round already queued.
+int rbe_snapshot_bytes(rbe_engine* e, uint64_t count, uint64_t* bytes) {
+  if (!e || !bytes || count == 0 || count > e->C.n_groups) return RBE_E_INVALID;
+  *bytes = sizeof(SnapHeader) + snap_body_bytes(e->P, e->C, count);
+  return RBE_OK;
+}
+
+int rbe_export_groups(rbe_engine* e, uint64_t first, uint64_t count, void* buf, uint64_t cap) {
+  if (!e || !buf || count == 0 || first >= e->C.n_groups || count > e->C.n_groups - first)
+    return RBE_E_INVALID;
+  const u64 body = snap_body_bytes(e->P, e->C, count);
+  if (cap < sizeof(SnapHeader) + body) return RBE_E_NOMEM;
+  HIP_OK(hipSetDevice(e->device));
+  SnapHeader h;
+  snap_fill_header(e->C, RBE_ABI_VERSION, e->round, first, count, body, &h);
+  memcpy(buf, &h, sizeof(h));
+  SnapPlane pl[kSnapPlanes];
+  snap_planes(e->P, e->C, pl);
+  u8* dst = (u8*)buf + sizeof(SnapHeader);
+  for (int i = 0; i < kSnapPlanes && pl[i].rows; i++) {
+    const u64 w = count * pl[i].group_bytes;
+    HIP_OK(hipMemcpy2DAsync(dst, w, pl[i].base + first * pl[i].group_bytes, pl[i].pitch, w,
+                            pl[i].rows, hipMemcpyDeviceToHost, e->stream));
+    dst += w * pl[i].rows;
+  }
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return RBE_OK;
+}
+
+int rbe_import_groups(rbe_engine* e, const void* buf, uint64_t bytes, uint32_t flags) {
+  if (!e || !buf) return RBE_E_INVALID;
+  SnapHeader h;
+  if (bytes < sizeof(h)) return RBE_E_INVALID;
+  memcpy(&h, buf, sizeof(h));
+  if (snap_check_header(e->C, RBE_ABI_VERSION, &h, bytes) ||
+      h.body_bytes != snap_body_bytes(e->P, e->C, h.count))
+    return RBE_E_INVALID;
+  const bool resume = (flags & RBE_IMPORT_RESUME) != 0;
+  if (resume && (h.first != 0 || h.count != e->C.n_groups)) return RBE_E_INVALID;
+  if (!resume && h.round != e->round) return RBE_E_STATE;
+  HIP_OK(hipSetDevice(e->device));
+  SnapPlane pl[kSnapPlanes];
+  snap_planes(e->P, e->C, pl);
+  const u8* src = (const u8*)buf + sizeof(SnapHeader);
+  for (int i = 0; i < kSnapPlanes && pl[i].rows; i++) {
+    const u64 w = h.count * pl[i].group_bytes;
+    HIP_OK(hipMemcpy2DAsync(pl[i].base + h.first * pl[i].group_bytes, pl[i].pitch, src, w, w,
+                            pl[i].rows, hipMemcpyHostToDevice, e->stream));
+    src += w * pl[i].rows;
+  }
+  if (resume) {
+    // the whole engine moves to the snapshot's round; the work lists of the
+    // coming round start empty, as after any round (k_triage clears them)
+    e->round = h.round;
+    HIP_OK(hipMemsetAsync(e->L.counts, 0, kListCounts * sizeof(u32), e->stream));
+    HIP_OK(hipMemcpyAsync(e->d_round, &e->round, sizeof(u32), hipMemcpyHostToDevice, e->stream));
+  }
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return RBE_OK;
+}
 
 int rbe_footprint(const rbe_config* cfg, uint64_t* bytes) {
   Params C;

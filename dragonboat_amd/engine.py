@@ -92,7 +92,7 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_step", "rbe_run"
            "rbe_get_views", "rbe_get_counters", "rbe_reset_counters", "rbe_fault_summary",
            "rbe_footprint", "rbe_profile_rounds", "rbe_get_kernel_counters", "rbe_kernel_name",
            "rbe_xchg_record_bytes", "rbe_xchg_pack", "rbe_xchg_unpack", "rbe_get_outbox",
-           "rbe_push_messages"]
+           "rbe_push_messages", "rbe_snapshot_bytes", "rbe_export_groups", "rbe_import_groups"]
 KERNEL_SLOTS = 4
 
 _lib = None
@@ -147,6 +147,9 @@ def load_library(path: Optional[str] = None):
         "rbe_xchg_record_bytes": (i32, [P(u64)]),
         "rbe_xchg_pack": (i32, [vp, vp, P(u64), P(u32)]),
         "rbe_xchg_unpack": (i32, [vp, vp, u64, vp, u64, vp, u64]),
+        "rbe_snapshot_bytes": (i32, [vp, u64, P(u64)]),
+        "rbe_export_groups": (i32, [vp, u64, u64, vp, u64]),
+        "rbe_import_groups": (i32, [vp, vp, u64, u32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -179,6 +182,12 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                      wl_read_permille=wl_read_permille, ext_inputs=int(ext_inputs),
                      iso_period=iso_period, iso_len=iso_len, iso_mod=iso_mod,
                      rep_world=rep_world, rep_rank=rep_rank)
+
+
+class SnapshotError(EngineError):
+    def __init__(self, rc: int, what: str):
+        super().__init__(f"{what} failed with rc={rc}")
+        self.rc = rc
 
 
 def _check(rc: int, what: str):
@@ -233,6 +242,32 @@ class Engine:
         r = C.c_uint32()
         _check(self.lib.rbe_round(self.h, C.byref(r)), "rbe_round")
         return r.value
+
+    # group-range snapshots (rbe_snap.h): checkpoint/resume and slow-path hand-off
+    def snapshot_bytes(self, count: Optional[int] = None) -> int:
+        n = C.c_uint64()
+        count = self.n_groups if count is None else count
+        _check(self.lib.rbe_snapshot_bytes(self.h, count, C.byref(n)), "rbe_snapshot_bytes")
+        return n.value
+
+    def export_groups(self, first: int = 0, count: Optional[int] = None,
+                      cap: Optional[int] = None) -> bytes:
+        """The protocol state of groups [first, first + count) after the last
+        queued round, as bytes (peer.go:64-87 / raft.go:283-330 restated)."""
+        count = self.n_groups - first if count is None else count
+        n = self.snapshot_bytes(count) if cap is None else cap
+        buf = C.create_string_buffer(max(1, n))
+        rc = self.lib.rbe_export_groups(self.h, first, count, buf, n)
+        if rc != 0:
+            raise SnapshotError(rc, "rbe_export_groups")
+        return buf.raw[:n]
+
+    def import_groups(self, snap: bytes, resume: bool = False):
+        """Overwrite the snapshot's groups; `resume` moves a whole engine to
+        the snapshot's round (RBE_IMPORT_RESUME)."""
+        rc = self.lib.rbe_import_groups(self.h, snap, len(snap), 1 if resume else 0)
+        if rc != 0:
+            raise SnapshotError(rc, "rbe_import_groups")
 
     # inputs
     def push_proposals(self, replicas, cmds: List[bytes]):

@@ -269,6 +269,24 @@ int rbe_get_outbox(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t c
 int rbe_push_messages(rbe_engine* e, uint64_t n, const uint64_t* group, const rbe_message* msgs,
                       const rbe_entry* ents);
 
+/* Group-range snapshots: the complete protocol state of groups [first, first + count)
+ * between two rounds (every replica's raft, remote, readIndex and log-window rows and
+ * the groups' in-flight messages), laid out as in dragonboat_amd/csrc/rbe_snap.h.
+ * Replaces what a restarted dragonboat node rebuilds from LogDB through Peer.Launch on
+ * an existing log (peer.go:64-87, raft.go:283-330 loadState), and is the hand-off a
+ * host slow path uses to run a rare handler on one group and put it back.
+ *   rbe_snapshot_bytes: the buffer size `count` groups need;
+ *   rbe_export_groups: copies the range into `buf` (host memory, cap bytes; RBE_E_NOMEM
+ *     when short), after every round already queued;
+ *   rbe_import_groups: overwrites the snapshot's range.  The engine must be at the
+ *     snapshot's round (RBE_E_STATE otherwise), unless flags has RBE_IMPORT_RESUME and
+ *     the snapshot covers every group: then the engine resumes at that round.
+ *     RBE_E_INVALID when the geometry (n, ring, capacities) differs. */
+#define RBE_IMPORT_RESUME 0x1u
+int rbe_snapshot_bytes(rbe_engine* e, uint64_t count, uint64_t* bytes);
+int rbe_export_groups(rbe_engine* e, uint64_t first, uint64_t count, void* buf, uint64_t cap);
+int rbe_import_groups(rbe_engine* e, const void* buf, uint64_t bytes, uint32_t flags);
+
 /* Device memory footprint (bytes) of a configuration, without allocating. */
 int rbe_footprint(const rbe_config* cfg, uint64_t* bytes);
 

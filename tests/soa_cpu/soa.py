@@ -41,8 +41,21 @@ def lib():
                                     C.POINTER(C.c_uint32)]
         L.soa_xchg_unpack.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
                                       C.c_uint64, C.c_void_p, C.c_uint64]
+        L.soa_snapshot_bytes.restype = C.c_uint64
+        L.soa_snapshot_bytes.argtypes = [C.c_void_p, C.c_uint64]
+        L.soa_export_groups.restype = C.c_int
+        L.soa_export_groups.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p,
+                                        C.c_uint64]
+        L.soa_import_groups.restype = C.c_int
+        L.soa_import_groups.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32]
         _lib = L
     return _lib
+
+
+class SnapshotError(RuntimeError):
+    def __init__(self, rc):
+        super().__init__(f"snapshot call failed with rc={rc}")
+        self.rc = rc
 
 
 class SoaCpu:
@@ -99,6 +112,21 @@ class SoaCpu:
         rc = lib().soa_push_messages(self.h, n, g, m, e)
         if rc != 0:
             raise RuntimeError(f"soa_push_messages rc={rc}")
+
+    # group-range snapshots, same contract as Engine.export_groups / import_groups
+    def export_groups(self, first=0, count=None, cap=None):
+        count = self.cfg.n_groups - first if count is None else count
+        n = lib().soa_snapshot_bytes(self.h, count) if cap is None else cap
+        buf = C.create_string_buffer(max(1, n))
+        rc = lib().soa_export_groups(self.h, first, count, buf, n)
+        if rc != 0:
+            raise SnapshotError(rc)
+        return buf.raw[:n]
+
+    def import_groups(self, snap, resume=False):
+        rc = lib().soa_import_groups(self.h, snap, len(snap), 1 if resume else 0)
+        if rc != 0:
+            raise SnapshotError(rc)
 
     def views(self):
         arr = (RbeReplicaView * self.n_rep)()

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../dragonboat_amd/csrc/rbe_fast.h"
+#include "../../dragonboat_amd/csrc/rbe_snap.h"
 #include "../../dragonboat_amd/csrc/rbe_xchg.h"
 #include "../../include/rbe.h"
 
@@ -165,11 +166,13 @@ void* soa_create(const rbe_config* cfg) {
   P.rq = alloc<ReadReq>(e, R * C.rq_cap);
   P.term_ring = alloc<u64>(e, (u64)C.ring * R);
   P.pay_ring = alloc<Body>(e, (u64)C.ring * R);
-  for (int p = 0; p < 2; p++) {
-    P.cnt[p] = alloc<u16>(e, G * N * N);
-    P.msgs[p] = alloc<Msg>(e, G * N * N * C.maxm);
-    P.arena[p] = alloc<Ent>(e, R * C.ecap);
-  }
+  // parity 1 follows parity 0 in one allocation, as on the device (rbe_snap.h)
+  P.cnt[0] = alloc<u16>(e, 2 * G * N * N);
+  P.cnt[1] = P.cnt[0] + G * N * N;
+  P.msgs[0] = alloc<Msg>(e, 2 * G * N * N * C.maxm);
+  P.msgs[1] = P.msgs[0] + G * N * N * C.maxm;
+  P.arena[0] = alloc<Ent>(e, 2 * R * C.ecap);
+  P.arena[1] = P.arena[0] + R * C.ecap;
   P.iso_mask = alloc<u8>(e, G);
   P.idle = alloc<u8>(e, R);
   P.iso_until = alloc<u32>(e, G);
@@ -340,4 +343,53 @@ extern "C" int soa_push_messages(void* h, uint64_t n, const uint64_t* group,
   if (e->C.n == 3) return soa_push_t<3>(e, n, group, msgs, ents);
   if (e->C.n == 5) return soa_push_t<5>(e, n, group, msgs, ents);
   return soa_push_t<1>(e, n, group, msgs, ents);
+}
+
+// Group-range snapshots in the engine's byte layout (rbe_export_groups /
+// rbe_import_groups run the same plane walk with hipMemcpy2DAsync).
+extern "C" uint64_t soa_snapshot_bytes(void* h, uint64_t count) {
+  SoaEngine* e = (SoaEngine*)h;
+  return sizeof(SnapHeader) + snap_body_bytes(e->P, e->C, count);
+}
+
+extern "C" int soa_export_groups(void* h, uint64_t first, uint64_t count, void* buf, uint64_t cap) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (count == 0 || first >= e->C.n_groups || count > e->C.n_groups - first) return RBE_E_INVALID;
+  const u64 body = snap_body_bytes(e->P, e->C, count);
+  if (cap < sizeof(SnapHeader) + body) return RBE_E_NOMEM;
+  SnapHeader hd;
+  snap_fill_header(e->C, RBE_ABI_VERSION, e->round, first, count, body, &hd);
+  memcpy(buf, &hd, sizeof(hd));
+  SnapPlane pl[kSnapPlanes];
+  snap_planes(e->P, e->C, pl);
+  u8* dst = (u8*)buf + sizeof(SnapHeader);
+  for (int i = 0; i < kSnapPlanes && pl[i].rows; i++) {
+    const u64 w = count * pl[i].group_bytes;
+    for (u64 row = 0; row < pl[i].rows; row++, dst += w)
+      memcpy(dst, pl[i].base + row * pl[i].pitch + first * pl[i].group_bytes, w);
+  }
+  return RBE_OK;
+}
+
+extern "C" int soa_import_groups(void* h, const void* buf, uint64_t bytes, uint32_t flags) {
+  SoaEngine* e = (SoaEngine*)h;
+  SnapHeader hd;
+  if (bytes < sizeof(hd)) return RBE_E_INVALID;
+  memcpy(&hd, buf, sizeof(hd));
+  if (snap_check_header(e->C, RBE_ABI_VERSION, &hd, bytes) ||
+      hd.body_bytes != snap_body_bytes(e->P, e->C, hd.count))
+    return RBE_E_INVALID;
+  const bool resume = (flags & RBE_IMPORT_RESUME) != 0;
+  if (resume && (hd.first != 0 || hd.count != e->C.n_groups)) return RBE_E_INVALID;
+  if (!resume && hd.round != e->round) return RBE_E_STATE;
+  SnapPlane pl[kSnapPlanes];
+  snap_planes(e->P, e->C, pl);
+  const u8* src = (const u8*)buf + sizeof(SnapHeader);
+  for (int i = 0; i < kSnapPlanes && pl[i].rows; i++) {
+    const u64 w = hd.count * pl[i].group_bytes;
+    for (u64 row = 0; row < pl[i].rows; row++, src += w)
+      memcpy(pl[i].base + row * pl[i].pitch + hd.first * pl[i].group_bytes, src, w);
+  }
+  if (resume) e->round = hd.round;
+  return RBE_OK;
 }
