@@ -435,9 +435,21 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
 #ifndef RBE_DIAG_NO_STATE_STORES
   if constexpr ((STG & STG_OUT) != 0) sr->upd = u;
   else P.upd[r] = u;
+  // the N count words of this sender's row (N odd): one 2-B and (N-1)/2
+  // 4-B stores instead of N 2-B stores, placed by the row's 4-B alignment
   u16* cnt = &P.cnt[o.par][o.g * N * N + o.k * N];
+  {
+    u32 w[N];
 #pragma unroll
-  for (u32 dd = 0; dd < N; dd++) cnt[dd] = (u16)o.get_pc(dd);
+    for (u32 dd = 0; dd < N; dd++) w[dd] = o.get_pc(dd) & 0xFFFFu;
+    const bool odd = ((uintptr_t)cnt & 2u) != 0;
+    *(odd ? cnt : cnt + (N - 1)) = (u16)(odd ? w[0] : w[N - 1]);
+#pragma unroll
+    for (u32 j = 0; j < (N - 1) / 2; j++) {
+      const u32 v = odd ? (w[1 + 2 * j] | (w[2 + 2 * j] << 16)) : (w[2 * j] | (w[2 * j + 1] << 16));
+      __builtin_memcpy(cnt + (odd ? 1 : 0) + 2 * j, &v, sizeof(v));
+    }
+  }
   h.flags = o.fault ? (u8)(flags | HF_FAULTED) : flags;
   h.election_tick = etick;
   h.heartbeat_tick = (u16)htick;
@@ -488,6 +500,10 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   }
   u64 match[N], next[N];
   u32 st[N];
+  // remote slots whose (match, next, state) changed this round: the scatter
+  // stores only those (a heartbeat/ReadIndex round changes none), which saves
+  // 2N scattered store requests per lane in the common case
+  u32 rdirty = 0;
 #pragma unroll
   for (u32 s = 0; s < N; s++) {
     RemoteMN x;
@@ -794,6 +810,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
       if (rs == RS_Replicate) next[s] = nx + cnt;
       else if (rs == RS_Retry) st[s] = (st[s] & ~3u) | RS_Wait;
       else o.set_fault(ctr, F_PANIC);
+      rdirty |= 1u << s;
     }
     o.send(P, C, ctr, m, arena + m.ent_off);
   };
@@ -900,6 +917,8 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
     const u32 jlo = s == 0 ? 0u : s - 1u;
     const u32 jhi = s + 1 >= N ? N - 2u : s;
     const bool use_lo = s > k;
+    const u64 match0 = match[s], next0 = next[s];
+    const u32 st0 = st[s];
 #pragma unroll 1
     for (u32 i = 0; i < nb; i++) {
       LeadIn m = use_lo ? inc[jlo][0] : inc[jhi][0];
@@ -942,6 +961,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
       }
       fan_out();
     }
+    if (match[s] != match0 || next[s] != next0 || st[s] != st0) rdirty |= 1u << s;
   }
   // batchedReadIndex → Peer.ReadIndex → handleLeaderReadIndex (raft.go:1633-1665)
   if (inp == 2) {
@@ -1047,6 +1067,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
 #pragma unroll
       for (u32 s = 0; s < N; s++)
         if (s == k) try_update(match[s], next[s], st[s], c.last_index);
+      rdirty |= 1u << k;
       rep_mask |= ((1u << N) - 1u) & ~(1u << k);
       fan_out();
     }
@@ -1059,9 +1080,13 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
     RemoteMN x;
     x.match = match[s];
     x.next = next[s];
-    if constexpr ((STG & STG_OUT) != 0) sr->rem[s] = x;
-    else P.rem[r * N + s] = x;
-    P.rem_st[r * N + s] = (u8)st[s];
+    if constexpr ((STG & STG_OUT) != 0) {
+      sr->rem[s] = x;
+      P.rem_st[r * N + s] = (u8)st[s];
+    } else if (rdirty & (1u << s)) {
+      P.rem[r * N + s] = x;
+      P.rem_st[r * N + s] = (u8)st[s];
+    }
   }
   if (rq_dirty) {
 #pragma unroll
