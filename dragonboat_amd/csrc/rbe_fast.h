@@ -336,7 +336,8 @@ struct FastQ {
 template <int N, bool TRACE, int STG = 0>
 RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, FastOut<N, TRACE>& o,
                         FastQ& q, u8 role, u8 flags, Hot h, Core c, u32 etick, u32 htick,
-                        u64 committed0, u64 digest0, StageRow<N>* sr = nullptr) {
+                        u64 committed0, u64 digest0, StageRow<N>* sr = nullptr,
+                        u32 core_dirty = 0xFu) {
   const u64 r = o.r;
   // stepNode: sendEnterQuiesceMessages (node.go:873-886)
   const bool send_q = q.qnew;
@@ -394,6 +395,11 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
   if (o.n_rtr) ctr.v[C_READS_CONFIRMED] += o.n_rtr;
   ctr.v[C_DROPPED_READS] += o.n_drop_ri;
   if (u.apply_hi >= u.apply_lo) c.processed = u.apply_hi;
+  // Core's 16-B chunks this step changed: [term, committed] [last_index,
+  // processed] [saved_to, vote..rq_count] [t_last, lead_start]; the caller
+  // passes the chunks its handlers wrote (all four for the leader)
+  core_dirty |= (c.committed != committed0 ? 1u : 0u) | (u.apply_hi >= u.apply_lo ? 2u : 0u) |
+                (c.saved_to != c.last_index ? 4u : 0u);
   c.saved_to = c.last_index;
   if (c.processed < c.committed) flags |= HF_APPLY_PENDING;
   else flags &= (u8)~HF_APPLY_PENDING;
@@ -462,7 +468,10 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
     sr->core = c;
   } else {
     P.hot[r] = h;
-    P.core[r] = c;
+#pragma unroll
+    for (u32 i = 0; i < 4; i++)
+      if (core_dirty & (1u << i))
+        __builtin_memcpy((char*)&P.core[r] + 16 * i, (const char*)&c + 16 * i, 16);
   }
   P.idle[r] = idle_byte(C, role, flags, q.qs);
 #endif
@@ -1185,6 +1194,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   const u32 until = C.iso_period ? P.iso_until[g] : 0u;
   const u8 isom = C.iso_period ? P.iso_mask[g] : (u8)0;
   const u64 digest0 = TRACE ? P.upd[r].digest : 0;
+  u32 cdirty = 0;  // Core chunks an append or a new leader wrote (fast_finish)
   if (h.role != R_Follower) return false;
   if (h.flags & (HF_APPLY_PENDING | HF_IS_LTT)) return false;
   if (c.ltt != 0) return false;
@@ -1401,6 +1411,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
               c.last_index = m.log_index + m.n_ent;
               c.t_last = tl;
               c.saved_to = umin64(c.saved_to, conflict - 1);
+              cdirty |= 0xEu;
             }
           }
           const u64 last_idx = m.log_index + m.n_ent;
@@ -1437,9 +1448,10 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
     etick++;  // nonLeaderTick; reaching the timeout is excluded above
     if (etick >= h.rand_et) o.set_fault(ctr, F_UNSUPPORTED);
   }
+  if (n_in && (u8)lid != c.leader) cdirty |= 4u;
   c.leader = n_in ? (u8)lid : c.leader;
   fast_finish<N, TRACE, STG>(P, C, ctr, o, q, R_Follower, flags, h, c, etick, htick, committed0,
-                        digest0, sr);
+                        digest0, sr, cdirty);
   RBE_STAMP(t5);
   RBE_RSTAMP(rt5);
   RBE_PHASE_ADD(1, 5, rt0, rt5);
