@@ -397,7 +397,7 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
   if (u.apply_hi >= u.apply_lo) c.processed = u.apply_hi;
   // Core's 16-B chunks this step changed: [term, committed] [last_index,
   // processed] [saved_to, vote..rq_count] [t_last, lead_start]; the caller
-  // passes the chunks its handlers wrote (all four for the leader)
+  // passes the chunks its handlers wrote
   core_dirty |= (c.committed != committed0 ? 1u : 0u) | (u.apply_hi >= u.apply_lo ? 2u : 0u) |
                 (c.saved_to != c.last_index ? 4u : 0u);
   c.saved_to = c.last_index;
@@ -560,6 +560,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   const u32 until = C.iso_period ? P.iso_until[g] : 0u;
   const u8 isom = C.iso_period ? P.iso_mask[g] : (u8)0;
   const u64 digest0 = TRACE ? P.upd[r].digest : 0;
+  u32 cdirty = 0;  // Core chunks a proposal or the readIndex queue wrote (fast_finish)
   // ---- eligibility on level-1 data
   if (h.role != R_Leader) return false;
   if (h.flags & (HF_APPLY_PENDING | HF_IS_LTT)) return false;
@@ -1070,6 +1071,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
       ctr.v[C_RING_ACCESS]++;
       c.last_index = idx;
       c.t_last = c.term;
+      cdirty |= 0xEu;
       prop_idx = idx;
       prop_lo = lo;
       prop_hi = hi;
@@ -1112,10 +1114,11 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
       }
     }
   }
+  if ((u8)rq_h != c.rq_head || (u8)rq_n != c.rq_count) cdirty |= 4u;
   c.rq_head = (u8)rq_h;
   c.rq_count = (u8)rq_n;
   fast_finish<N, TRACE, STG>(P, C, ctr, o, q, R_Leader, flags, h, c, etick, htick, committed0,
-                                digest0, sr);
+                                digest0, sr, cdirty);
   RBE_STAMP(t5);
   RBE_RSTAMP(rt5);
   RBE_PHASE_ADD(0, 5, rt0, rt5);
