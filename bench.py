@@ -61,6 +61,12 @@ WORKLOADS = {
 }
 
 
+# bounded CPU-baseline samples (groups for the T-thread run, groups for the
+# 1-thread run), sized for ~5-15 s of host time each on the GPU box
+CPU_SAMPLE = {"c4": (300_000, 30_000), "c2": (10_000, 10_000), "c2m": (100_000, 10_000),
+              "c3": (50_000, 5_000), "c5": (100_000, 10_000)}
+
+
 def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -68,9 +74,28 @@ def dist_env():
     return ws, rank, local
 
 
-def cpu_baseline(name, groups, settle, rounds, threads):
-    """The oracle (C++ restatement of internal/raft, test infrastructure) on a
-    bounded sample of the same workload, timed on this host's cores."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_threads():
+    """Threads the CPU baseline may use: BASELINE.md asks for T = nproc, but on
+    the GPU box nproc reports the whole machine while the job is granted a
+    share (OMP_NUM_THREADS, 16 per GPU); T is the smaller of the affinity set
+    and that share."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(aff, share) if share > 0 else aff), aff
+
+
+def _oracle_rate(name, groups, settle, rounds, threads):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     kw, _, _ = WORKLOADS[name]
@@ -84,19 +109,51 @@ def cpu_baseline(name, groups, settle, rounds, threads):
     h.run(rounds)
     dt = time.perf_counter() - t0
     c1 = h.counters()
-    steps = c1["steps"] - c0["steps"]
+    return ((c1["steps"] - c0["steps"]) / dt, (c1["committed"] - c0["committed"]) / dt,
+            (c1["reads_confirmed"] - c0["reads_confirmed"]) / dt, dt)
+
+
+def cpu_baseline(name, groups, settle, rounds, threads, groups_1t, rounds_1t):
+    """The oracle (C++ restatement of internal/raft, test infrastructure) on a
+    bounded sample of the same workload, timed on this host's cores: T threads
+    with groups partitioned cid % T (FixedPartitioner), plus a 1-thread run
+    (CPU baseline plan)."""
+    v, ce, rc, dt = _oracle_rate(name, groups, settle, rounds, threads)
+    v1, ce1, rc1, dt1 = _oracle_rate(name, groups_1t, settle, rounds_1t, 1)
+    _, aff = host_threads()
+    kw, _, _ = WORKLOADS[name]
     return {
-        "value": steps / dt,
+        "value": v,
         "unit": "group-steps/s",
         "cores": threads,
         "kind": "port",
+        "cpu_model": cpu_model(),
+        "host_cpus_visible": aff,
+        "nproc": os.cpu_count(),
         "sample": (f"{groups} groups x {kw['n_replicas']} replicas of the same workload, "
                    f"{rounds} timed rounds after a {settle}-round settle; C++ restatement "
                    f"of internal/raft (oracle/), not Go; {threads} threads, groups "
                    f"partitioned cid % threads"),
-        "committed_entries_per_s": (c1["committed"] - c0["committed"]) / dt,
+        "committed_entries_per_s": ce,
+        "read_confirmations_per_s": rc,
         "seconds": dt,
+        "one_thread": {"value": v1, "unit": "group-steps/s", "cores": 1,
+                       "committed_entries_per_s": ce1, "read_confirmations_per_s": rc1,
+                       "sample": f"{groups_1t} groups, {rounds_1t} timed rounds",
+                       "seconds": dt1},
     }
+
+
+def lib_identity():
+    """Path and content hash of the engine library this process loaded (RBE_LIB
+    can point at an A/B build; the bench line records which one it timed)."""
+    import hashlib
+    from dragonboat_amd import engine as E
+    p = os.environ.get("RBE_LIB") or E.LIB_PATH
+    h = hashlib.sha256()
+    with open(p, "rb") as f:
+        h.update(f.read())
+    return {"path": os.path.relpath(p, ROOT), "sha256_16": h.hexdigest()[:16]}
 
 
 def alg_bytes(c):
@@ -234,10 +291,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--prof-rounds", type=int, default=50,
                     help="rounds profiled per kernel with HIP events after the timed region")
-    ap.add_argument("--cpu-groups", type=int, default=300000)
+    ap.add_argument("--cpu-groups", type=int, default=0,
+                    help="groups in the T-thread CPU sample (0 = per-workload default)")
     ap.add_argument("--cpu-rounds", type=int, default=100)
-    ap.add_argument("--cpu-threads", type=int,
-                    default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = host_threads()")
+    ap.add_argument("--cpu-groups-1t", type=int, default=0,
+                    help="groups in the 1-thread CPU sample (0 = per-workload default)")
     ap.add_argument("--xchg-gloo", action="store_true",
                     help="c5 rehearsal: all ranks on cuda:0, exchange over gloo via host memory")
     args = ap.parse_args()
@@ -368,10 +427,15 @@ def main():
                 "kernels": kernels,
             },
         }
+        out["library"] = lib_identity()
         if not args.no_cpu_baseline and ws == 1:
             try:
-                out["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_groups,
-                                                   settle, args.cpu_rounds, args.cpu_threads)
+                ng = int(kw["n_groups"])
+                g_t = args.cpu_groups or min(ng, CPU_SAMPLE[args.workload][0])
+                g_1 = args.cpu_groups_1t or min(ng, CPU_SAMPLE[args.workload][1])
+                threads = args.cpu_threads or host_threads()[0]
+                out["cpu_baseline"] = cpu_baseline(args.workload, g_t, settle, args.cpu_rounds,
+                                                   threads, g_1, args.cpu_rounds)
             except Exception as ex:  # the baseline must not hide the GPU number
                 out["cpu_baseline"] = {"error": repr(ex)}
         print(json.dumps(out), flush=True)

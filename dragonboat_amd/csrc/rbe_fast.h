@@ -443,6 +443,7 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
   else P.upd[r] = u;
   // the N count words of this sender's row (N odd): one 2-B and (N-1)/2
   // 4-B stores instead of N 2-B stores, placed by the row's 4-B alignment
+  static_assert(N % 2 == 1, "the packed count-word store covers odd N only");
   u16* cnt = &P.cnt[o.par][o.g * N * N + o.k * N];
   {
     u32 w[N];

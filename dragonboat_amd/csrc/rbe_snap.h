@@ -79,6 +79,25 @@ inline u64 snap_body_bytes(const Planes& P, const Params& C, u64 count) {
   return b;
 }
 
+// Hash of every Params field that changes how a replica steps (timeouts,
+// quorum check, quiesce, the injected PRNG seed, cluster-id mapping, entry
+// size limit, workload, fault schedule, replica placement): a snapshot only
+// resumes bit-exact under the configuration that wrote it, so import rejects
+// a mismatch instead of diverging silently (reserved[0] of the header).
+inline u64 snap_behavior_hash(const Params& C) {
+  const u64 f[] = {C.election_rtt, C.heartbeat_rtt, C.check_quorum, C.quiesce, C.seed,
+                   C.cid_base, C.cid_stride, C.max_entry_size, C.wl_enabled, C.wl_start_round,
+                   C.wl_stop_round, C.wl_active_mod, C.wl_read_permille, C.ext_inputs,
+                   C.iso_period, C.iso_len, C.iso_mod, C.rep_world, C.rep_rank,
+                   C.snapshot_entries, C.compaction_overhead, C.heap_bytes, C.ext_apply};
+  u64 h = 0x243F6A8885A308D3ull;
+  for (u64 x : f) {
+    h ^= x + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    h *= 0xBF58476D1CE4E5B9ull;
+  }
+  return h;
+}
+
 inline void snap_fill_header(const Params& C, u32 abi, u32 round, u64 first, u64 count, u64 body,
                              SnapHeader* h) {
   *h = SnapHeader{};
@@ -96,6 +115,7 @@ inline void snap_fill_header(const Params& C, u32 abi, u32 round, u64 first, u64
   h->first = first;
   h->count = count;
   h->body_bytes = body;
+  h->reserved[0] = snap_behavior_hash(C);
 }
 
 // 0 if the header describes a range this geometry can take, else RBE_E_INVALID.
@@ -106,6 +126,7 @@ inline int snap_check_header(const Params& C, u32 abi, const SnapHeader* h, u64 
   if (h->n != C.n || h->ring != C.ring || h->rq_cap != C.rq_cap || h->maxm != C.maxm ||
       h->ecap != C.ecap || h->rtr_cap != C.rtr_cap || h->dri_cap != C.dri_cap)
     return -1;
+  if (h->reserved[0] != snap_behavior_hash(C)) return -1;
   if (h->count == 0 || h->first >= C.n_groups || h->count > C.n_groups - h->first) return -1;
   if (buf_bytes < sizeof(SnapHeader) + h->body_bytes) return -1;
   return 0;

@@ -105,6 +105,33 @@ RBE_HD u8 idle_byte(const Params& C, u8 role, u8 flags, u32 qs) {
 }
 RBE_HD u32 idle_role(u8 ib) { return (ib >> IB_ROLE_SHIFT) & 7u; }
 
+// The Update helpers of peer.go on the engine's range form of an Update
+// (EntriesToSave = [save_lo, save_hi], CommittedEntries = [apply_lo,
+// apply_hi], empty when lo > hi).
+// setFastApply (peer.go:209-226)
+RBE_HD bool update_fast_apply(bool has_snapshot, u64 save_lo, u64 save_hi, u64 apply_lo,
+                              u64 apply_hi) {
+  if (has_snapshot) return false;
+  if (apply_lo <= apply_hi && save_lo <= save_hi && apply_hi >= save_lo && apply_hi <= save_hi)
+    return false;
+  return true;
+}
+// validateUpdate (peer.go:228-245): false where the reference panics
+RBE_HD bool update_valid(u64 commit, u64 save_lo, u64 save_hi, u64 apply_lo, u64 apply_hi) {
+  if (commit > 0 && apply_lo <= apply_hi && apply_hi > commit) return false;
+  if (apply_lo <= apply_hi && save_lo <= save_hi && apply_hi > save_hi) return false;
+  return true;
+}
+// getUpdateCommit (peer.go:410-427): {processed, stable_log_to,
+// stable_snapshot_to}; StableLogTerm is the term of entry save_hi
+RBE_HD void update_commit(u64 save_lo, u64 save_hi, u64 apply_lo, u64 apply_hi, u64 snap_index,
+                          u64* processed, u64* stable_log_to, u64* stable_snapshot_to) {
+  *processed = apply_lo <= apply_hi ? apply_hi : 0;
+  *stable_log_to = save_lo <= save_hi ? save_hi : 0;
+  *stable_snapshot_to = snap_index;
+  if (snap_index != 0 && snap_index > *processed) *processed = snap_index;
+}
+
 RBE_HD bool is_leader_message(u32 t) {  // raft.go:1382-1385
   return t == M_Replicate || t == M_InstallSnapshot || t == M_Heartbeat || t == M_TimeoutNow ||
          t == M_ReadIndexResp;

@@ -200,7 +200,11 @@ struct Params {
   u32 iso_period, iso_len, iso_mod;
   u32 rep_world;      // replica-per-GPU mode when > 1 (rbe_xchg.h)
   u32 rep_rank;
+  u32 ext_apply;      // applied index comes from rbe_notify_applied (raft.applied lags processed)
+  u32 snapshot_entries;     // config.SnapshotEntries: snapshot + compact every that many applied entries (0 = never)
+  u32 compaction_overhead;  // config.CompactionOverhead: entries kept below the snapshot
   u32 pad;
+  u64 heap_bytes;     // per-replica payload heap for commands > 16 B (0 = inline commands only)
 };
 
 // device pointers of every plane

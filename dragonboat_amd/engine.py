@@ -276,7 +276,9 @@ class Engine:
         buf = (C.c_uint8 * (16 * n))()
         lens = (C.c_uint32 * n)()
         for i, c in enumerate(cmds):
-            for j, b in enumerate(c[:16]):
+            if len(c) > 16:  # the C side rejects it too (RBE_E_INVALID); never truncate
+                raise ValueError(f"proposal {i} is {len(c)} bytes; inline commands are <= 16")
+            for j, b in enumerate(c):
                 buf[16 * i + j] = b
             lens[i] = min(16, len(c))
         _check(self.lib.rbe_push_proposals(self.h, n, rep, buf, lens), "rbe_push_proposals")
@@ -359,13 +361,14 @@ class Engine:
         u = self.updates()
         return np.array([x.digest for x in u], dtype=np.uint64)
 
-    def messages(self, replica: int):
-        cap = 256
+    def messages(self, replica: int, cap: int = 256):
         arr = (RbeMessage * cap)()
         n = C.c_uint32()
         _check(self.lib.rbe_get_messages(self.h, replica, arr, cap, C.byref(n)),
                "rbe_get_messages")
-        return [arr[i] for i in range(min(n.value, cap))]
+        if n.value > cap:  # never truncate silently (outbox() raises the same way)
+            return self.messages(replica, n.value)
+        return [arr[i] for i in range(n.value)]
 
     def outbox(self, replica: int, cap: int = 256, ent_cap: int = 1024):
         """The last round's messages of `replica` in transport order, with the

@@ -73,6 +73,62 @@ struct ReplicaView {  // mirrors rbe_replica_view in include/rbe.h
   u32 rstate[8], ractive[8];
 };
 
+// ------------------------------------------------------------ quiesce.go
+// (node-side; also unit-tested against quiesce_test.go through orc_quiesce_*)
+struct QuiesceManager {  // quiesce.go:23-33
+  u64 tick = 0, electionTick = 0, quiescedSince = 0, noActivitySince = 0,
+      exitQuiesceTick = 0;
+  bool enabled = false;
+  bool newFlag = false;
+
+  bool newQuiesceState() {  // quiesce.go:39-41
+    bool v = newFlag;
+    newFlag = false;
+    return v;
+  }
+  u64 threshold() const { return electionTick * 10; }  // quiesce.go:84-86
+  bool quiesced() const { return enabled && quiescedSince > 0; }  // quiesce.go:57-62
+  bool newToQuiesce() const {  // quiesce.go:88-93
+    if (!quiesced()) return false;
+    return tick - quiescedSince < electionTick;
+  }
+  bool justExitedQuiesce() const {  // quiesce.go:95-100
+    if (quiesced()) return false;
+    return tick - exitQuiesceTick < threshold();
+  }
+  void enterQuiesce() {  // quiesce.go:112-117
+    quiescedSince = tick;
+    noActivitySince = tick;
+    newFlag = true;
+  }
+  void exitQuiesce() {  // quiesce.go:119-122
+    quiescedSince = 0;
+    exitQuiesceTick = tick;
+  }
+  u64 increaseQuiesceTick() {  // quiesce.go:43-55
+    if (!enabled) return 0;
+    u64 th = threshold();
+    tick++;
+    if (!quiesced()) {
+      if (tick - noActivitySince > th) enterQuiesce();
+    }
+    return tick;
+  }
+  void recordActivity(int t) {  // quiesce.go:64-82
+    if (!enabled) return;
+    if (t == Heartbeat || t == HeartbeatResp) {
+      if (!quiesced()) return;
+      if (newToQuiesce()) return;
+    }
+    noActivitySince = tick;
+    if (quiesced()) exitQuiesce();
+  }
+  void tryEnterQuiesce() {  // quiesce.go:102-110
+    if (justExitedQuiesce()) return;
+    if (!quiesced()) enterQuiesce();
+  }
+};
+
 struct Harness;
 Harness* harness_create(const HarnessConfig& cfg);
 void harness_destroy(Harness* h);

@@ -379,7 +379,8 @@ _CALLS = ["become_follower", "become_candidate", "become_leader", "tick", "quies
           "handle_vote_resp", "can_grant_vote", "inmem_try_resize", "inmem_resize",
           "log_has_entries_to_apply", "log_first_not_applied_index", "inmem_saved_log_to",
           "time_for_election", "set_randomized_election_timeout", "abort_leader_transfer",
-          "leader_transfering", "quiesced_tick_direct", "non_leader_tick", "leader_tick"]
+          "leader_transfering", "quiesced_tick_direct", "non_leader_tick", "leader_tick",
+          "load_state"]
 _CALL_IDX = {n: i for i, n in enumerate(_CALLS)}
 KIND = {"remotes": 0, "observers": 1, "witnesses": 2}
 

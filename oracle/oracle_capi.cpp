@@ -344,7 +344,7 @@ enum RaftCall {
   C_HANDLE_VOTE_RESP, C_CAN_GRANT_VOTE, C_INMEM_TRY_RESIZE, C_INMEM_RESIZE,
   C_LOG_HAS_ENTRIES_TO_APPLY, C_LOG_FIRST_NOT_APPLIED, C_LOG_SAVED_LOG_TO, C_TIME_FOR_ELECTION,
   C_SET_RANDOMIZED_ET, C_ABORT_LT, C_LEADER_TRANSFERING, C_QUIESCED_TICK_DIRECT,
-  C_NON_LEADER_TICK, C_LEADER_TICK
+  C_NON_LEADER_TICK, C_LEADER_TICK, C_LOAD_STATE
 };
 
 int64_t orc_raft_call(void* rp, int fn, uint64_t a, uint64_t b) {
@@ -394,6 +394,7 @@ int64_t orc_raft_call(void* rp, int fn, uint64_t a, uint64_t b) {
     case C_QUIESCED_TICK_DIRECT: r->quiescedTick(); return 0;
     case C_NON_LEADER_TICK: r->nonLeaderTick(); return 0;
     case C_LEADER_TICK: r->leaderTick(); return 0;
+    case C_LOAD_STATE: { PState st; st.term = a; st.commit = b; r->loadState(st); return 0; }
     default: g_err = "bad call"; return -1000;
   }
   GUARD_END(-999)
@@ -835,3 +836,150 @@ int orc_view_size() { return (int)sizeof(ReplicaView); }
 uint64_t orc_splitmix64(uint64_t x) { return splitmix64(x); }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- quiesce.go
+// Unit access to the node-side quiesce manager (quiesce.go:23-123), pinned by
+// quiesce_test.go (tests/test_quiesce.py).
+extern "C" {
+void* orc_quiesce_new(uint64_t election_tick, int enabled) {
+  auto* q = new QuiesceManager();
+  q->electionTick = election_tick;
+  q->enabled = enabled != 0;
+  return q;
+}
+void orc_quiesce_free(void* q) { delete (QuiesceManager*)q; }
+// op: 0 increaseQuiesceTick, 1 recordActivity(a), 2 tryEnterQuiesce,
+//     3 quiesced, 4 newToQuiesce, 5 quiesceThreshold, 6 tick, 7 noActivitySince,
+//     8 quiescedSince, 9 exitQuiesceTick, 10 newQuiesceState, 11 set enabled(a)
+uint64_t orc_quiesce_op(void* qp, int op, uint64_t a) {
+  auto* q = (QuiesceManager*)qp;
+  switch (op) {
+    case 0: return q->increaseQuiesceTick();
+    case 1: q->recordActivity((int)a); return 0;
+    case 2: q->tryEnterQuiesce(); return 0;
+    case 3: return q->quiesced() ? 1 : 0;
+    case 4: return q->newToQuiesce() ? 1 : 0;
+    case 5: return q->threshold();
+    case 6: return q->tick;
+    case 7: return q->noActivitySince;
+    case 8: return q->quiescedSince;
+    case 9: return q->exitQuiesceTick;
+    case 10: return q->newQuiesceState() ? 1 : 0;
+    case 11: q->enabled = a != 0; return 0;
+    default: return ~0ull;
+  }
+}
+}
+
+// ---------------------------------------------------------------- inmemory.go
+// Unit access to the in-memory entry window (inmemory.go:36-246), pinned by
+// inmemory_test.go (tests/test_oracle_inmem.py).
+extern "C" {
+void* orc_inmem_new(uint64_t marker, const orc_entry* ents, int n, uint64_t saved_to, int shrunk) {
+  auto* im = new InMemory();
+  im->markerIndex = marker;
+  for (int i = 0; i < n; i++) im->entries.push_back(to_entry(ents[i]));
+  im->savedTo = saved_to;
+  im->shrunk = shrunk != 0;
+  return im;
+}
+void orc_inmem_free(void* h) { delete (InMemory*)h; }
+int orc_inmem_merge(void* h, const orc_entry* ents, int n) {
+  GUARD_BEGIN
+  std::vector<Entry> v;
+  for (int i = 0; i < n; i++) v.push_back(to_entry(ents[i]));
+  ((InMemory*)h)->merge(v);
+  return 0;
+  GUARD_END(-1)
+}
+// op: 0 savedLogTo(a, b), 1 appliedLogTo(a), 2 getLastIndex (-1 when !ok),
+//     3 getTerm(a) (-1 when !ok), 4 markerIndex, 5 savedTo, 6 shrunk, 7 len(entries),
+//     8 entries[0].Index (-1 when empty), 9 restore(Snapshot{Index: a, Term: b}), 10 resize
+int64_t orc_inmem_op(void* h, int op, uint64_t a, uint64_t b) {
+  GUARD_BEGIN
+  auto* im = (InMemory*)h;
+  u64 v = 0;
+  switch (op) {
+    case 0: im->savedLogTo(a, b); return 0;
+    case 1: im->appliedLogTo(a); return 0;
+    case 2: return im->getLastIndex(&v) ? (int64_t)v : -1;
+    case 3: return im->getTerm(a, &v) ? (int64_t)v : -1;
+    case 4: return (int64_t)im->markerIndex;
+    case 5: return (int64_t)im->savedTo;
+    case 6: return im->shrunk ? 1 : 0;
+    case 7: return (int64_t)im->entries.size();
+    case 8: return im->entries.empty() ? -1 : (int64_t)im->entries[0].index;
+    case 9: {
+      Snapshot ss;
+      ss.index = a;
+      ss.term = b;
+      im->restore(ss);
+      return 0;
+    }
+    case 10: im->resize(); return 0;
+    default: return -2;
+  }
+  GUARD_END(-3)
+}
+int orc_inmem_entries_to_save(void* h, orc_entry* out, int cap) {
+  GUARD_BEGIN
+  auto v = ((InMemory*)h)->entriesToSave();
+  int n = 0;
+  for (auto& e : v) {
+    if (n < cap) from_entry(e, &out[n]);
+    n++;
+  }
+  return n;
+  GUARD_END(-1)
+}
+}
+
+// ---------------------------------------------------------------- Update helpers
+// getUpdateCommit / validateUpdate / setFastApply (peer.go:209-245, 410-427) on
+// an Update built from (index, term) pairs, for peer_test.go's tables
+// (tests/test_update.py).  fn 0: getUpdateCommit → out6 = {processed,
+// last_applied, stable_log_to, stable_log_term, stable_snapshot_to,
+// ready_to_read}; fn 1: validateUpdate (-1 = panic); fn 2: setFastApply →
+// out6[0] = FastApply.
+extern "C" int orc_update_fn(int fn, uint64_t commit, const uint64_t* cents, int nc,
+                             const uint64_t* sents, int ns, uint64_t snap_index,
+                             uint64_t last_applied, uint64_t* out6) {
+  GUARD_BEGIN
+  Update ud;
+  ud.state.commit = commit;
+  for (int i = 0; i < nc; i++) {
+    Entry e;
+    e.index = cents[2 * i];
+    e.term = cents[2 * i + 1];
+    ud.committed_entries.push_back(e);
+  }
+  for (int i = 0; i < ns; i++) {
+    Entry e;
+    e.index = sents[2 * i];
+    e.term = sents[2 * i + 1];
+    ud.entries_to_save.push_back(e);
+  }
+  ud.snapshot.index = snap_index;
+  ud.last_applied = last_applied;
+  if (fn == 0) {
+    UpdateCommit uc = getUpdateCommit(ud);
+    out6[0] = uc.processed;
+    out6[1] = uc.last_applied;
+    out6[2] = uc.stable_log_to;
+    out6[3] = uc.stable_log_term;
+    out6[4] = uc.stable_snapshot_to;
+    out6[5] = uc.ready_to_read;
+    return 0;
+  }
+  if (fn == 1) {
+    validateUpdate(ud);
+    return 0;
+  }
+  if (fn == 2) {
+    ud.fast_apply = true;
+    out6[0] = setFastApply(ud).fast_apply ? 1 : 0;
+    return 0;
+  }
+  return -2;
+  GUARD_END(-1)
+}

@@ -393,3 +393,90 @@ extern "C" int soa_import_groups(void* h, const void* buf, uint64_t bytes, uint3
   if (resume) e->round = hd.round;
   return RBE_OK;
 }
+
+// ---------------------------------------------------------------- quiesce FSM
+// The device-side quiesce manager restatements (Lane::q_* used by the full
+// handler table, FastQ used by the fast steps), driven op by op so the
+// reference's quiesce_test.go vectors pin them directly (tests/test_quiesce.py).
+struct SoaQuiesce {
+  Params C;
+  Planes P;
+  StepCounters ctr;
+  Lane<3, false, MODE_FULL>* lane;
+  FastQ fq;
+  int which;  // 0 = Lane, 1 = FastQ
+};
+extern "C" void* soa_quiesce_new(uint64_t election_tick, int enabled, int which) {
+  auto* s = new SoaQuiesce();
+  memset(&s->C, 0, sizeof(s->C));
+  memset(&s->P, 0, sizeof(s->P));
+  memset(&s->ctr, 0, sizeof(s->ctr));
+  s->C.election_rtt = (u32)(election_tick / 2);  // node.go:165 electionTick = 2 x ElectionRTT
+  s->C.quiesce = enabled ? 1 : 0;
+  s->lane = new Lane<3, false, MODE_FULL>(s->P, s->C, 0, 0, s->ctr);
+  s->lane->q_tick = s->lane->q_qs = s->lane->q_nas = s->lane->q_eqt = 0;
+  s->lane->q_new = false;
+  s->fq.tick = s->fq.qs = s->fq.nas = s->fq.eqt = 0;
+  s->fq.qnew = false;
+  s->which = which;
+  return s;
+}
+extern "C" void soa_quiesce_free(void* h) {
+  auto* s = (SoaQuiesce*)h;
+  delete s->lane;
+  delete s;
+}
+// same op codes as orc_quiesce_op (oracle/oracle_capi.cpp)
+extern "C" uint64_t soa_quiesce_op(void* h, int op, uint64_t a) {
+  auto* s = (SoaQuiesce*)h;
+  auto& L = *s->lane;
+  auto& q = s->fq;
+  const bool lane = s->which == 0;
+  switch (op) {
+    case 0:
+      if (lane) L.q_increase_tick();
+      else q.increase_tick(s->C);
+      return lane ? L.q_tick : q.tick;
+    case 1:
+      if (lane) L.q_record_activity((u32)a);
+      else q.record_activity(s->C, (u32)a);
+      return 0;
+    case 2:
+      if (lane) L.q_try_enter();
+      else q.try_enter(s->C);
+      return 0;
+    case 3: return (lane ? L.q_quiesced() : q.quiesced(s->C)) ? 1 : 0;
+    case 4: return (lane ? L.q_new_to_quiesce() : q.new_to_quiesce(s->C)) ? 1 : 0;
+    case 5: return lane ? L.q_threshold() : s->C.election_rtt * 20;
+    case 6: return lane ? L.q_tick : q.tick;
+    case 7: return lane ? L.q_nas : q.nas;
+    case 8: return lane ? L.q_qs : q.qs;
+    case 9: return lane ? L.q_eqt : q.eqt;
+    case 10: {
+      bool v = lane ? L.q_new : q.qnew;
+      if (lane) L.q_new = false;
+      else q.qnew = false;
+      return v ? 1 : 0;
+    }
+    case 11: s->C.quiesce = a ? 1 : 0; return 0;
+    default: return ~0ull;
+  }
+}
+
+// ---------------------------------------------------------------- Update helpers
+// the engine's range-form restatements of getUpdateCommit / validateUpdate /
+// setFastApply (rbe_step.h update_*), same fn codes as orc_update_fn
+extern "C" int soa_update_fn(int fn, uint64_t commit, uint64_t apply_lo, uint64_t apply_hi,
+                             uint64_t save_lo, uint64_t save_hi, uint64_t snap_index,
+                             uint64_t* out3) {
+  if (fn == 0) {
+    update_commit(save_lo, save_hi, apply_lo, apply_hi, snap_index, &out3[0], &out3[1], &out3[2]);
+    return 0;
+  }
+  if (fn == 1) return update_valid(commit, save_lo, save_hi, apply_lo, apply_hi) ? 0 : -1;
+  if (fn == 2) {
+    out3[0] = update_fast_apply(snap_index != 0, save_lo, save_hi, apply_lo, apply_hi) ? 1 : 0;
+    return 0;
+  }
+  return -2;
+}
