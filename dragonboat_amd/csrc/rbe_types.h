@@ -140,11 +140,21 @@ struct alignas(16) Upd {
   u16 n_drop_ri;    // DroppedReadIndexes
   u32 fault;        // sticky F_* bits
   u16 flags;        // UF_* bits
-  u16 pad;
+  u16 events;       // EV_* bits: IRaftEventListener calls of the step
   u32 round;        // round this record was written in (idle rounds leave it stale)
   u32 pad2;
 };
 enum : u32 { UF_STATE_CHANGED = 1, UF_SENT_QUIESCE = 2, UF_HAS_UPDATE = 4 };
+// server.IRaftEventListener (internal/server/event.go) calls a step made, one
+// bit per event kind (raft.go:354, 1090, 1333, 1368, 1503, 1995, 2010).
+// LeaderUpdated fires on every setLeaderID call in the reference, unchanged
+// leaders included (SURVEY.md appendix trap 9); EV_LEADER_UPDATED marks a step
+// whose leader value changed, the event a listener acts on (event.go:93-95).
+enum : u32 {
+  EV_LEADER_UPDATED = 1, EV_CAMPAIGN_LAUNCHED = 2, EV_CAMPAIGN_SKIPPED = 4,
+  EV_SNAPSHOT_REJECTED = 8, EV_REPLICATION_REJECTED = 16, EV_PROPOSAL_DROPPED = 32,
+  EV_READ_INDEX_DROPPED = 64
+};
 
 struct RTR {  // ReadyToRead, raftpb/raft.go:52-56
   u64 index, low, high;
@@ -153,14 +163,24 @@ struct DropRI {  // SystemCtx
   u64 low, high;
 };
 
-// external (host-pushed) client input for one replica, consumed by the next
-// step (rbe_push_proposals / rbe_push_read_index)
+// Host-pushed input of one replica, consumed by the next step: the node-side
+// events of handleEvents (node.go:1030-1067) that are not network messages
+// (rbe_push_proposals / rbe_push_read_index / rbe_request_leader_transfer /
+// rbe_report_unreachable / rbe_report_snapshot_status).  `flags` says which
+// parts are present; a replica takes at most one of each per step, as the
+// node batches them (one ReadIndex ctx per step, node.go:1379-1382; one
+// proposal batch, 1091-1106; one pending transfer, 1069-1075).
+enum : u32 { EXT_PROPOSE = 1, EXT_READ = 2, EXT_XFER = 4, EXT_UNREACH = 8, EXT_SNAPST = 16 };
 struct alignas(16) ExtIn {
-  u32 kind;  // 0 none, 1 propose, 2 read index
-  u32 len;
-  u64 lo, hi;       // proposal Cmd
-  u64 ctx_low, ctx_high;
-  u64 pad;
+  u32 flags;
+  u32 n_prop;        // entries of the proposal batch (EXT_PROPOSE)
+  u32 prop_off;      // its first entry in Planes::in_ents
+  u8 xfer_target;    // RequestLeaderTransfer target node id (EXT_XFER)
+  u8 unreach;        // ReportUnreachableNode: bit (id-1) per node (EXT_UNREACH)
+  u8 snap_nodes;     // ReportSnapshotStatus: bit (id-1) per node (EXT_SNAPST)
+  u8 snap_reject;    //   ... reject flag per node
+  u64 ctx_low, ctx_high;  // ReadIndex SystemCtx (EXT_READ)
+  u64 pad[4];
 };
 
 // counters (shared numbering with oracle/harness.h HC_*)
@@ -203,8 +223,18 @@ struct Params {
   u32 ext_apply;      // applied index comes from rbe_notify_applied (raft.applied lags processed)
   u32 snapshot_entries;     // config.SnapshotEntries: snapshot + compact every that many applied entries (0 = never)
   u32 compaction_overhead;  // config.CompactionOverhead: entries kept below the snapshot
-  u32 pad;
+  u32 in_cap;         // host-pushed proposal entries per step (Planes::in_ents)
   u64 heap_bytes;     // per-replica payload heap for commands > 16 B (0 = inline commands only)
+  // leader-transfer schedule (RequestLeaderTransfer on a seeded replica), 0 = off
+  u32 xfer_period;
+  u32 xfer_mod;
+};
+
+// The clock of one round: `round` numbers every rbe_step, `tclk` counts the
+// ticks before it (every replica ticks together, as tickWorkerMain ticks
+// every node, nodehost.go:1668-1684), `tick` says whether this round ticks.
+struct Clk {
+  u32 round, tclk, tick;
 };
 
 // device pointers of every plane
@@ -227,6 +257,8 @@ struct Planes {
   RTR* rtr;           // [n_rep * rtr_cap]
   DropRI* dri;        // [n_rep * dri_cap]
   ExtIn* ext;         // [n_rep]
+  Ent* in_ents;       // [in_cap] proposal entries pushed for the next step
+  u64* applied;       // [n_rep] raft.applied from rbe_notify_applied (ext_apply)
   u64* counters;      // [C_NUM]
 };
 
