@@ -17,6 +17,7 @@
 
 #include "../../include/rbe.h"
 #include "rbe_fast.h"
+#include "rbe_host.h"
 #include "rbe_snap.h"
 #include "rbe_xchg.h"
 
@@ -59,6 +60,21 @@ static constexpr int kCtrStripes = 64;   // counter stripes per kernel slot (flu
 enum : int { KS_TRIAGE = 0, KS_FAST_LEAD = 1, KS_FAST_FOLL = 2, KS_FULL = 3, KS_NUM = 4 };
 static constexpr u64 kCtrWords = (u64)KS_NUM * kCtrStripes * C_NUM;
 
+// Where a kernel finds its round: the device clock {round, tclk} at `ptr`
+// (graph replay, advanced on device by k_advance) or 0, plus offsets; `tick`
+// says whether the round ticks (rbe_step_ex with RBE_STEP_NO_TICK: no).
+struct RoundArg {
+  const u32* ptr;
+  u32 round_add, tclk_add, tick;
+};
+__device__ __forceinline__ Clk clk_of(const RoundArg& a) {
+  Clk c;
+  c.round = (a.ptr ? a.ptr[0] : 0u) + a.round_add;
+  c.tclk = (a.ptr ? a.ptr[1] : 0u) + a.tclk_add;
+  c.tick = a.tick;
+  return c;
+}
+
 // ------------------------------------------------------------------ kernels
 __device__ __forceinline__ u32 wave_sum(u32 v) {
 #pragma unroll
@@ -96,14 +112,13 @@ __device__ __forceinline__ void flush_counters(const Planes& P, const StepCounte
 
 // The whole handler table over every replica (reference mode, RBE_MODE=full).
 template <int N, bool TRACE>
-__global__ __launch_bounds__(kBlock) void k_step(Planes P, Params C, const u32* round_ptr,
-                                                 u32 round_add) {
-  const u32 round = (round_ptr ? *round_ptr : 0u) + round_add;
+__global__ __launch_bounds__(kBlock) void k_step(Planes P, Params C, RoundArg ra) {
+  const Clk ck = clk_of(ra);
   const u64 r = (u64)blockIdx.x * kBlock + threadIdx.x;
   StepCounters c;
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
-  if (r < C.n_rep && owned<N>(C, r)) step_replica<N, TRACE>(P, C, r, round, c);
+  if (r < C.n_rep && owned<N>(C, r)) step_replica<N, TRACE>(P, C, r, ck, c);
   flush_counters<KS_FULL>(P, c);
 }
 
@@ -157,11 +172,11 @@ __device__ __forceinline__ void list_push(const Lists& L, u32 list, u32 par, boo
 // atomics, then reserves space in each global list with ONE atomic per list
 // and copies its entries out coalesced.
 template <int N, bool TRACE>
-__global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, const u32* round_ptr,
-                                                   u32 round_add, Lists L) {
+__global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg ra, Lists L) {
   __shared__ u32 s_idx[3][kTriChunk];
   __shared__ u32 s_n[5], s_base[5];  // fronts of lists 0..2, backs of lists 0..1
-  const u32 round = (round_ptr ? *round_ptr : 0u) + round_add;
+  const Clk ck = clk_of(ra);
+  const u32 round = ck.round;
   const u32 par = round & 1u;
   if (blockIdx.x == 0 && threadIdx.x < 5)
     L.counts[(threadIdx.x < 3 ? threadIdx.x * 2 : 6 + (threadIdx.x - 3) * 2) + (par ^ 1u)] = 0;
@@ -218,12 +233,12 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, const u32
     const u32 inb = (inbp >> (3 * i)) & 7u;
     u32 cls = T_DONE;
     if (r < C.n_rep && owned<N>(C, r)) {
-      if (shortcut && triage_lazy<N>(P, C, r, round, ib, inb & 1u, c))
+      if (shortcut && triage_lazy<N>(P, C, r, ck, ib, inb & 1u, c))
         cls = T_DONE;
       else if (inb & 2u)
         cls = class_of_role(idle_role(ib));
       else
-        cls = triage_replica<N, TRACE>(P, C, r, round, c);
+        cls = triage_replica<N, TRACE>(P, C, r, ck, c);
     }
     // the back of the list: a leader proposing this round, a follower
     // receiving a Replicate
@@ -284,11 +299,11 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, const u32
 // lists never touch HBM, and the latency-bound protocol work of some blocks
 // overlaps the streaming triage of others.
 template <int N, bool TRACE>
-__global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_round(Planes P, Params C, const u32* round_ptr,
-                                                  u32 round_add, Lists L) {
+__global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_round(Planes P, Params C, RoundArg ra, Lists L) {
   __shared__ u32 s_idx[kTriChunk];
   __shared__ u32 s_nl, s_nf;
-  const u32 round = (round_ptr ? *round_ptr : 0u) + round_add;
+  const Clk ck = clk_of(ra);
+  const u32 round = ck.round;
   const u32 par = round & 1u;
   if (blockIdx.x == 0 && threadIdx.x == 0) L.counts[2 * 2 + (par ^ 1u)] = 0;
   if (threadIdx.x == 0) s_nl = s_nf = 0;
@@ -301,7 +316,7 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_round(Planes P, Para
   for (u32 j = threadIdx.x; j < kTriChunk; j += kBlock) {
     const u64 r = lo + j;
     u32 cls = T_DONE;
-    if (r < C.n_rep && owned<N>(C, r)) cls = triage_replica<N, TRACE>(P, C, r, round, c);
+    if (r < C.n_rep && owned<N>(C, r)) cls = triage_replica<N, TRACE>(P, C, r, ck, c);
 #pragma unroll
     for (u32 li = 0; li < 2; li++) {
       const bool want = cls == li + 1;
@@ -324,10 +339,10 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_round(Planes P, Para
     u32 r = 0;
     if (i < nl) {
       r = s_idx[i];
-      slow = !step_fast<N, TRACE, MODE_LEAD>(P, C, r, round, c);
+      slow = !step_fast<N, TRACE, MODE_LEAD>(P, C, r, ck, c);
     } else if (i < nt) {
       r = s_idx[kTriChunk - 1u - (i - nl)];
-      slow = !step_fast<N, TRACE, MODE_FOLL>(P, C, r, round, c);
+      slow = !step_fast<N, TRACE, MODE_FOLL>(P, C, r, ck, c);
     }
     list_push(L, 2, par, slow, r);
   }
@@ -337,9 +352,9 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_round(Planes P, Para
 // Pass 2: the steady-state subset for one role over its list (persistent,
 // grid-stride); rounds outside the subset are moved to the full list.
 template <int N, bool TRACE, int MODE>
-__global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_list(Planes P, Params C, const u32* round_ptr,
-                                                      u32 round_add, Lists L) {
-  const u32 round = (round_ptr ? *round_ptr : 0u) + round_add;
+__global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_list(Planes P, Params C, RoundArg ra, Lists L) {
+  const Clk ck = clk_of(ra);
+  const u32 round = ck.round;
   const u32 par = round & 1u;
   const u32 li = MODE == MODE_LEAD ? 0u : 1u;
   const u32 nfront = list_front(L, li, par), n = nfront + list_back(L, li, par);
@@ -353,7 +368,7 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_list(Planes P, 
     u32 r = 0;
     if (i < n) {
       r = list_at(L, li, nfront, i);
-      slow = !step_fast<N, TRACE, MODE>(P, C, r, round, c);
+      slow = !step_fast<N, TRACE, MODE>(P, C, r, ck, c);
     }
     list_push(L, 2, par, slow, r);
   }
@@ -464,10 +479,10 @@ __device__ __forceinline__ void stage_out_wave(const Planes& P, const StageRow<N
 // (stage_in_wave / stage_out_wave); the step works on its LDS row.
 template <int N, bool TRACE>
 __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, Params C,
-                                                                     const u32* round_ptr,
-                                                                     u32 round_add, Lists L) {
+                                                                     RoundArg ra, Lists L) {
   __shared__ StageRow<N> s_rows[kBlock];
-  const u32 round = (round_ptr ? *round_ptr : 0u) + round_add;
+  const Clk ck = clk_of(ra);
+  const u32 round = ck.round;
   const u32 par = round & 1u;
   const u32 nlf = list_front(L, 0, par), nl = nlf + list_back(L, 0, par);
   const u32 nff = list_front(L, 1, par), n = nl + nff + list_back(L, 1, par);
@@ -499,9 +514,9 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, 
         wave_lds_sync();
       }
       if (lead)
-        ok = step_fast<N, TRACE, MODE_LEAD, SL, kListAux<N>>(P, C, r, round, c, mine, aux);
+        ok = step_fast<N, TRACE, MODE_LEAD, SL, kListAux<N>>(P, C, r, ck, c, mine, aux);
       else if (any)
-        ok = step_fast<N, TRACE, MODE_FOLL, SF, kListAux<N>>(P, C, r, round, c, mine, aux);
+        ok = step_fast<N, TRACE, MODE_FOLL, SF, kListAux<N>>(P, C, r, ck, c, mine, aux);
       if constexpr ((SL | SF) != 0) {
         wave_lds_sync();
         const u64 m_ok = __ballot(ok) & m_out;
@@ -516,15 +531,15 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, 
 
 // Pass 3: the whole handler table over the full list (persistent, grid-stride).
 template <int N, bool TRACE>
-__global__ __launch_bounds__(kBlock) void k_full_list(Planes P, Params C, const u32* round_ptr,
-                                                      u32 round_add, Lists L) {
-  const u32 round = (round_ptr ? *round_ptr : 0u) + round_add;
+__global__ __launch_bounds__(kBlock) void k_full_list(Planes P, Params C, RoundArg ra, Lists L) {
+  const Clk ck = clk_of(ra);
+  const u32 round = ck.round;
   const u32 n = L.counts[2 * 2 + (round & 1u)];
   StepCounters c;
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
   for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock)
-    step_replica<N, TRACE>(P, C, L.idx[2 * L.cap + i], round, c);
+    step_replica<N, TRACE>(P, C, L.idx[2 * L.cap + i], ck, c);
   flush_counters<KS_FULL>(P, c);
 }
 
@@ -540,7 +555,22 @@ __global__ __launch_bounds__(kBlock) void k_isolate(Planes P, Params C, u32 roun
   if (g < C.n_groups) iso_group<N>(P, C, g, round);
 }
 
-__global__ void k_advance(u32* round_ptr, u32 k) { *round_ptr += k; }
+// Host input staged by rbe_push_* / rbe_notify_applied (rbe_host.h), one
+// launch per step that has any: records to their replicas' ExtIn slots,
+// applied indexes to the applied plane.
+__global__ __launch_bounds__(kBlock) void k_ext_scatter(Planes P, const u64* reps,
+                                                        const ExtIn* recs, u64 n,
+                                                        const u64* app_rep, const u64* app_val,
+                                                        u64 na) {
+  const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) P.ext[reps[i]] = recs[i];
+  if (i < na) P.applied[app_rep[i]] = app_val[i];
+}
+
+__global__ void k_advance(u32* clk, u32 k) {
+  clk[0] += k;
+  clk[1] += k;
+}
 
 // ---- replica-per-GPU exchange (rbe_xchg.h)
 struct XchgCaps {
@@ -604,7 +634,8 @@ struct rbe_engine {
   int device = 0;
   hipStream_t stream = nullptr;
   u32 round = 0;
-  u32* d_round = nullptr;
+  u32 tclk = 0;              // ticks before the next round (Clk::tclk)
+  u32* d_clk = nullptr;      // device copy {round, tclk} read by graph replays
   std::vector<void*> allocs;
   hipGraphExec_t graph = nullptr;
   u32 graph_rounds = 0;
@@ -613,14 +644,21 @@ struct rbe_engine {
                              // 3 both (default: triage + one merged fast launch)
   Lists L;                   // per-round work lists (triage → fast → full)
   u32* xcount = nullptr;     // replica-per-GPU pack counters [rep_world * XS_NUM]
+  HostInputs hin;            // rbe_push_* staged for the next step (rbe_host.h)
+  u64 in_used = 0;
+  u8* in_pinned = nullptr;   // pinned upload buffer of the staged input
+  u8* in_dev = nullptr;      // its device copy (replicas, records, applied pairs)
+  u64 in_bytes = 0;          // capacity of both
+  hipEvent_t in_ev = nullptr;  // the last upload out of in_pinned has finished
 };
 
 static constexpr unsigned kFastGrid = 2048;  // persistent grid of k_fast_list
 static constexpr unsigned kFullGrid = 512;  // persistent grid of k_full_list: 2 waves per SIMD, its kernels' occupancy cap
 
+static constexpr int kPlaneAllocs = 19;
 static u64 bytes_of(const Params& C, u64* parts) {
   const u64 N = C.n, G = C.n_groups, R = C.n_rep;
-  u64 p[17] = {
+  u64 p[kPlaneAllocs] = {
       R * sizeof(Hot),
       R * sizeof(Core),
       R * N * sizeof(RemoteMN),
@@ -638,9 +676,11 @@ static u64 bytes_of(const Params& C, u64* parts) {
       R * C.dri_cap * sizeof(DropRI),
       R * sizeof(ExtIn),
       R * sizeof(u8),
+      (u64)C.in_cap * sizeof(Ent),
+      R * sizeof(u64),
   };
   u64 t = 0;
-  for (int i = 0; i < 17; i++) {
+  for (int i = 0; i < kPlaneAllocs; i++) {
     if (parts) parts[i] = p[i];
     t += (p[i] + 255) & ~255ull;
   }
@@ -694,6 +734,14 @@ static int make_params(const rbe_config* cfg, Params* out) {
   // replica-per-GPU mode: the fault schedule needs every replica's role and
   // host-pushed inputs are per replica; both stay group-per-GPU features
   if (C.rep_world > 1 && (C.iso_period || C.ext_inputs)) return RBE_E_INVALID;
+  C.ext_apply = cfg->ext_apply;
+  if (C.ext_apply && !C.ext_inputs) return RBE_E_INVALID;  // applied comes from rbe_notify_applied
+  C.in_cap = cfg->in_cap ? cfg->in_cap : (u32)(cfg->n_groups > 1024 ? cfg->n_groups : 1024);
+  if (cfg->n_groups > 0xFFFFFFFFull && !cfg->in_cap) C.in_cap = 0xFFFFFFFFu;
+  C.xfer_period = cfg->xfer_period;
+  C.xfer_mod = cfg->xfer_mod;
+  // not yet on the device: snapshots/compaction and the payload heap
+  if (cfg->snapshot_entries || cfg->compaction_overhead || cfg->heap_bytes) return RBE_E_INVALID;
   *out = C;
   return RBE_OK;
 }
@@ -720,7 +768,7 @@ static unsigned grid_for(u64 n) { return (unsigned)((n + kBlock - 1) / kBlock); 
 // on the engine stream before the first and after every pipeline kernel, so
 // ev[i]..ev[i+1] brackets kernel section i (rbe_profile_rounds).
 template <int N, bool TRACE>
-static int launch_step_t(rbe_engine* e, const u32* round_ptr, u32 round_add,
+static int launch_step_t(rbe_engine* e, RoundArg ra,
                          hipEvent_t* ev = nullptr) {
   const unsigned g = grid_for(e->C.n_rep);
   auto mark = [&](int i) {
@@ -734,57 +782,56 @@ static int launch_step_t(rbe_engine* e, const u32* round_ptr, u32 round_add,
     mark(2);
     mark(3);
     hipLaunchKernelGGL((k_step<N, TRACE>), dim3(g), dim3(kBlock), 0, e->stream, e->P, e->C,
-                       round_ptr, round_add);
+                       ra);
     mark(4);
   } else if (e->mode == 0) {
     mark(0);
     hipLaunchKernelGGL((k_round<N, TRACE>), dim3(gt), dim3(kBlock), 0, e->stream, e->P, e->C,
-                       round_ptr, round_add, e->L);
+                       ra, e->L);
     mark(1);
     mark(2);
     mark(3);
     hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kBlock), 0, e->stream, e->P, e->C,
-                       round_ptr, round_add, e->L);
+                       ra, e->L);
     mark(4);
   } else if (e->mode == 3) {
     mark(0);
     hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(gt), dim3(kBlock), 0, e->stream, e->P, e->C,
-                       round_ptr, round_add, e->L);
+                       ra, e->L);
     mark(1);
     const unsigned gf = g < kFastGrid ? g : kFastGrid;
     hipLaunchKernelGGL((k_fast_both<N, TRACE>), dim3(gf), dim3(kBlock), 0, e->stream, e->P, e->C,
-                       round_ptr, round_add, e->L);
+                       ra, e->L);
     mark(2);
     mark(3);
     hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kBlock), 0, e->stream, e->P, e->C,
-                       round_ptr, round_add, e->L);
+                       ra, e->L);
     mark(4);
   } else {
     mark(0);
     hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(gt), dim3(kBlock), 0, e->stream, e->P, e->C,
-                       round_ptr, round_add, e->L);
+                       ra, e->L);
     mark(1);
     const unsigned gf = g < kFastGrid ? g : kFastGrid;
     hipLaunchKernelGGL((k_fast_list<N, TRACE, MODE_LEAD>), dim3(gf), dim3(kBlock), 0, e->stream,
-                       e->P, e->C, round_ptr, round_add, e->L);
+                       e->P, e->C, ra, e->L);
     mark(2);
     hipLaunchKernelGGL((k_fast_list<N, TRACE, MODE_FOLL>), dim3(gf), dim3(kBlock), 0, e->stream,
-                       e->P, e->C, round_ptr, round_add, e->L);
+                       e->P, e->C, ra, e->L);
     mark(3);
     hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kBlock), 0, e->stream, e->P, e->C,
-                       round_ptr, round_add, e->L);
+                       ra, e->L);
     mark(4);
   }
   HIP_OK(hipGetLastError());
   return RBE_OK;
 }
 
-static int launch_step(rbe_engine* e, const u32* round_ptr, u32 round_add,
+static int launch_step(rbe_engine* e, RoundArg ra,
                        hipEvent_t* ev = nullptr) {
   return dispatch_n(e->C.n, [&](auto NN) {
     constexpr int N = decltype(NN)::value;
-    return e->C.trace ? launch_step_t<N, true>(e, round_ptr, round_add, ev)
-                      : launch_step_t<N, false>(e, round_ptr, round_add, ev);
+    return e->C.trace ? launch_step_t<N, true>(e, ra, ev) : launch_step_t<N, false>(e, ra, ev);
   });
 }
 
@@ -807,6 +854,15 @@ extern "C" {
 
 int rbe_abi_version(void) { return RBE_ABI_VERSION; }
 
+int rbe_abi_sizes(uint64_t* out, uint32_t cap) {
+  const uint64_t sz[6] = {sizeof(rbe_config), sizeof(rbe_replica_view), sizeof(rbe_update),
+                          sizeof(rbe_message), sizeof(rbe_entry), sizeof(rbe_ready_to_read)};
+  if (!out) return RBE_E_INVALID;
+  uint32_t n = cap < 6 ? cap : 6;
+  for (uint32_t i = 0; i < n; i++) out[i] = sz[i];
+  return (int)n;
+}
+
 // Group-range snapshots (rbe_snap.h): one 2-D copy per plane on the engine
 // stream, ordered after every round already queued.
 int rbe_snapshot_bytes(rbe_engine* e, uint64_t count, uint64_t* bytes) {
@@ -822,7 +878,7 @@ int rbe_export_groups(rbe_engine* e, uint64_t first, uint64_t count, void* buf, 
   if (cap < sizeof(SnapHeader) + body) return RBE_E_NOMEM;
   HIP_OK(hipSetDevice(e->device));
   SnapHeader h;
-  snap_fill_header(e->C, RBE_ABI_VERSION, e->round, first, count, body, &h);
+  snap_fill_header(e->C, RBE_ABI_VERSION, e->round, e->tclk, first, count, body, &h);
   memcpy(buf, &h, sizeof(h));
   SnapPlane pl[kSnapPlanes];
   snap_planes(e->P, e->C, pl);
@@ -858,12 +914,21 @@ int rbe_import_groups(rbe_engine* e, const void* buf, uint64_t bytes, uint32_t f
                             pl[i].rows, hipMemcpyHostToDevice, e->stream));
     src += w * pl[i].rows;
   }
+  {  // the host mirror of the applied plane follows the imported rows
+    std::vector<u64> app(h.count * e->C.n);
+    HIP_OK(hipMemcpyAsync(app.data(), e->P.applied + h.first * e->C.n, app.size() * sizeof(u64),
+                          hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    e->hin.resync_applied(app.data(), h.first * e->C.n, app.size());
+  }
   if (resume) {
     // the whole engine moves to the snapshot's round; the work lists of the
     // coming round start empty, as after any round (k_triage clears them)
     e->round = h.round;
     HIP_OK(hipMemsetAsync(e->L.counts, 0, kListCounts * sizeof(u32), e->stream));
-    HIP_OK(hipMemcpyAsync(e->d_round, &e->round, sizeof(u32), hipMemcpyHostToDevice, e->stream));
+    e->tclk = h.tclk;
+    const u32 clk[2] = {e->round, e->tclk};
+    HIP_OK(hipMemcpyAsync(e->d_clk, clk, sizeof(clk), hipMemcpyHostToDevice, e->stream));
   }
   HIP_OK(hipStreamSynchronize(e->stream));
   return RBE_OK;
@@ -883,9 +948,12 @@ int rbe_destroy(rbe_engine* e) {
   if (e->stream) HIP_IGNORE(hipStreamSynchronize(e->stream));
   if (e->graph) HIP_IGNORE(hipGraphExecDestroy(e->graph));
   for (void* p : e->allocs) HIP_IGNORE(hipFree(p));
-  if (e->d_round) HIP_IGNORE(hipFree(e->d_round));
+  if (e->d_clk) HIP_IGNORE(hipFree(e->d_clk));
   if (e->ev0) HIP_IGNORE(hipEventDestroy(e->ev0));
   if (e->ev1) HIP_IGNORE(hipEventDestroy(e->ev1));
+  if (e->in_ev) HIP_IGNORE(hipEventDestroy(e->in_ev));
+  if (e->in_pinned) HIP_IGNORE(hipHostFree(e->in_pinned));
+  if (e->in_dev) HIP_IGNORE(hipFree(e->in_dev));
   if (e->stream) HIP_IGNORE(hipStreamDestroy(e->stream));
   delete e;
   return RBE_OK;
@@ -912,10 +980,11 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   }
   HIP_IGNORE(hipEventCreate(&e->ev0));
   HIP_IGNORE(hipEventCreate(&e->ev1));
-  u64 parts[17];
+  HIP_IGNORE(hipEventCreateWithFlags(&e->in_ev, hipEventDisableTiming));
+  u64 parts[kPlaneAllocs];
   bytes_of(C, parts);
-  void* ptrs[17];
-  for (int i = 0; i < 17; i++) {
+  void* ptrs[kPlaneAllocs];
+  for (int i = 0; i < kPlaneAllocs; i++) {
     u64 b = parts[i] ? parts[i] : 16;
     if (hipMalloc(&ptrs[i], b) != hipSuccess) {
       for (int j = 0; j < i; j++) e->allocs.push_back(ptrs[j]);
@@ -952,17 +1021,20 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   P.dri = (DropRI*)ptrs[14];
   P.ext = (ExtIn*)ptrs[15];
   P.idle = (u8*)ptrs[16];
+  P.in_ents = (Ent*)ptrs[17];
+  P.applied = (u64*)ptrs[18];
+  e->hin.init(C.n_rep, C.n, C.in_cap);
   if (hipMalloc(&P.counters, kCtrWords * sizeof(u64)) != hipSuccess) {
     rbe_destroy(e);
     return RBE_E_NOMEM;
   }
   e->allocs.push_back(P.counters);
   HIP_IGNORE(hipMemsetAsync(P.counters, 0, kCtrWords * sizeof(u64), e->stream));
-  if (hipMalloc(&e->d_round, sizeof(u32)) != hipSuccess) {
+  if (hipMalloc(&e->d_clk, 2 * sizeof(u32)) != hipSuccess) {
     rbe_destroy(e);
     return RBE_E_NOMEM;
   }
-  HIP_IGNORE(hipMemsetAsync(e->d_round, 0, sizeof(u32), e->stream));
+  HIP_IGNORE(hipMemsetAsync(e->d_clk, 0, 2 * sizeof(u32), e->stream));
   const char* mode = getenv("RBE_MODE");
   // default: k_triage → k_fast_both → k_full_list; RBE_MODE=split runs the two
   // roles as separate launches, RBE_MODE=fused k_round + k_full_list,
@@ -1020,12 +1092,64 @@ static int launch_iso(rbe_engine* e) {
   });
 }
 
-static int step_one(rbe_engine* e) {
-  int rc = launch_iso(e);
+// Upload the input staged since the last step (rbe_host.h) through the pinned
+// buffer in one copy and scatter it on device, ahead of the round's kernels.
+static int flush_inputs(rbe_engine* e) {
+  HostInputs& h = e->hin;
+  if (h.empty()) return RBE_OK;
+  const u64 n = h.reps.size(), na = h.app_rep.size();
+  const u64 need = n * (sizeof(u64) + sizeof(ExtIn)) + na * 2 * sizeof(u64) + 64;
+  HIP_OK(hipEventSynchronize(e->in_ev));  // the previous upload is out of in_pinned
+  if (need > e->in_bytes) {
+    if (e->in_pinned) HIP_OK(hipHostFree(e->in_pinned));
+    if (e->in_dev) HIP_OK(hipFree(e->in_dev));
+    e->in_pinned = nullptr;
+    e->in_dev = nullptr;
+    e->in_bytes = 0;
+    const u64 cap = need * 2;
+    HIP_OK(hipHostMalloc((void**)&e->in_pinned, cap, hipHostMallocDefault));
+    HIP_OK(hipMalloc((void**)&e->in_dev, cap));
+    e->in_bytes = cap;
+  }
+  // layout: replicas | records (16-B aligned) | applied replicas | applied values
+  u8* b = e->in_pinned;
+  const u64 o_rec = (n * sizeof(u64) + 15) & ~15ull;
+  const u64 o_ar = o_rec + n * sizeof(ExtIn), o_av = o_ar + na * sizeof(u64);
+  const u64 total = o_av + na * sizeof(u64);
+  if (n) {
+    memcpy(b, h.reps.data(), n * sizeof(u64));
+    memcpy(b + o_rec, h.recs.data(), n * sizeof(ExtIn));
+  }
+  if (na) {
+    memcpy(b + o_ar, h.app_rep.data(), na * sizeof(u64));
+    memcpy(b + o_av, h.app_val.data(), na * sizeof(u64));
+  }
+  HIP_OK(hipMemcpyAsync(e->in_dev, b, total, hipMemcpyHostToDevice, e->stream));
+  if (!h.ents.empty())
+    HIP_OK(hipMemcpyAsync(e->P.in_ents, h.ents.data(), h.ents.size() * sizeof(Ent),
+                          hipMemcpyHostToDevice, e->stream));
+  const u64 m = n > na ? n : na;
+  hipLaunchKernelGGL(k_ext_scatter, dim3(grid_for(m)), dim3(kBlock), 0, e->stream, e->P,
+                     (const u64*)e->in_dev, (const ExtIn*)(e->in_dev + o_rec), n,
+                     (const u64*)(e->in_dev + o_ar), (const u64*)(e->in_dev + o_av), na);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(e->in_ev, e->stream));
+  // the entries came from pageable memory: wait for that copy before the
+  // vectors are reused (inputs are the host-driven path, not the bench path)
+  if (!h.ents.empty()) HIP_OK(hipEventSynchronize(e->in_ev));
+  h.clear();
+  return RBE_OK;
+}
+
+static int step_one(rbe_engine* e, bool tick = true) {
+  int rc = flush_inputs(e);
   if (rc) return rc;
-  rc = launch_step(e, nullptr, e->round);
+  rc = launch_iso(e);
+  if (rc) return rc;
+  rc = launch_step(e, RoundArg{nullptr, e->round, e->tclk, tick ? 1u : 0u});
   if (rc) return rc;
   e->round++;
+  if (tick) e->tclk++;
   return RBE_OK;
 }
 
@@ -1035,6 +1159,12 @@ int rbe_step(rbe_engine* e) {
   return step_one(e);
 }
 
+int rbe_step_ex(rbe_engine* e, uint32_t flags) {
+  if (!e || (flags & ~RBE_STEP_NO_TICK)) return RBE_E_INVALID;
+  HIP_OK(hipSetDevice(e->device));
+  return step_one(e, (flags & RBE_STEP_NO_TICK) == 0);
+}
+
 // K rounds as one graph: K step launches reading the round from device memory,
 // then one advance of that counter.
 static int run_graph(rbe_engine* e, u32 rounds) {
@@ -1042,28 +1172,30 @@ static int run_graph(rbe_engine* e, u32 rounds) {
     HIP_IGNORE(hipGraphExecDestroy(e->graph));
     e->graph = nullptr;
   }
+  const u32 clk[2] = {e->round, e->tclk};
   if (!e->graph) {
-    HIP_OK(hipMemcpyAsync(e->d_round, &e->round, sizeof(u32), hipMemcpyHostToDevice, e->stream));
+    HIP_OK(hipMemcpyAsync(e->d_clk, clk, sizeof(clk), hipMemcpyHostToDevice, e->stream));
     HIP_OK(hipStreamSynchronize(e->stream));
     hipGraph_t g;
     HIP_OK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
     for (u32 i = 0; i < rounds; i++) {
-      int rc = launch_step(e, e->d_round, i);
+      int rc = launch_step(e, RoundArg{e->d_clk, i, i, 1u});
       if (rc) {
         HIP_IGNORE(hipStreamEndCapture(e->stream, &g));
         return rc;
       }
     }
-    hipLaunchKernelGGL(k_advance, dim3(1), dim3(1), 0, e->stream, e->d_round, rounds);
+    hipLaunchKernelGGL(k_advance, dim3(1), dim3(1), 0, e->stream, e->d_clk, rounds);
     HIP_OK(hipStreamEndCapture(e->stream, &g));
     HIP_OK(hipGraphInstantiate(&e->graph, g, nullptr, nullptr, 0));
     HIP_IGNORE(hipGraphDestroy(g));
     e->graph_rounds = rounds;
   } else {
-    HIP_OK(hipMemcpyAsync(e->d_round, &e->round, sizeof(u32), hipMemcpyHostToDevice, e->stream));
+    HIP_OK(hipMemcpyAsync(e->d_clk, clk, sizeof(clk), hipMemcpyHostToDevice, e->stream));
   }
   HIP_OK(hipGraphLaunch(e->graph, e->stream));
   e->round += rounds;
+  e->tclk += rounds;
   return RBE_OK;
 }
 
@@ -1102,9 +1234,10 @@ int rbe_profile_rounds(rbe_engine* e, uint32_t rounds, float* ms_per_kernel) {
   for (u32 k = 0; k < rounds && rc == RBE_OK; k++) {
     rc = launch_iso(e);
     if (rc) break;
-    rc = launch_step(e, nullptr, e->round, ev);
+    rc = launch_step(e, RoundArg{nullptr, e->round, e->tclk, 1u}, ev);
     if (rc) break;
     e->round++;
+    e->tclk++;
     if (hipEventSynchronize(ev[KS_NUM]) != hipSuccess) {
       rc = RBE_E_HIP;
       break;
@@ -1131,39 +1264,47 @@ int rbe_round(const rbe_engine* e, uint32_t* round) {
   return RBE_OK;
 }
 
-int rbe_push_proposals(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint8_t* cmd16,
-                       const uint32_t* cmd_len) {
-  if (!e || !e->C.ext_inputs) return RBE_E_STATE;
-  HIP_OK(hipSetDevice(e->device));
-  for (u64 i = 0; i < n; i++) {
-    if (replica[i] >= e->C.n_rep || cmd_len[i] > 16) return RBE_E_INVALID;
-    ExtIn x;
-    memset(&x, 0, sizeof(x));
-    x.kind = 1;
-    x.len = cmd_len[i];
-    memcpy(&x.lo, cmd16 + 16 * i, 8);
-    memcpy(&x.hi, cmd16 + 16 * i + 8, 8);
-    HIP_OK(hipMemcpyAsync(&e->P.ext[replica[i]], &x, sizeof(x), hipMemcpyHostToDevice, e->stream));
-  }
-  HIP_OK(hipStreamSynchronize(e->stream));
-  return RBE_OK;
+// Node-layer input for the next step (rbe.h; staged host-side, rbe_host.h)
+int rbe_push_proposals(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint32_t* n_ents,
+                       const uint32_t* type, const uint32_t* cmd_len, const uint8_t* cmd) {
+  if (!e) return RBE_E_INVALID;
+  if (!e->C.ext_inputs) return RBE_E_STATE;
+  return e->hin.push_proposals(n, replica, n_ents, type, cmd_len, cmd);
 }
 
 int rbe_push_read_index(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint64_t* lo,
                         const uint64_t* hi) {
-  if (!e || !e->C.ext_inputs) return RBE_E_STATE;
-  HIP_OK(hipSetDevice(e->device));
-  for (u64 i = 0; i < n; i++) {
-    if (replica[i] >= e->C.n_rep || lo[i] == 0) return RBE_E_INVALID;  // requests.go:726
-    ExtIn x;
-    memset(&x, 0, sizeof(x));
-    x.kind = 2;
-    x.ctx_low = lo[i];
-    x.ctx_high = hi[i];
-    HIP_OK(hipMemcpyAsync(&e->P.ext[replica[i]], &x, sizeof(x), hipMemcpyHostToDevice, e->stream));
-  }
-  HIP_OK(hipStreamSynchronize(e->stream));
-  return RBE_OK;
+  if (!e) return RBE_E_INVALID;
+  if (!e->C.ext_inputs) return RBE_E_STATE;
+  return e->hin.push_read_index(n, replica, lo, hi);
+}
+
+int rbe_request_leader_transfer(rbe_engine* e, uint64_t n, const uint64_t* replica,
+                                const uint64_t* target) {
+  if (!e) return RBE_E_INVALID;
+  if (!e->C.ext_inputs) return RBE_E_STATE;
+  return e->hin.request_leader_transfer(n, replica, target);
+}
+
+int rbe_report_unreachable(rbe_engine* e, uint64_t n, const uint64_t* replica,
+                           const uint64_t* node_id) {
+  if (!e) return RBE_E_INVALID;
+  if (!e->C.ext_inputs) return RBE_E_STATE;
+  return e->hin.report_unreachable(n, replica, node_id);
+}
+
+int rbe_report_snapshot_status(rbe_engine* e, uint64_t n, const uint64_t* replica,
+                               const uint64_t* node_id, const uint8_t* reject) {
+  if (!e) return RBE_E_INVALID;
+  if (!e->C.ext_inputs) return RBE_E_STATE;
+  return e->hin.report_snapshot_status(n, replica, node_id, reject);
+}
+
+int rbe_notify_applied(rbe_engine* e, uint64_t n, const uint64_t* replica,
+                       const uint64_t* applied) {
+  if (!e) return RBE_E_INVALID;
+  if (!e->C.ext_apply) return RBE_E_STATE;
+  return e->hin.notify_applied(n, replica, applied);
 }
 
 #ifdef RBE_PHASE_TIMING
@@ -1345,7 +1486,7 @@ int rbe_get_views(rbe_engine* e, uint64_t first, uint64_t count, rbe_replica_vie
   for (u64 i = 0; i < count; i++) {
     rbe_replica_view& v = out[i];
     memset(&v, 0, sizeof(v));
-    const Hot h = materialize_hot(hot[i], e->C, e->round);
+    const Hot h = materialize_hot(hot[i], e->C, e->tclk);
     const Core& c = core[i];
     v.term = c.term;
     v.vote = c.vote;
@@ -1367,6 +1508,7 @@ int rbe_get_views(rbe_engine* e, uint64_t first, uint64_t count, rbe_replica_vie
     v.rq_count = c.rq_count;
     v.votes_resp = h.votes_resp;
     v.votes_granted = h.votes_granted;
+    v.events = (e->round > 0 && upd[i].round == e->round - 1) ? upd[i].events : 0u;
     if (h.role == R_Leader) {
       for (u32 s = 0; s < N && s < 8; s++) {
         v.match[s] = rem[i * N + s].match;
@@ -1407,10 +1549,21 @@ int rbe_get_updates(rbe_engine* e, uint64_t first, uint64_t count, rbe_update* o
       u.n_dropped_entries = upd[i].n_drop_ent;
       u.n_dropped_read_indexes = upd[i].n_drop_ri;
       u.flags = upd[i].flags;
+      u.events = upd[i].events;
     } else {  // an idle round (triage) left the record untouched: empty Update
       u.save_lo = u.apply_lo = 1;
       u.save_hi = u.apply_hi = 0;
     }
+    // Peer.HasUpdate (peer.go:253-280) and setFastApply / validateUpdate
+    // (peer.go:209-245) on the range form
+    const bool has = (u.flags & RBE_UF_STATE_CHANGED) || u.n_messages || u.n_ready_to_read ||
+                     u.n_dropped_entries || u.n_dropped_read_indexes || u.save_lo <= u.save_hi ||
+                     u.apply_lo <= u.apply_hi || (u.flags & RBE_UF_SENT_QUIESCE);
+    if (has) u.flags |= RBE_UF_HAS_UPDATE;
+    if (update_fast_apply(false, u.save_lo, u.save_hi, u.apply_lo, u.apply_hi))
+      u.flags |= RBE_UF_FAST_APPLY;
+    if (!update_valid(u.commit, u.save_lo, u.save_hi, u.apply_lo, u.apply_hi))
+      u.fault |= RBE_FAULT_PANIC;
     u.role = hot[i].role;
     u.leader_id = core[i].leader;
   }

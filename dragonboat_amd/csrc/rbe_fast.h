@@ -175,6 +175,7 @@ struct FastOut {
   // bump, which puts the counter array in scratch memory — and a scratch
   // reload after the lane's first store waits for every store before it
   u32 fault0, n_out, n_drop_msg, n_ent_out;
+  u32 events;  // EV_* of the step (Upd::events)
 
   RBE_HD u32 get_pc(u32 d) const {
     return d < 4 ? (u32)((pc >> (16 * d)) & 0xFFFFu) : (u32)((pc_hi >> (16 * (d - 4))) & 0xFFFFu);
@@ -252,6 +253,7 @@ struct FastOut {
     x.high = high;
     P.dri[r * C.dri_cap + n_drop_ri] = x;
     n_drop_ri++;
+    events |= EV_READ_INDEX_DROPPED;
     if (TRACE) {
       drop_hash = hfold(drop_hash, low);
       drop_hash = hfold(drop_hash, high);
@@ -403,6 +405,8 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
   c.saved_to = c.last_index;
   if (c.processed < c.committed) flags |= HF_APPLY_PENDING;
   else flags &= (u8)~HF_APPLY_PENDING;
+  if (u.apply_hi >= u.apply_lo && !C.ext_apply) flags |= HF_APPLIED_NEW;
+  else flags &= (u8)~HF_APPLIED_NEW;
   if (role == R_Leader) {
     ctr.v[C_COMMITTED] += (u32)(c.committed - committed0);
     ctr.v[C_LEADER_STEPS]++;
@@ -435,7 +439,7 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
   ctr.v[C_FAULTS] += popc8(o.fault & ~o.fault0 & 0xFFu);
   u.flags = (u16)((c.committed != committed0 ? UF_STATE_CHANGED : 0u) |
                   (send_q ? UF_SENT_QUIESCE : 0u));
-  u.pad = 0;
+  u.events = (u16)o.events;
   u.round = o.round_;
   u.pad2 = 0;
 #ifndef RBE_DIAG_NO_STATE_STORES
@@ -485,8 +489,9 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
 //   local ReadIndex → tick → proposal, each followed by the deferred fan-out
 //   (Replicate sends in ascending slot order, heartbeats, readIndex confirm).
 template <int N, bool TRACE, int STG = 0, bool AUX = false>
-RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCounters& ctr,
+RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, StepCounters& ctr,
                       StageRow<N>* sr = nullptr, u32 aux = 0) {
+  const u32 round = ck.round;
   using Cap = FastCaps<N>;
   constexpr u32 Q = N / 2 + 1;
   if constexpr (N < 3) {
@@ -502,10 +507,10 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   Hot h;
   Core c;
   if constexpr ((STG & STG_IN) != 0) {
-    h = materialize_hot(sr->hot, C, round);
+    h = materialize_hot(sr->hot, C, ck.tclk);
     c = sr->core;
   } else {
-    h = load_hot(P, C, r, round);
+    h = load_hot(P, C, r, ck.tclk);
     c = P.core[r];
   }
   u64 match[N], next[N];
@@ -566,7 +571,9 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   if (h.role != R_Leader) return false;
   if (h.flags & (HF_APPLY_PENDING | HF_IS_LTT)) return false;
   if (c.ltt != 0) return false;
-  if (C.ext_inputs && P.ext[r].kind) return false;
+  if (!ck.tick) return false;
+  if (C.xfer_period && xfer_input(C, cid, round, k)) return false;
+  if (C.ext_inputs && P.ext[r].flags) return false;
   if (c.rq_count >= Cap::RQ) return false;
   u32 n_in = 0;
 #pragma unroll
@@ -665,6 +672,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   o.n_out = o.n_drop_msg = o.n_ent_out = 0;
   o.fault0 = o.fault;
   o.msg_hash = o.rtr_hash = o.drop_hash = 0;
+  o.events = 0;
   o.term = c.term;
   u8 flags = h.flags;
   u32 etick = h.election_tick, htick = h.heartbeat_tick;
@@ -1139,8 +1147,9 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
 // (Replicate / Heartbeat / ReadIndexResp of the current term), no client
 // input, a tick that does not start an election.
 template <int N, bool TRACE, int STG = 0, bool AUX = false>
-RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCounters& ctr,
+RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, StepCounters& ctr,
                       StageRow<N>* sr = nullptr, u32 aux = 0) {
+  const u32 round = ck.round;
   using Cap = FastCaps<N>;
   if constexpr (N < 3) {
     return false;
@@ -1154,10 +1163,10 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   Hot h;
   Core c;
   if constexpr ((STG & STG_IN) != 0) {
-    h = materialize_hot(sr->hot, C, round);
+    h = materialize_hot(sr->hot, C, ck.tclk);
     c = sr->core;
   } else {
-    h = load_hot(P, C, r, round);
+    h = load_hot(P, C, r, ck.tclk);
     c = P.core[r];
   }
   u32 pcin[N];
@@ -1202,7 +1211,9 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   if (h.role != R_Follower) return false;
   if (h.flags & (HF_APPLY_PENDING | HF_IS_LTT)) return false;
   if (c.ltt != 0) return false;
-  if (C.ext_inputs && P.ext[r].kind) return false;
+  if (!ck.tick) return false;
+  if (C.xfer_period && xfer_input(C, C.cid_base + g * C.cid_stride, round, k)) return false;
+  if (C.ext_inputs && P.ext[r].flags) return false;
   const u32 ls = (u32)c.leader - 1u;  // leader slot (0xFFFFFFFF when no leader)
   u32 n_in = 0;
 #pragma unroll
@@ -1321,6 +1332,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
   o.n_out = o.n_drop_msg = o.n_ent_out = 0;
   o.fault0 = o.fault;
   o.msg_hash = o.rtr_hash = o.drop_hash = 0;
+  o.events = 0;
   o.term = c.term;
   u8 flags = h.flags;
   u32 etick = h.election_tick;
@@ -1425,6 +1437,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
           resp.reject = 1;
           resp.log_index = m.log_index;
           resp.hint = c.last_index;
+          o.events |= EV_REPLICATION_REJECTED;
         }
         o.send(P, C, ctr, resp, nullptr);
       } else if (m.type == M_Heartbeat) {  // handleHeartbeatMessage, raft.go:1301-1309
@@ -1452,7 +1465,10 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
     etick++;  // nonLeaderTick; reaching the timeout is excluded above
     if (etick >= h.rand_et) o.set_fault(ctr, F_UNSUPPORTED);
   }
-  if (n_in && (u8)lid != c.leader) cdirty |= 4u;
+  if (n_in && (u8)lid != c.leader) {
+    cdirty |= 4u;
+    o.events |= EV_LEADER_UPDATED;
+  }
   c.leader = n_in ? (u8)lid : c.leader;
   fast_finish<N, TRACE, STG>(P, C, ctr, o, q, R_Follower, flags, h, c, etick, htick, committed0,
                         digest0, sr, cdirty);
@@ -1471,11 +1487,11 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCo
 
 // the fast step of one role (k_round, k_fast_list)
 template <int N, bool TRACE, int MODE, int STG = 0, bool AUX = false>
-RBE_HD bool step_fast(const Planes& P, const Params& C, u64 r, u32 round, StepCounters& ctr,
+RBE_HD bool step_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, StepCounters& ctr,
                       StageRow<N>* sr = nullptr, u32 aux = 0) {
   if constexpr (MODE == MODE_LEAD)
-    return lead_fast<N, TRACE, STG, AUX>(P, C, r, round, ctr, sr, aux);
-  else return foll_fast<N, TRACE, STG, AUX>(P, C, r, round, ctr, sr, aux);
+    return lead_fast<N, TRACE, STG, AUX>(P, C, r, ck, ctr, sr, aux);
+  else return foll_fast<N, TRACE, STG, AUX>(P, C, r, ck, ctr, sr, aux);
 }
 
 }  // namespace rbe

@@ -1,0 +1,210 @@
+// rbe_host.h — host-side staging of the node-layer inputs (rbe_push_*,
+// rbe_request_leader_transfer, rbe_report_*, rbe_notify_applied), shared by
+// the HIP engine and the test-only host build of the step.
+//
+// In dragonboat the node layer hands these to *raft.Peer one call at a time
+// under raftMu (node.go:1030-1067 handleEvents → peer.go:106-315).  Here a call
+// stages a whole batch host-side: it is checked completely before anything is
+// staged (a bad replica or argument stages nothing), and the staged records go
+// to the device in one copy plus one scatter launch when the next step starts.
+// A replica takes one proposal batch, one ReadIndex ctx and one leader-transfer
+// request per step, the way the node batches them (incomingProposals.get,
+// node.go:1091-1106; batchedReadIndex, 1379-1382; pendingLeaderTransfer,
+// 1069-1075): a second one is RBE_E_STATE instead of silently replacing the
+// first.
+#pragma once
+#include <cstring>
+#include <vector>
+
+#include "../../include/rbe.h"
+#include "rbe_types.h"
+
+namespace rbe {
+
+struct HostInputs {
+  u64 n_rep = 0;
+  u32 n = 0;
+  u32 in_cap = 0;
+  std::vector<u32> slot;    // [n_rep] index into recs, ~0u = nothing staged
+  std::vector<u32> mark;    // [n_rep] duplicate check within one call (epoch stamps)
+  u32 epoch = 0;
+  std::vector<u64> reps;    // staged replicas ...
+  std::vector<ExtIn> recs;  // ... and their input records
+  std::vector<Ent> ents;    // staged proposal entries (Planes::in_ents)
+  std::vector<u64> app_rep, app_val;  // staged rbe_notify_applied values
+  std::vector<u64> applied;  // [n_rep] host mirror of Planes::applied (the host is its only writer)
+
+  void init(u64 n_rep_, u32 n_, u32 in_cap_) {
+    n_rep = n_rep_;
+    n = n_;
+    in_cap = in_cap_;
+    slot.assign(n_rep, ~0u);
+    mark.assign(n_rep, 0u);
+    applied.assign(n_rep, 0);
+  }
+  bool empty() const { return reps.empty() && app_rep.empty(); }
+  void clear() {
+    for (u64 r : reps) slot[r] = ~0u;
+    reps.clear();
+    recs.clear();
+    ents.clear();
+    app_rep.clear();
+    app_val.clear();
+  }
+  ExtIn& rec(u64 r) {
+    if (slot[r] == ~0u) {
+      slot[r] = (u32)recs.size();
+      reps.push_back(r);
+      ExtIn z;
+      memset(&z, 0, sizeof(z));
+      recs.push_back(z);
+    }
+    return recs[slot[r]];
+  }
+  u32 staged_flags(u64 r) const { return slot[r] == ~0u ? 0u : recs[slot[r]].flags; }
+  // 0, or RBE_E_INVALID / RBE_E_STATE for the whole batch: every replica in
+  // range, none twice in the batch, none with `flag` already staged
+  int check_replicas(u64 cnt, const u64* replica, u32 flag) {
+    if (cnt && !replica) return RBE_E_INVALID;
+    for (u64 i = 0; i < cnt; i++)
+      if (replica[i] >= n_rep) return RBE_E_INVALID;
+    if (!flag) return RBE_OK;
+    if (++epoch == 0) {
+      mark.assign(n_rep, 0u);
+      epoch = 1;
+    }
+    for (u64 i = 0; i < cnt; i++) {
+      const u64 r = replica[i];
+      if (mark[r] == epoch || (staged_flags(r) & flag)) return RBE_E_STATE;
+      mark[r] = epoch;
+    }
+    return RBE_OK;
+  }
+
+  int push_proposals(u64 cnt, const u64* replica, const u32* n_ents, const u32* type,
+                     const u32* cmd_len, const u8* cmd) {
+    if (cnt && (!n_ents || !type || !cmd_len)) return RBE_E_INVALID;
+    int rc = check_replicas(cnt, replica, EXT_PROPOSE);
+    if (rc) return rc;
+    u64 total = 0, bytes = 0;
+    for (u64 i = 0; i < cnt; i++) {
+      if (n_ents[i] == 0 || n_ents[i] > 0xFFFFu) return RBE_E_INVALID;
+      total += n_ents[i];
+    }
+    for (u64 j = 0; j < total; j++) {
+      // Cmd is inline (<= 16 bytes); config changes go through
+      // ProposeConfigChange, a membership path the device does not run
+      if (cmd_len[j] > 16 || type[j] == E_ConfigChange || type[j] > E_Metadata)
+        return RBE_E_INVALID;
+      bytes += cmd_len[j];
+    }
+    if (bytes && !cmd) return RBE_E_INVALID;
+    if (ents.size() + total > in_cap) return RBE_E_NOMEM;
+    u64 j = 0, off = 0;
+    for (u64 i = 0; i < cnt; i++) {
+      ExtIn& x = rec(replica[i]);
+      x.flags |= EXT_PROPOSE;
+      x.n_prop = n_ents[i];
+      x.prop_off = (u32)ents.size();
+      for (u32 t = 0; t < n_ents[i]; t++, j++) {
+        Ent e;
+        memset(&e, 0, sizeof(e));
+        e.term = 0;  // stamped by the leader (appendEntries, raft.go:909-920)
+        e.type = type[j];
+        e.len = cmd_len[j];
+        u8 b[16];
+        memset(b, 0, sizeof(b));
+        if (cmd_len[j]) memcpy(b, cmd + off, cmd_len[j]);
+        off += cmd_len[j];
+        memcpy(&e.lo, b, 8);
+        memcpy(&e.hi, b + 8, 8);
+        ents.push_back(e);
+      }
+    }
+    return RBE_OK;
+  }
+  int push_read_index(u64 cnt, const u64* replica, const u64* lo, const u64* hi) {
+    if (cnt && (!lo || !hi)) return RBE_E_INVALID;
+    for (u64 i = 0; i < cnt; i++)
+      if (lo[i] == 0) return RBE_E_INVALID;  // ctx.Low is never 0 (requests.go:726)
+    int rc = check_replicas(cnt, replica, EXT_READ);
+    if (rc) return rc;
+    for (u64 i = 0; i < cnt; i++) {
+      ExtIn& x = rec(replica[i]);
+      x.flags |= EXT_READ;
+      x.ctx_low = lo[i];
+      x.ctx_high = hi[i];
+    }
+    return RBE_OK;
+  }
+  int request_leader_transfer(u64 cnt, const u64* replica, const u64* target) {
+    if (cnt && !target) return RBE_E_INVALID;
+    for (u64 i = 0; i < cnt; i++)
+      if (target[i] < 1 || target[i] > n) return RBE_E_INVALID;  // NoNode panics, raft.go:1715
+    int rc = check_replicas(cnt, replica, EXT_XFER);
+    if (rc) return rc;
+    for (u64 i = 0; i < cnt; i++) {
+      ExtIn& x = rec(replica[i]);
+      x.flags |= EXT_XFER;
+      x.xfer_target = (u8)target[i];
+    }
+    return RBE_OK;
+  }
+  int report_unreachable(u64 cnt, const u64* replica, const u64* node) {
+    if (cnt && !node) return RBE_E_INVALID;
+    for (u64 i = 0; i < cnt; i++)
+      if (node[i] < 1 || node[i] > n) return RBE_E_INVALID;
+    int rc = check_replicas(cnt, replica, 0);
+    if (rc) return rc;
+    for (u64 i = 0; i < cnt; i++) {
+      ExtIn& x = rec(replica[i]);
+      x.flags |= EXT_UNREACH;
+      x.unreach |= (u8)(1u << (node[i] - 1));
+    }
+    return RBE_OK;
+  }
+  int report_snapshot_status(u64 cnt, const u64* replica, const u64* node, const u8* reject) {
+    if (cnt && (!node || !reject)) return RBE_E_INVALID;
+    for (u64 i = 0; i < cnt; i++)
+      if (node[i] < 1 || node[i] > n) return RBE_E_INVALID;
+    int rc = check_replicas(cnt, replica, 0);
+    if (rc) return rc;
+    for (u64 i = 0; i < cnt; i++) {
+      ExtIn& x = rec(replica[i]);
+      const u8 bit = (u8)(1u << (node[i] - 1));
+      x.flags |= EXT_SNAPST;
+      x.snap_nodes |= bit;
+      x.snap_reject = (u8)(reject[i] ? (x.snap_reject | bit) : (x.snap_reject & ~bit));
+    }
+    return RBE_OK;
+  }
+  int notify_applied(u64 cnt, const u64* replica, const u64* value) {
+    if (cnt && !value) return RBE_E_INVALID;
+    int rc = check_replicas(cnt, replica, 0);
+    if (rc) return rc;
+    for (u64 i = 0; i < cnt; i++)  // applied never moves backwards (node.go:911-913)
+      if (value[i] < applied[replica[i]]) return RBE_E_INVALID;
+    for (u64 i = 0; i < cnt; i++) {
+      const u64 r = replica[i];
+      app_rep.push_back(r);
+      app_val.push_back(value[i]);
+      // a changed applied index is an event of the step (node.go:1033)
+      if (value[i] != applied[r]) rec(r).flags |= EXT_APPLIED;
+      applied[r] = value[i];
+    }
+    return RBE_OK;
+  }
+  // Write the staged input into host-resident planes (the test-only host build;
+  // the HIP engine uploads the same vectors and scatters them on device).
+  // resync the applied mirror after the plane was overwritten (snapshot import)
+  void resync_applied(const u64* plane, u64 first, u64 count) {
+    for (u64 i = 0; i < count; i++) applied[first + i] = plane[i];
+  }
+  void apply_host(const Planes& P) {
+    for (size_t i = 0; i < reps.size(); i++) P.ext[reps[i]] = recs[i];
+    for (size_t i = 0; i < ents.size(); i++) P.in_ents[i] = ents[i];
+    for (size_t i = 0; i < app_rep.size(); i++) P.applied[app_rep[i]] = app_val[i];
+  }
+};
+
+}  // namespace rbe

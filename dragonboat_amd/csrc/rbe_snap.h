@@ -23,7 +23,7 @@
 namespace rbe {
 
 static constexpr u64 kSnapMagic = 0x31504E5345425255ull;  // "URBESNP1"
-static constexpr int kSnapPlanes = 18;
+static constexpr int kSnapPlanes = 19;
 
 struct SnapHeader {
   u64 magic;
@@ -31,7 +31,8 @@ struct SnapHeader {
   u32 round, hdr_bytes;
   u64 first, count;
   u64 body_bytes;
-  u64 reserved[2];
+  u64 behavior;  // snap_behavior_hash of the writing configuration
+  u64 tclk;      // ticks before `round` (Clk::tclk)
 };
 static_assert(sizeof(SnapHeader) == 88, "snapshot header layout");
 
@@ -67,6 +68,7 @@ inline void snap_planes(const Planes& P, const Params& C, SnapPlane* out) {
   add(P.dri, 1, R * C.dri_cap * sizeof(DropRI), N * C.dri_cap * sizeof(DropRI));
   add(P.ext, 1, R * sizeof(ExtIn), N * sizeof(ExtIn));
   add(P.idle, 1, R, N);
+  add(P.applied, 1, R * sizeof(u64), N * sizeof(u64));
   // the per-replica fault words live in Hot/Core/Upd; nothing else is carried
   out[i++] = SnapPlane{nullptr, 0, 0, 0};
 }
@@ -83,13 +85,14 @@ inline u64 snap_body_bytes(const Planes& P, const Params& C, u64 count) {
 // quorum check, quiesce, the injected PRNG seed, cluster-id mapping, entry
 // size limit, workload, fault schedule, replica placement): a snapshot only
 // resumes bit-exact under the configuration that wrote it, so import rejects
-// a mismatch instead of diverging silently (reserved[0] of the header).
+// a mismatch instead of diverging silently (SnapHeader::behavior).
 inline u64 snap_behavior_hash(const Params& C) {
   const u64 f[] = {C.election_rtt, C.heartbeat_rtt, C.check_quorum, C.quiesce, C.seed,
                    C.cid_base, C.cid_stride, C.max_entry_size, C.wl_enabled, C.wl_start_round,
                    C.wl_stop_round, C.wl_active_mod, C.wl_read_permille, C.ext_inputs,
                    C.iso_period, C.iso_len, C.iso_mod, C.rep_world, C.rep_rank,
-                   C.snapshot_entries, C.compaction_overhead, C.heap_bytes, C.ext_apply};
+                   C.snapshot_entries, C.compaction_overhead, C.heap_bytes, C.ext_apply,
+                   C.xfer_period, C.xfer_mod};
   u64 h = 0x243F6A8885A308D3ull;
   for (u64 x : f) {
     h ^= x + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
@@ -98,8 +101,8 @@ inline u64 snap_behavior_hash(const Params& C) {
   return h;
 }
 
-inline void snap_fill_header(const Params& C, u32 abi, u32 round, u64 first, u64 count, u64 body,
-                             SnapHeader* h) {
+inline void snap_fill_header(const Params& C, u32 abi, u32 round, u32 tclk, u64 first, u64 count,
+                             u64 body, SnapHeader* h) {
   *h = SnapHeader{};
   h->magic = kSnapMagic;
   h->abi = abi;
@@ -115,7 +118,8 @@ inline void snap_fill_header(const Params& C, u32 abi, u32 round, u64 first, u64
   h->first = first;
   h->count = count;
   h->body_bytes = body;
-  h->reserved[0] = snap_behavior_hash(C);
+  h->behavior = snap_behavior_hash(C);
+  h->tclk = tclk;
 }
 
 // 0 if the header describes a range this geometry can take, else RBE_E_INVALID.
@@ -126,7 +130,7 @@ inline int snap_check_header(const Params& C, u32 abi, const SnapHeader* h, u64 
   if (h->n != C.n || h->ring != C.ring || h->rq_cap != C.rq_cap || h->maxm != C.maxm ||
       h->ecap != C.ecap || h->rtr_cap != C.rtr_cap || h->dri_cap != C.dri_cap)
     return -1;
-  if (h->reserved[0] != snap_behavior_hash(C)) return -1;
+  if (h->behavior != snap_behavior_hash(C)) return -1;
   if (h->count == 0 || h->first >= C.n_groups || h->count > C.n_groups - h->first) return -1;
   if (buf_bytes < sizeof(SnapHeader) + h->body_bytes) return -1;
   return 0;

@@ -62,6 +62,21 @@ RBE_HD u32 wl_input(const Params& C, u64 cid, u32 round) {
   u32 u = below(mix64(C.seed ^ (cid * 0xC2B2AE3D27D4EB4FULL) ^ ((u64)round << 20)), 1000);
   return u < C.wl_read_permille ? 2u : 1u;
 }
+// leader-transfer schedule: at every xfer_period-th
+// round, in groups selected by hash, one seeded replica (any role) gets a
+// Peer.RequestLeaderTransfer(target) (node.go:1069-1075 → peer.go:106-113)
+// with a seeded target node id; returns the target, 0 for none.  Restated
+// independently in oracle/harness.cpp.
+RBE_HD u32 xfer_input(const Params& C, u64 cid, u32 round, u32 k) {
+  if (!C.xfer_period || round == 0 || round % C.xfer_period != 0) return 0;
+  const u64 epoch = round / C.xfer_period;
+  if (C.xfer_mod > 1 &&
+      below(mix64(C.seed ^ (cid * 0xA24BAED4963EE407ULL) ^ (epoch << 36)), C.xfer_mod) != 0)
+    return 0;
+  const u64 h = mix64(C.seed ^ (cid * 0x9FB21C651E98DF25ULL) ^ (epoch << 12) ^ 0x5851F42DULL);
+  if (below(h, C.n) != k) return 0;
+  return below(mix64(h), C.n) + 1;
+}
 RBE_HD bool iso_selected(const Params& C, u64 cid, u32 epoch) {
   if (C.iso_mod <= 1) return true;
   return below(mix64(C.seed ^ (cid * 0x94D049BB133111EBULL) ^ ((u64)epoch << 40)), C.iso_mod) ==
@@ -100,7 +115,8 @@ RBE_HD Hot load_hot(const Planes& P, const Params& C, u64 r, u32 round) {
 //            without reading Hot.
 enum : u8 { IB_LAZY = 1, IB_LEAD = 2, IB_H1 = 4, IB_H2 = 8, IB_ROLE_SHIFT = 4 };
 RBE_HD u8 idle_byte(const Params& C, u8 role, u8 flags, u32 qs) {
-  const bool lazy = C.quiesce && qs > 0 && (flags & HF_RAFT_QUIESCE) && !(flags & HF_APPLY_PENDING);
+  const bool lazy = C.quiesce && qs > 0 && (flags & HF_RAFT_QUIESCE) &&
+                    !(flags & (HF_APPLY_PENDING | HF_APPLIED_NEW));
   return (u8)((lazy ? IB_LAZY : 0) | (role == R_Leader ? IB_LEAD : 0) | ((role & 7u) << IB_ROLE_SHIFT));
 }
 RBE_HD u32 idle_role(u8 ib) { return (ib >> IB_ROLE_SHIFT) & 7u; }
@@ -157,6 +173,7 @@ struct Lane {
   const u32 k;      // slot; node id = k + 1
   const u32 round;
   const u32 par;    // round & 1: outbox buffer written this round
+  const Clk clk;    // round, ticks before it, whether it ticks
   const u64 cid;
   const u8 self;    // node id
 
@@ -181,6 +198,7 @@ struct Lane {
   u64 msg_hash, rtr_hash, drop_hash;
   u32 n_msgs, n_rtr, n_drop_ent, n_drop_ri;
   u32 fault;
+  u32 events;        // EV_* of this step (Upd::events)
   // deferred fan-out actions, executed in this order after each event
   u32 rep_mask;      // slots to sendReplicateMessage to
   u8 tn_to;          // TimeoutNow target
@@ -191,9 +209,10 @@ struct Lane {
   u8 rq_from;
   StepCounters& ctr;
 
-  RBE_HD Lane(const Planes& P_, const Params& C_, u64 r_, u32 round_, StepCounters& c_)
-      : P(P_), C(C_), r(r_), g(r_ / N), k((u32)(r_ % N)), round(round_), par(round_ & 1u),
-        cid(C_.cid_base + (r_ / N) * C_.cid_stride), self((u8)(r_ % N + 1)), ctr(c_) {}
+  RBE_HD Lane(const Planes& P_, const Params& C_, u64 r_, Clk clk_, StepCounters& c_)
+      : P(P_), C(C_), r(r_), g(r_ / N), k((u32)(r_ % N)), round(clk_.round),
+        par(clk_.round & 1u), clk(clk_), cid(C_.cid_base + (r_ / N) * C_.cid_stride),
+        self((u8)(r_ % N + 1)), ctr(c_) {}
 
   // ------------------------------------------------------------- faults
   RBE_HD void set_fault(u32 f) {
@@ -562,8 +581,10 @@ struct Lane {
   }
   RBE_HD void report_dropped_read_index(u64 low, u64 high) {  // raft.go:1999-2012
     add_dropped_ri(low, high);
+    events |= EV_READ_INDEX_DROPPED;
   }
   RBE_HD void report_dropped_proposal(const Ent* e, u32 cnt) {  // raft.go:1987-1997
+    if (cnt) events |= EV_PROPOSAL_DROPPED;
     for (u32 i = 0; i < cnt; i++) {
       n_drop_ent++;
       if (TRACE) {
@@ -909,6 +930,7 @@ struct Lane {
       resp.reject = 1;
       resp.log_index = m.log_index;
       resp.hint = last;
+      events |= EV_REPLICATION_REJECTED;  // raft.go:1359-1369
     }
     send(resp);
   }
@@ -924,6 +946,7 @@ struct Lane {
   RBE_HD void campaign() {  // raft.go:1080-1116
     become_candidate();
     ctr.v[C_CAMPAIGNS]++;
+    events |= EV_CAMPAIGN_LAUNCHED;
     // handleVoteResp(self, false)
     vresp |= (u8)(1u << k);
     vgrant |= (u8)(1u << k);
@@ -947,9 +970,17 @@ struct Lane {
       send(m);
     }
   }
+  // raft.applied: NotifyRaftLastApplied at the start of the step (node.go:
+  // 1010-1014); without ext_apply the harness applies every committed entry
+  // the step it is returned, so it equals `processed` at step start
+  RBE_HD u64 applied_index() const { return C.ext_apply ? P.applied[r] : processed; }
   RBE_HD void on_election() {  // handleNodeElection, raft.go:1482-1512
     if (role != R_Leader) {
-      if (committed > processed) return;  // hasConfigChangeToApply: committed > applied
+      // hasConfigChangeToApply (raft.go:1460-1472): committed > applied
+      if (committed > applied_index()) {
+        events |= EV_CAMPAIGN_SKIPPED;
+        return;
+      }
       campaign();
     }
   }
@@ -1249,7 +1280,9 @@ struct Lane {
     if (flags & HF_APPLY_PENDING) return false;
     if (ltt != 0 || (flags & HF_IS_LTT)) return false;
     if (role == R_Follower && inp) return false;
-    if (C.ext_inputs && P.ext[r].kind) return false;
+    if (!clk.tick) return false;
+    if (C.xfer_period && xfer_input(C, cid, round, k)) return false;
+    if (C.ext_inputs && P.ext[r].flags) return false;
     bool from_leader = false;
     u32 n_in = 0;
     if (round > 0) {
@@ -1302,7 +1335,7 @@ struct Lane {
 
   // ------------------------------------------------------------- the step
   RBE_HD void load() {
-    Hot h = load_hot(P, C, r, round);
+    Hot h = load_hot(P, C, r, clk.tclk);
     role = h.role;
     flags = h.flags;
     vresp = h.votes_resp;
@@ -1402,41 +1435,88 @@ struct Lane {
     } else {
       iso = 0;
     }
-    ctr.v[C_STEPS]++;
     const u64 committed0 = committed;
     const u64 term0 = term, vote0 = vote;
-    // client input of this round goes to replicas that lead at round start
-    u32 inp = role == R_Leader ? wl_input(C, cid, round) : 0u;
-    ExtIn ext;
-    ext.kind = 0;
-    ext.len = 0;
-    ext.lo = ext.hi = ext.ctx_low = ext.ctx_high = ext.pad = 0;
+    const u8 leader0 = leader;
+    events = 0;
+    // Client input of the round.  The synthetic workload goes to replicas
+    // that lead at round start; host-pushed input (ExtIn) to the replica it
+    // names, any role, with the ReadIndex ctx / proposal batch it carries.
+    const u32 wl = role == R_Leader ? wl_input(C, cid, round) : 0u;
+    bool do_read = wl == 2, do_prop = wl == 1;
+    u64 read_lo = 0, read_hi = 0;
+    u32 prop_n = 0, xfer = C.xfer_period ? xfer_input(C, cid, round, k) : 0u;
+    const Ent* prop_ents = nullptr;
+    u8 unreach = 0, snap_nodes = 0, snap_reject = 0;
+    bool ext_applied = false;
     if (C.ext_inputs) {
-      ext = P.ext[r];
-      if (ext.kind) {
+      const ExtIn ext = P.ext[r];
+      if (ext.flags) {
         ExtIn z;
-        z.kind = 0;
-        z.len = 0;
-        z.lo = z.hi = z.ctx_low = z.ctx_high = z.pad = 0;
+        z.flags = z.n_prop = z.prop_off = 0;
+        z.xfer_target = z.unreach = z.snap_nodes = z.snap_reject = 0;
+        z.ctx_low = z.ctx_high = 0;
+        z.pad[0] = z.pad[1] = z.pad[2] = z.pad[3] = 0;
         P.ext[r] = z;
-        inp = ext.kind;
+        if (ext.flags & EXT_READ) {
+          do_read = true;
+          read_lo = ext.ctx_low;
+          read_hi = ext.ctx_high;
+        }
+        if (ext.flags & EXT_PROPOSE) {
+          do_prop = true;
+          prop_n = ext.n_prop;
+          prop_ents = &P.in_ents[ext.prop_off];
+        }
+        if (ext.flags & EXT_XFER) xfer = ext.xfer_target;
+        ext_applied = (ext.flags & EXT_APPLIED) != 0;
+        if (ext.flags & EXT_UNREACH) unreach = ext.unreach;
+        if (ext.flags & EXT_SNAPST) {
+          snap_nodes = ext.snap_nodes;
+          snap_reject = ext.snap_reject;
+        }
       }
     }
+    if (!clk.tick) {
+      // a round without a tick is a step only if handleEvents finds an event
+      // (node.go:1030-1067): a message or notice, client input, an entry to apply
+      bool ev = do_read || do_prop || xfer || unreach || snap_nodes || ext_applied ||
+                (flags & (HF_APPLY_PENDING | HF_APPLIED_NEW));
+      if (round > 0)
+        for (u32 s = 0; s < N; s++)
+          if (s != k && P.cnt[par ^ 1u][g * N * N + s * N + k] != 0) ev = true;
+      if (!ev) {
+        u16* cnt = &P.cnt[par][g * N * N + k * N];
+        for (u32 dd = 0; dd < N; dd++) cnt[dd] = 0;
+        return true;
+      }
+    }
+    ctr.v[C_STEPS]++;
+    if (do_read && !(C.ext_inputs && read_lo != 0)) {  // the workload's ctx
+      read_lo = ((u64)(round + 1) << 32) | (u64)self;
+      read_hi = cid + 1;
+    }
     // handleReadIndexRequests (node.go:1108-1118)
-    if (inp == 2) {
+    if (do_read) {
       q_record_activity(M_ReadIndex);
       ctr.v[C_READS]++;
     }
-    // One event loop, one handle() site.  Events in node order:
+    // One event loop, one handle() site.  Events in node order (handleEvents,
+    // node.go:1030-1067):
+    //   host-reported Unreachable / SnapshotStatus (node-handled messages of
+    //     the inbox, node.go:1207-1220: no activity recorded), delivered first
     //   handleReceivedMessages (node.go:1171-1205): inbox in (sender, stream) order
     //   batchedReadIndex (node.go:1379-1382) → Peer.ReadIndex
-    //   handleLocalTickMessage → node.tick (node.go:1384-1399): one tick per round
+    //   handleLocalTickMessage → node.tick (node.go:1384-1399): one tick per
+    //     ticking round
     //   handleProposals (node.go:1091-1106) → Peer.ProposeEntries
+    //   handleLeaderTransferRequest (node.go:1069-1075) → Peer.RequestLeaderTransfer
     const u32 ppar = par ^ 1u;
     const u16* icnt = &P.cnt[ppar][g * N * N];
     u32 cs = 0, ci = 0, cn = 0, cna = 0;  // inbox cursor: sender, index, count, #A
     bool copen = false;
-    u32 phase = round > 0 ? 0u : 1u;
+    u32 phase = (unreach | snap_nodes) ? 0u : (round > 0 ? 1u : 2u);
+    u32 rep_bit = 0;  // local reports: next node bit
     rep_mask = 0;
     tn_to = 0;
     hb_pending = rq_pending = false;
@@ -1446,9 +1526,30 @@ struct Lane {
     for (;;) {
       u32 kind = 0;  // 0 none, 1 inbox message, 2 local message, 3 tick
       Msg m;
-      u64 ents_off = 0;  // entries of m: P.arena[ents_par] + ents_off
-      u32 ents_par = ppar;
+      const Ent* ents = nullptr;
       if (phase == 0) {
+        // Peer.ReportUnreachableNode / ReportSnapshotStatus (peer.go:168-183)
+#pragma unroll 1
+        while (rep_bit < 2 * N) {
+          const u32 b = rep_bit++;
+          const u32 node = b < N ? b : b - N;
+          if (b < N && ((unreach >> node) & 1u)) {
+            m = mk(M_Unreachable, self);
+            m.from = (u8)(node + 1);
+            kind = 2;
+            break;
+          }
+          if (b >= N && ((snap_nodes >> node) & 1u)) {
+            m = mk(M_SnapshotStatus, self);
+            m.from = (u8)(node + 1);
+            m.reject = (u8)((snap_reject >> node) & 1u);
+            kind = 2;
+            break;
+          }
+        }
+        if (kind == 0) phase = round > 0 ? 1u : 2u;
+      }
+      if (kind == 0 && phase == 1) {
 #pragma unroll 1
         while (cs < N) {
           if (!copen) {
@@ -1469,7 +1570,7 @@ struct Lane {
           if (ci < cn) {
             const Msg* lst = &P.msgs[ppar][msg_slot_base(cs, k)];
             m = ci < cna ? lst[ci] : lst[C.maxm - 1u - (ci - cna)];
-            ents_off = (g * N + cs) * (u64)C.ecap + m.ent_off;
+            ents = &P.arena[ppar][(g * N + cs) * (u64)C.ecap + m.ent_off];
             ci++;
             kind = 1;
             break;
@@ -1477,53 +1578,56 @@ struct Lane {
           cs++;
           copen = false;
         }
-        if (kind == 0) phase = 1;
-      }
-      if (kind == 0 && phase == 1) {
-        phase = 2;
-        if (inp == 2) {
-          m = mk(M_ReadIndex, 0);
-          if (C.ext_inputs && ext.kind == 2) {
-            m.hint = ext.ctx_low;
-            m.hint_high = ext.ctx_high;
-          } else {
-            m.hint = ((u64)(round + 1) << 32) | (u64)self;
-            m.hint_high = cid + 1;
-          }
-          kind = 2;
-        }
+        if (kind == 0) phase = 2;
       }
       if (kind == 0 && phase == 2) {
         phase = 3;
-        kind = 3;
+        if (do_read) {
+          m = mk(M_ReadIndex, 0);
+          m.hint = read_lo;
+          m.hint_high = read_hi;
+          kind = 2;
+        }
       }
       if (kind == 0 && phase == 3) {
         phase = 4;
-        if (inp == 1) {
-          Ent e;
-          e.term = 0;
-          e.type = E_Application;
-          if (C.ext_inputs && ext.kind == 1) {
-            e.len = ext.len;
-            e.lo = ext.lo;
-            e.hi = ext.hi;
-          } else {
+        if (clk.tick) kind = 3;
+      }
+      if (kind == 0 && phase == 4) {
+        phase = 5;
+        if (do_prop) {
+          if (prop_ents == nullptr) {
+            // the workload's proposal, staged in this round's arena so every
+            // handler reads entries from global memory
+            Ent e;
+            e.term = 0;
+            e.type = E_Application;
             e.len = 16;
             e.lo = wl_payload_lo(C.seed, cid, round);
             e.hi = mix64(e.lo);
+            u32 off = 0;
+            if (arena_put(&e, 1, &off)) {
+              prop_ents = &P.arena[par][r * (u64)C.ecap + off];
+              prop_n = 1;
+            }
           }
-          // the proposed entry is staged in this round's arena so every
-          // handler reads entries from global memory
-          u32 off = 0;
-          if (arena_put(&e, 1, &off)) {
+          if (prop_ents != nullptr) {
             m = mk(M_Propose, 0);
             m.from = self;  // Peer.ProposeEntries (peer.go:117-123)
-            m.n_ent = 1;
-            ents_par = par;
-            ents_off = r * (u64)C.ecap + off;
+            m.n_ent = (u16)prop_n;
+            ents = prop_ents;
             kind = 2;
           }
           ctr.v[C_PROPOSALS]++;
+        }
+      }
+      if (kind == 0 && phase == 5) {
+        phase = 6;
+        if (xfer) {  // Peer.RequestLeaderTransfer (peer.go:106-113)
+          m = mk(M_LeaderTransfer, self);
+          m.from = (u8)xfer;
+          m.hint = xfer;
+          kind = 2;
         }
       }
       if (kind == 0) break;
@@ -1547,7 +1651,7 @@ struct Lane {
           else
             q_record_activity(m.type);
         }
-        handle(m, &P.arena[ents_par][ents_off]);
+        handle(m, ents);
       }
       // deferred fan-out, in the reference's emission order
 #pragma unroll 1
@@ -1622,6 +1726,8 @@ struct Lane {
     saved_to = last;
     if (processed < committed) flags |= HF_APPLY_PENDING;
     else flags &= (u8)~HF_APPLY_PENDING;
+    if (u.apply_hi >= u.apply_lo && !C.ext_apply) flags |= HF_APPLIED_NEW;
+    else flags &= (u8)~HF_APPLIED_NEW;
     if (fault) flags |= HF_FAULTED;
     if (role == R_Leader) {
       ctr.v[C_COMMITTED] += (u32)(committed - committed0);
@@ -1661,7 +1767,7 @@ struct Lane {
     u.flags = (u16)((term != term0 || vote != vote0 || committed != committed0 ? UF_STATE_CHANGED
                                                                                 : 0u) |
                     (send_q ? UF_SENT_QUIESCE : 0u));
-    u.pad = 0;
+    u.events = (u16)(events | (leader != leader0 ? EV_LEADER_UPDATED : 0u));
     u.round = round;
     u.pad2 = 0;
     P.upd[r] = u;
@@ -1682,16 +1788,16 @@ RBE_HD void Lane<N, TRACE, MODE>::raft_tick() {  // raft.go:551-564
 
 // the full handler table: always completes the round
 template <int N, bool TRACE>
-RBE_HD void step_replica(const Planes& P, const Params& C, u64 r, u32 round, StepCounters& ctr) {
-  Lane<N, TRACE, MODE_FULL> lane(P, C, r, round, ctr);
+RBE_HD void step_replica(const Planes& P, const Params& C, u64 r, Clk ck, StepCounters& ctr) {
+  Lane<N, TRACE, MODE_FULL> lane(P, C, r, ck, ctr);
   lane.run();
 }
 // the steady-state subset: returns false (nothing written) when the round
 // needs the full table
 template <int N, bool TRACE, int MODE>
-RBE_HD bool step_replica_fast(const Planes& P, const Params& C, u64 r, u32 round,
+RBE_HD bool step_replica_fast(const Planes& P, const Params& C, u64 r, Clk ck,
                               StepCounters& ctr) {
-  Lane<N, TRACE, MODE> lane(P, C, r, round, ctr);
+  Lane<N, TRACE, MODE> lane(P, C, r, ck, ctr);
   return lane.run();
 }
 
@@ -1757,7 +1863,7 @@ RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   u.n_msgs = u.n_rtr = u.n_drop_ent = u.n_drop_ri = 0;
   u.fault = 0;
   u.flags = 0;
-  u.pad = 0;
+  u.events = 0;
   u.round = ~0u;
   u.pad2 = 0;
   P.upd[r] = u;
@@ -1782,15 +1888,21 @@ enum : u32 { T_DONE = 0, T_LEAD = 1, T_FOLL = 2, T_FULL = 3 };
 // caller has loaded `ib` and `inbound` (k_triage prefetches them for all the
 // replicas a lane owns).  Returns true when the round is complete.
 template <int N>
-RBE_HD bool triage_lazy(const Planes& P, const Params& C, u64 r, u32 round, u8 ib, bool inbound,
-                        StepCounters& ctr) {
+RBE_HD bool triage_lazy(const Planes& P, const Params& C, u64 r, const Clk& ck, u8 ib,
+                        bool inbound, StepCounters& ctr) {
   if (!(ib & IB_LAZY) || inbound) return false;
+  const u32 round = ck.round;
   const u32 g = (u32)r / (u32)N;  // replica indices fit u32 (work lists hold u32)
-  if ((ib & IB_LEAD) && wl_input(C, C.cid_base + (u64)g * C.cid_stride, round)) return false;
-  if (C.ext_inputs && P.ext[r].kind) return false;
-  ctr.v[C_STEPS]++;
-  ctr.v[C_QUIESCED_TICKS]++;
-  ctr.v[C_LEADER_STEPS] += (ib & IB_LEAD) ? 1u : 0u;
+  const u64 cid = C.cid_base + (u64)g * C.cid_stride;
+  if ((ib & IB_LEAD) && wl_input(C, cid, round)) return false;
+  if (C.xfer_period && xfer_input(C, cid, round, (u32)r - g * (u32)N)) return false;
+  if (C.ext_inputs && P.ext[r].flags) return false;
+  // a round without a tick and without input is no step at all (handleEvents
+  // finds no event, node.go:1030-1067): only the count row is kept clean
+  const u32 t = ck.tick ? 1u : 0u;
+  ctr.v[C_STEPS] += t;
+  ctr.v[C_QUIESCED_TICKS] += t;
+  ctr.v[C_LEADER_STEPS] += (ib & IB_LEAD) ? t : 0u;
   if (!(ib & IB_H2)) {  // this parity's outbox counts may still be non-zero
     u16* cnt = &P.cnt[round & 1u][(u64)g * (N * N) + ((u32)r - g * (u32)N) * N];
     for (u32 d = 0; d < N; d++) cnt[d] = 0;
@@ -1861,12 +1973,13 @@ RBE_HD u32 class_of_role(u32 role) {
 }
 
 template <int N, bool TRACE>
-RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, u32 round,
+RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, const Clk& ck,
                           StepCounters& ctr) {
   const u64 g = r / N;
   const u32 k = (u32)(r % N);
+  const u32 round = ck.round;
   const u32 par = round & 1u;
-  const Hot h = load_hot(P, C, r, round);
+  const Hot h = load_hot(P, C, r, ck.tclk);
   u32 nmsg = 0, qbits = 0;
   if (round > 0) {
     const u16* icnt = &P.cnt[par ^ 1u][g * N * N];
@@ -1880,8 +1993,10 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, u32 round,
   const u64 cid = C.cid_base + g * C.cid_stride;
   const u32 cls = h.role == R_Leader ? T_LEAD : (h.role == R_Follower ? T_FOLL : T_FULL);
   if (nmsg || (h.flags & HF_APPLY_PENDING)) return cls;
+  if (!ck.tick && (h.flags & HF_APPLIED_NEW)) return cls;
   if (h.role == R_Leader && wl_input(C, cid, round)) return cls;
-  if (C.ext_inputs && P.ext[r].kind) return cls;
+  if (C.xfer_period && xfer_input(C, cid, round, k)) return cls;
+  if (C.ext_inputs && P.ext[r].flags) return cls;
   // quiesceManager (quiesce.go) on registers
   const u32 et2 = C.election_rtt * 2, thr = et2 * 10;
   u32 qt = h.q_tick, qs = h.q_quiesced_since, qn = h.q_no_activity_since, qe = h.q_exit_quiesce_tick;
@@ -1897,7 +2012,7 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, u32 round,
       qnew = true;
     }
   }
-  if (C.quiesce) {  // increaseQuiesceTick
+  if (C.quiesce && ck.tick) {  // increaseQuiesceTick
     qt++;
     if (!(qs > 0) && qt - qn > thr) {
       qs = qt;
@@ -1907,24 +2022,30 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, u32 round,
   }
   const bool quiesced = C.quiesce && qs > 0;
   u32 etick = h.election_tick;
-  u8 flags = h.flags;
-  if (quiesced) {
-    flags |= HF_RAFT_QUIESCE;  // quiescedTick
-    etick++;
-  } else {
-    if (h.role == R_Leader) return cls;          // leaderTick broadcasts heartbeats
-    if (etick + 1u >= h.rand_et) return cls;     // nonLeaderTick would elect
-    flags &= (u8)~HF_RAFT_QUIESCE;
-    etick++;
+  u8 flags = (u8)(h.flags & ~HF_APPLIED_NEW);  // this step returns no entries
+  if (ck.tick) {
+    if (quiesced) {
+      flags |= HF_RAFT_QUIESCE;  // quiescedTick
+      etick++;
+    } else {
+      if (h.role == R_Leader) return cls;          // leaderTick broadcasts heartbeats
+      if (etick + 1u >= h.rand_et) return cls;     // nonLeaderTick would elect
+      flags &= (u8)~HF_RAFT_QUIESCE;
+      etick++;
+    }
   }
+  // a round without a tick, input or Quiesce notice is no step at all
+  // (handleEvents finds no event): nothing but a clean count row
+  const bool noop = !ck.tick && qbits == 0;
   // commit the idle round
-  ctr.v[C_STEPS]++;
+  const u32 st = noop ? 0u : 1u;
+  ctr.v[C_STEPS] += st;
   ctr.v[C_MSG_IN] += popc8(qbits);
   // branch-free bumps (see FastOut in rbe_fast.h: sibling branches bumping
   // different counters become one indexed bump and the counters go to scratch)
-  ctr.v[C_QUIESCED_TICKS] += quiesced ? 1u : 0u;
-  ctr.v[C_ACTIVE_TICKS] += quiesced ? 0u : 1u;
-  ctr.v[C_LEADER_STEPS] += h.role == R_Leader ? 1u : 0u;
+  ctr.v[C_QUIESCED_TICKS] += ck.tick && quiesced ? 1u : 0u;
+  ctr.v[C_ACTIVE_TICKS] += ck.tick && !quiesced ? 1u : 0u;
+  ctr.v[C_LEADER_STEPS] += h.role == R_Leader ? st : 0u;
   u8 iso = 0;
   if (qnew && C.iso_period) {
     const u32 until = P.iso_until[g];
@@ -1933,7 +2054,8 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, u32 round,
   // A round that is only a QuiescedTick of an already-flagged replica writes
   // nothing (lazy ticks, materialize_hot); its outbox counts are written only
   // if the buffer of this parity still holds a non-zero word.
-  const bool lazy = !TRACE && quiesced && !qnew && qbits == 0 && (h.flags & HF_RAFT_QUIESCE);
+  const bool lazy = noop || (!TRACE && quiesced && !qnew && qbits == 0 &&
+                             (h.flags & HF_RAFT_QUIESCE));
   u16* cnt = &P.cnt[par][g * N * N + k * N];
   bool dirty = !lazy;
   if (lazy)
@@ -1961,7 +2083,7 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, u32 round,
     P.hot[r] = o;
     P.idle[r] = idle_byte(C, h.role, flags, qs);
   }
-  if (TRACE) {
+  if (TRACE && !noop) {
     const Core c = P.core[r];
     Upd u = P.upd[r];
     u64 d = u.digest;
@@ -1984,6 +2106,7 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, u32 round,
     u.apply_hi = c.committed;
     u.n_msgs = u.n_rtr = u.n_drop_ent = u.n_drop_ri = 0;
     u.flags = (u16)(qnew ? UF_SENT_QUIESCE : 0u);
+    u.events = 0;
     u.round = round;
     P.upd[r] = u;
   }

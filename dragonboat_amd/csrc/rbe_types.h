@@ -67,6 +67,9 @@ enum : u8 {
   HF_IS_LTT = 4,        // raft.isLeaderTransferTarget
   HF_APPLY_PENDING = 8, // processed < committed after the step (apply limited by size)
   HF_FAULTED = 16,      // Upd.fault != 0 (the sticky fault word is read only then)
+  HF_APPLIED_NEW = 32,  // the last step returned committed entries: the node's
+                        // confirmedIndex lags its applied index until the next
+                        // step (node.go:907-923, 1033), an event of its own
 };
 
 // core plane (64 B per replica)
@@ -170,7 +173,10 @@ struct DropRI {  // SystemCtx
 // parts are present; a replica takes at most one of each per step, as the
 // node batches them (one ReadIndex ctx per step, node.go:1379-1382; one
 // proposal batch, 1091-1106; one pending transfer, 1069-1075).
-enum : u32 { EXT_PROPOSE = 1, EXT_READ = 2, EXT_XFER = 4, EXT_UNREACH = 8, EXT_SNAPST = 16 };
+enum : u32 {
+  EXT_PROPOSE = 1, EXT_READ = 2, EXT_XFER = 4, EXT_UNREACH = 8, EXT_SNAPST = 16,
+  EXT_APPLIED = 32,  // rbe_notify_applied changed raft.applied (an event, node.go:1033)
+};
 struct alignas(16) ExtIn {
   u32 flags;
   u32 n_prop;        // entries of the proposal batch (EXT_PROPOSE)

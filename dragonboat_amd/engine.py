@@ -14,7 +14,7 @@ import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libdragonboat_amd.so")
-RBE_ABI_VERSION = 1
+RBE_ABI_VERSION = 2
 
 COUNTER_NAMES = ["steps", "committed", "msg_in", "msg_out", "ent_in", "ent_out",
                  "reads_confirmed", "proposals", "reads", "quiesced_ticks", "active_ticks",
@@ -41,7 +41,10 @@ class RbeConfig(C.Structure):
                 ("ext_inputs", C.c_uint32), ("iso_period", C.c_uint32),
                 ("iso_len", C.c_uint32), ("iso_mod", C.c_uint32),
                 ("rep_world", C.c_uint32), ("rep_rank", C.c_uint32),
-                ("reserved", C.c_uint32 * 5)]
+                ("ext_apply", C.c_uint32), ("in_cap", C.c_uint32),
+                ("xfer_period", C.c_uint32), ("xfer_mod", C.c_uint32),
+                ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
+                ("heap_bytes", C.c_uint64), ("reserved", C.c_uint32 * 4)]
 
 
 class RbeReplicaView(C.Structure):
@@ -55,7 +58,8 @@ class RbeReplicaView(C.Structure):
                 ("raft_quiesce", C.c_uint32), ("rq_count", C.c_uint32),
                 ("votes_resp", C.c_uint32), ("votes_granted", C.c_uint32),
                 ("match", C.c_uint64 * 8), ("next", C.c_uint64 * 8),
-                ("rstate", C.c_uint32 * 8), ("ractive", C.c_uint32 * 8)]
+                ("rstate", C.c_uint32 * 8), ("ractive", C.c_uint32 * 8),
+                ("events", C.c_uint32), ("pad", C.c_uint32)]
 
 
 class RbeUpdate(C.Structure):
@@ -65,7 +69,13 @@ class RbeUpdate(C.Structure):
                 ("n_messages", C.c_uint32), ("n_ready_to_read", C.c_uint32),
                 ("n_dropped_entries", C.c_uint32), ("n_dropped_read_indexes", C.c_uint32),
                 ("fault", C.c_uint32), ("flags", C.c_uint32), ("role", C.c_uint32),
-                ("leader_id", C.c_uint32)]
+                ("leader_id", C.c_uint32), ("events", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+# Update flags and listener events (include/rbe.h RBE_UF_* / RBE_EV_*)
+UF_STATE_CHANGED, UF_SENT_QUIESCE, UF_FAST_APPLY, UF_HAS_UPDATE = 1, 2, 8, 16
+EV_LEADER_UPDATED, EV_CAMPAIGN_LAUNCHED, EV_CAMPAIGN_SKIPPED, EV_SNAPSHOT_REJECTED = 1, 2, 4, 8
+EV_REPLICATION_REJECTED, EV_PROPOSAL_DROPPED, EV_READ_INDEX_DROPPED = 16, 32, 64
 
 
 class RbeMessage(C.Structure):
@@ -86,7 +96,9 @@ class RbeReadyToRead(C.Structure):
 
 
 # exported symbols of include/rbe.h (checked by tests/test_capi.py)
-EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_step", "rbe_run", "rbe_sync",
+EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe_step", "rbe_step_ex", "rbe_run",
+           "rbe_sync", "rbe_request_leader_transfer", "rbe_report_unreachable",
+           "rbe_report_snapshot_status", "rbe_notify_applied",
            "rbe_round", "rbe_run_timed", "rbe_push_proposals", "rbe_push_read_index",
            "rbe_get_updates", "rbe_get_messages", "rbe_get_ready_to_reads", "rbe_get_entries",
            "rbe_get_views", "rbe_get_counters", "rbe_reset_counters", "rbe_fault_summary",
@@ -98,7 +110,8 @@ KERNEL_SLOTS = 4
 _lib = None
 
 
-RBE_E_NOMEM = -3
+RBE_E_INVALID, RBE_E_NOMEM, RBE_E_STATE = -1, -3, -5
+RBE_STEP_NO_TICK = 1
 
 
 class EngineError(RuntimeError):
@@ -123,12 +136,18 @@ def load_library(path: Optional[str] = None):
         "rbe_create": (i32, [P(RbeConfig), P(vp)]),
         "rbe_destroy": (i32, [vp]),
         "rbe_abi_version": (i32, []),
+        "rbe_abi_sizes": (i32, [P(u64), u32]),
         "rbe_step": (i32, [vp]),
+        "rbe_step_ex": (i32, [vp, u32]),
+        "rbe_request_leader_transfer": (i32, [vp, u64, P(u64), P(u64)]),
+        "rbe_report_unreachable": (i32, [vp, u64, P(u64), P(u64)]),
+        "rbe_report_snapshot_status": (i32, [vp, u64, P(u64), P(u64), P(C.c_uint8)]),
+        "rbe_notify_applied": (i32, [vp, u64, P(u64), P(u64)]),
         "rbe_run": (i32, [vp, u32]),
         "rbe_sync": (i32, [vp]),
         "rbe_round": (i32, [vp, P(u32)]),
         "rbe_run_timed": (i32, [vp, u32, P(C.c_float)]),
-        "rbe_push_proposals": (i32, [vp, u64, P(u64), P(C.c_uint8), P(u32)]),
+        "rbe_push_proposals": (i32, [vp, u64, P(u64), P(u32), P(u32), P(u32), P(C.c_uint8)]),
         "rbe_push_read_index": (i32, [vp, u64, P(u64), P(u64), P(u64)]),
         "rbe_get_updates": (i32, [vp, u64, u64, P(RbeUpdate)]),
         "rbe_get_messages": (i32, [vp, u64, P(RbeMessage), u32, P(u32)]),
@@ -157,6 +176,11 @@ def load_library(path: Optional[str] = None):
         fn.argtypes = args
     if L.rbe_abi_version() != RBE_ABI_VERSION:
         raise EngineError("ABI version mismatch")
+    sz = (C.c_uint64 * 6)()
+    mine = [C.sizeof(t) for t in (RbeConfig, RbeReplicaView, RbeUpdate, RbeMessage, RbeEntry,
+                                  RbeReadyToRead)]
+    if L.rbe_abi_sizes(sz, 6) != 6 or list(sz) != mine:
+        raise EngineError(f"ABI struct sizes differ: library {list(sz)}, binding {mine}")
     if path is None:
         _lib = L
     return L
@@ -170,7 +194,8 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                 wl_start_round: int = 0, wl_stop_round: int = 0, wl_active_mod: int = 1,
                 wl_read_permille: int = 0, ext_inputs: bool = False, iso_period: int = 0,
                 iso_len: int = 0, iso_mod: int = 10, rep_world: int = 0,
-                rep_rank: int = 0) -> RbeConfig:
+                rep_rank: int = 0, ext_apply: bool = False, in_cap: int = 0,
+                xfer_period: int = 0, xfer_mod: int = 1) -> RbeConfig:
     return RbeConfig(abi_version=RBE_ABI_VERSION, device=device, n_groups=n_groups,
                      n_replicas=n_replicas, election_rtt=election_rtt,
                      heartbeat_rtt=heartbeat_rtt, check_quorum=int(check_quorum),
@@ -181,7 +206,27 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                      wl_stop_round=wl_stop_round, wl_active_mod=wl_active_mod,
                      wl_read_permille=wl_read_permille, ext_inputs=int(ext_inputs),
                      iso_period=iso_period, iso_len=iso_len, iso_mod=iso_mod,
-                     rep_world=rep_world, rep_rank=rep_rank)
+                     rep_world=rep_world, rep_rank=rep_rank, ext_apply=int(ext_apply),
+                     in_cap=in_cap, xfer_period=xfer_period, xfer_mod=xfer_mod)
+
+
+class InputError(EngineError):
+    """An rbe_push_* / rbe_request_* / rbe_report_* / rbe_notify_applied call
+    refused its batch (nothing of it was staged)."""
+
+    def __init__(self, rc: int, what: str):
+        super().__init__(f"{what} refused the batch (rc={rc})")
+        self.rc = rc
+
+
+def _u64s(v):
+    n = len(v)
+    return (C.c_uint64 * max(1, n))(*v)
+
+
+def _check_input(rc: int, what: str):
+    if rc != 0:
+        raise InputError(rc, what)
 
 
 class SnapshotError(EngineError):
@@ -195,8 +240,61 @@ def _check(rc: int, what: str):
         raise EngineError(f"{what} failed with rc={rc}")
 
 
-class Engine:
+class NodeInputs:
+    """The node-layer input calls (include/rbe.h rbe_push_proposals ...
+    rbe_notify_applied), marshalled once for the HIP engine and for the
+    test-only host build; a subclass supplies `_input(name, *args)`."""
+
+    # node-layer inputs for the next step (rbe.h; each call is all-or-nothing)
+    def push_proposals(self, replicas, batches):
+        """Peer.ProposeEntries: batches[i] is a list of Cmd byte strings (or
+        (entry_type, Cmd) pairs) proposed at replicas[i]."""
+        n = len(replicas)
+        counts, types, lens, blob = [], [], [], bytearray()
+        for b in batches:
+            counts.append(len(b))
+            for e in b:
+                t, c = (e if isinstance(e, tuple) else (0, e))
+                types.append(t)
+                lens.append(len(c))
+                blob += c
+        u32a = lambda v: (C.c_uint32 * max(1, len(v)))(*v)  # noqa: E731
+        buf = (C.c_uint8 * max(1, len(blob))).from_buffer_copy(bytes(blob) or b"\0")
+        _check_input(self._input("push_proposals", n, _u64s(replicas), u32a(counts),
+                                                 u32a(types), u32a(lens), buf),
+                     "rbe_push_proposals")
+
+    def push_read_index(self, replicas, ctxs):
+        lo = [c[0] for c in ctxs]
+        hi = [c[1] for c in ctxs]
+        _check_input(self._input("push_read_index", len(replicas), _u64s(replicas),
+                                                  _u64s(lo), _u64s(hi)), "rbe_push_read_index")
+
+    def request_leader_transfer(self, replicas, targets):
+        _check_input(self._input("request_leader_transfer", len(replicas), _u64s(replicas),
+                                                          _u64s(targets)),
+                     "rbe_request_leader_transfer")
+
+    def report_unreachable(self, replicas, nodes):
+        _check_input(self._input("report_unreachable", len(replicas), _u64s(replicas),
+                                                     _u64s(nodes)), "rbe_report_unreachable")
+
+    def report_snapshot_status(self, replicas, nodes, rejects):
+        rej = (C.c_uint8 * max(1, len(rejects)))(*[1 if x else 0 for x in rejects])
+        _check_input(self._input("report_snapshot_status", len(replicas), _u64s(replicas),
+                                                         _u64s(nodes), rej),
+                     "rbe_report_snapshot_status")
+
+    def notify_applied(self, replicas, applied):
+        _check_input(self._input("notify_applied", len(replicas), _u64s(replicas),
+                                                 _u64s(applied)), "rbe_notify_applied")
+
+
+class Engine(NodeInputs):
     """One batched Raft step engine on one GPU (one rbe_engine handle)."""
+
+    def _input(self, name, *args):
+        return getattr(self.lib, "rbe_" + name)(self.h, *args)
 
     def __init__(self, cfg: Optional[RbeConfig] = None, **kw):
         self.lib = load_library()
@@ -223,8 +321,11 @@ class Engine:
         self.close()
 
     # rounds
-    def step(self):
-        _check(self.lib.rbe_step(self.h), "rbe_step")
+    def step(self, tick: bool = True):
+        if tick:
+            _check(self.lib.rbe_step(self.h), "rbe_step")
+        else:
+            _check(self.lib.rbe_step_ex(self.h, RBE_STEP_NO_TICK), "rbe_step_ex")
 
     def run(self, rounds: int):
         _check(self.lib.rbe_run(self.h, rounds), "rbe_run")
@@ -268,27 +369,6 @@ class Engine:
         rc = self.lib.rbe_import_groups(self.h, snap, len(snap), 1 if resume else 0)
         if rc != 0:
             raise SnapshotError(rc, "rbe_import_groups")
-
-    # inputs
-    def push_proposals(self, replicas, cmds: List[bytes]):
-        n = len(replicas)
-        rep = (C.c_uint64 * n)(*replicas)
-        buf = (C.c_uint8 * (16 * n))()
-        lens = (C.c_uint32 * n)()
-        for i, c in enumerate(cmds):
-            if len(c) > 16:  # the C side rejects it too (RBE_E_INVALID); never truncate
-                raise ValueError(f"proposal {i} is {len(c)} bytes; inline commands are <= 16")
-            for j, b in enumerate(c):
-                buf[16 * i + j] = b
-            lens[i] = min(16, len(c))
-        _check(self.lib.rbe_push_proposals(self.h, n, rep, buf, lens), "rbe_push_proposals")
-
-    def push_read_index(self, replicas, ctxs):
-        n = len(replicas)
-        rep = (C.c_uint64 * n)(*replicas)
-        lo = (C.c_uint64 * n)(*[c[0] for c in ctxs])
-        hi = (C.c_uint64 * n)(*[c[1] for c in ctxs])
-        _check(self.lib.rbe_push_read_index(self.h, n, rep, lo, hi), "rbe_push_read_index")
 
     # outputs
     def counters(self) -> Dict[str, int]:

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RBE_ABI_VERSION 1
+#define RBE_ABI_VERSION 2
 
 /* error codes */
 #define RBE_OK 0
@@ -121,7 +121,19 @@ typedef struct rbe_config {
    * cross-GPU messages between rounds (rbe_xchg_*); 0/1 = off */
   uint32_t rep_world;
   uint32_t rep_rank;
-  uint32_t reserved[5];
+  /* host-driven node layer */
+  uint32_t ext_apply;        /* raft.applied comes from rbe_notify_applied (peer.go:312);
+                                0 = the step's committed entries count as applied */
+  uint32_t in_cap;           /* proposal entries rbe_push_proposals may stage per step,
+                                0 = max(1024, n_groups) */
+  /* leader-transfer schedule (RequestLeaderTransfer on a seeded replica every
+   * xfer_period rounds in groups selected 1 in xfer_mod), 0 = off */
+  uint32_t xfer_period;
+  uint32_t xfer_mod;
+  uint32_t snapshot_entries;     /* reserved: config.SnapshotEntries, must be 0 */
+  uint32_t compaction_overhead;  /* reserved: config.CompactionOverhead, must be 0 */
+  uint64_t heap_bytes;           /* reserved: payload heap for Cmd > 16 B, must be 0 */
+  uint32_t reserved[4];
 } rbe_config;
 
 /* Snapshot of one replica (tests, debugging, rbe_get_views). */
@@ -132,6 +144,8 @@ typedef struct rbe_replica_view {
   uint32_t raft_quiesce, rq_count, votes_resp, votes_granted;
   uint64_t match[8], next[8];
   uint32_t rstate[8], ractive[8];
+  uint32_t events;  /* RBE_EV_* of the last round's step (0 when it made no step) */
+  uint32_t pad;
 } rbe_replica_view;
 
 /* Per-replica step result: the Update of peer.go:201-207 / raftpb Update
@@ -145,9 +159,23 @@ typedef struct rbe_update {
   uint32_t n_messages, n_ready_to_read, n_dropped_entries, n_dropped_read_indexes;
   uint32_t fault, flags;
   uint32_t role, leader_id;
+  uint32_t events, reserved; /* RBE_EV_* of the step */
 } rbe_update;
 #define RBE_UF_STATE_CHANGED 1u
 #define RBE_UF_SENT_QUIESCE 2u
+#define RBE_UF_FAST_APPLY 8u      /* Update.FastApply (peer.go:209-226 setFastApply) */
+#define RBE_UF_HAS_UPDATE 16u     /* the step produced an Update (Peer.HasUpdate, peer.go:253-280) */
+
+/* server.IRaftEventListener calls of a step (internal/server/event.go;
+ * raft.go:354, 1090, 1333, 1368, 1503, 1995, 2010), one bit per kind.
+ * RBE_EV_LEADER_UPDATED marks a step whose leader value changed. */
+#define RBE_EV_LEADER_UPDATED 1u
+#define RBE_EV_CAMPAIGN_LAUNCHED 2u
+#define RBE_EV_CAMPAIGN_SKIPPED 4u
+#define RBE_EV_SNAPSHOT_REJECTED 8u
+#define RBE_EV_REPLICATION_REJECTED 16u
+#define RBE_EV_PROPOSAL_DROPPED 32u
+#define RBE_EV_READ_INDEX_DROPPED 64u
 
 /* raftpb Message (raft.pb.go:1019-1033) as emitted by the engine. */
 typedef struct rbe_message {
@@ -175,6 +203,10 @@ typedef struct rbe_engine rbe_engine;
 int rbe_create(const rbe_config* cfg, rbe_engine** out);
 int rbe_destroy(rbe_engine* e);
 int rbe_abi_version(void);
+/* sizeof the ABI structs, in this order: rbe_config, rbe_replica_view,
+ * rbe_update, rbe_message, rbe_entry, rbe_ready_to_read (a binding checks its
+ * mirrors of them against these); returns how many were written */
+int rbe_abi_sizes(uint64_t* out, uint32_t cap);
 
 /* One lockstep round for every replica: the stepNode/handleEvents/getUpdate/
  * Commit sequence of node.go:1016-1067, 907-994 driven by execEngine.execNodes
@@ -182,6 +214,12 @@ int rbe_abi_version(void);
  * (DESIGN.md §Round semantics).  rbe_run runs `rounds` rounds back to back
  * (HIP-graph replay when the configuration allows). */
 int rbe_step(rbe_engine* e);
+/* rbe_step with options: RBE_STEP_NO_TICK steps without the round's tick
+ * (the host steps faster than its RTT tick, nodehost.go:1668-1684); a replica
+ * with no message, client input or entry to apply then makes no step at all,
+ * as handleEvents finds no event (node.go:1030-1067). */
+#define RBE_STEP_NO_TICK 1u
+int rbe_step_ex(rbe_engine* e, uint32_t flags);
 int rbe_run(rbe_engine* e, uint32_t rounds);
 int rbe_sync(rbe_engine* e);
 int rbe_round(const rbe_engine* e, uint32_t* round);
@@ -205,13 +243,41 @@ int rbe_kernel_name(const rbe_engine* e, int32_t slot, char* buf, uint32_t cap);
  * kernel's total elapsed time. */
 int rbe_profile_rounds(rbe_engine* e, uint32_t rounds, float* ms_per_kernel);
 
-/* Client input for the next round.  Replaces Peer.ProposeEntries (peer.go:117)
- * and Peer.ReadIndex (peer.go:297); requires cfg.ext_inputs.  replica =
- * g * n_replicas + (node_id - 1). */
+/* Host input for the next step (requires cfg.ext_inputs), the node-side events
+ * of handleEvents (node.go:1030-1067).  replica = g * n_replicas + (node_id - 1).
+ * Each call checks its whole batch before staging any of it (RBE_E_INVALID on a
+ * bad replica/argument, nothing staged); staged input is uploaded by the next
+ * rbe_step in one copy.  A replica takes one proposal batch, one ReadIndex and
+ * one leader transfer per step, as the node batches them; a second one for the
+ * same replica, within a batch or across calls, is RBE_E_STATE (nothing staged).
+ *   rbe_push_proposals: Peer.ProposeEntries (peer.go:117-123); batch i holds
+ *     n_ents[i] entries for replica[i]; the entries' types, Cmd lengths and Cmd
+ *     bytes (concatenated in order) follow in type[], cmd_len[], cmd.  Cmd is at
+ *     most 16 bytes.  RBE_E_NOMEM when the step's cfg.in_cap entries are used up.
+ *   rbe_push_read_index: Peer.ReadIndex (peer.go:297-303), ctx_low != 0
+ *     (requests.go:726).
+ *   rbe_request_leader_transfer: Peer.RequestLeaderTransfer (peer.go:106-113),
+ *     target in 1..n_replicas.
+ *   rbe_report_unreachable: Peer.ReportUnreachableNode (peer.go:168-174).
+ *   rbe_report_snapshot_status: Peer.ReportSnapshotStatus (peer.go:177-184).
+ *     Unreachable / SnapshotStatus reports are delivered before the step's
+ *     network messages (node.go:1207-1220 handles them in the inbox).
+ *   rbe_notify_applied: Peer.NotifyRaftLastApplied (peer.go:312-315): the
+ *     applied index the state machine confirmed, raft.applied, which gates
+ *     campaigns (hasConfigChangeToApply, raft.go:1460-1472); needs cfg.ext_apply. */
 int rbe_push_proposals(rbe_engine* e, uint64_t n, const uint64_t* replica,
-                       const uint8_t* cmd16, const uint32_t* cmd_len);
+                       const uint32_t* n_ents, const uint32_t* type, const uint32_t* cmd_len,
+                       const uint8_t* cmd);
 int rbe_push_read_index(rbe_engine* e, uint64_t n, const uint64_t* replica,
                         const uint64_t* ctx_low, const uint64_t* ctx_high);
+int rbe_request_leader_transfer(rbe_engine* e, uint64_t n, const uint64_t* replica,
+                                const uint64_t* target);
+int rbe_report_unreachable(rbe_engine* e, uint64_t n, const uint64_t* replica,
+                           const uint64_t* node_id);
+int rbe_report_snapshot_status(rbe_engine* e, uint64_t n, const uint64_t* replica,
+                               const uint64_t* node_id, const uint8_t* reject);
+int rbe_notify_applied(rbe_engine* e, uint64_t n, const uint64_t* replica,
+                       const uint64_t* applied);
 
 /* Results of the last round.  Replaces Peer.GetUpdate (peer.go:201-207);
  * Peer.Commit (peer.go:282-293) is implicit (the harness persists and

@@ -31,6 +31,20 @@ int wl_input(const HarnessConfig& c, u64 cid, u32 round) {
   return u < c.wl_read_permille ? 2 : 1;
 }
 
+// leader-transfer schedule: at every xfer_period-th round, in groups selected
+// by hash, one seeded replica (any role) gets RequestLeaderTransfer(target)
+// (node.go:1069-1075 handleLeaderTransferRequest → peer.go:106-113).
+u64 xfer_input(const HarnessConfig& c, u64 cid, u32 round, u32 k) {
+  if (!c.xfer_period || round == 0 || round % c.xfer_period != 0) return 0;
+  const u64 epoch = round / c.xfer_period;
+  if (c.xfer_mod > 1 &&
+      below(splitmix64(c.seed ^ (cid * 0xA24BAED4963EE407ULL) ^ (epoch << 36)), c.xfer_mod) != 0)
+    return 0;
+  const u64 h = splitmix64(c.seed ^ (cid * 0x9FB21C651E98DF25ULL) ^ (epoch << 12) ^ 0x5851F42DULL);
+  if (below(h, c.n_replicas) != k) return 0;
+  return below(splitmix64(h), c.n_replicas) + 1;
+}
+
 bool iso_selected(const HarnessConfig& c, u64 cid, u32 epoch) {
   if (c.iso_mod <= 1) return true;
   return below(splitmix64(c.seed ^ (cid * 0x94D049BB133111EBULL) ^ ((u64)epoch << 40)),
@@ -46,6 +60,14 @@ struct Node {
   u64 smAppliedIndex = 0;
   u64 tickCount = 0;
   u64 digest = 0;
+  u32 events = 0;               // EV_* bits of the last step
+  // host inputs staged for the next step (harness_push)
+  bool x_prop = false, x_read = false;
+  std::vector<Entry> x_ents;
+  SystemCtx x_ctx;
+  u64 x_xfer = 0;
+  u32 x_unreach = 0, x_snap = 0, x_snap_reject = 0;
+  u64 x_applied = 0;
   std::vector<Message> in[8];   // this round's inbox, per sender slot (stream order)
   std::vector<Message> nxt[8];  // next round's inbox
   ~Node() { delete peer; }
@@ -148,27 +170,66 @@ Harness* harness_create(const HarnessConfig& cfg) {
 void harness_destroy(Harness* h) { delete h; }
 
 // One stepNode + update processing for replica k of group gr in round r.
-static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, u64* ctr) {
+// EV_* bits (dragonboat_amd/csrc/rbe_types.h) from the listener calls a step made
+static u32 event_bits(const Events& a, const Events& b, u64 leader0, u64 leader1) {
+  u32 e = 0;
+  if (leader1 != leader0) e |= 1;
+  if (b.campaignLaunched != a.campaignLaunched) e |= 2;
+  if (b.campaignSkipped != a.campaignSkipped) e |= 4;
+  if (b.snapshotRejected != a.snapshotRejected) e |= 8;
+  if (b.replicationRejected != a.replicationRejected) e |= 16;
+  if (b.proposalDropped != a.proposalDropped) e |= 32;
+  if (b.readIndexDropped != a.readIndexDropped) e |= 64;
+  return e;
+}
+
+static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool tick, u64* ctr) {
   Node* nd = gr->nodes[k];
   Peer* p = nd->peer;
   Raft* R = p->raft;
   const u32 n = cfg.n_replicas;
+  nd->events = 0;
+  // client input of this round: the workload goes to replicas that lead at
+  // round start, host input (harness_push) to the replica it names
+  const int wl = R->state == Leader ? wl_input(cfg, gr->cid, r) : 0;
+  const bool do_read = wl == 2 || nd->x_read;
+  const bool do_prop = wl == 1 || nd->x_prop;
+  u64 xfer = nd->x_xfer ? nd->x_xfer : xfer_input(cfg, gr->cid, r, k);
+  // updateBatchedLastApplied (node.go:1010-1014): with ext_apply the state
+  // machine's applied index is the host's, else the harness applies each
+  // step's committed entries at once
+  if (cfg.ext_apply) nd->smAppliedIndex = nd->x_applied;
+  const u64 applied = nd->smAppliedIndex;
+  if (!tick) {
+    // a round without a tick is a step only if handleEvents finds an event
+    // (node.go:1030-1067)
+    bool ev = do_read || do_prop || xfer || nd->x_unreach || nd->x_snap ||
+              p->HasEntryToApply() || applied != nd->confirmedIndex;
+    for (u32 s = 0; s < n; s++) ev = ev || !nd->in[s].empty();
+    if (!ev) return;
+  }
   ctr[HC_STEPS]++;
+  const Events ev0 = R->events;
+  const u64 leader0 = R->leaderID;
   // handleEvents: updateBatchedLastApplied (node.go:1002-1006, 1032)
-  p->NotifyRaftLastApplied(nd->smAppliedIndex);
-  // client input of this round goes to replicas that lead at round start
-  int inp = R->state == Leader ? wl_input(cfg, gr->cid, r) : 0;
+  p->NotifyRaftLastApplied(applied);
   const u64 committed0 = R->log.committed;
   const u64 campaigns0 = R->events.campaignLaunched;
   // handleReadIndexRequests (node.go:1108-1118)
   u64 readReq = 0;
-  if (inp == 2) {
+  if (do_read) {
     nd->q.recordActivity(ReadIndex);
     readReq = 1;
     ctr[HC_READS]++;
   }
-  // handleReceivedMessages (node.go:1171-1205); one LocalTick per round
-  u64 ltCount = 1;
+  // host-reported Unreachable / SnapshotStatus: node-handled messages of the
+  // inbox (node.go:1207-1220), delivered first, no activity recorded
+  for (u32 s = 0; s < n; s++)
+    if ((nd->x_unreach >> s) & 1u) p->ReportUnreachableNode(s + 1);
+  for (u32 s = 0; s < n; s++)
+    if ((nd->x_snap >> s) & 1u) p->ReportSnapshotStatus(s + 1, ((nd->x_snap_reject >> s) & 1u) != 0);
+  // handleReceivedMessages (node.go:1171-1205); one LocalTick per ticking round
+  u64 ltCount = tick ? 1 : 0;
   for (u32 s = 0; s < n; s++) {
     for (auto& m : nd->in[s]) {
       ctr[HC_MSG_IN]++;
@@ -188,8 +249,12 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, u64*
   }
   if (readReq > 0) {  // batchedReadIndex, node.go:1379-1382
     SystemCtx ctx;
-    ctx.low = ((u64)(r + 1) << 32) | (u64)(k + 1);
-    ctx.high = gr->cid + 1;
+    if (nd->x_read) {
+      ctx = nd->x_ctx;
+    } else {
+      ctx.low = ((u64)(r + 1) << 32) | (u64)(k + 1);
+      ctx.high = gr->cid + 1;
+    }
     p->ReadIndex(ctx);
   }
   // handleLocalTickMessage (node.go:1152-1159) → node.tick (1384-1399)
@@ -206,13 +271,23 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, u64*
     }
   }
   // handleProposals (node.go:1091-1106)
-  if (inp == 1) {
-    std::vector<Entry> ents(1);
-    ents[0].type = ApplicationEntry;
-    ents[0].cmd = payload_cmd(cfg.seed, gr->cid, r);
-    p->ProposeEntries(ents);
+  if (do_prop) {
+    if (nd->x_prop) {
+      p->ProposeEntries(nd->x_ents);
+    } else {
+      std::vector<Entry> ents(1);
+      ents[0].type = ApplicationEntry;
+      ents[0].cmd = payload_cmd(cfg.seed, gr->cid, r);
+      p->ProposeEntries(ents);
+    }
     ctr[HC_PROPOSALS]++;
   }
+  // handleLeaderTransferRequest (node.go:1069-1075)
+  if (xfer) p->RequestLeaderTransfer(xfer);
+  nd->x_prop = nd->x_read = false;
+  nd->x_ents.clear();
+  nd->x_xfer = 0;
+  nd->x_unreach = nd->x_snap = nd->x_snap_reject = 0;
   // stepNode: quiesce state (node.go:1021-1023)
   const bool sendQ = nd->q.newQuiesceState();
   // getUpdate (node.go:907-923)
@@ -249,7 +324,8 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, u64*
     // applyRaftUpdates: the harness state machine applies immediately
     for (auto& e : ud.committed_entries) applyHash = hash_entry(applyHash, e);
     ctr[HC_ENT_APPLIED] += ud.committed_entries.size();
-    if (!ud.committed_entries.empty()) nd->smAppliedIndex = ud.committed_entries.back().index;
+    if (!ud.committed_entries.empty() && !cfg.ext_apply)
+      nd->smAppliedIndex = ud.committed_entries.back().index;
     // sendReplicateMessages (node.go:897-905) then, after persistence,
     // sendMessages (node.go:888-895)
     for (auto& m : ud.messages)
@@ -277,6 +353,7 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, u64*
     p->Commit(ud);  // commitRaftUpdate
   }
   ctr[HC_CAMPAIGNS] += R->events.campaignLaunched - campaigns0;
+  nd->events = event_bits(ev0, R->events, leader0, R->leaderID);
   if (R->state == Leader) {
     ctr[HC_COMMITTED] += R->log.committed - committed0;
     ctr[HC_LEADER_STEPS]++;
@@ -303,7 +380,7 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, u64*
   }
 }
 
-static void run_group_round(const HarnessConfig& cfg, Group* gr, u32 r, u64* ctr) {
+static void run_group_round(const HarnessConfig& cfg, Group* gr, u32 r, bool tick, u64* ctr) {
   // fault schedule: isolation decided from round-start roles
   if (gr->iso_mask && r >= gr->iso_until) gr->iso_mask = 0;
   if (cfg.iso_period && r > 0 && r % cfg.iso_period == 0 &&
@@ -316,7 +393,7 @@ static void run_group_round(const HarnessConfig& cfg, Group* gr, u32 r, u64* ctr
       gr->iso_until = r + cfg.iso_len;
     }
   }
-  for (u32 k = 0; k < cfg.n_replicas; k++) step_replica(cfg, gr, k, r, ctr);
+  for (u32 k = 0; k < cfg.n_replicas; k++) step_replica(cfg, gr, k, r, tick, ctr);
   for (u32 k = 0; k < cfg.n_replicas; k++) {
     Node* nd = gr->nodes[k];
     for (u32 s = 0; s < cfg.n_replicas; s++) {
@@ -326,14 +403,14 @@ static void run_group_round(const HarnessConfig& cfg, Group* gr, u32 r, u64* ctr
   }
 }
 
-void harness_run(Harness* h, u32 rounds) {
+static void run_rounds(Harness* h, u32 rounds, bool tick) {
   const u32 T = std::max<u32>(1, h->cfg.threads);
   const u32 r0 = h->round;
   std::vector<std::vector<u64>> ctrs(T, std::vector<u64>(HC_NUM, 0));
   auto worker = [&](u32 t) {
     for (u32 r = r0; r < r0 + rounds; r++)
       for (u64 g = t; g < h->groups.size(); g += T)
-        run_group_round(h->cfg, h->groups[g], r, ctrs[t].data());
+        run_group_round(h->cfg, h->groups[g], r, tick, ctrs[t].data());
   };
   if (T == 1) {
     worker(0);
@@ -355,6 +432,35 @@ void harness_run(Harness* h, u32 rounds) {
   for (u32 t = 0; t < T; t++)
     for (int i = 0; i < HC_NUM; i++) h->counters[i] += ctrs[t][i];
   h->round += rounds;
+}
+
+void harness_run(Harness* h, u32 rounds) { run_rounds(h, rounds, true); }
+void harness_step(Harness* h, bool tick) { run_rounds(h, 1, tick); }
+
+int harness_push(Harness* h, int kind, u64 replica, u64 a, u64 b, const Entry* ents, u32 n) {
+  const u32 N = h->cfg.n_replicas;
+  if (replica >= h->groups.size() * N) return -1;
+  Node* nd = h->groups[replica / N]->nodes[replica % N];
+  switch (kind) {
+    case PUSH_PROPOSE:
+      nd->x_prop = true;
+      nd->x_ents.assign(ents, ents + n);
+      return 0;
+    case PUSH_READ:
+      nd->x_read = true;
+      nd->x_ctx.low = a;
+      nd->x_ctx.high = b;
+      return 0;
+    case PUSH_XFER: nd->x_xfer = a; return 0;
+    case PUSH_UNREACH: nd->x_unreach |= 1u << (a - 1); return 0;
+    case PUSH_SNAPST:
+      nd->x_snap |= 1u << (a - 1);
+      if (b) nd->x_snap_reject |= 1u << (a - 1);
+      else nd->x_snap_reject &= ~(1u << (a - 1));
+      return 0;
+    case PUSH_APPLIED: nd->x_applied = a; return 0;
+    default: return -1;
+  }
 }
 
 u32 harness_round(const Harness* h) { return h->round; }
@@ -394,6 +500,7 @@ void harness_views(const Harness* h, ReplicaView* out) {
       }
       v.votes_resp = resp;
       v.votes_granted = granted;
+      v.events = nd->events;
       if (R->state == Leader) {
         for (auto& kv : R->remotes) {
           if (kv.first >= 1 && kv.first <= 8) {

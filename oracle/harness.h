@@ -62,7 +62,16 @@ struct HarnessConfig {
   // tracing
   u32 trace = 1;               // compute per-replica digests
   u32 threads = 1;             // worker threads (groups partitioned cid % T)
+  // leader-transfer schedule: RequestLeaderTransfer on a seeded replica
+  u32 xfer_period = 0;         // 0 = off
+  u32 xfer_mod = 1;
+  // host-driven mode: raft.applied comes from harness_push(PUSH_APPLIED)
+  u32 ext_apply = 0;
 };
+
+// host inputs for the next round (the engine's rbe_push_* / rbe_notify_applied)
+enum HarnessPush { PUSH_PROPOSE = 1, PUSH_READ = 2, PUSH_XFER = 3, PUSH_UNREACH = 4,
+                   PUSH_SNAPST = 5, PUSH_APPLIED = 6 };
 
 struct ReplicaView {  // mirrors rbe_replica_view in include/rbe.h
   u64 term, vote, leader_id, committed, last_index, processed, saved_to, digest;
@@ -71,6 +80,7 @@ struct ReplicaView {  // mirrors rbe_replica_view in include/rbe.h
   u32 raft_quiesce, rq_count, votes_resp, votes_granted;
   u64 match[8], next[8];
   u32 rstate[8], ractive[8];
+  u32 events, pad;  // EV_* bits of the last round's step (rbe_types.h)
 };
 
 // ------------------------------------------------------------ quiesce.go
@@ -133,6 +143,10 @@ struct Harness;
 Harness* harness_create(const HarnessConfig& cfg);
 void harness_destroy(Harness* h);
 void harness_run(Harness* h, u32 rounds);
+// one round; tick = false steps without the tick (rbe_step_ex RBE_STEP_NO_TICK)
+void harness_step(Harness* h, bool tick);
+// stage host input for replica g*n+k for the next round; returns 0
+int harness_push(Harness* h, int kind, u64 replica, u64 a, u64 b, const Entry* ents, u32 n);
 u32 harness_round(const Harness* h);
 void harness_views(const Harness* h, ReplicaView* out);  // n_groups*n_replicas views
 void harness_counters(const Harness* h, u64* out);       // HC_NUM counters
@@ -143,6 +157,7 @@ u64 wl_payload_lo(u64 seed, u64 cid, u64 round);
 bool wl_group_active(const HarnessConfig& c, u64 cid);
 int wl_input(const HarnessConfig& c, u64 cid, u32 round);  // 0 none, 1 propose, 2 read
 bool iso_selected(const HarnessConfig& c, u64 cid, u32 epoch);
+u64 xfer_input(const HarnessConfig& c, u64 cid, u32 round, u32 k);  // 0 = none
 inline u64 hfold(u64 h, u64 x) { return splitmix64(h ^ x); }
 
 }  // namespace orc

@@ -77,7 +77,8 @@ class OrcHarnessConfig(C.Structure):
                 ("wl_active_mod", C.c_uint32), ("wl_read_permille", C.c_uint32),
                 ("iso_period", C.c_uint32), ("iso_len", C.c_uint32), ("iso_mod", C.c_uint32),
                 ("trace", C.c_uint32), ("threads", C.c_uint32), ("pad", C.c_uint32),
-                ("cid_stride", C.c_uint64)]
+                ("cid_stride", C.c_uint64), ("xfer_period", C.c_uint32),
+                ("xfer_mod", C.c_uint32), ("ext_apply", C.c_uint32), ("pad2", C.c_uint32)]
 
 
 class ReplicaView(C.Structure):
@@ -92,10 +93,13 @@ class ReplicaView(C.Structure):
                 ("raft_quiesce", C.c_uint32), ("rq_count", C.c_uint32),
                 ("votes_resp", C.c_uint32), ("votes_granted", C.c_uint32),
                 ("match", C.c_uint64 * 8), ("next", C.c_uint64 * 8),
-                ("rstate", C.c_uint32 * 8), ("ractive", C.c_uint32 * 8)]
+                ("rstate", C.c_uint32 * 8), ("ractive", C.c_uint32 * 8),
+                ("events", C.c_uint32), ("pad", C.c_uint32)]
 
 
-VIEW_FIELDS = [f[0] for f in ReplicaView._fields_]
+VIEW_FIELDS = [f[0] for f in ReplicaView._fields_ if f[0] != "pad"]
+# harness_push kinds (oracle/harness.h HarnessPush)
+PUSH_PROPOSE, PUSH_READ, PUSH_XFER, PUSH_UNREACH, PUSH_SNAPST, PUSH_APPLIED = range(1, 7)
 
 _lib = None
 
@@ -171,6 +175,8 @@ def lib():
             "orc_harness_create": (vp, [P(OrcHarnessConfig)]),
             "orc_harness_destroy": (None, [vp]),
             "orc_harness_run": (i32, [vp, u32]),
+            "orc_harness_step": (i32, [vp, i32]),
+            "orc_harness_push": (i32, [vp, i32, u64, u64, u64, P(OrcEntry), i32]),
             "orc_harness_round": (u32, [vp]),
             "orc_harness_views": (None, [vp, vp]),
             "orc_harness_counters": (None, [vp, P(u64)]),
@@ -878,7 +884,8 @@ class Harness:
                  check_quorum=False, quiesce=False, seed=0x5EEDD8A6, max_entry_size=0,
                  wl_enabled=False, wl_start_round=0, wl_stop_round=0, wl_active_mod=1,
                  wl_read_permille=0, iso_period=0, iso_len=0, iso_mod=10, trace=True,
-                 threads=1, cid_stride=1):
+                 threads=1, cid_stride=1, xfer_period=0, xfer_mod=1, ext_apply=False,
+                 ext_inputs=False):
         c = OrcHarnessConfig(
             n_groups=n_groups, n_replicas=n_replicas, check_quorum=int(check_quorum),
             cid_base=cid_base, election_rtt=election_rtt, heartbeat_rtt=heartbeat_rtt,
@@ -886,7 +893,8 @@ class Harness:
             wl_enabled=int(wl_enabled), wl_start_round=wl_start_round,
             wl_stop_round=wl_stop_round, wl_active_mod=wl_active_mod,
             wl_read_permille=wl_read_permille, iso_period=iso_period, iso_len=iso_len,
-            iso_mod=iso_mod, trace=int(trace), threads=threads, cid_stride=cid_stride)
+            iso_mod=iso_mod, trace=int(trace), threads=threads, cid_stride=cid_stride,
+            xfer_period=xfer_period, xfer_mod=xfer_mod, ext_apply=int(ext_apply))
         self.n_groups, self.n_replicas = n_groups, n_replicas
         self.h = lib().orc_harness_create(C.byref(c))
         if not self.h:
@@ -899,6 +907,17 @@ class Harness:
 
     def run(self, rounds=1):
         if lib().orc_harness_run(self.h, rounds) != 0:
+            raise _err()
+
+    def step(self, tick=True):
+        """One round; tick=False is rbe_step_ex(RBE_STEP_NO_TICK)."""
+        if lib().orc_harness_step(self.h, int(tick)) != 0:
+            raise _err()
+
+    def push(self, kind, replica, a=0, b=0, entries=()):
+        """Stage host input for the next round (the engine's rbe_push_* calls)."""
+        arr = entries_array(list(entries))
+        if lib().orc_harness_push(self.h, kind, replica, a, b, arr, len(entries)) != 0:
             raise _err()
 
     @property

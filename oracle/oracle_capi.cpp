@@ -45,6 +45,7 @@ typedef struct {
   uint32_t wl_active_mod, wl_read_permille, iso_period, iso_len;
   uint32_t iso_mod, trace, threads, pad;
   uint64_t cid_stride;
+  uint32_t xfer_period, xfer_mod, ext_apply, pad2;
 } orc_harness_config;
 
 static thread_local std::string g_err;
@@ -816,10 +817,27 @@ void* orc_harness_create(const orc_harness_config* c) {
   h.iso_mod = c->iso_mod;
   h.trace = c->trace;
   h.threads = c->threads;
+  h.xfer_period = c->xfer_period;
+  h.xfer_mod = c->xfer_mod ? c->xfer_mod : 1;
+  h.ext_apply = c->ext_apply;
   return harness_create(h);
   GUARD_END(nullptr)
 }
 void orc_harness_destroy(void* h) { harness_destroy((Harness*)h); }
+int orc_harness_step(void* h, int tick) {
+  GUARD_BEGIN
+  harness_step((Harness*)h, tick != 0);
+  return 0;
+  GUARD_END(-1)
+}
+int orc_harness_push(void* h, int kind, uint64_t replica, uint64_t a, uint64_t b,
+                     const orc_entry* ents, int n) {
+  GUARD_BEGIN
+  std::vector<Entry> v;
+  for (int i = 0; i < n; i++) v.push_back(to_entry(ents[i]));
+  return harness_push((Harness*)h, kind, replica, a, b, v.data(), (u32)n);
+  GUARD_END(-1)
+}
 int orc_harness_run(void* h, uint32_t rounds) {
   GUARD_BEGIN
   harness_run((Harness*)h, rounds);

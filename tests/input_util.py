@@ -1,0 +1,105 @@
+"""Drive an engine (the HIP engine or the test-only host build) and the oracle
+harness with the same host input, round by round: the node-layer calls of
+handleEvents (node.go:1030-1067) — proposal batches, ReadIndex, leader
+transfer, Unreachable / SnapshotStatus reports, the state machine's applied
+index — plus rounds without a tick.  The schedule is a seeded function of the
+round and of the state both sides already agree on (processed indexes), so
+both receive identical input."""
+from __future__ import annotations
+
+import random
+
+import oracle as O
+from parity_util import counters_match, view_diff
+
+
+def _cmd(rng):
+    return bytes(rng.randrange(256) for _ in range(rng.randrange(17)))
+
+
+def plan_round(rng, n_rep, n, rnd, views, ext_apply, density=0.3, applied=None):
+    """One round of host input: a list of (kind, replica, args)."""
+    ops = []
+    for r in range(n_rep):
+        if rng.random() < density:
+            ops.append(("prop", r, [(rng.choice((0, 0, 2, 3)), _cmd(rng))
+                                    for _ in range(rng.randrange(1, 4))]))
+        if rng.random() < density:
+            ops.append(("read", r, ((rnd + 1) << 32 | (r + 1), rng.randrange(1 << 40))))
+        if rng.random() < density / 6:
+            ops.append(("xfer", r, rng.randrange(1, n + 1)))
+        if rng.random() < density / 8:
+            ops.append(("unreach", r, rng.randrange(1, n + 1)))
+        if rng.random() < density / 8:
+            ops.append(("snapst", r, (rng.randrange(1, n + 1), rng.random() < 0.5)))
+        if ext_apply:
+            # the state machine lags the entries handed to it by 0-3 entries;
+            # its applied index never moves backwards (node.go:911-913)
+            v = max(applied[r], views[r].processed - rng.randrange(4))
+            applied[r] = v
+            ops.append(("applied", r, v))
+    return ops
+
+
+def apply_engine(eng, ops):
+    by = {}
+    for kind, r, a in ops:
+        by.setdefault(kind, []).append((r, a))
+    if "prop" in by:
+        eng.push_proposals([r for r, _ in by["prop"]], [a for _, a in by["prop"]])
+    if "read" in by:
+        eng.push_read_index([r for r, _ in by["read"]], [a for _, a in by["read"]])
+    if "xfer" in by:
+        eng.request_leader_transfer([r for r, _ in by["xfer"]], [a for _, a in by["xfer"]])
+    if "unreach" in by:
+        eng.report_unreachable([r for r, _ in by["unreach"]], [a for _, a in by["unreach"]])
+    if "snapst" in by:
+        eng.report_snapshot_status([r for r, _ in by["snapst"]], [a[0] for _, a in by["snapst"]],
+                                   [a[1] for _, a in by["snapst"]])
+    if "applied" in by:
+        eng.notify_applied([r for r, _ in by["applied"]], [a for _, a in by["applied"]])
+
+
+def apply_oracle(h, ops):
+    for kind, r, a in ops:
+        if kind == "prop":
+            h.push(O.PUSH_PROPOSE, r, entries=[O.Entry(type=t, cmd=c) for t, c in a])
+        elif kind == "read":
+            h.push(O.PUSH_READ, r, a[0], a[1])
+        elif kind == "xfer":
+            h.push(O.PUSH_XFER, r, a)
+        elif kind == "unreach":
+            h.push(O.PUSH_UNREACH, r, a)
+        elif kind == "snapst":
+            h.push(O.PUSH_SNAPST, r, a[0], int(a[1]))
+        elif kind == "applied":
+            h.push(O.PUSH_APPLIED, r, a)
+
+
+def run_driven(eng, ref, rounds, seed=1, tick_every=1, inputs=True, ext_apply=False,
+               density=0.3, skip=()):
+    """Step both `rounds` rounds with the same input; every `tick_every`-th
+    round ticks, the others are RBE_STEP_NO_TICK rounds.  Returns the first
+    divergence (round, replica, field, engine, oracle) or None."""
+    rng = random.Random(seed)
+    n = eng.cfg.n_replicas
+    n_rep = eng.n_rep
+    views = ref.views()
+    applied = [0] * n_rep
+    for rnd in range(rounds):
+        if inputs:
+            ops = plan_round(rng, n_rep, n, rnd, views, ext_apply, density, applied)
+            apply_engine(eng, ops)
+            apply_oracle(ref, ops)
+        tick = (rnd % tick_every) == 0
+        eng.step(tick=tick)
+        ref.step(tick=tick)
+        ev, views = eng.views(), ref.views()
+        for i in range(n_rep):
+            d = view_diff(ev[i], views[i], skip)
+            if d is not None:
+                return (rnd, i) + d
+    bad = counters_match(eng.counters(), ref.counters())
+    if bad:
+        return ("counters", bad)
+    return None

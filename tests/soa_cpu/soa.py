@@ -5,8 +5,8 @@ Never imported by the dragonboat_amd package; see soa_cpu.cpp.
 import ctypes as C
 import os
 
-from dragonboat_amd.engine import (CTR_NUM, COUNTER_NAMES, RbeEntry, RbeMessage, RbeReplicaView,
-                                   make_config)
+from dragonboat_amd.engine import (CTR_NUM, COUNTER_NAMES, NodeInputs, RbeEntry, RbeMessage,
+                                   RbeReplicaView, make_config)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _lib = None
@@ -48,6 +48,18 @@ def lib():
                                         C.c_uint64]
         L.soa_import_groups.restype = C.c_int
         L.soa_import_groups.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32]
+        u64p, u32p = P(C.c_uint64), P(C.c_uint32)
+        L.soa_step_ex.argtypes = [C.c_void_p, C.c_uint32]
+        for name, args in {
+                "push_proposals": [C.c_uint64, u64p, u32p, u32p, u32p, P(C.c_uint8)],
+                "push_read_index": [C.c_uint64, u64p, u64p, u64p],
+                "request_leader_transfer": [C.c_uint64, u64p, u64p],
+                "report_unreachable": [C.c_uint64, u64p, u64p],
+                "report_snapshot_status": [C.c_uint64, u64p, u64p, P(C.c_uint8)],
+                "notify_applied": [C.c_uint64, u64p, u64p]}.items():
+            fn = getattr(L, "soa_" + name)
+            fn.restype = C.c_int
+            fn.argtypes = [C.c_void_p] + args
         _lib = L
     return _lib
 
@@ -58,7 +70,10 @@ class SnapshotError(RuntimeError):
         self.rc = rc
 
 
-class SoaCpu:
+class SoaCpu(NodeInputs):
+    def _input(self, name, *args):
+        return getattr(lib(), "soa_" + name)(self.h, *args)
+
     def __init__(self, full_only=False, staged=0, **kw):
         self.cfg = make_config(**kw)
         self.n_rep = self.cfg.n_groups * self.cfg.n_replicas
@@ -79,8 +94,11 @@ class SoaCpu:
     def run(self, rounds=1):
         lib().soa_run(self.h, rounds)
 
-    def step(self):
-        lib().soa_run(self.h, 1)
+    def step(self, tick=True):
+        if tick:
+            lib().soa_run(self.h, 1)
+        else:
+            lib().soa_step_ex(self.h, 1)
 
     # replica-per-GPU exchange, same contract as Engine.xchg_pack / xchg_unpack
     def xchg_pack(self, buf_ptr, caps):

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../dragonboat_amd/csrc/rbe_fast.h"
+#include "../../dragonboat_amd/csrc/rbe_host.h"
 #include "../../dragonboat_amd/csrc/rbe_snap.h"
 #include "../../dragonboat_amd/csrc/rbe_xchg.h"
 #include "../../include/rbe.h"
@@ -20,6 +21,8 @@ struct SoaEngine {
   Planes P;
   std::vector<std::vector<uint8_t>> bufs;
   u32 round = 0;
+  u32 tclk = 0;
+  HostInputs hin;
   u64 counters[C_NUM] = {0};
   bool full_only = false;
   int staged = 0;  // STG_* bits: fast steps on a staged row (StageRow); 4: counts from inbound_aux
@@ -33,7 +36,12 @@ static T* alloc(SoaEngine* e, u64 n) {
 }
 
 template <int N>
-static void run_round(SoaEngine* e) {
+static void run_round(SoaEngine* e, bool tick = true) {
+  const Clk ck{e->round, e->tclk, tick ? 1u : 0u};
+  if (!e->hin.empty()) {  // the HIP engine uploads and scatters the same records
+    e->hin.apply_host(e->P);
+    e->hin.clear();
+  }
   if (e->C.iso_period && e->round > 0 && e->round % e->C.iso_period == 0)
     for (u64 g = 0; g < e->C.n_groups; g++) iso_group<N>(e->P, e->C, g, e->round);
   // the GPU pipeline, sequentially: triage → leader fast list → follower fast
@@ -47,13 +55,13 @@ static void run_round(SoaEngine* e) {
     if (!e->full_only) {
       const u8 ib = e->P.idle[r];
       const u32 inb = inbound_bits<N>(e->P, r, e->round);
-      if (!e->C.trace && e->C.quiesce && triage_lazy<N>(e->P, e->C, r, e->round, ib, inb & 1u, c))
+      if (!e->C.trace && e->C.quiesce && triage_lazy<N>(e->P, e->C, r, ck, ib, inb & 1u, c))
         cls = T_DONE;
       else if (inb & 2u)  // messages: the role decides the list (as triage_replica would)
         cls = class_of_role(idle_role(ib));
       else
-        cls = e->C.trace ? triage_replica<N, true>(e->P, e->C, r, e->round, c)
-                         : triage_replica<N, false>(e->P, e->C, r, e->round, c);
+        cls = e->C.trace ? triage_replica<N, true>(e->P, e->C, r, ck, c)
+                         : triage_replica<N, false>(e->P, e->C, r, ck, c);
     }
     if (cls != T_DONE) lists[cls - 1].push_back(r);
     for (int i = 0; i < C_NUM; i++) e->counters[i] += c.v[i];
@@ -69,39 +77,39 @@ static void run_round(SoaEngine* e) {
         const u32 aux = inbound_aux<N>(w, k, e->round);
         if (li == 0)
           ok = e->C.trace
-                   ? step_fast<N, true, MODE_LEAD, 0, true>(e->P, e->C, r, e->round, c, nullptr, aux)
-                   : step_fast<N, false, MODE_LEAD, 0, true>(e->P, e->C, r, e->round, c, nullptr, aux);
+                   ? step_fast<N, true, MODE_LEAD, 0, true>(e->P, e->C, r, ck, c, nullptr, aux)
+                   : step_fast<N, false, MODE_LEAD, 0, true>(e->P, e->C, r, ck, c, nullptr, aux);
         else
           ok = e->C.trace
-                   ? step_fast<N, true, MODE_FOLL, 0, true>(e->P, e->C, r, e->round, c, nullptr, aux)
-                   : step_fast<N, false, MODE_FOLL, 0, true>(e->P, e->C, r, e->round, c, nullptr, aux);
+                   ? step_fast<N, true, MODE_FOLL, 0, true>(e->P, e->C, r, ck, c, nullptr, aux)
+                   : step_fast<N, false, MODE_FOLL, 0, true>(e->P, e->C, r, ck, c, nullptr, aux);
       } else if (e->staged == (STG_OUT | STG_IN)) {
         StageRow<N> row;
         memset(&row, 0xA5, sizeof(row));  // nothing the step reads may come from here unset
         stage_row_in<N>(e->P, r, li == 0, row);
         if (li == 0)
-          ok = e->C.trace ? step_fast<N, true, MODE_LEAD, 3>(e->P, e->C, r, e->round, c, &row)
-                          : step_fast<N, false, MODE_LEAD, 3>(e->P, e->C, r, e->round, c, &row);
+          ok = e->C.trace ? step_fast<N, true, MODE_LEAD, 3>(e->P, e->C, r, ck, c, &row)
+                          : step_fast<N, false, MODE_LEAD, 3>(e->P, e->C, r, ck, c, &row);
         else
-          ok = e->C.trace ? step_fast<N, true, MODE_FOLL, 3>(e->P, e->C, r, e->round, c, &row)
-                          : step_fast<N, false, MODE_FOLL, 3>(e->P, e->C, r, e->round, c, &row);
+          ok = e->C.trace ? step_fast<N, true, MODE_FOLL, 3>(e->P, e->C, r, ck, c, &row)
+                          : step_fast<N, false, MODE_FOLL, 3>(e->P, e->C, r, ck, c, &row);
         if (ok) stage_row_out<N>(e->P, r, li == 0, row);
       } else if (e->staged == STG_OUT) {
         StageRow<N> row;
         memset(&row, 0xA5, sizeof(row));
         if (li == 0)
-          ok = e->C.trace ? step_fast<N, true, MODE_LEAD, 1>(e->P, e->C, r, e->round, c, &row)
-                          : step_fast<N, false, MODE_LEAD, 1>(e->P, e->C, r, e->round, c, &row);
+          ok = e->C.trace ? step_fast<N, true, MODE_LEAD, 1>(e->P, e->C, r, ck, c, &row)
+                          : step_fast<N, false, MODE_LEAD, 1>(e->P, e->C, r, ck, c, &row);
         else
-          ok = e->C.trace ? step_fast<N, true, MODE_FOLL, 1>(e->P, e->C, r, e->round, c, &row)
-                          : step_fast<N, false, MODE_FOLL, 1>(e->P, e->C, r, e->round, c, &row);
+          ok = e->C.trace ? step_fast<N, true, MODE_FOLL, 1>(e->P, e->C, r, ck, c, &row)
+                          : step_fast<N, false, MODE_FOLL, 1>(e->P, e->C, r, ck, c, &row);
         if (ok) stage_row_out<N>(e->P, r, li == 0, row);
       } else if (li == 0) {
-        ok = e->C.trace ? step_fast<N, true, MODE_LEAD>(e->P, e->C, r, e->round, c)
-                        : step_fast<N, false, MODE_LEAD>(e->P, e->C, r, e->round, c);
+        ok = e->C.trace ? step_fast<N, true, MODE_LEAD>(e->P, e->C, r, ck, c)
+                        : step_fast<N, false, MODE_LEAD>(e->P, e->C, r, ck, c);
       } else {
-        ok = e->C.trace ? step_fast<N, true, MODE_FOLL>(e->P, e->C, r, e->round, c)
-                        : step_fast<N, false, MODE_FOLL>(e->P, e->C, r, e->round, c);
+        ok = e->C.trace ? step_fast<N, true, MODE_FOLL>(e->P, e->C, r, ck, c)
+                        : step_fast<N, false, MODE_FOLL>(e->P, e->C, r, ck, c);
       }
       if (!ok) lists[2].push_back(r);
       for (int i = 0; i < C_NUM; i++) e->counters[i] += c.v[i];
@@ -110,12 +118,13 @@ static void run_round(SoaEngine* e) {
   std::vector<u64>& slow = lists[2];
   for (u64 r : slow) {
     memset(&c, 0, sizeof(c));
-    if (e->C.trace) step_replica<N, true>(e->P, e->C, r, e->round, c);
-    else step_replica<N, false>(e->P, e->C, r, e->round, c);
+    if (e->C.trace) step_replica<N, true>(e->P, e->C, r, ck, c);
+    else step_replica<N, false>(e->P, e->C, r, ck, c);
     for (int i = 0; i < C_NUM; i++) e->counters[i] += c.v[i];
   }
   e->slow_total += slow.size();
   e->round++;
+  if (tick) e->tclk++;
 }
 
 extern "C" {
@@ -147,7 +156,11 @@ void* soa_create(const rbe_config* cfg) {
   C.wl_stop_round = cfg->wl_stop_round;
   C.wl_active_mod = cfg->wl_active_mod;
   C.wl_read_permille = cfg->wl_read_permille;
-  C.ext_inputs = 0;
+  C.ext_inputs = cfg->ext_inputs;
+  C.ext_apply = cfg->ext_apply;
+  C.in_cap = cfg->in_cap ? cfg->in_cap : (u32)(cfg->n_groups > 1024 ? cfg->n_groups : 1024);
+  C.xfer_period = cfg->xfer_period;
+  C.xfer_mod = cfg->xfer_mod;
   C.iso_period = cfg->iso_period;
   C.iso_len = cfg->iso_len;
   C.iso_mod = cfg->iso_mod;
@@ -180,6 +193,9 @@ void* soa_create(const rbe_config* cfg) {
   P.rtr = alloc<RTR>(e, R * C.rtr_cap);
   P.dri = alloc<DropRI>(e, R * C.dri_cap);
   P.ext = alloc<ExtIn>(e, R);
+  P.in_ents = alloc<Ent>(e, C.in_cap);
+  P.applied = alloc<u64>(e, R);
+  e->hin.init(R, C.n, C.in_cap);
   P.counters = nullptr;
   for (u64 r = 0; r < R; r++) {
     if (N == 1) launch_replica<1>(P, C, r);
@@ -203,6 +219,52 @@ void soa_run(void* h, uint32_t rounds) {
   }
 }
 
+// rbe_step_ex (RBE_STEP_NO_TICK = 1)
+void soa_step_ex(void* h, uint32_t flags) {
+  SoaEngine* e = (SoaEngine*)h;
+  const bool tick = (flags & 1u) == 0;
+  if (e->C.n == 1) run_round<1>(e, tick);
+  else if (e->C.n == 3) run_round<3>(e, tick);
+  else run_round<5>(e, tick);
+}
+
+// rbe_push_* / rbe_request_leader_transfer / rbe_report_* / rbe_notify_applied
+// through the same staging code (rbe_host.h) as the HIP engine
+int soa_push_proposals(void* h, uint64_t n, const uint64_t* replica, const uint32_t* n_ents,
+                       const uint32_t* type, const uint32_t* cmd_len, const uint8_t* cmd) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (!e->C.ext_inputs) return RBE_E_STATE;
+  return e->hin.push_proposals(n, replica, n_ents, type, cmd_len, cmd);
+}
+int soa_push_read_index(void* h, uint64_t n, const uint64_t* replica, const uint64_t* lo,
+                        const uint64_t* hi) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (!e->C.ext_inputs) return RBE_E_STATE;
+  return e->hin.push_read_index(n, replica, lo, hi);
+}
+int soa_request_leader_transfer(void* h, uint64_t n, const uint64_t* replica,
+                                const uint64_t* target) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (!e->C.ext_inputs) return RBE_E_STATE;
+  return e->hin.request_leader_transfer(n, replica, target);
+}
+int soa_report_unreachable(void* h, uint64_t n, const uint64_t* replica, const uint64_t* node) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (!e->C.ext_inputs) return RBE_E_STATE;
+  return e->hin.report_unreachable(n, replica, node);
+}
+int soa_report_snapshot_status(void* h, uint64_t n, const uint64_t* replica, const uint64_t* node,
+                               const uint8_t* reject) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (!e->C.ext_inputs) return RBE_E_STATE;
+  return e->hin.report_snapshot_status(n, replica, node, reject);
+}
+int soa_notify_applied(void* h, uint64_t n, const uint64_t* replica, const uint64_t* applied) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (!e->C.ext_apply) return RBE_E_STATE;
+  return e->hin.notify_applied(n, replica, applied);
+}
+
 void soa_counters(void* h, uint64_t* out) {
   SoaEngine* e = (SoaEngine*)h;
   for (int i = 0; i < C_NUM; i++) out[i] = e->counters[i];
@@ -214,7 +276,7 @@ void soa_views(void* h, rbe_replica_view* out) {
   for (u64 i = 0; i < e->C.n_rep; i++) {
     rbe_replica_view& v = out[i];
     memset(&v, 0, sizeof(v));
-    const Hot hh = materialize_hot(e->P.hot[i], e->C, e->round);
+    const Hot hh = materialize_hot(e->P.hot[i], e->C, e->tclk);
     const Core& c = e->P.core[i];
     v.term = c.term;
     v.vote = c.vote;
@@ -236,6 +298,7 @@ void soa_views(void* h, rbe_replica_view* out) {
     v.rq_count = c.rq_count;
     v.votes_resp = hh.votes_resp;
     v.votes_granted = hh.votes_granted;
+    v.events = (e->round > 0 && e->P.upd[i].round == e->round - 1) ? e->P.upd[i].events : 0u;
     if (hh.role == R_Leader) {
       for (u32 s = 0; s < N && s < 8; s++) {
         v.match[s] = e->P.rem[i * N + s].match;
@@ -358,7 +421,7 @@ extern "C" int soa_export_groups(void* h, uint64_t first, uint64_t count, void* 
   const u64 body = snap_body_bytes(e->P, e->C, count);
   if (cap < sizeof(SnapHeader) + body) return RBE_E_NOMEM;
   SnapHeader hd;
-  snap_fill_header(e->C, RBE_ABI_VERSION, e->round, first, count, body, &hd);
+  snap_fill_header(e->C, RBE_ABI_VERSION, e->round, e->tclk, first, count, body, &hd);
   memcpy(buf, &hd, sizeof(hd));
   SnapPlane pl[kSnapPlanes];
   snap_planes(e->P, e->C, pl);
@@ -390,7 +453,11 @@ extern "C" int soa_import_groups(void* h, const void* buf, uint64_t bytes, uint3
     for (u64 row = 0; row < pl[i].rows; row++, src += w)
       memcpy(pl[i].base + row * pl[i].pitch + hd.first * pl[i].group_bytes, src, w);
   }
-  if (resume) e->round = hd.round;
+  e->hin.resync_applied(e->P.applied + hd.first * e->C.n, hd.first * e->C.n, hd.count * e->C.n);
+  if (resume) {
+    e->round = hd.round;
+    e->tclk = (u32)hd.tclk;
+  }
   return RBE_OK;
 }
 
@@ -413,7 +480,7 @@ extern "C" void* soa_quiesce_new(uint64_t election_tick, int enabled, int which)
   memset(&s->ctr, 0, sizeof(s->ctr));
   s->C.election_rtt = (u32)(election_tick / 2);  // node.go:165 electionTick = 2 x ElectionRTT
   s->C.quiesce = enabled ? 1 : 0;
-  s->lane = new Lane<3, false, MODE_FULL>(s->P, s->C, 0, 0, s->ctr);
+  s->lane = new Lane<3, false, MODE_FULL>(s->P, s->C, 0, Clk{0, 0, 1}, s->ctr);
   s->lane->q_tick = s->lane->q_qs = s->lane->q_nas = s->lane->q_eqt = 0;
   s->lane->q_new = false;
   s->fq.tick = s->fq.qs = s->fq.nas = s->fq.eqt = 0;

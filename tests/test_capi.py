@@ -71,7 +71,13 @@ def test_struct_layouts_match_header():
     assert C.sizeof(E.RbeMessage) == 8 + 9 * 8 + 8
     assert C.sizeof(E.RbeEntry) == 40
     assert C.sizeof(E.RbeReadyToRead) == 24
-    assert C.sizeof(E.RbeUpdate) == 8 * 8 + 8 * 4
+    assert C.sizeof(E.RbeUpdate) == 8 * 8 + 10 * 4
+    # and every binding struct against the library's own sizeof (rbe_abi_sizes)
+    lib = E.load_library()
+    sz = (C.c_uint64 * 6)()
+    assert lib.rbe_abi_sizes(sz, 6) == 6
+    assert list(sz) == [C.sizeof(t) for t in (E.RbeConfig, E.RbeReplicaView, E.RbeUpdate,
+                                               E.RbeMessage, E.RbeEntry, E.RbeReadyToRead)]
 
 
 def test_create_fails_loudly_without_gpu():

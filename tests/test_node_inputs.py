@@ -1,0 +1,163 @@
+"""The node-layer boundary on the CPU tier: the device step code (rbe_step.h /
+rbe_fast.h, compiled for the host in tests/soa_cpu) driven through the same
+input staging as the HIP engine (rbe_host.h), against the oracle harness, round
+by round, every replica field plus its trace digest and listener events.
+
+Covers (include/rbe.h):
+  * rbe_push_proposals (multi-entry batches, 0-16 B Cmd) / rbe_push_read_index
+    at any replica: followers forward, candidates drop (ProposalDropped /
+    ReadIndexDropped events), leaders append / queue — peer.go:117, 297;
+  * rbe_request_leader_transfer (peer.go:106): LeaderTransfer → TimeoutNow →
+    the target campaigns with the transfer hint (raft.go:1712-1734, 1906-1916);
+  * rbe_report_unreachable / rbe_report_snapshot_status (peer.go:168, 177);
+  * rbe_notify_applied with ext_apply: raft.applied lags processed, and
+    hasConfigChangeToApply (committed > applied, raft.go:1460-1472) skips
+    campaigns (CampaignSkipped);
+  * RBE_STEP_NO_TICK rounds (a replica without an event makes no step);
+  * the seeded leader-transfer schedule (xfer_period) of the harness.
+"""
+import pytest
+
+import oracle as O
+from input_util import run_driven
+from parity_util import C2, C3, C4, MIXED, run_lockstep
+from soa_cpu.soa import SoaCpu
+
+EXTRA = {"C3": dict(ring=128), "MIXED": dict(ring=128, rq_cap=64, maxm=24)}
+
+
+# Host-driven rounds put more traffic on one (sender, destination) stream than
+# the lockstep workloads (a forwarded ReadIndex each triggers a heartbeat
+# broadcast, every forwarded proposal a Replicate): the per-round message and
+# entry capacities are raised so the test exercises the protocol, not F_OUTBOX.
+DRIVEN = dict(maxm=40, ecap=64, rq_cap=32)
+
+
+def _pair(kw, name="", **more):
+    kw = dict(kw, **more)
+    eng_kw = dict(kw)
+    eng_kw.update(EXTRA.get(name, {}))
+    if kw.get("ext_inputs"):
+        eng_kw.update(DRIVEN)
+    return SoaCpu(trace=True, **eng_kw), O.Harness(**kw)
+
+
+@pytest.mark.parametrize("name,kw", [("C2", C2), ("C3", C3), ("C4", C4)])
+def test_driven_inputs_parity(name, kw):
+    kw = dict(kw, n_groups=min(kw["n_groups"], 16))
+    eng, ref = _pair(kw, name, ext_inputs=True)
+    d = run_driven(eng, ref, 160, seed=7)
+    assert d is None, f"{name}: first divergence {d}"
+    assert eng.faults()[0] == 0
+
+
+def test_driven_inputs_with_lagging_applied():
+    """ext_apply: the host reports an applied index 0-3 entries behind what it
+    was handed; an election falls due while committed > applied is skipped."""
+    kw = dict(C3, n_groups=12)
+    eng, ref = _pair(kw, "C3", ext_inputs=True, ext_apply=True)
+    d = run_driven(eng, ref, 200, seed=11, ext_apply=True)
+    assert d is None, f"first divergence {d}"
+    assert eng.faults()[0] == 0
+
+
+def test_campaign_skipped_while_applied_lags():
+    """hasConfigChangeToApply (raft.go:1460-1472): with the state machine
+    holding applied at 0, an election timeout skips the campaign and fires
+    CampaignSkipped; once applied catches up the node campaigns."""
+    kw = dict(n_groups=1, n_replicas=3)
+    eng, ref = _pair(kw, ext_inputs=True, ext_apply=True)
+    skipped = launched = 0
+    for rnd in range(40):
+        if rnd >= 25:  # the state machine catches up
+            for r in range(3):
+                v = ref.views()[r]
+                eng.notify_applied([r], [v.processed])
+                ref.push(O.PUSH_APPLIED, r, v.processed)
+        eng.step()
+        ref.step()
+        ev, rv = eng.views(), ref.views()
+        for i in range(3):
+            assert ev[i].events == rv[i].events and ev[i].term == rv[i].term, (rnd, i)
+            skipped += bool(rv[i].events & 4)
+            launched += bool(rv[i].events & 2)
+    assert skipped > 0 and launched > 0
+
+
+@pytest.mark.parametrize("tick_every", [2, 3])
+def test_rounds_without_tick(tick_every):
+    kw = dict(C4, n_groups=24)
+    eng, ref = _pair(kw, ext_inputs=True)
+    d = run_driven(eng, ref, 300, seed=3, tick_every=tick_every, density=0.05)
+    assert d is None, f"first divergence {d}"
+    # untraced: lazy quiesced ticks must count ticks, not rounds
+    eng2 = SoaCpu(trace=False, **dict(kw, ext_inputs=True))
+    ref2 = O.Harness(**dict(kw, ext_inputs=True))
+    d = run_driven(eng2, ref2, 300, seed=3, tick_every=tick_every, density=0.05,
+                   skip=("digest",))
+    assert d is None, f"untraced: first divergence {d}"
+
+
+@pytest.mark.parametrize("name,kw", [("C2", C2), ("C3", C3), ("MIXED", MIXED)])
+def test_leader_transfer_schedule_parity(name, kw):
+    """The seeded RequestLeaderTransfer schedule: transfers happen (TimeoutNow,
+    a campaign with the transfer hint, a new leader) and every replica stays
+    bit-exact with the oracle; also through the full handler table only."""
+    kw = dict(kw, xfer_period=23, xfer_mod=2)
+    eng, ref = _pair(kw, name)
+    d = run_lockstep(eng, ref, 400, every=1)
+    assert d is None, f"{name}: first divergence {d}"
+    assert eng.faults()[0] == 0
+    c = ref.counters()
+    assert c["campaigns"] > kw["n_groups"], "the transfers never started a campaign"
+    full, ref2 = SoaCpu(trace=True, full_only=True, **dict(kw, **EXTRA.get(name, {}))), O.Harness(**kw)
+    d = run_lockstep(full, ref2, 200, every=1)
+    assert d is None, f"{name} (full table only): first divergence {d}"
+
+
+def test_transfer_moves_leadership():
+    """RequestLeaderTransfer at the leader: the target becomes leader of the
+    next term (raft.go:1712-1734 → TimeoutNow → handleFollowerTimeoutNow)."""
+    kw = dict(n_groups=1, n_replicas=3)
+    eng, ref = _pair(kw, ext_inputs=True)
+    eng.run(30)
+    ref.run(30)
+    v = ref.views()
+    lead = [i for i in range(3) if v[i].role == O.LEADER][0]
+    target = (lead + 1) % 3 + 1
+    eng.request_leader_transfer([lead], [target])
+    ref.push(O.PUSH_XFER, lead, target)
+    for _ in range(6):
+        eng.step()
+        ref.step()
+    ev, rv = eng.views(), ref.views()
+    assert rv[target - 1].role == O.LEADER and rv[target - 1].term == v[lead].term + 1
+    for i in range(3):
+        assert (ev[i].role, ev[i].term, ev[i].leader_id, ev[i].digest) == \
+            (rv[i].role, rv[i].term, rv[i].leader_id, rv[i].digest)
+
+
+def test_push_batches_are_all_or_nothing():
+    from dragonboat_amd.engine import InputError, RBE_E_INVALID, RBE_E_STATE
+    eng = SoaCpu(trace=True, n_groups=2, n_replicas=3, ext_inputs=True)
+    with pytest.raises(InputError) as ei:  # a replica out of range stages nothing
+        eng.push_proposals([0, 99], [[b"a"], [b"b"]])
+    assert ei.value.rc == RBE_E_INVALID
+    with pytest.raises(InputError) as ei:  # the same replica twice in one batch
+        eng.push_read_index([1, 1], [(5, 0), (6, 0)])
+    assert ei.value.rc == RBE_E_STATE
+    eng.push_proposals([0], [[b"x" * 16]])
+    with pytest.raises(InputError) as ei:  # a second batch for a replica this step
+        eng.push_proposals([0], [[b"y"]])
+    assert ei.value.rc == RBE_E_STATE
+    with pytest.raises(InputError) as ei:  # Cmd > 16 bytes without a payload heap
+        eng.push_proposals([1], [[b"z" * 17]])
+    assert ei.value.rc == RBE_E_INVALID
+    with pytest.raises(InputError):  # ctx.Low == 0 (requests.go:726)
+        eng.push_read_index([2], [(0, 1)])
+    with pytest.raises(InputError):  # transfer target outside the group
+        eng.request_leader_transfer([2], [4])
+    with pytest.raises(InputError):  # applied without ext_apply
+        eng.notify_applied([0], [1])
+    eng.step()
+    eng.push_proposals([0], [[b"y"]])  # the next step takes a new batch

@@ -39,13 +39,17 @@ def test_resume_matches_uninterrupted_oracle(name):
 
 
 def test_partial_import_overwrites_only_its_groups():
-    """Two engines with different seeds diverge; importing A's groups [5, 17)
-    into B makes exactly those groups equal A's, and leaves B's others alone."""
-    kw = dict(C3)
+    """Two engines of one configuration diverge (B gets extra host-pushed
+    proposals); importing A's groups [5, 17) into B makes exactly those groups
+    equal A's, and leaves B's others alone."""
+    kw = dict(C3, ext_inputs=True)
     a = SoaCpu(trace=True, **kw, ring=128)
-    b = SoaCpu(trace=True, **dict(kw, seed=0xBADC0DE), ring=128)
-    a.run(90)
-    b.run(90)
+    b = SoaCpu(trace=True, **kw, ring=128)
+    a.run(89)
+    b.run(88)
+    # B diverges through host-pushed proposals at every replica of every group
+    b.push_proposals(list(range(b.n_rep)), [[b"div-%d" % i] for i in range(b.n_rep)])
+    b.run(1)
     before = [tuple(getattr(v, "digest") for v in [x]) for x in b.views()]
     b.import_groups(a.export_groups(5, 12))
     n = kw["n_replicas"]
@@ -59,6 +63,22 @@ def test_partial_import_overwrites_only_its_groups():
     # the snapshot body is the group range only: sizes add up per group
     s1, s12 = len(a.export_groups(0, 1)), len(a.export_groups(0, 12))
     assert (s12 - s1) % 11 == 0 and s12 > s1
+
+
+def test_import_rejects_other_behaviour():
+    """A snapshot resumes bit-exact only under the configuration that wrote it:
+    a different seed (or timeout, quorum check, workload ...) is refused."""
+    a = SoaCpu(trace=True, **C4)
+    b = SoaCpu(trace=True, **dict(C4, seed=0xBADC0DE))
+    a.run(3)
+    b.run(3)
+    with pytest.raises(SnapshotError) as ei:
+        b.import_groups(a.export_groups(0, 2))
+    assert ei.value.rc == RBE_E_INVALID
+    c = SoaCpu(trace=True, **dict(C4, election_rtt=12))
+    c.run(3)
+    with pytest.raises(SnapshotError):
+        c.import_groups(a.export_groups(0, 2))
 
 
 def test_export_import_roundtrip_is_identity():
