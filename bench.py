@@ -51,7 +51,8 @@ WORKLOADS = {
     "c2m": (dict(n_groups=1_000_000, n_replicas=3, wl_enabled=True, wl_start_round=30,
                  ring=64), 60, "C2 at 1M groups x 3: 1 proposal per group per round"),
     "c3": (dict(n_groups=100_000, n_replicas=5, check_quorum=True, wl_enabled=True,
-                wl_start_round=40, iso_period=50, iso_len=30, iso_mod=10, ring=128),
+                wl_start_round=40, iso_period=50, iso_len=30, iso_mod=10, ring=128,
+                ecap=256),
            100, "C3: 100k groups x 5, CheckQuorum, leader isolation 30/50 rounds for 10%"),
     # groups per GPU; every rank holds the planes of all N x 500k groups and
     # steps the replicas it owns
@@ -60,6 +61,10 @@ WORKLOADS = {
                "(g+k) % N), steady replication, cross-rank messages by all-to-all each round"),
 }
 
+
+# engine capacities (per-replica window and per-round buffers) that the oracle
+# does not have: it keeps every entry and message in growable containers
+ENGINE_ONLY = ("ring", "ecap", "maxm", "rq_cap", "rtr_cap", "dri_cap")
 
 # bounded CPU-baseline samples (groups for the T-thread run, groups for the
 # 1-thread run), sized for ~5-15 s of host time each on the GPU box
@@ -99,8 +104,7 @@ def _oracle_rate(name, groups, settle, rounds, threads):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     kw, _, _ = WORKLOADS[name]
-    kw = dict(kw)
-    kw.pop("ring", None)
+    kw = {k: v for k, v in kw.items() if k not in ENGINE_ONLY}
     kw["n_groups"] = groups
     h = O.Harness(**kw, trace=False, threads=threads)
     h.run(settle)

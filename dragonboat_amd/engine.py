@@ -62,6 +62,22 @@ class RbeReplicaView(C.Structure):
                 ("events", C.c_uint32), ("pad", C.c_uint32)]
 
 
+def _np_dtype(struct):
+    names, formats, offsets = [], [], []
+    for name, t in struct._fields_:
+        names.append(name)
+        base = getattr(t, "_type_", t)
+        n = getattr(t, "_length_", None)
+        code = np.dtype(base)
+        formats.append((code, (n,)) if n else code)
+        offsets.append(getattr(struct, name).offset)
+    return np.dtype({"names": names, "formats": formats, "offsets": offsets,
+                     "itemsize": C.sizeof(struct)})
+
+
+VIEW_DTYPE = _np_dtype(RbeReplicaView)
+
+
 class RbeUpdate(C.Structure):
     _fields_ = [("term", C.c_uint64), ("vote", C.c_uint64), ("commit", C.c_uint64),
                 ("save_lo", C.c_uint64), ("save_hi", C.c_uint64), ("apply_lo", C.c_uint64),
@@ -430,6 +446,11 @@ class Engine(NodeInputs):
         arr = (RbeReplicaView * count)()
         _check(self.lib.rbe_get_views(self.h, first, count, arr), "rbe_get_views")
         return arr
+
+    def views_np(self, first: int = 0, count: Optional[int] = None) -> np.ndarray:
+        """views() as a numpy structured array (zero-copy over the ctypes array)."""
+        arr = self.views(first, count)
+        return np.frombuffer(arr, dtype=VIEW_DTYPE)
 
     def updates(self, first: int = 0, count: Optional[int] = None):
         count = self.n_rep - first if count is None else count
