@@ -75,7 +75,7 @@ def test_ext_inputs_path(gpu_available):
     leaders = [i for i, v in enumerate(views) if v.role == 2]
     assert len(leaders) == 4
     c0 = [views[i].committed for i in leaders]
-    eng.push_proposals(leaders, [b"hello-raft-%02d" % i for i in range(4)])
+    eng.push_proposals(leaders, [[b"hello-raft-%02d" % i] for i in range(4)])
     eng.run(3)
     views = eng.views()
     for j, i in enumerate(leaders):

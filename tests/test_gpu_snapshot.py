@@ -60,11 +60,15 @@ def test_host_build_snapshot_resumes_gpu_engine(gpu_available, name):
 
 
 def test_gpu_partial_import(gpu_available):
-    kw = dict(C3)
+    # one configuration (a snapshot imports only under the behaviour that wrote
+    # it); B diverges through host-pushed proposals at every replica
+    kw = dict(C3, ext_inputs=True)
     a = _engine(kw, "C3")
-    b = _engine(dict(kw, seed=0xBADC0DE), "C3")
+    b = _engine(kw, "C3")
     a.run(90)
-    b.run(90)
+    b.run(89)
+    b.push_proposals(list(range(b.n_rep)), [[b"div-%d" % i] for i in range(b.n_rep)])
+    b.run(1)
     before = [v.digest for v in b.views()]
     b.import_groups(a.export_groups(5, 12))
     n = kw["n_replicas"]
