@@ -579,8 +579,8 @@ struct XchgCaps {
 // Pack: one lane per replica; each block reserves its records' slots with one
 // global atomic per (peer, stream) after an LDS reduction of its lanes' counts.
 template <int N>
-__global__ __launch_bounds__(kBlock) void k_xchg_pack(Planes P, Params C, u32 par, u8* buf,
-                                                      XchgCaps caps, u32* gcount) {
+__global__ __launch_bounds__(kBlock) void k_xchg_pack(Planes P, Params C, u32 par, u32 round,
+                                                      u8* buf, XchgCaps caps, u32* gcount) {
   __shared__ u32 s_cnt[kXchgMaxWorld * XS_NUM];
   __shared__ u32 s_base[kXchgMaxWorld * XS_NUM];
   const u32 nc = C.rep_world * XS_NUM;
@@ -591,7 +591,7 @@ __global__ __launch_bounds__(kBlock) void k_xchg_pack(Planes P, Params C, u32 pa
   u32 cnt[kXchgMaxWorld * XS_NUM];
   u32 base[kXchgMaxWorld * XS_NUM];
   for (u32 i = 0; i < nc; i++) cnt[i] = 0;
-  if (mine) xchg_sender<N, false>(P, C, r, par, cnt, nullptr, nullptr, caps.cap);
+  if (mine) xchg_sender<N, false>(P, C, r, par, round, cnt, nullptr, nullptr, caps.cap);
   for (u32 i = 0; i < nc; i++) base[i] = cnt[i] ? atomicAdd(&s_cnt[i], cnt[i]) : 0u;
   __syncthreads();
   for (u32 i = threadIdx.x; i < nc; i += kBlock)
@@ -602,13 +602,8 @@ __global__ __launch_bounds__(kBlock) void k_xchg_pack(Planes P, Params C, u32 pa
       base[i] += s_base[i];
       cnt[i] = 0;
     }
-    xchg_sender<N, true>(P, C, r, par, cnt, base, buf, caps.cap);
+    xchg_sender<N, true>(P, C, r, par, round, cnt, base, buf, caps.cap);
   }
-}
-template <int N>
-__global__ __launch_bounds__(kBlock) void k_xchg_clear(Planes P, Params C, u32 par) {
-  const u64 r = (u64)blockIdx.x * kBlock + threadIdx.x;
-  if (r < C.n_rep && owned<N>(C, r)) xchg_clear<N>(P, C, r, par);
 }
 __global__ __launch_bounds__(kBlock) void k_xchg_put_cnt(Planes P, Params C, u32 par,
                                                          const XCnt* x, u64 n) {
@@ -666,7 +661,7 @@ static u64 bytes_of(const Params& C, u64* parts) {
       R * C.rq_cap * sizeof(ReadReq),
       (u64)C.ring * R * sizeof(u64),
       (u64)C.ring * R * sizeof(Body),
-      2 * G * N * N * sizeof(u16),
+      2 * R * sizeof(CntRow),
       2 * G * N * N * C.maxm * sizeof(Msg),
       2 * R * C.ecap * sizeof(Ent),
       G * sizeof(u8),
@@ -1005,9 +1000,8 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   P.rq = (ReadReq*)ptrs[4];
   P.term_ring = (u64*)ptrs[5];
   P.pay_ring = (Body*)ptrs[6];
-  u64 cnt_half = C.n_groups * C.n * C.n;
-  P.cnt[0] = (u16*)ptrs[7];
-  P.cnt[1] = P.cnt[0] + cnt_half;
+  P.cnt[0] = (CntRow*)ptrs[7];
+  P.cnt[1] = P.cnt[0] + C.n_rep;
   u64 msg_half = C.n_groups * C.n * C.n * C.maxm;
   P.msgs[0] = (Msg*)ptrs[8];
   P.msgs[1] = P.msgs[0] + msg_half;
@@ -1336,7 +1330,7 @@ int rbe_xchg_pack(rbe_engine* e, void* buf, const uint64_t* cap3, uint32_t* coun
   int rc = dispatch_n(e->C.n, [&](auto NN) {
     constexpr int N = decltype(NN)::value;
     hipLaunchKernelGGL(k_xchg_pack<N>, dim3(grid_for(e->C.n_rep)), dim3(kBlock), 0, e->stream,
-                       e->P, e->C, par, (u8*)buf, caps, e->xcount);
+                       e->P, e->C, par, e->round, (u8*)buf, caps, e->xcount);
     HIP_OK(hipGetLastError());
     return RBE_OK;
   });
@@ -1348,19 +1342,11 @@ int rbe_xchg_pack(rbe_engine* e, void* buf, const uint64_t* cap3, uint32_t* coun
   return RBE_OK;
 }
 
-// clear the remote senders' count words of the last round's parity, then
-// scatter exchange records (device pointers) into the planes
+// scatter exchange records (device pointers) into the planes of the last
+// round's parity (stale outbox headers of silent senders read as empty)
 static int xchg_scatter(rbe_engine* e, const void* cnt, uint64_t n_cnt, const void* msg,
                         uint64_t n_msg, const void* ent, uint64_t n_ent) {
   const u32 par = (e->round - 1) & 1u;
-  int rc = dispatch_n(e->C.n, [&](auto NN) {
-    constexpr int N = decltype(NN)::value;
-    hipLaunchKernelGGL(k_xchg_clear<N>, dim3(grid_for(e->C.n_rep)), dim3(kBlock), 0, e->stream,
-                       e->P, e->C, par);
-    HIP_OK(hipGetLastError());
-    return RBE_OK;
-  });
-  if (rc) return rc;
   if (n_cnt)
     hipLaunchKernelGGL(k_xchg_put_cnt, dim3(grid_for(n_cnt)), dim3(kBlock), 0, e->stream, e->P,
                        e->C, par, (const XCnt*)cnt, n_cnt);
@@ -1390,11 +1376,11 @@ int rbe_get_outbox(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t c
   const u32 N = e->C.n, par = (e->round - 1) & 1u;
   const u64 g = replica / N;
   const u32 k = (u32)(replica % N);
-  std::vector<u16> cnt(N);
+  CntRow row;
   std::vector<Msg> lst((size_t)N * e->C.maxm);
   std::vector<Ent> arena(e->C.ecap);
-  HIP_OK(hipMemcpyAsync(cnt.data(), e->P.cnt[par] + g * N * N + k * N, N * sizeof(u16),
-                        hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipMemcpyAsync(&row, e->P.cnt[par] + replica, sizeof(row), hipMemcpyDeviceToHost,
+                        e->stream));
   HIP_OK(hipMemcpyAsync(lst.data(), e->P.msgs[par] + (g * N + k) * N * (u64)e->C.maxm,
                         lst.size() * sizeof(Msg), hipMemcpyDeviceToHost, e->stream));
   HIP_OK(hipMemcpyAsync(arena.data(), e->P.arena[par] + replica * e->C.ecap,
@@ -1402,8 +1388,8 @@ int rbe_get_outbox(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t c
   HIP_OK(hipStreamSynchronize(e->stream));
   return dispatch_n(N, [&](auto NN) {
     constexpr int NC = decltype(NN)::value;
-    outbox_messages<NC>(e->C, g, k, cnt.data(), lst.data(), arena.data(), out, cap, ents, ent_cap,
-                        n_out, n_ents);
+    outbox_messages<NC>(e->C, g, k, row, e->round, lst.data(), arena.data(), out, cap, ents,
+                        ent_cap, n_out, n_ents);
     return RBE_OK;
   });
 }
@@ -1418,7 +1404,7 @@ int rbe_push_messages(rbe_engine* e, uint64_t n, const uint64_t* group, const rb
   std::vector<XEnt> x;
   int rc = dispatch_n(e->C.n, [&](auto NN) {
     constexpr int N = decltype(NN)::value;
-    return messages_to_records<N>(e->C, n, group, msgs, ents, c, m, x);
+    return messages_to_records<N>(e->C, e->round, n, group, msgs, ents, c, m, x);
   });
   if (rc) return rc;
   const size_t bytes = c.size() * sizeof(XCnt) + m.size() * sizeof(XMsg) + x.size() * sizeof(XEnt);
@@ -1577,16 +1563,16 @@ int rbe_get_messages(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t
   const u32 N = e->C.n, par = (e->round - 1) & 1u;
   const u64 g = replica / N;
   const u32 k = (u32)(replica % N);
-  std::vector<u16> cnt(N);
-  HIP_OK(hipMemcpyAsync(cnt.data(), e->P.cnt[par] + g * N * N + k * N, N * sizeof(u16),
-                        hipMemcpyDeviceToHost, e->stream));
+  CntRow row;
+  HIP_OK(hipMemcpyAsync(&row, e->P.cnt[par] + replica, sizeof(row), hipMemcpyDeviceToHost,
+                        e->stream));
   std::vector<Msg> lst((size_t)N * e->C.maxm);
   HIP_OK(hipMemcpyAsync(lst.data(), e->P.msgs[par] + (g * N + k) * N * (u64)e->C.maxm,
                         lst.size() * sizeof(Msg), hipMemcpyDeviceToHost, e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
   u32 n = 0;
   for (u32 d = 0; d < N; d++) {
-    const u32 pc = cnt[d], na = pc & 0x7F, nb = (pc >> 7) & 0x7F;
+    const u32 pc = row_word(row, d, e->round), na = pc & 0x7F, nb = (pc >> 7) & 0x7F;
     for (u32 i = 0; i < na + nb; i++) {
       const Msg& m = i < na ? lst[d * e->C.maxm + i] : lst[d * e->C.maxm + e->C.maxm - 1 - (i - na)];
       if (n < cap && out) {

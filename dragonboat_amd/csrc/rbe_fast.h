@@ -445,21 +445,12 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
 #ifndef RBE_DIAG_NO_STATE_STORES
   if constexpr ((STG & STG_OUT) != 0) sr->upd = u;
   else P.upd[r] = u;
-  // the N count words of this sender's row (N odd): one 2-B and (N-1)/2
-  // 4-B stores instead of N 2-B stores, placed by the row's 4-B alignment
-  static_assert(N % 2 == 1, "the packed count-word store covers odd N only");
-  u16* cnt = &P.cnt[o.par][o.g * N * N + o.k * N];
+  // this sender's outbox header: stamp + the N count words, one 16-B store
   {
     u32 w[N];
 #pragma unroll
     for (u32 dd = 0; dd < N; dd++) w[dd] = o.get_pc(dd) & 0xFFFFu;
-    const bool odd = ((uintptr_t)cnt & 2u) != 0;
-    *(odd ? cnt : cnt + (N - 1)) = (u16)(odd ? w[0] : w[N - 1]);
-#pragma unroll
-    for (u32 j = 0; j < (N - 1) / 2; j++) {
-      const u32 v = odd ? (w[1 + 2 * j] | (w[2 + 2 * j] << 16)) : (w[2 * j] | (w[2 * j + 1] << 16));
-      __builtin_memcpy(cnt + (odd ? 1 : 0) + 2 * j, &v, sizeof(v));
-    }
+    put_row(P, r, o.round_, N, w);
   }
   h.flags = o.fault ? (u8)(flags | HF_FAULTED) : flags;
   h.election_tick = etick;
@@ -534,8 +525,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
     for (u32 s = 0; s < N; s++) pcin[s] = s == k ? 0u : aux_count_word<N>(aux, k, s);
   } else {
 #pragma unroll
-    for (u32 s = 0; s < N; s++)
-      pcin[s] = (round > 0 && s != k) ? (u32)P.cnt[ppar][g * N * N + s * N + k] : 0u;
+    for (u32 s = 0; s < N; s++) pcin[s] = s != k ? in_word<N>(P, g, s, k, round) : 0u;
   }
   // one row per other sender (row j is sender j + (j >= k)): no registers
   // for the lane's own slot, which is what keeps the step out of scratch.
@@ -1199,8 +1189,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
     if (na_a > 0) spec0 = P.arena[ppar][(g * N + sa) * (u64)C.ecap];
   } else {
 #pragma unroll
-    for (u32 s = 0; s < N; s++)
-      pcin[s] = (round > 0 && s != k) ? (u32)P.cnt[ppar][g * N * N + s * N + k] : 0u;
+    for (u32 s = 0; s < N; s++) pcin[s] = s != k ? in_word<N>(P, g, s, k, round) : 0u;
   }
   // the isolation schedule and the Update record are read only when in use:
   // two of the lane's scattered lines saved in the steady state

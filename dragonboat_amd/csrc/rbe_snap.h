@@ -58,7 +58,7 @@ inline void snap_planes(const Planes& P, const Params& C, SnapPlane* out) {
   add(P.term_ring, C.ring, R * sizeof(u64), N * sizeof(u64));
   add(P.pay_ring, C.ring, R * sizeof(Body), N * sizeof(Body));
   // the network planes: parity 1 starts right after parity 0 (rbe_create)
-  add(P.cnt[0], 2, G * N * N * sizeof(u16), N * N * sizeof(u16));
+  add(P.cnt[0], 2, R * sizeof(CntRow), N * sizeof(CntRow));
   add(P.msgs[0], 2, G * N * N * C.maxm * sizeof(Msg), N * N * C.maxm * sizeof(Msg));
   add(P.arena[0], 2, R * C.ecap * sizeof(Ent), N * C.ecap * sizeof(Ent));
   add(P.iso_mask, 1, G, 1);

@@ -109,17 +109,34 @@ RBE_HD Hot load_hot(const Planes& P, const Params& C, u64 r, u32 round) {
 //   IB_LAZY  the next round is a pure QuiescedTick unless an input arrives
 //            (Quiesce on, quiesced, RAFT_QUIESCE already set, nothing to apply);
 //   IB_LEAD  the replica leads (only a leader takes client input);
-//   IB_H1/H2 history: the last / second-last round was skipped lazily, so the
-//            outbox-count words of this round's parity are known to be zero;
 //   bits 4-6 the role, so a replica with inbound messages is classified
 //            without reading Hot.
-enum : u8 { IB_LAZY = 1, IB_LEAD = 2, IB_H1 = 4, IB_H2 = 8, IB_ROLE_SHIFT = 4 };
+enum : u8 { IB_LAZY = 1, IB_LEAD = 2, IB_ROLE_SHIFT = 4 };
 RBE_HD u8 idle_byte(const Params& C, u8 role, u8 flags, u32 qs) {
   const bool lazy = C.quiesce && qs > 0 && (flags & HF_RAFT_QUIESCE) &&
                     !(flags & (HF_APPLY_PENDING | HF_APPLIED_NEW));
   return (u8)((lazy ? IB_LAZY : 0) | (role == R_Leader ? IB_LEAD : 0) | ((role & 7u) << IB_ROLE_SHIFT));
 }
 RBE_HD u32 idle_role(u8 ib) { return (ib >> IB_ROLE_SHIFT) & 7u; }
+
+// The count word of list (sender slot s → destination slot d) that a step of
+// round `round` reads: the sender's outbox header of the previous round's
+// parity, valid only if that round wrote it (CntRow::stamp == round).
+RBE_HD u32 row_word(const CntRow& row, u32 d, u32 round) {
+  return row.stamp == round ? (u32)row.w[d] : 0u;
+}
+template <int N>
+RBE_HD u32 in_word(const Planes& P, u64 g, u32 s, u32 d, u32 round) {
+  if (round == 0) return 0u;
+  return row_word(P.cnt[(round & 1u) ^ 1u][g * N + s], d, round);
+}
+// This sender's outbox header of round `round` (one 16-B store).
+RBE_HD void put_row(const Planes& P, u64 r, u32 round, u32 n, const u32* w) {
+  CntRow row;
+  row.stamp = round + 1u;
+  for (u32 d = 0; d < 6; d++) row.w[d] = (u16)(d < n ? w[d] : 0u);
+  P.cnt[round & 1u][r] = row;
+}
 
 // The Update helpers of peer.go on the engine's range form of an Update
 // (EntriesToSave = [save_lo, save_hi], CommittedEntries = [apply_lo,
@@ -1287,10 +1304,9 @@ struct Lane {
     u32 n_in = 0;
     if (round > 0) {
       const u32 ppar = par ^ 1u;
-      const u16* icnt = &P.cnt[ppar][g * N * N];
       for (u32 s = 0; s < N; s++) {
         if (s == k) continue;
-        const u32 pc = icnt[s * N + k];
+        const u32 pc = in_word<N>(P, g, s, k, round);
         const u32 na = pc & 0x7Fu, n = na + ((pc >> 7) & 0x7Fu);
         n_in += n;
         const Msg* lst = &P.msgs[ppar][msg_slot_base(s, k)];
@@ -1482,14 +1498,9 @@ struct Lane {
       // (node.go:1030-1067): a message or notice, client input, an entry to apply
       bool ev = do_read || do_prop || xfer || unreach || snap_nodes || ext_applied ||
                 (flags & (HF_APPLY_PENDING | HF_APPLIED_NEW));
-      if (round > 0)
-        for (u32 s = 0; s < N; s++)
-          if (s != k && P.cnt[par ^ 1u][g * N * N + s * N + k] != 0) ev = true;
-      if (!ev) {
-        u16* cnt = &P.cnt[par][g * N * N + k * N];
-        for (u32 dd = 0; dd < N; dd++) cnt[dd] = 0;
-        return true;
-      }
+      for (u32 s = 0; s < N; s++)
+        if (s != k && in_word<N>(P, g, s, k, round) != 0) ev = true;
+      if (!ev) return true;  // no step: no outbox header either
     }
     ctr.v[C_STEPS]++;
     if (do_read && !(C.ext_inputs && read_lo != 0)) {  // the workload's ctx
@@ -1512,7 +1523,6 @@ struct Lane {
     //   handleProposals (node.go:1091-1106) → Peer.ProposeEntries
     //   handleLeaderTransferRequest (node.go:1069-1075) → Peer.RequestLeaderTransfer
     const u32 ppar = par ^ 1u;
-    const u16* icnt = &P.cnt[ppar][g * N * N];
     u32 cs = 0, ci = 0, cn = 0, cna = 0;  // inbox cursor: sender, index, count, #A
     bool copen = false;
     u32 phase = (unreach | snap_nodes) ? 0u : (round > 0 ? 1u : 2u);
@@ -1557,7 +1567,7 @@ struct Lane {
               cs++;
               continue;
             }
-            const u32 pc = icnt[cs * N + k];
+            const u32 pc = in_word<N>(P, g, cs, k, round);
             if (pc & 0x8000u) {  // Quiesce first in the sender's stream (node.go:1207-1210)
               ctr.v[C_MSG_IN]++;
               q_try_enter();
@@ -1771,9 +1781,12 @@ struct Lane {
     u.round = round;
     u.pad2 = 0;
     P.upd[r] = u;
-    // this round's outbox counts for every destination (zeros included)
-    u16* cnt = &P.cnt[par][g * N * N + k * N];
-    for (u32 dd = 0; dd < N; dd++) cnt[dd] = (u16)get_pc(dd);
+    // this round's outbox header: the count word of every destination list
+    {
+      u32 w[N];
+      for (u32 dd = 0; dd < N; dd++) w[dd] = get_pc(dd);
+      put_row(P, r, round, N, w);
+    }
     store();
     return true;
   }
@@ -1884,7 +1897,8 @@ enum : u32 { T_DONE = 0, T_LEAD = 1, T_FOLL = 2, T_FULL = 3 };
 // replica whose idle byte says IB_LAZY, with no inbound message or Quiesce
 // notice (`inbound` = any non-zero inbound count word) and no client input,
 // runs a round that is one QuiescedTick: it is applied lazily
-// (materialize_hot), so neither Hot nor the outbox counts are touched.  The
+// (materialize_hot), so it writes nothing at all (its outbox header of this
+// parity stays stale, which reads as empty).  The
 // caller has loaded `ib` and `inbound` (k_triage prefetches them for all the
 // replicas a lane owns).  Returns true when the round is complete.
 template <int N>
@@ -1898,17 +1912,11 @@ RBE_HD bool triage_lazy(const Planes& P, const Params& C, u64 r, const Clk& ck, 
   if (C.xfer_period && xfer_input(C, cid, round, (u32)r - g * (u32)N)) return false;
   if (C.ext_inputs && P.ext[r].flags) return false;
   // a round without a tick and without input is no step at all (handleEvents
-  // finds no event, node.go:1030-1067): only the count row is kept clean
+  // finds no event, node.go:1030-1067)
   const u32 t = ck.tick ? 1u : 0u;
   ctr.v[C_STEPS] += t;
   ctr.v[C_QUIESCED_TICKS] += t;
   ctr.v[C_LEADER_STEPS] += (ib & IB_LEAD) ? t : 0u;
-  if (!(ib & IB_H2)) {  // this parity's outbox counts may still be non-zero
-    u16* cnt = &P.cnt[round & 1u][(u64)g * (N * N) + ((u32)r - g * (u32)N) * N];
-    for (u32 d = 0; d < N; d++) cnt[d] = 0;
-  }
-  const u8 nb = (u8)((ib & ~(IB_H1 | IB_H2)) | IB_H1 | ((ib & IB_H1) ? IB_H2 : 0));
-  if (nb != ib) P.idle[r] = nb;
   return true;
 }
 // the inbound count words of replica r in this round: bit 0 = any non-zero
@@ -1919,8 +1927,11 @@ RBE_HD bool triage_lazy(const Planes& P, const Params& C, u64 r, const Clk& ck, 
 // own slot is masked in the fold, so no load sits behind a branch.
 template <int N>
 RBE_HD void inbound_load(const Planes& P, u32 g, u32 k, u32 round, u16 (&w)[N]) {
-  const u16* icnt = &P.cnt[(round & 1u) ^ 1u][(u64)g * (N * N) + k];
-  for (u32 s = 0; s < N; s++) w[s] = icnt[s * N];
+  const CntRow* rows = &P.cnt[(round & 1u) ^ 1u][(u64)g * N];
+  for (u32 s = 0; s < N; s++) {
+    const CntRow row = rows[s];
+    w[s] = (u16)row_word(row, k, round);
+  }
 }
 template <int N>
 RBE_HD u32 inbound_fold(const u16 (&w)[N], u32 k, u32 round) {
@@ -1978,14 +1989,12 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, const Clk& ck
   const u64 g = r / N;
   const u32 k = (u32)(r % N);
   const u32 round = ck.round;
-  const u32 par = round & 1u;
   const Hot h = load_hot(P, C, r, ck.tclk);
   u32 nmsg = 0, qbits = 0;
   if (round > 0) {
-    const u16* icnt = &P.cnt[par ^ 1u][g * N * N];
     for (u32 s = 0; s < N; s++) {
       if (s == k) continue;
-      const u32 pc = icnt[s * N + k];
+      const u32 pc = in_word<N>(P, g, s, k, round);
       nmsg += (pc & 0x7Fu) + ((pc >> 7) & 0x7Fu);
       if (pc & 0x8000u) qbits |= 1u << s;
     }
@@ -2052,25 +2061,22 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, const Clk& ck
     iso = round < until ? P.iso_mask[g] : (u8)0;
   }
   // A round that is only a QuiescedTick of an already-flagged replica writes
-  // nothing (lazy ticks, materialize_hot); its outbox counts are written only
-  // if the buffer of this parity still holds a non-zero word.
+  // nothing (lazy ticks, materialize_hot; its stale outbox header reads as
+  // empty); any other step writes its header, Quiesce notices included.
   const bool lazy = noop || (!TRACE && quiesced && !qnew && qbits == 0 &&
-                             (h.flags & HF_RAFT_QUIESCE));
-  u16* cnt = &P.cnt[par][g * N * N + k * N];
-  bool dirty = !lazy;
-  if (lazy)
-    for (u32 d = 0; d < N; d++) dirty |= cnt[d] != 0;
-  if (dirty) {
+                             (h.flags & HF_RAFT_QUIESCE) && !(h.flags & HF_APPLIED_NEW));
+  if (!lazy) {
+    u32 w[N];
     for (u32 d = 0; d < N; d++) {
-      u16 v = 0;
+      w[d] = 0;
       if (qnew && d != k) {  // sendEnterQuiesceMessages (node.go:873-886)
         const u32 drop = ((iso >> k) & 1u) | ((iso >> d) & 1u);
         ctr.v[C_MSG_DROPPED] += drop;
         ctr.v[C_MSG_OUT] += 1u - drop;
-        v = drop ? (u16)0 : (u16)0x8000u;
+        w[d] = drop ? 0u : 0x8000u;
       }
-      cnt[d] = v;
     }
+    put_row(P, r, round, N, w);
   }
   if (!lazy) {
     Hot o = h;

@@ -122,6 +122,17 @@ struct alignas(16) Msg {
   u64 term, log_term, log_index, commit, hint, hint_high;
 };
 
+// Outbox header of one sender replica for one round (16 B): the count word of
+// each destination list — A (Replicate messages, front of the list) | B (the
+// rest, back of the list) << 7 | Quiesce notice << 15 — stamped with the round
+// that reads it (the writer's round + 1).  A sender that makes no step in a
+// round (a lazily skipped quiesced tick) writes no row, and the stale row of
+// that parity reads as empty, so nothing ever has to be cleared.
+struct alignas(16) CntRow {
+  u32 stamp;
+  u16 w[6];
+};
+
 // arena entry: 32 B (index implicit: log_index + 1 + i for Replicate)
 struct alignas(16) Ent {
   u64 term;
@@ -252,7 +263,7 @@ struct Planes {
   ReadReq* rq;        // [n_rep * rq_cap]
   u64* term_ring;     // [ring][n_rep]
   Body* pay_ring;     // [ring][n_rep]
-  u16* cnt[2];        // [n_groups * N * N]  A | B << 7 | quiesce << 15
+  CntRow* cnt[2];     // [n_rep] outbox header of each sender, by round parity
   Msg* msgs[2];       // [n_groups * N * N * maxm]
   Ent* arena[2];      // [n_rep * ecap]
   u8* iso_mask;       // [n_groups]

@@ -7,10 +7,10 @@
 // outbox-count word and Replicate entry that a rank's senders produced for a
 // replica owned elsewhere is packed into fixed-size records, moved with one
 // all-to-all (RCCL over xGMI on GPUs; gloo in the CPU tests), and scattered by
-// the receiver into the same positions of its own planes.  The receiver first
-// clears the count words of its remote senders for that parity, so silence
-// (no record) reads as an empty list.  Record order is irrelevant: every
-// record names its destination slot.
+// the receiver into the same positions of its own planes.  Outbox headers are
+// round-stamped (CntRow), so a remote sender that sent nothing leaves a stale
+// header that reads as empty: silence needs no record and nothing is cleared.
+// Record order is irrelevant: every record names its destination slot.
 #pragma once
 #include "rbe_fast.h"
 #include "../../include/rbe.h"
@@ -23,9 +23,10 @@ namespace rbe {
 enum : u32 { XS_CNT = 0, XS_MSG = 1, XS_ENT = 2, XS_NUM = 3 };
 constexpr u32 kXchgMaxWorld = 16;
 
-struct alignas(16) XCnt {  // outbox-count word of list (g, s, d)
-  u64 key;                 // (g * N + s) * N + d
-  u64 word;
+struct alignas(16) XCnt {  // outbox header of sender replica g * N + s
+  u64 key;                 // g * N + s
+  u64 pad;
+  CntRow row;
 };
 struct alignas(16) XMsg {  // one message of list (g, s, d) at `slot`
   u64 key;
@@ -59,21 +60,25 @@ RBE_HD u64 xchg_region(const u64* cap, u32 p, u32 t) {
   return off;
 }
 
-// Records sender replica r (owned) produced in parity `par` for replicas
-// owned elsewhere.  WRITE = false counts them into cnt[peer * XS_NUM + t];
-// WRITE = true writes them at slot base[peer * XS_NUM + t] + running index
-// of the pack buffer (overflow past cap is counted, not written).
+// Records sender replica r (owned) produced in round `round` - 1 (parity
+// `par`) for replicas owned elsewhere: its outbox header once per peer that
+// owns a destination with a non-empty list, and those lists' messages and
+// entries.  WRITE = false counts them into cnt[peer * XS_NUM + t]; WRITE =
+// true writes them at slot base[peer * XS_NUM + t] + running index of the pack
+// buffer (overflow past cap is counted, not written).
 template <int N, bool WRITE>
-RBE_HD void xchg_sender(const Planes& P, const Params& C, u64 r, u32 par, u32* cnt, const u32* base,
-                        u8* buf, const u64* cap) {
+RBE_HD void xchg_sender(const Planes& P, const Params& C, u64 r, u32 par, u32 round, u32* cnt,
+                        const u32* base, u8* buf, const u64* cap) {
   const u64 g = r / N;
   const u32 s = (u32)(r % N);
+  const CntRow row = P.cnt[par][r];
+  u32 sent_to = 0;  // peers that have this header already
   for (u32 d = 0; d < N; d++) {
     if (d == s) continue;
     const u32 peer = owner_of<N>(C, g, d);
     if (peer == C.rep_rank) continue;
     const u64 key = (g * N + s) * N + d;
-    const u32 word = P.cnt[par][key];
+    const u32 word = row_word(row, d, round);
     if (word == 0) continue;
     auto put = [&](u32 t) -> u8* {
       const u32 i = cnt[peer * XS_NUM + t]++;
@@ -82,11 +87,15 @@ RBE_HD void xchg_sender(const Planes& P, const Params& C, u64 r, u32 par, u32* c
       if (at >= cap[t]) return nullptr;
       return buf + xchg_region(cap, peer, t) + (u64)at * kXRecBytes[t];
     };
-    if (u8* p = put(XS_CNT)) {
-      XCnt x;
-      x.key = key;
-      x.word = word;
-      *(XCnt*)p = x;
+    if (!((sent_to >> peer) & 1u)) {
+      sent_to |= 1u << peer;
+      if (u8* p = put(XS_CNT)) {
+        XCnt x;
+        x.key = r;
+        x.pad = 0;
+        x.row = row;
+        *(XCnt*)p = x;
+      }
     }
     const u32 na = word & 0x7Fu, nb = (word >> 7) & 0x7Fu;
     const Msg* lst = &P.msgs[par][key * (u64)C.maxm];
@@ -116,20 +125,8 @@ RBE_HD void xchg_sender(const Planes& P, const Params& C, u64 r, u32 par, u32* c
   }
 }
 
-// Before the scatter: the count words of parity `par` of every list whose
-// sender is remote and whose destination replica r is owned here.
-template <int N>
-RBE_HD void xchg_clear(const Planes& P, const Params& C, u64 r, u32 par) {
-  const u64 g = r / N;
-  const u32 d = (u32)(r % N);
-  for (u32 s = 0; s < N; s++) {
-    if (s == d || owner_of<N>(C, g, s) == C.rep_rank) continue;
-    P.cnt[par][(g * N + s) * N + d] = 0;
-  }
-}
-
 RBE_HD void xchg_put_cnt(const Planes& P, const Params& C, u32 par, const XCnt& x) {
-  P.cnt[par][x.key] = (u16)x.word;
+  P.cnt[par][x.key] = x.row;
 }
 RBE_HD void xchg_put_msg(const Planes& P, const Params& C, u32 par, const XMsg& x) {
   P.msgs[par][x.key * (u64)C.maxm + x.slot] = x.m;
@@ -152,12 +149,13 @@ RBE_HD void xchg_put_ent(const Planes& P, const Params& C, u32 par, const XEnt& 
 // lockstep ordering of DESIGN.md §2): the Quiesce notice (node.go:873-886),
 // Replicate messages (sent before persistence, node.go:897-905), the rest.
 // A Replicate's entries follow in `ents` (rbe_message.n_entries of them,
-// Index = LogIndex + 1 + i).  cnt_row = the N count words of (g, k, *),
-// lst = the N * maxm message slots of (g, k, *), arena = the sender's ecap
-// arena entries, all host copies.  Counts beyond the capacities are reported
-// in *n_msg / *n_ent and not written.
+// Index = LogIndex + 1 + i).  row = the sender's outbox header of that
+// round's parity, `round` the round that reads it, lst = the N * maxm message
+// slots of (g, k, *), arena = the sender's ecap arena entries, all host
+// copies.  Counts beyond the capacities are reported in *n_msg / *n_ent and
+// not written.
 template <int N>
-void outbox_messages(const Params& C, u64 g, u32 k, const u16* cnt_row, const Msg* lst,
+void outbox_messages(const Params& C, u64 g, u32 k, const CntRow& row, u32 round, const Msg* lst,
                      const Ent* arena, rbe_message* out, u32 cap, rbe_entry* ents, u32 ent_cap,
                      u32* n_msg, u32* n_ent) {
   const u64 cid = C.cid_base + g * C.cid_stride;
@@ -182,7 +180,7 @@ void outbox_messages(const Params& C, u64 g, u32 k, const u16* cnt_row, const Ms
     n++;
   };
   for (u32 d = 0; d < N; d++) {
-    const u32 pc = cnt_row[d], na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
+    const u32 pc = row_word(row, d, round), na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
     if (pc & 0x8000u) {
       Msg q = mk_msg(M_Quiesce, d + 1);
       emit(q, M_Quiesce, d + 1);
@@ -218,15 +216,16 @@ void outbox_messages(const Params& C, u64 g, u32 k, const u16* cnt_row, const Ms
 // msgs[i].to (one it does), carrying msgs[i].n_entries entries taken in order
 // from `ents`.  Per (sender, destination) the Replicate messages keep their
 // order in the A list, the others in the B list, and a Quiesce message sets
-// the notice bit, exactly the layout a local sender's step writes.  The
-// records cover every list named; lists not named stay empty after the
-// unpack's clear.  Returns RBE_OK, RBE_E_INVALID (ids, ownership, entry
-// indexes) or RBE_E_NOMEM (more than maxm messages in one list, or more
-// than ecap entries from one sender).
+// the notice bit, exactly the layout a local sender's step writes.  Each
+// sender named gets one outbox header stamped for `round` (the round that
+// reads them); a sender not named keeps a stale header, which reads as
+// empty.  Returns RBE_OK,
+// RBE_E_INVALID (ids, ownership, entry indexes) or RBE_E_NOMEM (more than
+// maxm messages in one list, or more than ecap entries from one sender).
 template <int N>
-int messages_to_records(const Params& C, u64 n, const u64* group, const rbe_message* msgs,
-                        const rbe_entry* ents, std::vector<XCnt>& oc, std::vector<XMsg>& om,
-                        std::vector<XEnt>& oe) {
+int messages_to_records(const Params& C, u32 round, u64 n, const u64* group,
+                        const rbe_message* msgs, const rbe_entry* ents, std::vector<XCnt>& oc,
+                        std::vector<XMsg>& om, std::vector<XEnt>& oe) {
   std::unordered_map<u64, u32> words;  // list key → count word
   std::vector<u64> order;              // list keys in first-use order
   std::unordered_map<u64, u32> used;   // sender replica → arena entries used
@@ -295,11 +294,22 @@ int messages_to_records(const Params& C, u64 n, const u64* group, const rbe_mess
     }
     om.push_back(x);
   }
+  // one stamped header per sender with the words of all its lists
+  std::unordered_map<u64, size_t> hdr;  // sender replica → index in oc
   for (u64 key : order) {
-    XCnt c;
-    c.key = key;
-    c.word = words[key];
-    oc.push_back(c);
+    const u64 sr = key / N;
+    const u32 d = (u32)(key % N);
+    auto it = hdr.find(sr);
+    if (it == hdr.end()) {
+      XCnt c;
+      c.key = sr;
+      c.pad = 0;
+      c.row.stamp = round;
+      for (int w = 0; w < 6; w++) c.row.w[w] = 0;
+      it = hdr.emplace(sr, oc.size()).first;
+      oc.push_back(c);
+    }
+    oc[it->second].row.w[d] = (u16)words[key];
   }
   return RBE_OK;
 }

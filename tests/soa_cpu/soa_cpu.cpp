@@ -180,8 +180,8 @@ void* soa_create(const rbe_config* cfg) {
   P.term_ring = alloc<u64>(e, (u64)C.ring * R);
   P.pay_ring = alloc<Body>(e, (u64)C.ring * R);
   // parity 1 follows parity 0 in one allocation, as on the device (rbe_snap.h)
-  P.cnt[0] = alloc<u16>(e, 2 * G * N * N);
-  P.cnt[1] = P.cnt[0] + G * N * N;
+  P.cnt[0] = alloc<CntRow>(e, 2 * R);
+  P.cnt[1] = P.cnt[0] + R;
   P.msgs[0] = alloc<Msg>(e, 2 * G * N * N * C.maxm);
   P.msgs[1] = P.msgs[0] + G * N * N * C.maxm;
   P.arena[0] = alloc<Ent>(e, 2 * R * C.ecap);
@@ -334,13 +334,13 @@ static int soa_xchg_pack_t(SoaEngine* e, uint8_t* buf, const uint64_t* cap, uint
   for (u64 r = 0; r < e->C.n_rep; r++) {
     if (!owned<N>(e->C, r)) continue;
     for (u32 i = 0; i < nc; i++) cnt[i] = 0;
-    xchg_sender<N, false>(e->P, e->C, r, par, cnt.data(), nullptr, nullptr, cap);
+    xchg_sender<N, false>(e->P, e->C, r, par, e->round, cnt.data(), nullptr, nullptr, cap);
     for (u32 i = 0; i < nc; i++) {
       base[i] = counts[i];
       counts[i] += cnt[i];
       cnt[i] = 0;
     }
-    xchg_sender<N, true>(e->P, e->C, r, par, cnt.data(), base.data(), buf, cap);
+    xchg_sender<N, true>(e->P, e->C, r, par, e->round, cnt.data(), base.data(), buf, cap);
   }
   for (u32 i = 0; i < nc; i++)
     if (counts[i] > cap[i % XS_NUM]) return -3;
@@ -350,8 +350,6 @@ template <int N>
 static void soa_xchg_unpack_t(SoaEngine* e, const XCnt* c, uint64_t nc, const XMsg* m, uint64_t nm,
                               const XEnt* x, uint64_t ne) {
   const u32 par = (e->round - 1) & 1u;
-  for (u64 r = 0; r < e->C.n_rep; r++)
-    if (owned<N>(e->C, r)) xchg_clear<N>(e->P, e->C, r, par);
   for (u64 i = 0; i < nc; i++) xchg_put_cnt(e->P, e->C, par, c[i]);
   for (u64 i = 0; i < nm; i++) xchg_put_msg(e->P, e->C, par, m[i]);
   for (u64 i = 0; i < ne; i++) xchg_put_ent(e->P, e->C, par, x[i]);
@@ -379,12 +377,13 @@ extern "C" int soa_get_outbox(void* h, uint64_t replica, rbe_message* out, uint3
   const u32 N = e->C.n, par = (e->round - 1) & 1u;
   const u64 g = replica / N;
   const u32 k = (u32)(replica % N);
-  const u16* cnt = e->P.cnt[par] + g * N * N + k * N;
+  const CntRow& row = e->P.cnt[par][replica];
   const Msg* lst = e->P.msgs[par] + (g * N + k) * N * (u64)e->C.maxm;
   const Ent* arena = e->P.arena[par] + replica * e->C.ecap;
-  if (N == 3) outbox_messages<3>(e->C, g, k, cnt, lst, arena, out, cap, ents, ent_cap, n_out, n_ents);
-  else if (N == 5) outbox_messages<5>(e->C, g, k, cnt, lst, arena, out, cap, ents, ent_cap, n_out, n_ents);
-  else outbox_messages<1>(e->C, g, k, cnt, lst, arena, out, cap, ents, ent_cap, n_out, n_ents);
+  const u32 rd = e->round;
+  if (N == 3) outbox_messages<3>(e->C, g, k, row, rd, lst, arena, out, cap, ents, ent_cap, n_out, n_ents);
+  else if (N == 5) outbox_messages<5>(e->C, g, k, row, rd, lst, arena, out, cap, ents, ent_cap, n_out, n_ents);
+  else outbox_messages<1>(e->C, g, k, row, rd, lst, arena, out, cap, ents, ent_cap, n_out, n_ents);
   return RBE_OK;
 }
 template <int N>
@@ -393,7 +392,7 @@ static int soa_push_t(SoaEngine* e, uint64_t n, const uint64_t* group, const rbe
   std::vector<XCnt> c;
   std::vector<XMsg> m;
   std::vector<XEnt> x;
-  const int rc = messages_to_records<N>(e->C, n, group, msgs, ents, c, m, x);
+  const int rc = messages_to_records<N>(e->C, e->round, n, group, msgs, ents, c, m, x);
   if (rc) return rc;
   soa_xchg_unpack_t<N>(e, c.data(), c.size(), m.data(), m.size(), x.data(), x.size());
   return RBE_OK;
