@@ -166,79 +166,136 @@ __device__ __forceinline__ void list_push(const Lists& L, u32 list, u32 par, boo
   if (want) L.idx[list * L.cap + base + __popcll(mask & ((1ull << lane) - 1ull))] = r;
 }
 
-// Pass 1 over every replica: idle rounds complete here; the rest is listed.
-// A block owns kTriChunk consecutive replicas (coalesced Hot loads, 8 per
-// lane), compacts its three work lists in LDS with wave-aggregated LDS
-// atomics, then reserves space in each global list with ONE atomic per list
-// and copies its entries out coalesced.
+// Pass 1 over every group: sleeping groups and idle rounds complete here; the
+// rest is listed.  A block owns kTriGroups<N> consecutive groups (at most
+// kTriChunk replicas).  It first reads one wake byte per group (group sleep,
+// rbe_step.h) and finishes the round of every sleeping group from it; the
+// replicas of the groups left (all of them without group sleep) are triaged
+// one lane each: the block compacts its three work lists in LDS with
+// wave-aggregated LDS atomics, then reserves space in each global list with
+// ONE atomic per list and copies its entries out coalesced.  A group whose
+// replicas all completed lazily falls asleep.
+template <int N>
+constexpr u32 kTriGroups = kTriChunk / N;
 template <int N, bool TRACE>
 __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg ra, Lists L) {
+  constexpr u32 GB = kTriGroups<N>;
   __shared__ u32 s_idx[3][kTriChunk];
+  __shared__ u16 s_grp[GB];  // block-local group index | was awake << 15, of the groups triaged
+  __shared__ u32 s_gst[GB];  // per triaged group: leaders + (replicas not lazy-done) << 8
   __shared__ u32 s_n[5], s_base[5];  // fronts of lists 0..2, backs of lists 0..1
+  __shared__ u32 s_ng;
   const Clk ck = clk_of(ra);
   const u32 round = ck.round;
   const u32 par = round & 1u;
   if (blockIdx.x == 0 && threadIdx.x < 5)
     L.counts[(threadIdx.x < 3 ? threadIdx.x * 2 : 6 + (threadIdx.x - 3) * 2) + (par ^ 1u)] = 0;
   if (threadIdx.x < 5) s_n[threadIdx.x] = 0;
+  if (threadIdx.x == 0) s_ng = 0;
   __syncthreads();
   StepCounters c;
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
   const int lane = threadIdx.x & 63;
-  // The idle bytes and inbound count words of all kPer replicas a lane owns
-  // (strided by the block size, so each load is coalesced across the wave and
-  // the work lists come out in replica order) are loaded before any of them
-  // is processed; most rounds are then decided without reading Hot: a lazy
-  // quiesced tick completes here, a replica with inbound messages is listed
-  // by the role its idle byte carries.
+  const bool shortcut = !TRACE && C.quiesce;
+  const u64 g0 = (u64)blockIdx.x * GB;
+  const u32 gn = (u32)(C.n_groups - g0 < GB ? C.n_groups - g0 : GB);
+  // phase 1: one lane per group
+  for (u32 j0 = 0; j0 < GB; j0 += kBlock) {
+    const u32 j = j0 + threadIdx.x;
+    bool work = false, awake = true;
+    if (j < gn) {
+      work = true;
+      if (shortcut) {
+        const u64 g = g0 + j;
+        const u8 gw = P.gwake[g];
+        awake = (gw & GW_AWAKE) != 0;
+        if (!awake && !group_forced(C, C.cid_base + g * C.cid_stride, round)) {
+          work = false;
+          u32 own = 0;
+          for (u32 k = 0; k < (u32)N; k++) own += owned<N>(C, g * N + k) ? 1u : 0u;
+          group_sleep_round(gw, own, ck, c);
+        }
+      }
+    }
+    const u64 mask = __ballot(work);
+    if (mask) {
+      const int first = __ffsll((unsigned long long)mask) - 1;
+      u32 base = 0;
+      if (lane == first) base = atomicAdd(&s_ng, (u32)__popcll(mask));
+      base = __shfl(base, first, 64);
+      if (work) {
+        const u32 pos = base + __popcll(mask & ((1ull << lane) - 1ull));
+        s_grp[pos] = (u16)(j | (awake ? 0x8000u : 0u));
+        s_gst[pos] = 0;
+      }
+    }
+  }
+  __syncthreads();
+  // phase 2: one lane per replica of a triaged group.  The idle bytes and
+  // inbound count words of all the replicas a lane owns (strided by the block
+  // size, so each load is coalesced across the wave) are loaded before any of
+  // them is processed; most rounds are then decided without reading Hot: a
+  // lazy quiesced tick completes here, a replica with inbound messages is
+  // listed by the role its idle byte carries.
   constexpr u32 kPer = kTriChunk / kBlock;
-  const u64 lo = (u64)blockIdx.x * kTriChunk + threadIdx.x;
-  // Every load is unconditional (a replica past the end reads replica 0 and
-  // is masked afterwards) and u32 index math: no load waits behind a branch
-  // or a 64-bit division, so all 8 * (N + 1) loads of a lane are in flight
-  // before the first wait.
+  const u32 nr = s_ng * (u32)N;
+  const u32 iters = (nr + kBlock - 1) / kBlock;  // uniform over the block
+  const u32 rb = (u32)(g0 * N);
+  // Loads of items past the end read the block's first replica and are masked
+  // afterwards, and index math is u32: no load waits behind a branch or a
+  // 64-bit division, so all the loads of a lane are in flight before the
+  // first wait.
   u8 ibs[kPer];
   u16 wv[kPer][N];
-  u32 kk[kPer];
 #pragma unroll
   for (u32 i = 0; i < kPer; i++) {
-    const u64 r = lo + (u64)i * kBlock;
-    const u32 rc = r < C.n_rep ? (u32)r : 0u;
-    ibs[i] = P.idle[rc];
-    const u32 g = rc / (u32)N;
-    kk[i] = rc - g * (u32)N;
-    inbound_load<N>(P, g, kk[i], round, wv[i]);
+    if (i < iters) {
+      const u32 t = threadIdx.x + i * kBlock;
+      const u32 tc = t < nr ? t : 0u;
+      const u32 slot = tc / (u32)N, k = tc - slot * (u32)N;
+      const u32 lg = s_grp[slot] & 0x7FFFu;
+      ibs[i] = P.idle[rb + lg * (u32)N + k];
+      inbound_load<N>(P, (u32)g0 + lg, k, round, wv[i]);
+    }
   }
-  // the per-replica bytes packed into two registers, so the classification
-  // loop below runs rolled (one copy of triage_lazy / triage_replica in the
+  // the per-replica bytes packed into registers, so the classification loop
+  // below runs rolled (one copy of triage_lazy / triage_replica in the
   // instruction stream instead of kPer) without indexing a register array
   u64 ibp = 0;
   u32 inbp = 0;
-  u64 auxp[2] = {0, 0};  // kListAux: 14-bit summary words, replicas 0-3 and 4-7
+  u64 aux_lo = 0, aux_hi = 0;  // kListAux: 14-bit summary words, items 0-3 and 4-7
 #pragma unroll
   for (u32 i = 0; i < kPer; i++) {
-    const u64 r = lo + (u64)i * kBlock;
-    const bool in = r < C.n_rep;
-    ibp |= (u64)(in ? ibs[i] : (u8)0) << (8 * i);
-    inbp |= (in ? inbound_fold<N>(wv[i], kk[i], round) : 0u) << (3 * i);
-    if constexpr (kListAux<N>)
-      auxp[i / 4] |= (u64)(inbound_aux<N>(wv[i], kk[i], round) & 0x3FFFu) << (14 * (i % 4));
+    if (i < iters) {
+      const u32 t = threadIdx.x + i * kBlock;
+      const u32 k = (t < nr ? t : 0u) % (u32)N;
+      ibp |= (u64)ibs[i] << (8 * i);
+      inbp |= inbound_fold<N>(wv[i], k, round) << (3 * i);
+      if constexpr (kListAux<N>)
+        (i < 4 ? aux_lo : aux_hi) |= (u64)(inbound_aux<N>(wv[i], k, round) & 0x3FFFu)
+                                     << (14 * (i % 4));
+    }
   }
-  const bool shortcut = !TRACE && C.quiesce;
 #pragma unroll 1
-  for (u32 i = 0; i < kPer; i++) {
-    const u64 r = lo + (u64)i * kBlock;
+  for (u32 i = 0; i < iters; i++) {
+    const u32 t = threadIdx.x + i * kBlock;
+    const u32 slot = (t < nr ? t : 0u) / (u32)N;
+    const u32 lr = (s_grp[slot] & 0x7FFFu) * (u32)N + (t < nr ? t : 0u) - slot * (u32)N;
+    const u64 r = (u64)rb + lr;
     const u8 ib = (u8)(ibp >> (8 * i));
     const u32 inb = (inbp >> (3 * i)) & 7u;
     u32 cls = T_DONE;
-    if (r < C.n_rep && owned<N>(C, r)) {
+    if (t < nr && owned<N>(C, r)) {
+      bool done = false;
       if (shortcut && triage_lazy<N>(P, C, r, ck, ib, inb & 1u, c))
-        cls = T_DONE;
+        done = true;
       else if (inb & 2u)
         cls = class_of_role(idle_role(ib));
       else
         cls = triage_replica<N, TRACE>(P, C, r, ck, c);
+      if (shortcut)
+        atomicAdd(&s_gst[slot], ((ib & IB_LEAD) ? 1u : 0u) + (done ? 0u : 256u));
     }
     // the back of the list: a leader proposing this round, a follower
     // receiving a Replicate
@@ -261,8 +318,7 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
       // fast lists with kListAux: block position | summary word << 11
       u32 ent = (u32)r;
       if (kListAux<N> && li < 2)
-        ent = (u32)(r - (u64)blockIdx.x * kTriChunk) |
-              ((u32)((auxp[i / 4] >> (14 * (i % 4))) & 0x3FFFu) << 11);
+        ent = lr | ((u32)(((i < 4 ? aux_lo : aux_hi) >> (14 * (i % 4))) & 0x3FFFu) << 11);
       if (want) s_idx[li][sl < 3 ? pos : kTriChunk - 1u - pos] = ent;
     }
   }
@@ -271,8 +327,14 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
     const u32 at = threadIdx.x < 3 ? threadIdx.x * 2 + par : 6 + (threadIdx.x - 3) * 2 + par;
     s_base[threadIdx.x] = s_n[threadIdx.x] ? atomicAdd(&L.counts[at], s_n[threadIdx.x]) : 0u;
   }
+  // groups whose replicas all completed lazily fall asleep
+  if (shortcut) {
+    for (u32 j = threadIdx.x; j < s_ng; j += kBlock) {
+      const u32 st = s_gst[j], e = s_grp[j];
+      if (st < 256u && (e & 0x8000u)) P.gwake[g0 + (e & 0x7FFFu)] = group_sleep_byte(st);
+    }
+  }
   __syncthreads();
-  const u32 rb = blockIdx.x * kTriChunk;
   auto put = [&](u32 li, u64 at, u32 ent) {
     if (kListAux<N> && li < 2) {
       L.idx[li * L.cap + at] = rb + (ent & 0x7FFu);
@@ -558,12 +620,15 @@ __global__ __launch_bounds__(kBlock) void k_isolate(Planes P, Params C, u32 roun
 // Host input staged by rbe_push_* / rbe_notify_applied (rbe_host.h), one
 // launch per step that has any: records to their replicas' ExtIn slots,
 // applied indexes to the applied plane.
-__global__ __launch_bounds__(kBlock) void k_ext_scatter(Planes P, const u64* reps,
+__global__ __launch_bounds__(kBlock) void k_ext_scatter(Planes P, u32 nrep, const u64* reps,
                                                         const ExtIn* recs, u64 n,
                                                         const u64* app_rep, const u64* app_val,
                                                         u64 na) {
   const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
-  if (i < n) P.ext[reps[i]] = recs[i];
+  if (i < n) {
+    P.ext[reps[i]] = recs[i];
+    P.gwake[reps[i] / nrep] = GW_AWAKE;  // input wakes a sleeping group
+  }
   if (i < na) P.applied[app_rep[i]] = app_val[i];
 }
 
@@ -650,7 +715,7 @@ struct rbe_engine {
 static constexpr unsigned kFastGrid = 2048;  // persistent grid of k_fast_list
 static constexpr unsigned kFullGrid = 512;  // persistent grid of k_full_list: 2 waves per SIMD, its kernels' occupancy cap
 
-static constexpr int kPlaneAllocs = 19;
+static constexpr int kPlaneAllocs = 20;
 static u64 bytes_of(const Params& C, u64* parts) {
   const u64 N = C.n, G = C.n_groups, R = C.n_rep;
   u64 p[kPlaneAllocs] = {
@@ -673,6 +738,7 @@ static u64 bytes_of(const Params& C, u64* parts) {
       R * sizeof(u8),
       (u64)C.in_cap * sizeof(Ent),
       R * sizeof(u64),
+      G * sizeof(u8),
   };
   u64 t = 0;
   for (int i = 0; i < kPlaneAllocs; i++) {
@@ -770,6 +836,7 @@ static int launch_step_t(rbe_engine* e, RoundArg ra,
     if (ev) HIP_IGNORE(hipEventRecord(ev[i], e->stream));
   };
   const unsigned gt = (unsigned)((e->C.n_rep + kTriChunk - 1) / kTriChunk);
+  const unsigned gtg = (unsigned)((e->C.n_groups + kTriGroups<N> - 1) / kTriGroups<N>);
   const unsigned gs = g < kFullGrid ? g : kFullGrid;
   if (e->mode == 2) {
     mark(0);
@@ -791,7 +858,7 @@ static int launch_step_t(rbe_engine* e, RoundArg ra,
     mark(4);
   } else if (e->mode == 3) {
     mark(0);
-    hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(gt), dim3(kBlock), 0, e->stream, e->P, e->C,
+    hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(gtg), dim3(kBlock), 0, e->stream, e->P, e->C,
                        ra, e->L);
     mark(1);
     const unsigned gf = g < kFastGrid ? g : kFastGrid;
@@ -804,7 +871,7 @@ static int launch_step_t(rbe_engine* e, RoundArg ra,
     mark(4);
   } else {
     mark(0);
-    hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(gt), dim3(kBlock), 0, e->stream, e->P, e->C,
+    hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(gtg), dim3(kBlock), 0, e->stream, e->P, e->C,
                        ra, e->L);
     mark(1);
     const unsigned gf = g < kFastGrid ? g : kFastGrid;
@@ -916,6 +983,8 @@ int rbe_import_groups(rbe_engine* e, const void* buf, uint64_t bytes, uint32_t f
     HIP_OK(hipStreamSynchronize(e->stream));
     e->hin.resync_applied(app.data(), h.first * e->C.n, app.size());
   }
+  // imported groups start awake (group sleep, rbe_step.h)
+  HIP_OK(hipMemsetAsync(e->P.gwake + h.first, GW_AWAKE, h.count, e->stream));
   if (resume) {
     // the whole engine moves to the snapshot's round; the work lists of the
     // coming round start empty, as after any round (k_triage clears them)
@@ -1017,6 +1086,8 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   P.idle = (u8*)ptrs[16];
   P.in_ents = (Ent*)ptrs[17];
   P.applied = (u64*)ptrs[18];
+  P.gwake = (u8*)ptrs[19];
+  HIP_IGNORE(hipMemsetAsync(P.gwake, GW_AWAKE, C.n_groups, e->stream));  // every group starts awake
   e->hin.init(C.n_rep, C.n, C.in_cap);
   if (hipMalloc(&P.counters, kCtrWords * sizeof(u64)) != hipSuccess) {
     rbe_destroy(e);
@@ -1124,7 +1195,7 @@ static int flush_inputs(rbe_engine* e) {
                           hipMemcpyHostToDevice, e->stream));
   const u64 m = n > na ? n : na;
   hipLaunchKernelGGL(k_ext_scatter, dim3(grid_for(m)), dim3(kBlock), 0, e->stream, e->P,
-                     (const u64*)e->in_dev, (const ExtIn*)(e->in_dev + o_rec), n,
+                     e->C.n, (const u64*)e->in_dev, (const ExtIn*)(e->in_dev + o_rec), n,
                      (const u64*)(e->in_dev + o_ar), (const u64*)(e->in_dev + o_av), na);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(e->in_ev, e->stream));

@@ -201,7 +201,10 @@ struct HostInputs {
     for (u64 i = 0; i < count; i++) applied[first + i] = plane[i];
   }
   void apply_host(const Planes& P) {
-    for (size_t i = 0; i < reps.size(); i++) P.ext[reps[i]] = recs[i];
+    for (size_t i = 0; i < reps.size(); i++) {
+      P.ext[reps[i]] = recs[i];
+      P.gwake[reps[i] / n] = GW_AWAKE;  // input wakes a sleeping group
+    }
     for (size_t i = 0; i < ents.size(); i++) P.in_ents[i] = ents[i];
     for (size_t i = 0; i < app_rep.size(); i++) P.applied[app_rep[i]] = app_val[i];
   }

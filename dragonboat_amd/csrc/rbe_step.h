@@ -1919,6 +1919,37 @@ RBE_HD bool triage_lazy(const Planes& P, const Params& C, u64 r, const Clk& ck, 
   ctr.v[C_LEADER_STEPS] += (ib & IB_LEAD) ? t : 0u;
   return true;
 }
+// Group sleep (Planes::gwake, one byte per group; bench configuration: no
+// trace, Quiesce on).  A group whose owned replicas all finished a round in
+// triage_lazy falls asleep: from the next round on k_triage completes its
+// rounds from this byte alone, without loading the replicas' idle bytes or
+// outbox headers, until something wakes it.  Nothing inside the step can: a
+// lazy replica has no timer (a quiesced replica neither campaigns nor
+// heartbeats, quiesce.go / raft.go:623-629), and messages come only from the
+// group's own replicas, which are lazy too.  What wakes a group is host input
+// (k_ext_scatter / HostInputs::apply_host), an exchanged outbox header
+// (xchg_put_cnt), an import or a launch (all groups awake), and the seeded
+// workload or transfer input of a round (group_forced, checked every round).
+//   bit 0     awake
+//   bits 1-3  leaders among the group's owned replicas (while asleep)
+RBE_HD bool group_forced(const Params& C, u64 cid, u32 round) {
+  if (wl_input(C, cid, round)) return true;
+  if (C.xfer_period && round % C.xfer_period == 0)
+    for (u32 k = 0; k < C.n; k++)
+      if (xfer_input(C, cid, round, k)) return true;
+  return false;
+}
+// the round of a sleeping group: one QuiescedTick per owned replica, exactly
+// what triage_lazy counts for each of them
+RBE_HD void group_sleep_round(u8 gw, u32 n_owned, const Clk& ck, StepCounters& ctr) {
+  const u32 t = ck.tick ? 1u : 0u;
+  ctr.v[C_STEPS] += t * n_owned;
+  ctr.v[C_QUIESCED_TICKS] += t * n_owned;
+  ctr.v[C_LEADER_STEPS] += t * ((gw >> 1) & 7u);
+}
+// the byte a group that fell asleep this round keeps
+RBE_HD u8 group_sleep_byte(u32 leaders) { return (u8)(leaders << 1); }
+
 // the inbound count words of replica r in this round: bit 0 = any non-zero
 // word, bit 1 = any message (a Quiesce notice alone leaves it clear), bit 2 =
 // any Replicate.  Split in a load phase and a fold so k_triage can issue the

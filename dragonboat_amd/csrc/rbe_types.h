@@ -254,6 +254,9 @@ struct Clk {
   u32 round, tclk, tick;
 };
 
+// Planes::gwake bit 0: the group is awake (rbe_step.h, group sleep)
+enum : u8 { GW_AWAKE = 1 };
+
 // device pointers of every plane
 struct Planes {
   Hot* hot;
@@ -276,6 +279,8 @@ struct Planes {
   ExtIn* ext;         // [n_rep]
   Ent* in_ents;       // [in_cap] proposal entries pushed for the next step
   u64* applied;       // [n_rep] raft.applied from rbe_notify_applied (ext_apply)
+  u8* gwake;          // [n_groups] GW_* bits: lets k_triage skip a sleeping group whole
+                      // (rbe_step.h, group sleep)
   u64* counters;      // [C_NUM]
 };
 

@@ -127,6 +127,7 @@ RBE_HD void xchg_sender(const Planes& P, const Params& C, u64 r, u32 par, u32 ro
 
 RBE_HD void xchg_put_cnt(const Planes& P, const Params& C, u32 par, const XCnt& x) {
   P.cnt[par][x.key] = x.row;
+  P.gwake[x.key / C.n] = GW_AWAKE;  // a message wakes the destination's group
 }
 RBE_HD void xchg_put_msg(const Planes& P, const Params& C, u32 par, const XMsg& x) {
   P.msgs[par][x.key * (u64)C.maxm + x.slot] = x.m;

@@ -29,6 +29,8 @@ def lib():
         L.soa_set_staged.argtypes = [C.c_void_p, C.c_int]
         L.soa_slow_total.restype = C.c_uint64
         L.soa_slow_total.argtypes = [C.c_void_p]
+        L.soa_sleeping_groups.restype = C.c_uint64
+        L.soa_sleeping_groups.argtypes = [C.c_void_p]
         P = C.POINTER
         L.soa_get_outbox.argtypes = [C.c_void_p, C.c_uint64, P(RbeMessage), C.c_uint32,
                                      P(C.c_uint32), P(RbeEntry), C.c_uint32, P(C.c_uint32)]
@@ -85,6 +87,9 @@ class SoaCpu(NodeInputs):
 
     def slow_total(self):
         return lib().soa_slow_total(self.h)
+
+    def sleeping_groups(self):
+        return lib().soa_sleeping_groups(self.h)
 
     def __del__(self):
         if getattr(self, "h", None):

@@ -48,23 +48,45 @@ static void run_round(SoaEngine* e, bool tick = true) {
   // list → full list (k_triage / k_fast_list / k_full_list)
   StepCounters c;
   std::vector<u64> lists[3];
-  for (u64 r = 0; r < e->C.n_rep; r++) {
-    if (!owned<N>(e->C, r)) continue;
-    memset(&c, 0, sizeof(c));
-    u32 cls = T_FULL;
-    if (!e->full_only) {
-      const u8 ib = e->P.idle[r];
-      const u32 inb = inbound_bits<N>(e->P, r, e->round);
-      if (!e->C.trace && e->C.quiesce && triage_lazy<N>(e->P, e->C, r, ck, ib, inb & 1u, c))
-        cls = T_DONE;
-      else if (inb & 2u)  // messages: the role decides the list (as triage_replica would)
-        cls = class_of_role(idle_role(ib));
-      else
-        cls = e->C.trace ? triage_replica<N, true>(e->P, e->C, r, ck, c)
-                         : triage_replica<N, false>(e->P, e->C, r, ck, c);
+  const u32 n = e->C.n;
+  const bool shortcut = !e->C.trace && e->C.quiesce && !e->full_only;
+  for (u64 g = 0; g < e->C.n_groups; g++) {
+    // group sleep as k_triage runs it (rbe_step.h)
+    const u8 gw = e->P.gwake[g];
+    if (shortcut && !(gw & GW_AWAKE) &&
+        !group_forced(e->C, e->C.cid_base + g * e->C.cid_stride, e->round)) {
+      memset(&c, 0, sizeof(c));
+      u32 own = 0;
+      for (u32 k = 0; k < n; k++) own += owned<N>(e->C, g * n + k) ? 1u : 0u;
+      group_sleep_round(gw, own, ck, c);
+      for (int i = 0; i < C_NUM; i++) e->counters[i] += c.v[i];
+      continue;
     }
-    if (cls != T_DONE) lists[cls - 1].push_back(r);
-    for (int i = 0; i < C_NUM; i++) e->counters[i] += c.v[i];
+    u32 leaders = 0, busy = 0;
+    for (u64 r = g * n; r < (g + 1) * n; r++) {
+      if (!owned<N>(e->C, r)) continue;
+      memset(&c, 0, sizeof(c));
+      u32 cls = T_FULL;
+      bool done = false;
+      if (!e->full_only) {
+        const u8 ib = e->P.idle[r];
+        const u32 inb = inbound_bits<N>(e->P, r, e->round);
+        leaders += (ib & IB_LEAD) ? 1u : 0u;
+        if (!e->C.trace && e->C.quiesce && triage_lazy<N>(e->P, e->C, r, ck, ib, inb & 1u, c)) {
+          cls = T_DONE;
+          done = true;
+        } else if (inb & 2u) {  // messages: the role decides the list (as triage_replica would)
+          cls = class_of_role(idle_role(ib));
+        } else {
+          cls = e->C.trace ? triage_replica<N, true>(e->P, e->C, r, ck, c)
+                           : triage_replica<N, false>(e->P, e->C, r, ck, c);
+        }
+      }
+      busy += done ? 0u : 1u;
+      if (cls != T_DONE) lists[cls - 1].push_back(r);
+      for (int i = 0; i < C_NUM; i++) e->counters[i] += c.v[i];
+    }
+    if (shortcut && busy == 0 && (gw & GW_AWAKE)) e->P.gwake[g] = group_sleep_byte(leaders);
   }
   for (int li = 0; li < 2; li++) {
     for (u64 r : lists[li]) {
@@ -195,6 +217,8 @@ void* soa_create(const rbe_config* cfg) {
   P.ext = alloc<ExtIn>(e, R);
   P.in_ents = alloc<Ent>(e, C.in_cap);
   P.applied = alloc<u64>(e, R);
+  P.gwake = alloc<u8>(e, G);
+  memset(P.gwake, GW_AWAKE, G);  // every group starts awake
   e->hin.init(R, C.n, C.in_cap);
   P.counters = nullptr;
   for (u64 r = 0; r < R; r++) {
@@ -209,6 +233,12 @@ void soa_destroy(void* h) { delete (SoaEngine*)h; }
 void soa_set_full_only(void* h, int v) { ((SoaEngine*)h)->full_only = v != 0; }
 void soa_set_staged(void* h, int v) { ((SoaEngine*)h)->staged = v; }
 uint64_t soa_slow_total(void* h) { return ((SoaEngine*)h)->slow_total; }
+uint64_t soa_sleeping_groups(void* h) {  // groups asleep after the last round (group sleep)
+  SoaEngine* e = (SoaEngine*)h;
+  uint64_t n = 0;
+  for (u64 g = 0; g < e->C.n_groups; g++) n += (e->P.gwake[g] & GW_AWAKE) ? 0 : 1;
+  return n;
+}
 
 void soa_run(void* h, uint32_t rounds) {
   SoaEngine* e = (SoaEngine*)h;
@@ -453,6 +483,7 @@ extern "C" int soa_import_groups(void* h, const void* buf, uint64_t bytes, uint3
       memcpy(pl[i].base + row * pl[i].pitch + hd.first * pl[i].group_bytes, src, w);
   }
   e->hin.resync_applied(e->P.applied + hd.first * e->C.n, hd.first * e->C.n, hd.count * e->C.n);
+  memset(e->P.gwake + hd.first, GW_AWAKE, hd.count);  // imported groups start awake
   if (resume) {
     e->round = hd.round;
     e->tclk = (u32)hd.tclk;

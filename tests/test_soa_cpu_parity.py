@@ -56,3 +56,26 @@ def test_soa_cpu_untraced_state_parity(name):
     assert eng.faults()[0] == 0
     bad = counters_match(eng.counters(), ref.counters())
     assert not bad, f"{name}: counters differ {bad}"
+    if name == "C4":  # quiesced groups fall asleep (group sleep, rbe_step.h)
+        assert eng.sleeping_groups() > 0
+
+
+def test_sleeping_groups_wake_on_input():
+    """A sleeping group (all replicas lazily quiesced) is woken by host input
+    and steps exactly like the oracle; it falls asleep again afterwards."""
+    kw = dict(n_groups=8, n_replicas=3, quiesce=True)
+    eng = SoaCpu(trace=False, ext_inputs=True, **kw)
+    ref = O.Harness(ext_inputs=True, **kw)
+    d = run_lockstep(eng, ref, 500, every=1, skip=("digest",))
+    assert d is None, f"first divergence {d}"
+    assert eng.sleeping_groups() == 8
+    v = ref.views()
+    leaders = [i for i in range(24) if v[i].role == O.LEADER]
+    eng.push_proposals(leaders[:2], [[b"wake"]] * 2)
+    for r in leaders[:2]:
+        ref.push(O.PUSH_PROPOSE, r, entries=[O.Entry(type=0, cmd=b"wake")])
+    d = run_lockstep(eng, ref, 300, every=1, skip=("digest",))
+    assert d is None, f"after wake: first divergence {d}"
+    assert eng.sleeping_groups() == 8
+    bad = counters_match(eng.counters(), ref.counters())
+    assert not bad, f"counters differ {bad}"
