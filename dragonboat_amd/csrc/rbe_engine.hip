@@ -123,47 +123,90 @@ __global__ __launch_bounds__(kBlock) void k_step(Planes P, Params C, RoundArg ra
 }
 
 // Work lists of a round: 0 = steady-state leaders, 1 = steady-state followers,
-// 2 = full handler table.  Lists 0 and 1 fill from both ends: the front holds
-// the common case (a leader without a proposal this round, a follower without
-// a Replicate), the back the rest, so the waves of the fast launch are mostly
-// homogeneous and skip the code paths none of their lanes take.  Front counts
-// live in counts[list * 2 + parity], back counts in counts[6 + list * 2 + parity];
-// the back of list l occupies idx[l * cap + cap - 1 - j].
+// 2 = full handler table.  Each list is kShards regions, one per shard: a
+// writing block appends to the region of shard blockIdx % kShards, so the
+// returning atomics that reserve list space are spread over kShards counters
+// per list, each on its own 256-B line (one counter word saturates at ~90
+// returning atomics per µs, and k_triage's ~1.5k blocks made five such words
+// the round's critical path).  Lists 0 and 1 fill each region from both ends:
+// the front holds the common case (a leader without a proposal this round, a
+// follower without a Replicate), the back the rest, so the waves of the fast
+// launch are mostly homogeneous and skip the code paths none of their lanes
+// take.  A consumer reads the regions as one sequence of segments (seg_build /
+// seg_find): fronts of every shard, then backs.
+static constexpr u32 kShards = 8;
+static constexpr u32 kSlots = 5;   // count slots: fronts of lists 0..2, backs of lists 0..1
+static constexpr u32 kCntPad = 64;  // u32 words from one count to the next (256 B)
+static constexpr u32 kListCounts = 2 * kSlots * kShards * kCntPad;  // by parity, slot, shard
 struct Lists {
-  u32* idx;     // [3][cap] replica indices
-  u32* aux;     // [2][cap] inbound summary words of the leader / follower entries (inbound_aux)
-  u32* counts;  // [3][2] front, then [2][2] back
-  u64 cap;
+  u32* idx;     // list li, shard s: [off[li] + s * scap[li], + scap[li]) replica indices
+  u32* aux;     // lists 0 and 1, same layout: inbound summary words (inbound_aux)
+  u32* counts;  // list_cnt
+  u64 scap[3];  // entries per shard region
+  u64 off[3];   // first entry of each list
 };
 // work-list entries carry their inbound summary word for N = 3 (14 bits; the
 // LDS compaction packs it with the 11-bit block position in one u32)
 template <int N>
 constexpr bool kListAux = N == 3 && RBE_TRI_CHUNK <= 2048 && RBE_LIST_AUX;
-static constexpr u32 kListCounts = 10;
-// length of list li (front + back) and its i-th entry (front first)
-__device__ __forceinline__ u32 list_front(const Lists& L, u32 li, u32 par) {
-  return L.counts[li * 2 + par];
+__device__ __forceinline__ u32* list_cnt(const Lists& L, u32 slot, u32 par, u32 sh) {
+  return &L.counts[((par * kSlots + slot) * kShards + sh) * kCntPad];
 }
-__device__ __forceinline__ u32 list_back(const Lists& L, u32 li, u32 par) {
-  return li < 2 ? L.counts[6 + li * 2 + par] : 0u;
+// position of the j-th front (or back) entry of list li, shard sh
+__device__ __forceinline__ u64 list_pos(const Lists& L, u32 li, u32 sh, bool back, u64 j) {
+  const u64 base = L.off[li] + (u64)sh * L.scap[li];
+  return back ? base + L.scap[li] - 1 - j : base + j;
 }
-__device__ __forceinline__ u32 list_at(const Lists& L, u32 li, u32 nfront, u64 i) {
-  return i < nfront ? L.idx[li * L.cap + i] : L.idx[li * L.cap + L.cap - 1 - (i - nfront)];
+// Every thread of a block calls seg_build: the first wave loads the counts of
+// the NQ slots `slots` (all kShards shards of each, segment q * kShards + sh)
+// and leaves their exclusive prefix in s_pre[0 .. NQ * kShards].
+template <u32 NQ>
+__device__ __forceinline__ void seg_build(const Lists& L, u32 par, const u32 (&slots)[NQ],
+                                          u32* s_pre) {
+  static_assert(NQ * kShards < 64, "one wave scans the segment counts");
+  if (threadIdx.x < 64) {
+    const u32 lane = threadIdx.x;
+    u32 v = 0;
+#pragma unroll
+    for (u32 q = 0; q < NQ; q++)
+      if (lane / kShards == q) v = *list_cnt(L, slots[q], par, lane % kShards);
+#pragma unroll
+    for (u32 o = 1; o < 64; o <<= 1) {
+      const u32 t = __shfl_up(v, o, 64);
+      if (lane >= o) v += t;
+    }
+    if (lane < NQ * kShards) s_pre[lane + 1] = v;
+    if (lane == 0) s_pre[0] = 0;
+  }
+  __syncthreads();
 }
-__device__ __forceinline__ u32 list_aux_at(const Lists& L, u32 li, u32 nfront, u64 i) {
-  return i < nfront ? L.aux[li * L.cap + i] : L.aux[li * L.cap + L.cap - 1 - (i - nfront)];
+// the segment holding sequence item i (< s_pre[NSEG]): the last one starting at or before i
+template <u32 NSEG>
+__device__ __forceinline__ u32 seg_find(const u32* s_pre, u32 i) {
+  u32 lo = 0;
+#pragma unroll
+  for (u32 step = 32; step; step >>= 1)
+    if (lo + step < NSEG && s_pre[lo + step] <= i) lo += step;
+  return lo;
 }
 
-// wave-aggregated append: one atomic per wave and list
+// wave-aggregated append to the front of list `list`: one atomic per wave
 __device__ __forceinline__ void list_push(const Lists& L, u32 list, u32 par, bool want, u32 r) {
   const u64 mask = __ballot(want);
   if (!mask) return;
   const int lane = threadIdx.x & 63;
   const int first = __ffsll((unsigned long long)mask) - 1;
+  const u32 sh = blockIdx.x % kShards;
   u32 base = 0;
-  if (lane == first) base = atomicAdd(&L.counts[list * 2 + par], (u32)__popcll(mask));
+  if (lane == first) base = atomicAdd(list_cnt(L, list, par, sh), (u32)__popcll(mask));
   base = __shfl(base, first, 64);
-  if (want) L.idx[list * L.cap + base + __popcll(mask & ((1ull << lane) - 1ull))] = r;
+  if (want) L.idx[list_pos(L, list, sh, false, base + __popcll(mask & ((1ull << lane) - 1ull)))] = r;
+}
+// the next round's counts (other parity) start at zero: block 0 of the
+// round's first kernel clears count slots [0, nslots)
+__device__ __forceinline__ void list_clear_next(const Lists& L, u32 par, u32 nslots) {
+  if (blockIdx.x == 0 && threadIdx.x < nslots * kShards)
+    *list_cnt(L, threadIdx.x / kShards, par ^ 1u, threadIdx.x % kShards) = 0;
 }
 
 // Pass 1 over every group: sleeping groups and idle rounds complete here; the
@@ -188,8 +231,7 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
   const Clk ck = clk_of(ra);
   const u32 round = ck.round;
   const u32 par = round & 1u;
-  if (blockIdx.x == 0 && threadIdx.x < 5)
-    L.counts[(threadIdx.x < 3 ? threadIdx.x * 2 : 6 + (threadIdx.x - 3) * 2) + (par ^ 1u)] = 0;
+  list_clear_next(L, par, kSlots);
   if (threadIdx.x < 5) s_n[threadIdx.x] = 0;
   if (threadIdx.x == 0) s_ng = 0;
   __syncthreads();
@@ -200,23 +242,25 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
   const bool shortcut = !TRACE && C.quiesce;
   const u64 g0 = (u64)blockIdx.x * GB;
   const u32 gn = (u32)(C.n_groups - g0 < GB ? C.n_groups - g0 : GB);
-  // phase 1: one lane per group
-  for (u32 j0 = 0; j0 < GB; j0 += kBlock) {
-    const u32 j = j0 + threadIdx.x;
-    bool work = false, awake = true;
-    if (j < gn) {
-      work = true;
-      if (shortcut) {
-        const u64 g = g0 + j;
-        const u8 gw = P.gwake[g];
-        awake = (gw & GW_AWAKE) != 0;
-        if (!awake && !group_forced(C, C.cid_base + g * C.cid_stride, round)) {
-          work = false;
-          u32 own = 0;
-          for (u32 k = 0; k < (u32)N; k++) own += owned<N>(C, g * N + k) ? 1u : 0u;
-          group_sleep_round(gw, own, ck, c);
-        }
-      }
+  // phase 1: one lane per group, every wake byte loaded before any is used
+  constexpr u32 kP1 = (GB + kBlock - 1) / kBlock;
+  u8 gws[kP1];
+#pragma unroll
+  for (u32 i = 0; i < kP1; i++) {
+    const u32 j = threadIdx.x + i * kBlock;
+    gws[i] = shortcut ? P.gwake[g0 + (j < gn ? j : 0u)] : (u8)GW_AWAKE;
+  }
+#pragma unroll
+  for (u32 i = 0; i < kP1; i++) {
+    const u32 j = threadIdx.x + i * kBlock;
+    const u64 g = g0 + j;
+    const bool awake = (gws[i] & GW_AWAKE) != 0;
+    bool work = j < gn;
+    if (work && !awake && !group_forced(C, C.cid_base + g * C.cid_stride, round)) {
+      work = false;
+      u32 own = 0;
+      for (u32 k = 0; k < (u32)N; k++) own += owned<N>(C, g * N + k) ? 1u : 0u;
+      group_sleep_round(gws[i], own, ck, c);
     }
     const u64 mask = __ballot(work);
     if (mask) {
@@ -323,10 +367,10 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
     }
   }
   __syncthreads();
-  if (threadIdx.x < 5) {
-    const u32 at = threadIdx.x < 3 ? threadIdx.x * 2 + par : 6 + (threadIdx.x - 3) * 2 + par;
-    s_base[threadIdx.x] = s_n[threadIdx.x] ? atomicAdd(&L.counts[at], s_n[threadIdx.x]) : 0u;
-  }
+  const u32 sh = blockIdx.x % kShards;
+  if (threadIdx.x < 5)
+    s_base[threadIdx.x] =
+        s_n[threadIdx.x] ? atomicAdd(list_cnt(L, threadIdx.x, par, sh), s_n[threadIdx.x]) : 0u;
   // groups whose replicas all completed lazily fall asleep
   if (shortcut) {
     for (u32 j = threadIdx.x; j < s_ng; j += kBlock) {
@@ -337,19 +381,20 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
   __syncthreads();
   auto put = [&](u32 li, u64 at, u32 ent) {
     if (kListAux<N> && li < 2) {
-      L.idx[li * L.cap + at] = rb + (ent & 0x7FFu);
-      L.aux[li * L.cap + at] = ent >> 11;
+      L.idx[at] = rb + (ent & 0x7FFu);
+      L.aux[at] = ent >> 11;
     } else {
-      L.idx[li * L.cap + at] = ent;
+      L.idx[at] = ent;
     }
   };
 #pragma unroll
   for (u32 li = 0; li < 3; li++)
-    for (u32 j = threadIdx.x; j < s_n[li]; j += kBlock) put(li, s_base[li] + j, s_idx[li][j]);
+    for (u32 j = threadIdx.x; j < s_n[li]; j += kBlock)
+      put(li, list_pos(L, li, sh, false, s_base[li] + j), s_idx[li][j]);
 #pragma unroll
   for (u32 li = 0; li < 2; li++)
     for (u32 j = threadIdx.x; j < s_n[3 + li]; j += kBlock)
-      put(li, L.cap - 1 - (s_base[3 + li] + j), s_idx[li][kTriChunk - 1u - j]);
+      put(li, list_pos(L, li, sh, true, s_base[3 + li] + j), s_idx[li][kTriChunk - 1u - j]);
   flush_counters<KS_TRIAGE>(P, c);
 }
 
@@ -367,7 +412,7 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_round(Planes P, Para
   const Clk ck = clk_of(ra);
   const u32 round = ck.round;
   const u32 par = round & 1u;
-  if (blockIdx.x == 0 && threadIdx.x == 0) L.counts[2 * 2 + (par ^ 1u)] = 0;
+  list_clear_next(L, par, 3);  // slot 2: the full list
   if (threadIdx.x == 0) s_nl = s_nf = 0;
   __syncthreads();
   StepCounters c;
@@ -419,7 +464,10 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_list(Planes P, 
   const u32 round = ck.round;
   const u32 par = round & 1u;
   const u32 li = MODE == MODE_LEAD ? 0u : 1u;
-  const u32 nfront = list_front(L, li, par), n = nfront + list_back(L, li, par);
+  __shared__ u32 s_pre[2 * kShards + 1];
+  const u32 slots[2] = {li, 3 + li};
+  seg_build<2>(L, par, slots, s_pre);
+  const u32 n = s_pre[2 * kShards];
   StepCounters c;
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
@@ -429,7 +477,8 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_list(Planes P, 
     bool slow = false;
     u32 r = 0;
     if (i < n) {
-      r = list_at(L, li, nfront, i);
+      const u32 sg = seg_find<2 * kShards>(s_pre, (u32)i);
+      r = L.idx[list_pos(L, li, sg % kShards, sg >= kShards, (u32)i - s_pre[sg])];
       slow = !step_fast<N, TRACE, MODE>(P, C, r, ck, c);
     }
     list_push(L, 2, par, slow, r);
@@ -546,8 +595,11 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, 
   const Clk ck = clk_of(ra);
   const u32 round = ck.round;
   const u32 par = round & 1u;
-  const u32 nlf = list_front(L, 0, par), nl = nlf + list_back(L, 0, par);
-  const u32 nff = list_front(L, 1, par), n = nl + nff + list_back(L, 1, par);
+  // segments: leader fronts, leader backs, follower fronts, follower backs
+  __shared__ u32 s_pre[4 * kShards + 1];
+  const u32 slots[4] = {0, 3, 1, 4};
+  seg_build<4>(L, par, slots, s_pre);
+  const u32 nl = s_pre[2 * kShards], n = s_pre[4 * kShards];
   StepCounters c;
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
@@ -558,12 +610,12 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, 
     const u64 i = i0 + threadIdx.x;
     const bool lead = i < nl, any = i < n;
     u32 r = 0, aux = 0;
-    if (lead) {
-      r = list_at(L, 0, nlf, i);
-      if constexpr (kListAux<N>) aux = list_aux_at(L, 0, nlf, i);
-    } else if (any) {
-      r = list_at(L, 1, nff, i - nl);
-      if constexpr (kListAux<N>) aux = list_aux_at(L, 1, nff, i - nl);
+    if (any) {
+      const u32 sg = seg_find<4 * kShards>(s_pre, (u32)i);
+      const u64 at = list_pos(L, sg / (2 * kShards), sg % kShards, (sg / kShards) & 1u,
+                              (u32)i - s_pre[sg]);
+      r = L.idx[at];
+      if constexpr (kListAux<N>) aux = L.aux[at];
     }
     const u64 m_any = __ballot(any), m_lead = __ballot(lead);
     bool ok = false;
@@ -596,12 +648,17 @@ template <int N, bool TRACE>
 __global__ __launch_bounds__(kBlock) void k_full_list(Planes P, Params C, RoundArg ra, Lists L) {
   const Clk ck = clk_of(ra);
   const u32 round = ck.round;
-  const u32 n = L.counts[2 * 2 + (round & 1u)];
+  __shared__ u32 s_pre[kShards + 1];
+  const u32 slots[1] = {2};
+  seg_build<1>(L, round & 1u, slots, s_pre);
+  const u32 n = s_pre[kShards];
   StepCounters c;
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
-  for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock)
-    step_replica<N, TRACE>(P, C, L.idx[2 * L.cap + i], ck, c);
+  for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock) {
+    const u32 sg = seg_find<kShards>(s_pre, (u32)i);
+    step_replica<N, TRACE>(P, C, L.idx[list_pos(L, 2, sg, false, (u32)i - s_pre[sg])], ck, c);
+  }
   flush_counters<KS_FULL>(P, c);
 }
 
@@ -1113,9 +1170,20 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
     rbe_destroy(e);
     return RBE_E_INVALID;  // list entries are 32-bit replica indices
   }
-  e->L.cap = C.n_rep;
-  if (hipMalloc(&e->L.idx, 3 * C.n_rep * sizeof(u32)) != hipSuccess ||
-      hipMalloc(&e->L.aux, 2 * C.n_rep * sizeof(u32)) != hipSuccess ||
+  {
+    // lists 0 and 1 come from k_triage alone: a shard's region holds the
+    // replicas of its blocks; list 2 takes pushes from every pipeline kernel,
+    // so any shard may get any replica (each at most once per round)
+    const u64 gpb = kTriChunk / C.n, nblk = (C.n_groups + gpb - 1) / gpb;
+    const u64 per = (nblk + kShards - 1) / kShards * gpb * C.n;
+    e->L.scap[0] = e->L.scap[1] = per;
+    e->L.scap[2] = C.n_rep;
+    e->L.off[0] = 0;
+    e->L.off[1] = kShards * per;
+    e->L.off[2] = 2 * kShards * per;
+  }
+  if (hipMalloc(&e->L.idx, (e->L.off[2] + kShards * C.n_rep) * sizeof(u32)) != hipSuccess ||
+      hipMalloc(&e->L.aux, e->L.off[2] * sizeof(u32)) != hipSuccess ||
       hipMalloc(&e->L.counts, kListCounts * sizeof(u32)) != hipSuccess) {
     rbe_destroy(e);
     return RBE_E_NOMEM;
