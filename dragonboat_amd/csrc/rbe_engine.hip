@@ -214,25 +214,31 @@ __device__ __forceinline__ void list_clear_next(const Lists& L, u32 par, u32 nsl
 // kTriChunk replicas).  It first reads one wake byte per group (group sleep,
 // rbe_step.h) and finishes the round of every sleeping group from it; the
 // replicas of the groups left (all of them without group sleep) are triaged
-// one lane each: the block compacts its three work lists in LDS with
-// wave-aggregated LDS atomics, then reserves space in each global list with
-// ONE atomic per list and copies its entries out coalesced.  A group whose
-// replicas all completed lazily falls asleep.
+// one lane each.  Each listed replica takes a position in one of five slots
+// (fronts of lists 0..2, backs of lists 0..1) from a wave-aggregated LDS
+// atomic; the block then reserves space in each global list with ONE atomic
+// per slot, lays the slots out back to back in one LDS array and copies them
+// out coalesced.  A group whose replicas all completed lazily falls asleep.
+// LDS stays near 11 KB, so every block of a 1M-group round is resident at
+// once (occupancy is set by registers, not LDS).
 template <int N>
 constexpr u32 kTriGroups = kTriChunk / N;
 template <int N, bool TRACE>
 __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg ra, Lists L) {
   constexpr u32 GB = kTriGroups<N>;
-  __shared__ u32 s_idx[3][kTriChunk];
-  __shared__ u16 s_grp[GB];  // block-local group index | was awake << 15, of the groups triaged
-  __shared__ u32 s_gst[GB];  // per triaged group: leaders + (replicas not lazy-done) << 8
-  __shared__ u32 s_n[5], s_base[5];  // fronts of lists 0..2, backs of lists 0..1
+  constexpr u32 kNone = 7u;  // slot code of a replica that is not listed
+  __shared__ u32 s_idx[kTriChunk];
+  // per triaged group: (block-local group | was awake << 15) << 16 | leaders +
+  // (replicas not lazy-done) << 8
+  __shared__ u32 s_gst[GB];
+  __shared__ u32 s_n[kSlots], s_base[kSlots], s_off[kSlots];
   __shared__ u32 s_ng;
   const Clk ck = clk_of(ra);
+  RBE_STAMP(tt0);
   const u32 round = ck.round;
   const u32 par = round & 1u;
   list_clear_next(L, par, kSlots);
-  if (threadIdx.x < 5) s_n[threadIdx.x] = 0;
+  if (threadIdx.x < kSlots) s_n[threadIdx.x] = 0;
   if (threadIdx.x == 0) s_ng = 0;
   __syncthreads();
   StepCounters c;
@@ -268,24 +274,29 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
       u32 base = 0;
       if (lane == first) base = atomicAdd(&s_ng, (u32)__popcll(mask));
       base = __shfl(base, first, 64);
-      if (work) {
-        const u32 pos = base + __popcll(mask & ((1ull << lane) - 1ull));
-        s_grp[pos] = (u16)(j | (awake ? 0x8000u : 0u));
-        s_gst[pos] = 0;
-      }
+      if (work)
+        s_gst[base + __popcll(mask & ((1ull << lane) - 1ull))] = (j | (awake ? 0x8000u : 0u)) << 16;
     }
   }
   __syncthreads();
-  // phase 2: one lane per replica of a triaged group.  The idle bytes and
-  // inbound count words of all the replicas a lane owns (strided by the block
-  // size, so each load is coalesced across the wave) are loaded before any of
-  // them is processed; most rounds are then decided without reading Hot: a
-  // lazy quiesced tick completes here, a replica with inbound messages is
-  // listed by the role its idle byte carries.
+  RBE_STAMP(tt1);
+  // phase 2: one lane per replica of a triaged group (item t: group slot t / N,
+  // replica t % N).  The idle bytes and inbound count words of all the items
+  // a lane owns (strided by the block size, so each load is coalesced across
+  // the wave) are loaded before any of them is processed; most rounds are then
+  // decided without reading Hot: a lazy quiesced tick completes here, a
+  // replica with inbound messages is listed by the role its idle byte carries.
   constexpr u32 kPer = kTriChunk / kBlock;
   const u32 nr = s_ng * (u32)N;
   const u32 iters = (nr + kBlock - 1) / kBlock;  // uniform over the block
   const u32 rb = (u32)(g0 * N);
+  // block-local replica index of item t (items past the end map to item 0)
+  auto item_lr = [&](u32 t, u32* slot_out) -> u32 {
+    const u32 tc = t < nr ? t : 0u;
+    const u32 slot = tc / (u32)N;
+    *slot_out = slot;
+    return ((s_gst[slot] >> 16) & 0x7FFFu) * (u32)N + (tc - slot * (u32)N);
+  };
   // Loads of items past the end read the block's first replica and are masked
   // afterwards, and index math is u32: no load waits behind a branch or a
   // 64-bit division, so all the loads of a lane are in flight before the
@@ -295,12 +306,11 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
 #pragma unroll
   for (u32 i = 0; i < kPer; i++) {
     if (i < iters) {
-      const u32 t = threadIdx.x + i * kBlock;
-      const u32 tc = t < nr ? t : 0u;
-      const u32 slot = tc / (u32)N, k = tc - slot * (u32)N;
-      const u32 lg = s_grp[slot] & 0x7FFFu;
-      ibs[i] = P.idle[rb + lg * (u32)N + k];
-      inbound_load<N>(P, (u32)g0 + lg, k, round, wv[i]);
+      u32 slot;
+      const u32 lr = item_lr(threadIdx.x + i * kBlock, &slot);
+      const u32 k = lr % (u32)N;
+      ibs[i] = P.idle[rb + lr];
+      inbound_load<N>(P, (u32)(g0 + lr / (u32)N), k, round, wv[i]);
     }
   }
   // the per-replica bytes packed into registers, so the classification loop
@@ -321,12 +331,14 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
                                      << (14 * (i % 4));
     }
   }
+  RBE_STAMP(tt2);
+  // per item: slot code (3 bits) | position in the slot (11 bits), items 0-3 and 4-7
+  u64 sp_lo = 0, sp_hi = 0;
 #pragma unroll 1
   for (u32 i = 0; i < iters; i++) {
     const u32 t = threadIdx.x + i * kBlock;
-    const u32 slot = (t < nr ? t : 0u) / (u32)N;
-    const u32 lr = (s_grp[slot] & 0x7FFFu) * (u32)N + (t < nr ? t : 0u) - slot * (u32)N;
-    const u64 r = (u64)rb + lr;
+    u32 slot;
+    const u64 r = (u64)rb + item_lr(t, &slot);
     const u8 ib = (u8)(ibp >> (8 * i));
     const u32 inb = (inbp >> (3 * i)) & 7u;
     u32 cls = T_DONE;
@@ -338,8 +350,7 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
         cls = class_of_role(idle_role(ib));
       else
         cls = triage_replica<N, TRACE>(P, C, r, ck, c);
-      if (shortcut)
-        atomicAdd(&s_gst[slot], ((ib & IB_LEAD) ? 1u : 0u) + (done ? 0u : 256u));
+      if (shortcut) atomicAdd(&s_gst[slot], ((ib & IB_LEAD) ? 1u : 0u) + (done ? 0u : 256u));
     }
     // the back of the list: a leader proposing this round, a follower
     // receiving a Replicate
@@ -348,54 +359,81 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
       back = wl_input(C, C.cid_base + (u64)((u32)r / (u32)N) * C.cid_stride, round) == 1u;
     else if (cls == T_FOLL)
       back = (inb & 4u) != 0;
+    const u32 code = cls == T_DONE ? kNone : (back ? cls + 2u : cls - 1u);
+    u32 pos = 0;
 #pragma unroll
-    for (u32 sl = 0; sl < 5; sl++) {  // slots: fronts 0..2, backs of lists 0..1
-      const u32 li = sl < 3 ? sl : sl - 3;
-      const bool want = cls == li + 1 && back == (sl >= 3);
+    for (u32 sl = 0; sl < kSlots; sl++) {
+      const bool want = code == sl;
       const u64 mask = __ballot(want);
       if (!mask) continue;
       const int first = __ffsll((unsigned long long)mask) - 1;
       u32 base = 0;
       if (lane == first) base = atomicAdd(&s_n[sl], (u32)__popcll(mask));
       base = __shfl(base, first, 64);
-      const u32 pos = base + __popcll(mask & ((1ull << lane) - 1ull));
-      // fast lists with kListAux: block position | summary word << 11
-      u32 ent = (u32)r;
-      if (kListAux<N> && li < 2)
-        ent = lr | ((u32)(((i < 4 ? aux_lo : aux_hi) >> (14 * (i % 4))) & 0x3FFFu) << 11);
-      if (want) s_idx[li][sl < 3 ? pos : kTriChunk - 1u - pos] = ent;
+      if (want) pos = base + __popcll(mask & ((1ull << lane) - 1ull));
     }
+    (i < 4 ? sp_lo : sp_hi) |= (u64)(code | (pos << 3)) << (14 * (i % 4));
   }
   __syncthreads();
   const u32 sh = blockIdx.x % kShards;
-  if (threadIdx.x < 5)
-    s_base[threadIdx.x] =
-        s_n[threadIdx.x] ? atomicAdd(list_cnt(L, threadIdx.x, par, sh), s_n[threadIdx.x]) : 0u;
+  if (threadIdx.x < kSlots) {
+    const u32 n = s_n[threadIdx.x];
+    s_base[threadIdx.x] = n ? atomicAdd(list_cnt(L, threadIdx.x, par, sh), n) : 0u;
+    u32 off = 0;
+    for (u32 q = 0; q < threadIdx.x; q++) off += s_n[q];
+    s_off[threadIdx.x] = off;
+  }
   // groups whose replicas all completed lazily fall asleep
   if (shortcut) {
     for (u32 j = threadIdx.x; j < s_ng; j += kBlock) {
-      const u32 st = s_gst[j], e = s_grp[j];
-      if (st < 256u && (e & 0x8000u)) P.gwake[g0 + (e & 0x7FFFu)] = group_sleep_byte(st);
+      const u32 st = s_gst[j];
+      if ((st & 0xFF00u) == 0 && (st >> 31))
+        P.gwake[g0 + ((st >> 16) & 0x7FFFu)] = group_sleep_byte(st & 0xFFu);
     }
   }
   __syncthreads();
-  auto put = [&](u32 li, u64 at, u32 ent) {
-    if (kListAux<N> && li < 2) {
-      L.idx[at] = rb + (ent & 0x7FFu);
-      L.aux[at] = ent >> 11;
-    } else {
-      L.idx[at] = ent;
+  RBE_STAMP(tt3);
+  // the slots back to back in s_idx; fast-list entries with kListAux carry
+  // block position | summary word << 11
+#pragma unroll 1
+  for (u32 i = 0; i < iters; i++) {
+    const u32 t = threadIdx.x + i * kBlock;
+    const u32 e = (u32)(((i < 4 ? sp_lo : sp_hi) >> (14 * (i % 4))) & 0x3FFFu);
+    const u32 code = e & 7u;
+    if (code == kNone) continue;
+    u32 slot;
+    const u32 lr = item_lr(t, &slot);
+    u32 ent = rb + lr;
+    if (kListAux<N> && code != 2u)
+      ent = lr | ((u32)(((i < 4 ? aux_lo : aux_hi) >> (14 * (i % 4))) & 0x3FFFu) << 11);
+    s_idx[s_off[code] + (e >> 3)] = ent;
+  }
+  __syncthreads();
+  RBE_STAMP(tt4);
+#pragma unroll
+  for (u32 sl = 0; sl < kSlots; sl++) {
+    const u32 li = sl < 3 ? sl : sl - 3;
+    for (u32 j = threadIdx.x; j < s_n[sl]; j += kBlock) {
+      const u32 ent = s_idx[s_off[sl] + j];
+      const u64 at = list_pos(L, li, sh, sl >= 3, s_base[sl] + j);
+      if (kListAux<N> && li < 2) {
+        L.idx[at] = rb + (ent & 0x7FFu);
+        L.aux[at] = ent >> 11;
+      } else {
+        L.idx[at] = ent;
+      }
     }
-  };
-#pragma unroll
-  for (u32 li = 0; li < 3; li++)
-    for (u32 j = threadIdx.x; j < s_n[li]; j += kBlock)
-      put(li, list_pos(L, li, sh, false, s_base[li] + j), s_idx[li][j]);
-#pragma unroll
-  for (u32 li = 0; li < 2; li++)
-    for (u32 j = threadIdx.x; j < s_n[3 + li]; j += kBlock)
-      put(li, list_pos(L, li, sh, true, s_base[3 + li] + j), s_idx[li][kTriChunk - 1u - j]);
+  }
+  RBE_STAMP(tt5);
   flush_counters<KS_TRIAGE>(P, c);
+  RBE_STAMP(tt6);
+  RBE_PHASE_ADD(2, 0, tt0, tt1);
+  RBE_PHASE_ADD(2, 1, tt1, tt2);
+  RBE_PHASE_ADD(2, 2, tt2, tt3);
+  RBE_PHASE_ADD(2, 3, tt3, tt4);
+  RBE_PHASE_ADD(2, 4, tt4, tt5);
+  RBE_PHASE_ADD(2, 5, tt5, tt6);
+  RBE_PHASE_ADD(2, 7, 0ull, 1ull);
 }
 
 // The fused round (default pipeline): a block triages kTriChunk consecutive
@@ -1442,10 +1480,10 @@ int rbe_notify_applied(rbe_engine* e, uint64_t n, const uint64_t* replica,
 
 #ifdef RBE_PHASE_TIMING
 // diagnostic build: read and clear the per-phase stamp sums (rbe_fast.h)
-int rbe_debug_phases(uint64_t* out16) {
-  unsigned long long h[16];
+int rbe_debug_phases(uint64_t* out24) {
+  unsigned long long h[24];
   HIP_OK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)));
-  for (int i = 0; i < 16; i++) out16[i] = h[i];
+  for (int i = 0; i < 24; i++) out24[i] = h[i];
   memset(h, 0, sizeof(h));
   HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), h, sizeof(h)));
   return RBE_OK;

@@ -33,7 +33,7 @@ namespace rbe {
 // Diagnostic build only (-DRBE_PHASE_TIMING, scripts/phase_timing.sh): per-wave
 // s_memtime stamps between the phases of the fast steps, summed per phase.
 #if defined(RBE_PHASE_TIMING) && (defined(__HIPCC__) || defined(__HIP__))
-__device__ unsigned long long g_phase[2][8];
+__device__ unsigned long long g_phase[3][8];  // leader, follower, k_triage
 #endif
 #if defined(RBE_PHASE_TIMING) && defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ unsigned long long rbe_stamp() {
