@@ -9,6 +9,7 @@
 // advance when no per-round host work is needed.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -805,6 +806,7 @@ struct rbe_engine {
   u8* in_dev = nullptr;      // its device copy (replicas, records, applied pairs)
   u64 in_bytes = 0;          // capacity of both
   hipEvent_t in_ev = nullptr;  // the last upload out of in_pinned has finished
+  u8* heap = nullptr;        // payload heap (cfg.heap_bytes; positions in hin.heap)
 };
 
 static constexpr unsigned kFastGrid = 2048;  // persistent grid of k_fast_list
@@ -896,8 +898,11 @@ static int make_params(const rbe_config* cfg, Params* out) {
   if (cfg->n_groups > 0xFFFFFFFFull && !cfg->in_cap) C.in_cap = 0xFFFFFFFFu;
   C.xfer_period = cfg->xfer_period;
   C.xfer_mod = cfg->xfer_mod;
-  // not yet on the device: snapshots/compaction and the payload heap
-  if (cfg->snapshot_entries || cfg->compaction_overhead || cfg->heap_bytes) return RBE_E_INVALID;
+  // not yet on the device: snapshots/compaction
+  if (cfg->snapshot_entries || cfg->compaction_overhead) return RBE_E_INVALID;
+  // the payload heap holds host-pushed Cmds longer than 16 bytes
+  C.heap_bytes = (cfg->heap_bytes + 255) & ~255ull;
+  if (C.heap_bytes && !C.ext_inputs) return RBE_E_INVALID;
   *out = C;
   return RBE_OK;
 }
@@ -1097,7 +1102,7 @@ int rbe_footprint(const rbe_config* cfg, uint64_t* bytes) {
   Params C;
   int rc = make_params(cfg, &C);
   if (rc) return rc;
-  *bytes = bytes_of(C, nullptr);
+  *bytes = bytes_of(C, nullptr) + C.heap_bytes;
   return RBE_OK;
 }
 
@@ -1183,7 +1188,14 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   P.applied = (u64*)ptrs[18];
   P.gwake = (u8*)ptrs[19];
   HIP_IGNORE(hipMemsetAsync(P.gwake, GW_AWAKE, C.n_groups, e->stream));  // every group starts awake
-  e->hin.init(C.n_rep, C.n, C.in_cap);
+  e->hin.init(C.n_rep, C.n, C.in_cap, C.heap_bytes);
+  if (C.heap_bytes) {
+    if (hipMalloc(&e->heap, C.heap_bytes) != hipSuccess) {
+      rbe_destroy(e);
+      return RBE_E_NOMEM;
+    }
+    e->allocs.push_back(e->heap);
+  }
   if (hipMalloc(&P.counters, kCtrWords * sizeof(u64)) != hipSuccess) {
     rbe_destroy(e);
     return RBE_E_NOMEM;
@@ -1268,6 +1280,14 @@ static int launch_iso(rbe_engine* e) {
 static int flush_inputs(rbe_engine* e) {
   HostInputs& h = e->hin;
   if (h.empty()) return RBE_OK;
+  // payload heap bytes of the staged proposals: positions [flushed, head),
+  // split where they cross the end of the ring
+  for (u64 p = h.heap.flushed; p < h.heap.head;) {
+    const u64 at = p % h.heap.cap, len = std::min(h.heap.head - p, h.heap.cap - at);
+    HIP_OK(hipMemcpyAsync(e->heap + at, h.heap.stage.data() + (p - h.heap.flushed), len,
+                          hipMemcpyHostToDevice, e->stream));
+    p += len;
+  }
   const u64 n = h.reps.size(), na = h.app_rep.size();
   const u64 need = n * (sizeof(u64) + sizeof(ExtIn)) + na * 2 * sizeof(u64) + 64;
   HIP_OK(hipEventSynchronize(e->in_ev));  // the previous upload is out of in_pinned
@@ -1305,9 +1325,10 @@ static int flush_inputs(rbe_engine* e) {
                      (const u64*)(e->in_dev + o_ar), (const u64*)(e->in_dev + o_av), na);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(e->in_ev, e->stream));
-  // the entries came from pageable memory: wait for that copy before the
-  // vectors are reused (inputs are the host-driven path, not the bench path)
-  if (!h.ents.empty()) HIP_OK(hipEventSynchronize(e->in_ev));
+  // the entries and heap bytes came from pageable memory: wait for those
+  // copies before the vectors are reused (inputs are the host-driven path, not
+  // the bench path)
+  if (!h.ents.empty() || !h.heap.stage.empty()) HIP_OK(hipEventSynchronize(e->in_ev));
   h.clear();
   return RBE_OK;
 }
@@ -1796,27 +1817,90 @@ int rbe_get_ready_to_reads(rbe_engine* e, uint64_t replica, rbe_ready_to_read* o
   return RBE_OK;
 }
 
-int rbe_get_entries(rbe_engine* e, uint64_t replica, uint64_t lo, uint64_t hi, rbe_entry* out) {
-  if (!e || !out || replica >= e->C.n_rep || lo == 0 || hi < lo) return RBE_E_INVALID;
+// Terms and bodies of entries [lo, hi] of one replica's log window, read on
+// the engine stream after every queued round.
+static int read_window(rbe_engine* e, u64 replica, u64 lo, u64 hi, std::vector<u64>& t,
+                       std::vector<Body>& b) {
+  if (replica >= e->C.n_rep || lo == 0 || hi < lo) return RBE_E_INVALID;
   HIP_OK(hipSetDevice(e->device));
   Core c;
-  HIP_OK(hipMemcpy(&c, e->P.core + replica, sizeof(c), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpyAsync(&c, e->P.core + replica, sizeof(c), hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
   if (hi > c.last_index || c.last_index - lo >= e->C.ring) return RBE_E_INVALID;
+  t.resize(hi - lo + 1);
+  b.resize(hi - lo + 1);
   for (u64 i = lo; i <= hi; i++) {
-    u64 slot = (i & (u64)(e->C.ring - 1)) * e->C.n_rep + replica;
-    u64 t;
-    Body b;
-    HIP_OK(hipMemcpy(&t, e->P.term_ring + slot, sizeof(t), hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(&b, e->P.pay_ring + slot, sizeof(b), hipMemcpyDeviceToHost));
+    const u64 slot = (i & (u64)(e->C.ring - 1)) * e->C.n_rep + replica;
+    HIP_OK(hipMemcpyAsync(&t[i - lo], e->P.term_ring + slot, sizeof(u64), hipMemcpyDeviceToHost,
+                          e->stream));
+    HIP_OK(hipMemcpyAsync(&b[i - lo], e->P.pay_ring + slot, sizeof(Body), hipMemcpyDeviceToHost,
+                          e->stream));
+  }
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return RBE_OK;
+}
+
+// Copy `len` heap bytes at absolute position `pos` (RBE_E_STATE once a later
+// lap of the ring has overwritten them).
+static int read_heap(rbe_engine* e, u64 pos, u64 len, u8* dst) {
+  if (!e->hin.heap.valid(pos, len)) return RBE_E_STATE;
+  HIP_OK(hipMemcpyAsync(dst, e->heap + pos % e->hin.heap.cap, len, hipMemcpyDeviceToHost,
+                        e->stream));
+  return RBE_OK;
+}
+
+int rbe_get_entries(rbe_engine* e, uint64_t replica, uint64_t lo, uint64_t hi, rbe_entry* out) {
+  if (!e || !out) return RBE_E_INVALID;
+  std::vector<u64> t;
+  std::vector<Body> b;
+  int rc = read_window(e, replica, lo, hi, t, b);
+  if (rc) return rc;
+  for (u64 i = lo; i <= hi; i++) {
+    const Body& x = b[i - lo];
     rbe_entry& o = out[i - lo];
     memset(&o, 0, sizeof(o));
     o.index = i;
-    o.term = t;
-    o.type = b.type;
-    o.cmd_len = b.len;
-    memcpy(o.cmd, &b.lo, 8);
-    memcpy(o.cmd + 8, &b.hi, 8);
+    o.term = t[i - lo];
+    o.type = x.type;
+    o.cmd_len = x.len;
+    if (x.len <= 16) {
+      memcpy(o.cmd, &x.lo, 8);
+      memcpy(o.cmd + 8, &x.hi, 8);
+    } else if ((rc = read_heap(e, x.hi, 16, o.cmd))) {
+      return rc;
+    }
   }
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return RBE_OK;
+}
+
+int rbe_get_entry_cmds(rbe_engine* e, uint64_t replica, uint64_t lo, uint64_t hi, uint8_t* buf,
+                       uint64_t cap, uint64_t* offsets) {
+  if (!e || !offsets) return RBE_E_INVALID;
+  std::vector<u64> t;
+  std::vector<Body> b;
+  int rc = read_window(e, replica, lo, hi, t, b);
+  if (rc) return rc;
+  u64 off = 0;
+  for (u64 i = 0; i < b.size(); i++) {
+    offsets[i] = off;
+    off += b[i].len;
+  }
+  offsets[b.size()] = off;
+  if (off > cap || (off && !buf)) return RBE_E_NOMEM;
+  for (u64 i = 0; i < b.size(); i++) {
+    const Body& x = b[i];
+    u8* d = buf + offsets[i];
+    if (x.len <= 16) {
+      u8 w[16];
+      memcpy(w, &x.lo, 8);
+      memcpy(w + 8, &x.hi, 8);
+      memcpy(d, w, x.len);
+    } else if ((rc = read_heap(e, x.hi, x.len, d))) {
+      return rc;
+    }
+  }
+  HIP_OK(hipStreamSynchronize(e->stream));
   return RBE_OK;
 }
 

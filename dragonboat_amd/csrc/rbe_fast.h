@@ -214,7 +214,7 @@ struct FastOut {
         h = hfold(h, e.term);
         h = hfold(h, (u64)e.type | ((u64)e.len << 32));
         h = hfold(h, e.lo);
-        h = hfold(h, e.hi);
+        h = hfold(h, cmd_hi(e.len, e.hi));
       }
       msg_hash = h;
     }
@@ -365,7 +365,8 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
     // limitSize (entryutils.go:52-64) with sizes 128 + len
     const u64 lo = c.processed + 1, hi = c.committed;
     u64 n = hi - lo + 1;
-    if (n * (128 + 16) > C.max_entry_size) {
+    // (no Cmd exceeds 16 bytes without the payload heap)
+    if (C.heap_bytes || n * (128 + 16) > C.max_entry_size) {
       u64 total = 128 + P.pay_ring[(lo & (u64)(C.ring - 1)) * C.n_rep + r].len;
       u64 inc = 1;
       for (; inc < n; inc++) {
@@ -389,7 +390,7 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
       apply_hash = hfold(apply_hash, P.term_ring[s]);
       apply_hash = hfold(apply_hash, (u64)b.type | ((u64)b.len << 32));
       apply_hash = hfold(apply_hash, b.lo);
-      apply_hash = hfold(apply_hash, b.hi);
+      apply_hash = hfold(apply_hash, cmd_hi(b.len, b.hi));
     }
   }
   if (u.apply_hi >= u.apply_lo) ctr.v[C_ENT_APPLIED] += (u32)(u.apply_hi - u.apply_lo + 1);
@@ -712,7 +713,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   };
   auto limit_count = [&](u64 lo, u64 hi) -> u64 {  // limitSize, entryutils.go:52-64
     const u64 n = hi - lo + 1;
-    if (n * (128 + 16) <= C.max_entry_size) return n;
+    if (!C.heap_bytes && n * (128 + 16) <= C.max_entry_size) return n;
     u64 total = 128 + ent_at(lo).len;
     u64 inc = 1;
     for (; inc < n; inc++) {

@@ -17,9 +17,48 @@
 #include <vector>
 
 #include "../../include/rbe.h"
+#include "rbe_step.h"
 #include "rbe_types.h"
 
 namespace rbe {
+
+// Fingerprint of a Cmd longer than 16 bytes (Body/Ent lo when the bytes live in
+// the payload heap): 64 bits over the zero-padded 8-byte words and the length.
+// The trace digest folds it in place of the inline bytes, so the fingerprint
+// stands for the payload in parity checks (oracle/harness.cpp restates it).
+inline u64 cmd_fingerprint(const u8* b, u64 len) {
+  u64 h = 0x243F6A8885A308D3ull ^ len;
+  for (u64 i = 0; i < len; i += 8) {
+    u64 w = 0;
+    for (u64 j = 0; j < 8 && i + j < len; j++) w |= (u64)b[i + j] << (8 * j);
+    h = mix64(h ^ w);
+  }
+  return mix64(h ^ (len << 1));
+}
+
+// Payload heap (cfg.heap_bytes): one device byte ring shared by every group.
+// A Cmd longer than 16 bytes is written there once, when its proposal is
+// staged, and every replica's log entry refers to it by (fingerprint, absolute
+// heap position) in Body/Ent lo/hi: a follower that appends the entry copies
+// the reference, never the bytes (the Log Matching property makes the bytes of
+// an (index, term) the same on every replica).  The host is the only writer,
+// so positions are assigned here, in push order.  Bytes at position p stay
+// valid while head <= p + cap (a later lap overwrites them); a reader of an
+// older entry gets RBE_E_STATE, the analog of ErrCompacted.
+struct HostHeap {
+  u64 cap = 0;      // bytes (0 = no heap: Cmd is at most 16 bytes)
+  u64 head = 0;     // next free absolute position
+  u64 flushed = 0;  // positions below this are on the device
+  std::vector<u8> stage;  // bytes of [flushed, head), position flushed at index 0
+  // reserve len bytes (16-B aligned, never split across the end of the ring)
+  u64 alloc(u64 len) {
+    u64 p = head;
+    if (p % cap + len > cap) p += cap - p % cap;
+    head = p + ((len + 15) & ~15ull);
+    return p;
+  }
+  bool valid(u64 pos, u64 len) const { return cap && pos + len <= head && head <= pos + cap; }
+};
 
 struct HostInputs {
   u64 n_rep = 0;
@@ -34,15 +73,18 @@ struct HostInputs {
   std::vector<u64> app_rep, app_val;  // staged rbe_notify_applied values
   std::vector<u64> applied;  // [n_rep] host mirror of Planes::applied (the host is its only writer)
 
-  void init(u64 n_rep_, u32 n_, u32 in_cap_) {
+  HostHeap heap;             // payload heap positions and staged bytes
+
+  void init(u64 n_rep_, u32 n_, u32 in_cap_, u64 heap_bytes = 0) {
     n_rep = n_rep_;
     n = n_;
     in_cap = in_cap_;
+    heap.cap = heap_bytes;
     slot.assign(n_rep, ~0u);
     mark.assign(n_rep, 0u);
     applied.assign(n_rep, 0);
   }
-  bool empty() const { return reps.empty() && app_rep.empty(); }
+  bool empty() const { return reps.empty() && app_rep.empty() && heap.stage.empty(); }
   void clear() {
     for (u64 r : reps) slot[r] = ~0u;
     reps.clear();
@@ -50,6 +92,8 @@ struct HostInputs {
     ents.clear();
     app_rep.clear();
     app_val.clear();
+    heap.stage.clear();
+    heap.flushed = heap.head;
   }
   ExtIn& rec(u64 r) {
     if (slot[r] == ~0u) {
@@ -91,15 +135,23 @@ struct HostInputs {
       if (n_ents[i] == 0 || n_ents[i] > 0xFFFFu) return RBE_E_INVALID;
       total += n_ents[i];
     }
+    u64 big = 0;  // heap bytes the batch needs (upper bound: alignment and lap skips)
     for (u64 j = 0; j < total; j++) {
-      // Cmd is inline (<= 16 bytes); config changes go through
-      // ProposeConfigChange, a membership path the device does not run
-      if (cmd_len[j] > 16 || type[j] == E_ConfigChange || type[j] > E_Metadata)
+      // Cmd is inline up to 16 bytes, longer ones need the payload heap and
+      // may take at most a quarter of it (the ErrPayloadTooBig check of
+      // requests.go:989-991, node.go:366-367); config changes go through ProposeConfigChange,
+      // a membership path the device does not run
+      if (type[j] == E_ConfigChange || type[j] > E_Metadata) return RBE_E_INVALID;
+      if (cmd_len[j] > 16 && (heap.cap == 0 || (u64)cmd_len[j] > heap.cap / 4))
         return RBE_E_INVALID;
+      if (cmd_len[j] > 16) big += (u64)cmd_len[j] + 16;
       bytes += cmd_len[j];
     }
     if (bytes && !cmd) return RBE_E_INVALID;
     if (ents.size() + total > in_cap) return RBE_E_NOMEM;
+    // the bytes staged for one step must not lap the ring (they would
+    // overwrite each other before the upload)
+    if (big && heap.head - heap.flushed + 2 * big > heap.cap) return RBE_E_NOMEM;
     u64 j = 0, off = 0;
     for (u64 i = 0; i < cnt; i++) {
       ExtIn& x = rec(replica[i]);
@@ -112,12 +164,21 @@ struct HostInputs {
         e.term = 0;  // stamped by the leader (appendEntries, raft.go:909-920)
         e.type = type[j];
         e.len = cmd_len[j];
-        u8 b[16];
-        memset(b, 0, sizeof(b));
-        if (cmd_len[j]) memcpy(b, cmd + off, cmd_len[j]);
+        if (cmd_len[j] > 16) {
+          // heap entry: lo = fingerprint, hi = absolute heap position
+          const u64 pos = heap.alloc(cmd_len[j]);
+          heap.stage.resize(heap.head - heap.flushed, 0);
+          memcpy(heap.stage.data() + (pos - heap.flushed), cmd + off, cmd_len[j]);
+          e.lo = cmd_fingerprint(cmd + off, cmd_len[j]);
+          e.hi = pos;
+        } else {
+          u8 b[16];
+          memset(b, 0, sizeof(b));
+          if (cmd_len[j]) memcpy(b, cmd + off, cmd_len[j]);
+          memcpy(&e.lo, b, 8);
+          memcpy(&e.hi, b + 8, 8);
+        }
         off += cmd_len[j];
-        memcpy(&e.lo, b, 8);
-        memcpy(&e.hi, b + 8, 8);
         ents.push_back(e);
       }
     }

@@ -33,6 +33,10 @@ RBE_HD u64 mix64(u64 x) {  // splitmix64 finalizer (same constants as the oracle
   return x ^ (x >> 31);
 }
 RBE_HD u64 hfold(u64 h, u64 x) { return mix64(h ^ x); }
+// The second Cmd word a trace digest folds: the inline bytes 8-15, or 0 for a
+// Cmd in the payload heap, whose `hi` is a heap position (rbe_host.h) and whose
+// `lo` fingerprint already stands for the bytes
+RBE_HD u64 cmd_hi(u32 len, u64 hi) { return len > 16 ? 0 : hi; }
 RBE_HD u64 umin64(u64 a, u64 b) { return a < b ? a : b; }
 RBE_HD u64 umax64(u64 a, u64 b) { return a > b ? a : b; }
 RBE_HD u32 popc8(u32 x) {
@@ -291,7 +295,7 @@ struct Lane {
   // limitSize (entryutils.go:52-64) over [lo, hi] with sizes 128 + len
   RBE_HD u64 limit_count(u64 lo, u64 hi) {
     u64 n = hi - lo + 1;
-    if (n * (128 + 16) <= C.max_entry_size) return n;
+    if (!C.heap_bytes && n * (128 + 16) <= C.max_entry_size) return n;  // Cmd <= 16 B
     u64 total = 128 + P.pay_ring[ring_slot(lo)].len;
     u64 inc = 1;
     for (; inc < n; inc++) {
@@ -454,7 +458,7 @@ struct Lane {
           h = hfold(h, e.term);
           h = hfold(h, (u64)e.type | ((u64)e.len << 32));
           h = hfold(h, e.lo);
-          h = hfold(h, e.hi);
+          h = hfold(h, cmd_hi(e.len, e.hi));
         }
       }
       msg_hash = h;
@@ -609,7 +613,7 @@ struct Lane {
         drop_hash = hfold(drop_hash, e[i].term);
         drop_hash = hfold(drop_hash, (u64)e[i].type | ((u64)e[i].len << 32));
         drop_hash = hfold(drop_hash, e[i].lo);
-        drop_hash = hfold(drop_hash, e[i].hi);
+        drop_hash = hfold(drop_hash, cmd_hi(e[i].len, e[i].hi));
       }
     }
   }
@@ -1724,7 +1728,7 @@ struct Lane {
         apply_hash = hfold(apply_hash, P.term_ring[s]);
         apply_hash = hfold(apply_hash, (u64)b.type | ((u64)b.len << 32));
         apply_hash = hfold(apply_hash, b.lo);
-        apply_hash = hfold(apply_hash, b.hi);
+        apply_hash = hfold(apply_hash, cmd_hi(b.len, b.hi));
       }
     }
     if (u.apply_hi >= u.apply_lo) ctr.v[C_ENT_APPLIED] += (u32)(u.apply_hi - u.apply_lo + 1);

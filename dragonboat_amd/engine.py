@@ -120,7 +120,8 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_get_views", "rbe_get_counters", "rbe_reset_counters", "rbe_fault_summary",
            "rbe_footprint", "rbe_profile_rounds", "rbe_get_kernel_counters", "rbe_kernel_name",
            "rbe_xchg_record_bytes", "rbe_xchg_pack", "rbe_xchg_unpack", "rbe_get_outbox",
-           "rbe_push_messages", "rbe_snapshot_bytes", "rbe_export_groups", "rbe_import_groups"]
+           "rbe_push_messages", "rbe_snapshot_bytes", "rbe_export_groups", "rbe_import_groups",
+           "rbe_get_entry_cmds"]
 KERNEL_SLOTS = 4
 
 _lib = None
@@ -171,6 +172,7 @@ def load_library(path: Optional[str] = None):
         "rbe_push_messages": (i32, [vp, u64, P(u64), P(RbeMessage), P(RbeEntry)]),
         "rbe_get_ready_to_reads": (i32, [vp, u64, P(RbeReadyToRead), u32, P(u32)]),
         "rbe_get_entries": (i32, [vp, u64, u64, u64, P(RbeEntry)]),
+        "rbe_get_entry_cmds": (i32, [vp, u64, u64, u64, vp, u64, P(u64)]),
         "rbe_get_views": (i32, [vp, u64, u64, P(RbeReplicaView)]),
         "rbe_get_counters": (i32, [vp, P(u64)]),
         "rbe_reset_counters": (i32, [vp]),
@@ -211,7 +213,7 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                 wl_read_permille: int = 0, ext_inputs: bool = False, iso_period: int = 0,
                 iso_len: int = 0, iso_mod: int = 10, rep_world: int = 0,
                 rep_rank: int = 0, ext_apply: bool = False, in_cap: int = 0,
-                xfer_period: int = 0, xfer_mod: int = 1) -> RbeConfig:
+                xfer_period: int = 0, xfer_mod: int = 1, heap_bytes: int = 0) -> RbeConfig:
     return RbeConfig(abi_version=RBE_ABI_VERSION, device=device, n_groups=n_groups,
                      n_replicas=n_replicas, election_rtt=election_rtt,
                      heartbeat_rtt=heartbeat_rtt, check_quorum=int(check_quorum),
@@ -223,7 +225,8 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                      wl_read_permille=wl_read_permille, ext_inputs=int(ext_inputs),
                      iso_period=iso_period, iso_len=iso_len, iso_mod=iso_mod,
                      rep_world=rep_world, rep_rank=rep_rank, ext_apply=int(ext_apply),
-                     in_cap=in_cap, xfer_period=xfer_period, xfer_mod=xfer_mod)
+                     in_cap=in_cap, xfer_period=xfer_period, xfer_mod=xfer_mod,
+                     heap_bytes=heap_bytes)
 
 
 class InputError(EngineError):
@@ -254,6 +257,20 @@ class SnapshotError(EngineError):
 def _check(rc: int, what: str):
     if rc != 0:
         raise EngineError(f"{what} failed with rc={rc}")
+
+
+def entry_cmds(fn, h, replica: int, lo: int, hi: int) -> List[bytes]:
+    """Cmd bytes of entries [lo, hi] through rbe_get_entry_cmds (or the host
+    build's twin): one call to size the buffer, one to fill it."""
+    offs = (C.c_uint64 * (hi - lo + 2))()
+    rc = fn(h, replica, lo, hi, None, 0, offs)
+    if rc not in (0, RBE_E_NOMEM):
+        raise EngineError(f"rbe_get_entry_cmds failed with rc={rc}")
+    total = offs[hi - lo + 1]
+    buf = C.create_string_buffer(max(1, total))
+    _check(fn(h, replica, lo, hi, buf, total, offs), "rbe_get_entry_cmds")
+    raw = buf.raw
+    return [raw[offs[i]:offs[i + 1]] for i in range(hi - lo + 1)]
 
 
 class NodeInputs:
@@ -500,9 +517,18 @@ class Engine(NodeInputs):
         return [(arr[i].index, arr[i].ctx_low, arr[i].ctx_high) for i in range(n.value)]
 
     def entries(self, replica: int, lo: int, hi: int):
+        """(Index, Term, Type, Cmd) of entries [lo, hi] of a replica's log window;
+        a Cmd longer than 16 bytes comes from the payload heap."""
         arr = (RbeEntry * (hi - lo + 1))()
         _check(self.lib.rbe_get_entries(self.h, replica, lo, hi, arr), "rbe_get_entries")
-        return [(e.index, e.term, e.type, bytes(e.cmd[:e.cmd_len])) for e in arr]
+        out = [(e.index, e.term, e.type, bytes(e.cmd[:min(16, e.cmd_len)])) for e in arr]
+        if any(e.cmd_len > 16 for e in arr):
+            cmds = self.entry_cmds(replica, lo, hi)
+            out = [(i, t, ty, c) for (i, t, ty, _), c in zip(out, cmds)]
+        return out
+
+    def entry_cmds(self, replica: int, lo: int, hi: int) -> List[bytes]:
+        return entry_cmds(self.lib.rbe_get_entry_cmds, self.h, replica, lo, hi)
 
     def fault_summary(self):
         n = C.c_uint64()

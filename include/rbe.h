@@ -132,7 +132,8 @@ typedef struct rbe_config {
   uint32_t xfer_mod;
   uint32_t snapshot_entries;     /* reserved: config.SnapshotEntries, must be 0 */
   uint32_t compaction_overhead;  /* reserved: config.CompactionOverhead, must be 0 */
-  uint64_t heap_bytes;           /* reserved: payload heap for Cmd > 16 B, must be 0 */
+  uint64_t heap_bytes;           /* payload heap for Cmd > 16 B (needs ext_inputs), 0 = none:
+                                    Cmd is then at most 16 bytes */
   uint32_t reserved[4];
 } rbe_config;
 
@@ -184,7 +185,9 @@ typedef struct rbe_message {
   uint32_t n_entries, reserved;
 } rbe_message;
 
-/* raftpb Entry (raft.pb.go:589-598): Index/Term/Type + up to 16 Cmd bytes. */
+/* raftpb Entry (raft.pb.go:589-598): Index/Term/Type and Cmd.  cmd holds the
+ * first min(cmd_len, 16) bytes; a longer Cmd (payload heap) is read whole with
+ * rbe_get_entry_cmds. */
 typedef struct rbe_entry {
   uint64_t index, term;
   uint32_t type, cmd_len;
@@ -253,7 +256,11 @@ int rbe_profile_rounds(rbe_engine* e, uint32_t rounds, float* ms_per_kernel);
  *   rbe_push_proposals: Peer.ProposeEntries (peer.go:117-123); batch i holds
  *     n_ents[i] entries for replica[i]; the entries' types, Cmd lengths and Cmd
  *     bytes (concatenated in order) follow in type[], cmd_len[], cmd.  Cmd is at
- *     most 16 bytes.  RBE_E_NOMEM when the step's cfg.in_cap entries are used up.
+ *     most 16 bytes without a payload heap; with cfg.heap_bytes a longer Cmd (at
+ *     most heap_bytes / 4, the ErrPayloadTooBig analog, requests.go:989-991) is
+ *     written to the heap once and every replica's entry refers to it.
+ *     RBE_E_NOMEM when the step's cfg.in_cap entries are used up, or its Cmd
+ *     bytes would lap the heap.
  *   rbe_push_read_index: Peer.ReadIndex (peer.go:297-303), ctx_low != 0
  *     (requests.go:726).
  *   rbe_request_leader_transfer: Peer.RequestLeaderTransfer (peer.go:106-113),
@@ -289,6 +296,15 @@ int rbe_get_ready_to_reads(rbe_engine* e, uint64_t replica, rbe_ready_to_read* o
                            uint32_t cap, uint32_t* n_out);
 int rbe_get_entries(rbe_engine* e, uint64_t replica, uint64_t lo, uint64_t hi,
                     rbe_entry* out);
+/* The Cmd bytes of entries [lo, hi] of a replica's log, concatenated in `buf`:
+ * entry lo + i occupies [offsets[i], offsets[i + 1]) (offsets has hi - lo + 2
+ * slots and is filled even when `cap` is short, which returns RBE_E_NOMEM).
+ * RBE_E_STATE when a heap Cmd has been overwritten by a later lap of the heap
+ * (the entry is older than the heap holds, as ErrCompacted for LogDB reads).
+ * Together with rbe_get_entries this is what the node reads out of
+ * Update.EntriesToSave / CommittedEntries (node.go:975-977, 959-968). */
+int rbe_get_entry_cmds(rbe_engine* e, uint64_t replica, uint64_t lo, uint64_t hi, uint8_t* buf,
+                       uint64_t cap, uint64_t* offsets);
 int rbe_get_views(rbe_engine* e, uint64_t first, uint64_t count, rbe_replica_view* out);
 int rbe_get_counters(rbe_engine* e, uint64_t* out /* RBE_CTR_NUM */);
 /* the counters one pipeline kernel (RBE_KERNEL_*) contributed */

@@ -42,7 +42,7 @@ class OrcEntry(C.Structure):
     _fields_ = [("term", C.c_uint64), ("index", C.c_uint64), ("key", C.c_uint64),
                 ("client_id", C.c_uint64), ("series_id", C.c_uint64),
                 ("responded_to", C.c_uint64), ("type", C.c_uint32),
-                ("cmd_len", C.c_uint32), ("cmd", C.c_uint8 * 64)]
+                ("cmd_len", C.c_uint32), ("cmd", C.c_uint8 * 64), ("data", C.c_void_p)]
 
 
 class OrcSnapshot(C.Structure):
@@ -220,6 +220,11 @@ class Entry:
         e.cmd_len = len(self.cmd)
         for i, b in enumerate(self.cmd[:64]):
             e.cmd[i] = b
+        if len(self.cmd) > 64:  # the whole Cmd by pointer; the caller keeps it alive
+            buf = C.create_string_buffer(bytes(self.cmd), len(self.cmd))
+            e.data = C.cast(buf, C.c_void_p)
+            return buf
+        return None
 
     @staticmethod
     def from_c(e: OrcEntry) -> "Entry":
@@ -230,8 +235,8 @@ class Entry:
 
 def entries_array(ents: List[Entry]):
     arr = (OrcEntry * max(1, len(ents)))()
-    for i, e in enumerate(ents):
-        e.to_c(arr[i])
+    keep = [e.to_c(arr[i]) for i, e in enumerate(ents)]
+    arr._keep = [k for k in keep if k is not None]  # Cmd buffers of long entries
     return arr
 
 

@@ -16,6 +16,7 @@ typedef struct {
   uint64_t term, index, key, client_id, series_id, responded_to;
   uint32_t type, cmd_len;
   uint8_t cmd[64];
+  const uint8_t* data;  // the whole Cmd when cmd_len > 64 (input only)
 } orc_entry;
 
 typedef struct {
@@ -68,7 +69,10 @@ static Entry to_entry(const orc_entry& e) {
   x.client_id = e.client_id;
   x.series_id = e.series_id;
   x.responded_to = e.responded_to;
-  x.cmd.assign((const char*)e.cmd, e.cmd_len > 64 ? 64 : e.cmd_len);
+  if (e.cmd_len > 64 && e.data)
+    x.cmd.assign((const char*)e.data, e.cmd_len);
+  else
+    x.cmd.assign((const char*)e.cmd, e.cmd_len > 64 ? 64 : e.cmd_len);
   return x;
 }
 

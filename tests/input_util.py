@@ -17,12 +17,14 @@ def _cmd(rng):
     return bytes(rng.randrange(256) for _ in range(rng.randrange(17)))
 
 
-def plan_round(rng, n_rep, n, rnd, views, ext_apply, density=0.3, applied=None):
-    """One round of host input: a list of (kind, replica, args)."""
+def plan_round(rng, n_rep, n, rnd, views, ext_apply, density=0.3, applied=None, cmd=None):
+    """One round of host input: a list of (kind, replica, args).  `cmd(rng)`
+    draws a proposal's Cmd (default: 0-16 bytes)."""
+    cmd = cmd or _cmd
     ops = []
     for r in range(n_rep):
         if rng.random() < density:
-            ops.append(("prop", r, [(rng.choice((0, 0, 2, 3)), _cmd(rng))
+            ops.append(("prop", r, [(rng.choice((0, 0, 2, 3)), cmd(rng))
                                     for _ in range(rng.randrange(1, 4))]))
         if rng.random() < density:
             ops.append(("read", r, ((rnd + 1) << 32 | (r + 1), rng.randrange(1 << 40))))
@@ -77,7 +79,7 @@ def apply_oracle(h, ops):
 
 
 def run_driven(eng, ref, rounds, seed=1, tick_every=1, inputs=True, ext_apply=False,
-               density=0.3, skip=()):
+               density=0.3, skip=(), cmd=None, on_ops=None):
     """Step both `rounds` rounds with the same input; every `tick_every`-th
     round ticks, the others are RBE_STEP_NO_TICK rounds.  Returns the first
     divergence (round, replica, field, engine, oracle) or None."""
@@ -88,7 +90,9 @@ def run_driven(eng, ref, rounds, seed=1, tick_every=1, inputs=True, ext_apply=Fa
     applied = [0] * n_rep
     for rnd in range(rounds):
         if inputs:
-            ops = plan_round(rng, n_rep, n, rnd, views, ext_apply, density, applied)
+            ops = plan_round(rng, n_rep, n, rnd, views, ext_apply, density, applied, cmd)
+            if on_ops:
+                on_ops(ops)
             apply_engine(eng, ops)
             apply_oracle(ref, ops)
         tick = (rnd % tick_every) == 0

@@ -6,7 +6,7 @@ import ctypes as C
 import os
 
 from dragonboat_amd.engine import (CTR_NUM, COUNTER_NAMES, NodeInputs, RbeEntry, RbeMessage,
-                                   RbeReplicaView, make_config)
+                                   RbeReplicaView, entry_cmds, make_config)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _lib = None
@@ -52,6 +52,9 @@ def lib():
         L.soa_import_groups.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32]
         u64p, u32p = P(C.c_uint64), P(C.c_uint32)
         L.soa_step_ex.argtypes = [C.c_void_p, C.c_uint32]
+        L.soa_get_entry_cmds.restype = C.c_int
+        L.soa_get_entry_cmds.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64,
+                                         C.c_void_p, C.c_uint64, u64p]
         for name, args in {
                 "push_proposals": [C.c_uint64, u64p, u32p, u32p, u32p, P(C.c_uint8)],
                 "push_read_index": [C.c_uint64, u64p, u64p, u64p],
@@ -98,6 +101,9 @@ class SoaCpu(NodeInputs):
 
     def run(self, rounds=1):
         lib().soa_run(self.h, rounds)
+
+    def entry_cmds(self, replica, lo, hi):
+        return entry_cmds(lib().soa_get_entry_cmds, self.h, replica, lo, hi)
 
     def step(self, tick=True):
         if tick:

@@ -27,6 +27,7 @@ struct SoaEngine {
   bool full_only = false;
   int staged = 0;  // STG_* bits: fast steps on a staged row (StageRow); 4: counts from inbound_aux
   u64 slow_total = 0;
+  std::vector<u8> heap;  // payload heap (cfg.heap_bytes), as on the device
 };
 
 template <typename T>
@@ -39,6 +40,8 @@ template <int N>
 static void run_round(SoaEngine* e, bool tick = true) {
   const Clk ck{e->round, e->tclk, tick ? 1u : 0u};
   if (!e->hin.empty()) {  // the HIP engine uploads and scatters the same records
+    HostHeap& hp = e->hin.heap;
+    for (u64 p = hp.flushed; p < hp.head; p++) e->heap[p % hp.cap] = hp.stage[p - hp.flushed];
     e->hin.apply_host(e->P);
     e->hin.clear();
   }
@@ -219,7 +222,9 @@ void* soa_create(const rbe_config* cfg) {
   P.applied = alloc<u64>(e, R);
   P.gwake = alloc<u8>(e, G);
   memset(P.gwake, GW_AWAKE, G);  // every group starts awake
-  e->hin.init(R, C.n, C.in_cap);
+  C.heap_bytes = (cfg->heap_bytes + 255) & ~255ull;
+  e->heap.assign(C.heap_bytes, 0);
+  e->hin.init(R, C.n, C.in_cap, C.heap_bytes);
   P.counters = nullptr;
   for (u64 r = 0; r < R; r++) {
     if (N == 1) launch_replica<1>(P, C, r);
@@ -230,6 +235,38 @@ void* soa_create(const rbe_config* cfg) {
 }
 
 void soa_destroy(void* h) { delete (SoaEngine*)h; }
+
+// rbe_get_entry_cmds: Cmd bytes of entries [lo, hi] of a replica, inline or
+// from the payload heap
+int soa_get_entry_cmds(void* h, uint64_t replica, uint64_t lo, uint64_t hi, uint8_t* buf,
+                       uint64_t cap, uint64_t* offsets) {
+  SoaEngine* e = (SoaEngine*)h;
+  const Params& C = e->C;
+  if (replica >= C.n_rep || lo == 0 || hi < lo) return RBE_E_INVALID;
+  const Core& c = e->P.core[replica];
+  if (hi > c.last_index || c.last_index - lo >= C.ring) return RBE_E_INVALID;
+  u64 off = 0;
+  for (u64 i = lo; i <= hi; i++) {
+    offsets[i - lo] = off;
+    off += e->P.pay_ring[(i & (C.ring - 1)) * C.n_rep + replica].len;
+  }
+  offsets[hi - lo + 1] = off;
+  if (off > cap) return RBE_E_NOMEM;
+  for (u64 i = lo; i <= hi; i++) {
+    const Body& b = e->P.pay_ring[(i & (C.ring - 1)) * C.n_rep + replica];
+    u8* d = buf + offsets[i - lo];
+    if (b.len <= 16) {
+      u8 w[16];
+      memcpy(w, &b.lo, 8);
+      memcpy(w + 8, &b.hi, 8);
+      memcpy(d, w, b.len);
+    } else {
+      if (!e->hin.heap.valid(b.hi, b.len)) return RBE_E_STATE;
+      memcpy(d, e->heap.data() + b.hi % e->hin.heap.cap, b.len);
+    }
+  }
+  return RBE_OK;
+}
 void soa_set_full_only(void* h, int v) { ((SoaEngine*)h)->full_only = v != 0; }
 void soa_set_staged(void* h, int v) { ((SoaEngine*)h)->staged = v; }
 uint64_t soa_slow_total(void* h) { return ((SoaEngine*)h)->slow_total; }
