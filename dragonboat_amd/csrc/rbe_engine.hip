@@ -17,713 +17,55 @@
 #include <vector>
 
 #include "../../include/rbe.h"
-#include "rbe_fast.h"
 #include "rbe_host.h"
+#include "rbe_kernels.h"
 #include "rbe_snap.h"
-#include "rbe_xchg.h"
 
 using namespace rbe;
 
-#define HIP_IGNORE(x) ((void)(x))
-#define HIP_OK(x)                                                      \
-  do {                                                                 \
-    hipError_t err__ = (x);                                            \
-    if (err__ != hipSuccess) {                                         \
-      fprintf(stderr, "rbe: %s failed: %s\n", #x, hipGetErrorString(err__)); \
-      return RBE_E_HIP;                                                \
-    }                                                                  \
-  } while (0)
-
-static constexpr int kBlock = 256;
-// minimum waves per SIMD requested for the fast-step kernels (caps their VGPRs:
-// 2 -> 256, 3 -> 168, 4 -> 128; beyond the cap the compiler spills to scratch)
-#ifndef RBE_FAST_WAVES
-#define RBE_FAST_WAVES 2
+#ifndef RBE_SINGLE_TU
+// the round pipeline per group size is instantiated in rbe_round.hip (one
+// translation unit per N, built in parallel)
+namespace rbe {
+#define RBE_EXTERN_ROUND(N, T)                                                            \
+  extern template int launch_round<N, T>(const Planes&, const Params&, const Lists&,      \
+                                         hipStream_t, int, RoundArg, hipEvent_t*);
+RBE_EXTERN_ROUND(1, true)
+RBE_EXTERN_ROUND(1, false)
+RBE_EXTERN_ROUND(3, true)
+RBE_EXTERN_ROUND(3, false)
+RBE_EXTERN_ROUND(5, true)
+RBE_EXTERN_ROUND(5, false)
+#undef RBE_EXTERN_ROUND
+}  // namespace rbe
 #endif
-#ifndef RBE_TRI_CHUNK
-#define RBE_TRI_CHUNK 2048
-#endif
-// work-list entries carry the inbound summary word (kListAux); 0 = A/B baseline
-#ifndef RBE_LIST_AUX
-#define RBE_LIST_AUX 1
-#endif
-// how the fast steps of k_fast_both use wave-staged rows (StageRow, rbe_fast.h):
-// 0 = direct, 1 = STG_OUT (row writes staged), 3 = STG_OUT | STG_IN
-#ifndef RBE_STAGE_LEAD
-#define RBE_STAGE_LEAD 0
-#endif
-#ifndef RBE_STAGE_FOLL
-#define RBE_STAGE_FOLL 0
-#endif
-static constexpr u32 kTriChunk = RBE_TRI_CHUNK;   // replicas per k_triage block (8 per lane)
-static constexpr int kCtrStripes = 64;   // counter stripes per kernel slot (flush_counters)
-// counter sections, one per pipeline kernel (rbe_get_kernel_counters)
-enum : int { KS_TRIAGE = 0, KS_FAST_LEAD = 1, KS_FAST_FOLL = 2, KS_FULL = 3, KS_NUM = 4 };
-static constexpr u64 kCtrWords = (u64)KS_NUM * kCtrStripes * C_NUM;
 
-// Where a kernel finds its round: the device clock {round, tclk} at `ptr`
-// (graph replay, advanced on device by k_advance) or 0, plus offsets; `tick`
-// says whether the round ticks (rbe_step_ex with RBE_STEP_NO_TICK: no).
-struct RoundArg {
-  const u32* ptr;
-  u32 round_add, tclk_add, tick;
-};
-__device__ __forceinline__ Clk clk_of(const RoundArg& a) {
-  Clk c;
-  c.round = (a.ptr ? a.ptr[0] : 0u) + a.round_add;
-  c.tclk = (a.ptr ? a.ptr[1] : 0u) + a.tclk_add;
-  c.tick = a.tick;
-  return c;
-}
-
-// ------------------------------------------------------------------ kernels
-__device__ __forceinline__ u32 wave_sum(u32 v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-
-// Event counters live in kCtrStripes stripes of C_NUM u64 (192 B apart, so
-// each stripe is its own L2 line).  A block reduces its lanes' counters through
-// shuffles and LDS and adds each non-zero total with ONE atomic into stripe
-// blockIdx % kCtrStripes: same-address atomics serialise in one L2 channel, so
-// one-atomic-per-wave into a single line was the round's bottleneck (r01 profile).
-// Every thread of the block must call this (it synchronises the block).
-template <int KS>
-__device__ __forceinline__ void flush_counters(const Planes& P, const StepCounters& c) {
-  __shared__ u32 s_ctr[kBlock / 64][C_NUM];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int i = 0; i < C_NUM; i++) {
-    u32 s = 0;
-    if (__ballot(c.v[i] != 0) != 0ull) s = wave_sum(c.v[i]);
-    if (lane == 0) s_ctr[w][i] = s;
-  }
-  __syncthreads();
-  if (threadIdx.x < C_NUM) {
-    u32 t = 0;
-#pragma unroll
-    for (int j = 0; j < kBlock / 64; j++) t += s_ctr[j][threadIdx.x];
-    if (t)
-      atomicAdd((unsigned long long*)&P.counters[((u64)KS * kCtrStripes + blockIdx.x % kCtrStripes) *
-                                                     C_NUM + threadIdx.x],
-                (unsigned long long)t);
-  }
-}
-
-// The whole handler table over every replica (reference mode, RBE_MODE=full).
-template <int N, bool TRACE>
-__global__ __launch_bounds__(kBlock) void k_step(Planes P, Params C, RoundArg ra) {
-  const Clk ck = clk_of(ra);
-  const u64 r = (u64)blockIdx.x * kBlock + threadIdx.x;
-  StepCounters c;
-#pragma unroll
-  for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
-  if (r < C.n_rep && owned<N>(C, r)) step_replica<N, TRACE>(P, C, r, ck, c);
-  flush_counters<KS_FULL>(P, c);
-}
-
-// Work lists of a round: 0 = steady-state leaders, 1 = steady-state followers,
-// 2 = full handler table.  Each list is kShards regions, one per shard: a
-// writing block appends to the region of shard blockIdx % kShards, so the
-// returning atomics that reserve list space are spread over kShards counters
-// per list, each on its own 256-B line (one counter word saturates at ~90
-// returning atomics per µs, and k_triage's ~1.5k blocks made five such words
-// the round's critical path).  Lists 0 and 1 fill each region from both ends:
-// the front holds the common case (a leader without a proposal this round, a
-// follower without a Replicate), the back the rest, so the waves of the fast
-// launch are mostly homogeneous and skip the code paths none of their lanes
-// take.  A consumer reads the regions as one sequence of segments (seg_build /
-// seg_find): fronts of every shard, then backs.
-static constexpr u32 kShards = 8;
-static constexpr u32 kSlots = 5;   // count slots: fronts of lists 0..2, backs of lists 0..1
-static constexpr u32 kCntPad = 64;  // u32 words from one count to the next (256 B)
-static constexpr u32 kListCounts = 2 * kSlots * kShards * kCntPad;  // by parity, slot, shard
-struct Lists {
-  u32* idx;     // list li, shard s: [off[li] + s * scap[li], + scap[li]) replica indices
-  u32* aux;     // lists 0 and 1, same layout: inbound summary words (inbound_aux)
-  u32* counts;  // list_cnt
-  u64 scap[3];  // entries per shard region
-  u64 off[3];   // first entry of each list
-};
-// work-list entries carry their inbound summary word for N = 3 (14 bits; the
-// LDS compaction packs it with the 11-bit block position in one u32)
-template <int N>
-constexpr bool kListAux = N == 3 && RBE_TRI_CHUNK <= 2048 && RBE_LIST_AUX;
-__device__ __forceinline__ u32* list_cnt(const Lists& L, u32 slot, u32 par, u32 sh) {
-  return &L.counts[((par * kSlots + slot) * kShards + sh) * kCntPad];
-}
-// position of the j-th front (or back) entry of list li, shard sh
-__device__ __forceinline__ u64 list_pos(const Lists& L, u32 li, u32 sh, bool back, u64 j) {
-  const u64 base = L.off[li] + (u64)sh * L.scap[li];
-  return back ? base + L.scap[li] - 1 - j : base + j;
-}
-// Every thread of a block calls seg_build: the first wave loads the counts of
-// the NQ slots `slots` (all kShards shards of each, segment q * kShards + sh)
-// and leaves their exclusive prefix in s_pre[0 .. NQ * kShards].
-template <u32 NQ>
-__device__ __forceinline__ void seg_build(const Lists& L, u32 par, const u32 (&slots)[NQ],
-                                          u32* s_pre) {
-  static_assert(NQ * kShards < 64, "one wave scans the segment counts");
-  if (threadIdx.x < 64) {
-    const u32 lane = threadIdx.x;
-    u32 v = 0;
-#pragma unroll
-    for (u32 q = 0; q < NQ; q++)
-      if (lane / kShards == q) v = *list_cnt(L, slots[q], par, lane % kShards);
-#pragma unroll
-    for (u32 o = 1; o < 64; o <<= 1) {
-      const u32 t = __shfl_up(v, o, 64);
-      if (lane >= o) v += t;
-    }
-    if (lane < NQ * kShards) s_pre[lane + 1] = v;
-    if (lane == 0) s_pre[0] = 0;
-  }
-  __syncthreads();
-}
-// the segment holding sequence item i (< s_pre[NSEG]): the last one starting at or before i
-template <u32 NSEG>
-__device__ __forceinline__ u32 seg_find(const u32* s_pre, u32 i) {
-  u32 lo = 0;
-#pragma unroll
-  for (u32 step = 32; step; step >>= 1)
-    if (lo + step < NSEG && s_pre[lo + step] <= i) lo += step;
-  return lo;
-}
-
-// wave-aggregated append to the front of list `list`: one atomic per wave
-__device__ __forceinline__ void list_push(const Lists& L, u32 list, u32 par, bool want, u32 r) {
-  const u64 mask = __ballot(want);
-  if (!mask) return;
-  const int lane = threadIdx.x & 63;
-  const int first = __ffsll((unsigned long long)mask) - 1;
-  const u32 sh = blockIdx.x % kShards;
-  u32 base = 0;
-  if (lane == first) base = atomicAdd(list_cnt(L, list, par, sh), (u32)__popcll(mask));
-  base = __shfl(base, first, 64);
-  if (want) L.idx[list_pos(L, list, sh, false, base + __popcll(mask & ((1ull << lane) - 1ull)))] = r;
-}
-// the next round's counts (other parity) start at zero: block 0 of the
-// round's first kernel clears count slots [0, nslots)
-__device__ __forceinline__ void list_clear_next(const Lists& L, u32 par, u32 nslots) {
-  if (blockIdx.x == 0 && threadIdx.x < nslots * kShards)
-    *list_cnt(L, threadIdx.x / kShards, par ^ 1u, threadIdx.x % kShards) = 0;
-}
-
-// Pass 1 over every group: sleeping groups and idle rounds complete here; the
-// rest is listed.  A block owns kTriGroups<N> consecutive groups (at most
-// kTriChunk replicas).  It first reads one wake byte per group (group sleep,
-// rbe_step.h) and finishes the round of every sleeping group from it; the
-// replicas of the groups left (all of them without group sleep) are triaged
-// one lane each.  Each listed replica takes a position in one of five slots
-// (fronts of lists 0..2, backs of lists 0..1) from a wave-aggregated LDS
-// atomic; the block then reserves space in each global list with ONE atomic
-// per slot, lays the slots out back to back in one LDS array and copies them
-// out coalesced.  A group whose replicas all completed lazily falls asleep.
-// LDS stays near 11 KB, so every block of a 1M-group round is resident at
-// once (occupancy is set by registers, not LDS).
-template <int N>
-constexpr u32 kTriGroups = kTriChunk / N;
-template <int N, bool TRACE>
-__global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg ra, Lists L) {
-  constexpr u32 GB = kTriGroups<N>;
-  constexpr u32 kNone = 7u;  // slot code of a replica that is not listed
-  __shared__ u32 s_idx[kTriChunk];
-  // per triaged group: (block-local group | was awake << 15) << 16 | leaders +
-  // (replicas not lazy-done) << 8
-  __shared__ u32 s_gst[GB];
-  __shared__ u32 s_n[kSlots], s_base[kSlots], s_off[kSlots];
-  __shared__ u32 s_ng;
-  const Clk ck = clk_of(ra);
-  RBE_STAMP(tt0);
-  const u32 round = ck.round;
-  const u32 par = round & 1u;
-  list_clear_next(L, par, kSlots);
-  if (threadIdx.x < kSlots) s_n[threadIdx.x] = 0;
-  if (threadIdx.x == 0) s_ng = 0;
-  __syncthreads();
-  StepCounters c;
-#pragma unroll
-  for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
-  const int lane = threadIdx.x & 63;
-  const bool shortcut = !TRACE && C.quiesce;
-  const u64 g0 = (u64)blockIdx.x * GB;
-  const u32 gn = (u32)(C.n_groups - g0 < GB ? C.n_groups - g0 : GB);
-  // phase 1: one lane per group, every wake byte loaded before any is used
-  constexpr u32 kP1 = (GB + kBlock - 1) / kBlock;
-  u8 gws[kP1];
-#pragma unroll
-  for (u32 i = 0; i < kP1; i++) {
-    const u32 j = threadIdx.x + i * kBlock;
-    gws[i] = shortcut ? P.gwake[g0 + (j < gn ? j : 0u)] : (u8)GW_AWAKE;
-  }
-#pragma unroll
-  for (u32 i = 0; i < kP1; i++) {
-    const u32 j = threadIdx.x + i * kBlock;
-    const u64 g = g0 + j;
-    const bool awake = (gws[i] & GW_AWAKE) != 0;
-    bool work = j < gn;
-    if (work && !awake && !group_forced(C, C.cid_base + g * C.cid_stride, round)) {
-      work = false;
-      u32 own = 0;
-      for (u32 k = 0; k < (u32)N; k++) own += owned<N>(C, g * N + k) ? 1u : 0u;
-      group_sleep_round(gws[i], own, ck, c);
-    }
-    const u64 mask = __ballot(work);
-    if (mask) {
-      const int first = __ffsll((unsigned long long)mask) - 1;
-      u32 base = 0;
-      if (lane == first) base = atomicAdd(&s_ng, (u32)__popcll(mask));
-      base = __shfl(base, first, 64);
-      if (work)
-        s_gst[base + __popcll(mask & ((1ull << lane) - 1ull))] = (j | (awake ? 0x8000u : 0u)) << 16;
-    }
-  }
-  __syncthreads();
-  RBE_STAMP(tt1);
-  // phase 2: one lane per replica of a triaged group (item t: group slot t / N,
-  // replica t % N).  The idle bytes and inbound count words of all the items
-  // a lane owns (strided by the block size, so each load is coalesced across
-  // the wave) are loaded before any of them is processed; most rounds are then
-  // decided without reading Hot: a lazy quiesced tick completes here, a
-  // replica with inbound messages is listed by the role its idle byte carries.
-  constexpr u32 kPer = kTriChunk / kBlock;
-  const u32 nr = s_ng * (u32)N;
-  const u32 iters = (nr + kBlock - 1) / kBlock;  // uniform over the block
-  const u32 rb = (u32)(g0 * N);
-  // block-local replica index of item t (items past the end map to item 0)
-  auto item_lr = [&](u32 t, u32* slot_out) -> u32 {
-    const u32 tc = t < nr ? t : 0u;
-    const u32 slot = tc / (u32)N;
-    *slot_out = slot;
-    return ((s_gst[slot] >> 16) & 0x7FFFu) * (u32)N + (tc - slot * (u32)N);
-  };
-  // Loads of items past the end read the block's first replica and are masked
-  // afterwards, and index math is u32: no load waits behind a branch or a
-  // 64-bit division, so all the loads of a lane are in flight before the
-  // first wait.
-  u8 ibs[kPer];
-  u16 wv[kPer][N];
-#pragma unroll
-  for (u32 i = 0; i < kPer; i++) {
-    if (i < iters) {
-      u32 slot;
-      const u32 lr = item_lr(threadIdx.x + i * kBlock, &slot);
-      const u32 k = lr % (u32)N;
-      ibs[i] = P.idle[rb + lr];
-      inbound_load<N>(P, (u32)(g0 + lr / (u32)N), k, round, wv[i]);
-    }
-  }
-  // the per-replica bytes packed into registers, so the classification loop
-  // below runs rolled (one copy of triage_lazy / triage_replica in the
-  // instruction stream instead of kPer) without indexing a register array
-  u64 ibp = 0;
-  u32 inbp = 0;
-  u64 aux_lo = 0, aux_hi = 0;  // kListAux: 14-bit summary words, items 0-3 and 4-7
-#pragma unroll
-  for (u32 i = 0; i < kPer; i++) {
-    if (i < iters) {
-      const u32 t = threadIdx.x + i * kBlock;
-      const u32 k = (t < nr ? t : 0u) % (u32)N;
-      ibp |= (u64)ibs[i] << (8 * i);
-      inbp |= inbound_fold<N>(wv[i], k, round) << (3 * i);
-      if constexpr (kListAux<N>)
-        (i < 4 ? aux_lo : aux_hi) |= (u64)(inbound_aux<N>(wv[i], k, round) & 0x3FFFu)
-                                     << (14 * (i % 4));
-    }
-  }
-  RBE_STAMP(tt2);
-  // per item: slot code (3 bits) | position in the slot (11 bits), items 0-3 and 4-7
-  u64 sp_lo = 0, sp_hi = 0;
-#pragma unroll 1
-  for (u32 i = 0; i < iters; i++) {
-    const u32 t = threadIdx.x + i * kBlock;
-    u32 slot;
-    const u64 r = (u64)rb + item_lr(t, &slot);
-    const u8 ib = (u8)(ibp >> (8 * i));
-    const u32 inb = (inbp >> (3 * i)) & 7u;
-    u32 cls = T_DONE;
-    if (t < nr && owned<N>(C, r)) {
-      bool done = false;
-      if (shortcut && triage_lazy<N>(P, C, r, ck, ib, inb & 1u, c))
-        done = true;
-      else if (inb & 2u)
-        cls = class_of_role(idle_role(ib));
-      else
-        cls = triage_replica<N, TRACE>(P, C, r, ck, c);
-      if (shortcut) atomicAdd(&s_gst[slot], ((ib & IB_LEAD) ? 1u : 0u) + (done ? 0u : 256u));
-    }
-    // the back of the list: a leader proposing this round, a follower
-    // receiving a Replicate
-    bool back = false;
-    if (cls == T_LEAD)
-      back = wl_input(C, C.cid_base + (u64)((u32)r / (u32)N) * C.cid_stride, round) == 1u;
-    else if (cls == T_FOLL)
-      back = (inb & 4u) != 0;
-    const u32 code = cls == T_DONE ? kNone : (back ? cls + 2u : cls - 1u);
-    u32 pos = 0;
-#pragma unroll
-    for (u32 sl = 0; sl < kSlots; sl++) {
-      const bool want = code == sl;
-      const u64 mask = __ballot(want);
-      if (!mask) continue;
-      const int first = __ffsll((unsigned long long)mask) - 1;
-      u32 base = 0;
-      if (lane == first) base = atomicAdd(&s_n[sl], (u32)__popcll(mask));
-      base = __shfl(base, first, 64);
-      if (want) pos = base + __popcll(mask & ((1ull << lane) - 1ull));
-    }
-    (i < 4 ? sp_lo : sp_hi) |= (u64)(code | (pos << 3)) << (14 * (i % 4));
-  }
-  __syncthreads();
-  const u32 sh = blockIdx.x % kShards;
-  if (threadIdx.x < kSlots) {
-    const u32 n = s_n[threadIdx.x];
-    s_base[threadIdx.x] = n ? atomicAdd(list_cnt(L, threadIdx.x, par, sh), n) : 0u;
-    u32 off = 0;
-    for (u32 q = 0; q < threadIdx.x; q++) off += s_n[q];
-    s_off[threadIdx.x] = off;
-  }
-  // groups whose replicas all completed lazily fall asleep
-  if (shortcut) {
-    for (u32 j = threadIdx.x; j < s_ng; j += kBlock) {
-      const u32 st = s_gst[j];
-      if ((st & 0xFF00u) == 0 && (st >> 31))
-        P.gwake[g0 + ((st >> 16) & 0x7FFFu)] = group_sleep_byte(st & 0xFFu);
-    }
-  }
-  __syncthreads();
-  RBE_STAMP(tt3);
-  // the slots back to back in s_idx; fast-list entries with kListAux carry
-  // block position | summary word << 11
-#pragma unroll 1
-  for (u32 i = 0; i < iters; i++) {
-    const u32 t = threadIdx.x + i * kBlock;
-    const u32 e = (u32)(((i < 4 ? sp_lo : sp_hi) >> (14 * (i % 4))) & 0x3FFFu);
-    const u32 code = e & 7u;
-    if (code == kNone) continue;
-    u32 slot;
-    const u32 lr = item_lr(t, &slot);
-    u32 ent = rb + lr;
-    if (kListAux<N> && code != 2u)
-      ent = lr | ((u32)(((i < 4 ? aux_lo : aux_hi) >> (14 * (i % 4))) & 0x3FFFu) << 11);
-    s_idx[s_off[code] + (e >> 3)] = ent;
-  }
-  __syncthreads();
-  RBE_STAMP(tt4);
-#pragma unroll
-  for (u32 sl = 0; sl < kSlots; sl++) {
-    const u32 li = sl < 3 ? sl : sl - 3;
-    for (u32 j = threadIdx.x; j < s_n[sl]; j += kBlock) {
-      const u32 ent = s_idx[s_off[sl] + j];
-      const u64 at = list_pos(L, li, sh, sl >= 3, s_base[sl] + j);
-      if (kListAux<N> && li < 2) {
-        L.idx[at] = rb + (ent & 0x7FFu);
-        L.aux[at] = ent >> 11;
-      } else {
-        L.idx[at] = ent;
-      }
-    }
-  }
-  RBE_STAMP(tt5);
-  flush_counters<KS_TRIAGE>(P, c);
-  RBE_STAMP(tt6);
-  RBE_PHASE_ADD(2, 0, tt0, tt1);
-  RBE_PHASE_ADD(2, 1, tt1, tt2);
-  RBE_PHASE_ADD(2, 2, tt2, tt3);
-  RBE_PHASE_ADD(2, 3, tt3, tt4);
-  RBE_PHASE_ADD(2, 4, tt4, tt5);
-  RBE_PHASE_ADD(2, 5, tt5, tt6);
-  RBE_PHASE_ADD(2, 7, 0ull, 1ull);
-}
-
-// The fused round (default pipeline): a block triages kTriChunk consecutive
-// replicas exactly like k_triage, but keeps its steady-state leaders (from the
-// front) and followers (from the back) in one LDS list and steps them itself
-// right away; only rounds that need the whole handler table go to the global
-// full list.  One launch replaces triage + two fast-list launches, the work
-// lists never touch HBM, and the latency-bound protocol work of some blocks
-// overlaps the streaming triage of others.
-template <int N, bool TRACE>
-__global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_round(Planes P, Params C, RoundArg ra, Lists L) {
-  __shared__ u32 s_idx[kTriChunk];
-  __shared__ u32 s_nl, s_nf;
-  const Clk ck = clk_of(ra);
-  const u32 round = ck.round;
-  const u32 par = round & 1u;
-  list_clear_next(L, par, 3);  // slot 2: the full list
-  if (threadIdx.x == 0) s_nl = s_nf = 0;
-  __syncthreads();
-  StepCounters c;
-#pragma unroll
-  for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
-  const int lane = threadIdx.x & 63;
-  const u64 lo = (u64)blockIdx.x * kTriChunk;
-  for (u32 j = threadIdx.x; j < kTriChunk; j += kBlock) {
-    const u64 r = lo + j;
-    u32 cls = T_DONE;
-    if (r < C.n_rep && owned<N>(C, r)) cls = triage_replica<N, TRACE>(P, C, r, ck, c);
-#pragma unroll
-    for (u32 li = 0; li < 2; li++) {
-      const bool want = cls == li + 1;
-      const u64 mask = __ballot(want);
-      if (!mask) continue;
-      const int first = __ffsll((unsigned long long)mask) - 1;
-      u32 base = 0;
-      if (lane == first) base = atomicAdd(li == 0 ? &s_nl : &s_nf, (u32)__popcll(mask));
-      base = __shfl(base, first, 64);
-      const u32 pos = base + __popcll(mask & ((1ull << lane) - 1ull));
-      if (want) s_idx[li == 0 ? pos : kTriChunk - 1u - pos] = (u32)r;
-    }
-    list_push(L, 2, par, cls == T_FULL, (u32)r);
-  }
-  __syncthreads();
-  const u32 nl = s_nl, nt = s_nl + s_nf;
-  for (u32 i0 = 0; i0 < nt; i0 += kBlock) {
-    const u32 i = i0 + threadIdx.x;
-    bool slow = false;
-    u32 r = 0;
-    if (i < nl) {
-      r = s_idx[i];
-      slow = !step_fast<N, TRACE, MODE_LEAD>(P, C, r, ck, c);
-    } else if (i < nt) {
-      r = s_idx[kTriChunk - 1u - (i - nl)];
-      slow = !step_fast<N, TRACE, MODE_FOLL>(P, C, r, ck, c);
-    }
-    list_push(L, 2, par, slow, r);
-  }
-  flush_counters<KS_TRIAGE>(P, c);
-}
-
-// Pass 2: the steady-state subset for one role over its list (persistent,
-// grid-stride); rounds outside the subset are moved to the full list.
-template <int N, bool TRACE, int MODE>
-__global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_list(Planes P, Params C, RoundArg ra, Lists L) {
-  const Clk ck = clk_of(ra);
-  const u32 round = ck.round;
-  const u32 par = round & 1u;
-  const u32 li = MODE == MODE_LEAD ? 0u : 1u;
-  __shared__ u32 s_pre[2 * kShards + 1];
-  const u32 slots[2] = {li, 3 + li};
-  seg_build<2>(L, par, slots, s_pre);
-  const u32 n = s_pre[2 * kShards];
-  StepCounters c;
-#pragma unroll
-  for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
-  const u64 stride = (u64)gridDim.x * kBlock;
-  for (u64 i0 = (u64)blockIdx.x * kBlock; i0 < n; i0 += stride) {
-    const u64 i = i0 + threadIdx.x;
-    bool slow = false;
-    u32 r = 0;
-    if (i < n) {
-      const u32 sg = seg_find<2 * kShards>(s_pre, (u32)i);
-      r = L.idx[list_pos(L, li, sg % kShards, sg >= kShards, (u32)i - s_pre[sg])];
-      slow = !step_fast<N, TRACE, MODE>(P, C, r, ck, c);
-    }
-    list_push(L, 2, par, slow, r);
-  }
-  flush_counters<MODE == MODE_LEAD ? KS_FAST_LEAD : KS_FAST_FOLL>(P, c);
-}
-
-// Orders a wave's LDS accesses around a cross-lane hand-off: the wave's DS
-// instructions execute in issue order, so a compiler barrier is all it takes.
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Wave-cooperative row moves for the staged fast steps (StageRow, rbe_fast.h).
-// Load `it` of a plane with CH 16-B chunks per row serves chunk idx % CH of
-// row idx / CH, idx = it * 64 + lane: CH consecutive lanes cover one row, so a
-// wave instruction touches 64 / CH rows.  Row j belongs to lane j (its replica
-// index comes over by shuffle); bit j of `m` says whether lane j takes part.
-template <int N>
-__device__ __forceinline__ void stage_in_wave(const Planes& P, StageRow<N>* rows, u32 r,
-                                              u64 m_any, u64 m_lead) {
-  const int lane = threadIdx.x & 63;
-  constexpr int CC = sizeof(Core) / 16, CH = sizeof(Hot) / 16;
-  uint4 vc[CC], vh[CH], vr[N];
-#pragma unroll
-  for (int it = 0; it < CC; it++) {
-    const int idx = it * 64 + lane, j = idx / CC, q = idx % CC;
-    const u32 rj = __shfl(r, j, 64);
-    if ((m_any >> j) & 1ull) vc[it] = reinterpret_cast<const uint4*>(P.core + rj)[q];
-  }
-#pragma unroll
-  for (int it = 0; it < CH; it++) {
-    const int idx = it * 64 + lane, j = idx / CH, q = idx % CH;
-    const u32 rj = __shfl(r, j, 64);
-    if ((m_any >> j) & 1ull) vh[it] = reinterpret_cast<const uint4*>(P.hot + rj)[q];
-  }
-  if (m_lead) {
-#pragma unroll
-    for (int it = 0; it < N; it++) {
-      const int idx = it * 64 + lane, j = idx / N, q = idx % N;
-      const u32 rj = __shfl(r, j, 64);
-      if ((m_lead >> j) & 1ull) vr[it] = reinterpret_cast<const uint4*>(P.rem + (u64)rj * N)[q];
-    }
-  }
-#pragma unroll
-  for (int it = 0; it < CC; it++) {
-    const int idx = it * 64 + lane, j = idx / CC, q = idx % CC;
-    if ((m_any >> j) & 1ull) reinterpret_cast<uint4*>(&rows[j].core)[q] = vc[it];
-  }
-#pragma unroll
-  for (int it = 0; it < CH; it++) {
-    const int idx = it * 64 + lane, j = idx / CH, q = idx % CH;
-    if ((m_any >> j) & 1ull) reinterpret_cast<uint4*>(&rows[j].hot)[q] = vh[it];
-  }
-  if (m_lead) {
-#pragma unroll
-    for (int it = 0; it < N; it++) {
-      const int idx = it * 64 + lane, j = idx / N, q = idx % N;
-      if ((m_lead >> j) & 1ull) reinterpret_cast<uint4*>(&rows[j].rem[0])[q] = vr[it];
-    }
-  }
-}
-
-template <int N>
-__device__ __forceinline__ void stage_out_wave(const Planes& P, const StageRow<N>* rows, u32 r,
-                                               u64 m_done, u64 m_lead) {
-  const int lane = threadIdx.x & 63;
-  constexpr int CC = sizeof(Core) / 16, CU = sizeof(Upd) / 16, CH = sizeof(Hot) / 16;
-#pragma unroll
-  for (int it = 0; it < CC; it++) {
-    const int idx = it * 64 + lane, j = idx / CC, q = idx % CC;
-    const u32 rj = __shfl(r, j, 64);
-    if ((m_done >> j) & 1ull)
-      reinterpret_cast<uint4*>(P.core + rj)[q] = reinterpret_cast<const uint4*>(&rows[j].core)[q];
-  }
-#pragma unroll
-  for (int it = 0; it < CU; it++) {
-    const int idx = it * 64 + lane, j = idx / CU, q = idx % CU;
-    const u32 rj = __shfl(r, j, 64);
-    if ((m_done >> j) & 1ull)
-      reinterpret_cast<uint4*>(P.upd + rj)[q] = reinterpret_cast<const uint4*>(&rows[j].upd)[q];
-  }
-#pragma unroll
-  for (int it = 0; it < CH; it++) {
-    const int idx = it * 64 + lane, j = idx / CH, q = idx % CH;
-    const u32 rj = __shfl(r, j, 64);
-    if ((m_done >> j) & 1ull)
-      reinterpret_cast<uint4*>(P.hot + rj)[q] = reinterpret_cast<const uint4*>(&rows[j].hot)[q];
-  }
-  if (m_lead) {
-#pragma unroll
-    for (int it = 0; it < N; it++) {
-      const int idx = it * 64 + lane, j = idx / N, q = idx % N;
-      const u32 rj = __shfl(r, j, 64);
-      if ((m_lead >> j) & 1ull)
-        reinterpret_cast<uint4*>(P.rem + (u64)rj * N)[q] =
-            reinterpret_cast<const uint4*>(&rows[j].rem[0])[q];
-    }
-  }
-}
-
-// Pass 2, merged (RBE_MODE=both, the default): the round's steady-state
-// leaders and followers in one launch, so the two roles' waves share the SIMDs
-// instead of running back to back; item i < n_lead is a leader, the rest
-// followers.  The rows a step reads and rewrites whole (Hot, Core, Upd, the
-// leader's remote slots) move between HBM and LDS wave-cooperatively
-// (stage_in_wave / stage_out_wave); the step works on its LDS row.
-template <int N, bool TRACE>
-__global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, Params C,
-                                                                     RoundArg ra, Lists L) {
-  __shared__ StageRow<N> s_rows[kBlock];
-  const Clk ck = clk_of(ra);
-  const u32 round = ck.round;
-  const u32 par = round & 1u;
-  // segments: leader fronts, leader backs, follower fronts, follower backs
-  __shared__ u32 s_pre[4 * kShards + 1];
-  const u32 slots[4] = {0, 3, 1, 4};
-  seg_build<4>(L, par, slots, s_pre);
-  const u32 nl = s_pre[2 * kShards], n = s_pre[4 * kShards];
-  StepCounters c;
-#pragma unroll
-  for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
-  StageRow<N>* wrows = &s_rows[threadIdx.x & ~63u];
-  StageRow<N>* mine = &s_rows[threadIdx.x];
-  const u64 stride = (u64)gridDim.x * kBlock;
-  for (u64 i0 = (u64)blockIdx.x * kBlock; i0 < n; i0 += stride) {
-    const u64 i = i0 + threadIdx.x;
-    const bool lead = i < nl, any = i < n;
-    u32 r = 0, aux = 0;
-    if (any) {
-      const u32 sg = seg_find<4 * kShards>(s_pre, (u32)i);
-      const u64 at = list_pos(L, sg / (2 * kShards), sg % kShards, (sg / kShards) & 1u,
-                              (u32)i - s_pre[sg]);
-      r = L.idx[at];
-      if constexpr (kListAux<N>) aux = L.aux[at];
-    }
-    const u64 m_any = __ballot(any), m_lead = __ballot(lead);
-    bool ok = false;
-    if (m_any) {
-      constexpr int SL = RBE_STAGE_LEAD, SF = RBE_STAGE_FOLL;
-      const u64 m_in = ((SL & STG_IN) ? m_lead : 0ull) | ((SF & STG_IN) ? m_any & ~m_lead : 0ull);
-      const u64 m_out = (SL ? m_lead : 0ull) | (SF ? m_any & ~m_lead : 0ull);
-      if ((SL | SF) & STG_IN) {
-        stage_in_wave<N>(P, wrows, r, m_in, (SL & STG_IN) ? m_lead : 0ull);
-        wave_lds_sync();
-      }
-      if (lead)
-        ok = step_fast<N, TRACE, MODE_LEAD, SL, kListAux<N>>(P, C, r, ck, c, mine, aux);
-      else if (any)
-        ok = step_fast<N, TRACE, MODE_FOLL, SF, kListAux<N>>(P, C, r, ck, c, mine, aux);
-      if constexpr ((SL | SF) != 0) {
-        wave_lds_sync();
-        const u64 m_ok = __ballot(ok) & m_out;
-        stage_out_wave<N>(P, wrows, r, m_ok, SL ? m_ok & m_lead : 0ull);
-        wave_lds_sync();
-      }
-    }
-    list_push(L, 2, par, any && !ok, r);
-  }
-  flush_counters<KS_FAST_LEAD>(P, c);
-}
-
-// Pass 3: the whole handler table over the full list (persistent, grid-stride).
-template <int N, bool TRACE>
-__global__ __launch_bounds__(kBlock) void k_full_list(Planes P, Params C, RoundArg ra, Lists L) {
-  const Clk ck = clk_of(ra);
-  const u32 round = ck.round;
-  __shared__ u32 s_pre[kShards + 1];
-  const u32 slots[1] = {2};
-  seg_build<1>(L, round & 1u, slots, s_pre);
-  const u32 n = s_pre[kShards];
-  StepCounters c;
-#pragma unroll
-  for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
-  for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock) {
-    const u32 sg = seg_find<kShards>(s_pre, (u32)i);
-    step_replica<N, TRACE>(P, C, L.idx[list_pos(L, 2, sg, false, (u32)i - s_pre[sg])], ck, c);
-  }
-  flush_counters<KS_FULL>(P, c);
-}
-
-template <int N>
-__global__ __launch_bounds__(kBlock) void k_launch(Planes P, Params C) {
-  const u64 r = (u64)blockIdx.x * kBlock + threadIdx.x;
-  if (r < C.n_rep) launch_replica<N>(P, C, r);
-}
-
-template <int N>
-__global__ __launch_bounds__(kBlock) void k_isolate(Planes P, Params C, u32 round) {
-  const u64 g = (u64)blockIdx.x * kBlock + threadIdx.x;
-  if (g < C.n_groups) iso_group<N>(P, C, g, round);
-}
-
-// Host input staged by rbe_push_* / rbe_notify_applied (rbe_host.h), one
-// launch per step that has any: records to their replicas' ExtIn slots,
-// applied indexes to the applied plane.
+// Input wakes a sleeping group.  In list mode (Lists::al_on) the group joins
+// the awake list of the round about to run (parity par) and leaves the
+// sleeping totals; the wake byte's word is updated atomically, so the replicas
+// of one group wake it once.
 __global__ __launch_bounds__(kBlock) void k_ext_scatter(Planes P, u32 nrep, const u64* reps,
                                                         const ExtIn* recs, u64 n,
                                                         const u64* app_rep, const u64* app_val,
-                                                        u64 na) {
+                                                        u64 na, Lists L, u32 par) {
   const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
   if (i < n) {
     P.ext[reps[i]] = recs[i];
-    P.gwake[reps[i] / nrep] = GW_AWAKE;  // input wakes a sleeping group
+    const u64 g = reps[i] / nrep;
+    if (L.al_on) {
+      const u32 sh = 8u * (u32)(g & 3u);
+      const u32 old = atomicOr((u32*)(P.gwake + (g & ~3ull)), (u32)GW_AWAKE << sh);
+      if (!((old >> sh) & GW_AWAKE)) {
+        const u32 lead = (old >> (sh + 1u)) & 7u;
+        atomicAdd((unsigned long long*)&L.slp[2 + 2 * (par ^ 1u)], (unsigned long long)(-(u64)nrep));
+        if (lead)
+          atomicAdd((unsigned long long*)&L.slp[3 + 2 * (par ^ 1u)], (unsigned long long)(-(u64)lead));
+        const u32 b = (u32)(g / L.al_gb);
+        L.al[par][(u64)b * L.al_gb + atomicAdd(&L.al_cnt[par * L.al_nblk + b], 1u)] = (u32)g;
+      }
+    } else {
+      P.gwake[g] = GW_AWAKE;
+    }
   }
   if (i < na) P.applied[app_rep[i]] = app_val[i];
 }
@@ -807,10 +149,9 @@ struct rbe_engine {
   u64 in_bytes = 0;          // capacity of both
   hipEvent_t in_ev = nullptr;  // the last upload out of in_pinned has finished
   u8* heap = nullptr;        // payload heap (cfg.heap_bytes; positions in hin.heap)
+  u32 scan_at = 0;           // host copy of Lists::scan_round (the source of its upload)
 };
 
-static constexpr unsigned kFastGrid = 2048;  // persistent grid of k_fast_list
-static constexpr unsigned kFullGrid = 512;  // persistent grid of k_full_list: 2 waves per SIMD, its kernels' occupancy cap
 
 static constexpr int kPlaneAllocs = 20;
 static u64 bytes_of(const Params& C, u64* parts) {
@@ -923,77 +264,13 @@ static int d2h(rbe_engine* e, T* dst, const T* src, u64 n) {
   return RBE_OK;
 }
 
-static unsigned grid_for(u64 n) { return (unsigned)((n + kBlock - 1) / kBlock); }
-
-// One round's launches.  With `ev` (KS_NUM + 1 events) an event is recorded
-// on the engine stream before the first and after every pipeline kernel, so
-// ev[i]..ev[i+1] brackets kernel section i (rbe_profile_rounds).
-template <int N, bool TRACE>
-static int launch_step_t(rbe_engine* e, RoundArg ra,
-                         hipEvent_t* ev = nullptr) {
-  const unsigned g = grid_for(e->C.n_rep);
-  auto mark = [&](int i) {
-    if (ev) HIP_IGNORE(hipEventRecord(ev[i], e->stream));
-  };
-  const unsigned gt = (unsigned)((e->C.n_rep + kTriChunk - 1) / kTriChunk);
-  const unsigned gtg = (unsigned)((e->C.n_groups + kTriGroups<N> - 1) / kTriGroups<N>);
-  const unsigned gs = g < kFullGrid ? g : kFullGrid;
-  if (e->mode == 2) {
-    mark(0);
-    mark(1);
-    mark(2);
-    mark(3);
-    hipLaunchKernelGGL((k_step<N, TRACE>), dim3(g), dim3(kBlock), 0, e->stream, e->P, e->C,
-                       ra);
-    mark(4);
-  } else if (e->mode == 0) {
-    mark(0);
-    hipLaunchKernelGGL((k_round<N, TRACE>), dim3(gt), dim3(kBlock), 0, e->stream, e->P, e->C,
-                       ra, e->L);
-    mark(1);
-    mark(2);
-    mark(3);
-    hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kBlock), 0, e->stream, e->P, e->C,
-                       ra, e->L);
-    mark(4);
-  } else if (e->mode == 3) {
-    mark(0);
-    hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(gtg), dim3(kBlock), 0, e->stream, e->P, e->C,
-                       ra, e->L);
-    mark(1);
-    const unsigned gf = g < kFastGrid ? g : kFastGrid;
-    hipLaunchKernelGGL((k_fast_both<N, TRACE>), dim3(gf), dim3(kBlock), 0, e->stream, e->P, e->C,
-                       ra, e->L);
-    mark(2);
-    mark(3);
-    hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kBlock), 0, e->stream, e->P, e->C,
-                       ra, e->L);
-    mark(4);
-  } else {
-    mark(0);
-    hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(gtg), dim3(kBlock), 0, e->stream, e->P, e->C,
-                       ra, e->L);
-    mark(1);
-    const unsigned gf = g < kFastGrid ? g : kFastGrid;
-    hipLaunchKernelGGL((k_fast_list<N, TRACE, MODE_LEAD>), dim3(gf), dim3(kBlock), 0, e->stream,
-                       e->P, e->C, ra, e->L);
-    mark(2);
-    hipLaunchKernelGGL((k_fast_list<N, TRACE, MODE_FOLL>), dim3(gf), dim3(kBlock), 0, e->stream,
-                       e->P, e->C, ra, e->L);
-    mark(3);
-    hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kBlock), 0, e->stream, e->P, e->C,
-                       ra, e->L);
-    mark(4);
-  }
-  HIP_OK(hipGetLastError());
-  return RBE_OK;
-}
 
 static int launch_step(rbe_engine* e, RoundArg ra,
                        hipEvent_t* ev = nullptr) {
   return dispatch_n(e->C.n, [&](auto NN) {
     constexpr int N = decltype(NN)::value;
-    return e->C.trace ? launch_step_t<N, true>(e, ra, ev) : launch_step_t<N, false>(e, ra, ev);
+    return e->C.trace ? launch_round<N, true>(e->P, e->C, e->L, e->stream, e->mode, ra, ev)
+                      : launch_round<N, false>(e->P, e->C, e->L, e->stream, e->mode, ra, ev);
   });
 }
 
@@ -1083,7 +360,8 @@ int rbe_import_groups(rbe_engine* e, const void* buf, uint64_t bytes, uint32_t f
     HIP_OK(hipStreamSynchronize(e->stream));
     e->hin.resync_applied(app.data(), h.first * e->C.n, app.size());
   }
-  // imported groups start awake (group sleep, rbe_step.h)
+  // imported groups start awake (group sleep, rbe_step.h); the next round
+  // scans every group to rebuild the awake list and the sleeping totals
   HIP_OK(hipMemsetAsync(e->P.gwake + h.first, GW_AWAKE, h.count, e->stream));
   if (resume) {
     // the whole engine moves to the snapshot's round; the work lists of the
@@ -1094,6 +372,12 @@ int rbe_import_groups(rbe_engine* e, const void* buf, uint64_t bytes, uint32_t f
     const u32 clk[2] = {e->round, e->tclk};
     HIP_OK(hipMemcpyAsync(e->d_clk, clk, sizeof(clk), hipMemcpyHostToDevice, e->stream));
   }
+  // the awake lists and the sleeping totals restart from the scan
+  HIP_OK(hipMemsetAsync(e->L.al_cnt, 0, 2 * e->L.al_nblk * sizeof(u32), e->stream));
+  HIP_OK(hipMemsetAsync(e->L.slp, 0, 6 * sizeof(u64), e->stream));
+  e->scan_at = e->round;
+  HIP_OK(hipMemcpyAsync((void*)e->L.scan_round, &e->scan_at, sizeof(u32), hipMemcpyHostToDevice,
+                        e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
   return RBE_OK;
 }
@@ -1241,6 +525,35 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   e->allocs.push_back(e->L.idx);
   e->allocs.push_back(e->L.aux);
   e->allocs.push_back(e->L.counts);
+  {
+    // group sleep in list mode (k_triage): two awake lists of one region per
+    // k_triage block, their counts, the sleeping totals and the scan-round
+    // word, which starts at round 0 (every group starts awake, round 0 scans)
+    const u32 gb = kTriChunk / C.n;
+    const u32 nblk = (u32)((C.n_groups + gb - 1) / gb);
+    u32* w = nullptr;
+    u8* al = nullptr;
+    const u64 wbytes = 2 * (u64)nblk * sizeof(u32) + 6 * sizeof(u64) + 256;
+    if (hipMalloc(&al, 2 * (u64)nblk * gb * sizeof(u32)) != hipSuccess ||
+        hipMalloc(&w, wbytes) != hipSuccess) {
+      if (al) HIP_IGNORE(hipFree(al));
+      rbe_destroy(e);
+      return RBE_E_NOMEM;
+    }
+    e->allocs.push_back(al);
+    e->allocs.push_back(w);
+    HIP_IGNORE(hipMemsetAsync(w, 0, wbytes, e->stream));
+    e->L.al[0] = (u32*)al;
+    e->L.al[1] = (u32*)al + (u64)nblk * gb;
+    e->L.al_nblk = nblk;
+    e->L.al_gb = gb;
+    e->L.slp = (u64*)((u8*)w + ((2 * (u64)nblk * sizeof(u32) + 63) & ~63ull));
+    e->L.al_cnt = w;
+    e->L.scan_round = (const u32*)(e->L.slp + 6);
+    const char* gl = getenv("RBE_GROUP_LIST");  // "0": scan every round (A/B)
+    e->L.al_on = C.quiesce && !C.trace && C.rep_world == 1 && (e->mode == 1 || e->mode == 3) &&
+                 !(gl && strcmp(gl, "0") == 0);
+  }
   if (hipMalloc(&e->xcount, kXchgMaxWorld * XS_NUM * sizeof(u32)) != hipSuccess) {
     rbe_destroy(e);
     return RBE_E_NOMEM;
@@ -1322,7 +635,8 @@ static int flush_inputs(rbe_engine* e) {
   const u64 m = n > na ? n : na;
   hipLaunchKernelGGL(k_ext_scatter, dim3(grid_for(m)), dim3(kBlock), 0, e->stream, e->P,
                      e->C.n, (const u64*)e->in_dev, (const ExtIn*)(e->in_dev + o_rec), n,
-                     (const u64*)(e->in_dev + o_ar), (const u64*)(e->in_dev + o_av), na);
+                     (const u64*)(e->in_dev + o_ar), (const u64*)(e->in_dev + o_av), na, e->L,
+                     e->round & 1u);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(e->in_ev, e->stream));
   // the entries and heap bytes came from pageable memory: wait for those

@@ -1953,6 +1953,17 @@ RBE_HD void group_sleep_round(u8 gw, u32 n_owned, const Clk& ck, StepCounters& c
 }
 // the byte a group that fell asleep this round keeps
 RBE_HD u8 group_sleep_byte(u32 leaders) { return (u8)(leaders << 1); }
+// What a triaged round does to a group's wake byte (`busy` owned replicas did
+// not finish lazily): an awake group whose replicas all finished lazily falls
+// asleep (GS_SLEEP) unless the next round forces input on it, so a sleeping
+// group is never forced outside a scan round (k_triage); a sleeping group that
+// a round forced to step wakes (GS_WAKE) when any replica made a real step, as
+// its messages of this round must be delivered next round.
+enum : u32 { GS_KEEP = 0, GS_SLEEP = 1, GS_WAKE = 2 };
+RBE_HD u32 group_transition(const Params& C, u64 cid, u32 round, bool awake, u32 busy) {
+  if (awake) return busy == 0 && !group_forced(C, cid, round + 1) ? GS_SLEEP : GS_KEEP;
+  return busy > 0 ? GS_WAKE : GS_KEEP;
+}
 
 // the inbound count words of replica r in this round: bit 0 = any non-zero
 // word, bit 1 = any message (a Quiesce notice alone leaves it clear), bit 2 =

@@ -188,7 +188,10 @@ def load_library(path: Optional[str] = None):
         "rbe_export_groups": (i32, [vp, u64, u64, vp, u64]),
         "rbe_import_groups": (i32, [vp, vp, u64, u32]),
     }
+    ab = path is None and os.environ.get("RBE_LIB")  # an older A/B build may lack newer calls
     for name, (res, args) in sig.items():
+        if ab and not hasattr(L, name):
+            continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

@@ -9,7 +9,7 @@ OUT=$ROOT/build/temps
 mkdir -p "$OUT"
 cd "$OUT"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared --save-temps "$@" \
-  -o "$OUT/libtmp.so" "$ROOT/dragonboat_amd/csrc/rbe_engine.hip" 2>/dev/null
+  -DRBE_SINGLE_TU -o "$OUT/libtmp.so" "$ROOT/dragonboat_amd/csrc/rbe_engine.hip" 2>/dev/null
 S=$(ls "$OUT"/*gfx950*.s | head -1)
 python3 - "$S" <<'EOF'
 import re

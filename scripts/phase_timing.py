@@ -2,7 +2,7 @@
 the RBE_PHASE_TIMING build (build/libdragonboat_amd_phase.so).
 
     hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DRBE_PHASE_TIMING \
-        -o build/libdragonboat_amd_phase.so dragonboat_amd/csrc/rbe_engine.hip
+        -DRBE_SINGLE_TU -o build/libdragonboat_amd_phase.so dragonboat_amd/csrc/rbe_engine.hip
     RBE_MODE=split python scripts/phase_timing.py c4
 """
 import ctypes as C

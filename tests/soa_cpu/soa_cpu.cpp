@@ -89,7 +89,12 @@ static void run_round(SoaEngine* e, bool tick = true) {
       if (cls != T_DONE) lists[cls - 1].push_back(r);
       for (int i = 0; i < C_NUM; i++) e->counters[i] += c.v[i];
     }
-    if (shortcut && busy == 0 && (gw & GW_AWAKE)) e->P.gwake[g] = group_sleep_byte(leaders);
+    if (shortcut) {
+      const u32 tr = group_transition(e->C, e->C.cid_base + g * e->C.cid_stride, e->round,
+                                      (gw & GW_AWAKE) != 0, busy);
+      if (tr == GS_SLEEP) e->P.gwake[g] = group_sleep_byte(leaders);
+      if (tr == GS_WAKE) e->P.gwake[g] = GW_AWAKE;
+    }
   }
   for (int li = 0; li < 2; li++) {
     for (u64 r : lists[li]) {
