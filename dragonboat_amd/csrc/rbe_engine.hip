@@ -1037,21 +1037,22 @@ int rbe_get_updates(rbe_engine* e, uint64_t first, uint64_t count, rbe_update* o
     u.commit = core[i].committed;
     u.digest = upd[i].digest;
     u.fault = upd[i].fault;
+    u.save_lo = u.apply_lo = 1;  // empty ranges unless the step wrote them
+    u.save_hi = u.apply_hi = 0;
     if (e->round > 0 && upd[i].round == e->round - 1) {
-      u.save_lo = upd[i].save_lo;
-      u.save_hi = upd[i].save_hi;
-      u.apply_lo = upd[i].apply_lo;
-      u.apply_hi = upd[i].apply_hi;
+      if (upd[i].flags & UF_RANGES) {  // chunks 0-2 of the record are this step's (Upd)
+        u.save_lo = upd[i].save_lo;
+        u.save_hi = upd[i].save_hi;
+        u.apply_lo = upd[i].apply_lo;
+        u.apply_hi = upd[i].apply_hi;
+        u.n_dropped_entries = upd[i].n_drop_ent;
+        u.n_dropped_read_indexes = upd[i].n_drop_ri;
+      }
       u.n_messages = upd[i].n_msgs;
       u.n_ready_to_read = upd[i].n_rtr;
-      u.n_dropped_entries = upd[i].n_drop_ent;
-      u.n_dropped_read_indexes = upd[i].n_drop_ri;
-      u.flags = upd[i].flags;
+      u.flags = upd[i].flags & ~UF_RANGES;
       u.events = upd[i].events;
-    } else {  // an idle round (triage) left the record untouched: empty Update
-      u.save_lo = u.apply_lo = 1;
-      u.save_hi = u.apply_hi = 0;
-    }
+    }  // else an idle round (triage) left the record untouched: empty Update
     // Peer.HasUpdate (peer.go:253-280) and setFastApply / validateUpdate
     // (peer.go:209-245) on the range form
     const bool has = (u.flags & RBE_UF_STATE_CHANGED) || u.n_messages || u.n_ready_to_read ||

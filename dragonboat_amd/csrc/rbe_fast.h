@@ -72,9 +72,12 @@ RBE_HD void rbe_wait_all_loads() {
 }
 
 // max inbound messages per sender held in registers
+#ifndef RBE_LEAD_MAXM3
+#define RBE_LEAD_MAXM3 4
+#endif
 template <int N>
 struct FastCaps {
-  static constexpr u32 MAXM = N <= 3 ? 4 : 5;  // leader: per follower
+  static constexpr u32 MAXM = N <= 3 ? RBE_LEAD_MAXM3 : 5;  // leader: per follower
   static constexpr u32 FMAXM = 6;              // follower: from its leader
   static constexpr u32 RQ = 3;                 // readIndex queue entries in registers
 };
@@ -438,14 +441,18 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
   u.n_drop_ri = (u16)o.n_drop_ri;
   u.fault = o.fault;
   ctr.v[C_FAULTS] += popc8(o.fault & ~o.fault0 & 0xFFu);
+  // chunks 0-2 only when they carry something (Upd, rbe_types.h)
+  const bool ranges = TRACE || (STG & STG_OUT) != 0 || u.save_lo <= u.save_hi ||
+                      u.apply_lo <= u.apply_hi || o.n_drop_ri != 0;
   u.flags = (u16)((c.committed != committed0 ? UF_STATE_CHANGED : 0u) |
-                  (send_q ? UF_SENT_QUIESCE : 0u));
+                  (send_q ? UF_SENT_QUIESCE : 0u) | (ranges ? UF_RANGES : 0u));
   u.events = (u16)o.events;
   u.round = o.round_;
-  u.pad2 = 0;
+  u.pad1 = 0;
 #ifndef RBE_DIAG_NO_STATE_STORES
   if constexpr ((STG & STG_OUT) != 0) sr->upd = u;
-  else P.upd[r] = u;
+  else if (ranges) P.upd[r] = u;
+  else __builtin_memcpy((char*)&P.upd[r] + 48, (const char*)&u + 48, 16);
   // this sender's outbox header: stamp + the N count words, one 16-B store
   {
     u32 w[N];

@@ -828,7 +828,7 @@ __global__ __launch_bounds__(kBlock) void k_isolate(Planes P, Params C, u32 roun
 // applied indexes to the applied plane.
 
 static constexpr unsigned kFastGrid = 2048;  // persistent grid of k_fast_list
-static constexpr unsigned kFullGrid = 512;  // persistent grid of k_full_list: 2 waves per SIMD, its kernels' occupancy cap
+static constexpr unsigned kFullGrid = 256;  // persistent grid of k_full_list: its ~420 registers allow one wave per SIMD, so 256 blocks of 4 waves fill the chip once
 static inline unsigned grid_for(u64 n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 // One round's launches.  With `ev` (KS_NUM + 1 events) an event is recorded

@@ -1780,10 +1780,10 @@ struct Lane {
     u.fault = fault;
     u.flags = (u16)((term != term0 || vote != vote0 || committed != committed0 ? UF_STATE_CHANGED
                                                                                 : 0u) |
-                    (send_q ? UF_SENT_QUIESCE : 0u));
+                    (send_q ? UF_SENT_QUIESCE : 0u) | UF_RANGES);
     u.events = (u16)(events | (leader != leader0 ? EV_LEADER_UPDATED : 0u));
     u.round = round;
-    u.pad2 = 0;
+    u.pad1 = 0;
     P.upd[r] = u;
     // this round's outbox header: the count word of every destination list
     {
@@ -1879,10 +1879,10 @@ RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   u.apply_hi = 0;
   u.n_msgs = u.n_rtr = u.n_drop_ent = u.n_drop_ri = 0;
   u.fault = 0;
-  u.flags = 0;
+  u.flags = UF_RANGES;
   u.events = 0;
   u.round = ~0u;
-  u.pad2 = 0;
+  u.pad1 = 0;
   P.upd[r] = u;
 }
 
@@ -2157,7 +2157,7 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, const Clk& ck
     u.apply_lo = c.processed + 1;
     u.apply_hi = c.committed;
     u.n_msgs = u.n_rtr = u.n_drop_ent = u.n_drop_ri = 0;
-    u.flags = (u16)(qnew ? UF_SENT_QUIESCE : 0u);
+    u.flags = (u16)((qnew ? UF_SENT_QUIESCE : 0u) | UF_RANGES);
     u.events = 0;
     u.round = round;
     P.upd[r] = u;

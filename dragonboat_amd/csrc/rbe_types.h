@@ -141,24 +141,30 @@ struct alignas(16) Ent {
   u64 lo, hi;
 };
 
-// per-replica step output record (Update summary)
+// per-replica step output record (Update summary).  Four
+// 16-B chunks; the last one (fault, flags, events, round, message and
+// ReadyToRead counts) is written by every step.  Chunks 0-2 (digest, the
+// EntriesToSave / CommittedEntries ranges, drop counts) are written only when
+// UF_RANGES is set in that step's flags: an untraced steady-state step with
+// empty ranges and no drops (most C4 rounds) stores one chunk, not four, and a
+// reader treats a record without UF_RANGES as empty ranges and no drops.
 struct alignas(16) Upd {
   u64 digest;       // running trace digest (trace mode)
   u64 save_lo;      // EntriesToSave = [save_lo, save_hi] (empty if lo > hi)
   u64 save_hi;
   u64 apply_lo;     // CommittedEntries = [apply_lo, apply_hi]
   u64 apply_hi;
-  u16 n_msgs;       // messages emitted this step (Update.Messages)
-  u16 n_rtr;        // ReadyToReads
   u16 n_drop_ent;   // DroppedEntries
   u16 n_drop_ri;    // DroppedReadIndexes
+  u32 pad1;
   u32 fault;        // sticky F_* bits
   u16 flags;        // UF_* bits
   u16 events;       // EV_* bits: IRaftEventListener calls of the step
   u32 round;        // round this record was written in (idle rounds leave it stale)
-  u32 pad2;
+  u16 n_msgs;       // messages emitted this step (Update.Messages)
+  u16 n_rtr;        // ReadyToReads
 };
-enum : u32 { UF_STATE_CHANGED = 1, UF_SENT_QUIESCE = 2, UF_HAS_UPDATE = 4 };
+enum : u32 { UF_STATE_CHANGED = 1, UF_SENT_QUIESCE = 2, UF_HAS_UPDATE = 4, UF_RANGES = 0x100 };
 // server.IRaftEventListener (internal/server/event.go) calls a step made, one
 // bit per event kind (raft.go:354, 1090, 1333, 1368, 1503, 1995, 2010).
 // LeaderUpdated fires on every setLeaderID call in the reference, unchanged

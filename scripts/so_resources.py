@@ -9,18 +9,22 @@ import tempfile
 lib = sys.argv[1]
 flt = sys.argv[2] if len(sys.argv) > 2 else ""
 blob = open(lib, "rb").read()
-i = blob.find(b"__CLANG_OFFLOAD_BUNDLE__")
-if i < 0:
+starts = [m.start() for m in re.finditer(b"__CLANG_OFFLOAD_BUNDLE__", blob)]
+if not starts:
     sys.exit("no offload bundle in " + lib)
+notes = ""
 with tempfile.TemporaryDirectory() as d:
-    fb = f"{d}/fat.bin"
-    open(fb, "wb").write(blob[i:])
-    co = f"{d}/co.o"
-    subprocess.run(["/opt/rocm/lib/llvm/bin/clang-offload-bundler", "--type=o", "--unbundle",
-                    f"--input={fb}", f"--output={co}",
-                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950"], check=True)
-    notes = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", co],
-                           capture_output=True, text=True).stdout
+    # one bundle per translation unit (rbe_engine.hip, rbe_round.hip per N and trace)
+    for k, i in enumerate(starts):
+        fb = f"{d}/fat{k}.bin"
+        open(fb, "wb").write(blob[i:starts[k + 1] if k + 1 < len(starts) else len(blob)])
+        co = f"{d}/co{k}.o"
+        r = subprocess.run(["/opt/rocm/lib/llvm/bin/clang-offload-bundler", "--type=o",
+                            "--unbundle", f"--input={fb}", f"--output={co}",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950"], capture_output=True)
+        if r.returncode == 0:
+            notes += subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", co],
+                                    capture_output=True, text=True).stdout
 cur = {}
 rows = []
 for line in notes.splitlines():
