@@ -67,7 +67,133 @@ __global__ __launch_bounds__(kBlock) void k_ext_scatter(Planes P, u32 nrep, cons
       P.gwake[g] = GW_AWAKE;
     }
   }
-  if (i < na) P.applied[app_rep[i]] = app_val[i];
+  if (i < na) apply_pair(P, app_rep[i], app_val[i]);
+}
+
+// ---- batched outputs (rbe_collect_outputs): count → scan → write
+// Exclusive prefix of v over the 256 lanes of a block; *total = the sum.
+__device__ __forceinline__ u32 block_excl_scan(u32 v, u32* total) {
+  __shared__ u32 s_w[kBlock / 64];
+  const u32 lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  u32 x = v;
+#pragma unroll
+  for (u32 o = 1; o < 64; o <<= 1) {
+    const u32 t = __shfl_up(x, o, 64);
+    if (lane >= o) x += t;
+  }
+  __syncthreads();  // s_w may still be read by a previous call
+  if (lane == 63) s_w[w] = x;
+  __syncthreads();
+  u32 off = 0, tot = 0;
+#pragma unroll
+  for (u32 q = 0; q < kBlock / 64; q++) {
+    off += q < w ? s_w[q] : 0u;
+    tot += s_w[q];
+  }
+  *total = tot;
+  return off + x - v;
+}
+// the message and ReadyToRead counts of replica r's last round (rbe_get_messages /
+// rbe_get_ready_to_reads restated per lane)
+__device__ __forceinline__ void out_counts(const Planes& P, const Params& C, u64 r, u32 round,
+                                           u32* nm, u32* nr) {
+  const u32 par = (round - 1u) & 1u;
+  const CntRow row = P.cnt[par][r];
+  u32 m = 0;
+  for (u32 d = 0; d < C.n; d++) {
+    const u32 pc = row_word(row, d, round);
+    m += (pc & 0x7Fu) + ((pc >> 7) & 0x7Fu);
+  }
+  *nm = m;
+  const Upd& u = P.upd[r];
+  *nr = u.round == round - 1u ? (u.n_rtr < C.rtr_cap ? u.n_rtr : C.rtr_cap) : 0u;
+}
+__global__ __launch_bounds__(kBlock) void k_out_count(Planes P, Params C, u64 first, u64 count,
+                                                      u32 round, u32* bsum) {
+  const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+  u32 nm = 0, nr = 0;
+  if (i < count) out_counts(P, C, first + i, round, &nm, &nr);
+  u32 tm, tr;
+  block_excl_scan(nm, &tm);
+  block_excl_scan(nr, &tr);
+  if (threadIdx.x == 0) {
+    bsum[2 * blockIdx.x] = tm;
+    bsum[2 * blockIdx.x + 1] = tr;
+  }
+}
+// one block: exclusive prefix of the block sums (pairs), totals in pre[2 * nb]
+__global__ __launch_bounds__(kBlock) void k_out_scan(const u32* bsum, u32 nb, u64* pre) {
+  u64 cm = 0, cr = 0;
+  for (u32 b0 = 0; b0 < nb; b0 += kBlock) {
+    const u32 b = b0 + threadIdx.x;
+    const u32 vm = b < nb ? bsum[2 * b] : 0u, vr = b < nb ? bsum[2 * b + 1] : 0u;
+    u32 tm, tr;
+    const u32 em = block_excl_scan(vm, &tm), er = block_excl_scan(vr, &tr);
+    if (b < nb) {
+      pre[2 * b] = cm + em;
+      pre[2 * b + 1] = cr + er;
+    }
+    cm += tm;
+    cr += tr;
+  }
+  if (threadIdx.x == 0) {
+    pre[2 * nb] = cm;
+    pre[2 * nb + 1] = cr;
+  }
+}
+__global__ __launch_bounds__(kBlock) void k_out_write(Planes P, Params C, u64 first, u64 count,
+                                                      u32 round, const u64* pre, u64* moff,
+                                                      rbe_message* om, u64* roff,
+                                                      rbe_ready_to_read* orr) {
+  const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+  u32 nm = 0, nr = 0;
+  if (i < count) out_counts(P, C, first + i, round, &nm, &nr);
+  u32 tm, tr;
+  const u64 bm = pre[2 * blockIdx.x] + block_excl_scan(nm, &tm);
+  const u64 br = pre[2 * blockIdx.x + 1] + block_excl_scan(nr, &tr);
+  if (i >= count) return;
+  moff[i] = bm;
+  roff[i] = br;
+  if (i + 1 == count) {
+    moff[count] = bm + nm;
+    roff[count] = br + nr;
+  }
+  const u64 r = first + i;
+  const u32 N = C.n, par = (round - 1u) & 1u;
+  const u64 g = r / N;
+  const u32 k = (u32)(r % N);
+  const CntRow row = P.cnt[par][r];
+  u64 at = bm;
+  for (u32 d = 0; d < N; d++) {
+    const u32 pc = row_word(row, d, round), na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
+    const Msg* lst = &P.msgs[par][((g * N + k) * N + d) * (u64)C.maxm];
+    for (u32 j = 0; j < na + nb; j++, at++) {
+      const Msg m = j < na ? lst[j] : lst[C.maxm - 1u - (j - na)];
+      rbe_message o;
+      o.type = m.type;
+      o.reject = m.reject;
+      o.to = m.to;
+      o.from = m.from;
+      o.cluster_id = C.cid_base + g * C.cid_stride;
+      o.term = m.term;
+      o.log_term = m.log_term;
+      o.log_index = m.log_index;
+      o.commit = m.commit;
+      o.hint = m.hint;
+      o.hint_high = m.hint_high;
+      o.n_entries = m.n_ent;
+      o.reserved = 0;
+      om[at] = o;
+    }
+  }
+  for (u32 j = 0; j < nr; j++) {
+    const RTR x = P.rtr[r * C.rtr_cap + j];
+    rbe_ready_to_read o;
+    o.index = x.index;
+    o.ctx_low = x.low;
+    o.ctx_high = x.high;
+    orr[br + j] = o;
+  }
 }
 
 __global__ void k_advance(u32* clk, u32 k) {
@@ -150,6 +276,11 @@ struct rbe_engine {
   hipEvent_t in_ev = nullptr;  // the last upload out of in_pinned has finished
   u8* heap = nullptr;        // payload heap (cfg.heap_bytes; positions in hin.heap)
   u32 scan_at = 0;           // host copy of Lists::scan_round (the source of its upload)
+  // rbe_collect_outputs: device scratch and the pinned host copy it returns
+  u8* out_dev = nullptr;
+  u64 out_dev_bytes = 0;
+  u8* out_host = nullptr;
+  u64 out_host_bytes = 0;
 };
 
 
@@ -402,6 +533,8 @@ int rbe_destroy(rbe_engine* e) {
   if (e->in_ev) HIP_IGNORE(hipEventDestroy(e->in_ev));
   if (e->in_pinned) HIP_IGNORE(hipHostFree(e->in_pinned));
   if (e->in_dev) HIP_IGNORE(hipFree(e->in_dev));
+  if (e->out_dev) HIP_IGNORE(hipFree(e->out_dev));
+  if (e->out_host) HIP_IGNORE(hipHostFree(e->out_host));
   if (e->stream) HIP_IGNORE(hipStreamDestroy(e->stream));
   delete e;
   return RBE_OK;
@@ -806,6 +939,12 @@ int rbe_report_snapshot_status(rbe_engine* e, uint64_t n, const uint64_t* replic
   return e->hin.report_snapshot_status(n, replica, node_id, reject);
 }
 
+int rbe_set_apply_ready(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint8_t* ready) {
+  if (!e) return RBE_E_INVALID;
+  if (!e->C.ext_inputs) return RBE_E_STATE;
+  return e->hin.set_apply_ready(n, replica, ready);
+}
+
 int rbe_notify_applied(rbe_engine* e, uint64_t n, const uint64_t* replica,
                        const uint64_t* applied) {
   if (!e) return RBE_E_INVALID;
@@ -1108,6 +1247,74 @@ int rbe_get_messages(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t
     }
   }
   *n_out = n;
+  return RBE_OK;
+}
+
+// grow a device (pinned = false) or pinned host buffer to at least `need` bytes
+static int grow(u8** p, u64* have, u64 need, bool pinned) {
+  if (need <= *have) return RBE_OK;
+  if (*p) HIP_OK(pinned ? hipHostFree(*p) : hipFree(*p));
+  *p = nullptr;
+  *have = 0;
+  const u64 cap = need + need / 2 + 4096;
+  if (pinned) HIP_OK(hipHostMalloc((void**)p, cap, hipHostMallocDefault));
+  else HIP_OK(hipMalloc((void**)p, cap));
+  *have = cap;
+  return RBE_OK;
+}
+
+int rbe_collect_outputs(rbe_engine* e, uint64_t first, uint64_t count, rbe_outputs* out) {
+  if (!e || !out || count == 0 || first >= e->C.n_rep || count > e->C.n_rep - first)
+    return RBE_E_INVALID;
+  memset(out, 0, sizeof(*out));
+  out->first = first;
+  out->count = count;
+  if (e->round == 0) return RBE_E_STATE;  // no round has run yet
+  HIP_OK(hipSetDevice(e->device));
+  const u32 nb = grid_for(count);
+  const u64 a8 = 256;
+  auto al = [&](u64 x) { return (x + a8 - 1) & ~(a8 - 1); };
+  // device scratch: block sums | block prefixes (+ totals) | offsets | records
+  const u64 o_pre = al(2ull * nb * sizeof(u32)), o_moff = o_pre + al((2ull * nb + 2) * sizeof(u64));
+  const u64 o_roff = o_moff + al((count + 1) * sizeof(u64));
+  const u64 o_rec = o_roff + al((count + 1) * sizeof(u64));
+  int rc = grow(&e->out_dev, &e->out_dev_bytes, o_rec, false);
+  if (rc) return rc;
+  u32* bsum = (u32*)e->out_dev;
+  u64* pre = (u64*)(e->out_dev + o_pre);
+  hipLaunchKernelGGL(k_out_count, dim3(nb), dim3(kBlock), 0, e->stream, e->P, e->C, (u64)first,
+                     (u64)count, e->round, bsum);
+  hipLaunchKernelGGL(k_out_scan, dim3(1), dim3(kBlock), 0, e->stream, bsum, nb, pre);
+  HIP_OK(hipGetLastError());
+  u64 tot[2];
+  HIP_OK(hipMemcpyAsync(tot, pre + 2ull * nb, sizeof(tot), hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  const u64 o_rtr = o_rec + al(tot[0] * sizeof(rbe_message));
+  const u64 need = o_rtr + al(tot[1] * sizeof(rbe_ready_to_read));
+  if (need > e->out_dev_bytes) {  // keep the block prefixes across the regrow
+    std::vector<u64> keep(2ull * nb + 2);
+    HIP_OK(hipMemcpy(keep.data(), pre, keep.size() * sizeof(u64), hipMemcpyDeviceToHost));
+    if ((rc = grow(&e->out_dev, &e->out_dev_bytes, need, false))) return rc;
+    pre = (u64*)(e->out_dev + o_pre);
+    HIP_OK(hipMemcpy(pre, keep.data(), keep.size() * sizeof(u64), hipMemcpyHostToDevice));
+  }
+  u8* d = e->out_dev;
+  hipLaunchKernelGGL(k_out_write, dim3(nb), dim3(kBlock), 0, e->stream, e->P, e->C, (u64)first,
+                     (u64)count, e->round, (const u64*)(d + o_pre), (u64*)(d + o_moff),
+                     (rbe_message*)(d + o_rec), (u64*)(d + o_roff),
+                     (rbe_ready_to_read*)(d + o_rtr));
+  HIP_OK(hipGetLastError());
+  // one copy of offsets and records into the pinned host buffer
+  if ((rc = grow(&e->out_host, &e->out_host_bytes, need - o_moff, true))) return rc;
+  HIP_OK(hipMemcpyAsync(e->out_host, d + o_moff, need - o_moff, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  u8* h = e->out_host;
+  out->n_messages = tot[0];
+  out->n_ready_to_reads = tot[1];
+  out->msg_off = (const uint64_t*)(h + (o_moff - o_moff));
+  out->rtr_off = (const uint64_t*)(h + (o_roff - o_moff));
+  out->messages = (const rbe_message*)(h + (o_rec - o_moff));
+  out->ready_to_reads = (const rbe_ready_to_read*)(h + (o_rtr - o_moff));
   return RBE_OK;
 }
 

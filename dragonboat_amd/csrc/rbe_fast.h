@@ -364,7 +364,9 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
   u.save_hi = c.last_index;
   u.apply_lo = c.processed + 1;
   u.apply_hi = c.committed;
-  if (c.committed > c.processed) {
+  if (flags & HF_APPLY_HELD) {  // moreEntriesToApply == false (node.go:908-915)
+    u.apply_hi = c.processed;
+  } else if (c.committed > c.processed) {
     // limitSize (entryutils.go:52-64) with sizes 128 + len
     const u64 lo = c.processed + 1, hi = c.committed;
     u64 n = hi - lo + 1;

@@ -60,6 +60,16 @@ struct HostHeap {
   bool valid(u64 pos, u64 len) const { return cap && pos + len <= head && head <= pos + cap; }
 };
 
+// One staged replica-value pair into the planes (k_ext_scatter does the same)
+RBE_HD void apply_pair(const Planes& P, u64 rep, u64 val) {
+  if (rep >> 63) {
+    Hot* h = &P.hot[rep & ~(1ull << 63)];
+    h->flags = val ? (u8)(h->flags & ~HF_APPLY_HELD) : (u8)(h->flags | HF_APPLY_HELD);
+  } else {
+    P.applied[rep] = val;
+  }
+}
+
 struct HostInputs {
   u64 n_rep = 0;
   u32 n = 0;
@@ -70,7 +80,9 @@ struct HostInputs {
   std::vector<u64> reps;    // staged replicas ...
   std::vector<ExtIn> recs;  // ... and their input records
   std::vector<Ent> ents;    // staged proposal entries (Planes::in_ents)
-  std::vector<u64> app_rep, app_val;  // staged rbe_notify_applied values
+  // staged replica-value pairs: rbe_notify_applied values, and with bit 63 of
+  // the replica word set, rbe_set_apply_ready flags (value 1 = ready)
+  std::vector<u64> app_rep, app_val;
   std::vector<u64> applied;  // [n_rep] host mirror of Planes::applied (the host is its only writer)
 
   HostHeap heap;             // payload heap positions and staged bytes
@@ -255,6 +267,16 @@ struct HostInputs {
     }
     return RBE_OK;
   }
+  int set_apply_ready(u64 cnt, const u64* replica, const u8* ready) {
+    if (cnt && !ready) return RBE_E_INVALID;
+    int rc = check_replicas(cnt, replica, 0);
+    if (rc) return rc;
+    for (u64 i = 0; i < cnt; i++) {
+      app_rep.push_back(replica[i] | (1ull << 63));
+      app_val.push_back(ready[i] ? 1u : 0u);
+    }
+    return RBE_OK;
+  }
   // Write the staged input into host-resident planes (the test-only host build;
   // the HIP engine uploads the same vectors and scatters them on device).
   // resync the applied mirror after the plane was overwritten (snapshot import)
@@ -267,7 +289,7 @@ struct HostInputs {
       P.gwake[reps[i] / n] = GW_AWAKE;  // input wakes a sleeping group
     }
     for (size_t i = 0; i < ents.size(); i++) P.in_ents[i] = ents[i];
-    for (size_t i = 0; i < app_rep.size(); i++) P.applied[app_rep[i]] = app_val[i];
+    for (size_t i = 0; i < app_rep.size(); i++) apply_pair(P, app_rep[i], app_val[i]);
   }
 };
 

@@ -169,6 +169,18 @@ RBE_HD void update_commit(u64 save_lo, u64 save_hi, u64 apply_lo, u64 apply_hi, 
   if (snap_index != 0 && snap_index > *processed) *processed = snap_index;
 }
 
+// entryutils.go:97-104 / 106-114: message types only a node makes for its own
+// raft (Peer.Handle panics on them), and response types (dropped when the
+// sender is not a member)
+RBE_HD bool is_local_message(u32 t) {
+  return t == M_Election || t == M_LeaderHeartbeat || t == M_Unreachable || t == M_SnapshotStatus ||
+         t == M_CheckQuorum || t == M_LocalTick || t == M_BatchedReadIndex;
+}
+RBE_HD bool is_response_message(u32 t) {
+  return t == M_ReplicateResp || t == M_RequestVoteResp || t == M_HeartbeatResp ||
+         t == M_ReadIndexResp || t == M_Unreachable || t == M_SnapshotStatus ||
+         t == M_LeaderTransfer;
+}
 RBE_HD bool is_leader_message(u32 t) {  // raft.go:1382-1385
   return t == M_Replicate || t == M_InstallSnapshot || t == M_Heartbeat || t == M_TimeoutNow ||
          t == M_ReadIndexResp;
@@ -1711,7 +1723,9 @@ struct Lane {
     u.save_hi = last;
     u.apply_lo = processed + 1;
     u.apply_hi = committed;
-    if (committed > processed) {
+    if (flags & HF_APPLY_HELD) {  // moreEntriesToApply == false (node.go:908-915)
+      u.apply_hi = processed;
+    } else if (committed > processed) {
       u64 cnt = limit_count(processed + 1, committed);
       u.apply_hi = processed + cnt;
     }

@@ -67,6 +67,9 @@ enum : u8 {
   HF_IS_LTT = 4,        // raft.isLeaderTransferTarget
   HF_APPLY_PENDING = 8, // processed < committed after the step (apply limited by size)
   HF_FAULTED = 16,      // Upd.fault != 0 (the sticky fault word is read only then)
+  HF_APPLY_HELD = 64,   // the node's apply queue is full (rbe_set_apply_ready, the
+                        // moreEntriesToApply = false of node.go:908-915): the step
+                        // returns no CommittedEntries
   HF_APPLIED_NEW = 32,  // the last step returned committed entries: the node's
                         // confirmedIndex lags its applied index until the next
                         // step (node.go:907-923, 1033), an event of its own

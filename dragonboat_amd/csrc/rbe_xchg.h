@@ -234,6 +234,12 @@ int messages_to_records(const Params& C, u32 round, u64 n, const u64* group,
   for (u64 i = 0; i < n; i++) {
     const rbe_message& m = msgs[i];
     const u64 g = group[i];
+    // Peer.Handle (peer.go:186-198): a local message type is a caller bug (the
+    // reference panics); a response from a node that is not a member of the
+    // group is dropped.  Other messages from non-members cannot be held by a
+    // slot-indexed group and are refused.
+    if (m.type >= 26 || is_local_message(m.type)) return RBE_E_INVALID;
+    if ((m.from < 1 || m.from > N) && is_response_message(m.type) && m.n_entries == 0) continue;
     if (g >= C.n_groups || m.from < 1 || m.from > N || m.to < 1 || m.to > N || m.from == m.to)
       return RBE_E_INVALID;
     const u32 s = (u32)m.from - 1u, d = (u32)m.to - 1u;

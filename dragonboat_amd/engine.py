@@ -111,6 +111,17 @@ class RbeReadyToRead(C.Structure):
     _fields_ = [("index", C.c_uint64), ("ctx_low", C.c_uint64), ("ctx_high", C.c_uint64)]
 
 
+class RbeOutputs(C.Structure):
+    _fields_ = [("first", C.c_uint64), ("count", C.c_uint64), ("n_messages", C.c_uint64),
+                ("n_ready_to_reads", C.c_uint64), ("msg_off", C.POINTER(C.c_uint64)),
+                ("messages", C.POINTER(RbeMessage)), ("rtr_off", C.POINTER(C.c_uint64)),
+                ("ready_to_reads", C.POINTER(RbeReadyToRead))]
+
+
+MESSAGE_DTYPE = _np_dtype(RbeMessage)
+RTR_DTYPE = _np_dtype(RbeReadyToRead)
+
+
 # exported symbols of include/rbe.h (checked by tests/test_capi.py)
 EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe_step", "rbe_step_ex", "rbe_run",
            "rbe_sync", "rbe_request_leader_transfer", "rbe_report_unreachable",
@@ -121,7 +132,7 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_footprint", "rbe_profile_rounds", "rbe_get_kernel_counters", "rbe_kernel_name",
            "rbe_xchg_record_bytes", "rbe_xchg_pack", "rbe_xchg_unpack", "rbe_get_outbox",
            "rbe_push_messages", "rbe_snapshot_bytes", "rbe_export_groups", "rbe_import_groups",
-           "rbe_get_entry_cmds"]
+           "rbe_get_entry_cmds", "rbe_set_apply_ready", "rbe_collect_outputs"]
 KERNEL_SLOTS = 4
 
 _lib = None
@@ -160,6 +171,7 @@ def load_library(path: Optional[str] = None):
         "rbe_report_unreachable": (i32, [vp, u64, P(u64), P(u64)]),
         "rbe_report_snapshot_status": (i32, [vp, u64, P(u64), P(u64), P(C.c_uint8)]),
         "rbe_notify_applied": (i32, [vp, u64, P(u64), P(u64)]),
+        "rbe_set_apply_ready": (i32, [vp, u64, P(u64), P(C.c_uint8)]),
         "rbe_run": (i32, [vp, u32]),
         "rbe_sync": (i32, [vp]),
         "rbe_round": (i32, [vp, P(u32)]),
@@ -174,6 +186,7 @@ def load_library(path: Optional[str] = None):
         "rbe_get_entries": (i32, [vp, u64, u64, u64, P(RbeEntry)]),
         "rbe_get_entry_cmds": (i32, [vp, u64, u64, u64, vp, u64, P(u64)]),
         "rbe_get_views": (i32, [vp, u64, u64, P(RbeReplicaView)]),
+        "rbe_collect_outputs": (i32, [vp, u64, u64, P(RbeOutputs)]),
         "rbe_get_counters": (i32, [vp, P(u64)]),
         "rbe_reset_counters": (i32, [vp]),
         "rbe_fault_summary": (i32, [vp, P(u64), P(u32)]),
@@ -324,6 +337,12 @@ class NodeInputs:
     def notify_applied(self, replicas, applied):
         _check_input(self._input("notify_applied", len(replicas), _u64s(replicas),
                                                  _u64s(applied)), "rbe_notify_applied")
+
+    def set_apply_ready(self, replicas, ready):
+        """node.canHaveMoreEntriesToApply per replica (sticky; ready by default)."""
+        r = (C.c_uint8 * max(1, len(ready)))(*[1 if x else 0 for x in ready])
+        _check_input(self._input("set_apply_ready", len(replicas), _u64s(replicas), r),
+                     "rbe_set_apply_ready")
 
 
 class Engine(NodeInputs):
@@ -510,6 +529,25 @@ class Engine(NodeInputs):
         m = (RbeMessage * max(1, n))(*msgs)
         e = (RbeEntry * max(1, len(ents)))(*ents)
         _check(self.lib.rbe_push_messages(self.h, n, g, m, e), "rbe_push_messages")
+
+    def collect_outputs(self, first: int = 0, count: Optional[int] = None):
+        """rbe_collect_outputs: (msg_off, messages, rtr_off, ready_to_reads) of
+        replicas [first, first + count) as numpy arrays (copies of the
+        engine's pinned buffers, which the next call or step reuses)."""
+        count = self.n_rep - first if count is None else count
+        o = RbeOutputs()
+        _check(self.lib.rbe_collect_outputs(self.h, first, count, C.byref(o)),
+               "rbe_collect_outputs")
+
+        def arr(ptr, n, dtype):
+            if n == 0:
+                return np.zeros(0, dtype=dtype)
+            raw = C.string_at(C.cast(ptr, C.c_void_p), n * dtype.itemsize)
+            return np.frombuffer(raw, dtype=dtype).copy()
+
+        u64 = np.dtype(np.uint64)
+        return (arr(o.msg_off, count + 1, u64), arr(o.messages, o.n_messages, MESSAGE_DTYPE),
+                arr(o.rtr_off, count + 1, u64), arr(o.ready_to_reads, o.n_ready_to_reads, RTR_DTYPE))
 
     def ready_to_reads(self, replica: int):
         cap = 64

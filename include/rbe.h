@@ -271,7 +271,12 @@ int rbe_profile_rounds(rbe_engine* e, uint32_t rounds, float* ms_per_kernel);
  *     network messages (node.go:1207-1220 handles them in the inbox).
  *   rbe_notify_applied: Peer.NotifyRaftLastApplied (peer.go:312-315): the
  *     applied index the state machine confirmed, raft.applied, which gates
- *     campaigns (hasConfigChangeToApply, raft.go:1460-1472); needs cfg.ext_apply. */
+ *     campaigns (hasConfigChangeToApply, raft.go:1460-1472); needs cfg.ext_apply.
+ *   rbe_set_apply_ready: whether the node can take more entries to apply
+ *     (node.canHaveMoreEntriesToApply, node.go:1002-1004, the moreEntriesToApply
+ *     argument of Peer.HasUpdate / GetUpdate, peer.go:201, 253, 329-331); sticky
+ *     per replica, ready by default.  While not ready a step returns no
+ *     CommittedEntries. */
 int rbe_push_proposals(rbe_engine* e, uint64_t n, const uint64_t* replica,
                        const uint32_t* n_ents, const uint32_t* type, const uint32_t* cmd_len,
                        const uint8_t* cmd);
@@ -285,6 +290,7 @@ int rbe_report_snapshot_status(rbe_engine* e, uint64_t n, const uint64_t* replic
                                const uint64_t* node_id, const uint8_t* reject);
 int rbe_notify_applied(rbe_engine* e, uint64_t n, const uint64_t* replica,
                        const uint64_t* applied);
+int rbe_set_apply_ready(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint8_t* ready);
 
 /* Results of the last round.  Replaces Peer.GetUpdate (peer.go:201-207);
  * Peer.Commit (peer.go:282-293) is implicit (the harness persists and
@@ -306,6 +312,24 @@ int rbe_get_entries(rbe_engine* e, uint64_t replica, uint64_t lo, uint64_t hi,
 int rbe_get_entry_cmds(rbe_engine* e, uint64_t replica, uint64_t lo, uint64_t hi, uint8_t* buf,
                        uint64_t cap, uint64_t* offsets);
 int rbe_get_views(rbe_engine* e, uint64_t first, uint64_t count, rbe_replica_view* out);
+
+/* The last round's Update.Messages and Update.ReadyToReads of replicas
+ * [first, first + count) in one call: compacted on the device (a count pass,
+ * a scan, a write pass) and copied once into engine-owned pinned buffers.
+ * Replica first + i owns messages[msg_off[i] .. msg_off[i + 1]) (per
+ * destination in ascending node id, Replicate messages first, as
+ * rbe_get_messages) and ready_to_reads[rtr_off[i] .. rtr_off[i + 1]).  The
+ * pointers stay valid until the next rbe_collect_outputs, rbe_step/rbe_run or
+ * rbe_destroy.  This is the batched read of the per-node Update the node loop
+ * does after stepping every node (node.go:907-923, execengine.go:494-560). */
+typedef struct rbe_outputs {
+  uint64_t first, count, n_messages, n_ready_to_reads;
+  const uint64_t* msg_off;              /* count + 1 */
+  const rbe_message* messages;
+  const uint64_t* rtr_off;              /* count + 1 */
+  const rbe_ready_to_read* ready_to_reads;
+} rbe_outputs;
+int rbe_collect_outputs(rbe_engine* e, uint64_t first, uint64_t count, rbe_outputs* out);
 int rbe_get_counters(rbe_engine* e, uint64_t* out /* RBE_CTR_NUM */);
 /* the counters one pipeline kernel (RBE_KERNEL_*) contributed */
 int rbe_get_kernel_counters(rbe_engine* e, int32_t kernel, uint64_t* out /* RBE_CTR_NUM */);

@@ -68,6 +68,7 @@ struct Node {
   u64 x_xfer = 0;
   u32 x_unreach = 0, x_snap = 0, x_snap_reject = 0;
   u64 x_applied = 0;
+  bool more_to_apply = true;    // node.canHaveMoreEntriesToApply (sticky, PUSH_APPLY_READY)
   std::vector<Message> in[8];   // this round's inbox, per sender slot (stream order)
   std::vector<Message> nxt[8];  // next round's inbox
   ~Node() { delete peer; }
@@ -329,8 +330,10 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
       deliver(m);
     }
   }
-  if (p->HasUpdate(true) || nd->confirmedIndex != nd->smAppliedIndex) {
-    Update ud = p->GetUpdate(true, nd->smAppliedIndex);
+  // node.getUpdate (node.go:907-923) with moreEntriesToApply from the node's
+  // apply queue (canHaveMoreEntriesToApply, node.go:1002-1004)
+  if (p->HasUpdate(nd->more_to_apply) || nd->confirmedIndex != nd->smAppliedIndex) {
+    Update ud = p->GetUpdate(nd->more_to_apply, nd->smAppliedIndex);
     nd->confirmedIndex = nd->smAppliedIndex;
     for (auto& m : ud.messages) {
       msgHash = hash_message(msgHash, m);
@@ -474,6 +477,7 @@ int harness_push(Harness* h, int kind, u64 replica, u64 a, u64 b, const Entry* e
       else nd->x_snap_reject &= ~(1u << (a - 1));
       return 0;
     case PUSH_APPLIED: nd->x_applied = a; return 0;
+    case PUSH_APPLY_READY: nd->more_to_apply = a != 0; return 0;
     default: return -1;
   }
 }

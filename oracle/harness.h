@@ -71,7 +71,7 @@ struct HarnessConfig {
 
 // host inputs for the next round (the engine's rbe_push_* / rbe_notify_applied)
 enum HarnessPush { PUSH_PROPOSE = 1, PUSH_READ = 2, PUSH_XFER = 3, PUSH_UNREACH = 4,
-                   PUSH_SNAPST = 5, PUSH_APPLIED = 6 };
+                   PUSH_SNAPST = 5, PUSH_APPLIED = 6, PUSH_APPLY_READY = 7 };
 
 struct ReplicaView {  // mirrors rbe_replica_view in include/rbe.h
   u64 term, vote, leader_id, committed, last_index, processed, saved_to, digest;

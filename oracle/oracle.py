@@ -99,7 +99,8 @@ class ReplicaView(C.Structure):
 
 VIEW_FIELDS = [f[0] for f in ReplicaView._fields_ if f[0] != "pad"]
 # harness_push kinds (oracle/harness.h HarnessPush)
-PUSH_PROPOSE, PUSH_READ, PUSH_XFER, PUSH_UNREACH, PUSH_SNAPST, PUSH_APPLIED = range(1, 7)
+PUSH_PROPOSE, PUSH_READ, PUSH_XFER, PUSH_UNREACH, PUSH_SNAPST, PUSH_APPLIED, PUSH_APPLY_READY = \
+    range(1, 8)
 
 _lib = None
 

@@ -17,7 +17,8 @@ def _cmd(rng):
     return bytes(rng.randrange(256) for _ in range(rng.randrange(17)))
 
 
-def plan_round(rng, n_rep, n, rnd, views, ext_apply, density=0.3, applied=None, cmd=None):
+def plan_round(rng, n_rep, n, rnd, views, ext_apply, density=0.3, applied=None, cmd=None,
+               ready=0.0):
     """One round of host input: a list of (kind, replica, args).  `cmd(rng)`
     draws a proposal's Cmd (default: 0-16 bytes)."""
     cmd = cmd or _cmd
@@ -40,6 +41,9 @@ def plan_round(rng, n_rep, n, rnd, views, ext_apply, density=0.3, applied=None, 
             v = max(applied[r], views[r].processed - rng.randrange(4))
             applied[r] = v
             ops.append(("applied", r, v))
+        if ready and rng.random() < ready:
+            # the node's apply queue fills up / drains (canHaveMoreEntriesToApply)
+            ops.append(("ready", r, rng.random() < 0.6))
     return ops
 
 
@@ -60,6 +64,8 @@ def apply_engine(eng, ops):
                                    [a[1] for _, a in by["snapst"]])
     if "applied" in by:
         eng.notify_applied([r for r, _ in by["applied"]], [a for _, a in by["applied"]])
+    if "ready" in by:
+        eng.set_apply_ready([r for r, _ in by["ready"]], [a for _, a in by["ready"]])
 
 
 def apply_oracle(h, ops):
@@ -76,10 +82,12 @@ def apply_oracle(h, ops):
             h.push(O.PUSH_SNAPST, r, a[0], int(a[1]))
         elif kind == "applied":
             h.push(O.PUSH_APPLIED, r, a)
+        elif kind == "ready":
+            h.push(O.PUSH_APPLY_READY, r, int(a))
 
 
 def run_driven(eng, ref, rounds, seed=1, tick_every=1, inputs=True, ext_apply=False,
-               density=0.3, skip=(), cmd=None, on_ops=None):
+               density=0.3, skip=(), cmd=None, on_ops=None, ready=0.0):
     """Step both `rounds` rounds with the same input; every `tick_every`-th
     round ticks, the others are RBE_STEP_NO_TICK rounds.  Returns the first
     divergence (round, replica, field, engine, oracle) or None."""
@@ -90,7 +98,7 @@ def run_driven(eng, ref, rounds, seed=1, tick_every=1, inputs=True, ext_apply=Fa
     applied = [0] * n_rep
     for rnd in range(rounds):
         if inputs:
-            ops = plan_round(rng, n_rep, n, rnd, views, ext_apply, density, applied, cmd)
+            ops = plan_round(rng, n_rep, n, rnd, views, ext_apply, density, applied, cmd, ready)
             if on_ops:
                 on_ops(ops)
             apply_engine(eng, ops)

@@ -308,6 +308,11 @@ int soa_push_proposals(void* h, uint64_t n, const uint64_t* replica, const uint3
   if (!e->C.ext_inputs) return RBE_E_STATE;
   return e->hin.push_proposals(n, replica, n_ents, type, cmd_len, cmd);
 }
+int soa_set_apply_ready(void* h, uint64_t n, const uint64_t* replica, const uint8_t* ready) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (!e->C.ext_inputs) return RBE_E_STATE;
+  return e->hin.set_apply_ready(n, replica, ready);
+}
 int soa_push_read_index(void* h, uint64_t n, const uint64_t* replica, const uint64_t* lo,
                         const uint64_t* hi) {
   SoaEngine* e = (SoaEngine*)h;

@@ -45,6 +45,20 @@ def test_gpu_driven_inputs_with_lagging_applied(gpu_available):
     eng.close()
 
 
+def test_gpu_apply_ready_gate(gpu_available):
+    """rbe_set_apply_ready toggled at random with a lagging applied index
+    (tests/test_node_inputs.py::test_apply_ready_gate on the HIP engine)."""
+    from dragonboat_amd.engine import Engine
+    kw = dict(C2, n_groups=12, ext_inputs=True, ext_apply=True)
+    # a held replica's unapplied entries must stay in the device window
+    eng = Engine(device=0, trace=True, ring=256, **dict(kw, **dict(DRIVEN, ecap=256)))
+    ref = O.Harness(**kw)
+    d = run_driven(eng, ref, 200, seed=13, ext_apply=True, ready=0.2)
+    assert d is None, f"first divergence {d}"
+    assert eng.fault_summary()[0] == 0
+    eng.close()
+
+
 @pytest.mark.parametrize("trace", [True, False])
 def test_gpu_rounds_without_tick(gpu_available, trace):
     kw = dict(C4, n_groups=24)

@@ -1,0 +1,65 @@
+"""rbe_collect_outputs on the HIP engine: the device-compacted batch of every
+replica's Update.Messages and ReadyToReads (node.go:907-923 read for all nodes
+at once) equals what the per-replica calls rbe_get_messages /
+rbe_get_ready_to_reads return, round after round, for whole engines and for
+replica sub-ranges; rounds that read at followers and leaders (C4) and
+elections with rejections (C3) included."""
+import numpy as np
+import pytest
+
+from parity_util import C2, C3, C4
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("type", "reject", "to", "from_", "cluster_id", "term", "log_term", "log_index",
+          "commit", "hint", "hint_high", "n_entries")
+
+
+def _check(eng, first, count):
+    moff, msgs, roff, rtrs = eng.collect_outputs(first, count)
+    assert moff[0] == 0 and roff[0] == 0
+    assert moff[-1] == len(msgs) and roff[-1] == len(rtrs)
+    for i in range(count):
+        ref = eng.messages(first + i)
+        got = msgs[moff[i]:moff[i + 1]]
+        assert len(got) == len(ref), (first + i, len(got), len(ref))
+        for a, b in zip(got, ref):
+            assert tuple(a[f] for f in FIELDS) == tuple(getattr(b, f) for f in FIELDS)
+        rr = eng.ready_to_reads(first + i)
+        gr = [tuple(x) for x in rtrs[roff[i]:roff[i + 1]].tolist()]
+        assert gr == [tuple(x) for x in rr], (first + i, gr, rr)
+    return len(msgs), len(rtrs)
+
+
+@pytest.mark.parametrize("name,kw,extra", [("C2", C2, {}), ("C3", C3, dict(ring=128)),
+                                           ("C4", C4, {})])
+def test_gpu_collect_outputs_match_per_replica(gpu_available, name, kw, extra):
+    from dragonboat_amd.engine import Engine
+    kw = dict(kw, n_groups=min(kw["n_groups"], 48))
+    eng = Engine(device=0, trace=True, **dict(kw, **extra))
+    nm = nr = 0
+    for rnd in range(120):
+        eng.step()
+        if rnd % 7 == 3 or rnd > 110:
+            a, b = _check(eng, 0, eng.n_rep)
+            nm, nr = nm + a, nr + b
+            _check(eng, 5, eng.n_rep - 11)  # a sub-range not aligned to groups or blocks
+    assert nm > 0
+    if name == "C4":
+        assert nr > 0
+    eng.close()
+
+
+def test_gpu_collect_outputs_large(gpu_available):
+    """A 200k-group C4 engine: offsets span several scan blocks' worth of lists."""
+    from dragonboat_amd.engine import Engine
+    eng = Engine(device=0, **dict(C4, n_groups=200_000))
+    eng.run(260)
+    moff, msgs, roff, rtrs = eng.collect_outputs()
+    assert np.all(np.diff(moff.astype(np.int64)) >= 0) and moff[-1] == len(msgs)
+    assert np.all(np.diff(roff.astype(np.int64)) >= 0) and roff[-1] == len(rtrs)
+    assert len(msgs) > 10_000 and len(rtrs) > 1_000
+    for r in (0, 1, 2, 99_999, 599_997, 599_999):
+        assert moff[r + 1] - moff[r] == len(eng.messages(r))
+        assert roff[r + 1] - roff[r] == len(eng.ready_to_reads(r))
+    eng.close()

@@ -61,6 +61,21 @@ def test_driven_inputs_with_lagging_applied():
     assert eng.faults()[0] == 0
 
 
+@pytest.mark.parametrize("name,kw", [("C2", C2), ("C3", C3)])
+def test_apply_ready_gate(name, kw):
+    """rbe_set_apply_ready: while a node's apply queue is full
+    (canHaveMoreEntriesToApply false, node.go:1002-1004) its Update carries no
+    CommittedEntries (peer.go:329-331, HasUpdate 253-280); entries wait and are
+    applied once it is ready again.  With a lagging applied index too."""
+    kw = dict(kw, n_groups=12)
+    eng, ref = _pair(kw, name, ext_inputs=True, ext_apply=True)
+    # a held replica's unapplied entries must stay in the device window
+    eng = SoaCpu(trace=True, **dict(kw, ext_inputs=True, ext_apply=True, **dict(DRIVEN, ecap=256), ring=256))
+    d = run_driven(eng, ref, 200, seed=13, ext_apply=True, ready=0.2)
+    assert d is None, f"{name}: first divergence {d}"
+    assert eng.faults()[0] == 0
+
+
 def test_campaign_skipped_while_applied_lags():
     """hasConfigChangeToApply (raft.go:1460-1472): with the state machine
     holding applied at 0, an election timeout skips the campaign and fires

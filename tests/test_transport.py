@@ -55,3 +55,21 @@ def test_push_rejects_bad_batches():
     one.step()
     with pytest.raises(RuntimeError):  # rep_world 1: every sender is local
         one.push_messages([0], [m], [])
+
+
+def test_push_filters_like_peer_handle():
+    """Peer.Handle (peer.go:186-198): a local message type is refused (the
+    reference panics), a response from a node outside the group is dropped,
+    and the rest of the batch is delivered."""
+    from dragonboat_amd.engine import RbeMessage
+    kw = dict(n_groups=4, n_replicas=3, wl_enabled=True, wl_start_round=5)
+    e = SoaCpu(trace=True, rep_world=2, rep_rank=0, **kw)
+    e.step()
+    for local in (1, 2, 8, 9, 10, 0, 11):  # Election ... BatchedReadIndex (entryutils.go:97-104)
+        with pytest.raises(RuntimeError):
+            e.push_messages([0], [RbeMessage(type=local, to=1, from_=2, term=1)], [])
+    # a HeartbeatResp from node 7, not a member of a 3-node group: dropped
+    e.push_messages([0], [RbeMessage(type=18, to=1, from_=7, term=1)], [])
+    # a RequestVote from a non-member cannot be represented: refused
+    with pytest.raises(RuntimeError):
+        e.push_messages([0], [RbeMessage(type=14, to=1, from_=7, term=9)], [])
