@@ -196,6 +196,23 @@ __global__ __launch_bounds__(kBlock) void k_out_write(Planes P, Params C, u64 fi
   }
 }
 
+// rbe_launch: one lane per relaunched replica (rbe_step.h relaunch_replica)
+struct LaunchRec {
+  u64 replica, term, vote, commit, last, off;  // off: first row in the terms/bodies arrays
+  u32 n, pad;
+};
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_relaunch(Planes P, Params C, const LaunchRec* rec,
+                                                     u64 n, const u64* terms, const Body* bodies,
+                                                     u32 ppar, u32 tclk) {
+  const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const LaunchRec x = rec[i];
+  relaunch_replica<N>(P, C, x.replica, x.term, x.vote, x.commit, x.last, x.n, terms + x.off,
+                      bodies + x.off, ppar, tclk);
+  P.gwake[x.replica / N] = GW_AWAKE;
+}
+
 __global__ void k_advance(u32* clk, u32 k) {
   clk[0] += k;
   clk[1] += k;
@@ -937,6 +954,54 @@ int rbe_report_snapshot_status(rbe_engine* e, uint64_t n, const uint64_t* replic
   if (!e) return RBE_E_INVALID;
   if (!e->C.ext_inputs) return RBE_E_STATE;
   return e->hin.report_snapshot_status(n, replica, node_id, reject);
+}
+
+int rbe_launch(rbe_engine* e, uint64_t n, const uint64_t* replica, const rbe_launch_state* st,
+               const rbe_entry* ents) {
+  if (!e) return RBE_E_INVALID;
+  std::vector<u64> terms;
+  std::vector<Body> bodies;
+  int rc = launch_rows(e->C, n, replica, st, ents, terms, bodies);
+  if (rc || n == 0) return rc;
+  {  // one replica at most once
+    std::vector<u64> v(replica, replica + n);
+    std::sort(v.begin(), v.end());
+    if (std::adjacent_find(v.begin(), v.end()) != v.end()) return RBE_E_INVALID;
+  }
+  HIP_OK(hipSetDevice(e->device));
+  std::vector<LaunchRec> rec(n);
+  u64 off = 0;
+  for (u64 i = 0; i < n; i++) {
+    rec[i] = LaunchRec{replica[i], st[i].term, st[i].vote, st[i].commit, st[i].last_index, off,
+                       st[i].n_entries, 0};
+    off += st[i].n_entries;
+  }
+  const u64 b_rec = n * sizeof(LaunchRec), b_t = terms.size() * sizeof(u64);
+  const u64 bytes = b_rec + b_t + bodies.size() * sizeof(Body) + 64;
+  u8* d = nullptr;
+  HIP_OK(hipMalloc(&d, bytes));
+  HIP_OK(hipMemcpyAsync(d, rec.data(), b_rec, hipMemcpyHostToDevice, e->stream));
+  if (b_t) {
+    HIP_OK(hipMemcpyAsync(d + b_rec, terms.data(), b_t, hipMemcpyHostToDevice, e->stream));
+    HIP_OK(hipMemcpyAsync(d + b_rec + b_t, bodies.data(), bodies.size() * sizeof(Body),
+                          hipMemcpyHostToDevice, e->stream));
+  }
+  const u32 ppar = (e->round & 1u) ^ 1u;
+  rc = dispatch_n(e->C.n, [&](auto NN) {
+    constexpr int N = decltype(NN)::value;
+    hipLaunchKernelGGL(k_relaunch<N>, dim3(grid_for(n)), dim3(kBlock), 0, e->stream, e->P, e->C,
+                       (const LaunchRec*)d, (u64)n, (const u64*)(d + b_rec),
+                       (const Body*)(d + b_rec + b_t), ppar, e->tclk);
+    HIP_OK(hipGetLastError());
+    return RBE_OK;
+  });
+  // the next round scans every group (group sleep: the relaunched groups are awake)
+  e->scan_at = e->round;
+  HIP_OK(hipMemcpyAsync((void*)e->L.scan_round, &e->scan_at, sizeof(u32), hipMemcpyHostToDevice,
+                        e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  HIP_IGNORE(hipFree(d));
+  return rc;
 }
 
 int rbe_set_apply_ready(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint8_t* ready) {

@@ -70,6 +70,43 @@ RBE_HD void apply_pair(const Planes& P, u64 rep, u64 val) {
   }
 }
 
+// Check an rbe_launch batch whole (rbe.h) and turn its entries into ring rows
+// (terms, bodies) in batch order; 0 or RBE_E_INVALID.
+inline int launch_rows(const Params& C, u64 n, const u64* replica, const rbe_launch_state* st,
+                       const rbe_entry* ents, std::vector<u64>& terms, std::vector<Body>& bodies) {
+  if (n && (!replica || !st)) return RBE_E_INVALID;
+  u64 total = 0;
+  std::vector<u8> seen;
+  for (u64 i = 0; i < n; i++) {
+    const rbe_launch_state& x = st[i];
+    if (replica[i] >= C.n_rep || x.n_entries > C.ring || x.n_entries > x.last_index ||
+        x.commit > x.last_index || x.vote > C.n || (x.last_index && !x.n_entries))
+      return RBE_E_INVALID;
+    total += x.n_entries;
+  }
+  if (total && !ents) return RBE_E_INVALID;
+  for (u64 j = 0, i = 0; i < n; i++) {
+    const rbe_launch_state& x = st[i];
+    for (u32 q = 0; q < x.n_entries; q++, j++) {
+      const rbe_entry& e = ents[j];
+      if (e.index != x.last_index - x.n_entries + 1 + q || e.cmd_len > 16 || e.term > x.term)
+        return RBE_E_INVALID;
+    }
+  }
+  terms.resize(total);
+  bodies.resize(total);
+  for (u64 j = 0; j < total; j++) {
+    const rbe_entry& e = ents[j];
+    terms[j] = e.term;
+    Body& b = bodies[j];
+    b.type = e.type;
+    b.len = e.cmd_len;
+    memcpy(&b.lo, e.cmd, 8);
+    memcpy(&b.hi, e.cmd + 8, 8);
+  }
+  return RBE_OK;
+}
+
 struct HostInputs {
   u64 n_rep = 0;
   u32 n = 0;

@@ -1900,6 +1900,72 @@ RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   P.upd[r] = u;
 }
 
+// Restart of replica r from persisted state (rbe_launch): Peer.Launch over an
+// existing log (peer.go:64-86 with initial = newNode = false) = newRaft
+// (raft.go:234-289: remotes next 1, loadState term/vote/commit) then
+// becomeFollower(term, NoLeader) (one randomized timeout drawn, count 0);
+// entryLog over the stored log: processed = firstIndex - 1 = 0, savedTo =
+// lastIndex (logentry.go:86-96, inmemory.go:46-56).  `t`/`b` hold the terms and
+// bodies of entries [last - n + 1, last].  The node restarts with it: fresh
+// quiesce state, and the messages in flight to and from the replica of the
+// round about to run (parity `ppar` lists) are dropped.
+template <int N>
+RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, u64 vote,
+                             u64 commit, u64 last, u32 n, const u64* t, const Body* b, u32 ppar,
+                             u32 tclk) {
+  const u32 k = (u32)(r % N);
+  const u64 g = r / N;
+  const u64 cid = C.cid_base + g * C.cid_stride;
+  const u64 self = k + 1;
+  const bool faulted = P.upd[r].fault != 0;
+  Hot h;
+  h.role = R_Follower;
+  h.flags = (u8)((commit > 0 ? HF_APPLY_PENDING : 0u) | (faulted ? HF_FAULTED : 0u));
+  h.votes_resp = h.votes_granted = 0;
+  h.election_tick = 0;
+  h.heartbeat_tick = 0;
+  h.rand_et = (u16)(C.election_rtt + below(rto_rand(C.seed, cid, self, 0), C.election_rtt));
+  // a fresh quiesce manager on the tick clock (oracle/harness.cpp
+  // harness_restart): quiesce.go compares only differences of its counters
+  const u32 q0 = C.quiesce ? tclk : 0u;
+  h.q_tick = h.q_no_activity_since = h.q_exit_quiesce_tick = q0;
+  h.q_quiesced_since = 0;
+  h.rng_count = 1;
+  P.hot[r] = h;
+  P.idle[r] = idle_byte(C, h.role, h.flags, 0);
+  Core c;
+  c.term = term;
+  c.committed = commit;
+  c.last_index = last;
+  c.processed = 0;
+  c.saved_to = last;
+  c.vote = (u8)vote;
+  c.leader = 0;
+  c.ltt = 0;
+  c.rq_head = c.rq_count = 0;
+  c.pad[0] = c.pad[1] = c.pad[2] = 0;
+  c.t_last = n ? t[n - 1] : 0;
+  c.lead_start = 0;
+  P.core[r] = c;
+  for (u32 s = 0; s < N; s++) {  // becomeFollower → reset → resetRemotes (raft.go:1023-1031)
+    RemoteMN x;
+    x.match = s == k ? last : 0;
+    x.next = last + 1;
+    P.rem[r * N + s] = x;
+    P.rem_st[r * N + s] = 0;
+  }
+  for (u32 i = 0; i < n; i++) {
+    const u64 idx = last - n + 1 + i;
+    const u64 slot = (idx & (u64)(C.ring - 1)) * C.n_rep + r;
+    P.term_ring[slot] = t[i];
+    P.pay_ring[slot] = b[i];
+  }
+  // messages in flight: none from this replica, none to it
+  P.cnt[ppar][r].stamp = 0;
+  for (u32 s = 0; s < N; s++)
+    if (s != k) P.cnt[ppar][g * N + s].w[k] = 0;
+}
+
 // ------------------------------------------------------------------ triage
 // First pass of every round over every replica.  A round with no inbound
 // message (Quiesce notices aside), no client input and a tick that neither

@@ -111,6 +111,11 @@ class RbeReadyToRead(C.Structure):
     _fields_ = [("index", C.c_uint64), ("ctx_low", C.c_uint64), ("ctx_high", C.c_uint64)]
 
 
+class RbeLaunchState(C.Structure):
+    _fields_ = [("term", C.c_uint64), ("vote", C.c_uint64), ("commit", C.c_uint64),
+                ("last_index", C.c_uint64), ("n_entries", C.c_uint32), ("reserved", C.c_uint32)]
+
+
 class RbeOutputs(C.Structure):
     _fields_ = [("first", C.c_uint64), ("count", C.c_uint64), ("n_messages", C.c_uint64),
                 ("n_ready_to_reads", C.c_uint64), ("msg_off", C.POINTER(C.c_uint64)),
@@ -132,7 +137,7 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_footprint", "rbe_profile_rounds", "rbe_get_kernel_counters", "rbe_kernel_name",
            "rbe_xchg_record_bytes", "rbe_xchg_pack", "rbe_xchg_unpack", "rbe_get_outbox",
            "rbe_push_messages", "rbe_snapshot_bytes", "rbe_export_groups", "rbe_import_groups",
-           "rbe_get_entry_cmds", "rbe_set_apply_ready", "rbe_collect_outputs"]
+           "rbe_get_entry_cmds", "rbe_set_apply_ready", "rbe_collect_outputs", "rbe_launch"]
 KERNEL_SLOTS = 4
 
 _lib = None
@@ -187,6 +192,7 @@ def load_library(path: Optional[str] = None):
         "rbe_get_entry_cmds": (i32, [vp, u64, u64, u64, vp, u64, P(u64)]),
         "rbe_get_views": (i32, [vp, u64, u64, P(RbeReplicaView)]),
         "rbe_collect_outputs": (i32, [vp, u64, u64, P(RbeOutputs)]),
+        "rbe_launch": (i32, [vp, u64, P(u64), P(RbeLaunchState), P(RbeEntry)]),
         "rbe_get_counters": (i32, [vp, P(u64)]),
         "rbe_reset_counters": (i32, [vp]),
         "rbe_fault_summary": (i32, [vp, P(u64), P(u32)]),
@@ -337,6 +343,24 @@ class NodeInputs:
     def notify_applied(self, replicas, applied):
         _check_input(self._input("notify_applied", len(replicas), _u64s(replicas),
                                                  _u64s(applied)), "rbe_notify_applied")
+
+    def launch(self, replicas, states, entries):
+        """rbe_launch: restart replicas[i] from states[i] = (term, vote, commit,
+        last_index) and entries[i] = [(index, term, type, cmd), ...], the tail
+        of its LogDB (Peer.Launch over an existing log, peer.go:64-86)."""
+        n = len(replicas)
+        st = (RbeLaunchState * max(1, n))()
+        flat = []
+        for i, ((term, vote, commit, last), ents) in enumerate(zip(states, entries)):
+            st[i] = RbeLaunchState(term=term, vote=vote, commit=commit, last_index=last,
+                                   n_entries=len(ents))
+            flat.extend(ents)
+        ea = (RbeEntry * max(1, len(flat)))()
+        for j, (idx, term, typ, cmd) in enumerate(flat):
+            ea[j].index, ea[j].term, ea[j].type, ea[j].cmd_len = idx, term, typ, len(cmd)
+            for b, x in enumerate(cmd[:16]):
+                ea[j].cmd[b] = x
+        _check_input(self._input("launch", n, _u64s(replicas), st, ea), "rbe_launch")
 
     def set_apply_ready(self, replicas, ready):
         """node.canHaveMoreEntriesToApply per replica (sticky; ready by default)."""

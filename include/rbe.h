@@ -200,10 +200,31 @@ typedef struct rbe_ready_to_read {  /* raftpb ReadyToRead, raftpb/raft.go:52-56 
 
 typedef struct rbe_engine rbe_engine;
 
+/* Persisted state of one replica for rbe_launch: pb.State (term, vote, commit)
+ * and the tail of its LogDB, entries [last_index - n_entries + 1, last_index]
+ * (the engine's in-memory window; Cmd at most 16 bytes). */
+typedef struct rbe_launch_state {
+  uint64_t term, vote, commit, last_index;
+  uint32_t n_entries, reserved;
+} rbe_launch_state;
+
 /* Lifecycle.  Replaces the per-group raft.Launch / newRaft (peer.go:64-86,
  * raft.go:234-289): creates every group's replicas and bootstraps them with
  * peer.go:378-408 semantics (initial = true, newNode = true). */
 int rbe_create(const rbe_config* cfg, rbe_engine** out);
+/* Restart replicas from persisted state between two rounds: Peer.Launch with
+ * initial = false, newNode = false (peer.go:64-86) over an existing LogDB, i.e.
+ * newRaft + loadState + becomeFollower(term, NoLeader) (raft.go:234-289,
+ * 429-437): follower without a leader, the persisted term/vote/commit, the log
+ * up to last_index, nothing applied yet (processed = firstIndex - 1 = 0,
+ * logentry.go:86-96), remotes next = last + 1.  The node around it restarts
+ * too (fresh quiesce state and tick count), and the messages in flight to and
+ * from a relaunched replica are lost.  replica[i] takes st[i] and the next
+ * st[i].n_entries entries of `ents` (n_entries <= cfg.ring; an entry the
+ * replica later needs below that window faults with RBE_FAULT_WINDOW).
+ * Checked whole before anything changes (RBE_E_INVALID). */
+int rbe_launch(rbe_engine* e, uint64_t n, const uint64_t* replica, const rbe_launch_state* st,
+               const rbe_entry* ents);
 int rbe_destroy(rbe_engine* e);
 int rbe_abi_version(void);
 /* sizeof the ABI structs, in this order: rbe_config, rbe_replica_view,

@@ -152,6 +152,25 @@ static std::string payload_cmd(u64 seed, u64 cid, u64 round) {
   return s;
 }
 
+static Config node_config(const HarnessConfig& cfg, u64 cid, u32 k) {
+  Config c;
+  c.nodeID = k + 1;
+  c.clusterID = cid;
+  c.electionRTT = cfg.election_rtt;
+  c.heartbeatRTT = cfg.heartbeat_rtt;
+  c.checkQuorum = cfg.check_quorum;
+  c.quiesce = cfg.quiesce;
+  c.rngSeed = cfg.seed;
+  c.maxEntrySize = cfg.max_entry_size;
+  return c;
+}
+
+static std::vector<std::pair<u64, std::string>> node_addrs(u32 n) {
+  std::vector<std::pair<u64, std::string>> addrs;
+  for (u32 k = 0; k < n; k++) addrs.push_back({k + 1, "node-" + std::to_string(k + 1)});
+  return addrs;
+}
+
 Harness* harness_create(const HarnessConfig& cfg) {
   if (cfg.n_replicas < 1 || cfg.n_replicas > 8) panicf("n_replicas must be 1..8");
   Harness* h = new Harness();
@@ -164,15 +183,7 @@ Harness* harness_create(const HarnessConfig& cfg) {
     gr->cid = cfg.cid_base + g * cfg.cid_stride;
     for (u32 k = 0; k < cfg.n_replicas; k++) {
       Node* n = new Node();
-      Config c;
-      c.nodeID = k + 1;
-      c.clusterID = gr->cid;
-      c.electionRTT = cfg.election_rtt;
-      c.heartbeatRTT = cfg.heartbeat_rtt;
-      c.checkQuorum = cfg.check_quorum;
-      c.quiesce = cfg.quiesce;
-      c.rngSeed = cfg.seed;
-      c.maxEntrySize = cfg.max_entry_size;
+      const Config c = node_config(cfg, gr->cid, k);
       n->peer = Peer::Launch(c, &n->db, addrs, true, true);  // node.go:280-292
       n->q.enabled = cfg.quiesce;
       n->q.electionTick = cfg.election_rtt * 2;  // node.go:165
@@ -483,6 +494,62 @@ int harness_push(Harness* h, int kind, u64 replica, u64 a, u64 b, const Entry* e
 }
 
 u32 harness_round(const Harness* h) { return h->round; }
+
+void harness_persisted(const Harness* h, u64 replica, u64 out4[4]) {
+  const u32 N = h->cfg.n_replicas;
+  TestLogDB& db = h->groups[replica / N]->nodes[replica % N]->db;
+  const PState st = db.state;
+  out4[0] = st.term;
+  out4[1] = st.vote;
+  out4[2] = st.commit;
+  out4[3] = db.lastIndex();
+}
+
+int harness_persisted_entries(const Harness* h, u64 replica, u64 lo, u64 hi, Entry* out) {
+  const u32 N = h->cfg.n_replicas;
+  TestLogDB& db = h->groups[replica / N]->nodes[replica % N]->db;
+  std::vector<Entry> v;
+  if (db.Entries(lo, hi + 1, ~0ull, &v) != ErrOK || v.size() != hi - lo + 1) return -1;
+  for (size_t i = 0; i < v.size(); i++) out[i] = v[i];
+  return 0;
+}
+
+// A node restart (rbe_launch): the raft comes back through Peer.Launch over its
+// LogDB (initial = newNode = false, peer.go:64-86), with the group's members as
+// the persisted membership (the static groups of this harness; dragonboat
+// reads them from the snapshot/LogDB, logdb.NodeState), and the node around it
+// starts afresh: quiesce state, tick count, apply bookkeeping, apply-queue
+// state.  Messages in flight to and from the node are lost.  Host input
+// already staged for it stays staged.
+void harness_restart(Harness* h, u64 replica) {
+  const HarnessConfig& cfg = h->cfg;
+  const u32 N = cfg.n_replicas;
+  Group* gr = h->groups[replica / N];
+  const u32 k = (u32)(replica % N);
+  Node* nd = gr->nodes[k];
+  for (u32 j = 0; j < N; j++)
+    nd->db.snapshot.membership.addresses[j + 1] = "node-" + std::to_string(j + 1);
+  delete nd->peer;
+  nd->peer = Peer::Launch(node_config(cfg, gr->cid, k), &nd->db, node_addrs(N), false, false);
+  // a fresh quiesceManager kept on the harness's tick clock: its counters are
+  // translated by the ticks before the restart (tick = noActivitySince =
+  // exitQuiesceTick = t, not quiesced), which quiesce.go cannot tell apart from
+  // all-zero counters (it compares only differences, and nothing can enter
+  // quiesce before the first tick: justExitedQuiesce holds then)
+  const u64 t = nd->q.tick;
+  nd->q = QuiesceManager();
+  nd->q.enabled = cfg.quiesce;
+  nd->q.electionTick = cfg.election_rtt * 2;  // node.go:165
+  nd->q.tick = nd->q.noActivitySince = nd->q.exitQuiesceTick = t;
+  nd->tickCount = 0;
+  nd->confirmedIndex = 0;
+  nd->smAppliedIndex = cfg.ext_apply ? nd->x_applied : 0;
+  nd->events = 0;
+  nd->more_to_apply = true;
+  for (u32 s = 0; s < N; s++) nd->in[s].clear();
+  for (u32 j = 0; j < N; j++)
+    if (j != k) gr->nodes[j]->in[k].clear();
+}
 
 void harness_views(const Harness* h, ReplicaView* out) {
   const u32 n = h->cfg.n_replicas;

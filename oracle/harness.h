@@ -151,6 +151,11 @@ u32 harness_round(const Harness* h);
 void harness_views(const Harness* h, ReplicaView* out);  // n_groups*n_replicas views
 void harness_counters(const Harness* h, u64* out);       // HC_NUM counters
 u64 harness_log_term(const Harness* h, u64 g, u32 k, u64 index);  // term of entry (0 if absent)
+// restart of one replica from its LogDB (Peer.Launch over an existing log; the
+// engine's rbe_launch): persisted state, persisted entries, the restart itself
+void harness_persisted(const Harness* h, u64 replica, u64 out4[4]);  // term, vote, commit, last
+int harness_persisted_entries(const Harness* h, u64 replica, u64 lo, u64 hi, Entry* out);
+void harness_restart(Harness* h, u64 replica);
 
 // shared helpers (restated independently in the engine)
 u64 wl_payload_lo(u64 seed, u64 cid, u64 round);

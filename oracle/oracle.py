@@ -182,6 +182,9 @@ def lib():
             "orc_harness_views": (None, [vp, vp]),
             "orc_harness_counters": (None, [vp, P(u64)]),
             "orc_harness_log_term": (u64, [vp, u64, u32, u64]),
+            "orc_harness_persisted": (None, [vp, u64, P(u64)]),
+            "orc_harness_persisted_entries": (i32, [vp, u64, u64, u64, P(OrcEntry)]),
+            "orc_harness_restart": (i32, [vp, u64]),
             "orc_view_size": (i32, []),
             "orc_splitmix64": (u64, [u64]),
         }
@@ -943,3 +946,20 @@ class Harness:
 
     def log_term(self, g, k, index):
         return lib().orc_harness_log_term(self.h, g, k, index)
+
+    def persisted(self, replica):
+        """(term, vote, commit, last_index) of a replica's LogDB."""
+        o = (C.c_uint64 * 4)()
+        lib().orc_harness_persisted(self.h, replica, o)
+        return tuple(o)
+
+    def persisted_entries(self, replica, lo, hi):
+        arr = (OrcEntry * max(1, hi - lo + 1))()
+        if lib().orc_harness_persisted_entries(self.h, replica, lo, hi, arr) != 0:
+            raise _err()
+        return [Entry.from_c(arr[i]) for i in range(hi - lo + 1)]
+
+    def restart(self, replica):
+        """Restart a replica from its LogDB (the engine's rbe_launch)."""
+        if lib().orc_harness_restart(self.h, replica) != 0:
+            raise _err()

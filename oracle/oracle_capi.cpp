@@ -854,6 +854,24 @@ void orc_harness_counters(void* h, uint64_t* out) { harness_counters((Harness*)h
 uint64_t orc_harness_log_term(void* h, uint64_t g, uint32_t k, uint64_t idx) {
   return harness_log_term((Harness*)h, g, k, idx);
 }
+void orc_harness_persisted(void* h, uint64_t replica, uint64_t* out4) {
+  harness_persisted((Harness*)h, replica, out4);
+}
+int orc_harness_persisted_entries(void* h, uint64_t replica, uint64_t lo, uint64_t hi,
+                                  orc_entry* out) {
+  GUARD_BEGIN
+  std::vector<Entry> v(hi - lo + 1);
+  if (harness_persisted_entries((Harness*)h, replica, lo, hi, v.data())) return -1;
+  for (size_t i = 0; i < v.size(); i++) from_entry(v[i], &out[i]);
+  return 0;
+  GUARD_END(-1)
+}
+int orc_harness_restart(void* h, uint64_t replica) {
+  GUARD_BEGIN
+  harness_restart((Harness*)h, replica);
+  return 0;
+  GUARD_END(-1)
+}
 int orc_view_size() { return (int)sizeof(ReplicaView); }
 uint64_t orc_splitmix64(uint64_t x) { return splitmix64(x); }
 

@@ -87,7 +87,7 @@ def apply_oracle(h, ops):
 
 
 def run_driven(eng, ref, rounds, seed=1, tick_every=1, inputs=True, ext_apply=False,
-               density=0.3, skip=(), cmd=None, on_ops=None, ready=0.0):
+               density=0.3, skip=(), cmd=None, on_ops=None, ready=0.0, before_round=None):
     """Step both `rounds` rounds with the same input; every `tick_every`-th
     round ticks, the others are RBE_STEP_NO_TICK rounds.  Returns the first
     divergence (round, replica, field, engine, oracle) or None."""
@@ -97,6 +97,9 @@ def run_driven(eng, ref, rounds, seed=1, tick_every=1, inputs=True, ext_apply=Fa
     views = ref.views()
     applied = [0] * n_rep
     for rnd in range(rounds):
+        if before_round:
+            before_round(rnd)
+            views = ref.views()
         if inputs:
             ops = plan_round(rng, n_rep, n, rnd, views, ext_apply, density, applied, cmd, ready)
             if on_ops:

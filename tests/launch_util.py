@@ -1,0 +1,18 @@
+"""Restart replicas from the oracle's persisted state on an engine (the HIP
+engine or the host build) and in the oracle harness, the way a dragonboat node
+restarts: Peer.Launch over its LogDB (peer.go:64-86, initial = newNode =
+false).  The engine is handed exactly what the node would read back: pb.State
+and the tail of the log (its in-memory window)."""
+
+
+def restart(eng, ref, replicas, ring):
+    states, ents = [], []
+    for r in replicas:
+        term, vote, commit, last = ref.persisted(r)
+        lo = max(1, last - ring + 1)
+        es = ref.persisted_entries(r, lo, last) if last else []
+        states.append((term, vote, commit, last))
+        ents.append([(e.index, e.term, e.type, e.cmd) for e in es])
+    eng.launch(replicas, states, ents)
+    for r in replicas:
+        ref.restart(r)

@@ -62,7 +62,8 @@ def lib():
                 "report_unreachable": [C.c_uint64, u64p, u64p],
                 "report_snapshot_status": [C.c_uint64, u64p, u64p, P(C.c_uint8)],
                 "notify_applied": [C.c_uint64, u64p, u64p],
-                "set_apply_ready": [C.c_uint64, u64p, P(C.c_uint8)]}.items():
+                "set_apply_ready": [C.c_uint64, u64p, P(C.c_uint8)],
+                "launch": [C.c_uint64, u64p, C.c_void_p, C.c_void_p]}.items():
             fn = getattr(L, "soa_" + name)
             fn.restype = C.c_int
             fn.argtypes = [C.c_void_p] + args

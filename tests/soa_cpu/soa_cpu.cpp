@@ -5,6 +5,7 @@
 // harness round by round (tests/test_soa_cpu_parity.py).  This library is
 // never loaded by the dragonboat_amd package or by any -m gpu test: the GPU
 // parity tests call libdragonboat_amd.so through the C ABI.
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -308,6 +309,39 @@ int soa_push_proposals(void* h, uint64_t n, const uint64_t* replica, const uint3
   if (!e->C.ext_inputs) return RBE_E_STATE;
   return e->hin.push_proposals(n, replica, n_ents, type, cmd_len, cmd);
 }
+// rbe_launch on the host build (same checks and per-replica restart)
+int soa_launch(void* h, uint64_t n, const uint64_t* replica, const rbe_launch_state* st,
+               const rbe_entry* ents) {
+  SoaEngine* e = (SoaEngine*)h;
+  std::vector<u64> terms;
+  std::vector<Body> bodies;
+  int rc = launch_rows(e->C, n, replica, st, ents, terms, bodies);
+  if (rc) return rc;
+  std::vector<u64> v(replica, replica + n);
+  std::sort(v.begin(), v.end());
+  if (std::adjacent_find(v.begin(), v.end()) != v.end()) return RBE_E_INVALID;
+  const u32 ppar = (e->round & 1u) ^ 1u;
+  u64 off = 0;
+  for (u64 i = 0; i < n; i++) {
+    const rbe_launch_state& x = st[i];
+    if (e->C.n == 1)
+      relaunch_replica<1>(e->P, e->C, replica[i], x.term, x.vote, x.commit, x.last_index,
+                          x.n_entries, terms.data() + off, bodies.data() + off, ppar,
+                          e->tclk);
+    else if (e->C.n == 3)
+      relaunch_replica<3>(e->P, e->C, replica[i], x.term, x.vote, x.commit, x.last_index,
+                          x.n_entries, terms.data() + off, bodies.data() + off, ppar,
+                          e->tclk);
+    else
+      relaunch_replica<5>(e->P, e->C, replica[i], x.term, x.vote, x.commit, x.last_index,
+                          x.n_entries, terms.data() + off, bodies.data() + off, ppar,
+                          e->tclk);
+    e->P.gwake[replica[i] / e->C.n] = GW_AWAKE;
+    off += x.n_entries;
+  }
+  return RBE_OK;
+}
+
 int soa_set_apply_ready(void* h, uint64_t n, const uint64_t* replica, const uint8_t* ready) {
   SoaEngine* e = (SoaEngine*)h;
   if (!e->C.ext_inputs) return RBE_E_STATE;
