@@ -75,6 +75,9 @@ RBE_HD void rbe_wait_all_loads() {
 #ifndef RBE_LEAD_MAXM3
 #define RBE_LEAD_MAXM3 4
 #endif
+#ifndef RBE_LDS_INBOX
+#define RBE_LDS_INBOX 0
+#endif
 template <int N>
 struct FastCaps {
   static constexpr u32 MAXM = N <= 3 ? RBE_LEAD_MAXM3 : 5;  // leader: per follower
@@ -619,6 +622,24 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   bool rq_dirty = false;
   // eligibility of the inbox, then only the fields the handlers read stay live
   LeadIn inc[N - 1][Cap::MAXM];
+  // With RBE_LDS_INBOX (N = 3 on the device) the kept fields move to LDS, one
+  // column per lane (field-major, so a wave's 64 lanes hit consecutive banks),
+  // and the rolled inbox loop reads its message from there by index: ~40
+  // registers fewer through the compute phase, so the compiler need not spill,
+  // and an LDS read waits on lgkmcnt, never behind the lane's stores (vmcnt).
+#if defined(__HIP_DEVICE_COMPILE__) && RBE_LDS_INBOX
+  constexpr bool kLdsIn = N == 3;
+  constexpr u32 kLdsSlots = kLdsIn ? (N - 1) * Cap::MAXM : 1;
+  constexpr u32 kLdsLanes = kLdsIn ? 256 : 1;
+  __shared__ u32 s_in_w[kLdsSlots][kLdsLanes];
+  __shared__ u64 s_in_a[kLdsSlots][kLdsLanes], s_in_b[kLdsSlots][kLdsLanes];
+  const u32 lds_lane = kLdsIn ? threadIdx.x : 0u;
+#else
+  constexpr bool kLdsIn = false;
+  u32 (*s_in_w)[1] = nullptr;
+  u64 (*s_in_a)[1] = nullptr, (*s_in_b)[1] = nullptr;
+  const u32 lds_lane = 0;
+#endif
 #pragma unroll
   for (u32 j = 0; j + 1 < N; j++) {
 #pragma unroll
@@ -631,6 +652,17 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
       if (t != M_ReplicateResp && t != M_HeartbeatResp) return false;
       if (in[j][i].term != c.term) return false;
       if (t == M_ReplicateResp && (in[j][i].w >> 24)) return false;  // rejection: decreaseTo
+    }
+  }
+  if constexpr (kLdsIn) {
+#pragma unroll
+    for (u32 j = 0; j + 1 < N; j++) {
+#pragma unroll
+      for (u32 i = 0; i < Cap::MAXM; i++) {
+        s_in_w[j * Cap::MAXM + i][lds_lane] = inc[j][i].w;
+        s_in_a[j * Cap::MAXM + i][lds_lane] = inc[j][i].a;
+        s_in_b[j * Cap::MAXM + i][lds_lane] = inc[j][i].b;
+      }
     }
   }
 #pragma unroll
@@ -940,10 +972,18 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
     const u32 st0 = st[s];
 #pragma unroll 1
     for (u32 i = 0; i < nb; i++) {
-      LeadIn m = use_lo ? inc[jlo][0] : inc[jhi][0];
+      LeadIn m;
+      if constexpr (kLdsIn) {
+        const u32 sl = (use_lo ? jlo : jhi) * Cap::MAXM + i;
+        m.w = s_in_w[sl][lds_lane];
+        m.a = s_in_a[sl][lds_lane];
+        m.b = s_in_b[sl][lds_lane];
+      } else {
+        m = use_lo ? inc[jlo][0] : inc[jhi][0];
 #pragma unroll
-      for (u32 j = 1; j < Cap::MAXM; j++)
-        if (i == j) m = use_lo ? inc[jlo][j] : inc[jhi][j];
+        for (u32 j = 1; j < Cap::MAXM; j++)
+          if (i == j) m = use_lo ? inc[jlo][j] : inc[jhi][j];
+      }
       ctr.v[C_MSG_IN]++;
       const u32 mtype = m.w & 0xFFu;
       if (mtype == M_HeartbeatResp && m.a > 0) q.record_activity(C, M_ReadIndex);
