@@ -76,7 +76,7 @@ RBE_HD void rbe_wait_all_loads() {
 #define RBE_LEAD_MAXM3 4
 #endif
 #ifndef RBE_LDS_INBOX
-#define RBE_LDS_INBOX 0
+#define RBE_LDS_INBOX 1
 #endif
 template <int N>
 struct FastCaps {
