@@ -196,7 +196,21 @@ def run_replica_mode(args, ws, rank, local, dist, dev, gloo_staged):
     eng = Engine(cfg)
     xch = None
     if ws > 1:
-        xch = ReplicaExchange(eng, buf_device=dev, comm_device="cpu" if gloo_staged else dev)
+        # --xchg-fixed: equal chunks with count headers, no host-side count read
+        # (rbe_xchg_pack_fixed; with RCCL the collective runs on the engine's stream)
+        caps = None
+        if args.xchg_fixed:
+            from dragonboat_amd.replica import initial_caps
+            c0 = initial_caps(kw["n_groups"] * kw["n_replicas"], kw["n_replicas"], ws)
+            caps = [c0[0], 3 * c0[1], 2 * c0[2]]
+        xch = ReplicaExchange(eng, buf_device=dev, comm_device="cpu" if gloo_staged else dev,
+                              caps=caps, fixed=args.xchg_fixed)
+
+    def one_exchange():
+        if xch.fixed:
+            xch.exchange_fixed()
+        else:
+            xch.exchange()
 
     def rounds(k, timed_xchg=None):
         for _ in range(k):
@@ -205,10 +219,13 @@ def run_replica_mode(args, ws, rank, local, dist, dev, gloo_staged):
                 if timed_xchg is not None:
                     eng.sync()
                     t = time.perf_counter()
-                    xch.exchange()
+                    one_exchange()
+                    eng.sync()
                     timed_xchg[0] += time.perf_counter() - t
                 else:
-                    xch.exchange()
+                    one_exchange()
+        if xch is not None:
+            xch.check()
 
     def barrier():
         if ws > 1:
@@ -303,6 +320,8 @@ def main():
                     help="groups in the 1-thread CPU sample (0 = per-workload default)")
     ap.add_argument("--xchg-gloo", action="store_true",
                     help="c5 rehearsal: all ranks on cuda:0, exchange over gloo via host memory")
+    ap.add_argument("--xchg-fixed", action="store_true",
+                    help="c5: fixed-capacity exchange (count headers, no host-side count read)")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()

@@ -226,7 +226,8 @@ struct XchgCaps {
 // global atomic per (peer, stream) after an LDS reduction of its lanes' counts.
 template <int N>
 __global__ __launch_bounds__(kBlock) void k_xchg_pack(Planes P, Params C, u32 par, u32 round,
-                                                      u8* buf, XchgCaps caps, u32* gcount) {
+                                                      u8* buf, XchgCaps caps, u32* gcount,
+                                                      u64 hdr) {
   __shared__ u32 s_cnt[kXchgMaxWorld * XS_NUM];
   __shared__ u32 s_base[kXchgMaxWorld * XS_NUM];
   const u32 nc = C.rep_world * XS_NUM;
@@ -237,7 +238,7 @@ __global__ __launch_bounds__(kBlock) void k_xchg_pack(Planes P, Params C, u32 pa
   u32 cnt[kXchgMaxWorld * XS_NUM];
   u32 base[kXchgMaxWorld * XS_NUM];
   for (u32 i = 0; i < nc; i++) cnt[i] = 0;
-  if (mine) xchg_sender<N, false>(P, C, r, par, round, cnt, nullptr, nullptr, caps.cap);
+  if (mine) xchg_sender<N, false>(P, C, r, par, round, cnt, nullptr, nullptr, caps.cap, hdr);
   for (u32 i = 0; i < nc; i++) base[i] = cnt[i] ? atomicAdd(&s_cnt[i], cnt[i]) : 0u;
   __syncthreads();
   for (u32 i = threadIdx.x; i < nc; i += kBlock)
@@ -248,8 +249,36 @@ __global__ __launch_bounds__(kBlock) void k_xchg_pack(Planes P, Params C, u32 pa
       base[i] += s_base[i];
       cnt[i] = 0;
     }
-    xchg_sender<N, true>(P, C, r, par, round, cnt, base, buf, caps.cap);
+    xchg_sender<N, true>(P, C, r, par, round, cnt, base, buf, caps.cap, hdr);
   }
+}
+// fixed layout: each peer's chunk header from the pack counts (one thread per
+// peer); an overflow also marks the engine's sticky flag
+__global__ void k_xchg_hdr(u8* buf, XchgCaps caps, const u32* gcount, u32 world, u32* flag) {
+  const u32 p = threadIdx.x;
+  if (p >= world) return;
+  XHdr h;
+  for (u32 i = 0; i < 12; i++) h.pad[i] = 0;
+  h.overflow = 0;
+  for (u32 t = 0; t < XS_NUM; t++) {
+    const u32 n = gcount[p * XS_NUM + t];
+    h.cnt[t] = n < caps.cap[t] ? n : (u32)caps.cap[t];
+    if (n > caps.cap[t]) h.overflow = 1;
+  }
+  if (h.overflow) atomicOr(flag, 1u);
+  *(XHdr*)(buf + p * xchg_chunk_bytes(caps.cap, kXHdrBytes)) = h;
+}
+// fixed layout, receive side: one lane per record slot of stream t of every
+// source chunk; slots past a chunk's count do nothing
+__global__ __launch_bounds__(kBlock) void k_xchg_put_fixed(Planes P, Params C, u32 par,
+                                                           const u8* recv, XchgCaps caps,
+                                                           u32 world, u32 t, u32* flag) {
+  const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+  const u64 cap = caps.cap[t];
+  if (i >= cap * world) return;
+  u32 ovf = 0;
+  xchg_put_fixed(P, C, par, recv, caps.cap, (u32)(i / cap), t, i % cap, &ovf);
+  if (ovf && i % cap == 0 && t == XS_CNT) atomicOr(flag, 1u);
 }
 __global__ __launch_bounds__(kBlock) void k_xchg_put_cnt(Planes P, Params C, u32 par,
                                                          const XCnt* x, u64 n) {
@@ -704,11 +733,13 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
     e->L.al_on = C.quiesce && !C.trace && C.rep_world == 1 && (e->mode == 1 || e->mode == 3) &&
                  !(gl && strcmp(gl, "0") == 0);
   }
-  if (hipMalloc(&e->xcount, kXchgMaxWorld * XS_NUM * sizeof(u32)) != hipSuccess) {
+  // pack counters, then the sticky overflow flag of the fixed-layout exchange
+  if (hipMalloc(&e->xcount, (kXchgMaxWorld * XS_NUM + 1) * sizeof(u32)) != hipSuccess) {
     rbe_destroy(e);
     return RBE_E_NOMEM;
   }
   e->allocs.push_back(e->xcount);
+  HIP_IGNORE(hipMemsetAsync(e->xcount, 0, (kXchgMaxWorld * XS_NUM + 1) * sizeof(u32), e->stream));
   HIP_IGNORE(hipMemsetAsync(e->L.counts, 0, kListCounts * sizeof(u32), e->stream));
   rc = dispatch_n(C.n, [&](auto NN) {
     constexpr int N = decltype(NN)::value;
@@ -1046,7 +1077,7 @@ int rbe_xchg_pack(rbe_engine* e, void* buf, const uint64_t* cap3, uint32_t* coun
   int rc = dispatch_n(e->C.n, [&](auto NN) {
     constexpr int N = decltype(NN)::value;
     hipLaunchKernelGGL(k_xchg_pack<N>, dim3(grid_for(e->C.n_rep)), dim3(kBlock), 0, e->stream,
-                       e->P, e->C, par, e->round, (u8*)buf, caps, e->xcount);
+                       e->P, e->C, par, e->round, (u8*)buf, caps, e->xcount, (u64)0);
     HIP_OK(hipGetLastError());
     return RBE_OK;
   });
@@ -1055,6 +1086,68 @@ int rbe_xchg_pack(rbe_engine* e, void* buf, const uint64_t* cap3, uint32_t* coun
   HIP_OK(hipStreamSynchronize(e->stream));
   for (u32 i = 0; i < nc; i++)
     if (counts[i] > cap3[i % XS_NUM]) return RBE_E_NOMEM;  // a region overflowed
+  return RBE_OK;
+}
+
+int rbe_xchg_chunk_bytes(const uint64_t* cap3, uint64_t* bytes) {
+  if (!cap3 || !bytes) return RBE_E_INVALID;
+  *bytes = xchg_chunk_bytes(cap3, kXHdrBytes);
+  return RBE_OK;
+}
+
+int rbe_xchg_pack_fixed(rbe_engine* e, void* buf, const uint64_t* cap3) {
+  if (!e || !buf || !cap3 || e->round == 0) return RBE_E_INVALID;
+  if (e->C.rep_world <= 1) return RBE_E_STATE;
+  HIP_OK(hipSetDevice(e->device));
+  XchgCaps caps;
+  for (u32 t = 0; t < XS_NUM; t++) caps.cap[t] = cap3[t];
+  const u32 par = (e->round - 1) & 1u, nc = e->C.rep_world * XS_NUM;
+  HIP_OK(hipMemsetAsync(e->xcount, 0, nc * sizeof(u32), e->stream));
+  int rc = dispatch_n(e->C.n, [&](auto NN) {
+    constexpr int N = decltype(NN)::value;
+    hipLaunchKernelGGL(k_xchg_pack<N>, dim3(grid_for(e->C.n_rep)), dim3(kBlock), 0, e->stream,
+                       e->P, e->C, par, e->round, (u8*)buf, caps, e->xcount, kXHdrBytes);
+    HIP_OK(hipGetLastError());
+    return RBE_OK;
+  });
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_xchg_hdr, dim3(1), dim3(64), 0, e->stream, (u8*)buf, caps,
+                     (const u32*)e->xcount, e->C.rep_world, e->xcount + kXchgMaxWorld * XS_NUM);
+  HIP_OK(hipGetLastError());
+  return RBE_OK;  // no host synchronisation: the counts travel in the chunk headers
+}
+
+int rbe_xchg_unpack_fixed(rbe_engine* e, const void* recv, const uint64_t* cap3) {
+  if (!e || !recv || !cap3 || e->round == 0) return RBE_E_INVALID;
+  if (e->C.rep_world <= 1) return RBE_E_STATE;
+  HIP_OK(hipSetDevice(e->device));
+  XchgCaps caps;
+  for (u32 t = 0; t < XS_NUM; t++) caps.cap[t] = cap3[t];
+  const u32 par = (e->round - 1) & 1u;
+  // count words first (they wake the destination groups), then messages, entries
+  for (u32 t = 0; t < XS_NUM; t++) {
+    const u64 n = caps.cap[t] * e->C.rep_world;
+    if (n)
+      hipLaunchKernelGGL(k_xchg_put_fixed, dim3(grid_for(n)), dim3(kBlock), 0, e->stream, e->P,
+                         e->C, par, (const u8*)recv, caps, e->C.rep_world, t,
+                         e->xcount + kXchgMaxWorld * XS_NUM);
+  }
+  HIP_OK(hipGetLastError());
+  return RBE_OK;
+}
+
+int rbe_xchg_status(rbe_engine* e, uint32_t* overflow) {
+  if (!e || !overflow) return RBE_E_INVALID;
+  HIP_OK(hipSetDevice(e->device));
+  HIP_OK(hipMemcpyAsync(overflow, e->xcount + kXchgMaxWorld * XS_NUM, sizeof(u32),
+                        hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return RBE_OK;
+}
+
+int rbe_stream(rbe_engine* e, void** stream) {
+  if (!e || !stream) return RBE_E_INVALID;
+  *stream = (void*)e->stream;
   return RBE_OK;
 }
 

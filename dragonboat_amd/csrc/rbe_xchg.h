@@ -50,12 +50,27 @@ RBE_HD bool owned(const Params& C, u64 r) {
   return owner_of<N>(C, r / N, (u32)(r % N)) == C.rep_rank;
 }
 
+// Fixed-capacity layout (rbe_xchg_pack_fixed): every peer's chunk starts with
+// this header, so the receiver learns the record counts from the data itself
+// and the exchange needs no host-side count read: one all-to-all of equal
+// chunks per round, capturable in a graph.
+struct alignas(16) XHdr {
+  u32 cnt[XS_NUM];  // records of each stream in this chunk (at most its capacity)
+  u32 overflow;     // the sender had more than fit: the round is lost, the run is invalid
+  u32 pad[12];
+};
+constexpr u64 kXHdrBytes = sizeof(XHdr);
+
 // Byte offset of stream t of peer p in a pack buffer with per-peer, per-stream
-// record capacities cap[t].
-RBE_HD u64 xchg_region(const u64* cap, u32 p, u32 t) {
-  u64 per_peer = 0;
+// record capacities cap[t]; `hdr` header bytes open each peer's chunk (0 for
+// the counted layout of rbe_xchg_pack, kXHdrBytes for the fixed one).
+RBE_HD u64 xchg_chunk_bytes(const u64* cap, u64 hdr) {
+  u64 per_peer = hdr;
   for (u32 i = 0; i < XS_NUM; i++) per_peer += cap[i] * kXRecBytes[i];
-  u64 off = p * per_peer;
+  return per_peer;
+}
+RBE_HD u64 xchg_region(const u64* cap, u32 p, u32 t, u64 hdr = 0) {
+  u64 off = p * xchg_chunk_bytes(cap, hdr) + hdr;
   for (u32 i = 0; i < t; i++) off += cap[i] * kXRecBytes[i];
   return off;
 }
@@ -68,7 +83,7 @@ RBE_HD u64 xchg_region(const u64* cap, u32 p, u32 t) {
 // buffer (overflow past cap is counted, not written).
 template <int N, bool WRITE>
 RBE_HD void xchg_sender(const Planes& P, const Params& C, u64 r, u32 par, u32 round, u32* cnt,
-                        const u32* base, u8* buf, const u64* cap) {
+                        const u32* base, u8* buf, const u64* cap, u64 hdr = 0) {
   const u64 g = r / N;
   const u32 s = (u32)(r % N);
   const CntRow row = P.cnt[par][r];
@@ -85,7 +100,7 @@ RBE_HD void xchg_sender(const Planes& P, const Params& C, u64 r, u32 par, u32 ro
       if (!WRITE) return nullptr;
       const u32 at = base[peer * XS_NUM + t] + i;
       if (at >= cap[t]) return nullptr;
-      return buf + xchg_region(cap, peer, t) + (u64)at * kXRecBytes[t];
+      return buf + xchg_region(cap, peer, t, hdr) + (u64)at * kXRecBytes[t];
     };
     if (!((sent_to >> peer) & 1u)) {
       sent_to |= 1u << peer;
@@ -134,6 +149,20 @@ RBE_HD void xchg_put_msg(const Planes& P, const Params& C, u32 par, const XMsg& 
 }
 RBE_HD void xchg_put_ent(const Planes& P, const Params& C, u32 par, const XEnt& x) {
   P.arena[par][x.key * C.ecap + x.off] = x.e;
+}
+// record i of stream t of source chunk p of a fixed-layout receive buffer, if
+// the chunk holds it (returns false past the chunk's count); *overflow gets
+// the chunk's overflow flag
+RBE_HD bool xchg_put_fixed(const Planes& P, const Params& C, u32 par, const u8* recv,
+                           const u64* cap, u32 p, u32 t, u64 i, u32* overflow) {
+  const XHdr* h = (const XHdr*)(recv + p * xchg_chunk_bytes(cap, kXHdrBytes));
+  *overflow = h->overflow;
+  if (i >= h->cnt[t]) return false;
+  const u8* rec = recv + xchg_region(cap, p, t, kXHdrBytes) + i * kXRecBytes[t];
+  if (t == XS_CNT) xchg_put_cnt(P, C, par, *(const XCnt*)rec);
+  else if (t == XS_MSG) xchg_put_msg(P, C, par, *(const XMsg*)rec);
+  else xchg_put_ent(P, C, par, *(const XEnt*)rec);
+  return true;
 }
 
 // ------------------------------------------------ transport boundary (host)

@@ -137,7 +137,9 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_footprint", "rbe_profile_rounds", "rbe_get_kernel_counters", "rbe_kernel_name",
            "rbe_xchg_record_bytes", "rbe_xchg_pack", "rbe_xchg_unpack", "rbe_get_outbox",
            "rbe_push_messages", "rbe_snapshot_bytes", "rbe_export_groups", "rbe_import_groups",
-           "rbe_get_entry_cmds", "rbe_set_apply_ready", "rbe_collect_outputs", "rbe_launch"]
+           "rbe_get_entry_cmds", "rbe_set_apply_ready", "rbe_collect_outputs", "rbe_launch",
+           "rbe_xchg_chunk_bytes", "rbe_xchg_pack_fixed", "rbe_xchg_unpack_fixed",
+           "rbe_xchg_status", "rbe_stream"]
 KERNEL_SLOTS = 4
 
 _lib = None
@@ -203,6 +205,11 @@ def load_library(path: Optional[str] = None):
         "rbe_xchg_record_bytes": (i32, [P(u64)]),
         "rbe_xchg_pack": (i32, [vp, vp, P(u64), P(u32)]),
         "rbe_xchg_unpack": (i32, [vp, vp, u64, vp, u64, vp, u64]),
+        "rbe_xchg_chunk_bytes": (i32, [P(u64), P(u64)]),
+        "rbe_xchg_pack_fixed": (i32, [vp, vp, P(u64)]),
+        "rbe_xchg_unpack_fixed": (i32, [vp, vp, P(u64)]),
+        "rbe_xchg_status": (i32, [vp, P(u32)]),
+        "rbe_stream": (i32, [vp, P(vp)]),
         "rbe_snapshot_bytes": (i32, [vp, u64, P(u64)]),
         "rbe_export_groups": (i32, [vp, u64, u64, vp, u64]),
         "rbe_import_groups": (i32, [vp, vp, u64, u32]),
@@ -495,6 +502,28 @@ class Engine(NodeInputs):
         _check(self.lib.rbe_xchg_unpack(self.h, C.c_void_p(cnt_ptr), n_cnt, C.c_void_p(msg_ptr),
                                         n_msg, C.c_void_p(ent_ptr), n_ent), "rbe_xchg_unpack")
 
+    # fixed-capacity exchange: no host synchronisation between pack and unpack
+    def xchg_pack_fixed(self, buf_ptr: int, caps):
+        cap = (C.c_uint64 * 3)(*caps)
+        _check(self.lib.rbe_xchg_pack_fixed(self.h, C.c_void_p(buf_ptr), cap),
+               "rbe_xchg_pack_fixed")
+
+    def xchg_unpack_fixed(self, recv_ptr: int, caps):
+        cap = (C.c_uint64 * 3)(*caps)
+        _check(self.lib.rbe_xchg_unpack_fixed(self.h, C.c_void_p(recv_ptr), cap),
+               "rbe_xchg_unpack_fixed")
+
+    def xchg_status(self) -> int:
+        o = C.c_uint32()
+        _check(self.lib.rbe_xchg_status(self.h, C.byref(o)), "rbe_xchg_status")
+        return o.value
+
+    def stream_handle(self) -> int:
+        """The engine's HIP stream (hipStream_t) as an integer."""
+        v = C.c_void_p()
+        _check(self.lib.rbe_stream(self.h, C.byref(v)), "rbe_stream")
+        return v.value or 0
+
     def owned(self, replica: int) -> bool:
         """Replica-per-GPU ownership: replica k of group g lives on rank (g + k) % world."""
         w = max(1, self.cfg.rep_world)
@@ -600,6 +629,14 @@ class Engine(NodeInputs):
         o = C.c_uint32()
         _check(self.lib.rbe_fault_summary(self.h, C.byref(n), C.byref(o)), "rbe_fault_summary")
         return n.value, o.value
+
+
+def xchg_chunk_bytes(caps) -> int:
+    """Bytes of one peer's chunk in the fixed-capacity exchange layout."""
+    o = C.c_uint64()
+    _check(load_library().rbe_xchg_chunk_bytes((C.c_uint64 * 3)(*caps), C.byref(o)),
+           "rbe_xchg_chunk_bytes")
+    return o.value
 
 
 def xchg_record_bytes() -> List[int]:

@@ -28,6 +28,9 @@ from typing import List, Optional, Sequence
 
 from .engine import xchg_record_bytes
 
+# the fixed-capacity layout's chunk header (rbe_xchg.h XHdr)
+XHDR_BYTES = 64
+
 STREAMS = 3  # count words, messages, entries
 
 
@@ -49,7 +52,7 @@ class ReplicaExchange:
     the comm device."""
 
     def __init__(self, engine, group=None, buf_device="cpu", comm_device="cpu",
-                 caps: Optional[Sequence[int]] = None):
+                 caps: Optional[Sequence[int]] = None, fixed: bool = False):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -71,6 +74,10 @@ class ReplicaExchange:
         self.comm_device = torch.device(comm_device)
         self.bytes_sent = 0
         self.records_sent = [0] * STREAMS
+        # fixed: equal chunks with a count header per peer, no host-side count
+        # read (rbe_xchg_pack_fixed); the capacities never grow, an overflow is
+        # reported by check()
+        self.fixed = fixed
         self._alloc()
 
     # --- layout: per peer p, streams t = 0..2, cap[t] records each (rbe_xchg.h xchg_region)
@@ -81,8 +88,41 @@ class ReplicaExchange:
         return p * self._per_peer() + sum(self.caps[i] * self.rec[i] for i in range(t))
 
     def _alloc(self):
-        self.buf = self.torch.empty(self.world * self._per_peer(), dtype=self.torch.uint8,
+        per = self._per_peer() + (XHDR_BYTES if self.fixed else 0)
+        self.buf = self.torch.empty(self.world * per, dtype=self.torch.uint8,
                                     device=self.buf_device)
+        if self.fixed:
+            self.recv = self.torch.empty_like(self.buf, device=self.comm_device)
+            self.recv_buf = self.recv if self.comm_device == self.buf_device else \
+                self.torch.empty_like(self.buf)
+
+    def exchange_fixed(self):
+        """One round's exchange without reading counts on the host: pack into
+        equal chunks (headers carry the counts), one all_to_all_single, unpack.
+        With the buffers on the engine's GPU and RCCL, the collective is
+        enqueued on the engine's own stream, so nothing waits on the host."""
+        torch, dist = self.torch, self.dist
+        self.eng.xchg_pack_fixed(self.buf.data_ptr(), self.caps)
+        if self.buf_device.type == "cuda" and self.comm_device == self.buf_device:
+            s = torch.cuda.ExternalStream(self.eng.stream_handle(), device=self.buf_device)
+            with torch.cuda.stream(s):
+                dist.all_to_all_single(self.recv, self.buf, group=self.group)
+        else:  # gloo: staged through host memory
+            if self.buf_device.type == "cuda":
+                self.eng.sync()
+            send = self.buf if self.buf.device == self.comm_device else self.buf.to(self.comm_device)
+            dist.all_to_all_single(self.recv, send, group=self.group)
+            if self.recv_buf is not self.recv:
+                self.recv_buf.copy_(self.recv)
+                torch.cuda.current_stream(self.buf_device).synchronize()
+        self.bytes_sent += self.buf.numel()
+        self.eng.xchg_unpack_fixed(self.recv_buf.data_ptr(), self.caps)
+
+    def check(self):
+        """Raise if a fixed-layout round overflowed a chunk (rbe_xchg_status)."""
+        if self.fixed and self.eng.xchg_status():
+            raise RuntimeError("replica exchange: a chunk overflowed its capacity; "
+                               "the rounds since are invalid (raise caps)")
 
     def grow(self, counts: Sequence[int]):
         need = [max(counts[p * STREAMS + t] for p in range(self.world)) for t in range(STREAMS)]
@@ -151,4 +191,8 @@ class ReplicaExchange:
         """`rounds` lockstep rounds of the owned replicas, exchanging after each."""
         for _ in range(rounds):
             self.eng.step()
-            self.exchange()
+            if self.fixed:
+                self.exchange_fixed()
+            else:
+                self.exchange()
+        self.check()

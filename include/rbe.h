@@ -371,6 +371,22 @@ int rbe_fault_summary(rbe_engine* e, uint64_t* n_faulty, uint32_t* fault_or);
  * Record sizes come from rbe_xchg_record_bytes.  Replaces, for replicas on
  * other GPUs, the transport hop of node.go:888-905 → nodehost.go:1724. */
 int rbe_xchg_record_bytes(uint64_t* out3);
+/* Fixed-capacity variant without a host synchronisation (one all-to-all of
+ * equal chunks per round, capturable in a graph): every peer's chunk of
+ * rbe_xchg_chunk_bytes(cap3) bytes opens with a header holding its record
+ * counts, so the receiver scatters what each chunk holds.
+ *   rbe_xchg_pack_fixed: packs the last round's records into `buf` (rep_world
+ *     chunks), enqueued on the engine stream, nothing read back;
+ *   rbe_xchg_unpack_fixed: scatters a received buffer of the same layout;
+ *   rbe_xchg_status: the sticky overflow flag (a chunk had more records than
+ *     its capacity: those rounds are not valid; size cap3 up and rerun);
+ *   rbe_stream: the engine's HIP stream (hipStream_t), so a collective can be
+ *     enqueued between pack and unpack without a host wait. */
+int rbe_xchg_chunk_bytes(const uint64_t* cap3, uint64_t* bytes);
+int rbe_xchg_pack_fixed(rbe_engine* e, void* buf, const uint64_t* cap3);
+int rbe_xchg_unpack_fixed(rbe_engine* e, const void* recv, const uint64_t* cap3);
+int rbe_xchg_status(rbe_engine* e, uint32_t* overflow);
+int rbe_stream(rbe_engine* e, void** stream);
 int rbe_xchg_pack(rbe_engine* e, void* buf, const uint64_t* cap3, uint32_t* counts);
 int rbe_xchg_unpack(rbe_engine* e, const void* cnt_recs, uint64_t n_cnt, const void* msg_recs,
                     uint64_t n_msg, const void* ent_recs, uint64_t n_ent);

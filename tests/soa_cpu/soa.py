@@ -52,6 +52,10 @@ def lib():
         L.soa_import_groups.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32]
         u64p, u32p = P(C.c_uint64), P(C.c_uint32)
         L.soa_step_ex.argtypes = [C.c_void_p, C.c_uint32]
+        L.soa_xchg_pack_fixed.argtypes = [C.c_void_p, C.c_void_p, P(C.c_uint64)]
+        L.soa_xchg_unpack_fixed.argtypes = [C.c_void_p, C.c_void_p, P(C.c_uint64)]
+        L.soa_xchg_status.restype = C.c_uint32
+        L.soa_xchg_status.argtypes = [C.c_void_p]
         L.soa_get_entry_cmds.restype = C.c_int
         L.soa_get_entry_cmds.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64,
                                          C.c_void_p, C.c_uint64, u64p]
@@ -120,6 +124,15 @@ class SoaCpu(NodeInputs):
         out = (C.c_uint32 * (3 * world))()
         rc = lib().soa_xchg_pack(self.h, C.c_void_p(buf_ptr), cap, out)
         return rc == 0, list(out)
+
+    def xchg_pack_fixed(self, buf_ptr, caps):
+        lib().soa_xchg_pack_fixed(self.h, C.c_void_p(buf_ptr), (C.c_uint64 * 3)(*caps))
+
+    def xchg_unpack_fixed(self, recv_ptr, caps):
+        lib().soa_xchg_unpack_fixed(self.h, C.c_void_p(recv_ptr), (C.c_uint64 * 3)(*caps))
+
+    def xchg_status(self):
+        return lib().soa_xchg_status(self.h)
 
     def xchg_unpack(self, cnt_ptr, n_cnt, msg_ptr, n_msg, ent_ptr, n_ent):
         lib().soa_xchg_unpack(self.h, C.c_void_p(cnt_ptr), n_cnt, C.c_void_p(msg_ptr), n_msg,

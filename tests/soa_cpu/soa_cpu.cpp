@@ -29,6 +29,7 @@ struct SoaEngine {
   int staged = 0;  // STG_* bits: fast steps on a staged row (StageRow); 4: counts from inbound_aux
   u64 slow_total = 0;
   std::vector<u8> heap;  // payload heap (cfg.heap_bytes), as on the device
+  u32 xflag = 0;         // fixed-layout exchange overflow (rbe_xchg_status)
 };
 
 template <typename T>
@@ -465,6 +466,55 @@ static void soa_xchg_unpack_t(SoaEngine* e, const XCnt* c, uint64_t nc, const XM
   for (u64 i = 0; i < nm; i++) xchg_put_msg(e->P, e->C, par, m[i]);
   for (u64 i = 0; i < ne; i++) xchg_put_ent(e->P, e->C, par, x[i]);
 }
+// fixed layout (rbe_xchg_pack_fixed / rbe_xchg_unpack_fixed) on the host build
+template <int N>
+static void soa_xchg_pack_fixed_t(SoaEngine* e, uint8_t* buf, const uint64_t* cap) {
+  const u32 par = (e->round - 1) & 1u, nc = e->C.rep_world * XS_NUM;
+  std::vector<u32> counts(nc, 0), cnt(nc), base(nc);
+  for (u64 r = 0; r < e->C.n_rep; r++) {
+    if (!owned<N>(e->C, r)) continue;
+    for (u32 i = 0; i < nc; i++) cnt[i] = 0;
+    xchg_sender<N, false>(e->P, e->C, r, par, e->round, cnt.data(), nullptr, nullptr, cap,
+                          kXHdrBytes);
+    for (u32 i = 0; i < nc; i++) {
+      base[i] = counts[i];
+      counts[i] += cnt[i];
+      cnt[i] = 0;
+    }
+    xchg_sender<N, true>(e->P, e->C, r, par, e->round, cnt.data(), base.data(), buf, cap,
+                         kXHdrBytes);
+  }
+  for (u32 p = 0; p < e->C.rep_world; p++) {
+    XHdr hd;
+    memset(&hd, 0, sizeof(hd));
+    for (u32 t = 0; t < XS_NUM; t++) {
+      const u32 n = counts[p * XS_NUM + t];
+      hd.cnt[t] = n < cap[t] ? n : (u32)cap[t];
+      if (n > cap[t]) hd.overflow = 1;
+    }
+    if (hd.overflow) e->xflag = 1;
+    memcpy(buf + p * xchg_chunk_bytes(cap, kXHdrBytes), &hd, sizeof(hd));
+  }
+}
+extern "C" void soa_xchg_pack_fixed(void* h, uint8_t* buf, const uint64_t* cap) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (e->C.n == 3) soa_xchg_pack_fixed_t<3>(e, buf, cap);
+  else if (e->C.n == 5) soa_xchg_pack_fixed_t<5>(e, buf, cap);
+  else soa_xchg_pack_fixed_t<1>(e, buf, cap);
+}
+extern "C" void soa_xchg_unpack_fixed(void* h, const uint8_t* recv, const uint64_t* cap) {
+  SoaEngine* e = (SoaEngine*)h;
+  const u32 par = (e->round - 1) & 1u;
+  for (u32 t = 0; t < XS_NUM; t++)
+    for (u32 p = 0; p < e->C.rep_world; p++)
+      for (u64 i = 0; i < cap[t]; i++) {
+        u32 ovf = 0;
+        if (!xchg_put_fixed(e->P, e->C, par, recv, cap, p, t, i, &ovf)) break;
+        if (ovf) e->xflag = 1;
+      }
+}
+extern "C" uint32_t soa_xchg_status(void* h) { return ((SoaEngine*)h)->xflag; }
+
 extern "C" int soa_xchg_pack(void* h, uint8_t* buf, const uint64_t* cap, uint32_t* counts) {
   SoaEngine* e = (SoaEngine*)h;
   if (e->C.n == 3) return soa_xchg_pack_t<3>(e, buf, cap, counts);

@@ -17,3 +17,9 @@ def test_gpu_replica_per_rank_matches_oracle(gpu_available, name):
 
 def test_gpu_replica_per_rank_untraced(gpu_available):
     run_case("C4_w3", gpu=True, trace=False)
+
+
+def test_gpu_replica_fixed_exchange(gpu_available):
+    """The fixed-capacity exchange on the HIP engine (pack and unpack enqueued
+    without reading counts back; gloo staging in this one-GPU rehearsal)."""
+    run_case("C2_w2", gpu=True, fixed=True)

@@ -38,7 +38,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, name, gpu, trace, q):
+def _worker(rank, world, port, name, gpu, trace, q, fixed=False):
     sys.path.insert(0, HERE)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -46,14 +46,18 @@ def _worker(rank, world, port, name, gpu, trace, q):
         from parity_util import FIELDS
         from dragonboat_amd.replica import ReplicaExchange
         kw, _, rounds, extra = CASES[name]
+        # counted exchange: tiny caps exercise grow(); fixed exchange: capacities
+        # that never grow (initial_caps), counts travel in the chunk headers
+        caps = None if fixed else [8, 8, 8]
         if gpu:  # the HIP engine, records staged through host memory for gloo
             from dragonboat_amd.engine import Engine
             eng = Engine(device=0, trace=trace, rep_world=world, rep_rank=rank, **kw, **extra)
-            xch = ReplicaExchange(eng, buf_device="cuda:0", comm_device="cpu", caps=[8, 8, 8])
+            xch = ReplicaExchange(eng, buf_device="cuda:0", comm_device="cpu", caps=caps,
+                                  fixed=fixed)
         else:
             from soa_cpu.soa import SoaCpu
             eng = SoaCpu(trace=trace, rep_world=world, rep_rank=rank, **kw, **extra)
-            xch = ReplicaExchange(eng, caps=[8, 8, 8])  # tiny caps: exercises grow()
+            xch = ReplicaExchange(eng, caps=caps, fixed=fixed)
         snaps = []
         for done in range(CHECK_EVERY, rounds + 1, CHECK_EVERY):
             xch.run(CHECK_EVERY)
@@ -64,7 +68,8 @@ def _worker(rank, world, port, name, gpu, trace, q):
                    for i in range(len(vs)) if (i // n + i % n) % world == rank}
             snaps.append((done, own))
         nf = eng.fault_summary()[0] if gpu else eng.faults()[0]
-        q.put((rank, snaps, eng.counters(), nf, xch.records_sent))
+        q.put((rank, snaps, eng.counters(), nf,
+               [xch.bytes_sent] * 3 if fixed else xch.records_sent))
     except Exception as ex:  # surface worker failures in the parent
         q.put((rank, repr(ex), None, None, None))
         raise
@@ -73,14 +78,14 @@ def _worker(rank, world, port, name, gpu, trace, q):
         dist.destroy_process_group()
 
 
-def run_case(name, gpu=False, trace=True):
+def run_case(name, gpu=False, trace=True, fixed=False):
     import oracle as O
     from parity_util import FIELDS
     kw, world, rounds, _ = CASES[name]
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, name, gpu, trace, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, gpu, trace, q, fixed))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -126,3 +131,10 @@ def test_replica_per_rank_matches_oracle(name):
 def test_replica_per_rank_untraced():
     """Without trace (the bench paths: lazy quiesced ticks, no digest)."""
     run_case("C4_w3", trace=False)
+
+
+@pytest.mark.parametrize("name", ["C2_w2", "N5_w4"])
+def test_replica_fixed_exchange_matches_oracle(name):
+    """The fixed-capacity exchange (rbe_xchg_pack_fixed: equal chunks whose
+    headers carry the counts, no host-side count read)."""
+    run_case(name, fixed=True)
