@@ -69,6 +69,9 @@ struct Node {
   u32 x_unreach = 0, x_snap = 0, x_snap_reject = 0;
   u64 x_applied = 0;
   bool more_to_apply = true;    // node.canHaveMoreEntriesToApply (sticky, PUSH_APPLY_READY)
+  // node snapshot state (node.go ss: snapshotIndex, reqSnapshotIndex, compactLogTo)
+  u64 ss_index = 0, ss_req = 0, compact_to = 0;
+  u32 snap_pend = 0, snap_pend_reject = 0;  // SnapshotStatus of InstallSnapshots sent
   std::vector<Message> in[8];   // this round's inbox, per sender slot (stream order)
   std::vector<Message> nxt[8];  // next round's inbox
   ~Node() { delete peer; }
@@ -132,8 +135,10 @@ static u64 hash_message(u64 h, const Message& m) {
   h = hfold(h, m.to);
   h = hfold(h, m.from);
   h = hfold(h, m.term);
-  h = hfold(h, m.log_term);
-  h = hfold(h, m.log_index);
+  // an InstallSnapshot carries its snapshot's (index, term) where other
+  // messages carry LogIndex / LogTerm (the engine's message record)
+  h = hfold(h, m.type == InstallSnapshot ? m.snapshot.term : m.log_term);
+  h = hfold(h, m.type == InstallSnapshot ? m.snapshot.index : m.log_index);
   h = hfold(h, m.commit);
   h = hfold(h, m.hint);
   h = hfold(h, m.hint_high);
@@ -253,8 +258,14 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
   // inbox (node.go:1207-1220), delivered first, no activity recorded
   for (u32 s = 0; s < n; s++)
     if ((nd->x_unreach >> s) & 1u) p->ReportUnreachableNode(s + 1);
-  for (u32 s = 0; s < n; s++)
-    if ((nd->x_snap >> s) & 1u) p->ReportSnapshotStatus(s + 1, ((nd->x_snap_reject >> s) & 1u) != 0);
+  {
+    // the transport's outcome of last round's InstallSnapshots, then host reports
+    const u32 snap = nd->x_snap | nd->snap_pend;
+    const u32 rej = (nd->x_snap_reject & nd->x_snap) | (nd->snap_pend_reject & ~nd->x_snap);
+    nd->snap_pend = nd->snap_pend_reject = 0;
+    for (u32 s = 0; s < n; s++)
+      if ((snap >> s) & 1u) p->ReportSnapshotStatus(s + 1, ((rej >> s) & 1u) != 0);
+  }
   // handleReceivedMessages (node.go:1171-1205); one LocalTick per ticking round
   u64 ltCount = tick ? 1 : 0;
   for (u32 s = 0; s < n; s++) {
@@ -322,7 +333,16 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
   auto deliver = [&](const Message& m) {
     if (m.to < 1 || m.to > n) return;  // not a member of this lockstep group
     u32 d = (u32)(m.to - 1);
-    if (((gr->iso_mask >> k) & 1) || ((gr->iso_mask >> d) & 1)) {
+    const bool dropped = ((gr->iso_mask >> k) & 1) || ((gr->iso_mask >> d) & 1);
+    if (m.type == InstallSnapshot) {
+      // the transport streams the snapshot and reports the outcome to the
+      // sender's node, which hands it to raft at its next step
+      // (ReportSnapshotStatus, peer.go:177-184; nodehost.go snapshot status)
+      nd->snap_pend |= 1u << d;
+      if (dropped) nd->snap_pend_reject |= 1u << d;
+      else nd->snap_pend_reject &= ~(1u << d);
+    }
+    if (dropped) {
       ctr[HC_MSG_DROPPED]++;
       return;
     }
@@ -379,7 +399,41 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
     ctr[HC_ENT_SAVED] += ud.entries_to_save.size();
     for (auto& m : ud.messages)
       if (m.type != Replicate) deliver(m);
+    // a snapshot received through InstallSnapshot: the LogDB takes it and the
+    // state machine recovers from it (node.go processSnapshot / rsm recover)
+    if (!isEmptySnapshot(ud.snapshot)) {
+      nd->db.ApplySnapshot(ud.snapshot);
+      if (!cfg.ext_apply) nd->smAppliedIndex = ud.snapshot.index;
+      nd->ss_index = ud.snapshot.index;
+    }
     p->Commit(ud);  // commitRaftUpdate
+  }
+  if (cfg.snapshot_entries) {
+    // compactLog (node.go:849-866): the compaction a snapshot asked for, at the
+    // node's next step; then saveSnapshotRequired / doSaveSnapshot /
+    // compactSnapshot (node.go:585-605, 619-692) with the state machine's
+    // applied index, done within the step (the lockstep definition of the
+    // snapshot worker)
+    if (nd->compact_to) {
+      nd->db.Compact(nd->compact_to);  // ErrCompacted / ErrUnavailable: nothing to do
+      nd->compact_to = 0;
+    }
+    const u64 S = cfg.snapshot_entries, la = nd->smAppliedIndex;
+    if (!(la <= S + nd->ss_index || la <= S + nd->ss_req)) {
+      nd->ss_req = la;
+      u64 t = 0;
+      if (R->log.term(la, &t) == ErrOK && t != 0) {
+        Snapshot ss;
+        ss.index = la;
+        ss.term = t;
+        for (u32 j = 0; j < n; j++)
+          ss.membership.addresses[j + 1] = "node-" + std::to_string(j + 1);
+        if (nd->db.CreateSnapshot(ss) == ErrOK) {
+          if (la > cfg.compaction_overhead) nd->compact_to = la - cfg.compaction_overhead;
+          nd->ss_index = la;
+        }
+      }
+    }
   }
   ctr[HC_CAMPAIGNS] += R->events.campaignLaunched - campaigns0;
   nd->events = event_bits(ev0, R->events, leader0, R->leaderID);

@@ -67,6 +67,11 @@ struct HarnessConfig {
   u32 xfer_mod = 1;
   // host-driven mode: raft.applied comes from harness_push(PUSH_APPLIED)
   u32 ext_apply = 0;
+  // config.SnapshotEntries / CompactionOverhead (config/config.go): the node
+  // snapshots every SnapshotEntries applied entries and compacts its LogDB to
+  // snapshot index - CompactionOverhead at its next step (harness.cpp)
+  u32 snapshot_entries = 0;
+  u32 compaction_overhead = 0;
 };
 
 // host inputs for the next round (the engine's rbe_push_* / rbe_notify_applied)

@@ -78,7 +78,9 @@ class OrcHarnessConfig(C.Structure):
                 ("iso_period", C.c_uint32), ("iso_len", C.c_uint32), ("iso_mod", C.c_uint32),
                 ("trace", C.c_uint32), ("threads", C.c_uint32), ("pad", C.c_uint32),
                 ("cid_stride", C.c_uint64), ("xfer_period", C.c_uint32),
-                ("xfer_mod", C.c_uint32), ("ext_apply", C.c_uint32), ("pad2", C.c_uint32)]
+                ("xfer_mod", C.c_uint32), ("ext_apply", C.c_uint32),
+                ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
+                ("pad3", C.c_uint32)]
 
 
 class ReplicaView(C.Structure):
@@ -894,7 +896,7 @@ class Harness:
                  wl_enabled=False, wl_start_round=0, wl_stop_round=0, wl_active_mod=1,
                  wl_read_permille=0, iso_period=0, iso_len=0, iso_mod=10, trace=True,
                  threads=1, cid_stride=1, xfer_period=0, xfer_mod=1, ext_apply=False,
-                 ext_inputs=False):
+                 ext_inputs=False, snapshot_entries=0, compaction_overhead=0):
         c = OrcHarnessConfig(
             n_groups=n_groups, n_replicas=n_replicas, check_quorum=int(check_quorum),
             cid_base=cid_base, election_rtt=election_rtt, heartbeat_rtt=heartbeat_rtt,
@@ -903,7 +905,8 @@ class Harness:
             wl_stop_round=wl_stop_round, wl_active_mod=wl_active_mod,
             wl_read_permille=wl_read_permille, iso_period=iso_period, iso_len=iso_len,
             iso_mod=iso_mod, trace=int(trace), threads=threads, cid_stride=cid_stride,
-            xfer_period=xfer_period, xfer_mod=xfer_mod, ext_apply=int(ext_apply))
+            xfer_period=xfer_period, xfer_mod=xfer_mod, ext_apply=int(ext_apply),
+            snapshot_entries=snapshot_entries, compaction_overhead=compaction_overhead)
         self.n_groups, self.n_replicas = n_groups, n_replicas
         self.h = lib().orc_harness_create(C.byref(c))
         if not self.h:

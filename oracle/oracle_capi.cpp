@@ -46,7 +46,8 @@ typedef struct {
   uint32_t wl_active_mod, wl_read_permille, iso_period, iso_len;
   uint32_t iso_mod, trace, threads, pad;
   uint64_t cid_stride;
-  uint32_t xfer_period, xfer_mod, ext_apply, pad2;
+  uint32_t xfer_period, xfer_mod, ext_apply, snapshot_entries;
+  uint32_t compaction_overhead, pad3;
 } orc_harness_config;
 
 static thread_local std::string g_err;
@@ -824,6 +825,8 @@ void* orc_harness_create(const orc_harness_config* c) {
   h.xfer_period = c->xfer_period;
   h.xfer_mod = c->xfer_mod ? c->xfer_mod : 1;
   h.ext_apply = c->ext_apply;
+  h.snapshot_entries = c->snapshot_entries;
+  h.compaction_overhead = c->compaction_overhead;
   return harness_create(h);
   GUARD_END(nullptr)
 }
