@@ -330,7 +330,7 @@ struct rbe_engine {
 };
 
 
-static constexpr int kPlaneAllocs = 20;
+static constexpr int kPlaneAllocs = 22;
 static u64 bytes_of(const Params& C, u64* parts) {
   const u64 N = C.n, G = C.n_groups, R = C.n_rep;
   u64 p[kPlaneAllocs] = {
@@ -354,6 +354,8 @@ static u64 bytes_of(const Params& C, u64* parts) {
       (u64)C.in_cap * sizeof(Ent),
       R * sizeof(u64),
       G * sizeof(u8),
+      C.snapshot_entries ? R * sizeof(SnapSt) : 0,
+      C.snapshot_entries ? R * N * sizeof(u64) : 0,
   };
   u64 t = 0;
   for (int i = 0; i < kPlaneAllocs; i++) {
@@ -416,8 +418,12 @@ static int make_params(const rbe_config* cfg, Params* out) {
   if (cfg->n_groups > 0xFFFFFFFFull && !cfg->in_cap) C.in_cap = 0xFFFFFFFFu;
   C.xfer_period = cfg->xfer_period;
   C.xfer_mod = cfg->xfer_mod;
-  // not yet on the device: snapshots/compaction
-  if (cfg->snapshot_entries || cfg->compaction_overhead) return RBE_E_INVALID;
+  // node snapshots + LogDB compaction (SnapSt; rbe_step.h node_snapshot): the
+  // snapshot is taken at the state machine's applied index, which is the
+  // engine's own (processed) only without ext_apply
+  C.snapshot_entries = cfg->snapshot_entries;
+  C.compaction_overhead = cfg->compaction_overhead;
+  if (C.snapshot_entries && C.ext_apply) return RBE_E_INVALID;
   // the payload heap holds host-pushed Cmds longer than 16 bytes
   C.heap_bytes = (cfg->heap_bytes + 255) & ~255ull;
   if (C.heap_bytes && !C.ext_inputs) return RBE_E_INVALID;
@@ -650,6 +656,8 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   P.in_ents = (Ent*)ptrs[17];
   P.applied = (u64*)ptrs[18];
   P.gwake = (u8*)ptrs[19];
+  P.snp = C.snapshot_entries ? (SnapSt*)ptrs[20] : nullptr;
+  P.rem_snap = C.snapshot_entries ? (u64*)ptrs[21] : nullptr;
   HIP_IGNORE(hipMemsetAsync(P.gwake, GW_AWAKE, C.n_groups, e->stream));  // every group starts awake
   e->hin.init(C.n_rep, C.n, C.in_cap, C.heap_bytes);
   if (C.heap_bytes) {
@@ -1354,15 +1362,27 @@ int rbe_get_updates(rbe_engine* e, uint64_t first, uint64_t count, rbe_update* o
     // (peer.go:209-245) on the range form
     const bool has = (u.flags & RBE_UF_STATE_CHANGED) || u.n_messages || u.n_ready_to_read ||
                      u.n_dropped_entries || u.n_dropped_read_indexes || u.save_lo <= u.save_hi ||
-                     u.apply_lo <= u.apply_hi || (u.flags & RBE_UF_SENT_QUIESCE);
+                     u.apply_lo <= u.apply_hi || (u.flags & (RBE_UF_SENT_QUIESCE | RBE_UF_SNAPSHOT));
     if (has) u.flags |= RBE_UF_HAS_UPDATE;
-    if (update_fast_apply(false, u.save_lo, u.save_hi, u.apply_lo, u.apply_hi))
+    if (update_fast_apply((u.flags & RBE_UF_SNAPSHOT) != 0, u.save_lo, u.save_hi, u.apply_lo,
+                          u.apply_hi))
       u.flags |= RBE_UF_FAST_APPLY;
     if (!update_valid(u.commit, u.save_lo, u.save_hi, u.apply_lo, u.apply_hi))
       u.fault |= RBE_FAULT_PANIC;
     u.role = hot[i].role;
     u.leader_id = core[i].leader;
   }
+  return RBE_OK;
+}
+
+int rbe_get_snapshot_state(rbe_engine* e, uint64_t first, uint64_t count, uint64_t* out6) {
+  if (!e || !out6 || first + count > e->C.n_rep || count == 0) return RBE_E_INVALID;
+  if (!e->C.snapshot_entries) return RBE_E_STATE;
+  HIP_OK(hipSetDevice(e->device));
+  std::vector<SnapSt> v(count);
+  if (d2h(e, v.data(), e->P.snp + first, count)) return RBE_E_HIP;
+  HIP_OK(hipStreamSynchronize(e->stream));
+  for (u64 i = 0; i < count; i++) snap_state_row(v[i], out6 + 6 * i);
   return RBE_OK;
 }
 

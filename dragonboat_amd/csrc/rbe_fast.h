@@ -572,6 +572,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   u32 cdirty = 0;  // Core chunks a proposal or the readIndex queue wrote (fast_finish)
   // ---- eligibility on level-1 data
   if (h.role != R_Leader) return false;
+  if (C.snapshot_entries) return false;  // node snapshots run the full table
   if (h.flags & (HF_APPLY_PENDING | HF_IS_LTT)) return false;
   if (c.ltt != 0) return false;
   if (!ck.tick) return false;
@@ -1248,6 +1249,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   const u64 digest0 = TRACE ? P.upd[r].digest : 0;
   u32 cdirty = 0;  // Core chunks an append or a new leader wrote (fast_finish)
   if (h.role != R_Follower) return false;
+  if (C.snapshot_entries) return false;  // node snapshots run the full table
   if (h.flags & (HF_APPLY_PENDING | HF_IS_LTT)) return false;
   if (c.ltt != 0) return false;
   if (!ck.tick) return false;

@@ -72,9 +72,22 @@ RBE_HD void apply_pair(const Planes& P, u64 rep, u64 val) {
 
 // Check an rbe_launch batch whole (rbe.h) and turn its entries into ring rows
 // (terms, bodies) in batch order; 0 or RBE_E_INVALID.
+// rbe_get_snapshot_state row: marker, marker term, snapshot index, snapshot
+// term, reqSnapshotIndex, compactLogTo
+inline void snap_state_row(const SnapSt& s, u64* o) {
+  o[0] = s.marker;
+  o[1] = s.marker_term;
+  o[2] = s.ss_index;
+  o[3] = s.ss_term;
+  o[4] = s.ss_req;
+  o[5] = s.compact_to;
+}
+
 inline int launch_rows(const Params& C, u64 n, const u64* replica, const rbe_launch_state* st,
                        const rbe_entry* ents, std::vector<u64>& terms, std::vector<Body>& bodies) {
   if (n && (!replica || !st)) return RBE_E_INVALID;
+  // a restart carries no LogDB snapshot / compaction marker (SnapSt) yet
+  if (n && C.snapshot_entries) return RBE_E_INVALID;
   u64 total = 0;
   std::vector<u8> seen;
   for (u64 i = 0; i < n; i++) {

@@ -23,7 +23,7 @@
 namespace rbe {
 
 static constexpr u64 kSnapMagic = 0x31504E5345425255ull;  // "URBESNP1"
-static constexpr int kSnapPlanes = 19;
+static constexpr int kSnapPlanes = 21;
 
 struct SnapHeader {
   u64 magic;
@@ -69,15 +69,19 @@ inline void snap_planes(const Planes& P, const Params& C, SnapPlane* out) {
   add(P.ext, 1, R * sizeof(ExtIn), N * sizeof(ExtIn));
   add(P.idle, 1, R, N);
   add(P.applied, 1, R * sizeof(u64), N * sizeof(u64));
+  if (C.snapshot_entries) {  // node snapshot / compaction state, remote snapshotIndex
+    add(P.snp, 1, R * sizeof(SnapSt), N * sizeof(SnapSt));
+    add(P.rem_snap, 1, R * N * sizeof(u64), N * N * sizeof(u64));
+  }
   // the per-replica fault words live in Hot/Core/Upd; nothing else is carried
-  out[i++] = SnapPlane{nullptr, 0, 0, 0};
+  while (i < kSnapPlanes) out[i++] = SnapPlane{nullptr, 0, 0, 0};
 }
 
 inline u64 snap_body_bytes(const Planes& P, const Params& C, u64 count) {
   SnapPlane pl[kSnapPlanes];
   snap_planes(P, C, pl);
   u64 b = 0;
-  for (int i = 0; i < kSnapPlanes; i++) b += pl[i].rows * pl[i].group_bytes * count;
+  for (int i = 0; i < kSnapPlanes && pl[i].rows; i++) b += pl[i].rows * pl[i].group_bytes * count;
   return b;
 }
 

@@ -118,7 +118,7 @@ RBE_HD Hot load_hot(const Planes& P, const Params& C, u64 r, u32 round) {
 enum : u8 { IB_LAZY = 1, IB_LEAD = 2, IB_ROLE_SHIFT = 4 };
 RBE_HD u8 idle_byte(const Params& C, u8 role, u8 flags, u32 qs) {
   const bool lazy = C.quiesce && qs > 0 && (flags & HF_RAFT_QUIESCE) &&
-                    !(flags & (HF_APPLY_PENDING | HF_APPLIED_NEW));
+                    !(flags & (HF_APPLY_PENDING | HF_APPLIED_NEW | HF_SNAP_WORK));
   return (u8)((lazy ? IB_LAZY : 0) | (role == R_Leader ? IB_LEAD : 0) | ((role & 7u) << IB_ROLE_SHIFT));
 }
 RBE_HD u32 idle_role(u8 ib) { return (ib >> IB_ROLE_SHIFT) & 7u; }
@@ -222,6 +222,12 @@ struct Lane {
   u64 c_match[N], c_next[N];  // LEAD: remote slots held in registers
   u32 c_st[N];
   u8 iso;  // isolation mask of this group for this round
+  // snapshot_entries > 0: the LogDB compaction marker (SnapSt), the
+  // InstallSnapshots sent this step (SnapshotStatus for the next one) and a
+  // snapshot restored from one received
+  u64 marker, marker_term;
+  u8 snp_pend, snp_rej;
+  bool snap_restored;
 
   // per-step outputs
   u64 pc_lo, pc_hi;  // per destination 16-bit A | B << 7 | quiesce << 15 (registers)
@@ -256,10 +262,12 @@ struct Lane {
   // ------------------------------------------------------------- log (term ring)
   RBE_HD u64 ring_slot(u64 idx) const { return (idx & (u64)(C.ring - 1)) * C.n_rep + r; }
   // entryLog.term (logentry.go:142-161): 0 with no error outside
-  // [firstIndex-1, lastIndex]; firstIndex is 1 (no compaction on device).
+  // [firstIndex-1, lastIndex]; firstIndex - 1 is the LogDB's compaction marker
+  // (0 without snapshot_entries), whose term the LogDB keeps (Term(marker)).
   RBE_HD u64 log_term(u64 idx) {
     if (idx > last || idx == 0) return 0;
     if (idx == last) return t_last;
+    if (C.snapshot_entries && idx <= marker) return idx == marker ? marker_term : 0;
     if (last - idx >= C.ring) {
       set_fault(F_WINDOW);
       return 0;
@@ -387,9 +395,15 @@ struct Lane {
   RBE_HD void wait_to_retry(u32 slot) {  // remote.go:94-98
     if (rstate(slot) == RS_Wait) set_rstate(slot, RS_Retry);
   }
-  RBE_HD void become_retry(u32 slot) {  // remote.go:75-83 (snapshotIndex is 0 on device)
-    set_rnext(slot, rmatch(slot) + 1);
+  RBE_HD void become_retry(u32 slot) {  // remote.go:75-83
+    u64 nx = rmatch(slot) + 1;
+    if (rstate(slot) == RS_Snapshot) nx = umax64(nx, P.rem_snap[r * N + slot] + 1);
+    set_rnext(slot, nx);
     set_rstate(slot, RS_Retry);
+  }
+  RBE_HD void become_snapshot(u32 slot, u64 idx) {  // remote.go:108-112
+    P.rem_snap[r * N + slot] = idx;
+    set_rstate(slot, RS_Snapshot);
   }
   RBE_HD void become_replicate(u32 slot) {  // remote.go:102-106
     set_rnext(slot, rmatch(slot) + 1);
@@ -414,7 +428,7 @@ struct Lane {
   RBE_HD void responded_to(u32 slot) {  // remote.go:145-153
     u32 s = rstate(slot);
     if (s == RS_Retry) become_replicate(slot);
-    else if (s == RS_Snapshot) become_retry(slot);  // match >= snapshotIndex (0 on device)
+    else if (s == RS_Snapshot && rmatch(slot) >= P.rem_snap[r * N + slot]) become_retry(slot);
   }
   RBE_HD bool decrease_to(u32 slot, u64 rejected, u64 lst) {  // remote.go:155-171
     if (rstate(slot) == RS_Replicate) {
@@ -722,6 +736,25 @@ struct Lane {
   RBE_HD void send_replicate(u32 slot) {  // raft.go:758-792
     if (is_paused(slot)) return;
     u64 next = rnext(slot);
+    if (C.snapshot_entries && next <= marker) {
+      // entries(next) is ErrCompacted (logentry.go:163-178): the remote gets
+      // the LogDB's snapshot if it is active (makeInstallSnapshotMessage,
+      // raft.go:684-697); the record carries its (index, term) as LogIndex /
+      // LogTerm, and the transport reports its outcome to the next step
+      if (!ractive(slot)) return;
+      const SnapSt& sp = P.snp[r];
+      const u64 si = sp.ss_index;
+      Msg m = mk(M_InstallSnapshot, (u8)(slot + 1));
+      m.log_index = si;
+      m.log_term = sp.ss_term;
+      become_snapshot(slot, si);
+      const u32 bit = 1u << slot;
+      snp_pend |= (u8)bit;
+      if (((iso >> k) & 1u) || ((iso >> slot) & 1u)) snp_rej |= (u8)bit;
+      else snp_rej &= (u8)~bit;
+      send(m);
+      return;
+    }
     // makeReplicateMessage (raft.go:709-740)
     u64 lt = log_term(next - 1);
     Msg m = mk(M_Replicate, (u8)(slot + 1));
@@ -967,6 +1000,39 @@ struct Lane {
     }
     send(resp);
   }
+  // handleInstallSnapshotMessage + restore (raft.go:1311-1337, 439-470) with
+  // entryLog.restore (logentry.go:396-401): the log becomes the snapshot
+  RBE_HD void on_install_snapshot(const Msg& m) {
+    Msg resp = mk(M_ReplicateResp, m.from);
+    const u64 si = m.log_index, st = m.log_term;
+    bool restored = false;
+    if (si > committed) {
+      if (match_term(si, st)) {
+        commit_to(si);
+      } else if (!C.snapshot_entries) {
+        set_fault(F_UNSUPPORTED);  // no SnapSt plane to take it
+      } else {
+        last = si;
+        t_last = st;
+        committed = processed = saved_to = si;
+        marker = si;
+        marker_term = st;
+        SnapSt& sp = P.snp[r];
+        sp.ss_index = si;  // LogDB.ApplySnapshot (after the step's Update)
+        sp.ss_term = st;
+        seg_len = 0;
+        snap_restored = true;
+        restored = true;
+      }
+    }
+    if (restored) {
+      resp.log_index = last;
+    } else {
+      resp.log_index = committed;
+      events |= EV_SNAPSHOT_REJECTED;
+    }
+    send(resp);
+  }
   RBE_HD void on_heartbeat(const Msg& m) {  // raft.go:1301-1309
     commit_to(m.commit);
     Msg resp = mk(M_HeartbeatResp, m.from);
@@ -1208,7 +1274,11 @@ struct Lane {
           case M_Election: on_election(); return;
           case M_RequestVote: on_request_vote(m); return;
           case M_TimeoutNow: on_timeout_now(); return;
-          case M_InstallSnapshot:
+          case M_InstallSnapshot:  // raft.go:1900-1904
+            etick = 0;
+            leader = m.from;
+            on_install_snapshot(m);
+            return;
           case M_ConfigChangeEvent:
           case M_SnapshotReceived: set_fault(F_UNSUPPORTED); return;
           default: return;
@@ -1231,7 +1301,10 @@ struct Lane {
           case M_RequestVoteResp: on_vote_resp(m); return;
           case M_Election: on_election(); return;
           case M_RequestVote: on_request_vote(m); return;
-          case M_InstallSnapshot:
+          case M_InstallSnapshot:  // raft.go:1954-1957
+            become_follower(term, m.from);
+            on_install_snapshot(m);
+            return;
           case M_ConfigChangeEvent:
           case M_SnapshotReceived: set_fault(F_UNSUPPORTED); return;
           default: return;
@@ -1253,7 +1326,14 @@ struct Lane {
             if (m.from >= 1 && m.from <= N && rstate(m.from - 1u) == RS_Replicate)
               become_retry(m.from - 1u);
             return;
-          case M_SnapshotStatus: return;  // no remote is ever in Snapshot state on device
+          case M_SnapshotStatus:  // raft.go:1758-1771
+            if (m.from >= 1 && m.from <= N && rstate(m.from - 1u) == RS_Snapshot) {
+              const u32 sl = m.from - 1u;
+              if (m.reject) P.rem_snap[r * N + sl] = 0;  // clearPendingSnapshot
+              become_retry(sl);                        // becomeWait
+              if (rstate(sl) == RS_Retry) set_rstate(sl, RS_Wait);
+            }
+            return;
           case M_Election: return;        // leader ignores Election
           case M_RequestVote: on_request_vote(m); return;
           case M_ConfigChangeEvent:
@@ -1309,6 +1389,7 @@ struct Lane {
   // Called after load() and before any state is written.  Reads only the
   // 24-byte message headers of the inbox.
   RBE_HD bool fast_eligible(u32 inp) const {
+    if (C.snapshot_entries) return false;  // node snapshots run the full table
     if (role != (LEAD ? R_Leader : R_Follower)) return false;
     if (flags & HF_APPLY_PENDING) return false;
     if (ltt != 0 || (flags & HF_IS_LTT)) return false;
@@ -1363,6 +1444,47 @@ struct Lane {
       if (C.check_quorum && !q_at_tick && etick + 1u >= C.election_rtt) return false;
     }
     return true;
+  }
+
+  // ------------------------------------------------------------- node snapshots
+  // After the step's Update (snapshot_entries > 0), in the node's order: a
+  // snapshot restored from InstallSnapshot is the LogDB's (ApplySnapshot) and
+  // the state machine's applied index; the compaction the last snapshot asked
+  // for runs (compactLog, node.go:849-866; LogDB.Compact: only inside
+  // (marker, lastIndex]); then saveSnapshotRequired (node.go:585-605) with the
+  // applied index makes a snapshot at it and asks for a compaction to
+  // index - CompactionOverhead at the next step (doSaveSnapshot /
+  // compactSnapshot, node.go:619-692), done within the step.
+  RBE_HD void node_snapshot() {
+    SnapSt sp = P.snp[r];
+    if (snap_restored) flags |= HF_APPLIED_NEW;  // smAppliedIndex moved to the snapshot
+    sp.marker = marker;
+    sp.marker_term = marker_term;
+    if (sp.compact_to) {
+      const u64 c = sp.compact_to;
+      if (c > marker && c <= last) {
+        sp.marker_term = log_term(c);
+        sp.marker = c;
+      }
+      sp.compact_to = 0;
+    }
+    const u64 S = C.snapshot_entries, la = processed;
+    if (la > S + sp.ss_index && la > S + sp.ss_req) {
+      sp.ss_req = la;
+      const u64 t = log_term(la);
+      if (t != 0) {
+        sp.ss_index = la;
+        sp.ss_term = t;
+        sp.compact_to = la > C.compaction_overhead ? la - C.compaction_overhead : 0;
+      }
+    }
+    sp.pend = snp_pend;
+    sp.pend_rej = snp_rej;
+    P.snp[r] = sp;
+    marker = sp.marker;
+    marker_term = sp.marker_term;
+    if (sp.compact_to || sp.pend) flags |= HF_SNAP_WORK;
+    else flags &= (u8)~HF_SNAP_WORK;
   }
 
   // ------------------------------------------------------------- the step
@@ -1454,6 +1576,17 @@ struct Lane {
     }
     fault = (flags & HF_FAULTED) ? P.upd[r].fault : 0u;
     const u64 digest0 = TRACE ? P.upd[r].digest : 0;
+    snp_pend = snp_rej = 0;
+    snap_restored = false;
+    u8 pend0 = 0, pend_rej0 = 0;
+    marker = marker_term = 0;
+    if (FULL && C.snapshot_entries) {
+      const SnapSt& sp = P.snp[r];
+      marker = sp.marker;
+      marker_term = sp.marker_term;
+      pend0 = sp.pend;
+      pend_rej0 = sp.pend_rej;
+    }
     pc_lo = pc_hi = 0;
     arena_used = 0;
     seg_lo = 0;
@@ -1508,6 +1641,12 @@ struct Lane {
           snap_reject = ext.snap_reject;
         }
       }
+    }
+    if (pend0) {
+      // the transport's outcome of last step's InstallSnapshots joins the host
+      // reports (ReportSnapshotStatus, peer.go:177-184), a host report winning
+      snap_reject = (u8)((snap_reject & snap_nodes) | (pend_rej0 & ~snap_nodes));
+      snap_nodes = (u8)(snap_nodes | pend0);
     }
     if (!clk.tick) {
       // a round without a tick is a step only if handleEvents finds an event
@@ -1756,6 +1895,7 @@ struct Lane {
     else flags &= (u8)~HF_APPLY_PENDING;
     if (u.apply_hi >= u.apply_lo && !C.ext_apply) flags |= HF_APPLIED_NEW;
     else flags &= (u8)~HF_APPLIED_NEW;
+    if (FULL && C.snapshot_entries) node_snapshot();
     if (fault) flags |= HF_FAULTED;
     if (role == R_Leader) {
       ctr.v[C_COMMITTED] += (u32)(committed - committed0);
@@ -1794,7 +1934,8 @@ struct Lane {
     u.fault = fault;
     u.flags = (u16)((term != term0 || vote != vote0 || committed != committed0 ? UF_STATE_CHANGED
                                                                                 : 0u) |
-                    (send_q ? UF_SENT_QUIESCE : 0u) | UF_RANGES);
+                    (send_q ? UF_SENT_QUIESCE : 0u) | (snap_restored ? UF_SNAPSHOT : 0u) |
+                    UF_RANGES);
     u.events = (u16)(events | (leader != leader0 ? EV_LEADER_UPDATED : 0u));
     u.round = round;
     u.pad1 = 0;
@@ -2128,6 +2269,7 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, const Clk& ck
   const u64 cid = C.cid_base + g * C.cid_stride;
   const u32 cls = h.role == R_Leader ? T_LEAD : (h.role == R_Follower ? T_FOLL : T_FULL);
   if (nmsg || (h.flags & HF_APPLY_PENDING)) return cls;
+  if (h.flags & HF_SNAP_WORK) return T_FULL;  // SnapshotStatus / compaction (node_snapshot)
   if (!ck.tick && (h.flags & HF_APPLIED_NEW)) return cls;
   if (h.role == R_Leader && wl_input(C, cid, round)) return cls;
   if (C.xfer_period && xfer_input(C, cid, round, k)) return cls;

@@ -73,6 +73,8 @@ enum : u8 {
   HF_APPLIED_NEW = 32,  // the last step returned committed entries: the node's
                         // confirmedIndex lags its applied index until the next
                         // step (node.go:907-923, 1033), an event of its own
+  HF_SNAP_WORK = 128,   // SnapSt has a compaction or a SnapshotStatus for the next
+                        // step (snapshot_entries > 0): triage sends it to k_full
 };
 
 // core plane (64 B per replica)
@@ -91,6 +93,21 @@ struct alignas(16) Core {
   u64 t_last;      // term of entry last_index (log-tail cache)
   u64 lead_start;  // leader: index of its no-op, the first entry of its term (raft.go:985);
                    // entries [lead_start, last_index] have term == term, earlier ones less
+};
+
+// node snapshot / LogDB compaction state (snapshot_entries > 0; 64 B per
+// replica).  marker is the LogDB's compaction marker (logdb: entries at or
+// below it are gone, Term(marker) = marker_term); ss_* the LogDB's latest
+// snapshot (CreateSnapshot or one received by InstallSnapshot, ApplySnapshot);
+// ss_req / compact_to the node's reqSnapshotIndex and compactLogTo (node.go
+// 585-605, 849-866); pend / pend_rej the SnapshotStatus the transport reports
+// for this replica's InstallSnapshots of the last step (bit id-1 per target).
+struct alignas(16) SnapSt {
+  u64 marker, marker_term;
+  u64 ss_index, ss_term;
+  u64 ss_req, compact_to;
+  u8 pend, pend_rej;
+  u8 pad[14];
 };
 
 // remote slot (remote.go:62-69): match/next; state|active<<2 lives in a u8 plane
@@ -167,7 +184,13 @@ struct alignas(16) Upd {
   u16 n_msgs;       // messages emitted this step (Update.Messages)
   u16 n_rtr;        // ReadyToReads
 };
-enum : u32 { UF_STATE_CHANGED = 1, UF_SENT_QUIESCE = 2, UF_HAS_UPDATE = 4, UF_RANGES = 0x100 };
+enum : u32 {
+  UF_STATE_CHANGED = 1, UF_SENT_QUIESCE = 2, UF_HAS_UPDATE = 4,
+  UF_SNAPSHOT = 0x20,  // the step restored a snapshot from InstallSnapshot: Update.Snapshot is
+                       // SnapSt::ss_index / ss_term (the state machine recovers from it);
+                       // the same bit as RBE_UF_SNAPSHOT
+  UF_RANGES = 0x100
+};
 // server.IRaftEventListener (internal/server/event.go) calls a step made, one
 // bit per event kind (raft.go:354, 1090, 1333, 1368, 1503, 1995, 2010).
 // LeaderUpdated fires on every setLeaderID call in the reference, unchanged
@@ -288,6 +311,8 @@ struct Planes {
   ExtIn* ext;         // [n_rep]
   Ent* in_ents;       // [in_cap] proposal entries pushed for the next step
   u64* applied;       // [n_rep] raft.applied from rbe_notify_applied (ext_apply)
+  SnapSt* snp;        // [n_rep] node snapshot state (snapshot_entries > 0, else null)
+  u64* rem_snap;      // [n_rep * N] remote.snapshotIndex (read only in RS_Snapshot)
   u8* gwake;          // [n_groups] GW_* bits: lets k_triage skip a sleeping group whole
                       // (rbe_step.h, group sleep)
   u64* counters;      // [C_NUM]

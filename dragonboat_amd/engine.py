@@ -89,7 +89,7 @@ class RbeUpdate(C.Structure):
 
 
 # Update flags and listener events (include/rbe.h RBE_UF_* / RBE_EV_*)
-UF_STATE_CHANGED, UF_SENT_QUIESCE, UF_FAST_APPLY, UF_HAS_UPDATE = 1, 2, 8, 16
+UF_STATE_CHANGED, UF_SENT_QUIESCE, UF_FAST_APPLY, UF_HAS_UPDATE, UF_SNAPSHOT = 1, 2, 8, 16, 32
 EV_LEADER_UPDATED, EV_CAMPAIGN_LAUNCHED, EV_CAMPAIGN_SKIPPED, EV_SNAPSHOT_REJECTED = 1, 2, 4, 8
 EV_REPLICATION_REJECTED, EV_PROPOSAL_DROPPED, EV_READ_INDEX_DROPPED = 16, 32, 64
 
@@ -139,7 +139,7 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_push_messages", "rbe_snapshot_bytes", "rbe_export_groups", "rbe_import_groups",
            "rbe_get_entry_cmds", "rbe_set_apply_ready", "rbe_collect_outputs", "rbe_launch",
            "rbe_xchg_chunk_bytes", "rbe_xchg_pack_fixed", "rbe_xchg_unpack_fixed",
-           "rbe_xchg_status", "rbe_stream"]
+           "rbe_xchg_status", "rbe_stream", "rbe_get_snapshot_state"]
 KERNEL_SLOTS = 4
 
 _lib = None
@@ -193,6 +193,7 @@ def load_library(path: Optional[str] = None):
         "rbe_get_entries": (i32, [vp, u64, u64, u64, P(RbeEntry)]),
         "rbe_get_entry_cmds": (i32, [vp, u64, u64, u64, vp, u64, P(u64)]),
         "rbe_get_views": (i32, [vp, u64, u64, P(RbeReplicaView)]),
+        "rbe_get_snapshot_state": (i32, [vp, u64, u64, P(u64)]),
         "rbe_collect_outputs": (i32, [vp, u64, u64, P(RbeOutputs)]),
         "rbe_launch": (i32, [vp, u64, P(u64), P(RbeLaunchState), P(RbeEntry)]),
         "rbe_get_counters": (i32, [vp, P(u64)]),
@@ -242,7 +243,8 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                 wl_read_permille: int = 0, ext_inputs: bool = False, iso_period: int = 0,
                 iso_len: int = 0, iso_mod: int = 10, rep_world: int = 0,
                 rep_rank: int = 0, ext_apply: bool = False, in_cap: int = 0,
-                xfer_period: int = 0, xfer_mod: int = 1, heap_bytes: int = 0) -> RbeConfig:
+                xfer_period: int = 0, xfer_mod: int = 1, heap_bytes: int = 0,
+                snapshot_entries: int = 0, compaction_overhead: int = 0) -> RbeConfig:
     return RbeConfig(abi_version=RBE_ABI_VERSION, device=device, n_groups=n_groups,
                      n_replicas=n_replicas, election_rtt=election_rtt,
                      heartbeat_rtt=heartbeat_rtt, check_quorum=int(check_quorum),
@@ -255,7 +257,8 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                      iso_period=iso_period, iso_len=iso_len, iso_mod=iso_mod,
                      rep_world=rep_world, rep_rank=rep_rank, ext_apply=int(ext_apply),
                      in_cap=in_cap, xfer_period=xfer_period, xfer_mod=xfer_mod,
-                     heap_bytes=heap_bytes)
+                     heap_bytes=heap_bytes, snapshot_entries=snapshot_entries,
+                     compaction_overhead=compaction_overhead)
 
 
 class InputError(EngineError):
@@ -538,6 +541,16 @@ class Engine(NodeInputs):
         arr = (RbeReplicaView * count)()
         _check(self.lib.rbe_get_views(self.h, first, count, arr), "rbe_get_views")
         return arr
+
+    def snapshot_state(self, first: int = 0, count: Optional[int] = None) -> np.ndarray:
+        """[count, 6] uint64: LogDB compaction marker, its term, snapshot index,
+        snapshot term, reqSnapshotIndex, pending compactLogTo per replica
+        (rbe_get_snapshot_state; snapshot_entries > 0)."""
+        count = self.n_rep - first if count is None else count
+        out = (C.c_uint64 * (6 * count))()
+        _check(self.lib.rbe_get_snapshot_state(self.h, first, count, out),
+               "rbe_get_snapshot_state")
+        return np.frombuffer(out, dtype=np.uint64).reshape(count, 6).copy()
 
     def views_np(self, first: int = 0, count: Optional[int] = None) -> np.ndarray:
         """views() as a numpy structured array (zero-copy over the ctypes array)."""

@@ -130,8 +130,12 @@ typedef struct rbe_config {
    * xfer_period rounds in groups selected 1 in xfer_mod), 0 = off */
   uint32_t xfer_period;
   uint32_t xfer_mod;
-  uint32_t snapshot_entries;     /* reserved: config.SnapshotEntries, must be 0 */
-  uint32_t compaction_overhead;  /* reserved: config.CompactionOverhead, must be 0 */
+  uint32_t snapshot_entries;     /* config.SnapshotEntries: a node snapshot at the applied
+                                    index every that many applied entries, 0 = never
+                                    (requires ext_apply = 0; rbe_launch then refused) */
+  uint32_t compaction_overhead;  /* config.CompactionOverhead: the LogDB keeps that many
+                                    entries below a snapshot (compacted at the next step);
+                                    a remote that needs older entries gets InstallSnapshot */
   uint64_t heap_bytes;           /* payload heap for Cmd > 16 B (needs ext_inputs), 0 = none:
                                     Cmd is then at most 16 bytes */
   uint32_t reserved[4];
@@ -166,6 +170,8 @@ typedef struct rbe_update {
 #define RBE_UF_SENT_QUIESCE 2u
 #define RBE_UF_FAST_APPLY 8u      /* Update.FastApply (peer.go:209-226 setFastApply) */
 #define RBE_UF_HAS_UPDATE 16u     /* the step produced an Update (Peer.HasUpdate, peer.go:253-280) */
+#define RBE_UF_SNAPSHOT 32u       /* Update.Snapshot: the replica restored the snapshot an
+                                     InstallSnapshot carried (rbe_get_snapshot_state) */
 
 /* server.IRaftEventListener calls of a step (internal/server/event.go;
  * raft.go:354, 1090, 1333, 1368, 1503, 1995, 2010), one bit per kind.
@@ -323,6 +329,13 @@ int rbe_get_ready_to_reads(rbe_engine* e, uint64_t replica, rbe_ready_to_read* o
                            uint32_t cap, uint32_t* n_out);
 int rbe_get_entries(rbe_engine* e, uint64_t replica, uint64_t lo, uint64_t hi,
                     rbe_entry* out);
+/* Node snapshot state of replicas [first, first + count) (snapshot_entries > 0,
+ * else RBE_E_STATE): six words each — the LogDB's compaction marker and its
+ * term (entries at or below it are gone: logdb.go Compact / RemoveEntriesTo),
+ * the latest snapshot's index and term (CreateSnapshot, or ApplySnapshot of one
+ * received), the node's reqSnapshotIndex and pending compactLogTo (node.go
+ * ss, 585-605 / 849-866). */
+int rbe_get_snapshot_state(rbe_engine* e, uint64_t first, uint64_t count, uint64_t* out6);
 /* The Cmd bytes of entries [lo, hi] of a replica's log, concatenated in `buf`:
  * entry lo + i occupies [offsets[i], offsets[i + 1]) (offsets has hi - lo + 2
  * slots and is filled even when `cap` is short, which returns RBE_E_NOMEM).

@@ -235,7 +235,7 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
   if (!tick) {
     // a round without a tick is a step only if handleEvents finds an event
     // (node.go:1030-1067)
-    bool ev = do_read || do_prop || xfer || nd->x_unreach || nd->x_snap ||
+    bool ev = do_read || do_prop || xfer || nd->x_unreach || nd->x_snap || nd->snap_pend ||
               p->HasEntryToApply() || applied != nd->confirmedIndex;
     for (u32 s = 0; s < n; s++) ev = ev || !nd->in[s].empty();
     if (!ev) return;
@@ -557,6 +557,17 @@ void harness_persisted(const Harness* h, u64 replica, u64 out4[4]) {
   out4[1] = st.vote;
   out4[2] = st.commit;
   out4[3] = db.lastIndex();
+}
+
+void harness_snapshot_state(const Harness* h, u64 replica, u64 out6[6]) {
+  const u32 N = h->cfg.n_replicas;
+  const Node* nd = h->groups[replica / N]->nodes[replica % N];
+  out6[0] = nd->db.markerIndex;
+  out6[1] = nd->db.markerTerm;
+  out6[2] = nd->db.snapshot.index;
+  out6[3] = nd->db.snapshot.term;
+  out6[4] = nd->ss_req;
+  out6[5] = nd->compact_to;
 }
 
 int harness_persisted_entries(const Harness* h, u64 replica, u64 lo, u64 hi, Entry* out) {

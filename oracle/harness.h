@@ -160,6 +160,8 @@ u64 harness_log_term(const Harness* h, u64 g, u32 k, u64 index);  // term of ent
 // engine's rbe_launch): persisted state, persisted entries, the restart itself
 void harness_persisted(const Harness* h, u64 replica, u64 out4[4]);  // term, vote, commit, last
 int harness_persisted_entries(const Harness* h, u64 replica, u64 lo, u64 hi, Entry* out);
+// LogDB marker, marker term, snapshot index, snapshot term; node reqSnapshotIndex, compactLogTo
+void harness_snapshot_state(const Harness* h, u64 replica, u64 out6[6]);
 void harness_restart(Harness* h, u64 replica);
 
 // shared helpers (restated independently in the engine)

@@ -185,6 +185,7 @@ def lib():
             "orc_harness_counters": (None, [vp, P(u64)]),
             "orc_harness_log_term": (u64, [vp, u64, u32, u64]),
             "orc_harness_persisted": (None, [vp, u64, P(u64)]),
+            "orc_harness_snapshot_state": (None, [vp, u64, P(u64)]),
             "orc_harness_persisted_entries": (i32, [vp, u64, u64, u64, P(OrcEntry)]),
             "orc_harness_restart": (i32, [vp, u64]),
             "orc_view_size": (i32, []),
@@ -954,6 +955,13 @@ class Harness:
         """(term, vote, commit, last_index) of a replica's LogDB."""
         o = (C.c_uint64 * 4)()
         lib().orc_harness_persisted(self.h, replica, o)
+        return tuple(o)
+
+    def snapshot_state(self, replica):
+        """(marker, marker_term, ss_index, ss_term, ss_req, compact_to): the
+        LogDB's compaction marker and snapshot, the node's snapshot request."""
+        o = (C.c_uint64 * 6)()
+        lib().orc_harness_snapshot_state(self.h, replica, o)
         return tuple(o)
 
     def persisted_entries(self, replica, lo, hi):

@@ -25,6 +25,7 @@ def lib():
         L.soa_run.argtypes = [C.c_void_p, C.c_uint32]
         L.soa_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         L.soa_views.argtypes = [C.c_void_p, C.c_void_p]
+        L.soa_snapshot_state.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         L.soa_set_full_only.argtypes = [C.c_void_p, C.c_int]
         L.soa_set_staged.argtypes = [C.c_void_p, C.c_int]
         L.soa_slow_total.restype = C.c_uint64
@@ -176,6 +177,11 @@ class SoaCpu(NodeInputs):
         arr = (RbeReplicaView * self.n_rep)()
         lib().soa_views(self.h, C.cast(arr, C.c_void_p))
         return arr
+
+    def snapshot_state(self):
+        o = (C.c_uint64 * (6 * self.n_rep))()
+        lib().soa_snapshot_state(self.h, o)
+        return [tuple(o[6 * r:6 * r + 6]) for r in range(self.n_rep)]
 
     def counters(self):
         o = (C.c_uint64 * CTR_NUM)()

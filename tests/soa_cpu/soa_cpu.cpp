@@ -198,6 +198,8 @@ void* soa_create(const rbe_config* cfg) {
   C.iso_mod = cfg->iso_mod;
   C.rep_world = cfg->rep_world > 1 ? cfg->rep_world : 1;
   C.rep_rank = cfg->rep_rank;
+  C.snapshot_entries = cfg->snapshot_entries;
+  C.compaction_overhead = cfg->compaction_overhead;
   if (C.n != 1 && C.n != 3 && C.n != 5) {
     delete e;
     return nullptr;
@@ -229,6 +231,8 @@ void* soa_create(const rbe_config* cfg) {
   P.applied = alloc<u64>(e, R);
   P.gwake = alloc<u8>(e, G);
   memset(P.gwake, GW_AWAKE, G);  // every group starts awake
+  P.snp = C.snapshot_entries ? alloc<SnapSt>(e, R) : nullptr;
+  P.rem_snap = C.snapshot_entries ? alloc<u64>(e, R * N) : nullptr;
   C.heap_bytes = (cfg->heap_bytes + 255) & ~255ull;
   e->heap.assign(C.heap_bytes, 0);
   e->hin.init(R, C.n, C.in_cap, C.heap_bytes);
@@ -375,6 +379,14 @@ int soa_notify_applied(void* h, uint64_t n, const uint64_t* replica, const uint6
   SoaEngine* e = (SoaEngine*)h;
   if (!e->C.ext_apply) return RBE_E_STATE;
   return e->hin.notify_applied(n, replica, applied);
+}
+
+void soa_snapshot_state(void* h, uint64_t* out6) {
+  SoaEngine* e = (SoaEngine*)h;
+  for (u64 r = 0; r < e->C.n_rep; r++) {
+    if (e->P.snp) snap_state_row(e->P.snp[r], out6 + 6 * r);
+    else memset(out6 + 6 * r, 0, 6 * sizeof(u64));
+  }
 }
 
 void soa_counters(void* h, uint64_t* out) {
