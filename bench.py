@@ -54,6 +54,16 @@ WORKLOADS = {
                 wl_start_round=40, iso_period=50, iso_len=30, iso_mod=10, ring=128,
                 ecap=256),
            100, "C3: 100k groups x 5, CheckQuorum, leader isolation 30/50 rounds for 10%"),
+    # node snapshots every 16 applied entries, LogDB compacted to 8 below
+    # (config.SnapshotEntries / CompactionOverhead), InstallSnapshot for laggards
+    "c2s": (dict(n_groups=1_000_000, n_replicas=3, wl_enabled=True, wl_start_round=30,
+                 ring=64, snapshot_entries=16, compaction_overhead=8), 60,
+            "C2 at 1M groups x 3 with SnapshotEntries=16, CompactionOverhead=8"),
+    "c3s": (dict(n_groups=100_000, n_replicas=5, check_quorum=True, wl_enabled=True,
+                 wl_start_round=40, iso_period=150, iso_len=100, iso_mod=10, ring=64,
+                 ecap=256, snapshot_entries=20, compaction_overhead=5), 100,
+            "C3 with 100-round isolations in a 64-entry window: SnapshotEntries=20, "
+            "CompactionOverhead=5, InstallSnapshot brings the isolated replicas back"),
     # groups per GPU; every rank holds the planes of all N x 500k groups and
     # steps the replicas it owns
     "c5": (dict(n_groups=500_000, n_replicas=3, wl_enabled=True, wl_start_round=30, ring=64),
@@ -69,7 +79,8 @@ ENGINE_ONLY = ("ring", "ecap", "maxm", "rq_cap", "rtr_cap", "dri_cap")
 # bounded CPU-baseline samples (groups for the T-thread run, groups for the
 # 1-thread run), sized for ~5-15 s of host time each on the GPU box
 CPU_SAMPLE = {"c4": (300_000, 30_000), "c2": (10_000, 10_000), "c2m": (100_000, 10_000),
-              "c3": (50_000, 5_000), "c5": (100_000, 10_000)}
+              "c3": (50_000, 5_000), "c5": (100_000, 10_000), "c2s": (100_000, 10_000),
+              "c3s": (50_000, 5_000)}
 
 
 def dist_env():

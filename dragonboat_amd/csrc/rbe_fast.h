@@ -338,6 +338,34 @@ struct FastQ {
   }
 };
 
+// saveSnapshotRequired / doSaveSnapshot (node.go:585-605, 619-692) after a
+// fast step that applied entries (snapshot_entries > 0): the snapshot at the
+// applied index la and the compaction it asks for (run by the next step, a
+// full one: HF_SNAP_WORK).  A fast step never restores or compacts, and with
+// nothing applied the threshold cannot have been crossed (Lane::node_snapshot).
+template <int N, bool TRACE>
+RBE_HD void fast_node_snapshot(const Planes& P, const Params& C, StepCounters& ctr,
+                               FastOut<N, TRACE>& o, u64 la, u64 last, u64 t_last, u8& flags) {
+  SnapSt* sp = &P.snp[o.r];
+  const u64 S = C.snapshot_entries;
+  if (!(la > S + sp->ss_index && la > S + sp->ss_req)) return;
+  sp->ss_req = la;
+  u64 t = t_last;
+  if (la != last) {
+    if (last - la >= C.ring) {
+      o.set_fault(ctr, F_WINDOW);
+      return;
+    }
+    t = P.term_ring[(la & (u64)(C.ring - 1)) * C.n_rep + o.r];
+  }
+  if (t == 0) return;
+  sp->ss_index = la;
+  sp->ss_term = t;
+  const u64 ct = la > C.compaction_overhead ? la - C.compaction_overhead : 0;
+  sp->compact_to = ct;
+  if (ct) flags |= HF_SNAP_WORK;
+}
+
 // Common epilogue: stepNode's quiesce send, getUpdate/Commit, the trace digest,
 // the Update record, this round's outbox counts, Hot/Core write-back.
 // Mirrors the tail of Lane::run().
@@ -416,6 +444,8 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
   else flags &= (u8)~HF_APPLY_PENDING;
   if (u.apply_hi >= u.apply_lo && !C.ext_apply) flags |= HF_APPLIED_NEW;
   else flags &= (u8)~HF_APPLIED_NEW;
+  if (C.snapshot_entries && u.apply_hi >= u.apply_lo)
+    fast_node_snapshot<N, TRACE>(P, C, ctr, o, c.processed, c.last_index, c.t_last, flags);
   if (role == R_Leader) {
     ctr.v[C_COMMITTED] += (u32)(c.committed - committed0);
     ctr.v[C_LEADER_STEPS]++;
@@ -572,7 +602,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   u32 cdirty = 0;  // Core chunks a proposal or the readIndex queue wrote (fast_finish)
   // ---- eligibility on level-1 data
   if (h.role != R_Leader) return false;
-  if (C.snapshot_entries) return false;  // node snapshots run the full table
+  if (h.flags & HF_SNAP_WORK) return false;  // compaction / SnapshotStatus: full table
   if (h.flags & (HF_APPLY_PENDING | HF_IS_LTT)) return false;
   if (c.ltt != 0) return false;
   if (!ck.tick) return false;
@@ -1249,7 +1279,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   const u64 digest0 = TRACE ? P.upd[r].digest : 0;
   u32 cdirty = 0;  // Core chunks an append or a new leader wrote (fast_finish)
   if (h.role != R_Follower) return false;
-  if (C.snapshot_entries) return false;  // node snapshots run the full table
+  if (h.flags & HF_SNAP_WORK) return false;  // compaction / SnapshotStatus: full table
   if (h.flags & (HF_APPLY_PENDING | HF_IS_LTT)) return false;
   if (c.ltt != 0) return false;
   if (!ck.tick) return false;

@@ -1017,6 +1017,7 @@ struct Lane {
         committed = processed = saved_to = si;
         marker = si;
         marker_term = st;
+        P.term_ring[ring_slot(si)] = st;  // the fast steps read Term(marker) from the ring
         SnapSt& sp = P.snp[r];
         sp.ss_index = si;  // LogDB.ApplySnapshot (after the step's Update)
         sp.ss_term = st;
@@ -1389,7 +1390,7 @@ struct Lane {
   // Called after load() and before any state is written.  Reads only the
   // 24-byte message headers of the inbox.
   RBE_HD bool fast_eligible(u32 inp) const {
-    if (C.snapshot_entries) return false;  // node snapshots run the full table
+    if (flags & HF_SNAP_WORK) return false;  // compaction / SnapshotStatus: full table
     if (role != (LEAD ? R_Leader : R_Follower)) return false;
     if (flags & HF_APPLY_PENDING) return false;
     if (ltt != 0 || (flags & HF_IS_LTT)) return false;
@@ -1580,7 +1581,7 @@ struct Lane {
     snap_restored = false;
     u8 pend0 = 0, pend_rej0 = 0;
     marker = marker_term = 0;
-    if (FULL && C.snapshot_entries) {
+    if (C.snapshot_entries) {
       const SnapSt& sp = P.snp[r];
       marker = sp.marker;
       marker_term = sp.marker_term;
@@ -1895,7 +1896,7 @@ struct Lane {
     else flags &= (u8)~HF_APPLY_PENDING;
     if (u.apply_hi >= u.apply_lo && !C.ext_apply) flags |= HF_APPLIED_NEW;
     else flags &= (u8)~HF_APPLIED_NEW;
-    if (FULL && C.snapshot_entries) node_snapshot();
+    if (C.snapshot_entries) node_snapshot();
     if (fault) flags |= HF_FAULTED;
     if (role == R_Leader) {
       ctr.v[C_COMMITTED] += (u32)(committed - committed0);

@@ -10,7 +10,8 @@ from test_log_compaction import CASES, run_case
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name", ["C3_SNAP", "C3_NOCQ_SNAP", "MIXED_SNAP", "C4_SNAP"])
+@pytest.mark.parametrize("name", ["C3_SNAP", "C3_NOCQ_SNAP", "C3_R64_ISO100", "MIXED_SNAP",
+                                  "C4_SNAP"])
 def test_gpu_compaction_install_snapshot_parity(gpu_available, name):
     from dragonboat_amd.engine import Engine
     kw, extra, rounds = CASES[name]

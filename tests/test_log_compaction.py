@@ -27,6 +27,8 @@ CASES = {
     # no check-quorum: an isolated remote stays active, so the leader streams it
     # snapshots the transport fails (SnapshotStatus reject, clearPendingSnapshot)
     "C3_NOCQ_SNAP": (dict(C3, check_quorum=False, **SNAP), dict(ring=128), 400),
+    # a 64-entry window and 100-round partitions, fault-free
+    "C3_R64_ISO100": (dict(C3, iso_period=150, iso_len=100, **SNAP), dict(ring=64), 600),
     "MIXED_SNAP": (dict(MIXED, snapshot_entries=10, compaction_overhead=0),
                    dict(ring=128, rq_cap=64, maxm=24), 500),
     "C4_SNAP": (dict(C4, **SNAP), {}, 400),
@@ -111,3 +113,25 @@ def test_compaction_config_rules():
     with pytest.raises(InputError) as ei:
         eng.launch([0], [(1, 0, 0, 0)], [[]])
     assert ei.value.rc == RBE_E_INVALID
+
+
+@pytest.mark.parametrize("mode", ["staged", "aux"])
+def test_compaction_fast_step_variants(mode):
+    """The fast steps' staged-row and summary-word variants (as k_fast_both runs
+    them) with node snapshots taken inside the fast epilogue."""
+    kw, extra, rounds = CASES["C3_SNAP"]
+    eng = SoaCpu(trace=True, staged={"staged": 3, "aux": 4}[mode], **kw, **extra)
+    ref = O.Harness(**kw)
+    assert run_case(eng, ref, rounds) > 0
+    assert eng.faults()[0] == 0
+
+
+def test_compaction_keeps_fast_paths():
+    """Snapshots are taken inside the fast steps; only the step after one (the
+    compaction) and InstallSnapshot traffic take the full handler table."""
+    from parity_util import C2
+    kw = dict(C2, snapshot_entries=20, compaction_overhead=5)
+    eng = SoaCpu(trace=True, **kw)
+    ref = O.Harness(**kw)
+    run_case(eng, ref, 200)
+    assert eng.slow_total() < 0.25 * eng.counters()["steps"]
