@@ -20,6 +20,7 @@
 #include "rbe_host.h"
 #include "rbe_kernels.h"
 #include "rbe_snap.h"
+#include "rbe_wire_kernels.h"
 
 using namespace rbe;
 
@@ -327,6 +328,15 @@ struct rbe_engine {
   u64 out_dev_bytes = 0;
   u8* out_host = nullptr;
   u64 out_host_bytes = 0;
+  // rbe_wire_encode / rbe_wire_decode scratch
+  u8* wire_dev = nullptr;    // encoded frames (encode) / inbound bytes (decode)
+  u64 wire_dev_bytes = 0;
+  u8* wire_meta = nullptr;   // cells, batches, frame index
+  u64 wire_meta_bytes = 0;
+  u8* wire_rec = nullptr;    // decoded records
+  u64 wire_rec_bytes = 0;
+  u64 wire_totals[4] = {0, 0, 0, 0};
+  u64 wire_frames_off = 0;   // frame index inside wire_meta
 };
 
 
@@ -587,6 +597,9 @@ int rbe_destroy(rbe_engine* e) {
   if (e->in_dev) HIP_IGNORE(hipFree(e->in_dev));
   if (e->out_dev) HIP_IGNORE(hipFree(e->out_dev));
   if (e->out_host) HIP_IGNORE(hipHostFree(e->out_host));
+  if (e->wire_dev) HIP_IGNORE(hipFree(e->wire_dev));
+  if (e->wire_meta) HIP_IGNORE(hipFree(e->wire_meta));
+  if (e->wire_rec) HIP_IGNORE(hipFree(e->wire_rec));
   if (e->stream) HIP_IGNORE(hipStreamDestroy(e->stream));
   delete e;
   return RBE_OK;
@@ -1623,3 +1636,210 @@ int rbe_fault_summary(rbe_engine* e, uint64_t* n_faulty, uint32_t* fault_or) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- wire format
+int rbe_wire_encode(rbe_engine* e, const rbe_wire_config* wc, uint64_t totals[4]) {
+  if (!e || !wc || !totals) return RBE_E_INVALID;
+  if (e->round == 0) return RBE_E_STATE;
+  const Params& C = e->C;
+  if (C.n < 2) return RBE_E_INVALID;  // no peer to send to
+  HIP_OK(hipSetDevice(e->device));
+  WireArgs A;
+  memset(&A, 0, sizeof(A));
+  A.deployment_id = wc->deployment_id;
+  A.bin_ver = wc->bin_ver;
+  const u64 gpb = wc->groups_per_batch ? wc->groups_per_batch : C.n_groups;
+  if (gpb > 0xFFFFFFFFull) return RBE_E_INVALID;
+  A.gpb = (u32)gpb;
+  A.nchunks = (u32)((C.n_groups + gpb - 1) / gpb);
+  A.npairs = C.n * (C.n - 1);
+  A.round = e->round;
+  for (u32 k = 0; k < C.n; k++) {
+    const char* s = wc->source_address[k];
+    const size_t l = s ? strlen(s) : 0;
+    if (l >= sizeof(A.addr[k])) return RBE_E_INVALID;
+    A.alen[k] = (u32)l;
+    if (l) memcpy(A.addr[k], s, l);
+  }
+  const u64 ncell = (u64)A.npairs * C.n_groups, nbatch = (u64)A.npairs * A.nchunks;
+  if (nbatch > 0xFFFFFFFFull) return RBE_E_INVALID;
+  auto al = [](u64 x) { return (x + 255) & ~255ull; };
+  const u64 o_msgs = al(ncell * 4), o_off = o_msgs + al(ncell * 4), o_pay = o_off + al(ncell * 4);
+  const u64 o_bm = o_pay + al(nbatch * 8), o_bi = o_bm + al(nbatch * 4), o_fo = o_bi + al(nbatch * 4);
+  const u64 o_fr = o_fo + al(nbatch * 8), o_tot = o_fr + al(nbatch * sizeof(WireFrame));
+  int rc = grow(&e->wire_meta, &e->wire_meta_bytes, o_tot + 64, false);
+  if (rc) return rc;
+  u8* m = e->wire_meta;
+  WireBufs B{(u32*)m, (u32*)(m + o_msgs), (u32*)(m + o_off), (u64*)(m + o_pay), (u32*)(m + o_bm),
+             (u32*)(m + o_bi), (u64*)(m + o_fo), (WireFrame*)(m + o_fr), (u64*)(m + o_tot)};
+  e->wire_frames_off = o_fr;
+  const unsigned gc = (unsigned)((ncell + 255) / 256);
+  rc = dispatch_n(C.n, [&](auto NN) {
+    constexpr int N = decltype(NN)::value;
+    hipLaunchKernelGGL((k_wire_size<N>), dim3(gc), dim3(256), 0, e->stream, e->P, C, A, B);
+    return RBE_OK;
+  });
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_wire_batch, dim3((unsigned)nbatch), dim3(256), 0, e->stream, C, A, B);
+  hipLaunchKernelGGL(k_wire_frames, dim3(1), dim3(256), 0, e->stream, C, A, B, (u32)nbatch);
+  HIP_OK(hipGetLastError());
+  u64 tot[4];
+  HIP_OK(hipMemcpyAsync(tot, B.totals, sizeof(tot), hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  rc = grow(&e->wire_dev, &e->wire_dev_bytes, tot[0] + 64, false);
+  if (rc) return rc;
+  if (tot[1]) {
+    rc = dispatch_n(C.n, [&](auto NN) {
+      constexpr int N = decltype(NN)::value;
+      hipLaunchKernelGGL((k_wire_write<N>), dim3(gc), dim3(256), 0, e->stream, e->P, C, A, B,
+                         (const u8*)e->heap, e->wire_dev);
+      return RBE_OK;
+    });
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_wire_trailers, dim3((unsigned)((nbatch + 255) / 256)), dim3(256), 0,
+                       e->stream, C, A, B, (u32)nbatch, e->wire_dev);
+    hipLaunchKernelGGL(k_wire_crc, dim3((unsigned)tot[1]), dim3(256), 0, e->stream, B,
+                       e->wire_dev);
+    HIP_OK(hipGetLastError());
+  }
+  HIP_OK(hipStreamSynchronize(e->stream));
+  for (int i = 0; i < 4; i++) totals[i] = e->wire_totals[i] = tot[i];
+  return RBE_OK;
+}
+
+int rbe_wire_fetch(rbe_engine* e, void* out, uint64_t cap, rbe_wire_frame* frames,
+                   uint32_t frames_cap) {
+  if (!e) return RBE_E_INVALID;
+  if (!e->wire_meta) return RBE_E_STATE;
+  HIP_OK(hipSetDevice(e->device));
+  const u64 bytes = e->wire_totals[0], nf = e->wire_totals[1];
+  if ((out && cap < bytes) || (frames && frames_cap < nf)) return RBE_E_NOMEM;
+  static_assert(sizeof(WireFrame) == sizeof(rbe_wire_frame), "frame index layout");
+  if (out && bytes)
+    HIP_OK(hipMemcpyAsync(out, e->wire_dev, bytes, hipMemcpyDeviceToHost, e->stream));
+  if (frames && nf)
+    HIP_OK(hipMemcpyAsync(frames, e->wire_meta + e->wire_frames_off, nf * sizeof(WireFrame),
+                          hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return RBE_OK;
+}
+
+int rbe_wire_decode(rbe_engine* e, const void* data, uint64_t bytes, rbe_message* msgs,
+                    uint32_t cap, uint32_t* n_msgs, rbe_entry* ents, uint32_t ent_cap,
+                    uint32_t* n_ents, uint8_t* cmd, uint64_t cmd_cap, uint64_t* cmd_bytes) {
+  if (!e || (bytes && !data) || !n_msgs || !n_ents || !cmd_bytes) return RBE_E_INVALID;
+  *n_msgs = *n_ents = 0;
+  *cmd_bytes = 0;
+  // the frame boundaries: magic + size of each header (the receiver's reads)
+  const u8* d = (const u8*)data;
+  std::vector<WireIn> fr;
+  for (u64 i = 0; i < bytes;) {
+    if (bytes - i < kWireHeader || d[i] != 0xAE || d[i + 1] != 0x7D) return RBE_E_CORRUPT;
+    u64 size = 0;
+    for (int b = 0; b < 8; b++) size = (size << 8) | d[i + 4 + b];
+    if (size == 0 || size > bytes - i - kWireHeader) return RBE_E_CORRUPT;
+    WireIn w;
+    memset(&w, 0, sizeof(w));
+    w.offset = i + kWireHeader;
+    w.size = size;
+    fr.push_back(w);
+    i += kWireHeader + size;
+  }
+  if (fr.empty()) return RBE_OK;
+  HIP_OK(hipSetDevice(e->device));
+  const u64 nf = fr.size();
+  auto al = [](u64 x) { return (x + 255) & ~255ull; };
+  int rc = grow(&e->wire_dev, &e->wire_dev_bytes, al(bytes) + al(nf * sizeof(WireIn)), false);
+  if (rc) return rc;
+  WireIn* dfr = (WireIn*)(e->wire_dev + al(bytes));
+  HIP_OK(hipMemcpyAsync(e->wire_dev, data, bytes, hipMemcpyHostToDevice, e->stream));
+  HIP_OK(hipMemcpyAsync(dfr, fr.data(), nf * sizeof(WireIn), hipMemcpyHostToDevice, e->stream));
+  const unsigned gf = (unsigned)((nf + 63) / 64);
+  hipLaunchKernelGGL(k_wire_verify, dim3((unsigned)nf), dim3(256), 0, e->stream, e->wire_dev, dfr);
+  hipLaunchKernelGGL(k_wire_bounds, dim3(gf), dim3(64), 0, e->stream, e->wire_dev, dfr, (u32)nf,
+                     0, nullptr);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(fr.data(), dfr, nf * sizeof(WireIn), hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  u64 tm = 0;
+  for (auto& w : fr) {
+    if (w.status) return RBE_E_CORRUPT;
+    w.msg0 = tm;
+    tm += w.n_msgs;
+  }
+  *n_msgs = (u32)(tm < 0xFFFFFFFFull ? tm : 0xFFFFFFFFull);
+  if (tm > 0xFFFFFFFFull) return RBE_E_NOMEM;
+  // per message: position, entry and Cmd counts (scanned), error flag, scan tops
+  const u64 nbk = (tm + 255) / 256;
+  const u64 o_ec = al(tm * sizeof(WireMsgPos)), o_cc = o_ec + al(tm * 8), o_t1 = o_cc + al(tm * 8);
+  const u64 o_t2 = o_t1 + al((nbk + 1) * 8), o_err = o_t2 + al((nbk + 1) * 8);
+  const u64 o_rec = o_err + 256;
+  rc = grow(&e->wire_rec, &e->wire_rec_bytes, o_rec, false);
+  if (rc) return rc;
+  u8* w = e->wire_rec;
+  WireMsgPos* pos = (WireMsgPos*)w;
+  u64 *ec = (u64*)(w + o_ec), *cc = (u64*)(w + o_cc), *t1 = (u64*)(w + o_t1), *t2 = (u64*)(w + o_t2);
+  u32* err = (u32*)(w + o_err);
+  HIP_OK(hipMemcpyAsync(dfr, fr.data(), nf * sizeof(WireIn), hipMemcpyHostToDevice, e->stream));
+  HIP_OK(hipMemsetAsync(err, 0, 4, e->stream));
+  hipLaunchKernelGGL(k_wire_bounds, dim3(gf), dim3(64), 0, e->stream, e->wire_dev, dfr, (u32)nf,
+                     1, pos);
+  const unsigned gm = (unsigned)nbk;
+  if (tm) {
+    hipLaunchKernelGGL(k_wire_parse, dim3(gm), dim3(256), 0, e->stream, e->wire_dev, pos, tm, 0,
+                       ec, cc, nullptr, nullptr, nullptr, err);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(gm), dim3(256), 0, e->stream, ec, tm, t1);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(gm), dim3(256), 0, e->stream, cc, tm, t2);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, e->stream, t1, (u32)nbk);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, e->stream, t2, (u32)nbk);
+    hipLaunchKernelGGL(k_scan_add, dim3(gm), dim3(256), 0, e->stream, ec, tm, t1);
+    hipLaunchKernelGGL(k_scan_add, dim3(gm), dim3(256), 0, e->stream, cc, tm, t2);
+  }
+  HIP_OK(hipGetLastError());
+  u64 te = 0, tc = 0;
+  u32 herr = 0;
+  if (tm) {
+    HIP_OK(hipMemcpyAsync(&te, t1 + nbk, 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipMemcpyAsync(&tc, t2 + nbk, 8, hipMemcpyDeviceToHost, e->stream));
+  }
+  HIP_OK(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  if (herr) return RBE_E_CORRUPT;
+  *n_ents = (u32)(te < 0xFFFFFFFFull ? te : 0xFFFFFFFFull);
+  *cmd_bytes = tc;
+  if (te > 0xFFFFFFFFull) return RBE_E_NOMEM;
+  if (tm > cap || te > ent_cap || tc > cmd_cap || (tm && !msgs) || (te && !ents) || (tc && !cmd))
+    return RBE_E_NOMEM;
+  const u64 o_m = o_rec, o_e = o_m + al(tm * sizeof(rbe_message)),
+            o_c = o_e + al(te * sizeof(rbe_entry));
+  {
+    // keep the scratch above while growing (a fresh buffer only when short)
+    const u64 need = o_c + al(tc) + 256;
+    if (need > e->wire_rec_bytes) {
+      u8* nb = nullptr;
+      HIP_OK(hipMalloc((void**)&nb, need + need / 2));
+      HIP_OK(hipMemcpyAsync(nb, e->wire_rec, o_rec, hipMemcpyDeviceToDevice, e->stream));
+      HIP_OK(hipStreamSynchronize(e->stream));
+      HIP_OK(hipFree(e->wire_rec));
+      e->wire_rec = nb;
+      e->wire_rec_bytes = need + need / 2;
+    }
+  }
+  w = e->wire_rec;
+  pos = (WireMsgPos*)w;
+  ec = (u64*)(w + o_ec);
+  cc = (u64*)(w + o_cc);
+  err = (u32*)(w + o_err);
+  rbe_message* dm = (rbe_message*)(w + o_m);
+  rbe_entry* de = (rbe_entry*)(w + o_e);
+  u8* dc = w + o_c;
+  if (tm)
+    hipLaunchKernelGGL(k_wire_parse, dim3(gm), dim3(256), 0, e->stream, e->wire_dev, pos, tm, 1,
+                       ec, cc, dm, de, dc, err);
+  HIP_OK(hipGetLastError());
+  if (tm) HIP_OK(hipMemcpyAsync(msgs, dm, tm * sizeof(rbe_message), hipMemcpyDeviceToHost, e->stream));
+  if (te) HIP_OK(hipMemcpyAsync(ents, de, te * sizeof(rbe_entry), hipMemcpyDeviceToHost, e->stream));
+  if (tc) HIP_OK(hipMemcpyAsync(cmd, dc, tc, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return RBE_OK;
+}

@@ -1,0 +1,270 @@
+// rbe_wire.h — the transport's wire format over the engine's outbox planes,
+// shared by the device codec (rbe_wire_kernels.h) and the test-only host build.
+//
+// What a dragonboat node puts on a TCP connection for Raft traffic
+// (internal/transport/tcp.go:149-185 writeMessage): the 2-byte magic 0xAE7D,
+// an 18-byte requestHeader (method 100, payload size, header crc32, payload
+// crc32; big endian; tcp.go:80-91), then a marshaled raftpb.MessageBatch
+// (raft.pb.go:2415-2443): its Requests as protobuf Messages (2230-2294), each
+// embedding a Snapshot (2140-2217) and its log entries in colfer form
+// (raftpb/raft_optimized.go:161-295), then DeploymentId, SourceAddress, BinVer.
+//
+// The engine's frame is one MessageBatch per (sender slot k, destination slot
+// d, range of `groups_per_batch` groups): every message the replicas k of
+// those groups sent to their replicas d in the last round, group by group, each
+// replica's in transport order (Quiesce notice, Replicate, the rest; the order
+// rbe_get_outbox reports).  InstallSnapshot messages never travel in a
+// MessageBatch (transport.go:400-403: they go through the snapshot chunk
+// stream), so they are counted and left out.  The engine's entries carry
+// Index, Term, Type and Cmd; Key, ClientID, SeriesID and RespondedTo are 0.
+//
+// One function, wire_cell, both sizes and writes a (group, k, d) cell, so the
+// size pass and the write pass cannot disagree.
+#pragma once
+
+#include "rbe_step.h"
+
+namespace rbe {
+
+static constexpr u32 kWireHeader = 20;  // magic + requestHeader
+static constexpr u32 kWireMethod = 100;  // tcp.go raftType
+static constexpr u32 kWireCrcPoly = 0xEDB88320u;
+
+RBE_HD u32 wsov(u64 x) {  // sovRaft (raft.pb.go:2879-2887)
+  u32 n = 1;
+  while (x >= 0x80) {
+    x >>= 7;
+    n++;
+  }
+  return n;
+}
+RBE_HD u32 wput(u8* o, u64 x) {  // encodeVarintRaft (raft.pb.go:2559-2567)
+  u32 i = 0;
+  while (x >= 0x80) {
+    o[i++] = (u8)(x | 0x80);
+    x >>= 7;
+  }
+  o[i++] = (u8)x;
+  return i;
+}
+// colfer u64 field (raft_optimized.go:164-178): absent when 0, 9 bytes from 2^49
+RBE_HD u32 colfer_u64_size(u64 x) { return x >= (1ull << 49) ? 9u : (x ? 1u + wsov(x) : 0u); }
+RBE_HD u32 colfer_u64_put(u8* o, u32 field, u64 x) {
+  if (x >= (1ull << 49)) {
+    o[0] = (u8)(field | 0x80);
+    for (u32 b = 0; b < 8; b++) o[1 + b] = (u8)(x >> (56 - 8 * b));
+    return 9;
+  }
+  if (!x) return 0;
+  o[0] = (u8)field;
+  return 1 + wput(o + 1, x);
+}
+// Entry.Size (raft_optimized.go:79-153)
+RBE_HD u32 wire_entry_size(u64 index, u64 term, u32 type, u32 len) {
+  u32 l = 1 + colfer_u64_size(term) + colfer_u64_size(index);
+  if (type) l += 1 + wsov(type);
+  if (len) l += 1 + wsov(len) + len;
+  return l;
+}
+// Entry.marshalTo (raft_optimized.go:161-295); cmd bytes from the inline body
+// (len <= 16: lo/hi little endian) or the payload heap (absolute position hi)
+RBE_HD u32 wire_entry_put(u8* o, u64 index, u64 term, u32 type, u32 len, u64 lo, u64 hi,
+                          const u8* heap, u64 heap_cap) {
+  u32 i = colfer_u64_put(o, 0, term);
+  i += colfer_u64_put(o + i, 1, index);
+  if (type) {
+    o[i++] = 2;
+    i += wput(o + i, type);
+  }
+  if (len) {
+    o[i++] = 7;
+    i += wput(o + i, len);
+    if (len <= 16) {
+      for (u32 b = 0; b < len; b++) o[i + b] = (u8)((b < 8 ? lo : hi) >> (8 * (b & 7)));
+    } else {
+      const u8* src = heap + (heap_cap ? hi % heap_cap : 0);
+      for (u32 b = 0; b < len; b++) o[i + b] = src[b];
+    }
+    i += len;
+  }
+  o[i++] = 0x7F;
+  return i;
+}
+
+// The Snapshot embedded in every MessageBatch message (no InstallSnapshot
+// travels there): Filepath "", FileSize 0, Index 0, Term 0, Membership
+// {ConfigChangeId 0}, Dummy, ClusterId, Type, Imported, OnDiskIndex, Witness.
+static constexpr u32 kWireEmptySnap = 24;
+RBE_HD u32 wire_empty_snap_put(u8* o) {
+  const u8 b[kWireEmptySnap] = {0x12, 0, 0x18, 0, 0x20, 0, 0x28, 0, 0x32, 2, 0x08, 0,
+                                0x48, 0, 0x50, 0, 0x58, 0, 0x60, 0, 0x68, 0, 0x70, 0};
+  for (u32 i = 0; i < kWireEmptySnap; i++) o[i] = b[i];
+  return kWireEmptySnap;
+}
+
+// Message.MarshalTo (raft.pb.go:2230-2294) of one outbox message, as a
+// MessageBatch request (tag 0x0a + length); `out` null = size only.
+RBE_HD u32 wire_message(const Msg& m, u32 type, u32 to, u32 from, u64 cid, const Ent* ents,
+                        const u8* heap, u64 heap_cap, u8* out) {
+  const u32 ne = type == M_Replicate ? m.n_ent : 0u;
+  u32 body = 1 + wsov(type) + 1 + wsov(to) + 1 + wsov(from) + 1 + wsov(cid) + 1 + wsov(m.term) +
+             1 + wsov(m.log_term) + 1 + wsov(m.log_index) + 1 + wsov(m.commit) + 2 + 1 +
+             wsov(m.hint) + 1 + 1 + kWireEmptySnap + 1 + wsov(m.hint_high);
+  for (u32 j = 0; j < ne; j++) {
+    const Ent& x = ents[j];
+    const u32 es = wire_entry_size(m.log_index + 1 + j, x.term, x.type, x.len);
+    body += 1 + wsov(es) + es;
+  }
+  const u32 total = 1 + wsov(body) + body;
+  if (!out) return total;
+  u32 i = 0;
+  out[i++] = 0x0A;
+  i += wput(out + i, body);
+  out[i++] = 0x08;
+  i += wput(out + i, type);
+  out[i++] = 0x10;
+  i += wput(out + i, to);
+  out[i++] = 0x18;
+  i += wput(out + i, from);
+  out[i++] = 0x20;
+  i += wput(out + i, cid);
+  out[i++] = 0x28;
+  i += wput(out + i, m.term);
+  out[i++] = 0x30;
+  i += wput(out + i, m.log_term);
+  out[i++] = 0x38;
+  i += wput(out + i, m.log_index);
+  out[i++] = 0x40;
+  i += wput(out + i, m.commit);
+  out[i++] = 0x48;
+  out[i++] = m.reject ? 1 : 0;
+  out[i++] = 0x50;
+  i += wput(out + i, m.hint);
+  for (u32 j = 0; j < ne; j++) {
+    const Ent& x = ents[j];
+    const u64 idx = m.log_index + 1 + j;
+    out[i++] = 0x5A;
+    i += wput(out + i, wire_entry_size(idx, x.term, x.type, x.len));
+    i += wire_entry_put(out + i, idx, x.term, x.type, x.len, x.lo, x.hi, heap, heap_cap);
+  }
+  out[i++] = 0x62;
+  out[i++] = (u8)kWireEmptySnap;
+  i += wire_empty_snap_put(out + i);
+  out[i++] = 0x68;
+  i += wput(out + i, m.hint_high);
+  return i;
+}
+
+// The requests replica (g, k) sent replica (g, d) in the round that produced
+// header `row` (written as round `round` - 1, parity (round - 1) & 1): their
+// bytes (written at `out` unless null); *n_msgs / *n_is count the messages
+// encoded and the InstallSnapshots left out.
+template <int N>
+RBE_HD u32 wire_cell(const Planes& P, const Params& C, const u8* heap, u64 g, u32 k, u32 d,
+                     u32 round, u8* out, u32* n_msgs, u32* n_is) {
+  const u32 par = (round - 1u) & 1u;
+  const u64 r = g * N + k;
+  const u64 cid = C.cid_base + g * C.cid_stride;
+  const u32 pc = row_word(P.cnt[par][r], d, round);
+  const u32 na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
+  u32 bytes = 0, nm = 0, ni = 0;
+  if (pc & 0x8000u) {  // sendEnterQuiesceMessages (node.go:873-886)
+    Msg q;
+    q.type = (u8)M_Quiesce;
+    q.from = q.to = q.reject = 0;
+    q.n_ent = 0;
+    q.pad0 = 0;
+    q.ent_off = q.pad1 = 0;
+    q.term = q.log_term = q.log_index = q.commit = q.hint = q.hint_high = 0;
+    bytes += wire_message(q, M_Quiesce, d + 1, k + 1, cid, nullptr, heap, C.heap_bytes,
+                          out ? out + bytes : nullptr);
+    nm++;
+  }
+  const Msg* lst = &P.msgs[par][((g * N + k) * N + d) * (u64)C.maxm];
+  const Ent* arena = &P.arena[par][r * C.ecap];
+  for (u32 i = 0; i < na + nb; i++) {
+    const Msg m = i < na ? lst[i] : lst[C.maxm - 1u - (i - na)];
+    if (m.type == M_InstallSnapshot) {
+      ni++;
+      continue;
+    }
+    bytes += wire_message(m, m.type, d + 1, k + 1, cid, arena + m.ent_off, heap, C.heap_bytes,
+                          out ? out + bytes : nullptr);
+    nm++;
+  }
+  *n_msgs = nm;
+  *n_is = ni;
+  return bytes;
+}
+
+// MessageBatch trailer (raft.pb.go:2432-2441): DeploymentId, SourceAddress, BinVer
+RBE_HD u32 wire_trailer(u64 deployment_id, const u8* addr, u32 addr_len, u32 bin_ver, u8* out) {
+  const u32 n = 1 + wsov(deployment_id) + 1 + wsov(addr_len) + addr_len + 1 + wsov(bin_ver);
+  if (!out) return n;
+  u32 i = 0;
+  out[i++] = 0x10;
+  i += wput(out + i, deployment_id);
+  out[i++] = 0x1A;
+  i += wput(out + i, addr_len);
+  for (u32 b = 0; b < addr_len; b++) out[i++] = addr[b];
+  out[i++] = 0x20;
+  i += wput(out + i, bin_ver);
+  return i;
+}
+
+// ---------------------------------------------------------------- crc32 (IEEE)
+// crc32.ChecksumIEEE; segments are combined with zlib's crc32_combine
+// (multmodp / x2nmodp over the reflected polynomial).
+RBE_HD u32 crc_table_entry(u32 i) {
+  u32 c = i;
+  for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ kWireCrcPoly : c >> 1;
+  return c;
+}
+RBE_HD u32 crc32_update(u32 crc, const u8* p, u64 n, const u32* table) {
+  u32 c = ~crc;
+  for (u64 i = 0; i < n; i++) c = table[(c ^ p[i]) & 0xFFu] ^ (c >> 8);
+  return ~c;
+}
+RBE_HD u32 crc_multmodp(u32 a, u32 b) {
+  u32 m = 1u << 31, p = 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1u)) == 0) break;
+    }
+    m >>= 1;
+    b = (b & 1u) ? (b >> 1) ^ kWireCrcPoly : b >> 1;
+  }
+  return p;
+}
+// x2n[k] = x^(2^k) mod P
+RBE_HD void crc_x2n_table(u32* x2n) {
+  x2n[0] = 1u << 30;
+  for (int k = 1; k < 32; k++) x2n[k] = crc_multmodp(x2n[k - 1], x2n[k - 1]);
+}
+RBE_HD u32 crc32_combine(u32 crc1, u32 crc2, u64 len2, const u32* x2n) {
+  u32 p = 1u << 31;  // x^(8 len2) mod P
+  u32 k = 3;
+  while (len2) {
+    if (len2 & 1u) p = crc_multmodp(x2n[k & 31], p);
+    len2 >>= 1;
+    k++;
+  }
+  return crc_multmodp(p, crc1) ^ crc2;
+}
+// requestHeader.encode (tcp.go:80-91) after the magic, for a payload of
+// `size` bytes with crc32 `pcrc`
+RBE_HD void wire_header_put(u8* o, u64 size, u32 pcrc, const u32* table) {
+  o[0] = 0xAE;
+  o[1] = 0x7D;
+  u8* h = o + 2;
+  h[0] = (u8)(kWireMethod >> 8);
+  h[1] = (u8)kWireMethod;
+  for (u32 b = 0; b < 8; b++) h[2 + b] = (u8)(size >> (56 - 8 * b));
+  for (u32 b = 0; b < 4; b++) h[10 + b] = 0;
+  for (u32 b = 0; b < 4; b++) h[14 + b] = (u8)(pcrc >> (24 - 8 * b));
+  const u32 hc = crc32_update(0, h, 18, table);
+  for (u32 b = 0; b < 4; b++) h[10 + b] = (u8)(hc >> (24 - 8 * b));
+}
+
+}  // namespace rbe

@@ -1,0 +1,527 @@
+// rbe_wire_kernels.h — device codec of the transport wire format (rbe_wire.h):
+// encode the last round's outbox into framed MessageBatches, decode framed
+// MessageBatches into raftpb-form records.  Included by rbe_engine.hip only.
+//
+// Encode is four passes over HBM, all byte/integer work (no MFMA):
+//   k_wire_size   one lane per (group, k, d) cell: bytes + messages of the cell
+//   k_wire_batch  one block per batch: exclusive scan of its cells' bytes
+//   k_wire_frames one block: frame offsets, the compacted frame index
+//   k_wire_write  one lane per cell: the cell's requests at their offset;
+//                 one lane per batch: the trailer
+//   k_wire_crc    one block per frame: payload crc32 by segments combined
+//                 with crc32_combine, then the header
+// Decode: k_wire_verify (block per frame: both crc32s), k_wire_bounds (lane
+// per frame: where its requests are), k_wire_parse (lane per message: count,
+// device scan, then the records).
+#pragma once
+
+#include "rbe_wire.h"
+
+namespace rbe {
+
+struct WireArgs {
+  u64 deployment_id;
+  u32 bin_ver, gpb;      // groups per batch
+  u32 nchunks, npairs;   // batches = npairs * nchunks
+  u32 round;
+  u32 alen[6];
+  u8 addr[6][48];        // source address of each slot
+};
+
+struct WireFrame {  // mirrors rbe_wire_frame (include/rbe.h)
+  u64 offset, bytes, first_group;
+  u32 src, dst, n_messages, n_groups;
+};
+
+struct WireBufs {
+  u32* cell_bytes;  // [npairs * n_groups]
+  u32* cell_msgs;
+  u32* cell_off;    // offset in its batch's payload
+  u64* batch_pay;   // [nbatch] payload bytes (0 = no message)
+  u32* batch_msgs;
+  u32* batch_is;
+  u64* frame_off;   // [nbatch]
+  WireFrame* frames;  // compacted, non-empty batches
+  u64* totals;      // [0] bytes, [1] frames, [2] messages, [3] InstallSnapshots left out
+};
+
+RBE_HD void wire_pair(u32 N, u32 p, u32* k, u32* d) {
+  *k = p / (N - 1u);
+  const u32 dd = p % (N - 1u);
+  *d = dd >= *k ? dd + 1u : dd;
+}
+
+template <int N>
+__global__ __launch_bounds__(256) void k_wire_size(Planes P, Params C, WireArgs A, WireBufs B) {
+  const u64 c = (u64)blockIdx.x * 256 + threadIdx.x;
+  if (c >= (u64)A.npairs * C.n_groups) return;
+  const u32 p = (u32)(c / C.n_groups);
+  const u64 g = c % C.n_groups;
+  u32 k, d;
+  wire_pair(N, p, &k, &d);
+  u32 nm = 0, ni = 0;
+  const u32 b = wire_cell<N>(P, C, nullptr, g, k, d, A.round, nullptr, &nm, &ni);
+  B.cell_bytes[c] = b;
+  B.cell_msgs[c] = nm | (ni << 16);
+}
+
+// block-wide exclusive scan of one value per thread; returns this thread's
+// prefix and the block total in *total
+__device__ __forceinline__ u64 block_scan_u64(u64 v, u64* total, u64* s_tmp) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  u64 x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const u64 y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_tmp[w] = x;
+  __syncthreads();
+  u64 base = 0, t = 0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); i++) {
+    if (i < w) base += s_tmp[i];
+    t += s_tmp[i];
+  }
+  __syncthreads();
+  *total = t;
+  return base + x - v;
+}
+
+__global__ __launch_bounds__(256) void k_wire_batch(Params C, WireArgs A, WireBufs B) {
+  __shared__ u64 s_tmp[4];
+  const u32 bt = blockIdx.x;
+  const u32 p = bt / A.nchunks, ch = bt % A.nchunks;
+  const u64 g0 = (u64)ch * A.gpb;
+  const u64 g1 = g0 + A.gpb < C.n_groups ? g0 + A.gpb : C.n_groups;
+  const u64 base = (u64)p * C.n_groups;
+  u64 carry = 0, msgs = 0, is = 0;
+  for (u64 g = g0; g < g1; g += 256) {
+    const u64 gi = g + threadIdx.x;
+    u64 v = 0;
+    u32 mm = 0;
+    if (gi < g1) {
+      v = B.cell_bytes[base + gi];
+      mm = B.cell_msgs[base + gi];
+    }
+    u64 tot = 0;
+    const u64 pre = block_scan_u64(v, &tot, s_tmp);
+    if (gi < g1) B.cell_off[base + gi] = (u32)(carry + pre);
+    carry += tot;
+    u64 t2 = 0;
+    block_scan_u64((u64)(mm & 0xFFFFu) | ((u64)(mm >> 16) << 32), &t2, s_tmp);
+    msgs += t2 & 0xFFFFFFFFull;
+    is += t2 >> 32;
+  }
+  if (threadIdx.x == 0) {
+    u32 k, d;
+    wire_pair(C.n, p, &k, &d);
+    B.batch_pay[bt] = msgs ? carry + wire_trailer(A.deployment_id, A.addr[k], A.alen[k], A.bin_ver,
+                                                  nullptr)
+                           : 0;
+    B.batch_msgs[bt] = (u32)msgs;
+    B.batch_is[bt] = (u32)is;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_wire_frames(Params C, WireArgs A, WireBufs B,
+                                                     u32 nbatch) {
+  __shared__ u64 s_tmp[4];
+  u64 carry = 0, fcarry = 0, msgs = 0, is = 0;
+  for (u32 b0 = 0; b0 < nbatch; b0 += 256) {
+    const u32 b = b0 + threadIdx.x;
+    u64 fb = 0, ne = 0;
+    if (b < nbatch && B.batch_msgs[b]) {
+      fb = kWireHeader + B.batch_pay[b];
+      ne = 1;
+    }
+    u64 tot = 0, ftot = 0;
+    const u64 off = block_scan_u64(fb, &tot, s_tmp);
+    const u64 fi = block_scan_u64(ne, &ftot, s_tmp);
+    if (b < nbatch) {
+      B.frame_off[b] = carry + off;
+      if (ne) {
+        const u32 p = b / A.nchunks, ch = b % A.nchunks;
+        u32 k, d;
+        wire_pair(C.n, p, &k, &d);
+        WireFrame f;
+        f.offset = carry + off;
+        f.bytes = fb;
+        f.first_group = (u64)ch * A.gpb;
+        const u64 g1 = f.first_group + A.gpb < C.n_groups ? f.first_group + A.gpb : C.n_groups;
+        f.src = k;
+        f.dst = d;
+        f.n_messages = B.batch_msgs[b];
+        f.n_groups = (u32)(g1 - f.first_group);
+        B.frames[fcarry + fi] = f;
+      }
+    }
+    u64 t3 = 0;
+    block_scan_u64(b < nbatch ? ((u64)B.batch_msgs[b] | ((u64)B.batch_is[b] << 32)) : 0, &t3,
+                   s_tmp);
+    msgs += t3 & 0xFFFFFFFFull;
+    is += t3 >> 32;
+    carry += tot;
+    fcarry += ftot;
+  }
+  if (threadIdx.x == 0) {
+    B.totals[0] = carry;
+    B.totals[1] = fcarry;
+    B.totals[2] = msgs;
+    B.totals[3] = is;
+  }
+}
+
+template <int N>
+__global__ __launch_bounds__(256) void k_wire_write(Planes P, Params C, WireArgs A, WireBufs B,
+                                                    const u8* heap, u8* out) {
+  const u64 c = (u64)blockIdx.x * 256 + threadIdx.x;
+  if (c >= (u64)A.npairs * C.n_groups) return;
+  if ((B.cell_msgs[c] & 0xFFFFu) == 0) return;
+  const u32 p = (u32)(c / C.n_groups);
+  const u64 g = c % C.n_groups;
+  const u32 bt = p * A.nchunks + (u32)(g / A.gpb);
+  u32 k, d;
+  wire_pair(N, p, &k, &d);
+  u32 nm = 0, ni = 0;
+  wire_cell<N>(P, C, heap, g, k, d, A.round, out + B.frame_off[bt] + kWireHeader + B.cell_off[c],
+               &nm, &ni);
+}
+
+__global__ __launch_bounds__(256) void k_wire_trailers(Params C, WireArgs A, WireBufs B,
+                                                       u32 nbatch, u8* out) {
+  const u32 b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= nbatch || !B.batch_msgs[b]) return;
+  u32 k, d;
+  wire_pair(C.n, b / A.nchunks, &k, &d);
+  const u32 tl = wire_trailer(A.deployment_id, A.addr[k], A.alen[k], A.bin_ver, nullptr);
+  wire_trailer(A.deployment_id, A.addr[k], A.alen[k], A.bin_ver,
+               out + B.frame_off[b] + kWireHeader + B.batch_pay[b] - tl);
+}
+
+// crc32 of [p, p + n) by this block: one contiguous segment per thread, the
+// segments' crcs combined pairwise in LDS
+__device__ u32 block_crc32(const u8* p, u64 n, const u32* table, const u32* x2n, u32* s_crc) {
+  const u32 T = blockDim.x, t = threadIdx.x;
+  const u64 seg = (n + T - 1) / T;
+  const u64 lo = seg * t < n ? seg * t : n;
+  const u64 hi = lo + seg < n ? lo + seg : n;
+  s_crc[t] = crc32_update(0, p + lo, hi - lo, table);
+  __syncthreads();
+  // tree: combine (i, i + s) with the length of segment group i + s
+  for (u32 s = 1; s < T; s <<= 1) {
+    if ((t % (2 * s)) == 0 && t + s < T) {
+      const u64 l2lo = seg * (t + s) < n ? seg * (t + s) : n;
+      const u64 l2hi = seg * (t + 2 * s) < n ? seg * (t + 2 * s) : n;
+      s_crc[t] = crc32_combine(s_crc[t], s_crc[t + s], l2hi - l2lo, x2n);
+    }
+    __syncthreads();
+  }
+  return s_crc[0];
+}
+
+__global__ __launch_bounds__(256) void k_wire_crc(WireBufs B, u8* out) {
+  __shared__ u32 s_table[256], s_x2n[32], s_crc[256];
+  s_table[threadIdx.x] = crc_table_entry(threadIdx.x);
+  if (threadIdx.x == 0) crc_x2n_table(s_x2n);
+  __syncthreads();
+  const WireFrame f = B.frames[blockIdx.x];
+  u8* fp = out + f.offset;
+  const u64 n = f.bytes - kWireHeader;
+  const u32 c = block_crc32(fp + kWireHeader, n, s_table, s_x2n, s_crc);
+  if (threadIdx.x == 0) wire_header_put(fp, n, c, s_table);
+}
+
+// ---------------------------------------------------------------- decode
+struct WireIn {  // one inbound frame
+  u64 offset, size;  // payload offset in the device copy, payload bytes
+  u64 msg0, ent0, cmd0;  // first output record / entry / Cmd byte
+  u32 n_msgs, n_ents;
+  u64 cmd_bytes;
+  u32 status;  // 0 ok, 1 header crc, 2 payload crc, 3 malformed
+  u32 pad;
+};
+
+__global__ __launch_bounds__(256) void k_wire_verify(const u8* data, WireIn* fr) {
+  __shared__ u32 s_table[256], s_x2n[32], s_crc[256];
+  s_table[threadIdx.x] = crc_table_entry(threadIdx.x);
+  if (threadIdx.x == 0) crc_x2n_table(s_x2n);
+  __syncthreads();
+  WireIn f = fr[blockIdx.x];
+  const u32 c = block_crc32(data + f.offset, f.size, s_table, s_x2n, s_crc);
+  if (threadIdx.x == 0) {
+    const u8* h = data + f.offset - 18;
+    u8 hb[18];
+    for (int i = 0; i < 18; i++) hb[i] = h[i];
+    const u32 inc = ((u32)hb[10] << 24) | ((u32)hb[11] << 16) | ((u32)hb[12] << 8) | hb[13];
+    hb[10] = hb[11] = hb[12] = hb[13] = 0;
+    const u32 pc = ((u32)hb[14] << 24) | ((u32)hb[15] << 16) | ((u32)hb[16] << 8) | hb[17];
+    u32 st = 0;
+    if (crc32_update(0, hb, 18, s_table) != inc) st = 1;
+    else if (pc != c) st = 2;
+    fr[blockIdx.x].status = st;
+  }
+}
+
+// sequential reader over one frame's payload
+struct WireRd {
+  const u8* p;
+  u64 n, i;
+  bool bad;
+  RBE_HD u8 byte() {
+    if (i >= n) {
+      bad = true;
+      return 0;
+    }
+    return p[i++];
+  }
+  RBE_HD u64 varint() {  // protobuf varint (Message.Unmarshal)
+    u64 x = 0;
+    for (u32 s = 0; s < 64; s += 7) {
+      const u8 b = byte();
+      x |= (u64)(b & 0x7F) << s;
+      if (b < 0x80 || bad) return x;
+    }
+    bad = true;
+    return x;
+  }
+  RBE_HD void skip(u32 wt) {  // skipRaft
+    if (wt == 0) varint();
+    else if (wt == 1) i += 8;
+    else if (wt == 2) i += varint();
+    else if (wt == 5) i += 4;
+    else bad = true;
+    if (i > n) bad = true;
+  }
+};
+
+// Entry.unmarshal (raft_optimized.go:303-651) of [rd.i, end)
+RBE_HD void wire_entry_get(WireRd& rd, u64 end, rbe_entry* e, u8* cmd) {
+  u64 vals[7] = {0, 0, 0, 0, 0, 0, 0};
+  u8 h = rd.byte();
+  for (u32 f = 0; f < 7; f++) {
+    if (h == f) {
+      u64 x = 0;
+      if (f == 2) {
+        x = rd.varint();
+      } else {
+        for (u32 s = 0;; s += 7) {
+          const u8 b = rd.byte();
+          if (b < 0x80 || s == 56) {
+            x |= (u64)b << s;
+            break;
+          }
+          x |= (u64)(b & 0x7F) << s;
+        }
+      }
+      vals[f] = x;
+      h = rd.byte();
+    } else if (h == (f | 0x80)) {
+      u64 x = 0;
+      if (f == 2) {
+        x = (u64)(u32)(0u - (u32)rd.varint());
+      } else {
+        for (int b = 0; b < 8; b++) x = (x << 8) | rd.byte();
+      }
+      vals[f] = x;
+      h = rd.byte();
+    }
+  }
+  u32 len = 0;
+  if (h == 7) {
+    len = (u32)rd.varint();
+    if (rd.i + len > end) rd.bad = true;
+    for (u32 b = 0; b < len && !rd.bad; b++) {
+      const u8 x = rd.byte();
+      if (cmd) cmd[b] = x;
+      if (e && b < 16) e->cmd[b] = x;
+    }
+    h = rd.byte();
+  }
+  if (h != 0x7F || rd.i != end) rd.bad = true;
+  if (e) {
+    e->term = vals[0];
+    e->index = vals[1];
+    e->type = (u32)vals[2];
+    e->cmd_len = len;
+  }
+}
+
+// Message.Unmarshal (raft_optimized.go:654-979) of [rd.i, end); entries to
+// ents[0..] and their Cmds to cmd[cmd_at..]; returns entries, *cmd_at advanced
+RBE_HD u32 wire_message_get(WireRd& rd, u64 end, rbe_message* m, rbe_entry* ents, u8* cmd,
+                            u64* cmd_at) {
+  u64 f[14] = {0};
+  u32 ne = 0;
+  while (rd.i < end && !rd.bad) {
+    const u64 tag = rd.varint();
+    const u32 fn = (u32)(tag >> 3), wt = (u32)(tag & 7);
+    if (fn >= 1 && fn <= 13 && fn != 11 && fn != 12 && wt == 0) {
+      f[fn] = rd.varint();
+    } else if (fn == 11 && wt == 2) {
+      const u64 l = rd.varint();
+      const u64 e_end = rd.i + l;
+      if (e_end > end) {
+        rd.bad = true;
+        break;
+      }
+      // Cmd length first (the colfer walk below writes at cmd + *cmd_at)
+      rbe_entry tmp;
+      rbe_entry* e = ents ? &ents[ne] : &tmp;
+      for (int b = 0; b < 16; b++) e->cmd[b] = 0;
+      wire_entry_get(rd, e_end, e, cmd ? cmd + *cmd_at : nullptr);
+      *cmd_at += e->cmd_len;
+      ne++;
+    } else {
+      rd.skip(wt);  // the embedded Snapshot included: no InstallSnapshot here
+    }
+  }
+  if (rd.i != end) rd.bad = true;
+  if (m) {
+    m->type = (u32)f[1];
+    m->to = f[2];
+    m->from = f[3];
+    m->cluster_id = f[4];
+    m->term = f[5];
+    m->log_term = f[6];
+    m->log_index = f[7];
+    m->commit = f[8];
+    m->reject = f[9] != 0;
+    m->hint = f[10];
+    m->hint_high = f[13];
+    m->n_entries = ne;
+    m->reserved = 0;
+  }
+  return ne;
+}
+
+// Decode is parallel per message: one lane per frame finds the top-level
+// requests of its MessageBatch (MessageBatch.Unmarshal, raft_optimized.go:
+// 1051-1204: field 1 = a Message, 2-4 the trailer), reading 16-B windows;
+// then one lane per message parses it (Message.Unmarshal), first counting its
+// entries and Cmd bytes (scanned on the device for the output offsets), then
+// writing the records.
+struct WireWin {  // 16-B window reader over one frame's payload
+  const u8* p;
+  u64 n, i;
+  u64 wbase;
+  uint4 w;
+  bool bad;
+  RBE_HD u8 byte() {
+    if (i >= n) {
+      bad = true;
+      return 0;
+    }
+    const u64 a = (u64)(p + i);
+    const u64 base = a & ~15ull;
+    if (base != wbase) {
+      w = *(const uint4*)base;
+      wbase = base;
+    }
+    const u32 o = (u32)(a - base);
+    const u32 word = o < 4 ? w.x : (o < 8 ? w.y : (o < 12 ? w.z : w.w));
+    i++;
+    return (u8)(word >> (8 * (o & 3)));
+  }
+  RBE_HD u64 varint() {
+    u64 x = 0;
+    for (u32 s = 0; s < 64; s += 7) {
+      const u8 b = byte();
+      x |= (u64)(b & 0x7F) << s;
+      if (b < 0x80 || bad) return x;
+    }
+    bad = true;
+    return x;
+  }
+};
+
+struct WireMsgPos {
+  u64 at, len;  // Message body [at, at + len) in the device copy of the input
+};
+
+// pass 0: count the frame's requests; pass 1: record where each one is
+__global__ __launch_bounds__(64) void k_wire_bounds(const u8* data, WireIn* fr, u32 nf, int pass,
+                                                    WireMsgPos* pos) {
+  const u32 i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= nf) return;
+  const WireIn f = fr[i];
+  if (f.status) return;
+  WireWin rd{data + f.offset, f.size, 0, ~0ull, make_uint4(0, 0, 0, 0), false};
+  u32 nm = 0;
+  while (rd.i < rd.n && !rd.bad) {
+    const u64 tag = rd.varint();
+    const u32 fn = (u32)(tag >> 3), wt = (u32)(tag & 7);
+    if (wt == 2) {
+      const u64 l = rd.varint();
+      if (l > rd.n - rd.i) {
+        rd.bad = true;
+        break;
+      }
+      if (fn == 1) {
+        if (pass) pos[f.msg0 + nm] = WireMsgPos{f.offset + rd.i, l};
+        nm++;
+      }
+      rd.i += l;
+    } else if (wt == 0) {
+      rd.varint();
+    } else if (wt == 1 || wt == 5) {
+      rd.i += wt == 1 ? 8 : 4;
+      if (rd.i > rd.n) rd.bad = true;
+    } else {
+      rd.bad = true;
+    }
+  }
+  if (rd.bad) fr[i].status = 3;
+  else if (!pass) fr[i].n_msgs = nm;
+}
+
+// pass 0: entries and Cmd bytes of each message; pass 1: the records
+__global__ __launch_bounds__(256) void k_wire_parse(const u8* data, const WireMsgPos* pos,
+                                                    u64 nm, int pass, u64* ecnt, u64* ccnt,
+                                                    rbe_message* msgs, rbe_entry* ents, u8* cmd,
+                                                    u32* err) {
+  const u64 j = (u64)blockIdx.x * 256 + threadIdx.x;
+  if (j >= nm) return;
+  const WireMsgPos q = pos[j];
+  WireRd rd{data, q.at + q.len, q.at, false};
+  u64 cb = pass ? ccnt[j] : 0;
+  const u32 ne = wire_message_get(rd, q.at + q.len, pass ? &msgs[j] : nullptr,
+                                  pass ? &ents[ecnt[j]] : nullptr, pass ? cmd : nullptr, &cb);
+  if (rd.bad) {
+    atomicOr(err, 1u);
+    return;
+  }
+  if (!pass) {
+    ecnt[j] = ne;
+    ccnt[j] = cb;
+  }
+}
+
+// exclusive scan of v[0, n) in place (three launches: block sums, their scan
+// by one block, the adds); top must hold grid + 1 words, top[grid] = total
+__global__ __launch_bounds__(256) void k_scan_blocks(u64* v, u64 n, u64* top) {
+  __shared__ u64 s_tmp[4];
+  const u64 j = (u64)blockIdx.x * 256 + threadIdx.x;
+  const u64 x = j < n ? v[j] : 0;
+  u64 t = 0;
+  const u64 pre = block_scan_u64(x, &t, s_tmp);
+  if (j < n) v[j] = pre;
+  if (threadIdx.x == 0) top[blockIdx.x] = t;
+}
+__global__ __launch_bounds__(256) void k_scan_top(u64* top, u32 nb) {
+  __shared__ u64 s_tmp[4];
+  u64 carry = 0;
+  for (u32 b0 = 0; b0 < nb; b0 += 256) {
+    const u32 b = b0 + threadIdx.x;
+    const u64 x = b < nb ? top[b] : 0;
+    u64 t = 0;
+    const u64 pre = block_scan_u64(x, &t, s_tmp);
+    if (b < nb) top[b] = carry + pre;
+    carry += t;
+  }
+  if (threadIdx.x == 0) top[nb] = carry;
+}
+__global__ __launch_bounds__(256) void k_scan_add(u64* v, u64 n, const u64* top) {
+  const u64 j = (u64)blockIdx.x * 256 + threadIdx.x;
+  if (j < n) v[j] += top[blockIdx.x];
+}
+
+}  // namespace rbe

@@ -123,6 +123,25 @@ class RbeOutputs(C.Structure):
                 ("ready_to_reads", C.POINTER(RbeReadyToRead))]
 
 
+class RbeWireFrame(C.Structure):
+    _fields_ = [("offset", C.c_uint64), ("bytes", C.c_uint64), ("first_group", C.c_uint64),
+                ("src", C.c_uint32), ("dst", C.c_uint32), ("n_messages", C.c_uint32),
+                ("n_groups", C.c_uint32)]
+
+
+class RbeWireConfig(C.Structure):
+    _fields_ = [("deployment_id", C.c_uint64), ("bin_ver", C.c_uint32),
+                ("groups_per_batch", C.c_uint32), ("source_address", C.c_char_p * 6)]
+
+
+def wire_config(deployment_id=0, bin_ver=0, groups_per_batch=0, source_address=()):
+    wc = RbeWireConfig(deployment_id=deployment_id, bin_ver=bin_ver,
+                       groups_per_batch=groups_per_batch)
+    for i, a in enumerate(source_address):
+        wc.source_address[i] = a.encode()
+    return wc
+
+
 MESSAGE_DTYPE = _np_dtype(RbeMessage)
 RTR_DTYPE = _np_dtype(RbeReadyToRead)
 
@@ -139,13 +158,14 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_push_messages", "rbe_snapshot_bytes", "rbe_export_groups", "rbe_import_groups",
            "rbe_get_entry_cmds", "rbe_set_apply_ready", "rbe_collect_outputs", "rbe_launch",
            "rbe_xchg_chunk_bytes", "rbe_xchg_pack_fixed", "rbe_xchg_unpack_fixed",
-           "rbe_xchg_status", "rbe_stream", "rbe_get_snapshot_state"]
+           "rbe_xchg_status", "rbe_stream", "rbe_get_snapshot_state", "rbe_wire_encode",
+           "rbe_wire_fetch", "rbe_wire_decode"]
 KERNEL_SLOTS = 4
 
 _lib = None
 
 
-RBE_E_INVALID, RBE_E_NOMEM, RBE_E_STATE = -1, -3, -5
+RBE_E_INVALID, RBE_E_NOMEM, RBE_E_STATE, RBE_E_CORRUPT = -1, -3, -5, -6
 RBE_STEP_NO_TICK = 1
 
 
@@ -194,6 +214,10 @@ def load_library(path: Optional[str] = None):
         "rbe_get_entry_cmds": (i32, [vp, u64, u64, u64, vp, u64, P(u64)]),
         "rbe_get_views": (i32, [vp, u64, u64, P(RbeReplicaView)]),
         "rbe_get_snapshot_state": (i32, [vp, u64, u64, P(u64)]),
+        "rbe_wire_encode": (i32, [vp, P(RbeWireConfig), P(u64)]),
+        "rbe_wire_fetch": (i32, [vp, vp, u64, P(RbeWireFrame), u32]),
+        "rbe_wire_decode": (i32, [vp, vp, u64, P(RbeMessage), u32, P(u32), P(RbeEntry), u32,
+                                  P(u32), vp, u64, P(u64)]),
         "rbe_collect_outputs": (i32, [vp, u64, u64, P(RbeOutputs)]),
         "rbe_launch": (i32, [vp, u64, P(u64), P(RbeLaunchState), P(RbeEntry)]),
         "rbe_get_counters": (i32, [vp, P(u64)]),
@@ -541,6 +565,41 @@ class Engine(NodeInputs):
         arr = (RbeReplicaView * count)()
         _check(self.lib.rbe_get_views(self.h, first, count, arr), "rbe_get_views")
         return arr
+
+    def wire_encode(self, deployment_id=0, bin_ver=0, groups_per_batch=0, source_address=()):
+        """rbe_wire_encode: the last round's outbox as framed MessageBatches in
+        device memory; returns (bytes, frames, messages, InstallSnapshots left out)."""
+        tot = (C.c_uint64 * 4)()
+        wc = wire_config(deployment_id, bin_ver, groups_per_batch, source_address)
+        _check(self.lib.rbe_wire_encode(self.h, C.byref(wc), tot), "rbe_wire_encode")
+        return tuple(tot)
+
+    def wire_fetch(self, totals):
+        """(stream bytes, [rbe_wire_frame]) of the last rbe_wire_encode."""
+        nbytes, nf = totals[0], totals[1]
+        buf = C.create_string_buffer(max(1, nbytes))
+        fr = (RbeWireFrame * max(1, nf))()
+        _check(self.lib.rbe_wire_fetch(self.h, buf, nbytes, fr, nf), "rbe_wire_fetch")
+        return buf.raw[:nbytes], [fr[i] for i in range(nf)]
+
+    def wire_decode(self, data: bytes, cap=1 << 16, ent_cap=1 << 16, cmd_cap=1 << 20):
+        """rbe_wire_decode: (messages, entries, cmd bytes); raises EngineError
+        with rc RBE_E_CORRUPT on a bad frame."""
+        msgs = (RbeMessage * cap)()
+        ents = (RbeEntry * ent_cap)()
+        cmd = C.create_string_buffer(max(1, cmd_cap))
+        nm, ne, nc = C.c_uint32(), C.c_uint32(), C.c_uint64()
+        rc = self.lib.rbe_wire_decode(self.h, data, len(data), msgs, cap, C.byref(nm), ents,
+                                      ent_cap, C.byref(ne), cmd, cmd_cap, C.byref(nc))
+        if rc == RBE_E_NOMEM:
+            return self.wire_decode(data, max(cap, nm.value), max(ent_cap, ne.value),
+                                    max(cmd_cap, nc.value))
+        if rc != 0:
+            err = EngineError(f"rbe_wire_decode failed with rc={rc}")
+            err.rc = rc
+            raise err
+        return ([msgs[i] for i in range(nm.value)], [ents[i] for i in range(ne.value)],
+                cmd.raw[:nc.value])
 
     def snapshot_state(self, first: int = 0, count: Optional[int] = None) -> np.ndarray:
         """[count, 6] uint64: LogDB compaction marker, its term, snapshot index,

@@ -41,6 +41,7 @@ extern "C" {
 #define RBE_E_NOMEM (-3)     /* device allocation failed */
 #define RBE_E_NODEV (-4)     /* no usable gfx950 device */
 #define RBE_E_STATE (-5)     /* call not valid in the current state */
+#define RBE_E_CORRUPT (-6)   /* rbe_wire_decode: a frame failed its crc32 or does not parse */
 
 /* sticky per-replica fault bits (see dragonboat_amd/csrc/rbe_types.h) */
 #define RBE_FAULT_WINDOW 0x01u
@@ -336,6 +337,46 @@ int rbe_get_entries(rbe_engine* e, uint64_t replica, uint64_t lo, uint64_t hi,
  * received), the node's reqSnapshotIndex and pending compactLogTo (node.go
  * ss, 585-605 / 849-866). */
 int rbe_get_snapshot_state(rbe_engine* e, uint64_t first, uint64_t count, uint64_t* out6);
+
+/* ---- Transport wire format ------------------------
+ * What a node writes on a TCP connection for Raft traffic: frames of a 2-byte
+ * magic 0xAE7D, the 18-byte requestHeader (method 100, payload size, header
+ * crc32, payload crc32, big endian; internal/transport/tcp.go:80-91, 149-185)
+ * and a marshaled raftpb.MessageBatch (raft.pb.go:2415-2443: Messages
+ * 2230-2294 with their colfer-form entries, raft_optimized.go:161-295).
+ * rbe_wire_encode builds, on the device, one frame per (sender slot, receiver
+ * slot, run of groups_per_batch groups) holding every message the last round
+ * sent between those replicas (group order; per replica the rbe_get_outbox
+ * order).  InstallSnapshot messages are left out and counted: the reference
+ * streams them as snapshot chunks, never in a MessageBatch
+ * (transport.go:400-403).  Entries carry Index/Term/Type/Cmd (payload-heap
+ * Cmds in full); Key/ClientID/SeriesID/RespondedTo are 0. */
+typedef struct rbe_wire_frame {
+  uint64_t offset, bytes;      /* frame (header included) in the encoded stream */
+  uint64_t first_group;
+  uint32_t src, dst;           /* sender / receiver replica slot (node id - 1) */
+  uint32_t n_messages, n_groups;
+} rbe_wire_frame;
+typedef struct rbe_wire_config {
+  uint64_t deployment_id;      /* MessageBatch.DeploymentId */
+  uint32_t bin_ver;            /* MessageBatch.BinVer (raftio.RPCBinVersion) */
+  uint32_t groups_per_batch;   /* 0 = every group in one batch per slot pair */
+  const char* source_address[6];  /* MessageBatch.SourceAddress per sender slot (< 48 B) */
+} rbe_wire_config;
+/* totals = {bytes, frames, messages, InstallSnapshots left out}; the frames
+ * stay in engine device memory until the next encode (rbe_wire_fetch). */
+int rbe_wire_encode(rbe_engine* e, const rbe_wire_config* wc, uint64_t totals[4]);
+int rbe_wire_fetch(rbe_engine* e, void* out, uint64_t cap, rbe_wire_frame* frames,
+                   uint32_t frames_cap);
+/* Decode back-to-back frames (host memory, as read from connections) on the
+ * device: both crc32s checked per frame (readMessage, tcp.go:187-244), then
+ * MessageBatch.Unmarshal (raft_optimized.go:654-1204) into records in frame
+ * order.  Entry Cmd bytes are concatenated in `cmd` (rbe_entry.cmd holds the
+ * first 16).  RBE_E_CORRUPT when any frame fails; RBE_E_NOMEM when a capacity
+ * is short (the counts are still reported). */
+int rbe_wire_decode(rbe_engine* e, const void* data, uint64_t bytes, rbe_message* msgs,
+                    uint32_t cap, uint32_t* n_msgs, rbe_entry* ents, uint32_t ent_cap,
+                    uint32_t* n_ents, uint8_t* cmd, uint64_t cmd_cap, uint64_t* cmd_bytes);
 /* The Cmd bytes of entries [lo, hi] of a replica's log, concatenated in `buf`:
  * entry lo + i occupies [offsets[i], offsets[i + 1]) (offsets has hi - lo + 2
  * slots and is filled even when `cap` is short, which returns RBE_E_NOMEM).

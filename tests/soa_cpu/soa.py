@@ -6,7 +6,7 @@ import ctypes as C
 import os
 
 from dragonboat_amd.engine import (CTR_NUM, COUNTER_NAMES, NodeInputs, RbeEntry, RbeMessage,
-                                   RbeReplicaView, entry_cmds, make_config)
+                                   RbeReplicaView, RbeWireFrame, entry_cmds, make_config)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _lib = None
@@ -26,6 +26,10 @@ def lib():
         L.soa_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         L.soa_views.argtypes = [C.c_void_p, C.c_void_p]
         L.soa_snapshot_state.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+        L.soa_wire_encode.restype = C.c_int64
+        L.soa_wire_encode.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
+                                      C.POINTER(C.c_char_p), C.c_void_p, C.c_uint64,
+                                      C.POINTER(RbeWireFrame), C.POINTER(C.c_uint32)]
         L.soa_set_full_only.argtypes = [C.c_void_p, C.c_int]
         L.soa_set_staged.argtypes = [C.c_void_p, C.c_int]
         L.soa_slow_total.restype = C.c_uint64
@@ -177,6 +181,21 @@ class SoaCpu(NodeInputs):
         arr = (RbeReplicaView * self.n_rep)()
         lib().soa_views(self.h, C.cast(arr, C.c_void_p))
         return arr
+
+    def wire_encode(self, deployment_id=0, bin_ver=0, groups_per_batch=0, source_address=()):
+        """Host-build rbe_wire_encode + rbe_wire_fetch: (stream bytes, frames)."""
+        addrs = (C.c_char_p * 6)(*[a.encode() for a in source_address])
+        n = self.cfg.n_replicas
+        gpb = groups_per_batch or self.cfg.n_groups
+        maxf = n * (n - 1) * ((self.cfg.n_groups + gpb - 1) // gpb)
+        fr = (RbeWireFrame * max(1, maxf))()
+        nf = C.c_uint32()
+        cap = 1 << 24
+        buf = C.create_string_buffer(cap)
+        got = lib().soa_wire_encode(self.h, deployment_id, bin_ver, groups_per_batch, addrs, buf,
+                                    cap, fr, C.byref(nf))
+        assert got >= 0
+        return buf.raw[:got], [fr[i] for i in range(nf.value)]
 
     def snapshot_state(self):
         o = (C.c_uint64 * (6 * self.n_rep))()

@@ -13,6 +13,7 @@
 #include "../../dragonboat_amd/csrc/rbe_host.h"
 #include "../../dragonboat_amd/csrc/rbe_snap.h"
 #include "../../dragonboat_amd/csrc/rbe_xchg.h"
+#include "../../dragonboat_amd/csrc/rbe_wire.h"
 #include "../../include/rbe.h"
 
 using namespace rbe;
@@ -379,6 +380,69 @@ int soa_notify_applied(void* h, uint64_t n, const uint64_t* replica, const uint6
   SoaEngine* e = (SoaEngine*)h;
   if (!e->C.ext_apply) return RBE_E_STATE;
   return e->hin.notify_applied(n, replica, applied);
+}
+
+// rbe_wire_encode on the host build: the same wire_cell / trailer / header
+// functions the device passes run, batch by batch, into `out` (cap bytes);
+// frames as rbe_wire_frame.  Returns total bytes (or -1 when cap is short).
+int64_t soa_wire_encode(void* h, uint64_t deployment_id, uint32_t bin_ver, uint32_t gpb,
+                        const char* const* addr, uint8_t* out, uint64_t cap,
+                        rbe_wire_frame* frames, uint32_t* n_frames) {
+  SoaEngine* e = (SoaEngine*)h;
+  const Params& C = e->C;
+  const u32 N = C.n;
+  if (!gpb) gpb = (u32)C.n_groups;
+  u32 table[256];
+  for (u32 i = 0; i < 256; i++) table[i] = crc_table_entry(i);
+  std::vector<u8> buf;
+  u32 nf = 0;
+  for (u32 p = 0; p < N * (N - 1); p++) {
+    const u32 k = p / (N - 1), dd = p % (N - 1), d = dd >= k ? dd + 1 : dd;
+    const u32 alen = addr && addr[k] ? (u32)strlen(addr[k]) : 0;
+    for (u64 g0 = 0; g0 < C.n_groups; g0 += gpb) {
+      const u64 g1 = g0 + gpb < C.n_groups ? g0 + gpb : C.n_groups;
+      std::vector<u8> pay;
+      u32 nm = 0;
+      for (u64 g = g0; g < g1; g++) {
+        u32 cm = 0, ci = 0;
+        u32 b = 0;
+        if (N == 3) b = wire_cell<3>(e->P, C, e->heap.data(), g, k, d, e->round, nullptr, &cm, &ci);
+        else b = wire_cell<5>(e->P, C, e->heap.data(), g, k, d, e->round, nullptr, &cm, &ci);
+        if (!cm) continue;
+        const size_t at = pay.size();
+        pay.resize(at + b);
+        if (N == 3) wire_cell<3>(e->P, C, e->heap.data(), g, k, d, e->round, pay.data() + at, &cm, &ci);
+        else wire_cell<5>(e->P, C, e->heap.data(), g, k, d, e->round, pay.data() + at, &cm, &ci);
+        nm += cm;
+      }
+      if (!nm) continue;
+      const u8* a = (const u8*)(alen ? addr[k] : "");
+      const u32 tl = wire_trailer(deployment_id, a, alen, bin_ver, nullptr);
+      const size_t at = pay.size();
+      pay.resize(at + tl);
+      wire_trailer(deployment_id, a, alen, bin_ver, pay.data() + at);
+      const size_t fo = buf.size();
+      buf.resize(fo + kWireHeader + pay.size());
+      memcpy(buf.data() + fo + kWireHeader, pay.data(), pay.size());
+      wire_header_put(buf.data() + fo, pay.size(), crc32_update(0, pay.data(), pay.size(), table),
+                      table);
+      if (frames) {
+        rbe_wire_frame& f = frames[nf];
+        f.offset = fo;
+        f.bytes = kWireHeader + pay.size();
+        f.first_group = g0;
+        f.src = k;
+        f.dst = d;
+        f.n_messages = nm;
+        f.n_groups = (u32)(g1 - g0);
+      }
+      nf++;
+    }
+  }
+  *n_frames = nf;
+  if (buf.size() > cap) return -1;
+  if (!buf.empty()) memcpy(out, buf.data(), buf.size());
+  return (int64_t)buf.size();
 }
 
 void soa_snapshot_state(void* h, uint64_t* out6) {

@@ -1,0 +1,85 @@
+"""Transport wire format on the GPU: rbe_wire_encode's frames equal, byte for
+byte, the oracle's restatement (oracle/wire.py) of MessageBatch marshaling and
+TCP framing applied to the engine's outbox records, and rbe_wire_decode reads
+them back into exactly those records (crc32s checked on the device)."""
+import random
+
+import pytest
+
+import wire as W
+from parity_util import C2, C3, C4
+from wire_util import ADDRS, check_decoded, check_frames, expected_stream, outbox_by_cell
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(**kw):
+    from dragonboat_amd.engine import Engine
+    return Engine(device=0, trace=True, **kw)
+
+
+@pytest.mark.parametrize("name,kw,extra,gpb", [
+    ("C2", C2, {}, 16), ("C3", C3, dict(ring=128), 0), ("C4", C4, {}, 7),
+    ("C3_SNAP", dict(C3, check_quorum=False, snapshot_entries=20, compaction_overhead=5),
+     dict(ring=128), 5)])
+def test_gpu_wire_encode_decode(gpu_available, name, kw, extra, gpb):
+    eng = _engine(**kw, **extra)
+    n, G = kw["n_replicas"], kw["n_groups"]
+    checked = 0
+    for rnd in range(160):
+        eng.run(1)
+        if rnd % 9 and rnd < 150:
+            continue
+        cells, n_is = outbox_by_cell(eng, G, n)
+        tot = eng.wire_encode(0xDB0A7, 210, gpb, ADDRS[:n])
+        stream, frames = eng.wire_fetch(tot)
+        exp, exp_frames = expected_stream(cells, G, n, gpb, 0xDB0A7, 210)
+        check_frames(stream, frames, exp, exp_frames)
+        assert tot[2] == sum(len(v) for v in cells.values()) and tot[3] == n_is
+        msgs, ents, cmd = eng.wire_decode(stream)
+        check_decoded(msgs, ents, cmd, cells, G, n, gpb)
+        checked += tot[2]
+    assert checked > 100
+    eng.close()
+
+
+def test_gpu_wire_heap_cmds(gpu_available):
+    from heap_util import mixed_cmd
+    kw = dict(C2, n_groups=8, ext_inputs=True, wl_enabled=False)
+    eng = _engine(**kw, heap_bytes=8 << 20)
+    n, G = 3, 8
+    rng = random.Random(4)
+    long_seen = 0
+    for rnd in range(120):
+        if rnd > 30:
+            reps = [g * n + rng.randrange(n) for g in range(G)]
+            eng.push_proposals(reps, [[mixed_cmd(rng)] for _ in reps])
+        eng.run(1)
+        cells, _ = outbox_by_cell(eng, G, n, cmds=lambda r, i: eng.entry_cmds(r, i, i)[0])
+        tot = eng.wire_encode(1, 2, 3, ADDRS[:n])
+        stream, frames = eng.wire_fetch(tot)
+        exp, exp_frames = expected_stream(cells, G, n, 3, 1, 2)
+        check_frames(stream, frames, exp, exp_frames)
+        msgs, ents, cmd = eng.wire_decode(stream)
+        check_decoded(msgs, ents, cmd, cells, G, n, 3)
+        long_seen += sum(1 for e in ents if e.cmd_len > 16)
+    assert long_seen > 20
+    eng.close()
+
+
+def test_gpu_wire_decode_rejects_corruption(gpu_available):
+    from dragonboat_amd.engine import RBE_E_CORRUPT, EngineError
+    eng = _engine(**C2)
+    eng.run(40)
+    tot = eng.wire_encode(5, 1, 0, ADDRS[:3])
+    stream, frames = eng.wire_fetch(tot)
+    assert len(frames) == 6
+    for pos in (frames[2].offset + 5, frames[3].offset + 30, len(stream) - 1):
+        bad = bytearray(stream)
+        bad[pos] ^= 0x10
+        with pytest.raises(EngineError) as ei:
+            eng.wire_decode(bytes(bad))
+        assert ei.value.rc == RBE_E_CORRUPT
+    # the oracle reads the same frames
+    assert len(W.frames_decode(stream)) == 6
+    eng.close()
