@@ -1754,9 +1754,8 @@ int rbe_wire_decode(rbe_engine* e, const void* data, uint64_t bytes, rbe_message
   WireIn* dfr = (WireIn*)(e->wire_dev + al(bytes));
   HIP_OK(hipMemcpyAsync(e->wire_dev, data, bytes, hipMemcpyHostToDevice, e->stream));
   HIP_OK(hipMemcpyAsync(dfr, fr.data(), nf * sizeof(WireIn), hipMemcpyHostToDevice, e->stream));
-  const unsigned gf = (unsigned)((nf + 63) / 64);
   hipLaunchKernelGGL(k_wire_verify, dim3((unsigned)nf), dim3(256), 0, e->stream, e->wire_dev, dfr);
-  hipLaunchKernelGGL(k_wire_bounds, dim3(gf), dim3(64), 0, e->stream, e->wire_dev, dfr, (u32)nf,
+  hipLaunchKernelGGL(k_wire_bounds, dim3((unsigned)nf), dim3(256), 0, e->stream, e->wire_dev, dfr,
                      0, nullptr);
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(fr.data(), dfr, nf * sizeof(WireIn), hipMemcpyDeviceToHost, e->stream));
@@ -1782,7 +1781,7 @@ int rbe_wire_decode(rbe_engine* e, const void* data, uint64_t bytes, rbe_message
   u32* err = (u32*)(w + o_err);
   HIP_OK(hipMemcpyAsync(dfr, fr.data(), nf * sizeof(WireIn), hipMemcpyHostToDevice, e->stream));
   HIP_OK(hipMemsetAsync(err, 0, 4, e->stream));
-  hipLaunchKernelGGL(k_wire_bounds, dim3(gf), dim3(64), 0, e->stream, e->wire_dev, dfr, (u32)nf,
+  hipLaunchKernelGGL(k_wire_bounds, dim3((unsigned)nf), dim3(256), 0, e->stream, e->wire_dev, dfr,
                      1, pos);
   const unsigned gm = (unsigned)nbk;
   if (tm) {

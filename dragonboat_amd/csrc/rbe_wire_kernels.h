@@ -10,7 +10,7 @@
 //                 one lane per batch: the trailer
 //   k_wire_crc    one block per frame: payload crc32 by segments combined
 //                 with crc32_combine, then the header
-// Decode: k_wire_verify (block per frame: both crc32s), k_wire_bounds (lane
+// Decode: k_wire_verify (block per frame: both crc32s), k_wire_bounds (block
 // per frame: where its requests are), k_wire_parse (lane per message: count,
 // device scan, then the records).
 #pragma once
@@ -197,6 +197,27 @@ __global__ __launch_bounds__(256) void k_wire_trailers(Params C, WireArgs A, Wir
                out + B.frame_off[b] + kWireHeader + B.batch_pay[b] - tl);
 }
 
+// crc32 of [p, p + n) by one lane, reading 16-B aligned words (the bytes
+// outside [p, p + n) of the first and last word are read, not used)
+__device__ u32 crc32_words(u32 crc, const u8* p, u64 n, const u32* table) {
+  if (!n) return crc;
+  u32 c = ~crc;
+  const u8* a = (const u8*)((u64)p & ~15ull);
+  u32 o = (u32)(p - a);
+  u64 left = n;
+  while (left) {
+    const uint4 w = *(const uint4*)a;
+    const u32 ws[4] = {w.x, w.y, w.z, w.w};
+    for (; o < 16 && left; o++, left--) {
+      const u8 b = (u8)(ws[o >> 2] >> (8 * (o & 3)));
+      c = table[(c ^ b) & 0xFFu] ^ (c >> 8);
+    }
+    a += 16;
+    o = 0;
+  }
+  return ~c;
+}
+
 // crc32 of [p, p + n) by this block: one contiguous segment per thread, the
 // segments' crcs combined pairwise in LDS
 __device__ u32 block_crc32(const u8* p, u64 n, const u32* table, const u32* x2n, u32* s_crc) {
@@ -204,7 +225,11 @@ __device__ u32 block_crc32(const u8* p, u64 n, const u32* table, const u32* x2n,
   const u64 seg = (n + T - 1) / T;
   const u64 lo = seg * t < n ? seg * t : n;
   const u64 hi = lo + seg < n ? lo + seg : n;
+#ifdef RBE_WIRE_BYTE_CRC
   s_crc[t] = crc32_update(0, p + lo, hi - lo, table);
+#else
+  s_crc[t] = crc32_words(0, p + lo, hi - lo, table);
+#endif
   __syncthreads();
   // tree: combine (i, i + s) with the length of segment group i + s
   for (u32 s = 1; s < T; s <<= 1) {
@@ -393,84 +418,131 @@ RBE_HD u32 wire_message_get(WireRd& rd, u64 end, rbe_message* m, rbe_entry* ents
   return ne;
 }
 
-// Decode is parallel per message: one lane per frame finds the top-level
+// Decode is parallel per message: one block per frame finds the top-level
 // requests of its MessageBatch (MessageBatch.Unmarshal, raft_optimized.go:
-// 1051-1204: field 1 = a Message, 2-4 the trailer), reading 16-B windows;
+// 1051-1204: field 1 = a Message, 2-4 the trailer) in LDS windows;
 // then one lane per message parses it (Message.Unmarshal), first counting its
 // entries and Cmd bytes (scanned on the device for the output offsets), then
 // writing the records.
-struct WireWin {  // 16-B window reader over one frame's payload
-  const u8* p;
-  u64 n, i;
-  u64 wbase;
-  uint4 w;
-  bool bad;
-  RBE_HD u8 byte() {
-    if (i >= n) {
-      bad = true;
-      return 0;
-    }
-    const u64 a = (u64)(p + i);
-    const u64 base = a & ~15ull;
-    if (base != wbase) {
-      w = *(const uint4*)base;
-      wbase = base;
-    }
-    const u32 o = (u32)(a - base);
-    const u32 word = o < 4 ? w.x : (o < 8 ? w.y : (o < 12 ? w.z : w.w));
-    i++;
-    return (u8)(word >> (8 * (o & 3)));
-  }
-  RBE_HD u64 varint() {
-    u64 x = 0;
-    for (u32 s = 0; s < 64; s += 7) {
-      const u8 b = byte();
-      x |= (u64)(b & 0x7F) << s;
-      if (b < 0x80 || bad) return x;
-    }
-    bad = true;
-    return x;
-  }
-};
-
 struct WireMsgPos {
   u64 at, len;  // Message body [at, at + len) in the device copy of the input
 };
 
-// pass 0: count the frame's requests; pass 1: record where each one is
-__global__ __launch_bounds__(64) void k_wire_bounds(const u8* data, WireIn* fr, u32 nf, int pass,
-                                                    WireMsgPos* pos) {
-  const u32 i = blockIdx.x * 64 + threadIdx.x;
-  if (i >= nf) return;
-  const WireIn f = fr[i];
+// pass 0: count the frame's requests; pass 1: record where each one is.
+// One block per frame: the block stages a 32 KB window of the payload in LDS
+// (coalesced), one lane walks the top-level fields inside it, and the window
+// moves to wherever the walk stops (a field header near the window's end, or
+// a request longer than the window, which is skipped without being read).
+static constexpr u32 kWireWin = 32768;
+__global__ __launch_bounds__(256) void k_wire_bounds(const u8* data, WireIn* fr, int pass,
+                                                     WireMsgPos* pos) {
+  __shared__ __attribute__((aligned(16))) u8 s_buf[kWireWin];
+  __shared__ u64 s_at, s_base, s_nm;
+  __shared__ u32 s_state;  // 0 walking, 1 done, 2 bad
+  const WireIn f = fr[blockIdx.x];
   if (f.status) return;
-  WireWin rd{data + f.offset, f.size, 0, ~0ull, make_uint4(0, 0, 0, 0), false};
-  u32 nm = 0;
-  while (rd.i < rd.n && !rd.bad) {
-    const u64 tag = rd.varint();
-    const u32 fn = (u32)(tag >> 3), wt = (u32)(tag & 7);
-    if (wt == 2) {
-      const u64 l = rd.varint();
-      if (l > rd.n - rd.i) {
-        rd.bad = true;
-        break;
-      }
-      if (fn == 1) {
-        if (pass) pos[f.msg0 + nm] = WireMsgPos{f.offset + rd.i, l};
-        nm++;
-      }
-      rd.i += l;
-    } else if (wt == 0) {
-      rd.varint();
-    } else if (wt == 1 || wt == 5) {
-      rd.i += wt == 1 ? 8 : 4;
-      if (rd.i > rd.n) rd.bad = true;
-    } else {
-      rd.bad = true;
-    }
+  const u8* p = data + f.offset;
+  const u64 n = f.size;
+  if (threadIdx.x == 0) {
+    s_at = 0;
+    s_nm = 0;
+    s_state = 0;
   }
-  if (rd.bad) fr[i].status = 3;
-  else if (!pass) fr[i].n_msgs = nm;
+  __syncthreads();
+  while (s_state == 0) {
+    // 16-B aligned words from the one holding byte `base`, all in flight at once
+    const u64 base = s_at;
+    const u8* a0 = (const u8*)((u64)(p + base) & ~15ull);
+    const u32 sh = (u32)((p + base) - a0);
+    const u64 avail = n - base < kWireWin - sh ? n - base : kWireWin - sh;
+    const u32 nw = (u32)((sh + avail + 15) / 16);
+#ifdef RBE_WIRE_BYTE_WIN
+    for (u32 j = threadIdx.x; j < nw * 16; j += 256) s_buf[j] = a0[j];
+#else
+#pragma unroll
+    for (u32 it = 0; it < kWireWin / 16 / 256; it++) {
+      const u32 wi = it * 256 + threadIdx.x;
+      if (wi < nw) ((uint4*)s_buf)[wi] = ((const uint4*)a0)[wi];
+    }
+#endif
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      u64 i = base, nm = s_nm;
+      u32 st = 0;
+      const u64 wend = base + avail;
+      // a field header (tag + length, <= 20 bytes) must lie in the window
+      // unless the frame ends first (s_buf indexed directly: LDS reads, not
+      // flat loads through a captured pointer)
+      for (;;) {
+        if (i >= n) {
+          st = 1;
+          break;
+        }
+        if (i + 20 > wend && wend < n) break;  // move the window to i
+        u64 tag = 0;
+        bool ok = false;
+        u64 q = i;
+        for (u32 bs = 0; bs < 64 && q < wend; bs += 7) {
+          const u8 b = s_buf[(u32)(q++ - base) + sh];
+          tag |= (u64)(b & 0x7F) << bs;
+          if (b < 0x80) {
+            ok = true;
+            break;
+          }
+        }
+        if (!ok) {
+          st = 2;
+          break;
+        }
+        const u32 fn = (u32)(tag >> 3), wt = (u32)(tag & 7);
+        if (wt == 0 || wt == 2) {
+          u64 v = 0;
+          ok = false;
+          for (u32 bs = 0; bs < 64 && q < wend; bs += 7) {
+            const u8 b = s_buf[(u32)(q++ - base) + sh];
+            v |= (u64)(b & 0x7F) << bs;
+            if (b < 0x80) {
+              ok = true;
+              break;
+            }
+          }
+          if (!ok) {
+            st = 2;
+            break;
+          }
+          if (wt == 2) {
+            if (v > n - q) {
+              st = 2;
+              break;
+            }
+            if (fn == 1) {
+              if (pass) pos[f.msg0 + nm] = WireMsgPos{f.offset + q, v};
+              nm++;
+            }
+            q += v;
+          }
+        } else if (wt == 1 || wt == 5) {
+          q += wt == 1 ? 8 : 4;
+          if (q > n) {
+            st = 2;
+            break;
+          }
+        } else {
+          st = 2;
+          break;
+        }
+        i = q;
+      }
+      s_at = i;
+      s_nm = nm;
+      s_state = st;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (s_state == 2) fr[blockIdx.x].status = 3;
+    else if (!pass) fr[blockIdx.x].n_msgs = (u32)s_nm;
+  }
 }
 
 // pass 0: entries and Cmd bytes of each message; pass 1: the records
