@@ -737,6 +737,9 @@ __device__ __forceinline__ void stage_out_wave(const Planes& P, const StageRow<N
 // followers.  The rows a step reads and rewrites whole (Hot, Core, Upd, the
 // leader's remote slots) move between HBM and LDS wave-cooperatively
 // (stage_in_wave / stage_out_wave); the step works on its LDS row.
+#ifndef RBE_XCD_FAST
+#define RBE_XCD_FAST 0  // measured slower (C4 k_fast_both 116.7-117.0 vs 110.5-110.9 us)
+#endif
 template <int N, bool TRACE>
 __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, Params C,
                                                                      RoundArg ra, Lists L) {
@@ -754,15 +757,37 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, 
   for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
   StageRow<N>* wrows = &s_rows[threadIdx.x & ~63u];
   StageRow<N>* mine = &s_rows[threadIdx.x];
-  const u64 stride = (u64)gridDim.x * kBlock;
-  for (u64 i0 = (u64)blockIdx.x * kBlock; i0 < n; i0 += stride) {
+  // XCD-aware item mapping (RBE_XCD_FAST): block b takes only the items of
+  // shard b % kShards, which k_triage blocks b' with b' % kShards == b %
+  // kShards wrote.  Blocks are dealt to the 8 XCDs round robin, so a group's
+  // leader and followers (one triage block, one shard) are stepped on the same
+  // XCD as each other and as its triage, and their partial-line writes to the
+  // group's rows meet in one L2 instead of being written back from several.
+  const bool xcd = RBE_XCD_FAST && gridDim.x >= kShards;
+  const u32 xsh = blockIdx.x % kShards;
+  u32 xcum[5] = {0, 0, 0, 0, 0};
+  if (xcd) {
+    for (u32 q = 0; q < 4; q++)
+      xcum[q + 1] = xcum[q] + (s_pre[q * kShards + xsh + 1] - s_pre[q * kShards + xsh]);
+  }
+  const u64 xn = xcum[4], xnl = xcum[2];
+  const u64 xblocks = (gridDim.x - xsh + kShards - 1) / kShards;
+  const u64 stride = xcd ? xblocks * kBlock : (u64)gridDim.x * kBlock;
+  const u64 lim = xcd ? xn : n;
+  for (u64 i0 = (u64)(xcd ? blockIdx.x / kShards : blockIdx.x) * kBlock; i0 < lim; i0 += stride) {
     const u64 i = i0 + threadIdx.x;
-    const bool lead = i < nl, any = i < n;
+    const bool lead = xcd ? i < xnl : i < nl, any = i < lim;
     u32 r = 0, aux = 0;
     if (any) {
-      const u32 sg = seg_find<4 * kShards>(s_pre, (u32)i);
-      const u64 at = list_pos(L, sg / (2 * kShards), sg % kShards, (sg / kShards) & 1u,
-                              (u32)i - s_pre[sg]);
+      u64 at;
+      if (xcd) {
+        const u32 q = (u32)(i >= xcum[1]) + (u32)(i >= xcum[2]) + (u32)(i >= xcum[3]);
+        at = list_pos(L, q / 2u, xsh, q & 1u, (u32)(i - xcum[q]));
+      } else {
+        const u32 sg = seg_find<4 * kShards>(s_pre, (u32)i);
+        at = list_pos(L, sg / (2 * kShards), sg % kShards, (sg / kShards) & 1u,
+                      (u32)i - s_pre[sg]);
+      }
       r = L.idx[at];
       if constexpr (kListAux<N>) aux = L.aux[at];
     }
