@@ -1749,19 +1749,34 @@ int rbe_wire_decode(rbe_engine* e, const void* data, uint64_t bytes, rbe_message
   HIP_OK(hipSetDevice(e->device));
   const u64 nf = fr.size();
   auto al = [](u64 x) { return (x + 255) & ~255ull; };
-  int rc = grow(&e->wire_dev, &e->wire_dev_bytes, al(bytes) + al(nf * sizeof(WireIn)), false);
+  // single-pass position slots: one per 16 payload bytes (a marshaled request
+  // is far longer; a frame that has more falls back to two walks)
+  u64 slots = 0;
+  for (auto& w : fr) {
+    w.pos0 = slots;
+    w.pos_cap = (u32)(w.size / 16 + 1);
+    slots += w.pos_cap;
+  }
+  const u64 o_fr = al(bytes), o_sp = o_fr + al(nf * sizeof(WireIn));
+  int rc = grow(&e->wire_dev, &e->wire_dev_bytes, o_sp + al(slots * sizeof(WireMsgPos)), false);
   if (rc) return rc;
-  WireIn* dfr = (WireIn*)(e->wire_dev + al(bytes));
+  WireIn* dfr = (WireIn*)(e->wire_dev + o_fr);
+  WireMsgPos* spos = (WireMsgPos*)(e->wire_dev + o_sp);
   HIP_OK(hipMemcpyAsync(e->wire_dev, data, bytes, hipMemcpyHostToDevice, e->stream));
   HIP_OK(hipMemcpyAsync(dfr, fr.data(), nf * sizeof(WireIn), hipMemcpyHostToDevice, e->stream));
   hipLaunchKernelGGL(k_wire_verify, dim3((unsigned)nf), dim3(256), 0, e->stream, e->wire_dev, dfr);
-  hipLaunchKernelGGL(k_wire_bounds, dim3((unsigned)nf), dim3(256), 0, e->stream, e->wire_dev, dfr,
-                     0, nullptr);
+  hipLaunchKernelGGL(k_wire_bounds, dim3((unsigned)nf), dim3(kWireWalkBlock), 0, e->stream,
+                     e->wire_dev, dfr, 2, spos);
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(fr.data(), dfr, nf * sizeof(WireIn), hipMemcpyDeviceToHost, e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
   u64 tm = 0;
+  bool refill = false;
   for (auto& w : fr) {
+    if (w.status == 4) {  // more requests than slots: positions from a second walk
+      refill = true;
+      w.status = 0;
+    }
     if (w.status) return RBE_E_CORRUPT;
     w.msg0 = tm;
     tm += w.n_msgs;
@@ -1781,8 +1796,12 @@ int rbe_wire_decode(rbe_engine* e, const void* data, uint64_t bytes, rbe_message
   u32* err = (u32*)(w + o_err);
   HIP_OK(hipMemcpyAsync(dfr, fr.data(), nf * sizeof(WireIn), hipMemcpyHostToDevice, e->stream));
   HIP_OK(hipMemsetAsync(err, 0, 4, e->stream));
-  hipLaunchKernelGGL(k_wire_bounds, dim3((unsigned)nf), dim3(256), 0, e->stream, e->wire_dev, dfr,
-                     1, pos);
+  if (refill)
+    hipLaunchKernelGGL(k_wire_bounds, dim3((unsigned)nf), dim3(kWireWalkBlock), 0, e->stream,
+                       e->wire_dev, dfr, 1, pos);
+  else
+    hipLaunchKernelGGL(k_wire_compact, dim3((unsigned)nf), dim3(256), 0, e->stream, dfr, spos,
+                       pos);
   const unsigned gm = (unsigned)nbk;
   if (tm) {
     hipLaunchKernelGGL(k_wire_parse, dim3(gm), dim3(256), 0, e->stream, e->wire_dev, pos, tm, 0,

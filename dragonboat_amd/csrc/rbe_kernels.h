@@ -853,7 +853,10 @@ __global__ __launch_bounds__(kBlock) void k_isolate(Planes P, Params C, u32 roun
 // applied indexes to the applied plane.
 
 static constexpr unsigned kFastGrid = 2048;  // persistent grid of k_fast_list
-static constexpr unsigned kFullGrid = 256;  // persistent grid of k_full_list: its ~420 registers allow one wave per SIMD, so 256 blocks of 4 waves fill the chip once
+#ifndef RBE_FULL_GRID
+#define RBE_FULL_GRID 256
+#endif
+static constexpr unsigned kFullGrid = RBE_FULL_GRID;  // persistent grid of k_full_list: its ~420 registers allow one wave per SIMD, so 256 blocks of 4 waves fill the chip once
 static inline unsigned grid_for(u64 n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 // One round's launches.  With `ev` (KS_NUM + 1 events) an event is recorded

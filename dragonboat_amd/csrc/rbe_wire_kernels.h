@@ -225,11 +225,7 @@ __device__ u32 block_crc32(const u8* p, u64 n, const u32* table, const u32* x2n,
   const u64 seg = (n + T - 1) / T;
   const u64 lo = seg * t < n ? seg * t : n;
   const u64 hi = lo + seg < n ? lo + seg : n;
-#ifdef RBE_WIRE_BYTE_CRC
-  s_crc[t] = crc32_update(0, p + lo, hi - lo, table);
-#else
   s_crc[t] = crc32_words(0, p + lo, hi - lo, table);
-#endif
   __syncthreads();
   // tree: combine (i, i + s) with the length of segment group i + s
   for (u32 s = 1; s < T; s <<= 1) {
@@ -258,10 +254,12 @@ __global__ __launch_bounds__(256) void k_wire_crc(WireBufs B, u8* out) {
 // ---------------------------------------------------------------- decode
 struct WireIn {  // one inbound frame
   u64 offset, size;  // payload offset in the device copy, payload bytes
-  u64 msg0, ent0, cmd0;  // first output record / entry / Cmd byte
-  u32 n_msgs, n_ents;
-  u64 cmd_bytes;
-  u32 status;  // 0 ok, 1 header crc, 2 payload crc, 3 malformed
+  u64 msg0;          // its first request in the output
+  u64 pos0;          // its first slot in the single-pass position area
+  u64 pad0;
+  u32 n_msgs, pos_cap;  // requests; slots reserved for them (single pass)
+  u64 pad1;
+  u32 status;  // 0 ok, 1 header crc, 2 payload crc, 3 malformed, 4 more requests than slots
   u32 pad;
 };
 
@@ -428,13 +426,17 @@ struct WireMsgPos {
   u64 at, len;  // Message body [at, at + len) in the device copy of the input
 };
 
-// pass 0: count the frame's requests; pass 1: record where each one is.
-// One block per frame: the block stages a 32 KB window of the payload in LDS
+// pass 0: count the frame's requests; pass 1: record where each one is (at
+// msg0); pass 2: both at once into the frame's pos_cap slots from pos0 (the
+// default: one walk; a frame with more requests than slots reports status 4
+// and the caller walks twice).
+// One block per frame: the block (one wave) stages an 8 KB window of the payload in LDS
 // (coalesced), one lane walks the top-level fields inside it, and the window
 // moves to wherever the walk stops (a field header near the window's end, or
 // a request longer than the window, which is skipped without being read).
-static constexpr u32 kWireWin = 32768;
-__global__ __launch_bounds__(256) void k_wire_bounds(const u8* data, WireIn* fr, int pass,
+static constexpr u32 kWireWin = 8192;
+static constexpr u32 kWireWalkBlock = 64;
+__global__ __launch_bounds__(kWireWalkBlock) void k_wire_bounds(const u8* data, WireIn* fr, int pass,
                                                      WireMsgPos* pos) {
   __shared__ __attribute__((aligned(16))) u8 s_buf[kWireWin + 16];
   __shared__ u64 s_at, s_base, s_nm;
@@ -456,15 +458,11 @@ __global__ __launch_bounds__(256) void k_wire_bounds(const u8* data, WireIn* fr,
     const u32 sh = (u32)((p + base) - a0);
     const u64 avail = n - base < kWireWin - sh ? n - base : kWireWin - sh;
     const u32 nw = (u32)((sh + avail + 15) / 16);
-#ifdef RBE_WIRE_BYTE_WIN
-    for (u32 j = threadIdx.x; j < nw * 16; j += 256) s_buf[j] = a0[j];
-#else
 #pragma unroll
-    for (u32 it = 0; it < kWireWin / 16 / 256; it++) {
-      const u32 wi = it * 256 + threadIdx.x;
+    for (u32 it = 0; it < kWireWin / 16 / kWireWalkBlock; it++) {
+      const u32 wi = it * kWireWalkBlock + threadIdx.x;
       if (wi < nw) ((uint4*)s_buf)[wi] = ((const uint4*)a0)[wi];
     }
-#endif
     __syncthreads();
     if (threadIdx.x == 0) {
       u64 i = base, nm = s_nm;
@@ -515,7 +513,8 @@ __global__ __launch_bounds__(256) void k_wire_bounds(const u8* data, WireIn* fr,
                 break;
               }
               if ((tg >> 3) == 1) {
-                if (pass) pos[f.msg0 + nm] = WireMsgPos{f.offset + q, v};
+                if (pass == 1) pos[f.msg0 + nm] = WireMsgPos{f.offset + q, v};
+                else if (pass == 2 && nm < f.pos_cap) pos[f.pos0 + nm] = WireMsgPos{f.offset + q, v};
                 nm++;
               }
               i = q + v;
@@ -560,7 +559,8 @@ __global__ __launch_bounds__(256) void k_wire_bounds(const u8* data, WireIn* fr,
               break;
             }
             if (fn == 1) {
-              if (pass) pos[f.msg0 + nm] = WireMsgPos{f.offset + q, v};
+              if (pass == 1) pos[f.msg0 + nm] = WireMsgPos{f.offset + q, v};
+                else if (pass == 2 && nm < f.pos_cap) pos[f.pos0 + nm] = WireMsgPos{f.offset + q, v};
               nm++;
             }
             q += v;
@@ -584,9 +584,20 @@ __global__ __launch_bounds__(256) void k_wire_bounds(const u8* data, WireIn* fr,
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    if (s_state == 2) fr[blockIdx.x].status = 3;
-    else if (!pass) fr[blockIdx.x].n_msgs = (u32)s_nm;
+    if (s_state == 2) {
+      fr[blockIdx.x].status = 3;
+    } else if (pass != 1) {
+      fr[blockIdx.x].n_msgs = (u32)s_nm;
+      if (pass == 2 && s_nm > f.pos_cap) fr[blockIdx.x].status = 4;
+    }
   }
+}
+
+// a frame's single-pass positions to their place in request order
+__global__ __launch_bounds__(256) void k_wire_compact(const WireIn* fr, const WireMsgPos* pos,
+                                                      WireMsgPos* out) {
+  const WireIn f = fr[blockIdx.x];
+  for (u32 j = threadIdx.x; j < f.n_msgs; j += 256) out[f.msg0 + j] = pos[f.pos0 + j];
 }
 
 // pass 0: entries and Cmd bytes of each message; pass 1: the records

@@ -83,3 +83,19 @@ def test_gpu_wire_decode_rejects_corruption(gpu_available):
     # the oracle reads the same frames
     assert len(W.frames_decode(stream)) == 6
     eng.close()
+
+
+def test_gpu_wire_decode_dense_requests(gpu_available):
+    """Requests shorter than 16 bytes (here empty Messages, valid protobuf)
+    overflow the single-pass position slots: the decoder walks the frame again
+    and still returns every request, in order (MessageBatch.Unmarshal)."""
+    eng = _engine(**C2)
+    eng.run(2)
+    payload = b"\x0a\x00" * 100 + b"\x0a\x04\x08\x11\x10\x02" + b"\x10\x05\x1a\x01a\x20\x01"
+    stream = W.frame(payload)
+    msgs, ents, cmd = eng.wire_decode(stream)
+    ref = W.batch_decode(W.frames_decode(stream)[0])["requests"]
+    assert len(msgs) == len(ref) == 101 and not ents and not cmd
+    assert [(m.type, m.to) for m in msgs] == [(r[0]["type"], r[0]["to"]) for r in ref]
+    assert (msgs[-1].type, msgs[-1].to) == (0x11, 2)
+    eng.close()
