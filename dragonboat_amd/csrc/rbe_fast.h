@@ -28,6 +28,11 @@
 #pragma once
 #include "rbe_step.h"
 
+// the fast leader step takes check-quorum ticks whose quorum holds (A/B knob)
+#ifndef RBE_FAST_CQ
+#define RBE_FAST_CQ 1
+#endif
+
 namespace rbe {
 
 // Diagnostic build only (-DRBE_PHASE_TIMING, scripts/phase_timing.sh): per-wave
@@ -671,6 +676,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   u64 (*s_in_a)[1] = nullptr, (*s_in_b)[1] = nullptr;
   const u32 lds_lane = 0;
 #endif
+  u32 resp = 0;  // bit j: inbound sender j (slot order without k) sent something
 #pragma unroll
   for (u32 j = 0; j + 1 < N; j++) {
 #pragma unroll
@@ -680,6 +686,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
       inc[j][i].a = t == M_ReplicateResp ? in[j][i].log_index : in[j][i].hint;
       inc[j][i].b = in[j][i].hint_high;
       if (t == 0xFFu) continue;  // no message in this slot
+      resp |= 1u << j;
       if (t != M_ReplicateResp && t != M_HeartbeatResp) return false;
       if (in[j][i].term != c.term) return false;
       if (t == M_ReplicateResp && (in[j][i].w >> 24)) return false;  // rejection: decreaseTo
@@ -712,7 +719,21 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
     const bool idle = n_in == 0 && inp == 0;
     const bool q_at_tick = idle && C.quiesce &&
                            (q.qs > 0 || (q.tick + 1u - q.nas > C.election_rtt * 20));
-    if (C.check_quorum && !q_at_tick && h.election_tick + 1u >= C.election_rtt) return false;
+    if (C.check_quorum && !q_at_tick && h.election_tick + 1u >= C.election_rtt) {
+      // the tick reaches the check-quorum boundary: leaderHasQuorum (raft.go:
+      // 378-388) counts self and the remotes active at the tick, i.e. active
+      // now or answering in this round's inbox (both response handlers
+      // setActive first).  Only a quorum that holds stays on the fast path.
+      if (!RBE_FAST_CQ) return false;
+      u32 act = 1;
+#pragma unroll
+      for (u32 s = 0; s < N; s++) {
+        if (s == k) continue;
+        const u32 j = s - (s > k ? 1u : 0u);
+        act += ((st[s] >> 2) & 1u) | ((resp >> j) & 1u);
+      }
+      if (act < N / 2 + 1) return false;
+    }
   }
   // ---- compute.  Every load above has completed before the first store
   // below: vmcnt counts loads and stores in order, so a wait for a load still
@@ -1105,7 +1126,20 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   } else {
     flags &= (u8)~HF_RAFT_QUIESCE;
     etick++;  // leaderTick
-    if (etick >= C.election_rtt) etick = 0;  // check-quorum boundary excluded above
+    if (etick >= C.election_rtt) {
+      etick = 0;
+      if (C.check_quorum) {
+        // handleLeaderCheckQuorum with the quorum eligibility established:
+        // leaderHasQuorum clears the active flag of everything it counted
+#pragma unroll
+        for (u32 s = 0; s < N; s++) {
+          if (st[s] & 4u) {
+            st[s] &= ~4u;
+            rdirty |= 1u << s;
+          }
+        }
+      }
+    }
     htick++;
     if (htick >= C.heartbeat_rtt) {
       htick = 0;
