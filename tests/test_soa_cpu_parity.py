@@ -79,3 +79,15 @@ def test_sleeping_groups_wake_on_input():
     assert eng.sleeping_groups() == 8
     bad = counters_match(eng.counters(), ref.counters())
     assert not bad, f"counters differ {bad}"
+
+
+def test_check_quorum_ticks_stay_on_fast_path():
+    """With CheckQuorum, a leader's tick at the election-timeout boundary runs
+    leaderHasQuorum (raft.go:378-388); when the quorum holds the fast leader
+    step takes it (rbe_fast.h), so a steady C3 group leaves the fast kernels
+    only for its first election."""
+    kw = dict(C3, iso_period=0)
+    eng = SoaCpu(trace=True, ring=128, **kw)
+    ref = O.Harness(**kw)
+    assert run_lockstep(eng, ref, 300, every=1) is None
+    assert eng.slow_total() < 0.03 * eng.counters()["steps"]
