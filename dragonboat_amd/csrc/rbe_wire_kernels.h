@@ -200,6 +200,7 @@ __global__ __launch_bounds__(256) void k_wire_trailers(Params C, WireArgs A, Wir
 // crc32 of [p, p + n) by one lane, reading 16-B aligned words (the bytes
 // outside [p, p + n) of the first and last word are read, not used)
 __device__ u32 crc32_words(u32 crc, const u8* p, u64 n, const u32* table) {
+  // table: 4 x 256 (slicing-by-4: table[k][i] = crc of byte i followed by k zeros)
   if (!n) return crc;
   u32 c = ~crc;
   const u8* a = (const u8*)((u64)p & ~15ull);
@@ -208,14 +209,35 @@ __device__ u32 crc32_words(u32 crc, const u8* p, u64 n, const u32* table) {
   while (left) {
     const uint4 w = *(const uint4*)a;
     const u32 ws[4] = {w.x, w.y, w.z, w.w};
-    for (; o < 16 && left; o++, left--) {
-      const u8 b = (u8)(ws[o >> 2] >> (8 * (o & 3)));
-      c = table[(c ^ b) & 0xFFu] ^ (c >> 8);
+    if (o == 0 && left >= 16) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const u32 x = c ^ ws[q];
+        c = table[768 + (x & 0xFFu)] ^ table[512 + ((x >> 8) & 0xFFu)] ^
+            table[256 + ((x >> 16) & 0xFFu)] ^ table[x >> 24];
+      }
+      left -= 16;
+    } else {
+      for (; o < 16 && left; o++, left--) {
+        const u8 b = (u8)(ws[o >> 2] >> (8 * (o & 3)));
+        c = table[(c ^ b) & 0xFFu] ^ (c >> 8);
+      }
     }
     a += 16;
     o = 0;
   }
   return ~c;
+}
+
+// the 4 x 256 slicing table in LDS (one block of 256 threads)
+__device__ __forceinline__ void crc_tables_lds(u32* t) {
+  const u32 i = threadIdx.x;
+  u32 v = crc_table_entry(i);
+  t[i] = v;
+  for (int k = 1; k < 4; k++) {
+    v = (v >> 8) ^ crc_table_entry(v & 0xFFu);
+    t[256 * k + i] = v;
+  }
 }
 
 // crc32 of [p, p + n) by this block: one contiguous segment per thread, the
@@ -240,8 +262,8 @@ __device__ u32 block_crc32(const u8* p, u64 n, const u32* table, const u32* x2n,
 }
 
 __global__ __launch_bounds__(256) void k_wire_crc(WireBufs B, u8* out) {
-  __shared__ u32 s_table[256], s_x2n[32], s_crc[256];
-  s_table[threadIdx.x] = crc_table_entry(threadIdx.x);
+  __shared__ u32 s_table[1024], s_x2n[32], s_crc[256];
+  crc_tables_lds(s_table);
   if (threadIdx.x == 0) crc_x2n_table(s_x2n);
   __syncthreads();
   const WireFrame f = B.frames[blockIdx.x];
@@ -264,8 +286,8 @@ struct WireIn {  // one inbound frame
 };
 
 __global__ __launch_bounds__(256) void k_wire_verify(const u8* data, WireIn* fr) {
-  __shared__ u32 s_table[256], s_x2n[32], s_crc[256];
-  s_table[threadIdx.x] = crc_table_entry(threadIdx.x);
+  __shared__ u32 s_table[1024], s_x2n[32], s_crc[256];
+  crc_tables_lds(s_table);
   if (threadIdx.x == 0) crc_x2n_table(s_x2n);
   __syncthreads();
   WireIn f = fr[blockIdx.x];
