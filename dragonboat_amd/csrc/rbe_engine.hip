@@ -214,6 +214,20 @@ __global__ __launch_bounds__(kBlock) void k_relaunch(Planes P, Params C, const L
   P.gwake[x.replica / N] = GW_AWAKE;
 }
 
+// the lowest live payload-heap position (rbe_host.h heap_low_group): one lane
+// per group, a wave minimum, one 64-bit atomicMin per wave
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_heap_low(Planes P, Params C, u32 round, u64* out) {
+  const u64 g = (u64)blockIdx.x * kBlock + threadIdx.x;
+  u64 lo = g < C.n_groups ? heap_low_group<N>(P, C, g, round) : ~0ull;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const u64 y = __shfl_xor(lo, o, 64);
+    lo = y < lo ? y : lo;
+  }
+  if ((threadIdx.x & 63u) == 0 && lo != ~0ull) atomicMin((unsigned long long*)out, lo);
+}
+
 __global__ void k_advance(u32* clk, u32 k) {
   clk[0] += k;
   clk[1] += k;
@@ -322,6 +336,9 @@ struct rbe_engine {
   u64 in_bytes = 0;          // capacity of both
   hipEvent_t in_ev = nullptr;  // the last upload out of in_pinned has finished
   u8* heap = nullptr;        // payload heap (cfg.heap_bytes; positions in hin.heap)
+  u64* heap_dev = nullptr;   // [0] heap head after the last upload (Planes::heap_head),
+                             // [1] k_heap_low result
+  u64 heap_head_host = 0;    // source of [0]
   u32 scan_at = 0;           // host copy of Lists::scan_round (the source of its upload)
   // rbe_collect_outputs: device scratch and the pinned host copy it returns
   u8* out_dev = nullptr;
@@ -329,15 +346,30 @@ struct rbe_engine {
   u8* out_host = nullptr;
   u64 out_host_bytes = 0;
   // rbe_wire_encode / rbe_wire_decode scratch
-  u8* wire_dev = nullptr;    // encoded frames (encode) / inbound bytes (decode)
+  u8* wire_dev = nullptr;    // the last rbe_wire_encode's frames (rbe_wire_fetch)
   u64 wire_dev_bytes = 0;
   u8* wire_meta = nullptr;   // cells, batches, frame index
   u64 wire_meta_bytes = 0;
   u8* wire_rec = nullptr;    // decoded records
   u64 wire_rec_bytes = 0;
+  u8* wire_in = nullptr;     // rbe_wire_decode: inbound bytes and per-frame scratch
+  u64 wire_in_bytes = 0;
   u64 wire_totals[4] = {0, 0, 0, 0};
   u64 wire_frames_off = 0;   // frame index inside wire_meta
 };
+
+
+// Copy `len` bytes at offset `off` of the heap record at absolute position
+// `pos`: still staged, from the host copy; else from the device after every
+// queued round (RBE_E_STATE once a later lap of the ring has overwritten them).
+static int read_heap(rbe_engine* e, u64 pos, u64 off, u64 len, u8* dst) {
+  const HostHeap& h = e->hin.heap;
+  if (!h.valid(pos, off + len)) return RBE_E_STATE;
+  if (h.read_staged(pos, off, len, dst)) return RBE_OK;
+  HIP_OK(hipMemcpyAsync(dst, e->heap + (pos + off) % h.cap, len, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return RBE_OK;
+}
 
 
 static constexpr int kPlaneAllocs = 22;
@@ -419,9 +451,9 @@ static int make_params(const rbe_config* cfg, Params* out) {
   C.rep_world = cfg->rep_world > 1 ? cfg->rep_world : 1;
   C.rep_rank = cfg->rep_rank;
   if (C.rep_world > kXchgMaxWorld || C.rep_rank >= C.rep_world) return RBE_E_INVALID;
-  // replica-per-GPU mode: the fault schedule needs every replica's role and
-  // host-pushed inputs are per replica; both stay group-per-GPU features
-  if (C.rep_world > 1 && (C.iso_period || C.ext_inputs)) return RBE_E_INVALID;
+  // replica-per-GPU mode: the fault schedule needs every replica's role, which
+  // a rank does not have for the replicas it does not step
+  if (C.rep_world > 1 && C.iso_period) return RBE_E_INVALID;
   C.ext_apply = cfg->ext_apply;
   if (C.ext_apply && !C.ext_inputs) return RBE_E_INVALID;  // applied comes from rbe_notify_applied
   C.in_cap = cfg->in_cap ? cfg->in_cap : (u32)(cfg->n_groups > 1024 ? cfg->n_groups : 1024);
@@ -434,6 +466,9 @@ static int make_params(const rbe_config* cfg, Params* out) {
   C.snapshot_entries = cfg->snapshot_entries;
   C.compaction_overhead = cfg->compaction_overhead;
   if (C.snapshot_entries && C.ext_apply) return RBE_E_INVALID;
+  // the compaction of a snapshot at index i reads Term(i - CompactionOverhead),
+  // which must still be in the in-memory window
+  if (C.snapshot_entries && C.compaction_overhead >= C.ring) return RBE_E_INVALID;
   // the payload heap holds host-pushed Cmds longer than 16 bytes
   C.heap_bytes = (cfg->heap_bytes + 255) & ~255ull;
   if (C.heap_bytes && !C.ext_inputs) return RBE_E_INVALID;
@@ -600,6 +635,7 @@ int rbe_destroy(rbe_engine* e) {
   if (e->wire_dev) HIP_IGNORE(hipFree(e->wire_dev));
   if (e->wire_meta) HIP_IGNORE(hipFree(e->wire_meta));
   if (e->wire_rec) HIP_IGNORE(hipFree(e->wire_rec));
+  if (e->wire_in) HIP_IGNORE(hipFree(e->wire_in));
   if (e->stream) HIP_IGNORE(hipStreamDestroy(e->stream));
   delete e;
   return RBE_OK;
@@ -673,12 +709,36 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   P.rem_snap = C.snapshot_entries ? (u64*)ptrs[21] : nullptr;
   HIP_IGNORE(hipMemsetAsync(P.gwake, GW_AWAKE, C.n_groups, e->stream));  // every group starts awake
   e->hin.init(C.n_rep, C.n, C.in_cap, C.heap_bytes);
+  e->hin.rep_world = C.rep_world;
+  e->hin.rep_rank = C.rep_rank;
   if (C.heap_bytes) {
-    if (hipMalloc(&e->heap, C.heap_bytes) != hipSuccess) {
+    if (hipMalloc(&e->heap, C.heap_bytes) != hipSuccess ||
+        hipMalloc(&e->heap_dev, 2 * sizeof(u64)) != hipSuccess) {
+      if (e->heap) e->allocs.push_back(e->heap);
       rbe_destroy(e);
       return RBE_E_NOMEM;
     }
     e->allocs.push_back(e->heap);
+    e->allocs.push_back(e->heap_dev);
+    HIP_IGNORE(hipMemsetAsync(e->heap_dev, 0, 2 * sizeof(u64), e->stream));
+    P.heap_head = e->heap_dev;
+    // the lowest live record, on demand (HostHeap::room)
+    e->hin.heap.low_fn = [e](u64* lo) -> int {
+      HIP_OK(hipSetDevice(e->device));
+      const u64 init = ~0ull;
+      HIP_OK(hipMemcpyAsync(e->heap_dev + 1, &init, sizeof(u64), hipMemcpyHostToDevice, e->stream));
+      int rc = dispatch_n(e->C.n, [&](auto NN) {
+        constexpr int N = decltype(NN)::value;
+        hipLaunchKernelGGL(k_heap_low<N>, dim3(grid_for(e->C.n_groups)), dim3(kBlock), 0,
+                           e->stream, e->P, e->C, e->round, e->heap_dev + 1);
+        HIP_OK(hipGetLastError());
+        return RBE_OK;
+      });
+      if (rc) return rc;
+      HIP_OK(hipMemcpyAsync(lo, e->heap_dev + 1, sizeof(u64), hipMemcpyDeviceToHost, e->stream));
+      HIP_OK(hipStreamSynchronize(e->stream));
+      return RBE_OK;
+    };
   }
   if (hipMalloc(&P.counters, kCtrWords * sizeof(u64)) != hipSuccess) {
     rbe_destroy(e);
@@ -802,6 +862,11 @@ static int flush_inputs(rbe_engine* e) {
     HIP_OK(hipMemcpyAsync(e->heap + at, h.heap.stage.data() + (p - h.heap.flushed), len,
                           hipMemcpyHostToDevice, e->stream));
     p += len;
+  }
+  if (h.heap.head != e->heap_head_host) {  // Planes::heap_head for the lapped-record checks
+    e->heap_head_host = h.heap.head;
+    HIP_OK(hipMemcpyAsync(e->heap_dev, &e->heap_head_host, sizeof(u64), hipMemcpyHostToDevice,
+                          e->stream));
   }
   const u64 n = h.reps.size(), na = h.app_rep.size();
   const u64 need = n * (sizeof(u64) + sizeof(ExtIn)) + na * 2 * sizeof(u64) + 64;
@@ -980,6 +1045,13 @@ int rbe_push_proposals(rbe_engine* e, uint64_t n, const uint64_t* replica, const
   return e->hin.push_proposals(n, replica, n_ents, type, cmd_len, cmd);
 }
 
+int rbe_propose_entries(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint32_t* n_ents,
+                        const rbe_entry* ents, const uint8_t* cmd) {
+  if (!e) return RBE_E_INVALID;
+  if (!e->C.ext_inputs) return RBE_E_STATE;
+  return e->hin.push_entries(n, replica, n_ents, ents, cmd);
+}
+
 int rbe_push_read_index(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint64_t* lo,
                         const uint64_t* hi) {
   if (!e) return RBE_E_INVALID;
@@ -1009,17 +1081,17 @@ int rbe_report_snapshot_status(rbe_engine* e, uint64_t n, const uint64_t* replic
 }
 
 int rbe_launch(rbe_engine* e, uint64_t n, const uint64_t* replica, const rbe_launch_state* st,
-               const rbe_entry* ents) {
+               const rbe_entry* ents, const uint8_t* cmd) {
   if (!e) return RBE_E_INVALID;
-  std::vector<u64> terms;
-  std::vector<Body> bodies;
-  int rc = launch_rows(e->C, n, replica, st, ents, terms, bodies);
-  if (rc || n == 0) return rc;
-  {  // one replica at most once
+  if (n && replica) {  // one replica at most once
     std::vector<u64> v(replica, replica + n);
     std::sort(v.begin(), v.end());
     if (std::adjacent_find(v.begin(), v.end()) != v.end()) return RBE_E_INVALID;
   }
+  std::vector<u64> terms;
+  std::vector<Body> bodies;
+  int rc = launch_rows(e->C, e->hin.heap, n, replica, st, ents, cmd, terms, bodies);
+  if (rc || n == 0) return rc;
   HIP_OK(hipSetDevice(e->device));
   std::vector<LaunchRec> rec(n);
   u64 off = 0;
@@ -1089,7 +1161,9 @@ int rbe_xchg_record_bytes(uint64_t* out3) {
 
 int rbe_xchg_pack(rbe_engine* e, void* buf, const uint64_t* cap3, uint32_t* counts) {
   if (!e || !buf || !cap3 || !counts || e->round == 0) return RBE_E_INVALID;
-  if (e->C.rep_world <= 1) return RBE_E_STATE;
+  // heap positions are this engine's: entries cross engines through
+  // rbe_get_outbox / rbe_push_messages, which carry their bytes
+  if (e->C.rep_world <= 1 || e->C.heap_bytes) return RBE_E_STATE;
   HIP_OK(hipSetDevice(e->device));
   XchgCaps caps;
   for (u32 t = 0; t < XS_NUM; t++) caps.cap[t] = cap3[t];
@@ -1118,7 +1192,7 @@ int rbe_xchg_chunk_bytes(const uint64_t* cap3, uint64_t* bytes) {
 
 int rbe_xchg_pack_fixed(rbe_engine* e, void* buf, const uint64_t* cap3) {
   if (!e || !buf || !cap3 || e->round == 0) return RBE_E_INVALID;
-  if (e->C.rep_world <= 1) return RBE_E_STATE;
+  if (e->C.rep_world <= 1 || e->C.heap_bytes) return RBE_E_STATE;
   HIP_OK(hipSetDevice(e->device));
   XchgCaps caps;
   for (u32 t = 0; t < XS_NUM; t++) caps.cap[t] = cap3[t];
@@ -1200,7 +1274,8 @@ int rbe_xchg_unpack(rbe_engine* e, const void* cnt, uint64_t n_cnt, const void* 
 }
 
 int rbe_get_outbox(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t cap,
-                   uint32_t* n_out, rbe_entry* ents, uint32_t ent_cap, uint32_t* n_ents) {
+                   uint32_t* n_out, rbe_entry* ents, uint32_t ent_cap, uint32_t* n_ents,
+                   uint8_t* cmd, uint64_t cmd_cap, uint64_t* cmd_bytes) {
   if (!e || !n_out || !n_ents || replica >= e->C.n_rep || e->round == 0) return RBE_E_INVALID;
   HIP_OK(hipSetDevice(e->device));
   const u32 N = e->C.n, par = (e->round - 1) & 1u;
@@ -1216,16 +1291,18 @@ int rbe_get_outbox(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t c
   HIP_OK(hipMemcpyAsync(arena.data(), e->P.arena[par] + replica * e->C.ecap,
                         arena.size() * sizeof(Ent), hipMemcpyDeviceToHost, e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
-  return dispatch_n(N, [&](auto NN) {
+  auto rd = [e](u64 pos, u64 off, u64 len, u8* dst) { return read_heap(e, pos, off, len, dst); };
+  const int rc = dispatch_n(N, [&](auto NN) {
     constexpr int NC = decltype(NN)::value;
-    outbox_messages<NC>(e->C, g, k, row, e->round, lst.data(), arena.data(), out, cap, ents,
-                        ent_cap, n_out, n_ents);
-    return RBE_OK;
+    return outbox_messages<NC>(e->C, g, k, row, e->round, lst.data(), arena.data(), out, cap, ents,
+                               ent_cap, n_out, n_ents, cmd, cmd_cap, cmd_bytes, rd);
   });
+  HIP_OK(hipStreamSynchronize(e->stream));  // heap reads
+  return rc;
 }
 
 int rbe_push_messages(rbe_engine* e, uint64_t n, const uint64_t* group, const rbe_message* msgs,
-                      const rbe_entry* ents) {
+                      const rbe_entry* ents, const uint8_t* cmd) {
   if (!e || e->round == 0 || (n && (!group || !msgs))) return RBE_E_INVALID;
   if (e->C.rep_world <= 1) return RBE_E_STATE;  // every sender is stepped here
   HIP_OK(hipSetDevice(e->device));
@@ -1234,7 +1311,8 @@ int rbe_push_messages(rbe_engine* e, uint64_t n, const uint64_t* group, const rb
   std::vector<XEnt> x;
   int rc = dispatch_n(e->C.n, [&](auto NN) {
     constexpr int N = decltype(NN)::value;
-    return messages_to_records<N>(e->C, e->round, n, group, msgs, ents, c, m, x);
+    return messages_to_records<N>(e->C, e->hin.heap, e->round, n, group, msgs, ents, cmd, c, m,
+                                  x);
   });
   if (rc) return rc;
   const size_t bytes = c.size() * sizeof(XCnt) + m.size() * sizeof(XMsg) + x.size() * sizeof(XEnt);
@@ -1553,14 +1631,7 @@ static int read_window(rbe_engine* e, u64 replica, u64 lo, u64 hi, std::vector<u
   return RBE_OK;
 }
 
-// Copy `len` heap bytes at absolute position `pos` (RBE_E_STATE once a later
-// lap of the ring has overwritten them).
-static int read_heap(rbe_engine* e, u64 pos, u64 len, u8* dst) {
-  if (!e->hin.heap.valid(pos, len)) return RBE_E_STATE;
-  HIP_OK(hipMemcpyAsync(dst, e->heap + pos % e->hin.heap.cap, len, hipMemcpyDeviceToHost,
-                        e->stream));
-  return RBE_OK;
-}
+
 
 int rbe_get_entries(rbe_engine* e, uint64_t replica, uint64_t lo, uint64_t hi, rbe_entry* out) {
   if (!e || !out) return RBE_E_INVALID;
@@ -1568,20 +1639,22 @@ int rbe_get_entries(rbe_engine* e, uint64_t replica, uint64_t lo, uint64_t hi, r
   std::vector<Body> b;
   int rc = read_window(e, replica, lo, hi, t, b);
   if (rc) return rc;
+  auto rd = [e](u64 pos, u64 off, u64 len, u8* dst) { return read_heap(e, pos, off, len, dst); };
   for (u64 i = lo; i <= hi; i++) {
     const Body& x = b[i - lo];
     rbe_entry& o = out[i - lo];
     memset(&o, 0, sizeof(o));
-    o.index = i;
-    o.term = t[i - lo];
-    o.type = x.type;
-    o.cmd_len = x.len;
-    if (x.len <= 16) {
-      memcpy(o.cmd, &x.lo, 8);
-      memcpy(o.cmd + 8, &x.hi, 8);
-    } else if ((rc = read_heap(e, x.hi, 16, o.cmd))) {
+    Ent en;
+    en.term = t[i - lo];
+    en.type = x.type;
+    en.len = x.len;
+    en.lo = x.lo;
+    en.hi = x.hi;
+    if ((rc = entry_out(en, &o, nullptr, rd))) {
+      HIP_IGNORE(hipStreamSynchronize(e->stream));
       return rc;
     }
+    o.index = i;
   }
   HIP_OK(hipStreamSynchronize(e->stream));
   return RBE_OK;
@@ -1604,12 +1677,13 @@ int rbe_get_entry_cmds(rbe_engine* e, uint64_t replica, uint64_t lo, uint64_t hi
   for (u64 i = 0; i < b.size(); i++) {
     const Body& x = b[i];
     u8* d = buf + offsets[i];
-    if (x.len <= 16) {
+    if (!ent_heap(x.type)) {
       u8 w[16];
       memcpy(w, &x.lo, 8);
       memcpy(w + 8, &x.hi, 8);
       memcpy(d, w, x.len);
-    } else if ((rc = read_heap(e, x.hi, x.len, d))) {
+    } else if (x.len && (rc = read_heap(e, x.hi, kHeapHdr, x.len, d))) {
+      HIP_IGNORE(hipStreamSynchronize(e->stream));
       return rc;
     }
   }
@@ -1654,6 +1728,9 @@ int rbe_wire_encode(rbe_engine* e, const rbe_wire_config* wc, uint64_t totals[4]
   A.nchunks = (u32)((C.n_groups + gpb - 1) / gpb);
   A.npairs = C.n * (C.n - 1);
   A.round = e->round;
+  // the device heap holds the positions below `flushed` (records staged since
+  // the last step are never in the last round's outbox)
+  A.heap_head = e->hin.heap.flushed;
   for (u32 k = 0; k < C.n; k++) {
     const char* s = wc->source_address[k];
     const size_t l = s ? strlen(s) : 0;
@@ -1670,22 +1747,26 @@ int rbe_wire_encode(rbe_engine* e, const rbe_wire_config* wc, uint64_t totals[4]
   int rc = grow(&e->wire_meta, &e->wire_meta_bytes, o_tot + 64, false);
   if (rc) return rc;
   u8* m = e->wire_meta;
+  HIP_OK(hipMemsetAsync(m + o_tot, 0, 64, e->stream));
   WireBufs B{(u32*)m, (u32*)(m + o_msgs), (u32*)(m + o_off), (u64*)(m + o_pay), (u32*)(m + o_bm),
              (u32*)(m + o_bi), (u64*)(m + o_fo), (WireFrame*)(m + o_fr), (u64*)(m + o_tot)};
   e->wire_frames_off = o_fr;
   const unsigned gc = (unsigned)((ncell + 255) / 256);
   rc = dispatch_n(C.n, [&](auto NN) {
     constexpr int N = decltype(NN)::value;
-    hipLaunchKernelGGL((k_wire_size<N>), dim3(gc), dim3(256), 0, e->stream, e->P, C, A, B);
+    hipLaunchKernelGGL((k_wire_size<N>), dim3(gc), dim3(256), 0, e->stream, e->P, C, A, B,
+                       (const u8*)e->heap);
     return RBE_OK;
   });
   if (rc) return rc;
   hipLaunchKernelGGL(k_wire_batch, dim3((unsigned)nbatch), dim3(256), 0, e->stream, C, A, B);
   hipLaunchKernelGGL(k_wire_frames, dim3(1), dim3(256), 0, e->stream, C, A, B, (u32)nbatch);
   HIP_OK(hipGetLastError());
-  u64 tot[4];
+  u64 tot[5];
   HIP_OK(hipMemcpyAsync(tot, B.totals, sizeof(tot), hipMemcpyDeviceToHost, e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
+  memset(e->wire_totals, 0, sizeof(e->wire_totals));
+  if (tot[4]) return RBE_E_STATE;  // an entry's heap record was overwritten: no frames
   rc = grow(&e->wire_dev, &e->wire_dev_bytes, tot[0] + 64, false);
   if (rc) return rc;
   if (tot[1]) {
@@ -1758,15 +1839,15 @@ int rbe_wire_decode(rbe_engine* e, const void* data, uint64_t bytes, rbe_message
     slots += w.pos_cap;
   }
   const u64 o_fr = al(bytes), o_sp = o_fr + al(nf * sizeof(WireIn));
-  int rc = grow(&e->wire_dev, &e->wire_dev_bytes, o_sp + al(slots * sizeof(WireMsgPos)), false);
+  int rc = grow(&e->wire_in, &e->wire_in_bytes, o_sp + al(slots * sizeof(WireMsgPos)), false);
   if (rc) return rc;
-  WireIn* dfr = (WireIn*)(e->wire_dev + o_fr);
-  WireMsgPos* spos = (WireMsgPos*)(e->wire_dev + o_sp);
-  HIP_OK(hipMemcpyAsync(e->wire_dev, data, bytes, hipMemcpyHostToDevice, e->stream));
+  WireIn* dfr = (WireIn*)(e->wire_in + o_fr);
+  WireMsgPos* spos = (WireMsgPos*)(e->wire_in + o_sp);
+  HIP_OK(hipMemcpyAsync(e->wire_in, data, bytes, hipMemcpyHostToDevice, e->stream));
   HIP_OK(hipMemcpyAsync(dfr, fr.data(), nf * sizeof(WireIn), hipMemcpyHostToDevice, e->stream));
-  hipLaunchKernelGGL(k_wire_verify, dim3((unsigned)nf), dim3(256), 0, e->stream, e->wire_dev, dfr);
+  hipLaunchKernelGGL(k_wire_verify, dim3((unsigned)nf), dim3(256), 0, e->stream, e->wire_in, dfr);
   hipLaunchKernelGGL(k_wire_bounds, dim3((unsigned)nf), dim3(kWireWalkBlock), 0, e->stream,
-                     e->wire_dev, dfr, 2, spos);
+                     e->wire_in, dfr, 2, spos);
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(fr.data(), dfr, nf * sizeof(WireIn), hipMemcpyDeviceToHost, e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
@@ -1798,13 +1879,13 @@ int rbe_wire_decode(rbe_engine* e, const void* data, uint64_t bytes, rbe_message
   HIP_OK(hipMemsetAsync(err, 0, 4, e->stream));
   if (refill)
     hipLaunchKernelGGL(k_wire_bounds, dim3((unsigned)nf), dim3(kWireWalkBlock), 0, e->stream,
-                       e->wire_dev, dfr, 1, pos);
+                       e->wire_in, dfr, 1, pos);
   else
     hipLaunchKernelGGL(k_wire_compact, dim3((unsigned)nf), dim3(256), 0, e->stream, dfr, spos,
                        pos);
   const unsigned gm = (unsigned)nbk;
   if (tm) {
-    hipLaunchKernelGGL(k_wire_parse, dim3(gm), dim3(256), 0, e->stream, e->wire_dev, pos, tm, 0,
+    hipLaunchKernelGGL(k_wire_parse, dim3(gm), dim3(256), 0, e->stream, e->wire_in, pos, tm, 0,
                        ec, cc, nullptr, nullptr, nullptr, err);
     hipLaunchKernelGGL(k_scan_blocks, dim3(gm), dim3(256), 0, e->stream, ec, tm, t1);
     hipLaunchKernelGGL(k_scan_blocks, dim3(gm), dim3(256), 0, e->stream, cc, tm, t2);
@@ -1852,7 +1933,7 @@ int rbe_wire_decode(rbe_engine* e, const void* data, uint64_t bytes, rbe_message
   rbe_entry* de = (rbe_entry*)(w + o_e);
   u8* dc = w + o_c;
   if (tm)
-    hipLaunchKernelGGL(k_wire_parse, dim3(gm), dim3(256), 0, e->stream, e->wire_dev, pos, tm, 1,
+    hipLaunchKernelGGL(k_wire_parse, dim3(gm), dim3(256), 0, e->stream, e->wire_in, pos, tm, 1,
                        ec, cc, dm, de, dc, err);
   HIP_OK(hipGetLastError());
   if (tm) HIP_OK(hipMemcpyAsync(msgs, dm, tm * sizeof(rbe_message), hipMemcpyDeviceToHost, e->stream));

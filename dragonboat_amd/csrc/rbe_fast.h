@@ -223,9 +223,9 @@ struct FastOut {
         const Ent e = ent[i];
         h = hfold(h, m.type == M_Replicate ? m.log_index + 1 + i : 0);
         h = hfold(h, e.term);
-        h = hfold(h, (u64)e.type | ((u64)e.len << 32));
+        h = hfold(h, ent_word(e.type, e.len));
         h = hfold(h, e.lo);
-        h = hfold(h, cmd_hi(e.len, e.hi));
+        h = hfold(h, cmd_hi(e.type, e.hi));
       }
       msg_hash = h;
     }
@@ -429,9 +429,9 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
       const Body b = P.pay_ring[s];
       apply_hash = hfold(apply_hash, i);
       apply_hash = hfold(apply_hash, P.term_ring[s]);
-      apply_hash = hfold(apply_hash, (u64)b.type | ((u64)b.len << 32));
+      apply_hash = hfold(apply_hash, ent_word(b.type, b.len));
       apply_hash = hfold(apply_hash, b.lo);
-      apply_hash = hfold(apply_hash, cmd_hi(b.len, b.hi));
+      apply_hash = hfold(apply_hash, cmd_hi(b.type, b.hi));
     }
   }
   if (u.apply_hi >= u.apply_lo) ctr.v[C_ENT_APPLIED] += (u32)(u.apply_hi - u.apply_lo + 1);

@@ -14,6 +14,7 @@
 // first.
 #pragma once
 #include <cstring>
+#include <functional>
 #include <vector>
 
 #include "../../include/rbe.h"
@@ -35,21 +36,52 @@ inline u64 cmd_fingerprint(const u8* b, u64 len) {
   }
   return mix64(h ^ (len << 1));
 }
+// Fingerprint of a payload-heap record (ET_HEAP): the Cmd's, extended by the
+// session fields {Key, ClientID, SeriesID, RespondedTo} when any is non-zero
+// (raft.pb.go:589-598; oracle/harness.cpp entry_fingerprint restates it).
+inline u64 entry_fingerprint(const u64* meta, const u8* cmd, u64 len) {
+  u64 h = cmd_fingerprint(cmd, len);
+  if (meta[0] | meta[1] | meta[2] | meta[3])
+    for (u64 i = 0; i < 4; i++) h = mix64(h ^ meta[i] ^ ((i + 1) << 60));
+  return h;
+}
+// An rbe_entry that needs a heap record: a Cmd longer than 16 bytes, or any
+// session field (requests.go:994-997 stamps them on every client proposal)
+inline bool entry_needs_heap(const rbe_entry& e) {
+  return e.cmd_len > 16 || (e.key | e.client_id | e.series_id | e.responded_to) != 0;
+}
+inline u64 heap_rec_bytes(u64 cmd_len) { return (kHeapHdr + cmd_len + 15) & ~15ull; }
 
 // Payload heap (cfg.heap_bytes): one device byte ring shared by every group.
-// A Cmd longer than 16 bytes is written there once, when its proposal is
-// staged, and every replica's log entry refers to it by (fingerprint, absolute
-// heap position) in Body/Ent lo/hi: a follower that appends the entry copies
-// the reference, never the bytes (the Log Matching property makes the bytes of
-// an (index, term) the same on every replica).  The host is the only writer,
-// so positions are assigned here, in push order.  Bytes at position p stay
-// valid while head <= p + cap (a later lap overwrites them); a reader of an
-// older entry gets RBE_E_STATE, the analog of ErrCompacted.
+// An entry with a Cmd longer than 16 bytes or session fields is written there
+// once, when it is staged, as a record {Key, ClientID, SeriesID, RespondedTo,
+// Cmd}; every replica's log entry refers to it by (fingerprint, absolute
+// position) in Body/Ent lo/hi with ET_HEAP in the type: a follower that
+// appends the entry copies the reference, never the bytes (the Log Matching
+// property makes the entry of an (index, term) the same on every replica).
+// The host is the only writer, so positions are assigned here, in push order.
+//
+// Lifetime.  The heap never laps a record some replica may still need: a push
+// that would overwrite one fails with RBE_E_NOMEM instead (the reference keeps
+// an entry until it is saved and applied, inmemory.go:116-166, and in LogDB
+// after that).  Live = referenced by an entry of some replica's log window
+// above its group's low mark min over the group's replicas of min(savedTo,
+// processed, applied) — what a replica of the group has not yet saved and
+// applied, including entries a lagging follower has not received — or by a
+// Propose in flight, or staged / uploaded by the last flush (`batch_lo`).  The
+// engine computes the lowest live position on demand (`low_fn`, a device
+// reduction), only when a push would cross the cached mark.  Bytes at a
+// position older than one lap are still refused to readers (RBE_E_STATE, as
+// ErrCompacted) and flagged F_WINDOW if a step ever tries to send them.
 struct HostHeap {
-  u64 cap = 0;      // bytes (0 = no heap: Cmd is at most 16 bytes)
-  u64 head = 0;     // next free absolute position
-  u64 flushed = 0;  // positions below this are on the device
+  u64 cap = 0;       // bytes (0 = no heap: Cmd is at most 16 bytes, no session fields)
+  u64 head = 0;      // next free absolute position
+  u64 flushed = 0;   // positions below this are on the device
+  u64 batch_lo = 0;  // first position of the last uploaded batch
+  u64 live_lo = 0;   // cached: no live record below it (0 = unknown)
   std::vector<u8> stage;  // bytes of [flushed, head), position flushed at index 0
+  // lowest position a live record of the device planes holds (~0 for none)
+  std::function<int(u64*)> low_fn;
   // reserve len bytes (16-B aligned, never split across the end of the ring)
   u64 alloc(u64 len) {
     u64 p = head;
@@ -58,7 +90,91 @@ struct HostHeap {
     return p;
   }
   bool valid(u64 pos, u64 len) const { return cap && pos + len <= head && head <= pos + cap; }
+  u64 floor() const { return live_lo < batch_lo ? live_lo : batch_lo; }
+  // room for `need` more bytes (alignment and the wrap skip included) without
+  // lapping a live record; refreshes the live mark once when the cached one is short
+  int room(u64 need) {
+    if (need > cap) return RBE_E_NOMEM;
+    if (head + need <= floor() + cap) return RBE_OK;
+    if (low_fn) {
+      u64 lo = ~0ull;
+      const int rc = low_fn(&lo);
+      if (rc) return rc;
+      live_lo = lo < head ? lo : head;
+    }
+    return head + need <= floor() + cap ? RBE_OK : RBE_E_NOMEM;
+  }
+  // stage one record; returns its position
+  u64 put_record(const u64* meta, const u8* cmd, u64 len) {
+    const u64 pos = alloc(kHeapHdr + len);
+    stage.resize(head - flushed, 0);
+    u8* d = stage.data() + (pos - flushed);
+    memcpy(d, meta, kHeapHdr);
+    if (len) memcpy(d + kHeapHdr, cmd, len);
+    return pos;
+  }
+  // `len` bytes of the record at `pos` from offset `off`, when still staged
+  // (not yet uploaded); false when the caller must read the device copy
+  bool read_staged(u64 pos, u64 off, u64 len, u8* dst) const {
+    if (pos < flushed) return false;
+    memcpy(dst, stage.data() + (pos - flushed) + off, len);
+    return true;
+  }
 };
+
+// Turn an rbe_entry with `cmd` (its Cmd bytes) into an arena/ring entry,
+// staging a heap record when it needs one; the caller checked heap.room.
+inline Ent stage_entry(HostHeap& heap, const rbe_entry& x, const u8* cmd) {
+  Ent e;
+  memset(&e, 0, sizeof(e));
+  e.term = x.term;
+  e.type = x.type & ET_TYPE_MASK;
+  e.len = x.cmd_len;
+  if (entry_needs_heap(x)) {
+    const u64 meta[4] = {x.key, x.client_id, x.series_id, x.responded_to};
+    e.type |= ET_HEAP;
+    e.lo = entry_fingerprint(meta, cmd, x.cmd_len);
+    e.hi = heap.put_record(meta, cmd, x.cmd_len);
+  } else {
+    u8 b[16];
+    memset(b, 0, sizeof(b));
+    if (x.cmd_len) memcpy(b, cmd, x.cmd_len);
+    memcpy(&e.lo, b, 8);
+    memcpy(&e.hi, b + 8, 8);
+  }
+  return e;
+}
+
+// The raftpb.Entry of a ring/arena entry, Index aside: type, Cmd length and
+// the first 16 Cmd bytes, session fields; `rd(pos, off, len, dst)` reads heap
+// record bytes (0, or RBE_E_STATE for an overwritten record).  With `cmd`
+// non-null the whole Cmd is copied there.
+template <typename RD>
+inline int entry_out(const Ent& x, rbe_entry* o, u8* cmd, RD&& rd) {
+  o->term = x.term;
+  o->type = ent_type(x.type);
+  o->cmd_len = x.len;
+  memset(o->cmd, 0, sizeof(o->cmd));
+  o->key = o->client_id = o->series_id = o->responded_to = 0;
+  if (!ent_heap(x.type)) {
+    u8 w[16];
+    memcpy(w, &x.lo, 8);
+    memcpy(w + 8, &x.hi, 8);
+    memcpy(o->cmd, w, 16);
+    if (cmd) memcpy(cmd, w, x.len);
+    return RBE_OK;
+  }
+  u64 meta[4];
+  int rc = rd(x.hi, 0, kHeapHdr, (u8*)meta);
+  if (!rc && x.len) rc = rd(x.hi, kHeapHdr, x.len < 16 ? x.len : 16, o->cmd);
+  if (!rc && cmd && x.len) rc = rd(x.hi, kHeapHdr, x.len, cmd);
+  if (rc) return rc;
+  o->key = meta[0];
+  o->client_id = meta[1];
+  o->series_id = meta[2];
+  o->responded_to = meta[3];
+  return RBE_OK;
+}
 
 // One staged replica-value pair into the planes (k_ext_scatter does the same)
 RBE_HD void apply_pair(const Planes& P, u64 rep, u64 val) {
@@ -70,8 +186,57 @@ RBE_HD void apply_pair(const Planes& P, u64 rep, u64 val) {
   }
 }
 
-// Check an rbe_launch batch whole (rbe.h) and turn its entries into ring rows
-// (terms, bodies) in batch order; 0 or RBE_E_INVALID.
+// The lowest payload-heap position the replicas of group g that this engine
+// steps may still need (~0 for none), for HostHeap::room: the records of
+// log-window entries above the group's low mark — min over those replicas of
+// min(savedTo, processed, applied), and of a leader's remote match values
+// (what its followers, here or behind the transport, have acknowledged) — and
+// of the entries the Proposes of the last round's outboxes forward.  `round` is
+// the round about to run.  One lane per group on the device (k_heap_low).
+template <int N>
+RBE_HD u64 heap_low_group(const Planes& P, const Params& C, u64 g, u32 round) {
+  u64 mark = ~0ull;
+  for (u32 k = 0; k < N; k++) {
+    if (C.rep_world > 1 && (g + k) % C.rep_world != C.rep_rank) continue;
+    const u64 r = g * N + k;
+    const Core c = P.core[r];
+    u64 m = c.saved_to < c.processed ? c.saved_to : c.processed;
+    if (C.ext_apply && P.applied[r] < m) m = P.applied[r];
+    if (P.hot[r].role == R_Leader)
+      for (u32 s = 0; s < N; s++)
+        if (s != k && P.rem[r * N + s].match < m) m = P.rem[r * N + s].match;
+    if (m < mark) mark = m;
+  }
+  u64 lo = ~0ull;
+  const u32 par = (round - 1u) & 1u;
+  for (u32 k = 0; k < N; k++) {
+    if (C.rep_world > 1 && (g + k) % C.rep_world != C.rep_rank) continue;
+    const u64 r = g * N + k;
+    const u64 last = P.core[r].last_index;
+    u64 from = last >= C.ring ? last - C.ring + 1 : 1;
+    if (mark + 1 > from) from = mark + 1;
+    for (u64 i = from; i <= last; i++) {
+      const Body b = P.pay_ring[(i & (u64)(C.ring - 1)) * C.n_rep + r];
+      if (ent_heap(b.type) && b.hi < lo) lo = b.hi;
+    }
+    if (round == 0) continue;
+    const CntRow row = P.cnt[par][r];
+    for (u32 d = 0; d < N; d++) {
+      const u32 nb = (row_word(row, d, round) >> 7) & 0x7Fu;
+      const Msg* lst = &P.msgs[par][((g * N + k) * N + d) * (u64)C.maxm];
+      for (u32 i = 0; i < nb; i++) {
+        const Msg m = lst[C.maxm - 1u - i];
+        if (m.type != M_Propose) continue;
+        for (u32 j = 0; j < m.n_ent && m.ent_off + j < C.ecap; j++) {
+          const Ent e = P.arena[par][r * C.ecap + m.ent_off + j];
+          if (ent_heap(e.type) && e.hi < lo) lo = e.hi;
+        }
+      }
+    }
+  }
+  return lo;
+}
+
 // rbe_get_snapshot_state row: marker, marker term, snapshot index, snapshot
 // term, reqSnapshotIndex, compactLogTo
 inline void snap_state_row(const SnapSt& s, u64* o) {
@@ -83,13 +248,40 @@ inline void snap_state_row(const SnapSt& s, u64* o) {
   o[5] = s.compact_to;
 }
 
-inline int launch_rows(const Params& C, u64 n, const u64* replica, const rbe_launch_state* st,
-                       const rbe_entry* ents, std::vector<u64>& terms, std::vector<Body>& bodies) {
+// Check a batch of entries whole: their types, and that the heap (if any
+// needs it) can take them; sets *need to the heap bytes.  `cmd` null: each
+// Cmd is the entry's inline cmd (at most 16 bytes).
+inline int check_entries(const HostHeap& heap, u64 total, const rbe_entry* ents, const u8* cmd,
+                         bool config_change_ok, u64* need) {
+  u64 big = 0, maxrec = 0;
+  for (u64 j = 0; j < total; j++) {
+    const rbe_entry& e = ents[j];
+    const u32 t = e.type;
+    if (t > E_Metadata || (t == E_ConfigChange && !config_change_ok)) return RBE_E_INVALID;
+    if (!cmd && e.cmd_len > 16) return RBE_E_INVALID;
+    if (!entry_needs_heap(e)) continue;
+    // a heap record takes at most a quarter of the heap (the ErrPayloadTooBig
+    // check of requests.go:989-991, node.go:366-367)
+    const u64 rb = heap_rec_bytes(e.cmd_len);
+    if (heap.cap == 0 || e.cmd_len > heap.cap / 4) return RBE_E_INVALID;
+    big += rb;
+    if (rb > maxrec) maxrec = rb;
+  }
+  // one wrap skip at most (the batch is below a lap)
+  *need = big ? big + maxrec : 0;
+  return RBE_OK;
+}
+
+// Check an rbe_launch batch whole (rbe.h) and turn its entries into ring rows
+// (terms, bodies) in batch order, staging heap records for the entries that
+// need one; 0, RBE_E_INVALID or RBE_E_NOMEM (heap full of live records).
+inline int launch_rows(const Params& C, HostHeap& heap, u64 n, const u64* replica,
+                       const rbe_launch_state* st, const rbe_entry* ents, const u8* cmd,
+                       std::vector<u64>& terms, std::vector<Body>& bodies) {
   if (n && (!replica || !st)) return RBE_E_INVALID;
   // a restart carries no LogDB snapshot / compaction marker (SnapSt) yet
   if (n && C.snapshot_entries) return RBE_E_INVALID;
   u64 total = 0;
-  std::vector<u8> seen;
   for (u64 i = 0; i < n; i++) {
     const rbe_launch_state& x = st[i];
     if (replica[i] >= C.n_rep || x.n_entries > C.ring || x.n_entries > x.last_index ||
@@ -102,21 +294,28 @@ inline int launch_rows(const Params& C, u64 n, const u64* replica, const rbe_lau
     const rbe_launch_state& x = st[i];
     for (u32 q = 0; q < x.n_entries; q++, j++) {
       const rbe_entry& e = ents[j];
-      if (e.index != x.last_index - x.n_entries + 1 + q || e.cmd_len > 16 || e.term > x.term)
-        return RBE_E_INVALID;
+      if (e.index != x.last_index - x.n_entries + 1 + q || e.term > x.term) return RBE_E_INVALID;
     }
   }
+  u64 need = 0;
+  int rc = check_entries(heap, total, ents, cmd, true, &need);
+  if (rc) return rc;
+  if (need && (rc = heap.room(need))) return rc;
   terms.resize(total);
   bodies.resize(total);
+  u64 off = 0;
   for (u64 j = 0; j < total; j++) {
     const rbe_entry& e = ents[j];
+    const Ent x = stage_entry(heap, e, cmd ? cmd + off : e.cmd);
+    if (cmd) off += e.cmd_len;
     terms[j] = e.term;
     Body& b = bodies[j];
-    b.type = e.type;
-    b.len = e.cmd_len;
-    memcpy(&b.lo, e.cmd, 8);
-    memcpy(&b.hi, e.cmd + 8, 8);
+    b.type = x.type;
+    b.len = x.len;
+    b.lo = x.lo;
+    b.hi = x.hi;
   }
+  heap.live_lo = 0;  // restarted replicas may need older records again: recompute
   return RBE_OK;
 }
 
@@ -134,6 +333,7 @@ struct HostInputs {
   // the replica word set, rbe_set_apply_ready flags (value 1 = ready)
   std::vector<u64> app_rep, app_val;
   std::vector<u64> applied;  // [n_rep] host mirror of Planes::applied (the host is its only writer)
+  u32 rep_world = 1, rep_rank = 0;  // replica-per-GPU mode: only owned replicas take input
 
   HostHeap heap;             // payload heap positions and staged bytes
 
@@ -155,6 +355,7 @@ struct HostInputs {
     app_rep.clear();
     app_val.clear();
     heap.stage.clear();
+    heap.batch_lo = heap.flushed;
     heap.flushed = heap.head;
   }
   ExtIn& rec(u64 r) {
@@ -172,8 +373,11 @@ struct HostInputs {
   // range, none twice in the batch, none with `flag` already staged
   int check_replicas(u64 cnt, const u64* replica, u32 flag) {
     if (cnt && !replica) return RBE_E_INVALID;
-    for (u64 i = 0; i < cnt; i++)
+    for (u64 i = 0; i < cnt; i++) {
       if (replica[i] >= n_rep) return RBE_E_INVALID;
+      if (rep_world > 1 && (replica[i] / n + replica[i] % n) % rep_world != rep_rank)
+        return RBE_E_INVALID;  // stepped by another engine
+    }
     if (!flag) return RBE_OK;
     if (++epoch == 0) {
       mark.assign(n_rep, 0u);
@@ -187,9 +391,14 @@ struct HostInputs {
     return RBE_OK;
   }
 
-  int push_proposals(u64 cnt, const u64* replica, const u32* n_ents, const u32* type,
-                     const u32* cmd_len, const u8* cmd) {
-    if (cnt && (!n_ents || !type || !cmd_len)) return RBE_E_INVALID;
+  // Peer.ProposeEntries batches (peer.go:117-123): batch i holds n_ents[i]
+  // entries for replica[i], whole raftpb.Entry values (Type, Key, ClientID,
+  // SeriesID, RespondedTo; Index/Term are stamped by the leader, raft.go:
+  // 909-920) with their Cmds concatenated in `cmd`.  Config changes go through
+  // ProposeConfigChange.
+  int push_entries(u64 cnt, const u64* replica, const u32* n_ents, const rbe_entry* pe,
+                   const u8* cmd) {
+    if (cnt && !n_ents) return RBE_E_INVALID;
     int rc = check_replicas(cnt, replica, EXT_PROPOSE);
     if (rc) return rc;
     u64 total = 0, bytes = 0;
@@ -197,23 +406,14 @@ struct HostInputs {
       if (n_ents[i] == 0 || n_ents[i] > 0xFFFFu) return RBE_E_INVALID;
       total += n_ents[i];
     }
-    u64 big = 0;  // heap bytes the batch needs (upper bound: alignment and lap skips)
-    for (u64 j = 0; j < total; j++) {
-      // Cmd is inline up to 16 bytes, longer ones need the payload heap and
-      // may take at most a quarter of it (the ErrPayloadTooBig check of
-      // requests.go:989-991, node.go:366-367); config changes go through ProposeConfigChange,
-      // a membership path the device does not run
-      if (type[j] == E_ConfigChange || type[j] > E_Metadata) return RBE_E_INVALID;
-      if (cmd_len[j] > 16 && (heap.cap == 0 || (u64)cmd_len[j] > heap.cap / 4))
-        return RBE_E_INVALID;
-      if (cmd_len[j] > 16) big += (u64)cmd_len[j] + 16;
-      bytes += cmd_len[j];
-    }
+    if (total && !pe) return RBE_E_INVALID;
+    for (u64 j = 0; j < total; j++) bytes += pe[j].cmd_len;
     if (bytes && !cmd) return RBE_E_INVALID;
+    u64 need = 0;
+    const u8* cb = cmd ? cmd : (const u8*)"";
+    if ((rc = check_entries(heap, total, pe, cb, false, &need))) return rc;
     if (ents.size() + total > in_cap) return RBE_E_NOMEM;
-    // the bytes staged for one step must not lap the ring (they would
-    // overwrite each other before the upload)
-    if (big && heap.head - heap.flushed + 2 * big > heap.cap) return RBE_E_NOMEM;
+    if (need && (rc = heap.room(need))) return rc;
     u64 j = 0, off = 0;
     for (u64 i = 0; i < cnt; i++) {
       ExtIn& x = rec(replica[i]);
@@ -221,30 +421,27 @@ struct HostInputs {
       x.n_prop = n_ents[i];
       x.prop_off = (u32)ents.size();
       for (u32 t = 0; t < n_ents[i]; t++, j++) {
-        Ent e;
-        memset(&e, 0, sizeof(e));
-        e.term = 0;  // stamped by the leader (appendEntries, raft.go:909-920)
-        e.type = type[j];
-        e.len = cmd_len[j];
-        if (cmd_len[j] > 16) {
-          // heap entry: lo = fingerprint, hi = absolute heap position
-          const u64 pos = heap.alloc(cmd_len[j]);
-          heap.stage.resize(heap.head - heap.flushed, 0);
-          memcpy(heap.stage.data() + (pos - heap.flushed), cmd + off, cmd_len[j]);
-          e.lo = cmd_fingerprint(cmd + off, cmd_len[j]);
-          e.hi = pos;
-        } else {
-          u8 b[16];
-          memset(b, 0, sizeof(b));
-          if (cmd_len[j]) memcpy(b, cmd + off, cmd_len[j]);
-          memcpy(&e.lo, b, 8);
-          memcpy(&e.hi, b + 8, 8);
-        }
-        off += cmd_len[j];
-        ents.push_back(e);
+        rbe_entry y = pe[j];
+        y.term = 0;  // stamped by the leader (appendEntries, raft.go:909-920)
+        ents.push_back(stage_entry(heap, y, cb + off));
+        off += y.cmd_len;
       }
     }
     return RBE_OK;
+  }
+  // rbe_push_proposals: the same without session fields
+  int push_proposals(u64 cnt, const u64* replica, const u32* n_ents, const u32* type,
+                     const u32* cmd_len, const u8* cmd) {
+    if (cnt && (!n_ents || !type || !cmd_len)) return RBE_E_INVALID;
+    u64 total = 0;
+    for (u64 i = 0; i < cnt; i++) total += n_ents ? n_ents[i] : 0;
+    std::vector<rbe_entry> pe(total);
+    for (u64 j = 0; j < total; j++) {
+      memset(&pe[j], 0, sizeof(rbe_entry));
+      pe[j].type = type[j];
+      pe[j].cmd_len = cmd_len[j];
+    }
+    return push_entries(cnt, replica, n_ents, pe.data(), cmd);
   }
   int push_read_index(u64 cnt, const u64* replica, const u64* lo, const u64* hi) {
     if (cnt && (!lo || !hi)) return RBE_E_INVALID;

@@ -33,10 +33,20 @@ RBE_HD u64 mix64(u64 x) {  // splitmix64 finalizer (same constants as the oracle
   return x ^ (x >> 31);
 }
 RBE_HD u64 hfold(u64 h, u64 x) { return mix64(h ^ x); }
+// Entry type and payload-heap bit of a Body/Ent `type` word (rbe_types.h ET_HEAP)
+RBE_HD u32 ent_type(u32 t) { return t & ET_TYPE_MASK; }
+RBE_HD bool ent_heap(u32 t) { return (t & ET_HEAP) != 0; }
 // The second Cmd word a trace digest folds: the inline bytes 8-15, or 0 for a
-// Cmd in the payload heap, whose `hi` is a heap position (rbe_host.h) and whose
-// `lo` fingerprint already stands for the bytes
-RBE_HD u64 cmd_hi(u32 len, u64 hi) { return len > 16 ? 0 : hi; }
+// payload-heap record, whose `hi` is a heap position (rbe_host.h) and whose
+// `lo` fingerprint already stands for the bytes and session fields
+RBE_HD u64 cmd_hi(u32 type, u64 hi) { return ent_heap(type) ? 0 : hi; }
+// The (type, Cmd length) word a trace digest folds for an entry
+RBE_HD u64 ent_word(u32 type, u32 len) { return (u64)ent_type(type) | ((u64)len << 32); }
+// A heap record at `pos` was overwritten by a later lap of the heap (the entry
+// is older than the in-memory window the heap keeps: F_WINDOW, as a ring miss)
+RBE_HD bool heap_lapped(const Planes& P, const Params& C, u32 type, u64 pos) {
+  return ent_heap(type) && C.heap_bytes && P.heap_head && pos + C.heap_bytes < *P.heap_head;
+}
 RBE_HD u64 umin64(u64 a, u64 b) { return a < b ? a : b; }
 RBE_HD u64 umax64(u64 a, u64 b) { return a > b ? a : b; }
 RBE_HD u32 popc8(u32 x) {
@@ -482,9 +492,9 @@ struct Lane {
           u64 idx = m.type == M_Replicate ? m.log_index + 1 + i : 0;
           h = hfold(h, idx);
           h = hfold(h, e.term);
-          h = hfold(h, (u64)e.type | ((u64)e.len << 32));
+          h = hfold(h, ent_word(e.type, e.len));
           h = hfold(h, e.lo);
-          h = hfold(h, cmd_hi(e.len, e.hi));
+          h = hfold(h, cmd_hi(e.type, e.hi));
         }
       }
       msg_hash = h;
@@ -546,6 +556,7 @@ struct Lane {
         if (last - idx >= C.ring) set_fault(F_WINDOW);
         u64 s = ring_slot(idx);
         Body b = P.pay_ring[s];
+        if (heap_lapped(P, C, b.type, b.hi)) set_fault(F_WINDOW);
         Ent e;
         e.term = P.term_ring[s];
         e.type = b.type;
@@ -569,6 +580,7 @@ struct Lane {
       if (last - idx >= C.ring) set_fault(F_WINDOW);
       u64 s = ring_slot(idx);
       Body b = P.pay_ring[s];
+      if (heap_lapped(P, C, b.type, b.hi)) set_fault(F_WINDOW);
       Ent e;
       e.term = P.term_ring[s];
       e.type = b.type;
@@ -637,9 +649,9 @@ struct Lane {
       if (TRACE) {
         drop_hash = hfold(drop_hash, 0);
         drop_hash = hfold(drop_hash, e[i].term);
-        drop_hash = hfold(drop_hash, (u64)e[i].type | ((u64)e[i].len << 32));
+        drop_hash = hfold(drop_hash, ent_word(e[i].type, e[i].len));
         drop_hash = hfold(drop_hash, e[i].lo);
-        drop_hash = hfold(drop_hash, cmd_hi(e[i].len, e[i].hi));
+        drop_hash = hfold(drop_hash, cmd_hi(e[i].type, e[i].hi));
       }
     }
   }
@@ -695,7 +707,7 @@ struct Lane {
         set_fault(F_WINDOW);
         break;
       }
-      if (P.pay_ring[ring_slot(i)].type == E_ConfigChange) ncc++;
+      if (ent_type(P.pay_ring[ring_slot(i)].type) == E_ConfigChange) ncc++;
     }
     if (ncc > 1) set_fault(F_PANIC);
     else if (ncc == 1) flags |= HF_PENDING_CC;
@@ -866,7 +878,7 @@ struct Lane {
       return;
     }
     for (u32 i = 0; i < cnt; i++) {
-      if (ents[i].type == E_ConfigChange) {
+      if (ent_type(ents[i].type) == E_ConfigChange) {
         set_fault(F_UNSUPPORTED);  // config change proposals are host slow path
         return;
       }
@@ -1421,9 +1433,9 @@ struct Lane {
               if (mt != term) return false;
             } else if (t == M_Propose || t == M_ReadIndex) {
               if (mt != 0) return false;
-              if (t == M_Propose && ((const Ent*)&P.arena[ppar][(g * N + s) * (u64)C.ecap +
-                                                              mp->ent_off])->type ==
-                                        E_ConfigChange)
+              if (t == M_Propose &&
+                  ent_type(P.arena[ppar][(g * N + s) * (u64)C.ecap + mp->ent_off].type) ==
+                      E_ConfigChange)
                 return false;
             } else {
               return false;
@@ -1880,9 +1892,9 @@ struct Lane {
         Body b = P.pay_ring[s];
         apply_hash = hfold(apply_hash, i);
         apply_hash = hfold(apply_hash, P.term_ring[s]);
-        apply_hash = hfold(apply_hash, (u64)b.type | ((u64)b.len << 32));
+        apply_hash = hfold(apply_hash, ent_word(b.type, b.len));
         apply_hash = hfold(apply_hash, b.lo);
-        apply_hash = hfold(apply_hash, cmd_hi(b.len, b.hi));
+        apply_hash = hfold(apply_hash, cmd_hi(b.type, b.hi));
       }
     }
     if (u.apply_hi >= u.apply_lo) ctr.v[C_ENT_APPLIED] += (u32)(u.apply_hi - u.apply_lo + 1);

@@ -32,6 +32,15 @@ enum : u8 { R_Follower = 0, R_Candidate = 1, R_Leader = 2, R_Observer = 3, R_Wit
 enum : u8 { RS_Retry = 0, RS_Wait = 1, RS_Replicate = 2, RS_Snapshot = 3 };
 // entry types, raft.pb.go:138-141
 enum : u32 { E_Application = 0, E_ConfigChange = 1, E_Encoded = 2, E_Metadata = 3 };
+// Body/Ent `type` bit 16: the entry is a payload-heap record.  Its Cmd (any
+// length) and its session fields live in the engine's heap at absolute position
+// `hi` as {Key, ClientID, SeriesID, RespondedTo} (kHeapHdr bytes, raft.pb.go:
+// 589-598) followed by the Cmd bytes; `lo` is the record's fingerprint
+// (rbe_host.h entry_fingerprint), which the trace digest folds for it.  An
+// entry without the bit carries Cmd <= 16 bytes inline in lo/hi and zero
+// session fields.  The entry type proper is `type & ET_TYPE_MASK`.
+enum : u32 { ET_HEAP = 1u << 16, ET_TYPE_MASK = 0xFFFFu };
+static constexpr u32 kHeapHdr = 32;
 
 // sticky per-replica fault bits (the engine-side analog of plog.Panicf: the
 // replica stops being trustworthy, the engine keeps running, the host sees it)
@@ -315,6 +324,9 @@ struct Planes {
   u64* rem_snap;      // [n_rep * N] remote.snapshotIndex (read only in RS_Snapshot)
   u8* gwake;          // [n_groups] GW_* bits: lets k_triage skip a sleeping group whole
                       // (rbe_step.h, group sleep)
+  const u64* heap_head;  // [1] payload heap: the host's next free position after the
+                         // last upload; a record at p < *heap_head - heap_bytes has been
+                         // overwritten by a later lap (null without a heap)
   u64* counters;      // [C_NUM]
 };
 

@@ -15,8 +15,10 @@
 // replica's in transport order (Quiesce notice, Replicate, the rest; the order
 // rbe_get_outbox reports).  InstallSnapshot messages never travel in a
 // MessageBatch (transport.go:400-403: they go through the snapshot chunk
-// stream), so they are counted and left out.  The engine's entries carry
-// Index, Term, Type and Cmd; Key, ClientID, SeriesID and RespondedTo are 0.
+// stream), so they are counted and left out.  Entries carry every field:
+// Index, Term, Type, the session fields and Cmd (a payload-heap record's from
+// the heap, rbe_types.h ET_HEAP); a Replicate's are numbered LogIndex + 1 + i,
+// a forwarded Propose's keep Index 0 (raft.go:1841-1853).
 //
 // One function, wire_cell, both sizes and writes a (group, k, d) cell, so the
 // size pass and the write pass cannot disagree.
@@ -59,32 +61,47 @@ RBE_HD u32 colfer_u64_put(u8* o, u32 field, u64 x) {
   o[0] = (u8)field;
   return 1 + wput(o + 1, x);
 }
-// Entry.Size (raft_optimized.go:79-153)
-RBE_HD u32 wire_entry_size(u64 index, u64 term, u32 type, u32 len) {
+// Entry.Size (raft_optimized.go:79-153); meta = {Key, ClientID, SeriesID,
+// RespondedTo}
+RBE_HD u32 wire_entry_size(u64 index, u64 term, u32 type, const u64* meta, u32 len) {
   u32 l = 1 + colfer_u64_size(term) + colfer_u64_size(index);
   if (type) l += 1 + wsov(type);
+  for (u32 f = 0; f < 4; f++) l += colfer_u64_size(meta[f]);
   if (len) l += 1 + wsov(len) + len;
   return l;
 }
-// Entry.marshalTo (raft_optimized.go:161-295); cmd bytes from the inline body
-// (len <= 16: lo/hi little endian) or the payload heap (absolute position hi)
-RBE_HD u32 wire_entry_put(u8* o, u64 index, u64 term, u32 type, u32 len, u64 lo, u64 hi,
-                          const u8* heap, u64 heap_cap) {
+// The wire view of an arena entry: its session fields and where its Cmd bytes
+// are (the inline lo/hi words in `inl`, or the heap record after its header)
+struct WireEnt {
+  u64 meta[4];
+  u8 inl[16];
+  const u8* cmd;
+};
+RBE_HD void wire_ent_view(const Ent& x, const u8* heap, u64 heap_cap, WireEnt& v) {
+  if (ent_heap(x.type) && heap_cap) {
+    const u8* rec = heap + x.hi % heap_cap;
+    const u64* h = (const u64*)rec;  // records are 16-B aligned
+    for (u32 f = 0; f < 4; f++) v.meta[f] = h[f];
+    v.cmd = rec + kHeapHdr;
+  } else {
+    for (u32 f = 0; f < 4; f++) v.meta[f] = 0;
+    for (u32 b = 0; b < 16; b++) v.inl[b] = (u8)((b < 8 ? x.lo : x.hi) >> (8 * (b & 7)));
+    v.cmd = v.inl;
+  }
+}
+// Entry.marshalTo (raft_optimized.go:161-295)
+RBE_HD u32 wire_entry_put(u8* o, u64 index, u64 term, u32 type, const WireEnt& v, u32 len) {
   u32 i = colfer_u64_put(o, 0, term);
   i += colfer_u64_put(o + i, 1, index);
   if (type) {
     o[i++] = 2;
     i += wput(o + i, type);
   }
+  for (u32 f = 0; f < 4; f++) i += colfer_u64_put(o + i, 3 + f, v.meta[f]);
   if (len) {
     o[i++] = 7;
     i += wput(o + i, len);
-    if (len <= 16) {
-      for (u32 b = 0; b < len; b++) o[i + b] = (u8)((b < 8 ? lo : hi) >> (8 * (b & 7)));
-    } else {
-      const u8* src = heap + (heap_cap ? hi % heap_cap : 0);
-      for (u32 b = 0; b < len; b++) o[i + b] = src[b];
-    }
+    for (u32 b = 0; b < len; b++) o[i + b] = v.cmd[b];
     i += len;
   }
   o[i++] = 0x7F;
@@ -103,16 +120,23 @@ RBE_HD u32 wire_empty_snap_put(u8* o) {
 }
 
 // Message.MarshalTo (raft.pb.go:2230-2294) of one outbox message, as a
-// MessageBatch request (tag 0x0a + length); `out` null = size only.
+// MessageBatch request (tag 0x0a + length); `out` null = size only.  An entry
+// whose heap record a later lap overwrote (position below heap_head - cap)
+// counts in *n_bad and is encoded from whatever the heap holds: the caller
+// refuses the whole encode then.
 RBE_HD u32 wire_message(const Msg& m, u32 type, u32 to, u32 from, u64 cid, const Ent* ents,
-                        const u8* heap, u64 heap_cap, u8* out) {
-  const u32 ne = type == M_Replicate ? m.n_ent : 0u;
+                        const u8* heap, u64 heap_cap, u64 heap_head, u8* out, u32* n_bad) {
+  const u32 ne = type == M_Replicate || type == M_Propose ? m.n_ent : 0u;
   u32 body = 1 + wsov(type) + 1 + wsov(to) + 1 + wsov(from) + 1 + wsov(cid) + 1 + wsov(m.term) +
              1 + wsov(m.log_term) + 1 + wsov(m.log_index) + 1 + wsov(m.commit) + 2 + 1 +
              wsov(m.hint) + 1 + 1 + kWireEmptySnap + 1 + wsov(m.hint_high);
   for (u32 j = 0; j < ne; j++) {
     const Ent& x = ents[j];
-    const u32 es = wire_entry_size(m.log_index + 1 + j, x.term, x.type, x.len);
+    const u64 idx = type == M_Replicate ? m.log_index + 1 + j : 0;
+    WireEnt v;
+    wire_ent_view(x, heap, heap_cap, v);
+    if (ent_heap(x.type) && (!heap_cap || x.hi + heap_cap < heap_head)) (*n_bad)++;
+    const u32 es = wire_entry_size(idx, x.term, ent_type(x.type), v.meta, x.len);
     body += 1 + wsov(es) + es;
   }
   const u32 total = 1 + wsov(body) + body;
@@ -142,10 +166,12 @@ RBE_HD u32 wire_message(const Msg& m, u32 type, u32 to, u32 from, u64 cid, const
   i += wput(out + i, m.hint);
   for (u32 j = 0; j < ne; j++) {
     const Ent& x = ents[j];
-    const u64 idx = m.log_index + 1 + j;
+    const u64 idx = type == M_Replicate ? m.log_index + 1 + j : 0;
+    WireEnt v;
+    wire_ent_view(x, heap, heap_cap, v);
     out[i++] = 0x5A;
-    i += wput(out + i, wire_entry_size(idx, x.term, x.type, x.len));
-    i += wire_entry_put(out + i, idx, x.term, x.type, x.len, x.lo, x.hi, heap, heap_cap);
+    i += wput(out + i, wire_entry_size(idx, x.term, ent_type(x.type), v.meta, x.len));
+    i += wire_entry_put(out + i, idx, x.term, ent_type(x.type), v, x.len);
   }
   out[i++] = 0x62;
   out[i++] = (u8)kWireEmptySnap;
@@ -158,16 +184,17 @@ RBE_HD u32 wire_message(const Msg& m, u32 type, u32 to, u32 from, u64 cid, const
 // The requests replica (g, k) sent replica (g, d) in the round that produced
 // header `row` (written as round `round` - 1, parity (round - 1) & 1): their
 // bytes (written at `out` unless null); *n_msgs / *n_is count the messages
-// encoded and the InstallSnapshots left out.
+// encoded and the InstallSnapshots left out, *n_bad the entries whose heap
+// record is gone (rbe_wire_encode fails then).
 template <int N>
-RBE_HD u32 wire_cell(const Planes& P, const Params& C, const u8* heap, u64 g, u32 k, u32 d,
-                     u32 round, u8* out, u32* n_msgs, u32* n_is) {
+RBE_HD u32 wire_cell(const Planes& P, const Params& C, const u8* heap, u64 heap_head, u64 g, u32 k,
+                     u32 d, u32 round, u8* out, u32* n_msgs, u32* n_is, u32* n_bad) {
   const u32 par = (round - 1u) & 1u;
   const u64 r = g * N + k;
   const u64 cid = C.cid_base + g * C.cid_stride;
   const u32 pc = row_word(P.cnt[par][r], d, round);
   const u32 na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
-  u32 bytes = 0, nm = 0, ni = 0;
+  u32 bytes = 0, nm = 0, ni = 0, bad = 0;
   if (pc & 0x8000u) {  // sendEnterQuiesceMessages (node.go:873-886)
     Msg q;
     q.type = (u8)M_Quiesce;
@@ -176,8 +203,8 @@ RBE_HD u32 wire_cell(const Planes& P, const Params& C, const u8* heap, u64 g, u3
     q.pad0 = 0;
     q.ent_off = q.pad1 = 0;
     q.term = q.log_term = q.log_index = q.commit = q.hint = q.hint_high = 0;
-    bytes += wire_message(q, M_Quiesce, d + 1, k + 1, cid, nullptr, heap, C.heap_bytes,
-                          out ? out + bytes : nullptr);
+    bytes += wire_message(q, M_Quiesce, d + 1, k + 1, cid, nullptr, heap, C.heap_bytes, heap_head,
+                          out ? out + bytes : nullptr, &bad);
     nm++;
   }
   const Msg* lst = &P.msgs[par][((g * N + k) * N + d) * (u64)C.maxm];
@@ -189,11 +216,12 @@ RBE_HD u32 wire_cell(const Planes& P, const Params& C, const u8* heap, u64 g, u3
       continue;
     }
     bytes += wire_message(m, m.type, d + 1, k + 1, cid, arena + m.ent_off, heap, C.heap_bytes,
-                          out ? out + bytes : nullptr);
+                          heap_head, out ? out + bytes : nullptr, &bad);
     nm++;
   }
   *n_msgs = nm;
   *n_is = ni;
+  *n_bad = bad;
   return bytes;
 }
 

@@ -24,6 +24,7 @@ struct WireArgs {
   u32 bin_ver, gpb;      // groups per batch
   u32 nchunks, npairs;   // batches = npairs * nchunks
   u32 round;
+  u64 heap_head;         // payload heap head at the last upload (lapped-record check)
   u32 alen[6];
   u8 addr[6][48];        // source address of each slot
 };
@@ -42,7 +43,8 @@ struct WireBufs {
   u32* batch_is;
   u64* frame_off;   // [nbatch]
   WireFrame* frames;  // compacted, non-empty batches
-  u64* totals;      // [0] bytes, [1] frames, [2] messages, [3] InstallSnapshots left out
+  u64* totals;      // [0] bytes, [1] frames, [2] messages, [3] InstallSnapshots left out,
+                    // [4] entries whose heap record a later lap overwrote
 };
 
 RBE_HD void wire_pair(u32 N, u32 p, u32* k, u32* d) {
@@ -52,17 +54,19 @@ RBE_HD void wire_pair(u32 N, u32 p, u32* k, u32* d) {
 }
 
 template <int N>
-__global__ __launch_bounds__(256) void k_wire_size(Planes P, Params C, WireArgs A, WireBufs B) {
+__global__ __launch_bounds__(256) void k_wire_size(Planes P, Params C, WireArgs A, WireBufs B,
+                                                   const u8* heap) {
   const u64 c = (u64)blockIdx.x * 256 + threadIdx.x;
   if (c >= (u64)A.npairs * C.n_groups) return;
   const u32 p = (u32)(c / C.n_groups);
   const u64 g = c % C.n_groups;
   u32 k, d;
   wire_pair(N, p, &k, &d);
-  u32 nm = 0, ni = 0;
-  const u32 b = wire_cell<N>(P, C, nullptr, g, k, d, A.round, nullptr, &nm, &ni);
+  u32 nm = 0, ni = 0, bad = 0;
+  const u32 b = wire_cell<N>(P, C, heap, A.heap_head, g, k, d, A.round, nullptr, &nm, &ni, &bad);
   B.cell_bytes[c] = b;
   B.cell_msgs[c] = nm | (ni << 16);
+  if (bad) atomicAdd((unsigned long long*)&B.totals[4], (unsigned long long)bad);
 }
 
 // block-wide exclusive scan of one value per thread; returns this thread's
@@ -181,9 +185,9 @@ __global__ __launch_bounds__(256) void k_wire_write(Planes P, Params C, WireArgs
   const u32 bt = p * A.nchunks + (u32)(g / A.gpb);
   u32 k, d;
   wire_pair(N, p, &k, &d);
-  u32 nm = 0, ni = 0;
-  wire_cell<N>(P, C, heap, g, k, d, A.round, out + B.frame_off[bt] + kWireHeader + B.cell_off[c],
-               &nm, &ni);
+  u32 nm = 0, ni = 0, bad = 0;
+  wire_cell<N>(P, C, heap, A.heap_head, g, k, d, A.round,
+               out + B.frame_off[bt] + kWireHeader + B.cell_off[c], &nm, &ni, &bad);
 }
 
 __global__ __launch_bounds__(256) void k_wire_trailers(Params C, WireArgs A, WireBufs B,
@@ -328,13 +332,23 @@ struct WireRd {
     bad = true;
     return x;
   }
-  RBE_HD void skip(u32 wt) {  // skipRaft
+  // skipRaft (raft.pb.go): a length or fixed width past the end is
+  // ErrInvalidLength / io.ErrUnexpectedEOF; compared as "l > n - i" so a
+  // length near 2^64 cannot wrap the position
+  RBE_HD void advance(u64 l) {
+    if (i > n || l > n - i) {
+      bad = true;
+      i = n;
+    } else {
+      i += l;
+    }
+  }
+  RBE_HD void skip(u32 wt) {
     if (wt == 0) varint();
-    else if (wt == 1) i += 8;
-    else if (wt == 2) i += varint();
-    else if (wt == 5) i += 4;
+    else if (wt == 1) advance(8);
+    else if (wt == 2) advance(varint());
+    else if (wt == 5) advance(4);
     else bad = true;
-    if (i > n) bad = true;
   }
 };
 
@@ -372,8 +386,9 @@ RBE_HD void wire_entry_get(WireRd& rd, u64 end, rbe_entry* e, u8* cmd) {
   }
   u32 len = 0;
   if (h == 7) {
-    len = (u32)rd.varint();
-    if (rd.i + len > end) rd.bad = true;
+    const u64 l = rd.varint();
+    if (rd.i > end || l > end - rd.i) rd.bad = true;
+    len = rd.bad ? 0u : (u32)l;
     for (u32 b = 0; b < len && !rd.bad; b++) {
       const u8 x = rd.byte();
       if (cmd) cmd[b] = x;
@@ -387,6 +402,10 @@ RBE_HD void wire_entry_get(WireRd& rd, u64 end, rbe_entry* e, u8* cmd) {
     e->index = vals[1];
     e->type = (u32)vals[2];
     e->cmd_len = len;
+    e->key = vals[3];
+    e->client_id = vals[4];
+    e->series_id = vals[5];
+    e->responded_to = vals[6];
   }
 }
 
@@ -403,11 +422,11 @@ RBE_HD u32 wire_message_get(WireRd& rd, u64 end, rbe_message* m, rbe_entry* ents
       f[fn] = rd.varint();
     } else if (fn == 11 && wt == 2) {
       const u64 l = rd.varint();
-      const u64 e_end = rd.i + l;
-      if (e_end > end) {
+      if (rd.bad || rd.i > end || l > end - rd.i) {
         rd.bad = true;
         break;
       }
+      const u64 e_end = rd.i + l;
       // Cmd length first (the colfer walk below writes at cmd + *cmd_at)
       rbe_entry tmp;
       rbe_entry* e = ents ? &ents[ne] : &tmp;

@@ -13,6 +13,7 @@
 // Record order is irrelevant: every record names its destination slot.
 #pragma once
 #include "rbe_fast.h"
+#include "rbe_host.h"
 #include "../../include/rbe.h"
 #include <unordered_map>
 #include <vector>
@@ -178,18 +179,22 @@ RBE_HD bool xchg_put_fixed(const Planes& P, const Params& C, u32 par, const u8* 
 // the order the receiving step handles it (node.go:1030-1067 with the
 // lockstep ordering of DESIGN.md §2): the Quiesce notice (node.go:873-886),
 // Replicate messages (sent before persistence, node.go:897-905), the rest.
-// A Replicate's entries follow in `ents` (rbe_message.n_entries of them,
-// Index = LogIndex + 1 + i).  row = the sender's outbox header of that
-// round's parity, `round` the round that reads it, lst = the N * maxm message
-// slots of (g, k, *), arena = the sender's ecap arena entries, all host
-// copies.  Counts beyond the capacities are reported in *n_msg / *n_ent and
-// not written.
-template <int N>
-void outbox_messages(const Params& C, u64 g, u32 k, const CntRow& row, u32 round, const Msg* lst,
-                     const Ent* arena, rbe_message* out, u32 cap, rbe_entry* ents, u32 ent_cap,
-                     u32* n_msg, u32* n_ent) {
+// A message's entries follow in `ents` (rbe_message.n_entries of them): a
+// Replicate's with Index = LogIndex + 1 + i, a forwarded Propose's with Index
+// 0 as the client proposed them (raft.go:1841-1853); their whole Cmds go to
+// `cmd` back to back (when non-null).  row = the sender's outbox header of
+// that round's parity, `round` the round that reads it, lst = the N * maxm
+// message slots of (g, k, *), arena = the sender's ecap arena entries, all
+// host copies; `rd` reads payload-heap record bytes (rbe_host.h entry_out).
+// Counts beyond the capacities are reported in *n_msg / *n_ent / *n_cmd and
+// not written.  Returns RBE_OK or the reader's error (an overwritten record).
+template <int N, typename RD>
+int outbox_messages(const Params& C, u64 g, u32 k, const CntRow& row, u32 round, const Msg* lst,
+                    const Ent* arena, rbe_message* out, u32 cap, rbe_entry* ents, u32 ent_cap,
+                    u32* n_msg, u32* n_ent, u8* cmd, u64 cmd_cap, u64* n_cmd, RD&& rd) {
   const u64 cid = C.cid_base + g * C.cid_stride;
   u32 n = 0, ne = 0;
+  u64 nc = 0;
   auto emit = [&](const Msg& m, u32 type, u32 to) {
     if (n < cap && out) {
       rbe_message& o = out[n];
@@ -205,7 +210,7 @@ void outbox_messages(const Params& C, u64 g, u32 k, const CntRow& row, u32 round
       o.commit = m.commit;
       o.hint = m.hint;
       o.hint_high = m.hint_high;
-      o.n_entries = type == M_Replicate ? m.n_ent : 0u;
+      o.n_entries = type == M_Replicate || type == M_Propose ? m.n_ent : 0u;
     }
     n++;
   };
@@ -218,136 +223,155 @@ void outbox_messages(const Params& C, u64 g, u32 k, const CntRow& row, u32 round
     for (u32 i = 0; i < na + nb; i++) {
       const Msg& m = i < na ? lst[d * C.maxm + i] : lst[d * C.maxm + C.maxm - 1u - (i - na)];
       emit(m, m.type, d + 1);
-      if (m.type != M_Replicate) continue;
-      for (u32 j = 0; j < m.n_ent; j++) {
-        if (ents && ne < ent_cap && m.ent_off + j < C.ecap) {
-          const Ent& x = arena[m.ent_off + j];
+      if (m.type != M_Replicate && m.type != M_Propose) continue;
+      for (u32 j = 0; j < m.n_ent && m.ent_off + j < C.ecap; j++) {
+        const Ent& x = arena[m.ent_off + j];
+        const bool room_c = cmd && nc + x.len <= cmd_cap;
+        if (ents && ne < ent_cap) {
           rbe_entry& e = ents[ne];
           e = rbe_entry{};
-          e.index = m.log_index + 1 + j;
-          e.term = x.term;
-          e.type = x.type;
-          e.cmd_len = x.len;
-          for (u32 b = 0; b < 8; b++) {
-            e.cmd[b] = (u8)(x.lo >> (8 * b));
-            e.cmd[8 + b] = (u8)(x.hi >> (8 * b));
-          }
+          const int rc = entry_out(x, &e, room_c ? cmd + nc : nullptr, rd);
+          if (rc) return rc;
+          e.index = m.type == M_Replicate ? m.log_index + 1 + j : 0;
+        } else if (room_c) {
+          rbe_entry e;
+          const int rc = entry_out(x, &e, cmd + nc, rd);
+          if (rc) return rc;
         }
         ne++;
+        nc += x.len;
       }
     }
   }
   *n_msg = n;
   *n_ent = ne;
+  if (n_cmd) *n_cmd = nc;
+  return RBE_OK;
 }
 
 // The inverse for one round's inbound batch: message i of group group[i]
 // from node msgs[i].from (a replica this engine does not step) to node
 // msgs[i].to (one it does), carrying msgs[i].n_entries entries taken in order
-// from `ents`.  Per (sender, destination) the Replicate messages keep their
-// order in the A list, the others in the B list, and a Quiesce message sets
-// the notice bit, exactly the layout a local sender's step writes.  Each
-// sender named gets one outbox header stamped for `round` (the round that
-// reads them); a sender not named keeps a stale header, which reads as
-// empty.  Returns RBE_OK,
-// RBE_E_INVALID (ids, ownership, entry indexes) or RBE_E_NOMEM (more than
-// maxm messages in one list, or more than ecap entries from one sender).
+// from `ents` with their Cmds back to back in `cmd` (null: each entry's inline
+// cmd, at most 16 bytes).  Per (sender, destination) the Replicate messages
+// keep their order in the A list, the others in the B list, and a Quiesce
+// message sets the notice bit, exactly the layout a local sender's step
+// writes.  Replicate and forwarded Propose messages carry entries (raft.go:
+// 1841-1853); entries with Cmds over 16 bytes or session fields are staged in
+// this engine's payload heap.  Each sender named gets one outbox header
+// stamped for `round` (the round that reads them); a sender not named keeps a
+// stale header, which reads as empty.  Checked whole before anything is
+// staged: RBE_OK, RBE_E_INVALID (ids, ownership, entry indexes or types) or
+// RBE_E_NOMEM (more than maxm messages in one list, more than ecap entries
+// from one sender, or no heap room).
 template <int N>
-int messages_to_records(const Params& C, u32 round, u64 n, const u64* group,
-                        const rbe_message* msgs, const rbe_entry* ents, std::vector<XCnt>& oc,
-                        std::vector<XMsg>& om, std::vector<XEnt>& oe) {
-  std::unordered_map<u64, u32> words;  // list key → count word
-  std::vector<u64> order;              // list keys in first-use order
-  std::unordered_map<u64, u32> used;   // sender replica → arena entries used
-  u64 ei = 0;
-  for (u64 i = 0; i < n; i++) {
-    const rbe_message& m = msgs[i];
-    const u64 g = group[i];
-    // Peer.Handle (peer.go:186-198): a local message type is a caller bug (the
-    // reference panics); a response from a node that is not a member of the
-    // group is dropped.  Other messages from non-members cannot be held by a
-    // slot-indexed group and are refused.
-    if (m.type >= 26 || is_local_message(m.type)) return RBE_E_INVALID;
-    if ((m.from < 1 || m.from > N) && is_response_message(m.type) && m.n_entries == 0) continue;
-    if (g >= C.n_groups || m.from < 1 || m.from > N || m.to < 1 || m.to > N || m.from == m.to)
-      return RBE_E_INVALID;
-    const u32 s = (u32)m.from - 1u, d = (u32)m.to - 1u;
-    if (owner_of<N>(C, g, s) == C.rep_rank || owner_of<N>(C, g, d) != C.rep_rank)
-      return RBE_E_INVALID;
-    const u64 key = (g * N + s) * N + d;
-    auto it = words.find(key);
-    if (it == words.end()) {
-      it = words.emplace(key, 0u).first;
-      order.push_back(key);
-    }
-    u32& w = it->second;
-    if (m.type == M_Quiesce) {
-      w |= 0x8000u;
-      continue;
-    }
-    if (m.type >= 26 || (m.n_entries && m.type != M_Replicate)) return RBE_E_INVALID;
-    const u32 na = w & 0x7Fu, nb = (w >> 7) & 0x7Fu;
-    if (na + nb >= C.maxm) return RBE_E_NOMEM;
-    XMsg x;
-    x.key = key;
-    x.m = mk_msg(m.type, m.to);
-    x.m.from = (u8)m.from;
-    x.m.reject = (u8)(m.reject ? 1 : 0);
-    x.m.term = m.term;
-    x.m.log_term = m.log_term;
-    x.m.log_index = m.log_index;
-    x.m.commit = m.commit;
-    x.m.hint = m.hint;
-    x.m.hint_high = m.hint_high;
-    if (m.type == M_Replicate) {
-      x.slot = na;
-      w += 1u;
-      const u64 sr = g * N + s;
-      u32& off = used[sr];
-      if (m.n_entries > 0xFFFFu || off + m.n_entries > C.ecap) return RBE_E_NOMEM;
-      x.m.n_ent = (u16)m.n_entries;
-      x.m.ent_off = off;
-      for (u32 j = 0; j < m.n_entries; j++, ei++) {
-        const rbe_entry& e = ents[ei];
-        if (e.index != m.log_index + 1 + j || e.cmd_len > 16) return RBE_E_INVALID;
-        XEnt y;
-        y.key = sr;
-        y.off = off + j;
-        y.e.term = e.term;
-        y.e.type = e.type;
-        y.e.len = e.cmd_len;
-        y.e.lo = y.e.hi = 0;
-        for (u32 b = 0; b < 8; b++) {
-          y.e.lo |= (u64)e.cmd[b] << (8 * b);
-          y.e.hi |= (u64)e.cmd[8 + b] << (8 * b);
-        }
-        oe.push_back(y);
+int messages_to_records(const Params& C, HostHeap& heap, u32 round, u64 n, const u64* group,
+                        const rbe_message* msgs, const rbe_entry* ents, const u8* cmd,
+                        std::vector<XCnt>& oc, std::vector<XMsg>& om, std::vector<XEnt>& oe) {
+  u64 total = 0;
+  for (u64 i = 0; i < n; i++) total += msgs[i].n_entries;
+  if (total && !ents) return RBE_E_INVALID;
+  u64 need = 0;
+  int rc = check_entries(heap, total, ents, cmd, true, &need);
+  if (rc) return rc;
+  auto pass = [&](bool write) -> int {
+    std::unordered_map<u64, u32> words;  // list key → count word
+    std::vector<u64> order;              // list keys in first-use order
+    std::unordered_map<u64, u32> used;   // sender replica → arena entries used
+    u64 ei = 0, coff = 0;
+    for (u64 i = 0; i < n; i++) {
+      const rbe_message& m = msgs[i];
+      const u64 g = group[i];
+      // Peer.Handle (peer.go:186-198): a local message type is a caller bug (the
+      // reference panics); a response from a node that is not a member of the
+      // group is dropped.  Other messages from non-members cannot be held by a
+      // slot-indexed group and are refused.
+      if (m.type >= 26 || is_local_message(m.type)) return RBE_E_INVALID;
+      if ((m.from < 1 || m.from > N) && is_response_message(m.type) && m.n_entries == 0) continue;
+      if (g >= C.n_groups || m.from < 1 || m.from > N || m.to < 1 || m.to > N || m.from == m.to)
+        return RBE_E_INVALID;
+      const u32 s = (u32)m.from - 1u, d = (u32)m.to - 1u;
+      if (owner_of<N>(C, g, s) == C.rep_rank || owner_of<N>(C, g, d) != C.rep_rank)
+        return RBE_E_INVALID;
+      const u64 key = (g * N + s) * N + d;
+      auto it = words.find(key);
+      if (it == words.end()) {
+        it = words.emplace(key, 0u).first;
+        order.push_back(key);
       }
-      off += m.n_entries;
-    } else {
-      x.slot = C.maxm - 1u - nb;
-      w += 1u << 7;
+      u32& w = it->second;
+      if (m.type == M_Quiesce) {
+        if (m.n_entries) return RBE_E_INVALID;
+        w |= 0x8000u;
+        continue;
+      }
+      const bool with_ents = m.type == M_Replicate || m.type == M_Propose;
+      if (m.n_entries && !with_ents) return RBE_E_INVALID;
+      const u32 na = w & 0x7Fu, nb = (w >> 7) & 0x7Fu;
+      if (na + nb >= C.maxm) return RBE_E_NOMEM;
+      XMsg x;
+      x.key = key;
+      x.m = mk_msg(m.type, m.to);
+      x.m.from = (u8)m.from;
+      x.m.reject = (u8)(m.reject ? 1 : 0);
+      x.m.term = m.term;
+      x.m.log_term = m.log_term;
+      x.m.log_index = m.log_index;
+      x.m.commit = m.commit;
+      x.m.hint = m.hint;
+      x.m.hint_high = m.hint_high;
+      if (m.type == M_Replicate) {
+        x.slot = na;
+        w += 1u;
+      } else {
+        x.slot = C.maxm - 1u - nb;
+        w += 1u << 7;
+      }
+      if (with_ents && m.n_entries) {
+        const u64 sr = g * N + s;
+        u32& off = used[sr];
+        if (m.n_entries > 0xFFFFu || off + m.n_entries > C.ecap) return RBE_E_NOMEM;
+        x.m.n_ent = (u16)m.n_entries;
+        x.m.ent_off = off;
+        for (u32 j = 0; j < m.n_entries; j++, ei++) {
+          const rbe_entry& e = ents[ei];
+          if (m.type == M_Replicate && e.index != m.log_index + 1 + j) return RBE_E_INVALID;
+          const u8* cb = cmd ? cmd + coff : e.cmd;
+          coff += cmd ? e.cmd_len : 0;
+          if (!write) continue;
+          XEnt y;
+          y.key = sr;
+          y.off = off + j;
+          y.e = stage_entry(heap, e, cb);
+          oe.push_back(y);
+        }
+        off += m.n_entries;
+      }
+      if (write) om.push_back(x);
     }
-    om.push_back(x);
-  }
-  // one stamped header per sender with the words of all its lists
-  std::unordered_map<u64, size_t> hdr;  // sender replica → index in oc
-  for (u64 key : order) {
-    const u64 sr = key / N;
-    const u32 d = (u32)(key % N);
-    auto it = hdr.find(sr);
-    if (it == hdr.end()) {
-      XCnt c;
-      c.key = sr;
-      c.pad = 0;
-      c.row.stamp = round;
-      for (int w = 0; w < 6; w++) c.row.w[w] = 0;
-      it = hdr.emplace(sr, oc.size()).first;
-      oc.push_back(c);
+    if (!write) return RBE_OK;
+    // one stamped header per sender with the words of all its lists
+    std::unordered_map<u64, size_t> hdr;  // sender replica → index in oc
+    for (u64 key : order) {
+      const u64 sr = key / N;
+      const u32 d = (u32)(key % N);
+      auto it = hdr.find(sr);
+      if (it == hdr.end()) {
+        XCnt c;
+        c.key = sr;
+        c.pad = 0;
+        c.row.stamp = round;
+        for (int w = 0; w < 6; w++) c.row.w[w] = 0;
+        it = hdr.emplace(sr, oc.size()).first;
+        oc.push_back(c);
+      }
+      oc[it->second].row.w[d] = (u16)words[key];
     }
-    oc[it->second].row.w[d] = (u16)words[key];
-  }
-  return RBE_OK;
+    return RBE_OK;
+  };
+  if ((rc = pass(false))) return rc;
+  if (need && (rc = heap.room(need))) return rc;
+  return pass(true);
 }
 
 }  // namespace rbe

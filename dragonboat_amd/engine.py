@@ -14,7 +14,7 @@ import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libdragonboat_amd.so")
-RBE_ABI_VERSION = 2
+RBE_ABI_VERSION = 3
 
 COUNTER_NAMES = ["steps", "committed", "msg_in", "msg_out", "ent_in", "ent_out",
                  "reads_confirmed", "proposals", "reads", "quiesced_ticks", "active_ticks",
@@ -103,8 +103,31 @@ class RbeMessage(C.Structure):
 
 
 class RbeEntry(C.Structure):
+    """raftpb.Entry (raft.pb.go:589-598); cmd holds the first 16 Cmd bytes."""
     _fields_ = [("index", C.c_uint64), ("term", C.c_uint64), ("type", C.c_uint32),
-                ("cmd_len", C.c_uint32), ("cmd", C.c_uint8 * 16)]
+                ("cmd_len", C.c_uint32), ("cmd", C.c_uint8 * 16), ("key", C.c_uint64),
+                ("client_id", C.c_uint64), ("series_id", C.c_uint64),
+                ("responded_to", C.c_uint64)]
+
+
+SESSION_FIELDS = ("key", "client_id", "series_id", "responded_to")
+
+
+def make_entry(index=0, term=0, type=0, cmd=b"", key=0, client_id=0, series_id=0,
+               responded_to=0) -> RbeEntry:
+    e = RbeEntry(index=index, term=term, type=type, cmd_len=len(cmd), key=key,
+                 client_id=client_id, series_id=series_id, responded_to=responded_to)
+    for b, x in enumerate(cmd[:16]):
+        e.cmd[b] = x
+    return e
+
+
+def entry_fields(e: RbeEntry, cmd: Optional[bytes] = None) -> dict:
+    """An RbeEntry as a dict of raftpb.Entry fields (cmd: the whole Cmd when given)."""
+    return dict(index=e.index, term=e.term, type=e.type,
+                cmd=cmd if cmd is not None else bytes(e.cmd[:min(16, e.cmd_len)]),
+                key=e.key, client_id=e.client_id, series_id=e.series_id,
+                responded_to=e.responded_to)
 
 
 class RbeReadyToRead(C.Structure):
@@ -159,7 +182,7 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_get_entry_cmds", "rbe_set_apply_ready", "rbe_collect_outputs", "rbe_launch",
            "rbe_xchg_chunk_bytes", "rbe_xchg_pack_fixed", "rbe_xchg_unpack_fixed",
            "rbe_xchg_status", "rbe_stream", "rbe_get_snapshot_state", "rbe_wire_encode",
-           "rbe_wire_fetch", "rbe_wire_decode"]
+           "rbe_wire_fetch", "rbe_wire_decode", "rbe_propose_entries"]
 KERNEL_SLOTS = 4
 
 _lib = None
@@ -204,11 +227,13 @@ def load_library(path: Optional[str] = None):
         "rbe_round": (i32, [vp, P(u32)]),
         "rbe_run_timed": (i32, [vp, u32, P(C.c_float)]),
         "rbe_push_proposals": (i32, [vp, u64, P(u64), P(u32), P(u32), P(u32), P(C.c_uint8)]),
+        "rbe_propose_entries": (i32, [vp, u64, P(u64), P(u32), P(RbeEntry), P(C.c_uint8)]),
         "rbe_push_read_index": (i32, [vp, u64, P(u64), P(u64), P(u64)]),
         "rbe_get_updates": (i32, [vp, u64, u64, P(RbeUpdate)]),
         "rbe_get_messages": (i32, [vp, u64, P(RbeMessage), u32, P(u32)]),
-        "rbe_get_outbox": (i32, [vp, u64, P(RbeMessage), u32, P(u32), P(RbeEntry), u32, P(u32)]),
-        "rbe_push_messages": (i32, [vp, u64, P(u64), P(RbeMessage), P(RbeEntry)]),
+        "rbe_get_outbox": (i32, [vp, u64, P(RbeMessage), u32, P(u32), P(RbeEntry), u32, P(u32),
+                                 vp, u64, P(u64)]),
+        "rbe_push_messages": (i32, [vp, u64, P(u64), P(RbeMessage), P(RbeEntry), vp]),
         "rbe_get_ready_to_reads": (i32, [vp, u64, P(RbeReadyToRead), u32, P(u32)]),
         "rbe_get_entries": (i32, [vp, u64, u64, u64, P(RbeEntry)]),
         "rbe_get_entry_cmds": (i32, [vp, u64, u64, u64, vp, u64, P(u64)]),
@@ -219,7 +244,7 @@ def load_library(path: Optional[str] = None):
         "rbe_wire_decode": (i32, [vp, vp, u64, P(RbeMessage), u32, P(u32), P(RbeEntry), u32,
                                   P(u32), vp, u64, P(u64)]),
         "rbe_collect_outputs": (i32, [vp, u64, u64, P(RbeOutputs)]),
-        "rbe_launch": (i32, [vp, u64, P(u64), P(RbeLaunchState), P(RbeEntry)]),
+        "rbe_launch": (i32, [vp, u64, P(u64), P(RbeLaunchState), P(RbeEntry), vp]),
         "rbe_get_counters": (i32, [vp, P(u64)]),
         "rbe_reset_counters": (i32, [vp]),
         "rbe_fault_summary": (i32, [vp, P(u64), P(u32)]),
@@ -329,6 +354,38 @@ def entry_cmds(fn, h, replica: int, lo: int, hi: int) -> List[bytes]:
     return [raw[offs[i]:offs[i + 1]] for i in range(hi - lo + 1)]
 
 
+def outbox_call(fn, h, replica, cap, ent_cap, cmd_cap):
+    """rbe_get_outbox (or the host build's twin), sized by the counts it reports."""
+    arr = (RbeMessage * cap)()
+    ents = (RbeEntry * ent_cap)()
+    cmd = C.create_string_buffer(max(1, cmd_cap))
+    n, ne, nc = C.c_uint32(), C.c_uint32(), C.c_uint64()
+    _check(fn(h, replica, arr, cap, C.byref(n), ents, ent_cap, C.byref(ne), cmd, cmd_cap,
+              C.byref(nc)), "rbe_get_outbox")
+    if n.value > cap or ne.value > ent_cap or nc.value > cmd_cap:
+        return outbox_call(fn, h, replica, max(cap, n.value), max(ent_cap, ne.value),
+                           max(cmd_cap, nc.value))
+    es = [ents[i] for i in range(ne.value)]
+    raw, cmds, off = cmd.raw, [], 0
+    for e in es:
+        cmds.append(raw[off:off + e.cmd_len])
+        off += e.cmd_len
+    return [arr[i] for i in range(n.value)], es, cmds
+
+
+def push_messages_call(fn, h, groups, msgs, ents, cmds=None):
+    """rbe_push_messages (or the host build's twin); raises InputError."""
+    n = len(msgs)
+    g = (C.c_uint64 * max(1, n))(*groups)
+    m = (RbeMessage * max(1, n))(*msgs)
+    e = (RbeEntry * max(1, len(ents)))(*ents)
+    buf = None
+    if cmds is not None:
+        blob = b"".join(cmds)
+        buf = C.create_string_buffer(blob, max(1, len(blob)))
+    _check_input(fn(h, n, g, m, e, buf), "rbe_push_messages")
+
+
 class NodeInputs:
     """The node-layer input calls (include/rbe.h rbe_push_proposals ...
     rbe_notify_applied), marshalled once for the HIP engine and for the
@@ -336,22 +393,38 @@ class NodeInputs:
 
     # node-layer inputs for the next step (rbe.h; each call is all-or-nothing)
     def push_proposals(self, replicas, batches):
-        """Peer.ProposeEntries: batches[i] is a list of Cmd byte strings (or
-        (entry_type, Cmd) pairs) proposed at replicas[i]."""
+        """Peer.ProposeEntries: batches[i] is a list of entries proposed at
+        replicas[i], each a Cmd byte string, an (entry_type, Cmd) pair, or an
+        object with raftpb.Entry attributes (type, cmd, key, client_id,
+        series_id, responded_to).  Plain entries go through rbe_push_proposals,
+        a batch with entry objects through rbe_propose_entries."""
         n = len(replicas)
-        counts, types, lens, blob = [], [], [], bytearray()
+        counts, ents, blob = [], [], bytearray()
+        full = False
         for b in batches:
             counts.append(len(b))
             for e in b:
-                t, c = (e if isinstance(e, tuple) else (0, e))
-                types.append(t)
-                lens.append(len(c))
+                if isinstance(e, (bytes, bytearray)):
+                    t, c, meta = 0, bytes(e), (0, 0, 0, 0)
+                elif isinstance(e, tuple):
+                    t, c, meta = e[0], bytes(e[1]), (0, 0, 0, 0)
+                else:
+                    full = True
+                    t, c = e.type, bytes(e.cmd)
+                    meta = tuple(getattr(e, f, 0) for f in SESSION_FIELDS)
+                ents.append(make_entry(type=t, cmd=c, key=meta[0], client_id=meta[1],
+                                       series_id=meta[2], responded_to=meta[3]))
                 blob += c
         u32a = lambda v: (C.c_uint32 * max(1, len(v)))(*v)  # noqa: E731
         buf = (C.c_uint8 * max(1, len(blob))).from_buffer_copy(bytes(blob) or b"\0")
+        if full:
+            ea = (RbeEntry * max(1, len(ents)))(*ents)
+            _check_input(self._input("propose_entries", n, _u64s(replicas), u32a(counts), ea,
+                                     buf), "rbe_propose_entries")
+            return
         _check_input(self._input("push_proposals", n, _u64s(replicas), u32a(counts),
-                                                 u32a(types), u32a(lens), buf),
-                     "rbe_push_proposals")
+                                 u32a([e.type for e in ents]), u32a([e.cmd_len for e in ents]),
+                                 buf), "rbe_push_proposals")
 
     def push_read_index(self, replicas, ctxs):
         lo = [c[0] for c in ctxs]
@@ -380,8 +453,9 @@ class NodeInputs:
 
     def launch(self, replicas, states, entries):
         """rbe_launch: restart replicas[i] from states[i] = (term, vote, commit,
-        last_index) and entries[i] = [(index, term, type, cmd), ...], the tail
-        of its LogDB (Peer.Launch over an existing log, peer.go:64-86)."""
+        last_index) and entries[i] = [(index, term, type, cmd[, key, client_id,
+        series_id, responded_to]), ...], the tail of its LogDB (Peer.Launch
+        over an existing log, peer.go:64-86)."""
         n = len(replicas)
         st = (RbeLaunchState * max(1, n))()
         flat = []
@@ -390,11 +464,14 @@ class NodeInputs:
                                    n_entries=len(ents))
             flat.extend(ents)
         ea = (RbeEntry * max(1, len(flat)))()
-        for j, (idx, term, typ, cmd) in enumerate(flat):
-            ea[j].index, ea[j].term, ea[j].type, ea[j].cmd_len = idx, term, typ, len(cmd)
-            for b, x in enumerate(cmd[:16]):
-                ea[j].cmd[b] = x
-        _check_input(self._input("launch", n, _u64s(replicas), st, ea), "rbe_launch")
+        blob = bytearray()
+        for j, x in enumerate(flat):
+            idx, term, typ, cmd = x[:4]
+            meta = tuple(x[4:8]) + (0,) * (8 - max(4, len(x)))
+            ea[j] = make_entry(idx, term, typ, cmd, *meta)
+            blob += cmd
+        buf = C.create_string_buffer(bytes(blob), max(1, len(blob)))
+        _check_input(self._input("launch", n, _u64s(replicas), st, ea, buf), "rbe_launch")
 
     def set_apply_ready(self, replicas, ready):
         """node.canHaveMoreEntriesToApply per replica (sticky; ready by default)."""
@@ -635,25 +712,16 @@ class Engine(NodeInputs):
             return self.messages(replica, n.value)
         return [arr[i] for i in range(n.value)]
 
-    def outbox(self, replica: int, cap: int = 256, ent_cap: int = 1024):
+    def outbox(self, replica: int, cap: int = 256, ent_cap: int = 1024, cmd_cap: int = 1 << 20):
         """The last round's messages of `replica` in transport order, with the
-        entries of its Replicate messages (rbe_get_outbox)."""
-        arr = (RbeMessage * cap)()
-        ents = (RbeEntry * ent_cap)()
-        n, ne = C.c_uint32(), C.c_uint32()
-        _check(self.lib.rbe_get_outbox(self.h, replica, arr, cap, C.byref(n), ents, ent_cap,
-                                       C.byref(ne)), "rbe_get_outbox")
-        if n.value > cap or ne.value > ent_cap:
-            raise EngineError(f"outbox of {replica}: {n.value} messages / {ne.value} entries")
-        return [arr[i] for i in range(n.value)], [ents[i] for i in range(ne.value)]
+        entries of its Replicate and forwarded Propose messages and their
+        whole Cmds (rbe_get_outbox): (messages, entries, cmds)."""
+        return outbox_call(self.lib.rbe_get_outbox, self.h, replica, cap, ent_cap, cmd_cap)
 
-    def push_messages(self, groups, msgs, ents):
-        """Deliver one round's inbound batch from remote senders (rbe_push_messages)."""
-        n = len(msgs)
-        g = (C.c_uint64 * max(1, n))(*groups)
-        m = (RbeMessage * max(1, n))(*msgs)
-        e = (RbeEntry * max(1, len(ents)))(*ents)
-        _check(self.lib.rbe_push_messages(self.h, n, g, m, e), "rbe_push_messages")
+    def push_messages(self, groups, msgs, ents, cmds=None):
+        """Deliver one round's inbound batch from remote senders (rbe_push_messages);
+        cmds[i] is entry i's whole Cmd (None: the entries' inline cmd)."""
+        push_messages_call(self.lib.rbe_push_messages, self.h, groups, msgs, ents, cmds)
 
     def collect_outputs(self, first: int = 0, count: Optional[int] = None):
         """rbe_collect_outputs: (msg_off, messages, rtr_off, ready_to_reads) of
@@ -685,13 +753,16 @@ class Engine(NodeInputs):
     def entries(self, replica: int, lo: int, hi: int):
         """(Index, Term, Type, Cmd) of entries [lo, hi] of a replica's log window;
         a Cmd longer than 16 bytes comes from the payload heap."""
+        return [(d["index"], d["term"], d["type"], d["cmd"])
+                for d in self.entry_records(replica, lo, hi)]
+
+    def entry_records(self, replica: int, lo: int, hi: int) -> List[dict]:
+        """Every raftpb.Entry field of entries [lo, hi] (rbe_get_entries + the
+        whole Cmds from rbe_get_entry_cmds)."""
         arr = (RbeEntry * (hi - lo + 1))()
         _check(self.lib.rbe_get_entries(self.h, replica, lo, hi, arr), "rbe_get_entries")
-        out = [(e.index, e.term, e.type, bytes(e.cmd[:min(16, e.cmd_len)])) for e in arr]
-        if any(e.cmd_len > 16 for e in arr):
-            cmds = self.entry_cmds(replica, lo, hi)
-            out = [(i, t, ty, c) for (i, t, ty, _), c in zip(out, cmds)]
-        return out
+        cmds = self.entry_cmds(replica, lo, hi)
+        return [entry_fields(e, c) for e, c in zip(arr, cmds)]
 
     def entry_cmds(self, replica: int, lo: int, hi: int) -> List[bytes]:
         return entry_cmds(self.lib.rbe_get_entry_cmds, self.h, replica, lo, hi)

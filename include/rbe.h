@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RBE_ABI_VERSION 2
+#define RBE_ABI_VERSION 3
 
 /* error codes */
 #define RBE_OK 0
@@ -137,8 +137,9 @@ typedef struct rbe_config {
   uint32_t compaction_overhead;  /* config.CompactionOverhead: the LogDB keeps that many
                                     entries below a snapshot (compacted at the next step);
                                     a remote that needs older entries gets InstallSnapshot */
-  uint64_t heap_bytes;           /* payload heap for Cmd > 16 B (needs ext_inputs), 0 = none:
-                                    Cmd is then at most 16 bytes */
+  uint64_t heap_bytes;           /* payload heap for entries with Cmd > 16 B or session
+                                    fields (needs ext_inputs), 0 = none: Cmd is then at
+                                    most 16 bytes and Key/ClientID/SeriesID/RespondedTo 0 */
   uint32_t reserved[4];
 } rbe_config;
 
@@ -192,13 +193,18 @@ typedef struct rbe_message {
   uint32_t n_entries, reserved;
 } rbe_message;
 
-/* raftpb Entry (raft.pb.go:589-598): Index/Term/Type and Cmd.  cmd holds the
- * first min(cmd_len, 16) bytes; a longer Cmd (payload heap) is read whole with
- * rbe_get_entry_cmds. */
+/* raftpb Entry (raft.pb.go:589-598), every field: Index, Term, Type, the
+ * session fields Key / ClientID / SeriesID / RespondedTo that the client
+ * layer stamps on each proposal (requests.go:994-997) and Cmd.  `cmd` holds
+ * the first min(cmd_len, 16) bytes; the calls that move whole Cmds take or
+ * return them concatenated in a separate byte buffer.  Inside the engine an
+ * entry with a Cmd longer than 16 bytes or any non-zero session field lives
+ * in the payload heap (cfg.heap_bytes), which such entries require. */
 typedef struct rbe_entry {
   uint64_t index, term;
   uint32_t type, cmd_len;
   uint8_t cmd[16];
+  uint64_t key, client_id, series_id, responded_to;
 } rbe_entry;
 
 typedef struct rbe_ready_to_read {  /* raftpb ReadyToRead, raftpb/raft.go:52-56 */
@@ -209,7 +215,7 @@ typedef struct rbe_engine rbe_engine;
 
 /* Persisted state of one replica for rbe_launch: pb.State (term, vote, commit)
  * and the tail of its LogDB, entries [last_index - n_entries + 1, last_index]
- * (the engine's in-memory window; Cmd at most 16 bytes). */
+ * (the engine's in-memory window). */
 typedef struct rbe_launch_state {
   uint64_t term, vote, commit, last_index;
   uint32_t n_entries, reserved;
@@ -228,10 +234,13 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out);
  * too (fresh quiesce state and tick count), and the messages in flight to and
  * from a relaunched replica are lost.  replica[i] takes st[i] and the next
  * st[i].n_entries entries of `ents` (n_entries <= cfg.ring; an entry the
- * replica later needs below that window faults with RBE_FAULT_WINDOW).
- * Checked whole before anything changes (RBE_E_INVALID). */
+ * replica later needs below that window faults with RBE_FAULT_WINDOW).  The
+ * entries' Cmds are concatenated in `cmd` (null: each is its rbe_entry.cmd,
+ * at most 16 bytes); entries with longer Cmds or session fields go to the
+ * payload heap.  Checked whole before anything changes (RBE_E_INVALID;
+ * RBE_E_NOMEM when the heap has no room for them). */
 int rbe_launch(rbe_engine* e, uint64_t n, const uint64_t* replica, const rbe_launch_state* st,
-               const rbe_entry* ents);
+               const rbe_entry* ents, const uint8_t* cmd);
 int rbe_destroy(rbe_engine* e);
 int rbe_abi_version(void);
 /* sizeof the ABI structs, in this order: rbe_config, rbe_replica_view,
@@ -281,14 +290,20 @@ int rbe_profile_rounds(rbe_engine* e, uint32_t rounds, float* ms_per_kernel);
  * rbe_step in one copy.  A replica takes one proposal batch, one ReadIndex and
  * one leader transfer per step, as the node batches them; a second one for the
  * same replica, within a batch or across calls, is RBE_E_STATE (nothing staged).
- *   rbe_push_proposals: Peer.ProposeEntries (peer.go:117-123); batch i holds
- *     n_ents[i] entries for replica[i]; the entries' types, Cmd lengths and Cmd
- *     bytes (concatenated in order) follow in type[], cmd_len[], cmd.  Cmd is at
- *     most 16 bytes without a payload heap; with cfg.heap_bytes a longer Cmd (at
- *     most heap_bytes / 4, the ErrPayloadTooBig analog, requests.go:989-991) is
- *     written to the heap once and every replica's entry refers to it.
- *     RBE_E_NOMEM when the step's cfg.in_cap entries are used up, or its Cmd
- *     bytes would lap the heap.
+ *   rbe_propose_entries: Peer.ProposeEntries (peer.go:117-123); batch i holds
+ *     n_ents[i] entries for replica[i], whole raftpb.Entry values in `ents`
+ *     (Type, Key, ClientID, SeriesID, RespondedTo, cmd_len; Index and Term are
+ *     the leader's to stamp, raft.go:909-920) with their Cmd bytes concatenated
+ *     in `cmd`.  Without a payload heap every Cmd is at most 16 bytes and the
+ *     session fields are 0; with cfg.heap_bytes an entry with a longer Cmd (at
+ *     most heap_bytes / 4, the ErrPayloadTooBig analog, requests.go:989-991)
+ *     or session fields is written to the heap once as a record and every
+ *     replica's entry refers to it.  RBE_E_NOMEM when the step's cfg.in_cap
+ *     entries are used up, or the heap has no room without overwriting a
+ *     record some replica has not yet saved and applied (never lapped: the
+ *     reference keeps an entry until then, inmemory.go:116-166).
+ *   rbe_push_proposals: rbe_propose_entries without session fields; the
+ *     entries' types and Cmd lengths in type[], cmd_len[].
  *   rbe_push_read_index: Peer.ReadIndex (peer.go:297-303), ctx_low != 0
  *     (requests.go:726).
  *   rbe_request_leader_transfer: Peer.RequestLeaderTransfer (peer.go:106-113),
@@ -305,6 +320,8 @@ int rbe_profile_rounds(rbe_engine* e, uint32_t rounds, float* ms_per_kernel);
  *     argument of Peer.HasUpdate / GetUpdate, peer.go:201, 253, 329-331); sticky
  *     per replica, ready by default.  While not ready a step returns no
  *     CommittedEntries. */
+int rbe_propose_entries(rbe_engine* e, uint64_t n, const uint64_t* replica,
+                        const uint32_t* n_ents, const rbe_entry* ents, const uint8_t* cmd);
 int rbe_push_proposals(rbe_engine* e, uint64_t n, const uint64_t* replica,
                        const uint32_t* n_ents, const uint32_t* type, const uint32_t* cmd_len,
                        const uint8_t* cmd);
@@ -449,22 +466,31 @@ int rbe_xchg_unpack(rbe_engine* e, const void* cnt_recs, uint64_t n_cnt, const v
  * the replicas of other ranks, or of other hosts behind dragonboat's transport).
  *   rbe_get_outbox: sender `replica`'s messages of the last round in raftpb form,
  *     per destination in ascending node id: the Quiesce notice (node.go:873-886),
- *     Replicate messages, the rest; each Replicate's entries follow in `ents`
- *     (n_entries of them).  Replaces reading Update.Messages for the transport
- *     (node.go:888-905 → nodehost.go:1724 sendMessages).
+ *     Replicate messages, the rest; each message's entries (a Replicate's, and
+ *     a forwarded Propose's, raft.go:1841-1853) follow in `ents` (n_entries of
+ *     them) with their whole Cmds concatenated in `cmd` (cmd_cap bytes;
+ *     *cmd_bytes = the total; null skips them).  Counts beyond a capacity are
+ *     reported and not written (RBE_OK; the caller compares).  RBE_E_STATE when
+ *     a heap record has been overwritten.  Replaces reading Update.Messages for
+ *     the transport (node.go:888-905 → nodehost.go:1724 sendMessages).
  *   rbe_push_messages: the round's inbound batch for the replicas this engine
  *     steps, delivered to the next rbe_step.  Replaces Peer.Handle (peer.go:186-198)
  *     as called by node.handleReceivedMessages (node.go:1030-1067): message i is
  *     for group group[i], from node msgs[i].from (not stepped here) to node
  *     msgs[i].to (stepped here), with msgs[i].n_entries entries taken in order from
- *     `ents` (Index = LogIndex + 1 + j).  One call per round carries every remote
- *     message of that round; lists it does not name are empty.  RBE_E_STATE when
+ *     `ents` (a Replicate's: Index = LogIndex + 1 + j; a Propose's: any Index)
+ *     and their Cmds concatenated in `cmd` (null: each is its rbe_entry.cmd).
+ *     One call per round carries every remote message of that round; lists it
+ *     does not name are empty.  Entries with Cmds over 16 bytes or session
+ *     fields are written to this engine's payload heap.  RBE_E_STATE when
  *     rep_world <= 1 (every sender is local), RBE_E_NOMEM when one (sender,
- *     destination) list exceeds cfg.maxm or one sender's entries cfg.ecap. */
+ *     destination) list exceeds cfg.maxm, one sender's entries cfg.ecap, or
+ *     the heap has no room. */
 int rbe_get_outbox(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t cap,
-                   uint32_t* n_out, rbe_entry* ents, uint32_t ent_cap, uint32_t* n_ents);
+                   uint32_t* n_out, rbe_entry* ents, uint32_t ent_cap, uint32_t* n_ents,
+                   uint8_t* cmd, uint64_t cmd_cap, uint64_t* cmd_bytes);
 int rbe_push_messages(rbe_engine* e, uint64_t n, const uint64_t* group, const rbe_message* msgs,
-                      const rbe_entry* ents);
+                      const rbe_entry* ents, const uint8_t* cmd);
 
 /* Group-range snapshots: the complete protocol state of groups [first, first + count)
  * between two rounds (every replica's raft, remote, readIndex and log-window rows and

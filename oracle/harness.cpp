@@ -106,22 +106,34 @@ static u64 cmd_word(const std::string& s, int w) {
   return x;
 }
 
-// A Cmd longer than 16 bytes is folded as a 64-bit fingerprint and a zero
-// word (the engine keeps it in its payload heap and digests the fingerprint;
-// dragonboat_amd/csrc/rbe_host.h cmd_fingerprint, restated here).
+// A Cmd longer than 16 bytes, or an entry with session fields, is folded as a
+// 64-bit fingerprint and a zero word (the engine keeps such an entry as a
+// payload-heap record and digests its fingerprint; dragonboat_amd/csrc/
+// rbe_host.h cmd_fingerprint / entry_fingerprint, restated here).
 static u64 cmd_fingerprint(const std::string& s) {
   const u64 len = s.size();
   u64 h = 0x243F6A8885A308D3ull ^ len;
   for (u64 i = 0; i < len; i += 8) h = splitmix64(h ^ cmd_word(s, (int)(i / 8)));
   return splitmix64(h ^ (len << 1));
 }
+static bool has_session(const Entry& e) {
+  return (e.key | e.client_id | e.series_id | e.responded_to) != 0;
+}
+static u64 entry_fingerprint(const Entry& e) {
+  u64 h = cmd_fingerprint(e.cmd);
+  if (has_session(e)) {
+    const u64 meta[4] = {e.key, e.client_id, e.series_id, e.responded_to};
+    for (u64 i = 0; i < 4; i++) h = splitmix64(h ^ meta[i] ^ ((i + 1) << 60));
+  }
+  return h;
+}
 
 static u64 hash_entry(u64 h, const Entry& e) {
   h = hfold(h, e.index);
   h = hfold(h, e.term);
   h = hfold(h, (u64)e.type | ((u64)e.cmd.size() << 32));
-  if (e.cmd.size() > 16) {
-    h = hfold(h, cmd_fingerprint(e.cmd));
+  if (e.cmd.size() > 16 || has_session(e)) {
+    h = hfold(h, entry_fingerprint(e));
     h = hfold(h, 0);
   } else {
     h = hfold(h, cmd_word(e.cmd, 0));

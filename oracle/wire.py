@@ -183,8 +183,9 @@ def entry_decode(data: bytes) -> dict:
             i += 1
     if h == 7:
         n, i = get_varint(data, i)
-        e["cmd"] = bytes(data[i:i + n])
-        i += n
+        end = _take(data, i, n)
+        e["cmd"] = bytes(data[i:end])
+        i = end
         h = data[i]
         i += 1
     if h != 0x7F:
@@ -269,16 +270,24 @@ def frame(payload: bytes) -> bytes:
     return MAGIC + bytes(h) + payload
 
 
+def _take(buf: bytes, i: int, n: int) -> int:
+    """The end of an n-byte field at i: ErrInvalidLength / io.ErrUnexpectedEOF
+    when it runs past the buffer (raft.pb.go skipRaft and the field reads)."""
+    if n > len(buf) - i:
+        raise ValueError("invalid length")
+    return i + n
+
+
 def _skip_field(buf: bytes, i: int, wt: int) -> int:  # skipRaft
     if wt == 0:
         _, i = get_varint(buf, i)
     elif wt == 1:
-        i += 8
+        i = _take(buf, i, 8)
     elif wt == 2:
         n, i = get_varint(buf, i)
-        i += n
+        i = _take(buf, i, n)
     elif wt == 5:
-        i += 4
+        i = _take(buf, i, 4)
     else:
         raise ValueError(f"bad wire type {wt}")
     return i
@@ -316,12 +325,14 @@ def message_decode(buf: bytes) -> tuple:
             m[MESSAGE_FIELDS[f]] = x
         elif f == 11 and wt == 2:
             n, i = get_varint(buf, i)
-            ents.append(entry_decode(buf[i:i + n]))
-            i += n
+            end = _take(buf, i, n)
+            ents.append(entry_decode(buf[i:end]))
+            i = end
         elif f == 12 and wt == 2:
             n, i = get_varint(buf, i)
-            m["snapshot"] = snapshot_decode(buf[i:i + n])
-            i += n
+            end = _take(buf, i, n)
+            m["snapshot"] = snapshot_decode(buf[i:end])
+            i = end
         else:
             i = _skip_field(buf, i, wt)
     m["reject"] = int(m["reject"] != 0)
@@ -337,8 +348,9 @@ def batch_decode(buf: bytes) -> dict:
         f, wt = tag >> 3, tag & 7
         if f == 1 and wt == 2:
             n, i = get_varint(buf, i)
-            out["requests"].append(message_decode(buf[i:i + n]))
-            i += n
+            end = _take(buf, i, n)
+            out["requests"].append(message_decode(buf[i:end]))
+            i = end
         elif f == 2 and wt == 0:
             out["deployment_id"], i = get_varint(buf, i)
         elif f == 3 and wt == 2:

@@ -17,16 +17,38 @@ def _cmd(rng):
     return bytes(rng.randrange(256) for _ in range(rng.randrange(17)))
 
 
+def session_entry(rng, cmd):
+    """A client proposal as requests.go:994-997 stamps it: Key, ClientID,
+    SeriesID, RespondedTo (values below 2^49 and colfer's 9-byte form above),
+    sometimes none (a NoOPSession proposal without a key)."""
+    def v():
+        u = rng.random()
+        return 0 if u < 0.15 else (rng.randrange(1, 1 << 20) if u < 0.6 else
+                                   rng.randrange(1 << 49, 1 << 64))
+    e = O.Entry(type=rng.choice((0, 0, 2, 3)), cmd=cmd(rng))
+    if rng.random() < 0.85:
+        e.key, e.client_id, e.series_id, e.responded_to = v(), v(), v(), v()
+    return e
+
+
 def plan_round(rng, n_rep, n, rnd, views, ext_apply, density=0.3, applied=None, cmd=None,
-               ready=0.0):
+               ready=0.0, session=False, props_only=False):
     """One round of host input: a list of (kind, replica, args).  `cmd(rng)`
-    draws a proposal's Cmd (default: 0-16 bytes)."""
+    draws a proposal's Cmd (default: 0-16 bytes); `session` proposes whole
+    raftpb.Entry values with session fields (session_entry); `props_only`
+    draws proposals alone."""
     cmd = cmd or _cmd
     ops = []
     for r in range(n_rep):
         if rng.random() < density:
-            ops.append(("prop", r, [(rng.choice((0, 0, 2, 3)), cmd(rng))
-                                    for _ in range(rng.randrange(1, 4))]))
+            if session:
+                ops.append(("prop", r, [session_entry(rng, cmd)
+                                        for _ in range(rng.randrange(1, 4))]))
+            else:
+                ops.append(("prop", r, [(rng.choice((0, 0, 2, 3)), cmd(rng))
+                                        for _ in range(rng.randrange(1, 4))]))
+        if props_only:
+            continue
         if rng.random() < density:
             ops.append(("read", r, ((rnd + 1) << 32 | (r + 1), rng.randrange(1 << 40))))
         if rng.random() < density / 6:
@@ -68,10 +90,17 @@ def apply_engine(eng, ops):
         eng.set_apply_ready([r for r, _ in by["ready"]], [a for _, a in by["ready"]])
 
 
+def _oracle_entry(x):
+    if isinstance(x, tuple):
+        return O.Entry(type=x[0], cmd=x[1])
+    return O.Entry(type=x.type, cmd=x.cmd, key=x.key, client_id=x.client_id,
+                   series_id=x.series_id, responded_to=x.responded_to)
+
+
 def apply_oracle(h, ops):
     for kind, r, a in ops:
         if kind == "prop":
-            h.push(O.PUSH_PROPOSE, r, entries=[O.Entry(type=t, cmd=c) for t, c in a])
+            h.push(O.PUSH_PROPOSE, r, entries=[_oracle_entry(x) for x in a])
         elif kind == "read":
             h.push(O.PUSH_READ, r, a[0], a[1])
         elif kind == "xfer":
@@ -87,7 +116,8 @@ def apply_oracle(h, ops):
 
 
 def run_driven(eng, ref, rounds, seed=1, tick_every=1, inputs=True, ext_apply=False,
-               density=0.3, skip=(), cmd=None, on_ops=None, ready=0.0, before_round=None):
+               density=0.3, skip=(), cmd=None, on_ops=None, ready=0.0, before_round=None,
+               session=False):
     """Step both `rounds` rounds with the same input; every `tick_every`-th
     round ticks, the others are RBE_STEP_NO_TICK rounds.  Returns the first
     divergence (round, replica, field, engine, oracle) or None."""
@@ -101,7 +131,8 @@ def run_driven(eng, ref, rounds, seed=1, tick_every=1, inputs=True, ext_apply=Fa
             before_round(rnd)
             views = ref.views()
         if inputs:
-            ops = plan_round(rng, n_rep, n, rnd, views, ext_apply, density, applied, cmd, ready)
+            ops = plan_round(rng, n_rep, n, rnd, views, ext_apply, density, applied, cmd, ready,
+                             session)
             if on_ops:
                 on_ops(ops)
             apply_engine(eng, ops)

@@ -6,7 +6,8 @@ import ctypes as C
 import os
 
 from dragonboat_amd.engine import (CTR_NUM, COUNTER_NAMES, NodeInputs, RbeEntry, RbeMessage,
-                                   RbeReplicaView, RbeWireFrame, entry_cmds, make_config)
+                                   RbeReplicaView, RbeWireFrame, entry_cmds, entry_fields,
+                                   make_config, outbox_call, push_messages_call)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _lib = None
@@ -37,10 +38,16 @@ def lib():
         L.soa_sleeping_groups.restype = C.c_uint64
         L.soa_sleeping_groups.argtypes = [C.c_void_p]
         P = C.POINTER
+        L.soa_get_outbox.restype = C.c_int
         L.soa_get_outbox.argtypes = [C.c_void_p, C.c_uint64, P(RbeMessage), C.c_uint32,
-                                     P(C.c_uint32), P(RbeEntry), C.c_uint32, P(C.c_uint32)]
+                                     P(C.c_uint32), P(RbeEntry), C.c_uint32, P(C.c_uint32),
+                                     C.c_void_p, C.c_uint64, P(C.c_uint64)]
+        L.soa_push_messages.restype = C.c_int
         L.soa_push_messages.argtypes = [C.c_void_p, C.c_uint64, P(C.c_uint64), P(RbeMessage),
-                                        P(RbeEntry)]
+                                        P(RbeEntry), C.c_void_p]
+        L.soa_get_entries.restype = C.c_int
+        L.soa_get_entries.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64,
+                                      P(RbeEntry)]
         L.soa_faults.restype = C.c_uint32
         L.soa_faults.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         L.soa_xchg_pack.restype = C.c_int
@@ -66,13 +73,14 @@ def lib():
                                          C.c_void_p, C.c_uint64, u64p]
         for name, args in {
                 "push_proposals": [C.c_uint64, u64p, u32p, u32p, u32p, P(C.c_uint8)],
+                "propose_entries": [C.c_uint64, u64p, u32p, P(RbeEntry), P(C.c_uint8)],
                 "push_read_index": [C.c_uint64, u64p, u64p, u64p],
                 "request_leader_transfer": [C.c_uint64, u64p, u64p],
                 "report_unreachable": [C.c_uint64, u64p, u64p],
                 "report_snapshot_status": [C.c_uint64, u64p, u64p, P(C.c_uint8)],
                 "notify_applied": [C.c_uint64, u64p, u64p],
                 "set_apply_ready": [C.c_uint64, u64p, P(C.c_uint8)],
-                "launch": [C.c_uint64, u64p, C.c_void_p, C.c_void_p]}.items():
+                "launch": [C.c_uint64, u64p, C.c_void_p, C.c_void_p, C.c_void_p]}.items():
             fn = getattr(L, "soa_" + name)
             fn.restype = C.c_int
             fn.argtypes = [C.c_void_p] + args
@@ -116,6 +124,14 @@ class SoaCpu(NodeInputs):
     def entry_cmds(self, replica, lo, hi):
         return entry_cmds(lib().soa_get_entry_cmds, self.h, replica, lo, hi)
 
+    def entry_records(self, replica, lo, hi):
+        """Every raftpb.Entry field of entries [lo, hi] (Engine.entry_records)."""
+        arr = (RbeEntry * (hi - lo + 1))()
+        rc = lib().soa_get_entries(self.h, replica, lo, hi, arr)
+        if rc != 0:
+            raise RuntimeError(f"soa_get_entries rc={rc}")
+        return [entry_fields(e, c) for e, c in zip(arr, self.entry_cmds(replica, lo, hi))]
+
     def step(self, tick=True):
         if tick:
             lib().soa_run(self.h, 1)
@@ -144,23 +160,11 @@ class SoaCpu(NodeInputs):
                               C.c_void_p(ent_ptr), n_ent)
 
     # transport boundary, same contract as Engine.outbox / Engine.push_messages
-    def outbox(self, replica, cap=256, ent_cap=1024):
-        arr = (RbeMessage * cap)()
-        ents = (RbeEntry * ent_cap)()
-        n, ne = C.c_uint32(), C.c_uint32()
-        rc = lib().soa_get_outbox(self.h, replica, arr, cap, C.byref(n), ents, ent_cap,
-                                  C.byref(ne))
-        assert rc == 0 and n.value <= cap and ne.value <= ent_cap, (rc, n.value, ne.value)
-        return [arr[i] for i in range(n.value)], [ents[i] for i in range(ne.value)]
+    def outbox(self, replica, cap=256, ent_cap=1024, cmd_cap=1 << 20):
+        return outbox_call(lib().soa_get_outbox, self.h, replica, cap, ent_cap, cmd_cap)
 
-    def push_messages(self, groups, msgs, ents):
-        n = len(msgs)
-        g = (C.c_uint64 * max(1, n))(*groups)
-        m = (RbeMessage * max(1, n))(*msgs)
-        e = (RbeEntry * max(1, len(ents)))(*ents)
-        rc = lib().soa_push_messages(self.h, n, g, m, e)
-        if rc != 0:
-            raise RuntimeError(f"soa_push_messages rc={rc}")
+    def push_messages(self, groups, msgs, ents, cmds=None):
+        push_messages_call(lib().soa_push_messages, self.h, groups, msgs, ents, cmds)
 
     # group-range snapshots, same contract as Engine.export_groups / import_groups
     def export_groups(self, first=0, count=None, cap=None):

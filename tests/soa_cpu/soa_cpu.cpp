@@ -30,8 +30,18 @@ struct SoaEngine {
   int staged = 0;  // STG_* bits: fast steps on a staged row (StageRow); 4: counts from inbound_aux
   u64 slow_total = 0;
   std::vector<u8> heap;  // payload heap (cfg.heap_bytes), as on the device
+  u64 heap_head = 0;     // Planes::heap_head
   u32 xflag = 0;         // fixed-layout exchange overflow (rbe_xchg_status)
 };
+
+// heap record bytes as rbe_engine.hip read_heap reads them
+static int soa_read_heap(SoaEngine* e, u64 pos, u64 off, u64 len, u8* dst) {
+  const HostHeap& h = e->hin.heap;
+  if (!h.valid(pos, off + len)) return RBE_E_STATE;
+  if (h.read_staged(pos, off, len, dst)) return RBE_OK;
+  for (u64 i = 0; i < len; i++) dst[i] = e->heap[(pos + off + i) % h.cap];
+  return RBE_OK;
+}
 
 template <typename T>
 static T* alloc(SoaEngine* e, u64 n) {
@@ -45,6 +55,7 @@ static void run_round(SoaEngine* e, bool tick = true) {
   if (!e->hin.empty()) {  // the HIP engine uploads and scatters the same records
     HostHeap& hp = e->hin.heap;
     for (u64 p = hp.flushed; p < hp.head; p++) e->heap[p % hp.cap] = hp.stage[p - hp.flushed];
+    e->heap_head = hp.head;
     e->hin.apply_host(e->P);
     e->hin.clear();
   }
@@ -237,6 +248,22 @@ void* soa_create(const rbe_config* cfg) {
   C.heap_bytes = (cfg->heap_bytes + 255) & ~255ull;
   e->heap.assign(C.heap_bytes, 0);
   e->hin.init(R, C.n, C.in_cap, C.heap_bytes);
+  e->hin.rep_world = C.rep_world;
+  e->hin.rep_rank = C.rep_rank;
+  if (C.heap_bytes) {
+    P.heap_head = &e->heap_head;
+    e->hin.heap.low_fn = [e](u64* lo) -> int {  // k_heap_low, group by group
+      u64 m = ~0ull;
+      for (u64 g = 0; g < e->C.n_groups; g++) {
+        u64 x = e->C.n == 1   ? heap_low_group<1>(e->P, e->C, g, e->round)
+                : e->C.n == 3 ? heap_low_group<3>(e->P, e->C, g, e->round)
+                              : heap_low_group<5>(e->P, e->C, g, e->round);
+        if (x < m) m = x;
+      }
+      *lo = m;
+      return RBE_OK;
+    };
+  }
   P.counters = nullptr;
   for (u64 r = 0; r < R; r++) {
     if (N == 1) launch_replica<1>(P, C, r);
@@ -267,15 +294,40 @@ int soa_get_entry_cmds(void* h, uint64_t replica, uint64_t lo, uint64_t hi, uint
   for (u64 i = lo; i <= hi; i++) {
     const Body& b = e->P.pay_ring[(i & (C.ring - 1)) * C.n_rep + replica];
     u8* d = buf + offsets[i - lo];
-    if (b.len <= 16) {
+    if (!ent_heap(b.type)) {
       u8 w[16];
       memcpy(w, &b.lo, 8);
       memcpy(w + 8, &b.hi, 8);
       memcpy(d, w, b.len);
-    } else {
-      if (!e->hin.heap.valid(b.hi, b.len)) return RBE_E_STATE;
-      memcpy(d, e->heap.data() + b.hi % e->hin.heap.cap, b.len);
+    } else if (b.len) {
+      const int rc = soa_read_heap(e, b.hi, kHeapHdr, b.len, d);
+      if (rc) return rc;
     }
+  }
+  return RBE_OK;
+}
+// rbe_get_entries: every raftpb.Entry field of entries [lo, hi] of a replica
+int soa_get_entries(void* h, uint64_t replica, uint64_t lo, uint64_t hi, rbe_entry* out) {
+  SoaEngine* e = (SoaEngine*)h;
+  const Params& C = e->C;
+  if (replica >= C.n_rep || lo == 0 || hi < lo) return RBE_E_INVALID;
+  const Core& c = e->P.core[replica];
+  if (hi > c.last_index || c.last_index - lo >= C.ring) return RBE_E_INVALID;
+  auto rd = [e](u64 pos, u64 off, u64 len, u8* dst) { return soa_read_heap(e, pos, off, len, dst); };
+  for (u64 i = lo; i <= hi; i++) {
+    const u64 sl = (i & (C.ring - 1)) * C.n_rep + replica;
+    const Body& b = e->P.pay_ring[sl];
+    Ent x;
+    x.term = e->P.term_ring[sl];
+    x.type = b.type;
+    x.len = b.len;
+    x.lo = b.lo;
+    x.hi = b.hi;
+    rbe_entry& o = out[i - lo];
+    memset(&o, 0, sizeof(o));
+    const int rc = entry_out(x, &o, nullptr, rd);
+    if (rc) return rc;
+    o.index = i;
   }
   return RBE_OK;
 }
@@ -315,17 +367,25 @@ int soa_push_proposals(void* h, uint64_t n, const uint64_t* replica, const uint3
   if (!e->C.ext_inputs) return RBE_E_STATE;
   return e->hin.push_proposals(n, replica, n_ents, type, cmd_len, cmd);
 }
+int soa_propose_entries(void* h, uint64_t n, const uint64_t* replica, const uint32_t* n_ents,
+                        const rbe_entry* ents, const uint8_t* cmd) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (!e->C.ext_inputs) return RBE_E_STATE;
+  return e->hin.push_entries(n, replica, n_ents, ents, cmd);
+}
 // rbe_launch on the host build (same checks and per-replica restart)
 int soa_launch(void* h, uint64_t n, const uint64_t* replica, const rbe_launch_state* st,
-               const rbe_entry* ents) {
+               const rbe_entry* ents, const uint8_t* cmd) {
   SoaEngine* e = (SoaEngine*)h;
+  if (n && replica) {
+    std::vector<u64> v(replica, replica + n);
+    std::sort(v.begin(), v.end());
+    if (std::adjacent_find(v.begin(), v.end()) != v.end()) return RBE_E_INVALID;
+  }
   std::vector<u64> terms;
   std::vector<Body> bodies;
-  int rc = launch_rows(e->C, n, replica, st, ents, terms, bodies);
+  int rc = launch_rows(e->C, e->hin.heap, n, replica, st, ents, cmd, terms, bodies);
   if (rc) return rc;
-  std::vector<u64> v(replica, replica + n);
-  std::sort(v.begin(), v.end());
-  if (std::adjacent_find(v.begin(), v.end()) != v.end()) return RBE_E_INVALID;
   const u32 ppar = (e->round & 1u) ^ 1u;
   u64 off = 0;
   for (u64 i = 0; i < n; i++) {
@@ -404,15 +464,18 @@ int64_t soa_wire_encode(void* h, uint64_t deployment_id, uint32_t bin_ver, uint3
       std::vector<u8> pay;
       u32 nm = 0;
       for (u64 g = g0; g < g1; g++) {
-        u32 cm = 0, ci = 0;
+        u32 cm = 0, ci = 0, bad = 0;
         u32 b = 0;
-        if (N == 3) b = wire_cell<3>(e->P, C, e->heap.data(), g, k, d, e->round, nullptr, &cm, &ci);
-        else b = wire_cell<5>(e->P, C, e->heap.data(), g, k, d, e->round, nullptr, &cm, &ci);
+        const u8* hp = e->heap.data();
+        const u64 hh = e->hin.heap.flushed;
+        if (N == 3) b = wire_cell<3>(e->P, C, hp, hh, g, k, d, e->round, nullptr, &cm, &ci, &bad);
+        else b = wire_cell<5>(e->P, C, hp, hh, g, k, d, e->round, nullptr, &cm, &ci, &bad);
+        if (bad) return -2;  // rbe_wire_encode: RBE_E_STATE
         if (!cm) continue;
         const size_t at = pay.size();
         pay.resize(at + b);
-        if (N == 3) wire_cell<3>(e->P, C, e->heap.data(), g, k, d, e->round, pay.data() + at, &cm, &ci);
-        else wire_cell<5>(e->P, C, e->heap.data(), g, k, d, e->round, pay.data() + at, &cm, &ci);
+        if (N == 3) wire_cell<3>(e->P, C, hp, hh, g, k, d, e->round, pay.data() + at, &cm, &ci, &bad);
+        else wire_cell<5>(e->P, C, hp, hh, g, k, d, e->round, pay.data() + at, &cm, &ci, &bad);
         nm += cm;
       }
       if (!nm) continue;
@@ -593,6 +656,7 @@ extern "C" uint32_t soa_xchg_status(void* h) { return ((SoaEngine*)h)->xflag; }
 
 extern "C" int soa_xchg_pack(void* h, uint8_t* buf, const uint64_t* cap, uint32_t* counts) {
   SoaEngine* e = (SoaEngine*)h;
+  if (e->C.heap_bytes) return RBE_E_STATE;  // as rbe_xchg_pack: heap positions are local
   if (e->C.n == 3) return soa_xchg_pack_t<3>(e, buf, cap, counts);
   if (e->C.n == 5) return soa_xchg_pack_t<5>(e, buf, cap, counts);
   return soa_xchg_pack_t<1>(e, buf, cap, counts);
@@ -608,7 +672,8 @@ extern "C" void soa_xchg_unpack(void* h, const void* c, uint64_t nc, const void*
 // transport boundary on the host build (rbe_get_outbox / rbe_push_messages)
 extern "C" int soa_get_outbox(void* h, uint64_t replica, rbe_message* out, uint32_t cap,
                               uint32_t* n_out, rbe_entry* ents, uint32_t ent_cap,
-                              uint32_t* n_ents) {
+                              uint32_t* n_ents, uint8_t* cmd, uint64_t cmd_cap,
+                              uint64_t* cmd_bytes) {
   SoaEngine* e = (SoaEngine*)h;
   if (replica >= e->C.n_rep || e->round == 0) return RBE_E_INVALID;
   const u32 N = e->C.n, par = (e->round - 1) & 1u;
@@ -618,30 +683,37 @@ extern "C" int soa_get_outbox(void* h, uint64_t replica, rbe_message* out, uint3
   const Msg* lst = e->P.msgs[par] + (g * N + k) * N * (u64)e->C.maxm;
   const Ent* arena = e->P.arena[par] + replica * e->C.ecap;
   const u32 rd = e->round;
-  if (N == 3) outbox_messages<3>(e->C, g, k, row, rd, lst, arena, out, cap, ents, ent_cap, n_out, n_ents);
-  else if (N == 5) outbox_messages<5>(e->C, g, k, row, rd, lst, arena, out, cap, ents, ent_cap, n_out, n_ents);
-  else outbox_messages<1>(e->C, g, k, row, rd, lst, arena, out, cap, ents, ent_cap, n_out, n_ents);
-  return RBE_OK;
+  auto hr = [e](u64 pos, u64 off, u64 len, u8* dst) { return soa_read_heap(e, pos, off, len, dst); };
+  if (N == 3)
+    return outbox_messages<3>(e->C, g, k, row, rd, lst, arena, out, cap, ents, ent_cap, n_out,
+                              n_ents, cmd, cmd_cap, cmd_bytes, hr);
+  if (N == 5)
+    return outbox_messages<5>(e->C, g, k, row, rd, lst, arena, out, cap, ents, ent_cap, n_out,
+                              n_ents, cmd, cmd_cap, cmd_bytes, hr);
+  return outbox_messages<1>(e->C, g, k, row, rd, lst, arena, out, cap, ents, ent_cap, n_out,
+                            n_ents, cmd, cmd_cap, cmd_bytes, hr);
 }
 template <int N>
 static int soa_push_t(SoaEngine* e, uint64_t n, const uint64_t* group, const rbe_message* msgs,
-                      const rbe_entry* ents) {
+                      const rbe_entry* ents, const uint8_t* cmd) {
   std::vector<XCnt> c;
   std::vector<XMsg> m;
   std::vector<XEnt> x;
-  const int rc = messages_to_records<N>(e->C, e->round, n, group, msgs, ents, c, m, x);
+  const int rc =
+      messages_to_records<N>(e->C, e->hin.heap, e->round, n, group, msgs, ents, cmd, c, m, x);
   if (rc) return rc;
   soa_xchg_unpack_t<N>(e, c.data(), c.size(), m.data(), m.size(), x.data(), x.size());
   return RBE_OK;
 }
 extern "C" int soa_push_messages(void* h, uint64_t n, const uint64_t* group,
-                                 const rbe_message* msgs, const rbe_entry* ents) {
+                                 const rbe_message* msgs, const rbe_entry* ents,
+                                 const uint8_t* cmd) {
   SoaEngine* e = (SoaEngine*)h;
   if (e->round == 0) return RBE_E_INVALID;
   if (e->C.rep_world <= 1) return RBE_E_STATE;
-  if (e->C.n == 3) return soa_push_t<3>(e, n, group, msgs, ents);
-  if (e->C.n == 5) return soa_push_t<5>(e, n, group, msgs, ents);
-  return soa_push_t<1>(e, n, group, msgs, ents);
+  if (e->C.n == 3) return soa_push_t<3>(e, n, group, msgs, ents, cmd);
+  if (e->C.n == 5) return soa_push_t<5>(e, n, group, msgs, ents, cmd);
+  return soa_push_t<1>(e, n, group, msgs, ents, cmd);
 }
 
 // Group-range snapshots in the engine's byte layout (rbe_export_groups /

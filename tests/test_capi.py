@@ -77,7 +77,7 @@ def test_null_handles_are_rejected():
 def test_struct_layouts_match_header():
     # sizes fixed by include/rbe.h (8-byte aligned C structs)
     assert C.sizeof(E.RbeMessage) == 8 + 9 * 8 + 8
-    assert C.sizeof(E.RbeEntry) == 40
+    assert C.sizeof(E.RbeEntry) == 40 + 4 * 8  # + Key, ClientID, SeriesID, RespondedTo
     assert C.sizeof(E.RbeReadyToRead) == 24
     assert C.sizeof(E.RbeUpdate) == 8 * 8 + 10 * 4
     # and every binding struct against the library's own sizeof (rbe_abi_sizes)

@@ -55,7 +55,7 @@ def test_gpu_wire_heap_cmds(gpu_available):
             reps = [g * n + rng.randrange(n) for g in range(G)]
             eng.push_proposals(reps, [[mixed_cmd(rng)] for _ in reps])
         eng.run(1)
-        cells, _ = outbox_by_cell(eng, G, n, cmds=lambda r, i: eng.entry_cmds(r, i, i)[0])
+        cells, _ = outbox_by_cell(eng, G, n)
         tot = eng.wire_encode(1, 2, 3, ADDRS[:n])
         stream, frames = eng.wire_fetch(tot)
         exp, exp_frames = expected_stream(cells, G, n, 3, 1, 2)

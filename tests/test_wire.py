@@ -121,8 +121,7 @@ def test_host_build_frames_with_snapshots_and_heap_cmds():
             reps = [g * n + rng.randrange(n) for g in range(G)]
             eng.push_proposals(reps, [[mixed_cmd(rng)] for _ in reps])
         eng.run(1)
-        cells, n_is = outbox_by_cell(eng, G, n,
-                                     cmds=lambda r, i: eng.entry_cmds(r, i, i)[0])
+        cells, n_is = outbox_by_cell(eng, G, n)
         saw_is += n_is
         saw_long += sum(1 for v in cells.values() for _, es in v for e in es
                         if len(e["cmd"]) > 16)

@@ -16,43 +16,52 @@ def deliver(engs, n, n_rep):
     """One transport hop: every engine's owned senders → the owners of the
     destinations.  Returns the number of messages moved."""
     world = len(engs)
-    batches = [([], [], []) for _ in range(world)]
+    batches = [([], [], [], []) for _ in range(world)]
     moved = 0
     for rank, e in enumerate(engs):
         for r in range(n_rep):
             g, k = divmod(r, n)
             if owner(g, k, world) != rank:
                 continue
-            msgs, ents = e.outbox(r)
+            msgs, ents, cmds = e.outbox(r)
             ei = 0
             for m in msgs:
                 ne = m.n_entries
                 dst = owner(g, m.to - 1, world)
                 if dst != rank:
-                    gs, ms, es = batches[dst]
+                    gs, ms, es, cs = batches[dst]
                     gs.append(g)
                     ms.append(m)
                     es.extend(ents[ei:ei + ne])
+                    cs.extend(cmds[ei:ei + ne])
                     moved += 1
                 ei += ne
             assert ei == len(ents)
     for rank, e in enumerate(engs):
-        gs, ms, es = batches[rank]
-        e.push_messages(gs, ms, es)
+        gs, ms, es, cs = batches[rank]
+        e.push_messages(gs, ms, es, cs)
     return moved
 
 
-def run_transport(engs, ref, n, rounds, every=25):
+def run_transport(engs, ref, n, rounds, every=25, inputs=None):
     """Step W engines and the oracle in lockstep with a transport hop after
     each round; compare every owned replica with the oracle every `every`
-    rounds.  Returns (first divergence or None, messages moved)."""
+    rounds.  `inputs(rnd)` returns host input ops for the round (input_util
+    plan_round form), applied to the owning engine and the oracle.  Returns
+    (first divergence or None, messages moved)."""
+    from input_util import apply_engine, apply_oracle
     world = len(engs)
     n_rep = len(ref.views())
     moved = 0
     for done in range(1, rounds + 1):
+        if inputs:
+            ops = inputs(done - 1)
+            for rank, e in enumerate(engs):
+                apply_engine(e, [op for op in ops if owner(op[1] // n, op[1] % n, world) == rank])
+            apply_oracle(ref, ops)
         for e in engs:
             e.step()
-        ref.run(1)
+        ref.step()
         moved += deliver(engs, n, n_rep)
         if done % every and done != rounds:
             continue

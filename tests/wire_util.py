@@ -16,26 +16,29 @@ def _msg_dict(m):
             "reject": m.reject, "hint": m.hint, "hint_high": m.hint_high}
 
 
-def _ent_dict(e, cmd=None):
-    return {"term": e.term, "index": e.index, "type": e.type,
-            "cmd": bytes(e.cmd[:e.cmd_len]) if cmd is None else cmd}
+SESSION = ("key", "client_id", "series_id", "responded_to")
 
 
-def outbox_by_cell(eng, n_groups, n, cmds=None):
+def _ent_dict(e, cmd):
+    d = {"term": e.term, "index": e.index, "type": e.type, "cmd": cmd}
+    d.update({f: getattr(e, f) for f in SESSION})
+    return d
+
+
+def outbox_by_cell(eng, n_groups, n):
     """{(g, k, d): [(message dict, [entry dicts])]} of the last round, InstallSnapshot
-    messages dropped; `cmds(replica, index)` supplies Cmds longer than 16 bytes."""
+    messages dropped; entries with their whole Cmds and session fields
+    (rbe_get_outbox)."""
     cells, n_is = {}, 0
     for r in range(n_groups * n):
         g, k = divmod(r, n)
-        msgs, ents = eng.outbox(r)
+        msgs, ents, cmds = eng.outbox(r)
         ei = 0
         for m in msgs:
             es = []
             for _ in range(m.n_entries):
-                e = ents[ei]
+                es.append(_ent_dict(ents[ei], cmds[ei]))
                 ei += 1
-                cmd = cmds(r, e.index) if (cmds and e.cmd_len > 16) else None
-                es.append(_ent_dict(e, cmd))
             if m.type == INSTALL_SNAPSHOT:
                 n_is += 1
                 continue
@@ -89,8 +92,7 @@ def check_decoded(msgs, ents, cmd, cells, n_groups, n, gpb):
         for x in ee:
             e = ents[ei]
             ei += 1
-            got = {"term": e.term, "index": e.index, "type": e.type,
-                   "cmd": cmd[ci:ci + e.cmd_len]}
+            got = _ent_dict(e, cmd[ci:ci + e.cmd_len])
             ci += e.cmd_len
             assert got == x
             assert bytes(e.cmd[:min(16, e.cmd_len)]) == x["cmd"][:16]
