@@ -895,16 +895,18 @@ static int flush_inputs(rbe_engine* e) {
     memcpy(b + o_ar, h.app_rep.data(), na * sizeof(u64));
     memcpy(b + o_av, h.app_val.data(), na * sizeof(u64));
   }
-  HIP_OK(hipMemcpyAsync(e->in_dev, b, total, hipMemcpyHostToDevice, e->stream));
+  if (total) HIP_OK(hipMemcpyAsync(e->in_dev, b, total, hipMemcpyHostToDevice, e->stream));
   if (!h.ents.empty())
     HIP_OK(hipMemcpyAsync(e->P.in_ents, h.ents.data(), h.ents.size() * sizeof(Ent),
                           hipMemcpyHostToDevice, e->stream));
   const u64 m = n > na ? n : na;
-  hipLaunchKernelGGL(k_ext_scatter, dim3(grid_for(m)), dim3(kBlock), 0, e->stream, e->P,
-                     e->C.n, (const u64*)e->in_dev, (const ExtIn*)(e->in_dev + o_rec), n,
-                     (const u64*)(e->in_dev + o_ar), (const u64*)(e->in_dev + o_av), na, e->L,
-                     e->round & 1u);
-  HIP_OK(hipGetLastError());
+  if (m) {  // (a flush of heap records alone, e.g. from rbe_push_messages, has none)
+    hipLaunchKernelGGL(k_ext_scatter, dim3(grid_for(m)), dim3(kBlock), 0, e->stream, e->P,
+                       e->C.n, (const u64*)e->in_dev, (const ExtIn*)(e->in_dev + o_rec), n,
+                       (const u64*)(e->in_dev + o_ar), (const u64*)(e->in_dev + o_av), na, e->L,
+                       e->round & 1u);
+    HIP_OK(hipGetLastError());
+  }
   HIP_OK(hipEventRecord(e->in_ev, e->stream));
   // the entries and heap bytes came from pageable memory: wait for those
   // copies before the vectors are reused (inputs are the host-driven path, not

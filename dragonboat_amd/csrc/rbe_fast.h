@@ -199,6 +199,13 @@ struct FastOut {
     (void)ctr;  // counted in fast_finish (new bits of the sticky word)
     fault |= f;
   }
+  // Fault and event bits are OR-ed in unconditionally (0 when the condition
+  // fails): two sibling branches that OR constants into different fields get
+  // merged by the compiler into one store through a selected pointer, which
+  // puts the whole FastOut in scratch memory — and a scratch reload after the
+  // lane's first store waits for every store before it (vmcnt is in order).
+  RBE_HD void fault_if(bool c, u32 f) { fault |= c ? f : 0u; }
+  RBE_HD void event_if(bool c, u32 e) { events |= c ? e : 0u; }
   // `ent` points at the message's entries in this round's arena (may be null
   // when n_ent == 0).
   RBE_HD void send(const Planes& P, const Params& C, StepCounters& ctr, Msg& m, const Ent* ent) {
@@ -235,7 +242,7 @@ struct FastOut {
     const u32 c = get_pc(d);
     const u32 a = c & 0x7Fu, b = (c >> 7) & 0x7Fu;
     const u32 full = drop ? 0u : (a + b >= C.maxm ? 1u : 0u);
-    if (full) fault |= F_OUTBOX;
+    fault_if(full != 0, F_OUTBOX);
     const u32 ok = 1u - drop - full;
     n_drop_msg += drop;
     n_out += ok;
@@ -255,16 +262,15 @@ struct FastOut {
   }
   RBE_HD void dropped_read_index(const Planes& P, const Params& C, StepCounters& ctr, u64 low,
                                  u64 high) {  // raft.go:1999-2012
-    if (n_drop_ri >= C.dri_cap) {
-      set_fault(ctr, F_DROPLIST);
-      return;
-    }
+    const bool full = n_drop_ri >= C.dri_cap;
+    fault_if(full, F_DROPLIST);
+    event_if(!full, EV_READ_INDEX_DROPPED);
+    if (full) return;
     DropRI x;
     x.low = low;
     x.high = high;
     P.dri[r * C.dri_cap + n_drop_ri] = x;
     n_drop_ri++;
-    events |= EV_READ_INDEX_DROPPED;
     if (TRACE) {
       drop_hash = hfold(drop_hash, low);
       drop_hash = hfold(drop_hash, high);
@@ -272,10 +278,9 @@ struct FastOut {
   }
   RBE_HD void ready_to_read(const Planes& P, const Params& C, StepCounters& ctr, u64 index,
                             u64 low, u64 high) {  // raft.go:1624-1630
-    if (n_rtr >= C.rtr_cap) {
-      set_fault(ctr, F_RTR);
-      return;
-    }
+    const bool full = n_rtr >= C.rtr_cap;
+    fault_if(full, F_RTR);
+    if (full) return;
     RTR x;
     x.index = index;
     x.low = low;
@@ -357,10 +362,9 @@ RBE_HD void fast_node_snapshot(const Planes& P, const Params& C, StepCounters& c
   sp->ss_req = la;
   u64 t = t_last;
   if (la != last) {
-    if (last - la >= C.ring) {
-      o.set_fault(ctr, F_WINDOW);
-      return;
-    }
+    const bool miss = last - la >= C.ring;
+    o.fault_if(miss, F_WINDOW);
+    if (miss) return;
     t = P.term_ring[(la & (u64)(C.ring - 1)) * C.n_rep + o.r];
   }
   if (t == 0) return;
@@ -421,10 +425,9 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
   u64 apply_hash = 0;
   if (TRACE && u.apply_hi >= u.apply_lo) {
     for (u64 i = u.apply_lo; i <= u.apply_hi; i++) {
-      if (c.last_index - i >= C.ring) {
-        o.set_fault(ctr, F_WINDOW);
-        break;
-      }
+      const bool miss = c.last_index - i >= C.ring;
+      o.fault_if(miss, F_WINDOW);
+      if (miss) break;
       const u64 s = (i & (u64)(C.ring - 1)) * C.n_rep + r;
       const Body b = P.pay_ring[s];
       apply_hash = hfold(apply_hash, i);
@@ -780,28 +783,21 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   auto log_term = [&](u64 idx) -> u64 {
     if (idx > c.last_index || idx == 0) return 0;
     if (idx == c.last_index) return c.t_last;
-    if (c.last_index - idx >= C.ring) {
-      o.set_fault(ctr, F_WINDOW);
-      return 0;
-    }
-    ctr.v[C_RING_ACCESS]++;
-    return idx >= c.lead_start ? c.term : 0;
+    const bool miss = c.last_index - idx >= C.ring;
+    o.fault_if(miss, F_WINDOW);
+    ctr.v[C_RING_ACCESS] += miss ? 0u : 1u;
+    return !miss && idx >= c.lead_start ? c.term : 0;
   };
   auto ent_at = [&](u64 idx) -> Ent {  // ring entry idx (registers when just proposed)
+    // anything else is excluded by the eligibility rule next[s] > last0
+    const bool hit = idx == prop_idx && prop_idx != 0;
+    o.fault_if(!hit, F_UNSUPPORTED);
     Ent e;
-    if (idx == prop_idx && prop_idx != 0) {
-      e.term = c.term;
-      e.type = E_Application;
-      e.len = 16;
-      e.lo = prop_lo;
-      e.hi = prop_hi;
-    } else {  // excluded by the eligibility rule next[s] > last0
-      o.set_fault(ctr, F_UNSUPPORTED);
-      e.term = 0;
-      e.type = E_Application;
-      e.len = 0;
-      e.lo = e.hi = 0;
-    }
+    e.term = hit ? c.term : 0;
+    e.type = E_Application;
+    e.len = hit ? 16u : 0u;
+    e.lo = hit ? prop_lo : 0;
+    e.hi = hit ? prop_hi : 0;
     return e;
   };
   auto limit_count = [&](u64 lo, u64 hi) -> u64 {  // limitSize, entryutils.go:52-64
@@ -823,13 +819,11 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
     if (seg_len && lo >= seg_lo && lo <= seg_lo + seg_len && seg_off + seg_len == arena_used) {
       const u64 have_hi = seg_lo + seg_len;
       const u32 extra = (u32)(lo + cnt - have_hi);
-      if (arena_used + extra > C.ecap) {
-        o.set_fault(ctr, F_ARENA);
-        return false;
-      }
+      o.fault_if(arena_used + extra > C.ecap, F_ARENA);
+      if (arena_used + extra > C.ecap) return false;
       for (u32 i = 0; i < extra; i++) {
         const u64 idx = have_hi + i;
-        if (c.last_index - idx >= C.ring) o.set_fault(ctr, F_WINDOW);
+        o.fault_if(c.last_index - idx >= C.ring, F_WINDOW);
         arena[arena_used + i] = ent_at(idx);
       }
       ctr.v[C_RING_ACCESS] += extra;
@@ -838,13 +832,11 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
       *off = seg_off + (u32)(lo - seg_lo);
       return true;
     }
-    if (arena_used + cnt > C.ecap) {
-      o.set_fault(ctr, F_ARENA);
-      return false;
-    }
+    o.fault_if(arena_used + cnt > C.ecap, F_ARENA);
+    if (arena_used + cnt > C.ecap) return false;
     for (u32 i = 0; i < cnt; i++) {
       const u64 idx = lo + i;
-      if (c.last_index - idx >= C.ring) o.set_fault(ctr, F_WINDOW);
+      o.fault_if(c.last_index - idx >= C.ring, F_WINDOW);
       arena[arena_used + i] = ent_at(idx);
     }
     ctr.v[C_RING_ACCESS] += cnt;
@@ -882,10 +874,8 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
     const u64 qv = m[N - Q];
     if (qv <= c.committed) return false;
     if (log_term(qv) != c.term) return false;
-    if (qv > c.last_index) {  // commitTo panics (logentry.go:324-333)
-      o.set_fault(ctr, F_PANIC);
-      return true;
-    }
+    o.fault_if(qv > c.last_index, F_PANIC);  // commitTo panics (logentry.go:324-333)
+    if (qv > c.last_index) return true;
     c.committed = qv;
     return true;
   };
@@ -912,7 +902,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
       // progress (remote.go:135-143)
       if (rs == RS_Replicate) next[s] = nx + cnt;
       else if (rs == RS_Retry) st[s] = (st[s] & ~3u) | RS_Wait;
-      else o.set_fault(ctr, F_PANIC);
+      o.fault_if(rs != RS_Replicate && rs != RS_Retry, F_PANIC);
       rdirty |= 1u << s;
     }
     o.send(P, C, ctr, m, arena + m.ent_off);
@@ -939,7 +929,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
 #pragma unroll
     for (u32 i = 0; i < Cap::RQ; i++) {
       if (i >= done) continue;
-      if (rq_ix[i] > sindex) o.set_fault(ctr, F_PANIC);
+      o.fault_if(rq_ix[i] > sindex, F_PANIC);
       if (rq_fr[i] == 0 || rq_fr[i] == o.self) {
         o.ready_to_read(P, C, ctr, sindex, rq_lo[i], rq_hi[i]);
       } else {
@@ -1090,10 +1080,9 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
 #pragma unroll
         for (u32 i = 0; i < Cap::RQ; i++)
           if (i + 1 == rq_n) back_ix = rq_ix[i];
-        if (rq_n > 0 && c.committed < back_ix) o.set_fault(ctr, F_PANIC);
-        if (rq_n >= C.rq_cap) {
-          o.set_fault(ctr, F_READQ);
-        } else {
+        o.fault_if(rq_n > 0 && c.committed < back_ix, F_PANIC);
+        o.fault_if(rq_n >= C.rq_cap, F_READQ);
+        if (rq_n < C.rq_cap) {
 #pragma unroll
           for (u32 i = 0; i < Cap::RQ; i++)
             if (i == rq_n) {
@@ -1161,9 +1150,8 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   if (inp == 1) {
     const u64 lo = wl_payload_lo(C.seed, cid, round), hi = mix64(lo);
     ctr.v[C_PROPOSALS]++;
-    if (arena_used + 1 > C.ecap) {
-      o.set_fault(ctr, F_ARENA);
-    } else {
+    o.fault_if(arena_used + 1 > C.ecap, F_ARENA);
+    if (arena_used + 1 <= C.ecap) {
       Ent e;  // staged in the arena as the Propose message carries it (term 0)
       e.term = 0;
       e.type = E_Application;
@@ -1450,20 +1438,16 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   auto log_term = [&](u64 idx) -> u64 {
     if (idx > c.last_index || idx == 0) return 0;
     if (idx == c.last_index) return c.t_last;
-    if (c.last_index - idx >= C.ring) {
-      o.set_fault(ctr, F_WINDOW);
-      return 0;
-    }
-    ctr.v[C_RING_ACCESS]++;
-    o.set_fault(ctr, F_UNSUPPORTED);  // excluded by the eligibility simulation
+    const bool miss = c.last_index - idx >= C.ring;
+    // a miss is F_WINDOW; a hit is excluded by the eligibility simulation
+    o.fault_if(true, miss ? F_WINDOW : F_UNSUPPORTED);
+    ctr.v[C_RING_ACCESS] += miss ? 0u : 1u;
     return 0;
   };
   auto commit_to = [&](u64 idx) {  // logentry.go:324-333
     if (idx <= c.committed) return;
-    if (idx > c.last_index) {
-      o.set_fault(ctr, F_PANIC);
-      return;
-    }
+    o.fault_if(idx > c.last_index, F_PANIC);
+    if (idx > c.last_index) return;
     c.committed = idx;
   };
   const u32 lid = ls + 1;
@@ -1509,12 +1493,11 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
             }
           }
           if (conflict != 0) {
-            if (conflict <= c.committed) {
-              o.set_fault(ctr, F_PANIC);
-            } else {
-              if (conflict - 1 >= 1 && conflict - 1 <= c.last_index &&
-                  log_term(conflict - 1) > ent(ci).term)
-                o.set_fault(ctr, F_PANIC);
+            o.fault_if(conflict <= c.committed, F_PANIC);
+            if (conflict > c.committed) {
+              o.fault_if(conflict - 1 >= 1 && conflict - 1 <= c.last_index &&
+                             log_term(conflict - 1) > ent(ci).term,
+                         F_PANIC);
               u64 tl = c.t_last;
               for (u32 e = ci; e < m.n_ent; e++) {
                 const Ent x = ent(e);
@@ -1542,7 +1525,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
           resp.reject = 1;
           resp.log_index = m.log_index;
           resp.hint = c.last_index;
-          o.events |= EV_REPLICATION_REJECTED;
+          o.event_if(true, EV_REPLICATION_REJECTED);
         }
         o.send(P, C, ctr, resp, nullptr);
       } else if (m.type == M_Heartbeat) {  // handleHeartbeatMessage, raft.go:1301-1309
@@ -1568,12 +1551,11 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   } else {
     flags &= (u8)~HF_RAFT_QUIESCE;
     etick++;  // nonLeaderTick; reaching the timeout is excluded above
-    if (etick >= h.rand_et) o.set_fault(ctr, F_UNSUPPORTED);
+    o.fault_if(etick >= h.rand_et, F_UNSUPPORTED);
   }
-  if (n_in && (u8)lid != c.leader) {
-    cdirty |= 4u;
-    o.events |= EV_LEADER_UPDATED;
-  }
+  const bool lchg = n_in && (u8)lid != c.leader;
+  cdirty |= lchg ? 4u : 0u;
+  o.event_if(lchg, EV_LEADER_UPDATED);
   c.leader = n_in ? (u8)lid : c.leader;
   fast_finish<N, TRACE, STG>(P, C, ctr, o, q, R_Follower, flags, h, c, etick, htick, committed0,
                         digest0, sr, cdirty);

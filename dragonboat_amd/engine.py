@@ -773,6 +773,10 @@ class Engine(NodeInputs):
         _check(self.lib.rbe_fault_summary(self.h, C.byref(n), C.byref(o)), "rbe_fault_summary")
         return n.value, o.value
 
+    def faults(self):
+        """(replicas with a sticky fault word, OR of the words): the host build's name."""
+        return self.fault_summary()
+
 
 def xchg_chunk_bytes(caps) -> int:
     """Bytes of one peer's chunk in the fixed-capacity exchange layout."""
