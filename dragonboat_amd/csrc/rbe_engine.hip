@@ -48,7 +48,8 @@ RBE_EXTERN_ROUND(5, false)
 __global__ __launch_bounds__(kBlock) void k_ext_scatter(Planes P, u32 nrep, const u64* reps,
                                                         const ExtIn* recs, u64 n,
                                                         const u64* app_rep, const u64* app_val,
-                                                        u64 na, Lists L, u32 par) {
+                                                        u64 na, const CommitRec* cr, u64 nc,
+                                                        Params C, Lists L, u32 par) {
   const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
   if (i < n) {
     P.ext[reps[i]] = recs[i];
@@ -69,6 +70,10 @@ __global__ __launch_bounds__(kBlock) void k_ext_scatter(Planes P, u32 nrep, cons
     }
   }
   if (i < na) apply_pair(P, app_rep[i], app_val[i]);
+  // rbe_commit records (one per replica, so lanes never share a row)
+  if (i < nc)
+    commit_update(P, C, cr[i].r, cr[i].stable_log_to, cr[i].stable_log_term, cr[i].processed,
+                  cr[i].last_applied);
 }
 
 // ---- batched outputs (rbe_collect_outputs): count → scan → write
@@ -201,6 +206,7 @@ __global__ __launch_bounds__(kBlock) void k_out_write(Planes P, Params C, u64 fi
 struct LaunchRec {
   u64 replica, term, vote, commit, last, off;  // off: first row in the terms/bodies arrays
   u32 n, pad;
+  u64 marker, marker_term, ss_index, ss_term;  // compacted LogDB (rbe_launch_state)
 };
 template <int N>
 __global__ __launch_bounds__(kBlock) void k_relaunch(Planes P, Params C, const LaunchRec* rec,
@@ -210,7 +216,7 @@ __global__ __launch_bounds__(kBlock) void k_relaunch(Planes P, Params C, const L
   if (i >= n) return;
   const LaunchRec x = rec[i];
   relaunch_replica<N>(P, C, x.replica, x.term, x.vote, x.commit, x.last, x.n, terms + x.off,
-                      bodies + x.off, ppar, tclk);
+                      bodies + x.off, ppar, tclk, x.marker, x.marker_term, x.ss_index, x.ss_term);
   P.gwake[x.replica / N] = GW_AWAKE;
 }
 
@@ -372,7 +378,7 @@ static int read_heap(rbe_engine* e, u64 pos, u64 off, u64 len, u8* dst) {
 }
 
 
-static constexpr int kPlaneAllocs = 22;
+static constexpr int kPlaneAllocs = 23;
 static u64 bytes_of(const Params& C, u64* parts) {
   const u64 N = C.n, G = C.n_groups, R = C.n_rep;
   u64 p[kPlaneAllocs] = {
@@ -398,6 +404,7 @@ static u64 bytes_of(const Params& C, u64* parts) {
       G * sizeof(u8),
       C.snapshot_entries ? R * sizeof(SnapSt) : 0,
       C.snapshot_entries ? R * N * sizeof(u64) : 0,
+      C.ext_commit ? R * sizeof(u64) : 0,
   };
   u64 t = 0;
   for (int i = 0; i < kPlaneAllocs; i++) {
@@ -456,6 +463,10 @@ static int make_params(const rbe_config* cfg, Params* out) {
   if (C.rep_world > 1 && C.iso_period) return RBE_E_INVALID;
   C.ext_apply = cfg->ext_apply;
   if (C.ext_apply && !C.ext_inputs) return RBE_E_INVALID;  // applied comes from rbe_notify_applied
+  // the host that persists an Update (rbe_commit) applies it too: raft.applied
+  // is then the host's (rbe_notify_applied), never the step's own
+  C.ext_commit = cfg->ext_commit;
+  if (C.ext_commit && !C.ext_apply) return RBE_E_INVALID;
   C.in_cap = cfg->in_cap ? cfg->in_cap : (u32)(cfg->n_groups > 1024 ? cfg->n_groups : 1024);
   if (cfg->n_groups > 0xFFFFFFFFull && !cfg->in_cap) C.in_cap = 0xFFFFFFFFu;
   C.xfer_period = cfg->xfer_period;
@@ -707,6 +718,7 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   P.gwake = (u8*)ptrs[19];
   P.snp = C.snapshot_entries ? (SnapSt*)ptrs[20] : nullptr;
   P.rem_snap = C.snapshot_entries ? (u64*)ptrs[21] : nullptr;
+  P.imark = C.ext_commit ? (u64*)ptrs[22] : nullptr;
   HIP_IGNORE(hipMemsetAsync(P.gwake, GW_AWAKE, C.n_groups, e->stream));  // every group starts awake
   e->hin.init(C.n_rep, C.n, C.in_cap, C.heap_bytes);
   e->hin.rep_world = C.rep_world;
@@ -868,8 +880,9 @@ static int flush_inputs(rbe_engine* e) {
     HIP_OK(hipMemcpyAsync(e->heap_dev, &e->heap_head_host, sizeof(u64), hipMemcpyHostToDevice,
                           e->stream));
   }
-  const u64 n = h.reps.size(), na = h.app_rep.size();
-  const u64 need = n * (sizeof(u64) + sizeof(ExtIn)) + na * 2 * sizeof(u64) + 64;
+  const u64 n = h.reps.size(), na = h.app_rep.size(), nc = h.commits.size();
+  const u64 need =
+      n * (sizeof(u64) + sizeof(ExtIn)) + na * 2 * sizeof(u64) + nc * sizeof(CommitRec) + 64;
   HIP_OK(hipEventSynchronize(e->in_ev));  // the previous upload is out of in_pinned
   if (need > e->in_bytes) {
     if (e->in_pinned) HIP_OK(hipHostFree(e->in_pinned));
@@ -882,11 +895,12 @@ static int flush_inputs(rbe_engine* e) {
     HIP_OK(hipMalloc((void**)&e->in_dev, cap));
     e->in_bytes = cap;
   }
-  // layout: replicas | records (16-B aligned) | applied replicas | applied values
+  // layout: replicas | records (16-B aligned) | applied replicas | applied values | commits
   u8* b = e->in_pinned;
   const u64 o_rec = (n * sizeof(u64) + 15) & ~15ull;
   const u64 o_ar = o_rec + n * sizeof(ExtIn), o_av = o_ar + na * sizeof(u64);
-  const u64 total = o_av + na * sizeof(u64);
+  const u64 o_cr = o_av + na * sizeof(u64);
+  const u64 total = o_cr + nc * sizeof(CommitRec);
   if (n) {
     memcpy(b, h.reps.data(), n * sizeof(u64));
     memcpy(b + o_rec, h.recs.data(), n * sizeof(ExtIn));
@@ -895,16 +909,17 @@ static int flush_inputs(rbe_engine* e) {
     memcpy(b + o_ar, h.app_rep.data(), na * sizeof(u64));
     memcpy(b + o_av, h.app_val.data(), na * sizeof(u64));
   }
+  if (nc) memcpy(b + o_cr, h.commits.data(), nc * sizeof(CommitRec));
   if (total) HIP_OK(hipMemcpyAsync(e->in_dev, b, total, hipMemcpyHostToDevice, e->stream));
   if (!h.ents.empty())
     HIP_OK(hipMemcpyAsync(e->P.in_ents, h.ents.data(), h.ents.size() * sizeof(Ent),
                           hipMemcpyHostToDevice, e->stream));
-  const u64 m = n > na ? n : na;
+  const u64 m = std::max(n, std::max(na, nc));
   if (m) {  // (a flush of heap records alone, e.g. from rbe_push_messages, has none)
     hipLaunchKernelGGL(k_ext_scatter, dim3(grid_for(m)), dim3(kBlock), 0, e->stream, e->P,
                        e->C.n, (const u64*)e->in_dev, (const ExtIn*)(e->in_dev + o_rec), n,
-                       (const u64*)(e->in_dev + o_ar), (const u64*)(e->in_dev + o_av), na, e->L,
-                       e->round & 1u);
+                       (const u64*)(e->in_dev + o_ar), (const u64*)(e->in_dev + o_av), na,
+                       (const CommitRec*)(e->in_dev + o_cr), nc, e->C, e->L, e->round & 1u);
     HIP_OK(hipGetLastError());
   }
   HIP_OK(hipEventRecord(e->in_ev, e->stream));
@@ -1098,8 +1113,10 @@ int rbe_launch(rbe_engine* e, uint64_t n, const uint64_t* replica, const rbe_lau
   std::vector<LaunchRec> rec(n);
   u64 off = 0;
   for (u64 i = 0; i < n; i++) {
-    rec[i] = LaunchRec{replica[i], st[i].term, st[i].vote, st[i].commit, st[i].last_index, off,
-                       st[i].n_entries, 0};
+    rec[i] = LaunchRec{replica[i], st[i].term,           st[i].vote,
+                       st[i].commit,     st[i].last_index,     off,
+                       st[i].n_entries,  0,                    st[i].marker,
+                       st[i].marker_term, st[i].snapshot_index, st[i].snapshot_term};
     off += st[i].n_entries;
   }
   const u64 b_rec = n * sizeof(LaunchRec), b_t = terms.size() * sizeof(u64);
@@ -1427,45 +1444,42 @@ int rbe_get_updates(rbe_engine* e, uint64_t first, uint64_t count, rbe_update* o
       d2h(e, hot.data(), e->P.hot + first, count))
     return RBE_E_HIP;
   HIP_OK(hipStreamSynchronize(e->stream));
+  for (u64 i = 0; i < count; i++) update_view(upd[i], core[i], hot[i], e->round, out[i]);
+  return RBE_OK;
+}
+
+int rbe_get_update_commits(rbe_engine* e, uint64_t first, uint64_t count, rbe_update_commit* out) {
+  if (!e || !out || first + count > e->C.n_rep) return RBE_E_INVALID;
+  if (!e->C.ext_commit) return RBE_E_STATE;
+  std::vector<rbe_update> u(count);
+  int rc = rbe_get_updates(e, first, count, u.data());
+  if (rc) return rc;
+  std::vector<Core> core(count);
+  std::vector<u64> app(count);
+  if (d2h(e, core.data(), e->P.core + first, count) || d2h(e, app.data(), e->P.applied + first, count))
+    return RBE_E_HIP;
+  HIP_OK(hipStreamSynchronize(e->stream));
   for (u64 i = 0; i < count; i++) {
-    rbe_update& u = out[i];
-    memset(&u, 0, sizeof(u));
-    u.term = core[i].term;
-    u.vote = core[i].vote;
-    u.commit = core[i].committed;
-    u.digest = upd[i].digest;
-    u.fault = upd[i].fault;
-    u.save_lo = u.apply_lo = 1;  // empty ranges unless the step wrote them
-    u.save_hi = u.apply_hi = 0;
-    if (e->round > 0 && upd[i].round == e->round - 1) {
-      if (upd[i].flags & UF_RANGES) {  // chunks 0-2 of the record are this step's (Upd)
-        u.save_lo = upd[i].save_lo;
-        u.save_hi = upd[i].save_hi;
-        u.apply_lo = upd[i].apply_lo;
-        u.apply_hi = upd[i].apply_hi;
-        u.n_dropped_entries = upd[i].n_drop_ent;
-        u.n_dropped_read_indexes = upd[i].n_drop_ri;
-      }
-      u.n_messages = upd[i].n_msgs;
-      u.n_ready_to_read = upd[i].n_rtr;
-      u.flags = upd[i].flags & ~UF_RANGES;
-      u.events = upd[i].events;
-    }  // else an idle round (triage) left the record untouched: empty Update
-    // Peer.HasUpdate (peer.go:253-280) and setFastApply / validateUpdate
-    // (peer.go:209-245) on the range form
-    const bool has = (u.flags & RBE_UF_STATE_CHANGED) || u.n_messages || u.n_ready_to_read ||
-                     u.n_dropped_entries || u.n_dropped_read_indexes || u.save_lo <= u.save_hi ||
-                     u.apply_lo <= u.apply_hi || (u.flags & (RBE_UF_SENT_QUIESCE | RBE_UF_SNAPSHOT));
-    if (has) u.flags |= RBE_UF_HAS_UPDATE;
-    if (update_fast_apply((u.flags & RBE_UF_SNAPSHOT) != 0, u.save_lo, u.save_hi, u.apply_lo,
-                          u.apply_hi))
-      u.flags |= RBE_UF_FAST_APPLY;
-    if (!update_valid(u.commit, u.save_lo, u.save_hi, u.apply_lo, u.apply_hi))
-      u.fault |= RBE_FAULT_PANIC;
-    u.role = hot[i].role;
-    u.leader_id = core[i].leader;
+    const u64 r = first + i;
+    int trc = RBE_OK;
+    auto term_of = [&](u64 idx) -> u64 {
+      if (idx == core[i].last_index) return core[i].t_last;
+      u64 t = 0;  // the log moved since the step (a relaunch): read the ring
+      if (hipMemcpy(&t, e->P.term_ring + (idx & (u64)(e->C.ring - 1)) * e->C.n_rep + r,
+                    sizeof(u64), hipMemcpyDeviceToHost) != hipSuccess)
+        trc = RBE_E_HIP;
+      return t;
+    };
+    update_commit_view(u[i], app[i], term_of, out[i]);
+    if (trc) return trc;
   }
   return RBE_OK;
+}
+
+int rbe_commit(rbe_engine* e, uint64_t n, const uint64_t* replica, const rbe_update_commit* uc) {
+  if (!e) return RBE_E_INVALID;
+  if (!e->C.ext_commit) return RBE_E_STATE;
+  return e->hin.commit(n, replica, uc);
 }
 
 int rbe_get_snapshot_state(rbe_engine* e, uint64_t first, uint64_t count, uint64_t* out6) {

@@ -441,13 +441,17 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
   if (u.save_hi >= u.save_lo) ctr.v[C_ENT_SAVED] += (u32)(u.save_hi - u.save_lo + 1);
   if (o.n_rtr) ctr.v[C_READS_CONFIRMED] += o.n_rtr;
   ctr.v[C_DROPPED_READS] += o.n_drop_ri;
-  if (u.apply_hi >= u.apply_lo) c.processed = u.apply_hi;
+  // Peer.Commit's log part: the harness's own unless the host sends it
+  // (rbe_commit, ext_commit; Lane::run)
+  const bool own_commit = !C.ext_commit;
+  const bool applies = own_commit && u.apply_hi >= u.apply_lo;
+  if (applies) c.processed = u.apply_hi;
   // Core's 16-B chunks this step changed: [term, committed] [last_index,
   // processed] [saved_to, vote..rq_count] [t_last, lead_start]; the caller
   // passes the chunks its handlers wrote
-  core_dirty |= (c.committed != committed0 ? 1u : 0u) | (u.apply_hi >= u.apply_lo ? 2u : 0u) |
-                (c.saved_to != c.last_index ? 4u : 0u);
-  c.saved_to = c.last_index;
+  core_dirty |= (c.committed != committed0 ? 1u : 0u) | (applies ? 2u : 0u) |
+                (own_commit && c.saved_to != c.last_index ? 4u : 0u);
+  if (own_commit) c.saved_to = c.last_index;
   if (c.processed < c.committed) flags |= HF_APPLY_PENDING;
   else flags &= (u8)~HF_APPLY_PENDING;
   if (u.apply_hi >= u.apply_lo && !C.ext_apply) flags |= HF_APPLIED_NEW;
@@ -611,6 +615,8 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   // ---- eligibility on level-1 data
   if (h.role != R_Leader) return false;
   if (h.flags & HF_SNAP_WORK) return false;  // compaction / SnapshotStatus: full table
+  // ext_commit: an Update whose unsaved entries left the in-memory log (Lane::run)
+  if (C.ext_commit && c.saved_to + 1 < P.imark[r]) return false;
   if (h.flags & (HF_APPLY_PENDING | HF_IS_LTT)) return false;
   if (c.ltt != 0) return false;
   if (!ck.tick) return false;
@@ -1302,6 +1308,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   u32 cdirty = 0;  // Core chunks an append or a new leader wrote (fast_finish)
   if (h.role != R_Follower) return false;
   if (h.flags & HF_SNAP_WORK) return false;  // compaction / SnapshotStatus: full table
+  if (C.ext_commit && c.saved_to + 1 < P.imark[r]) return false;  // (lead_fast)
   if (h.flags & (HF_APPLY_PENDING | HF_IS_LTT)) return false;
   if (c.ltt != 0) return false;
   if (!ck.tick) return false;

@@ -186,6 +186,70 @@ RBE_HD void apply_pair(const Planes& P, u64 rep, u64 val) {
   }
 }
 
+// The rbe_update of replica r after round `round` - 1 from its Upd, Core and
+// Hot rows (rbe_get_updates).  A replica that made no Update-writing step in
+// that round (an idle round finished in triage) has an empty Update.
+inline void update_view(const Upd& d, const Core& c, const Hot& h, u32 round, rbe_update& u) {
+  memset(&u, 0, sizeof(u));
+  u.term = c.term;
+  u.vote = c.vote;
+  u.commit = c.committed;
+  u.digest = d.digest;
+  u.fault = d.fault;
+  u.save_lo = u.apply_lo = 1;  // empty ranges unless the step wrote them
+  u.save_hi = u.apply_hi = 0;
+  if (round > 0 && d.round == round - 1) {
+    if (d.flags & UF_RANGES) {  // chunks 0-2 of the record are this step's (Upd)
+      u.save_lo = d.save_lo;
+      u.save_hi = d.save_hi;
+      u.apply_lo = d.apply_lo;
+      u.apply_hi = d.apply_hi;
+      u.n_dropped_entries = d.n_drop_ent;
+      u.n_dropped_read_indexes = d.n_drop_ri;
+    }
+    u.n_messages = d.n_msgs;
+    u.n_ready_to_read = d.n_rtr;
+    u.flags = d.flags & ~UF_RANGES;
+    u.events = d.events;
+  }
+  // Peer.HasUpdate (peer.go:253-280) and setFastApply / validateUpdate
+  // (peer.go:209-245) on the range form
+  const bool has = (u.flags & RBE_UF_STATE_CHANGED) || u.n_messages || u.n_ready_to_read ||
+                   u.n_dropped_entries || u.n_dropped_read_indexes || u.save_lo <= u.save_hi ||
+                   u.apply_lo <= u.apply_hi ||
+                   (u.flags & (RBE_UF_SENT_QUIESCE | RBE_UF_SNAPSHOT | RBE_UF_APPLIED));
+  if (has) u.flags |= RBE_UF_HAS_UPDATE;
+  if (update_fast_apply((u.flags & RBE_UF_SNAPSHOT) != 0, u.save_lo, u.save_hi, u.apply_lo,
+                        u.apply_hi))
+    u.flags |= RBE_UF_FAST_APPLY;
+  if (!update_valid(u.commit, u.save_lo, u.save_hi, u.apply_lo, u.apply_hi))
+    u.fault |= RBE_FAULT_PANIC;
+  u.role = h.role;
+  u.leader_id = c.leader;
+}
+// getUpdateCommit (peer.go:410-427) of an rbe_update: `applied` is the
+// applied index the step ran with (GetUpdate's lastApplied), `term_of(i)` the
+// term of log entry i (the last EntriesToSave entry)
+template <typename TermFn>
+inline void update_commit_view(const rbe_update& u, u64 applied, TermFn&& term_of,
+                               rbe_update_commit& o) {
+  memset(&o, 0, sizeof(o));
+  if (!(u.flags & RBE_UF_HAS_UPDATE)) return;
+  o.ready_to_read = u.n_ready_to_read;
+  o.last_applied = applied;
+  if (u.apply_lo <= u.apply_hi) o.processed = u.apply_hi;
+  if (u.save_lo <= u.save_hi) {
+    o.stable_log_to = u.save_hi;
+    o.stable_log_term = term_of(u.save_hi);
+  }
+}
+
+// One staged rbe_commit (Peer.Commit's log part, ext_commit mode); applied by
+// commit_update (rbe_step.h) in k_ext_scatter / HostInputs::apply_host.
+struct CommitRec {
+  u64 r, stable_log_to, stable_log_term, processed, last_applied;
+};
+
 // The lowest payload-heap position the replicas of group g that this engine
 // steps may still need (~0 for none), for HostHeap::room: the records of
 // log-window entries above the group's low mark — min over those replicas of
@@ -279,13 +343,21 @@ inline int launch_rows(const Params& C, HostHeap& heap, u64 n, const u64* replic
                        const rbe_launch_state* st, const rbe_entry* ents, const u8* cmd,
                        std::vector<u64>& terms, std::vector<Body>& bodies) {
   if (n && (!replica || !st)) return RBE_E_INVALID;
-  // a restart carries no LogDB snapshot / compaction marker (SnapSt) yet
-  if (n && C.snapshot_entries) return RBE_E_INVALID;
   u64 total = 0;
   for (u64 i = 0; i < n; i++) {
     const rbe_launch_state& x = st[i];
+    // a compacted LogDB (marker > 0) only with snapshots on; the entries lie
+    // above the marker, the commit (loadState, raft.go:429-437) and the
+    // snapshot at or above it, and Term(marker) is in the in-memory window
+    const bool snap = x.marker || x.marker_term || x.snapshot_index || x.snapshot_term;
+    if (snap && !C.snapshot_entries) return RBE_E_INVALID;
+    if (x.marker > x.last_index || x.n_entries > x.last_index - x.marker ||
+        x.commit < x.marker || x.snapshot_index < x.marker || x.snapshot_index > x.last_index ||
+        (x.marker && !x.marker_term) || (x.snapshot_index && !x.snapshot_term) ||
+        (x.marker && x.last_index - x.marker >= C.ring))
+      return RBE_E_INVALID;
     if (replica[i] >= C.n_rep || x.n_entries > C.ring || x.n_entries > x.last_index ||
-        x.commit > x.last_index || x.vote > C.n || (x.last_index && !x.n_entries))
+        x.commit > x.last_index || x.vote > C.n || (x.last_index > x.marker && !x.n_entries))
       return RBE_E_INVALID;
     total += x.n_entries;
   }
@@ -333,6 +405,8 @@ struct HostInputs {
   // the replica word set, rbe_set_apply_ready flags (value 1 = ready)
   std::vector<u64> app_rep, app_val;
   std::vector<u64> applied;  // [n_rep] host mirror of Planes::applied (the host is its only writer)
+  std::vector<CommitRec> commits;  // rbe_commit records for the next step, in call order
+  std::vector<u8> committing;      // [n_rep] a commit is staged (one per replica per step)
   u32 rep_world = 1, rep_rank = 0;  // replica-per-GPU mode: only owned replicas take input
 
   HostHeap heap;             // payload heap positions and staged bytes
@@ -345,8 +419,11 @@ struct HostInputs {
     slot.assign(n_rep, ~0u);
     mark.assign(n_rep, 0u);
     applied.assign(n_rep, 0);
+    committing.assign(n_rep, 0);
   }
-  bool empty() const { return reps.empty() && app_rep.empty() && heap.stage.empty(); }
+  bool empty() const {
+    return reps.empty() && app_rep.empty() && heap.stage.empty() && commits.empty();
+  }
   void clear() {
     for (u64 r : reps) slot[r] = ~0u;
     reps.clear();
@@ -354,6 +431,8 @@ struct HostInputs {
     ents.clear();
     app_rep.clear();
     app_val.clear();
+    for (const CommitRec& c : commits) committing[c.r] = 0;
+    commits.clear();
     heap.stage.clear();
     heap.batch_lo = heap.flushed;
     heap.flushed = heap.head;
@@ -524,19 +603,40 @@ struct HostInputs {
     }
     return RBE_OK;
   }
+  // rbe_commit: Peer.Commit's log part (rbe.h), checked whole, one per replica
+  int commit(u64 cnt, const u64* replica, const rbe_update_commit* uc) {
+    if (cnt && !uc) return RBE_E_INVALID;
+    int rc = check_replicas(cnt, replica, 0);
+    if (rc) return rc;
+    for (u64 i = 0; i < cnt; i++)
+      if (uc[i].stable_snapshot_to != 0) return RBE_E_INVALID;
+    for (u64 i = 0; i < cnt; i++)
+      if (committing[replica[i]]) return RBE_E_STATE;
+    for (u64 i = 0; i < cnt; i++)  // within the batch too
+      for (u64 j = 0; j < i; j++)
+        if (replica[j] == replica[i]) return RBE_E_STATE;
+    for (u64 i = 0; i < cnt; i++) {
+      committing[replica[i]] = 1;
+      commits.push_back(CommitRec{replica[i], uc[i].stable_log_to, uc[i].stable_log_term,
+                                  uc[i].processed, uc[i].last_applied});
+    }
+    return RBE_OK;
+  }
   // Write the staged input into host-resident planes (the test-only host build;
   // the HIP engine uploads the same vectors and scatters them on device).
   // resync the applied mirror after the plane was overwritten (snapshot import)
   void resync_applied(const u64* plane, u64 first, u64 count) {
     for (u64 i = 0; i < count; i++) applied[first + i] = plane[i];
   }
-  void apply_host(const Planes& P) {
+  void apply_host(const Planes& P, const Params& C_) {
     for (size_t i = 0; i < reps.size(); i++) {
       P.ext[reps[i]] = recs[i];
       P.gwake[reps[i] / n] = GW_AWAKE;  // input wakes a sleeping group
     }
     for (size_t i = 0; i < ents.size(); i++) P.in_ents[i] = ents[i];
     for (size_t i = 0; i < app_rep.size(); i++) apply_pair(P, app_rep[i], app_val[i]);
+    for (const CommitRec& c : commits)
+      commit_update(P, C_, c.r, c.stable_log_to, c.stable_log_term, c.processed, c.last_applied);
   }
 };
 

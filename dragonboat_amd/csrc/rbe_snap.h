@@ -23,7 +23,7 @@
 namespace rbe {
 
 static constexpr u64 kSnapMagic = 0x31504E5345425255ull;  // "URBESNP1"
-static constexpr int kSnapPlanes = 21;
+static constexpr int kSnapPlanes = 22;
 
 struct SnapHeader {
   u64 magic;
@@ -73,6 +73,7 @@ inline void snap_planes(const Planes& P, const Params& C, SnapPlane* out) {
     add(P.snp, 1, R * sizeof(SnapSt), N * sizeof(SnapSt));
     add(P.rem_snap, 1, R * N * sizeof(u64), N * N * sizeof(u64));
   }
+  if (C.ext_commit) add(P.imark, 1, R * sizeof(u64), N * sizeof(u64));  // inMemory markers
   // the per-replica fault words live in Hot/Core/Upd; nothing else is carried
   while (i < kSnapPlanes) out[i++] = SnapPlane{nullptr, 0, 0, 0};
 }
@@ -96,7 +97,7 @@ inline u64 snap_behavior_hash(const Params& C) {
                    C.wl_stop_round, C.wl_active_mod, C.wl_read_permille, C.ext_inputs,
                    C.iso_period, C.iso_len, C.iso_mod, C.rep_world, C.rep_rank,
                    C.snapshot_entries, C.compaction_overhead, C.heap_bytes, C.ext_apply,
-                   C.xfer_period, C.xfer_mod};
+                   C.xfer_period, C.xfer_mod, C.ext_commit};
   u64 h = 0x243F6A8885A308D3ull;
   for (u64 x : f) {
     h ^= x + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);

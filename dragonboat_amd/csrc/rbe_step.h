@@ -127,7 +127,9 @@ RBE_HD Hot load_hot(const Planes& P, const Params& C, u64 r, u32 round) {
 //            without reading Hot.
 enum : u8 { IB_LAZY = 1, IB_LEAD = 2, IB_ROLE_SHIFT = 4 };
 RBE_HD u8 idle_byte(const Params& C, u8 role, u8 flags, u32 qs) {
-  const bool lazy = C.quiesce && qs > 0 && (flags & HF_RAFT_QUIESCE) &&
+  // with ext_commit a quiesced step may still owe an Update (entries the host
+  // has not acknowledged as saved are returned again), so no round is lazy
+  const bool lazy = C.quiesce && qs > 0 && (flags & HF_RAFT_QUIESCE) && !C.ext_commit &&
                     !(flags & (HF_APPLY_PENDING | HF_APPLIED_NEW | HF_SNAP_WORK));
   return (u8)((lazy ? IB_LAZY : 0) | (role == R_Leader ? IB_LEAD : 0) | ((role & 7u) << IB_ROLE_SHIFT));
 }
@@ -177,6 +179,50 @@ RBE_HD void update_commit(u64 save_lo, u64 save_hi, u64 apply_lo, u64 apply_hi, 
   *stable_log_to = save_lo <= save_hi ? save_hi : 0;
   *stable_snapshot_to = snap_index;
   if (snap_index != 0 && snap_index > *processed) *processed = snap_index;
+}
+
+// Peer.Commit's log part with a host-supplied UpdateCommit (rbe_commit,
+// ext_commit mode): entryLog.commitUpdate (logentry.go:335-355) =
+// inMemory.commitUpdate → savedLogTo (inmemory.go:108-137), then processed,
+// then inMemory.appliedLogTo (139-167).  `imark` is inMemory.markerIndex; the
+// in-memory log holds [imark, last_index] (empty when imark > last_index).
+// A reference panic sets F_PANIC in the sticky fault word and changes nothing
+// further.  stable_snapshot_to has nothing to clear: snapshots are not carried
+// with ext_commit.  Returns the fault bits raised.
+RBE_HD u32 commit_update(const Planes& P, const Params& C, u64 r, u64 stable_log_to,
+                         u64 stable_log_term, u64 processed, u64 last_applied) {
+  Core c = P.core[r];
+  u64 mark = P.imark[r];
+  u32 fault = 0;
+  const bool held = mark <= c.last_index;  // len(im.entries) > 0
+  if (stable_log_to > 0 && held && stable_log_to >= mark && stable_log_to <= c.last_index) {
+    u64 t = c.t_last;
+    if (stable_log_to != c.last_index) {
+      if (c.last_index - stable_log_to >= C.ring) fault |= F_WINDOW;
+      else t = P.term_ring[(stable_log_to & (u64)(C.ring - 1)) * C.n_rep + r];
+    }
+    if (!fault && t == stable_log_term) c.saved_to = stable_log_to;
+  }
+  if (!fault && processed > 0) {
+    if (processed < c.processed || processed > c.committed) fault |= F_PANIC;
+    else c.processed = processed;
+  }
+  if (!fault && last_applied > 0) {
+    if (last_applied > c.committed || last_applied > c.processed) fault |= F_PANIC;
+    else if (held && last_applied >= mark && last_applied <= c.last_index) mark = last_applied;
+  }
+  P.core[r] = c;
+  P.imark[r] = mark;
+  Hot* h = &P.hot[r];
+  u8 f = h->flags;
+  if (c.processed < c.committed) f |= HF_APPLY_PENDING;
+  else f &= (u8)~HF_APPLY_PENDING;
+  if (fault) {
+    f |= HF_FAULTED;
+    P.upd[r].fault |= fault;
+  }
+  h->flags = f;
+  return fault;
 }
 
 // entryutils.go:97-104 / 106-114: message types only a node makes for its own
@@ -238,6 +284,7 @@ struct Lane {
   u64 marker, marker_term;
   u8 snp_pend, snp_rej;
   bool snap_restored;
+  u64 applied0;  // raft.applied of this step (NotifyRaftLastApplied at its start)
 
   // per-step outputs
   u64 pc_lo, pc_hi;  // per destination 16-bit A | B << 7 | quiesce << 15 (registers)
@@ -998,6 +1045,7 @@ struct Lane {
           last = m.log_index + m.n_ent;
           t_last = ents[m.n_ent - 1].term;
           saved_to = umin64(saved_to, conflict - 1);
+          if (C.ext_commit && conflict <= P.imark[r]) P.imark[r] = conflict;
           seg_len = 0;
         }
       }
@@ -1083,9 +1131,12 @@ struct Lane {
     }
   }
   // raft.applied: NotifyRaftLastApplied at the start of the step (node.go:
-  // 1010-1014); without ext_apply the harness applies every committed entry
-  // the step it is returned, so it equals `processed` at step start
-  RBE_HD u64 applied_index() const { return C.ext_apply ? P.applied[r] : processed; }
+  // 1010-1014), the value run() captured in applied0: with ext_apply the
+  // host's; else the harness's state machine, which applies every committed
+  // entry the step it is returned, so `processed` at step start — or the
+  // LogDB snapshot it recovered from at a restart while the re-applied
+  // entries are still below it (rsm skips entries it already holds)
+  RBE_HD u64 applied_index() const { return applied0; }
   RBE_HD void on_election() {  // handleNodeElection, raft.go:1482-1512
     if (role != R_Leader) {
       // hasConfigChangeToApply (raft.go:1460-1472): committed > applied
@@ -1593,12 +1644,14 @@ struct Lane {
     snap_restored = false;
     u8 pend0 = 0, pend_rej0 = 0;
     marker = marker_term = 0;
+    applied0 = C.ext_apply ? P.applied[r] : processed;
     if (C.snapshot_entries) {
       const SnapSt& sp = P.snp[r];
       marker = sp.marker;
       marker_term = sp.marker_term;
       pend0 = sp.pend;
       pend_rej0 = sp.pend_rej;
+      applied0 = umax64(applied0, sp.ss_index);
     }
     pc_lo = pc_hi = 0;
     arena_used = 0;
@@ -1873,6 +1926,10 @@ struct Lane {
     Upd u;
     u.save_lo = saved_to + 1;
     u.save_hi = last;
+    // entriesToSave (inmemory.go:117-123) returns nothing when the in-memory
+    // log no longer holds savedTo + 1: with ext_commit a host that reported an
+    // entry applied (appliedLogTo) before saving it never sees it to save again
+    if (C.ext_commit && saved_to + 1 < P.imark[r]) u.save_lo = last + 1;
     u.apply_lo = processed + 1;
     u.apply_hi = committed;
     if (flags & HF_APPLY_HELD) {  // moreEntriesToApply == false (node.go:908-915)
@@ -1902,11 +1959,18 @@ struct Lane {
     if (n_rtr) ctr.v[C_READS_CONFIRMED] += n_rtr;
     ctr.v[C_DROPPED_PROPOSALS] += n_drop_ent;
     ctr.v[C_DROPPED_READS] += n_drop_ri;
-    if (u.apply_hi >= u.apply_lo) processed = u.apply_hi;
-    saved_to = last;
+    // Peer.Commit (peer.go:282-293): the outputs are consumed here; its log
+    // part (savedTo, processed) is the harness's own unless the host sends it
+    // (rbe_commit, ext_commit), as the node does after SaveRaftState
+    if (!C.ext_commit) {
+      if (u.apply_hi >= u.apply_lo) processed = u.apply_hi;
+      saved_to = last;
+    }
     if (processed < committed) flags |= HF_APPLY_PENDING;
     else flags &= (u8)~HF_APPLY_PENDING;
-    if (u.apply_hi >= u.apply_lo && !C.ext_apply) flags |= HF_APPLIED_NEW;
+    // the state machine's applied index moved (entries it held already, re-applied
+    // after a restart, leave it): the node confirms it with the next Update
+    if (u.apply_hi >= u.apply_lo && !C.ext_apply && u.apply_hi > applied0) flags |= HF_APPLIED_NEW;
     else flags &= (u8)~HF_APPLIED_NEW;
     if (C.snapshot_entries) node_snapshot();
     if (fault) flags |= HF_FAULTED;
@@ -1948,7 +2012,7 @@ struct Lane {
     u.flags = (u16)((term != term0 || vote != vote0 || committed != committed0 ? UF_STATE_CHANGED
                                                                                 : 0u) |
                     (send_q ? UF_SENT_QUIESCE : 0u) | (snap_restored ? UF_SNAPSHOT : 0u) |
-                    UF_RANGES);
+                    (ext_applied ? UF_APPLIED : 0u) | UF_RANGES);
     u.events = (u16)(events | (leader != leader0 ? EV_LEADER_UPDATED : 0u));
     u.round = round;
     u.pad1 = 0;
@@ -2022,6 +2086,7 @@ RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   c.t_last = 1;  // bootstrap entries are at term 1
   c.lead_start = 0;
   P.core[r] = c;
+  if (C.ext_commit) P.imark[r] = 1;  // inMemory.init(0), then bootstrap appends 1..N
   for (u32 s = 0; s < N; s++) {
     RemoteMN x;
     x.match = 0;
@@ -2058,23 +2123,43 @@ RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
 // existing log (peer.go:64-86 with initial = newNode = false) = newRaft
 // (raft.go:234-289: remotes next 1, loadState term/vote/commit) then
 // becomeFollower(term, NoLeader) (one randomized timeout drawn, count 0);
-// entryLog over the stored log: processed = firstIndex - 1 = 0, savedTo =
-// lastIndex (logentry.go:86-96, inmemory.go:46-56).  `t`/`b` hold the terms and
-// bodies of entries [last - n + 1, last].  The node restarts with it: fresh
-// quiesce state, and the messages in flight to and from the replica of the
-// round about to run (parity `ppar` lists) are dropped.
+// entryLog over the stored log: committed = processed = firstIndex - 1 = the
+// LogDB's compaction marker, then loadState's commit; savedTo = lastIndex
+// (logentry.go:86-96, inmemory.go:46-56).  `t`/`b` hold the terms and bodies of
+// entries [last - n + 1, last].  With snapshots the LogDB's marker and latest
+// snapshot go to SnapSt (the node's pending compaction and snapshot request
+// stay, as the harness keeps them) and the state machine recovers from that
+// snapshot (Lane::applied0), which the node confirms with its first Update.
+// The node restarts with it: fresh quiesce state, and the messages in flight
+// to and from the replica of the round about to run (parity `ppar` lists) are
+// dropped.
 template <int N>
 RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, u64 vote,
                              u64 commit, u64 last, u32 n, const u64* t, const Body* b, u32 ppar,
-                             u32 tclk) {
+                             u32 tclk, u64 marker = 0, u64 marker_term = 0, u64 ss_index = 0,
+                             u64 ss_term = 0) {
   const u32 k = (u32)(r % N);
   const u64 g = r / N;
   const u64 cid = C.cid_base + g * C.cid_stride;
   const u64 self = k + 1;
   const bool faulted = P.upd[r].fault != 0;
+  u8 snap_flags = 0;
+  if (C.snapshot_entries) {
+    SnapSt& sp = P.snp[r];
+    sp.marker = marker;
+    sp.marker_term = marker_term;
+    sp.ss_index = ss_index;
+    sp.ss_term = ss_term;
+    if (sp.compact_to || sp.pend) snap_flags |= HF_SNAP_WORK;
+    if (ss_index) snap_flags |= HF_APPLIED_NEW;  // recovered: confirmedIndex 0 lags it
+    // Term(marker) for the steps' log lookups (the ring slot is free: the
+    // entries above the marker are fewer than the ring)
+    if (marker) P.term_ring[(marker & (u64)(C.ring - 1)) * C.n_rep + r] = marker_term;
+  }
   Hot h;
   h.role = R_Follower;
-  h.flags = (u8)((commit > 0 ? HF_APPLY_PENDING : 0u) | (faulted ? HF_FAULTED : 0u));
+  h.flags = (u8)((commit > marker ? HF_APPLY_PENDING : 0u) | (faulted ? HF_FAULTED : 0u) |
+                 snap_flags);
   h.votes_resp = h.votes_granted = 0;
   h.election_tick = 0;
   h.heartbeat_tick = 0;
@@ -2091,16 +2176,17 @@ RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, 
   c.term = term;
   c.committed = commit;
   c.last_index = last;
-  c.processed = 0;
+  c.processed = marker;
   c.saved_to = last;
   c.vote = (u8)vote;
   c.leader = 0;
   c.ltt = 0;
   c.rq_head = c.rq_count = 0;
   c.pad[0] = c.pad[1] = c.pad[2] = 0;
-  c.t_last = n ? t[n - 1] : 0;
+  c.t_last = n ? t[n - 1] : (last == marker ? marker_term : 0);
   c.lead_start = 0;
   P.core[r] = c;
+  if (C.ext_commit) P.imark[r] = last + 1;  // inMemory.init(lastIndex), inmemory.go:46-57
   for (u32 s = 0; s < N; s++) {  // becomeFollower → reset → resetRemotes (raft.go:1023-1031)
     RemoteMN x;
     x.match = s == k ? last : 0;
@@ -2282,6 +2368,7 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, const Clk& ck
   const u64 cid = C.cid_base + g * C.cid_stride;
   const u32 cls = h.role == R_Leader ? T_LEAD : (h.role == R_Follower ? T_FOLL : T_FULL);
   if (nmsg || (h.flags & HF_APPLY_PENDING)) return cls;
+  if (C.ext_commit) return cls;  // the step may owe entries to save (Core is not read here)
   if (h.flags & HF_SNAP_WORK) return T_FULL;  // SnapshotStatus / compaction (node_snapshot)
   if (!ck.tick && (h.flags & HF_APPLIED_NEW)) return cls;
   if (h.role == R_Leader && wl_input(C, cid, round)) return cls;

@@ -198,6 +198,9 @@ enum : u32 {
   UF_SNAPSHOT = 0x20,  // the step restored a snapshot from InstallSnapshot: Update.Snapshot is
                        // SnapSt::ss_index / ss_term (the state machine recovers from it);
                        // the same bit as RBE_UF_SNAPSHOT
+  UF_APPLIED = 0x40,   // ext_apply: the state machine's applied index changed for this step,
+                       // so the node takes an Update even without other content (node.go:
+                       // 907-923 confirmedIndex); the same bit as RBE_UF_APPLIED
   UF_RANGES = 0x100
 };
 // server.IRaftEventListener (internal/server/event.go) calls a step made, one
@@ -279,6 +282,7 @@ struct Params {
   u32 rep_world;      // replica-per-GPU mode when > 1 (rbe_xchg.h)
   u32 rep_rank;
   u32 ext_apply;      // applied index comes from rbe_notify_applied (raft.applied lags processed)
+  u32 ext_commit;     // Peer.Commit's log part comes from rbe_commit (savedTo/processed lag)
   u32 snapshot_entries;     // config.SnapshotEntries: snapshot + compact every that many applied entries (0 = never)
   u32 compaction_overhead;  // config.CompactionOverhead: entries kept below the snapshot
   u32 in_cap;         // host-pushed proposal entries per step (Planes::in_ents)
@@ -324,6 +328,9 @@ struct Planes {
   u64* rem_snap;      // [n_rep * N] remote.snapshotIndex (read only in RS_Snapshot)
   u8* gwake;          // [n_groups] GW_* bits: lets k_triage skip a sleeping group whole
                       // (rbe_step.h, group sleep)
+  u64* imark;         // [n_rep] inMemory.markerIndex (ext_commit only, else null): the first
+                      // entry the in-memory log holds (inmemory.go:36-44), which bounds
+                      // what savedLogTo / appliedLogTo accept
   const u64* heap_head;  // [1] payload heap: the host's next free position after the
                          // last upload; a record at p < *heap_head - heap_bytes has been
                          // overwritten by a later lap (null without a heap)

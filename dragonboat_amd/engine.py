@@ -14,7 +14,7 @@ import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libdragonboat_amd.so")
-RBE_ABI_VERSION = 3
+RBE_ABI_VERSION = 4
 
 COUNTER_NAMES = ["steps", "committed", "msg_in", "msg_out", "ent_in", "ent_out",
                  "reads_confirmed", "proposals", "reads", "quiesced_ticks", "active_ticks",
@@ -44,7 +44,8 @@ class RbeConfig(C.Structure):
                 ("ext_apply", C.c_uint32), ("in_cap", C.c_uint32),
                 ("xfer_period", C.c_uint32), ("xfer_mod", C.c_uint32),
                 ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
-                ("heap_bytes", C.c_uint64), ("reserved", C.c_uint32 * 4)]
+                ("heap_bytes", C.c_uint64), ("ext_commit", C.c_uint32),
+                ("reserved", C.c_uint32 * 3)]
 
 
 class RbeReplicaView(C.Structure):
@@ -130,13 +131,21 @@ def entry_fields(e: RbeEntry, cmd: Optional[bytes] = None) -> dict:
                 responded_to=e.responded_to)
 
 
+class RbeUpdateCommit(C.Structure):  # raftpb UpdateCommit (raftpb/raft.go:60-70)
+    _fields_ = [("processed", C.c_uint64), ("last_applied", C.c_uint64),
+                ("stable_log_to", C.c_uint64), ("stable_log_term", C.c_uint64),
+                ("stable_snapshot_to", C.c_uint64), ("ready_to_read", C.c_uint64)]
+
+
 class RbeReadyToRead(C.Structure):
     _fields_ = [("index", C.c_uint64), ("ctx_low", C.c_uint64), ("ctx_high", C.c_uint64)]
 
 
 class RbeLaunchState(C.Structure):
     _fields_ = [("term", C.c_uint64), ("vote", C.c_uint64), ("commit", C.c_uint64),
-                ("last_index", C.c_uint64), ("n_entries", C.c_uint32), ("reserved", C.c_uint32)]
+                ("last_index", C.c_uint64), ("n_entries", C.c_uint32), ("reserved", C.c_uint32),
+                ("marker", C.c_uint64), ("marker_term", C.c_uint64),
+                ("snapshot_index", C.c_uint64), ("snapshot_term", C.c_uint64)]
 
 
 class RbeOutputs(C.Structure):
@@ -182,7 +191,8 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_get_entry_cmds", "rbe_set_apply_ready", "rbe_collect_outputs", "rbe_launch",
            "rbe_xchg_chunk_bytes", "rbe_xchg_pack_fixed", "rbe_xchg_unpack_fixed",
            "rbe_xchg_status", "rbe_stream", "rbe_get_snapshot_state", "rbe_wire_encode",
-           "rbe_wire_fetch", "rbe_wire_decode", "rbe_propose_entries"]
+           "rbe_wire_fetch", "rbe_wire_decode", "rbe_propose_entries", "rbe_commit",
+           "rbe_get_update_commits"]
 KERNEL_SLOTS = 4
 
 _lib = None
@@ -222,6 +232,8 @@ def load_library(path: Optional[str] = None):
         "rbe_report_snapshot_status": (i32, [vp, u64, P(u64), P(u64), P(C.c_uint8)]),
         "rbe_notify_applied": (i32, [vp, u64, P(u64), P(u64)]),
         "rbe_set_apply_ready": (i32, [vp, u64, P(u64), P(C.c_uint8)]),
+        "rbe_commit": (i32, [vp, u64, P(u64), P(RbeUpdateCommit)]),
+        "rbe_get_update_commits": (i32, [vp, u64, u64, P(RbeUpdateCommit)]),
         "rbe_run": (i32, [vp, u32]),
         "rbe_sync": (i32, [vp]),
         "rbe_round": (i32, [vp, P(u32)]),
@@ -293,7 +305,8 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                 iso_len: int = 0, iso_mod: int = 10, rep_world: int = 0,
                 rep_rank: int = 0, ext_apply: bool = False, in_cap: int = 0,
                 xfer_period: int = 0, xfer_mod: int = 1, heap_bytes: int = 0,
-                snapshot_entries: int = 0, compaction_overhead: int = 0) -> RbeConfig:
+                snapshot_entries: int = 0, compaction_overhead: int = 0,
+                ext_commit: bool = False) -> RbeConfig:
     return RbeConfig(abi_version=RBE_ABI_VERSION, device=device, n_groups=n_groups,
                      n_replicas=n_replicas, election_rtt=election_rtt,
                      heartbeat_rtt=heartbeat_rtt, check_quorum=int(check_quorum),
@@ -307,7 +320,7 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                      rep_world=rep_world, rep_rank=rep_rank, ext_apply=int(ext_apply),
                      in_cap=in_cap, xfer_period=xfer_period, xfer_mod=xfer_mod,
                      heap_bytes=heap_bytes, snapshot_entries=snapshot_entries,
-                     compaction_overhead=compaction_overhead)
+                     compaction_overhead=compaction_overhead, ext_commit=int(ext_commit))
 
 
 class InputError(EngineError):
@@ -453,15 +466,19 @@ class NodeInputs:
 
     def launch(self, replicas, states, entries):
         """rbe_launch: restart replicas[i] from states[i] = (term, vote, commit,
-        last_index) and entries[i] = [(index, term, type, cmd[, key, client_id,
-        series_id, responded_to]), ...], the tail of its LogDB (Peer.Launch
-        over an existing log, peer.go:64-86)."""
+        last_index[, marker, marker_term, snapshot_index, snapshot_term]) and
+        entries[i] = [(index, term, type, cmd[, key, client_id, series_id,
+        responded_to]), ...], the tail of its LogDB (Peer.Launch over an
+        existing log, peer.go:64-86)."""
         n = len(replicas)
         st = (RbeLaunchState * max(1, n))()
         flat = []
-        for i, ((term, vote, commit, last), ents) in enumerate(zip(states, entries)):
+        for i, (s, ents) in enumerate(zip(states, entries)):
+            term, vote, commit, last = s[:4]
+            snap = tuple(s[4:8]) + (0,) * (8 - max(4, len(s)))
             st[i] = RbeLaunchState(term=term, vote=vote, commit=commit, last_index=last,
-                                   n_entries=len(ents))
+                                   n_entries=len(ents), marker=snap[0], marker_term=snap[1],
+                                   snapshot_index=snap[2], snapshot_term=snap[3])
             flat.extend(ents)
         ea = (RbeEntry * max(1, len(flat)))()
         blob = bytearray()
@@ -472,6 +489,14 @@ class NodeInputs:
             blob += cmd
         buf = C.create_string_buffer(bytes(blob), max(1, len(blob)))
         _check_input(self._input("launch", n, _u64s(replicas), st, ea, buf), "rbe_launch")
+
+    def commit(self, replicas, ucs):
+        """Peer.Commit's log part (rbe_commit; cfg.ext_commit): ucs[i] =
+        (processed, last_applied, stable_log_to, stable_log_term,
+        stable_snapshot_to, ready_to_read) for replicas[i]."""
+        n = len(replicas)
+        arr = (RbeUpdateCommit * max(1, n))(*[RbeUpdateCommit(*u) for u in ucs])
+        _check_input(self._input("commit", n, _u64s(replicas), arr), "rbe_commit")
 
     def set_apply_ready(self, replicas, ready):
         """node.canHaveMoreEntriesToApply per replica (sticky; ready by default)."""
@@ -698,6 +723,16 @@ class Engine(NodeInputs):
         arr = (RbeUpdate * count)()
         _check(self.lib.rbe_get_updates(self.h, first, count, arr), "rbe_get_updates")
         return arr
+
+    def update_commits(self, first: int = 0, count: Optional[int] = None):
+        """getUpdateCommit of the last round's Updates (rbe_get_update_commits)
+        as tuples in UpdateCommit field order."""
+        count = self.n_rep - first if count is None else count
+        arr = (RbeUpdateCommit * max(1, count))()
+        _check(self.lib.rbe_get_update_commits(self.h, first, count, arr),
+               "rbe_get_update_commits")
+        return [tuple(getattr(arr[i], f) for f, _ in RbeUpdateCommit._fields_)
+                for i in range(count)]
 
     def digests(self) -> np.ndarray:
         u = self.updates()

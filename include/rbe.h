@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RBE_ABI_VERSION 3
+#define RBE_ABI_VERSION 4
 
 /* error codes */
 #define RBE_OK 0
@@ -140,7 +140,11 @@ typedef struct rbe_config {
   uint64_t heap_bytes;           /* payload heap for entries with Cmd > 16 B or session
                                     fields (needs ext_inputs), 0 = none: Cmd is then at
                                     most 16 bytes and Key/ClientID/SeriesID/RespondedTo 0 */
-  uint32_t reserved[4];
+  uint32_t ext_commit;           /* the log part of Peer.Commit (savedTo, processed, the
+                                    in-memory log's applied marker) comes from rbe_commit,
+                                    as the node sends it after SaveRaftState (needs
+                                    ext_apply); 0 = every step commits its own Update */
+  uint32_t reserved[3];
 } rbe_config;
 
 /* Snapshot of one replica (tests, debugging, rbe_get_views). */
@@ -174,6 +178,10 @@ typedef struct rbe_update {
 #define RBE_UF_HAS_UPDATE 16u     /* the step produced an Update (Peer.HasUpdate, peer.go:253-280) */
 #define RBE_UF_SNAPSHOT 32u       /* Update.Snapshot: the replica restored the snapshot an
                                      InstallSnapshot carried (rbe_get_snapshot_state) */
+#define RBE_UF_APPLIED 64u        /* the applied index rbe_notify_applied reported changed for
+                                     this step: the node takes an Update (with only
+                                     LastApplied, if nothing else) to confirm it
+                                     (node.go:907-923) */
 
 /* server.IRaftEventListener calls of a step (internal/server/event.go;
  * raft.go:354, 1090, 1333, 1368, 1503, 1995, 2010), one bit per kind.
@@ -215,10 +223,15 @@ typedef struct rbe_engine rbe_engine;
 
 /* Persisted state of one replica for rbe_launch: pb.State (term, vote, commit)
  * and the tail of its LogDB, entries [last_index - n_entries + 1, last_index]
- * (the engine's in-memory window). */
+ * (the engine's in-memory window).  With cfg.snapshot_entries the LogDB may be
+ * compacted: `marker` is its compaction marker (entries at or below it are
+ * gone, Term(marker) = marker_term; logdb GetRange first = marker + 1) and
+ * snapshot_index / snapshot_term its latest snapshot, which the state machine
+ * recovers from; all four are 0 without snapshots. */
 typedef struct rbe_launch_state {
   uint64_t term, vote, commit, last_index;
   uint32_t n_entries, reserved;
+  uint64_t marker, marker_term, snapshot_index, snapshot_term;
 } rbe_launch_state;
 
 /* Lifecycle.  Replaces the per-group raft.Launch / newRaft (peer.go:64-86,
@@ -229,8 +242,11 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out);
  * initial = false, newNode = false (peer.go:64-86) over an existing LogDB, i.e.
  * newRaft + loadState + becomeFollower(term, NoLeader) (raft.go:234-289,
  * 429-437): follower without a leader, the persisted term/vote/commit, the log
- * up to last_index, nothing applied yet (processed = firstIndex - 1 = 0,
- * logentry.go:86-96), remotes next = last + 1.  The node around it restarts
+ * up to last_index, nothing applied above the LogDB's first index yet
+ * (processed = firstIndex - 1 = marker, logentry.go:86-96; the state machine
+ * recovers from the latest snapshot), remotes next = last + 1.  Over a
+ * compacted LogDB (snapshot_entries) st[i].commit must be >= the marker
+ * (loadState panics below it, raft.go:429-437) and the entries lie above it.  The node around it restarts
  * too (fresh quiesce state and tick count), and the messages in flight to and
  * from a relaunched replica are lost.  replica[i] takes st[i] and the next
  * st[i].n_entries entries of `ents` (n_entries <= cfg.ring; an entry the
@@ -337,9 +353,11 @@ int rbe_notify_applied(rbe_engine* e, uint64_t n, const uint64_t* replica,
                        const uint64_t* applied);
 int rbe_set_apply_ready(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint8_t* ready);
 
-/* Results of the last round.  Replaces Peer.GetUpdate (peer.go:201-207);
- * Peer.Commit (peer.go:282-293) is implicit (the harness persists and
- * applies every round). */
+/* Results of the last round.  Replaces Peer.GetUpdate (peer.go:201-207).
+ * Peer.Commit (peer.go:282-293) consumes a step's outputs at the step; its log
+ * part is implicit (the step's entries count as saved and its committed
+ * entries as processed) unless cfg.ext_commit, where the host sends it with
+ * rbe_commit. */
 int rbe_get_updates(rbe_engine* e, uint64_t first, uint64_t count, rbe_update* out);
 int rbe_get_messages(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t cap,
                      uint32_t* n_out);
@@ -354,6 +372,34 @@ int rbe_get_entries(rbe_engine* e, uint64_t replica, uint64_t lo, uint64_t hi,
  * received), the node's reqSnapshotIndex and pending compactLogTo (node.go
  * ss, 585-605 / 849-866). */
 int rbe_get_snapshot_state(rbe_engine* e, uint64_t first, uint64_t count, uint64_t* out6);
+
+/* raftpb UpdateCommit (raftpb/raft.go:60-70). */
+typedef struct rbe_update_commit {
+  uint64_t processed, last_applied, stable_log_to, stable_log_term, stable_snapshot_to,
+      ready_to_read;
+} rbe_update_commit;
+/* getUpdateCommit (peer.go:410-427) of the last round's Update of replicas
+ * [first, first + count): processed = last CommittedEntries index,
+ * last_applied = the applied index the step ran with (rbe_notify_applied),
+ * stable_log_to / stable_log_term = the last EntriesToSave entry,
+ * ready_to_read = number of ReadyToReads; all zero for a replica whose step
+ * made no Update (RBE_UF_HAS_UPDATE clear).  Needs cfg.ext_commit. */
+int rbe_get_update_commits(rbe_engine* e, uint64_t first, uint64_t count, rbe_update_commit* out);
+/* Peer.Commit's log part (peer.go:282-293 → entryLog.commitUpdate,
+ * logentry.go:335-355; inMemory.savedLogTo / appliedLogTo, inmemory.go:
+ * 108-167) for replica[i] with uc[i], as the node calls it once SaveRaftState
+ * has persisted the Update (node.go:975-994): savedTo advances only to an
+ * entry the in-memory log still holds with that term, processed to
+ * uc.processed, the in-memory marker to uc.last_applied.  A host that lags
+ * (or never) commits gets the unsaved entries and unprocessed committed
+ * entries again in the next Update, as the reference's Peer does.  Staged and
+ * applied before the next step, in call order; a replica takes one commit per
+ * step (RBE_E_STATE for a second).  A reference panic (processed below the
+ * current value or above committed; last_applied above committed or
+ * processed) sets RBE_FAULT_PANIC in the replica's fault word.  Needs
+ * cfg.ext_commit (RBE_E_STATE); stable_snapshot_to must be 0 (no snapshots
+ * with ext_commit, RBE_E_INVALID). */
+int rbe_commit(rbe_engine* e, uint64_t n, const uint64_t* replica, const rbe_update_commit* uc);
 
 /* ---- Transport wire format ------------------------
  * What a node writes on a TCP connection for Raft traffic: frames of a 2-byte

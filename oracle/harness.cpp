@@ -72,6 +72,7 @@ struct Node {
   // node snapshot state (node.go ss: snapshotIndex, reqSnapshotIndex, compactLogTo)
   u64 ss_index = 0, ss_req = 0, compact_to = 0;
   u32 snap_pend = 0, snap_pend_reject = 0;  // SnapshotStatus of InstallSnapshots sent
+  UpdateCommit uc;              // ext_commit: getUpdateCommit of the last step's Update
   std::vector<Message> in[8];   // this round's inbox, per sender slot (stream order)
   std::vector<Message> nxt[8];  // next round's inbox
   ~Node() { delete peer; }
@@ -233,6 +234,7 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
   Raft* R = p->raft;
   const u32 n = cfg.n_replicas;
   nd->events = 0;
+  nd->uc = UpdateCommit();
   // client input of this round: the workload goes to replicas that lead at
   // round start, host input (harness_push) to the replica it names
   const int wl = R->state == Leader ? wl_input(cfg, gr->cid, r) : 0;
@@ -385,8 +387,10 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
     // applyRaftUpdates: the harness state machine applies immediately
     for (auto& e : ud.committed_entries) applyHash = hash_entry(applyHash, e);
     ctr[HC_ENT_APPLIED] += ud.committed_entries.size();
+    // (a state machine that recovered from a snapshot at a restart skips the
+    // committed entries it already holds, rsm/statemachine.go)
     if (!ud.committed_entries.empty() && !cfg.ext_apply)
-      nd->smAppliedIndex = ud.committed_entries.back().index;
+      nd->smAppliedIndex = std::max(nd->smAppliedIndex, ud.committed_entries.back().index);
     // sendReplicateMessages (node.go:897-905) then, after persistence,
     // sendMessages (node.go:888-895)
     for (auto& m : ud.messages)
@@ -418,7 +422,19 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
       if (!cfg.ext_apply) nd->smAppliedIndex = ud.snapshot.index;
       nd->ss_index = ud.snapshot.index;
     }
-    p->Commit(ud);  // commitRaftUpdate
+    if (!cfg.ext_commit) {
+      p->Commit(ud);  // commitRaftUpdate
+    } else {
+      // Peer.Commit (peer.go:282-293) with its log part deferred: the step's
+      // outputs are consumed here, entryLog.commitUpdate runs when the host
+      // sends the UpdateCommit (harness_commit, the engine's rbe_commit)
+      R->msgs.clear();
+      R->droppedEntries.clear();
+      R->droppedReadIndexes.clear();
+      if (!isEmptyState(ud.state)) p->prevState = ud.state;
+      if (ud.update_commit.ready_to_read > 0) R->readyToRead.clear();
+      nd->uc = ud.update_commit;
+    }
   }
   if (cfg.snapshot_entries) {
     // compactLog (node.go:849-866): the compaction a snapshot asked for, at the
@@ -620,12 +636,24 @@ void harness_restart(Harness* h, u64 replica) {
   nd->q.tick = nd->q.noActivitySince = nd->q.exitQuiesceTick = t;
   nd->tickCount = 0;
   nd->confirmedIndex = 0;
-  nd->smAppliedIndex = cfg.ext_apply ? nd->x_applied : 0;
+  // the state machine recovers from the LogDB's latest snapshot (rsm
+  // RecoverFromSnapshot; 0 without snapshots)
+  nd->smAppliedIndex = cfg.ext_apply ? nd->x_applied : nd->db.snapshot.index;
   nd->events = 0;
   nd->more_to_apply = true;
   for (u32 s = 0; s < N; s++) nd->in[s].clear();
   for (u32 j = 0; j < N; j++)
     if (j != k) gr->nodes[j]->in[k].clear();
+}
+
+void harness_update_commit(const Harness* h, u64 replica, UpdateCommit* out) {
+  const u32 N = h->cfg.n_replicas;
+  *out = h->groups[replica / N]->nodes[replica % N]->uc;
+}
+
+void harness_commit(Harness* h, u64 replica, const UpdateCommit& uc) {
+  const u32 N = h->cfg.n_replicas;
+  h->groups[replica / N]->nodes[replica % N]->peer->raft->log.commitUpdate(uc);
 }
 
 void harness_views(const Harness* h, ReplicaView* out) {

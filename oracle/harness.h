@@ -72,6 +72,9 @@ struct HarnessConfig {
   // snapshot index - CompactionOverhead at its next step (harness.cpp)
   u32 snapshot_entries = 0;
   u32 compaction_overhead = 0;
+  // host-driven persistence: Peer.Commit's log part (entryLog.commitUpdate)
+  // comes from harness_commit, the engine's rbe_commit (needs ext_apply)
+  u32 ext_commit = 0;
 };
 
 // host inputs for the next round (the engine's rbe_push_* / rbe_notify_applied)
@@ -163,6 +166,11 @@ int harness_persisted_entries(const Harness* h, u64 replica, u64 lo, u64 hi, Ent
 // LogDB marker, marker term, snapshot index, snapshot term; node reqSnapshotIndex, compactLogTo
 void harness_snapshot_state(const Harness* h, u64 replica, u64 out6[6]);
 void harness_restart(Harness* h, u64 replica);
+// ext_commit: the UpdateCommit of the replica's last step (zero when it made no
+// Update; getUpdateCommit, peer.go:410-427), and Peer.Commit's log part with a
+// host-chosen UpdateCommit (entryLog.commitUpdate, logentry.go:335-355)
+void harness_update_commit(const Harness* h, u64 replica, UpdateCommit* out);
+void harness_commit(Harness* h, u64 replica, const UpdateCommit& uc);
 
 // shared helpers (restated independently in the engine)
 u64 wl_payload_lo(u64 seed, u64 cid, u64 round);

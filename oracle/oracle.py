@@ -80,7 +80,7 @@ class OrcHarnessConfig(C.Structure):
                 ("cid_stride", C.c_uint64), ("xfer_period", C.c_uint32),
                 ("xfer_mod", C.c_uint32), ("ext_apply", C.c_uint32),
                 ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
-                ("pad3", C.c_uint32)]
+                ("ext_commit", C.c_uint32)]
 
 
 class ReplicaView(C.Structure):
@@ -188,6 +188,8 @@ def lib():
             "orc_harness_snapshot_state": (None, [vp, u64, P(u64)]),
             "orc_harness_persisted_entries": (i32, [vp, u64, u64, u64, P(OrcEntry)]),
             "orc_harness_restart": (i32, [vp, u64]),
+            "orc_harness_update_commit": (None, [vp, u64, P(u64)]),
+            "orc_harness_commit": (i32, [vp, u64, P(u64)]),
             "orc_view_size": (i32, []),
             "orc_splitmix64": (u64, [u64]),
         }
@@ -897,7 +899,8 @@ class Harness:
                  wl_enabled=False, wl_start_round=0, wl_stop_round=0, wl_active_mod=1,
                  wl_read_permille=0, iso_period=0, iso_len=0, iso_mod=10, trace=True,
                  threads=1, cid_stride=1, xfer_period=0, xfer_mod=1, ext_apply=False,
-                 ext_inputs=False, snapshot_entries=0, compaction_overhead=0):
+                 ext_inputs=False, snapshot_entries=0, compaction_overhead=0,
+                 ext_commit=False):
         c = OrcHarnessConfig(
             n_groups=n_groups, n_replicas=n_replicas, check_quorum=int(check_quorum),
             cid_base=cid_base, election_rtt=election_rtt, heartbeat_rtt=heartbeat_rtt,
@@ -907,7 +910,8 @@ class Harness:
             wl_read_permille=wl_read_permille, iso_period=iso_period, iso_len=iso_len,
             iso_mod=iso_mod, trace=int(trace), threads=threads, cid_stride=cid_stride,
             xfer_period=xfer_period, xfer_mod=xfer_mod, ext_apply=int(ext_apply),
-            snapshot_entries=snapshot_entries, compaction_overhead=compaction_overhead)
+            snapshot_entries=snapshot_entries, compaction_overhead=compaction_overhead,
+            ext_commit=int(ext_commit))
         self.n_groups, self.n_replicas = n_groups, n_replicas
         self.h = lib().orc_harness_create(C.byref(c))
         if not self.h:
@@ -969,6 +973,21 @@ class Harness:
         if lib().orc_harness_persisted_entries(self.h, replica, lo, hi, arr) != 0:
             raise _err()
         return [Entry.from_c(arr[i]) for i in range(hi - lo + 1)]
+
+    def update_commit(self, replica):
+        """ext_commit: getUpdateCommit of the replica's last step (peer.go:410-427)
+        as (processed, last_applied, stable_log_to, stable_log_term,
+        stable_snapshot_to, ready_to_read); zeros when it made no Update."""
+        o = (C.c_uint64 * 6)()
+        lib().orc_harness_update_commit(self.h, replica, o)
+        return tuple(o)
+
+    def commit(self, replica, uc):
+        """ext_commit: Peer.Commit's log part with a host-chosen UpdateCommit
+        (entryLog.commitUpdate, logentry.go:335-355); raises where it panics."""
+        a = (C.c_uint64 * 6)(*uc)
+        if lib().orc_harness_commit(self.h, replica, a) != 0:
+            raise _err()
 
     def restart(self, replica):
         """Restart a replica from its LogDB (the engine's rbe_launch)."""

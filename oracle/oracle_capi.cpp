@@ -47,7 +47,7 @@ typedef struct {
   uint32_t iso_mod, trace, threads, pad;
   uint64_t cid_stride;
   uint32_t xfer_period, xfer_mod, ext_apply, snapshot_entries;
-  uint32_t compaction_overhead, pad3;
+  uint32_t compaction_overhead, ext_commit;
 } orc_harness_config;
 
 static thread_local std::string g_err;
@@ -827,6 +827,7 @@ void* orc_harness_create(const orc_harness_config* c) {
   h.ext_apply = c->ext_apply;
   h.snapshot_entries = c->snapshot_entries;
   h.compaction_overhead = c->compaction_overhead;
+  h.ext_commit = c->ext_commit;
   return harness_create(h);
   GUARD_END(nullptr)
 }
@@ -869,6 +870,31 @@ int orc_harness_persisted_entries(void* h, uint64_t replica, uint64_t lo, uint64
   std::vector<Entry> v(hi - lo + 1);
   if (harness_persisted_entries((Harness*)h, replica, lo, hi, v.data())) return -1;
   for (size_t i = 0; i < v.size(); i++) from_entry(v[i], &out[i]);
+  return 0;
+  GUARD_END(-1)
+}
+// ext_commit: {processed, last_applied, stable_log_to, stable_log_term,
+// stable_snapshot_to, ready_to_read} of the last step / sent by the host
+void orc_harness_update_commit(void* h, uint64_t replica, uint64_t* out6) {
+  UpdateCommit u;
+  harness_update_commit((Harness*)h, replica, &u);
+  out6[0] = u.processed;
+  out6[1] = u.last_applied;
+  out6[2] = u.stable_log_to;
+  out6[3] = u.stable_log_term;
+  out6[4] = u.stable_snapshot_to;
+  out6[5] = u.ready_to_read;
+}
+int orc_harness_commit(void* h, uint64_t replica, const uint64_t* uc6) {
+  GUARD_BEGIN
+  UpdateCommit u;
+  u.processed = uc6[0];
+  u.last_applied = uc6[1];
+  u.stable_log_to = uc6[2];
+  u.stable_log_term = uc6[3];
+  u.stable_snapshot_to = uc6[4];
+  u.ready_to_read = uc6[5];
+  harness_commit((Harness*)h, replica, u);
   return 0;
   GUARD_END(-1)
 }

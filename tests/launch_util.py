@@ -5,13 +5,21 @@ false).  The engine is handed exactly what the node would read back: pb.State
 and the tail of the log (its in-memory window)."""
 
 
-def restart(eng, ref, replicas, ring):
+def restart(eng, ref, replicas, ring, snapshots=False):
+    """`snapshots`: the LogDB may be compacted; the launch state carries its
+    marker and latest snapshot (harness_snapshot_state) and the entries above
+    the marker."""
     states, ents = [], []
     for r in replicas:
         term, vote, commit, last = ref.persisted(r)
+        snap = ()
         lo = max(1, last - ring + 1)
-        es = ref.persisted_entries(r, lo, last) if last else []
-        states.append((term, vote, commit, last))
+        if snapshots:
+            marker, mterm, ssi, sst = ref.snapshot_state(r)[:4]
+            snap = (marker, mterm, ssi, sst)
+            lo = max(lo, marker + 1)
+        es = ref.persisted_entries(r, lo, last) if last >= lo else []
+        states.append((term, vote, commit, last) + snap)
         ents.append([(e.index, e.term, e.type, e.cmd) for e in es])
     eng.launch(replicas, states, ents)
     for r in replicas:

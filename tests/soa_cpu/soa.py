@@ -6,8 +6,8 @@ import ctypes as C
 import os
 
 from dragonboat_amd.engine import (CTR_NUM, COUNTER_NAMES, NodeInputs, RbeEntry, RbeMessage,
-                                   RbeReplicaView, RbeWireFrame, entry_cmds, entry_fields,
-                                   make_config, outbox_call, push_messages_call)
+                                   RbeReplicaView, RbeUpdateCommit, RbeWireFrame, entry_cmds,
+                                   entry_fields, make_config, outbox_call, push_messages_call)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _lib = None
@@ -80,6 +80,8 @@ def lib():
                 "report_snapshot_status": [C.c_uint64, u64p, u64p, P(C.c_uint8)],
                 "notify_applied": [C.c_uint64, u64p, u64p],
                 "set_apply_ready": [C.c_uint64, u64p, P(C.c_uint8)],
+                "commit": [C.c_uint64, u64p, P(RbeUpdateCommit)],
+                "get_update_commits": [C.c_uint64, C.c_uint64, P(RbeUpdateCommit)],
                 "launch": [C.c_uint64, u64p, C.c_void_p, C.c_void_p, C.c_void_p]}.items():
             fn = getattr(L, "soa_" + name)
             fn.restype = C.c_int
@@ -120,6 +122,15 @@ class SoaCpu(NodeInputs):
 
     def run(self, rounds=1):
         lib().soa_run(self.h, rounds)
+
+    def update_commits(self, first=0, count=None):
+        count = self.n_rep - first if count is None else count
+        arr = (RbeUpdateCommit * max(1, count))()
+        rc = lib().soa_get_update_commits(self.h, first, count, arr)
+        if rc:
+            raise RuntimeError(f"soa_get_update_commits rc={rc}")
+        return [tuple(getattr(arr[i], f) for f, _ in RbeUpdateCommit._fields_)
+                for i in range(count)]
 
     def entry_cmds(self, replica, lo, hi):
         return entry_cmds(lib().soa_get_entry_cmds, self.h, replica, lo, hi)

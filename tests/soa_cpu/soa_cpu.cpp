@@ -56,7 +56,7 @@ static void run_round(SoaEngine* e, bool tick = true) {
     HostHeap& hp = e->hin.heap;
     for (u64 p = hp.flushed; p < hp.head; p++) e->heap[p % hp.cap] = hp.stage[p - hp.flushed];
     e->heap_head = hp.head;
-    e->hin.apply_host(e->P);
+    e->hin.apply_host(e->P, e->C);
     e->hin.clear();
   }
   if (e->C.iso_period && e->round > 0 && e->round % e->C.iso_period == 0)
@@ -202,6 +202,7 @@ void* soa_create(const rbe_config* cfg) {
   C.wl_read_permille = cfg->wl_read_permille;
   C.ext_inputs = cfg->ext_inputs;
   C.ext_apply = cfg->ext_apply;
+  C.ext_commit = cfg->ext_commit;
   C.in_cap = cfg->in_cap ? cfg->in_cap : (u32)(cfg->n_groups > 1024 ? cfg->n_groups : 1024);
   C.xfer_period = cfg->xfer_period;
   C.xfer_mod = cfg->xfer_mod;
@@ -245,6 +246,7 @@ void* soa_create(const rbe_config* cfg) {
   memset(P.gwake, GW_AWAKE, G);  // every group starts awake
   P.snp = C.snapshot_entries ? alloc<SnapSt>(e, R) : nullptr;
   P.rem_snap = C.snapshot_entries ? alloc<u64>(e, R * N) : nullptr;
+  P.imark = C.ext_commit ? alloc<u64>(e, R) : nullptr;
   C.heap_bytes = (cfg->heap_bytes + 255) & ~255ull;
   e->heap.assign(C.heap_bytes, 0);
   e->hin.init(R, C.n, C.in_cap, C.heap_bytes);
@@ -390,18 +392,20 @@ int soa_launch(void* h, uint64_t n, const uint64_t* replica, const rbe_launch_st
   u64 off = 0;
   for (u64 i = 0; i < n; i++) {
     const rbe_launch_state& x = st[i];
+    const u64* t = terms.data() + off;
+    const Body* b = bodies.data() + off;
     if (e->C.n == 1)
       relaunch_replica<1>(e->P, e->C, replica[i], x.term, x.vote, x.commit, x.last_index,
-                          x.n_entries, terms.data() + off, bodies.data() + off, ppar,
-                          e->tclk);
+                          x.n_entries, t, b, ppar, e->tclk, x.marker, x.marker_term,
+                          x.snapshot_index, x.snapshot_term);
     else if (e->C.n == 3)
       relaunch_replica<3>(e->P, e->C, replica[i], x.term, x.vote, x.commit, x.last_index,
-                          x.n_entries, terms.data() + off, bodies.data() + off, ppar,
-                          e->tclk);
+                          x.n_entries, t, b, ppar, e->tclk, x.marker, x.marker_term,
+                          x.snapshot_index, x.snapshot_term);
     else
       relaunch_replica<5>(e->P, e->C, replica[i], x.term, x.vote, x.commit, x.last_index,
-                          x.n_entries, terms.data() + off, bodies.data() + off, ppar,
-                          e->tclk);
+                          x.n_entries, t, b, ppar, e->tclk, x.marker, x.marker_term,
+                          x.snapshot_index, x.snapshot_term);
     e->P.gwake[replica[i] / e->C.n] = GW_AWAKE;
     off += x.n_entries;
   }
@@ -440,6 +444,29 @@ int soa_notify_applied(void* h, uint64_t n, const uint64_t* replica, const uint6
   SoaEngine* e = (SoaEngine*)h;
   if (!e->C.ext_apply) return RBE_E_STATE;
   return e->hin.notify_applied(n, replica, applied);
+}
+// rbe_commit / rbe_get_update_commits on the host build
+int soa_commit(void* h, uint64_t n, const uint64_t* replica, const rbe_update_commit* uc) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (!e->C.ext_commit) return RBE_E_STATE;
+  return e->hin.commit(n, replica, uc);
+}
+int soa_get_update_commits(void* h, uint64_t first, uint64_t count, rbe_update_commit* out) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (!e->C.ext_commit) return RBE_E_STATE;
+  if (!out || first + count > e->C.n_rep) return RBE_E_INVALID;
+  for (u64 i = 0; i < count; i++) {
+    const u64 r = first + i;
+    rbe_update u;
+    update_view(e->P.upd[r], e->P.core[r], e->P.hot[r], e->round, u);
+    auto term_of = [&](u64 idx) -> u64 {
+      const Core& c = e->P.core[r];
+      return idx == c.last_index ? c.t_last
+                                 : e->P.term_ring[(idx & (u64)(e->C.ring - 1)) * e->C.n_rep + r];
+    };
+    update_commit_view(u, e->P.applied[r], term_of, out[i]);
+  }
+  return RBE_OK;
 }
 
 // rbe_wire_encode on the host build: the same wire_cell / trailer / header

@@ -1,0 +1,41 @@
+"""Explicit Peer.Commit on the HIP engine (rbe_commit / rbe_get_update_commits
+through the C ABI, cfg.ext_commit) against the oracle harness, round by round:
+a host whose persistence lags and sometimes saves only a prefix of an Update
+(tests/commit_util.py).  Every replica field and trace digest, and every
+UpdateCommit the engine reports, equal the oracle's.  CPU-tier twin:
+tests/test_ext_commit.py."""
+import pytest
+
+import oracle as O
+from commit_util import run_commit_driven
+from parity_util import C2, C3, C4
+
+pytestmark = pytest.mark.gpu
+
+DRIVEN = dict(maxm=40, ecap=64, rq_cap=32, ring=256)
+
+
+@pytest.mark.parametrize("name,kw", [("C2", C2), ("C3", C3), ("C4", C4)])
+def test_gpu_delayed_persist_parity(gpu_available, name, kw):
+    from dragonboat_amd.engine import Engine
+    base = dict(kw, n_groups=12, ext_inputs=True, ext_apply=True, ext_commit=True)
+    eng, ref = Engine(device=0, trace=True, **dict(base, **DRIVEN)), O.Harness(**base)
+    d, st = run_commit_driven(eng, ref, 160, seed=5)
+    assert d is None, f"{name}: first divergence {d}"
+    assert eng.fault_summary()[0] == 0
+    assert st["committed"] > 100 and st["partial"] > 5, st
+    eng.close()
+
+
+def test_gpu_commit_panic_faults(gpu_available):
+    from dragonboat_amd.engine import Engine
+    eng = Engine(device=0, trace=True, n_groups=1, n_replicas=3, ext_inputs=True,
+                 ext_apply=True, ext_commit=True)
+    for _ in range(3):
+        eng.step()
+    c = eng.views()[0].committed
+    eng.commit([0], [(c + 5, 0, 0, 0, 0, 0)])  # processed above committed: commitUpdate panics
+    eng.step()
+    n, bits = eng.fault_summary()
+    assert n == 1 and bits & 0x20
+    eng.close()

@@ -105,14 +105,52 @@ def test_compaction_state_survives_group_export():
     assert b.faults()[0] == 0
 
 
-def test_compaction_config_rules():
+def test_compaction_launch_checks():
+    """rbe_launch over a compacted LogDB: the batch is refused whole when the
+    commit lies below the marker (loadState panics, raft.go:429-437), when
+    entries reach down to the marker, or when there is no snapshot plane."""
     from dragonboat_amd.engine import RBE_E_INVALID, InputError
     eng = SoaCpu(trace=True, **dict(C3, **SNAP), ring=128)
     eng.run(5)
-    # a restart carries no LogDB snapshot / compaction marker
-    with pytest.raises(InputError) as ei:
-        eng.launch([0], [(1, 0, 0, 0)], [[]])
+    ents = [[(i, 2, 0, b"") for i in range(11, 21)]]
+    with pytest.raises(InputError) as ei:  # commit below the marker
+        eng.launch([0], [(2, 0, 9, 20, 10, 2, 10, 2)], ents)
     assert ei.value.rc == RBE_E_INVALID
+    with pytest.raises(InputError):  # an entry at the marker
+        eng.launch([0], [(2, 0, 12, 20, 10, 2, 10, 2)], [[(i, 2, 0, b"") for i in range(10, 21)]])
+    with pytest.raises(InputError):  # a marker without its term
+        eng.launch([0], [(2, 0, 12, 20, 10, 0, 10, 2)], ents)
+    plain = SoaCpu(trace=True, **C3, ring=128)
+    with pytest.raises(InputError):  # no snapshots configured
+        plain.launch([0], [(2, 0, 12, 20, 10, 2, 10, 2)], ents)
+    eng.launch([0], [(2, 0, 12, 20, 10, 2, 10, 2)], ents)
+
+
+@pytest.mark.parametrize("name", ["C3_SNAP", "C3_NOCQ_SNAP", "MIXED_SNAP"])
+def test_restart_after_compaction(name):
+    """Restarts over compacted LogDBs (Peer.Launch over an existing log,
+    peer.go:64-86; entryLog from GetRange: processed = marker,
+    logentry.go:86-96; Term(marker) from the LogDB): replicas restarted with
+    their LogDB's marker, snapshot and entries above the marker continue
+    bit-exact with the oracle's restarted nodes, which recover their state
+    machine from that snapshot."""
+    from launch_util import restart
+    kw, extra, rounds = CASES[name]
+    eng = SoaCpu(trace=True, **kw, **extra)
+    ref = O.Harness(**kw)
+    run_case(eng, ref, 180)
+    ring = extra.get("ring", 64)
+    n = kw["n_replicas"]
+    compacted = [i for i in range(eng.n_rep) if ref.snapshot_state(i)[0] > 0]
+    assert len(compacted) > 5
+    lead = [i for i, v in enumerate(ref.views()) if v.role == O.LEADER and i in compacted]
+    picks = sorted(set(compacted[:4] + lead[:3] + list(range(2 * n, 3 * n))))
+    restart(eng, ref, picks, ring, snapshots=True)
+    run_case(eng, ref, 120)
+    restart(eng, ref, compacted[-3:], ring, snapshots=True)
+    run_case(eng, ref, 80)
+    assert eng.faults()[0] == 0
+    assert not counters_match(eng.counters(), ref.counters())
 
 
 @pytest.mark.parametrize("mode", ["staged", "aux"])
