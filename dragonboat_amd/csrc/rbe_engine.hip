@@ -467,6 +467,10 @@ static int make_params(const rbe_config* cfg, Params* out) {
   // is then the host's (rbe_notify_applied), never the step's own
   C.ext_commit = cfg->ext_commit;
   if (C.ext_commit && !C.ext_apply) return RBE_E_INVALID;
+  C.membership = cfg->membership;
+  C.cc_period = cfg->cc_period;
+  C.cc_mod = cfg->cc_mod ? cfg->cc_mod : 1;
+  if (C.cc_period && !C.membership) return RBE_E_INVALID;
   C.in_cap = cfg->in_cap ? cfg->in_cap : (u32)(cfg->n_groups > 1024 ? cfg->n_groups : 1024);
   if (cfg->n_groups > 0xFFFFFFFFull && !cfg->in_cap) C.in_cap = 0xFFFFFFFFu;
   C.xfer_period = cfg->xfer_period;
@@ -1153,6 +1157,26 @@ int rbe_set_apply_ready(rbe_engine* e, uint64_t n, const uint64_t* replica, cons
   return e->hin.set_apply_ready(n, replica, ready);
 }
 
+int rbe_propose_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica,
+                              const uint32_t* type, const uint64_t* node_id) {
+  if (!e) return RBE_E_INVALID;
+  if (!e->C.membership || !e->C.ext_inputs) return RBE_E_STATE;
+  return e->hin.propose_config_change(n, replica, type, node_id);
+}
+
+int rbe_apply_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica,
+                            const uint64_t* node_id, const uint32_t* type) {
+  if (!e) return RBE_E_INVALID;
+  if (!e->C.membership || !e->C.ext_apply) return RBE_E_STATE;
+  return e->hin.apply_config_change(n, replica, node_id, type, false);
+}
+
+int rbe_reject_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica) {
+  if (!e) return RBE_E_INVALID;
+  if (!e->C.membership || !e->C.ext_inputs) return RBE_E_STATE;
+  return e->hin.apply_config_change(n, replica, nullptr, nullptr, true);
+}
+
 int rbe_notify_applied(rbe_engine* e, uint64_t n, const uint64_t* replica,
                        const uint64_t* applied) {
   if (!e) return RBE_E_INVALID;
@@ -1422,8 +1446,10 @@ int rbe_get_views(rbe_engine* e, uint64_t first, uint64_t count, rbe_replica_vie
     v.votes_resp = h.votes_resp;
     v.votes_granted = h.votes_granted;
     v.events = (e->round > 0 && upd[i].round == e->round - 1) ? upd[i].events : 0u;
+    v.removed = c.members & MB_REMOVED;
     if (h.role == R_Leader) {
       for (u32 s = 0; s < N && s < 8; s++) {
+        if ((v.removed >> s) & 1u) continue;  // not in raft.remotes
         v.match[s] = rem[i * N + s].match;
         v.next[s] = rem[i * N + s].next;
         v.rstate[s] = rst[i * N + s] & 3;
@@ -1717,7 +1743,7 @@ int rbe_fault_summary(rbe_engine* e, uint64_t* n_faulty, uint32_t* fault_or) {
   u64 n = 0;
   u32 o = 0;
   for (u64 i = 0; i < R; i++) {
-    if (upd[i].fault) n++;
+    if (upd[i].fault & ~F_HANDOFF) n++;  // a hand-off is not a fault (rbe.h)
     o |= upd[i].fault;
   }
   *n_faulty = n;

@@ -615,6 +615,11 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   // ---- eligibility on level-1 data
   if (h.role != R_Leader) return false;
   if (h.flags & HF_SNAP_WORK) return false;  // compaction / SnapshotStatus: full table
+  // membership: a changed voter set, a ConfigChange in the log or to apply,
+  // or one to propose this round (full handler table)
+  if (C.membership && ((c.members | c.cc_apply) != 0 ||
+                       (C.cc_period && cc_selected(C, cid, round))))
+    return false;
   // ext_commit: an Update whose unsaved entries left the in-memory log (Lane::run)
   if (C.ext_commit && c.saved_to + 1 < P.imark[r]) return false;
   if (h.flags & (HF_APPLY_PENDING | HF_IS_LTT)) return false;
@@ -1308,6 +1313,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   u32 cdirty = 0;  // Core chunks an append or a new leader wrote (fast_finish)
   if (h.role != R_Follower) return false;
   if (h.flags & HF_SNAP_WORK) return false;  // compaction / SnapshotStatus: full table
+  if (C.membership && (c.members | c.cc_apply) != 0) return false;  // (lead_fast)
   if (C.ext_commit && c.saved_to + 1 < P.imark[r]) return false;  // (lead_fast)
   if (h.flags & (HF_APPLY_PENDING | HF_IS_LTT)) return false;
   if (c.ltt != 0) return false;
@@ -1401,6 +1407,10 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
         if (m.log_index != L) return false;      // a ring lookup (or past the tail)
         if (m.log_term != T) continue;           // rejected: no lookups, no change
         if (m.n_ent > 1 || (m.n_ent == 1 && i >= 4)) return false;
+        if (C.membership && m.n_ent == 1 &&      // a ConfigChange entry: full table
+            ent_type(i == 0 ? pre0.type : (i == 1 ? pre1.type : (i == 2 ? pre2.type : pre3.type))) ==
+                E_ConfigChange)
+          return false;
         if (m.n_ent == 1) {                      // conflict at L + 1: append
           T = i == 0 ? pre0.term : (i == 1 ? pre1.term : (i == 2 ? pre2.term : pre3.term));
           L = L + 1;

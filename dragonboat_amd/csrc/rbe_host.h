@@ -577,6 +577,35 @@ struct HostInputs {
     }
     return RBE_OK;
   }
+  // rbe_propose_config_change / rbe_apply_config_change / rbe_reject_config_change
+  int propose_config_change(u64 cnt, const u64* replica, const u32* type, const u64* node) {
+    if (cnt && (!type || !node)) return RBE_E_INVALID;
+    for (u64 i = 0; i < cnt; i++)
+      if (type[i] > CC_AddWitness || node[i] < 1 || node[i] > n) return RBE_E_INVALID;
+    int rc = check_replicas(cnt, replica, EXT_CC_PROPOSE);
+    if (rc) return rc;
+    for (u64 i = 0; i < cnt; i++) {
+      ExtIn& x = rec(replica[i]);
+      x.flags |= EXT_CC_PROPOSE;
+      x.pad[0] = (u64)type[i] | (node[i] << 8);
+    }
+    return RBE_OK;
+  }
+  int apply_config_change(u64 cnt, const u64* replica, const u64* node, const u32* type,
+                          bool reject) {
+    if (cnt && !reject && (!type || !node)) return RBE_E_INVALID;
+    for (u64 i = 0; i < cnt && !reject; i++)
+      if (type[i] > CC_AddWitness || node[i] > n) return RBE_E_INVALID;
+    int rc = check_replicas(cnt, replica, EXT_CC_APPLY);
+    if (rc) return rc;
+    for (u64 i = 0; i < cnt; i++) {
+      ExtIn& x = rec(replica[i]);
+      x.flags |= EXT_CC_APPLY;
+      x.pad[1] = reject ? (u64)(CCA_VALID | CCA_REJECT)
+                        : (u64)(CCA_VALID | (type[i] << 3) | (u32)node[i]);
+    }
+    return RBE_OK;
+  }
   int notify_applied(u64 cnt, const u64* replica, const u64* value) {
     if (cnt && !value) return RBE_E_INVALID;
     int rc = check_replicas(cnt, replica, 0);

@@ -97,7 +97,8 @@ inline u64 snap_behavior_hash(const Params& C) {
                    C.wl_stop_round, C.wl_active_mod, C.wl_read_permille, C.ext_inputs,
                    C.iso_period, C.iso_len, C.iso_mod, C.rep_world, C.rep_rank,
                    C.snapshot_entries, C.compaction_overhead, C.heap_bytes, C.ext_apply,
-                   C.xfer_period, C.xfer_mod, C.ext_commit};
+                   C.xfer_period, C.xfer_mod, C.ext_commit, C.membership, C.cc_period,
+                   C.cc_mod};
   u64 h = 0x243F6A8885A308D3ull;
   for (u64 x : f) {
     h ^= x + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);

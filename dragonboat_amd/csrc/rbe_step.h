@@ -91,6 +91,28 @@ RBE_HD u32 xfer_input(const Params& C, u64 cid, u32 round, u32 k) {
   if (below(h, C.n) != k) return 0;
   return below(mix64(h), C.n) + 1;
 }
+// config-change schedule (restated in oracle/harness.cpp
+// cc_selected / cc_target): every cc_period-th round, in groups selected 1 in
+// cc_mod, the replica leading at round start proposes removing a seeded voter
+// (while more than two vote) or adding it back
+RBE_HD bool cc_selected(const Params& C, u64 cid, u32 round) {
+  if (!C.cc_period || round == 0 || round % C.cc_period != 0) return false;
+  const u64 epoch = round / C.cc_period;
+  return C.cc_mod <= 1 ||
+         below(mix64(C.seed ^ (cid * 0xE7037ED1A0B428DBULL) ^ (epoch << 28)), C.cc_mod) == 0;
+}
+RBE_HD u32 cc_target(const Params& C, u64 cid, u32 round) {
+  const u64 epoch = round / C.cc_period;
+  return below(mix64(C.seed ^ (cid * 0x8EBC6AF09C88C6E3ULL) ^ (epoch << 20) ^ 0xCC), C.n) + 1;
+}
+// The stand-in ConfigChange Cmd the engine shares with the oracle harness (8
+// bytes, LE of 0xCC << 56 | type << 48 | node id; bootstrap's entries are its
+// AddNode form): what the engine's own state machine decodes when it applies
+// a committed ConfigChange entry (cfg.membership without ext_apply).
+RBE_HD u64 cc_word(u32 type, u64 node) {
+  return 0xCC00000000000000ULL | ((u64)(type & 0xFFu) << 48) | (node & 0xFFFFFFFFFFFFULL);
+}
+
 RBE_HD bool iso_selected(const Params& C, u64 cid, u32 epoch) {
   if (C.iso_mod <= 1) return true;
   return below(mix64(C.seed ^ (cid * 0x94D049BB133111EBULL) ^ ((u64)epoch << 40)), C.iso_mod) ==
@@ -275,6 +297,7 @@ struct Lane {
   u64 t_last;  // term of entry `last` (log-tail cache, kept in Core)
   u64 lead_start;  // leader: index of its no-op (Core::lead_start)
   u8 vote, leader, ltt, rq_head, rq_count;
+  u8 members, cc_apply;  // Core::members / cc_apply (membership)
   u64 c_match[N], c_next[N];  // LEAD: remote slots held in registers
   u32 c_st[N];
   u8 iso;  // isolation mask of this group for this round
@@ -769,7 +792,67 @@ struct Lane {
     last = idx;
     t_last = term;
     try_update(k, last);
-    if (N / 2 + 1 == 1) try_commit();
+    if (quorum() == 1) try_commit();
+  }
+
+  // ------------------------------------------------------------- membership
+  // raft.remotes of this replica's view: every slot not in Core::members'
+  // removed bits (raft.go:366-416 numVotingMembers / quorum / votingMembers;
+  // observers and witnesses are handed to the host, F_HANDOFF)
+  RBE_HD bool voter(u32 s) const { return !((members >> s) & 1u); }
+  RBE_HD u32 voters_mask() const { return ((1u << N) - 1u) & ~(u32)members; }
+  RBE_HD u32 quorum() const { return popc8(voters_mask()) / 2 + 1; }
+  RBE_HD bool from_member(u32 from) const { return from >= 1 && from <= N && voter(from - 1u); }
+  RBE_HD void set_handoff() {  // not a fault (rbe_types.h F_HANDOFF): no fault counted
+    fault |= F_HANDOFF;
+  }
+  // handleNodeConfigChange (raft.go:1537-1556) → addNode / removeNode
+  // (raft.go:1135-1198); `m.hint` = node id, `m.hint_high` = ConfigChangeType
+  RBE_HD void on_config_change(const Msg& m) {
+    if (!C.membership) {
+      set_fault(F_UNSUPPORTED);
+      return;
+    }
+    if (m.reject) {  // RejectConfigChange: clearPendingConfigChange
+      flags &= (u8)~HF_PENDING_CC;
+      return;
+    }
+    const u64 nid = m.hint;
+    const u32 type = (u32)m.hint_high;
+    if (type == CC_AddObserver || type == CC_AddWitness) {
+      flags &= (u8)~HF_PENDING_CC;
+      set_handoff();
+      return;
+    }
+    if (type > CC_AddWitness) {
+      set_fault(F_PANIC);  // "unexpected config change type"
+      return;
+    }
+    if (nid < 1 || nid > N) {  // a node outside the group's slots
+      set_fault(F_UNSUPPORTED);
+      return;
+    }
+    const u32 s = (u32)nid - 1u;
+    flags &= (u8)~HF_PENDING_CC;  // clearPendingConfigChange
+    if (type == CC_AddNode) {
+      if (voter(s)) return;  // already a voting member
+      members &= (u8)~(1u << s);
+      set_rmatch(s, 0);  // setRemote(id, 0, lastIndex + 1): Retry, not active
+      set_rnext(s, last + 1);
+      set_rst(s, 0);
+      return;
+    }
+    // RemoveNode (deleteRemote; no observer or witness to delete)
+    members |= (u8)(1u << s);
+    if (s == k && role == R_Leader) become_follower(term, 0);
+    if (ltt != 0 && role == R_Leader && ltt == (u8)nid) ltt = 0;  // abortLeaderTransfer
+    if (role == R_Leader && voters_mask() != 0) {
+      if (try_commit()) broadcast_replicate();
+    }
+  }
+  // a log entry that is a ConfigChange: MB_CC_IN_LOG until it is applied
+  RBE_HD void note_cc(u32 type) {
+    if (ent_type(type) == E_ConfigChange) members |= MB_CC_IN_LOG;
   }
 
   // ------------------------------------------------------------- commit (kernel 1)
@@ -777,7 +860,10 @@ struct Lane {
   // values = the quorum-th largest; a register-resident selection over N.
   RBE_HD u64 kth_match() {
     u64 m[N];
-    for (u32 s = 0; s < N; s++) m[s] = rmatch(s);
+    // non-voters sort below every voter (match 0), so the quorum-th largest of
+    // the voters is the quorum-th largest of all N (raft.go tryCommit over
+    // r.remotes and r.witnesses)
+    for (u32 s = 0; s < N; s++) m[s] = voter(s) ? rmatch(s) : 0;
     // odd-even transposition sort (fully unrolled for a compile-time N)
     for (u32 pass = 0; pass < N; pass++) {
       for (u32 i = pass & 1u; i + 1 < N; i += 2) {
@@ -787,7 +873,7 @@ struct Lane {
       }
     }
     ctr.v[C_REMOTE_TOUCH] += N;
-    return m[N - (N / 2 + 1)];
+    return m[N - quorum()];
   }
   RBE_HD bool try_commit() { return log_try_commit(kth_match(), term); }
 
@@ -833,8 +919,8 @@ struct Lane {
   }
   // Fan-out sends are deferred to the single post-event site in run() (same
   // emission order: every handler requests them as its last action).
-  RBE_HD void broadcast_replicate() {  // raft.go:794-808
-    rep_mask |= ((1u << N) - 1u) & ~(1u << k);
+  RBE_HD void broadcast_replicate() {  // raft.go:794-808 (r.nodes(): the voting members)
+    rep_mask |= voters_mask() & ~(1u << k);
   }
   RBE_HD void request_replicate(u32 slot) { rep_mask |= 1u << slot; }  // sendReplicateMessage
   RBE_HD void send_heartbeat(u32 slot, u64 low, u64 high) {  // raft.go:810-820
@@ -897,7 +983,7 @@ struct Lane {
     ReadReq* p = rq_at((u32)pos);
     p->confirmed |= (u8)(1u << (from - 1));
     ctr.v[C_RQ_TOUCH]++;
-    if ((int)popc8(p->confirmed) + 1 < (int)(N / 2 + 1)) return;
+    if ((int)popc8(p->confirmed) + 1 < (int)quorum()) return;
     u64 sindex = p->index;
     u32 done = (u32)pos + 1;
     for (u32 i = 0; i < done; i++) {
@@ -924,24 +1010,46 @@ struct Lane {
       report_dropped_proposal(ents, cnt);
       return;
     }
-    for (u32 i = 0; i < cnt; i++) {
-      if (ent_type(ents[i].type) == E_ConfigChange) {
-        set_fault(F_UNSUPPORTED);  // config change proposals are host slow path
-        return;
+    if (!C.membership) {
+      for (u32 i = 0; i < cnt; i++) {
+        if (ent_type(ents[i].type) == E_ConfigChange) {
+          set_fault(F_UNSUPPORTED);  // config change proposals need cfg.membership
+          return;
+        }
       }
     }
     for (u32 i = 0; i < cnt; i++) {
       u64 idx = last + 1;
-      ring_put(idx, term, ents[i].type, ents[i].len, ents[i].lo, ents[i].hi);
+      Ent e = ents[i];
+      if (ent_type(e.type) == E_ConfigChange) {
+        if (flags & HF_PENDING_CC) {
+          // reportDroppedConfigChange (raft.go:1983-1985): the entry joins
+          // DroppedEntries and an empty application entry takes its place
+          n_drop_ent++;
+          if (TRACE) {
+            drop_hash = hfold(drop_hash, 0);
+            drop_hash = hfold(drop_hash, e.term);
+            drop_hash = hfold(drop_hash, ent_word(e.type, e.len));
+            drop_hash = hfold(drop_hash, e.lo);
+            drop_hash = hfold(drop_hash, cmd_hi(e.type, e.hi));
+          }
+          e.type = E_Application;
+          e.len = 0;
+          e.lo = e.hi = 0;
+        }
+        flags |= HF_PENDING_CC;  // setPendingConfigChange
+      }
+      note_cc(e.type);
+      ring_put(idx, term, e.type, e.len, e.lo, e.hi);
       last = idx;
       t_last = term;
     }
     try_update(k, last);
-    if (N / 2 + 1 == 1) try_commit();
+    if (quorum() == 1) try_commit();
     broadcast_replicate();
   }
   RBE_HD void on_leader_read_index(u64 low, u64 high, u8 from) {  // raft.go:1633-1665
-    if (N / 2 + 1 != 1) {
+    if (quorum() != 1) {
       // hasCommittedEntryAtCurrentTerm (raft.go:1609-1618)
       if (log_term(committed) != term) {
         report_dropped_read_index(low, high);
@@ -1000,15 +1108,16 @@ struct Lane {
       send(t);
     }
   }
-  RBE_HD bool leader_has_quorum() {  // raft.go:378-388
+  RBE_HD bool leader_has_quorum() {  // raft.go:378-388 (votingMembers)
     u32 c = 0;
     for (u32 s = 0; s < N; s++) {
+      if (!voter(s)) continue;
       if (s == k || ractive(s)) {
         c++;
         set_active(s, false);
       }
     }
-    return c >= N / 2 + 1;
+    return c >= quorum();
   }
 
   // ------------------------------------------------------------- follower side (kernel 2)
@@ -1039,9 +1148,11 @@ struct Lane {
           // truncate-and-append; savedTo = min(savedTo, first-1)
           if (conflict - 1 >= 1 && conflict - 1 <= last && log_term(conflict - 1) > ents[ci].term)
             set_fault(F_PANIC);
-          for (u32 i = ci; i < m.n_ent; i++)
+          for (u32 i = ci; i < m.n_ent; i++) {
             ring_put(m.log_index + 1 + i, ents[i].term, ents[i].type, ents[i].len, ents[i].lo,
                      ents[i].hi);
+            note_cc(ents[i].type);
+          }
           last = m.log_index + m.n_ent;
           t_last = ents[m.n_ent - 1].term;
           saved_to = umin64(saved_to, conflict - 1);
@@ -1110,7 +1221,7 @@ struct Lane {
     // handleVoteResp(self, false)
     vresp |= (u8)(1u << k);
     vgrant |= (u8)(1u << k);
-    if (N / 2 + 1 == 1) {
+    if (quorum() == 1) {  // isSingleNodeQuorum
       become_leader();
       return;
     }
@@ -1121,7 +1232,7 @@ struct Lane {
     }
     u64 lt = log_term(last);
     for (u32 s = 0; s < N; s++) {
-      if (s == k) continue;
+      if (s == k || !voter(s)) continue;
       Msg m = mk(M_RequestVote, (u8)(s + 1));
       m.term = term;
       m.log_index = last;
@@ -1166,7 +1277,7 @@ struct Lane {
       if (!m.reject) vgrant |= bit;
     }
     u32 count = popc8(vgrant);
-    u32 q = N / 2 + 1;
+    u32 q = quorum();
     if (count == q) {
       become_leader();
       broadcast_replicate();
@@ -1179,7 +1290,7 @@ struct Lane {
   RBE_HD void raft_tick();
   RBE_HD void non_leader_tick() {  // raft.go:566-590
     etick++;
-    if (etick >= ret) {  // !selfRemoved() && timeForElection()
+    if (voter(k) && etick >= ret) {  // !selfRemoved() && timeForElection()
       etick = 0;
       // Handle(Election): term 0 passes the gate; handled in any role
       if constexpr (FULL) on_election();
@@ -1343,7 +1454,7 @@ struct Lane {
             leader = m.from;
             on_install_snapshot(m);
             return;
-          case M_ConfigChangeEvent:
+          case M_ConfigChangeEvent: on_config_change(m); return;
           case M_SnapshotReceived: set_fault(F_UNSUPPORTED); return;
           default: return;
         }
@@ -1369,7 +1480,7 @@ struct Lane {
             become_follower(term, m.from);
             on_install_snapshot(m);
             return;
-          case M_ConfigChangeEvent:
+          case M_ConfigChangeEvent: on_config_change(m); return;
           case M_SnapshotReceived: set_fault(F_UNSUPPORTED); return;
           default: return;
         }
@@ -1377,21 +1488,23 @@ struct Lane {
         switch (m.type) {
           case M_Propose: on_leader_propose(ents, m.n_ent); return;
           case M_ReadIndex: on_leader_read_index(m.hint, m.hint_high, m.from); return;
+          // lw (raft.go:2013-2035): the remote of m.From, or nothing when
+          // it is not a member of this replica's view
           case M_ReplicateResp:
-            if (m.from >= 1 && m.from <= N) on_replicate_resp(m, m.from - 1u);
+            if (from_member(m.from)) on_replicate_resp(m, m.from - 1u);
             return;
           case M_HeartbeatResp:
-            if (m.from >= 1 && m.from <= N) on_heartbeat_resp(m, m.from - 1u);
+            if (from_member(m.from)) on_heartbeat_resp(m, m.from - 1u);
             return;
           case M_LeaderTransfer:
-            if (m.from >= 1 && m.from <= N) on_leader_transfer(m, m.from - 1u);
+            if (from_member(m.from)) on_leader_transfer(m, m.from - 1u);
             return;
           case M_Unreachable:  // raft.go:1773-1777
-            if (m.from >= 1 && m.from <= N && rstate(m.from - 1u) == RS_Replicate)
+            if (from_member(m.from) && rstate(m.from - 1u) == RS_Replicate)
               become_retry(m.from - 1u);
             return;
           case M_SnapshotStatus:  // raft.go:1758-1771
-            if (m.from >= 1 && m.from <= N && rstate(m.from - 1u) == RS_Snapshot) {
+            if (from_member(m.from) && rstate(m.from - 1u) == RS_Snapshot) {
               const u32 sl = m.from - 1u;
               if (m.reject) P.rem_snap[r * N + sl] = 0;  // clearPendingSnapshot
               become_retry(sl);                        // becomeWait
@@ -1400,7 +1513,7 @@ struct Lane {
             return;
           case M_Election: return;        // leader ignores Election
           case M_RequestVote: on_request_vote(m); return;
-          case M_ConfigChangeEvent:
+          case M_ConfigChangeEvent: on_config_change(m); return;
           case M_SnapshotReceived: set_fault(F_UNSUPPORTED); return;
           default: return;  // RateLimit: limiter disabled → dropped
         }
@@ -1510,6 +1623,37 @@ struct Lane {
     return true;
   }
 
+  // ------------------------------------------------------------- membership bookkeeping
+  // After the step's Update: without ext_apply the engine's state machine
+  // applies the CommittedEntries, and a ConfigChange among them goes back to
+  // raft at the node's next step (cc_apply; the last one of the range: raft
+  // allows one pending config change, and bootstrap's AddNodes are no-ops);
+  // MB_CC_IN_LOG is dropped once (processed, last] holds no ConfigChange.
+  RBE_HD void membership_after_update(const Upd& u) {
+    if (!C.ext_apply && u.apply_hi >= u.apply_lo) {
+      for (u64 i = u.apply_lo; i <= u.apply_hi; i++) {
+        if (last - i >= C.ring) break;  // F_WINDOW already raised by the apply
+        const Body b = P.pay_ring[ring_slot(i)];
+        if (ent_type(b.type) != E_ConfigChange) continue;
+        const u64 w = b.lo;
+        const u32 t = (u32)((w >> 48) & 0xFFu);
+        const u64 nid = w & 0xFFFFFFFFFFFFULL;
+        if (ent_heap(b.type) || b.len != 8 || (w >> 56) != 0xCCu || t > CC_AddWitness || nid > N) {
+          set_fault(F_UNSUPPORTED);  // not a ConfigChange the engine can decode
+          continue;
+        }
+        cc_apply = (u8)(CCA_VALID | (t << 3) | (u32)nid);
+      }
+    }
+    if (members & MB_CC_IN_LOG) {
+      bool any = false;
+      for (u64 i = processed + 1; i <= last && !any; i++)
+        if (last - i < C.ring && ent_type(P.pay_ring[ring_slot(i)].type) == E_ConfigChange)
+          any = true;
+      if (!any) members &= (u8)~MB_CC_IN_LOG;
+    }
+  }
+
   // ------------------------------------------------------------- node snapshots
   // After the step's Update (snapshot_entries > 0), in the node's order: a
   // snapshot restored from InstallSnapshot is the LogDB's (ApplySnapshot) and
@@ -1579,6 +1723,8 @@ struct Lane {
     ltt = c.ltt;
     rq_head = c.rq_head;
     rq_count = c.rq_count;
+    members = c.members;
+    cc_apply = c.cc_apply;
   }
   RBE_HD void store() {
     Hot h;
@@ -1607,7 +1753,9 @@ struct Lane {
     c.ltt = ltt;
     c.rq_head = rq_head;
     c.rq_count = rq_count;
-    c.pad[0] = c.pad[1] = c.pad[2] = 0;
+    c.members = members;
+    c.cc_apply = cc_apply;
+    c.pad = 0;
     c.t_last = t_last;
     c.lead_start = lead_start;
     P.core[r] = c;
@@ -1675,6 +1823,20 @@ struct Lane {
     // names, any role, with the ReadIndex ctx / proposal batch it carries.
     const u32 wl = role == R_Leader ? wl_input(C, cid, round) : 0u;
     bool do_read = wl == 2, do_prop = wl == 1;
+    // Peer.ProposeConfigChange of the round: the config-change schedule at the
+    // replica leading at round start (its membership before this step), or host
+    // input (EXT_CC_PROPOSE); the entry carries the stand-in Cmd (cc_word)
+    bool do_cc = false;
+    u32 cc_type = 0;
+    u64 cc_node = 0;
+    if (C.membership && C.cc_period && role == R_Leader && cc_selected(C, cid, round)) {
+      cc_node = cc_target(C, cid, round);
+      const bool v = voter((u32)cc_node - 1u);
+      if (!v || popc8(voters_mask()) > 2) {
+        do_cc = true;
+        cc_type = v ? CC_RemoveNode : CC_AddNode;
+      }
+    }
     u64 read_lo = 0, read_hi = 0;
     u32 prop_n = 0, xfer = C.xfer_period ? xfer_input(C, cid, round, k) : 0u;
     const Ent* prop_ents = nullptr;
@@ -1706,6 +1868,12 @@ struct Lane {
           snap_nodes = ext.snap_nodes;
           snap_reject = ext.snap_reject;
         }
+        if (ext.flags & EXT_CC_PROPOSE) {
+          do_cc = true;
+          cc_type = (u32)(ext.pad[0] & 0xFFu);
+          cc_node = ext.pad[0] >> 8;
+        }
+        if (ext.flags & EXT_CC_APPLY) cc_apply = (u8)ext.pad[1];
       }
     }
     if (pend0) {
@@ -1717,8 +1885,8 @@ struct Lane {
     if (!clk.tick) {
       // a round without a tick is a step only if handleEvents finds an event
       // (node.go:1030-1067): a message or notice, client input, an entry to apply
-      bool ev = do_read || do_prop || xfer || unreach || snap_nodes || ext_applied ||
-                (flags & (HF_APPLY_PENDING | HF_APPLIED_NEW));
+      bool ev = do_read || do_prop || xfer || unreach || snap_nodes || ext_applied || do_cc ||
+                cc_apply || (flags & (HF_APPLY_PENDING | HF_APPLIED_NEW));
       for (u32 s = 0; s < N; s++)
         if (s != k && in_word<N>(P, g, s, k, round) != 0) ev = true;
       if (!ev) return true;  // no step: no outbox header either
@@ -1746,7 +1914,12 @@ struct Lane {
     const u32 ppar = par ^ 1u;
     u32 cs = 0, ci = 0, cn = 0, cna = 0;  // inbox cursor: sender, index, count, #A
     bool copen = false;
-    u32 phase = (unreach | snap_nodes) ? 0u : (round > 0 ? 1u : 2u);
+    const u32 phase0 = (unreach | snap_nodes) ? 0u : (round > 0 ? 1u : 2u);
+    // a ConfigChange applied since the last step comes first: Peer.
+    // ApplyConfigChange / RejectConfigChange are direct calls under raftMu
+    // between two steps (node.go applyConfigChange; peer.go:138-157)
+    u32 phase = cc_apply ? 8u : phase0;
+    bool cc_proposed = false;
     u32 rep_bit = 0;  // local reports: next node bit
     rep_mask = 0;
     tn_to = 0;
@@ -1758,7 +1931,24 @@ struct Lane {
       u32 kind = 0;  // 0 none, 1 inbox message, 2 local message, 3 tick
       Msg m;
       const Ent* ents = nullptr;
-      if (phase == 0) {
+      if (phase == 8) {
+        phase = phase0;
+        const u8 a = cc_apply;
+        cc_apply = 0;
+        if (a & CCA_REJECT) {
+          m = mk(M_ConfigChangeEvent, self);
+          m.reject = 1;
+          kind = 2;
+        } else if ((a & 7u) == 0) {
+          flags &= (u8)~HF_PENDING_CC;  // ApplyConfigChange(NoNode): clearPendingConfigChange
+        } else {
+          m = mk(M_ConfigChangeEvent, self);
+          m.hint = a & 7u;
+          m.hint_high = (a >> 3) & 7u;
+          kind = 2;
+        }
+      }
+      if (kind == 0 && phase == 0) {
         // Peer.ReportUnreachableNode / ReportSnapshotStatus (peer.go:168-183)
 #pragma unroll 1
         while (rep_bit < 2 * N) {
@@ -1824,6 +2014,26 @@ struct Lane {
         phase = 4;
         if (clk.tick) kind = 3;
       }
+      if (kind == 0 && phase == 4 && do_cc && !cc_proposed) {
+        // handleConfigChangeMessage (node.go:1120-1142): recordActivity, then
+        // ProposeConfigChange (peer.go:126-135), one ConfigChange entry
+        cc_proposed = true;
+        q_record_activity(M_ConfigChangeEvent);
+        Ent e;
+        e.term = 0;
+        e.type = E_ConfigChange;
+        e.len = 8;
+        e.lo = cc_word(cc_type, cc_node);
+        e.hi = 0;
+        u32 off = 0;
+        if (arena_put(&e, 1, &off)) {
+          m = mk(M_Propose, 0);
+          m.from = self;
+          m.n_ent = 1;
+          ents = &P.arena[par][r * (u64)C.ecap + off];
+          kind = 2;
+        }
+      }
       if (kind == 0 && phase == 4) {
         phase = 5;
         if (do_prop) {
@@ -1873,6 +2083,7 @@ struct Lane {
           ctr.v[C_ACTIVE_TICKS]++;
         }
       } else {
+        bool deliver = true;
         if (kind == 1) {
           ctr.v[C_MSG_IN]++;
           ctr.v[C_ENT_IN] += m.n_ent;
@@ -1881,8 +2092,11 @@ struct Lane {
             q_record_activity(M_ReadIndex);
           else
             q_record_activity(m.type);
+          // Peer.Handle (peer.go:186-198): a response from a node that is not a
+          // member of this replica's view is dropped
+          if (C.membership && is_response_message(m.type) && !voter(m.from - 1u)) deliver = false;
         }
-        handle(m, ents);
+        if (deliver) handle(m, ents);
       }
       // deferred fan-out, in the reference's emission order
 #pragma unroll 1
@@ -1900,7 +2114,7 @@ struct Lane {
         hb_pending = false;
 #pragma unroll 1
         for (u32 s = 0; s < N; s++)
-          if (s != k) send_heartbeat(s, hb_lo, hb_hi);
+          if (s != k && voter(s)) send_heartbeat(s, hb_lo, hb_hi);
         ctr.v[C_REMOTE_TOUCH] += N - 1;
       }
       if (rq_pending) {
@@ -1972,6 +2186,7 @@ struct Lane {
     // after a restart, leave it): the node confirms it with the next Update
     if (u.apply_hi >= u.apply_lo && !C.ext_apply && u.apply_hi > applied0) flags |= HF_APPLIED_NEW;
     else flags &= (u8)~HF_APPLIED_NEW;
+    if (C.membership) membership_after_update(u);
     if (C.snapshot_entries) node_snapshot();
     if (fault) flags |= HF_FAULTED;
     if (role == R_Leader) {
@@ -2082,9 +2297,10 @@ RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   c.leader = 0;
   c.ltt = 0;
   c.rq_head = c.rq_count = 0;
-  c.pad[0] = c.pad[1] = c.pad[2] = 0;
+  c.members = c.cc_apply = c.pad = 0;
   c.t_last = 1;  // bootstrap entries are at term 1
   c.lead_start = 0;
+  if (C.membership) c.members = MB_CC_IN_LOG;  // the bootstrap ConfigChanges, applied in round 0
   P.core[r] = c;
   if (C.ext_commit) P.imark[r] = 1;  // inMemory.init(0), then bootstrap appends 1..N
   for (u32 s = 0; s < N; s++) {
@@ -2182,9 +2398,14 @@ RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, 
   c.leader = 0;
   c.ltt = 0;
   c.rq_head = c.rq_count = 0;
-  c.pad[0] = c.pad[1] = c.pad[2] = 0;
+  c.members = c.cc_apply = c.pad = 0;
   c.t_last = n ? t[n - 1] : (last == marker ? marker_term : 0);
   c.lead_start = 0;
+  // the restarted raft reads the group's members from the LogDB (the static
+  // group: every slot a voter, as oracle/harness.cpp harness_restart)
+  if (C.membership)
+    for (u32 i = 0; i < n; i++)
+      if (ent_type(b[i].type) == E_ConfigChange) c.members = MB_CC_IN_LOG;
   P.core[r] = c;
   if (C.ext_commit) P.imark[r] = last + 1;  // inMemory.init(lastIndex), inmemory.go:46-57
   for (u32 s = 0; s < N; s++) {  // becomeFollower → reset → resetRemotes (raft.go:1023-1031)
@@ -2233,6 +2454,7 @@ RBE_HD bool triage_lazy(const Planes& P, const Params& C, u64 r, const Clk& ck, 
   const u32 g = (u32)r / (u32)N;  // replica indices fit u32 (work lists hold u32)
   const u64 cid = C.cid_base + (u64)g * C.cid_stride;
   if ((ib & IB_LEAD) && wl_input(C, cid, round)) return false;
+  if ((ib & IB_LEAD) && C.cc_period && cc_selected(C, cid, round)) return false;
   if (C.xfer_period && xfer_input(C, cid, round, (u32)r - g * (u32)N)) return false;
   if (C.ext_inputs && P.ext[r].flags) return false;
   // a round without a tick and without input is no step at all (handleEvents
@@ -2258,6 +2480,7 @@ RBE_HD bool triage_lazy(const Planes& P, const Params& C, u64 r, const Clk& ck, 
 //   bits 1-3  leaders among the group's owned replicas (while asleep)
 RBE_HD bool group_forced(const Params& C, u64 cid, u32 round) {
   if (wl_input(C, cid, round)) return true;
+  if (C.cc_period && cc_selected(C, cid, round)) return true;
   if (C.xfer_period && round % C.xfer_period == 0)
     for (u32 k = 0; k < C.n; k++)
       if (xfer_input(C, cid, round, k)) return true;
@@ -2368,7 +2591,10 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, const Clk& ck
   const u64 cid = C.cid_base + g * C.cid_stride;
   const u32 cls = h.role == R_Leader ? T_LEAD : (h.role == R_Follower ? T_FOLL : T_FULL);
   if (nmsg || (h.flags & HF_APPLY_PENDING)) return cls;
-  if (C.ext_commit) return cls;  // the step may owe entries to save (Core is not read here)
+  if (C.ext_commit) return cls;
+  // a step after an apply may owe raft a ConfigChange (Core::cc_apply)
+  if (C.membership && (h.flags & HF_APPLIED_NEW)) return cls;
+  if (C.cc_period && h.role == R_Leader && cc_selected(C, cid, round)) return cls;  // the step may owe entries to save (Core is not read here)
   if (h.flags & HF_SNAP_WORK) return T_FULL;  // SnapshotStatus / compaction (node_snapshot)
   if (!ck.tick && (h.flags & HF_APPLIED_NEW)) return cls;
   if (h.role == R_Leader && wl_input(C, cid, round)) return cls;

@@ -53,6 +53,10 @@ enum : u32 {
   F_PANIC = 1u << 5,        // a reference panic condition (e.g. commitTo > lastIndex)
   F_UNSUPPORTED = 1u << 6,  // a slow-path message/entry type reached the device
   F_DROPLIST = 1u << 7,     // dropped-ReadIndex output list full
+  // not a fault: an observer or witness joined the replica's membership, which
+  // the device does not step; the host takes the group over (rbe_export_groups
+  // / its own slow path / rbe_import_groups).  The replica's view is unchanged.
+  F_HANDOFF = 1u << 8,
 };
 
 // hot plane: everything a quiesced tick touches (32 B per replica)
@@ -86,6 +90,15 @@ enum : u8 {
                         // step (snapshot_entries > 0): triage sends it to k_full
 };
 
+// Core::members / Core::cc_apply bits
+enum : u8 {
+  MB_REMOVED = 0x1F,   // slots that are not voting members
+  MB_CC_IN_LOG = 0x80,
+  CCA_VALID = 0x80, CCA_REJECT = 0x40,  // cc_apply: node id bits 0-2, ConfigChangeType bits 3-5
+};
+// pb.ConfigChangeType (raft.pb.go)
+enum : u32 { CC_AddNode = 0, CC_RemoveNode = 1, CC_AddObserver = 2, CC_AddWitness = 3 };
+
 // core plane (64 B per replica)
 struct alignas(16) Core {
   u64 term;
@@ -98,7 +111,14 @@ struct alignas(16) Core {
   u8 ltt;          // leaderTransferTarget
   u8 rq_head;      // readIndex queue ring head
   u8 rq_count;
-  u8 pad[3];
+  // membership (cfg.membership; all zero otherwise): bits 0-4 the slots that
+  // are not voting members of this replica's raft.remotes (the group starts
+  // with every slot a voter), MB_CC_IN_LOG a ConfigChange entry may sit in
+  // (processed, last_index]; cc_apply a ConfigChange for the next step
+  // (CCA_* bits: the state machine applied one, or the host sent it)
+  u8 members;
+  u8 cc_apply;
+  u8 pad;
   u64 t_last;      // term of entry last_index (log-tail cache)
   u64 lead_start;  // leader: index of its no-op, the first entry of its term (raft.go:985);
                    // entries [lead_start, last_index] have term == term, earlier ones less
@@ -231,6 +251,8 @@ struct DropRI {  // SystemCtx
 enum : u32 {
   EXT_PROPOSE = 1, EXT_READ = 2, EXT_XFER = 4, EXT_UNREACH = 8, EXT_SNAPST = 16,
   EXT_APPLIED = 32,  // rbe_notify_applied changed raft.applied (an event, node.go:1033)
+  EXT_CC_PROPOSE = 64,  // Peer.ProposeConfigChange: ExtIn::pad[0] = type | node id << 8
+  EXT_CC_APPLY = 128,   // Peer.ApplyConfigChange / RejectConfigChange: pad[1] = a cc_apply byte
 };
 struct alignas(16) ExtIn {
   u32 flags;
@@ -283,6 +305,8 @@ struct Params {
   u32 rep_rank;
   u32 ext_apply;      // applied index comes from rbe_notify_applied (raft.applied lags processed)
   u32 ext_commit;     // Peer.Commit's log part comes from rbe_commit (savedTo/processed lag)
+  u32 membership;     // ConfigChange entries on the device (Core::members / cc_apply)
+  u32 cc_period, cc_mod;  // config-change schedule (rbe_step.h cc_selected), 0 = off
   u32 snapshot_entries;     // config.SnapshotEntries: snapshot + compact every that many applied entries (0 = never)
   u32 compaction_overhead;  // config.CompactionOverhead: entries kept below the snapshot
   u32 in_cap;         // host-pushed proposal entries per step (Planes::in_ents)

@@ -45,7 +45,7 @@ class RbeConfig(C.Structure):
                 ("xfer_period", C.c_uint32), ("xfer_mod", C.c_uint32),
                 ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
                 ("heap_bytes", C.c_uint64), ("ext_commit", C.c_uint32),
-                ("reserved", C.c_uint32 * 3)]
+                ("membership", C.c_uint32), ("cc_period", C.c_uint32), ("cc_mod", C.c_uint32)]
 
 
 class RbeReplicaView(C.Structure):
@@ -60,7 +60,7 @@ class RbeReplicaView(C.Structure):
                 ("votes_resp", C.c_uint32), ("votes_granted", C.c_uint32),
                 ("match", C.c_uint64 * 8), ("next", C.c_uint64 * 8),
                 ("rstate", C.c_uint32 * 8), ("ractive", C.c_uint32 * 8),
-                ("events", C.c_uint32), ("pad", C.c_uint32)]
+                ("events", C.c_uint32), ("removed", C.c_uint32)]
 
 
 def _np_dtype(struct):
@@ -192,7 +192,8 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_xchg_chunk_bytes", "rbe_xchg_pack_fixed", "rbe_xchg_unpack_fixed",
            "rbe_xchg_status", "rbe_stream", "rbe_get_snapshot_state", "rbe_wire_encode",
            "rbe_wire_fetch", "rbe_wire_decode", "rbe_propose_entries", "rbe_commit",
-           "rbe_get_update_commits"]
+           "rbe_get_update_commits", "rbe_propose_config_change", "rbe_apply_config_change",
+           "rbe_reject_config_change"]
 KERNEL_SLOTS = 4
 
 _lib = None
@@ -233,6 +234,9 @@ def load_library(path: Optional[str] = None):
         "rbe_notify_applied": (i32, [vp, u64, P(u64), P(u64)]),
         "rbe_set_apply_ready": (i32, [vp, u64, P(u64), P(C.c_uint8)]),
         "rbe_commit": (i32, [vp, u64, P(u64), P(RbeUpdateCommit)]),
+        "rbe_propose_config_change": (i32, [vp, u64, P(u64), P(u32), P(u64)]),
+        "rbe_apply_config_change": (i32, [vp, u64, P(u64), P(u64), P(u32)]),
+        "rbe_reject_config_change": (i32, [vp, u64, P(u64)]),
         "rbe_get_update_commits": (i32, [vp, u64, u64, P(RbeUpdateCommit)]),
         "rbe_run": (i32, [vp, u32]),
         "rbe_sync": (i32, [vp]),
@@ -306,7 +310,8 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                 rep_rank: int = 0, ext_apply: bool = False, in_cap: int = 0,
                 xfer_period: int = 0, xfer_mod: int = 1, heap_bytes: int = 0,
                 snapshot_entries: int = 0, compaction_overhead: int = 0,
-                ext_commit: bool = False) -> RbeConfig:
+                ext_commit: bool = False, membership: bool = False, cc_period: int = 0,
+                cc_mod: int = 1) -> RbeConfig:
     return RbeConfig(abi_version=RBE_ABI_VERSION, device=device, n_groups=n_groups,
                      n_replicas=n_replicas, election_rtt=election_rtt,
                      heartbeat_rtt=heartbeat_rtt, check_quorum=int(check_quorum),
@@ -320,7 +325,8 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                      rep_world=rep_world, rep_rank=rep_rank, ext_apply=int(ext_apply),
                      in_cap=in_cap, xfer_period=xfer_period, xfer_mod=xfer_mod,
                      heap_bytes=heap_bytes, snapshot_entries=snapshot_entries,
-                     compaction_overhead=compaction_overhead, ext_commit=int(ext_commit))
+                     compaction_overhead=compaction_overhead, ext_commit=int(ext_commit),
+                     membership=int(membership), cc_period=cc_period, cc_mod=cc_mod)
 
 
 class InputError(EngineError):
@@ -489,6 +495,23 @@ class NodeInputs:
             blob += cmd
         buf = C.create_string_buffer(bytes(blob), max(1, len(blob)))
         _check_input(self._input("launch", n, _u64s(replicas), st, ea, buf), "rbe_launch")
+
+    def propose_config_change(self, replicas, types, nodes):
+        """Peer.ProposeConfigChange (rbe_propose_config_change; cfg.membership)."""
+        u32a = (C.c_uint32 * max(1, len(types)))(*types)
+        _check_input(self._input("propose_config_change", len(replicas), _u64s(replicas), u32a,
+                                 _u64s(nodes)), "rbe_propose_config_change")
+
+    def apply_config_change(self, replicas, nodes, types):
+        """Peer.ApplyConfigChange (rbe_apply_config_change; membership + ext_apply)."""
+        u32a = (C.c_uint32 * max(1, len(types)))(*types)
+        _check_input(self._input("apply_config_change", len(replicas), _u64s(replicas),
+                                 _u64s(nodes), u32a), "rbe_apply_config_change")
+
+    def reject_config_change(self, replicas):
+        """Peer.RejectConfigChange (rbe_reject_config_change)."""
+        _check_input(self._input("reject_config_change", len(replicas), _u64s(replicas)),
+                     "rbe_reject_config_change")
 
     def commit(self, replicas, ucs):
         """Peer.Commit's log part (rbe_commit; cfg.ext_commit): ucs[i] =

@@ -52,6 +52,11 @@ extern "C" {
 #define RBE_FAULT_PANIC 0x20u
 #define RBE_FAULT_UNSUPPORTED 0x40u
 #define RBE_FAULT_DROPLIST 0x80u
+/* not a protocol fault: an observer or witness joined the replica's membership
+ * (AddObserver / AddWitness), which the device does not step; the host takes
+ * the group over (rbe_export_groups, its own slow path, rbe_import_groups).
+ * rbe_fault_summary counts it apart from the faults. */
+#define RBE_FAULT_HANDOFF 0x100u
 
 /* counter slots (rbe_get_counters) */
 enum rbe_counter {
@@ -144,7 +149,17 @@ typedef struct rbe_config {
                                     in-memory log's applied marker) comes from rbe_commit,
                                     as the node sends it after SaveRaftState (needs
                                     ext_apply); 0 = every step commits its own Update */
-  uint32_t reserved[3];
+  /* membership change on the device (raft.go:1135-1237): ConfigChange entries
+   * (rbe_propose_config_change) add or remove voting members among the group's
+   * slots; the engine's own state machine applies committed ones (their Cmd in
+   * the engine's 8-byte form, cc_word in rbe_step.h) unless ext_apply, where
+   * the host does (rbe_apply_config_change); 0 = ConfigChange entries fault
+   * (RBE_FAULT_UNSUPPORTED) */
+  uint32_t membership;
+  uint32_t cc_period;        /* config-change schedule (remove / re-add a seeded voter at the
+                                leader every cc_period rounds in groups selected 1 in
+                                cc_mod; needs membership), 0 = off */
+  uint32_t cc_mod;
 } rbe_config;
 
 /* Snapshot of one replica (tests, debugging, rbe_get_views). */
@@ -156,7 +171,7 @@ typedef struct rbe_replica_view {
   uint64_t match[8], next[8];
   uint32_t rstate[8], ractive[8];
   uint32_t events;  /* RBE_EV_* of the last round's step (0 when it made no step) */
-  uint32_t pad;
+  uint32_t removed; /* bit (id-1): not a voting member in this replica's view (cfg.membership) */
 } rbe_replica_view;
 
 /* Per-replica step result: the Update of peer.go:201-207 / raftpb Update
@@ -352,6 +367,24 @@ int rbe_report_snapshot_status(rbe_engine* e, uint64_t n, const uint64_t* replic
 int rbe_notify_applied(rbe_engine* e, uint64_t n, const uint64_t* replica,
                        const uint64_t* applied);
 int rbe_set_apply_ready(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint8_t* ready);
+/* Membership change (cfg.membership; RBE_E_STATE otherwise), staged like every
+ * input above (one of each per replica per step):
+ *   rbe_propose_config_change: Peer.ProposeConfigChange (peer.go:126-135) at
+ *     replica[i]: a ConfigChange entry of type[i] (pb.ConfigChangeType:
+ *     0 AddNode, 1 RemoveNode, 2 AddObserver, 3 AddWitness) for node_id[i]
+ *     (1..n_replicas), proposed after the step's messages and tick, before its
+ *     proposals (node.go:1030-1067 handleConfigChangeMessage); a leader with a
+ *     config change pending drops it (DroppedEntries) for an empty entry.
+ *   rbe_apply_config_change: Peer.ApplyConfigChange (peer.go:138-149), what the
+ *     node calls once its state machine applied a committed ConfigChange
+ *     (node_id 0 = NoNode: clearPendingConfigChange only); applied before the
+ *     replica's next step.  Needs cfg.ext_apply (else the engine applies them).
+ *   rbe_reject_config_change: Peer.RejectConfigChange (peer.go:152-157). */
+int rbe_propose_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica,
+                              const uint32_t* type, const uint64_t* node_id);
+int rbe_apply_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica,
+                            const uint64_t* node_id, const uint32_t* type);
+int rbe_reject_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica);
 
 /* Results of the last round.  Replaces Peer.GetUpdate (peer.go:201-207).
  * Peer.Commit (peer.go:282-293) consumes a step's outputs at the step; its log
@@ -472,7 +505,8 @@ int rbe_get_counters(rbe_engine* e, uint64_t* out /* RBE_CTR_NUM */);
 /* the counters one pipeline kernel (RBE_KERNEL_*) contributed */
 int rbe_get_kernel_counters(rbe_engine* e, int32_t kernel, uint64_t* out /* RBE_CTR_NUM */);
 int rbe_reset_counters(rbe_engine* e);
-/* number of replicas whose sticky fault word is non-zero, and the OR of all */
+/* number of replicas whose sticky fault word holds a fault (RBE_FAULT_HANDOFF
+ * aside), and the OR of all words */
 int rbe_fault_summary(rbe_engine* e, uint64_t* n_faulty, uint32_t* fault_or);
 
 /* Replica-per-GPU mode (cfg.rep_world > 1).  The engine steps

@@ -45,6 +45,34 @@ u64 xfer_input(const HarnessConfig& c, u64 cid, u32 round, u32 k) {
   return below(splitmix64(h), c.n_replicas) + 1;
 }
 
+// config-change schedule (restated on device, rbe_step.h cc_selected/cc_target)
+bool cc_selected(const HarnessConfig& c, u64 cid, u32 round) {
+  if (!c.cc_period || round == 0 || round % c.cc_period != 0) return false;
+  const u64 epoch = round / c.cc_period;
+  return c.cc_mod <= 1 ||
+         below(splitmix64(c.seed ^ (cid * 0xE7037ED1A0B428DBULL) ^ (epoch << 28)), c.cc_mod) == 0;
+}
+u64 cc_target(const HarnessConfig& c, u64 cid, u32 round) {
+  const u64 epoch = round / c.cc_period;
+  return below(splitmix64(c.seed ^ (cid * 0x8EBC6AF09C88C6E3ULL) ^ (epoch << 20) ^ 0xCC),
+               c.n_replicas) + 1;
+}
+std::string cc_cmd(int type, u64 node_id) {
+  const u64 w = 0xCC00000000000000ULL | ((u64)(type & 0xFF) << 48) | (node_id & 0xFFFFFFFFFFFFULL);
+  std::string s(8, '\0');
+  for (int b = 0; b < 8; b++) s[b] = (char)((w >> (8 * b)) & 0xff);
+  return s;
+}
+bool cc_decode(const std::string& cmd, int* type, u64* node_id) {
+  if (cmd.size() != 8) return false;
+  u64 w = 0;
+  for (int b = 0; b < 8; b++) w |= (u64)(uint8_t)cmd[b] << (8 * b);
+  if ((w >> 56) != 0xCC) return false;
+  *type = (int)((w >> 48) & 0xFF);
+  *node_id = w & 0xFFFFFFFFFFFFULL;
+  return true;
+}
+
 bool iso_selected(const HarnessConfig& c, u64 cid, u32 epoch) {
   if (c.iso_mod <= 1) return true;
   return below(splitmix64(c.seed ^ (cid * 0x94D049BB133111EBULL) ^ ((u64)epoch << 40)),
@@ -73,6 +101,15 @@ struct Node {
   u64 ss_index = 0, ss_req = 0, compact_to = 0;
   u32 snap_pend = 0, snap_pend_reject = 0;  // SnapshotStatus of InstallSnapshots sent
   UpdateCommit uc;              // ext_commit: getUpdateCommit of the last step's Update
+  // a ConfigChange to apply to raft at the next step: applied by the state
+  // machine (membership, a committed stand-in entry) or sent by the host
+  bool cc_pend = false, cc_reject = false;
+  int cc_type = 0;
+  u64 cc_node = 0;
+  // host ProposeConfigChange for the next step (PUSH_CC_PROPOSE)
+  bool x_cc = false;
+  int x_cc_type = 0;
+  u64 x_cc_node = 0;
   std::vector<Message> in[8];   // this round's inbox, per sender slot (stream order)
   std::vector<Message> nxt[8];  // next round's inbox
   ~Node() { delete peer; }
@@ -238,6 +275,18 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
   // client input of this round: the workload goes to replicas that lead at
   // round start, host input (harness_push) to the replica it names
   const int wl = R->state == Leader ? wl_input(cfg, gr->cid, r) : 0;
+  // the config-change schedule proposes at the replica leading at round start
+  bool do_cc = nd->x_cc;
+  int cc_type = nd->x_cc_type;
+  u64 cc_node = nd->x_cc_node;
+  if (!do_cc && cfg.membership && R->state == Leader && cc_selected(cfg, gr->cid, r)) {
+    cc_node = cc_target(cfg, gr->cid, r);
+    const bool voter = R->remotes.count(cc_node) > 0;
+    if (!voter || R->remotes.size() > 2) {
+      do_cc = true;
+      cc_type = voter ? RemoveNode : AddNode;
+    }
+  }
   const bool do_read = wl == 2 || nd->x_read;
   const bool do_prop = wl == 1 || nd->x_prop;
   u64 xfer = nd->x_xfer ? nd->x_xfer : xfer_input(cfg, gr->cid, r, k);
@@ -250,13 +299,21 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
     // a round without a tick is a step only if handleEvents finds an event
     // (node.go:1030-1067)
     bool ev = do_read || do_prop || xfer || nd->x_unreach || nd->x_snap || nd->snap_pend ||
-              p->HasEntryToApply() || applied != nd->confirmedIndex;
+              p->HasEntryToApply() || applied != nd->confirmedIndex || do_cc || nd->cc_pend;
     for (u32 s = 0; s < n; s++) ev = ev || !nd->in[s].empty();
     if (!ev) return;
   }
   ctr[HC_STEPS]++;
   const Events ev0 = R->events;
   const u64 leader0 = R->leaderID;
+  // a ConfigChange the state machine applied (or the host sent) since the
+  // last step: Peer.ApplyConfigChange / RejectConfigChange (peer.go:138-157),
+  // direct calls under raftMu between two steps (node.go applyConfigChange)
+  if (nd->cc_pend) {
+    nd->cc_pend = false;
+    if (nd->cc_reject) p->RejectConfigChange();
+    else p->ApplyConfigChange(nd->cc_node, nd->cc_type);
+  }
   // handleEvents: updateBatchedLastApplied (node.go:1002-1006, 1032)
   p->NotifyRaftLastApplied(applied);
   const u64 committed0 = R->log.committed;
@@ -322,6 +379,12 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
       ctr[HC_ACTIVE_TICKS]++;
     }
   }
+  // handleConfigChangeMessage (node.go:1120-1142): recordActivity, then
+  // Peer.ProposeConfigChange with the marshaled ConfigChange (stand-in Cmd)
+  if (do_cc) {
+    nd->q.recordActivity(ConfigChangeEvent);
+    p->ProposeConfigChange(cc_cmd(cc_type, cc_node), 0);
+  }
   // handleProposals (node.go:1091-1106)
   if (do_prop) {
     if (nd->x_prop) {
@@ -337,6 +400,7 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
   // handleLeaderTransferRequest (node.go:1069-1075)
   if (xfer) p->RequestLeaderTransfer(xfer);
   nd->x_prop = nd->x_read = false;
+  nd->x_cc = false;
   nd->x_ents.clear();
   nd->x_xfer = 0;
   nd->x_unreach = nd->x_snap = nd->x_snap_reject = 0;
@@ -384,8 +448,20 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
       msgHash = hash_message(msgHash, m);
       nMsgs++;
     }
-    // applyRaftUpdates: the harness state machine applies immediately
-    for (auto& e : ud.committed_entries) applyHash = hash_entry(applyHash, e);
+    // applyRaftUpdates: the harness state machine applies immediately; a
+    // ConfigChange entry is handed back to raft at the next step (membership)
+    for (auto& e : ud.committed_entries) {
+      applyHash = hash_entry(applyHash, e);
+      int t;
+      u64 nid;
+      if (cfg.membership && !cfg.ext_apply && e.type == ConfigChangeEntry &&
+          cc_decode(e.cmd, &t, &nid)) {
+        nd->cc_pend = true;
+        nd->cc_reject = false;
+        nd->cc_type = t;
+        nd->cc_node = nid;
+      }
+    }
     ctr[HC_ENT_APPLIED] += ud.committed_entries.size();
     // (a state machine that recovered from a snapshot at a restart skips the
     // committed entries it already holds, rsm/statemachine.go)
@@ -571,6 +647,21 @@ int harness_push(Harness* h, int kind, u64 replica, u64 a, u64 b, const Entry* e
       return 0;
     case PUSH_APPLIED: nd->x_applied = a; return 0;
     case PUSH_APPLY_READY: nd->more_to_apply = a != 0; return 0;
+    case PUSH_CC_PROPOSE:
+      nd->x_cc = true;
+      nd->x_cc_type = (int)a;
+      nd->x_cc_node = b;
+      return 0;
+    case PUSH_CC_APPLY:
+      nd->cc_pend = true;
+      nd->cc_reject = false;
+      nd->cc_node = a;
+      nd->cc_type = (int)b;
+      return 0;
+    case PUSH_CC_REJECT:
+      nd->cc_pend = true;
+      nd->cc_reject = true;
+      return 0;
     default: return -1;
   }
 }
@@ -651,6 +742,29 @@ void harness_update_commit(const Harness* h, u64 replica, UpdateCommit* out) {
   *out = h->groups[replica / N]->nodes[replica % N]->uc;
 }
 
+u32 harness_inbox(const Harness* h, u64 replica, u32 sender, u64* out, u32 cap) {
+  const u32 N = h->cfg.n_replicas;
+  const auto& in = h->groups[replica / N]->nodes[replica % N]->in[sender];
+  u32 n = 0;
+  for (const Message& m : in) {
+    if (n < cap) {
+      u64* o = out + 10 * n;
+      o[0] = m.type;
+      o[1] = m.from;
+      o[2] = m.to;
+      o[3] = m.term;
+      o[4] = m.log_term;
+      o[5] = m.log_index;
+      o[6] = m.commit;
+      o[7] = m.reject ? 1 : 0;
+      o[8] = m.hint;
+      o[9] = m.entries.size();
+    }
+    n++;
+  }
+  return n;
+}
+
 void harness_commit(Harness* h, u64 replica, const UpdateCommit& uc) {
   const u32 N = h->cfg.n_replicas;
   h->groups[replica / N]->nodes[replica % N]->peer->raft->log.commitUpdate(uc);
@@ -691,6 +805,8 @@ void harness_views(const Harness* h, ReplicaView* out) {
       }
       v.votes_resp = resp;
       v.votes_granted = granted;
+      for (u32 s = 0; s < n; s++)
+        if (!R->remotes.count(s + 1)) v.removed |= 1u << s;
       v.events = nd->events;
       if (R->state == Leader) {
         for (auto& kv : R->remotes) {

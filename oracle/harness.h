@@ -75,11 +75,24 @@ struct HarnessConfig {
   // host-driven persistence: Peer.Commit's log part (entryLog.commitUpdate)
   // comes from harness_commit, the engine's rbe_commit (needs ext_apply)
   u32 ext_commit = 0;
+  // membership change (raft.go:1135-1237, peer.go:126-157): committed
+  // ConfigChange entries in the harness's stand-in encoding (cc_cmd) are
+  // applied to raft at the node's next step (ApplyConfigChange), unless the
+  // host applies them (ext_apply: PUSH_CC_APPLY / PUSH_CC_REJECT)
+  u32 membership = 0;
+  // config-change schedule: every cc_period-th round, in groups selected 1 in
+  // cc_mod, the replica leading at round start proposes removing a seeded
+  // voter (while more than two vote) or adding it back (cc_input)
+  u32 cc_period = 0;
+  u32 cc_mod = 1;
 };
 
 // host inputs for the next round (the engine's rbe_push_* / rbe_notify_applied)
 enum HarnessPush { PUSH_PROPOSE = 1, PUSH_READ = 2, PUSH_XFER = 3, PUSH_UNREACH = 4,
-                   PUSH_SNAPST = 5, PUSH_APPLIED = 6, PUSH_APPLY_READY = 7 };
+                   PUSH_SNAPST = 5, PUSH_APPLIED = 6, PUSH_APPLY_READY = 7,
+                   PUSH_CC_PROPOSE = 8,  // a = ConfigChangeType, b = node id (ProposeConfigChange)
+                   PUSH_CC_APPLY = 9,    // a = node id (0 = NoNode), b = type (ApplyConfigChange)
+                   PUSH_CC_REJECT = 10 };  // RejectConfigChange
 
 struct ReplicaView {  // mirrors rbe_replica_view in include/rbe.h
   u64 term, vote, leader_id, committed, last_index, processed, saved_to, digest;
@@ -88,7 +101,8 @@ struct ReplicaView {  // mirrors rbe_replica_view in include/rbe.h
   u32 raft_quiesce, rq_count, votes_resp, votes_granted;
   u64 match[8], next[8];
   u32 rstate[8], ractive[8];
-  u32 events, pad;  // EV_* bits of the last round's step (rbe_types.h)
+  u32 events;   // EV_* bits of the last round's step (rbe_types.h)
+  u32 removed;  // bit (id-1): not a voting member in this replica's view (raft.remotes)
 };
 
 // ------------------------------------------------------------ quiesce.go
@@ -171,6 +185,10 @@ void harness_restart(Harness* h, u64 replica);
 // host-chosen UpdateCommit (entryLog.commitUpdate, logentry.go:335-355)
 void harness_update_commit(const Harness* h, u64 replica, UpdateCommit* out);
 void harness_commit(Harness* h, u64 replica, const UpdateCommit& uc);
+// debugging: the messages replica `replica` receives from slot `sender` next
+// round (delivered by the last round), as 10 words each: type, from, to, term,
+// log_term, log_index, commit, reject, hint, number of entries; returns the count
+u32 harness_inbox(const Harness* h, u64 replica, u32 sender, u64* out, u32 cap);
 
 // shared helpers (restated independently in the engine)
 u64 wl_payload_lo(u64 seed, u64 cid, u64 round);
@@ -178,6 +196,12 @@ bool wl_group_active(const HarnessConfig& c, u64 cid);
 int wl_input(const HarnessConfig& c, u64 cid, u32 round);  // 0 none, 1 propose, 2 read
 bool iso_selected(const HarnessConfig& c, u64 cid, u32 epoch);
 u64 xfer_input(const HarnessConfig& c, u64 cid, u32 round, u32 k);  // 0 = none
+bool cc_selected(const HarnessConfig& c, u64 cid, u32 round);       // a cc_period round for cid
+u64 cc_target(const HarnessConfig& c, u64 cid, u32 round);          // its seeded node id
+// the stand-in ConfigChange Cmd the harness and the engine share: 8 bytes, LE
+// of 0xCC << 56 | type << 48 | node id (bootstrap's entries are type AddNode)
+std::string cc_cmd(int type, u64 node_id);
+bool cc_decode(const std::string& cmd, int* type, u64* node_id);
 inline u64 hfold(u64 h, u64 x) { return splitmix64(h ^ x); }
 
 }  // namespace orc

@@ -80,7 +80,8 @@ class OrcHarnessConfig(C.Structure):
                 ("cid_stride", C.c_uint64), ("xfer_period", C.c_uint32),
                 ("xfer_mod", C.c_uint32), ("ext_apply", C.c_uint32),
                 ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
-                ("ext_commit", C.c_uint32)]
+                ("ext_commit", C.c_uint32), ("membership", C.c_uint32),
+                ("cc_period", C.c_uint32), ("cc_mod", C.c_uint32), ("pad4", C.c_uint32)]
 
 
 class ReplicaView(C.Structure):
@@ -96,13 +97,16 @@ class ReplicaView(C.Structure):
                 ("votes_resp", C.c_uint32), ("votes_granted", C.c_uint32),
                 ("match", C.c_uint64 * 8), ("next", C.c_uint64 * 8),
                 ("rstate", C.c_uint32 * 8), ("ractive", C.c_uint32 * 8),
-                ("events", C.c_uint32), ("pad", C.c_uint32)]
+                ("events", C.c_uint32), ("removed", C.c_uint32)]
 
 
 VIEW_FIELDS = [f[0] for f in ReplicaView._fields_ if f[0] != "pad"]
 # harness_push kinds (oracle/harness.h HarnessPush)
 PUSH_PROPOSE, PUSH_READ, PUSH_XFER, PUSH_UNREACH, PUSH_SNAPST, PUSH_APPLIED, PUSH_APPLY_READY = \
     range(1, 8)
+PUSH_CC_PROPOSE, PUSH_CC_APPLY, PUSH_CC_REJECT = 8, 9, 10
+# pb.ConfigChangeType (raft.pb.go): AddNode, RemoveNode, AddObserver, AddWitness
+CC_ADD_NODE, CC_REMOVE_NODE, CC_ADD_OBSERVER, CC_ADD_WITNESS = 0, 1, 2, 3
 
 _lib = None
 
@@ -190,6 +194,7 @@ def lib():
             "orc_harness_restart": (i32, [vp, u64]),
             "orc_harness_update_commit": (None, [vp, u64, P(u64)]),
             "orc_harness_commit": (i32, [vp, u64, P(u64)]),
+            "orc_harness_inbox": (u32, [vp, u64, u32, P(u64), u32]),
             "orc_view_size": (i32, []),
             "orc_splitmix64": (u64, [u64]),
         }
@@ -900,7 +905,7 @@ class Harness:
                  wl_read_permille=0, iso_period=0, iso_len=0, iso_mod=10, trace=True,
                  threads=1, cid_stride=1, xfer_period=0, xfer_mod=1, ext_apply=False,
                  ext_inputs=False, snapshot_entries=0, compaction_overhead=0,
-                 ext_commit=False):
+                 ext_commit=False, membership=False, cc_period=0, cc_mod=1):
         c = OrcHarnessConfig(
             n_groups=n_groups, n_replicas=n_replicas, check_quorum=int(check_quorum),
             cid_base=cid_base, election_rtt=election_rtt, heartbeat_rtt=heartbeat_rtt,
@@ -911,7 +916,8 @@ class Harness:
             iso_mod=iso_mod, trace=int(trace), threads=threads, cid_stride=cid_stride,
             xfer_period=xfer_period, xfer_mod=xfer_mod, ext_apply=int(ext_apply),
             snapshot_entries=snapshot_entries, compaction_overhead=compaction_overhead,
-            ext_commit=int(ext_commit))
+            ext_commit=int(ext_commit), membership=int(membership), cc_period=cc_period,
+            cc_mod=cc_mod)
         self.n_groups, self.n_replicas = n_groups, n_replicas
         self.h = lib().orc_harness_create(C.byref(c))
         if not self.h:
@@ -988,6 +994,14 @@ class Harness:
         a = (C.c_uint64 * 6)(*uc)
         if lib().orc_harness_commit(self.h, replica, a) != 0:
             raise _err()
+
+    def inbox(self, replica, sender):
+        """Debugging: the messages `replica` receives from slot `sender` next
+        round, as (type, from, to, term, log_term, log_index, commit, reject,
+        hint, n_entries) tuples."""
+        o = (C.c_uint64 * 640)()
+        n = lib().orc_harness_inbox(self.h, replica, sender, o, 64)
+        return [tuple(o[10 * i:10 * i + 10]) for i in range(min(n, 64))]
 
     def restart(self, replica):
         """Restart a replica from its LogDB (the engine's rbe_launch)."""

@@ -48,6 +48,7 @@ typedef struct {
   uint64_t cid_stride;
   uint32_t xfer_period, xfer_mod, ext_apply, snapshot_entries;
   uint32_t compaction_overhead, ext_commit;
+  uint32_t membership, cc_period, cc_mod, pad4;
 } orc_harness_config;
 
 static thread_local std::string g_err;
@@ -828,6 +829,9 @@ void* orc_harness_create(const orc_harness_config* c) {
   h.snapshot_entries = c->snapshot_entries;
   h.compaction_overhead = c->compaction_overhead;
   h.ext_commit = c->ext_commit;
+  h.membership = c->membership;
+  h.cc_period = c->cc_period;
+  h.cc_mod = c->cc_mod ? c->cc_mod : 1;
   return harness_create(h);
   GUARD_END(nullptr)
 }
@@ -897,6 +901,10 @@ int orc_harness_commit(void* h, uint64_t replica, const uint64_t* uc6) {
   harness_commit((Harness*)h, replica, u);
   return 0;
   GUARD_END(-1)
+}
+uint32_t orc_harness_inbox(void* h, uint64_t replica, uint32_t sender, uint64_t* out,
+                           uint32_t cap) {
+  return harness_inbox((Harness*)h, replica, sender, out, cap);
 }
 int orc_harness_restart(void* h, uint64_t replica) {
   GUARD_BEGIN

@@ -1713,6 +1713,17 @@ void Peer::ProposeEntries(const std::vector<Entry>& ents) {  // peer.go:117-123
   raft->Handle(m);
 }
 
+void Peer::ProposeConfigChange(const std::string& data, u64 key) {  // peer.go:126-135
+  Message m;
+  m.type = Propose;
+  Entry e;
+  e.type = ConfigChangeEntry;
+  e.cmd = data;
+  e.key = key;
+  m.entries.push_back(e);
+  raft->Handle(m);
+}
+
 void Peer::ApplyConfigChange(u64 nodeID, int ccType) {  // peer.go:138-149
   if (nodeID == NoLeader) {
     raft->pendingConfigChange = false;

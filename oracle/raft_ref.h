@@ -536,6 +536,7 @@ struct Peer {
   void QuiescedTick();
   void RequestLeaderTransfer(u64 target);
   void ProposeEntries(const std::vector<Entry>& ents);
+  void ProposeConfigChange(const std::string& data, u64 key);  // data: the marshaled ConfigChange
   void ApplyConfigChange(u64 nodeID, int ccType);
   void RejectConfigChange();
   void RestoreRemotes(const Snapshot& ss);

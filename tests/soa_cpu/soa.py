@@ -81,6 +81,9 @@ def lib():
                 "notify_applied": [C.c_uint64, u64p, u64p],
                 "set_apply_ready": [C.c_uint64, u64p, P(C.c_uint8)],
                 "commit": [C.c_uint64, u64p, P(RbeUpdateCommit)],
+                "propose_config_change": [C.c_uint64, u64p, u32p, u64p],
+                "apply_config_change": [C.c_uint64, u64p, u64p, u32p],
+                "reject_config_change": [C.c_uint64, u64p],
                 "get_update_commits": [C.c_uint64, C.c_uint64, P(RbeUpdateCommit)],
                 "launch": [C.c_uint64, u64p, C.c_void_p, C.c_void_p, C.c_void_p]}.items():
             fn = getattr(L, "soa_" + name)

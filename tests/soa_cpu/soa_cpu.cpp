@@ -203,6 +203,9 @@ void* soa_create(const rbe_config* cfg) {
   C.ext_inputs = cfg->ext_inputs;
   C.ext_apply = cfg->ext_apply;
   C.ext_commit = cfg->ext_commit;
+  C.membership = cfg->membership;
+  C.cc_period = cfg->cc_period;
+  C.cc_mod = cfg->cc_mod ? cfg->cc_mod : 1;
   C.in_cap = cfg->in_cap ? cfg->in_cap : (u32)(cfg->n_groups > 1024 ? cfg->n_groups : 1024);
   C.xfer_period = cfg->xfer_period;
   C.xfer_mod = cfg->xfer_mod;
@@ -445,6 +448,24 @@ int soa_notify_applied(void* h, uint64_t n, const uint64_t* replica, const uint6
   if (!e->C.ext_apply) return RBE_E_STATE;
   return e->hin.notify_applied(n, replica, applied);
 }
+// membership inputs on the host build
+int soa_propose_config_change(void* h, uint64_t n, const uint64_t* replica, const uint32_t* type,
+                              const uint64_t* node) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (!e->C.membership || !e->C.ext_inputs) return RBE_E_STATE;
+  return e->hin.propose_config_change(n, replica, type, node);
+}
+int soa_apply_config_change(void* h, uint64_t n, const uint64_t* replica, const uint64_t* node,
+                            const uint32_t* type) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (!e->C.membership || !e->C.ext_apply) return RBE_E_STATE;
+  return e->hin.apply_config_change(n, replica, node, type, false);
+}
+int soa_reject_config_change(void* h, uint64_t n, const uint64_t* replica) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (!e->C.membership || !e->C.ext_inputs) return RBE_E_STATE;
+  return e->hin.apply_config_change(n, replica, nullptr, nullptr, true);
+}
 // rbe_commit / rbe_get_update_commits on the host build
 int soa_commit(void* h, uint64_t n, const uint64_t* replica, const rbe_update_commit* uc) {
   SoaEngine* e = (SoaEngine*)h;
@@ -577,8 +598,10 @@ void soa_views(void* h, rbe_replica_view* out) {
     v.votes_resp = hh.votes_resp;
     v.votes_granted = hh.votes_granted;
     v.events = (e->round > 0 && e->P.upd[i].round == e->round - 1) ? e->P.upd[i].events : 0u;
+    v.removed = c.members & MB_REMOVED;
     if (hh.role == R_Leader) {
       for (u32 s = 0; s < N && s < 8; s++) {
+        if ((v.removed >> s) & 1u) continue;  // not in raft.remotes
         v.match[s] = e->P.rem[i * N + s].match;
         v.next[s] = e->P.rem[i * N + s].next;
         v.rstate[s] = e->P.rem_st[i * N + s] & 3;
@@ -593,7 +616,7 @@ uint32_t soa_faults(void* h, uint64_t* n_faulty) {
   uint32_t o = 0;
   uint64_t n = 0;
   for (u64 i = 0; i < e->C.n_rep; i++) {
-    if (e->P.upd[i].fault) n++;
+    if (e->P.upd[i].fault & ~F_HANDOFF) n++;
     o |= e->P.upd[i].fault;
   }
   *n_faulty = n;
