@@ -66,6 +66,16 @@ WORKLOADS = {
             "CompactionOverhead=5, InstallSnapshot brings the isolated replicas back"),
     # groups per GPU; every rank holds the planes of all N x 500k groups and
     # steps the replicas it owns
+    # C4 driven from the host through the C ABI, as the node layer would drive
+    # it: every round the host stages the ReadIndex / proposal input of the
+    # active groups at their leaders (rbe_push_read_index / rbe_push_proposals)
+    # and reads back every replica's Update and the round's Messages /
+    # ReadyToReads (rbe_get_updates, rbe_collect_outputs); run_host_driven
+    "c4h": (dict(n_groups=1_000_000, n_replicas=3, quiesce=True, ext_inputs=True, ring=64,
+                 in_cap=200_000), 260,
+            "C4 host-driven: 1M groups x 3, Quiesce on, 10% active groups get a ReadIndex "
+            "(90%) or a 16 B proposal (10%) per round at their leader through rbe_push_*, "
+            "every Update and output read back through rbe_get_updates / rbe_collect_outputs"),
     "c5": (dict(n_groups=500_000, n_replicas=3, wl_enabled=True, wl_start_round=30, ring=64),
            60, "C5: 500k groups x 3 per GPU, replica-per-GPU (replica k of group g on rank "
                "(g+k) % N), steady replication, cross-rank messages by all-to-all each round"),
@@ -176,17 +186,22 @@ def alg_bytes(c):
     return sum(BYTES[k] * c[k] for k in BYTES)
 
 
-def load_traffic(name, kernel):
+def load_traffic(name, kernel, lib):
     """Measured HBM bytes per launch of `kernel` from the committed PMC summary
-    (profiles/traffic_<workload>.json, written by scripts/pmc_traffic.py), if any."""
+    (profiles/traffic_<workload>.json, written by scripts/pmc_traffic.py), only
+    when it was measured on this very library (same content hash); else None."""
     p = os.path.join(ROOT, "profiles", f"traffic_{name}.json")
     if not os.path.exists(p):
-        return None
+        return None, "no PMC summary"
     try:
         with open(p) as f:
-            return json.load(f).get("bytes_per_launch", {}).get(kernel)
-    except (OSError, ValueError, AttributeError):
-        return None
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, "unreadable PMC summary"
+    if d.get("library_sha256_16") != lib.get("sha256_16"):
+        return None, (f"PMC summary measured on library {d.get('library_sha256_16')}, "
+                      f"not this one ({lib.get('sha256_16')})")
+    return d.get("bytes_per_launch", {}).get(kernel), "same library"
 
 
 def run_replica_mode(args, ws, rank, local, dist, dev, gloo_staged):
@@ -313,6 +328,145 @@ def run_replica_mode(args, ws, rank, local, dist, dev, gloo_staged):
     eng.close()
 
 
+def run_host_driven(args, ws, rank, local, dist):
+    """c4h: the C4 round driven through the C ABI as dragonboat's node layer
+    drives Peer (node.go:1030-1067 handleEvents, 907-923 getUpdate,
+    execengine.go:474-560): each round (1) the ReadIndex / proposal input of
+    the active groups is staged at their leaders (rbe_push_read_index,
+    rbe_push_proposals with 16 B Cmds; leaders known from the last Updates),
+    (2) one rbe_step, (3) the Updates of the replicas that have one
+    (rbe_collect_updates, compacted on the device) and the round's Messages /
+    ReadyToReads (rbe_collect_outputs) come back to the host.
+    The timed region holds all three; the boundary's share (1 + 3) is reported
+    beside the device time (HIP events around the step)."""
+    import ctypes as C
+    import numpy as np
+    from dragonboat_amd.engine import (UPDATE_DTYPE, Engine, RbeOutputs, RbeUpdateList, _check,
+                                       footprint, make_config)
+    from dragonboat_amd.shard import reduce_results, shard_params
+
+    kw, settle, desc = WORKLOADS["c4h"]
+    kw = dict(kw)
+    if args.groups:
+        kw["n_groups"] = args.groups
+    n_groups, N = int(kw["n_groups"]), int(kw["n_replicas"])
+    n_rep = n_groups * N
+    cid_base, cid_stride = shard_params(rank, ws)
+    cfg = make_config(device=local, cid_base=cid_base, cid_stride=cid_stride, trace=False, **kw)
+    eng = Engine(cfg)
+    L, h = eng.lib, eng.h
+    rng = np.random.default_rng(7 + rank)
+    active = np.arange(0, n_groups, 10, dtype=np.uint64)  # 10% of the groups
+    ul = RbeUpdateList()
+    outs = RbeOutputs()
+    leader_of = np.zeros(n_groups, dtype=np.uint64)  # leader slot + 1 per group, 0 = none
+    cmd = np.frombuffer(rng.bytes(16 * len(active)), dtype=np.uint8).copy()
+    ptr = lambda a, t: a.ctypes.data_as(C.POINTER(t))  # noqa: E731
+    stats = {"push": 0.0, "step": 0.0, "out": 0.0, "reads": 0, "props": 0, "msgs": 0, "rtr": 0,
+             "upd": 0}
+
+    def read_back():
+        _check(L.rbe_collect_updates(h, 0, n_rep, C.byref(ul)), "rbe_collect_updates")
+        _check(L.rbe_collect_outputs(h, 0, n_rep, C.byref(outs)), "rbe_collect_outputs")
+        n = ul.n
+        if n:  # the engine's pinned buffers, read in place
+            rep = np.ctypeslib.as_array(ul.replica, shape=(n,))
+            ups = np.frombuffer((C.c_uint8 * (n * UPDATE_DTYPE.itemsize)).from_address(
+                C.addressof(ul.updates.contents)), dtype=UPDATE_DTYPE)
+            lid = ups["leader_id"]
+            known = lid != 0
+            leader_of[(rep[known] // np.uint64(N)).astype(np.int64)] = lid[known]
+        return outs.n_messages, outs.n_ready_to_reads, n
+
+    def one_round(rnd, timed):
+        t0 = time.perf_counter()
+        lg = leader_of[active.astype(np.int64)]
+        has = lg != 0
+        g = active[has]
+        reps = g * np.uint64(N) + (lg[has] - np.uint64(1))
+        is_read = rng.random(len(reps)) < 0.9
+        rr, pr = reps[is_read].copy(), reps[~is_read].copy()
+        if len(rr):
+            lo = (np.uint64(rnd + 1) << np.uint64(32)) | (rr + np.uint64(1))
+            hi = rr.copy()
+            _check(L.rbe_push_read_index(h, len(rr), ptr(rr, C.c_uint64), ptr(lo, C.c_uint64),
+                                         ptr(hi, C.c_uint64)), "rbe_push_read_index")
+        if len(pr):
+            one = np.ones(len(pr), dtype=np.uint32)
+            zero = np.zeros(len(pr), dtype=np.uint32)
+            ln = np.full(len(pr), 16, dtype=np.uint32)
+            _check(L.rbe_push_proposals(h, len(pr), ptr(pr, C.c_uint64), ptr(one, C.c_uint32),
+                                        ptr(zero, C.c_uint32), ptr(ln, C.c_uint32),
+                                        ptr(cmd, C.c_uint8)), "rbe_push_proposals")
+        t1 = time.perf_counter()
+        eng.step()
+        eng.sync()
+        t2 = time.perf_counter()
+        nm, nr, nu = read_back()
+        t3 = time.perf_counter()
+        if timed:
+            stats["push"] += t1 - t0
+            stats["step"] += t2 - t1
+            stats["out"] += t3 - t2
+            stats["reads"] += len(rr)
+            stats["props"] += len(pr)
+            stats["msgs"] += nm
+            stats["rtr"] += nr
+            stats["upd"] += nu
+
+    for r in range(settle + max(1, args.warmup)):
+        if r < settle:
+            eng.step()
+            if r == settle - 1:
+                eng.sync()
+                read_back()
+        else:
+            one_round(r, False)
+    eng.sync()
+    eng.reset_counters()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for r in range(args.steps):
+        one_round(settle + args.warmup + r, True)
+    eng.sync()
+    if dist is not None:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    c = eng.counters()
+    nf, fo = eng.fault_summary()
+    wall_max, (steps, committed, reads) = reduce_results(
+        dist, wall, [c["steps"], c["committed"], c["reads_confirmed"]])
+    K = args.steps
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": steps / wall_max, "unit": "group-steps/s", "n_gpus": ws,
+            "steps": K, "warmup": args.warmup, "ms_per_step": wall_max * 1e3 / K,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic",
+            "config": {"workload": desc, "groups_per_gpu": n_groups, "replicas_per_group": N,
+                       "total_groups": n_groups * ws, "parallelism": f"group-per-GPU x{ws}",
+                       "election_rtt": 10, "heartbeat_rtt": 1, "settle_rounds": settle,
+                       "device_bytes_per_gpu": footprint(cfg)},
+            "committed_entries_per_s": committed / wall_max,
+            "read_confirmations_per_s": reads / wall_max,
+            "faulty_replicas": int(nf), "fault_bits_rank0": fo,
+            "boundary": {
+                "push_ms_per_round": stats["push"] * 1e3 / K,
+                "step_ms_per_round": stats["step"] * 1e3 / K,
+                "outputs_ms_per_round": stats["out"] * 1e3 / K,
+                "boundary_share": (stats["push"] + stats["out"]) / max(1e-12, wall),
+                "reads_pushed_per_round": stats["reads"] / K,
+                "proposals_pushed_per_round": stats["props"] / K,
+                "messages_read_per_round": stats["msgs"] / K,
+                "ready_to_reads_per_round": stats["rtr"] / K,
+                "updates_read_per_round": stats["upd"] / K,
+            },
+            "library": lib_identity(),
+        }), flush=True)
+    eng.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -348,6 +502,11 @@ def main():
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
     dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+    if args.workload == "c4h":
+        run_host_driven(args, ws, rank, local, dist if use_dist else None)
+        if use_dist:
+            dist.destroy_process_group()
+        return
     if args.workload == "c5":
         run_replica_mode(args, ws, rank, local, dist, dev, gloo_staged)
         if use_dist:
@@ -411,7 +570,8 @@ def main():
         kernels.append({"kernel": name, "avg_us": us, "alg_bytes_per_launch": b,
                         "achieved_gbs": (b / (us * 1e-6) / 1e9) if us > 0 else 0.0})
     dom = max(kernels, key=lambda k: k["avg_us"])
-    traffic = load_traffic(args.workload, dom["kernel"])
+    lib = lib_identity()
+    traffic, traffic_src = load_traffic(args.workload, dom["kernel"], lib)
 
     if rank == 0:
         out = {
@@ -448,6 +608,7 @@ def main():
                 "unit": "GB/s",
                 "frac": dom["achieved_gbs"] / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": dom["kernel"],
                 "alg_bytes_per_launch": dom["alg_bytes_per_launch"],
                 "avg_launch_us": dom["avg_us"],
@@ -461,7 +622,7 @@ def main():
                 "kernels": kernels,
             },
         }
-        out["library"] = lib_identity()
+        out["library"] = lib
         if not args.no_cpu_baseline and ws == 1:
             try:
                 ng = int(kw["n_groups"])

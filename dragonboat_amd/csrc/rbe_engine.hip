@@ -76,6 +76,16 @@ __global__ __launch_bounds__(kBlock) void k_ext_scatter(Planes P, u32 nrep, cons
                   cr[i].last_applied);
 }
 
+// ---- batched Updates (rbe_collect_updates): flag → scan → write
+__device__ __forceinline__ bool upd_of(const Planes& P, u64 r, u32 round, rbe_update* u) {
+  update_view(P.upd[r], P.core[r], P.hot[r], round, *u);
+  return (u->flags & RBE_UF_HAS_UPDATE) != 0;
+}
+__global__ __launch_bounds__(kBlock) void k_upd_count(Planes P, u64 first, u64 count, u32 round,
+                                                      u32* bsum);
+__global__ __launch_bounds__(kBlock) void k_upd_write(Planes P, u64 first, u64 count, u32 round,
+                                                      const u64* pre, u64* rep, rbe_update* ou);
+
 // ---- batched outputs (rbe_collect_outputs): count → scan → write
 // Exclusive prefix of v over the 256 lanes of a block; *total = the sum.
 __device__ __forceinline__ u32 block_excl_scan(u32 v, u32* total) {
@@ -200,6 +210,30 @@ __global__ __launch_bounds__(kBlock) void k_out_write(Planes P, Params C, u64 fi
     o.ctx_high = x.high;
     orr[br + j] = o;
   }
+}
+
+__global__ __launch_bounds__(kBlock) void k_upd_count(Planes P, u64 first, u64 count, u32 round,
+                                                      u32* bsum) {
+  const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+  rbe_update u;
+  const u32 f = i < count && upd_of(P, first + i, round, &u) ? 1u : 0u;
+  u32 t;
+  block_excl_scan(f, &t);
+  if (threadIdx.x == 0) {
+    bsum[2 * blockIdx.x] = t;
+    bsum[2 * blockIdx.x + 1] = 0;
+  }
+}
+__global__ __launch_bounds__(kBlock) void k_upd_write(Planes P, u64 first, u64 count, u32 round,
+                                                      const u64* pre, u64* rep, rbe_update* ou) {
+  const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+  rbe_update u;
+  const u32 f = i < count && upd_of(P, first + i, round, &u) ? 1u : 0u;
+  u32 t;
+  const u64 at = pre[2 * blockIdx.x] + block_excl_scan(f, &t);
+  if (!f) return;
+  rep[at] = first + i;
+  ou[at] = u;
 }
 
 // rbe_launch: one lane per relaunched replica (rbe_step.h relaunch_replica)
@@ -351,6 +385,11 @@ struct rbe_engine {
   u64 out_dev_bytes = 0;
   u8* out_host = nullptr;
   u64 out_host_bytes = 0;
+  // rbe_collect_updates: the same for the compacted Updates
+  u8* upd_dev = nullptr;
+  u64 upd_dev_bytes = 0;
+  u8* upd_host = nullptr;
+  u64 upd_host_bytes = 0;
   // rbe_wire_encode / rbe_wire_decode scratch
   u8* wire_dev = nullptr;    // the last rbe_wire_encode's frames (rbe_wire_fetch)
   u64 wire_dev_bytes = 0;
@@ -647,6 +686,8 @@ int rbe_destroy(rbe_engine* e) {
   if (e->in_dev) HIP_IGNORE(hipFree(e->in_dev));
   if (e->out_dev) HIP_IGNORE(hipFree(e->out_dev));
   if (e->out_host) HIP_IGNORE(hipHostFree(e->out_host));
+  if (e->upd_dev) HIP_IGNORE(hipFree(e->upd_dev));
+  if (e->upd_host) HIP_IGNORE(hipHostFree(e->upd_host));
   if (e->wire_dev) HIP_IGNORE(hipFree(e->wire_dev));
   if (e->wire_meta) HIP_IGNORE(hipFree(e->wire_meta));
   if (e->wire_rec) HIP_IGNORE(hipFree(e->wire_rec));
@@ -1626,6 +1667,52 @@ int rbe_collect_outputs(rbe_engine* e, uint64_t first, uint64_t count, rbe_outpu
   out->rtr_off = (const uint64_t*)(h + (o_roff - o_moff));
   out->messages = (const rbe_message*)(h + (o_rec - o_moff));
   out->ready_to_reads = (const rbe_ready_to_read*)(h + (o_rtr - o_moff));
+  return RBE_OK;
+}
+
+int rbe_collect_updates(rbe_engine* e, uint64_t first, uint64_t count, rbe_update_list* out) {
+  if (!e || !out || count == 0 || first >= e->C.n_rep || count > e->C.n_rep - first)
+    return RBE_E_INVALID;
+  memset(out, 0, sizeof(*out));
+  out->first = first;
+  out->count = count;
+  if (e->round == 0) return RBE_E_STATE;
+  HIP_OK(hipSetDevice(e->device));
+  const u32 nb = grid_for(count);
+  auto al = [](u64 x) { return (x + 255) & ~255ull; };
+  // device scratch: block sums (pairs) | block prefixes (+ totals) | replicas | records
+  const u64 o_pre = al(2ull * nb * sizeof(u32)), o_rep = o_pre + al((2ull * nb + 2) * sizeof(u64));
+  int rc = grow(&e->upd_dev, &e->upd_dev_bytes, o_rep, false);
+  if (rc) return rc;
+  u64* pre = (u64*)(e->upd_dev + o_pre);
+  hipLaunchKernelGGL(k_upd_count, dim3(nb), dim3(kBlock), 0, e->stream, e->P, (u64)first,
+                     (u64)count, e->round, (u32*)e->upd_dev);
+  hipLaunchKernelGGL(k_out_scan, dim3(1), dim3(kBlock), 0, e->stream, (const u32*)e->upd_dev, nb,
+                     pre);
+  HIP_OK(hipGetLastError());
+  u64 tot[2];
+  HIP_OK(hipMemcpyAsync(tot, pre + 2ull * nb, sizeof(tot), hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  const u64 o_rec = o_rep + al(tot[0] * sizeof(u64)), need = o_rec + al(tot[0] * sizeof(rbe_update));
+  if (need > e->upd_dev_bytes) {  // keep the block prefixes across the regrow
+    std::vector<u64> keep(2ull * nb + 2);
+    HIP_OK(hipMemcpy(keep.data(), pre, keep.size() * sizeof(u64), hipMemcpyDeviceToHost));
+    if ((rc = grow(&e->upd_dev, &e->upd_dev_bytes, need, false))) return rc;
+    pre = (u64*)(e->upd_dev + o_pre);
+    HIP_OK(hipMemcpy(pre, keep.data(), keep.size() * sizeof(u64), hipMemcpyHostToDevice));
+  }
+  u8* d = e->upd_dev;
+  hipLaunchKernelGGL(k_upd_write, dim3(nb), dim3(kBlock), 0, e->stream, e->P, (u64)first,
+                     (u64)count, e->round, (const u64*)(d + o_pre), (u64*)(d + o_rep),
+                     (rbe_update*)(d + o_rec));
+  HIP_OK(hipGetLastError());
+  if ((rc = grow(&e->upd_host, &e->upd_host_bytes, need - o_rep, true))) return rc;
+  if (need > o_rep)
+    HIP_OK(hipMemcpyAsync(e->upd_host, d + o_rep, need - o_rep, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  out->n = tot[0];
+  out->replica = (const uint64_t*)e->upd_host;
+  out->updates = (const rbe_update*)(e->upd_host + (o_rec - o_rep));
   return RBE_OK;
 }
 

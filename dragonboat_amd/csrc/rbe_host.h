@@ -189,8 +189,8 @@ RBE_HD void apply_pair(const Planes& P, u64 rep, u64 val) {
 // The rbe_update of replica r after round `round` - 1 from its Upd, Core and
 // Hot rows (rbe_get_updates).  A replica that made no Update-writing step in
 // that round (an idle round finished in triage) has an empty Update.
-inline void update_view(const Upd& d, const Core& c, const Hot& h, u32 round, rbe_update& u) {
-  memset(&u, 0, sizeof(u));
+RBE_HD void update_view(const Upd& d, const Core& c, const Hot& h, u32 round, rbe_update& u) {
+  u = rbe_update{};
   u.term = c.term;
   u.vote = c.vote;
   u.commit = c.committed;

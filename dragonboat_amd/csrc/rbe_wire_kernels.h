@@ -304,7 +304,11 @@ __global__ __launch_bounds__(256) void k_wire_verify(const u8* data, WireIn* fr)
     hb[10] = hb[11] = hb[12] = hb[13] = 0;
     const u32 pc = ((u32)hb[14] << 24) | ((u32)hb[15] << 16) | ((u32)hb[16] << 8) | hb[17];
     u32 st = 0;
+    // requestHeader.decode (tcp.go:93-112): the header crc, then the method —
+    // a MessageBatch frame is raftType (100); snapshotType frames carry chunks
+    const u32 method = ((u32)hb[0] << 8) | hb[1];
     if (crc32_update(0, hb, 18, s_table) != inc) st = 1;
+    else if (method != 100u) st = 3;
     else if (pc != c) st = 2;
     fr[blockIdx.x].status = st;
   }

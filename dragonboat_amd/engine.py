@@ -174,7 +174,13 @@ def wire_config(deployment_id=0, bin_ver=0, groups_per_batch=0, source_address=(
     return wc
 
 
+class RbeUpdateList(C.Structure):
+    _fields_ = [("first", C.c_uint64), ("count", C.c_uint64), ("n", C.c_uint64),
+                ("replica", C.POINTER(C.c_uint64)), ("updates", C.POINTER(RbeUpdate))]
+
+
 MESSAGE_DTYPE = _np_dtype(RbeMessage)
+UPDATE_DTYPE = _np_dtype(RbeUpdate)
 RTR_DTYPE = _np_dtype(RbeReadyToRead)
 
 
@@ -188,7 +194,7 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_footprint", "rbe_profile_rounds", "rbe_get_kernel_counters", "rbe_kernel_name",
            "rbe_xchg_record_bytes", "rbe_xchg_pack", "rbe_xchg_unpack", "rbe_get_outbox",
            "rbe_push_messages", "rbe_snapshot_bytes", "rbe_export_groups", "rbe_import_groups",
-           "rbe_get_entry_cmds", "rbe_set_apply_ready", "rbe_collect_outputs", "rbe_launch",
+           "rbe_get_entry_cmds", "rbe_set_apply_ready", "rbe_collect_outputs", "rbe_collect_updates", "rbe_launch",
            "rbe_xchg_chunk_bytes", "rbe_xchg_pack_fixed", "rbe_xchg_unpack_fixed",
            "rbe_xchg_status", "rbe_stream", "rbe_get_snapshot_state", "rbe_wire_encode",
            "rbe_wire_fetch", "rbe_wire_decode", "rbe_propose_entries", "rbe_commit",
@@ -246,6 +252,7 @@ def load_library(path: Optional[str] = None):
         "rbe_propose_entries": (i32, [vp, u64, P(u64), P(u32), P(RbeEntry), P(C.c_uint8)]),
         "rbe_push_read_index": (i32, [vp, u64, P(u64), P(u64), P(u64)]),
         "rbe_get_updates": (i32, [vp, u64, u64, P(RbeUpdate)]),
+        "rbe_collect_updates": (i32, [vp, u64, u64, P(RbeUpdateList)]),
         "rbe_get_messages": (i32, [vp, u64, P(RbeMessage), u32, P(u32)]),
         "rbe_get_outbox": (i32, [vp, u64, P(RbeMessage), u32, P(u32), P(RbeEntry), u32, P(u32),
                                  vp, u64, P(u64)]),
@@ -746,6 +753,21 @@ class Engine(NodeInputs):
         arr = (RbeUpdate * count)()
         _check(self.lib.rbe_get_updates(self.h, first, count, arr), "rbe_get_updates")
         return arr
+
+    def collect_updates(self, first: int = 0, count: Optional[int] = None):
+        """rbe_collect_updates: (replica ids, Updates) of the replicas in
+        [first, first + count) that have an Update, as numpy arrays (copies of
+        the engine's pinned buffer)."""
+        count = self.n_rep - first if count is None else count
+        o = RbeUpdateList()
+        _check(self.lib.rbe_collect_updates(self.h, first, count, C.byref(o)),
+               "rbe_collect_updates")
+        if o.n == 0:
+            return np.zeros(0, np.uint64), np.zeros(0, UPDATE_DTYPE)
+        rep = np.frombuffer(C.string_at(C.cast(o.replica, C.c_void_p), o.n * 8), np.uint64)
+        ups = np.frombuffer(C.string_at(C.cast(o.updates, C.c_void_p),
+                                        o.n * UPDATE_DTYPE.itemsize), UPDATE_DTYPE)
+        return rep.copy(), ups.copy()
 
     def update_commits(self, first: int = 0, count: Optional[int] = None):
         """getUpdateCommit of the last round's Updates (rbe_get_update_commits)

@@ -501,6 +501,19 @@ typedef struct rbe_outputs {
   const rbe_ready_to_read* ready_to_reads;
 } rbe_outputs;
 int rbe_collect_outputs(rbe_engine* e, uint64_t first, uint64_t count, rbe_outputs* out);
+/* The last round's Updates of replicas [first, first + count) that have one
+ * (RBE_UF_HAS_UPDATE: Peer.HasUpdate, peer.go:253-280), compacted on the
+ * device and copied once into an engine-owned pinned buffer: replica[i]'s
+ * Update is updates[i], replicas ascending.  This is the node loop's read of
+ * the Updates of the nodes that have one (execengine.go:494-560; a quiesced
+ * node without events has none).  Valid until the next rbe_collect_updates,
+ * rbe_step/rbe_run or rbe_destroy. */
+typedef struct rbe_update_list {
+  uint64_t first, count, n;
+  const uint64_t* replica;
+  const rbe_update* updates;
+} rbe_update_list;
+int rbe_collect_updates(rbe_engine* e, uint64_t first, uint64_t count, rbe_update_list* out);
 int rbe_get_counters(rbe_engine* e, uint64_t* out /* RBE_CTR_NUM */);
 /* the counters one pipeline kernel (RBE_KERNEL_*) contributed */
 int rbe_get_kernel_counters(rbe_engine* e, int32_t kernel, uint64_t* out /* RBE_CTR_NUM */);

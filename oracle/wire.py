@@ -27,8 +27,8 @@ reference-produced bytes (no Go toolchain here).
 from __future__ import annotations
 
 MAGIC = b"\xAE\x7D"
-RAFT_TYPE = 100          # tcp.go:58 raftType
-HEADER_SIZE = 18         # tcp.go:57 requestHeaderSize
+RAFT_TYPE = 100          # tcp.go:61 raftType
+HEADER_SIZE = 18         # tcp.go:60 requestHeaderSize
 INSTALL_SNAPSHOT = 16    # raftpb MessageType (raft.pb.go:23-51)
 
 # ------------------------------------------------------------------ crc32 (IEEE)
@@ -199,12 +199,16 @@ def _field_varint(out: bytearray, tag: int, x: int):
     put_varint(out, x)
 
 
-def snapshot_bytes(index: int = 0, term: int = 0) -> bytes:
-    """Snapshot.MarshalTo (raft.pb.go:2140-2217) with no file, membership,
-    checksum or flags: the Snapshot every non-InstallSnapshot message embeds."""
+def snapshot_bytes(index: int = 0, term: int = 0, filepath: str = "", file_size: int = 0) -> bytes:
+    """Snapshot.MarshalTo (raft.pb.go:2140-2217) with no membership, checksum
+    or flags: the Snapshot every non-InstallSnapshot message embeds (empty), or
+    getMaxSizedMsg's (raftpb/raft_test.go:319-346: path, size, index, term)."""
     out = bytearray()
-    _field_varint(out, 0x12, 0)      # Filepath ""
-    _field_varint(out, 0x18, 0)      # FileSize
+    fp = filepath.encode()
+    out.append(0x12)                 # Filepath
+    put_varint(out, len(fp))
+    out += fp
+    _field_varint(out, 0x18, file_size)  # FileSize
     _field_varint(out, 0x20, index)  # Index
     _field_varint(out, 0x28, term)   # Term
     out += b"\x32\x02\x08\x00"      # Membership{ConfigChangeId: 0}
@@ -217,8 +221,9 @@ def snapshot_bytes(index: int = 0, term: int = 0) -> bytes:
     return bytes(out)
 
 
-def message_bytes(m: dict, entries: list) -> bytes:
-    """Message.MarshalTo (raft.pb.go:2230-2294)."""
+def message_bytes(m: dict, entries: list, snapshot: bytes = None) -> bytes:
+    """Message.MarshalTo (raft.pb.go:2230-2294); `snapshot` the marshaled
+    Snapshot field (default: the empty one)."""
     out = bytearray()
     _field_varint(out, 0x08, m["type"])
     _field_varint(out, 0x10, m["to"])
@@ -235,7 +240,7 @@ def message_bytes(m: dict, entries: list) -> bytes:
         out.append(0x5A)
         put_varint(out, len(eb))
         out += eb
-    sb = snapshot_bytes()
+    sb = snapshot_bytes() if snapshot is None else snapshot
     out.append(0x62)
     put_varint(out, len(sb))
     out += sb
@@ -260,14 +265,60 @@ def batch_bytes(msgs: list, deployment_id: int, source_address: str, bin_ver: in
     return bytes(out)
 
 
+SNAPSHOT_TYPE = 200      # tcp.go:62 snapshotType
+
+
+def request_header_encode(method: int, size: int, crc: int) -> bytes:
+    """requestHeader.encode (tcp.go:80-91): method, size, a zero crc slot, the
+    payload crc; then the IEEE crc32 of those 18 bytes goes into the slot."""
+    h = bytearray(HEADER_SIZE)
+    h[0:2] = method.to_bytes(2, "big")
+    h[2:10] = size.to_bytes(8, "big")
+    h[14:18] = crc.to_bytes(4, "big")
+    h[10:14] = crc32(bytes(h)).to_bytes(4, "big")
+    return bytes(h)
+
+
+def request_header_decode(buf: bytes):
+    """requestHeader.decode (tcp.go:93-112): None when the header crc fails or
+    the method is neither raftType nor snapshotType, else (method, size, crc)."""
+    if len(buf) < HEADER_SIZE:
+        return None
+    h = bytearray(buf[:HEADER_SIZE])
+    inc = int.from_bytes(h[10:14], "big")
+    h[10:14] = b"\0\0\0\0"
+    if crc32(bytes(h)) != inc:
+        return None
+    method = int.from_bytes(h[0:2], "big")
+    if method not in (RAFT_TYPE, SNAPSHOT_TYPE):
+        return None
+    return method, int.from_bytes(h[2:10], "big"), int.from_bytes(h[14:18], "big")
+
+
 def frame(payload: bytes) -> bytes:
     """writeMessage (tcp.go:149-185): magic, requestHeader.encode (80-91), payload."""
-    h = bytearray(HEADER_SIZE)
-    h[0:2] = RAFT_TYPE.to_bytes(2, "big")
-    h[2:10] = len(payload).to_bytes(8, "big")
-    h[14:18] = crc32(payload).to_bytes(4, "big")
-    h[10:14] = crc32(bytes(h)).to_bytes(4, "big")
-    return MAGIC + bytes(h) + payload
+    return MAGIC + request_header_encode(RAFT_TYPE, len(payload), crc32(payload)) + payload
+
+
+# ------------------------------------------------------------------ size bounds
+ENTRY_NON_CMD_FIELDS_SIZE = 16 * 8  # settings.EntryNonCmdFieldsSize (soft.go:20)
+
+
+def entry_size_upper_limit(cmd_len: int) -> int:
+    """Entry.SizeUpperLimit (raft_optimized.go:71-76)."""
+    return ENTRY_NON_CMD_FIELDS_SIZE + cmd_len
+
+
+def message_size_upper_limit(entry_cmd_lens: list, snapshot: bytes = None) -> int:
+    """Message.SizeUpperLimit (raft_optimized.go:1204-1216): 16 x 12 for the
+    scalar fields, the Snapshot's own size, 16 + the bound of every entry."""
+    sb = snapshot_bytes() if snapshot is None else snapshot
+    return 16 * 12 + len(sb) + sum(16 + entry_size_upper_limit(n) for n in entry_cmd_lens)
+
+
+def batch_size_upper_limit(source_address: str, message_bounds: list) -> int:
+    """MessageBatch.SizeUpperLimit (raft_optimized.go:1218-1227)."""
+    return 16 * 3 + len(source_address) + sum(16 + b for b in message_bounds)
 
 
 def _take(buf: bytes, i: int, n: int) -> int:

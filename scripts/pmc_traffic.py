@@ -58,8 +58,13 @@ def main():
     w, fdir, wdir = sys.argv[1:4]
     fetch = per_kernel(fdir, "FETCH_SIZE")
     write = per_kernel(wdir, "WRITE_SIZE")
+    import hashlib
+    lib = os.environ.get("RBE_LIB") or os.path.join(ROOT, "dragonboat_amd", "libdragonboat_amd.so")
+    with open(lib, "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    # bench.py reports this traffic only for the same library (content hash)
     res = {"workload": w, "unit": "bytes per launch", "dispatches_averaged": LAST,
-           "fetch_raw": fetch, "write": write, "bytes_per_launch": {}}
+           "library_sha256_16": sha, "fetch_raw": fetch, "write": write, "bytes_per_launch": {}}
     for k in set(fetch) | set(write):
         res["bytes_per_launch"][k] = 2.0 * fetch.get(k, 0.0) + write.get(k, 0.0)
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)

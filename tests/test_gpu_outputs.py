@@ -63,3 +63,40 @@ def test_gpu_collect_outputs_large(gpu_available):
         assert moff[r + 1] - moff[r] == len(eng.messages(r))
         assert roff[r + 1] - roff[r] == len(eng.ready_to_reads(r))
     eng.close()
+
+
+@pytest.mark.parametrize("name,kw,extra", [("C3", C3, dict(ring=128)), ("C4", C4, {})])
+def test_gpu_collect_updates_match_per_replica(gpu_available, name, kw, extra):
+    """rbe_collect_updates returns exactly the replicas whose rbe_get_updates
+    record has RBE_UF_HAS_UPDATE, ascending, each with the same record."""
+    from dragonboat_amd import engine as E
+    kw = dict(kw, n_groups=min(kw["n_groups"], 48))
+    eng = E.Engine(device=0, trace=True, **dict(kw, **extra))
+    seen = 0
+    for rnd in range(120):
+        eng.step()
+        if rnd % 5 != 2 and rnd < 110:
+            continue
+        for first, count in ((0, eng.n_rep), (5, eng.n_rep - 11)):
+            rep, ups = eng.collect_updates(first, count)
+            full = np.frombuffer(bytes(eng.updates(first, count)), E.UPDATE_DTYPE)
+            want = np.nonzero(full["flags"] & E.UF_HAS_UPDATE)[0]
+            assert rep.tolist() == (want + first).tolist()
+            assert ups.tobytes() == full[want].tobytes()
+            seen += len(rep)
+    assert seen > 0
+    eng.close()
+
+
+def test_gpu_collect_updates_large(gpu_available):
+    """200k C4 groups: the compacted Updates span many scan blocks."""
+    from dragonboat_amd import engine as E
+    eng = E.Engine(device=0, **dict(C4, n_groups=200_000))
+    eng.run(260)
+    rep, ups = eng.collect_updates()
+    full = np.frombuffer(bytes(eng.updates()), E.UPDATE_DTYPE)
+    want = np.nonzero(full["flags"] & E.UF_HAS_UPDATE)[0]
+    assert len(want) > 1000
+    assert np.array_equal(rep, want.astype(np.uint64))
+    assert ups.tobytes() == full[want].tobytes()
+    eng.close()

@@ -99,3 +99,58 @@ def test_gpu_wire_decode_dense_requests(gpu_available):
     assert [(m.type, m.to) for m in msgs] == [(r[0]["type"], r[0]["to"]) for r in ref]
     assert (msgs[-1].type, msgs[-1].to) == (0x11, 2)
     eng.close()
+
+
+def test_gpu_wire_decode_max_sized_messages(gpu_available):
+    """getMaxSizedMsg-shaped requests (raftpb/raft_test.go:319-346): every u64
+    field max-valued (10-byte varints, colfer's 9-byte form), Entry session
+    fields at 2^64-1 and just above 2^49, 1 KiB Cmds, an embedded Snapshot with
+    a file path — decoded on the device exactly as oracle/wire.py reads them;
+    a frame with an unknown method (tcp.go:93-112) is refused."""
+    from dragonboat_amd.engine import RBE_E_CORRUPT, EngineError
+    M = (1 << 64) - 1
+    big = (1 << 49) + 12345
+    msgs = []
+    for i in range(6):
+        m = dict(type=[12, 4, 13][i % 3], to=M - i, cluster_id=M, term=M, log_term=big,
+                 log_index=M, commit=big + i, reject=i % 2 == 1, hint=M, hint_high=big)
+        m["from"] = M - 7
+        ents = [dict(term=M, index=big + j, type=j % 4, key=M, client_id=big, series_id=M - j,
+                     responded_to=big + j, cmd=bytes((i + j + k) & 0xFF for k in range(1024)))
+                for j in range(3 if i % 3 == 0 else 0)]
+        snap = W.snapshot_bytes(M, M, "longfilepathisherexxxxxxxxxxxxxxxxx", M) if i == 1 else None
+        msgs.append((m, ents, snap))
+    payload = bytearray()
+    for m, ents, snap in msgs:
+        b = W.message_bytes(m, ents, snap)
+        payload.append(0x0A)
+        W.put_varint(payload, len(b))
+        payload += b
+    W._field_varint(payload, 0x10, M)
+    payload += b"\x1a\x05node1"
+    W._field_varint(payload, 0x20, (1 << 32) - 1)
+    stream = W.frame(bytes(payload))
+    eng = _engine(**C2)
+    eng.run(2)
+    dm, de, dcmd = eng.wire_decode(stream)
+    ref = W.batch_decode(W.frames_decode(stream)[0])["requests"]
+    assert len(dm) == len(ref) == 6
+    ei, off = 0, 0
+    for got, (rm, rents) in zip(dm, [(r[0], r[1]) for r in ref]):
+        for f in ("type", "to", "cluster_id", "term", "log_term", "log_index", "commit", "hint",
+                  "hint_high"):
+            assert getattr(got, f) == rm[f], f
+        assert got.from_ == rm["from"] and bool(got.reject) == bool(rm["reject"])
+        assert got.n_entries == len(rents)
+        for re_ in rents:
+            e = de[ei]
+            ei += 1
+            for f in ("term", "index", "type", "key", "client_id", "series_id", "responded_to"):
+                assert getattr(e, f) == re_[f], f
+            assert e.cmd_len == len(re_["cmd"]) and dcmd[off:off + e.cmd_len] == re_["cmd"]
+            off += e.cmd_len
+    bad = W.MAGIC + W.request_header_encode(1024, len(payload), W.crc32(bytes(payload))) + bytes(payload)
+    with pytest.raises(EngineError) as exc:
+        eng.wire_decode(bad)
+    assert exc.value.rc == RBE_E_CORRUPT
+    eng.close()
