@@ -75,7 +75,7 @@ WORKLOADS = {
                  in_cap=200_000), 260,
             "C4 host-driven: 1M groups x 3, Quiesce on, 10% active groups get a ReadIndex "
             "(90%) or a 16 B proposal (10%) per round at their leader through rbe_push_*, "
-            "every Update and output read back through rbe_get_updates / rbe_collect_outputs"),
+            "the Updates of the replicas that have one and every output read back through rbe_collect_updates / rbe_collect_outputs"),
     "c5": (dict(n_groups=500_000, n_replicas=3, wl_enabled=True, wl_start_round=30, ring=64),
            60, "C5: 500k groups x 3 per GPU, replica-per-GPU (replica k of group g on rank "
                "(g+k) % N), steady replication, cross-rank messages by all-to-all each round"),
@@ -417,8 +417,10 @@ def run_host_driven(args, ws, rank, local, dist):
     for r in range(settle + max(1, args.warmup)):
         if r < settle:
             eng.step()
-            if r == settle - 1:
+            if r == settle - 1:  # leaders of every group, quiesced ones included (untimed)
                 eng.sync()
+                lid = np.frombuffer(bytes(eng.updates()), UPDATE_DTYPE)["leader_id"]
+                leader_of[:] = lid.reshape(n_groups, N).max(axis=1)
                 read_back()
         else:
             one_round(r, False)
