@@ -22,6 +22,12 @@
 #include "rbe_snap.h"
 #include "rbe_wire_kernels.h"
 
+namespace rbe {
+int dev_sort_pairs(void* tmp, size_t* tmp_bytes, const uint64_t* kin, uint64_t* kout,
+                   const uint32_t* vin, uint32_t* vout, uint64_t n, int end_bit,
+                   hipStream_t stream);  // rbe_sort.hip
+}
+
 using namespace rbe;
 
 #ifndef RBE_SINGLE_TU
@@ -385,6 +391,9 @@ struct rbe_engine {
   u64 out_dev_bytes = 0;
   u8* out_host = nullptr;
   u64 out_host_bytes = 0;
+  // rbe_wire_ingest scratch (keys, indexes, heap offsets, sort temporary)
+  u8* ing_dev = nullptr;
+  u64 ing_dev_bytes = 0;
   // rbe_collect_updates: the same for the compacted Updates
   u8* upd_dev = nullptr;
   u64 upd_dev_bytes = 0;
@@ -687,6 +696,7 @@ int rbe_destroy(rbe_engine* e) {
   if (e->out_dev) HIP_IGNORE(hipFree(e->out_dev));
   if (e->out_host) HIP_IGNORE(hipHostFree(e->out_host));
   if (e->upd_dev) HIP_IGNORE(hipFree(e->upd_dev));
+  if (e->ing_dev) HIP_IGNORE(hipFree(e->ing_dev));
   if (e->upd_host) HIP_IGNORE(hipHostFree(e->upd_host));
   if (e->wire_dev) HIP_IGNORE(hipFree(e->wire_dev));
   if (e->wire_meta) HIP_IGNORE(hipFree(e->wire_meta));
@@ -911,7 +921,10 @@ static int launch_iso(rbe_engine* e) {
 // buffer in one copy and scatter it on device, ahead of the round's kernels.
 static int flush_inputs(rbe_engine* e) {
   HostInputs& h = e->hin;
-  if (h.empty()) return RBE_OK;
+  if (h.empty()) {
+    h.heap.settle();
+    return RBE_OK;
+  }
   // payload heap bytes of the staged proposals: positions [flushed, head),
   // split where they cross the end of the ring
   for (u64 p = h.heap.flushed; p < h.heap.head;) {
@@ -1851,6 +1864,9 @@ int rbe_wire_encode(rbe_engine* e, const rbe_wire_config* wc, uint64_t totals[4]
   memset(&A, 0, sizeof(A));
   A.deployment_id = wc->deployment_id;
   A.bin_ver = wc->bin_ver;
+  if (wc->dst_rank >= (int32_t)C.rep_world || (wc->dst_rank >= 0 && C.rep_world <= 1))
+    return RBE_E_INVALID;
+  A.dst_rank = wc->dst_rank;
   const u64 gpb = wc->groups_per_batch ? wc->groups_per_batch : C.n_groups;
   if (gpb > 0xFFFFFFFFull) return RBE_E_INVALID;
   A.gpb = (u32)gpb;
@@ -1934,12 +1950,22 @@ int rbe_wire_fetch(rbe_engine* e, void* out, uint64_t cap, rbe_wire_frame* frame
   return RBE_OK;
 }
 
-int rbe_wire_decode(rbe_engine* e, const void* data, uint64_t bytes, rbe_message* msgs,
-                    uint32_t cap, uint32_t* n_msgs, rbe_entry* ents, uint32_t ent_cap,
-                    uint32_t* n_ents, uint8_t* cmd, uint64_t cmd_cap, uint64_t* cmd_bytes) {
-  if (!e || (bytes && !data) || !n_msgs || !n_ents || !cmd_bytes) return RBE_E_INVALID;
-  *n_msgs = *n_ents = 0;
-  *cmd_bytes = 0;
+// Decoded records of a byte stream, left in device memory (e->wire_rec):
+// messages in frame order, their entries (message j's from ent0[j]) and Cmd
+// bytes (message j's from cmd0[j]).
+struct WireDecoded {
+  u64 frames = 0, tm = 0, te = 0, tc = 0;
+  rbe_message* msgs = nullptr;
+  rbe_entry* ents = nullptr;
+  u8* cmd = nullptr;
+  u64 *ent0 = nullptr, *cmd0 = nullptr;
+};
+
+// rbe_wire_decode's device part: verify, find, count, scan and parse.  With
+// `caps` non-null (the caller's capacities: messages, entries, Cmd bytes) the
+// records are not parsed when one is short (RBE_E_NOMEM, counts reported).
+static int wire_decode_dev(rbe_engine* e, const void* data, uint64_t bytes, WireDecoded* o,
+                           const u64* caps) {
   // the frame boundaries: magic + size of each header (the receiver's reads)
   const u8* d = (const u8*)data;
   std::vector<WireIn> fr;
@@ -1991,7 +2017,8 @@ int rbe_wire_decode(rbe_engine* e, const void* data, uint64_t bytes, rbe_message
     w.msg0 = tm;
     tm += w.n_msgs;
   }
-  *n_msgs = (u32)(tm < 0xFFFFFFFFull ? tm : 0xFFFFFFFFull);
+  o->frames = nf;
+  o->tm = tm;
   if (tm > 0xFFFFFFFFull) return RBE_E_NOMEM;
   // per message: position, entry and Cmd counts (scanned), error flag, scan tops
   const u64 nbk = (tm + 255) / 256;
@@ -2033,11 +2060,10 @@ int rbe_wire_decode(rbe_engine* e, const void* data, uint64_t bytes, rbe_message
   HIP_OK(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
   if (herr) return RBE_E_CORRUPT;
-  *n_ents = (u32)(te < 0xFFFFFFFFull ? te : 0xFFFFFFFFull);
-  *cmd_bytes = tc;
+  o->te = te;
+  o->tc = tc;
   if (te > 0xFFFFFFFFull) return RBE_E_NOMEM;
-  if (tm > cap || te > ent_cap || tc > cmd_cap || (tm && !msgs) || (te && !ents) || (tc && !cmd))
-    return RBE_E_NOMEM;
+  if (caps && (tm > caps[0] || te > caps[1] || tc > caps[2])) return RBE_E_NOMEM;
   const u64 o_m = o_rec, o_e = o_m + al(tm * sizeof(rbe_message)),
             o_c = o_e + al(te * sizeof(rbe_entry));
   {
@@ -2065,9 +2091,144 @@ int rbe_wire_decode(rbe_engine* e, const void* data, uint64_t bytes, rbe_message
     hipLaunchKernelGGL(k_wire_parse, dim3(gm), dim3(256), 0, e->stream, e->wire_in, pos, tm, 1,
                        ec, cc, dm, de, dc, err);
   HIP_OK(hipGetLastError());
-  if (tm) HIP_OK(hipMemcpyAsync(msgs, dm, tm * sizeof(rbe_message), hipMemcpyDeviceToHost, e->stream));
-  if (te) HIP_OK(hipMemcpyAsync(ents, de, te * sizeof(rbe_entry), hipMemcpyDeviceToHost, e->stream));
-  if (tc) HIP_OK(hipMemcpyAsync(cmd, dc, tc, hipMemcpyDeviceToHost, e->stream));
+  o->msgs = dm;
+  o->ents = de;
+  o->cmd = dc;
+  o->ent0 = ec;
+  o->cmd0 = cc;
+  return RBE_OK;
+}
+
+int rbe_wire_decode(rbe_engine* e, const void* data, uint64_t bytes, rbe_message* msgs,
+                    uint32_t cap, uint32_t* n_msgs, rbe_entry* ents, uint32_t ent_cap,
+                    uint32_t* n_ents, uint8_t* cmd, uint64_t cmd_cap, uint64_t* cmd_bytes) {
+  if (!e || (bytes && !data) || !n_msgs || !n_ents || !cmd_bytes) return RBE_E_INVALID;
+  *n_msgs = *n_ents = 0;
+  *cmd_bytes = 0;
+  WireDecoded o;
+  const u64 caps[3] = {msgs ? cap : 0u, ents ? ent_cap : 0u, cmd ? cmd_cap : 0u};
+  const int rc = wire_decode_dev(e, data, bytes, &o, caps);
+  *n_msgs = (u32)(o.tm < 0xFFFFFFFFull ? o.tm : 0xFFFFFFFFull);
+  *n_ents = (u32)(o.te < 0xFFFFFFFFull ? o.te : 0xFFFFFFFFull);
+  *cmd_bytes = o.tc;
+  if (rc) return rc;
+  if (o.tm) HIP_OK(hipMemcpyAsync(msgs, o.msgs, o.tm * sizeof(rbe_message), hipMemcpyDeviceToHost, e->stream));
+  if (o.te) HIP_OK(hipMemcpyAsync(ents, o.ents, o.te * sizeof(rbe_entry), hipMemcpyDeviceToHost, e->stream));
+  if (o.tc) HIP_OK(hipMemcpyAsync(cmd, o.cmd, o.tc, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return RBE_OK;
+}
+
+// Device ingest of inbound frames (rbe_ingest.h): decode, check, sort by inbox
+// list, check capacities, one read-back, reserve heap room, write the lists.
+int rbe_wire_ingest(rbe_engine* e, const void* data, uint64_t bytes, rbe_wire_ingest_stats* st) {
+  if (!e || (bytes && !data) || !st || e->round == 0) return RBE_E_INVALID;
+  memset(st, 0, sizeof(*st));
+  const Params& C = e->C;
+  if (C.rep_world <= 1) return RBE_E_STATE;  // every sender is stepped here
+  HIP_OK(hipSetDevice(e->device));
+  WireDecoded o;
+  int rc = wire_decode_dev(e, data, bytes, &o, nullptr);
+  st->frames = o.frames;
+  st->messages = o.tm;
+  st->entries = o.te;
+  st->cmd_bytes = o.tc;
+  if (rc) return rc;
+  const u64 tm = o.tm;
+  if (tm == 0) return RBE_OK;
+  if (tm > 0x7FFFFFFFull) return RBE_E_NOMEM;
+  const u64 nbk = (tm + 255) / 256;
+  const u64 drop = (u64)C.n_rep * C.n;
+  int bits = 1;
+  while (bits < 64 && (drop >> bits)) bits++;
+  size_t tb = 0;
+  if (dev_sort_pairs(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, tm, bits, e->stream))
+    return RBE_E_HIP;
+  auto al = [](u64 x) { return (x + 255) & ~255ull; };
+  // keys | sorted keys | heap bytes | sorted heap offsets | idx | sorted idx | tops | err | sort tmp
+  const u64 o_sk = al(tm * 8), o_hb = o_sk + al(tm * 8), o_hs = o_hb + al(tm * 8);
+  const u64 o_ix = o_hs + al(tm * 8), o_si = o_ix + al(tm * 4), o_top = o_si + al(tm * 4);
+  const u64 o_err = o_top + al((nbk + 1) * 8), o_tmp = o_err + 256;
+  if ((rc = grow(&e->ing_dev, &e->ing_dev_bytes, o_tmp + al(tb), false))) return rc;
+  u8* b = e->ing_dev;
+  u64 *key = (u64*)b, *skey = (u64*)(b + o_sk), *hb = (u64*)(b + o_hb), *hs = (u64*)(b + o_hs);
+  u32 *idx = (u32*)(b + o_ix), *sidx = (u32*)(b + o_si);
+  u64* top = (u64*)(b + o_top);
+  u32* err = (u32*)(b + o_err);
+  unsigned long long* ndrop = (unsigned long long*)(b + o_err + 8);
+  HIP_OK(hipMemsetAsync(b + o_err, 0, 16, e->stream));
+  const u32 par = (e->round - 1) & 1u;
+  rc = dispatch_n(C.n, [&](auto NN) {
+    constexpr int N = decltype(NN)::value;
+    hipLaunchKernelGGL(k_ing_key<N>, dim3((unsigned)nbk), dim3(256), 0, e->stream, C,
+                       (u64)C.heap_bytes, (const rbe_message*)o.msgs, (const rbe_entry*)o.ents,
+                       (const u64*)o.ent0, tm, key, idx, hb, err, ndrop);
+    return RBE_OK;
+  });
+  if (rc) return rc;
+  HIP_OK(hipGetLastError());
+  if (dev_sort_pairs(b + o_tmp, &tb, key, skey, idx, sidx, tm, bits, e->stream)) return RBE_E_HIP;
+  hipLaunchKernelGGL(k_ing_gather, dim3((unsigned)nbk), dim3(256), 0, e->stream, (const u32*)sidx,
+                     (const u64*)hb, hs, tm);
+  hipLaunchKernelGGL(k_scan_blocks, dim3((unsigned)nbk), dim3(256), 0, e->stream, hs, tm, top);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, e->stream, top, (u32)nbk);
+  hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nbk), dim3(256), 0, e->stream, hs, tm,
+                     (const u64*)top);
+  auto walk = [&](bool write, u64 base) {
+    return dispatch_n(C.n, [&](auto NN) {
+      constexpr int N = decltype(NN)::value;
+      if (write)
+        hipLaunchKernelGGL((k_ing_walk<N, true>), dim3((unsigned)nbk), dim3(256), 0, e->stream,
+                           e->P, C, par, e->round, (const u64*)skey, (const u32*)sidx, tm,
+                           (const rbe_message*)o.msgs, (const rbe_entry*)o.ents,
+                           (const u64*)o.ent0, (const u64*)o.cmd0, (const u8*)o.cmd, e->heap,
+                           (u64)C.heap_bytes, base, (const u64*)hs, err);
+      else
+        hipLaunchKernelGGL((k_ing_walk<N, false>), dim3((unsigned)nbk), dim3(256), 0, e->stream,
+                           e->P, C, par, e->round, (const u64*)skey, (const u32*)sidx, tm,
+                           (const rbe_message*)o.msgs, (const rbe_entry*)o.ents,
+                           (const u64*)o.ent0, (const u64*)o.cmd0, (const u8*)o.cmd, e->heap,
+                           (u64)C.heap_bytes, base, (const u64*)hs, err);
+      HIP_OK(hipGetLastError());
+      return RBE_OK;
+    });
+  };
+  if ((rc = walk(false, 0))) return rc;
+  u64 back[3];  // err | drops, heap bytes
+  HIP_OK(hipMemcpyAsync(back, b + o_err, 16, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipMemcpyAsync(back + 2, top + nbk, 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  const u32 ferr = (u32)back[0];
+  if (ferr & ING_INVALID) return RBE_E_INVALID;
+  if (ferr & ING_NOMEM) return RBE_E_NOMEM;
+  st->dropped = back[1];
+  const u64 need = back[2];
+  st->heap_bytes = need;
+  HostHeap& H = e->hin.heap;
+  u64 base = 0;
+  if (need) {
+    // records staged by earlier pushes of this round go up first, so the
+    // device region follows them and the stage stays [flushed, head)
+    for (u64 p = H.flushed; p < H.head;) {
+      const u64 at = p % H.cap, len = std::min(H.head - p, H.cap - at);
+      HIP_OK(hipMemcpyAsync(e->heap + at, H.stage.data() + (p - H.flushed), len,
+                            hipMemcpyHostToDevice, e->stream));
+      p += len;
+    }
+    HIP_OK(hipStreamSynchronize(e->stream));  // the stage is pageable
+    // one region that does not cross the end of the ring
+    const u64 skip = H.head % H.cap + need > H.cap ? H.cap - H.head % H.cap : 0;
+    if ((rc = H.room(need + skip))) return rc;
+    if (H.flushed < H.round_lo) H.round_lo = H.flushed;
+    H.stage.clear();
+    base = H.head + skip;
+    H.head = base + need;
+    H.flushed = H.head;
+    e->heap_head_host = H.head;  // Planes::heap_head for the lapped-record checks
+    HIP_OK(hipMemcpyAsync(e->heap_dev, &e->heap_head_host, sizeof(u64), hipMemcpyHostToDevice,
+                          e->stream));
+  }
+  if ((rc = walk(true, base))) return rc;
   HIP_OK(hipStreamSynchronize(e->stream));
   return RBE_OK;
 }

@@ -27,7 +27,7 @@ namespace rbe {
 // the payload heap): 64 bits over the zero-padded 8-byte words and the length.
 // The trace digest folds it in place of the inline bytes, so the fingerprint
 // stands for the payload in parity checks (oracle/harness.cpp restates it).
-inline u64 cmd_fingerprint(const u8* b, u64 len) {
+RBE_HD u64 cmd_fingerprint(const u8* b, u64 len) {
   u64 h = 0x243F6A8885A308D3ull ^ len;
   for (u64 i = 0; i < len; i += 8) {
     u64 w = 0;
@@ -39,7 +39,7 @@ inline u64 cmd_fingerprint(const u8* b, u64 len) {
 // Fingerprint of a payload-heap record (ET_HEAP): the Cmd's, extended by the
 // session fields {Key, ClientID, SeriesID, RespondedTo} when any is non-zero
 // (raft.pb.go:589-598; oracle/harness.cpp entry_fingerprint restates it).
-inline u64 entry_fingerprint(const u64* meta, const u8* cmd, u64 len) {
+RBE_HD u64 entry_fingerprint(const u64* meta, const u8* cmd, u64 len) {
   u64 h = cmd_fingerprint(cmd, len);
   if (meta[0] | meta[1] | meta[2] | meta[3])
     for (u64 i = 0; i < 4; i++) h = mix64(h ^ meta[i] ^ ((i + 1) << 60));
@@ -47,10 +47,10 @@ inline u64 entry_fingerprint(const u64* meta, const u8* cmd, u64 len) {
 }
 // An rbe_entry that needs a heap record: a Cmd longer than 16 bytes, or any
 // session field (requests.go:994-997 stamps them on every client proposal)
-inline bool entry_needs_heap(const rbe_entry& e) {
+RBE_HD bool entry_needs_heap(const rbe_entry& e) {
   return e.cmd_len > 16 || (e.key | e.client_id | e.series_id | e.responded_to) != 0;
 }
-inline u64 heap_rec_bytes(u64 cmd_len) { return (kHeapHdr + cmd_len + 15) & ~15ull; }
+RBE_HD u64 heap_rec_bytes(u64 cmd_len) { return (kHeapHdr + cmd_len + 15) & ~15ull; }
 
 // Payload heap (cfg.heap_bytes): one device byte ring shared by every group.
 // An entry with a Cmd longer than 16 bytes or session fields is written there
@@ -78,6 +78,8 @@ struct HostHeap {
   u64 head = 0;      // next free absolute position
   u64 flushed = 0;   // positions below this are on the device
   u64 batch_lo = 0;  // first position of the last uploaded batch
+  u64 round_lo = ~0ull;  // first position written straight to the device since the last
+                         // step (rbe_wire_ingest); becomes batch_lo at the next step
   u64 live_lo = 0;   // cached: no live record below it (0 = unknown)
   std::vector<u8> stage;  // bytes of [flushed, head), position flushed at index 0
   // lowest position a live record of the device planes holds (~0 for none)
@@ -103,6 +105,13 @@ struct HostHeap {
       live_lo = lo < head ? lo : head;
     }
     return head + need <= floor() + cap ? RBE_OK : RBE_E_NOMEM;
+  }
+  // at a step: the batch uploaded (or written by the device) since the last
+  // one stays live through it; the stage is empty
+  void settle() {
+    batch_lo = flushed < round_lo ? flushed : round_lo;
+    round_lo = ~0ull;
+    flushed = head;
   }
   // stage one record; returns its position
   u64 put_record(const u64* meta, const u8* cmd, u64 len) {
@@ -434,8 +443,7 @@ struct HostInputs {
     for (const CommitRec& c : commits) committing[c.r] = 0;
     commits.clear();
     heap.stage.clear();
-    heap.batch_lo = heap.flushed;
-    heap.flushed = heap.head;
+    heap.settle();
   }
   ExtIn& rec(u64 r) {
     if (slot[r] == ~0u) {

@@ -295,4 +295,152 @@ RBE_HD void wire_header_put(u8* o, u64 size, u32 pcrc, const u32* table) {
   for (u32 b = 0; b < 4; b++) h[10 + b] = (u8)(hc >> (24 - 8 * b));
 }
 
+// ---------------------------------------------------------------- decode
+// sequential reader over one frame's payload
+struct WireRd {
+  const u8* p;
+  u64 n, i;
+  bool bad;
+  RBE_HD u8 byte() {
+    if (i >= n) {
+      bad = true;
+      return 0;
+    }
+    return p[i++];
+  }
+  RBE_HD u64 varint() {  // protobuf varint (Message.Unmarshal)
+    u64 x = 0;
+    for (u32 s = 0; s < 64; s += 7) {
+      const u8 b = byte();
+      x |= (u64)(b & 0x7F) << s;
+      if (b < 0x80 || bad) return x;
+    }
+    bad = true;
+    return x;
+  }
+  // skipRaft (raft.pb.go): a length or fixed width past the end is
+  // ErrInvalidLength / io.ErrUnexpectedEOF; compared as "l > n - i" so a
+  // length near 2^64 cannot wrap the position
+  RBE_HD void advance(u64 l) {
+    if (i > n || l > n - i) {
+      bad = true;
+      i = n;
+    } else {
+      i += l;
+    }
+  }
+  RBE_HD void skip(u32 wt) {
+    if (wt == 0) varint();
+    else if (wt == 1) advance(8);
+    else if (wt == 2) advance(varint());
+    else if (wt == 5) advance(4);
+    else bad = true;
+  }
+};
+
+// Entry.unmarshal (raft_optimized.go:303-651) of [rd.i, end)
+RBE_HD void wire_entry_get(WireRd& rd, u64 end, rbe_entry* e, u8* cmd) {
+  u64 vals[7] = {0, 0, 0, 0, 0, 0, 0};
+  u8 h = rd.byte();
+  for (u32 f = 0; f < 7; f++) {
+    if (h == f) {
+      u64 x = 0;
+      if (f == 2) {
+        x = rd.varint();
+      } else {
+        for (u32 s = 0;; s += 7) {
+          const u8 b = rd.byte();
+          if (b < 0x80 || s == 56) {
+            x |= (u64)b << s;
+            break;
+          }
+          x |= (u64)(b & 0x7F) << s;
+        }
+      }
+      vals[f] = x;
+      h = rd.byte();
+    } else if (h == (f | 0x80)) {
+      u64 x = 0;
+      if (f == 2) {
+        x = (u64)(u32)(0u - (u32)rd.varint());
+      } else {
+        for (int b = 0; b < 8; b++) x = (x << 8) | rd.byte();
+      }
+      vals[f] = x;
+      h = rd.byte();
+    }
+  }
+  u32 len = 0;
+  if (h == 7) {
+    const u64 l = rd.varint();
+    if (rd.i > end || l > end - rd.i) rd.bad = true;
+    len = rd.bad ? 0u : (u32)l;
+    for (u32 b = 0; b < len && !rd.bad; b++) {
+      const u8 x = rd.byte();
+      if (cmd) cmd[b] = x;
+      if (e && b < 16) e->cmd[b] = x;
+    }
+    h = rd.byte();
+  }
+  if (h != 0x7F || rd.i != end) rd.bad = true;
+  if (e) {
+    e->term = vals[0];
+    e->index = vals[1];
+    e->type = (u32)vals[2];
+    e->cmd_len = len;
+    e->key = vals[3];
+    e->client_id = vals[4];
+    e->series_id = vals[5];
+    e->responded_to = vals[6];
+  }
+}
+
+// Message.Unmarshal (raft_optimized.go:654-979) of [rd.i, end); entries to
+// ents[0..] and their Cmds to cmd[cmd_at..]; returns entries, *cmd_at advanced
+RBE_HD u32 wire_message_get(WireRd& rd, u64 end, rbe_message* m, rbe_entry* ents, u8* cmd,
+                            u64* cmd_at) {
+  u64 f[14] = {0};
+  u32 ne = 0;
+  while (rd.i < end && !rd.bad) {
+    const u64 tag = rd.varint();
+    const u32 fn = (u32)(tag >> 3), wt = (u32)(tag & 7);
+    if (fn >= 1 && fn <= 13 && fn != 11 && fn != 12 && wt == 0) {
+      f[fn] = rd.varint();
+    } else if (fn == 11 && wt == 2) {
+      const u64 l = rd.varint();
+      if (rd.bad || rd.i > end || l > end - rd.i) {
+        rd.bad = true;
+        break;
+      }
+      const u64 e_end = rd.i + l;
+      // Cmd length first (the colfer walk below writes at cmd + *cmd_at)
+      rbe_entry tmp;
+      rbe_entry* e = ents ? &ents[ne] : &tmp;
+      for (int b = 0; b < 16; b++) e->cmd[b] = 0;
+      wire_entry_get(rd, e_end, e, cmd ? cmd + *cmd_at : nullptr);
+      *cmd_at += e->cmd_len;
+      ne++;
+    } else {
+      rd.skip(wt);  // the embedded Snapshot included: no InstallSnapshot here
+    }
+  }
+  if (rd.i != end) rd.bad = true;
+  if (m) {
+    m->type = (u32)f[1];
+    m->to = f[2];
+    m->from = f[3];
+    m->cluster_id = f[4];
+    m->term = f[5];
+    m->log_term = f[6];
+    m->log_index = f[7];
+    m->commit = f[8];
+    m->reject = f[9] != 0;
+    m->hint = f[10];
+    m->hint_high = f[13];
+    m->n_entries = ne;
+    m->reserved = 0;
+  }
+  return ne;
+}
+
 }  // namespace rbe

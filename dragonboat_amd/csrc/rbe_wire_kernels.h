@@ -16,6 +16,7 @@
 #pragma once
 
 #include "rbe_wire.h"
+#include "rbe_ingest.h"
 
 namespace rbe {
 
@@ -25,6 +26,8 @@ struct WireArgs {
   u32 nchunks, npairs;   // batches = npairs * nchunks
   u32 round;
   u64 heap_head;         // payload heap head at the last upload (lapped-record check)
+  int32_t dst_rank;      // replica mode: receivers of this rank only (-1: every remote rank)
+  u32 pad;
   u32 alen[6];
   u8 addr[6][48];        // source address of each slot
 };
@@ -62,6 +65,11 @@ __global__ __launch_bounds__(256) void k_wire_size(Planes P, Params C, WireArgs 
   const u64 g = c % C.n_groups;
   u32 k, d;
   wire_pair(N, p, &k, &d);
+  if (!wire_cell_sent<N>(C, A.dst_rank, g, k, d)) {
+    B.cell_bytes[c] = 0;
+    B.cell_msgs[c] = 0;
+    return;
+  }
   u32 nm = 0, ni = 0, bad = 0;
   const u32 b = wire_cell<N>(P, C, heap, A.heap_head, g, k, d, A.round, nullptr, &nm, &ni, &bad);
   B.cell_bytes[c] = b;
@@ -314,153 +322,6 @@ __global__ __launch_bounds__(256) void k_wire_verify(const u8* data, WireIn* fr)
   }
 }
 
-// sequential reader over one frame's payload
-struct WireRd {
-  const u8* p;
-  u64 n, i;
-  bool bad;
-  RBE_HD u8 byte() {
-    if (i >= n) {
-      bad = true;
-      return 0;
-    }
-    return p[i++];
-  }
-  RBE_HD u64 varint() {  // protobuf varint (Message.Unmarshal)
-    u64 x = 0;
-    for (u32 s = 0; s < 64; s += 7) {
-      const u8 b = byte();
-      x |= (u64)(b & 0x7F) << s;
-      if (b < 0x80 || bad) return x;
-    }
-    bad = true;
-    return x;
-  }
-  // skipRaft (raft.pb.go): a length or fixed width past the end is
-  // ErrInvalidLength / io.ErrUnexpectedEOF; compared as "l > n - i" so a
-  // length near 2^64 cannot wrap the position
-  RBE_HD void advance(u64 l) {
-    if (i > n || l > n - i) {
-      bad = true;
-      i = n;
-    } else {
-      i += l;
-    }
-  }
-  RBE_HD void skip(u32 wt) {
-    if (wt == 0) varint();
-    else if (wt == 1) advance(8);
-    else if (wt == 2) advance(varint());
-    else if (wt == 5) advance(4);
-    else bad = true;
-  }
-};
-
-// Entry.unmarshal (raft_optimized.go:303-651) of [rd.i, end)
-RBE_HD void wire_entry_get(WireRd& rd, u64 end, rbe_entry* e, u8* cmd) {
-  u64 vals[7] = {0, 0, 0, 0, 0, 0, 0};
-  u8 h = rd.byte();
-  for (u32 f = 0; f < 7; f++) {
-    if (h == f) {
-      u64 x = 0;
-      if (f == 2) {
-        x = rd.varint();
-      } else {
-        for (u32 s = 0;; s += 7) {
-          const u8 b = rd.byte();
-          if (b < 0x80 || s == 56) {
-            x |= (u64)b << s;
-            break;
-          }
-          x |= (u64)(b & 0x7F) << s;
-        }
-      }
-      vals[f] = x;
-      h = rd.byte();
-    } else if (h == (f | 0x80)) {
-      u64 x = 0;
-      if (f == 2) {
-        x = (u64)(u32)(0u - (u32)rd.varint());
-      } else {
-        for (int b = 0; b < 8; b++) x = (x << 8) | rd.byte();
-      }
-      vals[f] = x;
-      h = rd.byte();
-    }
-  }
-  u32 len = 0;
-  if (h == 7) {
-    const u64 l = rd.varint();
-    if (rd.i > end || l > end - rd.i) rd.bad = true;
-    len = rd.bad ? 0u : (u32)l;
-    for (u32 b = 0; b < len && !rd.bad; b++) {
-      const u8 x = rd.byte();
-      if (cmd) cmd[b] = x;
-      if (e && b < 16) e->cmd[b] = x;
-    }
-    h = rd.byte();
-  }
-  if (h != 0x7F || rd.i != end) rd.bad = true;
-  if (e) {
-    e->term = vals[0];
-    e->index = vals[1];
-    e->type = (u32)vals[2];
-    e->cmd_len = len;
-    e->key = vals[3];
-    e->client_id = vals[4];
-    e->series_id = vals[5];
-    e->responded_to = vals[6];
-  }
-}
-
-// Message.Unmarshal (raft_optimized.go:654-979) of [rd.i, end); entries to
-// ents[0..] and their Cmds to cmd[cmd_at..]; returns entries, *cmd_at advanced
-RBE_HD u32 wire_message_get(WireRd& rd, u64 end, rbe_message* m, rbe_entry* ents, u8* cmd,
-                            u64* cmd_at) {
-  u64 f[14] = {0};
-  u32 ne = 0;
-  while (rd.i < end && !rd.bad) {
-    const u64 tag = rd.varint();
-    const u32 fn = (u32)(tag >> 3), wt = (u32)(tag & 7);
-    if (fn >= 1 && fn <= 13 && fn != 11 && fn != 12 && wt == 0) {
-      f[fn] = rd.varint();
-    } else if (fn == 11 && wt == 2) {
-      const u64 l = rd.varint();
-      if (rd.bad || rd.i > end || l > end - rd.i) {
-        rd.bad = true;
-        break;
-      }
-      const u64 e_end = rd.i + l;
-      // Cmd length first (the colfer walk below writes at cmd + *cmd_at)
-      rbe_entry tmp;
-      rbe_entry* e = ents ? &ents[ne] : &tmp;
-      for (int b = 0; b < 16; b++) e->cmd[b] = 0;
-      wire_entry_get(rd, e_end, e, cmd ? cmd + *cmd_at : nullptr);
-      *cmd_at += e->cmd_len;
-      ne++;
-    } else {
-      rd.skip(wt);  // the embedded Snapshot included: no InstallSnapshot here
-    }
-  }
-  if (rd.i != end) rd.bad = true;
-  if (m) {
-    m->type = (u32)f[1];
-    m->to = f[2];
-    m->from = f[3];
-    m->cluster_id = f[4];
-    m->term = f[5];
-    m->log_term = f[6];
-    m->log_index = f[7];
-    m->commit = f[8];
-    m->reject = f[9] != 0;
-    m->hint = f[10];
-    m->hint_high = f[13];
-    m->n_entries = ne;
-    m->reserved = 0;
-  }
-  return ne;
-}
-
 // Decode is parallel per message: one block per frame finds the top-level
 // requests of its MessageBatch (MessageBatch.Unmarshal, raft_optimized.go:
 // 1051-1204: field 1 = a Message, 2-4 the trailer) in LDS windows;
@@ -694,6 +555,50 @@ __global__ __launch_bounds__(256) void k_scan_top(u64* top, u32 nb) {
 __global__ __launch_bounds__(256) void k_scan_add(u64* v, u64 n, const u64* top) {
   const u64 j = (u64)blockIdx.x * 256 + threadIdx.x;
   if (j < n) v[j] += top[blockIdx.x];
+}
+
+}  // namespace rbe
+
+// ---------------------------------------------------------------- ingest
+// rbe_wire_ingest (rbe_ingest.h): decoded records → inbox plane slots.
+namespace rbe {
+
+template <int N>
+__global__ __launch_bounds__(256) void k_ing_key(Params C, u64 heap_cap, const rbe_message* msgs,
+                                                 const rbe_entry* ents, const u64* ent0, u64 nm,
+                                                 u64* key, u32* idx, u64* hb, u32* err,
+                                                 unsigned long long* ndrop) {
+  const u64 j = (u64)blockIdx.x * 256 + threadIdx.x;
+  if (j >= nm) return;
+  u32 e = 0;
+  u64 h = 0;
+  const u64 k = ingest_check<N>(C, heap_cap, msgs[j], ents + ent0[j], &e, &h);
+  key[j] = k;
+  idx[j] = (u32)j;
+  hb[j] = h;
+  if (e) atomicOr(err, e);
+  else if (k == ing_drop_key(C)) atomicAdd(ndrop, 1ull);
+}
+
+// heap bytes in sorted order (scanned next into each message's heap offset)
+__global__ __launch_bounds__(256) void k_ing_gather(const u32* sidx, const u64* hb, u64* hs, u64 nm) {
+  const u64 p = (u64)blockIdx.x * 256 + threadIdx.x;
+  if (p < nm) hs[p] = hb[sidx[p]];
+}
+
+template <int N, bool WRITE>
+__global__ __launch_bounds__(256) void k_ing_walk(Planes P, Params C, u32 par, u32 round,
+                                                  const u64* skey, const u32* sidx, u64 nm,
+                                                  const rbe_message* msgs, const rbe_entry* ents,
+                                                  const u64* ent0, const u64* cmd0, const u8* cmd,
+                                                  u8* heap, u64 heap_cap, u64 base, const u64* hs,
+                                                  u32* err) {
+  const u64 p = (u64)blockIdx.x * 256 + threadIdx.x;
+  if (p >= nm || !ingest_run_start(C, skey, p)) return;
+  const u64 q = ingest_run_end(C, skey, p, nm);
+  const u32 e = ingest_sender<N, WRITE>(P, C, par, round, skey, sidx, p, q, msgs, ents, ent0, cmd0,
+                                        cmd, heap, heap_cap, base, hs);
+  if (e) atomicOr(err, e);
 }
 
 }  // namespace rbe

@@ -14,7 +14,7 @@ import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libdragonboat_amd.so")
-RBE_ABI_VERSION = 4
+RBE_ABI_VERSION = 5
 
 COUNTER_NAMES = ["steps", "committed", "msg_in", "msg_out", "ent_in", "ent_out",
                  "reads_confirmed", "proposals", "reads", "quiesced_ticks", "active_ticks",
@@ -163,12 +163,18 @@ class RbeWireFrame(C.Structure):
 
 class RbeWireConfig(C.Structure):
     _fields_ = [("deployment_id", C.c_uint64), ("bin_ver", C.c_uint32),
-                ("groups_per_batch", C.c_uint32), ("source_address", C.c_char_p * 6)]
+                ("groups_per_batch", C.c_uint32), ("source_address", C.c_char_p * 6),
+                ("dst_rank", C.c_int32), ("pad", C.c_uint32)]
 
 
-def wire_config(deployment_id=0, bin_ver=0, groups_per_batch=0, source_address=()):
+class RbeWireIngestStats(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in ("frames", "messages", "dropped", "entries",
+                                          "cmd_bytes", "heap_bytes")]
+
+
+def wire_config(deployment_id=0, bin_ver=0, groups_per_batch=0, source_address=(), dst_rank=-1):
     wc = RbeWireConfig(deployment_id=deployment_id, bin_ver=bin_ver,
-                       groups_per_batch=groups_per_batch)
+                       groups_per_batch=groups_per_batch, dst_rank=dst_rank)
     for i, a in enumerate(source_address):
         wc.source_address[i] = a.encode()
     return wc
@@ -197,7 +203,7 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_get_entry_cmds", "rbe_set_apply_ready", "rbe_collect_outputs", "rbe_collect_updates", "rbe_launch",
            "rbe_xchg_chunk_bytes", "rbe_xchg_pack_fixed", "rbe_xchg_unpack_fixed",
            "rbe_xchg_status", "rbe_stream", "rbe_get_snapshot_state", "rbe_wire_encode",
-           "rbe_wire_fetch", "rbe_wire_decode", "rbe_propose_entries", "rbe_commit",
+           "rbe_wire_fetch", "rbe_wire_decode", "rbe_wire_ingest", "rbe_propose_entries", "rbe_commit",
            "rbe_get_update_commits", "rbe_propose_config_change", "rbe_apply_config_change",
            "rbe_reject_config_change"]
 KERNEL_SLOTS = 4
@@ -264,6 +270,7 @@ def load_library(path: Optional[str] = None):
         "rbe_get_snapshot_state": (i32, [vp, u64, u64, P(u64)]),
         "rbe_wire_encode": (i32, [vp, P(RbeWireConfig), P(u64)]),
         "rbe_wire_fetch": (i32, [vp, vp, u64, P(RbeWireFrame), u32]),
+        "rbe_wire_ingest": (i32, [vp, vp, u64, P(RbeWireIngestStats)]),
         "rbe_wire_decode": (i32, [vp, vp, u64, P(RbeMessage), u32, P(u32), P(RbeEntry), u32,
                                   P(u32), vp, u64, P(u64)]),
         "rbe_collect_outputs": (i32, [vp, u64, u64, P(RbeOutputs)]),
@@ -364,6 +371,14 @@ class SnapshotError(EngineError):
 def _check(rc: int, what: str):
     if rc != 0:
         raise EngineError(f"{what} failed with rc={rc}")
+
+
+def wire_ingest_call(fn, h, data: bytes) -> dict:
+    """rbe_wire_ingest (or the host build's twin): the stats as a dict;
+    raises InputError with the return code on a refused batch."""
+    st = RbeWireIngestStats()
+    _check_input(fn(h, data, len(data), C.byref(st)), "rbe_wire_ingest")
+    return {f: getattr(st, f) for f, _ in RbeWireIngestStats._fields_}
 
 
 def entry_cmds(fn, h, replica: int, lo: int, hi: int) -> List[bytes]:
@@ -698,11 +713,18 @@ class Engine(NodeInputs):
         _check(self.lib.rbe_get_views(self.h, first, count, arr), "rbe_get_views")
         return arr
 
-    def wire_encode(self, deployment_id=0, bin_ver=0, groups_per_batch=0, source_address=()):
+    def wire_ingest(self, data: bytes) -> dict:
+        """rbe_wire_ingest: deliver one round's inbound frames to the next step
+        on the device; returns the stats as a dict (raises InputError with the
+        return code on a refused batch)."""
+        return wire_ingest_call(self.lib.rbe_wire_ingest, self.h, data)
+
+    def wire_encode(self, deployment_id=0, bin_ver=0, groups_per_batch=0, source_address=(),
+                    dst_rank=-1):
         """rbe_wire_encode: the last round's outbox as framed MessageBatches in
         device memory; returns (bytes, frames, messages, InstallSnapshots left out)."""
         tot = (C.c_uint64 * 4)()
-        wc = wire_config(deployment_id, bin_ver, groups_per_batch, source_address)
+        wc = wire_config(deployment_id, bin_ver, groups_per_batch, source_address, dst_rank)
         _check(self.lib.rbe_wire_encode(self.h, C.byref(wc), tot), "rbe_wire_encode")
         return tuple(tot)
 

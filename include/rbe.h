@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RBE_ABI_VERSION 4
+#define RBE_ABI_VERSION 5
 
 /* error codes */
 #define RBE_OK 0
@@ -458,6 +458,12 @@ typedef struct rbe_wire_config {
   uint32_t bin_ver;            /* MessageBatch.BinVer (raftio.RPCBinVersion) */
   uint32_t groups_per_batch;   /* 0 = every group in one batch per slot pair */
   const char* source_address[6];  /* MessageBatch.SourceAddress per sender slot (< 48 B) */
+  /* replica mode (rep_world > 1): only the messages of the replicas stepped
+   * here to replicas stepped by rank dst_rank (-1: by any other rank); the
+   * stream for one remote engine, as a transport keeps one connection per
+   * remote NodeHost.  Must be -1 with one replica set per engine. */
+  int32_t dst_rank;
+  uint32_t pad;
 } rbe_wire_config;
 /* totals = {bytes, frames, messages, InstallSnapshots left out}; the frames
  * stay in engine device memory until the next encode (rbe_wire_fetch). */
@@ -473,6 +479,23 @@ int rbe_wire_fetch(rbe_engine* e, void* out, uint64_t cap, rbe_wire_frame* frame
 int rbe_wire_decode(rbe_engine* e, const void* data, uint64_t bytes, rbe_message* msgs,
                     uint32_t cap, uint32_t* n_msgs, rbe_entry* ents, uint32_t ent_cap,
                     uint32_t* n_ents, uint8_t* cmd, uint64_t cmd_cap, uint64_t* cmd_bytes);
+/* The receive side of the transport on the device (replica mode, rep_world >
+ * 1): decode back-to-back frames as rbe_wire_decode does and deliver every
+ * message to the next rbe_step exactly as rbe_push_messages would — the
+ * records never come back to the host.  The group of a message is the one
+ * whose cluster id is its ClusterId (cid_base + g * cid_stride); a response
+ * from a node that is not a member is dropped (Peer.Handle, peer.go:186-198);
+ * a message for a replica not stepped here, a local message type or a bad
+ * entry is RBE_E_INVALID, a list over cfg.maxm messages, a sender over
+ * cfg.ecap entries or a full payload heap RBE_E_NOMEM, a bad frame
+ * RBE_E_CORRUPT — checked whole before anything is delivered.  All frames of
+ * one round come in one call (concatenated streams of several senders are
+ * fine); lists it does not name are empty.  Replaces transport.go:318-350
+ * handleRequest → node.handleReceivedMessages (node.go:1030-1067). */
+typedef struct rbe_wire_ingest_stats {
+  uint64_t frames, messages, dropped, entries, cmd_bytes, heap_bytes;
+} rbe_wire_ingest_stats;
+int rbe_wire_ingest(rbe_engine* e, const void* data, uint64_t bytes, rbe_wire_ingest_stats* st);
 /* The Cmd bytes of entries [lo, hi] of a replica's log, concatenated in `buf`:
  * entry lo + i occupies [offsets[i], offsets[i + 1]) (offsets has hi - lo + 2
  * slots and is filled even when `cap` is short, which returns RBE_E_NOMEM).

@@ -82,7 +82,7 @@ def session_frames_decode(make, device_decode=False):
     assert seen > 200 and ses > 50 and props > 5, (seen, ses, props)
 
 
-def session_over_transport(make, world):
+def session_over_transport(make, world, wire=False):
     """W engines, each stepping the replicas it owns, exchange every message
     (forwarded Proposes and Replicates with session entries and KiB Cmds
     included) through rbe_get_outbox / rbe_push_messages; the receiver stages
@@ -99,7 +99,7 @@ def session_over_transport(make, world):
         return plan_round(rng, n_rep, 3, rnd, None, False, 0.25, None, mixed_cmd,
                           session=True, props_only=True)
 
-    d, moved = run_transport(engs, ref, 3, 100, every=10, inputs=inputs)
+    d, moved = run_transport(engs, ref, 3, 100, every=10, inputs=inputs, wire=wire)
     assert d is None, f"first divergence {d}"
     assert moved > 300
     for e in engs:

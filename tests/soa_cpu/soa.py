@@ -7,7 +7,8 @@ import os
 
 from dragonboat_amd.engine import (CTR_NUM, COUNTER_NAMES, NodeInputs, RbeEntry, RbeMessage,
                                    RbeReplicaView, RbeUpdateCommit, RbeWireFrame, entry_cmds,
-                                   entry_fields, make_config, outbox_call, push_messages_call)
+                                   entry_fields, make_config, outbox_call, push_messages_call,
+                                   RbeWireIngestStats, wire_ingest_call)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _lib = None
@@ -30,7 +31,10 @@ def lib():
         L.soa_wire_encode.restype = C.c_int64
         L.soa_wire_encode.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
                                       C.POINTER(C.c_char_p), C.c_void_p, C.c_uint64,
-                                      C.POINTER(RbeWireFrame), C.POINTER(C.c_uint32)]
+                                      C.POINTER(RbeWireFrame), C.POINTER(C.c_uint32), C.c_int32]
+        L.soa_wire_ingest.restype = C.c_int
+        L.soa_wire_ingest.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64,
+                                      C.POINTER(RbeWireIngestStats)]
         L.soa_set_full_only.argtypes = [C.c_void_p, C.c_int]
         L.soa_set_staged.argtypes = [C.c_void_p, C.c_int]
         L.soa_slow_total.restype = C.c_uint64
@@ -200,7 +204,12 @@ class SoaCpu(NodeInputs):
         lib().soa_views(self.h, C.cast(arr, C.c_void_p))
         return arr
 
-    def wire_encode(self, deployment_id=0, bin_ver=0, groups_per_batch=0, source_address=()):
+    def wire_ingest(self, data):
+        """Host-build rbe_wire_ingest (Engine.wire_ingest)."""
+        return wire_ingest_call(lib().soa_wire_ingest, self.h, data)
+
+    def wire_encode(self, deployment_id=0, bin_ver=0, groups_per_batch=0, source_address=(),
+                    dst_rank=-1):
         """Host-build rbe_wire_encode + rbe_wire_fetch: (stream bytes, frames)."""
         addrs = (C.c_char_p * 6)(*[a.encode() for a in source_address])
         n = self.cfg.n_replicas
@@ -211,7 +220,7 @@ class SoaCpu(NodeInputs):
         cap = 1 << 24
         buf = C.create_string_buffer(cap)
         got = lib().soa_wire_encode(self.h, deployment_id, bin_ver, groups_per_batch, addrs, buf,
-                                    cap, fr, C.byref(nf))
+                                    cap, fr, C.byref(nf), dst_rank)
         assert got >= 0
         return buf.raw[:got], [fr[i] for i in range(nf.value)]
 

@@ -14,6 +14,7 @@
 #include "../../dragonboat_amd/csrc/rbe_snap.h"
 #include "../../dragonboat_amd/csrc/rbe_xchg.h"
 #include "../../dragonboat_amd/csrc/rbe_wire.h"
+#include "../../dragonboat_amd/csrc/rbe_ingest.h"
 #include "../../include/rbe.h"
 
 using namespace rbe;
@@ -58,6 +59,8 @@ static void run_round(SoaEngine* e, bool tick = true) {
     e->heap_head = hp.head;
     e->hin.apply_host(e->P, e->C);
     e->hin.clear();
+  } else {
+    e->hin.heap.settle();
   }
   if (e->C.iso_period && e->round > 0 && e->round % e->C.iso_period == 0)
     for (u64 g = 0; g < e->C.n_groups; g++) iso_group<N>(e->P, e->C, g, e->round);
@@ -495,7 +498,7 @@ int soa_get_update_commits(void* h, uint64_t first, uint64_t count, rbe_update_c
 // frames as rbe_wire_frame.  Returns total bytes (or -1 when cap is short).
 int64_t soa_wire_encode(void* h, uint64_t deployment_id, uint32_t bin_ver, uint32_t gpb,
                         const char* const* addr, uint8_t* out, uint64_t cap,
-                        rbe_wire_frame* frames, uint32_t* n_frames) {
+                        rbe_wire_frame* frames, uint32_t* n_frames, int32_t dst_rank) {
   SoaEngine* e = (SoaEngine*)h;
   const Params& C = e->C;
   const u32 N = C.n;
@@ -514,6 +517,8 @@ int64_t soa_wire_encode(void* h, uint64_t deployment_id, uint32_t bin_ver, uint3
       for (u64 g = g0; g < g1; g++) {
         u32 cm = 0, ci = 0, bad = 0;
         u32 b = 0;
+        if (N == 3 ? !wire_cell_sent<3>(C, dst_rank, g, k, d) : !wire_cell_sent<5>(C, dst_rank, g, k, d))
+          continue;
         const u8* hp = e->heap.data();
         const u64 hh = e->hin.heap.flushed;
         if (N == 3) b = wire_cell<3>(e->P, C, hp, hh, g, k, d, e->round, nullptr, &cm, &ci, &bad);
@@ -555,6 +560,140 @@ int64_t soa_wire_encode(void* h, uint64_t deployment_id, uint32_t bin_ver, uint3
   if (!buf.empty()) memcpy(out, buf.data(), buf.size());
   return (int64_t)buf.size();
 }
+
+}  // extern "C"
+
+// rbe_wire_ingest on the host build: frames checked and walked on the host
+// (the device's k_wire_verify / k_wire_bounds rules for well-formed streams),
+// messages parsed with the device's wire_message_get, then the same
+// ingest_check / ingest_sender functions the device kernels run, in the
+// order of a stable sort by list key.  stats6 as rbe_wire_ingest_stats.
+template <int N>
+static int soa_ingest_t(SoaEngine* e, const uint8_t* d, uint64_t bytes, uint64_t* st) {
+  const Params& C = e->C;
+  u32 table[256];
+  for (u32 i = 0; i < 256; i++) table[i] = crc_table_entry(i);
+  std::vector<std::pair<u64, u64>> pos;  // message bodies
+  for (u64 i = 0; i < bytes;) {
+    if (bytes - i < kWireHeader || d[i] != 0xAE || d[i + 1] != 0x7D) return RBE_E_CORRUPT;
+    u64 size = 0;
+    for (int b = 0; b < 8; b++) size = (size << 8) | d[i + 4 + b];
+    if (size == 0 || size > bytes - i - kWireHeader) return RBE_E_CORRUPT;
+    u8 hb[18];
+    memcpy(hb, d + i + 2, 18);
+    const u32 inc = ((u32)hb[10] << 24) | ((u32)hb[11] << 16) | ((u32)hb[12] << 8) | hb[13];
+    const u32 pc = ((u32)hb[14] << 24) | ((u32)hb[15] << 16) | ((u32)hb[16] << 8) | hb[17];
+    hb[10] = hb[11] = hb[12] = hb[13] = 0;
+    const u64 off = i + kWireHeader;
+    if (crc32_update(0, hb, 18, table) != inc || (((u32)hb[0] << 8) | hb[1]) != kWireMethod ||
+        crc32_update(0, d + off, size, table) != pc)
+      return RBE_E_CORRUPT;
+    WireRd rd{d + off, size, 0, false};
+    while (rd.i < size && !rd.bad) {
+      const u64 tag = rd.varint();
+      const u32 fn = (u32)(tag >> 3), wt = (u32)(tag & 7);
+      if (fn == 1 && wt == 2) {
+        const u64 l = rd.varint();
+        if (rd.bad || l > size - rd.i) return RBE_E_CORRUPT;
+        pos.emplace_back(off + rd.i, l);
+        rd.i += l;
+      } else {
+        rd.skip(wt);
+      }
+    }
+    if (rd.bad) return RBE_E_CORRUPT;
+    st[0]++;
+    i = off + size;
+  }
+  const u64 tm = pos.size();
+  std::vector<u64> ent0(tm + 1, 0), cmd0(tm + 1, 0);
+  for (u64 j = 0; j < tm; j++) {
+    WireRd rd{d, pos[j].first + pos[j].second, pos[j].first, false};
+    u64 cb = 0;
+    const u32 ne = wire_message_get(rd, pos[j].first + pos[j].second, nullptr, nullptr, nullptr, &cb);
+    if (rd.bad) return RBE_E_CORRUPT;
+    ent0[j + 1] = ent0[j] + ne;
+    cmd0[j + 1] = cmd0[j] + cb;
+  }
+  std::vector<rbe_message> msgs(tm);
+  std::vector<rbe_entry> ents(ent0[tm] + 1);
+  std::vector<u8> cmd(cmd0[tm] + 1);
+  for (u64 j = 0; j < tm; j++) {
+    WireRd rd{d, pos[j].first + pos[j].second, pos[j].first, false};
+    u64 cb = cmd0[j];
+    wire_message_get(rd, pos[j].first + pos[j].second, &msgs[j], ents.data() + ent0[j], cmd.data(),
+                     &cb);
+  }
+  st[1] = tm;
+  st[3] = ent0[tm];
+  st[4] = cmd0[tm];
+  if (!tm) return RBE_OK;
+  HostHeap& H = e->hin.heap;
+  std::vector<u64> key(tm), hb(tm);
+  u32 err = 0;
+  for (u64 j = 0; j < tm; j++) {
+    u32 x = 0;
+    key[j] = ingest_check<N>(C, H.cap, msgs[j], ents.data() + ent0[j], &x, &hb[j]);
+    err |= x;
+    if (!x && key[j] == ing_drop_key(C)) st[2]++;
+  }
+  if (err & ING_INVALID) return RBE_E_INVALID;
+  if (err & ING_NOMEM) return RBE_E_NOMEM;
+  std::vector<u32> sidx(tm);
+  for (u64 j = 0; j < tm; j++) sidx[j] = (u32)j;
+  std::stable_sort(sidx.begin(), sidx.end(), [&](u32 a, u32 b) { return key[a] < key[b]; });
+  std::vector<u64> skey(tm), hs(tm);
+  u64 need = 0;
+  for (u64 p = 0; p < tm; p++) {
+    skey[p] = key[sidx[p]];
+    hs[p] = need;
+    need += hb[sidx[p]];
+  }
+  auto walk = [&](bool write, u64 base) {
+    u32 x = 0;
+    for (u64 p = 0; p < tm; p++) {
+      if (!ingest_run_start(C, skey.data(), p)) continue;
+      const u64 q = ingest_run_end(C, skey.data(), p, tm);
+      if (write)
+        x |= ingest_sender<N, true>(e->P, C, (e->round - 1) & 1u, e->round, skey.data(),
+                                    sidx.data(), p, q, msgs.data(), ents.data(), ent0.data(),
+                                    cmd0.data(), cmd.data(), e->heap.data(), H.cap, base, hs.data());
+      else
+        x |= ingest_sender<N, false>(e->P, C, (e->round - 1) & 1u, e->round, skey.data(),
+                                     sidx.data(), p, q, msgs.data(), ents.data(), ent0.data(),
+                                     cmd0.data(), cmd.data(), nullptr, H.cap, base, hs.data());
+    }
+    return x;
+  };
+  if (walk(false, 0)) return RBE_E_NOMEM;
+  st[5] = need;
+  u64 base = 0;
+  if (need) {
+    for (u64 p = H.flushed; p < H.head; p++) e->heap[p % H.cap] = H.stage[p - H.flushed];
+    const u64 skip = H.head % H.cap + need > H.cap ? H.cap - H.head % H.cap : 0;
+    const int rc = H.room(need + skip);
+    if (rc) return rc;
+    if (H.flushed < H.round_lo) H.round_lo = H.flushed;
+    H.stage.clear();
+    base = H.head + skip;
+    H.head = base + need;
+    H.flushed = H.head;
+    e->heap_head = H.head;
+  }
+  walk(true, base);
+  return RBE_OK;
+}
+extern "C" int soa_wire_ingest(void* h, const uint8_t* data, uint64_t bytes, uint64_t* stats6) {
+  SoaEngine* e = (SoaEngine*)h;
+  memset(stats6, 0, 6 * sizeof(u64));
+  if (e->round == 0) return RBE_E_INVALID;
+  if (e->C.rep_world <= 1) return RBE_E_STATE;
+  if (e->C.n == 3) return soa_ingest_t<3>(e, data, bytes, stats6);
+  if (e->C.n == 5) return soa_ingest_t<5>(e, data, bytes, stats6);
+  return soa_ingest_t<1>(e, data, bytes, stats6);
+}
+
+extern "C" {
 
 void soa_snapshot_state(void* h, uint64_t* out6) {
   SoaEngine* e = (SoaEngine*)h;

@@ -43,10 +43,35 @@ def deliver(engs, n, n_rep):
     return moved
 
 
-def run_transport(engs, ref, n, rounds, every=25, inputs=None):
+def encode_for(e, rank):
+    """The wire stream of engine e's last round for the replicas of `rank`
+    (rbe_wire_encode with dst_rank + rbe_wire_fetch, or the host build's twin)."""
+    if hasattr(e, "wire_fetch"):
+        data, _ = e.wire_fetch(e.wire_encode(dst_rank=rank))
+    else:
+        data, _ = e.wire_encode(dst_rank=rank)
+    return data
+
+
+def deliver_wire(engs):
+    """One transport hop as bytes: every engine encodes, per destination
+    engine, the MessageBatch frames of its owned senders (rbe_wire_encode),
+    and each destination takes the concatenated streams of all its sources in
+    one rbe_wire_ingest, on the device.  Returns (messages moved, bytes)."""
+    moved = nbytes = 0
+    for rank, e in enumerate(engs):
+        data = b"".join(encode_for(src, rank) for r2, src in enumerate(engs) if r2 != rank)
+        st = e.wire_ingest(data)
+        moved += st["messages"] - st["dropped"]
+        nbytes += len(data)
+    return moved, nbytes
+
+
+def run_transport(engs, ref, n, rounds, every=25, inputs=None, wire=False):
     """Step W engines and the oracle in lockstep with a transport hop after
-    each round; compare every owned replica with the oracle every `every`
-    rounds.  `inputs(rnd)` returns host input ops for the round (input_util
+    each round (wire=True: as encoded frames through rbe_wire_ingest, else
+    through rbe_get_outbox / rbe_push_messages); compare every owned replica
+    with the oracle every `every` rounds.  `inputs(rnd)` returns host input ops for the round (input_util
     plan_round form), applied to the owning engine and the oracle.  Returns
     (first divergence or None, messages moved)."""
     from input_util import apply_engine, apply_oracle
@@ -62,7 +87,7 @@ def run_transport(engs, ref, n, rounds, every=25, inputs=None):
         for e in engs:
             e.step()
         ref.step()
-        moved += deliver(engs, n, n_rep)
+        moved += deliver_wire(engs)[0] if wire else deliver(engs, n, n_rep)
         if done % every and done != rounds:
             continue
         hv = ref.views()
