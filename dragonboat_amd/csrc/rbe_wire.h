@@ -253,7 +253,7 @@ RBE_HD u32 crc32_update(u32 crc, const u8* p, u64 n, const u32* table) {
   for (u64 i = 0; i < n; i++) c = table[(c ^ p[i]) & 0xFFu] ^ (c >> 8);
   return ~c;
 }
-RBE_HD u32 crc_multmodp(u32 a, u32 b) {
+RBE_HD constexpr u32 crc_multmodp(u32 a, u32 b) {
   u32 m = 1u << 31, p = 0;
   for (;;) {
     if (a & m) {
@@ -265,11 +265,17 @@ RBE_HD u32 crc_multmodp(u32 a, u32 b) {
   }
   return p;
 }
-// x2n[k] = x^(2^k) mod P
-RBE_HD void crc_x2n_table(u32* x2n) {
-  x2n[0] = 1u << 30;
-  for (int k = 1; k < 32; k++) x2n[k] = crc_multmodp(x2n[k - 1], x2n[k - 1]);
+// x2n[k] = x^(2^k) mod P, evaluated at compile time
+struct CrcX2n {
+  u32 v[32];
+};
+constexpr CrcX2n crc_x2n_make() {
+  CrcX2n t{};
+  t.v[0] = 1u << 30;
+  for (int k = 1; k < 32; k++) t.v[k] = crc_multmodp(t.v[k - 1], t.v[k - 1]);
+  return t;
 }
+static constexpr CrcX2n kCrcX2n = crc_x2n_make();
 RBE_HD u32 crc32_combine(u32 crc1, u32 crc2, u64 len2, const u32* x2n) {
   u32 p = 1u << 31;  // x^(8 len2) mod P
   u32 k = 3;

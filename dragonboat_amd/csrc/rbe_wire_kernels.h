@@ -252,31 +252,38 @@ __device__ __forceinline__ void crc_tables_lds(u32* t) {
   }
 }
 
-// crc32 of [p, p + n) by this block: one contiguous segment per thread, the
-// segments' crcs combined pairwise in LDS
+// crc32 of [p, p + n) by this block: one contiguous segment per thread.
+// crc32_combine(c1, c2, l2) = c1 · x^(8 l2) ^ c2 is linear, so the whole
+// crc is the XOR over segments of each segment's crc shifted to the end,
+// c_t · x^(8 (n - hi_t)): every lane shifts its own crc (a few multmodp over
+// the set bits of its distance to the end) and the block XOR-reduces, with no
+// serial combine tree.
 __device__ u32 block_crc32(const u8* p, u64 n, const u32* table, const u32* x2n, u32* s_crc) {
   const u32 T = blockDim.x, t = threadIdx.x;
   const u64 seg = (n + T - 1) / T;
   const u64 lo = seg * t < n ? seg * t : n;
   const u64 hi = lo + seg < n ? lo + seg : n;
-  s_crc[t] = crc32_words(0, p + lo, hi - lo, table);
-  __syncthreads();
-  // tree: combine (i, i + s) with the length of segment group i + s
-  for (u32 s = 1; s < T; s <<= 1) {
-    if ((t % (2 * s)) == 0 && t + s < T) {
-      const u64 l2lo = seg * (t + s) < n ? seg * (t + s) : n;
-      const u64 l2hi = seg * (t + 2 * s) < n ? seg * (t + 2 * s) : n;
-      s_crc[t] = crc32_combine(s_crc[t], s_crc[t + s], l2hi - l2lo, x2n);
-    }
-    __syncthreads();
+  u32 c = crc32_words(0, p + lo, hi - lo, table);
+  u64 rest = n - hi;
+  if (c && rest) {
+    u32 sh = 1u << 31;  // x^(8 rest) mod P
+    for (u32 k = 3; rest; rest >>= 1, k++)
+      if (rest & 1u) sh = crc_multmodp(x2n[k & 31], sh);
+    c = crc_multmodp(sh, c);
   }
-  return s_crc[0];
+  for (int o = 32; o; o >>= 1) c ^= __shfl_xor(c, o, 64);
+  if ((t & 63u) == 0) s_crc[t >> 6] = c;
+  __syncthreads();
+  u32 r = 0;
+  for (u32 w = 0; w < T / 64; w++) r ^= s_crc[w];
+  __syncthreads();
+  return r;
 }
 
 __global__ __launch_bounds__(256) void k_wire_crc(WireBufs B, u8* out) {
   __shared__ u32 s_table[1024], s_x2n[32], s_crc[256];
   crc_tables_lds(s_table);
-  if (threadIdx.x == 0) crc_x2n_table(s_x2n);
+  if (threadIdx.x < 32) s_x2n[threadIdx.x] = kCrcX2n.v[threadIdx.x];
   __syncthreads();
   const WireFrame f = B.frames[blockIdx.x];
   u8* fp = out + f.offset;
@@ -300,7 +307,7 @@ struct WireIn {  // one inbound frame
 __global__ __launch_bounds__(256) void k_wire_verify(const u8* data, WireIn* fr) {
   __shared__ u32 s_table[1024], s_x2n[32], s_crc[256];
   crc_tables_lds(s_table);
-  if (threadIdx.x == 0) crc_x2n_table(s_x2n);
+  if (threadIdx.x < 32) s_x2n[threadIdx.x] = kCrcX2n.v[threadIdx.x];
   __syncthreads();
   WireIn f = fr[blockIdx.x];
   const u32 c = block_crc32(data + f.offset, f.size, s_table, s_x2n, s_crc);
