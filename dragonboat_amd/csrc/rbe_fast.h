@@ -68,6 +68,31 @@ __device__ __forceinline__ unsigned long long rbe_rstamp() {
 #define RBE_PHASE_ADD(role, i, a, b)
 #endif
 
+// Outbound messages staged in LDS (k_fast_both, RBE_MSG_STAGE): send() puts
+// a message's 64 B in the lane's next LDS slot and its destination beside it,
+// and after the step the wave writes every staged message back cooperatively,
+// four lanes per message: one 64-B write request per message instead of four
+// scattered 16-B ones (messages are over half of the fast kernel's write
+// requests on C4).  LDS writes count in lgkmcnt, so staging never waits
+// behind the lane's stores.  A lane with more than kMsgStage messages in one
+// step writes the rest directly.  Device build only; the host build always
+// writes directly.
+#ifndef RBE_MSG_STAGE
+#define RBE_MSG_STAGE 0
+#endif
+constexpr u32 kMsgStage = 2;
+constexpr u32 kMsgStageLanes = 256;  // one slot row per thread of a 256-thread block
+#if defined(__HIPCC__) || defined(__HIP__)
+__device__ __forceinline__ Msg (&msg_stage_slots())[kMsgStage][kMsgStageLanes] {
+  __shared__ Msg s_slots[kMsgStage][kMsgStageLanes];
+  return s_slots;
+}
+__device__ __forceinline__ u32 (&msg_stage_dst())[kMsgStage][kMsgStageLanes] {
+  __shared__ u32 s_dst[kMsgStage][kMsgStageLanes];
+  return s_dst;
+}
+#endif
+
 // Wait until every outstanding load of the lane has returned (a no-op on the
 // host build).  Placed between the gather and the first store of a fast step.
 RBE_HD void rbe_wait_all_loads() {
@@ -186,6 +211,8 @@ struct FastOut {
   // bump, which puts the counter array in scratch memory — and a scratch
   // reload after the lane's first store waits for every store before it
   u32 fault0, n_out, n_drop_msg, n_ent_out;
+  u32 n_staged;  // messages staged in LDS this step (msg_stage)
+  bool msg_stage;
   u32 events;  // EV_* of the step (Upd::events)
 
   RBE_HD u32 get_pc(u32 d) const {
@@ -257,7 +284,18 @@ struct FastOut {
       add_pc(d, 1u << 7);
     }
 #ifndef RBE_DIAG_NO_MSG_STORES
-    P.msgs[par][((g * N + k) * N + d) * (u64)C.maxm + slot] = m;
+    const u64 at = ((g * N + k) * N + d) * (u64)C.maxm + slot;
+    Msg* to = &P.msgs[par][at];
+#if defined(__HIP_DEVICE_COMPILE__)
+    // one store path either way (a generic pointer into LDS or HBM): two
+    // store paths at every inlined send site cost registers and code
+    if (msg_stage && n_staged < kMsgStage) {  // `at` fits 32 bits (rbe_create checks)
+      msg_stage_dst()[n_staged][threadIdx.x] = (u32)at;
+      to = &msg_stage_slots()[n_staged][threadIdx.x];
+      n_staged++;
+    }
+#endif
+    *to = m;
 #endif
   }
   RBE_HD void dropped_read_index(const Planes& P, const Params& C, StepCounters& ctr, u64 low,
@@ -534,9 +572,9 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
 //   inbox (ascending sender; Quiesce marker, then the sender's messages) →
 //   local ReadIndex → tick → proposal, each followed by the deferred fan-out
 //   (Replicate sends in ascending slot order, heartbeats, readIndex confirm).
-template <int N, bool TRACE, int STG = 0, bool AUX = false>
+template <int N, bool TRACE, int STG = 0, bool AUX = false, bool MSG = false>
 RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, StepCounters& ctr,
-                      StageRow<N>* sr = nullptr, u32 aux = 0) {
+                      StageRow<N>* sr = nullptr, u32 aux = 0, u32* staged = nullptr) {
   const u32 round = ck.round;
   using Cap = FastCaps<N>;
   constexpr u32 Q = N / 2 + 1;
@@ -761,6 +799,8 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   o.g = g;
   o.k = k;
   o.par = par;
+  o.n_staged = 0;
+  o.msg_stage = MSG;
   o.self = k + 1;
   o.round_ = round;
   o.iso = round < until ? isom : (u8)0;
@@ -1232,6 +1272,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   c.rq_count = (u8)rq_n;
   fast_finish<N, TRACE, STG>(P, C, ctr, o, q, R_Leader, flags, h, c, etick, htick, committed0,
                                 digest0, sr, cdirty);
+  if constexpr (MSG) *staged = o.n_staged;
   RBE_STAMP(t5);
   RBE_RSTAMP(rt5);
   RBE_PHASE_ADD(0, 5, rt0, rt5);
@@ -1250,9 +1291,9 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
 // One steady-state follower round: inbox from the known leader only
 // (Replicate / Heartbeat / ReadIndexResp of the current term), no client
 // input, a tick that does not start an election.
-template <int N, bool TRACE, int STG = 0, bool AUX = false>
+template <int N, bool TRACE, int STG = 0, bool AUX = false, bool MSG = false>
 RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, StepCounters& ctr,
-                      StageRow<N>* sr = nullptr, u32 aux = 0) {
+                      StageRow<N>* sr = nullptr, u32 aux = 0, u32* staged = nullptr) {
   const u32 round = ck.round;
   using Cap = FastCaps<N>;
   if constexpr (N < 3) {
@@ -1433,6 +1474,8 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   o.g = g;
   o.k = k;
   o.par = par;
+  o.n_staged = 0;
+  o.msg_stage = MSG;
   o.self = k + 1;
   o.round_ = round;
   o.iso = round < until ? isom : (u8)0;
@@ -1576,6 +1619,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   c.leader = n_in ? (u8)lid : c.leader;
   fast_finish<N, TRACE, STG>(P, C, ctr, o, q, R_Follower, flags, h, c, etick, htick, committed0,
                         digest0, sr, cdirty);
+  if constexpr (MSG) *staged = o.n_staged;
   RBE_STAMP(t5);
   RBE_RSTAMP(rt5);
   RBE_PHASE_ADD(1, 5, rt0, rt5);
@@ -1590,12 +1634,12 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
 }
 
 // the fast step of one role (k_round, k_fast_list)
-template <int N, bool TRACE, int MODE, int STG = 0, bool AUX = false>
+template <int N, bool TRACE, int MODE, int STG = 0, bool AUX = false, bool MSG = false>
 RBE_HD bool step_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, StepCounters& ctr,
-                      StageRow<N>* sr = nullptr, u32 aux = 0) {
+                      StageRow<N>* sr = nullptr, u32 aux = 0, u32* staged = nullptr) {
   if constexpr (MODE == MODE_LEAD)
-    return lead_fast<N, TRACE, STG, AUX>(P, C, r, ck, ctr, sr, aux);
-  else return foll_fast<N, TRACE, STG, AUX>(P, C, r, ck, ctr, sr, aux);
+    return lead_fast<N, TRACE, STG, AUX, MSG>(P, C, r, ck, ctr, sr, aux, staged);
+  else return foll_fast<N, TRACE, STG, AUX, MSG>(P, C, r, ck, ctr, sr, aux, staged);
 }
 
 }  // namespace rbe

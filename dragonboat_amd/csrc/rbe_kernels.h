@@ -45,6 +45,13 @@ static constexpr int kBlock = 256;
 #endif
 // how the fast steps of k_fast_both use wave-staged rows (StageRow, rbe_fast.h):
 // 0 = direct, 1 = STG_OUT (row writes staged), 3 = STG_OUT | STG_IN
+#ifndef RBE_FULL_SORT
+#define RBE_FULL_SORT 0  // measured: no change on C3 (263 vs 264 us)
+#endif
+#ifndef RBE_FULL_DEFER
+#define RBE_FULL_DEFER 1
+#endif
+static constexpr int kFullMode = RBE_FULL_DEFER ? MODE_FULL_DEFER : MODE_FULL;
 #ifndef RBE_STAGE_LEAD
 #define RBE_STAGE_LEAD 0
 #endif
@@ -731,6 +738,36 @@ __device__ __forceinline__ void stage_out_wave(const Planes& P, const StageRow<N
   }
 }
 
+// Write back the messages the wave's lanes staged in LDS (FastOut::send with
+// msg_stage): the wave lists its staged (lane, slot) pairs in lane order, then
+// four consecutive lanes move one 64-B message, 16 messages per instruction.
+__device__ __forceinline__ void msg_stage_flush(Msg* out, u32 staged) {
+  __shared__ u8 s_list[kMsgStageLanes * kMsgStage];
+  const u32 lane = threadIdx.x & 63u, w0 = threadIdx.x & ~63u;
+  const u64 below = (1ull << lane) - 1ull;
+  u32 pre = 0, tot = 0;
+#pragma unroll
+  for (u32 b = 0; (1u << b) <= kMsgStage; b++) {
+    const u64 m = __ballot((staged >> b) & 1u);
+    pre += (u32)__popcll(m & below) << b;
+    tot += (u32)__popcll(m) << b;
+  }
+  if (tot == 0) return;
+  u8* lst = &s_list[w0 * kMsgStage];
+  for (u32 j = 0; j < staged; j++) lst[pre + j] = (u8)(lane | (j << 6));
+  wave_lds_sync();
+  for (u32 b0 = 0; b0 < tot; b0 += 16) {
+    const u32 mi = b0 + (lane >> 2), q = lane & 3u;
+    if (mi < tot) {
+      const u32 e = lst[mi];
+      const u32 t = w0 + (e & 63u), j = e >> 6;
+      const uint4 v = reinterpret_cast<const uint4*>(&msg_stage_slots()[j][t])[q];
+      reinterpret_cast<uint4*>(out + msg_stage_dst()[j][t])[q] = v;
+    }
+  }
+  wave_lds_sync();  // the slots are free for the wave's next items
+}
+
 // Pass 2, merged (RBE_MODE=both, the default): the round's steady-state
 // leaders and followers in one launch, so the two roles' waves share the SIMDs
 // instead of running back to back; item i < n_lead is a leader, the rest
@@ -801,10 +838,15 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, 
         stage_in_wave<N>(P, wrows, r, m_in, (SL & STG_IN) ? m_lead : 0ull);
         wave_lds_sync();
       }
+      u32 staged = 0;
+      constexpr bool ML = (RBE_MSG_STAGE & 2) != 0, MF = (RBE_MSG_STAGE & 1) != 0;
       if (lead)
-        ok = step_fast<N, TRACE, MODE_LEAD, SL, kListAux<N>>(P, C, r, ck, c, mine, aux);
+        ok = step_fast<N, TRACE, MODE_LEAD, SL, kListAux<N>, ML>(P, C, r, ck, c, mine, aux,
+                                                                &staged);
       else if (any)
-        ok = step_fast<N, TRACE, MODE_FOLL, SF, kListAux<N>>(P, C, r, ck, c, mine, aux);
+        ok = step_fast<N, TRACE, MODE_FOLL, SF, kListAux<N>, MF>(P, C, r, ck, c, mine, aux,
+                                                                &staged);
+      if constexpr (RBE_MSG_STAGE != 0) msg_stage_flush(P.msgs[par], staged);
       if constexpr ((SL | SF) != 0) {
         wave_lds_sync();
         const u64 m_ok = __ballot(ok) & m_out;
@@ -829,10 +871,53 @@ __global__ __launch_bounds__(kBlock) void k_full_list(Planes P, Params C, RoundA
   StepCounters c;
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
+#if RBE_FULL_SORT
+  // Block-local class sort: the general step's time is set by its slowest
+  // lanes, and a wave whose lanes take different handlers runs every handler's
+  // path in turn.  Each block takes 256 items, orders them by (role, any
+  // inbound message) with an LDS counting sort, and steps them in that order,
+  // so a wave mostly holds one kind of step (campaigns, vote tallies, replies).
+  __shared__ u32 s_hist[16], s_sorted[kBlock];
+  for (u64 b0 = (u64)blockIdx.x * kBlock; b0 < n; b0 += (u64)gridDim.x * kBlock) {
+    const u64 i = b0 + threadIdx.x;
+    u32 r = ~0u, cls = 15;
+    if (i < n) {
+      const u32 sg = seg_find<kShards>(s_pre, (u32)i);
+      r = L.idx[list_pos(L, 2, sg, false, (u32)i - s_pre[sg])];
+      const u64 g = r / N;
+      const u32 k = (u32)(r % N);
+      u32 inb = 0;
+#pragma unroll
+      for (u32 s = 0; s < N; s++)
+        if (s != k) inb |= in_word<N>(P, g, s, k, round);
+      cls = (idle_role(P.idle[r]) << 1) | (inb != 0 ? 1u : 0u);
+    }
+    if (threadIdx.x < 16) s_hist[threadIdx.x] = 0;
+    __syncthreads();
+    const u32 rank = atomicAdd(&s_hist[cls], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      u32 acc = 0;
+      for (u32 q = 0; q < 16; q++) {
+        const u32 v = s_hist[q];
+        s_hist[q] = acc;
+        acc += v;
+      }
+    }
+    __syncthreads();
+    s_sorted[s_hist[cls] + rank] = r;
+    __syncthreads();
+    const u32 rr = s_sorted[threadIdx.x];
+    if (rr != ~0u) step_replica<N, TRACE, kFullMode>(P, C, rr, ck, c);
+    __syncthreads();
+  }
+#else
   for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock) {
     const u32 sg = seg_find<kShards>(s_pre, (u32)i);
-    step_replica<N, TRACE>(P, C, L.idx[list_pos(L, 2, sg, false, (u32)i - s_pre[sg])], ck, c);
+    step_replica<N, TRACE, kFullMode>(P, C, L.idx[list_pos(L, 2, sg, false, (u32)i - s_pre[sg])],
+                                      ck, c);
   }
+#endif
   flush_counters<KS_FULL>(P, c);
 }
 

@@ -270,11 +270,33 @@ struct StepCounters {
 };
 
 // ----------------------------------------------------------------- the lane
-enum : int { MODE_FULL = 0, MODE_LEAD = 1, MODE_FOLL = 2 };
+enum : int { MODE_FULL = 0, MODE_LEAD = 1, MODE_FOLL = 2, MODE_FULL_DEFER = 3 };
+
+// Deferred message stores of the general step (MODE_FULL_DEFER, k_full_list):
+// send() keeps up to kLaneDefer messages of the lane in LDS and the step
+// writes them after everything else.  On CDNA vmcnt counts loads and stores
+// in order, so a load issued after a store also waits for that store: the
+// handler table interleaves sends with later inbox, ring and arena reads, and
+// every such read would otherwise pay for the messages sent before it.
+constexpr u32 kLaneDefer = 6;
+// entries per batch of the general step's entry loops (Lane::copy_ring_to_arena,
+// on_replicate): loads of a batch are issued together, then its stores
+constexpr u32 kEntBatch = 8;
+#if defined(__HIPCC__) || defined(__HIP__)
+__device__ __forceinline__ Msg (&lane_defer_msgs())[kLaneDefer][256] {
+  __shared__ Msg s_msgs[kLaneDefer][256];
+  return s_msgs;
+}
+__device__ __forceinline__ u64 (&lane_defer_dst())[kLaneDefer][256] {
+  __shared__ u64 s_dst[kLaneDefer][256];
+  return s_dst;
+}
+#endif
 
 template <int N, bool TRACE, int MODE>
 struct Lane {
-  static constexpr bool FULL = MODE == MODE_FULL;  // the whole handler table
+  static constexpr bool FULL = MODE == MODE_FULL || MODE == MODE_FULL_DEFER;  // the whole handler table
+  static constexpr bool DEFER = MODE == MODE_FULL_DEFER;  // sends kept in LDS until the end
   static constexpr bool LEAD = MODE == MODE_LEAD;  // steady-state leader subset
   static constexpr bool FOLL = MODE == MODE_FOLL;  // steady-state follower subset
   const Planes& P;
@@ -284,6 +306,7 @@ struct Lane {
   const u32 k;      // slot; node id = k + 1
   const u32 round;
   const u32 par;    // round & 1: outbox buffer written this round
+  u32 n_defer = 0;  // sends held in LDS (DEFER)
   const Clk clk;    // round, ticks before it, whether it ticks
   const u64 cid;
   const u8 self;    // node id
@@ -356,6 +379,22 @@ struct Lane {
     return P.term_ring[ring_slot(idx)];
   }
   RBE_HD bool match_term(u64 idx, u64 t) { return log_term(idx) == t; }  // logentry.go:357-363
+  // log_term split for batched lookups: the value without side effects (a
+  // prefetch that may run ahead of the loop that uses it), and the fault and
+  // ring-access count log_term would have raised for it
+  RBE_HD u64 log_term_peek(u64 idx) const {
+    if (idx > last || idx == 0) return 0;
+    if (idx == last) return t_last;
+    if (C.snapshot_entries && idx <= marker) return idx == marker ? marker_term : 0;
+    if (last - idx >= C.ring) return 0;
+    return P.term_ring[ring_slot(idx)];
+  }
+  RBE_HD void log_term_account(u64 idx) {
+    if (idx > last || idx == 0 || idx == last) return;
+    if (C.snapshot_entries && idx <= marker) return;
+    if (last - idx >= C.ring) set_fault(F_WINDOW);
+    else ctr.v[C_RING_ACCESS]++;
+  }
   RBE_HD bool up_to_date(u64 idx, u64 t) {  // logentry.go:365-377
     u64 lt = log_term(last);
     if (t >= lt) {
@@ -589,9 +628,30 @@ struct Lane {
       slot = C.maxm - 1u - b;
       add_pc(d, 1u << 7);
     }
-    P.msgs[par][msg_slot_base(k, d) + slot] = m;
+    const u64 at = msg_slot_base(k, d) + slot;
     ctr.v[C_MSG_OUT]++;
     ctr.v[C_ENT_OUT] += m.n_ent;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (DEFER) {
+      if (n_defer < kLaneDefer) {
+        lane_defer_msgs()[n_defer][threadIdx.x] = m;
+        lane_defer_dst()[n_defer][threadIdx.x] = at;
+        n_defer++;
+        return;
+      }
+    }
+#endif
+    P.msgs[par][at] = m;
+  }
+  // the deferred sends, after every other access of the step
+  RBE_HD void flush_deferred() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (DEFER) {
+      for (u32 j = 0; j < n_defer; j++)
+        P.msgs[par][lane_defer_dst()[j][threadIdx.x]] = lane_defer_msgs()[j][threadIdx.x];
+      n_defer = 0;
+    }
+#endif
   }
   RBE_HD Msg mk(u32 type, u8 to) const {
     Msg m;
@@ -605,6 +665,32 @@ struct Lane {
     m.pad1 = 0;
     m.term = m.log_term = m.log_index = m.commit = m.hint = m.hint_high = 0;
     return m;
+  }
+  // log entries [lo, lo + cnt) from the ring to `out`, kEntBatch at a time
+  // (every load of a batch before its stores)
+  RBE_HD void copy_ring_to_arena(u64 lo, u32 cnt, Ent* out) {
+    for (u32 i0 = 0; i0 < cnt; i0 += kEntBatch) {
+      Ent e[kEntBatch];
+#pragma unroll
+      for (u32 j = 0; j < kEntBatch; j++) {
+        if (i0 + j >= cnt) continue;
+        const u64 idx = lo + i0 + j;
+        if (last - idx >= C.ring) set_fault(F_WINDOW);
+        const u64 s = ring_slot(idx);
+        const Body b = P.pay_ring[s];
+        e[j].term = P.term_ring[s];
+        e[j].type = b.type;
+        e[j].len = b.len;
+        e[j].lo = b.lo;
+        e[j].hi = b.hi;
+      }
+#pragma unroll
+      for (u32 j = 0; j < kEntBatch; j++) {
+        if (i0 + j >= cnt) continue;
+        if (heap_lapped(P, C, e[j].type, e[j].hi)) set_fault(F_WINDOW);
+        out[i0 + j] = e[j];
+      }
+    }
   }
   // copy log entries [lo, lo+cnt) into this round's arena (reusing the last
   // copied segment when it already covers them); returns the arena offset
@@ -621,20 +707,7 @@ struct Lane {
         set_fault(F_ARENA);
         return false;
       }
-      for (u32 i = 0; i < extra; i++) {
-        u64 idx = have_hi + i;
-        if (last - idx >= C.ring) set_fault(F_WINDOW);
-        u64 s = ring_slot(idx);
-        Body b = P.pay_ring[s];
-        if (heap_lapped(P, C, b.type, b.hi)) set_fault(F_WINDOW);
-        Ent e;
-        e.term = P.term_ring[s];
-        e.type = b.type;
-        e.len = b.len;
-        e.lo = b.lo;
-        e.hi = b.hi;
-        a[arena_used + i] = e;
-      }
+      copy_ring_to_arena(have_hi, extra, a + arena_used);
       ctr.v[C_RING_ACCESS] += extra;
       arena_used += extra;
       seg_len += extra;
@@ -645,20 +718,7 @@ struct Lane {
       set_fault(F_ARENA);
       return false;
     }
-    for (u32 i = 0; i < cnt; i++) {
-      u64 idx = lo + i;
-      if (last - idx >= C.ring) set_fault(F_WINDOW);
-      u64 s = ring_slot(idx);
-      Body b = P.pay_ring[s];
-      if (heap_lapped(P, C, b.type, b.hi)) set_fault(F_WINDOW);
-      Ent e;
-      e.term = P.term_ring[s];
-      e.type = b.type;
-      e.len = b.len;
-      e.lo = b.lo;
-      e.hi = b.hi;
-      a[arena_used + i] = e;
-    }
+    copy_ring_to_arena(lo, cnt, a + arena_used);
     ctr.v[C_RING_ACCESS] += cnt;
     seg_lo = lo;
     seg_off = arena_used;
@@ -1130,14 +1190,31 @@ struct Lane {
     }
     if (match_term(m.log_index, m.log_term)) {
       // tryAppend (logentry.go:291-302) / getConflictIndex (315-322)
+      // The lookups go in batches of kEntBatch: all loads of a batch are
+      // issued before any is used, instead of one dependent round trip per entry
       u64 conflict = 0;
       u32 ci = 0;
-      for (u32 i = 0; i < m.n_ent; i++) {
-        u64 idx = m.log_index + 1 + i;
-        if (!match_term(idx, ents[i].term)) {
-          conflict = idx;
-          ci = i;
-          break;
+      for (u32 i0 = 0; i0 < m.n_ent && conflict == 0; i0 += kEntBatch) {
+        u64 et[kEntBatch], lt[kEntBatch];
+#pragma unroll
+        for (u32 j = 0; j < kEntBatch; j++) {
+          et[j] = lt[j] = 0;
+          if (i0 + j < m.n_ent) {
+            et[j] = ents[i0 + j].term;
+            lt[j] = log_term_peek(m.log_index + 1 + i0 + j);
+          }
+        }
+#pragma unroll
+        for (u32 j = 0; j < kEntBatch; j++) {
+          const u32 i = i0 + j;
+          if (conflict == 0 && i < m.n_ent) {
+            const u64 idx = m.log_index + 1 + i;
+            log_term_account(idx);
+            if (lt[j] != et[j]) {
+              conflict = idx;
+              ci = i;
+            }
+          }
         }
       }
       if (conflict != 0) {
@@ -1148,13 +1225,25 @@ struct Lane {
           // truncate-and-append; savedTo = min(savedTo, first-1)
           if (conflict - 1 >= 1 && conflict - 1 <= last && log_term(conflict - 1) > ents[ci].term)
             set_fault(F_PANIC);
-          for (u32 i = ci; i < m.n_ent; i++) {
-            ring_put(m.log_index + 1 + i, ents[i].term, ents[i].type, ents[i].len, ents[i].lo,
-                     ents[i].hi);
-            note_cc(ents[i].type);
+          // batched: a batch's entries are loaded before any ring store, so no
+          // load waits behind the stores of earlier entries (vmcnt is in order)
+          u64 tl = 0;
+          for (u32 i0 = ci; i0 < m.n_ent; i0 += kEntBatch) {
+            Ent e[kEntBatch];
+#pragma unroll
+            for (u32 j = 0; j < kEntBatch; j++)
+              if (i0 + j < m.n_ent) e[j] = ents[i0 + j];
+#pragma unroll
+            for (u32 j = 0; j < kEntBatch; j++) {
+              if (i0 + j < m.n_ent) {
+                ring_put(m.log_index + 1 + i0 + j, e[j].term, e[j].type, e[j].len, e[j].lo, e[j].hi);
+                note_cc(e[j].type);
+                tl = e[j].term;
+              }
+            }
           }
           last = m.log_index + m.n_ent;
-          t_last = ents[m.n_ent - 1].term;
+          t_last = tl;
           saved_to = umin64(saved_to, conflict - 1);
           if (C.ext_commit && conflict <= P.imark[r]) P.imark[r] = conflict;
           seg_len = 0;
@@ -2251,10 +2340,11 @@ RBE_HD void Lane<N, TRACE, MODE>::raft_tick() {  // raft.go:551-564
 }
 
 // the full handler table: always completes the round
-template <int N, bool TRACE>
+template <int N, bool TRACE, int MODE = MODE_FULL>
 RBE_HD void step_replica(const Planes& P, const Params& C, u64 r, Clk ck, StepCounters& ctr) {
-  Lane<N, TRACE, MODE_FULL> lane(P, C, r, ck, ctr);
+  Lane<N, TRACE, MODE> lane(P, C, r, ck, ctr);
   lane.run();
+  lane.flush_deferred();
 }
 // the steady-state subset: returns false (nothing written) when the round
 // needs the full table
