@@ -240,7 +240,10 @@ def run_replica_mode(args, ws, rank, local, dist, dev, gloo_staged):
 
     def rounds(k, timed_xchg=None):
         for _ in range(k):
-            eng.step()
+            if xch is not None:
+                xch.step()
+            else:
+                eng.step()
             if xch is not None:
                 if timed_xchg is not None:
                     eng.sync()
@@ -286,6 +289,8 @@ def run_replica_mode(args, ws, rank, local, dist, dev, gloo_staged):
     eng.reset_counters()
     kms = [0.0] * 4
     for _ in range(prof_rounds):
+        if xch is not None:
+            xch.iso_sync()
         for i, v in enumerate(eng.profile_rounds(1)):
             kms[i] += v
         if xch is not None:

@@ -391,6 +391,10 @@ struct rbe_engine {
   u64 out_dev_bytes = 0;
   u8* out_host = nullptr;
   u64 out_host_bytes = 0;
+  // replica mode with the isolation schedule: every rank's leader bits, ORed
+  // by the host, for the epoch round iso_round (rbe_set_iso_leaders)
+  u8* iso_dev = nullptr;
+  u32 iso_round = ~0u;
   // rbe_wire_ingest scratch (keys, indexes, heap offsets, sort temporary)
   u8* ing_dev = nullptr;
   u64 ing_dev_bytes = 0;
@@ -508,7 +512,6 @@ static int make_params(const rbe_config* cfg, Params* out) {
   if (C.rep_world > kXchgMaxWorld || C.rep_rank >= C.rep_world) return RBE_E_INVALID;
   // replica-per-GPU mode: the fault schedule needs every replica's role, which
   // a rank does not have for the replicas it does not step
-  if (C.rep_world > 1 && C.iso_period) return RBE_E_INVALID;
   C.ext_apply = cfg->ext_apply;
   if (C.ext_apply && !C.ext_inputs) return RBE_E_INVALID;  // applied comes from rbe_notify_applied
   // the host that persists an Update (rbe_commit) applies it too: raft.applied
@@ -697,6 +700,7 @@ int rbe_destroy(rbe_engine* e) {
   if (e->out_host) HIP_IGNORE(hipHostFree(e->out_host));
   if (e->upd_dev) HIP_IGNORE(hipFree(e->upd_dev));
   if (e->ing_dev) HIP_IGNORE(hipFree(e->ing_dev));
+  if (e->iso_dev) HIP_IGNORE(hipFree(e->iso_dev));
   if (e->upd_host) HIP_IGNORE(hipHostFree(e->upd_host));
   if (e->wire_dev) HIP_IGNORE(hipFree(e->wire_dev));
   if (e->wire_meta) HIP_IGNORE(hipFree(e->wire_meta));
@@ -908,6 +912,16 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
 static int launch_iso(rbe_engine* e) {
   const Params& C = e->C;
   if (!(C.iso_period && e->round > 0 && e->round % C.iso_period == 0)) return RBE_OK;
+  if (C.rep_world > 1) {  // the leaders of groups whose replicas other ranks step
+    if (e->iso_round != e->round || !e->iso_dev) return RBE_E_STATE;
+    return dispatch_n(C.n, [&](auto NN) {
+      constexpr int N = decltype(NN)::value;
+      hipLaunchKernelGGL(k_iso_set<N>, dim3(grid_for(C.n_groups)), dim3(kBlock), 0, e->stream,
+                         e->P, e->C, e->round, (const u8*)e->iso_dev);
+      HIP_OK(hipGetLastError());
+      return RBE_OK;
+    });
+  }
   return dispatch_n(C.n, [&](auto NN) {
     constexpr int N = decltype(NN)::value;
     hipLaunchKernelGGL(k_isolate<N>, dim3(grid_for(C.n_groups)), dim3(kBlock), 0, e->stream,
@@ -2230,5 +2244,39 @@ int rbe_wire_ingest(rbe_engine* e, const void* data, uint64_t bytes, rbe_wire_in
   }
   if ((rc = walk(true, base))) return rc;
   HIP_OK(hipStreamSynchronize(e->stream));
+  return RBE_OK;
+}
+
+// Replica mode with the isolation schedule: the epoch's leader
+// bits of this engine's replicas, and the OR over ranks back in.
+int rbe_iso_leaders(rbe_engine* e, uint8_t* out, uint32_t* epoch) {
+  if (!e || !epoch) return RBE_E_INVALID;
+  const Params& C = e->C;
+  *epoch = C.iso_period && e->round > 0 && e->round % C.iso_period == 0 ? 1u : 0u;
+  if (!*epoch || !out) return RBE_OK;
+  HIP_OK(hipSetDevice(e->device));
+  if (!e->iso_dev) HIP_OK(hipMalloc((void**)&e->iso_dev, C.n_groups));
+  const int rc = dispatch_n(C.n, [&](auto NN) {
+    constexpr int N = decltype(NN)::value;
+    hipLaunchKernelGGL(k_iso_bits<N>, dim3(grid_for(C.n_groups)), dim3(kBlock), 0, e->stream,
+                       e->P, e->C, e->iso_dev);
+    HIP_OK(hipGetLastError());
+    return RBE_OK;
+  });
+  if (rc) return rc;
+  HIP_OK(hipMemcpyAsync(out, e->iso_dev, C.n_groups, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  return RBE_OK;
+}
+
+int rbe_set_iso_leaders(rbe_engine* e, const uint8_t* bits) {
+  if (!e || !bits) return RBE_E_INVALID;
+  const Params& C = e->C;
+  if (!(C.iso_period && e->round > 0 && e->round % C.iso_period == 0)) return RBE_E_STATE;
+  HIP_OK(hipSetDevice(e->device));
+  if (!e->iso_dev) HIP_OK(hipMalloc((void**)&e->iso_dev, C.n_groups));
+  HIP_OK(hipMemcpyAsync(e->iso_dev, bits, C.n_groups, hipMemcpyHostToDevice, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  e->iso_round = e->round;
   return RBE_OK;
 }

@@ -2805,17 +2805,31 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, const Clk& ck
 
 // fault schedule: at epoch rounds, isolate the replicas of
 // selected groups that lead at round start; one lane per group.
-template <int N>
-RBE_HD void iso_group(const Planes& P, const Params& C, u64 g, u32 round) {
+// The epoch's isolation of group g from its leaders' slots (`mask`)
+RBE_HD void iso_apply(const Planes& P, const Params& C, u64 g, u32 round, u32 mask) {
   const u64 cid = C.cid_base + g * C.cid_stride;
   if (!iso_selected(C, cid, round / C.iso_period)) return;
-  u32 mask = 0;
-  for (u32 k = 0; k < N; k++)
-    if (P.hot[g * N + k].role == R_Leader) mask |= 1u << k;
   if (mask) {
     P.iso_mask[g] = (u8)mask;
     P.iso_until[g] = round + C.iso_len;
   }
+}
+// Slots of group g's leaders among the replicas this engine steps (all of
+// them with one replica set per engine; replica mode ORs every rank's bits,
+// rbe_iso_leaders / rbe_set_iso_leaders)
+template <int N>
+RBE_HD u32 iso_leader_bits(const Planes& P, const Params& C, u64 g) {
+  u32 mask = 0;
+  for (u32 k = 0; k < N; k++) {
+    const u64 r = g * N + k;
+    const bool own = C.rep_world <= 1 || (u32)((g + k) % C.rep_world) == C.rep_rank;
+    if (own && P.hot[r].role == R_Leader) mask |= 1u << k;
+  }
+  return mask;
+}
+template <int N>
+RBE_HD void iso_group(const Planes& P, const Params& C, u64 g, u32 round) {
+  iso_apply(P, C, g, round, iso_leader_bits<N>(P, C, g));
 }
 
 }  // namespace rbe

@@ -203,7 +203,7 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_get_entry_cmds", "rbe_set_apply_ready", "rbe_collect_outputs", "rbe_collect_updates", "rbe_launch",
            "rbe_xchg_chunk_bytes", "rbe_xchg_pack_fixed", "rbe_xchg_unpack_fixed",
            "rbe_xchg_status", "rbe_stream", "rbe_get_snapshot_state", "rbe_wire_encode",
-           "rbe_wire_fetch", "rbe_wire_decode", "rbe_wire_ingest", "rbe_propose_entries", "rbe_commit",
+           "rbe_wire_fetch", "rbe_wire_decode", "rbe_wire_ingest", "rbe_iso_leaders", "rbe_set_iso_leaders", "rbe_propose_entries", "rbe_commit",
            "rbe_get_update_commits", "rbe_propose_config_change", "rbe_apply_config_change",
            "rbe_reject_config_change"]
 KERNEL_SLOTS = 4
@@ -271,6 +271,8 @@ def load_library(path: Optional[str] = None):
         "rbe_wire_encode": (i32, [vp, P(RbeWireConfig), P(u64)]),
         "rbe_wire_fetch": (i32, [vp, vp, u64, P(RbeWireFrame), u32]),
         "rbe_wire_ingest": (i32, [vp, vp, u64, P(RbeWireIngestStats)]),
+        "rbe_iso_leaders": (i32, [vp, vp, P(u32)]),
+        "rbe_set_iso_leaders": (i32, [vp, vp]),
         "rbe_wire_decode": (i32, [vp, vp, u64, P(RbeMessage), u32, P(u32), P(RbeEntry), u32,
                                   P(u32), vp, u64, P(u64)]),
         "rbe_collect_outputs": (i32, [vp, u64, u64, P(RbeOutputs)]),
@@ -371,6 +373,18 @@ class SnapshotError(EngineError):
 def _check(rc: int, what: str):
     if rc != 0:
         raise EngineError(f"{what} failed with rc={rc}")
+
+
+def iso_leaders_call(fn, h, n_groups: int):
+    """rbe_iso_leaders (or the host build's twin): None off-epoch, else the
+    leader bits per group."""
+    ep = C.c_uint32()
+    _check(fn(h, None, C.byref(ep)), "rbe_iso_leaders")
+    if not ep.value:
+        return None
+    out = np.zeros(n_groups, np.uint8)
+    _check(fn(h, out.ctypes.data, C.byref(ep)), "rbe_iso_leaders")
+    return out
 
 
 def wire_ingest_call(fn, h, data: bytes) -> dict:
@@ -712,6 +726,15 @@ class Engine(NodeInputs):
         arr = (RbeReplicaView * count)()
         _check(self.lib.rbe_get_views(self.h, first, count, arr), "rbe_get_views")
         return arr
+
+    def iso_leaders(self):
+        """rbe_iso_leaders: None unless the next step is an isolation epoch
+        round, else this engine's leader bits per group (numpy uint8)."""
+        return iso_leaders_call(self.lib.rbe_iso_leaders, self.h, self.n_groups)
+
+    def set_iso_leaders(self, bits):
+        _check(self.lib.rbe_set_iso_leaders(self.h, np.ascontiguousarray(bits, np.uint8).ctypes.data),
+               "rbe_set_iso_leaders")
 
     def wire_ingest(self, data: bytes) -> dict:
         """rbe_wire_ingest: deliver one round's inbound frames to the next step

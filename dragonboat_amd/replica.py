@@ -187,10 +187,28 @@ class ReplicaExchange:
         self.eng.xchg_unpack(cat[0].data_ptr(), n[0], cat[1].data_ptr(), n[1],
                              cat[2].data_ptr(), n[2])
 
+    def iso_sync(self):
+        """Before an isolation-schedule epoch round (cfg.iso_period): the
+        leader bits of every rank's replicas, ORed (a sum: each replica has
+        one owner) and handed to the engine (rbe_iso_leaders /
+        rbe_set_iso_leaders).  A no-op on other rounds."""
+        bits = self.eng.iso_leaders()
+        if bits is None:
+            return
+        t = self.torch.from_numpy(bits.astype("int32")).to(self.comm_device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+        self.eng.set_iso_leaders(t.cpu().numpy().astype("uint8"))
+
+    def step(self):
+        """One round of the owned replicas (the exchange of the round before
+        must have run)."""
+        self.iso_sync()
+        self.eng.step()
+
     def run(self, rounds: int):
         """`rounds` lockstep rounds of the owned replicas, exchanging after each."""
         for _ in range(rounds):
-            self.eng.step()
+            self.step()
             if self.fixed:
                 self.exchange_fixed()
             else:

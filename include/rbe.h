@@ -577,6 +577,18 @@ int rbe_stream(rbe_engine* e, void** stream);
 int rbe_xchg_pack(rbe_engine* e, void* buf, const uint64_t* cap3, uint32_t* counts);
 int rbe_xchg_unpack(rbe_engine* e, const void* cnt_recs, uint64_t n_cnt, const void* msg_recs,
                     uint64_t n_msg, const void* ent_recs, uint64_t n_ent);
+/* The isolation fault schedule (cfg.iso_period) in replica mode.  At an epoch
+ * round the schedule cuts off the current leader of each selected group, and
+ * no rank steps every replica of a group: before the step of an epoch round
+ * each rank reads its replicas' leader bits (rbe_iso_leaders: *epoch = 1 when
+ * the next step is an epoch round, then out[g] holds bit k for each replica
+ * k of group g stepped here that is a leader; n_groups bytes), the host ORs
+ * them over ranks (the bits are disjoint, so a sum all-reduce does it) and
+ * hands the result back (rbe_set_iso_leaders).  rbe_step returns
+ * RBE_E_STATE at an epoch round without it.  With one replica set per engine
+ * the step does this itself. */
+int rbe_iso_leaders(rbe_engine* e, uint8_t* out, uint32_t* epoch);
+int rbe_set_iso_leaders(rbe_engine* e, const uint8_t* bits);
 
 /* Transport boundary for replicas whose peers another engine steps (cfg.rep_world > 1:
  * the replicas of other ranks, or of other hosts behind dragonboat's transport).

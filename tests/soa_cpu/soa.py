@@ -8,7 +8,7 @@ import os
 from dragonboat_amd.engine import (CTR_NUM, COUNTER_NAMES, NodeInputs, RbeEntry, RbeMessage,
                                    RbeReplicaView, RbeUpdateCommit, RbeWireFrame, entry_cmds,
                                    entry_fields, make_config, outbox_call, push_messages_call,
-                                   RbeWireIngestStats, wire_ingest_call)
+                                   RbeWireIngestStats, iso_leaders_call, wire_ingest_call)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _lib = None
@@ -32,6 +32,10 @@ def lib():
         L.soa_wire_encode.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
                                       C.POINTER(C.c_char_p), C.c_void_p, C.c_uint64,
                                       C.POINTER(RbeWireFrame), C.POINTER(C.c_uint32), C.c_int32]
+        L.soa_iso_leaders.restype = C.c_int
+        L.soa_iso_leaders.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint32)]
+        L.soa_set_iso_leaders.restype = C.c_int
+        L.soa_set_iso_leaders.argtypes = [C.c_void_p, C.c_void_p]
         L.soa_wire_ingest.restype = C.c_int
         L.soa_wire_ingest.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64,
                                       C.POINTER(RbeWireIngestStats)]
@@ -203,6 +207,14 @@ class SoaCpu(NodeInputs):
         arr = (RbeReplicaView * self.n_rep)()
         lib().soa_views(self.h, C.cast(arr, C.c_void_p))
         return arr
+
+    def iso_leaders(self):
+        return iso_leaders_call(lib().soa_iso_leaders, self.h, self.cfg.n_groups)
+
+    def set_iso_leaders(self, bits):
+        import numpy as np
+        b = np.ascontiguousarray(bits, np.uint8)
+        lib().soa_set_iso_leaders(self.h, b.ctypes.data)
 
     def wire_ingest(self, data):
         """Host-build rbe_wire_ingest (Engine.wire_ingest)."""

@@ -33,6 +33,8 @@ struct SoaEngine {
   std::vector<u8> heap;  // payload heap (cfg.heap_bytes), as on the device
   u64 heap_head = 0;     // Planes::heap_head
   u32 xflag = 0;         // fixed-layout exchange overflow (rbe_xchg_status)
+  std::vector<u8> iso_bits;  // replica mode: ORed leader bits of the epoch round iso_round
+  u32 iso_round = ~0u;
 };
 
 // heap record bytes as rbe_engine.hip read_heap reads them
@@ -62,8 +64,14 @@ static void run_round(SoaEngine* e, bool tick = true) {
   } else {
     e->hin.heap.settle();
   }
-  if (e->C.iso_period && e->round > 0 && e->round % e->C.iso_period == 0)
-    for (u64 g = 0; g < e->C.n_groups; g++) iso_group<N>(e->P, e->C, g, e->round);
+  if (e->C.iso_period && e->round > 0 && e->round % e->C.iso_period == 0) {
+    if (e->C.rep_world > 1) {  // the ORed leader bits of every rank (soa_set_iso_leaders)
+      if (e->iso_round != e->round) abort();
+      for (u64 g = 0; g < e->C.n_groups; g++) iso_apply(e->P, e->C, g, e->round, e->iso_bits[g]);
+    } else {
+      for (u64 g = 0; g < e->C.n_groups; g++) iso_group<N>(e->P, e->C, g, e->round);
+    }
+  }
   // the GPU pipeline, sequentially: triage → leader fast list → follower fast
   // list → full list (k_triage / k_fast_list / k_full_list)
   StepCounters c;
@@ -694,6 +702,24 @@ extern "C" int soa_wire_ingest(void* h, const uint8_t* data, uint64_t bytes, uin
 }
 
 extern "C" {
+
+// rbe_iso_leaders / rbe_set_iso_leaders on the host build
+int soa_iso_leaders(void* h, uint8_t* out, uint32_t* epoch) {
+  SoaEngine* e = (SoaEngine*)h;
+  const Params& C = e->C;
+  *epoch = C.iso_period && e->round > 0 && e->round % C.iso_period == 0 ? 1u : 0u;
+  if (!*epoch || !out) return RBE_OK;
+  for (u64 g = 0; g < C.n_groups; g++)
+    out[g] = (u8)(C.n == 5 ? iso_leader_bits<5>(e->P, C, g)
+                           : C.n == 3 ? iso_leader_bits<3>(e->P, C, g) : iso_leader_bits<1>(e->P, C, g));
+  return RBE_OK;
+}
+int soa_set_iso_leaders(void* h, const uint8_t* bits) {
+  SoaEngine* e = (SoaEngine*)h;
+  e->iso_bits.assign(bits, bits + e->C.n_groups);
+  e->iso_round = e->round;
+  return RBE_OK;
+}
 
 void soa_snapshot_state(void* h, uint64_t* out6) {
   SoaEngine* e = (SoaEngine*)h;

@@ -26,6 +26,15 @@ CASES = {
     "N5_w4": (dict(n_groups=16, n_replicas=5, check_quorum=True, quiesce=True, wl_enabled=True,
                    wl_start_round=25, wl_active_mod=2, wl_read_permille=500, seed=777), 4, 300,
               dict(ring=128, rq_cap=64, maxm=24)),
+    # C3 with its isolation schedule (leaders cut off for 30 of every 50
+    # rounds): each rank knows only its own replicas' roles, so the epoch's
+    # leader bits are ORed over ranks before the step (ReplicaExchange.iso_sync)
+    "C3_iso_w2": (dict(n_groups=20, n_replicas=5, check_quorum=True, wl_enabled=True,
+                       wl_start_round=40, iso_period=50, iso_len=30, iso_mod=3), 2, 300,
+                  dict(ring=128)),
+    "C3_iso_w4": (dict(n_groups=20, n_replicas=5, check_quorum=True, wl_enabled=True,
+                       wl_start_round=40, iso_period=50, iso_len=30, iso_mod=3), 4, 300,
+                  dict(ring=128)),
 }
 CHECK_EVERY = 50
 

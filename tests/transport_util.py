@@ -84,6 +84,13 @@ def run_transport(engs, ref, n, rounds, every=25, inputs=None, wire=False):
             for rank, e in enumerate(engs):
                 apply_engine(e, [op for op in ops if owner(op[1] // n, op[1] % n, world) == rank])
             apply_oracle(ref, ops)
+        iso = [e.iso_leaders() for e in engs]  # isolation epochs: the ORed leader bits
+        if iso[0] is not None:
+            bits = iso[0].copy()
+            for b in iso[1:]:
+                bits |= b
+            for e in engs:
+                e.set_iso_leaders(bits)
         for e in engs:
             e.step()
         ref.step()
