@@ -217,8 +217,11 @@ def run_replica_mode(args, ws, rank, local, dist, dev, gloo_staged):
     kw = dict(kw)
     per_gpu = args.groups or kw["n_groups"]
     kw["n_groups"] = per_gpu * ws
+    # rep_compact: each rank allocates only the groups it steps a replica of
+    # (3/8 of them at 8 ranks)
     cfg = make_config(device=0 if gloo_staged else local, trace=False,
-                      rep_world=ws if ws > 1 else 0, rep_rank=rank, **kw)
+                      rep_world=ws if ws > 1 else 0, rep_rank=rank,
+                      rep_compact=ws > 1 and not args.no_compact, **kw)
     eng = Engine(cfg)
     xch = None
     if ws > 1:
@@ -482,6 +485,8 @@ def main():
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
     ap.add_argument("--groups", type=int, default=0, help="override groups per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-compact", action="store_true",
+                    help="c5: allocate every group's planes on every rank")
     ap.add_argument("--prof-rounds", type=int, default=50,
                     help="rounds profiled per kernel with HIP events after the timed region")
     ap.add_argument("--cpu-groups", type=int, default=0,

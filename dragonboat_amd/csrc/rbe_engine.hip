@@ -196,7 +196,7 @@ __global__ __launch_bounds__(kBlock) void k_out_write(Planes P, Params C, u64 fi
       o.reject = m.reject;
       o.to = m.to;
       o.from = m.from;
-      o.cluster_id = C.cid_base + g * C.cid_stride;
+      o.cluster_id = cid_of(C, g);
       o.term = m.term;
       o.log_term = m.log_term;
       o.log_index = m.log_index;
@@ -510,8 +510,7 @@ static int make_params(const rbe_config* cfg, Params* out) {
   C.rep_world = cfg->rep_world > 1 ? cfg->rep_world : 1;
   C.rep_rank = cfg->rep_rank;
   if (C.rep_world > kXchgMaxWorld || C.rep_rank >= C.rep_world) return RBE_E_INVALID;
-  // replica-per-GPU mode: the fault schedule needs every replica's role, which
-  // a rank does not have for the replicas it does not step
+  rep_compact_setup(C, cfg->rep_compact != 0);
   C.ext_apply = cfg->ext_apply;
   if (C.ext_apply && !C.ext_inputs) return RBE_E_INVALID;  // applied comes from rbe_notify_applied
   // the host that persists an Update (rbe_commit) applies it too: raft.applied
@@ -780,8 +779,7 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   P.imark = C.ext_commit ? (u64*)ptrs[22] : nullptr;
   HIP_IGNORE(hipMemsetAsync(P.gwake, GW_AWAKE, C.n_groups, e->stream));  // every group starts awake
   e->hin.init(C.n_rep, C.n, C.in_cap, C.heap_bytes);
-  e->hin.rep_world = C.rep_world;
-  e->hin.rep_rank = C.rep_rank;
+  e->hin.owner = C.rep_world > 1 ? &e->C : nullptr;
   if (C.heap_bytes) {
     if (hipMalloc(&e->heap, C.heap_bytes) != hipSuccess ||
         hipMalloc(&e->heap_dev, 2 * sizeof(u64)) != hipSuccess) {
@@ -1613,7 +1611,7 @@ int rbe_get_messages(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t
         o.reject = m.reject;
         o.to = m.to;
         o.from = m.from;
-        o.cluster_id = e->C.cid_base + g * e->C.cid_stride;
+        o.cluster_id = cid_of(e->C, g);
         o.term = m.term;
         o.log_term = m.log_term;
         o.log_index = m.log_index;
@@ -2255,7 +2253,8 @@ int rbe_iso_leaders(rbe_engine* e, uint8_t* out, uint32_t* epoch) {
   *epoch = C.iso_period && e->round > 0 && e->round % C.iso_period == 0 ? 1u : 0u;
   if (!*epoch || !out) return RBE_OK;
   HIP_OK(hipSetDevice(e->device));
-  if (!e->iso_dev) HIP_OK(hipMalloc((void**)&e->iso_dev, C.n_groups));
+  if (!e->iso_dev) HIP_OK(hipMalloc((void**)&e->iso_dev, C.n_groups_glob));
+  HIP_OK(hipMemsetAsync(e->iso_dev, 0, C.n_groups_glob, e->stream));
   const int rc = dispatch_n(C.n, [&](auto NN) {
     constexpr int N = decltype(NN)::value;
     hipLaunchKernelGGL(k_iso_bits<N>, dim3(grid_for(C.n_groups)), dim3(kBlock), 0, e->stream,
@@ -2264,7 +2263,7 @@ int rbe_iso_leaders(rbe_engine* e, uint8_t* out, uint32_t* epoch) {
     return RBE_OK;
   });
   if (rc) return rc;
-  HIP_OK(hipMemcpyAsync(out, e->iso_dev, C.n_groups, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipMemcpyAsync(out, e->iso_dev, C.n_groups_glob, hipMemcpyDeviceToHost, e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
   return RBE_OK;
 }
@@ -2274,9 +2273,20 @@ int rbe_set_iso_leaders(rbe_engine* e, const uint8_t* bits) {
   const Params& C = e->C;
   if (!(C.iso_period && e->round > 0 && e->round % C.iso_period == 0)) return RBE_E_STATE;
   HIP_OK(hipSetDevice(e->device));
-  if (!e->iso_dev) HIP_OK(hipMalloc((void**)&e->iso_dev, C.n_groups));
-  HIP_OK(hipMemcpyAsync(e->iso_dev, bits, C.n_groups, hipMemcpyHostToDevice, e->stream));
+  if (!e->iso_dev) HIP_OK(hipMalloc((void**)&e->iso_dev, C.n_groups_glob));
+  HIP_OK(hipMemcpyAsync(e->iso_dev, bits, C.n_groups_glob, hipMemcpyHostToDevice, e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
   e->iso_round = e->round;
+  return RBE_OK;
+}
+
+int rbe_local_groups(rbe_engine* e, uint64_t* n_local, uint64_t* global_of) {
+  if (!e || !n_local) return RBE_E_INVALID;
+  *n_local = e->C.n_groups;
+  if (global_of)
+    for (u64 g = 0; g < e->C.n_groups; g++) {
+      const u64 gg = group_global(e->C, g);
+      global_of[g] = gg < e->C.n_groups_glob ? gg : ~0ull;
+    }
   return RBE_OK;
 }

@@ -270,7 +270,7 @@ template <int N>
 RBE_HD u64 heap_low_group(const Planes& P, const Params& C, u64 g, u32 round) {
   u64 mark = ~0ull;
   for (u32 k = 0; k < N; k++) {
-    if (C.rep_world > 1 && (g + k) % C.rep_world != C.rep_rank) continue;
+    if (!owns_replica(C, g, k)) continue;
     const u64 r = g * N + k;
     const Core c = P.core[r];
     u64 m = c.saved_to < c.processed ? c.saved_to : c.processed;
@@ -283,7 +283,7 @@ RBE_HD u64 heap_low_group(const Planes& P, const Params& C, u64 g, u32 round) {
   u64 lo = ~0ull;
   const u32 par = (round - 1u) & 1u;
   for (u32 k = 0; k < N; k++) {
-    if (C.rep_world > 1 && (g + k) % C.rep_world != C.rep_rank) continue;
+    if (!owns_replica(C, g, k)) continue;
     const u64 r = g * N + k;
     const u64 last = P.core[r].last_index;
     u64 from = last >= C.ring ? last - C.ring + 1 : 1;
@@ -416,7 +416,7 @@ struct HostInputs {
   std::vector<u64> applied;  // [n_rep] host mirror of Planes::applied (the host is its only writer)
   std::vector<CommitRec> commits;  // rbe_commit records for the next step, in call order
   std::vector<u8> committing;      // [n_rep] a commit is staged (one per replica per step)
-  u32 rep_world = 1, rep_rank = 0;  // replica-per-GPU mode: only owned replicas take input
+  const Params* owner = nullptr;  // replica-per-GPU mode: only owned replicas take input
 
   HostHeap heap;             // payload heap positions and staged bytes
 
@@ -462,7 +462,7 @@ struct HostInputs {
     if (cnt && !replica) return RBE_E_INVALID;
     for (u64 i = 0; i < cnt; i++) {
       if (replica[i] >= n_rep) return RBE_E_INVALID;
-      if (rep_world > 1 && (replica[i] / n + replica[i] % n) % rep_world != rep_rank)
+      if (owner && !owns_replica(*owner, replica[i] / n, (u32)(replica[i] % n)))
         return RBE_E_INVALID;  // stepped by another engine
     }
     if (!flag) return RBE_OK;

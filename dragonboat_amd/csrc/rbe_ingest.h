@@ -65,9 +65,10 @@ RBE_HD u64 ingest_check(const Params& C, u64 heap_cap, const rbe_message& m, con
   if ((m.from < 1 || m.from > N) && is_response_message(m.type) && m.n_entries == 0) return drop;
   const u64 cid = m.cluster_id;
   const u64 st = C.cid_stride ? C.cid_stride : 1;
-  const u64 g = (cid - C.cid_base) / st;
-  if (cid < C.cid_base || (cid - C.cid_base) % st != 0 || g >= C.n_groups || m.from < 1 ||
-      m.from > N || m.to < 1 || m.to > N || m.from == m.to) {
+  u64 g = 0;  // the local group of global group (cid - cid_base) / stride
+  if (cid < C.cid_base || (cid - C.cid_base) % st != 0 ||
+      !group_local(C, (cid - C.cid_base) / st, &g) || m.from < 1 || m.from > N || m.to < 1 ||
+      m.to > N || m.from == m.to) {
     *err |= ING_INVALID;
     return drop;
   }

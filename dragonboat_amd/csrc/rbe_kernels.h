@@ -323,7 +323,7 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
     const u32 g = gids[i];
     const bool awake = (gws[i] & GW_AWAKE) != 0;
     bool work = j < gn;
-    if (work && !awake && !group_forced(C, C.cid_base + (u64)g * C.cid_stride, round)) {
+    if (work && !awake && !group_forced(C, cid_of(C, (u64)g), round)) {
       work = false;
       u32 own = 0;
       for (u32 k = 0; k < (u32)N; k++) own += owned<N>(C, (u64)g * N + k) ? 1u : 0u;
@@ -425,7 +425,7 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
     // receiving a Replicate
     bool back = false;
     if (cls == T_LEAD)
-      back = wl_input(C, C.cid_base + (u64)((u32)r / (u32)N) * C.cid_stride, round) == 1u;
+      back = wl_input(C, cid_of(C, (u64)((u32)r / (u32)N)), round) == 1u;
     else if (cls == T_FOLL)
       back = (inb & 4u) != 0;
     const u32 code = cls == T_DONE ? kNone : (back ? cls + 2u : cls - 1u);
@@ -469,7 +469,7 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
         const u32 st = s_gst[j];
         g = s_gid[j];
         const bool awake = (st >> 31) != 0;
-        const u32 tr = group_transition(C, C.cid_base + (u64)g * C.cid_stride, round, awake,
+        const u32 tr = group_transition(C, cid_of(C, (u64)g), round, awake,
                                         (st >> 8) & 0xFFu);
         if (tr == GS_SLEEP) P.gwake[g] = group_sleep_byte(st & 0xFFu);
         if (tr == GS_WAKE) P.gwake[g] = GW_AWAKE;
@@ -930,12 +930,16 @@ __global__ __launch_bounds__(kBlock) void k_launch(Planes P, Params C) {
 template <int N>
 __global__ __launch_bounds__(kBlock) void k_iso_bits(Planes P, Params C, u8* out) {
   const u64 g = (u64)blockIdx.x * kBlock + threadIdx.x;
-  if (g < C.n_groups) out[g] = (u8)iso_leader_bits<N>(P, C, g);
+  if (g >= C.n_groups) return;
+  const u64 gg = group_global(C, g);  // bits are exchanged by global group
+  if (gg < C.n_groups_glob) out[gg] = (u8)iso_leader_bits<N>(P, C, g);
 }
 template <int N>
 __global__ __launch_bounds__(kBlock) void k_iso_set(Planes P, Params C, u32 round, const u8* bits) {
   const u64 g = (u64)blockIdx.x * kBlock + threadIdx.x;
-  if (g < C.n_groups) iso_apply(P, C, g, round, bits[g]);
+  if (g >= C.n_groups) return;
+  const u64 gg = group_global(C, g);
+  if (gg < C.n_groups_glob) iso_apply(P, C, g, round, bits[gg]);
 }
 
 template <int N>

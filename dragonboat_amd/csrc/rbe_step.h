@@ -26,6 +26,55 @@
 
 namespace rbe {
 
+// Global group of local group g (rep_compact), and its cluster id
+RBE_HD u64 group_global(const Params& C, u64 g) {
+  return C.rep_compact ? (g / C.n) * C.rep_world + C.res[g % C.n] : g;
+}
+RBE_HD u64 cid_of(const Params& C, u64 g) { return C.cid_base + group_global(C, g) * C.cid_stride; }
+// Is replica k of local group g stepped by this engine?  (replica mode:
+// replica k of global group G is stepped on rank (G + k) % rep_world; the
+// padding groups of a compacted engine by none)
+RBE_HD bool owns_replica(const Params& C, u64 g, u32 k) {
+  if (C.rep_world <= 1) return true;
+  const u64 gg = group_global(C, g);
+  return gg < C.n_groups_glob && (u32)((gg + k) % C.rep_world) == C.rep_rank;
+}
+// cfg.rep_compact: keep only the groups this rank steps a replica of.  The
+// rank touches global group G iff G % W is one of the N residues (rank - k)
+// mod W; local group l is G = (l / N) * W + res[l % N] (the last block may
+// hold padding groups past the global count, which no rank steps).
+RBE_HD void rep_compact_setup(Params& C, bool on) {
+  C.n_groups_glob = C.n_groups;
+  C.rep_compact = 0;
+  for (int i = 0; i < 8; i++) C.res[i] = 0;
+  if (on && C.rep_world > 1 && C.n < C.rep_world) {
+    u32 m = 0;
+    for (u32 rho = 0; rho < C.rep_world; rho++)
+      for (u32 k = 0; k < C.n; k++)
+        if ((rho + k) % C.rep_world == C.rep_rank) {
+          C.res[m++] = (u8)rho;
+          break;
+        }
+    C.rep_compact = 1;
+    C.n_groups = (C.n_groups_glob + C.rep_world - 1) / C.rep_world * C.n;
+  }
+  C.n_rep = C.n_groups * C.n;
+}
+// Local group of global group gg, if this engine holds it
+RBE_HD bool group_local(const Params& C, u64 gg, u64* g) {
+  if (!C.rep_compact) {
+    *g = gg;
+    return gg < C.n_groups;
+  }
+  const u32 rho = (u32)(gg % C.rep_world);
+  for (u32 j = 0; j < C.n; j++)
+    if (C.res[j] == rho) {
+      *g = (gg / C.rep_world) * C.n + j;
+      return gg < C.n_groups_glob;
+    }
+  return false;
+}
+
 RBE_HD u64 mix64(u64 x) {  // splitmix64 finalizer (same constants as the oracle)
   x += 0x9E3779B97F4A7C15ULL;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -353,7 +402,7 @@ struct Lane {
 
   RBE_HD Lane(const Planes& P_, const Params& C_, u64 r_, Clk clk_, StepCounters& c_)
       : P(P_), C(C_), r(r_), g(r_ / N), k((u32)(r_ % N)), round(clk_.round),
-        par(clk_.round & 1u), clk(clk_), cid(C_.cid_base + (r_ / N) * C_.cid_stride),
+        par(clk_.round & 1u), clk(clk_), cid(cid_of(C_, r_ / N)),
         self((u8)(r_ % N + 1)), ctr(c_) {}
 
   // ------------------------------------------------------------- faults
@@ -2363,7 +2412,7 @@ RBE_HD bool step_replica_fast(const Planes& P, const Params& C, u64 r, Clk ck,
 template <int N>
 RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   const u32 k = (u32)(r % N);
-  const u64 cid = C.cid_base + (r / N) * C.cid_stride;
+  const u64 cid = cid_of(C, r / N);
   const u64 self = k + 1;
   Hot h;
   h.role = R_Follower;
@@ -2446,7 +2495,7 @@ RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, 
                              u64 ss_term = 0) {
   const u32 k = (u32)(r % N);
   const u64 g = r / N;
-  const u64 cid = C.cid_base + g * C.cid_stride;
+  const u64 cid = cid_of(C, g);
   const u64 self = k + 1;
   const bool faulted = P.upd[r].fault != 0;
   u8 snap_flags = 0;
@@ -2542,7 +2591,7 @@ RBE_HD bool triage_lazy(const Planes& P, const Params& C, u64 r, const Clk& ck, 
   if (!(ib & IB_LAZY) || inbound) return false;
   const u32 round = ck.round;
   const u32 g = (u32)r / (u32)N;  // replica indices fit u32 (work lists hold u32)
-  const u64 cid = C.cid_base + (u64)g * C.cid_stride;
+  const u64 cid = cid_of(C, (u64)g);
   if ((ib & IB_LEAD) && wl_input(C, cid, round)) return false;
   if ((ib & IB_LEAD) && C.cc_period && cc_selected(C, cid, round)) return false;
   if (C.xfer_period && xfer_input(C, cid, round, (u32)r - g * (u32)N)) return false;
@@ -2678,7 +2727,7 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, const Clk& ck
       if (pc & 0x8000u) qbits |= 1u << s;
     }
   }
-  const u64 cid = C.cid_base + g * C.cid_stride;
+  const u64 cid = cid_of(C, g);
   const u32 cls = h.role == R_Leader ? T_LEAD : (h.role == R_Follower ? T_FOLL : T_FULL);
   if (nmsg || (h.flags & HF_APPLY_PENDING)) return cls;
   if (C.ext_commit) return cls;
@@ -2807,7 +2856,7 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, const Clk& ck
 // selected groups that lead at round start; one lane per group.
 // The epoch's isolation of group g from its leaders' slots (`mask`)
 RBE_HD void iso_apply(const Planes& P, const Params& C, u64 g, u32 round, u32 mask) {
-  const u64 cid = C.cid_base + g * C.cid_stride;
+  const u64 cid = cid_of(C, g);
   if (!iso_selected(C, cid, round / C.iso_period)) return;
   if (mask) {
     P.iso_mask[g] = (u8)mask;
@@ -2822,7 +2871,7 @@ RBE_HD u32 iso_leader_bits(const Planes& P, const Params& C, u64 g) {
   u32 mask = 0;
   for (u32 k = 0; k < N; k++) {
     const u64 r = g * N + k;
-    const bool own = C.rep_world <= 1 || (u32)((g + k) % C.rep_world) == C.rep_rank;
+    const bool own = owns_replica(C, g, k);
     if (own && P.hot[r].role == R_Leader) mask |= 1u << k;
   }
   return mask;

@@ -314,6 +314,11 @@ struct Params {
   // leader-transfer schedule (RequestLeaderTransfer on a seeded replica), 0 = off
   u32 xfer_period;
   u32 xfer_mod;
+  // replica mode with compacted planes (rbe_xchg.h rep_compact_setup): local
+  // group l is global group (l / n) * rep_world + res[l % n]
+  u32 rep_compact;
+  u64 n_groups_glob;  // global group count (= n_groups without compaction)
+  u8 res[8];          // the n residues g % rep_world of the groups this rank touches, ascending
 };
 
 // The clock of one round: `round` numbers every rbe_step, `tclk` counts the

@@ -191,7 +191,7 @@ RBE_HD u32 wire_cell(const Planes& P, const Params& C, const u8* heap, u64 heap_
                      u32 d, u32 round, u8* out, u32* n_msgs, u32* n_is, u32* n_bad) {
   const u32 par = (round - 1u) & 1u;
   const u64 r = g * N + k;
-  const u64 cid = C.cid_base + g * C.cid_stride;
+  const u64 cid = cid_of(C, g);
   const u32 pc = row_word(P.cnt[par][r], d, round);
   const u32 na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
   u32 bytes = 0, nm = 0, ni = 0, bad = 0;

@@ -41,9 +41,13 @@ struct alignas(16) XEnt {  // one arena entry of sender replica g * N + s
 };
 constexpr u64 kXRecBytes[XS_NUM] = {sizeof(XCnt), sizeof(XMsg), sizeof(XEnt)};
 
+// rank that steps replica k of local group g (rep_world for a padding group
+// of a compacted engine: nobody)
 template <int N>
 RBE_HD u32 owner_of(const Params& C, u64 g, u32 k) {
-  return (u32)((g + k) % C.rep_world);
+  const u64 gg = group_global(C, g);
+  if (gg >= C.n_groups_glob) return C.rep_world;
+  return (u32)((gg + k) % C.rep_world);
 }
 template <int N>
 RBE_HD bool owned(const Params& C, u64 r) {
@@ -93,7 +97,8 @@ RBE_HD void xchg_sender(const Planes& P, const Params& C, u64 r, u32 par, u32 ro
     if (d == s) continue;
     const u32 peer = owner_of<N>(C, g, d);
     if (peer == C.rep_rank) continue;
-    const u64 key = (g * N + s) * N + d;
+    const u64 gg = group_global(C, g);  // records carry global indexes
+    const u64 key = (gg * N + s) * N + d;
     const u32 word = row_word(row, d, round);
     if (word == 0) continue;
     auto put = [&](u32 t) -> u8* {
@@ -107,14 +112,14 @@ RBE_HD void xchg_sender(const Planes& P, const Params& C, u64 r, u32 par, u32 ro
       sent_to |= 1u << peer;
       if (u8* p = put(XS_CNT)) {
         XCnt x;
-        x.key = r;
+        x.key = gg * N + s;
         x.pad = 0;
         x.row = row;
         *(XCnt*)p = x;
       }
     }
     const u32 na = word & 0x7Fu, nb = (word >> 7) & 0x7Fu;
-    const Msg* lst = &P.msgs[par][key * (u64)C.maxm];
+    const Msg* lst = &P.msgs[par][((g * N + s) * N + d) * (u64)C.maxm];  // local list
     for (u32 i = 0; i < na + nb; i++) {
       const u32 slot = i < na ? i : C.maxm - 1u - (i - na);
       const Msg m = lst[slot];
@@ -131,7 +136,7 @@ RBE_HD void xchg_sender(const Planes& P, const Params& C, u64 r, u32 par, u32 ro
         if (off >= C.ecap) break;
         if (u8* p = put(XS_ENT)) {
           XEnt x;
-          x.key = r;
+          x.key = gg * N + s;
           x.off = off;
           x.e = P.arena[par][r * C.ecap + off];
           *(XEnt*)p = x;
@@ -141,15 +146,28 @@ RBE_HD void xchg_sender(const Planes& P, const Params& C, u64 r, u32 par, u32 ro
   }
 }
 
+// a record's global replica (or list, with `per` = N * N) key in this
+// engine's local numbering (rep_compact); ~0 when it holds no such group
+RBE_HD u64 xchg_local_key(const Params& C, u64 key, u64 per) {
+  u64 g;
+  if (!group_local(C, key / per, &g)) return ~0ull;
+  return g * per + key % per;
+}
 RBE_HD void xchg_put_cnt(const Planes& P, const Params& C, u32 par, const XCnt& x) {
-  P.cnt[par][x.key] = x.row;
-  P.gwake[x.key / C.n] = GW_AWAKE;  // a message wakes the destination's group
+  const u64 key = xchg_local_key(C, x.key, C.n);
+  if (key == ~0ull) return;
+  P.cnt[par][key] = x.row;
+  P.gwake[key / C.n] = GW_AWAKE;  // a message wakes the destination's group
 }
 RBE_HD void xchg_put_msg(const Planes& P, const Params& C, u32 par, const XMsg& x) {
-  P.msgs[par][x.key * (u64)C.maxm + x.slot] = x.m;
+  const u64 key = xchg_local_key(C, x.key, (u64)C.n * C.n);
+  if (key == ~0ull) return;
+  P.msgs[par][key * (u64)C.maxm + x.slot] = x.m;
 }
 RBE_HD void xchg_put_ent(const Planes& P, const Params& C, u32 par, const XEnt& x) {
-  P.arena[par][x.key * C.ecap + x.off] = x.e;
+  const u64 key = xchg_local_key(C, x.key, C.n);
+  if (key == ~0ull) return;
+  P.arena[par][key * C.ecap + x.off] = x.e;
 }
 // record i of stream t of source chunk p of a fixed-layout receive buffer, if
 // the chunk holds it (returns false past the chunk's count); *overflow gets
@@ -192,7 +210,7 @@ template <int N, typename RD>
 int outbox_messages(const Params& C, u64 g, u32 k, const CntRow& row, u32 round, const Msg* lst,
                     const Ent* arena, rbe_message* out, u32 cap, rbe_entry* ents, u32 ent_cap,
                     u32* n_msg, u32* n_ent, u8* cmd, u64 cmd_cap, u64* n_cmd, RD&& rd) {
-  const u64 cid = C.cid_base + g * C.cid_stride;
+  const u64 cid = cid_of(C, g);
   u32 n = 0, ne = 0;
   u64 nc = 0;
   auto emit = [&](const Msg& m, u32 type, u32 to) {
@@ -293,7 +311,7 @@ int messages_to_records(const Params& C, HostHeap& heap, u32 round, u64 n, const
       const u32 s = (u32)m.from - 1u, d = (u32)m.to - 1u;
       if (owner_of<N>(C, g, s) == C.rep_rank || owner_of<N>(C, g, d) != C.rep_rank)
         return RBE_E_INVALID;
-      const u64 key = (g * N + s) * N + d;
+      const u64 key = (group_global(C, g) * N + s) * N + d;  // records carry global indexes
       auto it = words.find(key);
       if (it == words.end()) {
         it = words.emplace(key, 0u).first;
@@ -328,7 +346,7 @@ int messages_to_records(const Params& C, HostHeap& heap, u32 round, u64 n, const
         w += 1u << 7;
       }
       if (with_ents && m.n_entries) {
-        const u64 sr = g * N + s;
+        const u64 sr = group_global(C, g) * N + s;
         u32& off = used[sr];
         if (m.n_entries > 0xFFFFu || off + m.n_entries > C.ecap) return RBE_E_NOMEM;
         x.m.n_ent = (u16)m.n_entries;

@@ -45,7 +45,8 @@ class RbeConfig(C.Structure):
                 ("xfer_period", C.c_uint32), ("xfer_mod", C.c_uint32),
                 ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
                 ("heap_bytes", C.c_uint64), ("ext_commit", C.c_uint32),
-                ("membership", C.c_uint32), ("cc_period", C.c_uint32), ("cc_mod", C.c_uint32)]
+                ("membership", C.c_uint32), ("cc_period", C.c_uint32), ("cc_mod", C.c_uint32),
+                ("rep_compact", C.c_uint32)]
 
 
 class RbeReplicaView(C.Structure):
@@ -203,7 +204,7 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_get_entry_cmds", "rbe_set_apply_ready", "rbe_collect_outputs", "rbe_collect_updates", "rbe_launch",
            "rbe_xchg_chunk_bytes", "rbe_xchg_pack_fixed", "rbe_xchg_unpack_fixed",
            "rbe_xchg_status", "rbe_stream", "rbe_get_snapshot_state", "rbe_wire_encode",
-           "rbe_wire_fetch", "rbe_wire_decode", "rbe_wire_ingest", "rbe_iso_leaders", "rbe_set_iso_leaders", "rbe_propose_entries", "rbe_commit",
+           "rbe_wire_fetch", "rbe_wire_decode", "rbe_wire_ingest", "rbe_iso_leaders", "rbe_set_iso_leaders", "rbe_local_groups", "rbe_propose_entries", "rbe_commit",
            "rbe_get_update_commits", "rbe_propose_config_change", "rbe_apply_config_change",
            "rbe_reject_config_change"]
 KERNEL_SLOTS = 4
@@ -273,6 +274,7 @@ def load_library(path: Optional[str] = None):
         "rbe_wire_ingest": (i32, [vp, vp, u64, P(RbeWireIngestStats)]),
         "rbe_iso_leaders": (i32, [vp, vp, P(u32)]),
         "rbe_set_iso_leaders": (i32, [vp, vp]),
+        "rbe_local_groups": (i32, [vp, P(u64), vp]),
         "rbe_wire_decode": (i32, [vp, vp, u64, P(RbeMessage), u32, P(u32), P(RbeEntry), u32,
                                   P(u32), vp, u64, P(u64)]),
         "rbe_collect_outputs": (i32, [vp, u64, u64, P(RbeOutputs)]),
@@ -327,7 +329,7 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                 xfer_period: int = 0, xfer_mod: int = 1, heap_bytes: int = 0,
                 snapshot_entries: int = 0, compaction_overhead: int = 0,
                 ext_commit: bool = False, membership: bool = False, cc_period: int = 0,
-                cc_mod: int = 1) -> RbeConfig:
+                cc_mod: int = 1, rep_compact: bool = False) -> RbeConfig:
     return RbeConfig(abi_version=RBE_ABI_VERSION, device=device, n_groups=n_groups,
                      n_replicas=n_replicas, election_rtt=election_rtt,
                      heartbeat_rtt=heartbeat_rtt, check_quorum=int(check_quorum),
@@ -342,7 +344,8 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                      in_cap=in_cap, xfer_period=xfer_period, xfer_mod=xfer_mod,
                      heap_bytes=heap_bytes, snapshot_entries=snapshot_entries,
                      compaction_overhead=compaction_overhead, ext_commit=int(ext_commit),
-                     membership=int(membership), cc_period=cc_period, cc_mod=cc_mod)
+                     membership=int(membership), cc_period=cc_period, cc_mod=cc_mod,
+                     rep_compact=int(rep_compact))
 
 
 class InputError(EngineError):
@@ -373,6 +376,13 @@ class SnapshotError(EngineError):
 def _check(rc: int, what: str):
     if rc != 0:
         raise EngineError(f"{what} failed with rc={rc}")
+
+
+def global_groups_call(fn, h, n_groups: int):
+    out = np.zeros(max(1, n_groups), np.uint64)
+    n = C.c_uint64()
+    _check(fn(h, C.byref(n), out.ctypes.data), "rbe_local_groups")
+    return out[:n.value]
 
 
 def iso_leaders_call(fn, h, n_groups: int):
@@ -576,7 +586,10 @@ class Engine(NodeInputs):
         h = C.c_void_p()
         _check(self.lib.rbe_create(C.byref(self.cfg), C.byref(h)), "rbe_create")
         self.h = h
-        self.n_groups = self.cfg.n_groups
+        # the engine's (local) groups: fewer than cfg.n_groups with rep_compact
+        ng = C.c_uint64()
+        _check(self.lib.rbe_local_groups(self.h, C.byref(ng), None), "rbe_local_groups")
+        self.n_groups = ng.value
         self.n_replicas = self.cfg.n_replicas
         self.n_rep = self.n_groups * self.n_replicas
 
@@ -727,10 +740,15 @@ class Engine(NodeInputs):
         _check(self.lib.rbe_get_views(self.h, first, count, arr), "rbe_get_views")
         return arr
 
+    def global_groups(self):
+        """rbe_local_groups: the global group of each local group (numpy
+        uint64; UINT64_MAX for padding groups of a compacted engine)."""
+        return global_groups_call(self.lib.rbe_local_groups, self.h, self.n_groups)
+
     def iso_leaders(self):
         """rbe_iso_leaders: None unless the next step is an isolation epoch
         round, else this engine's leader bits per group (numpy uint8)."""
-        return iso_leaders_call(self.lib.rbe_iso_leaders, self.h, self.n_groups)
+        return iso_leaders_call(self.lib.rbe_iso_leaders, self.h, self.cfg.n_groups)
 
     def set_iso_leaders(self, bits):
         _check(self.lib.rbe_set_iso_leaders(self.h, np.ascontiguousarray(bits, np.uint8).ctypes.data),

@@ -160,6 +160,12 @@ typedef struct rbe_config {
                                 leader every cc_period rounds in groups selected 1 in
                                 cc_mod; needs membership), 0 = off */
   uint32_t cc_mod;
+  /* replica mode (rep_world > 1, n_replicas < rep_world): allocate the planes
+   * of only the groups this rank steps a replica of (n_replicas of every
+   * rep_world groups: 3/8 at N = 3, W = 8).  Replica and group indexes of
+   * every call are then the engine's local ones; rbe_local_groups maps them
+   * to the global group (n_groups stays the global count). */
+  uint32_t rep_compact;
 } rbe_config;
 
 /* Snapshot of one replica (tests, debugging, rbe_get_views). */
@@ -581,13 +587,18 @@ int rbe_xchg_unpack(rbe_engine* e, const void* cnt_recs, uint64_t n_cnt, const v
  * round the schedule cuts off the current leader of each selected group, and
  * no rank steps every replica of a group: before the step of an epoch round
  * each rank reads its replicas' leader bits (rbe_iso_leaders: *epoch = 1 when
- * the next step is an epoch round, then out[g] holds bit k for each replica
- * k of group g stepped here that is a leader; n_groups bytes), the host ORs
+ * the next step is an epoch round, then out[G] holds bit k for each replica
+ * k of global group G stepped here that is a leader; cfg.n_groups bytes,
+ * indexed by global group also with rep_compact), the host ORs
  * them over ranks (the bits are disjoint, so a sum all-reduce does it) and
  * hands the result back (rbe_set_iso_leaders).  rbe_step returns
  * RBE_E_STATE at an epoch round without it.  With one replica set per engine
  * the step does this itself. */
 int rbe_iso_leaders(rbe_engine* e, uint8_t* out, uint32_t* epoch);
+/* The engine's group count and, when global_of is non-null, the global group
+ * of each local group (UINT64_MAX for the padding groups of a compacted
+ * engine, which no rank steps).  Without cfg.rep_compact local = global. */
+int rbe_local_groups(rbe_engine* e, uint64_t* n_local, uint64_t* global_of);
 int rbe_set_iso_leaders(rbe_engine* e, const uint8_t* bits);
 
 /* Transport boundary for replicas whose peers another engine steps (cfg.rep_world > 1:

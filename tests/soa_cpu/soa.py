@@ -8,7 +8,8 @@ import os
 from dragonboat_amd.engine import (CTR_NUM, COUNTER_NAMES, NodeInputs, RbeEntry, RbeMessage,
                                    RbeReplicaView, RbeUpdateCommit, RbeWireFrame, entry_cmds,
                                    entry_fields, make_config, outbox_call, push_messages_call,
-                                   RbeWireIngestStats, iso_leaders_call, wire_ingest_call)
+                                   RbeWireIngestStats, global_groups_call, iso_leaders_call,
+                                   wire_ingest_call)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _lib = None
@@ -32,6 +33,8 @@ def lib():
         L.soa_wire_encode.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
                                       C.POINTER(C.c_char_p), C.c_void_p, C.c_uint64,
                                       C.POINTER(RbeWireFrame), C.POINTER(C.c_uint32), C.c_int32]
+        L.soa_local_groups.restype = C.c_int
+        L.soa_local_groups.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p]
         L.soa_iso_leaders.restype = C.c_int
         L.soa_iso_leaders.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint32)]
         L.soa_set_iso_leaders.restype = C.c_int
@@ -113,10 +116,13 @@ class SoaCpu(NodeInputs):
 
     def __init__(self, full_only=False, staged=0, **kw):
         self.cfg = make_config(**kw)
-        self.n_rep = self.cfg.n_groups * self.cfg.n_replicas
         self.h = lib().soa_create(C.byref(self.cfg))
         if not self.h:
             raise RuntimeError("soa_create failed")
+        ng = C.c_uint64()
+        lib().soa_local_groups(self.h, C.byref(ng), None)
+        self.n_groups = ng.value
+        self.n_rep = self.n_groups * self.cfg.n_replicas
         lib().soa_set_full_only(self.h, int(full_only))
         lib().soa_set_staged(self.h, int(staged))
 
@@ -190,7 +196,7 @@ class SoaCpu(NodeInputs):
 
     # group-range snapshots, same contract as Engine.export_groups / import_groups
     def export_groups(self, first=0, count=None, cap=None):
-        count = self.cfg.n_groups - first if count is None else count
+        count = self.n_groups - first if count is None else count
         n = lib().soa_snapshot_bytes(self.h, count) if cap is None else cap
         buf = C.create_string_buffer(max(1, n))
         rc = lib().soa_export_groups(self.h, first, count, buf, n)
@@ -207,6 +213,9 @@ class SoaCpu(NodeInputs):
         arr = (RbeReplicaView * self.n_rep)()
         lib().soa_views(self.h, C.cast(arr, C.c_void_p))
         return arr
+
+    def global_groups(self):
+        return global_groups_call(lib().soa_local_groups, self.h, self.n_groups)
 
     def iso_leaders(self):
         return iso_leaders_call(lib().soa_iso_leaders, self.h, self.cfg.n_groups)
@@ -225,8 +234,8 @@ class SoaCpu(NodeInputs):
         """Host-build rbe_wire_encode + rbe_wire_fetch: (stream bytes, frames)."""
         addrs = (C.c_char_p * 6)(*[a.encode() for a in source_address])
         n = self.cfg.n_replicas
-        gpb = groups_per_batch or self.cfg.n_groups
-        maxf = n * (n - 1) * ((self.cfg.n_groups + gpb - 1) // gpb)
+        gpb = groups_per_batch or self.n_groups
+        maxf = n * (n - 1) * ((self.n_groups + gpb - 1) // gpb)
         fr = (RbeWireFrame * max(1, maxf))()
         nf = C.c_uint32()
         cap = 1 << 24

@@ -67,7 +67,10 @@ static void run_round(SoaEngine* e, bool tick = true) {
   if (e->C.iso_period && e->round > 0 && e->round % e->C.iso_period == 0) {
     if (e->C.rep_world > 1) {  // the ORed leader bits of every rank (soa_set_iso_leaders)
       if (e->iso_round != e->round) abort();
-      for (u64 g = 0; g < e->C.n_groups; g++) iso_apply(e->P, e->C, g, e->round, e->iso_bits[g]);
+      for (u64 g = 0; g < e->C.n_groups; g++) {
+        const u64 gg = group_global(e->C, g);
+        if (gg < e->C.n_groups_glob) iso_apply(e->P, e->C, g, e->round, e->iso_bits[gg]);
+      }
     } else {
       for (u64 g = 0; g < e->C.n_groups; g++) iso_group<N>(e->P, e->C, g, e->round);
     }
@@ -225,6 +228,7 @@ void* soa_create(const rbe_config* cfg) {
   C.iso_mod = cfg->iso_mod;
   C.rep_world = cfg->rep_world > 1 ? cfg->rep_world : 1;
   C.rep_rank = cfg->rep_rank;
+  rep_compact_setup(C, cfg->rep_compact != 0);
   C.snapshot_entries = cfg->snapshot_entries;
   C.compaction_overhead = cfg->compaction_overhead;
   if (C.n != 1 && C.n != 3 && C.n != 5) {
@@ -264,8 +268,7 @@ void* soa_create(const rbe_config* cfg) {
   C.heap_bytes = (cfg->heap_bytes + 255) & ~255ull;
   e->heap.assign(C.heap_bytes, 0);
   e->hin.init(R, C.n, C.in_cap, C.heap_bytes);
-  e->hin.rep_world = C.rep_world;
-  e->hin.rep_rank = C.rep_rank;
+  e->hin.owner = C.rep_world > 1 ? &e->C : nullptr;
   if (C.heap_bytes) {
     P.heap_head = &e->heap_head;
     e->hin.heap.low_fn = [e](u64* lo) -> int {  // k_heap_low, group by group
@@ -709,14 +712,28 @@ int soa_iso_leaders(void* h, uint8_t* out, uint32_t* epoch) {
   const Params& C = e->C;
   *epoch = C.iso_period && e->round > 0 && e->round % C.iso_period == 0 ? 1u : 0u;
   if (!*epoch || !out) return RBE_OK;
-  for (u64 g = 0; g < C.n_groups; g++)
-    out[g] = (u8)(C.n == 5 ? iso_leader_bits<5>(e->P, C, g)
-                           : C.n == 3 ? iso_leader_bits<3>(e->P, C, g) : iso_leader_bits<1>(e->P, C, g));
+  memset(out, 0, C.n_groups_glob);
+  for (u64 g = 0; g < C.n_groups; g++) {
+    const u64 gg = group_global(C, g);  // exchanged by global group
+    if (gg >= C.n_groups_glob) continue;
+    out[gg] = (u8)(C.n == 5 ? iso_leader_bits<5>(e->P, C, g)
+                            : C.n == 3 ? iso_leader_bits<3>(e->P, C, g) : iso_leader_bits<1>(e->P, C, g));
+  }
+  return RBE_OK;
+}
+int soa_local_groups(void* h, uint64_t* n_local, uint64_t* global_of) {
+  SoaEngine* e = (SoaEngine*)h;
+  *n_local = e->C.n_groups;
+  if (global_of)
+    for (u64 g = 0; g < e->C.n_groups; g++) {
+      const u64 gg = group_global(e->C, g);
+      global_of[g] = gg < e->C.n_groups_glob ? gg : ~0ull;
+    }
   return RBE_OK;
 }
 int soa_set_iso_leaders(void* h, const uint8_t* bits) {
   SoaEngine* e = (SoaEngine*)h;
-  e->iso_bits.assign(bits, bits + e->C.n_groups);
+  e->iso_bits.assign(bits, bits + e->C.n_groups_glob);
   e->iso_round = e->round;
   return RBE_OK;
 }

@@ -35,6 +35,15 @@ CASES = {
     "C3_iso_w4": (dict(n_groups=20, n_replicas=5, check_quorum=True, wl_enabled=True,
                        wl_start_round=40, iso_period=50, iso_len=30, iso_mod=3), 4, 300,
                   dict(ring=128)),
+    # compacted planes (rep_compact): 3 replicas over 4 ranks, each rank holds
+    # the 3/4 of the groups it steps a replica of (W = 8: 3/8); n_groups not a
+    # multiple of W leaves padding groups; the second case adds the isolation
+    # schedule, whose leader bits are exchanged by global group
+    "C2_w4c": (dict(n_groups=22, n_replicas=3, wl_enabled=True, wl_start_round=30), 4, 200,
+               dict(rep_compact=True)),
+    "C3_iso_w4c": (dict(n_groups=22, n_replicas=3, check_quorum=True, wl_enabled=True,
+                        wl_start_round=40, iso_period=50, iso_len=30, iso_mod=3), 4, 300,
+                   dict(ring=128, rep_compact=True)),
 }
 CHECK_EVERY = 50
 
@@ -68,13 +77,20 @@ def _worker(rank, world, port, name, gpu, trace, q, fixed=False):
             eng = SoaCpu(trace=trace, rep_world=world, rep_rank=rank, **kw, **extra)
             xch = ReplicaExchange(eng, caps=caps, fixed=fixed)
         snaps = []
+        n = kw["n_replicas"]
+        gmap = eng.global_groups()  # local group -> global group (rep_compact)
         for done in range(CHECK_EVERY, rounds + 1, CHECK_EVERY):
             xch.run(CHECK_EVERY)
             vs = eng.views()
-            n = kw["n_replicas"]
-            own = {i: tuple(tuple(getattr(vs[i], f)) if hasattr(getattr(vs[i], f), "__len__")
-                            else getattr(vs[i], f) for f in FIELDS)
-                   for i in range(len(vs)) if (i // n + i % n) % world == rank}
+            own = {}
+            for i in range(len(vs)):
+                gl, k = divmod(i, n)
+                gg = int(gmap[gl])
+                if gg >= kw["n_groups"] or (gg + k) % world != rank:
+                    continue
+                own[gg * n + k] = tuple(tuple(getattr(vs[i], f))
+                                        if hasattr(getattr(vs[i], f), "__len__")
+                                        else getattr(vs[i], f) for f in FIELDS)
             snaps.append((done, own))
         nf = eng.fault_summary()[0] if gpu else eng.faults()[0]
         q.put((rank, snaps, eng.counters(), nf,
