@@ -451,8 +451,9 @@ int rbe_commit(rbe_engine* e, uint64_t n, const uint64_t* replica, const rbe_upd
  * sent between those replicas (group order; per replica the rbe_get_outbox
  * order).  InstallSnapshot messages are left out and counted: the reference
  * streams them as snapshot chunks, never in a MessageBatch
- * (transport.go:400-403).  Entries carry Index/Term/Type/Cmd (payload-heap
- * Cmds in full); Key/ClientID/SeriesID/RespondedTo are 0. */
+ * (transport.go:400-403).  Entries carry every raftpb.Entry field (payload-heap
+ * Cmds and session fields in full); a forwarded Propose carries its entries
+ * (raft.go:1841-1853). */
 typedef struct rbe_wire_frame {
   uint64_t offset, bytes;      /* frame (header included) in the encoded stream */
   uint64_t first_group;
