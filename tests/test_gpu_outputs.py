@@ -100,3 +100,41 @@ def test_gpu_collect_updates_large(gpu_available):
     assert np.array_equal(rep, want.astype(np.uint64))
     assert ups.tobytes() == full[want].tobytes()
     eng.close()
+
+
+@pytest.mark.parametrize("name,kw,extra", [("C3", C3, dict(ring=128)), ("C4", C4, {})])
+def test_gpu_collect_outputs_match_oracle(gpu_available, name, kw, extra):
+    """rbe_collect_outputs against the oracle harness itself, not the engine's
+    own getters: every sender's messages of the round, per destination, equal
+    (type, from, to, term, log_term, log_index, commit, reject, hint, number
+    of entries) the messages the oracle's network delivers to that destination
+    from that sender next round (the Quiesce notice aside: it is not a
+    Update.Messages entry in the engine's list form)."""
+    import oracle as O
+    from dragonboat_amd.engine import Engine
+    kw = dict(kw, n_groups=min(kw["n_groups"], 40))
+    eng = Engine(device=0, trace=True, **dict(kw, **extra))
+    ref = O.Harness(**kw)
+    n = kw["n_replicas"]
+    checked = 0
+    for rnd in range(150):
+        eng.step()
+        ref.step()
+        if rnd % 3:
+            continue
+        moff, msgs, _, _ = eng.collect_outputs()
+        for s in range(eng.n_rep):
+            g, k = divmod(s, n)
+            got = msgs[moff[s]:moff[s + 1]]
+            for d in range(n):
+                if d == k:
+                    continue
+                mine = [(int(m["type"]), int(m["from_"]), int(m["to"]), int(m["term"]),
+                         int(m["log_term"]), int(m["log_index"]), int(m["commit"]),
+                         int(m["reject"]), int(m["hint"]), int(m["n_entries"]))
+                        for m in got if int(m["to"]) == d + 1]
+                want = [t for t in ref.inbox(g * n + d, k) if t[0] != 21]
+                assert mine == want, (rnd + 1, s, d, mine, want)
+                checked += len(want)
+    assert checked > 500
+    eng.close()
