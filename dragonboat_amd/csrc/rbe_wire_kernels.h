@@ -347,6 +347,10 @@ struct WireMsgPos {
 // (coalesced), one lane walks the top-level fields inside it, and the window
 // moves to wherever the walk stops (a field header near the window's end, or
 // a request longer than the window, which is skipped without being read).
+__device__ __forceinline__ u32 uni32(u32 x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ u64 uni64(u64 x) {
+  return ((u64)uni32((u32)(x >> 32)) << 32) | uni32((u32)x);
+}
 static constexpr u32 kWireWin = 8192;
 static constexpr u32 kWireWalkBlock = 64;
 __global__ __launch_bounds__(kWireWalkBlock) void k_wire_bounds(const u8* data, WireIn* fr, int pass,
@@ -357,7 +361,7 @@ __global__ __launch_bounds__(kWireWalkBlock) void k_wire_bounds(const u8* data, 
   const WireIn f = fr[blockIdx.x];
   if (f.status) return;
   const u8* p = data + f.offset;
-  const u64 n = f.size;
+  const u64 n = uni64(f.size);
   if (threadIdx.x == 0) {
     s_at = 0;
     s_nm = 0;
@@ -366,7 +370,7 @@ __global__ __launch_bounds__(kWireWalkBlock) void k_wire_bounds(const u8* data, 
   __syncthreads();
   while (s_state == 0) {
     // 16-B aligned words from the one holding byte `base`, all in flight at once
-    const u64 base = s_at;
+    const u64 base = uni64(s_at);
     const u8* a0 = (const u8*)((u64)(p + base) & ~15ull);
     const u32 sh = (u32)((p + base) - a0);
     const u64 avail = n - base < kWireWin - sh ? n - base : kWireWin - sh;
@@ -377,8 +381,12 @@ __global__ __launch_bounds__(kWireWalkBlock) void k_wire_bounds(const u8* data, 
       if (wi < nw) ((uint4*)s_buf)[wi] = ((const uint4*)a0)[wi];
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      u64 i = base, nm = s_nm;
+    {
+      // Every lane of the wave runs the walk with the same values (each LDS
+      // read goes through readfirstlane), so the compiler keeps the walk in
+      // scalar registers and scalar branches: a single-lane vector walk paid
+      // a full wave issue for every instruction.
+      u64 i = uni64(base), nm = uni64(s_nm);
       u32 st = 0;
       const u64 wend = base + avail;
       // a field header (tag + length, <= 20 bytes) must lie in the window
@@ -395,7 +403,8 @@ __global__ __launch_bounds__(kWireWalkBlock) void k_wire_bounds(const u8* data, 
           // from 8 bytes taken with three aligned 4-byte LDS reads
           const u32 x = (u32)(i - base) + sh;
           const u32* w4 = (const u32*)s_buf;
-          const u32 a = w4[x >> 2], b = w4[(x >> 2) + 1], c = w4[(x >> 2) + 2];
+          const u32 a = uni32(w4[x >> 2]), b = uni32(w4[(x >> 2) + 1]),
+                    c = uni32(w4[(x >> 2) + 2]);
           const u32 s8 = (x & 3u) * 8u;
           const u64 lo = (u64)a | ((u64)b << 32);
           const u64 w8 = s8 ? (lo >> s8) | ((u64)c << (64 - s8)) : lo;
@@ -426,8 +435,10 @@ __global__ __launch_bounds__(kWireWalkBlock) void k_wire_bounds(const u8* data, 
                 break;
               }
               if ((tg >> 3) == 1) {
-                if (pass == 1) pos[f.msg0 + nm] = WireMsgPos{f.offset + q, v};
-                else if (pass == 2 && nm < f.pos_cap) pos[f.pos0 + nm] = WireMsgPos{f.offset + q, v};
+                if (threadIdx.x == 0) {
+                  if (pass == 1) pos[f.msg0 + nm] = WireMsgPos{f.offset + q, v};
+                  else if (pass == 2 && nm < f.pos_cap) pos[f.pos0 + nm] = WireMsgPos{f.offset + q, v};
+                }
                 nm++;
               }
               i = q + v;
@@ -439,7 +450,7 @@ __global__ __launch_bounds__(kWireWalkBlock) void k_wire_bounds(const u8* data, 
         bool ok = false;
         u64 q = i;
         for (u32 bs = 0; bs < 64 && q < wend; bs += 7) {
-          const u8 b = s_buf[(u32)(q++ - base) + sh];
+          const u8 b = (u8)uni32(s_buf[(u32)(q++ - base) + sh]);
           tag |= (u64)(b & 0x7F) << bs;
           if (b < 0x80) {
             ok = true;
@@ -455,7 +466,7 @@ __global__ __launch_bounds__(kWireWalkBlock) void k_wire_bounds(const u8* data, 
           u64 v = 0;
           ok = false;
           for (u32 bs = 0; bs < 64 && q < wend; bs += 7) {
-            const u8 b = s_buf[(u32)(q++ - base) + sh];
+            const u8 b = (u8)uni32(s_buf[(u32)(q++ - base) + sh]);
             v |= (u64)(b & 0x7F) << bs;
             if (b < 0x80) {
               ok = true;
@@ -472,8 +483,10 @@ __global__ __launch_bounds__(kWireWalkBlock) void k_wire_bounds(const u8* data, 
               break;
             }
             if (fn == 1) {
-              if (pass == 1) pos[f.msg0 + nm] = WireMsgPos{f.offset + q, v};
+              if (threadIdx.x == 0) {
+                if (pass == 1) pos[f.msg0 + nm] = WireMsgPos{f.offset + q, v};
                 else if (pass == 2 && nm < f.pos_cap) pos[f.pos0 + nm] = WireMsgPos{f.offset + q, v};
+              }
               nm++;
             }
             q += v;
@@ -490,9 +503,12 @@ __global__ __launch_bounds__(kWireWalkBlock) void k_wire_bounds(const u8* data, 
         }
         i = q;
       }
-      s_at = i;
-      s_nm = nm;
-      s_state = st;
+      __syncthreads();  // every lane has read the window before lane 0 moves it
+      if (threadIdx.x == 0) {
+        s_at = i;
+        s_nm = nm;
+        s_state = st;
+      }
     }
     __syncthreads();
   }
