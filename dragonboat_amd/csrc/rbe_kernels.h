@@ -62,6 +62,10 @@ static constexpr int kFullMode = RBE_FULL_DEFER ? MODE_FULL_DEFER : MODE_FULL;
 #define RBE_STAGE_FOLL 0
 #endif
 static constexpr u32 kTriChunk = RBE_TRI_CHUNK;   // replicas per k_triage block (8 per lane)
+#ifndef RBE_SMALL_TRI_MAX
+#define RBE_SMALL_TRI_MAX (1u << 22)
+#endif
+static constexpr u64 kSmallTriMax = RBE_SMALL_TRI_MAX;  // replicas up to which scan-only engines triage 256 per block
 static constexpr int kCtrStripes = 64;   // counter stripes per kernel slot (flush_counters)
 // counter sections, one per pipeline kernel (rbe_get_kernel_counters)
 enum : int { KS_TRIAGE = 0, KS_FAST_LEAD = 1, KS_FAST_FOLL = 2, KS_FULL = 3, KS_NUM = 4 };
@@ -250,11 +254,11 @@ __device__ __forceinline__ void list_clear_next(const Lists& L, u32 par, u32 nsl
 // round's awake list.
 template <int N>
 constexpr u32 kTriGroups = kTriChunk / N;
-template <int N, bool TRACE>
+template <int N, bool TRACE, u32 CHUNK = kTriChunk>
 __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg ra, Lists L) {
-  constexpr u32 GB = kTriGroups<N>;
+  constexpr u32 GB = CHUNK / N;
   constexpr u32 kNone = 7u;  // slot code of a replica that is not listed
-  __shared__ u32 s_idx[kTriChunk];
+  __shared__ u32 s_idx[CHUNK];
   __shared__ u32 s_gid[GB];  // triaged groups
   __shared__ u32 s_gst[GB];  // per triaged group: awake << 31 | busy replicas << 8 | leaders
   __shared__ u32 s_alg[GB];  // groups for the next round's awake list
@@ -359,7 +363,7 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
   // the wave) are loaded before any of them is processed; most rounds are then
   // decided without reading Hot: a lazy quiesced tick completes here, a
   // replica with inbound messages is listed by the role its idle byte carries.
-  constexpr u32 kPer = kTriChunk / kBlock;
+  constexpr u32 kPer = CHUNK / kBlock;
   const u32 nr = s_ng * (u32)N;
   const u32 iters = (nr + kBlock - 1) / kBlock;  // uniform over the block
   // global replica index of item t (items past the end map to item 0)
@@ -1023,8 +1027,16 @@ int launch_round(const Planes& P, const Params& C, const Lists& L, hipStream_t s
     mark(4);
   } else if (mode == 3) {
     mark(0);
-    hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(gtg), dim3(kBlock), 0, stream, P, C,
-                       ra, L);
+    // Without group sleep (list mode needs Quiesce and no trace) the block to
+    // group mapping is free: 256 replicas per block instead of 2,048, so a
+    // small engine (C2: 10k groups) is triaged by 118 blocks, not 15
+    if (!(C.quiesce && !TRACE) && C.n_rep <= kSmallTriMax)
+      hipLaunchKernelGGL((k_triage<N, TRACE, kBlock>),
+                         dim3((unsigned)((C.n_groups + kBlock / N - 1) / (kBlock / N))),
+                         dim3(kBlock), 0, stream, P, C, ra, L);
+    else
+      hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(gtg), dim3(kBlock), 0, stream, P, C,
+                         ra, L);
     mark(1);
     const unsigned gf = g < kFastGrid ? g : kFastGrid;
     hipLaunchKernelGGL((k_fast_both<N, TRACE>), dim3(gf), dim3(kBlock), 0, stream, P, C,
@@ -1036,8 +1048,16 @@ int launch_round(const Planes& P, const Params& C, const Lists& L, hipStream_t s
     mark(4);
   } else {
     mark(0);
-    hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(gtg), dim3(kBlock), 0, stream, P, C,
-                       ra, L);
+    // Without group sleep (list mode needs Quiesce and no trace) the block to
+    // group mapping is free: 256 replicas per block instead of 2,048, so a
+    // small engine (C2: 10k groups) is triaged by 118 blocks, not 15
+    if (!(C.quiesce && !TRACE) && C.n_rep <= kSmallTriMax)
+      hipLaunchKernelGGL((k_triage<N, TRACE, kBlock>),
+                         dim3((unsigned)((C.n_groups + kBlock / N - 1) / (kBlock / N))),
+                         dim3(kBlock), 0, stream, P, C, ra, L);
+    else
+      hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(gtg), dim3(kBlock), 0, stream, P, C,
+                         ra, L);
     mark(1);
     const unsigned gf = g < kFastGrid ? g : kFastGrid;
     hipLaunchKernelGGL((k_fast_list<N, TRACE, MODE_LEAD>), dim3(gf), dim3(kBlock), 0, stream,
