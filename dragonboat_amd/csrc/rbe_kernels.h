@@ -66,6 +66,13 @@ static constexpr u32 kTriChunk = RBE_TRI_CHUNK;   // replicas per k_triage block
 #define RBE_SMALL_TRI_MAX (1u << 22)
 #endif
 static constexpr u64 kSmallTriMax = RBE_SMALL_TRI_MAX;  // replicas up to which scan-only engines triage 256 per block
+#ifndef RBE_FAST_HALF_MAX
+#define RBE_FAST_HALF_MAX (1u << 17)  // below ~512 blocks of 256: C2 fast step 48.5 -> 45.6 us; C3 (500k) must not (352 -> 483 us)
+#endif
+// items per k_fast_both block chunk (and its grid: one block per chunk up to kFastGrid)
+RBE_HD u32 fast_items_per_block(const Params& C) {
+  return C.n_rep <= RBE_FAST_HALF_MAX ? 128u : 256u;
+}
 static constexpr int kCtrStripes = 64;   // counter stripes per kernel slot (flush_counters)
 // counter sections, one per pipeline kernel (rbe_get_kernel_counters)
 enum : int { KS_TRIAGE = 0, KS_FAST_LEAD = 1, KS_FAST_FOLL = 2, KS_FULL = 3, KS_NUM = 4 };
@@ -825,7 +832,10 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, 
   const u64 nlc = (nl + kBlock - 1) / kBlock, nfc = (n - nl + kBlock - 1) / kBlock;
   const u64 mix = nlc < nfc ? nlc : nfc;
   const bool mixed = RBE_FAST_MIX && !xcd;
-  const u64 nchunks = mixed ? nlc + nfc : (lim + kBlock - 1) / kBlock;
+  // a small engine spreads its items over twice the blocks (half of each
+  // block's lanes take an item), so more CUs share the step's memory traffic
+  const u32 per = fast_items_per_block(C);
+  const u64 nchunks = mixed ? nlc + nfc : (lim + per - 1) / per;
   const u64 cstride = xcd ? xblocks : gridDim.x;
   (void)stride;
   for (u64 ch = xcd ? blockIdx.x / kShards : blockIdx.x; ch < nchunks; ch += cstride) {
@@ -845,9 +855,9 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, 
       any = i < (lc ? (u64)nl : (u64)n);
       lead = lc && any;
     } else {
-      i = ch * kBlock + threadIdx.x;
-      lead = xcd ? i < xnl : i < nl;
-      any = i < lim;
+      i = ch * per + threadIdx.x;
+      any = threadIdx.x < per && i < lim;
+      lead = any && (xcd ? i < xnl : i < nl);
     }
     u32 r = 0, aux = 0;
     if (any) {
@@ -1038,7 +1048,8 @@ int launch_round(const Planes& P, const Params& C, const Lists& L, hipStream_t s
       hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(gtg), dim3(kBlock), 0, stream, P, C,
                          ra, L);
     mark(1);
-    const unsigned gf = g < kFastGrid ? g : kFastGrid;
+    const unsigned gfn = (unsigned)((C.n_rep + fast_items_per_block(C) - 1) / fast_items_per_block(C));
+    const unsigned gf = gfn < kFastGrid ? gfn : kFastGrid;
     hipLaunchKernelGGL((k_fast_both<N, TRACE>), dim3(gf), dim3(kBlock), 0, stream, P, C,
                        ra, L);
     mark(2);
@@ -1059,7 +1070,8 @@ int launch_round(const Planes& P, const Params& C, const Lists& L, hipStream_t s
       hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(gtg), dim3(kBlock), 0, stream, P, C,
                          ra, L);
     mark(1);
-    const unsigned gf = g < kFastGrid ? g : kFastGrid;
+    const unsigned gfn = (unsigned)((C.n_rep + fast_items_per_block(C) - 1) / fast_items_per_block(C));
+    const unsigned gf = gfn < kFastGrid ? gfn : kFastGrid;
     hipLaunchKernelGGL((k_fast_list<N, TRACE, MODE_LEAD>), dim3(gf), dim3(kBlock), 0, stream,
                        P, C, ra, L);
     mark(2);
