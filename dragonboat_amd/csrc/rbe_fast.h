@@ -584,7 +584,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   const u64 g = r / N;
   const u32 k = (u32)(r % N);
   const u32 par = round & 1u, ppar = par ^ 1u;
-  const u64 cid = cid_of(C, g);
+  const u64 cid = cid_of_n<N>(C, g);
   // ---- gather, level 1: independent loads
   RBE_RSTAMP(rt0);
   RBE_STAMP(t0);
@@ -1359,7 +1359,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   if (h.flags & (HF_APPLY_PENDING | HF_IS_LTT)) return false;
   if (c.ltt != 0) return false;
   if (!ck.tick) return false;
-  if (C.xfer_period && xfer_input(C, cid_of(C, g), round, k)) return false;
+  if (C.xfer_period && xfer_input(C, cid_of_n<N>(C, g), round, k)) return false;
   if (C.ext_inputs && P.ext[r].flags) return false;
   const u32 ls = (u32)c.leader - 1u;  // leader slot (0xFFFFFFFF when no leader)
   u32 n_in = 0;

@@ -337,7 +337,7 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
     const u32 g = gids[i];
     const bool awake = (gws[i] & GW_AWAKE) != 0;
     bool work = j < gn;
-    if (work && !awake && !group_forced(C, cid_of(C, (u64)g), round)) {
+    if (work && !awake && !group_forced(C, cid_of_n<N>(C, (u64)g), round)) {
       work = false;
       u32 own = 0;
       for (u32 k = 0; k < (u32)N; k++) own += owned<N>(C, (u64)g * N + k) ? 1u : 0u;
@@ -439,7 +439,7 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
     // receiving a Replicate
     bool back = false;
     if (cls == T_LEAD)
-      back = wl_input(C, cid_of(C, (u64)((u32)r / (u32)N)), round) == 1u;
+      back = wl_input(C, cid_of_n<N>(C, (u64)((u32)r / (u32)N)), round) == 1u;
     else if (cls == T_FOLL)
       back = (inb & 4u) != 0;
     const u32 code = cls == T_DONE ? kNone : (back ? cls + 2u : cls - 1u);
@@ -483,7 +483,7 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
         const u32 st = s_gst[j];
         g = s_gid[j];
         const bool awake = (st >> 31) != 0;
-        const u32 tr = group_transition(C, cid_of(C, (u64)g), round, awake,
+        const u32 tr = group_transition(C, cid_of_n<N>(C, (u64)g), round, awake,
                                         (st >> 8) & 0xFFu);
         if (tr == GS_SLEEP) P.gwake[g] = group_sleep_byte(st & 0xFFu);
         if (tr == GS_WAKE) P.gwake[g] = GW_AWAKE;
@@ -834,8 +834,10 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, 
   const bool mixed = RBE_FAST_MIX && !xcd;
   // a small engine spreads its items over twice the blocks (half of each
   // block's lanes take an item), so more CUs share the step's memory traffic
+  // (a power of two: shifts, no 64-bit division in this kernel's registers)
   const u32 per = fast_items_per_block(C);
-  const u64 nchunks = mixed ? nlc + nfc : (lim + per - 1) / per;
+  const u32 per_log = per == 128u ? 7u : 8u;
+  const u64 nchunks = mixed ? nlc + nfc : (lim + per - 1) >> per_log;
   const u64 cstride = xcd ? xblocks : gridDim.x;
   (void)stride;
   for (u64 ch = xcd ? blockIdx.x / kShards : blockIdx.x; ch < nchunks; ch += cstride) {
@@ -855,7 +857,7 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, 
       any = i < (lc ? (u64)nl : (u64)n);
       lead = lc && any;
     } else {
-      i = ch * per + threadIdx.x;
+      i = (ch << per_log) + threadIdx.x;
       any = threadIdx.x < per && i < lim;
       lead = any && (xcd ? i < xnl : i < nl);
     }

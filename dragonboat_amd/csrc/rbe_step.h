@@ -31,6 +31,13 @@ RBE_HD u64 group_global(const Params& C, u64 g) {
   return C.rep_compact ? (g / C.n) * C.rep_world + C.res[g % C.n] : g;
 }
 RBE_HD u64 cid_of(const Params& C, u64 g) { return C.cid_base + group_global(C, g) * C.cid_stride; }
+// the same with the group size a compile-time constant (the step kernels:
+// no 64-bit division by a runtime value in their register budget)
+template <int N>
+RBE_HD u64 cid_of_n(const Params& C, u64 g) {
+  const u64 gg = C.rep_compact ? (g / N) * C.rep_world + C.res[g % N] : g;
+  return C.cid_base + gg * C.cid_stride;
+}
 // Is replica k of local group g stepped by this engine?  (replica mode:
 // replica k of global group G is stepped on rank (G + k) % rep_world; the
 // padding groups of a compacted engine by none)
