@@ -405,7 +405,12 @@ _CALLS = ["become_follower", "become_candidate", "become_leader", "tick", "quies
           "log_has_entries_to_apply", "log_first_not_applied_index", "inmem_saved_log_to",
           "time_for_election", "set_randomized_election_timeout", "abort_leader_transfer",
           "leader_transfering", "quiesced_tick_direct", "non_leader_tick", "leader_tick",
-          "load_state"]
+          "load_state",
+          # rate limiter (server/rate.go; raft.go:660-683, 1779-1785)
+          "rl_set_max", "rl_get", "rl_tick", "rl_rate_limited", "rl_enabled", "rl_increase",
+          "rl_decrease", "rl_set", "rl_set_follower", "rl_follower_count", "rl_follower_size",
+          "rl_follower_tick", "rl_heartbeat_tick", "rl_gc", "rl_reset_followers",
+          "rl_handle_leader_rate_limit", "rl_append_entries"]
 _CALL_IDX = {n: i for i, n in enumerate(_CALLS)}
 KIND = {"remotes": 0, "observers": 1, "witnesses": 2}
 

@@ -351,7 +351,12 @@ enum RaftCall {
   C_HANDLE_VOTE_RESP, C_CAN_GRANT_VOTE, C_INMEM_TRY_RESIZE, C_INMEM_RESIZE,
   C_LOG_HAS_ENTRIES_TO_APPLY, C_LOG_FIRST_NOT_APPLIED, C_LOG_SAVED_LOG_TO, C_TIME_FOR_ELECTION,
   C_SET_RANDOMIZED_ET, C_ABORT_LT, C_LEADER_TRANSFERING, C_QUIESCED_TICK_DIRECT,
-  C_NON_LEADER_TICK, C_LEADER_TICK, C_LOAD_STATE
+  C_NON_LEADER_TICK, C_LEADER_TICK, C_LOAD_STATE,
+  // rate limiter (server/rate.go, raft.go:660-683, 1779-1785)
+  C_RL_SET_MAX, C_RL_GET, C_RL_TICK, C_RL_RATE_LIMITED, C_RL_ENABLED, C_RL_INCREASE,
+  C_RL_DECREASE, C_RL_SET, C_RL_SET_FOLLOWER, C_RL_FOLLOWER_COUNT, C_RL_FOLLOWER_SIZE,
+  C_RL_FOLLOWER_TICK, C_RL_HEARTBEAT_TICK, C_RL_GC, C_RL_RESET_FOLLOWERS,
+  C_RL_HANDLE_LEADER_RATE_LIMIT, C_RL_APPEND_ENTRIES
 };
 
 int64_t orc_raft_call(void* rp, int fn, uint64_t a, uint64_t b) {
@@ -402,6 +407,42 @@ int64_t orc_raft_call(void* rp, int fn, uint64_t a, uint64_t b) {
     case C_NON_LEADER_TICK: r->nonLeaderTick(); return 0;
     case C_LEADER_TICK: r->leaderTick(); return 0;
     case C_LOAD_STATE: { PState st; st.term = a; st.commit = b; r->loadState(st); return 0; }
+    case C_RL_SET_MAX: r->rl.maxSize = a; return 0;  // newRateLimitedTestRaft
+    case C_RL_GET: return (int64_t)r->rl.get();
+    case C_RL_TICK: return (int64_t)r->rl.tick;
+    case C_RL_RATE_LIMITED: return r->rl.rateLimited() ? 1 : 0;
+    case C_RL_ENABLED: return r->rl.enabled() ? 1 : 0;
+    case C_RL_INCREASE: r->rl.increase(a); return 0;
+    case C_RL_DECREASE: r->rl.decrease(a); return 0;
+    case C_RL_SET: r->rl.set(a); return 0;
+    case C_RL_SET_FOLLOWER: r->rl.setFollowerState(a, b); return 0;
+    case C_RL_FOLLOWER_COUNT: return (int64_t)r->rl.followerSizes.size();
+    case C_RL_FOLLOWER_SIZE: {
+      auto it = r->rl.followerSizes.find(a);
+      return it == r->rl.followerSizes.end() ? -1 : (int64_t)it->second.second;
+    }
+    case C_RL_FOLLOWER_TICK: {
+      auto it = r->rl.followerSizes.find(a);
+      return it == r->rl.followerSizes.end() ? -1 : (int64_t)it->second.first;
+    }
+    case C_RL_HEARTBEAT_TICK: r->rl.heartbeatTick(); return 0;
+    case C_RL_GC: r->rl.gc(); return 0;
+    case C_RL_RESET_FOLLOWERS: r->rl.resetFollowerState(); return 0;
+    case C_RL_HANDLE_LEADER_RATE_LIMIT: {
+      Message m;
+      m.type = RateLimit;
+      m.from = a;
+      m.hint = b;
+      r->handleLeaderRateLimit(m);
+      return 0;
+    }
+    case C_RL_APPEND_ENTRIES: {  // appendEntries of one ApplicationEntry with a b-byte Cmd
+      std::vector<Entry> ents(1);
+      ents[0].type = ApplicationEntry;
+      ents[0].cmd.assign((size_t)b, '\0');
+      r->appendEntries(ents);
+      return 0;
+    }
     default: g_err = "bad call"; return -1000;
   }
   GUARD_END(-999)
@@ -963,7 +1004,11 @@ void* orc_inmem_new(uint64_t marker, const orc_entry* ents, int n, uint64_t save
   im->shrunk = shrunk != 0;
   return im;
 }
-void orc_inmem_free(void* h) { delete (InMemory*)h; }
+void orc_inmem_free(void* h) {
+  auto* im = (InMemory*)h;
+  delete im->rl;  // unit handles own their limiter (op 11)
+  delete im;
+}
 int orc_inmem_merge(void* h, const orc_entry* ents, int n) {
   GUARD_BEGIN
   std::vector<Entry> v;
@@ -974,7 +1019,9 @@ int orc_inmem_merge(void* h, const orc_entry* ents, int n) {
 }
 // op: 0 savedLogTo(a, b), 1 appliedLogTo(a), 2 getLastIndex (-1 when !ok),
 //     3 getTerm(a) (-1 when !ok), 4 markerIndex, 5 savedTo, 6 shrunk, 7 len(entries),
-//     8 entries[0].Index (-1 when empty), 9 restore(Snapshot{Index: a, Term: b}), 10 resize
+//     8 entries[0].Index (-1 when empty), 9 restore(Snapshot{Index: a, Term: b}), 10 resize,
+//     11 attach a RateLimiter of maxSize a (newInMemory(_, server.NewRateLimiter(a))),
+//     12 rl.Get(), 13 newEntries
 int64_t orc_inmem_op(void* h, int op, uint64_t a, uint64_t b) {
   GUARD_BEGIN
   auto* im = (InMemory*)h;
@@ -997,6 +1044,14 @@ int64_t orc_inmem_op(void* h, int op, uint64_t a, uint64_t b) {
       return 0;
     }
     case 10: im->resize(); return 0;
+    case 11: {
+      delete im->rl;
+      im->rl = new RateLimiter();
+      im->rl->maxSize = a;
+      return 0;
+    }
+    case 12: return im->rl ? (int64_t)im->rl->get() : -1;
+    case 13: return im->newEntries ? 1 : 0;
     default: return -2;
   }
   GUARD_END(-3)

@@ -221,13 +221,22 @@ void InMemory::appliedLogTo(u64 index) {  // inmemory.go:139-167
   if (entries.empty()) return;
   if (index > entries.back().index) return;
   u64 newMarkerIndex = index;
+  // applied := entries[:move], less its first entry (the previous marker,
+  // already counted off) unless the window was rebuilt since
+  u64 move = newMarkerIndex - markerIndex;
+  if (newMarkerIndex - markerIndex + 1 <= (u64)entries.size()) move = newMarkerIndex - markerIndex + 1;
+  u64 appliedSz = 0;
+  if (rateLimited()) {
+    std::vector<Entry> applied(entries.begin() + (newEntries ? 0 : 1), entries.begin() + move);
+    appliedSz = entrySliceInMemSize(applied);
+  }
   newEntries = false;
   shrunk = true;
   entries.erase(entries.begin(), entries.begin() + (newMarkerIndex - markerIndex));
   markerIndex = newMarkerIndex;
   resizeEntrySlice();
   checkMarkerIndex();
-  // rate limiter (im.rl.Decrease) is disabled: MaxInMemLogSize=0
+  if (rateLimited()) rl->decrease(appliedSz);
 }
 
 void InMemory::savedSnapshotTo(u64 index) {  // inmemory.go:169-175
@@ -250,11 +259,16 @@ void InMemory::merge(const std::vector<Entry>& ents) {  // inmemory.go:201-234
   if (firstNewIndex == markerIndex + entries.size()) {
     checkEntriesToAppend(entries, ents);
     entries.insert(entries.end(), ents.begin(), ents.end());
+    if (rateLimited()) rl->increase(entrySliceInMemSize(ents));
   } else if (firstNewIndex <= markerIndex) {
     markerIndex = firstNewIndex;
     shrunk = false;
     entries = ents;
     savedTo = firstNewIndex - 1;
+    if (rateLimited()) {
+      newEntries = true;
+      rl->set(entrySliceInMemSize(ents));
+    }
   } else {
     std::vector<Entry> existing = getEntries(markerIndex, firstNewIndex);
     checkEntriesToAppend(existing, ents);
@@ -262,6 +276,10 @@ void InMemory::merge(const std::vector<Entry>& ents) {  // inmemory.go:201-234
     entries = existing;
     entries.insert(entries.end(), ents.begin(), ents.end());
     savedTo = umin(savedTo, firstNewIndex - 1);
+    if (rateLimited()) {
+      rl->set(entrySliceInMemSize(ents) + entrySliceInMemSize(existing));
+      newEntries = true;
+    }
   }
   checkMarkerIndex();
 }
@@ -273,6 +291,47 @@ void InMemory::restore(const Snapshot& ss) {  // inmemory.go:236-246
   shrunk = false;
   entries.clear();
   savedTo = ss.index;
+  if (rateLimited()) {
+    newEntries = true;
+    rl->set(0);
+  }
+}
+
+// ---------------------------------------------------------------- server/rate.go
+bool RateLimiter::rateLimited() {  // limitedByInMemSize, rate.go:113-137
+  if (!enabled()) return false;
+  u64 maxInMemSize = 0;
+  bool gcNeeded = false;
+  for (auto& kv : followerSizes) {
+    if (tick - kv.second.first > RateLimitGcTick) {
+      gcNeeded = true;
+      continue;
+    }
+    if (kv.second.second > maxInMemSize) maxInMemSize = kv.second.second;
+  }
+  u64 sz = get();
+  if (sz > maxInMemSize) maxInMemSize = sz;
+  if (gcNeeded) gc();
+  return maxInMemSize > maxSize;
+}
+
+void RateLimiter::gc() {  // rate.go:139-149
+  for (auto it = followerSizes.begin(); it != followerSizes.end();) {
+    if (tick - it->second.first > RateLimitGcTick) it = followerSizes.erase(it);
+    else ++it;
+  }
+}
+
+u64 entrySliceSize(const std::vector<Entry>& ents) {  // raftpb/raft.go:301-307
+  u64 sz = 0;
+  for (auto& e : ents) sz += e.sizeUpperLimit();
+  return sz;
+}
+
+u64 entrySliceInMemSize(const std::vector<Entry>& ents) {  // raftpb/raft.go:311-322
+  u64 sz = 0;
+  for (auto& e : ents) sz += (u64)e.cmd.size() + GoEntryStructSize;
+  return sz;
 }
 
 // ---------------------------------------------------------------- logentry.go
@@ -626,8 +685,9 @@ Raft::Raft(const Config& c, ILogDB* logdb) {  // newRaft, raft.go:234-289
   if (c.nodeID == 0) panicf("invalid node id");
   if (c.electionRTT == 0 || c.heartbeatRTT == 0 || c.electionRTT <= 2 * c.heartbeatRTT)
     panicf("invalid election/heartbeat rtt");  // config.go Validate
-  if (c.maxInMemLogSize != 0) panicf("rate limiter not supported by the oracle");
   if (logdb == nullptr) panicf("logdb is nil");
+  rl.maxSize = c.maxInMemLogSize;  // server.NewRateLimiter(c.MaxInMemLogSize)
+  log.inmem.rl = &rl;
   clusterID = c.clusterID;
   nodeID = c.nodeID;
   leaderID = NoLeader;
@@ -766,7 +826,10 @@ void Raft::tick() {  // raft.go:551-564
 void Raft::nonLeaderTick() {  // raft.go:566-590
   if (isLeader()) panicf("noleader tick called on leader node");
   electionTick++;
-  // rate limit check: rl disabled (MaxInMemLogSize=0)
+  if (timeForRateLimitCheck() && rl.enabled()) {
+    rl.heartbeatTick();
+    sendRateLimitMessage();
+  }
   if (isObserver() || isWitness()) return;
   if (!selfRemoved() && timeForElection()) {
     electionTick = 0;
@@ -780,6 +843,7 @@ void Raft::nonLeaderTick() {  // raft.go:566-590
 void Raft::leaderTick() {  // raft.go:592-621
   mustBeLeader();
   electionTick++;
+  if (timeForRateLimitCheck() && rl.enabled()) rl.heartbeatTick();
   bool abortLT = timeToAbortLeaderTransfer();
   if (timeForCheckQuorum()) {
     electionTick = 0;
@@ -1022,6 +1086,7 @@ void Raft::reset(u64 t) {  // raft.go:989-1008
     term = t;
     vote = NoLeader;
   }
+  if (rl.enabled()) rl.resetFollowerState();
   votes.clear();
   electionTick = 0;
   heartbeatTick = 0;
@@ -1459,7 +1524,26 @@ void Raft::handleLeaderSnapshotStatus(const Message& m, Remote* rp) {  // raft.g
 
 void Raft::handleLeaderUnreachable(const Message&, Remote* rp) { enterRetryState(rp); }  // raft.go:1773-1777
 
-void Raft::handleLeaderRateLimit(const Message&) {}  // raft.go:1779-1785: rl disabled → dropped
+void Raft::handleLeaderRateLimit(const Message& m) {  // raft.go:1779-1785
+  if (rl.enabled()) rl.setFollowerState(m.from, m.hint);
+  // else: dropped (rl disabled)
+}
+
+void Raft::sendRateLimitMessage() {  // raft.go:660-683
+  if (isLeader()) panicf("leader node called sendRateLimitMessage");
+  if (leaderID == NoLeader) return;  // skipped, no leader
+  if (!rl.enabled()) return;
+  u64 mv = 0;
+  if (rl.rateLimited()) {
+    // max(inmemSz-notCommitedSz, 0) on uint64: the difference wraps
+    mv = rl.get() - entrySliceSize(log.getUncommittedEntries());
+  }
+  Message m;
+  m.type = RateLimit;
+  m.to = leaderID;
+  m.hint = mv;
+  send(m);
+}
 
 void Raft::handleFollowerPropose(Message& m) {  // raft.go:1841-1853
   if (leaderID == NoLeader) {

@@ -225,6 +225,33 @@ struct TestLogDB : ILogDB {
   Err Append(const std::vector<Entry>& entries) override;
 };
 
+// internal/server/rate.go:33-137: the in-memory log size limiter.  Go's
+// follower map holds (tick, inMemLogSize) per follower; gc() drops the states
+// older than gcTick heartbeat ticks.
+constexpr u64 RateLimitGcTick = 2;  // rate.go:25 gcTick
+struct RateLimiter {
+  u64 size = 0;
+  u64 tick = 0;
+  u64 maxSize = 0;
+  std::map<u64, std::pair<u64, u64>> followerSizes;  // nodeID -> (tick, inMemLogSize)
+
+  bool enabled() const { return maxSize > 0 && maxSize != ~0ull; }  // rate.go:59-61
+  void heartbeatTick() { tick++; }                                    // rate.go:64-66
+  void increase(u64 sz) { size += sz; }                               // rate.go:74-76
+  void decrease(u64 sz) { size -= sz; }  // rate.go:79-81 (AddUint64 of ^(sz-1): wraps)
+  void set(u64 sz) { size = sz; }
+  u64 get() const { return size; }
+  void resetFollowerState() { followerSizes.clear(); }              // rate.go:94-96
+  void setFollowerState(u64 nodeID, u64 sz) { followerSizes[nodeID] = {tick, sz}; }
+  bool rateLimited();                                                 // rate.go:109-111
+  void gc();                                                          // rate.go:139-149
+};
+// raftpb/raft.go:301-322: SizeUpperLimit sum, and the in-memory size (Cmd
+// bytes + unsafe.Sizeof(pb.Entry) = 80 on 64-bit Go: 7 words + a slice header)
+constexpr u64 GoEntryStructSize = 80;
+u64 entrySliceSize(const std::vector<Entry>& ents);
+u64 entrySliceInMemSize(const std::vector<Entry>& ents);
+
 // inmemory.go:36-44
 struct InMemory {
   bool shrunk = false;
@@ -234,7 +261,9 @@ struct InMemory {
   std::vector<Entry> entries;
   u64 markerIndex = 0;
   u64 savedTo = 0;
+  RateLimiter* rl = nullptr;  // the raft's limiter (newEntryLog(logdb, rl))
 
+  bool rateLimited() const { return rl != nullptr && rl->enabled(); }  // inmemory.go:248-250
   void init(u64 lastIndex);  // newInMemory, inmemory.go:46-57
   void checkMarkerIndex() const;
   std::vector<Entry> getEntries(u64 low, u64 high) const;
@@ -346,7 +375,7 @@ struct Config {
   bool quiesce = false;
   bool isObserver = false;
   bool isWitness = false;
-  u64 maxInMemLogSize = 0;  // rate limiter: only 0 (disabled) supported
+  u64 maxInMemLogSize = 0;  // rate limiter (server.NewRateLimiter), 0 = disabled
   u64 rngSeed = 0x5EEDD8A6ULL;  // injected PRNG seed (replaces goutils random)
   u64 maxEntrySize = DefaultMaxEntrySize;
 };
@@ -395,6 +424,7 @@ struct Raft {
   u64 rngSeed = 0;
   u64 rngCount = 0;  // number of randomized timeouts drawn so far
   u64 maxEntrySize = DefaultMaxEntrySize;
+  RateLimiter rl;  // raft.go:204; the in-memory log reports its size to it
 
   Raft(const Config& c, ILogDB* logdb);  // newRaft, raft.go:234-289
   void setTestPeers(const std::vector<u64>& peers);
@@ -438,6 +468,7 @@ struct Raft {
   void broadcastHeartbeatMessage();
   void broadcastHeartbeatMessageWithHint(SystemCtx ctx);
   void sendTimeoutNowMessage(u64 nodeID);
+  void sendRateLimitMessage();  // raft.go:660-683
   void sortMatchValues();
   bool tryCommit();
   void appendEntries(std::vector<Entry> entries);
@@ -527,6 +558,7 @@ struct Raft {
 struct Peer {
   Raft* raft = nullptr;
   PState prevState;
+  bool rateLimited() { return raft->rl.rateLimited(); }  // peer.go:245-249
 
   ~Peer() { delete raft; }
   static Peer* Launch(const Config& c, ILogDB* logdb,
