@@ -430,7 +430,7 @@ static int read_heap(rbe_engine* e, u64 pos, u64 off, u64 len, u8* dst) {
 }
 
 
-static constexpr int kPlaneAllocs = 23;
+static constexpr int kPlaneAllocs = 24;
 static u64 bytes_of(const Params& C, u64* parts) {
   const u64 N = C.n, G = C.n_groups, R = C.n_rep;
   u64 p[kPlaneAllocs] = {
@@ -456,7 +456,8 @@ static u64 bytes_of(const Params& C, u64* parts) {
       G * sizeof(u8),
       C.snapshot_entries ? R * sizeof(SnapSt) : 0,
       C.snapshot_entries ? R * N * sizeof(u64) : 0,
-      C.ext_commit ? R * sizeof(u64) : 0,
+      (C.ext_commit || C.rl_max) ? R * sizeof(u64) : 0,
+      C.rl_max ? R * sizeof(RlSt) : 0,
   };
   u64 t = 0;
   for (int i = 0; i < kPlaneAllocs; i++) {
@@ -517,6 +518,8 @@ static int make_params(const rbe_config* cfg, Params* out) {
   // is then the host's (rbe_notify_applied), never the step's own
   C.ext_commit = cfg->ext_commit;
   if (C.ext_commit && !C.ext_apply) return RBE_E_INVALID;
+  C.rl_max = cfg->max_inmem_log_size;
+  if (C.rl_max && C.ext_commit) return RBE_E_INVALID;  // appliedLogTo of rbe_commit: not yet
   C.membership = cfg->membership;
   C.cc_period = cfg->cc_period;
   C.cc_mod = cfg->cc_mod ? cfg->cc_mod : 1;
@@ -776,7 +779,8 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   P.gwake = (u8*)ptrs[19];
   P.snp = C.snapshot_entries ? (SnapSt*)ptrs[20] : nullptr;
   P.rem_snap = C.snapshot_entries ? (u64*)ptrs[21] : nullptr;
-  P.imark = C.ext_commit ? (u64*)ptrs[22] : nullptr;
+  P.imark = (C.ext_commit || C.rl_max) ? (u64*)ptrs[22] : nullptr;
+  P.rl = C.rl_max ? (RlSt*)ptrs[23] : nullptr;
   HIP_IGNORE(hipMemsetAsync(P.gwake, GW_AWAKE, C.n_groups, e->stream));  // every group starts awake
   e->hin.init(C.n_rep, C.n, C.in_cap, C.heap_bytes);
   e->hin.owner = C.rep_world > 1 ? &e->C : nullptr;
@@ -1468,6 +1472,21 @@ int rbe_reset_counters(rbe_engine* e) {
   HIP_OK(hipSetDevice(e->device));
   HIP_OK(hipMemsetAsync(e->P.counters, 0, kCtrWords * sizeof(u64), e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
+  return RBE_OK;
+}
+
+int rbe_rate_limited(rbe_engine* e, uint64_t first, uint64_t count, uint8_t* limited,
+                     uint64_t* in_mem_log_size) {
+  if (!e || count == 0 || first >= e->C.n_rep || count > e->C.n_rep - first) return RBE_E_INVALID;
+  if (!e->P.rl) return RBE_E_STATE;
+  HIP_OK(hipSetDevice(e->device));
+  std::vector<RlSt> rl(count);
+  if (d2h(e, rl.data(), e->P.rl + first, count)) return RBE_E_HIP;
+  HIP_OK(hipStreamSynchronize(e->stream));
+  for (u64 i = 0; i < count; i++) {
+    if (limited) limited[i] = rl_limited(rl[i], e->C.rl_max) ? 1 : 0;
+    if (in_mem_log_size) in_mem_log_size[i] = rl[i].size;
+  }
   return RBE_OK;
 }
 

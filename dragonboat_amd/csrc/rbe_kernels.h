@@ -430,7 +430,7 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
       if (shortcut && triage_lazy<N>(P, C, r, ck, ib, inb & 1u, c))
         done = true;
       else if (inb & 2u)
-        cls = class_of_role(idle_role(ib));
+        cls = C.rl_max ? T_FULL : class_of_role(idle_role(ib));
       else
         cls = triage_replica<N, TRACE>(P, C, r, ck, c);
       if (shortcut) atomicAdd(&s_gst[slot], ((ib & IB_LEAD) ? 1u : 0u) + (done ? 0u : 256u));

@@ -33,6 +33,28 @@ RBE_HD u64 group_global(const Params& C, u64 g) {
 RBE_HD u64 cid_of(const Params& C, u64 g) { return C.cid_base + group_global(C, g) * C.cid_stride; }
 // the same with the group size a compile-time constant (the step kernels:
 // no 64-bit division by a runtime value in their register budget)
+// rate limiter (server/rate.go): Enabled and RateLimited with its gc (rate.go:
+// 109-149): the largest fresh follower report or the replica's own in-memory
+// log size above the limit
+RBE_HD bool rl_enabled(u64 max) { return max > 0 && max != ~0ull; }  // rate.go:59-61
+// rl.RateLimited() (rate.go:109-137) with its gc: the largest fresh follower
+// report or the replica's own size above the limit
+RBE_HD bool rl_limited(RlSt& s, u64 max) {
+  if (!rl_enabled(max)) return false;
+  u64 m = 0;
+  for (u32 i = 0; i < 8; i++) {
+    if (!((s.fmask >> i) & 1u)) continue;
+    if (s.tick - s.f_tick[i] > kRlGcTick) {
+      s.fmask &= ~(1u << i);  // gc()
+      continue;
+    }
+    if (s.f_size[i] > m) m = s.f_size[i];
+  }
+  if (s.size > m) m = s.size;
+  return m > max;
+}
+// the in-memory marker (Planes::imark) is kept for rbe_commit and for the limiter
+RBE_HD bool imark_on(const Params& C) { return C.ext_commit || C.rl_max; }
 template <int N>
 RBE_HD u64 cid_of_n(const Params& C, u64 g) {
   const u64 gg = C.rep_compact ? (g / N) * C.rep_world + C.res[g % N] : g;
@@ -869,6 +891,7 @@ struct Lane {
     ltt = 0;
     reset_remotes();
     seg_len = 0;
+    if (rl_on()) P.rl[r].fmask = 0;  // rl.ResetFollowerState
   }
   RBE_HD void become_follower(u64 t, u8 lid) {  // raft.go:947-955
     role = R_Follower;
@@ -904,11 +927,70 @@ struct Lane {
   // appendEntries (raft.go:909-920) for one entry
   RBE_HD void append_entry(u32 type, u32 len, u64 lo, u64 hi) {
     u64 idx = last + 1;
+    rl_grow(len);
     ring_put(idx, term, type, len, lo, hi);
     last = idx;
     t_last = term;
     try_update(k, last);
     if (quorum() == 1) try_commit();
+  }
+
+  // ------------------------------------------------------------- rate limiter
+  // server.RateLimiter through the in-memory log's size hooks (inmemory.go:
+  // 139-246) and raft.go:660-683; sizes from the payload ring's Cmd lengths
+  RBE_HD bool rl_on() const { return rl_enabled(C.rl_max); }
+  RBE_HD void rl_grow(u32 len) {  // merge of an appended entry: rl.Increase
+    if (rl_on()) P.rl[r].size += kEntryInMem + len;
+  }
+  // sum over log entries [lo, hi] of `base` + Cmd length (the ring holds them
+  // while last - i < ring; F_WINDOW otherwise)
+  RBE_HD u64 rl_range(u64 lo, u64 hi, u64 base) {
+    u64 s = 0;
+    for (u64 i = lo; i <= hi && i >= lo; i++) {
+      if (last - i >= C.ring) {
+        set_fault(F_WINDOW);
+        break;
+      }
+      s += base + P.pay_ring[ring_slot(i)].len;
+    }
+    return s;
+  }
+  // inMemory.merge (inmemory.go:201-234) of entries from `first` on, before
+  // the ring takes them: append, replace or cut-and-append
+  RBE_HD void rl_merge(u64 first, const Ent* ents, u32 cnt) {
+    RlSt& s = P.rl[r];
+    u64 add = 0;
+    for (u32 i = 0; i < cnt; i++) add += kEntryInMem + ents[i].len;
+    const u64 im = P.imark[r];
+    if (first == last + 1) {
+      s.size += add;
+    } else if (first <= im) {
+      s.new_ent = 1;
+      s.size = add;
+    } else {
+      s.size = add + rl_range(im, first - 1, kEntryInMem);
+      s.new_ent = 1;
+    }
+  }
+  // inMemory.appliedLogTo (inmemory.go:139-167): the marker moves to `idx` and
+  // the entries applied leave the count, the old marker only after a rebuild
+  RBE_HD void rl_applied_to(u64 idx) {
+    const u64 im = P.imark[r];
+    if (idx < im || im > last || idx > last) return;
+    RlSt& s = P.rl[r];
+    const u64 lo = s.new_ent ? im : im + 1;
+    if (lo <= idx) s.size -= rl_range(lo, idx, kEntryInMem);
+    s.new_ent = 0;
+    P.imark[r] = idx;
+  }
+  RBE_HD void send_rate_limit() {  // sendRateLimitMessage, raft.go:660-683 (not a leader)
+    if (leader == 0) return;  // skipped, no leader
+    u64 mv = 0;
+    if (rl_limited(P.rl[r], C.rl_max))  // max(inmemSz-notCommitedSz, 0) on uint64: wraps
+      mv = P.rl[r].size - (committed < last ? rl_range(committed + 1, last, kEntryNonCmd) : 0);
+    Msg x = mk(M_RateLimit, leader);
+    x.hint = mv;
+    send(x);
   }
 
   // ------------------------------------------------------------- membership
@@ -1156,6 +1238,7 @@ struct Lane {
         flags |= HF_PENDING_CC;  // setPendingConfigChange
       }
       note_cc(e.type);
+      rl_grow(e.len);
       ring_put(idx, term, e.type, e.len, e.lo, e.hi);
       last = idx;
       t_last = term;
@@ -1281,6 +1364,7 @@ struct Lane {
           // truncate-and-append; savedTo = min(savedTo, first-1)
           if (conflict - 1 >= 1 && conflict - 1 <= last && log_term(conflict - 1) > ents[ci].term)
             set_fault(F_PANIC);
+          if (rl_on()) rl_merge(conflict, ents + ci, m.n_ent - ci);
           // batched: a batch's entries are loaded before any ring store, so no
           // load waits behind the stores of earlier entries (vmcnt is in order)
           u64 tl = 0;
@@ -1301,7 +1385,7 @@ struct Lane {
           last = m.log_index + m.n_ent;
           t_last = tl;
           saved_to = umin64(saved_to, conflict - 1);
-          if (C.ext_commit && conflict <= P.imark[r]) P.imark[r] = conflict;
+          if (imark_on(C) && conflict <= P.imark[r]) P.imark[r] = conflict;
           seg_len = 0;
         }
       }
@@ -1337,6 +1421,11 @@ struct Lane {
         SnapSt& sp = P.snp[r];
         sp.ss_index = si;  // LogDB.ApplySnapshot (after the step's Update)
         sp.ss_term = st;
+        if (rl_on()) {  // inMemory.restore (inmemory.go:236-246)
+          P.imark[r] = si + 1;
+          P.rl[r].new_ent = 1;
+          P.rl[r].size = 0;
+        }
         seg_len = 0;
         snap_restored = true;
         restored = true;
@@ -1435,6 +1524,10 @@ struct Lane {
   RBE_HD void raft_tick();
   RBE_HD void non_leader_tick() {  // raft.go:566-590
     etick++;
+    if (rl_on() && P.rl[r].tick_count % C.election_rtt == 0) {  // timeForRateLimitCheck
+      P.rl[r].tick++;  // rl.HeartbeatTick
+      send_rate_limit();
+    }
     if (voter(k) && etick >= ret) {  // !selfRemoved() && timeForElection()
       etick = 0;
       // Handle(Election): term 0 passes the gate; handled in any role
@@ -1444,6 +1537,7 @@ struct Lane {
   }
   RBE_HD void leader_tick() {  // raft.go:592-621
     etick++;
+    if (rl_on() && P.rl[r].tick_count % C.election_rtt == 0) P.rl[r].tick++;
     bool abort_lt = ltt != 0 && role == R_Leader && etick >= C.election_rtt;
     if (etick >= C.election_rtt) {
       etick = 0;
@@ -1660,7 +1754,15 @@ struct Lane {
           case M_RequestVote: on_request_vote(m); return;
           case M_ConfigChangeEvent: on_config_change(m); return;
           case M_SnapshotReceived: set_fault(F_UNSUPPORTED); return;
-          default: return;  // RateLimit: limiter disabled → dropped
+          case M_RateLimit:  // handleLeaderRateLimit (raft.go:1779-1785)
+            if (rl_on() && m.from >= 1 && m.from <= N) {
+              RlSt& s = P.rl[r];
+              s.fmask |= 1u << (m.from - 1u);
+              s.f_tick[m.from - 1u] = s.tick;
+              s.f_size[m.from - 1u] = m.hint;
+            }
+            return;  // rl disabled: dropped
+          default: return;
         }
       default:
         set_fault(F_UNSUPPORTED);
@@ -1711,6 +1813,7 @@ struct Lane {
   // Called after load() and before any state is written.  Reads only the
   // 24-byte message headers of the inbox.
   RBE_HD bool fast_eligible(u32 inp) const {
+    if (C.rl_max) return false;  // rate limiter: full handler table
     if (flags & HF_SNAP_WORK) return false;  // compaction / SnapshotStatus: full table
     if (role != (LEAD ? R_Leader : R_Follower)) return false;
     if (flags & HF_APPLY_PENDING) return false;
@@ -2325,6 +2428,16 @@ struct Lane {
       if (u.apply_hi >= u.apply_lo) processed = u.apply_hi;
       saved_to = last;
     }
+    // the limiter's appliedLogTo(LastApplied) (logentry.go:335-355) runs only in
+    // a Peer.Commit, i.e. for a step the node takes an Update from: HasUpdate
+    // (peer.go:253-280) or an applied index to confirm (node.go:907-923)
+    if (C.rl_max && !C.ext_commit && applied0 > 0 && rl_on()) {
+      const bool has = term != term0 || vote != vote0 || committed != committed0 || n_msgs ||
+                       n_rtr || n_drop_ent || n_drop_ri || u.save_hi >= u.save_lo ||
+                       u.apply_hi >= u.apply_lo || send_q || snap_restored || ext_applied ||
+                       (flags & HF_APPLIED_NEW);
+      if (has) rl_applied_to(applied0);
+    }
     if (processed < committed) flags |= HF_APPLY_PENDING;
     else flags &= (u8)~HF_APPLY_PENDING;
     // the state machine's applied index moved (entries it held already, re-applied
@@ -2391,6 +2504,7 @@ struct Lane {
 template <int N, bool TRACE, int MODE>
 RBE_HD void Lane<N, TRACE, MODE>::raft_tick() {  // raft.go:551-564
   flags &= (u8)~HF_RAFT_QUIESCE;
+  if (rl_on()) P.rl[r].tick_count++;  // tickCount
   if (role == R_Leader) leader_tick();
   else non_leader_tick();
 }
@@ -2448,7 +2562,13 @@ RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   c.lead_start = 0;
   if (C.membership) c.members = MB_CC_IN_LOG;  // the bootstrap ConfigChanges, applied in round 0
   P.core[r] = c;
-  if (C.ext_commit) P.imark[r] = 1;  // inMemory.init(0), then bootstrap appends 1..N
+  if (imark_on(C)) P.imark[r] = 1;  // inMemory.init(0), then bootstrap appends 1..N
+  if (C.rl_max) {  // newRateLimiter; bootstrap's append is a merge that adds its entries
+    RlSt s = {};
+    s.new_ent = 1;
+    s.size = rl_enabled(C.rl_max) ? N * (kEntryInMem + 8) : 0;
+    P.rl[r] = s;
+  }
   for (u32 s = 0; s < N; s++) {
     RemoteMN x;
     x.match = 0;
@@ -2553,7 +2673,12 @@ RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, 
     for (u32 i = 0; i < n; i++)
       if (ent_type(b[i].type) == E_ConfigChange) c.members = MB_CC_IN_LOG;
   P.core[r] = c;
-  if (C.ext_commit) P.imark[r] = last + 1;  // inMemory.init(lastIndex), inmemory.go:46-57
+  if (imark_on(C)) P.imark[r] = last + 1;  // inMemory.init(lastIndex), inmemory.go:46-57
+  if (C.rl_max) {  // a new raft: a fresh limiter over an empty in-memory log
+    RlSt s = {};
+    s.new_ent = 1;
+    P.rl[r] = s;
+  }
   for (u32 s = 0; s < N; s++) {  // becomeFollower → reset → resetRemotes (raft.go:1023-1031)
     RemoteMN x;
     x.match = s == k ? last : 0;
@@ -2735,7 +2860,9 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, const Clk& ck
     }
   }
   const u64 cid = cid_of(C, g);
-  const u32 cls = h.role == R_Leader ? T_LEAD : (h.role == R_Follower ? T_FOLL : T_FULL);
+  // the rate limiter's hooks live in the full handler table only
+  const u32 cls = C.rl_max ? T_FULL
+                           : (h.role == R_Leader ? T_LEAD : (h.role == R_Follower ? T_FOLL : T_FULL));
   if (nmsg || (h.flags & HF_APPLY_PENDING)) return cls;
   if (C.ext_commit) return cls;
   // a step after an apply may owe raft a ConfigChange (Core::cc_apply)
@@ -2779,6 +2906,7 @@ RBE_HD u32 triage_replica(const Planes& P, const Params& C, u64 r, const Clk& ck
     } else {
       if (h.role == R_Leader) return cls;          // leaderTick broadcasts heartbeats
       if (etick + 1u >= h.rand_et) return cls;     // nonLeaderTick would elect
+      if (C.rl_max) return T_FULL;                 // tickCount and the rate-limit check
       flags &= (u8)~HF_RAFT_QUIESCE;
       etick++;
     }

@@ -319,7 +319,26 @@ struct Params {
   u32 rep_compact;
   u64 n_groups_glob;  // global group count (= n_groups without compaction)
   u8 res[8];          // the n residues g % rep_world of the groups this rank touches, ascending
+  u64 rl_max;         // config.MaxInMemLogSize (server.NewRateLimiter); 0 = limiter off
 };
+
+// The rate limiter of one replica (internal/server/rate.go:33-137, raft.go:204)
+// with the raft fields only it reads: raft.tickCount (raft.go:551-564) and
+// inMemory.newEntries (inmemory.go:36-44).  Follower reports are kept per node
+// slot.  Allocated only when Params::rl_max enables the limiter.
+struct alignas(16) RlSt {
+  u64 size;        // rl.size: in-memory log bytes (Cmd + 80 per entry, raftpb/raft.go:311-322)
+  u64 tick;        // rl.tick (HeartbeatTick)
+  u64 tick_count;  // raft.tickCount
+  u32 new_ent;     // inMemory.newEntries
+  u32 fmask;       // followerSizes holds node slot s
+  u64 f_tick[8];
+  u64 f_size[8];
+};
+static constexpr u64 kRlGcTick = 2;           // rate.go:25 gcTick
+static constexpr u64 kEntryInMem = 80;        // unsafe.Sizeof(pb.Entry) on 64-bit Go
+static constexpr u64 kEntryNonCmd = 16 * 8;   // settings.EntryNonCmdFieldsSize (soft.go:20)
+
 
 // The clock of one round: `round` numbers every rbe_step, `tclk` counts the
 // ticks before it (every replica ticks together, as tickWorkerMain ticks
@@ -357,7 +376,8 @@ struct Planes {
   u64* rem_snap;      // [n_rep * N] remote.snapshotIndex (read only in RS_Snapshot)
   u8* gwake;          // [n_groups] GW_* bits: lets k_triage skip a sleeping group whole
                       // (rbe_step.h, group sleep)
-  u64* imark;         // [n_rep] inMemory.markerIndex (ext_commit only, else null): the first
+  RlSt* rl;           // [n_rep] rate limiters (Params::rl_max != 0, else null)
+  u64* imark;         // [n_rep] inMemory.markerIndex (ext_commit or rl_max, else null): the first
                       // entry the in-memory log holds (inmemory.go:36-44), which bounds
                       // what savedLogTo / appliedLogTo accept
   const u64* heap_head;  // [1] payload heap: the host's next free position after the

@@ -14,7 +14,7 @@ import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libdragonboat_amd.so")
-RBE_ABI_VERSION = 5
+RBE_ABI_VERSION = 6
 
 COUNTER_NAMES = ["steps", "committed", "msg_in", "msg_out", "ent_in", "ent_out",
                  "reads_confirmed", "proposals", "reads", "quiesced_ticks", "active_ticks",
@@ -46,7 +46,8 @@ class RbeConfig(C.Structure):
                 ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
                 ("heap_bytes", C.c_uint64), ("ext_commit", C.c_uint32),
                 ("membership", C.c_uint32), ("cc_period", C.c_uint32), ("cc_mod", C.c_uint32),
-                ("rep_compact", C.c_uint32)]
+                ("rep_compact", C.c_uint32), ("reserved0", C.c_uint32),
+                ("max_inmem_log_size", C.c_uint64)]
 
 
 class RbeReplicaView(C.Structure):
@@ -206,7 +207,7 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_xchg_status", "rbe_stream", "rbe_get_snapshot_state", "rbe_wire_encode",
            "rbe_wire_fetch", "rbe_wire_decode", "rbe_wire_ingest", "rbe_iso_leaders", "rbe_set_iso_leaders", "rbe_local_groups", "rbe_propose_entries", "rbe_commit",
            "rbe_get_update_commits", "rbe_propose_config_change", "rbe_apply_config_change",
-           "rbe_reject_config_change"]
+           "rbe_reject_config_change", "rbe_rate_limited"]
 KERNEL_SLOTS = 4
 
 _lib = None
@@ -268,6 +269,7 @@ def load_library(path: Optional[str] = None):
         "rbe_get_entries": (i32, [vp, u64, u64, u64, P(RbeEntry)]),
         "rbe_get_entry_cmds": (i32, [vp, u64, u64, u64, vp, u64, P(u64)]),
         "rbe_get_views": (i32, [vp, u64, u64, P(RbeReplicaView)]),
+        "rbe_rate_limited": (i32, [vp, u64, u64, vp, vp]),
         "rbe_get_snapshot_state": (i32, [vp, u64, u64, P(u64)]),
         "rbe_wire_encode": (i32, [vp, P(RbeWireConfig), P(u64)]),
         "rbe_wire_fetch": (i32, [vp, vp, u64, P(RbeWireFrame), u32]),
@@ -329,7 +331,8 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                 xfer_period: int = 0, xfer_mod: int = 1, heap_bytes: int = 0,
                 snapshot_entries: int = 0, compaction_overhead: int = 0,
                 ext_commit: bool = False, membership: bool = False, cc_period: int = 0,
-                cc_mod: int = 1, rep_compact: bool = False) -> RbeConfig:
+                cc_mod: int = 1, rep_compact: bool = False,
+                max_inmem_log_size: int = 0) -> RbeConfig:
     return RbeConfig(abi_version=RBE_ABI_VERSION, device=device, n_groups=n_groups,
                      n_replicas=n_replicas, election_rtt=election_rtt,
                      heartbeat_rtt=heartbeat_rtt, check_quorum=int(check_quorum),
@@ -345,7 +348,7 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                      heap_bytes=heap_bytes, snapshot_entries=snapshot_entries,
                      compaction_overhead=compaction_overhead, ext_commit=int(ext_commit),
                      membership=int(membership), cc_period=cc_period, cc_mod=cc_mod,
-                     rep_compact=int(rep_compact))
+                     rep_compact=int(rep_compact), max_inmem_log_size=max_inmem_log_size)
 
 
 class InputError(EngineError):
@@ -383,6 +386,14 @@ def global_groups_call(fn, h, n_groups: int):
     n = C.c_uint64()
     _check(fn(h, C.byref(n), out.ctypes.data), "rbe_local_groups")
     return out[:n.value]
+
+
+def rate_limited_call(fn, h, n_rep: int):
+    """rbe_rate_limited (or the host build's twin) over replicas [0, n_rep)."""
+    lim = np.zeros(max(1, n_rep), np.uint8)
+    size = np.zeros(max(1, n_rep), np.uint64)
+    _check(fn(h, 0, n_rep, lim.ctypes.data, size.ctypes.data), "rbe_rate_limited")
+    return lim[:n_rep].astype(bool), size[:n_rep]
 
 
 def iso_leaders_call(fn, h, n_groups: int):
@@ -739,6 +750,11 @@ class Engine(NodeInputs):
         arr = (RbeReplicaView * count)()
         _check(self.lib.rbe_get_views(self.h, first, count, arr), "rbe_get_views")
         return arr
+
+    def rate_limited(self):
+        """rbe_rate_limited over every replica: (Peer.RateLimited per replica as
+        numpy bool, rl.Get() in-memory log bytes as numpy uint64)."""
+        return rate_limited_call(self.lib.rbe_rate_limited, self.h, self.n_rep)
 
     def global_groups(self):
         """rbe_local_groups: the global group of each local group (numpy

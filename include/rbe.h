@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RBE_ABI_VERSION 5
+#define RBE_ABI_VERSION 6
 
 /* error codes */
 #define RBE_OK 0
@@ -88,7 +88,7 @@ enum rbe_counter {
 /*
  * Engine configuration.  Protocol fields mirror config.Config
  * (config/config.go:60-171): ElectionRTT, HeartbeatRTT, CheckQuorum, Quiesce;
- * MaxInMemLogSize is 0 (rate limiter off).  max_entry_size mirrors
+ * MaxInMemLogSize is max_inmem_log_size (0 = rate limiter off).  max_entry_size mirrors
  * settings.Soft.MaxEntrySize (soft.go:226).
  */
 typedef struct rbe_config {
@@ -166,6 +166,12 @@ typedef struct rbe_config {
    * every call are then the engine's local ones; rbe_local_groups maps them
    * to the global group (n_groups stays the global count). */
   uint32_t rep_compact;
+  uint32_t reserved0;
+  /* config.MaxInMemLogSize (config.go:118-131): the rate limiter
+   * (internal/server/rate.go, raft.go:660-683, 1779-1785) over each replica's
+   * in-memory log bytes; 0 (or UINT64_MAX) = off.  Rate-limited engines step
+   * every ticking replica on the full handler table; not with ext_commit. */
+  uint64_t max_inmem_log_size;
 } rbe_config;
 
 /* Snapshot of one replica (tests, debugging, rbe_get_views). */
@@ -513,6 +519,14 @@ int rbe_wire_ingest(rbe_engine* e, const void* data, uint64_t bytes, rbe_wire_in
 int rbe_get_entry_cmds(rbe_engine* e, uint64_t replica, uint64_t lo, uint64_t hi, uint8_t* buf,
                        uint64_t cap, uint64_t* offsets);
 int rbe_get_views(rbe_engine* e, uint64_t first, uint64_t count, rbe_replica_view* out);
+/* Rate limiter of replicas [first, first + count) (cfg.max_inmem_log_size):
+ * Peer.RateLimited (peer.go:245-249, server/rate.go:109-137), one byte per
+ * replica (1 = limited: its in-memory log or a follower report fresh within
+ * two rate-limit ticks exceeds the limit), and rl.Get(), the in-memory log
+ * bytes (Cmd + 80 per entry, raftpb/raft.go:311-322).  Either output may be
+ * null.  RBE_E_STATE when the engine has no limiter. */
+int rbe_rate_limited(rbe_engine* e, uint64_t first, uint64_t count, uint8_t* limited,
+                     uint64_t* in_mem_log_size);
 
 /* The last round's Update.Messages and Update.ReadyToReads of replicas
  * [first, first + count) in one call: compacted on the device (a count pass,

@@ -217,6 +217,7 @@ static Config node_config(const HarnessConfig& cfg, u64 cid, u32 k) {
   c.quiesce = cfg.quiesce;
   c.rngSeed = cfg.seed;
   c.maxEntrySize = cfg.max_entry_size;
+  c.maxInMemLogSize = cfg.max_inmem_log_size;
   return c;
 }
 
@@ -768,6 +769,16 @@ u32 harness_inbox(const Harness* h, u64 replica, u32 sender, u64* out, u32 cap) 
 void harness_commit(Harness* h, u64 replica, const UpdateCommit& uc) {
   const u32 N = h->cfg.n_replicas;
   h->groups[replica / N]->nodes[replica % N]->peer->raft->log.commitUpdate(uc);
+}
+
+void harness_rate_limited(Harness* h, uint8_t* limited, u64* size) {
+  const u32 n = h->cfg.n_replicas;
+  for (u64 g = 0; g < h->groups.size(); g++)
+    for (u32 k = 0; k < n; k++) {
+      Peer* p = h->groups[g]->nodes[k]->peer;
+      if (limited) limited[g * n + k] = p->rateLimited() ? 1 : 0;
+      if (size) size[g * n + k] = p->raft->rl.get();
+    }
 }
 
 void harness_views(const Harness* h, ReplicaView* out) {

@@ -85,6 +85,8 @@ struct HarnessConfig {
   // voter (while more than two vote) or adding it back (cc_input)
   u32 cc_period = 0;
   u32 cc_mod = 1;
+  // config.MaxInMemLogSize: every raft's rate limiter (0 = off)
+  u64 max_inmem_log_size = 0;
 };
 
 // host inputs for the next round (the engine's rbe_push_* / rbe_notify_applied)
@@ -171,6 +173,8 @@ void harness_step(Harness* h, bool tick);
 int harness_push(Harness* h, int kind, u64 replica, u64 a, u64 b, const Entry* ents, u32 n);
 u32 harness_round(const Harness* h);
 void harness_views(const Harness* h, ReplicaView* out);  // n_groups*n_replicas views
+// Peer.RateLimited and rl.Get() of every replica (n_groups*n_replicas each)
+void harness_rate_limited(Harness* h, uint8_t* limited, u64* size);
 void harness_counters(const Harness* h, u64* out);       // HC_NUM counters
 u64 harness_log_term(const Harness* h, u64 g, u32 k, u64 index);  // term of entry (0 if absent)
 // restart of one replica from its LogDB (Peer.Launch over an existing log; the

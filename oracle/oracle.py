@@ -81,7 +81,8 @@ class OrcHarnessConfig(C.Structure):
                 ("xfer_mod", C.c_uint32), ("ext_apply", C.c_uint32),
                 ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
                 ("ext_commit", C.c_uint32), ("membership", C.c_uint32),
-                ("cc_period", C.c_uint32), ("cc_mod", C.c_uint32), ("pad4", C.c_uint32)]
+                ("cc_period", C.c_uint32), ("cc_mod", C.c_uint32), ("pad4", C.c_uint32),
+                ("max_inmem_log_size", C.c_uint64)]
 
 
 class ReplicaView(C.Structure):
@@ -186,6 +187,7 @@ def lib():
             "orc_harness_push": (i32, [vp, i32, u64, u64, u64, P(OrcEntry), i32]),
             "orc_harness_round": (u32, [vp]),
             "orc_harness_views": (None, [vp, vp]),
+            "orc_harness_rate_limited": (None, [vp, vp, vp]),
             "orc_harness_counters": (None, [vp, P(u64)]),
             "orc_harness_log_term": (u64, [vp, u64, u32, u64]),
             "orc_harness_persisted": (None, [vp, u64, P(u64)]),
@@ -910,7 +912,8 @@ class Harness:
                  wl_read_permille=0, iso_period=0, iso_len=0, iso_mod=10, trace=True,
                  threads=1, cid_stride=1, xfer_period=0, xfer_mod=1, ext_apply=False,
                  ext_inputs=False, snapshot_entries=0, compaction_overhead=0,
-                 ext_commit=False, membership=False, cc_period=0, cc_mod=1):
+                 ext_commit=False, membership=False, cc_period=0, cc_mod=1,
+                 max_inmem_log_size=0):
         c = OrcHarnessConfig(
             n_groups=n_groups, n_replicas=n_replicas, check_quorum=int(check_quorum),
             cid_base=cid_base, election_rtt=election_rtt, heartbeat_rtt=heartbeat_rtt,
@@ -922,7 +925,7 @@ class Harness:
             xfer_period=xfer_period, xfer_mod=xfer_mod, ext_apply=int(ext_apply),
             snapshot_entries=snapshot_entries, compaction_overhead=compaction_overhead,
             ext_commit=int(ext_commit), membership=int(membership), cc_period=cc_period,
-            cc_mod=cc_mod)
+            cc_mod=cc_mod, max_inmem_log_size=max_inmem_log_size)
         self.n_groups, self.n_replicas = n_groups, n_replicas
         self.h = lib().orc_harness_create(C.byref(c))
         if not self.h:
@@ -957,6 +960,16 @@ class Harness:
         arr = (ReplicaView * n)()
         lib().orc_harness_views(self.h, C.cast(arr, C.c_void_p))
         return arr
+
+    def rate_limited(self):
+        """(Peer.RateLimited per replica as numpy bool, rl.Get() as uint64)."""
+        import numpy as np
+        n = self.n_groups * self.n_replicas
+        lim = np.zeros(max(1, n), np.uint8)
+        size = np.zeros(max(1, n), np.uint64)
+        lib().orc_harness_rate_limited(self.h, C.c_void_p(lim.ctypes.data),
+                                       C.c_void_p(size.ctypes.data))
+        return lim[:n].astype(bool), size[:n]
 
     def counters(self) -> Dict[str, int]:
         o = (C.c_uint64 * HC_NUM)()

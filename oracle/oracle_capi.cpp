@@ -49,6 +49,7 @@ typedef struct {
   uint32_t xfer_period, xfer_mod, ext_apply, snapshot_entries;
   uint32_t compaction_overhead, ext_commit;
   uint32_t membership, cc_period, cc_mod, pad4;
+  uint64_t max_inmem_log_size;
 } orc_harness_config;
 
 static thread_local std::string g_err;
@@ -873,6 +874,7 @@ void* orc_harness_create(const orc_harness_config* c) {
   h.membership = c->membership;
   h.cc_period = c->cc_period;
   h.cc_mod = c->cc_mod ? c->cc_mod : 1;
+  h.max_inmem_log_size = c->max_inmem_log_size;
   return harness_create(h);
   GUARD_END(nullptr)
 }
@@ -899,6 +901,9 @@ int orc_harness_run(void* h, uint32_t rounds) {
 }
 uint32_t orc_harness_round(void* h) { return harness_round((Harness*)h); }
 void orc_harness_views(void* h, void* out) { harness_views((Harness*)h, (ReplicaView*)out); }
+void orc_harness_rate_limited(void* h, uint8_t* limited, uint64_t* size) {
+  harness_rate_limited((Harness*)h, limited, size);
+}
 void orc_harness_counters(void* h, uint64_t* out) { harness_counters((Harness*)h, out); }
 uint64_t orc_harness_log_term(void* h, uint64_t g, uint32_t k, uint64_t idx) {
   return harness_log_term((Harness*)h, g, k, idx);

@@ -9,7 +9,7 @@ from dragonboat_amd.engine import (CTR_NUM, COUNTER_NAMES, NodeInputs, RbeEntry,
                                    RbeReplicaView, RbeUpdateCommit, RbeWireFrame, entry_cmds,
                                    entry_fields, make_config, outbox_call, push_messages_call,
                                    RbeWireIngestStats, global_groups_call, iso_leaders_call,
-                                   wire_ingest_call)
+                                   rate_limited_call, wire_ingest_call)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _lib = None
@@ -33,6 +33,9 @@ def lib():
         L.soa_wire_encode.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
                                       C.POINTER(C.c_char_p), C.c_void_p, C.c_uint64,
                                       C.POINTER(RbeWireFrame), C.POINTER(C.c_uint32), C.c_int32]
+        L.soa_rate_limited.restype = C.c_int
+        L.soa_rate_limited.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p,
+                                       C.c_void_p]
         L.soa_local_groups.restype = C.c_int
         L.soa_local_groups.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p]
         L.soa_iso_leaders.restype = C.c_int
@@ -216,6 +219,9 @@ class SoaCpu(NodeInputs):
 
     def global_groups(self):
         return global_groups_call(lib().soa_local_groups, self.h, self.n_groups)
+
+    def rate_limited(self):
+        return rate_limited_call(lib().soa_rate_limited, self.h, self.n_rep)
 
     def iso_leaders(self):
         return iso_leaders_call(lib().soa_iso_leaders, self.h, self.cfg.n_groups)

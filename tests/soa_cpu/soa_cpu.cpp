@@ -107,7 +107,7 @@ static void run_round(SoaEngine* e, bool tick = true) {
           cls = T_DONE;
           done = true;
         } else if (inb & 2u) {  // messages: the role decides the list (as triage_replica would)
-          cls = class_of_role(idle_role(ib));
+          cls = e->C.rl_max ? T_FULL : class_of_role(idle_role(ib));
         } else {
           cls = e->C.trace ? triage_replica<N, true>(e->P, e->C, r, ck, c)
                            : triage_replica<N, false>(e->P, e->C, r, ck, c);
@@ -231,7 +231,8 @@ void* soa_create(const rbe_config* cfg) {
   rep_compact_setup(C, cfg->rep_compact != 0);
   C.snapshot_entries = cfg->snapshot_entries;
   C.compaction_overhead = cfg->compaction_overhead;
-  if (C.n != 1 && C.n != 3 && C.n != 5) {
+  C.rl_max = cfg->max_inmem_log_size;
+  if ((C.n != 1 && C.n != 3 && C.n != 5) || (C.rl_max && C.ext_commit)) {
     delete e;
     return nullptr;
   }
@@ -264,7 +265,8 @@ void* soa_create(const rbe_config* cfg) {
   memset(P.gwake, GW_AWAKE, G);  // every group starts awake
   P.snp = C.snapshot_entries ? alloc<SnapSt>(e, R) : nullptr;
   P.rem_snap = C.snapshot_entries ? alloc<u64>(e, R * N) : nullptr;
-  P.imark = C.ext_commit ? alloc<u64>(e, R) : nullptr;
+  P.imark = (C.ext_commit || C.rl_max) ? alloc<u64>(e, R) : nullptr;
+  P.rl = C.rl_max ? alloc<RlSt>(e, R) : nullptr;
   C.heap_bytes = (cfg->heap_bytes + 255) & ~255ull;
   e->heap.assign(C.heap_bytes, 0);
   e->hin.init(R, C.n, C.in_cap, C.heap_bytes);
@@ -718,6 +720,18 @@ int soa_iso_leaders(void* h, uint8_t* out, uint32_t* epoch) {
     if (gg >= C.n_groups_glob) continue;
     out[gg] = (u8)(C.n == 5 ? iso_leader_bits<5>(e->P, C, g)
                             : C.n == 3 ? iso_leader_bits<3>(e->P, C, g) : iso_leader_bits<1>(e->P, C, g));
+  }
+  return RBE_OK;
+}
+int soa_rate_limited(void* h, uint64_t first, uint64_t count, uint8_t* limited,
+                     uint64_t* size) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (count == 0 || first >= e->C.n_rep || count > e->C.n_rep - first) return RBE_E_INVALID;
+  if (!e->P.rl) return RBE_E_STATE;
+  for (u64 i = 0; i < count; i++) {
+    RlSt s = e->P.rl[first + i];  // a copy: the query's gc is not kept (unobservable)
+    if (limited) limited[i] = rl_limited(s, e->C.rl_max) ? 1 : 0;
+    if (size) size[i] = s.size;
   }
   return RBE_OK;
 }
