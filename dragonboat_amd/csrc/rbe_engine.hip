@@ -519,7 +519,6 @@ static int make_params(const rbe_config* cfg, Params* out) {
   C.ext_commit = cfg->ext_commit;
   if (C.ext_commit && !C.ext_apply) return RBE_E_INVALID;
   C.rl_max = cfg->max_inmem_log_size;
-  if (C.rl_max && C.ext_commit) return RBE_E_INVALID;  // appliedLogTo of rbe_commit: not yet
   C.membership = cfg->membership;
   C.cc_period = cfg->cc_period;
   C.cc_mod = cfg->cc_mod ? cfg->cc_mod : 1;

@@ -308,8 +308,24 @@ RBE_HD u32 commit_update(const Planes& P, const Params& C, u64 r, u64 stable_log
     else c.processed = processed;
   }
   if (!fault && last_applied > 0) {
-    if (last_applied > c.committed || last_applied > c.processed) fault |= F_PANIC;
-    else if (held && last_applied >= mark && last_applied <= c.last_index) mark = last_applied;
+    if (last_applied > c.committed || last_applied > c.processed) {
+      fault |= F_PANIC;
+    } else if (held && last_applied >= mark && last_applied <= c.last_index) {
+      if (rl_enabled(C.rl_max)) {  // the limiter's part of appliedLogTo (Lane::rl_applied_to)
+        RlSt& s = P.rl[r];
+        u64 sum = 0;
+        for (u64 i = s.new_ent ? mark : mark + 1; i <= last_applied; i++) {
+          if (c.last_index - i >= C.ring) {
+            fault |= F_WINDOW;
+            break;
+          }
+          sum += kEntryInMem + P.pay_ring[(i & (u64)(C.ring - 1)) * C.n_rep + r].len;
+        }
+        s.size -= sum;
+        s.new_ent = 0;
+      }
+      mark = last_applied;
+    }
   }
   P.core[r] = c;
   P.imark[r] = mark;

@@ -170,7 +170,7 @@ typedef struct rbe_config {
   /* config.MaxInMemLogSize (config.go:118-131): the rate limiter
    * (internal/server/rate.go, raft.go:660-683, 1779-1785) over each replica's
    * in-memory log bytes; 0 (or UINT64_MAX) = off.  Rate-limited engines step
-   * every ticking replica on the full handler table; not with ext_commit. */
+   * every ticking replica on the full handler table. */
   uint64_t max_inmem_log_size;
 } rbe_config;
 

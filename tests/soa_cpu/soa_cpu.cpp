@@ -232,7 +232,7 @@ void* soa_create(const rbe_config* cfg) {
   C.snapshot_entries = cfg->snapshot_entries;
   C.compaction_overhead = cfg->compaction_overhead;
   C.rl_max = cfg->max_inmem_log_size;
-  if ((C.n != 1 && C.n != 3 && C.n != 5) || (C.rl_max && C.ext_commit)) {
+  if (C.n != 1 && C.n != 3 && C.n != 5) {
     delete e;
     return nullptr;
   }

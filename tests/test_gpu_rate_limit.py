@@ -34,3 +34,21 @@ def test_gpu_rate_limiter_untraced(gpu_available):
     ref = O.Harness(max_inmem_log_size=limit, **kw)
     assert _lockstep_rl(eng, ref, rounds, skip=("digest",)) > 0
     eng.close()
+
+
+def test_gpu_rate_limiter_ext_commit(gpu_available):
+    """appliedLogTo inside the host's rbe_commit (ext_commit), persisted late or partly."""
+    from commit_util import run_commit_driven
+    from dragonboat_amd.engine import Engine
+    from parity_util import C3
+    kw = dict(C3, n_groups=12, ext_inputs=True, ext_apply=True, ext_commit=True,
+              max_inmem_log_size=400)
+    eng = Engine(device=0, trace=True, maxm=40, ecap=64, rq_cap=32, ring=256, **kw)
+    ref = O.Harness(**kw)
+    d, st = run_commit_driven(eng, ref, 160, seed=5)
+    assert d is None, f"first divergence {d}"
+    el, es = eng.rate_limited()
+    rl, rs = ref.rate_limited()
+    assert (es == rs).all() and (el == rl).all()
+    assert eng.fault_summary()[0] == 0
+    eng.close()

@@ -76,6 +76,26 @@ def test_rate_limit_messages_reach_the_leader():
     assert not el.any() and es.max() > 0
 
 
+@pytest.mark.parametrize("name", ["C2", "C3"])
+def test_rate_limiter_ext_commit(name):
+    """Host-driven persistence (ext_commit): appliedLogTo runs inside the host's
+    rbe_commit, which persists late or partly (tests/commit_util.py)."""
+    from commit_util import run_commit_driven
+    from parity_util import C3
+    kw = dict({"C2": C2, "C3": C3}[name], n_groups=12, ext_inputs=True, ext_apply=True,
+              ext_commit=True, max_inmem_log_size=400)
+    eng = SoaCpu(trace=True, maxm=40, ecap=64, rq_cap=32, ring=256, **kw)
+    ref = O.Harness(**kw)
+    # views and trace digests (RateLimit Hints) every round, the limiters at the end
+    d, st = run_commit_driven(eng, ref, 160, seed=5)
+    assert d is None, f"{name}: first divergence {d}"
+    el, es = eng.rate_limited()
+    rl, rs = ref.rate_limited()
+    assert (es == rs).all() and (el == rl).all()
+    assert eng.faults()[0] == 0
+    assert st["committed"] > 100 and es.max() > 0, st
+
+
 def test_limiter_off_by_default():
     eng = SoaCpu(trace=True, **dict(C2, n_groups=4))
     with pytest.raises(Exception):
