@@ -33,6 +33,11 @@ RBE_HD u64 group_global(const Params& C, u64 g) {
 RBE_HD u64 cid_of(const Params& C, u64 g) { return C.cid_base + group_global(C, g) * C.cid_stride; }
 // the same with the group size a compile-time constant (the step kernels:
 // no 64-bit division by a runtime value in their register budget)
+template <int N>
+RBE_HD u64 cid_of_n(const Params& C, u64 g) {
+  const u64 gg = C.rep_compact ? (g / N) * C.rep_world + C.res[g % N] : g;
+  return C.cid_base + gg * C.cid_stride;
+}
 // rate limiter (server/rate.go): Enabled and RateLimited with its gc (rate.go:
 // 109-149): the largest fresh follower report or the replica's own in-memory
 // log size above the limit
@@ -55,11 +60,6 @@ RBE_HD bool rl_limited(RlSt& s, u64 max) {
 }
 // the in-memory marker (Planes::imark) is kept for rbe_commit and for the limiter
 RBE_HD bool imark_on(const Params& C) { return C.ext_commit || C.rl_max; }
-template <int N>
-RBE_HD u64 cid_of_n(const Params& C, u64 g) {
-  const u64 gg = C.rep_compact ? (g / N) * C.rep_world + C.res[g % N] : g;
-  return C.cid_base + gg * C.cid_stride;
-}
 // Is replica k of local group g stepped by this engine?  (replica mode:
 // replica k of global group G is stepped on rank (G + k) % rep_world; the
 // padding groups of a compacted engine by none)
@@ -321,10 +321,12 @@ RBE_HD u32 commit_update(const Planes& P, const Params& C, u64 r, u64 stable_log
           }
           sum += kEntryInMem + P.pay_ring[(i & (u64)(C.ring - 1)) * C.n_rep + r].len;
         }
-        s.size -= sum;
-        s.new_ent = 0;
+        if (!fault) {  // a fault exit changes nothing further (size, marker)
+          s.size -= sum;
+          s.new_ent = 0;
+        }
       }
-      mark = last_applied;
+      if (!fault) mark = last_applied;
     }
   }
   P.core[r] = c;
@@ -1002,8 +1004,13 @@ struct Lane {
   RBE_HD void send_rate_limit() {  // sendRateLimitMessage, raft.go:660-683 (not a leader)
     if (leader == 0) return;  // skipped, no leader
     u64 mv = 0;
-    if (rl_limited(P.rl[r], C.rl_max))  // max(inmemSz-notCommitedSz, 0) on uint64: wraps
-      mv = P.rl[r].size - (committed < last ? rl_range(committed + 1, last, kEntryNonCmd) : 0);
+    if (rl_limited(P.rl[r], C.rl_max)) {  // max(inmemSz-notCommitedSz, 0) on uint64: wraps
+      // getUncommittedEntries (logentry.go:180-183) reads the in-memory log
+      // only: [max(committed + 1, markerIndex), last] (getEntriesFromInMem,
+      // logentry.go:205-211)
+      const u64 lo = umax64(committed + 1, P.imark[r]);
+      mv = P.rl[r].size - (lo <= last ? rl_range(lo, last, kEntryNonCmd) : 0);
+    }
     Msg x = mk(M_RateLimit, leader);
     x.hint = mv;
     send(x);

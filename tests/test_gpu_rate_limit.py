@@ -36,6 +36,20 @@ def test_gpu_rate_limiter_untraced(gpu_available):
     eng.close()
 
 
+def test_gpu_rate_limiter_after_relaunch(gpu_available):
+    """Followers relaunched with commit < last: RateLimit Hints count only the
+    in-memory uncommitted entries (logentry.go:180-183, 205-211)."""
+    from dragonboat_amd.engine import Engine
+    from parity_util import C2
+    from test_rate_limit import relaunch_lagging_groups
+    kw = dict(C2, n_groups=64)
+    eng = Engine(device=0, trace=True, max_inmem_log_size=50, **kw)
+    ref = O.Harness(max_inmem_log_size=50, **kw)
+    relaunch_lagging_groups(eng, ref)
+    assert eng.fault_summary()[0] == 0
+    eng.close()
+
+
 def test_gpu_rate_limiter_ext_commit(gpu_available):
     """appliedLogTo inside the host's rbe_commit (ext_commit), persisted late or partly."""
     from commit_util import run_commit_driven

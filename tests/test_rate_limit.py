@@ -96,6 +96,38 @@ def test_rate_limiter_ext_commit(name):
     assert st["committed"] > 100 and es.max() > 0, st
 
 
+def relaunch_lagging_groups(eng, ref, rounds=90):
+    """Relaunch whole groups whose replicas' commit lags their last index
+    (rbe_launch: the in-memory log starts empty at last + 1,
+    inMemory.init(lastIndex)), then keep the limiters in lockstep.  After the
+    re-election a follower holds the new no-op in memory (over the limit) while
+    its commit is still below the relaunched last index: its RateLimit Hint
+    subtracts only the uncommitted entries the in-memory log holds,
+    [max(committed + 1, markerIndex), last] (getUncommittedEntries,
+    logentry.go:180-183, 205-211), not the LogDB's."""
+    from launch_util import restart
+    _lockstep_rl(eng, ref, 40)
+    n = ref.n_replicas
+    picks = []
+    for g in range(len(ref.views()) // n):
+        reps = list(range(g * n, (g + 1) * n))
+        if all(ref.persisted(r)[2] < ref.persisted(r)[3] for r in reps):
+            picks += reps
+    assert len(picks) >= 3 * n, "too few groups with commit < last: the case tests nothing"
+    restart(eng, ref, picks, 64)
+    _lockstep_rl(eng, ref, rounds)
+    return picks
+
+
+def test_rate_limiter_after_relaunch():
+    # a limit below one entry's in-memory size: every follower holding an entry is limited
+    kw = dict(C2, n_groups=64)
+    eng = SoaCpu(trace=True, max_inmem_log_size=50, **kw)
+    ref = O.Harness(max_inmem_log_size=50, **kw)
+    relaunch_lagging_groups(eng, ref)
+    assert eng.faults()[0] == 0
+
+
 def test_limiter_off_by_default():
     eng = SoaCpu(trace=True, **dict(C2, n_groups=4))
     with pytest.raises(Exception):
