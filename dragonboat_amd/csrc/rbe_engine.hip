@@ -204,7 +204,7 @@ __global__ __launch_bounds__(kBlock) void k_out_write(Planes P, Params C, u64 fi
       o.hint = m.hint;
       o.hint_high = m.hint_high;
       o.n_entries = m.n_ent;
-      o.reserved = 0;
+      o.reserved = msg_reserved(m);
       om[at] = o;
     }
   }
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(kBlock) void k_upd_write(Planes P, u64 first, u64 c
 // rbe_launch: one lane per relaunched replica (rbe_step.h relaunch_replica)
 struct LaunchRec {
   u64 replica, term, vote, commit, last, off;  // off: first row in the terms/bodies arrays
-  u32 n, pad;
+  u32 n, removed;                              // removed: rbe_launch_state::removed
   u64 marker, marker_term, ss_index, ss_term;  // compacted LogDB (rbe_launch_state)
 };
 template <int N>
@@ -256,7 +256,8 @@ __global__ __launch_bounds__(kBlock) void k_relaunch(Planes P, Params C, const L
   if (i >= n) return;
   const LaunchRec x = rec[i];
   relaunch_replica<N>(P, C, x.replica, x.term, x.vote, x.commit, x.last, x.n, terms + x.off,
-                      bodies + x.off, ppar, tclk, x.marker, x.marker_term, x.ss_index, x.ss_term);
+                      bodies + x.off, ppar, tclk, x.marker, x.marker_term, x.ss_index, x.ss_term,
+                      (u8)x.removed);
   P.gwake[x.replica / N] = GW_AWAKE;
 }
 
@@ -1188,7 +1189,7 @@ int rbe_launch(rbe_engine* e, uint64_t n, const uint64_t* replica, const rbe_lau
   for (u64 i = 0; i < n; i++) {
     rec[i] = LaunchRec{replica[i], st[i].term,           st[i].vote,
                        st[i].commit,     st[i].last_index,     off,
-                       st[i].n_entries,  0,                    st[i].marker,
+                       st[i].n_entries,  st[i].removed,        st[i].marker,
                        st[i].marker_term, st[i].snapshot_index, st[i].snapshot_term};
     off += st[i].n_entries;
   }
@@ -1244,6 +1245,13 @@ int rbe_reject_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica)
   if (!e) return RBE_E_INVALID;
   if (!e->C.membership || !e->C.ext_inputs) return RBE_E_STATE;
   return e->hin.apply_config_change(n, replica, nullptr, nullptr, true);
+}
+
+int rbe_restore_remotes(rbe_engine* e, uint64_t n, const uint64_t* replica,
+                        const uint32_t* n_voters, const uint64_t* voter_ids) {
+  if (!e) return RBE_E_INVALID;
+  if (!e->C.membership || !e->C.ext_inputs) return RBE_E_STATE;
+  return e->hin.restore_remotes(n, replica, n_voters, voter_ids);
 }
 
 int rbe_notify_applied(rbe_engine* e, uint64_t n, const uint64_t* replica,
@@ -1592,14 +1600,14 @@ int rbe_commit(rbe_engine* e, uint64_t n, const uint64_t* replica, const rbe_upd
   return e->hin.commit(n, replica, uc);
 }
 
-int rbe_get_snapshot_state(rbe_engine* e, uint64_t first, uint64_t count, uint64_t* out6) {
-  if (!e || !out6 || first + count > e->C.n_rep || count == 0) return RBE_E_INVALID;
+int rbe_get_snapshot_state(rbe_engine* e, uint64_t first, uint64_t count, uint64_t* out8) {
+  if (!e || !out8 || first + count > e->C.n_rep || count == 0) return RBE_E_INVALID;
   if (!e->C.snapshot_entries) return RBE_E_STATE;
   HIP_OK(hipSetDevice(e->device));
   std::vector<SnapSt> v(count);
   if (d2h(e, v.data(), e->P.snp + first, count)) return RBE_E_HIP;
   HIP_OK(hipStreamSynchronize(e->stream));
-  for (u64 i = 0; i < count; i++) snap_state_row(v[i], out6 + 6 * i);
+  for (u64 i = 0; i < count; i++) snap_state_row(v[i], out8 + 8 * i);
   return RBE_OK;
 }
 
@@ -1637,6 +1645,7 @@ int rbe_get_messages(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t
         o.hint = m.hint;
         o.hint_high = m.hint_high;
         o.n_entries = m.n_ent;
+        o.reserved = msg_reserved(m);
       }
       n++;
     }

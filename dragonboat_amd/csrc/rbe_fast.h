@@ -408,6 +408,7 @@ RBE_HD void fast_node_snapshot(const Planes& P, const Params& C, StepCounters& c
   if (t == 0) return;
   sp->ss_index = la;
   sp->ss_term = t;
+  sp->ss_rem = sp->sm_rem;  // a fast step applies no ConfigChange: the state machine's membership
   const u64 ct = la > C.compaction_overhead ? la - C.compaction_overhead : 0;
   sp->compact_to = ct;
   if (ct) flags |= HF_SNAP_WORK;

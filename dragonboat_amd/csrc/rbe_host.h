@@ -311,7 +311,8 @@ RBE_HD u64 heap_low_group(const Planes& P, const Params& C, u64 g, u32 round) {
 }
 
 // rbe_get_snapshot_state row: marker, marker term, snapshot index, snapshot
-// term, reqSnapshotIndex, compactLogTo
+// term, reqSnapshotIndex, compactLogTo, the snapshot's and the state
+// machine's membership (removed masks)
 inline void snap_state_row(const SnapSt& s, u64* o) {
   o[0] = s.marker;
   o[1] = s.marker_term;
@@ -319,6 +320,8 @@ inline void snap_state_row(const SnapSt& s, u64* o) {
   o[3] = s.ss_term;
   o[4] = s.ss_req;
   o[5] = s.compact_to;
+  o[6] = s.ss_rem;
+  o[7] = s.sm_rem;
 }
 
 // Check a batch of entries whole: their types, and that the heap (if any
@@ -368,6 +371,8 @@ inline int launch_rows(const Params& C, HostHeap& heap, u64 n, const u64* replic
     if (replica[i] >= C.n_rep || x.n_entries > C.ring || x.n_entries > x.last_index ||
         x.commit > x.last_index || x.vote > C.n || (x.last_index > x.marker && !x.n_entries))
       return RBE_E_INVALID;
+    // the LogDB's membership: voters among the group's slots, only with cfg.membership
+    if (x.removed >> C.n || (x.removed && !C.membership)) return RBE_E_INVALID;
     total += x.n_entries;
   }
   if (total && !ents) return RBE_E_INVALID;
@@ -611,6 +616,30 @@ struct HostInputs {
       x.flags |= EXT_CC_APPLY;
       x.pad[1] = reject ? (u64)(CCA_VALID | CCA_REJECT)
                         : (u64)(CCA_VALID | (type[i] << 3) | (u32)node[i]);
+    }
+    return RBE_OK;
+  }
+  // rbe_restore_remotes: replica[i]'s snapshot lists n_voters[i] voters, their
+  // node ids next in `ids`; staged as the removed mask of the group's slots
+  int restore_remotes(u64 cnt, const u64* replica, const u32* n_voters, const u64* ids) {
+    if (cnt && !n_voters) return RBE_E_INVALID;
+    std::vector<u64> rem(cnt);
+    u64 j = 0;
+    for (u64 i = 0; i < cnt; i++) {
+      u32 listed = 0;
+      if (n_voters[i] && !ids) return RBE_E_INVALID;
+      for (u32 q = 0; q < n_voters[i]; q++, j++) {
+        if (ids[j] < 1 || ids[j] > n || ((listed >> (ids[j] - 1)) & 1u)) return RBE_E_INVALID;
+        listed |= 1u << (ids[j] - 1);
+      }
+      rem[i] = ((1u << n) - 1u) & ~listed;
+    }
+    int rc = check_replicas(cnt, replica, EXT_RESTORE);
+    if (rc) return rc;
+    for (u64 i = 0; i < cnt; i++) {
+      ExtIn& x = rec(replica[i]);
+      x.flags |= EXT_RESTORE;
+      x.pad[2] = rem[i];
     }
     return RBE_OK;
   }

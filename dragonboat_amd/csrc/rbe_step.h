@@ -355,6 +355,9 @@ RBE_HD bool is_response_message(u32 t) {
          t == M_ReadIndexResp || t == M_Unreachable || t == M_SnapshotStatus ||
          t == M_LeaderTransfer;
 }
+// rbe_message.reserved of an engine message: an InstallSnapshot's snapshot
+// membership (Snapshot.Membership as the removed mask, Msg::pad0), else 0
+RBE_HD u32 msg_reserved(const Msg& m) { return m.type == M_InstallSnapshot ? (u32)m.pad0 : 0u; }
 RBE_HD bool is_leader_message(u32 t) {  // raft.go:1382-1385
   return t == M_Replicate || t == M_InstallSnapshot || t == M_Heartbeat || t == M_TimeoutNow ||
          t == M_ReadIndexResp;
@@ -426,6 +429,7 @@ struct Lane {
   u64 marker, marker_term;
   u8 snp_pend, snp_rej;
   bool snap_restored;
+  u8 sm_rem;  // SnapSt::sm_rem: the state machine's membership (snapshot_entries)
   u64 applied0;  // raft.applied of this step (NotifyRaftLastApplied at its start)
 
   // per-step outputs
@@ -1071,6 +1075,22 @@ struct Lane {
       if (try_commit()) broadcast_replicate();
     }
   }
+  // restoreRemotes (raft.go:472-517) for Handle(SnapshotReceived), which
+  // Peer.RestoreRemotes sends once the state machine recovered from a snapshot
+  // (peer.go:159-165): the voters become the snapshot's (`rem`, the removed
+  // mask), every remote restarts at match 0 / next lastIndex + 1 (self: match
+  // lastIndex), Retry and inactive; a leader the snapshot no longer lists
+  // steps down.  No observers or witnesses here (F_HANDOFF groups are the host's).
+  RBE_HD void restore_remotes(u8 rem) {
+    members = (u8)((members & MB_CC_IN_LOG) | (rem & MB_REMOVED));
+    for (u32 s = 0; s < N; s++) {
+      set_rmatch(s, s == k ? last : 0);
+      set_rnext(s, last + 1);
+      set_rst(s, 0);
+    }
+    ctr.v[C_REMOTE_TOUCH] += N;
+    if (!voter(k) && role == R_Leader) become_follower(term, 0);  // selfRemoved() && isLeader()
+  }
   // a log entry that is a ConfigChange: MB_CC_IN_LOG until it is applied
   RBE_HD void note_cc(u32 type) {
     if (ent_type(type) == E_ConfigChange) members |= MB_CC_IN_LOG;
@@ -1113,6 +1133,7 @@ struct Lane {
       Msg m = mk(M_InstallSnapshot, (u8)(slot + 1));
       m.log_index = si;
       m.log_term = sp.ss_term;
+      m.pad0 = sp.ss_rem;  // Snapshot.Membership: the voters it lists (removed mask)
       become_snapshot(slot, si);
       const u32 bit = 1u << slot;
       snp_pend |= (u8)bit;
@@ -1444,6 +1465,7 @@ struct Lane {
         SnapSt& sp = P.snp[r];
         sp.ss_index = si;  // LogDB.ApplySnapshot (after the step's Update)
         sp.ss_term = st;
+        sp.ss_rem = (u8)(m.pad0 & MB_REMOVED);  // and its membership
         if (rl_on()) {  // inMemory.restore (inmemory.go:236-246)
           P.imark[r] = si + 1;
           P.rl[r].new_ent = 1;
@@ -1717,7 +1739,7 @@ struct Lane {
             on_install_snapshot(m);
             return;
           case M_ConfigChangeEvent: on_config_change(m); return;
-          case M_SnapshotReceived: set_fault(F_UNSUPPORTED); return;
+          case M_SnapshotReceived: restore_remotes((u8)m.hint); return;  // raft.go:1566
           default: return;
         }
       case R_Candidate:
@@ -1743,7 +1765,7 @@ struct Lane {
             on_install_snapshot(m);
             return;
           case M_ConfigChangeEvent: on_config_change(m); return;
-          case M_SnapshotReceived: set_fault(F_UNSUPPORTED); return;
+          case M_SnapshotReceived: restore_remotes((u8)m.hint); return;  // raft.go:1566
           default: return;
         }
       case R_Leader:
@@ -1776,7 +1798,7 @@ struct Lane {
           case M_Election: return;        // leader ignores Election
           case M_RequestVote: on_request_vote(m); return;
           case M_ConfigChangeEvent: on_config_change(m); return;
-          case M_SnapshotReceived: set_fault(F_UNSUPPORTED); return;
+          case M_SnapshotReceived: restore_remotes((u8)m.hint); return;  // raft.go:1566
           case M_RateLimit:  // handleLeaderRateLimit (raft.go:1779-1785)
             if (rl_on() && m.from >= 1 && m.from <= N) {
               RlSt& s = P.rl[r];
@@ -1914,6 +1936,10 @@ struct Lane {
           continue;
         }
         cc_apply = (u8)(CCA_VALID | (t << 3) | (u32)nid);
+        // the state machine's own membership (rsm membership.go: addNode /
+        // removeNode), which the next snapshot records
+        if (t == CC_AddNode && nid >= 1) sm_rem &= (u8)~(1u << (nid - 1));
+        if (t == CC_RemoveNode && nid >= 1) sm_rem |= (u8)(1u << (nid - 1));
       }
     }
     if (members & MB_CC_IN_LOG) {
@@ -1937,6 +1963,11 @@ struct Lane {
   RBE_HD void node_snapshot() {
     SnapSt sp = P.snp[r];
     if (snap_restored) flags |= HF_APPLIED_NEW;  // smAppliedIndex moved to the snapshot
+    // the state machine recovered from the snapshot: its membership is the
+    // snapshot's, and the node restores raft's remotes from it at the next
+    // step (RestoreRemotes, rsm/statemachine.go:236); the last step's is done
+    sm_rem = snap_restored ? sp.ss_rem : sm_rem;
+    sp.rr_pend = (u8)(snap_restored && C.membership ? 1 : 0);
     sp.marker = marker;
     sp.marker_term = marker_term;
     if (sp.compact_to) {
@@ -1954,15 +1985,17 @@ struct Lane {
       if (t != 0) {
         sp.ss_index = la;
         sp.ss_term = t;
+        sp.ss_rem = sm_rem;  // Snapshot.Membership: the state machine's at la
         sp.compact_to = la > C.compaction_overhead ? la - C.compaction_overhead : 0;
       }
     }
     sp.pend = snp_pend;
     sp.pend_rej = snp_rej;
+    sp.sm_rem = sm_rem;
     P.snp[r] = sp;
     marker = sp.marker;
     marker_term = sp.marker_term;
-    if (sp.compact_to || sp.pend) flags |= HF_SNAP_WORK;
+    if (sp.compact_to || sp.pend || sp.rr_pend) flags |= HF_SNAP_WORK;
     else flags &= (u8)~HF_SNAP_WORK;
   }
 
@@ -2064,6 +2097,11 @@ struct Lane {
     u8 pend0 = 0, pend_rej0 = 0;
     marker = marker_term = 0;
     applied0 = C.ext_apply ? P.applied[r] : processed;
+    // RestoreRemotes due at this step (bit 8 | the removed mask): the state
+    // machine recovered from a received snapshot at the end of the last step
+    // (SnapSt::rr_pend), or the host calls it (EXT_RESTORE, below)
+    u32 restore = 0;
+    sm_rem = 0;
     if (C.snapshot_entries) {
       const SnapSt& sp = P.snp[r];
       marker = sp.marker;
@@ -2071,6 +2109,8 @@ struct Lane {
       pend0 = sp.pend;
       pend_rej0 = sp.pend_rej;
       applied0 = umax64(applied0, sp.ss_index);
+      sm_rem = sp.sm_rem;
+      if (sp.rr_pend) restore = 0x100u | sp.ss_rem;
     }
     pc_lo = pc_hi = 0;
     arena_used = 0;
@@ -2145,6 +2185,8 @@ struct Lane {
           cc_node = ext.pad[0] >> 8;
         }
         if (ext.flags & EXT_CC_APPLY) cc_apply = (u8)ext.pad[1];
+        // the host's RestoreRemotes (it comes after the device's own, which it replaces)
+        if (ext.flags & EXT_RESTORE) restore = 0x100u | (u32)(ext.pad[2] & MB_REMOVED);
       }
     }
     if (pend0) {
@@ -2157,7 +2199,7 @@ struct Lane {
       // a round without a tick is a step only if handleEvents finds an event
       // (node.go:1030-1067): a message or notice, client input, an entry to apply
       bool ev = do_read || do_prop || xfer || unreach || snap_nodes || ext_applied || do_cc ||
-                cc_apply || (flags & (HF_APPLY_PENDING | HF_APPLIED_NEW));
+                cc_apply || restore || (flags & (HF_APPLY_PENDING | HF_APPLIED_NEW));
       for (u32 s = 0; s < N; s++)
         if (s != k && in_word<N>(P, g, s, k, round) != 0) ev = true;
       if (!ev) return true;  // no step: no outbox header either
@@ -2186,10 +2228,12 @@ struct Lane {
     u32 cs = 0, ci = 0, cn = 0, cna = 0;  // inbox cursor: sender, index, count, #A
     bool copen = false;
     const u32 phase0 = (unreach | snap_nodes) ? 0u : (round > 0 ? 1u : 2u);
-    // a ConfigChange applied since the last step comes first: Peer.
-    // ApplyConfigChange / RejectConfigChange are direct calls under raftMu
-    // between two steps (node.go applyConfigChange; peer.go:138-157)
-    u32 phase = cc_apply ? 8u : phase0;
+    // calls the node makes under raftMu between two steps come first:
+    // Peer.RestoreRemotes (peer.go:159-165, after the state machine recovered
+    // from a snapshot), then a ConfigChange the state machine applied: Peer.
+    // ApplyConfigChange / RejectConfigChange (node.go applyConfigChange;
+    // peer.go:138-157)
+    u32 phase = restore ? 9u : (cc_apply ? 8u : phase0);
     bool cc_proposed = false;
     u32 rep_bit = 0;  // local reports: next node bit
     rep_mask = 0;
@@ -2202,7 +2246,12 @@ struct Lane {
       u32 kind = 0;  // 0 none, 1 inbox message, 2 local message, 3 tick
       Msg m;
       const Ent* ents = nullptr;
-      if (phase == 8) {
+      if (phase == 9) {  // Handle(SnapshotReceived) with the snapshot's membership
+        phase = cc_apply ? 8u : phase0;
+        m = mk(M_SnapshotReceived, self);
+        m.hint = restore & 0xFFu;
+        kind = 2;
+      } else if (phase == 8) {
         phase = phase0;
         const u8 a = cc_apply;
         cc_apply = 0;
@@ -2642,7 +2691,7 @@ template <int N>
 RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, u64 vote,
                              u64 commit, u64 last, u32 n, const u64* t, const Body* b, u32 ppar,
                              u32 tclk, u64 marker = 0, u64 marker_term = 0, u64 ss_index = 0,
-                             u64 ss_term = 0) {
+                             u64 ss_term = 0, u8 removed = 0) {
   const u32 k = (u32)(r % N);
   const u64 g = r / N;
   const u64 cid = cid_of(C, g);
@@ -2655,6 +2704,8 @@ RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, 
     sp.marker_term = marker_term;
     sp.ss_index = ss_index;
     sp.ss_term = ss_term;
+    sp.ss_rem = sp.sm_rem = removed;  // the snapshot's membership; the state machine recovers it
+    sp.rr_pend = 0;
     if (sp.compact_to || sp.pend) snap_flags |= HF_SNAP_WORK;
     if (ss_index) snap_flags |= HF_APPLIED_NEW;  // recovered: confirmedIndex 0 lags it
     // Term(marker) for the steps' log lookups (the ring slot is free: the
@@ -2690,11 +2741,14 @@ RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, 
   c.members = c.cc_apply = c.pad = 0;
   c.t_last = n ? t[n - 1] : (last == marker ? marker_term : 0);
   c.lead_start = 0;
-  // the restarted raft reads the group's members from the LogDB (the static
-  // group: every slot a voter, as oracle/harness.cpp harness_restart)
-  if (C.membership)
+  // the restarted raft reads the group's members from the LogDB (NodeState:
+  // its snapshot's membership, raft.go:260-270; every slot a voter without one,
+  // as oracle/harness.cpp harness_restart)
+  if (C.membership) {
+    c.members = (u8)(removed & MB_REMOVED);
     for (u32 i = 0; i < n; i++)
-      if (ent_type(b[i].type) == E_ConfigChange) c.members = MB_CC_IN_LOG;
+      if (ent_type(b[i].type) == E_ConfigChange) c.members |= MB_CC_IN_LOG;
+  }
   P.core[r] = c;
   if (imark_on(C)) P.imark[r] = last + 1;  // inMemory.init(lastIndex), inmemory.go:46-57
   if (C.rl_max) {  // a new raft: a fresh limiter over an empty in-memory log

@@ -131,12 +131,21 @@ struct alignas(16) Core {
 // ss_req / compact_to the node's reqSnapshotIndex and compactLogTo (node.go
 // 585-605, 849-866); pend / pend_rej the SnapshotStatus the transport reports
 // for this replica's InstallSnapshots of the last step (bit id-1 per target).
+// Membership (cfg.membership; the Core::members encoding, bit id-1 = not a
+// voting member): ss_rem of the LogDB's snapshot (pb.Snapshot.Membership,
+// raft.pb.go:733-739, the voters it lists), sm_rem the state machine's own
+// (rsm membership: every ConfigChange it applied, or the snapshot it
+// recovered from), which a new snapshot records; rr_pend = a
+// RestoreRemotes(ss_rem) is due at the next step (the node calls it once the
+// state machine recovered from a snapshot, rsm/statemachine.go:236 →
+// peer.go:159-165).
 struct alignas(16) SnapSt {
   u64 marker, marker_term;
   u64 ss_index, ss_term;
   u64 ss_req, compact_to;
   u8 pend, pend_rej;
-  u8 pad[14];
+  u8 ss_rem, sm_rem, rr_pend;
+  u8 pad[11];
 };
 
 // remote slot (remote.go:62-69): match/next; state|active<<2 lives in a u8 plane
@@ -253,6 +262,7 @@ enum : u32 {
   EXT_APPLIED = 32,  // rbe_notify_applied changed raft.applied (an event, node.go:1033)
   EXT_CC_PROPOSE = 64,  // Peer.ProposeConfigChange: ExtIn::pad[0] = type | node id << 8
   EXT_CC_APPLY = 128,   // Peer.ApplyConfigChange / RejectConfigChange: pad[1] = a cc_apply byte
+  EXT_RESTORE = 256,    // Peer.RestoreRemotes: pad[2] = the snapshot's membership (removed mask)
 };
 struct alignas(16) ExtIn {
   u32 flags;

@@ -229,6 +229,7 @@ int outbox_messages(const Params& C, u64 g, u32 k, const CntRow& row, u32 round,
       o.hint = m.hint;
       o.hint_high = m.hint_high;
       o.n_entries = type == M_Replicate || type == M_Propose ? m.n_ent : 0u;
+      o.reserved = msg_reserved(m);
     }
     n++;
   };
@@ -338,6 +339,9 @@ int messages_to_records(const Params& C, HostHeap& heap, u32 round, u64 n, const
       x.m.commit = m.commit;
       x.m.hint = m.hint;
       x.m.hint_high = m.hint_high;
+      // an InstallSnapshot's snapshot membership (rbe_message.reserved, msg_reserved)
+      if (m.type == M_InstallSnapshot) x.m.pad0 = (u16)(m.reserved & MB_REMOVED);
+      if (m.type == M_InstallSnapshot && (m.reserved >> N)) return RBE_E_INVALID;
       if (m.type == M_Replicate) {
         x.slot = na;
         w += 1u;

@@ -14,7 +14,7 @@ import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libdragonboat_amd.so")
-RBE_ABI_VERSION = 6
+RBE_ABI_VERSION = 7
 
 COUNTER_NAMES = ["steps", "committed", "msg_in", "msg_out", "ent_in", "ent_out",
                  "reads_confirmed", "proposals", "reads", "quiesced_ticks", "active_ticks",
@@ -145,7 +145,7 @@ class RbeReadyToRead(C.Structure):
 
 class RbeLaunchState(C.Structure):
     _fields_ = [("term", C.c_uint64), ("vote", C.c_uint64), ("commit", C.c_uint64),
-                ("last_index", C.c_uint64), ("n_entries", C.c_uint32), ("reserved", C.c_uint32),
+                ("last_index", C.c_uint64), ("n_entries", C.c_uint32), ("removed", C.c_uint32),
                 ("marker", C.c_uint64), ("marker_term", C.c_uint64),
                 ("snapshot_index", C.c_uint64), ("snapshot_term", C.c_uint64)]
 
@@ -207,7 +207,7 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_xchg_status", "rbe_stream", "rbe_get_snapshot_state", "rbe_wire_encode",
            "rbe_wire_fetch", "rbe_wire_decode", "rbe_wire_ingest", "rbe_iso_leaders", "rbe_set_iso_leaders", "rbe_local_groups", "rbe_propose_entries", "rbe_commit",
            "rbe_get_update_commits", "rbe_propose_config_change", "rbe_apply_config_change",
-           "rbe_reject_config_change", "rbe_rate_limited"]
+           "rbe_reject_config_change", "rbe_rate_limited", "rbe_restore_remotes"]
 KERNEL_SLOTS = 4
 
 _lib = None
@@ -251,6 +251,7 @@ def load_library(path: Optional[str] = None):
         "rbe_propose_config_change": (i32, [vp, u64, P(u64), P(u32), P(u64)]),
         "rbe_apply_config_change": (i32, [vp, u64, P(u64), P(u64), P(u32)]),
         "rbe_reject_config_change": (i32, [vp, u64, P(u64)]),
+        "rbe_restore_remotes": (i32, [vp, u64, P(u64), P(u32), P(u64)]),
         "rbe_get_update_commits": (i32, [vp, u64, u64, P(RbeUpdateCommit)]),
         "rbe_run": (i32, [vp, u32]),
         "rbe_sync": (i32, [vp]),
@@ -529,7 +530,9 @@ class NodeInputs:
 
     def launch(self, replicas, states, entries):
         """rbe_launch: restart replicas[i] from states[i] = (term, vote, commit,
-        last_index[, marker, marker_term, snapshot_index, snapshot_term]) and
+        last_index[, marker, marker_term, snapshot_index, snapshot_term[,
+        removed]]) (removed: bit id-1 per node the LogDB's membership does
+        not list as a voter) and
         entries[i] = [(index, term, type, cmd[, key, client_id, series_id,
         responded_to]), ...], the tail of its LogDB (Peer.Launch over an
         existing log, peer.go:64-86)."""
@@ -538,10 +541,11 @@ class NodeInputs:
         flat = []
         for i, (s, ents) in enumerate(zip(states, entries)):
             term, vote, commit, last = s[:4]
-            snap = tuple(s[4:8]) + (0,) * (8 - max(4, len(s)))
+            snap = tuple(s[4:9]) + (0,) * (9 - max(4, len(s)))
             st[i] = RbeLaunchState(term=term, vote=vote, commit=commit, last_index=last,
                                    n_entries=len(ents), marker=snap[0], marker_term=snap[1],
-                                   snapshot_index=snap[2], snapshot_term=snap[3])
+                                   snapshot_index=snap[2], snapshot_term=snap[3],
+                                   removed=snap[4])
             flat.extend(ents)
         ea = (RbeEntry * max(1, len(flat)))()
         blob = bytearray()
@@ -564,6 +568,15 @@ class NodeInputs:
         u32a = (C.c_uint32 * max(1, len(types)))(*types)
         _check_input(self._input("apply_config_change", len(replicas), _u64s(replicas),
                                  _u64s(nodes), u32a), "rbe_apply_config_change")
+
+    def restore_remotes(self, replicas, voters):
+        """Peer.RestoreRemotes (rbe_restore_remotes; cfg.membership): replicas[i]'s
+        snapshot membership lists the node ids voters[i] (peer.go:159-165)."""
+        n = [len(v) for v in voters]
+        ids = [x for v in voters for x in v]
+        u32a = (C.c_uint32 * max(1, len(n)))(*n)
+        _check_input(self._input("restore_remotes", len(replicas), _u64s(replicas), u32a,
+                                 _u64s(ids)), "rbe_restore_remotes")
 
     def reject_config_change(self, replicas):
         """Peer.RejectConfigChange (rbe_reject_config_change)."""
@@ -813,14 +826,15 @@ class Engine(NodeInputs):
                 cmd.raw[:nc.value])
 
     def snapshot_state(self, first: int = 0, count: Optional[int] = None) -> np.ndarray:
-        """[count, 6] uint64: LogDB compaction marker, its term, snapshot index,
-        snapshot term, reqSnapshotIndex, pending compactLogTo per replica
+        """[count, 8] uint64: LogDB compaction marker, its term, snapshot index,
+        snapshot term, reqSnapshotIndex, pending compactLogTo, the snapshot's
+        membership and the state machine's (removed masks) per replica
         (rbe_get_snapshot_state; snapshot_entries > 0)."""
         count = self.n_rep - first if count is None else count
-        out = (C.c_uint64 * (6 * count))()
+        out = (C.c_uint64 * (8 * count))()
         _check(self.lib.rbe_get_snapshot_state(self.h, first, count, out),
                "rbe_get_snapshot_state")
-        return np.frombuffer(out, dtype=np.uint64).reshape(count, 6).copy()
+        return np.frombuffer(out, dtype=np.uint64).reshape(count, 8).copy()
 
     def views_np(self, first: int = 0, count: Optional[int] = None) -> np.ndarray:
         """views() as a numpy structured array (zero-copy over the ctypes array)."""

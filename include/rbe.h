@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RBE_ABI_VERSION 6
+#define RBE_ABI_VERSION 7
 
 /* error codes */
 #define RBE_OK 0
@@ -225,7 +225,11 @@ typedef struct rbe_update {
 typedef struct rbe_message {
   uint32_t type, reject;
   uint64_t to, from, cluster_id, term, log_term, log_index, commit, hint, hint_high;
-  uint32_t n_entries, reserved;
+  uint32_t n_entries;
+  /* InstallSnapshot: the snapshot's membership (Snapshot.Membership, raft.pb.go:
+   * 733-739) as the node ids it does not list as voters, bit (id-1) (its index
+   * and term are log_index / log_term); 0 for every other type */
+  uint32_t reserved;
 } rbe_message;
 
 /* raftpb Entry (raft.pb.go:589-598), every field: Index, Term, Type, the
@@ -257,7 +261,12 @@ typedef struct rbe_engine rbe_engine;
  * recovers from; all four are 0 without snapshots. */
 typedef struct rbe_launch_state {
   uint64_t term, vote, commit, last_index;
-  uint32_t n_entries, reserved;
+  uint32_t n_entries;
+  /* the membership the restarted raft reads from the LogDB (logdb NodeState =
+   * its latest snapshot's, raft.go:260-270), as the node ids that are not
+   * voting members: bit (id-1); needs cfg.membership when non-zero.  With
+   * snapshots it is also the snapshot's and the state machine's membership. */
+  uint32_t removed;
   uint64_t marker, marker_term, snapshot_index, snapshot_term;
 } rbe_launch_state;
 
@@ -397,6 +406,19 @@ int rbe_propose_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica
 int rbe_apply_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica,
                             const uint64_t* node_id, const uint32_t* type);
 int rbe_reject_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica);
+/* Peer.RestoreRemotes (peer.go:159-165 → raft.go:1566 handleRestoreRemote →
+ * restoreRemotes, 472-517), what the node calls once its state machine has
+ * recovered from a snapshot (rsm/statemachine.go:236 via node.go:241-264):
+ * replica[i]'s snapshot membership lists n_voters[i] voting members, their
+ * node ids (1..n_replicas, no repeats) next in voter_ids.  Before the replica's
+ * next step raft's voters become exactly those, every remote restarts (match 0,
+ * next lastIndex + 1; its own match lastIndex), and a leader the snapshot does
+ * not list steps down.  Staged like the inputs above (one per replica per
+ * step; the engine's own RestoreRemotes after an InstallSnapshot it restored
+ * runs first and is replaced by this one).  Needs cfg.membership and
+ * cfg.ext_inputs (RBE_E_STATE). */
+int rbe_restore_remotes(rbe_engine* e, uint64_t n, const uint64_t* replica,
+                        const uint32_t* n_voters, const uint64_t* voter_ids);
 
 /* Results of the last round.  Replaces Peer.GetUpdate (peer.go:201-207).
  * Peer.Commit (peer.go:282-293) consumes a step's outputs at the step; its log
@@ -411,12 +433,16 @@ int rbe_get_ready_to_reads(rbe_engine* e, uint64_t replica, rbe_ready_to_read* o
 int rbe_get_entries(rbe_engine* e, uint64_t replica, uint64_t lo, uint64_t hi,
                     rbe_entry* out);
 /* Node snapshot state of replicas [first, first + count) (snapshot_entries > 0,
- * else RBE_E_STATE): six words each — the LogDB's compaction marker and its
+ * else RBE_E_STATE): eight words each — the LogDB's compaction marker and its
  * term (entries at or below it are gone: logdb.go Compact / RemoveEntriesTo),
  * the latest snapshot's index and term (CreateSnapshot, or ApplySnapshot of one
  * received), the node's reqSnapshotIndex and pending compactLogTo (node.go
- * ss, 585-605 / 849-866). */
-int rbe_get_snapshot_state(rbe_engine* e, uint64_t first, uint64_t count, uint64_t* out6);
+ * ss, 585-605 / 849-866), the latest snapshot's membership and the state
+ * machine's current one, each as the node ids that are not voting members,
+ * bit (id-1) (pb.Snapshot.Membership, raft.pb.go:733-739; a snapshot records
+ * the state machine's membership at its index, and a node that restores one
+ * sends it to raft with RestoreRemotes at its next step). */
+int rbe_get_snapshot_state(rbe_engine* e, uint64_t first, uint64_t count, uint64_t* out8);
 
 /* raftpb UpdateCommit (raftpb/raft.go:60-70). */
 typedef struct rbe_update_commit {

@@ -106,6 +106,15 @@ struct Node {
   bool cc_pend = false, cc_reject = false;
   int cc_type = 0;
   u64 cc_node = 0;
+  // the state machine's membership (rsm membership: the ConfigChanges it
+  // applied, or the snapshot it recovered from), as the slots that are not
+  // voters, bit k; a snapshot records it (pb.Snapshot.Membership)
+  u32 sm_rem = 0;
+  // RestoreRemotes for the next step: the state machine recovered from a
+  // received snapshot (rr_pend: the LogDB's snapshot), or the host calls it
+  // (PUSH_RESTORE: x_rr_mask)
+  bool rr_pend = false, x_rr = false;
+  u32 x_rr_mask = 0;
   // host ProposeConfigChange for the next step (PUSH_CC_PROPOSE)
   bool x_cc = false;
   int x_cc_type = 0;
@@ -221,6 +230,23 @@ static Config node_config(const HarnessConfig& cfg, u64 cid, u32 k) {
   return c;
 }
 
+// pb.Membership of a group's slots from a removed mask (bit k = node k + 1 is
+// not a voter), and back: the harness's node addresses are "node-<id>"
+static Membership membership_of(u32 rem, u32 n) {
+  Membership m;
+  for (u32 j = 0; j < n; j++) {
+    if ((rem >> j) & 1u) m.removed[j + 1] = true;
+    else m.addresses[j + 1] = "node-" + std::to_string(j + 1);
+  }
+  return m;
+}
+static u32 removed_of(const Membership& m, u32 n) {
+  u32 rem = 0;
+  for (u32 j = 0; j < n; j++)
+    if (!m.addresses.count(j + 1)) rem |= 1u << j;
+  return rem;
+}
+
 static std::vector<std::pair<u64, std::string>> node_addrs(u32 n) {
   std::vector<std::pair<u64, std::string>> addrs;
   for (u32 k = 0; k < n; k++) addrs.push_back({k + 1, "node-" + std::to_string(k + 1)});
@@ -300,16 +326,25 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
     // a round without a tick is a step only if handleEvents finds an event
     // (node.go:1030-1067)
     bool ev = do_read || do_prop || xfer || nd->x_unreach || nd->x_snap || nd->snap_pend ||
-              p->HasEntryToApply() || applied != nd->confirmedIndex || do_cc || nd->cc_pend;
+              p->HasEntryToApply() || applied != nd->confirmedIndex || do_cc || nd->cc_pend ||
+              nd->rr_pend || nd->x_rr;
     for (u32 s = 0; s < n; s++) ev = ev || !nd->in[s].empty();
     if (!ev) return;
   }
   ctr[HC_STEPS]++;
   const Events ev0 = R->events;
   const u64 leader0 = R->leaderID;
-  // a ConfigChange the state machine applied (or the host sent) since the
-  // last step: Peer.ApplyConfigChange / RejectConfigChange (peer.go:138-157),
-  // direct calls under raftMu between two steps (node.go applyConfigChange)
+  // Peer.RestoreRemotes (peer.go:159-165) once the state machine recovered
+  // from a snapshot (rsm/statemachine.go:236 → node.go:241-264), or the
+  // host's; then a ConfigChange the state machine applied (or the host sent)
+  // since the last step: Peer.ApplyConfigChange / RejectConfigChange
+  // (peer.go:138-157).  Direct calls under raftMu between two steps.
+  if (nd->x_rr || nd->rr_pend) {
+    Snapshot ss = nd->db.snapshot;
+    if (nd->x_rr) ss.membership = membership_of(nd->x_rr_mask, n);
+    nd->x_rr = nd->rr_pend = false;
+    p->RestoreRemotes(ss);
+  }
   if (nd->cc_pend) {
     nd->cc_pend = false;
     if (nd->cc_reject) p->RejectConfigChange();
@@ -461,6 +496,9 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
         nd->cc_reject = false;
         nd->cc_type = t;
         nd->cc_node = nid;
+        // the state machine's membership (rsm membership.go addNode / removeNode)
+        if (t == AddNode && nid >= 1 && nid <= n) nd->sm_rem &= ~(1u << (nid - 1));
+        if (t == RemoveNode && nid >= 1 && nid <= n) nd->sm_rem |= 1u << (nid - 1);
       }
     }
     ctr[HC_ENT_APPLIED] += ud.committed_entries.size();
@@ -498,6 +536,10 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
       nd->db.ApplySnapshot(ud.snapshot);
       if (!cfg.ext_apply) nd->smAppliedIndex = ud.snapshot.index;
       nd->ss_index = ud.snapshot.index;
+      // the state machine takes the snapshot's membership, and the node
+      // restores raft's remotes from it at the next step (RestoreRemotes)
+      nd->sm_rem = removed_of(ud.snapshot.membership, n);
+      nd->rr_pend = cfg.membership != 0;
     }
     if (!cfg.ext_commit) {
       p->Commit(ud);  // commitRaftUpdate
@@ -531,8 +573,7 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
         Snapshot ss;
         ss.index = la;
         ss.term = t;
-        for (u32 j = 0; j < n; j++)
-          ss.membership.addresses[j + 1] = "node-" + std::to_string(j + 1);
+        ss.membership = membership_of(nd->sm_rem, n);  // the state machine's at la
         if (nd->db.CreateSnapshot(ss) == ErrOK) {
           if (la > cfg.compaction_overhead) nd->compact_to = la - cfg.compaction_overhead;
           nd->ss_index = la;
@@ -663,6 +704,11 @@ int harness_push(Harness* h, int kind, u64 replica, u64 a, u64 b, const Entry* e
       nd->cc_pend = true;
       nd->cc_reject = true;
       return 0;
+    case PUSH_RESTORE:
+      if (a >> N) return -1;
+      nd->x_rr = true;
+      nd->x_rr_mask = (u32)a;
+      return 0;
     default: return -1;
   }
 }
@@ -679,15 +725,17 @@ void harness_persisted(const Harness* h, u64 replica, u64 out4[4]) {
   out4[3] = db.lastIndex();
 }
 
-void harness_snapshot_state(const Harness* h, u64 replica, u64 out6[6]) {
+void harness_snapshot_state(const Harness* h, u64 replica, u64 out8[8]) {
   const u32 N = h->cfg.n_replicas;
   const Node* nd = h->groups[replica / N]->nodes[replica % N];
-  out6[0] = nd->db.markerIndex;
-  out6[1] = nd->db.markerTerm;
-  out6[2] = nd->db.snapshot.index;
-  out6[3] = nd->db.snapshot.term;
-  out6[4] = nd->ss_req;
-  out6[5] = nd->compact_to;
+  out8[0] = nd->db.markerIndex;
+  out8[1] = nd->db.markerTerm;
+  out8[2] = nd->db.snapshot.index;
+  out8[3] = nd->db.snapshot.term;
+  out8[4] = nd->ss_req;
+  out8[5] = nd->compact_to;
+  out8[6] = nd->db.snapshot.index ? removed_of(nd->db.snapshot.membership, N) : 0;
+  out8[7] = nd->sm_rem;
 }
 
 int harness_persisted_entries(const Harness* h, u64 replica, u64 lo, u64 hi, Entry* out) {
@@ -700,9 +748,10 @@ int harness_persisted_entries(const Harness* h, u64 replica, u64 lo, u64 hi, Ent
 }
 
 // A node restart (rbe_launch): the raft comes back through Peer.Launch over its
-// LogDB (initial = newNode = false, peer.go:64-86), with the group's members as
-// the persisted membership (the static groups of this harness; dragonboat
-// reads them from the snapshot/LogDB, logdb.NodeState), and the node around it
+// LogDB (initial = newNode = false, peer.go:64-86) with the LogDB's membership
+// (logdb.NodeState: its latest snapshot's, raft.go:260-270; without a snapshot
+// the group's bootstrap members, all of this harness's static slots), and the
+// state machine recovers that snapshot's membership too; the node around it
 // starts afresh: quiesce state, tick count, apply bookkeeping, apply-queue
 // state.  Messages in flight to and from the node are lost.  Host input
 // already staged for it stays staged.
@@ -712,8 +761,9 @@ void harness_restart(Harness* h, u64 replica) {
   Group* gr = h->groups[replica / N];
   const u32 k = (u32)(replica % N);
   Node* nd = gr->nodes[k];
-  for (u32 j = 0; j < N; j++)
-    nd->db.snapshot.membership.addresses[j + 1] = "node-" + std::to_string(j + 1);
+  if (nd->db.snapshot.index == 0) nd->db.snapshot.membership = membership_of(0, N);
+  nd->sm_rem = removed_of(nd->db.snapshot.membership, N);
+  nd->rr_pend = false;
   delete nd->peer;
   nd->peer = Peer::Launch(node_config(cfg, gr->cid, k), &nd->db, node_addrs(N), false, false);
   // a fresh quiesceManager kept on the harness's tick clock: its counters are

@@ -94,7 +94,8 @@ enum HarnessPush { PUSH_PROPOSE = 1, PUSH_READ = 2, PUSH_XFER = 3, PUSH_UNREACH 
                    PUSH_SNAPST = 5, PUSH_APPLIED = 6, PUSH_APPLY_READY = 7,
                    PUSH_CC_PROPOSE = 8,  // a = ConfigChangeType, b = node id (ProposeConfigChange)
                    PUSH_CC_APPLY = 9,    // a = node id (0 = NoNode), b = type (ApplyConfigChange)
-                   PUSH_CC_REJECT = 10 };  // RejectConfigChange
+                   PUSH_CC_REJECT = 10,  // RejectConfigChange
+                   PUSH_RESTORE = 11 };  // a = removed mask (RestoreRemotes with that membership)
 
 struct ReplicaView {  // mirrors rbe_replica_view in include/rbe.h
   u64 term, vote, leader_id, committed, last_index, processed, saved_to, digest;
@@ -182,7 +183,7 @@ u64 harness_log_term(const Harness* h, u64 g, u32 k, u64 index);  // term of ent
 void harness_persisted(const Harness* h, u64 replica, u64 out4[4]);  // term, vote, commit, last
 int harness_persisted_entries(const Harness* h, u64 replica, u64 lo, u64 hi, Entry* out);
 // LogDB marker, marker term, snapshot index, snapshot term; node reqSnapshotIndex, compactLogTo
-void harness_snapshot_state(const Harness* h, u64 replica, u64 out6[6]);
+void harness_snapshot_state(const Harness* h, u64 replica, u64 out8[8]);
 void harness_restart(Harness* h, u64 replica);
 // ext_commit: the UpdateCommit of the replica's last step (zero when it made no
 // Update; getUpdateCommit, peer.go:410-427), and Peer.Commit's log part with a

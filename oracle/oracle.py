@@ -105,7 +105,7 @@ VIEW_FIELDS = [f[0] for f in ReplicaView._fields_ if f[0] != "pad"]
 # harness_push kinds (oracle/harness.h HarnessPush)
 PUSH_PROPOSE, PUSH_READ, PUSH_XFER, PUSH_UNREACH, PUSH_SNAPST, PUSH_APPLIED, PUSH_APPLY_READY = \
     range(1, 8)
-PUSH_CC_PROPOSE, PUSH_CC_APPLY, PUSH_CC_REJECT = 8, 9, 10
+PUSH_CC_PROPOSE, PUSH_CC_APPLY, PUSH_CC_REJECT, PUSH_RESTORE = 8, 9, 10, 11
 # pb.ConfigChangeType (raft.pb.go): AddNode, RemoveNode, AddObserver, AddWitness
 CC_ADD_NODE, CC_REMOVE_NODE, CC_ADD_OBSERVER, CC_ADD_WITNESS = 0, 1, 2, 3
 
@@ -986,9 +986,11 @@ class Harness:
         return tuple(o)
 
     def snapshot_state(self, replica):
-        """(marker, marker_term, ss_index, ss_term, ss_req, compact_to): the
-        LogDB's compaction marker and snapshot, the node's snapshot request."""
-        o = (C.c_uint64 * 6)()
+        """(marker, marker_term, ss_index, ss_term, ss_req, compact_to, ss_removed,
+        sm_removed): the LogDB's compaction marker and snapshot, the node's
+        snapshot request, the snapshot's membership and the state machine's
+        (bit k: node k + 1 is not a voter)."""
+        o = (C.c_uint64 * 8)()
         lib().orc_harness_snapshot_state(self.h, replica, o)
         return tuple(o)
 

@@ -911,8 +911,8 @@ uint64_t orc_harness_log_term(void* h, uint64_t g, uint32_t k, uint64_t idx) {
 void orc_harness_persisted(void* h, uint64_t replica, uint64_t* out4) {
   harness_persisted((Harness*)h, replica, out4);
 }
-void orc_harness_snapshot_state(void* h, uint64_t replica, uint64_t* out6) {
-  harness_snapshot_state((Harness*)h, replica, out6);
+void orc_harness_snapshot_state(void* h, uint64_t replica, uint64_t* out8) {
+  harness_snapshot_state((Harness*)h, replica, out8);
 }
 int orc_harness_persisted_entries(void* h, uint64_t replica, uint64_t lo, uint64_t hi,
                                   orc_entry* out) {

@@ -16,7 +16,8 @@ def restart(eng, ref, replicas, ring, snapshots=False):
         lo = max(1, last - ring + 1)
         if snapshots:
             marker, mterm, ssi, sst = ref.snapshot_state(r)[:4]
-            snap = (marker, mterm, ssi, sst)
+            # the LogDB's membership (its snapshot's; all voters without one)
+            snap = (marker, mterm, ssi, sst, ref.snapshot_state(r)[6])
             lo = max(lo, marker + 1)
         es = ref.persisted_entries(r, lo, last) if last >= lo else []
         states.append((term, vote, commit, last) + snap)

@@ -98,6 +98,7 @@ def lib():
                 "propose_config_change": [C.c_uint64, u64p, u32p, u64p],
                 "apply_config_change": [C.c_uint64, u64p, u64p, u32p],
                 "reject_config_change": [C.c_uint64, u64p],
+                "restore_remotes": [C.c_uint64, u64p, u32p, u64p],
                 "get_update_commits": [C.c_uint64, C.c_uint64, P(RbeUpdateCommit)],
                 "launch": [C.c_uint64, u64p, C.c_void_p, C.c_void_p, C.c_void_p]}.items():
             fn = getattr(L, "soa_" + name)
@@ -252,9 +253,9 @@ class SoaCpu(NodeInputs):
         return buf.raw[:got], [fr[i] for i in range(nf.value)]
 
     def snapshot_state(self):
-        o = (C.c_uint64 * (6 * self.n_rep))()
+        o = (C.c_uint64 * (8 * self.n_rep))()
         lib().soa_snapshot_state(self.h, o)
-        return [tuple(o[6 * r:6 * r + 6]) for r in range(self.n_rep)]
+        return [tuple(o[8 * r:8 * r + 8]) for r in range(self.n_rep)]
 
     def counters(self):
         o = (C.c_uint64 * CTR_NUM)()

@@ -416,15 +416,15 @@ int soa_launch(void* h, uint64_t n, const uint64_t* replica, const rbe_launch_st
     if (e->C.n == 1)
       relaunch_replica<1>(e->P, e->C, replica[i], x.term, x.vote, x.commit, x.last_index,
                           x.n_entries, t, b, ppar, e->tclk, x.marker, x.marker_term,
-                          x.snapshot_index, x.snapshot_term);
+                          x.snapshot_index, x.snapshot_term, (u8)x.removed);
     else if (e->C.n == 3)
       relaunch_replica<3>(e->P, e->C, replica[i], x.term, x.vote, x.commit, x.last_index,
                           x.n_entries, t, b, ppar, e->tclk, x.marker, x.marker_term,
-                          x.snapshot_index, x.snapshot_term);
+                          x.snapshot_index, x.snapshot_term, (u8)x.removed);
     else
       relaunch_replica<5>(e->P, e->C, replica[i], x.term, x.vote, x.commit, x.last_index,
                           x.n_entries, t, b, ppar, e->tclk, x.marker, x.marker_term,
-                          x.snapshot_index, x.snapshot_term);
+                          x.snapshot_index, x.snapshot_term, (u8)x.removed);
     e->P.gwake[replica[i] / e->C.n] = GW_AWAKE;
     off += x.n_entries;
   }
@@ -481,6 +481,12 @@ int soa_reject_config_change(void* h, uint64_t n, const uint64_t* replica) {
   SoaEngine* e = (SoaEngine*)h;
   if (!e->C.membership || !e->C.ext_inputs) return RBE_E_STATE;
   return e->hin.apply_config_change(n, replica, nullptr, nullptr, true);
+}
+int soa_restore_remotes(void* h, uint64_t n, const uint64_t* replica, const uint32_t* n_voters,
+                        const uint64_t* ids) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (!e->C.membership || !e->C.ext_inputs) return RBE_E_STATE;
+  return e->hin.restore_remotes(n, replica, n_voters, ids);
 }
 // rbe_commit / rbe_get_update_commits on the host build
 int soa_commit(void* h, uint64_t n, const uint64_t* replica, const rbe_update_commit* uc) {
@@ -752,11 +758,11 @@ int soa_set_iso_leaders(void* h, const uint8_t* bits) {
   return RBE_OK;
 }
 
-void soa_snapshot_state(void* h, uint64_t* out6) {
+void soa_snapshot_state(void* h, uint64_t* out8) {
   SoaEngine* e = (SoaEngine*)h;
   for (u64 r = 0; r < e->C.n_rep; r++) {
-    if (e->P.snp) snap_state_row(e->P.snp[r], out6 + 6 * r);
-    else memset(out6 + 6 * r, 0, 6 * sizeof(u64));
+    if (e->P.snp) snap_state_row(e->P.snp[r], out8 + 8 * r);
+    else memset(out8 + 8 * r, 0, 8 * sizeof(u64));
   }
 }
 
