@@ -55,6 +55,7 @@ __global__ __launch_bounds__(kBlock) void k_ext_scatter(Planes P, u32 nrep, cons
                                                         const ExtIn* recs, u64 n,
                                                         const u64* app_rep, const u64* app_val,
                                                         u64 na, const CommitRec* cr, u64 nc,
+                                                        const SnapRec* sr, u64 ns,
                                                         Params C, Lists L, u32 par) {
   const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
   if (i < n) {
@@ -80,6 +81,8 @@ __global__ __launch_bounds__(kBlock) void k_ext_scatter(Planes P, u32 nrep, cons
   if (i < nc)
     commit_update(P, C, cr[i].r, cr[i].stable_log_to, cr[i].stable_log_term, cr[i].processed,
                   cr[i].last_applied);
+  // rbe_snapshot_saved / rbe_compact records (one per replica)
+  if (i < ns) snap_rec_apply(P, sr[i]);
 }
 
 // ---- batched Updates (rbe_collect_updates): flag → scan → write
@@ -531,9 +534,13 @@ static int make_params(const rbe_config* cfg, Params* out) {
   // node snapshots + LogDB compaction (SnapSt; rbe_step.h node_snapshot): the
   // snapshot is taken at the state machine's applied index, which is the
   // engine's own (processed) only without ext_apply
+  // With ext_apply the host's state machine is snapshotted by the host's
+  // snapshot worker, which tells the engine (rbe_snapshot_saved, rbe_compact);
+  // the engine then never snapshots by itself.  Not with ext_commit (a
+  // snapshot's UpdateCommit.StableSnapshotTo is not carried).
   C.snapshot_entries = cfg->snapshot_entries;
   C.compaction_overhead = cfg->compaction_overhead;
-  if (C.snapshot_entries && C.ext_apply) return RBE_E_INVALID;
+  if (C.snapshot_entries && C.ext_commit) return RBE_E_INVALID;
   // the compaction of a snapshot at index i reads Term(i - CompactionOverhead),
   // which must still be in the in-memory window
   if (C.snapshot_entries && C.compaction_overhead >= C.ring) return RBE_E_INVALID;
@@ -954,9 +961,10 @@ static int flush_inputs(rbe_engine* e) {
     HIP_OK(hipMemcpyAsync(e->heap_dev, &e->heap_head_host, sizeof(u64), hipMemcpyHostToDevice,
                           e->stream));
   }
-  const u64 n = h.reps.size(), na = h.app_rep.size(), nc = h.commits.size();
-  const u64 need =
-      n * (sizeof(u64) + sizeof(ExtIn)) + na * 2 * sizeof(u64) + nc * sizeof(CommitRec) + 64;
+  const u64 n = h.reps.size(), na = h.app_rep.size(), nc = h.commits.size(),
+            ns = h.snaps.size();
+  const u64 need = n * (sizeof(u64) + sizeof(ExtIn)) + na * 2 * sizeof(u64) +
+                   nc * sizeof(CommitRec) + ns * sizeof(SnapRec) + 64;
   HIP_OK(hipEventSynchronize(e->in_ev));  // the previous upload is out of in_pinned
   if (need > e->in_bytes) {
     if (e->in_pinned) HIP_OK(hipHostFree(e->in_pinned));
@@ -970,11 +978,13 @@ static int flush_inputs(rbe_engine* e) {
     e->in_bytes = cap;
   }
   // layout: replicas | records (16-B aligned) | applied replicas | applied values | commits
+  // | snapshot records
   u8* b = e->in_pinned;
   const u64 o_rec = (n * sizeof(u64) + 15) & ~15ull;
   const u64 o_ar = o_rec + n * sizeof(ExtIn), o_av = o_ar + na * sizeof(u64);
   const u64 o_cr = o_av + na * sizeof(u64);
-  const u64 total = o_cr + nc * sizeof(CommitRec);
+  const u64 o_sr = o_cr + nc * sizeof(CommitRec);
+  const u64 total = o_sr + ns * sizeof(SnapRec);
   if (n) {
     memcpy(b, h.reps.data(), n * sizeof(u64));
     memcpy(b + o_rec, h.recs.data(), n * sizeof(ExtIn));
@@ -984,16 +994,18 @@ static int flush_inputs(rbe_engine* e) {
     memcpy(b + o_av, h.app_val.data(), na * sizeof(u64));
   }
   if (nc) memcpy(b + o_cr, h.commits.data(), nc * sizeof(CommitRec));
+  if (ns) memcpy(b + o_sr, h.snaps.data(), ns * sizeof(SnapRec));
   if (total) HIP_OK(hipMemcpyAsync(e->in_dev, b, total, hipMemcpyHostToDevice, e->stream));
   if (!h.ents.empty())
     HIP_OK(hipMemcpyAsync(e->P.in_ents, h.ents.data(), h.ents.size() * sizeof(Ent),
                           hipMemcpyHostToDevice, e->stream));
-  const u64 m = std::max(n, std::max(na, nc));
+  const u64 m = std::max(std::max(n, ns), std::max(na, nc));
   if (m) {  // (a flush of heap records alone, e.g. from rbe_push_messages, has none)
     hipLaunchKernelGGL(k_ext_scatter, dim3(grid_for(m)), dim3(kBlock), 0, e->stream, e->P,
                        e->C.n, (const u64*)e->in_dev, (const ExtIn*)(e->in_dev + o_rec), n,
                        (const u64*)(e->in_dev + o_ar), (const u64*)(e->in_dev + o_av), na,
-                       (const CommitRec*)(e->in_dev + o_cr), nc, e->C, e->L, e->round & 1u);
+                       (const CommitRec*)(e->in_dev + o_cr), nc,
+                       (const SnapRec*)(e->in_dev + o_sr), ns, e->C, e->L, e->round & 1u);
     HIP_OK(hipGetLastError());
   }
   HIP_OK(hipEventRecord(e->in_ev, e->stream));
@@ -1245,6 +1257,19 @@ int rbe_reject_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica)
   if (!e) return RBE_E_INVALID;
   if (!e->C.membership || !e->C.ext_inputs) return RBE_E_STATE;
   return e->hin.apply_config_change(n, replica, nullptr, nullptr, true);
+}
+
+int rbe_snapshot_saved(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint64_t* index,
+                       const uint64_t* term, const uint32_t* removed) {
+  if (!e) return RBE_E_INVALID;
+  if (!e->C.snapshot_entries || !e->C.ext_apply) return RBE_E_STATE;
+  return e->hin.snapshot_op(n, replica, SR_SAVE, index, term, removed, e->C.membership != 0);
+}
+
+int rbe_compact(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint64_t* to) {
+  if (!e) return RBE_E_INVALID;
+  if (!e->C.snapshot_entries || !e->C.ext_apply) return RBE_E_STATE;
+  return e->hin.snapshot_op(n, replica, SR_COMPACT, to, nullptr, nullptr, false);
 }
 
 int rbe_restore_remotes(rbe_engine* e, uint64_t n, const uint64_t* replica,

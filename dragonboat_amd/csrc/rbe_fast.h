@@ -495,7 +495,7 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
   else flags &= (u8)~HF_APPLY_PENDING;
   if (u.apply_hi >= u.apply_lo && !C.ext_apply) flags |= HF_APPLIED_NEW;
   else flags &= (u8)~HF_APPLIED_NEW;
-  if (C.snapshot_entries && u.apply_hi >= u.apply_lo)
+  if (C.snapshot_entries && !C.ext_apply && u.apply_hi >= u.apply_lo)  // (host's with ext_apply)
     fast_node_snapshot<N, TRACE>(P, C, ctr, o, c.processed, c.last_index, c.t_last, flags);
   if (role == R_Leader) {
     ctr.v[C_COMMITTED] += (u32)(c.committed - committed0);

@@ -421,6 +421,8 @@ struct HostInputs {
   std::vector<u64> applied;  // [n_rep] host mirror of Planes::applied (the host is its only writer)
   std::vector<CommitRec> commits;  // rbe_commit records for the next step, in call order
   std::vector<u8> committing;      // [n_rep] a commit is staged (one per replica per step)
+  std::vector<SnapRec> snaps;      // rbe_snapshot_saved / rbe_compact, one record per replica
+  std::vector<u32> snap_slot;      // [n_rep] index into snaps, ~0u = none
   const Params* owner = nullptr;  // replica-per-GPU mode: only owned replicas take input
 
   HostHeap heap;             // payload heap positions and staged bytes
@@ -434,9 +436,11 @@ struct HostInputs {
     mark.assign(n_rep, 0u);
     applied.assign(n_rep, 0);
     committing.assign(n_rep, 0);
+    snap_slot.assign(n_rep, ~0u);
   }
   bool empty() const {
-    return reps.empty() && app_rep.empty() && heap.stage.empty() && commits.empty();
+    return reps.empty() && app_rep.empty() && heap.stage.empty() && commits.empty() &&
+           snaps.empty();
   }
   void clear() {
     for (u64 r : reps) slot[r] = ~0u;
@@ -447,6 +451,8 @@ struct HostInputs {
     app_val.clear();
     for (const CommitRec& c : commits) committing[c.r] = 0;
     commits.clear();
+    for (const SnapRec& x : snaps) snap_slot[x.r] = ~0u;
+    snaps.clear();
     heap.stage.clear();
     heap.settle();
   }
@@ -669,6 +675,46 @@ struct HostInputs {
     }
     return RBE_OK;
   }
+  // rbe_snapshot_saved / rbe_compact (snapshot_entries with ext_apply): one of
+  // each per replica per step; a snapshot no newer than the state machine's
+  // applied index (what rbe_notify_applied reported), with its membership
+  int snapshot_op(u64 cnt, const u64* replica, u32 kind, const u64* index, const u64* term,
+                  const u32* removed, bool membership) {
+    if (cnt && !index) return RBE_E_INVALID;
+    if (kind == SR_SAVE && cnt && !term) return RBE_E_INVALID;
+    int rc = check_replicas(cnt, replica, 0);
+    if (rc) return rc;
+    for (u64 i = 0; i < cnt; i++) {
+      if (index[i] == 0) return RBE_E_INVALID;
+      if (kind == SR_SAVE) {
+        const u32 rem = removed ? removed[i] : 0u;
+        if (term[i] == 0 || index[i] > applied[replica[i]] || (rem >> n) || (rem && !membership))
+          return RBE_E_INVALID;
+      }
+      const u32 s = snap_slot[replica[i]];
+      if (s != ~0u && (snaps[s].kind & kind)) return RBE_E_STATE;
+      for (u64 j = 0; j < i; j++)
+        if (replica[j] == replica[i]) return RBE_E_STATE;
+    }
+    for (u64 i = 0; i < cnt; i++) {
+      const u64 r = replica[i];
+      if (snap_slot[r] == ~0u) {
+        snap_slot[r] = (u32)snaps.size();
+        snaps.push_back(SnapRec{r, 0, 0, 0, 0, 0});
+      }
+      SnapRec& x = snaps[snap_slot[r]];
+      x.kind |= kind;
+      if (kind == SR_SAVE) {
+        x.index = index[i];
+        x.term = term[i];
+        x.rem = removed ? removed[i] : 0u;
+      } else {
+        x.compact_to = index[i];
+      }
+      rec(r);  // an (empty) input record wakes a sleeping group
+    }
+    return RBE_OK;
+  }
   // rbe_commit: Peer.Commit's log part (rbe.h), checked whole, one per replica
   int commit(u64 cnt, const u64* replica, const rbe_update_commit* uc) {
     if (cnt && !uc) return RBE_E_INVALID;
@@ -703,6 +749,7 @@ struct HostInputs {
     for (size_t i = 0; i < app_rep.size(); i++) apply_pair(P, app_rep[i], app_val[i]);
     for (const CommitRec& c : commits)
       commit_update(P, C_, c.r, c.stable_log_to, c.stable_log_term, c.processed, c.last_applied);
+    for (const SnapRec& x : snaps) snap_rec_apply(P, x);
   }
 };
 

@@ -343,6 +343,34 @@ RBE_HD u32 commit_update(const Planes& P, const Params& C, u64 r, u64 stable_log
   return fault;
 }
 
+// Host-driven node snapshots (snapshot_entries with ext_apply; rbe_snapshot_saved
+// / rbe_compact): the node's snapshot worker saved a snapshot of the host's
+// state machine and the LogDB took it (doSaveSnapshot → LogReader.CreateSnapshot,
+// node.go:619-692; ErrSnapshotOutOfDate at or below the LogDB's: ignored), or
+// the node asks for a compaction (compactSnapshot's compactLogTo, run by the
+// replica's next step as compactLog, node.go:849-866).  One record per
+// replica between two steps, applied in place (the step re-reads SnapSt).
+struct SnapRec {
+  u64 r, index, term, compact_to;
+  u32 rem;   // the snapshot's membership (removed mask)
+  u32 kind;  // SR_SAVE | SR_COMPACT
+};
+enum : u32 { SR_SAVE = 1, SR_COMPACT = 2 };
+RBE_HD void snap_rec_apply(const Planes& P, const SnapRec& x) {
+  SnapSt& sp = P.snp[x.r];
+  if ((x.kind & SR_SAVE) && x.index > sp.ss_index) {
+    sp.ss_index = x.index;
+    sp.ss_term = x.term;
+    sp.ss_rem = (u8)x.rem;
+  }
+  if (x.kind & SR_COMPACT) {
+    sp.compact_to = x.compact_to;
+    // the next step takes the full table and compacts after its Update
+    P.hot[x.r].flags |= HF_SNAP_WORK;
+    P.idle[x.r] &= (u8)~IB_LAZY;
+  }
+}
+
 // entryutils.go:97-104 / 106-114: message types only a node makes for its own
 // raft (Peer.Handle panics on them), and response types (dropped when the
 // sender is not a member)
@@ -1962,24 +1990,29 @@ struct Lane {
   // compactSnapshot, node.go:619-692), done within the step.
   RBE_HD void node_snapshot() {
     SnapSt sp = P.snp[r];
-    if (snap_restored) flags |= HF_APPLIED_NEW;  // smAppliedIndex moved to the snapshot
+    // smAppliedIndex moved to the snapshot (with ext_apply the host's state
+    // machine recovers it and reports its applied index itself)
+    if (snap_restored && !C.ext_apply) flags |= HF_APPLIED_NEW;
     // the state machine recovered from the snapshot: its membership is the
     // snapshot's, and the node restores raft's remotes from it at the next
     // step (RestoreRemotes, rsm/statemachine.go:236); the last step's is done
     sm_rem = snap_restored ? sp.ss_rem : sm_rem;
-    sp.rr_pend = (u8)(snap_restored && C.membership ? 1 : 0);
+    sp.rr_pend = (u8)(snap_restored && C.membership && !C.ext_apply ? 1 : 0);
     sp.marker = marker;
     sp.marker_term = marker_term;
     if (sp.compact_to) {
+      // LogDB.Compact inside (marker, lastIndex], never past its snapshot
       const u64 c = sp.compact_to;
-      if (c > marker && c <= last) {
+      if (c > marker && c <= last && c <= sp.ss_index) {
         sp.marker_term = log_term(c);
         sp.marker = c;
       }
       sp.compact_to = 0;
     }
+    // saveSnapshotRequired: the engine's own state machine only; with ext_apply
+    // the host's snapshot worker decides (rbe_snapshot_saved / rbe_compact)
     const u64 S = C.snapshot_entries, la = processed;
-    if (la > S + sp.ss_index && la > S + sp.ss_req) {
+    if (!C.ext_apply && la > S + sp.ss_index && la > S + sp.ss_req) {
       sp.ss_req = la;
       const u64 t = log_term(la);
       if (t != 0) {
@@ -2108,7 +2141,9 @@ struct Lane {
       marker_term = sp.marker_term;
       pend0 = sp.pend;
       pend_rej0 = sp.pend_rej;
-      applied0 = umax64(applied0, sp.ss_index);
+      // the state machine recovered from the LogDB's snapshot (with ext_apply
+      // the host reports what its state machine has applied)
+      if (!C.ext_apply) applied0 = umax64(applied0, sp.ss_index);
       sm_rem = sp.sm_rem;
       if (sp.rr_pend) restore = 0x100u | sp.ss_rem;
     }
@@ -2707,7 +2742,7 @@ RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, 
     sp.ss_rem = sp.sm_rem = removed;  // the snapshot's membership; the state machine recovers it
     sp.rr_pend = 0;
     if (sp.compact_to || sp.pend) snap_flags |= HF_SNAP_WORK;
-    if (ss_index) snap_flags |= HF_APPLIED_NEW;  // recovered: confirmedIndex 0 lags it
+    if (ss_index && !C.ext_apply) snap_flags |= HF_APPLIED_NEW;  // recovered: confirmedIndex 0 lags it
     // Term(marker) for the steps' log lookups (the ring slot is free: the
     // entries above the marker are fewer than the ring)
     if (marker) P.term_ring[(marker & (u64)(C.ring - 1)) * C.n_rep + r] = marker_term;

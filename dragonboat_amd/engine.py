@@ -207,7 +207,8 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_xchg_status", "rbe_stream", "rbe_get_snapshot_state", "rbe_wire_encode",
            "rbe_wire_fetch", "rbe_wire_decode", "rbe_wire_ingest", "rbe_iso_leaders", "rbe_set_iso_leaders", "rbe_local_groups", "rbe_propose_entries", "rbe_commit",
            "rbe_get_update_commits", "rbe_propose_config_change", "rbe_apply_config_change",
-           "rbe_reject_config_change", "rbe_rate_limited", "rbe_restore_remotes"]
+           "rbe_reject_config_change", "rbe_rate_limited", "rbe_restore_remotes",
+           "rbe_snapshot_saved", "rbe_compact"]
 KERNEL_SLOTS = 4
 
 _lib = None
@@ -252,6 +253,8 @@ def load_library(path: Optional[str] = None):
         "rbe_apply_config_change": (i32, [vp, u64, P(u64), P(u64), P(u32)]),
         "rbe_reject_config_change": (i32, [vp, u64, P(u64)]),
         "rbe_restore_remotes": (i32, [vp, u64, P(u64), P(u32), P(u64)]),
+        "rbe_snapshot_saved": (i32, [vp, u64, P(u64), P(u64), P(u64), P(u32)]),
+        "rbe_compact": (i32, [vp, u64, P(u64), P(u64)]),
         "rbe_get_update_commits": (i32, [vp, u64, u64, P(RbeUpdateCommit)]),
         "rbe_run": (i32, [vp, u32]),
         "rbe_sync": (i32, [vp]),
@@ -577,6 +580,21 @@ class NodeInputs:
         u32a = (C.c_uint32 * max(1, len(n)))(*n)
         _check_input(self._input("restore_remotes", len(replicas), _u64s(replicas), u32a,
                                  _u64s(ids)), "rbe_restore_remotes")
+
+    def snapshot_saved(self, replicas, indexes, terms, removed=None):
+        """The host's snapshot worker saved a snapshot of its state machine and the
+        LogDB took it (rbe_snapshot_saved; snapshot_entries with ext_apply):
+        LogReader.CreateSnapshot in doSaveSnapshot (node.go:619-692)."""
+        rem = removed if removed is not None else [0] * len(replicas)
+        u32a = (C.c_uint32 * max(1, len(rem)))(*rem)
+        _check_input(self._input("snapshot_saved", len(replicas), _u64s(replicas),
+                                 _u64s(indexes), _u64s(terms), u32a), "rbe_snapshot_saved")
+
+    def compact(self, replicas, to):
+        """compactSnapshot's compactLogTo: the replica's next step compacts the
+        LogDB to `to` (compactLog, node.go:849-866; rbe_compact)."""
+        _check_input(self._input("compact", len(replicas), _u64s(replicas), _u64s(to)),
+                     "rbe_compact")
 
     def reject_config_change(self, replicas):
         """Peer.RejectConfigChange (rbe_reject_config_change)."""

@@ -137,8 +137,10 @@ typedef struct rbe_config {
   uint32_t xfer_period;
   uint32_t xfer_mod;
   uint32_t snapshot_entries;     /* config.SnapshotEntries: a node snapshot at the applied
-                                    index every that many applied entries, 0 = never
-                                    (requires ext_apply = 0; rbe_launch then refused) */
+                                    index every that many applied entries, 0 = never.
+                                    With ext_apply the host's snapshot worker decides
+                                    (rbe_snapshot_saved / rbe_compact) and any non-zero
+                                    value only turns snapshots on.  Not with ext_commit. */
   uint32_t compaction_overhead;  /* config.CompactionOverhead: the LogDB keeps that many
                                     entries below a snapshot (compacted at the next step);
                                     a remote that needs older entries gets InstallSnapshot */
@@ -406,6 +408,27 @@ int rbe_propose_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica
 int rbe_apply_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica,
                             const uint64_t* node_id, const uint32_t* type);
 int rbe_reject_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica);
+/* Host-driven snapshots (cfg.snapshot_entries with cfg.ext_apply; RBE_E_STATE
+ * otherwise): the node's snapshot worker around a state machine the host
+ * applies (node.go:585-692 saveSnapshotRequired / doSaveSnapshot /
+ * compactSnapshot, 849-866 compactLog).  One of each per replica between two
+ * steps, checked whole (RBE_E_INVALID / RBE_E_STATE, nothing staged).
+ *   rbe_snapshot_saved: the state machine's snapshot of replica[i] at index[i]
+ *     (at most the applied index last reported with rbe_notify_applied) of
+ *     term[i], listing the voters of removed[i] (bit (id-1): not a voter; null
+ *     = all; non-zero needs cfg.membership), was saved and the LogDB took it
+ *     (LogReader.CreateSnapshot; one at or below the LogDB's latest is out of
+ *     date and ignored).  A remote that needs entries the LogDB compacted away
+ *     gets this snapshot by InstallSnapshot (raft.go:684-697).
+ *   rbe_compact: compactLogTo = to[i]: the replica's next step compacts the
+ *     LogDB after its Update (LogReader.Compact: only inside (marker,
+ *     lastIndex] and never past the latest snapshot).
+ * A replica that restores a received snapshot reports RBE_UF_SNAPSHOT; the host
+ * recovers its state machine from it, reports the applied index
+ * (rbe_notify_applied) and calls rbe_restore_remotes. */
+int rbe_snapshot_saved(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint64_t* index,
+                       const uint64_t* term, const uint32_t* removed);
+int rbe_compact(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint64_t* to);
 /* Peer.RestoreRemotes (peer.go:159-165 → raft.go:1566 handleRestoreRemote →
  * restoreRemotes, 472-517), what the node calls once its state machine has
  * recovered from a snapshot (rsm/statemachine.go:236 via node.go:241-264):

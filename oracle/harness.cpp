@@ -539,7 +539,7 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
       // the state machine takes the snapshot's membership, and the node
       // restores raft's remotes from it at the next step (RestoreRemotes)
       nd->sm_rem = removed_of(ud.snapshot.membership, n);
-      nd->rr_pend = cfg.membership != 0;
+      nd->rr_pend = cfg.membership && !cfg.ext_apply;  // ext_apply: the host calls it
     }
     if (!cfg.ext_commit) {
       p->Commit(ud);  // commitRaftUpdate
@@ -562,11 +562,14 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
     // applied index, done within the step (the lockstep definition of the
     // snapshot worker)
     if (nd->compact_to) {
-      nd->db.Compact(nd->compact_to);  // ErrCompacted / ErrUnavailable: nothing to do
+      // ErrCompacted / ErrUnavailable: nothing to do; never past the snapshot
+      if (nd->compact_to <= nd->db.snapshot.index) nd->db.Compact(nd->compact_to);
       nd->compact_to = 0;
     }
+    // with ext_apply the host's snapshot worker decides (harness_snapshot_saved /
+    // harness_compact, the engine's rbe_snapshot_saved / rbe_compact)
     const u64 S = cfg.snapshot_entries, la = nd->smAppliedIndex;
-    if (!(la <= S + nd->ss_index || la <= S + nd->ss_req)) {
+    if (!cfg.ext_apply && !(la <= S + nd->ss_index || la <= S + nd->ss_req)) {
       nd->ss_req = la;
       u64 t = 0;
       if (R->log.term(la, &t) == ErrOK && t != 0) {
@@ -711,6 +714,29 @@ int harness_push(Harness* h, int kind, u64 replica, u64 a, u64 b, const Entry* e
       return 0;
     default: return -1;
   }
+}
+
+// Host-driven snapshots (ext_apply): the snapshot worker saved the state
+// machine's snapshot at `index` and the LogDB took it (doSaveSnapshot →
+// LogReader.CreateSnapshot, node.go:619-692; out of date: ignored), or asks
+// the next step to compact (compactSnapshot → compactLog, node.go:849-866).
+int harness_snapshot_saved(Harness* h, u64 replica, u64 index, u64 term, u32 removed) {
+  const u32 N = h->cfg.n_replicas;
+  if (replica >= h->groups.size() * N || index == 0 || term == 0 || (removed >> N)) return -1;
+  Node* nd = h->groups[replica / N]->nodes[replica % N];
+  if (index > nd->x_applied) return -1;  // only what the state machine applied
+  Snapshot ss;
+  ss.index = index;
+  ss.term = term;
+  ss.membership = membership_of(removed, N);
+  if (nd->db.CreateSnapshot(ss) == ErrOK) nd->ss_index = index;
+  return 0;
+}
+int harness_compact(Harness* h, u64 replica, u64 to) {
+  const u32 N = h->cfg.n_replicas;
+  if (replica >= h->groups.size() * N || to == 0) return -1;
+  h->groups[replica / N]->nodes[replica % N]->compact_to = to;
+  return 0;
 }
 
 u32 harness_round(const Harness* h) { return h->round; }

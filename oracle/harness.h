@@ -173,6 +173,8 @@ void harness_step(Harness* h, bool tick);
 // stage host input for replica g*n+k for the next round; returns 0
 int harness_push(Harness* h, int kind, u64 replica, u64 a, u64 b, const Entry* ents, u32 n);
 u32 harness_round(const Harness* h);
+int harness_snapshot_saved(Harness* h, u64 replica, u64 index, u64 term, u32 removed);
+int harness_compact(Harness* h, u64 replica, u64 to);
 void harness_views(const Harness* h, ReplicaView* out);  // n_groups*n_replicas views
 // Peer.RateLimited and rl.Get() of every replica (n_groups*n_replicas each)
 void harness_rate_limited(Harness* h, uint8_t* limited, u64* size);

@@ -194,6 +194,8 @@ def lib():
             "orc_harness_snapshot_state": (None, [vp, u64, P(u64)]),
             "orc_harness_persisted_entries": (i32, [vp, u64, u64, u64, P(OrcEntry)]),
             "orc_harness_restart": (i32, [vp, u64]),
+            "orc_harness_snapshot_saved": (i32, [vp, u64, u64, u64, u32]),
+            "orc_harness_compact": (i32, [vp, u64, u64]),
             "orc_harness_update_commit": (None, [vp, u64, P(u64)]),
             "orc_harness_commit": (i32, [vp, u64, P(u64)]),
             "orc_harness_inbox": (u32, [vp, u64, u32, P(u64), u32]),
@@ -1022,6 +1024,17 @@ class Harness:
         o = (C.c_uint64 * 640)()
         n = lib().orc_harness_inbox(self.h, replica, sender, o, 64)
         return [tuple(o[10 * i:10 * i + 10]) for i in range(min(n, 64))]
+
+    def snapshot_saved(self, replica, index, term, removed=0):
+        """ext_apply: the host's snapshot worker saved a snapshot and the LogDB
+        took it (the engine's rbe_snapshot_saved)."""
+        if lib().orc_harness_snapshot_saved(self.h, replica, index, term, removed) != 0:
+            raise _err()
+
+    def compact(self, replica, to):
+        """ext_apply: compactLogTo for the replica's next step (rbe_compact)."""
+        if lib().orc_harness_compact(self.h, replica, to) != 0:
+            raise _err()
 
     def restart(self, replica):
         """Restart a replica from its LogDB (the engine's rbe_launch)."""

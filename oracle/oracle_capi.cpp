@@ -952,6 +952,17 @@ uint32_t orc_harness_inbox(void* h, uint64_t replica, uint32_t sender, uint64_t*
                            uint32_t cap) {
   return harness_inbox((Harness*)h, replica, sender, out, cap);
 }
+int orc_harness_snapshot_saved(void* h, uint64_t replica, uint64_t index, uint64_t term,
+                               uint32_t removed) {
+  GUARD_BEGIN
+  return harness_snapshot_saved((Harness*)h, replica, index, term, removed);
+  GUARD_END(-1)
+}
+int orc_harness_compact(void* h, uint64_t replica, uint64_t to) {
+  GUARD_BEGIN
+  return harness_compact((Harness*)h, replica, to);
+  GUARD_END(-1)
+}
 int orc_harness_restart(void* h, uint64_t replica) {
   GUARD_BEGIN
   harness_restart((Harness*)h, replica);

@@ -99,6 +99,8 @@ def lib():
                 "apply_config_change": [C.c_uint64, u64p, u64p, u32p],
                 "reject_config_change": [C.c_uint64, u64p],
                 "restore_remotes": [C.c_uint64, u64p, u32p, u64p],
+                "snapshot_saved": [C.c_uint64, u64p, u64p, u64p, u32p],
+                "compact": [C.c_uint64, u64p, u64p],
                 "get_update_commits": [C.c_uint64, C.c_uint64, P(RbeUpdateCommit)],
                 "launch": [C.c_uint64, u64p, C.c_void_p, C.c_void_p, C.c_void_p]}.items():
             fn = getattr(L, "soa_" + name)

@@ -482,6 +482,17 @@ int soa_reject_config_change(void* h, uint64_t n, const uint64_t* replica) {
   if (!e->C.membership || !e->C.ext_inputs) return RBE_E_STATE;
   return e->hin.apply_config_change(n, replica, nullptr, nullptr, true);
 }
+int soa_snapshot_saved(void* h, uint64_t n, const uint64_t* replica, const uint64_t* index,
+                       const uint64_t* term, const uint32_t* removed) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (!e->C.snapshot_entries || !e->C.ext_apply) return RBE_E_STATE;
+  return e->hin.snapshot_op(n, replica, SR_SAVE, index, term, removed, e->C.membership != 0);
+}
+int soa_compact(void* h, uint64_t n, const uint64_t* replica, const uint64_t* to) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (!e->C.snapshot_entries || !e->C.ext_apply) return RBE_E_STATE;
+  return e->hin.snapshot_op(n, replica, SR_COMPACT, to, nullptr, nullptr, false);
+}
 int soa_restore_remotes(void* h, uint64_t n, const uint64_t* replica, const uint32_t* n_voters,
                         const uint64_t* ids) {
   SoaEngine* e = (SoaEngine*)h;

@@ -57,14 +57,17 @@ def test_footprint_and_validation():
     wrong_abi = E.make_config(n_groups=10)
     wrong_abi.abi_version = 99
     assert lib.rbe_footprint(C.byref(wrong_abi), C.byref(b)) == -1
-    # node snapshots: accepted, with their planes in the footprint; not with
-    # ext_apply (the snapshot index is the host's applied index there)
+    # node snapshots: accepted, with their planes in the footprint
     snap = C.c_uint64()
     assert lib.rbe_footprint(C.byref(E.make_config(n_groups=1000, snapshot_entries=16,
                                                    compaction_overhead=4)), C.byref(snap)) == 0
     assert snap.value >= b.value + 1000 * 3 * (64 + 3 * 8)
+    # host-driven snapshots (ext_apply) are fine; not with ext_commit
     assert lib.rbe_footprint(C.byref(E.make_config(n_groups=10, snapshot_entries=16, ext_inputs=True,
-                                                   ext_apply=True)), C.byref(b)) == -1
+                                                   ext_apply=True)), C.byref(b)) == 0
+    assert lib.rbe_footprint(C.byref(E.make_config(n_groups=10, snapshot_entries=16, ext_inputs=True,
+                                                   ext_apply=True, ext_commit=True)),
+                             C.byref(b)) == -1
 
 
 def test_null_handles_are_rejected():
