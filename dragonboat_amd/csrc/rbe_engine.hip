@@ -39,10 +39,16 @@ namespace rbe {
                                          hipStream_t, int, RoundArg, hipEvent_t*);
 RBE_EXTERN_ROUND(1, true)
 RBE_EXTERN_ROUND(1, false)
+RBE_EXTERN_ROUND(2, true)
+RBE_EXTERN_ROUND(2, false)
 RBE_EXTERN_ROUND(3, true)
 RBE_EXTERN_ROUND(3, false)
+RBE_EXTERN_ROUND(4, true)
+RBE_EXTERN_ROUND(4, false)
 RBE_EXTERN_ROUND(5, true)
 RBE_EXTERN_ROUND(5, false)
+RBE_EXTERN_ROUND(6, true)
+RBE_EXTERN_ROUND(6, false)
 #undef RBE_EXTERN_ROUND
 }  // namespace rbe
 #endif
@@ -476,7 +482,8 @@ static int make_params(const rbe_config* cfg, Params* out) {
   Params C;
   memset(&C, 0, sizeof(C));
   C.n = cfg->n_replicas;
-  if (C.n != 1 && C.n != 3 && C.n != 5) return RBE_E_INVALID;
+  if (!valid_n(C.n)) return RBE_E_INVALID;
+  C.n_voters = cfg->n_voters ? cfg->n_voters : C.n;
   if (cfg->n_groups == 0) return RBE_E_INVALID;
   C.n_groups = cfg->n_groups;
   C.n_rep = cfg->n_groups * C.n;
@@ -527,6 +534,8 @@ static int make_params(const rbe_config* cfg, Params* out) {
   C.cc_period = cfg->cc_period;
   C.cc_mod = cfg->cc_mod ? cfg->cc_mod : 1;
   if (C.cc_period && !C.membership) return RBE_E_INVALID;
+  // spare slots (nodes that join later) need membership change
+  if (C.n_voters > C.n || (C.n_voters < C.n && !C.membership)) return RBE_E_INVALID;
   C.in_cap = cfg->in_cap ? cfg->in_cap : (u32)(cfg->n_groups > 1024 ? cfg->n_groups : 1024);
   if (cfg->n_groups > 0xFFFFFFFFull && !cfg->in_cap) C.in_cap = 0xFFFFFFFFu;
   C.xfer_period = cfg->xfer_period;
@@ -553,12 +562,8 @@ static int make_params(const rbe_config* cfg, Params* out) {
 
 template <typename F>
 static int dispatch_n(u32 n, F&& f) {
-  switch (n) {
-    case 1: return f(std::integral_constant<int, 1>());
-    case 3: return f(std::integral_constant<int, 3>());
-    case 5: return f(std::integral_constant<int, 5>());
-    default: return RBE_E_INVALID;
-  }
+  if (!valid_n(n)) return RBE_E_INVALID;
+  return with_n(n, f);
 }
 
 template <typename T>

@@ -579,7 +579,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
   const u32 round = ck.round;
   using Cap = FastCaps<N>;
   constexpr u32 Q = N / 2 + 1;
-  if constexpr (N < 3) {
+  if constexpr (!kFastN<N>) {
     return false;
   } else {
   const u64 g = r / N;
@@ -1297,7 +1297,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
                       StageRow<N>* sr = nullptr, u32 aux = 0, u32* staged = nullptr) {
   const u32 round = ck.round;
   using Cap = FastCaps<N>;
-  if constexpr (N < 3) {
+  if constexpr (!kFastN<N>) {
     return false;
   } else {
   const u64 g = r / N;

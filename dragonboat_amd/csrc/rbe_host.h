@@ -15,6 +15,7 @@
 #pragma once
 #include <cstring>
 #include <functional>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/rbe.h"
@@ -22,6 +23,23 @@
 #include "rbe_types.h"
 
 namespace rbe {
+
+// The group sizes the engine is built for (voting slots per group): every
+// kernel and host routine templated on N is instantiated for each.
+inline bool valid_n(u32 n) { return n >= 1 && n <= kMaxN; }
+// f(std::integral_constant<int, N>()) for the runtime group size n (checked
+// by the caller with valid_n; anything else takes N = 1)
+template <typename F>
+inline auto with_n(u32 n, F&& f) -> decltype(f(std::integral_constant<int, 1>())) {
+  switch (n) {
+    case 2: return f(std::integral_constant<int, 2>());
+    case 3: return f(std::integral_constant<int, 3>());
+    case 4: return f(std::integral_constant<int, 4>());
+    case 5: return f(std::integral_constant<int, 5>());
+    case 6: return f(std::integral_constant<int, 6>());
+    default: return f(std::integral_constant<int, 1>());
+  }
+}
 
 // Fingerprint of a Cmd longer than 16 bytes (Body/Ent lo when the bytes live in
 // the payload heap): 64 bits over the zero-padded 8-byte words and the length.

@@ -433,6 +433,7 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
         cls = C.rl_max ? T_FULL : class_of_role(idle_role(ib));
       else
         cls = triage_replica<N, TRACE>(P, C, r, ck, c);
+      if (!kFastN<N> && (cls == T_LEAD || cls == T_FOLL)) cls = T_FULL;  // no fast step for N
       if (shortcut) atomicAdd(&s_gst[slot], ((ib & IB_LEAD) ? 1u : 0u) + (done ? 0u : 256u));
     }
     // the back of the list: a leader proposing this round, a follower

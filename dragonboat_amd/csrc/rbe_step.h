@@ -2633,18 +2633,29 @@ RBE_HD bool step_replica_fast(const Planes& P, const Params& C, u64 r, Clk ck,
 }
 
 // ------------------------------------------------------------------ launch
+// The voters a replica starts with, as the slots it does not count (removed
+// mask): the initial members for one of them, nobody for a slot that joins
+// later (Params::n_voters; the membership its LogDB reports before any snapshot)
+RBE_HD u32 boot_removed(const Params& C, u32 k) {
+  const u32 all = (1u << C.n) - 1u;
+  return k < C.n_voters ? all & ~((1u << C.n_voters) - 1u) : all;
+}
 // Launch (peer.go:64-86) + bootstrap (peer.go:378-408) for one replica:
 // newRaft → becomeFollower(0) draws a timeout, Launch → becomeFollower(1)
-// draws another; N config-change entries at term 1, committed; remotes
-// {match 0, next N+1}.
+// draws another; one config-change entry per initial voter at term 1,
+// committed; remotes {match 0, next V+1}.  A slot beyond the initial voters is
+// a node that joins later (node.go:280-292, no peers, initial = false): term
+// 1, an empty log, no remotes.
 template <int N>
 RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   const u32 k = (u32)(r % N);
   const u64 cid = cid_of(C, r / N);
   const u64 self = k + 1;
+  const bool boot = k < C.n_voters;
+  const u32 V = boot ? C.n_voters : 0u;  // bootstrap entries in this replica's log
   Hot h;
   h.role = R_Follower;
-  h.flags = HF_APPLY_PENDING;  // the bootstrap entries are saved and applied in round 0
+  h.flags = boot ? HF_APPLY_PENDING : (u8)0;  // the bootstrap entries are saved and applied in round 0
   h.votes_resp = h.votes_granted = 0;
   h.election_tick = 0;
   h.heartbeat_tick = 0;
@@ -2656,8 +2667,8 @@ RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   P.idle[r] = idle_byte(C, h.role, h.flags, 0);
   Core c;
   c.term = 1;
-  c.committed = N;
-  c.last_index = N;
+  c.committed = V;
+  c.last_index = V;
   c.processed = 0;
   c.saved_to = 0;
   c.vote = 0;
@@ -2665,25 +2676,32 @@ RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   c.ltt = 0;
   c.rq_head = c.rq_count = 0;
   c.members = c.cc_apply = c.pad = 0;
-  c.t_last = 1;  // bootstrap entries are at term 1
+  c.t_last = boot ? 1 : 0;  // bootstrap entries are at term 1
   c.lead_start = 0;
-  if (C.membership) c.members = MB_CC_IN_LOG;  // the bootstrap ConfigChanges, applied in round 0
+  // the bootstrap ConfigChanges, applied in round 0; the slots outside the
+  // replica's initial membership
+  if (C.membership) c.members = (u8)((boot ? MB_CC_IN_LOG : 0u) | boot_removed(C, k));
   P.core[r] = c;
-  if (imark_on(C)) P.imark[r] = 1;  // inMemory.init(0), then bootstrap appends 1..N
+  if (imark_on(C)) P.imark[r] = 1;  // inMemory.init(0), then bootstrap appends 1..V
   if (C.rl_max) {  // newRateLimiter; bootstrap's append is a merge that adds its entries
     RlSt s = {};
     s.new_ent = 1;
-    s.size = rl_enabled(C.rl_max) ? N * (kEntryInMem + 8) : 0;
+    s.size = rl_enabled(C.rl_max) ? V * (kEntryInMem + 8) : 0;
     P.rl[r] = s;
+  }
+  if (C.snapshot_entries) {  // the LogDB's membership before any snapshot: the bootstrap's
+    SnapSt sp = {};
+    sp.ss_rem = sp.sm_rem = (u8)boot_removed(C, k);
+    P.snp[r] = sp;
   }
   for (u32 s = 0; s < N; s++) {
     RemoteMN x;
     x.match = 0;
-    x.next = N + 1;
+    x.next = V + 1;
     P.rem[r * N + s] = x;
     P.rem_st[r * N + s] = 0;
   }
-  for (u32 i = 1; i <= N; i++) {
+  for (u32 i = 1; i <= V; i++) {
     u64 slot = (i & (u64)(C.ring - 1)) * C.n_rep + r;
     P.term_ring[slot] = 1;
     Body b;
@@ -2951,6 +2969,10 @@ RBE_HD u32 aux_count_word(u32 aux, u32 k, u32 s) {
   return (f & 7u) | (((f >> 3) & 7u) << 7) | (((f >> 6) & 1u) << 15);
 }
 
+// the group sizes with steady-state fast steps (rbe_fast.h lead_fast /
+// foll_fast); other sizes step every replica-round on the full handler table
+template <int N>
+constexpr bool kFastN = N >= 3 && N <= 5;
 RBE_HD u32 class_of_role(u32 role) {
   return role == R_Leader ? 1u /*T_LEAD*/ : (role == R_Follower ? 2u /*T_FOLL*/ : 3u /*T_FULL*/);
 }

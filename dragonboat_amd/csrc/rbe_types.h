@@ -15,6 +15,9 @@ typedef uint32_t u32;
 typedef uint16_t u16;
 typedef uint8_t u8;
 
+// the largest group size (voting slots per group) the engine is built for
+static constexpr u32 kMaxN = 6;
+
 // raftpb MessageType, raft.pb.go:23-51
 enum : u32 {
   M_LocalTick = 0, M_Election = 1, M_LeaderHeartbeat = 2, M_ConfigChangeEvent = 3,
@@ -92,7 +95,7 @@ enum : u8 {
 
 // Core::members / Core::cc_apply bits
 enum : u8 {
-  MB_REMOVED = 0x1F,   // slots that are not voting members
+  MB_REMOVED = 0x7F,   // slots that are not voting members (bit s = slot s)
   MB_CC_IN_LOG = 0x80,
   CCA_VALID = 0x80, CCA_REJECT = 0x40,  // cc_apply: node id bits 0-2, ConfigChangeType bits 3-5
 };
@@ -294,7 +297,8 @@ struct Params {
   u64 cid_stride;
   u64 seed;
   u64 max_entry_size;
-  u32 n;              // replicas per group (N)
+  u32 n;              // replica slots per group (N)
+  u32 n_voters;       // slots 0..n_voters-1 bootstrap the group, the rest join later
   u32 ring;           // term/payload ring entries (power of two)
   u32 rq_cap;         // readIndex queue capacity
   u32 maxm;           // message slots per (sender, dest) per round

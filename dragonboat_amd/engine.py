@@ -46,7 +46,7 @@ class RbeConfig(C.Structure):
                 ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
                 ("heap_bytes", C.c_uint64), ("ext_commit", C.c_uint32),
                 ("membership", C.c_uint32), ("cc_period", C.c_uint32), ("cc_mod", C.c_uint32),
-                ("rep_compact", C.c_uint32), ("reserved0", C.c_uint32),
+                ("rep_compact", C.c_uint32), ("n_voters", C.c_uint32),
                 ("max_inmem_log_size", C.c_uint64)]
 
 
@@ -336,7 +336,7 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                 snapshot_entries: int = 0, compaction_overhead: int = 0,
                 ext_commit: bool = False, membership: bool = False, cc_period: int = 0,
                 cc_mod: int = 1, rep_compact: bool = False,
-                max_inmem_log_size: int = 0) -> RbeConfig:
+                max_inmem_log_size: int = 0, n_voters: int = 0) -> RbeConfig:
     return RbeConfig(abi_version=RBE_ABI_VERSION, device=device, n_groups=n_groups,
                      n_replicas=n_replicas, election_rtt=election_rtt,
                      heartbeat_rtt=heartbeat_rtt, check_quorum=int(check_quorum),
@@ -352,7 +352,8 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                      heap_bytes=heap_bytes, snapshot_entries=snapshot_entries,
                      compaction_overhead=compaction_overhead, ext_commit=int(ext_commit),
                      membership=int(membership), cc_period=cc_period, cc_mod=cc_mod,
-                     rep_compact=int(rep_compact), max_inmem_log_size=max_inmem_log_size)
+                     rep_compact=int(rep_compact), max_inmem_log_size=max_inmem_log_size,
+                     n_voters=n_voters)
 
 
 class InputError(EngineError):

@@ -95,7 +95,7 @@ typedef struct rbe_config {
   uint32_t abi_version;      /* RBE_ABI_VERSION */
   int32_t device;            /* HIP device ordinal */
   uint64_t n_groups;         /* groups owned by this engine */
-  uint32_t n_replicas;       /* voting replicas per group: 1, 3 or 5 */
+  uint32_t n_replicas;       /* replica slots per group, 1..6 (the group's largest size) */
   uint32_t election_rtt;     /* ticks, config.ElectionRTT */
   uint32_t heartbeat_rtt;    /* ticks, config.HeartbeatRTT */
   uint32_t check_quorum;     /* config.CheckQuorum */
@@ -168,7 +168,12 @@ typedef struct rbe_config {
    * every call are then the engine's local ones; rbe_local_groups maps them
    * to the global group (n_groups stays the global count). */
   uint32_t rep_compact;
-  uint32_t reserved0;
+  /* voting members a group starts with (0 = n_replicas): slots (node ids)
+   * 1..n_voters bootstrap the group (peer.go:378-408); the other slots are
+   * nodes that join later — started with no peers and an empty log
+   * (node.go:280-292 with join), taking part once an AddNode for them is
+   * applied.  Fewer than n_replicas needs cfg.membership. */
+  uint32_t n_voters;
   /* config.MaxInMemLogSize (config.go:118-131): the rate limiter
    * (internal/server/rate.go, raft.go:660-683, 1779-1785) over each replica's
    * in-memory log bytes; 0 (or UINT64_MAX) = off.  Rate-limited engines step

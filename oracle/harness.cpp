@@ -247,6 +247,14 @@ static u32 removed_of(const Membership& m, u32 n) {
   return rem;
 }
 
+// the voters a node starts with (its bootstrap): the initial members for one of
+// them, nobody for a node that joins later (removed masks)
+static u32 boot_removed(const HarnessConfig& cfg, u32 k) {
+  const u32 n = cfg.n_replicas, nv = cfg.n_voters ? cfg.n_voters : n;
+  const u32 all = (1u << n) - 1u;
+  return k < nv ? all & ~((1u << nv) - 1u) : all;
+}
+
 static std::vector<std::pair<u64, std::string>> node_addrs(u32 n) {
   std::vector<std::pair<u64, std::string>> addrs;
   for (u32 k = 0; k < n; k++) addrs.push_back({k + 1, "node-" + std::to_string(k + 1)});
@@ -255,18 +263,25 @@ static std::vector<std::pair<u64, std::string>> node_addrs(u32 n) {
 
 Harness* harness_create(const HarnessConfig& cfg) {
   if (cfg.n_replicas < 1 || cfg.n_replicas > 8) panicf("n_replicas must be 1..8");
+  const u32 nv = cfg.n_voters ? cfg.n_voters : cfg.n_replicas;
+  if (nv > cfg.n_replicas || (nv < cfg.n_replicas && !cfg.membership))
+    panicf("n_voters must be 1..n_replicas (fewer only with membership)");
   Harness* h = new Harness();
   h->cfg = cfg;
   std::vector<std::pair<u64, std::string>> addrs;
-  for (u32 k = 0; k < cfg.n_replicas; k++)
-    addrs.push_back({k + 1, "node-" + std::to_string(k + 1)});
+  for (u32 k = 0; k < nv; k++) addrs.push_back({k + 1, "node-" + std::to_string(k + 1)});
   for (u64 g = 0; g < cfg.n_groups; g++) {
     Group* gr = new Group();
     gr->cid = cfg.cid_base + g * cfg.cid_stride;
     for (u32 k = 0; k < cfg.n_replicas; k++) {
       Node* n = new Node();
       const Config c = node_config(cfg, gr->cid, k);
-      n->peer = Peer::Launch(c, &n->db, addrs, true, true);  // node.go:280-292
+      // node.go:280-292: the initial members bootstrap the group; the other
+      // slots are nodes that join later (StartCluster with join: no peers,
+      // initial = false, an empty log)
+      if (k < nv) n->peer = Peer::Launch(c, &n->db, addrs, true, true);
+      else n->peer = Peer::Launch(c, &n->db, {}, false, true);
+      n->sm_rem = boot_removed(cfg, k);
       n->q.enabled = cfg.quiesce;
       n->q.electionTick = cfg.election_rtt * 2;  // node.go:165
       gr->nodes.push_back(n);
@@ -334,6 +349,10 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
   ctr[HC_STEPS]++;
   const Events ev0 = R->events;
   const u64 leader0 = R->leaderID;
+  // the step's counters start here, before the calls made between two steps
+  // (the engine counts an entry a RemoveNode lets the leader commit with the step)
+  const u64 committed0 = R->log.committed;
+  const u64 campaigns0 = R->events.campaignLaunched;
   // Peer.RestoreRemotes (peer.go:159-165) once the state machine recovered
   // from a snapshot (rsm/statemachine.go:236 → node.go:241-264), or the
   // host's; then a ConfigChange the state machine applied (or the host sent)
@@ -352,8 +371,6 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
   }
   // handleEvents: updateBatchedLastApplied (node.go:1002-1006, 1032)
   p->NotifyRaftLastApplied(applied);
-  const u64 committed0 = R->log.committed;
-  const u64 campaigns0 = R->events.campaignLaunched;
   // handleReadIndexRequests (node.go:1108-1118)
   u64 readReq = 0;
   if (do_read) {
@@ -760,7 +777,9 @@ void harness_snapshot_state(const Harness* h, u64 replica, u64 out8[8]) {
   out8[3] = nd->db.snapshot.term;
   out8[4] = nd->ss_req;
   out8[5] = nd->compact_to;
-  out8[6] = nd->db.snapshot.index ? removed_of(nd->db.snapshot.membership, N) : 0;
+  // the LogDB's membership (NodeState): its latest snapshot's, else the bootstrap's
+  out8[6] = nd->db.snapshot.index ? removed_of(nd->db.snapshot.membership, N)
+                                  : boot_removed(h->cfg, (u32)(replica % N));
   out8[7] = nd->sm_rem;
 }
 
@@ -787,7 +806,8 @@ void harness_restart(Harness* h, u64 replica) {
   Group* gr = h->groups[replica / N];
   const u32 k = (u32)(replica % N);
   Node* nd = gr->nodes[k];
-  if (nd->db.snapshot.index == 0) nd->db.snapshot.membership = membership_of(0, N);
+  if (nd->db.snapshot.index == 0)
+    nd->db.snapshot.membership = membership_of(boot_removed(cfg, k), N);
   nd->sm_rem = removed_of(nd->db.snapshot.membership, N);
   nd->rr_pend = false;
   delete nd->peer;

@@ -85,6 +85,11 @@ struct HarnessConfig {
   // voter (while more than two vote) or adding it back (cc_input)
   u32 cc_period = 0;
   u32 cc_mod = 1;
+  // voting members a group starts with (0 = n_replicas): slots 0..n_voters-1
+  // bootstrap the group, the others are nodes that join later (Launch with
+  // no peers, initial = false: an empty log, no remotes) once an AddNode for
+  // them is applied (needs membership)
+  u32 n_voters = 0;
   // config.MaxInMemLogSize: every raft's rate limiter (0 = off)
   u64 max_inmem_log_size = 0;
 };

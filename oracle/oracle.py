@@ -81,7 +81,7 @@ class OrcHarnessConfig(C.Structure):
                 ("xfer_mod", C.c_uint32), ("ext_apply", C.c_uint32),
                 ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
                 ("ext_commit", C.c_uint32), ("membership", C.c_uint32),
-                ("cc_period", C.c_uint32), ("cc_mod", C.c_uint32), ("pad4", C.c_uint32),
+                ("cc_period", C.c_uint32), ("cc_mod", C.c_uint32), ("n_voters", C.c_uint32),
                 ("max_inmem_log_size", C.c_uint64)]
 
 
@@ -915,7 +915,7 @@ class Harness:
                  threads=1, cid_stride=1, xfer_period=0, xfer_mod=1, ext_apply=False,
                  ext_inputs=False, snapshot_entries=0, compaction_overhead=0,
                  ext_commit=False, membership=False, cc_period=0, cc_mod=1,
-                 max_inmem_log_size=0):
+                 max_inmem_log_size=0, n_voters=0):
         c = OrcHarnessConfig(
             n_groups=n_groups, n_replicas=n_replicas, check_quorum=int(check_quorum),
             cid_base=cid_base, election_rtt=election_rtt, heartbeat_rtt=heartbeat_rtt,
@@ -927,7 +927,7 @@ class Harness:
             xfer_period=xfer_period, xfer_mod=xfer_mod, ext_apply=int(ext_apply),
             snapshot_entries=snapshot_entries, compaction_overhead=compaction_overhead,
             ext_commit=int(ext_commit), membership=int(membership), cc_period=cc_period,
-            cc_mod=cc_mod, max_inmem_log_size=max_inmem_log_size)
+            cc_mod=cc_mod, max_inmem_log_size=max_inmem_log_size, n_voters=n_voters)
         self.n_groups, self.n_replicas = n_groups, n_replicas
         self.h = lib().orc_harness_create(C.byref(c))
         if not self.h:

@@ -48,7 +48,7 @@ typedef struct {
   uint64_t cid_stride;
   uint32_t xfer_period, xfer_mod, ext_apply, snapshot_entries;
   uint32_t compaction_overhead, ext_commit;
-  uint32_t membership, cc_period, cc_mod, pad4;
+  uint32_t membership, cc_period, cc_mod, n_voters;
   uint64_t max_inmem_log_size;
 } orc_harness_config;
 
@@ -874,6 +874,7 @@ void* orc_harness_create(const orc_harness_config* c) {
   h.membership = c->membership;
   h.cc_period = c->cc_period;
   h.cc_mod = c->cc_mod ? c->cc_mod : 1;
+  h.n_voters = c->n_voters;
   h.max_inmem_log_size = c->max_inmem_log_size;
   return harness_create(h);
   GUARD_END(nullptr)

@@ -232,7 +232,8 @@ void* soa_create(const rbe_config* cfg) {
   C.snapshot_entries = cfg->snapshot_entries;
   C.compaction_overhead = cfg->compaction_overhead;
   C.rl_max = cfg->max_inmem_log_size;
-  if (C.n != 1 && C.n != 3 && C.n != 5) {
+  C.n_voters = cfg->n_voters ? cfg->n_voters : C.n;
+  if (!valid_n(C.n) || C.n_voters > C.n || (C.n_voters < C.n && !C.membership)) {
     delete e;
     return nullptr;
   }
@@ -276,9 +277,9 @@ void* soa_create(const rbe_config* cfg) {
     e->hin.heap.low_fn = [e](u64* lo) -> int {  // k_heap_low, group by group
       u64 m = ~0ull;
       for (u64 g = 0; g < e->C.n_groups; g++) {
-        u64 x = e->C.n == 1   ? heap_low_group<1>(e->P, e->C, g, e->round)
-                : e->C.n == 3 ? heap_low_group<3>(e->P, e->C, g, e->round)
-                              : heap_low_group<5>(e->P, e->C, g, e->round);
+        u64 x = with_n(e->C.n, [&](auto NN) {
+          return heap_low_group<decltype(NN)::value>(e->P, e->C, g, e->round);
+        });
         if (x < m) m = x;
       }
       *lo = m;
@@ -287,9 +288,7 @@ void* soa_create(const rbe_config* cfg) {
   }
   P.counters = nullptr;
   for (u64 r = 0; r < R; r++) {
-    if (N == 1) launch_replica<1>(P, C, r);
-    else if (N == 3) launch_replica<3>(P, C, r);
-    else launch_replica<5>(P, C, r);
+    with_n(N, [&](auto NN) { launch_replica<decltype(NN)::value>(P, C, r); });
   }
   return e;
 }
@@ -365,9 +364,7 @@ uint64_t soa_sleeping_groups(void* h) {  // groups asleep after the last round (
 void soa_run(void* h, uint32_t rounds) {
   SoaEngine* e = (SoaEngine*)h;
   for (u32 i = 0; i < rounds; i++) {
-    if (e->C.n == 1) run_round<1>(e);
-    else if (e->C.n == 3) run_round<3>(e);
-    else run_round<5>(e);
+    with_n(e->C.n, [&](auto NN) { run_round<decltype(NN)::value>(e); });
   }
 }
 
@@ -375,9 +372,7 @@ void soa_run(void* h, uint32_t rounds) {
 void soa_step_ex(void* h, uint32_t flags) {
   SoaEngine* e = (SoaEngine*)h;
   const bool tick = (flags & 1u) == 0;
-  if (e->C.n == 1) run_round<1>(e, tick);
-  else if (e->C.n == 3) run_round<3>(e, tick);
-  else run_round<5>(e, tick);
+  with_n(e->C.n, [&](auto NN) { run_round<decltype(NN)::value>(e, tick); });
 }
 
 // rbe_push_* / rbe_request_leader_transfer / rbe_report_* / rbe_notify_applied
@@ -413,18 +408,12 @@ int soa_launch(void* h, uint64_t n, const uint64_t* replica, const rbe_launch_st
     const rbe_launch_state& x = st[i];
     const u64* t = terms.data() + off;
     const Body* b = bodies.data() + off;
-    if (e->C.n == 1)
-      relaunch_replica<1>(e->P, e->C, replica[i], x.term, x.vote, x.commit, x.last_index,
-                          x.n_entries, t, b, ppar, e->tclk, x.marker, x.marker_term,
-                          x.snapshot_index, x.snapshot_term, (u8)x.removed);
-    else if (e->C.n == 3)
-      relaunch_replica<3>(e->P, e->C, replica[i], x.term, x.vote, x.commit, x.last_index,
-                          x.n_entries, t, b, ppar, e->tclk, x.marker, x.marker_term,
-                          x.snapshot_index, x.snapshot_term, (u8)x.removed);
-    else
-      relaunch_replica<5>(e->P, e->C, replica[i], x.term, x.vote, x.commit, x.last_index,
-                          x.n_entries, t, b, ppar, e->tclk, x.marker, x.marker_term,
-                          x.snapshot_index, x.snapshot_term, (u8)x.removed);
+    with_n(e->C.n, [&](auto NN) {
+      relaunch_replica<decltype(NN)::value>(e->P, e->C, replica[i], x.term, x.vote, x.commit,
+                                            x.last_index, x.n_entries, t, b, ppar, e->tclk,
+                                            x.marker, x.marker_term, x.snapshot_index,
+                                            x.snapshot_term, (u8)x.removed);
+    });
     e->P.gwake[replica[i] / e->C.n] = GW_AWAKE;
     off += x.n_entries;
   }
@@ -547,18 +536,22 @@ int64_t soa_wire_encode(void* h, uint64_t deployment_id, uint32_t bin_ver, uint3
       for (u64 g = g0; g < g1; g++) {
         u32 cm = 0, ci = 0, bad = 0;
         u32 b = 0;
-        if (N == 3 ? !wire_cell_sent<3>(C, dst_rank, g, k, d) : !wire_cell_sent<5>(C, dst_rank, g, k, d))
+        if (!with_n(N, [&](auto NN) { return wire_cell_sent<decltype(NN)::value>(C, dst_rank, g, k, d); }))
           continue;
         const u8* hp = e->heap.data();
         const u64 hh = e->hin.heap.flushed;
-        if (N == 3) b = wire_cell<3>(e->P, C, hp, hh, g, k, d, e->round, nullptr, &cm, &ci, &bad);
-        else b = wire_cell<5>(e->P, C, hp, hh, g, k, d, e->round, nullptr, &cm, &ci, &bad);
+        b = with_n(N, [&](auto NN) {
+          return wire_cell<decltype(NN)::value>(e->P, C, hp, hh, g, k, d, e->round, nullptr, &cm,
+                                                &ci, &bad);
+        });
         if (bad) return -2;  // rbe_wire_encode: RBE_E_STATE
         if (!cm) continue;
         const size_t at = pay.size();
         pay.resize(at + b);
-        if (N == 3) wire_cell<3>(e->P, C, hp, hh, g, k, d, e->round, pay.data() + at, &cm, &ci, &bad);
-        else wire_cell<5>(e->P, C, hp, hh, g, k, d, e->round, pay.data() + at, &cm, &ci, &bad);
+        with_n(N, [&](auto NN) {
+          return wire_cell<decltype(NN)::value>(e->P, C, hp, hh, g, k, d, e->round,
+                                                pay.data() + at, &cm, &ci, &bad);
+        });
         nm += cm;
       }
       if (!nm) continue;
@@ -718,9 +711,9 @@ extern "C" int soa_wire_ingest(void* h, const uint8_t* data, uint64_t bytes, uin
   memset(stats6, 0, 6 * sizeof(u64));
   if (e->round == 0) return RBE_E_INVALID;
   if (e->C.rep_world <= 1) return RBE_E_STATE;
-  if (e->C.n == 3) return soa_ingest_t<3>(e, data, bytes, stats6);
-  if (e->C.n == 5) return soa_ingest_t<5>(e, data, bytes, stats6);
-  return soa_ingest_t<1>(e, data, bytes, stats6);
+  return with_n(e->C.n, [&](auto NN) {
+    return soa_ingest_t<decltype(NN)::value>(e, data, bytes, stats6);
+  });
 }
 
 extern "C" {
@@ -735,8 +728,9 @@ int soa_iso_leaders(void* h, uint8_t* out, uint32_t* epoch) {
   for (u64 g = 0; g < C.n_groups; g++) {
     const u64 gg = group_global(C, g);  // exchanged by global group
     if (gg >= C.n_groups_glob) continue;
-    out[gg] = (u8)(C.n == 5 ? iso_leader_bits<5>(e->P, C, g)
-                            : C.n == 3 ? iso_leader_bits<3>(e->P, C, g) : iso_leader_bits<1>(e->P, C, g));
+    out[gg] = (u8)with_n(C.n, [&](auto NN) {
+      return (u32)iso_leader_bits<decltype(NN)::value>(e->P, C, g);
+    });
   }
   return RBE_OK;
 }
@@ -900,9 +894,7 @@ static void soa_xchg_pack_fixed_t(SoaEngine* e, uint8_t* buf, const uint64_t* ca
 }
 extern "C" void soa_xchg_pack_fixed(void* h, uint8_t* buf, const uint64_t* cap) {
   SoaEngine* e = (SoaEngine*)h;
-  if (e->C.n == 3) soa_xchg_pack_fixed_t<3>(e, buf, cap);
-  else if (e->C.n == 5) soa_xchg_pack_fixed_t<5>(e, buf, cap);
-  else soa_xchg_pack_fixed_t<1>(e, buf, cap);
+  with_n(e->C.n, [&](auto NN) { soa_xchg_pack_fixed_t<decltype(NN)::value>(e, buf, cap); });
 }
 extern "C" void soa_xchg_unpack_fixed(void* h, const uint8_t* recv, const uint64_t* cap) {
   SoaEngine* e = (SoaEngine*)h;
@@ -920,16 +912,17 @@ extern "C" uint32_t soa_xchg_status(void* h) { return ((SoaEngine*)h)->xflag; }
 extern "C" int soa_xchg_pack(void* h, uint8_t* buf, const uint64_t* cap, uint32_t* counts) {
   SoaEngine* e = (SoaEngine*)h;
   if (e->C.heap_bytes) return RBE_E_STATE;  // as rbe_xchg_pack: heap positions are local
-  if (e->C.n == 3) return soa_xchg_pack_t<3>(e, buf, cap, counts);
-  if (e->C.n == 5) return soa_xchg_pack_t<5>(e, buf, cap, counts);
-  return soa_xchg_pack_t<1>(e, buf, cap, counts);
+  return with_n(e->C.n, [&](auto NN) {
+    return soa_xchg_pack_t<decltype(NN)::value>(e, buf, cap, counts);
+  });
 }
 extern "C" void soa_xchg_unpack(void* h, const void* c, uint64_t nc, const void* m, uint64_t nm,
                                 const void* x, uint64_t ne) {
   SoaEngine* e = (SoaEngine*)h;
-  if (e->C.n == 3) soa_xchg_unpack_t<3>(e, (const XCnt*)c, nc, (const XMsg*)m, nm, (const XEnt*)x, ne);
-  else if (e->C.n == 5) soa_xchg_unpack_t<5>(e, (const XCnt*)c, nc, (const XMsg*)m, nm, (const XEnt*)x, ne);
-  else soa_xchg_unpack_t<1>(e, (const XCnt*)c, nc, (const XMsg*)m, nm, (const XEnt*)x, ne);
+  with_n(e->C.n, [&](auto NN) {
+    soa_xchg_unpack_t<decltype(NN)::value>(e, (const XCnt*)c, nc, (const XMsg*)m, nm,
+                                           (const XEnt*)x, ne);
+  });
 }
 
 // transport boundary on the host build (rbe_get_outbox / rbe_push_messages)
@@ -947,14 +940,11 @@ extern "C" int soa_get_outbox(void* h, uint64_t replica, rbe_message* out, uint3
   const Ent* arena = e->P.arena[par] + replica * e->C.ecap;
   const u32 rd = e->round;
   auto hr = [e](u64 pos, u64 off, u64 len, u8* dst) { return soa_read_heap(e, pos, off, len, dst); };
-  if (N == 3)
-    return outbox_messages<3>(e->C, g, k, row, rd, lst, arena, out, cap, ents, ent_cap, n_out,
-                              n_ents, cmd, cmd_cap, cmd_bytes, hr);
-  if (N == 5)
-    return outbox_messages<5>(e->C, g, k, row, rd, lst, arena, out, cap, ents, ent_cap, n_out,
-                              n_ents, cmd, cmd_cap, cmd_bytes, hr);
-  return outbox_messages<1>(e->C, g, k, row, rd, lst, arena, out, cap, ents, ent_cap, n_out,
-                            n_ents, cmd, cmd_cap, cmd_bytes, hr);
+  return with_n(N, [&](auto NN) {
+    return outbox_messages<decltype(NN)::value>(e->C, g, k, row, rd, lst, arena, out, cap, ents,
+                                                ent_cap, n_out, n_ents, cmd, cmd_cap, cmd_bytes,
+                                                hr);
+  });
 }
 template <int N>
 static int soa_push_t(SoaEngine* e, uint64_t n, const uint64_t* group, const rbe_message* msgs,
@@ -974,9 +964,9 @@ extern "C" int soa_push_messages(void* h, uint64_t n, const uint64_t* group,
   SoaEngine* e = (SoaEngine*)h;
   if (e->round == 0) return RBE_E_INVALID;
   if (e->C.rep_world <= 1) return RBE_E_STATE;
-  if (e->C.n == 3) return soa_push_t<3>(e, n, group, msgs, ents, cmd);
-  if (e->C.n == 5) return soa_push_t<5>(e, n, group, msgs, ents, cmd);
-  return soa_push_t<1>(e, n, group, msgs, ents, cmd);
+  return with_n(e->C.n, [&](auto NN) {
+    return soa_push_t<decltype(NN)::value>(e, n, group, msgs, ents, cmd);
+  });
 }
 
 // Group-range snapshots in the engine's byte layout (rbe_export_groups /
