@@ -94,6 +94,7 @@ __global__ __launch_bounds__(kBlock) void k_ext_scatter(Planes P, u32 nrep, cons
 // ---- batched Updates (rbe_collect_updates): flag → scan → write
 __device__ __forceinline__ bool upd_of(const Planes& P, u64 r, u32 round, rbe_update* u) {
   update_view(P.upd[r], P.core[r], P.hot[r], round, *u);
+  update_ids(*u, P.node_ids, P.ids_n, P.node_ids ? r / P.ids_n : 0);
   return (u->flags & RBE_UF_HAS_UPDATE) != 0;
 }
 __global__ __launch_bounds__(kBlock) void k_upd_count(Planes P, u64 first, u64 count, u32 round,
@@ -201,19 +202,7 @@ __global__ __launch_bounds__(kBlock) void k_out_write(Planes P, Params C, u64 fi
     for (u32 j = 0; j < na + nb; j++, at++) {
       const Msg m = j < na ? lst[j] : lst[C.maxm - 1u - (j - na)];
       rbe_message o;
-      o.type = m.type;
-      o.reject = m.reject;
-      o.to = m.to;
-      o.from = m.from;
-      o.cluster_id = cid_of(C, g);
-      o.term = m.term;
-      o.log_term = m.log_term;
-      o.log_index = m.log_index;
-      o.commit = m.commit;
-      o.hint = m.hint;
-      o.hint_high = m.hint_high;
-      o.n_entries = m.n_ent;
-      o.reserved = msg_reserved(m);
+      msg_out(m, cid_of(C, g), P.node_ids, N, g, o);
       om[at] = o;
     }
   }
@@ -793,6 +782,8 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   P.rem_snap = C.snapshot_entries ? (u64*)ptrs[21] : nullptr;
   P.imark = (C.ext_commit || C.rl_max) ? (u64*)ptrs[22] : nullptr;
   P.rl = C.rl_max ? (RlSt*)ptrs[23] : nullptr;
+  P.node_ids = nullptr;  // slot s is node s + 1 until rbe_set_node_ids
+  P.ids_n = C.n;
   HIP_IGNORE(hipMemsetAsync(P.gwake, GW_AWAKE, C.n_groups, e->stream));  // every group starts awake
   e->hin.init(C.n_rep, C.n, C.in_cap, C.heap_bytes);
   e->hin.owner = C.rep_world > 1 ? &e->C : nullptr;
@@ -1188,9 +1179,12 @@ int rbe_report_snapshot_status(rbe_engine* e, uint64_t n, const uint64_t* replic
   return e->hin.report_snapshot_status(n, replica, node_id, reject);
 }
 
-int rbe_launch(rbe_engine* e, uint64_t n, const uint64_t* replica, const rbe_launch_state* st,
+int rbe_launch(rbe_engine* e, uint64_t n, const uint64_t* replica, const rbe_launch_state* st_ids,
                const rbe_entry* ents, const uint8_t* cmd) {
   if (!e) return RBE_E_INVALID;
+  std::vector<rbe_launch_state> stv;  // votes as internal ids
+  if (!e->hin.map_votes(n, replica, st_ids, stv)) return RBE_E_INVALID;
+  const rbe_launch_state* st = stv.data();
   if (n && replica) {  // one replica at most once
     std::vector<u64> v(replica, replica + n);
     std::sort(v.begin(), v.end());
@@ -1275,6 +1269,29 @@ int rbe_compact(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint64
   if (!e) return RBE_E_INVALID;
   if (!e->C.snapshot_entries || !e->C.ext_apply) return RBE_E_STATE;
   return e->hin.snapshot_op(n, replica, SR_COMPACT, to, nullptr, nullptr, false);
+}
+
+int rbe_set_node_ids(rbe_engine* e, uint64_t first_group, uint64_t count, const uint64_t* ids) {
+  if (!e) return RBE_E_INVALID;
+  if (e->round != 0) return RBE_E_STATE;  // messages in flight name slots by node id
+  int rc = e->hin.set_node_ids(e->C.n_groups, first_group, count, ids);
+  if (rc || count == 0) return rc;
+  HIP_OK(hipSetDevice(e->device));
+  const u64 bytes = e->hin.ids.size() * sizeof(u64);
+  if (!e->P.node_ids) {
+    u64* d = nullptr;
+    if (hipMalloc(&d, bytes) != hipSuccess) return RBE_E_NOMEM;
+    e->allocs.push_back(d);
+    e->P.node_ids = d;
+  }
+  HIP_OK(hipMemcpyAsync((void*)e->P.node_ids, e->hin.ids.data(), bytes, hipMemcpyHostToDevice,
+                        e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  if (e->graph) {  // kernels take the planes by value: a captured graph holds the old ones
+    HIP_OK(hipGraphExecDestroy(e->graph));
+    e->graph = nullptr;
+  }
+  return RBE_OK;
 }
 
 int rbe_restore_remotes(rbe_engine* e, uint64_t n, const uint64_t* replica,
@@ -1445,7 +1462,7 @@ int rbe_get_outbox(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t c
   const int rc = dispatch_n(N, [&](auto NN) {
     constexpr int NC = decltype(NN)::value;
     return outbox_messages<NC>(e->C, g, k, row, e->round, lst.data(), arena.data(), out, cap, ents,
-                               ent_cap, n_out, n_ents, cmd, cmd_cap, cmd_bytes, rd);
+                               ent_cap, n_out, n_ents, cmd, cmd_cap, cmd_bytes, e->hin.id_table(), rd);
   });
   HIP_OK(hipStreamSynchronize(e->stream));  // heap reads
   return rc;
@@ -1462,7 +1479,7 @@ int rbe_push_messages(rbe_engine* e, uint64_t n, const uint64_t* group, const rb
   int rc = dispatch_n(e->C.n, [&](auto NN) {
     constexpr int N = decltype(NN)::value;
     return messages_to_records<N>(e->C, e->hin.heap, e->round, n, group, msgs, ents, cmd, c, m,
-                                  x);
+                                  x, e->hin.id_table());
   });
   if (rc) return rc;
   const size_t bytes = c.size() * sizeof(XCnt) + m.size() * sizeof(XMsg) + x.size() * sizeof(XEnt);
@@ -1548,8 +1565,8 @@ int rbe_get_views(rbe_engine* e, uint64_t first, uint64_t count, rbe_replica_vie
     const Hot h = materialize_hot(hot[i], e->C, e->tclk);
     const Core& c = core[i];
     v.term = c.term;
-    v.vote = c.vote;
-    v.leader_id = c.leader;
+    v.vote = ext_id(e->hin.id_table(), N, (first + i) / N, c.vote);
+    v.leader_id = ext_id(e->hin.id_table(), N, (first + i) / N, c.leader);
     v.committed = c.committed;
     v.last_index = c.last_index;
     v.processed = c.processed;
@@ -1592,7 +1609,10 @@ int rbe_get_updates(rbe_engine* e, uint64_t first, uint64_t count, rbe_update* o
       d2h(e, hot.data(), e->P.hot + first, count))
     return RBE_E_HIP;
   HIP_OK(hipStreamSynchronize(e->stream));
-  for (u64 i = 0; i < count; i++) update_view(upd[i], core[i], hot[i], e->round, out[i]);
+  for (u64 i = 0; i < count; i++) {
+    update_view(upd[i], core[i], hot[i], e->round, out[i]);
+    update_ids(out[i], e->hin.id_table(), e->C.n, (first + i) / e->C.n);
+  }
   return RBE_OK;
 }
 
@@ -1660,23 +1680,7 @@ int rbe_get_messages(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t
     const u32 pc = row_word(row, d, e->round), na = pc & 0x7F, nb = (pc >> 7) & 0x7F;
     for (u32 i = 0; i < na + nb; i++) {
       const Msg& m = i < na ? lst[d * e->C.maxm + i] : lst[d * e->C.maxm + e->C.maxm - 1 - (i - na)];
-      if (n < cap && out) {
-        rbe_message& o = out[n];
-        memset(&o, 0, sizeof(o));
-        o.type = m.type;
-        o.reject = m.reject;
-        o.to = m.to;
-        o.from = m.from;
-        o.cluster_id = cid_of(e->C, g);
-        o.term = m.term;
-        o.log_term = m.log_term;
-        o.log_index = m.log_index;
-        o.commit = m.commit;
-        o.hint = m.hint;
-        o.hint_high = m.hint_high;
-        o.n_entries = m.n_ent;
-        o.reserved = msg_reserved(m);
-      }
+      if (n < cap && out) msg_out(m, cid_of(e->C, g), e->hin.id_table(), N, g, out[n]);
       n++;
     }
   }
@@ -2230,8 +2234,8 @@ int rbe_wire_ingest(rbe_engine* e, const void* data, uint64_t bytes, rbe_wire_in
   rc = dispatch_n(C.n, [&](auto NN) {
     constexpr int N = decltype(NN)::value;
     hipLaunchKernelGGL(k_ing_key<N>, dim3((unsigned)nbk), dim3(256), 0, e->stream, C,
-                       (u64)C.heap_bytes, (const rbe_message*)o.msgs, (const rbe_entry*)o.ents,
-                       (const u64*)o.ent0, tm, key, idx, hb, err, ndrop);
+                       (u64)C.heap_bytes, (rbe_message*)o.msgs, (const rbe_entry*)o.ents,
+                       (const u64*)o.ent0, tm, key, idx, hb, err, ndrop, e->P.node_ids);
     return RBE_OK;
   });
   if (rc) return rc;

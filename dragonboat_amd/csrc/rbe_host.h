@@ -13,6 +13,7 @@
 // 1069-1075): a second one is RBE_E_STATE instead of silently replacing the
 // first.
 #pragma once
+#include <algorithm>
 #include <cstring>
 #include <functional>
 #include <type_traits>
@@ -254,6 +255,29 @@ RBE_HD void update_view(const Upd& d, const Core& c, const Hot& h, u32 round, rb
   u.role = h.role;
   u.leader_id = c.leader;
 }
+// An engine message in raftpb form (Update.Messages): its node ids (From, To,
+// and the Hint of RequestVote / LeaderTransfer) from the internal ids of local
+// group g, whose cluster id is `cid`
+RBE_HD void msg_out(const Msg& m, u64 cid, const u64* ids, u32 n, u64 g, rbe_message& o) {
+  o.type = m.type;
+  o.reject = m.reject;
+  o.to = ext_id(ids, n, g, m.to);
+  o.from = ext_id(ids, n, g, m.from);
+  o.cluster_id = cid;
+  o.term = m.term;
+  o.log_term = m.log_term;
+  o.log_index = m.log_index;
+  o.commit = m.commit;
+  o.hint = hint_is_node(m.type) ? ext_id(ids, n, g, m.hint) : m.hint;
+  o.hint_high = m.hint_high;
+  o.n_entries = m.n_ent;
+  o.reserved = msg_reserved(m);
+}
+// an rbe_update's node ids (vote, leader) from the internal ids of group g
+RBE_HD void update_ids(rbe_update& u, const u64* ids, u32 n, u64 g) {
+  u.vote = ext_id(ids, n, g, u.vote);
+  u.leader_id = ext_id(ids, n, g, u.leader_id);
+}
 // getUpdateCommit (peer.go:410-427) of an rbe_update: `applied` is the
 // applied index the step ran with (GetUpdate's lastApplied), `term_of(i)` the
 // term of log entry i (the last EntriesToSave entry)
@@ -444,6 +468,52 @@ struct HostInputs {
   const Params* owner = nullptr;  // replica-per-GPU mode: only owned replicas take input
 
   HostHeap heap;             // payload heap positions and staged bytes
+  // [n_groups * n] node ids of the groups' slots (rbe_set_node_ids), empty =
+  // slot s is node s + 1
+  std::vector<u64> ids;
+
+  const u64* id_table() const { return ids.empty() ? nullptr : ids.data(); }
+  // rbe_set_node_ids: groups [first, first + count), n ids each, non-zero and
+  // ascending within a group (the canonical node order is the slot order)
+  int set_node_ids(u64 n_groups, u64 first, u64 count, const u64* v) {
+    if (first > n_groups || count > n_groups - first || (count && !v)) return RBE_E_INVALID;
+    for (u64 i = 0; i < count; i++)
+      for (u32 s = 0; s < n; s++)
+        if (v[i * n + s] == 0 || (s && v[i * n + s] <= v[i * n + s - 1])) return RBE_E_INVALID;
+    if (ids.empty()) {
+      ids.resize(n_groups * n);
+      for (u64 i = 0; i < n_groups * n; i++) ids[i] = i % n + 1;
+    }
+    std::copy(v, v + count * n, ids.begin() + first * n);
+    return RBE_OK;
+  }
+  // node id → internal id (slot + 1) in replica r's group; 0 when no slot has it
+  u64 in_id(u64 r, u64 id) const {
+    if (r >= n_rep || id == 0) return 0;
+    if (ids.empty()) return id <= n ? id : 0;
+    const u64* row = &ids[(r / n) * n];
+    for (u32 s = 0; s < n; s++)
+      if (row[s] == id) return s + 1;
+    return 0;
+  }
+  // launch states with their votes (node ids) as internal ids; false when a
+  // vote is not a slot of the replica's group (or the replica not a replica)
+  bool map_votes(u64 cnt, const u64* replica, const rbe_launch_state* st,
+                 std::vector<rbe_launch_state>& out) const {
+    if (cnt && (!replica || !st)) return false;
+    out.assign(st, st + cnt);
+    for (u64 i = 0; i < cnt; i++)
+      if (out[i].vote && (out[i].vote = in_id(replica[i], st[i].vote)) == 0) return false;
+    return true;
+  }
+  // a batch of node ids of replica[i]'s groups; false when one is not a slot
+  bool map_ids(u64 cnt, const u64* replica, const u64* node, std::vector<u64>& out) const {
+    if (cnt && (!replica || !node)) return false;
+    out.resize(cnt);
+    for (u64 i = 0; i < cnt; i++)
+      if ((out[i] = in_id(replica[i], node[i])) == 0) return false;
+    return true;
+  }
 
   void init(u64 n_rep_, u32 n_, u32 in_cap_, u64 heap_bytes = 0) {
     n_rep = n_rep_;
@@ -573,10 +643,10 @@ struct HostInputs {
     }
     return RBE_OK;
   }
-  int request_leader_transfer(u64 cnt, const u64* replica, const u64* target) {
-    if (cnt && !target) return RBE_E_INVALID;
-    for (u64 i = 0; i < cnt; i++)
-      if (target[i] < 1 || target[i] > n) return RBE_E_INVALID;  // NoNode panics, raft.go:1715
+  int request_leader_transfer(u64 cnt, const u64* replica, const u64* target_id) {
+    std::vector<u64> tv;  // NoNode panics (raft.go:1715), as does a node not in the group
+    if (!map_ids(cnt, replica, target_id, tv)) return RBE_E_INVALID;
+    const u64* target = tv.data();
     int rc = check_replicas(cnt, replica, EXT_XFER);
     if (rc) return rc;
     for (u64 i = 0; i < cnt; i++) {
@@ -586,10 +656,10 @@ struct HostInputs {
     }
     return RBE_OK;
   }
-  int report_unreachable(u64 cnt, const u64* replica, const u64* node) {
-    if (cnt && !node) return RBE_E_INVALID;
-    for (u64 i = 0; i < cnt; i++)
-      if (node[i] < 1 || node[i] > n) return RBE_E_INVALID;
+  int report_unreachable(u64 cnt, const u64* replica, const u64* node_id) {
+    std::vector<u64> nv;
+    if (!map_ids(cnt, replica, node_id, nv)) return RBE_E_INVALID;
+    const u64* node = nv.data();
     int rc = check_replicas(cnt, replica, 0);
     if (rc) return rc;
     for (u64 i = 0; i < cnt; i++) {
@@ -599,10 +669,10 @@ struct HostInputs {
     }
     return RBE_OK;
   }
-  int report_snapshot_status(u64 cnt, const u64* replica, const u64* node, const u8* reject) {
-    if (cnt && (!node || !reject)) return RBE_E_INVALID;
-    for (u64 i = 0; i < cnt; i++)
-      if (node[i] < 1 || node[i] > n) return RBE_E_INVALID;
+  int report_snapshot_status(u64 cnt, const u64* replica, const u64* node_id, const u8* reject) {
+    std::vector<u64> nv;
+    if ((cnt && !reject) || !map_ids(cnt, replica, node_id, nv)) return RBE_E_INVALID;
+    const u64* node = nv.data();
     int rc = check_replicas(cnt, replica, 0);
     if (rc) return rc;
     for (u64 i = 0; i < cnt; i++) {
@@ -615,10 +685,12 @@ struct HostInputs {
     return RBE_OK;
   }
   // rbe_propose_config_change / rbe_apply_config_change / rbe_reject_config_change
-  int propose_config_change(u64 cnt, const u64* replica, const u32* type, const u64* node) {
-    if (cnt && (!type || !node)) return RBE_E_INVALID;
+  int propose_config_change(u64 cnt, const u64* replica, const u32* type, const u64* node_id) {
+    std::vector<u64> nv;
+    if ((cnt && !type) || !map_ids(cnt, replica, node_id, nv)) return RBE_E_INVALID;
+    const u64* node = nv.data();
     for (u64 i = 0; i < cnt; i++)
-      if (type[i] > CC_AddWitness || node[i] < 1 || node[i] > n) return RBE_E_INVALID;
+      if (type[i] > CC_AddWitness) return RBE_E_INVALID;
     int rc = check_replicas(cnt, replica, EXT_CC_PROPOSE);
     if (rc) return rc;
     for (u64 i = 0; i < cnt; i++) {
@@ -628,11 +700,15 @@ struct HostInputs {
     }
     return RBE_OK;
   }
-  int apply_config_change(u64 cnt, const u64* replica, const u64* node, const u32* type,
+  int apply_config_change(u64 cnt, const u64* replica, const u64* node_id, const u32* type,
                           bool reject) {
-    if (cnt && !reject && (!type || !node)) return RBE_E_INVALID;
-    for (u64 i = 0; i < cnt && !reject; i++)
-      if (type[i] > CC_AddWitness || node[i] > n) return RBE_E_INVALID;
+    if (cnt && !reject && (!type || !node_id)) return RBE_E_INVALID;
+    std::vector<u64> nv(reject ? 0 : cnt);
+    for (u64 i = 0; i < cnt && !reject; i++) {  // node id 0 = NoNode
+      nv[i] = node_id[i] ? in_id(replica ? replica[i] : ~0ull, node_id[i]) : 0;
+      if (type[i] > CC_AddWitness || (node_id[i] && !nv[i])) return RBE_E_INVALID;
+    }
+    const u64* node = nv.data();
     int rc = check_replicas(cnt, replica, EXT_CC_APPLY);
     if (rc) return rc;
     for (u64 i = 0; i < cnt; i++) {
@@ -645,16 +721,17 @@ struct HostInputs {
   }
   // rbe_restore_remotes: replica[i]'s snapshot lists n_voters[i] voters, their
   // node ids next in `ids`; staged as the removed mask of the group's slots
-  int restore_remotes(u64 cnt, const u64* replica, const u32* n_voters, const u64* ids) {
+  int restore_remotes(u64 cnt, const u64* replica, const u32* n_voters, const u64* vids) {
     if (cnt && !n_voters) return RBE_E_INVALID;
     std::vector<u64> rem(cnt);
     u64 j = 0;
     for (u64 i = 0; i < cnt; i++) {
       u32 listed = 0;
-      if (n_voters[i] && !ids) return RBE_E_INVALID;
+      if (n_voters[i] && !vids) return RBE_E_INVALID;
       for (u32 q = 0; q < n_voters[i]; q++, j++) {
-        if (ids[j] < 1 || ids[j] > n || ((listed >> (ids[j] - 1)) & 1u)) return RBE_E_INVALID;
-        listed |= 1u << (ids[j] - 1);
+        const u64 x = in_id(replica ? replica[i] : ~0ull, vids[j]);
+        if (!x || ((listed >> (x - 1)) & 1u)) return RBE_E_INVALID;
+        listed |= 1u << (x - 1);
       }
       rem[i] = ((1u << n) - 1u) & ~listed;
     }

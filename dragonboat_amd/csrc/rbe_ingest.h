@@ -47,6 +47,22 @@ RBE_HD bool wire_cell_sent(const Params& C, int dst_rank, u64 g, u32 k, u32 d) {
 // member of the group, as Peer.Handle drops it): past every list key.
 RBE_HD u64 ing_drop_key(const Params& C) { return C.n_rep * (u64)C.n; }
 
+// A decoded message's node ids (From, To, a RequestVote's / LeaderTransfer's
+// Hint) as internal ids of the group its ClusterId names (rbe_set_node_ids;
+// 0 = none of the group's slots, which ingest_check then drops or refuses)
+template <int N>
+RBE_HD void ingest_ids(const Params& C, const u64* ids, rbe_message& m) {
+  if (!ids) return;
+  const u64 cid = m.cluster_id, st = C.cid_stride ? C.cid_stride : 1;
+  u64 g = 0;
+  if (cid < C.cid_base || (cid - C.cid_base) % st != 0 ||
+      !group_local(C, (cid - C.cid_base) / st, &g))
+    return;  // refused by ingest_check
+  m.from = int_id<N>(ids, g, m.from);
+  m.to = int_id<N>(ids, g, m.to);
+  if (hint_is_node(m.type)) m.hint = int_id<N>(ids, g, m.hint);
+}
+
 // Peer.Handle's filter and rbe_push_messages's checks for decoded message m
 // (its entries at `ents`): the list key (g * N + from - 1) * N + to - 1, or
 // the drop key; *err gets ING_INVALID / ING_NOMEM, *heap the payload-heap

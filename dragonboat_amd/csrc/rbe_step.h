@@ -383,6 +383,27 @@ RBE_HD bool is_response_message(u32 t) {
          t == M_ReadIndexResp || t == M_Unreachable || t == M_SnapshotStatus ||
          t == M_LeaderTransfer;
 }
+// The node id of internal id x (slot + 1; 0 = NoNode) of local group g: the
+// group's node-id table (Planes::node_ids on the device, the host copy in host
+// code; rbe_set_node_ids) or, without one, x itself
+RBE_HD u64 ext_id(const u64* ids, u32 n, u64 g, u64 x) {
+  return (ids && x >= 1 && x <= n) ? ids[g * n + x - 1] : x;
+}
+// message fields that hold a node id besides From/To: a RequestVote's Hint
+// (the leader-transfer candidate, raft.go:1098-1102) and a LeaderTransfer's
+// (its target, raft.go:1712-1734)
+RBE_HD bool hint_is_node(u32 type) { return type == M_RequestVote || type == M_LeaderTransfer; }
+// The internal id (slot + 1) of node id `id` in local group g, 0 when none of
+// the group's slots has it (0 = NoNode stays 0); without a table the id itself
+template <int N>
+RBE_HD u64 int_id(const u64* ids, u64 g, u64 id) {
+  if (!ids) return id;
+  if (id == 0) return 0;
+  for (u32 s = 0; s < (u32)N; s++)
+    if (ids[g * N + s] == id) return s + 1;
+  return 0;
+}
+
 // rbe_message.reserved of an engine message: an InstallSnapshot's snapshot
 // membership (Snapshot.Membership as the removed mask, Msg::pad0), else 0
 RBE_HD u32 msg_reserved(const Msg& m) { return m.type == M_InstallSnapshot ? (u32)m.pad0 : 0u; }

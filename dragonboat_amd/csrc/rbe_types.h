@@ -398,6 +398,11 @@ struct Planes {
                          // last upload; a record at p < *heap_head - heap_bytes has been
                          // overwritten by a later lap (null without a heap)
   u64* counters;      // [C_NUM]
+  // [n_groups * N] the node id of each group's slots (rbe_set_node_ids), or
+  // null: slot s is node s + 1.  Only the boundary's converters read it: the
+  // protocol state inside the engine names nodes by slot + 1
+  const u64* node_ids;
+  u32 ids_n;          // slots per group (Params::n), for indexing node_ids in kernels without Params
 };
 
 }  // namespace rbe

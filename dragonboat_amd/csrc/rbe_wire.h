@@ -124,7 +124,7 @@ RBE_HD u32 wire_empty_snap_put(u8* o) {
 // whose heap record a later lap overwrote (position below heap_head - cap)
 // counts in *n_bad and is encoded from whatever the heap holds: the caller
 // refuses the whole encode then.
-RBE_HD u32 wire_message(const Msg& m, u32 type, u32 to, u32 from, u64 cid, const Ent* ents,
+RBE_HD u32 wire_message(const Msg& m, u32 type, u64 to, u64 from, u64 cid, const Ent* ents,
                         const u8* heap, u64 heap_cap, u64 heap_head, u8* out, u32* n_bad) {
   const u32 ne = type == M_Replicate || type == M_Propose ? m.n_ent : 0u;
   u32 body = 1 + wsov(type) + 1 + wsov(to) + 1 + wsov(from) + 1 + wsov(cid) + 1 + wsov(m.term) +
@@ -195,6 +195,8 @@ RBE_HD u32 wire_cell(const Planes& P, const Params& C, const u8* heap, u64 heap_
   const u32 pc = row_word(P.cnt[par][r], d, round);
   const u32 na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
   u32 bytes = 0, nm = 0, ni = 0, bad = 0;
+  // Message.To / From (and a RequestVote's / LeaderTransfer's Hint) as node ids
+  const u64 to_id = ext_id(P.node_ids, N, g, d + 1), from_id = ext_id(P.node_ids, N, g, k + 1);
   if (pc & 0x8000u) {  // sendEnterQuiesceMessages (node.go:873-886)
     Msg q;
     q.type = (u8)M_Quiesce;
@@ -203,19 +205,20 @@ RBE_HD u32 wire_cell(const Planes& P, const Params& C, const u8* heap, u64 heap_
     q.pad0 = 0;
     q.ent_off = q.pad1 = 0;
     q.term = q.log_term = q.log_index = q.commit = q.hint = q.hint_high = 0;
-    bytes += wire_message(q, M_Quiesce, d + 1, k + 1, cid, nullptr, heap, C.heap_bytes, heap_head,
-                          out ? out + bytes : nullptr, &bad);
+    bytes += wire_message(q, M_Quiesce, to_id, from_id, cid, nullptr, heap, C.heap_bytes,
+                          heap_head, out ? out + bytes : nullptr, &bad);
     nm++;
   }
   const Msg* lst = &P.msgs[par][((g * N + k) * N + d) * (u64)C.maxm];
   const Ent* arena = &P.arena[par][r * C.ecap];
   for (u32 i = 0; i < na + nb; i++) {
-    const Msg m = i < na ? lst[i] : lst[C.maxm - 1u - (i - na)];
+    Msg m = i < na ? lst[i] : lst[C.maxm - 1u - (i - na)];
     if (m.type == M_InstallSnapshot) {
       ni++;
       continue;
     }
-    bytes += wire_message(m, m.type, d + 1, k + 1, cid, arena + m.ent_off, heap, C.heap_bytes,
+    if (hint_is_node(m.type)) m.hint = ext_id(P.node_ids, N, g, m.hint);
+    bytes += wire_message(m, m.type, to_id, from_id, cid, arena + m.ent_off, heap, C.heap_bytes,
                           heap_head, out ? out + bytes : nullptr, &bad);
     nm++;
   }

@@ -587,14 +587,19 @@ __global__ __launch_bounds__(256) void k_scan_add(u64* v, u64 n, const u64* top)
 namespace rbe {
 
 template <int N>
-__global__ __launch_bounds__(256) void k_ing_key(Params C, u64 heap_cap, const rbe_message* msgs,
+__global__ __launch_bounds__(256) void k_ing_key(Params C, u64 heap_cap, rbe_message* msgs,
                                                  const rbe_entry* ents, const u64* ent0, u64 nm,
                                                  u64* key, u32* idx, u64* hb, u32* err,
-                                                 unsigned long long* ndrop) {
+                                                 unsigned long long* ndrop, const u64* ids) {
   const u64 j = (u64)blockIdx.x * 256 + threadIdx.x;
   if (j >= nm) return;
   u32 e = 0;
   u64 h = 0;
+  if (ids) {  // node ids → internal ids, in place for the walk that scatters them
+    rbe_message m = msgs[j];
+    ingest_ids<N>(C, ids, m);
+    msgs[j] = m;
+  }
   const u64 k = ingest_check<N>(C, heap_cap, msgs[j], ents + ent0[j], &e, &h);
   key[j] = k;
   idx[j] = (u32)j;

@@ -209,7 +209,8 @@ RBE_HD bool xchg_put_fixed(const Planes& P, const Params& C, u32 par, const u8* 
 template <int N, typename RD>
 int outbox_messages(const Params& C, u64 g, u32 k, const CntRow& row, u32 round, const Msg* lst,
                     const Ent* arena, rbe_message* out, u32 cap, rbe_entry* ents, u32 ent_cap,
-                    u32* n_msg, u32* n_ent, u8* cmd, u64 cmd_cap, u64* n_cmd, RD&& rd) {
+                    u32* n_msg, u32* n_ent, u8* cmd, u64 cmd_cap, u64* n_cmd, const u64* ids,
+                    RD&& rd) {
   const u64 cid = cid_of(C, g);
   u32 n = 0, ne = 0;
   u64 nc = 0;
@@ -217,19 +218,12 @@ int outbox_messages(const Params& C, u64 g, u32 k, const CntRow& row, u32 round,
     if (n < cap && out) {
       rbe_message& o = out[n];
       o = rbe_message{};
-      o.type = type;
-      o.reject = m.reject;
-      o.to = to;
-      o.from = k + 1;
-      o.cluster_id = cid;
-      o.term = m.term;
-      o.log_term = m.log_term;
-      o.log_index = m.log_index;
-      o.commit = m.commit;
-      o.hint = m.hint;
-      o.hint_high = m.hint_high;
-      o.n_entries = type == M_Replicate || type == M_Propose ? m.n_ent : 0u;
-      o.reserved = msg_reserved(m);
+      Msg x = m;
+      x.type = (u8)type;
+      x.to = (u8)to;
+      x.from = (u8)(k + 1);
+      if (!(type == M_Replicate || type == M_Propose)) x.n_ent = 0;
+      msg_out(x, cid, ids, N, g, o);
     }
     n++;
   };
@@ -286,7 +280,8 @@ int outbox_messages(const Params& C, u64 g, u32 k, const CntRow& row, u32 round,
 template <int N>
 int messages_to_records(const Params& C, HostHeap& heap, u32 round, u64 n, const u64* group,
                         const rbe_message* msgs, const rbe_entry* ents, const u8* cmd,
-                        std::vector<XCnt>& oc, std::vector<XMsg>& om, std::vector<XEnt>& oe) {
+                        std::vector<XCnt>& oc, std::vector<XMsg>& om, std::vector<XEnt>& oe,
+                        const u64* ids = nullptr) {
   u64 total = 0;
   for (u64 i = 0; i < n; i++) total += msgs[i].n_entries;
   if (total && !ents) return RBE_E_INVALID;
@@ -299,8 +294,13 @@ int messages_to_records(const Params& C, HostHeap& heap, u32 round, u64 n, const
     std::unordered_map<u64, u32> used;   // sender replica → arena entries used
     u64 ei = 0, coff = 0;
     for (u64 i = 0; i < n; i++) {
-      const rbe_message& m = msgs[i];
+      rbe_message m = msgs[i];
       const u64 g = group[i];
+      if (ids && g < C.n_groups) {  // node ids → internal ids (rbe_set_node_ids)
+        m.from = int_id<N>(ids, g, m.from);
+        m.to = int_id<N>(ids, g, m.to);
+        if (hint_is_node(m.type)) m.hint = int_id<N>(ids, g, m.hint);
+      }
       // Peer.Handle (peer.go:186-198): a local message type is a caller bug (the
       // reference panics); a response from a node that is not a member of the
       // group is dropped.  Other messages from non-members cannot be held by a

@@ -88,7 +88,7 @@ class RbeUpdate(C.Structure):
                 ("n_messages", C.c_uint32), ("n_ready_to_read", C.c_uint32),
                 ("n_dropped_entries", C.c_uint32), ("n_dropped_read_indexes", C.c_uint32),
                 ("fault", C.c_uint32), ("flags", C.c_uint32), ("role", C.c_uint32),
-                ("leader_id", C.c_uint32), ("events", C.c_uint32), ("reserved", C.c_uint32)]
+                ("events", C.c_uint32), ("leader_id", C.c_uint64)]
 
 
 # Update flags and listener events (include/rbe.h RBE_UF_* / RBE_EV_*)
@@ -208,7 +208,7 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_wire_fetch", "rbe_wire_decode", "rbe_wire_ingest", "rbe_iso_leaders", "rbe_set_iso_leaders", "rbe_local_groups", "rbe_propose_entries", "rbe_commit",
            "rbe_get_update_commits", "rbe_propose_config_change", "rbe_apply_config_change",
            "rbe_reject_config_change", "rbe_rate_limited", "rbe_restore_remotes",
-           "rbe_snapshot_saved", "rbe_compact"]
+           "rbe_snapshot_saved", "rbe_compact", "rbe_set_node_ids"]
 KERNEL_SLOTS = 4
 
 _lib = None
@@ -255,6 +255,7 @@ def load_library(path: Optional[str] = None):
         "rbe_restore_remotes": (i32, [vp, u64, P(u64), P(u32), P(u64)]),
         "rbe_snapshot_saved": (i32, [vp, u64, P(u64), P(u64), P(u64), P(u32)]),
         "rbe_compact": (i32, [vp, u64, P(u64), P(u64)]),
+        "rbe_set_node_ids": (i32, [vp, u64, u64, P(u64)]),
         "rbe_get_update_commits": (i32, [vp, u64, u64, P(RbeUpdateCommit)]),
         "rbe_run": (i32, [vp, u32]),
         "rbe_sync": (i32, [vp]),
@@ -581,6 +582,13 @@ class NodeInputs:
         u32a = (C.c_uint32 * max(1, len(n)))(*n)
         _check_input(self._input("restore_remotes", len(replicas), _u64s(replicas), u32a,
                                  _u64s(ids)), "rbe_restore_remotes")
+
+    def set_node_ids(self, first_group, ids):
+        """rbe_set_node_ids: the node ids of groups first_group.. (a list of
+        n_replicas-long ascending id lists), before the first step."""
+        flat = [x for row in ids for x in row]
+        _check_input(self._input("set_node_ids", first_group, len(ids), _u64s(flat)),
+                     "rbe_set_node_ids")
 
     def snapshot_saved(self, replicas, indexes, terms, removed=None):
         """The host's snapshot worker saved a snapshot of its state machine and the

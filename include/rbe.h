@@ -18,10 +18,14 @@
  *     abort the process: they set a sticky per-replica fault word
  *     (RBE_FAULT_*) that rbe_get_updates/rbe_get_views report.
  *
- * Node IDs inside a group are 1..n (slot + 1); the group of cluster id c is
- * the engine-local index g with c = cid_base + g * cid_stride, which is
- * dragonboat's FixedPartitioner rule (internal/server/partition.go:38-40)
- * when cid_stride = number of GPUs and cid_base = 1 + rank.
+ * A group has n_replicas slots; slot s is node id s + 1 unless the host gives
+ * the group's node ids (rbe_set_node_ids: any non-zero uint64, ascending with
+ * the slots).  Every node id the ABI takes or returns is such an id; masks
+ * (removed, votes) and per-slot arrays (match, next) are indexed by slot.  The
+ * group of cluster id c is the engine-local index g with c = cid_base + g *
+ * cid_stride, which is dragonboat's FixedPartitioner rule
+ * (internal/server/partition.go:38-40) when cid_stride = number of GPUs and
+ * cid_base = 1 + rank.
  */
 #ifndef DRAGONBOAT_AMD_RBE_H_
 #define DRAGONBOAT_AMD_RBE_H_
@@ -203,8 +207,8 @@ typedef struct rbe_update {
   uint64_t digest;              /* trace digest */
   uint32_t n_messages, n_ready_to_read, n_dropped_entries, n_dropped_read_indexes;
   uint32_t fault, flags;
-  uint32_t role, leader_id;
-  uint32_t events, reserved; /* RBE_EV_* of the step */
+  uint32_t role, events;     /* events: RBE_EV_* of the step */
+  uint64_t leader_id;
 } rbe_update;
 #define RBE_UF_STATE_CHANGED 1u
 #define RBE_UF_SENT_QUIESCE 2u
@@ -300,6 +304,15 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out);
  * RBE_E_NOMEM when the heap has no room for them). */
 int rbe_launch(rbe_engine* e, uint64_t n, const uint64_t* replica, const rbe_launch_state* st,
                const rbe_entry* ents, const uint8_t* cmd);
+/* The node ids of groups [first_group, first_group + count): n_replicas per
+ * group in slot order, non-zero and strictly ascending within a group (the
+ * engine's canonical order of a group's nodes — raft.go's map iterations,
+ * SURVEY.md §8c — is ascending node id, which is then the slot order).  The
+ * node ids of raft.Config.NodeID and pb.Message From/To (config.go, raft.pb.go)
+ * that a dragonboat deployment assigns; a slot beyond the initial voters
+ * (cfg.n_voters) is the id a joining node will have.  Only before the first
+ * step (RBE_E_STATE after).  Without it slot s is node s + 1. */
+int rbe_set_node_ids(rbe_engine* e, uint64_t first_group, uint64_t count, const uint64_t* ids);
 int rbe_destroy(rbe_engine* e);
 int rbe_abi_version(void);
 /* sizeof the ABI structs, in this order: rbe_config, rbe_replica_view,

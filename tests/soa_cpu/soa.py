@@ -99,6 +99,7 @@ def lib():
                 "apply_config_change": [C.c_uint64, u64p, u64p, u32p],
                 "reject_config_change": [C.c_uint64, u64p],
                 "restore_remotes": [C.c_uint64, u64p, u32p, u64p],
+                "set_node_ids": [C.c_uint64, C.c_uint64, u64p],
                 "snapshot_saved": [C.c_uint64, u64p, u64p, u64p, u32p],
                 "compact": [C.c_uint64, u64p, u64p],
                 "get_update_commits": [C.c_uint64, C.c_uint64, P(RbeUpdateCommit)],

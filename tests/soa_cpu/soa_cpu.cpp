@@ -287,6 +287,8 @@ void* soa_create(const rbe_config* cfg) {
     };
   }
   P.counters = nullptr;
+  P.node_ids = nullptr;  // slot s is node s + 1 until soa_set_node_ids
+  P.ids_n = (u32)N;
   for (u64 r = 0; r < R; r++) {
     with_n(N, [&](auto NN) { launch_replica<decltype(NN)::value>(P, C, r); });
   }
@@ -390,9 +392,12 @@ int soa_propose_entries(void* h, uint64_t n, const uint64_t* replica, const uint
   return e->hin.push_entries(n, replica, n_ents, ents, cmd);
 }
 // rbe_launch on the host build (same checks and per-replica restart)
-int soa_launch(void* h, uint64_t n, const uint64_t* replica, const rbe_launch_state* st,
+int soa_launch(void* h, uint64_t n, const uint64_t* replica, const rbe_launch_state* st_ids,
                const rbe_entry* ents, const uint8_t* cmd) {
   SoaEngine* e = (SoaEngine*)h;
+  std::vector<rbe_launch_state> stv;  // votes as internal ids
+  if (!e->hin.map_votes(n, replica, st_ids, stv)) return RBE_E_INVALID;
+  const rbe_launch_state* st = stv.data();
   if (n && replica) {
     std::vector<u64> v(replica, replica + n);
     std::sort(v.begin(), v.end());
@@ -481,6 +486,14 @@ int soa_compact(void* h, uint64_t n, const uint64_t* replica, const uint64_t* to
   SoaEngine* e = (SoaEngine*)h;
   if (!e->C.snapshot_entries || !e->C.ext_apply) return RBE_E_STATE;
   return e->hin.snapshot_op(n, replica, SR_COMPACT, to, nullptr, nullptr, false);
+}
+int soa_set_node_ids(void* h, uint64_t first, uint64_t count, const uint64_t* ids) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (e->round != 0) return RBE_E_STATE;
+  int rc = e->hin.set_node_ids(e->C.n_groups, first, count, ids);
+  if (rc) return rc;
+  e->P.node_ids = e->hin.id_table();  // the host build's planes are host memory
+  return RBE_OK;
 }
 int soa_restore_remotes(void* h, uint64_t n, const uint64_t* replica, const uint32_t* n_voters,
                         const uint64_t* ids) {
@@ -656,6 +669,7 @@ static int soa_ingest_t(SoaEngine* e, const uint8_t* d, uint64_t bytes, uint64_t
   u32 err = 0;
   for (u64 j = 0; j < tm; j++) {
     u32 x = 0;
+    ingest_ids<N>(C, e->hin.id_table(), msgs[j]);
     key[j] = ingest_check<N>(C, H.cap, msgs[j], ents.data() + ent0[j], &x, &hb[j]);
     err |= x;
     if (!x && key[j] == ing_drop_key(C)) st[2]++;
@@ -785,8 +799,8 @@ void soa_views(void* h, rbe_replica_view* out) {
     const Hot hh = materialize_hot(e->P.hot[i], e->C, e->tclk);
     const Core& c = e->P.core[i];
     v.term = c.term;
-    v.vote = c.vote;
-    v.leader_id = c.leader;
+    v.vote = ext_id(e->hin.id_table(), N, i / N, c.vote);
+    v.leader_id = ext_id(e->hin.id_table(), N, i / N, c.leader);
     v.committed = c.committed;
     v.last_index = c.last_index;
     v.processed = c.processed;
@@ -943,7 +957,7 @@ extern "C" int soa_get_outbox(void* h, uint64_t replica, rbe_message* out, uint3
   return with_n(N, [&](auto NN) {
     return outbox_messages<decltype(NN)::value>(e->C, g, k, row, rd, lst, arena, out, cap, ents,
                                                 ent_cap, n_out, n_ents, cmd, cmd_cap, cmd_bytes,
-                                                hr);
+                                                e->hin.id_table(), hr);
   });
 }
 template <int N>
@@ -953,7 +967,8 @@ static int soa_push_t(SoaEngine* e, uint64_t n, const uint64_t* group, const rbe
   std::vector<XMsg> m;
   std::vector<XEnt> x;
   const int rc =
-      messages_to_records<N>(e->C, e->hin.heap, e->round, n, group, msgs, ents, cmd, c, m, x);
+      messages_to_records<N>(e->C, e->hin.heap, e->round, n, group, msgs, ents, cmd, c, m, x,
+                             e->hin.id_table());
   if (rc) return rc;
   soa_xchg_unpack_t<N>(e, c.data(), c.size(), m.data(), m.size(), x.data(), x.size());
   return RBE_OK;
