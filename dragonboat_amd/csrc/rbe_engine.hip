@@ -255,7 +255,7 @@ __global__ __launch_bounds__(kBlock) void k_relaunch(Planes P, Params C, const L
   const LaunchRec x = rec[i];
   relaunch_replica<N>(P, C, x.replica, x.term, x.vote, x.commit, x.last, x.n, terms + x.off,
                       bodies + x.off, ppar, tclk, x.marker, x.marker_term, x.ss_index, x.ss_term,
-                      (u8)x.removed);
+                      x.removed);
   P.gwake[x.replica / N] = GW_AWAKE;
 }
 
@@ -429,7 +429,7 @@ static int read_heap(rbe_engine* e, u64 pos, u64 off, u64 len, u8* dst) {
 }
 
 
-static constexpr int kPlaneAllocs = 24;
+static constexpr int kPlaneAllocs = 25;
 static u64 bytes_of(const Params& C, u64* parts) {
   const u64 N = C.n, G = C.n_groups, R = C.n_rep;
   u64 p[kPlaneAllocs] = {
@@ -457,6 +457,7 @@ static u64 bytes_of(const Params& C, u64* parts) {
       C.snapshot_entries ? R * N * sizeof(u64) : 0,
       (C.ext_commit || C.rl_max) ? R * sizeof(u64) : 0,
       C.rl_max ? R * sizeof(RlSt) : 0,
+      C.membership ? R * sizeof(u16) : 0,
   };
   u64 t = 0;
   for (int i = 0; i < kPlaneAllocs; i++) {
@@ -523,8 +524,17 @@ static int make_params(const rbe_config* cfg, Params* out) {
   C.cc_period = cfg->cc_period;
   C.cc_mod = cfg->cc_mod ? cfg->cc_mod : 1;
   if (C.cc_period && !C.membership) return RBE_E_INVALID;
-  // spare slots (nodes that join later) need membership change
+  // spare slots (nodes that join later) need membership change; observer and
+  // witness slots are disjoint spare slots
   if (C.n_voters > C.n || (C.n_voters < C.n && !C.membership)) return RBE_E_INVALID;
+  C.obs_slots = cfg->observer_slots;
+  C.wit_slots = cfg->witness_slots;
+  {
+    const u32 spare = ((1u << C.n) - 1u) & ~((1u << C.n_voters) - 1u);
+    if (((C.obs_slots | C.wit_slots) & ~spare) || (C.obs_slots & C.wit_slots) ||
+        ((C.obs_slots | C.wit_slots) && !C.membership))
+      return RBE_E_INVALID;
+  }
   C.in_cap = cfg->in_cap ? cfg->in_cap : (u32)(cfg->n_groups > 1024 ? cfg->n_groups : 1024);
   if (cfg->n_groups > 0xFFFFFFFFull && !cfg->in_cap) C.in_cap = 0xFFFFFFFFu;
   C.xfer_period = cfg->xfer_period;
@@ -782,6 +792,7 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   P.rem_snap = C.snapshot_entries ? (u64*)ptrs[21] : nullptr;
   P.imark = (C.ext_commit || C.rl_max) ? (u64*)ptrs[22] : nullptr;
   P.rl = C.rl_max ? (RlSt*)ptrs[23] : nullptr;
+  P.roles = C.membership ? (u16*)ptrs[24] : nullptr;
   P.node_ids = nullptr;  // slot s is node s + 1 until rbe_set_node_ids
   P.ids_n = C.n;
   HIP_IGNORE(hipMemsetAsync(P.gwake, GW_AWAKE, C.n_groups, e->stream));  // every group starts awake
@@ -1553,10 +1564,12 @@ int rbe_get_views(rbe_engine* e, uint64_t first, uint64_t count, rbe_replica_vie
   std::vector<RemoteMN> rem(count * N);
   std::vector<u8> rst(count * N);
   std::vector<Upd> upd(count);
+  std::vector<u16> roles(count, 0);
   if (d2h(e, hot.data(), e->P.hot + first, count) || d2h(e, core.data(), e->P.core + first, count) ||
       d2h(e, rem.data(), e->P.rem + first * N, count * N) ||
       d2h(e, rst.data(), e->P.rem_st + first * N, count * N) ||
-      d2h(e, upd.data(), e->P.upd + first, count))
+      d2h(e, upd.data(), e->P.upd + first, count) ||
+      (e->C.membership && d2h(e, roles.data(), e->P.roles + first, count)))
     return RBE_E_HIP;
   HIP_OK(hipStreamSynchronize(e->stream));
   for (u64 i = 0; i < count; i++) {
@@ -1586,9 +1599,14 @@ int rbe_get_views(rbe_engine* e, uint64_t first, uint64_t count, rbe_replica_vie
     v.votes_granted = h.votes_granted;
     v.events = (e->round > 0 && upd[i].round == e->round - 1) ? upd[i].events : 0u;
     v.removed = c.members & MB_REMOVED;
+    if (c.members & MB_ROLES) {  // Planes::roles is only current while MB_ROLES is set
+      v.observers = roles[i] & 0xFFu;
+      v.witnesses = roles[i] >> 8;
+    }
     if (h.role == R_Leader) {
       for (u32 s = 0; s < N && s < 8; s++) {
-        if ((v.removed >> s) & 1u) continue;  // not in raft.remotes
+        // remotes, observers and witnesses
+        if ((v.removed >> s) & ~((v.observers | v.witnesses) >> s) & 1u) continue;
         v.match[s] = rem[i * N + s].match;
         v.next[s] = rem[i * N + s].next;
         v.rstate[s] = rst[i * N + s] & 3;
@@ -1916,7 +1934,7 @@ int rbe_fault_summary(rbe_engine* e, uint64_t* n_faulty, uint32_t* fault_or) {
   u64 n = 0;
   u32 o = 0;
   for (u64 i = 0; i < R; i++) {
-    if (upd[i].fault & ~F_HANDOFF) n++;  // a hand-off is not a fault (rbe.h)
+    if (upd[i].fault) n++;
     o |= upd[i].fault;
   }
   *n_faulty = n;

@@ -408,7 +408,10 @@ RBE_HD void fast_node_snapshot(const Planes& P, const Params& C, StepCounters& c
   if (t == 0) return;
   sp->ss_index = la;
   sp->ss_term = t;
-  sp->ss_rem = sp->sm_rem;  // a fast step applies no ConfigChange: the state machine's membership
+  // a fast step applies no ConfigChange: the state machine's membership
+  sp->ss_rem = sp->sm_rem;
+  sp->ss_obs = sp->sm_obs;
+  sp->ss_wit = sp->sm_wit;
   const u64 ct = la > C.compaction_overhead ? la - C.compaction_overhead : 0;
   sp->compact_to = ct;
   if (ct) flags |= HF_SNAP_WORK;

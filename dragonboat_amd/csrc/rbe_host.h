@@ -362,8 +362,8 @@ inline void snap_state_row(const SnapSt& s, u64* o) {
   o[3] = s.ss_term;
   o[4] = s.ss_req;
   o[5] = s.compact_to;
-  o[6] = s.ss_rem;
-  o[7] = s.sm_rem;
+  o[6] = pack_ms(s.ss_rem, s.ss_obs, s.ss_wit);
+  o[7] = pack_ms(s.sm_rem, s.sm_obs, s.sm_wit);
 }
 
 // Check a batch of entries whole: their types, and that the heap (if any
@@ -413,8 +413,9 @@ inline int launch_rows(const Params& C, HostHeap& heap, u64 n, const u64* replic
     if (replica[i] >= C.n_rep || x.n_entries > C.ring || x.n_entries > x.last_index ||
         x.commit > x.last_index || x.vote > C.n || (x.last_index > x.marker && !x.n_entries))
       return RBE_E_INVALID;
-    // the LogDB's membership: voters among the group's slots, only with cfg.membership
-    if (x.removed >> C.n || (x.removed && !C.membership)) return RBE_E_INVALID;
+    // the LogDB's membership (packed: slots not in Addresses | Observers << 8 |
+    // Witnesses << 16), only with cfg.membership
+    if (!ms_valid(x.removed, C.n) || (x.removed && !C.membership)) return RBE_E_INVALID;
     total += x.n_entries;
   }
   if (total && !ents) return RBE_E_INVALID;
@@ -719,21 +720,25 @@ struct HostInputs {
     }
     return RBE_OK;
   }
-  // rbe_restore_remotes: replica[i]'s snapshot lists n_voters[i] voters, their
-  // node ids next in `ids`; staged as the removed mask of the group's slots
-  int restore_remotes(u64 cnt, const u64* replica, const u32* n_voters, const u64* vids) {
-    if (cnt && !n_voters) return RBE_E_INVALID;
+  // rbe_restore_remotes: replica[i]'s snapshot lists counts[3i] voters,
+  // counts[3i + 1] observers and counts[3i + 2] witnesses, their node ids next in
+  // `ids` in that order; staged packed (pack_ms)
+  int restore_remotes(u64 cnt, const u64* replica, const u32* counts, const u64* vids) {
+    if (cnt && !counts) return RBE_E_INVALID;
     std::vector<u64> rem(cnt);
     u64 j = 0;
     for (u64 i = 0; i < cnt; i++) {
-      u32 listed = 0;
-      if (n_voters[i] && !vids) return RBE_E_INVALID;
-      for (u32 q = 0; q < n_voters[i]; q++, j++) {
-        const u64 x = in_id(replica ? replica[i] : ~0ull, vids[j]);
-        if (!x || ((listed >> (x - 1)) & 1u)) return RBE_E_INVALID;
-        listed |= 1u << (x - 1);
+      u32 sets[3] = {0, 0, 0}, listed = 0;
+      for (u32 c = 0; c < 3; c++) {
+        if (counts[3 * i + c] && !vids) return RBE_E_INVALID;
+        for (u32 q = 0; q < counts[3 * i + c]; q++, j++) {
+          const u64 x = in_id(replica ? replica[i] : ~0ull, vids[j]);
+          if (!x || ((listed >> (x - 1)) & 1u)) return RBE_E_INVALID;  // each node in one set
+          listed |= 1u << (x - 1);
+          sets[c] |= 1u << (x - 1);
+        }
       }
-      rem[i] = ((1u << n) - 1u) & ~listed;
+      rem[i] = pack_ms(((1u << n) - 1u) & ~sets[0], sets[1], sets[2]);
     }
     int rc = check_replicas(cnt, replica, EXT_RESTORE);
     if (rc) return rc;
@@ -783,7 +788,8 @@ struct HostInputs {
       if (index[i] == 0) return RBE_E_INVALID;
       if (kind == SR_SAVE) {
         const u32 rem = removed ? removed[i] : 0u;
-        if (term[i] == 0 || index[i] > applied[replica[i]] || (rem >> n) || (rem && !membership))
+        if (term[i] == 0 || index[i] > applied[replica[i]] || !ms_valid(rem, n) ||
+            (rem && !membership))
           return RBE_E_INVALID;
       }
       const u32 s = snap_slot[replica[i]];

@@ -75,6 +75,7 @@ inline void snap_planes(const Planes& P, const Params& C, SnapPlane* out) {
   }
   if (C.ext_commit || C.rl_max) add(P.imark, 1, R * sizeof(u64), N * sizeof(u64));  // inMemory markers
   if (C.rl_max) add(P.rl, 1, R * sizeof(RlSt), N * sizeof(RlSt));  // rate limiters
+  if (C.membership) add(P.roles, 1, R * sizeof(u16), N * sizeof(u16));  // observers / witnesses
   // the per-replica fault words live in Hot/Core/Upd; nothing else is carried
   while (i < kSnapPlanes) out[i++] = SnapPlane{nullptr, 0, 0, 0};
 }
@@ -99,7 +100,7 @@ inline u64 snap_behavior_hash(const Params& C) {
                    C.iso_period, C.iso_len, C.iso_mod, C.rep_world, C.rep_rank,
                    C.snapshot_entries, C.compaction_overhead, C.heap_bytes, C.ext_apply,
                    C.xfer_period, C.xfer_mod, C.ext_commit, C.membership, C.cc_period,
-                   C.cc_mod, C.rl_max};
+                   C.cc_mod, C.rl_max, C.n_voters, C.obs_slots, C.wit_slots};
   u64 h = 0x243F6A8885A308D3ull;
   for (u64 x : f) {
     h ^= x + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);

@@ -183,6 +183,59 @@ RBE_HD u32 cc_target(const Params& C, u64 cid, u32 round) {
   const u64 epoch = round / C.cc_period;
   return below(mix64(C.seed ^ (cid * 0x8EBC6AF09C88C6E3ULL) ^ (epoch << 20) ^ 0xCC), C.n) + 1;
 }
+// A group's membership packed as slot masks (bit s = slot s): bits 0-7 the
+// slots not in Addresses (raft.remotes), 8-15 Observers, 16-23 Witnesses
+// (pb.Membership, raft.pb.go:733-739; rbe_launch_state::removed, the snapshot
+// state, rbe_restore_remotes)
+RBE_HD u32 pack_ms(u32 rem, u32 obs, u32 wit) {
+  return (rem & 0xFFu) | ((obs & 0xFFu) << 8) | ((wit & 0xFFu) << 16);
+}
+// a packed membership over n slots: each node in at most one of observers /
+// witnesses, and those not in Addresses
+RBE_HD bool ms_valid(u32 ms, u32 n) {
+  const u32 rem = ms & 0xFFu, obs = (ms >> 8) & 0xFFu, wit = (ms >> 16) & 0xFFu;
+  return !(ms >> 24) && !(rem >> n) && !(obs >> n) && !(wit >> n) && !(obs & wit) &&
+         !((obs | wit) & ~rem);
+}
+// Whether the state machine accepts a committed ConfigChange (rsm
+// membership.go:299-321 handleConfigChange), judged on the membership `ms`
+// (packed) raft holds when the entry is applied: an add of a node that already
+// is a voter, observer or witness is rejected — alreadyMember,
+// nodeBecomingObserver / Witness, witnessBecomingNode, observerBecomingWitness
+// — except AddNode of an observer (isPromotingObserver); removing the only
+// voter is rejected (isDeletingOnlyNode).  A rejected one goes back to raft as
+// RejectConfigChange.  (The stand-in keeps no Removed set, so re-adding a
+// removed node is accepted: the membership schedule relies on it.)
+RBE_HD bool cc_accepted(u32 ms, u32 t, u64 nid, u32 n) {
+  if (nid < 1 || nid > n) return true;
+  const u32 b = 1u << (nid - 1), rem = ms & 0xFFu, obs = (ms >> 8) & 0xFFu, wit = (ms >> 16) & 0xFFu;
+  const u32 voters = ((1u << n) - 1u) & ~rem;
+  if (t == CC_RemoveNode) return voters != b;
+  if (t == CC_AddNode && (obs & b)) return true;
+  return !((voters | obs | wit) & b);
+}
+// the state machine's membership after applying a ConfigChange (rsm
+// membership.go: AddNode also promotes an observer; RemoveNode drops the node
+// from every set)
+RBE_HD void ms_apply(u32& ms, u32 t, u64 nid, u32 n) {
+  if (nid < 1 || nid > n) return;
+  const u32 b = 1u << (nid - 1);
+  u32 rem = ms & 0xFFu, obs = (ms >> 8) & 0xFFu, wit = (ms >> 16) & 0xFFu;
+  if (t == CC_AddNode) {
+    rem &= ~b;
+    obs &= ~b;
+  } else if (t == CC_RemoveNode) {
+    rem |= b;
+    obs &= ~b;
+    wit &= ~b;
+  } else if (t == CC_AddObserver) {
+    obs |= b;
+  } else if (t == CC_AddWitness) {
+    wit |= b;
+  }
+  ms = pack_ms(rem, obs, wit);
+}
+
 // The stand-in ConfigChange Cmd the engine shares with the oracle harness (8
 // bytes, LE of 0xCC << 56 | type << 48 | node id; bootstrap's entries are its
 // AddNode form): what the engine's own state machine decodes when it applies
@@ -361,7 +414,9 @@ RBE_HD void snap_rec_apply(const Planes& P, const SnapRec& x) {
   if ((x.kind & SR_SAVE) && x.index > sp.ss_index) {
     sp.ss_index = x.index;
     sp.ss_term = x.term;
-    sp.ss_rem = (u8)x.rem;
+    sp.ss_rem = (u8)(x.rem & 0xFFu);  // packed membership (pack_ms)
+    sp.ss_obs = (u8)((x.rem >> 8) & 0xFFu);
+    sp.ss_wit = (u8)((x.rem >> 16) & 0xFFu);
   }
   if (x.kind & SR_COMPACT) {
     sp.compact_to = x.compact_to;
@@ -406,7 +461,9 @@ RBE_HD u64 int_id(const u64* ids, u64 g, u64 id) {
 
 // rbe_message.reserved of an engine message: an InstallSnapshot's snapshot
 // membership (Snapshot.Membership as the removed mask, Msg::pad0), else 0
-RBE_HD u32 msg_reserved(const Msg& m) { return m.type == M_InstallSnapshot ? (u32)m.pad0 : 0u; }
+RBE_HD u32 msg_reserved(const Msg& m) {
+  return m.type == M_InstallSnapshot ? ((u32)m.pad0 | ((m.pad1 & 0xFFFFu) << 8)) : 0u;
+}
 RBE_HD bool is_leader_message(u32 t) {  // raft.go:1382-1385
   return t == M_Replicate || t == M_InstallSnapshot || t == M_Heartbeat || t == M_TimeoutNow ||
          t == M_ReadIndexResp;
@@ -469,6 +526,8 @@ struct Lane {
   u64 lead_start;  // leader: index of its no-op (Core::lead_start)
   u8 vote, leader, ltt, rq_head, rq_count;
   u8 members, cc_apply;  // Core::members / cc_apply (membership)
+  u8 obs, wit;           // raft.observers / raft.witnesses (Planes::roles; membership)
+  u8 roles0;             // MB_ROLES at load: Planes::roles holds something to rewrite
   u64 c_match[N], c_next[N];  // LEAD: remote slots held in registers
   u32 c_st[N];
   u8 iso;  // isolation mask of this group for this round
@@ -478,7 +537,7 @@ struct Lane {
   u64 marker, marker_term;
   u8 snp_pend, snp_rej;
   bool snap_restored;
-  u8 sm_rem;  // SnapSt::sm_rem: the state machine's membership (snapshot_entries)
+  u32 sm_ms;  // SnapSt::sm_*: the state machine's membership, packed (snapshot_entries)
   u64 applied0;  // raft.applied of this step (NotifyRaftLastApplied at its start)
 
   // per-step outputs
@@ -486,6 +545,8 @@ struct Lane {
   u32 arena_used;
   u64 seg_lo;
   u32 seg_off, seg_len;
+  u64 mseg_lo;  // the last metadata copy for a witness (arena_meta_range)
+  u32 mseg_off, mseg_len;
   u64 msg_hash, rtr_hash, drop_hash;
   u32 n_msgs, n_rtr, n_drop_ent, n_drop_ri;
   u32 fault;
@@ -876,6 +937,34 @@ struct Lane {
     arena_used += cnt;
     return true;
   }
+  // entries [lo, lo+cnt) for a witness (makeMetadataEntries, raft.go:742-756):
+  // a copy of their own in the arena where every entry but a ConfigChange is a
+  // MetadataEntry with only its index and term
+  RBE_HD bool arena_meta_range(u64 lo, u32 cnt, u32* off) {
+    if (mseg_len && lo >= mseg_lo && lo + cnt <= mseg_lo + mseg_len) {
+      *off = mseg_off + (u32)(lo - mseg_lo);
+      return true;
+    }
+    if (arena_used + cnt > C.ecap) {
+      set_fault(F_ARENA);
+      return false;
+    }
+    Ent* a = &P.arena[par][r * C.ecap + arena_used];
+    copy_ring_to_arena(lo, cnt, a);
+    ctr.v[C_RING_ACCESS] += cnt;
+    for (u32 i = 0; i < cnt; i++)
+      if (ent_type(a[i].type) != E_ConfigChange) {
+        a[i].type = E_Metadata;
+        a[i].len = 0;
+        a[i].lo = a[i].hi = 0;
+      }
+    mseg_lo = lo;
+    mseg_off = arena_used;
+    mseg_len = cnt;
+    *off = arena_used;
+    arena_used += cnt;
+    return true;
+  }
   RBE_HD bool arena_put(const Ent* src, u32 cnt, u32* off) {
     if (arena_used + cnt > C.ecap) {
       set_fault(F_ARENA);
@@ -961,11 +1050,16 @@ struct Lane {
     flags &= (u8)~HF_PENDING_CC;
     ltt = 0;
     reset_remotes();
-    seg_len = 0;
+    seg_len = mseg_len = 0;
     if (rl_on()) P.rl[r].fmask = 0;  // rl.ResetFollowerState
   }
   RBE_HD void become_follower(u64 t, u8 lid) {  // raft.go:947-955
+    if (role == R_Witness) set_fault(F_PANIC);  // "transitioning to follower from witness state"
     role = R_Follower;
+    reset(t);
+    leader = lid;
+  }
+  RBE_HD void become_nonvoting(u64 t, u8 lid) {  // becomeObserver / becomeWitness, raft.go:926-946
     reset(t);
     leader = lid;
   }
@@ -1071,17 +1165,26 @@ struct Lane {
 
   // ------------------------------------------------------------- membership
   // raft.remotes of this replica's view: every slot not in Core::members'
-  // removed bits (raft.go:366-416 numVotingMembers / quorum / votingMembers;
-  // observers and witnesses are handed to the host, F_HANDOFF)
-  RBE_HD bool voter(u32 s) const { return !((members >> s) & 1u); }
+  // removed bits (raft.go:366-416 numVotingMembers / quorum / votingMembers);
+  // observers and witnesses in Planes::roles (obs / wit)
+  RBE_HD bool voter(u32 s) const { return !((members >> s) & 1u); }  // in raft.remotes
   RBE_HD u32 voters_mask() const { return ((1u << N) - 1u) & ~(u32)members; }
-  RBE_HD u32 quorum() const { return popc8(voters_mask()) / 2 + 1; }
-  RBE_HD bool from_member(u32 from) const { return from >= 1 && from <= N && voter(from - 1u); }
-  RBE_HD void set_handoff() {  // not a fault (rbe_types.h F_HANDOFF): no fault counted
-    fault |= F_HANDOFF;
+  RBE_HD bool is_obs(u32 s) const { return (obs >> s) & 1u; }
+  RBE_HD bool is_wit(u32 s) const { return (wit >> s) & 1u; }
+  // votingMembers (raft.go:410-419): remotes and witnesses
+  RBE_HD u32 vmask() const { return voters_mask() | wit; }
+  RBE_HD u32 quorum() const { return popc8(vmask()) / 2 + 1; }  // raft.go:366-372
+  // remotes, observers and witnesses: lw (raft.go:2013-2027), Peer.Handle
+  RBE_HD bool member(u32 s) const { return voter(s) || is_obs(s) || is_wit(s); }
+  RBE_HD bool from_member(u32 from) const { return from >= 1 && from <= N && member(from - 1u); }
+  RBE_HD void set_remote(u32 s) {  // setRemote / setObserver / setWitness(id, 0, lastIndex + 1)
+    set_rmatch(s, 0);
+    set_rnext(s, last + 1);
+    set_rst(s, 0);
   }
-  // handleNodeConfigChange (raft.go:1537-1556) → addNode / removeNode
-  // (raft.go:1135-1198); `m.hint` = node id, `m.hint_high` = ConfigChangeType
+  // handleNodeConfigChange (raft.go:1537-1556) → addNode / removeNode /
+  // addObserver / addWitness (raft.go:1135-1198); `m.hint` = node id,
+  // `m.hint_high` = ConfigChangeType
   RBE_HD void on_config_change(const Msg& m) {
     if (!C.membership) {
       set_fault(F_UNSUPPORTED);
@@ -1093,11 +1196,6 @@ struct Lane {
     }
     const u64 nid = m.hint;
     const u32 type = (u32)m.hint_high;
-    if (type == CC_AddObserver || type == CC_AddWitness) {
-      flags &= (u8)~HF_PENDING_CC;
-      set_handoff();
-      return;
-    }
     if (type > CC_AddWitness) {
       set_fault(F_PANIC);  // "unexpected config change type"
       return;
@@ -1107,31 +1205,72 @@ struct Lane {
       return;
     }
     const u32 s = (u32)nid - 1u;
+    const u8 bit = (u8)(1u << s);
     flags &= (u8)~HF_PENDING_CC;  // clearPendingConfigChange
     if (type == CC_AddNode) {
+      if (s == k && role == R_Witness) {  // "is a witness"
+        set_fault(F_PANIC);
+        return;
+      }
       if (voter(s)) return;  // already a voting member
-      members &= (u8)~(1u << s);
-      set_rmatch(s, 0);  // setRemote(id, 0, lastIndex + 1): Retry, not active
-      set_rnext(s, last + 1);
-      set_rst(s, 0);
+      if (is_obs(s)) {  // an observer is promoted with its progress (raft.go:1144-1151)
+        obs &= (u8)~bit;
+        members &= (u8)~bit;
+        if (s == k) become_follower(term, leader);
+        return;
+      }
+      if (is_wit(s)) {  // "could not promote witness to a full member"
+        set_fault(F_PANIC);
+        return;
+      }
+      members &= (u8)~bit;
+      set_remote(s);
       return;
     }
-    // RemoveNode (deleteRemote; no observer or witness to delete)
-    members |= (u8)(1u << s);
+    if (type == CC_AddObserver || type == CC_AddWitness) {  // raft.go:1159-1180
+      const bool ob = type == CC_AddObserver;
+      if (s == k && role != (ob ? R_Observer : R_Witness)) {  // "is not an observer / a witness"
+        set_fault(F_PANIC);
+        return;
+      }
+      if (ob ? is_obs(s) : is_wit(s)) return;
+      if (member(s)) {  // a node in two of the maps at once: not held by a slot
+        set_fault(F_UNSUPPORTED);
+        return;
+      }
+      if (ob) obs |= bit;
+      else wit |= bit;
+      set_remote(s);
+      return;
+    }
+    // RemoveNode: deleteRemote / deleteObserver / deleteWitness
+    members |= bit;
+    obs &= (u8)~bit;
+    wit &= (u8)~bit;
     if (s == k && role == R_Leader) become_follower(term, 0);
     if (ltt != 0 && role == R_Leader && ltt == (u8)nid) ltt = 0;  // abortLeaderTransfer
-    if (role == R_Leader && voters_mask() != 0) {
+    if (role == R_Leader && vmask() != 0) {
       if (try_commit()) broadcast_replicate();
     }
   }
   // restoreRemotes (raft.go:472-517) for Handle(SnapshotReceived), which
   // Peer.RestoreRemotes sends once the state machine recovered from a snapshot
-  // (peer.go:159-165): the voters become the snapshot's (`rem`, the removed
-  // mask), every remote restarts at match 0 / next lastIndex + 1 (self: match
-  // lastIndex), Retry and inactive; a leader the snapshot no longer lists
-  // steps down.  No observers or witnesses here (F_HANDOFF groups are the host's).
-  RBE_HD void restore_remotes(u8 rem) {
-    members = (u8)((members & MB_CC_IN_LOG) | (rem & MB_REMOVED));
+  // (peer.go:159-165): raft.remotes / observers / witnesses become the
+  // snapshot's (`ms`: slots not in Addresses | Observers << 8 | Witnesses << 16),
+  // every remote restarts at match 0 / next lastIndex + 1 (self: match
+  // lastIndex), Retry and inactive; an observer the snapshot lists as a voter
+  // becomes a follower, a leader it does not list steps down.
+  RBE_HD void restore_remotes(u32 ms) {
+    const u32 full = (1u << N) - 1u;
+    const u32 addr = full & ~(ms & 0xFFu);
+    if (addr & wit) {  // "Assumed witness could not promote to full member"
+      set_fault(F_PANIC);
+      return;
+    }
+    if (((addr >> k) & 1u) && role == R_Observer) become_follower(term, leader);
+    members = (u8)((members & MB_CC_IN_LOG) | (~addr & MB_REMOVED & full));
+    obs = (u8)((ms >> 8) & full);
+    wit = (u8)((ms >> 16) & full);
     for (u32 s = 0; s < N; s++) {
       set_rmatch(s, s == k ? last : 0);
       set_rnext(s, last + 1);
@@ -1153,7 +1292,7 @@ struct Lane {
     // non-voters sort below every voter (match 0), so the quorum-th largest of
     // the voters is the quorum-th largest of all N (raft.go tryCommit over
     // r.remotes and r.witnesses)
-    for (u32 s = 0; s < N; s++) m[s] = voter(s) ? rmatch(s) : 0;
+    for (u32 s = 0; s < N; s++) m[s] = (voter(s) || is_wit(s)) ? rmatch(s) : 0;
     // odd-even transposition sort (fully unrolled for a compile-time N)
     for (u32 pass = 0; pass < N; pass++) {
       for (u32 i = pass & 1u; i + 1 < N; i += 2) {
@@ -1182,7 +1321,8 @@ struct Lane {
       Msg m = mk(M_InstallSnapshot, (u8)(slot + 1));
       m.log_index = si;
       m.log_term = sp.ss_term;
-      m.pad0 = sp.ss_rem;  // Snapshot.Membership: the voters it lists (removed mask)
+      m.pad0 = sp.ss_rem;  // Snapshot.Membership: the slots not in Addresses,
+      m.pad1 = (u32)sp.ss_obs | ((u32)sp.ss_wit << 8);  // its Observers and Witnesses
       become_snapshot(slot, si);
       const u32 bit = 1u << slot;
       snp_pend |= (u8)bit;
@@ -1200,7 +1340,9 @@ struct Lane {
     if (next <= last) {
       u64 cnt = limit_count(next, last);
       u32 off = 0;
-      if (arena_log_range(next, (u32)cnt, &off)) {
+      const bool ok = ((wit >> slot) & 1u) ? arena_meta_range(next, (u32)cnt, &off)
+                                           : arena_log_range(next, (u32)cnt, &off);
+      if (ok) {
         m.n_ent = (u16)cnt;
         m.ent_off = off;
       }
@@ -1210,8 +1352,8 @@ struct Lane {
   }
   // Fan-out sends are deferred to the single post-event site in run() (same
   // emission order: every handler requests them as its last action).
-  RBE_HD void broadcast_replicate() {  // raft.go:794-808 (r.nodes(): the voting members)
-    rep_mask |= voters_mask() & ~(1u << k);
+  RBE_HD void broadcast_replicate() {  // raft.go:794-808 (r.nodes(): remotes, observers, witnesses)
+    rep_mask |= (voters_mask() | obs | wit) & ~(1u << k);
   }
   RBE_HD void request_replicate(u32 slot) { rep_mask |= 1u << slot; }  // sendReplicateMessage
   RBE_HD void send_heartbeat(u32 slot, u64 low, u64 high) {  // raft.go:810-820
@@ -1403,7 +1545,7 @@ struct Lane {
   RBE_HD bool leader_has_quorum() {  // raft.go:378-388 (votingMembers)
     u32 c = 0;
     for (u32 s = 0; s < N; s++) {
-      if (!voter(s)) continue;
+      if (!((vmask() >> s) & 1u)) continue;  // votingMembers
       if (s == k || ractive(s)) {
         c++;
         set_active(s, false);
@@ -1479,7 +1621,7 @@ struct Lane {
           t_last = tl;
           saved_to = umin64(saved_to, conflict - 1);
           if (imark_on(C) && conflict <= P.imark[r]) P.imark[r] = conflict;
-          seg_len = 0;
+          seg_len = mseg_len = 0;
         }
       }
       u64 last_idx = m.log_index + m.n_ent;
@@ -1500,6 +1642,13 @@ struct Lane {
     const u64 si = m.log_index, st = m.log_term;
     bool restored = false;
     if (si > committed) {
+      // restore (raft.go:444-459): a snapshot listing this node as an observer
+      // or a witness it is not panics
+      const u32 sobs = m.pad1 & 0xFFu, swit = (m.pad1 >> 8) & 0xFFu;
+      if ((role != R_Observer && ((sobs >> k) & 1u)) || (role != R_Witness && ((swit >> k) & 1u))) {
+        set_fault(F_PANIC);
+        return;
+      }
       if (match_term(si, st)) {
         commit_to(si);
       } else if (!C.snapshot_entries) {
@@ -1515,12 +1664,14 @@ struct Lane {
         sp.ss_index = si;  // LogDB.ApplySnapshot (after the step's Update)
         sp.ss_term = st;
         sp.ss_rem = (u8)(m.pad0 & MB_REMOVED);  // and its membership
+        sp.ss_obs = (u8)(m.pad1 & 0xFFu);
+        sp.ss_wit = (u8)((m.pad1 >> 8) & 0xFFu);
         if (rl_on()) {  // inMemory.restore (inmemory.go:236-246)
           P.imark[r] = si + 1;
           P.rl[r].new_ent = 1;
           P.rl[r].size = 0;
         }
-        seg_len = 0;
+        seg_len = mseg_len = 0;
         snap_restored = true;
         restored = true;
       }
@@ -1560,7 +1711,7 @@ struct Lane {
     }
     u64 lt = log_term(last);
     for (u32 s = 0; s < N; s++) {
-      if (s == k || !voter(s)) continue;
+      if (s == k || !((vmask() >> s) & 1u)) continue;  // votingMembers
       Msg m = mk(M_RequestVote, (u8)(s + 1));
       m.term = term;
       m.log_index = last;
@@ -1622,7 +1773,8 @@ struct Lane {
       P.rl[r].tick++;  // rl.HeartbeatTick
       send_rate_limit();
     }
-    if (voter(k) && etick >= ret) {  // !selfRemoved() && timeForElection()
+    // non-voting members and witnesses never campaign (raft.go:577-581)
+    if (role != R_Observer && role != R_Witness && voter(k) && etick >= ret) {  // !selfRemoved() && timeForElection()
       etick = 0;
       // Handle(Election): term 0 passes the gate; handled in any role
       if constexpr (FULL) on_election();
@@ -1725,7 +1877,9 @@ struct Lane {
       }
       if (m.term > term) {
         u8 lid = is_leader_message(m.type) ? m.from : (u8)0;
-        become_follower(m.term, lid);
+        // an observer / a witness keeps its state (raft.go:1430-1436)
+        if (role == R_Observer || role == R_Witness) become_nonvoting(m.term, lid);
+        else become_follower(m.term, lid);
       } else {
         if (is_leader_message(m.type) && C.check_quorum) {
           Msg x = mk(M_NoOP, m.from);
@@ -1788,7 +1942,7 @@ struct Lane {
             on_install_snapshot(m);
             return;
           case M_ConfigChangeEvent: on_config_change(m); return;
-          case M_SnapshotReceived: restore_remotes((u8)m.hint); return;  // raft.go:1566
+          case M_SnapshotReceived: restore_remotes((u32)m.hint); return;  // raft.go:1566
           default: return;
         }
       case R_Candidate:
@@ -1814,7 +1968,7 @@ struct Lane {
             on_install_snapshot(m);
             return;
           case M_ConfigChangeEvent: on_config_change(m); return;
-          case M_SnapshotReceived: restore_remotes((u8)m.hint); return;  // raft.go:1566
+          case M_SnapshotReceived: restore_remotes((u32)m.hint); return;  // raft.go:1566
           default: return;
         }
       case R_Leader:
@@ -1847,7 +2001,7 @@ struct Lane {
           case M_Election: return;        // leader ignores Election
           case M_RequestVote: on_request_vote(m); return;
           case M_ConfigChangeEvent: on_config_change(m); return;
-          case M_SnapshotReceived: restore_remotes((u8)m.hint); return;  // raft.go:1566
+          case M_SnapshotReceived: restore_remotes((u32)m.hint); return;  // raft.go:1566
           case M_RateLimit:  // handleLeaderRateLimit (raft.go:1779-1785)
             if (rl_on() && m.from >= 1 && m.from <= N) {
               RlSt& s = P.rl[r];
@@ -1856,6 +2010,74 @@ struct Lane {
               s.f_size[m.from - 1u] = m.hint;
             }
             return;  // rl disabled: dropped
+          default: return;
+        }
+      case R_Observer:  // raft.go:2084-2092: the follower handlers for the data path
+        switch (m.type) {
+          case M_Heartbeat:  // handleObserverHeartbeat
+            etick = 0;
+            leader = m.from;
+            on_heartbeat(m);
+            return;
+          case M_Replicate:  // handleObserverReplicate
+            etick = 0;
+            leader = m.from;
+            on_replicate(m, ents);
+            return;
+          case M_InstallSnapshot:  // handleObserverSnapshot
+            etick = 0;
+            leader = m.from;
+            on_install_snapshot(m);
+            return;
+          case M_Propose:  // handleObserverPropose
+            if (leader == 0) {
+              report_dropped_proposal(ents, m.n_ent);
+            } else {
+              Msg f = m;
+              f.to = leader;
+              u32 off = 0;
+              if (m.n_ent && arena_put(ents, m.n_ent, &off)) f.ent_off = off;
+              send(f);
+            }
+            return;
+          case M_ReadIndex:  // handleObserverReadIndex
+            if (leader == 0) {
+              report_dropped_read_index(m.hint, m.hint_high);
+            } else {
+              Msg f = m;
+              f.to = leader;
+              send(f);
+            }
+            return;
+          case M_ReadIndexResp:  // handleObserverReadIndexResp
+            etick = 0;
+            leader = m.from;
+            add_ready_to_read(m.log_index, m.hint, m.hint_high);
+            return;
+          case M_ConfigChangeEvent: on_config_change(m); return;
+          case M_SnapshotReceived: restore_remotes((u32)m.hint); return;
+          default: return;
+        }
+      case R_Witness:  // raft.go:2093-2097
+        switch (m.type) {
+          case M_Heartbeat:  // handleWitnessHeartbeat
+            etick = 0;
+            leader = m.from;
+            on_heartbeat(m);
+            return;
+          case M_Replicate:  // handleWitnessReplicate
+            etick = 0;
+            leader = m.from;
+            on_replicate(m, ents);
+            return;
+          case M_InstallSnapshot:  // handleWitnessSnapshot
+            etick = 0;
+            leader = m.from;
+            on_install_snapshot(m);
+            return;
+          case M_RequestVote: on_request_vote(m); return;
+          case M_ConfigChangeEvent: on_config_change(m); return;
+          case M_SnapshotReceived: restore_remotes((u32)m.hint); return;
           default: return;
         }
       default:
@@ -1973,6 +2195,7 @@ struct Lane {
   // MB_CC_IN_LOG is dropped once (processed, last] holds no ConfigChange.
   RBE_HD void membership_after_update(const Upd& u) {
     if (!C.ext_apply && u.apply_hi >= u.apply_lo) {
+      u32 ms = pack_ms(members & MB_REMOVED, obs, wit);  // raft's, as accepted changes go by
       for (u64 i = u.apply_lo; i <= u.apply_hi; i++) {
         if (last - i >= C.ring) break;  // F_WINDOW already raised by the apply
         const Body b = P.pay_ring[ring_slot(i)];
@@ -1984,11 +2207,14 @@ struct Lane {
           set_fault(F_UNSUPPORTED);  // not a ConfigChange the engine can decode
           continue;
         }
+        if (!cc_accepted(ms, t, nid, N)) {
+          cc_apply = (u8)(CCA_VALID | CCA_REJECT);
+          continue;
+        }
         cc_apply = (u8)(CCA_VALID | (t << 3) | (u32)nid);
-        // the state machine's own membership (rsm membership.go: addNode /
-        // removeNode), which the next snapshot records
-        if (t == CC_AddNode && nid >= 1) sm_rem &= (u8)~(1u << (nid - 1));
-        if (t == CC_RemoveNode && nid >= 1) sm_rem |= (u8)(1u << (nid - 1));
+        ms_apply(ms, t, nid, N);
+        // the state machine's own membership, which the next snapshot records
+        ms_apply(sm_ms, t, nid, N);
       }
     }
     if (members & MB_CC_IN_LOG) {
@@ -2017,7 +2243,7 @@ struct Lane {
     // the state machine recovered from the snapshot: its membership is the
     // snapshot's, and the node restores raft's remotes from it at the next
     // step (RestoreRemotes, rsm/statemachine.go:236); the last step's is done
-    sm_rem = snap_restored ? sp.ss_rem : sm_rem;
+    if (snap_restored) sm_ms = pack_ms(sp.ss_rem, sp.ss_obs, sp.ss_wit);
     sp.rr_pend = (u8)(snap_restored && C.membership && !C.ext_apply ? 1 : 0);
     sp.marker = marker;
     sp.marker_term = marker_term;
@@ -2039,13 +2265,17 @@ struct Lane {
       if (t != 0) {
         sp.ss_index = la;
         sp.ss_term = t;
-        sp.ss_rem = sm_rem;  // Snapshot.Membership: the state machine's at la
+        sp.ss_rem = (u8)(sm_ms & 0xFFu);  // Snapshot.Membership: the state machine's at la
+        sp.ss_obs = (u8)((sm_ms >> 8) & 0xFFu);
+        sp.ss_wit = (u8)((sm_ms >> 16) & 0xFFu);
         sp.compact_to = la > C.compaction_overhead ? la - C.compaction_overhead : 0;
       }
     }
     sp.pend = snp_pend;
     sp.pend_rej = snp_rej;
-    sp.sm_rem = sm_rem;
+    sp.sm_rem = (u8)(sm_ms & 0xFFu);
+    sp.sm_obs = (u8)((sm_ms >> 8) & 0xFFu);
+    sp.sm_wit = (u8)((sm_ms >> 16) & 0xFFu);
     P.snp[r] = sp;
     marker = sp.marker;
     marker_term = sp.marker_term;
@@ -2083,6 +2313,13 @@ struct Lane {
     rq_count = c.rq_count;
     members = c.members;
     cc_apply = c.cc_apply;
+    roles0 = (u8)(members & MB_ROLES);
+    obs = wit = 0;
+    if (roles0) {
+      const u16 x = P.roles[r];
+      obs = (u8)(x & 0xFFu);
+      wit = (u8)(x >> 8);
+    }
   }
   RBE_HD void store() {
     Hot h;
@@ -2111,6 +2348,9 @@ struct Lane {
     c.ltt = ltt;
     c.rq_head = rq_head;
     c.rq_count = rq_count;
+    // MB_ROLES: the replica has observers or witnesses (Planes::roles)
+    members = (u8)((members & ~MB_ROLES) | ((obs | wit) ? MB_ROLES : 0u));
+    if (C.membership && (roles0 || (obs | wit))) P.roles[r] = (u16)(obs | ((u16)wit << 8));
     c.members = members;
     c.cc_apply = cc_apply;
     c.pad = 0;
@@ -2151,11 +2391,11 @@ struct Lane {
     u8 pend0 = 0, pend_rej0 = 0;
     marker = marker_term = 0;
     applied0 = C.ext_apply ? P.applied[r] : processed;
-    // RestoreRemotes due at this step (bit 8 | the removed mask): the state
-    // machine recovered from a received snapshot at the end of the last step
-    // (SnapSt::rr_pend), or the host calls it (EXT_RESTORE, below)
+    // RestoreRemotes due at this step (bit 31 | the packed membership): the
+    // state machine recovered from a received snapshot at the end of the last
+    // step (SnapSt::rr_pend), or the host calls it (EXT_RESTORE, below)
     u32 restore = 0;
-    sm_rem = 0;
+    sm_ms = 0;
     if (C.snapshot_entries) {
       const SnapSt& sp = P.snp[r];
       marker = sp.marker;
@@ -2165,13 +2405,15 @@ struct Lane {
       // the state machine recovered from the LogDB's snapshot (with ext_apply
       // the host reports what its state machine has applied)
       if (!C.ext_apply) applied0 = umax64(applied0, sp.ss_index);
-      sm_rem = sp.sm_rem;
-      if (sp.rr_pend) restore = 0x100u | sp.ss_rem;
+      sm_ms = pack_ms(sp.sm_rem, sp.sm_obs, sp.sm_wit);
+      if (sp.rr_pend) restore = 0x80000000u | pack_ms(sp.ss_rem, sp.ss_obs, sp.ss_wit);
     }
     pc_lo = pc_hi = 0;
     arena_used = 0;
     seg_lo = 0;
     seg_off = seg_len = 0;
+    mseg_lo = 0;
+    mseg_off = mseg_len = 0;
     msg_hash = rtr_hash = drop_hash = 0;
     n_msgs = n_rtr = n_drop_ent = n_drop_ri = 0;
     q_new = false;
@@ -2197,9 +2439,20 @@ struct Lane {
     u32 cc_type = 0;
     u64 cc_node = 0;
     if (C.membership && C.cc_period && role == R_Leader && cc_selected(C, cid, round)) {
+      // (oracle/harness.cpp step_replica): a voter is removed while more than
+      // two are in raft.remotes, and added back; an observer slot's node is
+      // added as an observer, then promoted and kept; a witness slot's node is
+      // added as a witness and removed again
       cc_node = cc_target(C, cid, round);
-      const bool v = voter((u32)cc_node - 1u);
-      if (!v || popc8(voters_mask()) > 2) {
+      const u32 s = (u32)cc_node - 1u;
+      const bool v = voter(s), big = popc8(voters_mask()) > 2;
+      if ((C.obs_slots >> s) & 1u) {
+        if (is_obs(s)) do_cc = true, cc_type = CC_AddNode;
+        else if (!v) do_cc = true, cc_type = CC_AddObserver;
+      } else if ((C.wit_slots >> s) & 1u) {
+        if (!is_wit(s)) do_cc = true, cc_type = CC_AddWitness;
+        else if (big) do_cc = true, cc_type = CC_RemoveNode;
+      } else if (!v || big) {
         do_cc = true;
         cc_type = v ? CC_RemoveNode : CC_AddNode;
       }
@@ -2242,7 +2495,7 @@ struct Lane {
         }
         if (ext.flags & EXT_CC_APPLY) cc_apply = (u8)ext.pad[1];
         // the host's RestoreRemotes (it comes after the device's own, which it replaces)
-        if (ext.flags & EXT_RESTORE) restore = 0x100u | (u32)(ext.pad[2] & MB_REMOVED);
+        if (ext.flags & EXT_RESTORE) restore = 0x80000000u | (u32)(ext.pad[2] & 0xFFFFFFu);
       }
     }
     if (pend0) {
@@ -2305,7 +2558,7 @@ struct Lane {
       if (phase == 9) {  // Handle(SnapshotReceived) with the snapshot's membership
         phase = cc_apply ? 8u : phase0;
         m = mk(M_SnapshotReceived, self);
-        m.hint = restore & 0xFFu;
+        m.hint = restore & 0xFFFFFFu;
         kind = 2;
       } else if (phase == 8) {
         phase = phase0;
@@ -2470,17 +2723,23 @@ struct Lane {
             q_record_activity(m.type);
           // Peer.Handle (peer.go:186-198): a response from a node that is not a
           // member of this replica's view is dropped
-          if (C.membership && is_response_message(m.type) && !voter(m.from - 1u)) deliver = false;
+          if (C.membership && is_response_message(m.type) && !from_member(m.from)) deliver = false;
         }
         if (deliver) handle(m, ents);
       }
       // deferred fan-out, in the reference's emission order
+      // remotes, then observers, then witnesses, each ascending (raft.go:390-402 nodes())
 #pragma unroll 1
-      while (rep_mask) {
-        const u32 s = (u32)__builtin_ctz(rep_mask);
-        rep_mask &= rep_mask - 1u;
-        send_replicate(s);
+      for (u32 cls = 0; cls < 3 && rep_mask; cls++) {
+        u32 mk_ = rep_mask & (cls == 0 ? voters_mask() : (cls == 1 ? (u32)obs : (u32)wit));
+        rep_mask &= ~mk_;
+        while (mk_) {
+          const u32 s = (u32)__builtin_ctz(mk_);
+          mk_ &= mk_ - 1u;
+          send_replicate(s);
+        }
       }
+      rep_mask = 0;
       if (tn_to) {
         Msg t = mk(M_TimeoutNow, tn_to);
         tn_to = 0;
@@ -2489,8 +2748,12 @@ struct Lane {
       if (hb_pending) {
         hb_pending = false;
 #pragma unroll 1
+        // votingMembers with the ctx, then observers when it is empty (raft.go:834-846)
         for (u32 s = 0; s < N; s++)
-          if (s != k && voter(s)) send_heartbeat(s, hb_lo, hb_hi);
+          if (s != k && ((vmask() >> s) & 1u)) send_heartbeat(s, hb_lo, hb_hi);
+        if (hb_lo == 0 && hb_hi == 0)
+          for (u32 s = 0; s < N; s++)
+            if (is_obs(s)) send_heartbeat(s, 0, 0);
         ctr.v[C_REMOTE_TOUCH] += N - 1;
       }
       if (rq_pending) {
@@ -2666,7 +2929,10 @@ RBE_HD u32 boot_removed(const Params& C, u32 k) {
 // draws another; one config-change entry per initial voter at term 1,
 // committed; remotes {match 0, next V+1}.  A slot beyond the initial voters is
 // a node that joins later (node.go:280-292, no peers, initial = false): term
-// 1, an empty log, no remotes.
+// 1, an empty log, no remotes; one started as an observer or a witness
+// (config.IsObserver / IsWitness: newRaft's becomeObserver / becomeWitness,
+// raft.go:274-281, and no becomeFollower(1), peer.go:71-73) stays at term 0
+// with its one randomized timeout.
 template <int N>
 RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   const u32 k = (u32)(r % N);
@@ -2674,20 +2940,22 @@ RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   const u64 self = k + 1;
   const bool boot = k < C.n_voters;
   const u32 V = boot ? C.n_voters : 0u;  // bootstrap entries in this replica's log
+  const bool nv = ((C.obs_slots | C.wit_slots) >> k) & 1u;  // a non-voting start
   Hot h;
-  h.role = R_Follower;
+  h.role = ((C.obs_slots >> k) & 1u) ? R_Observer : (((C.wit_slots >> k) & 1u) ? R_Witness : R_Follower);
   h.flags = boot ? HF_APPLY_PENDING : (u8)0;  // the bootstrap entries are saved and applied in round 0
   h.votes_resp = h.votes_granted = 0;
   h.election_tick = 0;
   h.heartbeat_tick = 0;
-  u64 rt = below(rto_rand(C.seed, cid, self, 1), C.election_rtt);  // the second draw wins
+  // the second draw wins (becomeFollower(0) then (1)); an observer / a witness draws once
+  u64 rt = below(rto_rand(C.seed, cid, self, nv ? 0 : 1), C.election_rtt);
   h.rand_et = (u16)(C.election_rtt + rt);
   h.q_tick = h.q_quiesced_since = h.q_no_activity_since = h.q_exit_quiesce_tick = 0;
-  h.rng_count = 2;
+  h.rng_count = nv ? 1 : 2;
   P.hot[r] = h;
   P.idle[r] = idle_byte(C, h.role, h.flags, 0);
   Core c;
-  c.term = 1;
+  c.term = nv ? 0 : 1;
   c.committed = V;
   c.last_index = V;
   c.processed = 0;
@@ -2765,7 +3033,7 @@ template <int N>
 RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, u64 vote,
                              u64 commit, u64 last, u32 n, const u64* t, const Body* b, u32 ppar,
                              u32 tclk, u64 marker = 0, u64 marker_term = 0, u64 ss_index = 0,
-                             u64 ss_term = 0, u8 removed = 0) {
+                             u64 ss_term = 0, u32 removed = 0) {
   const u32 k = (u32)(r % N);
   const u64 g = r / N;
   const u64 cid = cid_of(C, g);
@@ -2778,7 +3046,10 @@ RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, 
     sp.marker_term = marker_term;
     sp.ss_index = ss_index;
     sp.ss_term = ss_term;
-    sp.ss_rem = sp.sm_rem = removed;  // the snapshot's membership; the state machine recovers it
+    // the snapshot's membership; the state machine recovers it
+    sp.ss_rem = sp.sm_rem = (u8)(removed & 0xFFu);
+    sp.ss_obs = sp.sm_obs = (u8)((removed >> 8) & 0xFFu);
+    sp.ss_wit = sp.sm_wit = (u8)((removed >> 16) & 0xFFu);
     sp.rr_pend = 0;
     if (sp.compact_to || sp.pend) snap_flags |= HF_SNAP_WORK;
     if (ss_index && !C.ext_apply) snap_flags |= HF_APPLIED_NEW;  // recovered: confirmedIndex 0 lags it
@@ -2787,7 +3058,12 @@ RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, 
     if (marker) P.term_ring[(marker & (u64)(C.ring - 1)) * C.n_rep + r] = marker_term;
   }
   Hot h;
-  h.role = R_Follower;
+  // newRaft in the node's configured state (raft.go:274-281): a witness slot's
+  // node is a witness, an observer slot's node an observer until it has been
+  // promoted into Addresses
+  h.role = ((C.wit_slots >> k) & 1u) ? R_Witness
+           : (((C.obs_slots >> k) & 1u) && ((removed >> k) & 1u)) ? R_Observer
+                                                                 : R_Follower;
   h.flags = (u8)((commit > marker ? HF_APPLY_PENDING : 0u) | (faulted ? HF_FAULTED : 0u) |
                  snap_flags);
   h.votes_resp = h.votes_granted = 0;
@@ -2819,7 +3095,9 @@ RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, 
   // its snapshot's membership, raft.go:260-270; every slot a voter without one,
   // as oracle/harness.cpp harness_restart)
   if (C.membership) {
-    c.members = (u8)(removed & MB_REMOVED);
+    const u16 roles = (u16)(((removed >> 8) & 0xFFu) | (((removed >> 16) & 0xFFu) << 8));
+    c.members = (u8)((removed & MB_REMOVED) | (roles ? MB_ROLES : 0u));
+    P.roles[r] = roles;
     for (u32 i = 0; i < n; i++)
       if (ent_type(b[i].type) == E_ConfigChange) c.members |= MB_CC_IN_LOG;
   }

@@ -56,10 +56,6 @@ enum : u32 {
   F_PANIC = 1u << 5,        // a reference panic condition (e.g. commitTo > lastIndex)
   F_UNSUPPORTED = 1u << 6,  // a slow-path message/entry type reached the device
   F_DROPLIST = 1u << 7,     // dropped-ReadIndex output list full
-  // not a fault: an observer or witness joined the replica's membership, which
-  // the device does not step; the host takes the group over (rbe_export_groups
-  // / its own slow path / rbe_import_groups).  The replica's view is unchanged.
-  F_HANDOFF = 1u << 8,
 };
 
 // hot plane: everything a quiesced tick touches (32 B per replica)
@@ -95,7 +91,8 @@ enum : u8 {
 
 // Core::members / Core::cc_apply bits
 enum : u8 {
-  MB_REMOVED = 0x7F,   // slots that are not voting members (bit s = slot s)
+  MB_REMOVED = 0x3F,   // slots that are not in raft.remotes (bit s = slot s, kMaxN = 6)
+  MB_ROLES = 0x40,     // some slot is an observer or a witness (Planes::roles)
   MB_CC_IN_LOG = 0x80,
   CCA_VALID = 0x80, CCA_REJECT = 0x40,  // cc_apply: node id bits 0-2, ConfigChangeType bits 3-5
 };
@@ -148,7 +145,10 @@ struct alignas(16) SnapSt {
   u64 ss_req, compact_to;
   u8 pend, pend_rej;
   u8 ss_rem, sm_rem, rr_pend;
-  u8 pad[11];
+  // observers / witnesses of the snapshot's and the state machine's membership
+  // (Membership.Observers / Witnesses, bit s = slot s)
+  u8 ss_obs, ss_wit, sm_obs, sm_wit;
+  u8 pad[7];
 };
 
 // remote slot (remote.go:62-69): match/next; state|active<<2 lives in a u8 plane
@@ -299,6 +299,8 @@ struct Params {
   u64 max_entry_size;
   u32 n;              // replica slots per group (N)
   u32 n_voters;       // slots 0..n_voters-1 bootstrap the group, the rest join later
+  u32 obs_slots;      // slots (beyond n_voters) whose nodes start as observers (config.IsObserver)
+  u32 wit_slots;      // ... as witnesses (config.IsWitness)
   u32 ring;           // term/payload ring entries (power of two)
   u32 rq_cap;         // readIndex queue capacity
   u32 maxm;           // message slots per (sender, dest) per round
@@ -402,7 +404,11 @@ struct Planes {
   // null: slot s is node s + 1.  Only the boundary's converters read it: the
   // protocol state inside the engine names nodes by slot + 1
   const u64* node_ids;
-  u32 ids_n;          // slots per group (Params::n), for indexing node_ids in kernels without Params
+  u32 ids_n;
+  // [n_rep] (membership) each replica's observers | witnesses << 8, bit s =
+  // slot s: raft.observers / raft.witnesses (raft.go:206-207), read by the full
+  // handler table only (Core::members has MB_ROLES while any is set)
+  u16* roles;          // slots per group (Params::n), for indexing node_ids in kernels without Params
 };
 
 }  // namespace rbe

@@ -340,8 +340,11 @@ int messages_to_records(const Params& C, HostHeap& heap, u32 round, u64 n, const
       x.m.hint = m.hint;
       x.m.hint_high = m.hint_high;
       // an InstallSnapshot's snapshot membership (rbe_message.reserved, msg_reserved)
-      if (m.type == M_InstallSnapshot) x.m.pad0 = (u16)(m.reserved & MB_REMOVED);
-      if (m.type == M_InstallSnapshot && (m.reserved >> N)) return RBE_E_INVALID;
+      if (m.type == M_InstallSnapshot) {
+        if (!ms_valid(m.reserved, N)) return RBE_E_INVALID;
+        x.m.pad0 = (u16)(m.reserved & 0xFFu);
+        x.m.pad1 = (m.reserved >> 8) & 0xFFFFu;
+      }
       if (m.type == M_Replicate) {
         x.slot = na;
         w += 1u;

@@ -47,7 +47,8 @@ class RbeConfig(C.Structure):
                 ("heap_bytes", C.c_uint64), ("ext_commit", C.c_uint32),
                 ("membership", C.c_uint32), ("cc_period", C.c_uint32), ("cc_mod", C.c_uint32),
                 ("rep_compact", C.c_uint32), ("n_voters", C.c_uint32),
-                ("max_inmem_log_size", C.c_uint64)]
+                ("max_inmem_log_size", C.c_uint64), ("observer_slots", C.c_uint32),
+                ("witness_slots", C.c_uint32)]
 
 
 class RbeReplicaView(C.Structure):
@@ -62,7 +63,8 @@ class RbeReplicaView(C.Structure):
                 ("votes_resp", C.c_uint32), ("votes_granted", C.c_uint32),
                 ("match", C.c_uint64 * 8), ("next", C.c_uint64 * 8),
                 ("rstate", C.c_uint32 * 8), ("ractive", C.c_uint32 * 8),
-                ("events", C.c_uint32), ("removed", C.c_uint32)]
+                ("events", C.c_uint32), ("removed", C.c_uint32),
+                ("observers", C.c_uint32), ("witnesses", C.c_uint32)]
 
 
 def _np_dtype(struct):
@@ -337,7 +339,8 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                 snapshot_entries: int = 0, compaction_overhead: int = 0,
                 ext_commit: bool = False, membership: bool = False, cc_period: int = 0,
                 cc_mod: int = 1, rep_compact: bool = False,
-                max_inmem_log_size: int = 0, n_voters: int = 0) -> RbeConfig:
+                max_inmem_log_size: int = 0, n_voters: int = 0, observer_slots: int = 0,
+                witness_slots: int = 0) -> RbeConfig:
     return RbeConfig(abi_version=RBE_ABI_VERSION, device=device, n_groups=n_groups,
                      n_replicas=n_replicas, election_rtt=election_rtt,
                      heartbeat_rtt=heartbeat_rtt, check_quorum=int(check_quorum),
@@ -354,7 +357,8 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                      compaction_overhead=compaction_overhead, ext_commit=int(ext_commit),
                      membership=int(membership), cc_period=cc_period, cc_mod=cc_mod,
                      rep_compact=int(rep_compact), max_inmem_log_size=max_inmem_log_size,
-                     n_voters=n_voters)
+                     n_voters=n_voters, observer_slots=observer_slots,
+                     witness_slots=witness_slots)
 
 
 class InputError(EngineError):
@@ -574,11 +578,16 @@ class NodeInputs:
         _check_input(self._input("apply_config_change", len(replicas), _u64s(replicas),
                                  _u64s(nodes), u32a), "rbe_apply_config_change")
 
-    def restore_remotes(self, replicas, voters):
+    def restore_remotes(self, replicas, voters, observers=None, witnesses=None):
         """Peer.RestoreRemotes (rbe_restore_remotes; cfg.membership): replicas[i]'s
-        snapshot membership lists the node ids voters[i] (peer.go:159-165)."""
-        n = [len(v) for v in voters]
-        ids = [x for v in voters for x in v]
+        snapshot membership lists the node ids voters[i], observers[i] and
+        witnesses[i] (peer.go:159-165)."""
+        obs = observers or [[] for _ in voters]
+        wit = witnesses or [[] for _ in voters]
+        n, ids = [], []
+        for v, o, w in zip(voters, obs, wit):
+            n += [len(v), len(o), len(w)]
+            ids += list(v) + list(o) + list(w)
         u32a = (C.c_uint32 * max(1, len(n)))(*n)
         _check_input(self._input("restore_remotes", len(replicas), _u64s(replicas), u32a,
                                  _u64s(ids)), "rbe_restore_remotes")

@@ -56,11 +56,6 @@ extern "C" {
 #define RBE_FAULT_PANIC 0x20u
 #define RBE_FAULT_UNSUPPORTED 0x40u
 #define RBE_FAULT_DROPLIST 0x80u
-/* not a protocol fault: an observer or witness joined the replica's membership
- * (AddObserver / AddWitness), which the device does not step; the host takes
- * the group over (rbe_export_groups, its own slow path, rbe_import_groups).
- * rbe_fault_summary counts it apart from the faults. */
-#define RBE_FAULT_HANDOFF 0x100u
 
 /* counter slots (rbe_get_counters) */
 enum rbe_counter {
@@ -183,6 +178,12 @@ typedef struct rbe_config {
    * in-memory log bytes; 0 (or UINT64_MAX) = off.  Rate-limited engines step
    * every ticking replica on the full handler table. */
   uint64_t max_inmem_log_size;
+  /* the slots beyond n_voters whose nodes start as observers (config.IsObserver)
+   * or witnesses (config.IsWitness), bit (id-1); they take part once an
+   * AddObserver / AddWitness for them is applied (raft.go:1159-1180).  Needs
+   * cfg.membership. */
+  uint32_t observer_slots;
+  uint32_t witness_slots;
 } rbe_config;
 
 /* Snapshot of one replica (tests, debugging, rbe_get_views). */
@@ -194,7 +195,8 @@ typedef struct rbe_replica_view {
   uint64_t match[8], next[8];
   uint32_t rstate[8], ractive[8];
   uint32_t events;  /* RBE_EV_* of the last round's step (0 when it made no step) */
-  uint32_t removed; /* bit (id-1): not a voting member in this replica's view (cfg.membership) */
+  uint32_t removed; /* bit (id-1): not in this replica's raft.remotes (cfg.membership) */
+  uint32_t observers, witnesses; /* bit (id-1): raft.observers / raft.witnesses */
 } rbe_replica_view;
 
 /* Per-replica step result: the Update of peer.go:201-207 / raftpb Update
@@ -274,9 +276,10 @@ typedef struct rbe_launch_state {
   uint64_t term, vote, commit, last_index;
   uint32_t n_entries;
   /* the membership the restarted raft reads from the LogDB (logdb NodeState =
-   * its latest snapshot's, raft.go:260-270), as the node ids that are not
-   * voting members: bit (id-1); needs cfg.membership when non-zero.  With
-   * snapshots it is also the snapshot's and the state machine's membership. */
+   * its latest snapshot's, raft.go:260-270): bits 0-7 the slots not in
+   * Membership.Addresses, 8-15 its Observers, 16-23 its Witnesses, bit s =
+   * slot s; needs cfg.membership when non-zero.  With snapshots it is also the
+   * snapshot's and the state machine's membership. */
   uint32_t removed;
   uint64_t marker, marker_term, snapshot_index, snapshot_term;
 } rbe_launch_state;
@@ -433,8 +436,9 @@ int rbe_reject_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica)
  * steps, checked whole (RBE_E_INVALID / RBE_E_STATE, nothing staged).
  *   rbe_snapshot_saved: the state machine's snapshot of replica[i] at index[i]
  *     (at most the applied index last reported with rbe_notify_applied) of
- *     term[i], listing the voters of removed[i] (bit (id-1): not a voter; null
- *     = all; non-zero needs cfg.membership), was saved and the LogDB took it
+ *     term[i], with the membership removed[i] (the packed form of
+ *     rbe_launch_state::removed; null = every slot a voter; non-zero needs
+ *     cfg.membership), was saved and the LogDB took it
  *     (LogReader.CreateSnapshot; one at or below the LogDB's latest is out of
  *     date and ignored).  A remote that needs entries the LogDB compacted away
  *     gets this snapshot by InstallSnapshot (raft.go:684-697).
@@ -450,16 +454,18 @@ int rbe_compact(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint64
 /* Peer.RestoreRemotes (peer.go:159-165 → raft.go:1566 handleRestoreRemote →
  * restoreRemotes, 472-517), what the node calls once its state machine has
  * recovered from a snapshot (rsm/statemachine.go:236 via node.go:241-264):
- * replica[i]'s snapshot membership lists n_voters[i] voting members, their
- * node ids (1..n_replicas, no repeats) next in voter_ids.  Before the replica's
- * next step raft's voters become exactly those, every remote restarts (match 0,
- * next lastIndex + 1; its own match lastIndex), and a leader the snapshot does
- * not list steps down.  Staged like the inputs above (one per replica per
- * step; the engine's own RestoreRemotes after an InstallSnapshot it restored
- * runs first and is replaced by this one).  Needs cfg.membership and
- * cfg.ext_inputs (RBE_E_STATE). */
+ * replica[i]'s snapshot membership lists counts[3i] voters (Addresses),
+ * counts[3i + 1] observers and counts[3i + 2] witnesses, their node ids next in
+ * `ids` in that order (each a node of the group, none twice).  Before the
+ * replica's next step raft's remotes / observers / witnesses become exactly
+ * those, every remote restarts (match 0, next lastIndex + 1; its own match
+ * lastIndex), an observer listed as a voter becomes a follower and a leader
+ * the snapshot does not list steps down.  Staged like the inputs above (one per
+ * replica per step; the engine's own RestoreRemotes after an InstallSnapshot
+ * it restored runs first and is replaced by this one).  Needs cfg.membership
+ * and cfg.ext_inputs (RBE_E_STATE). */
 int rbe_restore_remotes(rbe_engine* e, uint64_t n, const uint64_t* replica,
-                        const uint32_t* n_voters, const uint64_t* voter_ids);
+                        const uint32_t* counts, const uint64_t* ids);
 
 /* Results of the last round.  Replaces Peer.GetUpdate (peer.go:201-207).
  * Peer.Commit (peer.go:282-293) consumes a step's outputs at the step; its log
@@ -629,8 +635,8 @@ int rbe_get_counters(rbe_engine* e, uint64_t* out /* RBE_CTR_NUM */);
 /* the counters one pipeline kernel (RBE_KERNEL_*) contributed */
 int rbe_get_kernel_counters(rbe_engine* e, int32_t kernel, uint64_t* out /* RBE_CTR_NUM */);
 int rbe_reset_counters(rbe_engine* e);
-/* number of replicas whose sticky fault word holds a fault (RBE_FAULT_HANDOFF
- * aside), and the OR of all words */
+/* number of replicas whose sticky fault word holds a fault, and the OR of all
+ * words */
 int rbe_fault_summary(rbe_engine* e, uint64_t* n_faulty, uint32_t* fault_or);
 
 /* Replica-per-GPU mode (cfg.rep_world > 1).  The engine steps

@@ -109,7 +109,7 @@ struct Node {
   // the state machine's membership (rsm membership: the ConfigChanges it
   // applied, or the snapshot it recovered from), as the slots that are not
   // voters, bit k; a snapshot records it (pb.Snapshot.Membership)
-  u32 sm_rem = 0;
+  u32 sm_rem = 0;  // packed (pack_ms): slots not in Addresses | Observers << 8 | Witnesses << 16
   // RestoreRemotes for the next step: the state machine recovered from a
   // received snapshot (rr_pend: the LogDB's snapshot), or the host calls it
   // (PUSH_RESTORE: x_rr_mask)
@@ -219,6 +219,8 @@ static std::string payload_cmd(u64 seed, u64 cid, u64 round) {
 static Config node_config(const HarnessConfig& cfg, u64 cid, u32 k) {
   Config c;
   c.nodeID = k + 1;
+  c.isObserver = ((cfg.observer_slots >> k) & 1u) != 0;
+  c.isWitness = ((cfg.witness_slots >> k) & 1u) != 0;
   c.clusterID = cid;
   c.electionRTT = cfg.election_rtt;
   c.heartbeatRTT = cfg.heartbeat_rtt;
@@ -230,21 +232,68 @@ static Config node_config(const HarnessConfig& cfg, u64 cid, u32 k) {
   return c;
 }
 
-// pb.Membership of a group's slots from a removed mask (bit k = node k + 1 is
-// not a voter), and back: the harness's node addresses are "node-<id>"
-static Membership membership_of(u32 rem, u32 n) {
+// A group's membership packed as slot masks (bit k = node k + 1): bits 0-7
+// the slots not in Addresses (the voters, raft.remotes), 8-15 Observers,
+// 16-23 Witnesses — the engine's rbe_launch_state::removed / snapshot-state
+// encoding.  pb.Membership of a packed word and back; the harness's node
+// addresses are "node-<id>".
+static u32 pack_ms(u32 rem, u32 obs, u32 wit) { return rem | (obs << 8) | (wit << 16); }
+static Membership membership_of(u32 ms, u32 n) {
   Membership m;
   for (u32 j = 0; j < n; j++) {
-    if ((rem >> j) & 1u) m.removed[j + 1] = true;
-    else m.addresses[j + 1] = "node-" + std::to_string(j + 1);
+    const std::string a = "node-" + std::to_string(j + 1);
+    if ((ms >> (8 + j)) & 1u) m.observers[j + 1] = a;
+    else if ((ms >> (16 + j)) & 1u) m.witnesses[j + 1] = a;
+    else if ((ms >> j) & 1u) m.removed[j + 1] = true;
+    else m.addresses[j + 1] = a;
   }
   return m;
 }
 static u32 removed_of(const Membership& m, u32 n) {
-  u32 rem = 0;
-  for (u32 j = 0; j < n; j++)
+  u32 rem = 0, obs = 0, wit = 0;
+  for (u32 j = 0; j < n; j++) {
     if (!m.addresses.count(j + 1)) rem |= 1u << j;
-  return rem;
+    if (m.observers.count(j + 1)) obs |= 1u << j;
+    if (m.witnesses.count(j + 1)) wit |= 1u << j;
+  }
+  return pack_ms(rem, obs, wit);
+}
+// Whether the state machine accepts a committed ConfigChange (rsm
+// membership.go:299-321 handleConfigChange), judged on the membership `ms`
+// (packed) raft holds when the entry is applied: an add of a node that already
+// is a voter, observer or witness is rejected — alreadyMember,
+// nodeBecomingObserver / Witness, witnessBecomingNode, observerBecomingWitness
+// — except AddNode of an observer (isPromotingObserver); removing the only
+// voter is rejected (isDeletingOnlyNode).  A rejected one goes back to raft as
+// RejectConfigChange.  (The stand-in keeps no Removed set, so re-adding a
+// removed node is accepted: the membership schedule relies on it.)
+static bool cc_accepted(u32 ms, int t, u64 nid, u32 n) {
+  if (nid < 1 || nid > n) return true;
+  const u32 b = 1u << (nid - 1), rem = ms & 0xFF, obs = (ms >> 8) & 0xFF, wit = (ms >> 16) & 0xFF;
+  const u32 voters = ((1u << n) - 1u) & ~rem;
+  if (t == RemoveNode) return !(voters == b);
+  if (t == AddNode && (obs & b)) return true;
+  return !((voters | obs | wit) & b);
+}
+// the state machine's membership after it applied a ConfigChange (rsm
+// membership.go applyConfigChange: AddNode also promotes an observer)
+static void ms_apply(u32& ms, int t, u64 nid, u32 n) {
+  if (nid < 1 || nid > n) return;
+  const u32 b = 1u << (nid - 1);
+  u32 rem = ms & 0xFF, obs = (ms >> 8) & 0xFF, wit = (ms >> 16) & 0xFF;
+  if (t == AddNode) {
+    rem &= ~b;
+    obs &= ~b;
+  } else if (t == RemoveNode) {
+    rem |= b;
+    obs &= ~b;
+    wit &= ~b;
+  } else if (t == AddObserver) {
+    obs |= b;
+  } else if (t == AddWitness) {
+    wit |= b;
+  }
+  ms = pack_ms(rem, obs, wit);
 }
 
 // the voters a node starts with (its bootstrap): the initial members for one of
@@ -266,6 +315,10 @@ Harness* harness_create(const HarnessConfig& cfg) {
   const u32 nv = cfg.n_voters ? cfg.n_voters : cfg.n_replicas;
   if (nv > cfg.n_replicas || (nv < cfg.n_replicas && !cfg.membership))
     panicf("n_voters must be 1..n_replicas (fewer only with membership)");
+  const u32 spare = ((1u << cfg.n_replicas) - 1u) & ~((1u << nv) - 1u);
+  if (((cfg.observer_slots | cfg.witness_slots) & ~spare) ||
+      (cfg.observer_slots & cfg.witness_slots))
+    panicf("observer / witness slots are disjoint spare slots (beyond n_voters)");
   Harness* h = new Harness();
   h->cfg = cfg;
   std::vector<std::pair<u64, std::string>> addrs;
@@ -279,6 +332,8 @@ Harness* harness_create(const HarnessConfig& cfg) {
       // node.go:280-292: the initial members bootstrap the group; the other
       // slots are nodes that join later (StartCluster with join: no peers,
       // initial = false, an empty log)
+      // a node that joins later may be an observer or a witness (config.IsObserver /
+      // IsWitness: newRaft starts it in that state, raft.go:274-281)
       if (k < nv) n->peer = Peer::Launch(c, &n->db, addrs, true, true);
       else n->peer = Peer::Launch(c, &n->db, {}, false, true);
       n->sm_rem = boot_removed(cfg, k);
@@ -322,9 +377,21 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
   int cc_type = nd->x_cc_type;
   u64 cc_node = nd->x_cc_node;
   if (!do_cc && cfg.membership && R->state == Leader && cc_selected(cfg, gr->cid, r)) {
+    // the seeded node: a voter is removed (while more than two are in
+    // raft.remotes) and added back; an observer slot's node is added as an
+    // observer, then promoted (AddNode) and kept; a witness slot's node is
+    // added as a witness and removed again (rbe_step.h cc_schedule)
     cc_node = cc_target(cfg, gr->cid, r);
+    const u32 b = 1u << (cc_node - 1);
     const bool voter = R->remotes.count(cc_node) > 0;
-    if (!voter || R->remotes.size() > 2) {
+    const bool big = R->remotes.size() > 2;
+    if (cfg.observer_slots & b) {
+      if (R->observers.count(cc_node)) do_cc = true, cc_type = AddNode;
+      else if (!voter) do_cc = true, cc_type = AddObserver;
+    } else if (cfg.witness_slots & b) {
+      if (!R->witnesses.count(cc_node)) do_cc = true, cc_type = AddWitness;
+      else if (big) do_cc = true, cc_type = RemoveNode;
+    } else if (!voter || big) {
       do_cc = true;
       cc_type = voter ? RemoveNode : AddNode;
     }
@@ -503,19 +570,31 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
     }
     // applyRaftUpdates: the harness state machine applies immediately; a
     // ConfigChange entry is handed back to raft at the next step (membership)
+    u32 raft_ms = 0;  // raft's membership as the accepted changes go by
+    bool have_ms = false;
     for (auto& e : ud.committed_entries) {
       applyHash = hash_entry(applyHash, e);
       int t;
       u64 nid;
       if (cfg.membership && !cfg.ext_apply && e.type == ConfigChangeEntry &&
           cc_decode(e.cmd, &t, &nid)) {
+        if (!have_ms) {
+          Membership m;
+          for (auto& kv : R->remotes) m.addresses[kv.first] = "";
+          for (auto& kv : R->observers) m.observers[kv.first] = "";
+          for (auto& kv : R->witnesses) m.witnesses[kv.first] = "";
+          raft_ms = removed_of(m, n);
+          have_ms = true;
+        }
         nd->cc_pend = true;
-        nd->cc_reject = false;
+        nd->cc_reject = !cc_accepted(raft_ms, t, nid, n);
         nd->cc_type = t;
         nd->cc_node = nid;
-        // the state machine's membership (rsm membership.go addNode / removeNode)
-        if (t == AddNode && nid >= 1 && nid <= n) nd->sm_rem &= ~(1u << (nid - 1));
-        if (t == RemoveNode && nid >= 1 && nid <= n) nd->sm_rem |= 1u << (nid - 1);
+        if (!nd->cc_reject) {
+          ms_apply(raft_ms, t, nid, n);
+          // the state machine's membership (rsm membership.go)
+          ms_apply(nd->sm_rem, t, nid, n);
+        }
       }
     }
     ctr[HC_ENT_APPLIED] += ud.committed_entries.size();
@@ -724,8 +803,9 @@ int harness_push(Harness* h, int kind, u64 replica, u64 a, u64 b, const Entry* e
       nd->cc_pend = true;
       nd->cc_reject = true;
       return 0;
-    case PUSH_RESTORE:
-      if (a >> N) return -1;
+    case PUSH_RESTORE:  // a: packed membership (pack_ms)
+      if (((a & 0xFF) >> N) || (((a >> 8) & 0xFF) >> N) || (((a >> 16) & 0xFF) >> N) || (a >> 24))
+        return -1;
       nd->x_rr = true;
       nd->x_rr_mask = (u32)a;
       return 0;
@@ -739,7 +819,9 @@ int harness_push(Harness* h, int kind, u64 replica, u64 a, u64 b, const Entry* e
 // the next step to compact (compactSnapshot → compactLog, node.go:849-866).
 int harness_snapshot_saved(Harness* h, u64 replica, u64 index, u64 term, u32 removed) {
   const u32 N = h->cfg.n_replicas;
-  if (replica >= h->groups.size() * N || index == 0 || term == 0 || (removed >> N)) return -1;
+  if (replica >= h->groups.size() * N || index == 0 || term == 0 || ((removed & 0xFF) >> N) ||
+      (((removed >> 8) & 0xFF) >> N) || (((removed >> 16) & 0xFF) >> N) || (removed >> 24))
+    return -1;
   Node* nd = h->groups[replica / N]->nodes[replica % N];
   if (index > nd->x_applied) return -1;  // only what the state machine applied
   Snapshot ss;
@@ -811,7 +893,10 @@ void harness_restart(Harness* h, u64 replica) {
   nd->sm_rem = removed_of(nd->db.snapshot.membership, N);
   nd->rr_pend = false;
   delete nd->peer;
-  nd->peer = Peer::Launch(node_config(cfg, gr->cid, k), &nd->db, node_addrs(N), false, false);
+  // an observer slot's node that was promoted (it is in Addresses) restarts as a follower
+  Config c = node_config(cfg, gr->cid, k);
+  if (c.isObserver && !(nd->sm_rem & (1u << k))) c.isObserver = false;
+  nd->peer = Peer::Launch(c, &nd->db, node_addrs(N), false, false);
   // a fresh quiesceManager kept on the harness's tick clock: its counters are
   // translated by the ticks before the restart (tick = noActivitySince =
   // exitQuiesceTick = t, not quiesced), which quiesce.go cannot tell apart from
@@ -912,17 +997,22 @@ void harness_views(const Harness* h, ReplicaView* out) {
       }
       v.votes_resp = resp;
       v.votes_granted = granted;
-      for (u32 s = 0; s < n; s++)
+      for (u32 s = 0; s < n; s++) {
         if (!R->remotes.count(s + 1)) v.removed |= 1u << s;
+        if (R->observers.count(s + 1)) v.observers |= 1u << s;
+        if (R->witnesses.count(s + 1)) v.witnesses |= 1u << s;
+      }
       v.events = nd->events;
-      if (R->state == Leader) {
-        for (auto& kv : R->remotes) {
-          if (kv.first >= 1 && kv.first <= 8) {
-            u32 s = (u32)(kv.first - 1);
-            v.match[s] = kv.second.match;
-            v.next[s] = kv.second.next;
-            v.rstate[s] = (u32)kv.second.state;
-            v.ractive[s] = kv.second.active ? 1 : 0;
+      if (R->state == Leader) {  // remotes, observers and witnesses (each slot in one)
+        for (const auto* mp : {&R->remotes, &R->observers, &R->witnesses}) {
+          for (auto& kv : *mp) {
+            if (kv.first >= 1 && kv.first <= 8) {
+              u32 s = (u32)(kv.first - 1);
+              v.match[s] = kv.second.match;
+              v.next[s] = kv.second.next;
+              v.rstate[s] = (u32)kv.second.state;
+              v.ractive[s] = kv.second.active ? 1 : 0;
+            }
           }
         }
       }

@@ -90,8 +90,10 @@ struct HarnessConfig {
   // no peers, initial = false: an empty log, no remotes) once an AddNode for
   // them is applied (needs membership)
   u32 n_voters = 0;
-  // config.MaxInMemLogSize: every raft's rate limiter (0 = off)
+  // config.MaxInMemLogSize (below), then the slots (beyond n_voters) whose nodes
+  // start as observers / witnesses (config.IsObserver / IsWitness): every raft's rate limiter (0 = off)
   u64 max_inmem_log_size = 0;
+  u32 observer_slots = 0, witness_slots = 0;
 };
 
 // host inputs for the next round (the engine's rbe_push_* / rbe_notify_applied)
@@ -110,7 +112,8 @@ struct ReplicaView {  // mirrors rbe_replica_view in include/rbe.h
   u64 match[8], next[8];
   u32 rstate[8], ractive[8];
   u32 events;   // EV_* bits of the last round's step (rbe_types.h)
-  u32 removed;  // bit (id-1): not a voting member in this replica's view (raft.remotes)
+  u32 removed;  // bit (id-1): not in this replica's raft.remotes
+  u32 observers, witnesses;  // bit (id-1): raft.observers / raft.witnesses
 };
 
 // ------------------------------------------------------------ quiesce.go

@@ -82,7 +82,8 @@ class OrcHarnessConfig(C.Structure):
                 ("snapshot_entries", C.c_uint32), ("compaction_overhead", C.c_uint32),
                 ("ext_commit", C.c_uint32), ("membership", C.c_uint32),
                 ("cc_period", C.c_uint32), ("cc_mod", C.c_uint32), ("n_voters", C.c_uint32),
-                ("max_inmem_log_size", C.c_uint64)]
+                ("max_inmem_log_size", C.c_uint64), ("observer_slots", C.c_uint32),
+                ("witness_slots", C.c_uint32)]
 
 
 class ReplicaView(C.Structure):
@@ -98,7 +99,8 @@ class ReplicaView(C.Structure):
                 ("votes_resp", C.c_uint32), ("votes_granted", C.c_uint32),
                 ("match", C.c_uint64 * 8), ("next", C.c_uint64 * 8),
                 ("rstate", C.c_uint32 * 8), ("ractive", C.c_uint32 * 8),
-                ("events", C.c_uint32), ("removed", C.c_uint32)]
+                ("events", C.c_uint32), ("removed", C.c_uint32),
+                ("observers", C.c_uint32), ("witnesses", C.c_uint32)]
 
 
 VIEW_FIELDS = [f[0] for f in ReplicaView._fields_ if f[0] != "pad"]
@@ -915,7 +917,7 @@ class Harness:
                  threads=1, cid_stride=1, xfer_period=0, xfer_mod=1, ext_apply=False,
                  ext_inputs=False, snapshot_entries=0, compaction_overhead=0,
                  ext_commit=False, membership=False, cc_period=0, cc_mod=1,
-                 max_inmem_log_size=0, n_voters=0):
+                 max_inmem_log_size=0, n_voters=0, observer_slots=0, witness_slots=0):
         c = OrcHarnessConfig(
             n_groups=n_groups, n_replicas=n_replicas, check_quorum=int(check_quorum),
             cid_base=cid_base, election_rtt=election_rtt, heartbeat_rtt=heartbeat_rtt,
@@ -927,7 +929,8 @@ class Harness:
             xfer_period=xfer_period, xfer_mod=xfer_mod, ext_apply=int(ext_apply),
             snapshot_entries=snapshot_entries, compaction_overhead=compaction_overhead,
             ext_commit=int(ext_commit), membership=int(membership), cc_period=cc_period,
-            cc_mod=cc_mod, max_inmem_log_size=max_inmem_log_size, n_voters=n_voters)
+            cc_mod=cc_mod, max_inmem_log_size=max_inmem_log_size, n_voters=n_voters,
+            observer_slots=observer_slots, witness_slots=witness_slots)
         self.n_groups, self.n_replicas = n_groups, n_replicas
         self.h = lib().orc_harness_create(C.byref(c))
         if not self.h:

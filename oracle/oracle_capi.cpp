@@ -50,6 +50,7 @@ typedef struct {
   uint32_t compaction_overhead, ext_commit;
   uint32_t membership, cc_period, cc_mod, n_voters;
   uint64_t max_inmem_log_size;
+  uint32_t observer_slots, witness_slots;
 } orc_harness_config;
 
 static thread_local std::string g_err;
@@ -875,6 +876,8 @@ void* orc_harness_create(const orc_harness_config* c) {
   h.cc_period = c->cc_period;
   h.cc_mod = c->cc_mod ? c->cc_mod : 1;
   h.n_voters = c->n_voters;
+  h.observer_slots = c->observer_slots;
+  h.witness_slots = c->witness_slots;
   h.max_inmem_log_size = c->max_inmem_log_size;
   return harness_create(h);
   GUARD_END(nullptr)

@@ -233,7 +233,12 @@ void* soa_create(const rbe_config* cfg) {
   C.compaction_overhead = cfg->compaction_overhead;
   C.rl_max = cfg->max_inmem_log_size;
   C.n_voters = cfg->n_voters ? cfg->n_voters : C.n;
-  if (!valid_n(C.n) || C.n_voters > C.n || (C.n_voters < C.n && !C.membership)) {
+  C.obs_slots = cfg->observer_slots;
+  C.wit_slots = cfg->witness_slots;
+  const u32 spare = ((1u << (C.n & 31)) - 1u) & ~((1u << (C.n_voters & 31)) - 1u);
+  if (!valid_n(C.n) || C.n_voters > C.n || (C.n_voters < C.n && !C.membership) ||
+      ((C.obs_slots | C.wit_slots) & ~spare) || (C.obs_slots & C.wit_slots) ||
+      ((C.obs_slots | C.wit_slots) && !C.membership)) {
     delete e;
     return nullptr;
   }
@@ -268,6 +273,7 @@ void* soa_create(const rbe_config* cfg) {
   P.rem_snap = C.snapshot_entries ? alloc<u64>(e, R * N) : nullptr;
   P.imark = (C.ext_commit || C.rl_max) ? alloc<u64>(e, R) : nullptr;
   P.rl = C.rl_max ? alloc<RlSt>(e, R) : nullptr;
+  P.roles = C.membership ? alloc<u16>(e, R) : nullptr;
   C.heap_bytes = (cfg->heap_bytes + 255) & ~255ull;
   e->heap.assign(C.heap_bytes, 0);
   e->hin.init(R, C.n, C.in_cap, C.heap_bytes);
@@ -417,7 +423,7 @@ int soa_launch(void* h, uint64_t n, const uint64_t* replica, const rbe_launch_st
       relaunch_replica<decltype(NN)::value>(e->P, e->C, replica[i], x.term, x.vote, x.commit,
                                             x.last_index, x.n_entries, t, b, ppar, e->tclk,
                                             x.marker, x.marker_term, x.snapshot_index,
-                                            x.snapshot_term, (u8)x.removed);
+                                            x.snapshot_term, x.removed);
     });
     e->P.gwake[replica[i] / e->C.n] = GW_AWAKE;
     off += x.n_entries;
@@ -495,11 +501,11 @@ int soa_set_node_ids(void* h, uint64_t first, uint64_t count, const uint64_t* id
   e->P.node_ids = e->hin.id_table();  // the host build's planes are host memory
   return RBE_OK;
 }
-int soa_restore_remotes(void* h, uint64_t n, const uint64_t* replica, const uint32_t* n_voters,
+int soa_restore_remotes(void* h, uint64_t n, const uint64_t* replica, const uint32_t* counts,
                         const uint64_t* ids) {
   SoaEngine* e = (SoaEngine*)h;
   if (!e->C.membership || !e->C.ext_inputs) return RBE_E_STATE;
-  return e->hin.restore_remotes(n, replica, n_voters, ids);
+  return e->hin.restore_remotes(n, replica, counts, ids);
 }
 // rbe_commit / rbe_get_update_commits on the host build
 int soa_commit(void* h, uint64_t n, const uint64_t* replica, const rbe_update_commit* uc) {
@@ -820,9 +826,14 @@ void soa_views(void* h, rbe_replica_view* out) {
     v.votes_granted = hh.votes_granted;
     v.events = (e->round > 0 && e->P.upd[i].round == e->round - 1) ? e->P.upd[i].events : 0u;
     v.removed = c.members & MB_REMOVED;
+    if (c.members & MB_ROLES) {  // Planes::roles is only current while MB_ROLES is set
+      v.observers = e->P.roles[i] & 0xFFu;
+      v.witnesses = e->P.roles[i] >> 8;
+    }
     if (hh.role == R_Leader) {
       for (u32 s = 0; s < N && s < 8; s++) {
-        if ((v.removed >> s) & 1u) continue;  // not in raft.remotes
+        // remotes, observers and witnesses
+        if ((v.removed >> s) & ~((v.observers | v.witnesses) >> s) & 1u) continue;
         v.match[s] = e->P.rem[i * N + s].match;
         v.next[s] = e->P.rem[i * N + s].next;
         v.rstate[s] = e->P.rem_st[i * N + s] & 3;
@@ -837,7 +848,7 @@ uint32_t soa_faults(void* h, uint64_t* n_faulty) {
   uint32_t o = 0;
   uint64_t n = 0;
   for (u64 i = 0; i < e->C.n_rep; i++) {
-    if (e->P.upd[i].fault & ~F_HANDOFF) n++;
+    if (e->P.upd[i].fault) n++;
     o |= e->P.upd[i].fault;
   }
   *n_faulty = n;

@@ -105,18 +105,6 @@ def test_host_config_changes():
     assert applied_cc > 10
 
 
-def test_observer_is_handed_off():
-    """AddObserver / AddWitness: not stepped on the device — the replica is
-    flagged RBE_FAULT_HANDOFF (not counted as a fault) and its view stays."""
-    kw = dict(n_groups=1, n_replicas=3, ext_inputs=True, ext_apply=True, membership=True)
-    eng = SoaCpu(trace=True, **kw)
-    eng.run(20)
-    eng.apply_config_change([1], [3], [O.CC_ADD_OBSERVER])
-    eng.step()
-    n, bits = eng.faults()
-    assert n == 0 and bits & 0x100
-
-
 def test_membership_calls_refused():
     from dragonboat_amd.engine import InputError, RBE_E_INVALID, RBE_E_STATE
     eng = SoaCpu(trace=True, n_groups=2, n_replicas=3, ext_inputs=True)
