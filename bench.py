@@ -226,14 +226,11 @@ def run_replica_mode(args, ws, rank, local, dist, dev, gloo_staged):
     xch = None
     if ws > 1:
         # --xchg-fixed: equal chunks with count headers, no host-side count read
-        # (rbe_xchg_pack_fixed; with RCCL the collective runs on the engine's stream)
-        caps = None
-        if args.xchg_fixed:
-            from dragonboat_amd.replica import initial_caps
-            c0 = initial_caps(kw["n_groups"] * kw["n_replicas"], kw["n_replicas"], ws)
-            caps = [c0[0], 3 * c0[1], 2 * c0[2]]
-        xch = ReplicaExchange(eng, buf_device=dev, comm_device="cpu" if gloo_staged else dev,
-                              caps=caps, fixed=args.xchg_fixed)
+        # (rbe_xchg_pack_fixed; with RCCL the collective runs on the engine's
+        # stream).  The settle and warmup rounds run the counted exchange; the
+        # chunks are then sized from the largest counts of the warmup rounds
+        # (ReplicaExchange.to_fixed) and the timed rounds run fixed
+        xch = ReplicaExchange(eng, buf_device=dev, comm_device="cpu" if gloo_staged else dev)
 
     def one_exchange():
         if xch.fixed:
@@ -265,7 +262,13 @@ def run_replica_mode(args, ws, rank, local, dist, dev, gloo_staged):
         eng.sync()
 
     rounds(settle)
+    if xch is not None:
+        xch.reset_peak()
     rounds(max(1, args.warmup))
+    rec0 = None
+    if xch is not None and args.xchg_fixed:
+        xch.to_fixed()
+        rec0 = sum(p * b for p, b in zip(xch.peak, xch.rec)) * (ws - 1)
     eng.sync()
     eng.reset_counters()
     b0 = xch.bytes_sent if xch else 0
@@ -324,7 +327,11 @@ def run_replica_mode(args, ws, rank, local, dist, dev, gloo_staged):
             "read_confirmations_per_s": reads / wall_max,
             "faulty_replicas": int(faulty), "fault_bits_rank0": fo,
             "exchange": {"bytes_per_round_all_ranks": sent_all / args.steps,
-                         "ms_per_round_mean_rank": xms_mean},
+                         "ms_per_round_mean_rank": xms_mean,
+                         "mode": "fixed" if (xch is not None and xch.fixed) else "counted",
+                         # fixed chunks moved per round over the largest counted
+                         # round's records (rank 0): the padding
+                         "fixed_pad": (xch.fixed_bytes_per_round() / rec0) if rec0 else None},
             "roofline": {"bound": "hbm", "achieved": dom["achieved_gbs"], "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": dom["achieved_gbs"] / HBM_PEAK_GBS,
                          "traffic": None, "kernel": dom["kernel"],

@@ -78,6 +78,9 @@ class ReplicaExchange:
         # read (rbe_xchg_pack_fixed); the capacities never grow, an overflow is
         # reported by check()
         self.fixed = fixed
+        # per stream: the most records one (rank, peer) pair moved in a counted
+        # exchange since reset_peak (what to_fixed sizes the chunks by)
+        self.peak = [0] * STREAMS
         self._alloc()
 
     # --- layout: per peer p, streams t = 0..2, cap[t] records each (rbe_xchg.h xchg_region)
@@ -124,6 +127,28 @@ class ReplicaExchange:
             raise RuntimeError("replica exchange: a chunk overflowed its capacity; "
                                "the rounds since are invalid (raise caps)")
 
+    def reset_peak(self):
+        self.peak = [0] * STREAMS
+
+    def to_fixed(self, margin: float = 1.25):
+        """Switch to the fixed-capacity exchange with chunks sized from the
+        counted rounds seen since reset_peak: every (peer, stream) capacity is
+        the largest count observed on any rank times `margin` (plus a small
+        floor), so the padding moved per round stays near `margin` times the
+        records instead of the worst-case bound of initial_caps.  Collective:
+        every rank calls it (the chunk size must agree).  An overflow in a
+        later round is reported by check()."""
+        t = self.torch.tensor(self.peak, dtype=self.torch.int64, device=self.comm_device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+        self.peak = [int(x) for x in t.tolist()]
+        self.caps = [int(p * margin) + 64 for p in self.peak]
+        self.fixed = True
+        self._alloc()
+
+    def fixed_bytes_per_round(self) -> int:
+        """Bytes one fixed-layout exchange moves from this rank (all peers)."""
+        return self.world * (self._per_peer() + XHDR_BYTES)
+
     def grow(self, counts: Sequence[int]):
         need = [max(counts[p * STREAMS + t] for p in range(self.world)) for t in range(STREAMS)]
         self.caps = [max(c, n + n // 4 + 64) for c, n in zip(self.caps, need)]
@@ -139,6 +164,9 @@ class ReplicaExchange:
             if not fits:
                 raise RuntimeError("replica exchange: pack overflow after growing")
         W, S = self.world, STREAMS
+        for t in range(S):
+            self.peak[t] = max([self.peak[t]] + [counts[p * S + t] for p in range(W)
+                                                 if p != self.rank])
         send_cnt = torch.tensor(counts, dtype=torch.int64, device=self.comm_device)
         recv_cnt = torch.empty_like(send_cnt)
         dist.all_to_all_single(recv_cnt, send_cnt, group=self.group)

@@ -65,8 +65,13 @@ def _worker(rank, world, port, name, gpu, trace, q, fixed=False):
         from dragonboat_amd.replica import ReplicaExchange
         kw, _, rounds, extra = CASES[name]
         # counted exchange: tiny caps exercise grow(); fixed exchange: capacities
-        # that never grow (initial_caps), counts travel in the chunk headers
-        caps = None if fixed else [8, 8, 8]
+        # that never grow (initial_caps), counts travel in the chunk headers;
+        # "cal": counted rounds first, then chunks sized from their peak counts
+        # (to_fixed, as bench.py --xchg-fixed does)
+        cal = fixed == "cal"
+        if cal:
+            fixed = False
+        caps = None if (fixed or cal) else [8, 8, 8]
         if gpu:  # the HIP engine, records staged through host memory for gloo
             from dragonboat_amd.engine import Engine
             eng = Engine(device=0, trace=trace, rep_world=world, rep_rank=rank, **kw, **extra)
@@ -80,6 +85,10 @@ def _worker(rank, world, port, name, gpu, trace, q, fixed=False):
         n = kw["n_replicas"]
         gmap = eng.global_groups()  # local group -> global group (rep_compact)
         for done in range(CHECK_EVERY, rounds + 1, CHECK_EVERY):
+            if cal and done == 2 * CHECK_EVERY:
+                xch.reset_peak()
+            if cal and done == 3 * CHECK_EVERY:
+                xch.to_fixed(1.5)
             xch.run(CHECK_EVERY)
             vs = eng.views()
             own = {}
@@ -93,6 +102,8 @@ def _worker(rank, world, port, name, gpu, trace, q, fixed=False):
                                         else getattr(vs[i], f) for f in FIELDS)
             snaps.append((done, own))
         nf = eng.fault_summary()[0] if gpu else eng.faults()[0]
+        if cal:
+            assert xch.fixed
         q.put((rank, snaps, eng.counters(), nf,
                [xch.bytes_sent] * 3 if fixed else xch.records_sent))
     except Exception as ex:  # surface worker failures in the parent
@@ -163,3 +174,10 @@ def test_replica_fixed_exchange_matches_oracle(name):
     """The fixed-capacity exchange (rbe_xchg_pack_fixed: equal chunks whose
     headers carry the counts, no host-side count read)."""
     run_case(name, fixed=True)
+
+
+def test_replica_calibrated_fixed_exchange():
+    """Counted rounds, then the fixed exchange with chunks sized from the
+    counted rounds' largest counts (ReplicaExchange.to_fixed): still
+    bit-exact, no overflow."""
+    run_case("C2_w2", fixed="cal")
