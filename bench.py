@@ -265,10 +265,8 @@ def run_replica_mode(args, ws, rank, local, dist, dev, gloo_staged):
     if xch is not None:
         xch.reset_peak()
     rounds(max(1, args.warmup))
-    rec0 = None
     if xch is not None and args.xchg_fixed:
         xch.to_fixed()
-        rec0 = sum(p * b for p, b in zip(xch.peak, xch.rec)) * (ws - 1)
     eng.sync()
     eng.reset_counters()
     b0 = xch.bytes_sent if xch else 0
@@ -329,9 +327,10 @@ def run_replica_mode(args, ws, rank, local, dist, dev, gloo_staged):
             "exchange": {"bytes_per_round_all_ranks": sent_all / args.steps,
                          "ms_per_round_mean_rank": xms_mean,
                          "mode": "fixed" if (xch is not None and xch.fixed) else "counted",
-                         # fixed chunks moved per round over the largest counted
-                         # round's records (rank 0): the padding
-                         "fixed_pad": (xch.fixed_bytes_per_round() / rec0) if rec0 else None},
+                         # one fixed chunk over the largest counted round's
+                         # records to one peer (rank 0): the padding
+                         "fixed_pad": xch.pad_ratio() if (xch is not None and xch.fixed)
+                         else None},
             "roofline": {"bound": "hbm", "achieved": dom["achieved_gbs"], "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": dom["achieved_gbs"] / HBM_PEAK_GBS,
                          "traffic": None, "kernel": dom["kernel"],

@@ -145,6 +145,12 @@ class ReplicaExchange:
         self.fixed = True
         self._alloc()
 
+    def pad_ratio(self) -> float:
+        """Bytes of one fixed chunk (one peer) over the bytes of the largest
+        counted round's records to one peer since reset_peak."""
+        rec = sum(p * b for p, b in zip(self.peak, self.rec))
+        return (self._per_peer() + XHDR_BYTES) / rec if rec else float("inf")
+
     def fixed_bytes_per_round(self) -> int:
         """Bytes one fixed-layout exchange moves from this rank (all peers)."""
         return self.world * (self._per_peer() + XHDR_BYTES)
