@@ -222,7 +222,8 @@ struct FastOut {
     if (d < 4) pc += (u64)v << (16 * d);
     else pc_hi += (u64)v << (16 * (d - 4));
   }
-  RBE_HD void set_fault(StepCounters& ctr, u32 f) {
+  template <class CT>
+  RBE_HD void set_fault(CT& ctr, u32 f) {
     (void)ctr;  // counted in fast_finish (new bits of the sticky word)
     fault |= f;
   }
@@ -235,7 +236,8 @@ struct FastOut {
   RBE_HD void event_if(bool c, u32 e) { events |= c ? e : 0u; }
   // `ent` points at the message's entries in this round's arena (may be null
   // when n_ent == 0).
-  RBE_HD void send(const Planes& P, const Params& C, StepCounters& ctr, Msg& m, const Ent* ent) {
+  template <class CT>
+  RBE_HD void send(const Planes& P, const Params& C, CT& ctr, Msg& m, const Ent* ent) {
     m.from = (u8)self;
     if (m.type != M_RequestVote) {
       if (m.type == M_Propose || m.type == M_ReadIndex) m.term = 0;
@@ -298,7 +300,8 @@ struct FastOut {
     *to = m;
 #endif
   }
-  RBE_HD void dropped_read_index(const Planes& P, const Params& C, StepCounters& ctr, u64 low,
+  template <class CT>
+  RBE_HD void dropped_read_index(const Planes& P, const Params& C, CT& ctr, u64 low,
                                  u64 high) {  // raft.go:1999-2012
     const bool full = n_drop_ri >= C.dri_cap;
     fault_if(full, F_DROPLIST);
@@ -314,7 +317,8 @@ struct FastOut {
       drop_hash = hfold(drop_hash, high);
     }
   }
-  RBE_HD void ready_to_read(const Planes& P, const Params& C, StepCounters& ctr, u64 index,
+  template <class CT>
+  RBE_HD void ready_to_read(const Planes& P, const Params& C, CT& ctr, u64 index,
                             u64 low, u64 high) {  // raft.go:1624-1630
     const bool full = n_rtr >= C.rtr_cap;
     fault_if(full, F_RTR);
@@ -391,8 +395,8 @@ struct FastQ {
 // applied index la and the compaction it asks for (run by the next step, a
 // full one: HF_SNAP_WORK).  A fast step never restores or compacts, and with
 // nothing applied the threshold cannot have been crossed (Lane::node_snapshot).
-template <int N, bool TRACE>
-RBE_HD void fast_node_snapshot(const Planes& P, const Params& C, StepCounters& ctr,
+template <int N, bool TRACE, class CT>
+RBE_HD void fast_node_snapshot(const Planes& P, const Params& C, CT& ctr,
                                FastOut<N, TRACE>& o, u64 la, u64 last, u64 t_last, u8& flags) {
   SnapSt* sp = &P.snp[o.r];
   const u64 S = C.snapshot_entries;
@@ -420,8 +424,8 @@ RBE_HD void fast_node_snapshot(const Planes& P, const Params& C, StepCounters& c
 // Common epilogue: stepNode's quiesce send, getUpdate/Commit, the trace digest,
 // the Update record, this round's outbox counts, Hot/Core write-back.
 // Mirrors the tail of Lane::run().
-template <int N, bool TRACE, int STG = 0>
-RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, FastOut<N, TRACE>& o,
+template <int N, bool TRACE, int STG = 0, class CT>
+RBE_HD void fast_finish(const Planes& P, const Params& C, CT& ctr, FastOut<N, TRACE>& o,
                         FastQ& q, u8 role, u8 flags, Hot h, Core c, u32 etick, u32 htick,
                         u64 committed0, u64 digest0, StageRow<N>* sr = nullptr,
                         u32 core_dirty = 0xFu) {
@@ -576,8 +580,8 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, StepCounters& ctr, Fas
 //   inbox (ascending sender; Quiesce marker, then the sender's messages) →
 //   local ReadIndex → tick → proposal, each followed by the deferred fan-out
 //   (Replicate sends in ascending slot order, heartbeats, readIndex confirm).
-template <int N, bool TRACE, int STG = 0, bool AUX = false, bool MSG = false>
-RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, StepCounters& ctr,
+template <int N, bool TRACE, int STG = 0, bool AUX = false, bool MSG = false, class CT>
+RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT& ctr,
                       StageRow<N>* sr = nullptr, u32 aux = 0, u32* staged = nullptr) {
   const u32 round = ck.round;
   using Cap = FastCaps<N>;
@@ -1295,8 +1299,8 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
 // One steady-state follower round: inbox from the known leader only
 // (Replicate / Heartbeat / ReadIndexResp of the current term), no client
 // input, a tick that does not start an election.
-template <int N, bool TRACE, int STG = 0, bool AUX = false, bool MSG = false>
-RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, StepCounters& ctr,
+template <int N, bool TRACE, int STG = 0, bool AUX = false, bool MSG = false, class CT>
+RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT& ctr,
                       StageRow<N>* sr = nullptr, u32 aux = 0, u32* staged = nullptr) {
   const u32 round = ck.round;
   using Cap = FastCaps<N>;
@@ -1638,8 +1642,8 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, St
 }
 
 // the fast step of one role (k_round, k_fast_list)
-template <int N, bool TRACE, int MODE, int STG = 0, bool AUX = false, bool MSG = false>
-RBE_HD bool step_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, StepCounters& ctr,
+template <int N, bool TRACE, int MODE, int STG = 0, bool AUX = false, bool MSG = false, class CT>
+RBE_HD bool step_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT& ctr,
                       StageRow<N>* sr = nullptr, u32 aux = 0, u32* staged = nullptr) {
   if constexpr (MODE == MODE_LEAD)
     return lead_fast<N, TRACE, STG, AUX, MSG>(P, C, r, ck, ctr, sr, aux, staged);

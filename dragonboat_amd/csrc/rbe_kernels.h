@@ -36,6 +36,9 @@ static constexpr int kBlock = 256;
 #ifndef RBE_FAST_WAVES
 #define RBE_FAST_WAVES 2
 #endif
+#ifndef RBE_FAST_LDS_CTR
+#define RBE_FAST_LDS_CTR 1  // k_fast_both's event counters in LDS (LdsCounters)
+#endif
 #ifndef RBE_TRI_CHUNK
 #define RBE_TRI_CHUNK 2048
 #endif
@@ -125,6 +128,48 @@ __device__ __forceinline__ void flush_counters(const Planes& P, const StepCounte
       atomicAdd((unsigned long long*)&P.counters[((u64)KS * kCtrStripes + blockIdx.x % kCtrStripes) *
                                                      C_NUM + threadIdx.x],
                 (unsigned long long)t);
+  }
+}
+
+// Event counters of the fast steps kept in LDS, one u32 slot per (counter,
+// lane) (RBE_FAST_LDS_CTR): `ctr.v[i] += k` is a no-return LDS add, so the
+// C_NUM running counts do not hold VGPRs across the persistent loop — at the
+// 256-register cap those registers are what the compiler spills, and a scratch
+// reload after the lane's first store waits for every store before it (vmcnt
+// is in order).
+struct LdsCounters {
+  struct Ref {
+    u32* a;
+    __device__ __forceinline__ void operator+=(u32 k) const {
+      __hip_atomic_fetch_add(a, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __device__ __forceinline__ void operator++(int) const { *this += 1u; }
+  };
+  struct Arr {
+    u32* base;  // &slots[0][threadIdx.x]
+    __device__ __forceinline__ Ref operator[](int i) const { return Ref{base + i * kBlock}; }
+  } v;
+};
+template <int KS>
+__device__ __forceinline__ void lds_counters_init(u32 (*slots)[kBlock]) {
+#pragma unroll
+  for (int i = 0; i < C_NUM; i++) slots[i][threadIdx.x] = 0;
+}
+// Every thread of the block must call this (it synchronises the block).
+template <int KS>
+__device__ __forceinline__ void flush_lds_counters(const Planes& P, u32 (*slots)[kBlock]) {
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // wave w sums counters w, w + 4, ...: lane l adds slots l, l + 64, ...
+  for (int i = w; i < C_NUM; i += kBlock / 64) {
+    u32 s = 0;
+#pragma unroll
+    for (int j = 0; j < kBlock / 64; j++) s += slots[i][lane + 64 * j];
+    s = wave_sum(s);
+    if (lane == 0 && s)
+      atomicAdd((unsigned long long*)&P.counters[((u64)KS * kCtrStripes + blockIdx.x % kCtrStripes) *
+                                                     C_NUM + i],
+                (unsigned long long)s);
   }
 }
 
@@ -285,9 +330,7 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
   const int lane = threadIdx.x & 63;
   const bool shortcut = !TRACE && C.quiesce;
   const bool use_list = shortcut && L.al_on;
-  const bool scan = !use_list || round == *L.scan_round ||
-                    (C.wl_enabled && round == C.wl_start_round) ||
-                    (C.xfer_period && round % C.xfer_period == 0);
+  const bool scan = !use_list || round == *L.scan_round || forced_round(C, round);
   const u32 t1 = ck.tick ? 1u : 0u;
   if (use_list && blockIdx.x == 0 && threadIdx.x == 0) {
     // the sleeping totals: last round's changes folded in (a scan recounts)
@@ -799,14 +842,21 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, 
   const Clk ck = clk_of(ra);
   const u32 round = ck.round;
   const u32 par = round & 1u;
+#if RBE_FAST_LDS_CTR
+  __shared__ u32 s_ctr_slots[C_NUM][kBlock];
+  lds_counters_init<KS_FAST_LEAD>(s_ctr_slots);
+  LdsCounters c{{&s_ctr_slots[0][threadIdx.x]}};
+#endif
   // segments: leader fronts, leader backs, follower fronts, follower backs
   __shared__ u32 s_pre[4 * kShards + 1];
   const u32 slots[4] = {0, 3, 1, 4};
   seg_build<4>(L, par, slots, s_pre);
   const u32 nl = s_pre[2 * kShards], n = s_pre[4 * kShards];
+#if !RBE_FAST_LDS_CTR
   StepCounters c;
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
+#endif
   StageRow<N>* wrows = &s_rows[threadIdx.x & ~63u];
   StageRow<N>* mine = &s_rows[threadIdx.x];
   // XCD-aware item mapping (RBE_XCD_FAST): block b takes only the items of
@@ -904,7 +954,11 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, 
     }
     list_push(L, 2, par, any && !ok, r);
   }
+#if RBE_FAST_LDS_CTR
+  flush_lds_counters<KS_FAST_LEAD>(P, s_ctr_slots);
+#else
   flush_counters<KS_FAST_LEAD>(P, c);
+#endif
 }
 
 // Pass 3: the whole handler table over the full list (persistent, grid-stride).

@@ -3186,6 +3186,16 @@ RBE_HD bool group_forced(const Params& C, u64 cid, u32 round) {
       if (xfer_input(C, cid, round, k)) return true;
   return false;
 }
+// The rounds on which group_forced may hold for a group that fell asleep
+// earlier (the workload's first round, leader-transfer and membership-schedule
+// rounds): k_triage's list mode reads every wake byte on them, besides the
+// host's scan rounds (launch, import), since the awake lists do not hold
+// sleeping groups.
+RBE_HD bool forced_round(const Params& C, u32 round) {
+  return (C.wl_enabled && round == C.wl_start_round) ||
+         (C.xfer_period && round % C.xfer_period == 0) ||
+         (C.cc_period && round % C.cc_period == 0);
+}
 // the round of a sleeping group: one QuiescedTick per owned replica, exactly
 // what triage_lazy counts for each of them
 RBE_HD void group_sleep_round(u8 gw, u32 n_owned, const Clk& ck, StepCounters& ctr) {

@@ -25,6 +25,7 @@ struct SoaEngine {
   std::vector<std::vector<uint8_t>> bufs;
   u32 round = 0;
   u32 tclk = 0;
+  u32 scan_at = 0;  // the host's last scan round (k_triage list mode: Lists::scan_round)
   HostInputs hin;
   u64 counters[C_NUM] = {0};
   bool full_only = false;
@@ -81,11 +82,14 @@ static void run_round(SoaEngine* e, bool tick = true) {
   std::vector<u64> lists[3];
   const u32 n = e->C.n;
   const bool shortcut = !e->C.trace && e->C.quiesce && !e->full_only;
+  // k_triage's list mode (one replica set per engine) sees a sleeping group
+  // only on scan rounds; replica mode scans every round
+  const bool scan = e->C.rep_world > 1 || e->round == e->scan_at || forced_round(e->C, e->round);
   for (u64 g = 0; g < e->C.n_groups; g++) {
     // group sleep as k_triage runs it (rbe_step.h)
     const u8 gw = e->P.gwake[g];
     if (shortcut && !(gw & GW_AWAKE) &&
-        !group_forced(e->C, e->C.cid_base + g * e->C.cid_stride, e->round)) {
+        (!scan || !group_forced(e->C, e->C.cid_base + g * e->C.cid_stride, e->round))) {
       memset(&c, 0, sizeof(c));
       u32 own = 0;
       for (u32 k = 0; k < n; k++) own += owned<N>(e->C, g * n + k) ? 1u : 0u;
@@ -428,6 +432,7 @@ int soa_launch(void* h, uint64_t n, const uint64_t* replica, const rbe_launch_st
     e->P.gwake[replica[i] / e->C.n] = GW_AWAKE;
     off += x.n_entries;
   }
+  e->scan_at = e->round;  // as rbe_launch: the next round scans every group
   return RBE_OK;
 }
 
@@ -1044,6 +1049,7 @@ extern "C" int soa_import_groups(void* h, const void* buf, uint64_t bytes, uint3
   memset(e->P.gwake + hd.first, GW_AWAKE, hd.count);  // imported groups start awake
   if (resume) {
     e->round = hd.round;
+    e->scan_at = hd.round;
     e->tclk = (u32)hd.tclk;
   }
   return RBE_OK;
