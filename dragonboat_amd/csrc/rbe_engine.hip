@@ -216,6 +216,115 @@ __global__ __launch_bounds__(kBlock) void k_out_write(Planes P, Params C, u64 fi
   }
 }
 
+// ---- rbe_collect_step: Updates, their messages and ReadyToReads, one pass
+// whether replica r's message to slot d is returned (RBE_COLLECT_REMOTE_MSGS:
+// only to replicas another rank steps)
+__device__ __forceinline__ bool out_msg_wanted(const Params& C, u64 g, u32 d, bool remote) {
+  if (!remote) return true;
+  if (C.rep_world <= 1) return false;
+  const u64 gg = group_global(C, g);
+  return gg < C.n_groups_glob && (u32)((gg + d) % C.rep_world) != C.rep_rank;
+}
+__device__ __forceinline__ void step_out_counts(const Planes& P, const Params& C, u64 r, u32 round,
+                                                bool remote, u32* f, u32* nm, u32* nr,
+                                                rbe_update* u) {
+  *f = upd_of(P, r, round, u) ? 1u : 0u;
+  *nm = *nr = 0;
+  if (!*f) return;
+  const u32 par = (round - 1u) & 1u, N = C.n;
+  const CntRow row = P.cnt[par][r];
+  const u64 g = r / N;
+  u32 m = 0;
+  for (u32 d = 0; d < N; d++) {
+    const u32 pc = row_word(row, d, round);
+    if (out_msg_wanted(C, g, d, remote)) m += (pc & 0x7Fu) + ((pc >> 7) & 0x7Fu);
+  }
+  *nm = m;
+  const Upd& x = P.upd[r];
+  *nr = x.round == round - 1u ? (x.n_rtr < C.rtr_cap ? x.n_rtr : C.rtr_cap) : 0u;
+}
+__global__ __launch_bounds__(kBlock) void k_cs_count(Planes P, Params C, u64 first, u64 count,
+                                                     u32 round, bool remote, u32* bsum) {
+  const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+  u32 f = 0, nm = 0, nr = 0;
+  rbe_update u;
+  if (i < count) step_out_counts(P, C, first + i, round, remote, &f, &nm, &nr, &u);
+  u32 tf, tm, tr;
+  block_excl_scan(f, &tf);
+  block_excl_scan(nm, &tm);
+  block_excl_scan(nr, &tr);
+  if (threadIdx.x == 0) {
+    bsum[3 * blockIdx.x] = tf;
+    bsum[3 * blockIdx.x + 1] = tm;
+    bsum[3 * blockIdx.x + 2] = tr;
+  }
+}
+// one block: exclusive prefixes of the block-sum triples, totals in pre[3 * nb]
+__global__ __launch_bounds__(kBlock) void k_cs_scan(const u32* bsum, u32 nb, u64* pre) {
+  u64 c[3] = {0, 0, 0};
+  for (u32 b0 = 0; b0 < nb; b0 += kBlock) {
+    const u32 b = b0 + threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      const u32 v = b < nb ? bsum[3 * b + q] : 0u;
+      u32 t;
+      const u32 ex = block_excl_scan(v, &t);
+      if (b < nb) pre[3 * b + q] = c[q] + ex;
+      c[q] += t;
+    }
+  }
+  if (threadIdx.x == 0)
+    for (int q = 0; q < 3; q++) pre[3 * nb + q] = c[q];
+}
+__global__ __launch_bounds__(kBlock) void k_cs_write(Planes P, Params C, u64 first, u64 count,
+                                                     u32 round, bool remote, const u64* pre,
+                                                     u64* rep, rbe_update* ou, u64* moff,
+                                                     rbe_message* om, u64* roff,
+                                                     rbe_ready_to_read* orr, u64 n_tot) {
+  const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+  u32 f = 0, nm = 0, nr = 0;
+  rbe_update u;
+  if (i < count) step_out_counts(P, C, first + i, round, remote, &f, &nm, &nr, &u);
+  u32 t;
+  const u64 at = pre[3 * blockIdx.x] + block_excl_scan(f, &t);
+  const u64 bm = pre[3 * blockIdx.x + 1] + block_excl_scan(nm, &t);
+  const u64 br = pre[3 * blockIdx.x + 2] + block_excl_scan(nr, &t);
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {  // the closing offsets
+    moff[n_tot] = pre[3 * gridDim.x + 1];
+    roff[n_tot] = pre[3 * gridDim.x + 2];
+  }
+  if (!f) return;
+  const u64 r = first + i;
+  rep[at] = r;
+  ou[at] = u;
+  moff[at] = bm;
+  roff[at] = br;
+  const u32 N = C.n, par = (round - 1u) & 1u;
+  const u64 g = r / N;
+  const u32 k = (u32)(r % N);
+  const CntRow row = P.cnt[par][r];
+  u64 w = bm;
+  for (u32 d = 0; d < N; d++) {
+    if (!out_msg_wanted(C, g, d, remote)) continue;
+    const u32 pc = row_word(row, d, round), na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
+    const Msg* lst = &P.msgs[par][((g * N + k) * N + d) * (u64)C.maxm];
+    for (u32 j = 0; j < na + nb; j++, w++) {
+      const Msg m = j < na ? lst[j] : lst[C.maxm - 1u - (j - na)];
+      rbe_message o;
+      msg_out(m, cid_of(C, g), P.node_ids, N, g, o);
+      om[w] = o;
+    }
+  }
+  for (u32 j = 0; j < nr; j++) {
+    const RTR x = P.rtr[r * C.rtr_cap + j];
+    rbe_ready_to_read o;
+    o.index = x.index;
+    o.ctx_low = x.low;
+    o.ctx_high = x.high;
+    orr[br + j] = o;
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_upd_count(Planes P, u64 first, u64 count, u32 round,
                                                       u32* bsum) {
   const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
@@ -402,6 +511,11 @@ struct rbe_engine {
   u64 upd_dev_bytes = 0;
   u8* upd_host = nullptr;
   u64 upd_host_bytes = 0;
+  // rbe_collect_step: the same for Updates + their outputs
+  u8* cs_dev = nullptr;
+  u64 cs_dev_bytes = 0;
+  u8* cs_host = nullptr;
+  u64 cs_host_bytes = 0;
   // rbe_wire_encode / rbe_wire_decode scratch
   u8* wire_dev = nullptr;    // the last rbe_wire_encode's frames (rbe_wire_fetch)
   u64 wire_dev_bytes = 0;
@@ -715,6 +829,8 @@ int rbe_destroy(rbe_engine* e) {
   if (e->ing_dev) HIP_IGNORE(hipFree(e->ing_dev));
   if (e->iso_dev) HIP_IGNORE(hipFree(e->iso_dev));
   if (e->upd_host) HIP_IGNORE(hipHostFree(e->upd_host));
+  if (e->cs_dev) HIP_IGNORE(hipFree(e->cs_dev));
+  if (e->cs_host) HIP_IGNORE(hipHostFree(e->cs_host));
   if (e->wire_dev) HIP_IGNORE(hipFree(e->wire_dev));
   if (e->wire_meta) HIP_IGNORE(hipFree(e->wire_meta));
   if (e->wire_rec) HIP_IGNORE(hipFree(e->wire_rec));
@@ -1771,6 +1887,70 @@ int rbe_collect_outputs(rbe_engine* e, uint64_t first, uint64_t count, rbe_outpu
   out->rtr_off = (const uint64_t*)(h + (o_roff - o_moff));
   out->messages = (const rbe_message*)(h + (o_rec - o_moff));
   out->ready_to_reads = (const rbe_ready_to_read*)(h + (o_rtr - o_moff));
+  return RBE_OK;
+}
+
+int rbe_collect_step(rbe_engine* e, uint64_t first, uint64_t count, uint32_t flags,
+                     rbe_step_outputs* out) {
+  if (!e || !out || count == 0 || first >= e->C.n_rep || count > e->C.n_rep - first ||
+      (flags & ~RBE_COLLECT_REMOTE_MSGS))
+    return RBE_E_INVALID;
+  memset(out, 0, sizeof(*out));
+  out->first = first;
+  out->count = count;
+  if (e->round == 0) return RBE_E_STATE;
+  HIP_OK(hipSetDevice(e->device));
+  const bool remote = (flags & RBE_COLLECT_REMOTE_MSGS) != 0;
+  const u32 nb = grid_for(count);
+  auto al = [](u64 x) { return (x + 255) & ~255ull; };
+  // device scratch: block sums (triples) | block prefixes (+ totals) | then the
+  // records, laid out as the host copy: replicas | updates | msg offsets |
+  // rtr offsets | messages | ReadyToReads
+  const u64 o_pre = al(3ull * nb * sizeof(u32)), o_rep = o_pre + al((3ull * nb + 3) * sizeof(u64));
+  int rc = grow(&e->cs_dev, &e->cs_dev_bytes, o_rep, false);
+  if (rc) return rc;
+  u64* pre = (u64*)(e->cs_dev + o_pre);
+  hipLaunchKernelGGL(k_cs_count, dim3(nb), dim3(kBlock), 0, e->stream, e->P, e->C, (u64)first,
+                     (u64)count, e->round, remote, (u32*)e->cs_dev);
+  hipLaunchKernelGGL(k_cs_scan, dim3(1), dim3(kBlock), 0, e->stream, (const u32*)e->cs_dev, nb,
+                     pre);
+  HIP_OK(hipGetLastError());
+  u64 tot[3];
+  HIP_OK(hipMemcpyAsync(tot, pre + 3ull * nb, sizeof(tot), hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  const u64 n = tot[0];
+  const u64 o_upd = o_rep + al(n * sizeof(u64));
+  const u64 o_moff = o_upd + al(n * sizeof(rbe_update));
+  const u64 o_roff = o_moff + al((n + 1) * sizeof(u64));
+  const u64 o_msg = o_roff + al((n + 1) * sizeof(u64));
+  const u64 o_rtr = o_msg + al(tot[1] * sizeof(rbe_message));
+  const u64 need = o_rtr + al(tot[2] * sizeof(rbe_ready_to_read));
+  if (need > e->cs_dev_bytes) {  // keep the block prefixes across the regrow
+    std::vector<u64> keep(3ull * nb + 3);
+    HIP_OK(hipMemcpy(keep.data(), pre, keep.size() * sizeof(u64), hipMemcpyDeviceToHost));
+    if ((rc = grow(&e->cs_dev, &e->cs_dev_bytes, need, false))) return rc;
+    pre = (u64*)(e->cs_dev + o_pre);
+    HIP_OK(hipMemcpy(pre, keep.data(), keep.size() * sizeof(u64), hipMemcpyHostToDevice));
+  }
+  u8* d = e->cs_dev;
+  hipLaunchKernelGGL(k_cs_write, dim3(nb), dim3(kBlock), 0, e->stream, e->P, e->C, (u64)first,
+                     (u64)count, e->round, remote, (const u64*)(d + o_pre), (u64*)(d + o_rep),
+                     (rbe_update*)(d + o_upd), (u64*)(d + o_moff), (rbe_message*)(d + o_msg),
+                     (u64*)(d + o_roff), (rbe_ready_to_read*)(d + o_rtr), n);
+  HIP_OK(hipGetLastError());
+  if ((rc = grow(&e->cs_host, &e->cs_host_bytes, need - o_rep, true))) return rc;
+  HIP_OK(hipMemcpyAsync(e->cs_host, d + o_rep, need - o_rep, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  u8* h = e->cs_host - o_rep;
+  out->n = n;
+  out->n_messages = tot[1];
+  out->n_ready_to_reads = tot[2];
+  out->replica = (const uint64_t*)(h + o_rep);
+  out->updates = (const rbe_update*)(h + o_upd);
+  out->msg_off = (const uint64_t*)(h + o_moff);
+  out->rtr_off = (const uint64_t*)(h + o_roff);
+  out->messages = (const rbe_message*)(h + o_msg);
+  out->ready_to_reads = (const rbe_ready_to_read*)(h + o_rtr);
   return RBE_OK;
 }
 

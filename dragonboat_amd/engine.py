@@ -159,6 +159,18 @@ class RbeOutputs(C.Structure):
                 ("ready_to_reads", C.POINTER(RbeReadyToRead))]
 
 
+class RbeStepOutputs(C.Structure):
+    _fields_ = [("first", C.c_uint64), ("count", C.c_uint64), ("n", C.c_uint64),
+                ("n_messages", C.c_uint64), ("n_ready_to_reads", C.c_uint64),
+                ("replica", C.POINTER(C.c_uint64)), ("updates", C.POINTER(RbeUpdate)),
+                ("msg_off", C.POINTER(C.c_uint64)), ("messages", C.POINTER(RbeMessage)),
+                ("rtr_off", C.POINTER(C.c_uint64)),
+                ("ready_to_reads", C.POINTER(RbeReadyToRead))]
+
+
+RBE_COLLECT_REMOTE_MSGS = 1
+
+
 class RbeWireFrame(C.Structure):
     _fields_ = [("offset", C.c_uint64), ("bytes", C.c_uint64), ("first_group", C.c_uint64),
                 ("src", C.c_uint32), ("dst", C.c_uint32), ("n_messages", C.c_uint32),
@@ -210,7 +222,7 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_wire_fetch", "rbe_wire_decode", "rbe_wire_ingest", "rbe_iso_leaders", "rbe_set_iso_leaders", "rbe_local_groups", "rbe_propose_entries", "rbe_commit",
            "rbe_get_update_commits", "rbe_propose_config_change", "rbe_apply_config_change",
            "rbe_reject_config_change", "rbe_rate_limited", "rbe_restore_remotes",
-           "rbe_snapshot_saved", "rbe_compact", "rbe_set_node_ids"]
+           "rbe_snapshot_saved", "rbe_compact", "rbe_set_node_ids", "rbe_collect_step"]
 KERNEL_SLOTS = 4
 
 _lib = None
@@ -268,6 +280,7 @@ def load_library(path: Optional[str] = None):
         "rbe_push_read_index": (i32, [vp, u64, P(u64), P(u64), P(u64)]),
         "rbe_get_updates": (i32, [vp, u64, u64, P(RbeUpdate)]),
         "rbe_collect_updates": (i32, [vp, u64, u64, P(RbeUpdateList)]),
+        "rbe_collect_step": (i32, [vp, u64, u64, u32, P(RbeStepOutputs)]),
         "rbe_get_messages": (i32, [vp, u64, P(RbeMessage), u32, P(u32)]),
         "rbe_get_outbox": (i32, [vp, u64, P(RbeMessage), u32, P(u32), P(RbeEntry), u32, P(u32),
                                  vp, u64, P(u64)]),
@@ -950,6 +963,27 @@ class Engine(NodeInputs):
         u64 = np.dtype(np.uint64)
         return (arr(o.msg_off, count + 1, u64), arr(o.messages, o.n_messages, MESSAGE_DTYPE),
                 arr(o.rtr_off, count + 1, u64), arr(o.ready_to_reads, o.n_ready_to_reads, RTR_DTYPE))
+
+    def collect_step(self, first: int = 0, count: Optional[int] = None, remote_only=False):
+        """rbe_collect_step: (replicas, Updates, msg_off, messages, rtr_off,
+        ready_to_reads) of the replicas in [first, first + count) with an
+        Update, as numpy arrays (copies of the engine's pinned buffer)."""
+        count = self.n_rep - first if count is None else count
+        o = RbeStepOutputs()
+        _check(self.lib.rbe_collect_step(self.h, first, count,
+                                         RBE_COLLECT_REMOTE_MSGS if remote_only else 0,
+                                         C.byref(o)), "rbe_collect_step")
+
+        def arr(ptr, n, dtype):
+            if n == 0:
+                return np.zeros(0, dtype=dtype)
+            raw = C.string_at(C.cast(ptr, C.c_void_p), n * dtype.itemsize)
+            return np.frombuffer(raw, dtype=dtype).copy()
+
+        u64 = np.dtype(np.uint64)
+        return (arr(o.replica, o.n, u64), arr(o.updates, o.n, UPDATE_DTYPE),
+                arr(o.msg_off, o.n + 1, u64), arr(o.messages, o.n_messages, MESSAGE_DTYPE),
+                arr(o.rtr_off, o.n + 1, u64), arr(o.ready_to_reads, o.n_ready_to_reads, RTR_DTYPE))
 
     def ready_to_reads(self, replica: int):
         cap = 64

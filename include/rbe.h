@@ -631,6 +631,30 @@ typedef struct rbe_update_list {
   const rbe_update* updates;
 } rbe_update_list;
 int rbe_collect_updates(rbe_engine* e, uint64_t first, uint64_t count, rbe_update_list* out);
+/* The node loop's whole read after a step in one call (execengine.go:494-560,
+ * node.go:888-923): the Updates of replicas [first, first + count) that have
+ * one, and only for those replicas (a replica with Messages or ReadyToReads
+ * always has an Update, peer.go:253-280) their ReadyToReads and Messages —
+ * compacted on the device, copied once into an engine-owned pinned buffer.
+ * replica[i] (ascending) has updates[i], messages[msg_off[i] .. msg_off[i+1])
+ * and ready_to_reads[rtr_off[i] .. rtr_off[i+1]).  With
+ * RBE_COLLECT_REMOTE_MSGS only the messages to replicas this engine does not
+ * step are returned (rep_world > 1: the transport's share); the others the
+ * engine delivers itself at the next step, so in group-per-GPU mode none is
+ * copied.  Valid until the next rbe_collect_step, rbe_step/rbe_run or
+ * rbe_destroy. */
+#define RBE_COLLECT_REMOTE_MSGS 1u
+typedef struct rbe_step_outputs {
+  uint64_t first, count, n, n_messages, n_ready_to_reads;
+  const uint64_t* replica;                 /* n */
+  const rbe_update* updates;               /* n */
+  const uint64_t* msg_off;                 /* n + 1 */
+  const rbe_message* messages;
+  const uint64_t* rtr_off;                 /* n + 1 */
+  const rbe_ready_to_read* ready_to_reads;
+} rbe_step_outputs;
+int rbe_collect_step(rbe_engine* e, uint64_t first, uint64_t count, uint32_t flags,
+                     rbe_step_outputs* out);
 int rbe_get_counters(rbe_engine* e, uint64_t* out /* RBE_CTR_NUM */);
 /* the counters one pipeline kernel (RBE_KERNEL_*) contributed */
 int rbe_get_kernel_counters(rbe_engine* e, int32_t kernel, uint64_t* out /* RBE_CTR_NUM */);

@@ -138,3 +138,45 @@ def test_gpu_collect_outputs_match_oracle(gpu_available, name, kw, extra):
                 checked += len(want)
     assert checked > 500
     eng.close()
+
+
+@pytest.mark.parametrize("name,kw,extra", [("C2", C2, {}), ("C3", C3, dict(ring=128)),
+                                           ("C4", C4, {})])
+def test_gpu_collect_step_matches(gpu_available, name, kw, extra):
+    """rbe_collect_step: the Updates of rbe_collect_updates, and for exactly
+    those replicas the messages / ReadyToReads of rbe_collect_outputs (every
+    replica with outputs has an Update); with RBE_COLLECT_REMOTE_MSGS and one
+    replica set per engine no message comes back (all are delivered on the
+    device)."""
+    from dragonboat_amd.engine import Engine
+    kw = dict(kw, n_groups=min(kw["n_groups"], 48))
+    eng = Engine(device=0, trace=True, **dict(kw, **extra))
+    seen = [0, 0, 0]
+    for rnd in range(120):
+        eng.step()
+        first, count = (0, eng.n_rep) if rnd % 3 else (5, eng.n_rep - 9)
+        rep, ups, moff, msgs, roff, rtrs = eng.collect_step(first, count)
+        rep_u, ups_u = eng.collect_updates(first, count)
+        assert list(rep) == list(rep_u)
+        assert ups.tobytes() == ups_u.tobytes()
+        om, allm, orr, allr = eng.collect_outputs(first, count)
+        assert moff[-1] == len(msgs) and roff[-1] == len(rtrs)
+        with_out = {first + i for i in range(count)
+                    if om[i + 1] > om[i] or orr[i + 1] > orr[i]}
+        assert with_out <= set(int(x) for x in rep), "outputs of a replica without an Update"
+        for j, r in enumerate(rep):
+            i = int(r) - first
+            a, b = msgs[moff[j]:moff[j + 1]], allm[om[i]:om[i + 1]]
+            assert a.tobytes() == b.tobytes(), (rnd, int(r))
+            a, b = rtrs[roff[j]:roff[j + 1]], allr[orr[i]:orr[i + 1]]
+            assert a.tobytes() == b.tobytes(), (rnd, int(r))
+        assert len(msgs) == len(allm) and len(rtrs) == len(allr)
+        r2, u2, mo2, m2, ro2, t2 = eng.collect_step(first, count, remote_only=True)
+        assert len(m2) == 0 and list(r2) == list(rep) and t2.tobytes() == rtrs.tobytes()
+        seen[0] += len(rep)
+        seen[1] += len(msgs)
+        seen[2] += len(rtrs)
+    assert seen[0] and seen[1], seen
+    if name == "C4":
+        assert seen[2], seen
+    eng.close()
