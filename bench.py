@@ -355,7 +355,8 @@ def run_host_driven(args, ws, rank, local, dist):
     beside the device time (HIP events around the step)."""
     import ctypes as C
     import numpy as np
-    from dragonboat_amd.engine import (UPDATE_DTYPE, Engine, RbeOutputs, RbeUpdateList, _check,
+    from dragonboat_amd.engine import (RBE_COLLECT_REMOTE_MSGS, UPDATE_DTYPE, Engine,
+                                       RbeOutputs, RbeStepOutputs, RbeUpdateList, _check,
                                        footprint, make_config)
     from dragonboat_amd.shard import reduce_results, shard_params
 
@@ -373,13 +374,30 @@ def run_host_driven(args, ws, rank, local, dist):
     active = np.arange(0, n_groups, 10, dtype=np.uint64)  # 10% of the groups
     ul = RbeUpdateList()
     outs = RbeOutputs()
+    so = RbeStepOutputs()
+    # --c4h-all-msgs: every message copied back as well (rbe_collect_updates +
+    # rbe_collect_outputs); default: rbe_collect_step with only the messages for
+    # other engines (none here: group-per-GPU, the engine delivers them itself)
+    all_msgs = args.c4h_all_msgs
     leader_of = np.zeros(n_groups, dtype=np.uint64)  # leader slot + 1 per group, 0 = none
     cmd = np.frombuffer(rng.bytes(16 * len(active)), dtype=np.uint8).copy()
     ptr = lambda a, t: a.ctypes.data_as(C.POINTER(t))  # noqa: E731
-    stats = {"push": 0.0, "step": 0.0, "out": 0.0, "reads": 0, "props": 0, "msgs": 0, "rtr": 0,
-             "upd": 0}
+    stats = {"push": 0.0, "step": 0.0, "enqueue": 0.0, "out": 0.0, "reads": 0, "props": 0,
+             "msgs": 0, "rtr": 0, "upd": 0}
 
     def read_back():
+        if not all_msgs:
+            _check(L.rbe_collect_step(h, 0, n_rep, RBE_COLLECT_REMOTE_MSGS, C.byref(so)),
+                   "rbe_collect_step")
+            n = so.n
+            if n:  # the engine's pinned buffer, read in place
+                rep = np.ctypeslib.as_array(so.replica, shape=(n,))
+                ups = np.frombuffer((C.c_uint8 * (n * UPDATE_DTYPE.itemsize)).from_address(
+                    C.addressof(so.updates.contents)), dtype=UPDATE_DTYPE)
+                lid = ups["leader_id"]
+                known = lid != 0
+                leader_of[(rep[known] // np.uint64(N)).astype(np.int64)] = lid[known]
+            return so.n_messages, so.n_ready_to_reads, n
         _check(L.rbe_collect_updates(h, 0, n_rep, C.byref(ul)), "rbe_collect_updates")
         _check(L.rbe_collect_outputs(h, 0, n_rep, C.byref(outs)), "rbe_collect_outputs")
         n = ul.n
@@ -414,6 +432,7 @@ def run_host_driven(args, ws, rank, local, dist):
                                         ptr(cmd, C.c_uint8)), "rbe_push_proposals")
         t1 = time.perf_counter()
         eng.step()
+        te = time.perf_counter()
         eng.sync()
         t2 = time.perf_counter()
         nm, nr, nu = read_back()
@@ -421,6 +440,7 @@ def run_host_driven(args, ws, rank, local, dist):
         if timed:
             stats["push"] += t1 - t0
             stats["step"] += t2 - t1
+            stats["enqueue"] += te - t1
             stats["out"] += t3 - t2
             stats["reads"] += len(rr)
             stats["props"] += len(pr)
@@ -470,6 +490,10 @@ def run_host_driven(args, ws, rank, local, dist):
             "boundary": {
                 "push_ms_per_round": stats["push"] * 1e3 / K,
                 "step_ms_per_round": stats["step"] * 1e3 / K,
+                # host part of the step call: input upload staging + launches
+                "step_enqueue_ms_per_round": stats["enqueue"] * 1e3 / K,
+                "read_back": "rbe_collect_updates + rbe_collect_outputs (every message)"
+                if all_msgs else "rbe_collect_step (messages for other engines only)",
                 "outputs_ms_per_round": stats["out"] * 1e3 / K,
                 "boundary_share": (stats["push"] + stats["out"]) / max(1e-12, wall),
                 "reads_pushed_per_round": stats["reads"] / K,
@@ -503,6 +527,8 @@ def main():
                     help="groups in the 1-thread CPU sample (0 = per-workload default)")
     ap.add_argument("--xchg-gloo", action="store_true",
                     help="c5 rehearsal: all ranks on cuda:0, exchange over gloo via host memory")
+    ap.add_argument("--c4h-all-msgs", action="store_true",
+                    help="c4h: read every message back too (rbe_collect_outputs)")
     ap.add_argument("--xchg-fixed", action="store_true",
                     help="c5: fixed-capacity exchange (count headers, no host-side count read)")
     args = ap.parse_args()
