@@ -1435,6 +1435,22 @@ int rbe_notify_applied(rbe_engine* e, uint64_t n, const uint64_t* replica,
   return e->hin.notify_applied(n, replica, applied);
 }
 
+#ifdef RBE_FULL_PROF
+// diagnostic build: the k_full_list wave records since the last call (at most
+// cap of them, 4 words each: wall-clock span, lane-class masks, lanes) and clear
+extern "C" int rbe_debug_full_prof(uint64_t* out, uint64_t cap, uint64_t* n) {
+  unsigned long long cnt = 0;
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(g_full_prof_n), sizeof(cnt)));
+  const u64 m = std::min<u64>(std::min<u64>(cnt, kFullProfCap), cap);
+  if (m) HIP_OK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_full_prof), m * 32));
+  *n = cnt;
+  cnt = 0;
+  HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_full_prof_n), &cnt, sizeof(cnt)));
+  return RBE_OK;
+}
+#endif
+
 #ifdef RBE_PHASE_TIMING
 // diagnostic build: read and clear the per-phase stamp sums (rbe_fast.h)
 int rbe_debug_phases(uint64_t* out24) {

@@ -672,8 +672,38 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   if (c.ltt != 0) return false;
   if (!ck.tick) return false;
   if (C.xfer_period && xfer_input(C, cid, round, k)) return false;
-  if (C.ext_inputs && P.ext[r].flags) return false;
   if (c.rq_count >= Cap::RQ) return false;
+  u32 inp = wl_input(C, cid, round);
+  // Host input (rbe_push_read_index / rbe_push_proposals): one ReadIndex, or
+  // one inline non-ConfigChange entry, takes the same path as the workload's
+  // (Lane::run reads it from Planes::ext; the entry stays in Planes::in_ents,
+  // not the arena); anything else takes the full handler table.
+  u64 xlo = 0, xhi = 0;
+  u32 xlen = 16, xtype = E_Application;
+  bool xin = false;
+  if (C.ext_inputs) {
+    const ExtIn* xp = &P.ext[r];
+    const u32 xf = xp->flags;
+    if (xf != 0) {
+      if (inp != 0) return false;
+      if (xf == EXT_READ) {
+        xlo = xp->ctx_low;
+        xhi = xp->ctx_high;
+        inp = 2;
+      } else if (xf == EXT_PROPOSE && xp->n_prop == 1) {
+        const Ent e = P.in_ents[xp->prop_off];
+        if ((e.type & ET_HEAP) || ent_type(e.type) == E_ConfigChange || e.len > 16) return false;
+        xlo = e.lo;
+        xhi = e.hi;
+        xlen = e.len;
+        xtype = e.type;
+        inp = 1;
+      } else {
+        return false;
+      }
+      xin = true;
+    }
+  }
   u32 n_in = 0;
 #pragma unroll
   for (u32 s = 0; s < N; s++) {
@@ -682,7 +712,6 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
     if (na != 0 || nb > Cap::MAXM) return false;
     n_in += nb;
   }
-  const u32 inp = wl_input(C, cid, round);
   // ---- gather, level 2: inbound message headers, readIndex queue
   RBE_STAMP(t1);
   // Loads only inside the branches; every use comes after the join, so no
@@ -831,6 +860,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   u64 seg_lo = 0;
   // the entry proposed this round (index prop_idx), still in registers
   u64 prop_idx = 0, prop_lo = 0, prop_hi = 0;
+  u32 prop_len = 16, prop_type = E_Application;
 
   // entryLog.term (logentry.go:142-161) without touching memory: a leader's
   // entries [lead_start, last] are of its term and earlier ones of a lower
@@ -853,8 +883,8 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
     o.fault_if(!hit, F_UNSUPPORTED);
     Ent e;
     e.term = hit ? c.term : 0;
-    e.type = E_Application;
-    e.len = hit ? 16u : 0u;
+    e.type = hit ? prop_type : (u32)E_Application;
+    e.len = hit ? prop_len : 0u;
     e.lo = hit ? prop_lo : 0;
     e.hi = hit ? prop_hi : 0;
     return e;
@@ -1125,7 +1155,8 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   }
   // batchedReadIndex → Peer.ReadIndex → handleLeaderReadIndex (raft.go:1633-1665)
   if (inp == 2) {
-    const u64 low = ((u64)(round + 1) << 32) | (u64)o.self, high = cid + 1;
+    const u64 low = xin ? xlo : (((u64)(round + 1) << 32) | (u64)o.self);
+    const u64 high = xin ? xhi : cid + 1;
     if (log_term(c.committed) != c.term) {
       o.dropped_read_index(P, C, ctr, low, high);
     } else {
@@ -1207,25 +1238,29 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   fan_out();
   // the proposal (handleProposals → Peer.ProposeEntries → handleLeaderPropose)
   if (inp == 1) {
-    const u64 lo = wl_payload_lo(C.seed, cid, round), hi = mix64(lo);
+    const u64 lo = xin ? xlo : wl_payload_lo(C.seed, cid, round), hi = xin ? xhi : mix64(lo);
     ctr.v[C_PROPOSALS]++;
-    o.fault_if(arena_used + 1 > C.ecap, F_ARENA);
-    if (arena_used + 1 <= C.ecap) {
-      Ent e;  // staged in the arena as the Propose message carries it (term 0)
-      e.term = 0;
-      e.type = E_Application;
-      e.len = 16;
-      e.lo = lo;
-      e.hi = hi;
-      arena[arena_used] = e;
-      arena_used++;
+    // the workload's entry is staged in the arena as the Propose message
+    // carries it (term 0); the host's stays in Planes::in_ents (Lane::run)
+    o.fault_if(!xin && arena_used + 1 > C.ecap, F_ARENA);
+    if (xin || arena_used + 1 <= C.ecap) {
+      if (!xin) {
+        Ent e;
+        e.term = 0;
+        e.type = E_Application;
+        e.len = 16;
+        e.lo = lo;
+        e.hi = hi;
+        arena[arena_used] = e;
+        arena_used++;
+      }
       // appendEntries (raft.go:909-920)
       const u64 idx = c.last_index + 1;
       const u64 sl = (idx & (u64)(C.ring - 1)) * C.n_rep + r;
       P.term_ring[sl] = c.term;
       Body b;
-      b.type = E_Application;
-      b.len = 16;
+      b.type = xtype;
+      b.len = xlen;
       b.lo = lo;
       b.hi = hi;
       P.pay_ring[sl] = b;
@@ -1236,6 +1271,8 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
       prop_idx = idx;
       prop_lo = lo;
       prop_hi = hi;
+      prop_len = xlen;
+      prop_type = xtype;
 #pragma unroll
       for (u32 s = 0; s < N; s++)
         if (s == k) try_update(match[s], next[s], st[s], c.last_index);
@@ -1247,6 +1284,10 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   (void)last0;
   // ---- scatter
   RBE_STAMP(t4);
+  if (xin) {  // the host input is consumed (Lane::run clears the record)
+    ExtIn z{};
+    P.ext[r] = z;
+  }
 #pragma unroll
   for (u32 s = 0; s < N; s++) {
     RemoteMN x;

@@ -149,3 +149,23 @@ def run_driven(eng, ref, rounds, seed=1, tick_every=1, inputs=True, ext_apply=Fa
     if bad:
         return ("counters", bad)
     return None
+
+
+def leader_inputs_round(rng, views, n, rnd, density=0.5, read_share=0.9):
+    """The node layer's steady traffic (bench c4h): at the leader of a share
+    of the groups one ReadIndex, or one proposal of 0-16 bytes (a single
+    inline entry, Application or Encoded)."""
+    ops = []
+    n_groups = len(views) // n
+    for g in range(n_groups):
+        if rng.random() >= density:
+            continue
+        lead = [g * n + k for k in range(n) if views[g * n + k].role == O.LEADER]
+        if not lead:
+            continue
+        r = lead[0]
+        if rng.random() < read_share:
+            ops.append(("read", r, ((rnd + 1) << 32 | (r + 1), rng.randrange(1 << 40))))
+        else:
+            ops.append(("prop", r, [(rng.choice((0, 0, 2)), _cmd(rng))]))
+    return ops

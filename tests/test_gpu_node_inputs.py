@@ -102,3 +102,31 @@ def test_gpu_update_flags_and_events(gpu_available):
         assert u.flags & E.UF_HAS_UPDATE
         assert u.save_lo <= u.save_hi  # the appended entry is to be saved
     eng.close()
+
+
+@pytest.mark.parametrize("quiesce", [False, True])
+def test_gpu_leader_inputs_fast_path(gpu_available, quiesce):
+    """Host ReadIndexes and single inline proposals at leaders on the HIP
+    engine (k_fast_both's leader step takes them), bit-exact with the oracle."""
+    import random
+    from dragonboat_amd.engine import Engine
+    from input_util import apply_engine, apply_oracle, leader_inputs_round
+    from parity_util import counters_match, view_diff
+    kw = dict(n_groups=40, n_replicas=3, quiesce=quiesce, ext_inputs=True)
+    eng = Engine(device=0, trace=True, **kw)
+    ref = O.Harness(**kw)
+    rng = random.Random(17)
+    views = ref.views()
+    for rnd in range(260):
+        if rnd >= 60:
+            ops = leader_inputs_round(rng, views, 3, rnd)
+            apply_engine(eng, ops)
+            apply_oracle(ref, ops)
+        eng.step()
+        ref.step()
+        ev, views = eng.views(), ref.views()
+        for i in range(len(views)):
+            d = view_diff(ev[i], views[i])
+            assert d is None, f"round {rnd} replica {i}: {d}"
+    assert not counters_match(eng.counters(), ref.counters())
+    eng.close()

@@ -176,3 +176,39 @@ def test_push_batches_are_all_or_nothing():
         eng.notify_applied([0], [1])
     eng.step()
     eng.push_proposals([0], [[b"y"]])  # the next step takes a new batch
+
+
+@pytest.mark.parametrize("quiesce", [False, True])
+def test_leader_inputs_fast_path(quiesce):
+    """Host ReadIndexes and single inline proposals at leaders (the node
+    layer's steady traffic, bench c4h) take the fast leader step, bit-exact
+    with the oracle; the full handler table sees only the rounds it would
+    without input."""
+    import random
+    from input_util import apply_engine, apply_oracle, leader_inputs_round
+    from parity_util import counters_match, view_diff
+    kw = dict(n_groups=40, n_replicas=3, quiesce=quiesce, ext_inputs=True)
+    eng = SoaCpu(trace=True, **kw)
+    ref = O.Harness(**kw)
+    rng = random.Random(17)
+    views = ref.views()
+    pushed = 0
+    slow0 = None
+    for rnd in range(260):
+        if rnd >= 60:
+            ops = leader_inputs_round(rng, views, 3, rnd)
+            pushed += len(ops)
+            apply_engine(eng, ops)
+            apply_oracle(ref, ops)
+        if rnd == 60:
+            slow0 = eng.slow_total()
+        eng.step()
+        ref.step()
+        ev, views = eng.views(), ref.views()
+        for i in range(len(views)):
+            d = view_diff(ev[i], views[i])
+            assert d is None, f"round {rnd} replica {i}: {d}"
+    assert not counters_match(eng.counters(), ref.counters())
+    assert pushed > 3000
+    # the 200 input rounds put ~4000 inputs at leaders; nearly all are stepped fast
+    assert eng.slow_total() - slow0 < pushed // 10, (eng.slow_total() - slow0, pushed)
