@@ -153,24 +153,27 @@ __global__ __launch_bounds__(kBlock) void k_out_count(Planes P, Params C, u64 fi
     bsum[2 * blockIdx.x + 1] = tr;
   }
 }
-// one block: exclusive prefix of the block sums (pairs), totals in pre[2 * nb]
-__global__ __launch_bounds__(kBlock) void k_out_scan(const u32* bsum, u32 nb, u64* pre) {
-  u64 cm = 0, cr = 0;
-  for (u32 b0 = 0; b0 < nb; b0 += kBlock) {
-    const u32 b = b0 + threadIdx.x;
-    const u32 vm = b < nb ? bsum[2 * b] : 0u, vr = b < nb ? bsum[2 * b + 1] : 0u;
-    u32 tm, tr;
-    const u32 em = block_excl_scan(vm, &tm), er = block_excl_scan(vr, &tr);
-    if (b < nb) {
-      pre[2 * b] = cm + em;
-      pre[2 * b + 1] = cr + er;
+// one block: exclusive prefixes of the Q-tuples of block sums, totals in
+// pre[Q * nb ..].  Thread t owns a contiguous run of ceil(nb / 256) blocks:
+// its run totals are scanned across the block once, then the run is walked
+// (a loop over 256-block slices with two barriers each took 77 us at 11.7k
+// blocks, more than the count and write passes it sits between).
+template <int Q>
+__global__ __launch_bounds__(kBlock) void k_scan_q(const u32* bsum, u32 nb, u64* pre) {
+  const u32 per = (nb + kBlock - 1) / kBlock;
+  const u32 b0 = threadIdx.x * per < nb ? threadIdx.x * per : nb;
+  const u32 b1 = b0 + per < nb ? b0 + per : nb;
+#pragma unroll
+  for (int q = 0; q < Q; q++) {
+    u32 loc = 0;
+    for (u32 b = b0; b < b1; b++) loc += bsum[Q * b + q];
+    u32 tot;
+    u64 run = block_excl_scan(loc, &tot);
+    for (u32 b = b0; b < b1; b++) {
+      pre[Q * b + q] = run;
+      run += bsum[Q * b + q];
     }
-    cm += tm;
-    cr += tr;
-  }
-  if (threadIdx.x == 0) {
-    pre[2 * nb] = cm;
-    pre[2 * nb + 1] = cr;
+    if (threadIdx.x == 0) pre[(u64)Q * nb + q] = tot;
   }
 }
 __global__ __launch_bounds__(kBlock) void k_out_write(Planes P, Params C, u64 first, u64 count,
@@ -226,9 +229,8 @@ __device__ __forceinline__ bool out_msg_wanted(const Params& C, u64 g, u32 d, bo
   return gg < C.n_groups_glob && (u32)((gg + d) % C.rep_world) != C.rep_rank;
 }
 __device__ __forceinline__ void step_out_counts(const Planes& P, const Params& C, u64 r, u32 round,
-                                                bool remote, u32* f, u32* nm, u32* nr,
-                                                rbe_update* u) {
-  *f = upd_of(P, r, round, u) ? 1u : 0u;
+                                                bool remote, u32* f, u32* nm, u32* nr) {
+  *f = upd_has(P.upd[r], round) ? 1u : 0u;
   *nm = *nr = 0;
   if (!*f) return;
   const u32 par = (round - 1u) & 1u, N = C.n;
@@ -247,8 +249,7 @@ __global__ __launch_bounds__(kBlock) void k_cs_count(Planes P, Params C, u64 fir
                                                      u32 round, bool remote, u32* bsum) {
   const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
   u32 f = 0, nm = 0, nr = 0;
-  rbe_update u;
-  if (i < count) step_out_counts(P, C, first + i, round, remote, &f, &nm, &nr, &u);
+  if (i < count) step_out_counts(P, C, first + i, round, remote, &f, &nm, &nr);
   u32 tf, tm, tr;
   block_excl_scan(f, &tf);
   block_excl_scan(nm, &tm);
@@ -259,23 +260,6 @@ __global__ __launch_bounds__(kBlock) void k_cs_count(Planes P, Params C, u64 fir
     bsum[3 * blockIdx.x + 2] = tr;
   }
 }
-// one block: exclusive prefixes of the block-sum triples, totals in pre[3 * nb]
-__global__ __launch_bounds__(kBlock) void k_cs_scan(const u32* bsum, u32 nb, u64* pre) {
-  u64 c[3] = {0, 0, 0};
-  for (u32 b0 = 0; b0 < nb; b0 += kBlock) {
-    const u32 b = b0 + threadIdx.x;
-#pragma unroll
-    for (int q = 0; q < 3; q++) {
-      const u32 v = b < nb ? bsum[3 * b + q] : 0u;
-      u32 t;
-      const u32 ex = block_excl_scan(v, &t);
-      if (b < nb) pre[3 * b + q] = c[q] + ex;
-      c[q] += t;
-    }
-  }
-  if (threadIdx.x == 0)
-    for (int q = 0; q < 3; q++) pre[3 * nb + q] = c[q];
-}
 __global__ __launch_bounds__(kBlock) void k_cs_write(Planes P, Params C, u64 first, u64 count,
                                                      u32 round, bool remote, const u64* pre,
                                                      u64* rep, rbe_update* ou, u64* moff,
@@ -283,8 +267,7 @@ __global__ __launch_bounds__(kBlock) void k_cs_write(Planes P, Params C, u64 fir
                                                      rbe_ready_to_read* orr, u64 n_tot) {
   const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
   u32 f = 0, nm = 0, nr = 0;
-  rbe_update u;
-  if (i < count) step_out_counts(P, C, first + i, round, remote, &f, &nm, &nr, &u);
+  if (i < count) step_out_counts(P, C, first + i, round, remote, &f, &nm, &nr);
   u32 t;
   const u64 at = pre[3 * blockIdx.x] + block_excl_scan(f, &t);
   const u64 bm = pre[3 * blockIdx.x + 1] + block_excl_scan(nm, &t);
@@ -295,6 +278,8 @@ __global__ __launch_bounds__(kBlock) void k_cs_write(Planes P, Params C, u64 fir
   }
   if (!f) return;
   const u64 r = first + i;
+  rbe_update u;
+  upd_of(P, r, round, &u);
   rep[at] = r;
   ou[at] = u;
   moff[at] = bm;
@@ -328,8 +313,7 @@ __global__ __launch_bounds__(kBlock) void k_cs_write(Planes P, Params C, u64 fir
 __global__ __launch_bounds__(kBlock) void k_upd_count(Planes P, u64 first, u64 count, u32 round,
                                                       u32* bsum) {
   const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
-  rbe_update u;
-  const u32 f = i < count && upd_of(P, first + i, round, &u) ? 1u : 0u;
+  const u32 f = i < count && upd_has(P.upd[first + i], round) ? 1u : 0u;
   u32 t;
   block_excl_scan(f, &t);
   if (threadIdx.x == 0) {
@@ -340,11 +324,12 @@ __global__ __launch_bounds__(kBlock) void k_upd_count(Planes P, u64 first, u64 c
 __global__ __launch_bounds__(kBlock) void k_upd_write(Planes P, u64 first, u64 count, u32 round,
                                                       const u64* pre, u64* rep, rbe_update* ou) {
   const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
-  rbe_update u;
-  const u32 f = i < count && upd_of(P, first + i, round, &u) ? 1u : 0u;
+  const u32 f = i < count && upd_has(P.upd[first + i], round) ? 1u : 0u;
   u32 t;
   const u64 at = pre[2 * blockIdx.x] + block_excl_scan(f, &t);
   if (!f) return;
+  rbe_update u;
+  upd_of(P, first + i, round, &u);
   rep[at] = first + i;
   ou[at] = u;
 }
@@ -830,6 +815,7 @@ int rbe_destroy(rbe_engine* e) {
   if (e->iso_dev) HIP_IGNORE(hipFree(e->iso_dev));
   if (e->upd_host) HIP_IGNORE(hipHostFree(e->upd_host));
   if (e->cs_dev) HIP_IGNORE(hipFree(e->cs_dev));
+  if (e->P.prof) HIP_IGNORE(hipFree(e->P.prof));
   if (e->cs_host) HIP_IGNORE(hipHostFree(e->cs_host));
   if (e->wire_dev) HIP_IGNORE(hipFree(e->wire_dev));
   if (e->wire_meta) HIP_IGNORE(hipFree(e->wire_meta));
@@ -1435,21 +1421,33 @@ int rbe_notify_applied(rbe_engine* e, uint64_t n, const uint64_t* replica,
   return e->hin.notify_applied(n, replica, applied);
 }
 
-#ifdef RBE_FULL_PROF
-// diagnostic build: the k_full_list wave records since the last call (at most
-// cap of them, 4 words each: wall-clock span, lane-class masks, lanes) and clear
-extern "C" int rbe_debug_full_prof(uint64_t* out, uint64_t cap, uint64_t* n) {
-  unsigned long long cnt = 0;
-  HIP_OK(hipDeviceSynchronize());
-  HIP_OK(hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(g_full_prof_n), sizeof(cnt)));
+// Diagnostic: the k_full_list wave records of an RBE_FULL_PROF build since
+// the last call (4 words each: wall-clock span, two lane-class masks, lanes |
+// max inbound << 8 | max outbound << 24), at most cap of them, and clear.  The
+// first call allocates the record buffer (and drops a captured graph, whose
+// kernels hold the planes by value); without RBE_FULL_PROF nothing is recorded.
+extern "C" int rbe_debug_full_prof(rbe_engine* e, uint64_t* out, uint64_t cap, uint64_t* n) {
+  if (!e || !n) return RBE_E_INVALID;
+  HIP_OK(hipSetDevice(e->device));
+  if (!e->P.prof) {
+    HIP_OK(hipMalloc((void**)&e->P.prof, (4 + 4 * kFullProfCap) * sizeof(u64)));
+    HIP_OK(hipMemset(e->P.prof, 0, 4 * sizeof(u64)));
+    if (e->graph) {
+      HIP_IGNORE(hipGraphExecDestroy(e->graph));
+      e->graph = nullptr;
+    }
+    *n = 0;
+    return RBE_OK;
+  }
+  HIP_OK(hipStreamSynchronize(e->stream));
+  u64 cnt = 0;
+  HIP_OK(hipMemcpy(&cnt, e->P.prof, sizeof(u64), hipMemcpyDeviceToHost));
   const u64 m = std::min<u64>(std::min<u64>(cnt, kFullProfCap), cap);
-  if (m) HIP_OK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_full_prof), m * 32));
+  if (m && out) HIP_OK(hipMemcpy(out, e->P.prof + 4, m * 4 * sizeof(u64), hipMemcpyDeviceToHost));
   *n = cnt;
-  cnt = 0;
-  HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_full_prof_n), &cnt, sizeof(cnt)));
+  HIP_OK(hipMemset(e->P.prof, 0, sizeof(u64)));
   return RBE_OK;
 }
-#endif
 
 #ifdef RBE_PHASE_TIMING
 // diagnostic build: read and clear the per-phase stamp sums (rbe_fast.h)
@@ -1872,7 +1870,7 @@ int rbe_collect_outputs(rbe_engine* e, uint64_t first, uint64_t count, rbe_outpu
   u64* pre = (u64*)(e->out_dev + o_pre);
   hipLaunchKernelGGL(k_out_count, dim3(nb), dim3(kBlock), 0, e->stream, e->P, e->C, (u64)first,
                      (u64)count, e->round, bsum);
-  hipLaunchKernelGGL(k_out_scan, dim3(1), dim3(kBlock), 0, e->stream, bsum, nb, pre);
+  hipLaunchKernelGGL(k_scan_q<2>, dim3(1), dim3(kBlock), 0, e->stream, bsum, nb, pre);
   HIP_OK(hipGetLastError());
   u64 tot[2];
   HIP_OK(hipMemcpyAsync(tot, pre + 2ull * nb, sizeof(tot), hipMemcpyDeviceToHost, e->stream));
@@ -1928,7 +1926,7 @@ int rbe_collect_step(rbe_engine* e, uint64_t first, uint64_t count, uint32_t fla
   u64* pre = (u64*)(e->cs_dev + o_pre);
   hipLaunchKernelGGL(k_cs_count, dim3(nb), dim3(kBlock), 0, e->stream, e->P, e->C, (u64)first,
                      (u64)count, e->round, remote, (u32*)e->cs_dev);
-  hipLaunchKernelGGL(k_cs_scan, dim3(1), dim3(kBlock), 0, e->stream, (const u32*)e->cs_dev, nb,
+  hipLaunchKernelGGL(k_scan_q<3>, dim3(1), dim3(kBlock), 0, e->stream, (const u32*)e->cs_dev, nb,
                      pre);
   HIP_OK(hipGetLastError());
   u64 tot[3];
@@ -1987,7 +1985,7 @@ int rbe_collect_updates(rbe_engine* e, uint64_t first, uint64_t count, rbe_updat
   u64* pre = (u64*)(e->upd_dev + o_pre);
   hipLaunchKernelGGL(k_upd_count, dim3(nb), dim3(kBlock), 0, e->stream, e->P, (u64)first,
                      (u64)count, e->round, (u32*)e->upd_dev);
-  hipLaunchKernelGGL(k_out_scan, dim3(1), dim3(kBlock), 0, e->stream, (const u32*)e->upd_dev, nb,
+  hipLaunchKernelGGL(k_scan_q<2>, dim3(1), dim3(kBlock), 0, e->stream, (const u32*)e->upd_dev, nb,
                      pre);
   HIP_OK(hipGetLastError());
   u64 tot[2];

@@ -217,6 +217,17 @@ RBE_HD void apply_pair(const Planes& P, u64 rep, u64 val) {
 // The rbe_update of replica r after round `round` - 1 from its Upd, Core and
 // Hot rows (rbe_get_updates).  A replica that made no Update-writing step in
 // that round (an idle round finished in triage) has an empty Update.
+// RBE_UF_HAS_UPDATE of update_view from the Upd record alone (the collect
+// passes test every replica; a stale record, the common case, is one 16-B read)
+RBE_HD bool upd_has(const Upd& d, u32 round) {
+  if (!(round > 0 && d.round == round - 1)) return false;
+  const u32 f = d.flags & ~UF_RANGES;
+  if ((f & RBE_UF_STATE_CHANGED) || d.n_msgs || d.n_rtr ||
+      (f & (RBE_UF_SENT_QUIESCE | RBE_UF_SNAPSHOT | RBE_UF_APPLIED | RBE_UF_HAS_UPDATE)))
+    return true;
+  return (d.flags & UF_RANGES) && (d.n_drop_ent || d.n_drop_ri || d.save_lo <= d.save_hi ||
+                                   d.apply_lo <= d.apply_hi);
+}
 RBE_HD void update_view(const Upd& d, const Core& c, const Hot& h, u32 round, rbe_update& u) {
   u = rbe_update{};
   u.term = c.term;

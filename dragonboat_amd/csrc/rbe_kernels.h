@@ -961,11 +961,7 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, 
 #endif
 }
 
-#if defined(RBE_FULL_PROF)
-static constexpr u64 kFullProfCap = 1u << 20;
-__device__ unsigned long long g_full_prof_n;
-__device__ unsigned long long g_full_prof[kFullProfCap][4];
-#endif
+static constexpr u64 kFullProfCap = 1u << 20;  // wave records of RBE_FULL_PROF builds
 
 // Pass 3: the whole handler table over the full list (persistent, grid-stride).
 template <int N, bool TRACE>
@@ -1020,28 +1016,35 @@ __global__ __launch_bounds__(kBlock) void k_full_list(Planes P, Params C, RoundA
     __syncthreads();
   }
 #elif defined(RBE_FULL_PROF)
-  // Diagnostic build: every wave iteration's s_memtime span and the classes of
-  // its lanes (role before, role after, any inbound message), for
+  // Diagnostic build: every wave iteration's s_memrealtime span, its active
+  // lanes, the classes of its lanes (role before, role after, any inbound
+  // message) and the most inbound / outbound messages of a lane, for
   // scripts/full_prof.py: what the slowest waves of the general step hold.
   for (u64 b0 = (u64)blockIdx.x * kBlock; b0 < n; b0 += (u64)gridDim.x * kBlock) {
     const u64 i = b0 + threadIdx.x;
-    u32 r = 0, cls_b = 0;
+    u32 r = 0, cls_b = 0, nin = 0;
     const bool on = i < n;
     if (on) {
       const u32 sg = seg_find<kShards>(s_pre, (u32)i);
       r = L.idx[list_pos(L, 2, sg, false, (u32)i - s_pre[sg])];
       const u64 g = r / N;
       const u32 k = (u32)(r % N);
-      u32 inb = 0;
       for (u32 s = 0; s < N; s++)
-        if (s != k) inb |= in_word<N>(P, g, s, k, round);
-      cls_b = ((u32)P.hot[r].role << 4) | (inb ? 1u : 0u);
+        if (s != k) {
+          const u32 w = in_word<N>(P, g, s, k, round);
+          nin += (w & 0x7Fu) + ((w >> 7) & 0x7Fu);
+        }
+      cls_b = ((u32)P.hot[r].role << 4) | (nin ? 1u : 0u);
     }
-    if (__ballot(on) == 0ull) continue;
+    const u64 m_on = __ballot(on);
+    if (m_on == 0ull) continue;
     const unsigned long long t0 = wall_clock64();
     if (on) step_replica<N, TRACE, kFullMode>(P, C, r, ck, c);
-    u32 cls = 0;
-    if (on) cls = cls_b | ((u32)P.hot[r].role << 1);
+    u32 cls = 0, nout = 0;
+    if (on) {
+      cls = cls_b | ((u32)P.hot[r].role << 1);
+      nout = P.upd[r].n_msgs;
+    }
     const unsigned long long t1 = wall_clock64();
     u64 mlo = 0, mhi = 0;
     for (u32 q = 0; q < 128; q++) {  // OR of the lanes' class bits (uniform loop)
@@ -1051,13 +1054,19 @@ __global__ __launch_bounds__(kBlock) void k_full_list(Planes P, Params C, RoundA
         else mhi |= 1ull << (q - 64);
       }
     }
-    if ((threadIdx.x & 63u) == 0) {
-      const u64 at = atomicAdd((unsigned long long*)&g_full_prof_n, 1ull);
+    u32 mx_in = nin, mx_out = nout;
+    for (int o = 32; o > 0; o >>= 1) {
+      mx_in = max(mx_in, (u32)__shfl_xor((int)mx_in, o, 64));
+      mx_out = max(mx_out, (u32)__shfl_xor((int)mx_out, o, 64));
+    }
+    if ((threadIdx.x & 63u) == 0 && P.prof) {
+      const u64 at = atomicAdd((unsigned long long*)&P.prof[0], 1ull);
       if (at < kFullProfCap) {
-        g_full_prof[at][0] = t1 - t0;
-        g_full_prof[at][1] = mlo;
-        g_full_prof[at][2] = mhi;
-        g_full_prof[at][3] = (u64)__popcll(__ballot(on));
+        u64* rec = &P.prof[4 + at * 4];
+        rec[0] = t1 - t0;
+        rec[1] = mlo;
+        rec[2] = mhi;
+        rec[3] = (u64)__popcll(m_on) | ((u64)mx_in << 8) | ((u64)mx_out << 24);
       }
     }
   }

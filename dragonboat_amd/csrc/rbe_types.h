@@ -404,11 +404,14 @@ struct Planes {
   // null: slot s is node s + 1.  Only the boundary's converters read it: the
   // protocol state inside the engine names nodes by slot + 1
   const u64* node_ids;
-  u32 ids_n;
+  u32 ids_n;           // slots per group (Params::n), for indexing node_ids in kernels without Params
   // [n_rep] (membership) each replica's observers | witnesses << 8, bit s =
   // slot s: raft.observers / raft.witnesses (raft.go:206-207), read by the full
   // handler table only (Core::members has MB_ROLES while any is set)
-  u16* roles;          // slots per group (Params::n), for indexing node_ids in kernels without Params
+  u16* roles;
+  // diagnostic builds only (-DRBE_FULL_PROF): k_full_list's wave records
+  // (rbe_debug_full_prof); null otherwise
+  u64* prof;
 };
 
 }  // namespace rbe

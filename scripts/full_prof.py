@@ -1,13 +1,13 @@
 """Diagnostic: what the slowest waves of k_full_list hold, from the
 RBE_FULL_PROF build (build/full_prof.so):
 
-    hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DRBE_SINGLE_TU -DRBE_FULL_PROF \
-        -o build/full_prof.so dragonboat_amd/csrc/rbe_engine.hip dragonboat_amd/csrc/rbe_sort.hip
+    scripts/build_variant.sh build/full_prof.so -DRBE_FULL_PROF
     RBE_LIB=$PWD/build/full_prof.so python scripts/full_prof.py c3
 
 Each record is one wave iteration of the general step: its wall-clock span
-(s_memrealtime, 100 MHz) and the classes of its lanes, a class being (role
-before, role after, any inbound message)."""
+(s_memrealtime, 100 MHz), its active lanes, the classes of its lanes, a class
+being (role before, role after, any inbound message), and the most inbound
+and outbound messages of one of its lanes."""
 import ctypes as C
 import os
 import sys
@@ -20,7 +20,7 @@ import bench  # noqa: E402
 from dragonboat_amd import engine as E  # noqa: E402
 
 lib = E.load_library(os.environ["RBE_LIB"])
-lib.rbe_debug_full_prof.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
+lib.rbe_debug_full_prof.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
 w = sys.argv[1] if len(sys.argv) > 1 else "c3"
 kw, settle, _ = bench.WORKLOADS[w]
 eng = E.Engine(**dict(kw))
@@ -29,10 +29,10 @@ eng.sync()
 cap = 1 << 20
 buf = np.zeros((cap, 4), np.uint64)
 n = C.c_uint64()
-lib.rbe_debug_full_prof(buf.ctypes.data, cap, C.byref(n))
+lib.rbe_debug_full_prof(eng.h, buf.ctypes.data, cap, C.byref(n))  # allocates, clears
 rounds = 20
 ms = eng.profile_rounds(rounds)
-lib.rbe_debug_full_prof(buf.ctypes.data, cap, C.byref(n))
+lib.rbe_debug_full_prof(eng.h, buf.ctypes.data, cap, C.byref(n))
 m = min(n.value, cap)
 rec = buf[:m]
 dt = rec[:, 0].astype(np.float64) * 10e-3  # us
@@ -43,7 +43,10 @@ for q in range(128):
     if rb < 5 and ra < 5:
         names[q] = f"{ROLES[rb]}->{ROLES[ra]}{'+in' if inb else ''}"
 print(f"{w}: {rounds} rounds, kernel split (ms/round) {[round(x / rounds, 4) for x in ms]}")
-print(f"wave iterations {m} ({m / rounds:.0f}/round), lanes/iter {rec[:, 3].mean():.1f}, "
+lanes = (rec[:, 3] & np.uint64(0xFF)).astype(np.int64)
+mx_in = ((rec[:, 3] >> np.uint64(8)) & np.uint64(0xFFFF)).astype(np.int64)
+mx_out = ((rec[:, 3] >> np.uint64(24)) & np.uint64(0xFFFF)).astype(np.int64)
+print(f"wave iterations {m} ({m / rounds:.0f}/round), lanes/iter {lanes.mean():.1f}, "
       f"span us: mean {dt.mean():.2f} p50 {np.median(dt):.2f} p99 {np.percentile(dt, 99):.2f} "
       f"max {dt.max():.2f}")
 stats = []
@@ -67,3 +70,11 @@ for q, nm in names.items():
         single.append((dt[only].mean(), nm, int(only.sum())))
 single.sort(reverse=True)
 print("single-class waves:", [(nm, round(mu, 2), c) for mu, nm, c in single[:12]])
+# span against the busiest lane's message counts
+for lo, hi in ((0, 2), (2, 5), (5, 10), (10, 20), (20, 1 << 16)):
+    sel = (mx_in >= lo) & (mx_in < hi)
+    if sel.any():
+        print(f"max inbound {lo:3d}-{hi:5d}: waves {int(sel.sum()):6d} span mean {dt[sel].mean():8.2f} "
+              f"max out mean {mx_out[sel].mean():6.1f} lanes {lanes[sel].mean():5.1f}")
+order = np.argsort(-dt)[:10]
+print("slowest:", [(round(float(dt[i]), 1), int(lanes[i]), int(mx_in[i]), int(mx_out[i])) for i in order])
