@@ -204,6 +204,43 @@ def load_traffic(name, kernel, lib):
     return d.get("bytes_per_launch", {}).get(kernel), "same library"
 
 
+def side_line(name, local, steps, prof_rounds):
+    """A short line of another BASELINE configuration on the same GPU (one
+    rank, untraced, same definitions as the main line): group-steps/s over
+    `steps` timed rounds and the per-kernel split of `prof_rounds` more."""
+    from dragonboat_amd.engine import Engine, make_config
+    kw, settle, desc = WORKLOADS[name]
+    eng = Engine(make_config(device=local, trace=False, **dict(kw)))
+    eng.run(settle + 10)
+    eng.sync()
+    eng.reset_counters()
+    t0 = time.perf_counter()
+    ev_ms = eng.run_timed(steps)
+    eng.sync()
+    wall = time.perf_counter() - t0
+    c = eng.counters()
+    nf, _ = eng.fault_summary()
+    eng.reset_counters()
+    kms = eng.profile_rounds(prof_rounds)
+    kernels = []
+    for ki, kn in enumerate(eng.kernel_names()):
+        if not kn:
+            continue
+        b = alg_bytes(eng.kernel_counters(ki)) / prof_rounds
+        us = kms[ki] * 1e3 / prof_rounds
+        kernels.append({"kernel": kn, "avg_us": us, "alg_bytes_per_launch": b,
+                        "achieved_gbs": (b / (us * 1e-6) / 1e9) if us > 0 else 0.0})
+    dom = max(kernels, key=lambda k: k["avg_us"])
+    eng.close()
+    return {"workload": desc, "value": c["steps"] / wall, "unit": "group-steps/s",
+            "ms_per_step": wall * 1e3 / steps, "event_ms_per_round": ev_ms / steps,
+            "steps": steps, "faulty_replicas": int(nf),
+            "committed_entries_per_s": c["committed"] / wall,
+            "dominant": {"kernel": dom["kernel"], "avg_us": dom["avg_us"],
+                         "frac": dom["achieved_gbs"] / HBM_PEAK_GBS},
+            "kernels": kernels}
+
+
 def run_replica_mode(args, ws, rank, local, dist, dev, gloo_staged):
     """C5: replica-per-GPU.  Every round = one engine round over the owned
     replicas + one exchange (pack → counts all-to-all → records
@@ -527,6 +564,8 @@ def main():
                     help="groups in the 1-thread CPU sample (0 = per-workload default)")
     ap.add_argument("--xchg-gloo", action="store_true",
                     help="c5 rehearsal: all ranks on cuda:0, exchange over gloo via host memory")
+    ap.add_argument("--also", default="c2,c3",
+                    help="other workloads timed briefly in the same run (comma list, '' = none)")
     ap.add_argument("--c4h-all-msgs", action="store_true",
                     help="c4h: read every message back too (rbe_collect_outputs)")
     ap.add_argument("--xchg-fixed", action="store_true",
@@ -667,6 +706,15 @@ def main():
             },
         }
         out["library"] = lib
+        # the other single-GPU BASELINE configurations, timed in the same run
+        # (parity cases elsewhere; here only their rate and kernel split)
+        if ws == 1 and args.also:
+            out["workloads"] = {}
+            for name in [x for x in args.also.split(",") if x and x != args.workload]:
+                try:
+                    out["workloads"][name] = side_line(name, local, 50, 20)
+                except Exception as ex:  # a side line must not hide the main one
+                    out["workloads"][name] = {"error": repr(ex)}
         if not args.no_cpu_baseline and ws == 1:
             try:
                 ng = int(kw["n_groups"])

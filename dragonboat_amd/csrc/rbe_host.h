@@ -463,8 +463,13 @@ struct HostInputs {
   u64 n_rep = 0;
   u32 n = 0;
   u32 in_cap = 0;
-  std::vector<u32> slot;    // [n_rep] index into recs, ~0u = nothing staged
-  std::vector<u32> mark;    // [n_rep] duplicate check within one call (epoch stamps)
+  // [n_rep] per replica: index into recs (~0u = nothing staged) and the
+  // duplicate-check stamp of the current call, side by side so a push touches
+  // one cache line per replica
+  struct SlotMark {
+    u32 slot, mark;
+  };
+  std::vector<SlotMark> sm;
   u32 epoch = 0;
   std::vector<u64> reps;    // staged replicas ...
   std::vector<ExtIn> recs;  // ... and their input records
@@ -532,8 +537,7 @@ struct HostInputs {
     n = n_;
     in_cap = in_cap_;
     heap.cap = heap_bytes;
-    slot.assign(n_rep, ~0u);
-    mark.assign(n_rep, 0u);
+    sm.assign(n_rep, SlotMark{~0u, 0u});
     applied.assign(n_rep, 0);
     committing.assign(n_rep, 0);
     snap_slot.assign(n_rep, ~0u);
@@ -543,7 +547,7 @@ struct HostInputs {
            snaps.empty();
   }
   void clear() {
-    for (u64 r : reps) slot[r] = ~0u;
+    for (u64 r : reps) sm[r].slot = ~0u;
     reps.clear();
     recs.clear();
     ents.clear();
@@ -557,16 +561,16 @@ struct HostInputs {
     heap.settle();
   }
   ExtIn& rec(u64 r) {
-    if (slot[r] == ~0u) {
-      slot[r] = (u32)recs.size();
+    if (sm[r].slot == ~0u) {
+      sm[r].slot = (u32)recs.size();
       reps.push_back(r);
       ExtIn z;
       memset(&z, 0, sizeof(z));
       recs.push_back(z);
     }
-    return recs[slot[r]];
+    return recs[sm[r].slot];
   }
-  u32 staged_flags(u64 r) const { return slot[r] == ~0u ? 0u : recs[slot[r]].flags; }
+  u32 staged_flags(u64 r) const { return sm[r].slot == ~0u ? 0u : recs[sm[r].slot].flags; }
   // 0, or RBE_E_INVALID / RBE_E_STATE for the whole batch: every replica in
   // range, none twice in the batch, none with `flag` already staged
   int check_replicas(u64 cnt, const u64* replica, u32 flag) {
@@ -578,13 +582,13 @@ struct HostInputs {
     }
     if (!flag) return RBE_OK;
     if (++epoch == 0) {
-      mark.assign(n_rep, 0u);
+      for (SlotMark& x : sm) x.mark = 0u;
       epoch = 1;
     }
     for (u64 i = 0; i < cnt; i++) {
       const u64 r = replica[i];
-      if (mark[r] == epoch || (staged_flags(r) & flag)) return RBE_E_STATE;
-      mark[r] = epoch;
+      if (sm[r].mark == epoch || (staged_flags(r) & flag)) return RBE_E_STATE;
+      sm[r].mark = epoch;
     }
     return RBE_OK;
   }

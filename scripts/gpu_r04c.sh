@@ -13,7 +13,7 @@ echo "tests ok $(( $(date +%s) - S ))s"; tail -1 gpurun_out/gpu_tests_b.log
 for i in 1 2; do
   for lib in dragonboat_amd/libdragonboat_amd.so build/ctr0.so; do
     for w in c4 c2m; do
-      RBE_LIB=$PWD/$lib timeout -k 10 200 python bench.py --workload $w --no-cpu-baseline --steps 100 --warmup 10 > gpurun_out/ab.json 2>gpurun_out/ab.err || { tail -20 gpurun_out/ab.err; exit 1; }
+      RBE_LIB=$PWD/$lib timeout -k 10 200 python bench.py --workload $w --no-cpu-baseline --also "" --steps 100 --warmup 10 > gpurun_out/ab.json 2>gpurun_out/ab.err || { tail -20 gpurun_out/ab.err; exit 1; }
       python3 scripts/summarize_bench.py gpurun_out/ab.json "$(basename $lib) $w" | head -1
     done
   done

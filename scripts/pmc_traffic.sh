@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 for w in ${WORKLOADS:-c4 c2m}; do
   for ctr in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 120 rocprofv3 --pmc $ctr -d gpurun_out/pmc_${w}_$ctr -o run --output-format csv -- python3 bench.py --workload $w --steps 10 --warmup 2 --prof-rounds 10 --no-cpu-baseline > gpurun_out/pmc_${w}_$ctr.log 2>&1
+    timeout -s KILL 120 rocprofv3 --pmc $ctr -d gpurun_out/pmc_${w}_$ctr -o run --output-format csv -- python3 bench.py --workload $w --steps 10 --warmup 2 --prof-rounds 10 --no-cpu-baseline --also "" > gpurun_out/pmc_${w}_$ctr.log 2>&1
   done
   python3 scripts/pmc_traffic.py $w gpurun_out/pmc_${w}_FETCH_SIZE gpurun_out/pmc_${w}_WRITE_SIZE
 done
