@@ -54,7 +54,11 @@ static constexpr int kBlock = 256;
 #ifndef RBE_FULL_DEFER
 #define RBE_FULL_DEFER 0  // measured: 207 us without, 211 us with (C3)
 #endif
-static constexpr int kFullMode = RBE_FULL_DEFER ? MODE_FULL_DEFER : MODE_FULL;
+#ifndef RBE_FULL_LREM
+#define RBE_FULL_LREM 1  // k_full_list keeps the replica's remote slots in LDS (MODE_FULL_LREM)
+#endif
+static constexpr int kFullMode = RBE_FULL_LREM ? (RBE_FULL_DEFER ? MODE_FULL_LREM_DEFER : MODE_FULL_LREM)
+                                               : (RBE_FULL_DEFER ? MODE_FULL_DEFER : MODE_FULL);
 #ifndef RBE_FAST_MIX
 #define RBE_FAST_MIX 0  // measured: C4 k_fast_both 138 vs 113 us, C3 399 vs 345 us
 #endif

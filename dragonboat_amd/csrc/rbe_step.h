@@ -475,7 +475,11 @@ struct StepCounters {
 };
 
 // ----------------------------------------------------------------- the lane
-enum : int { MODE_FULL = 0, MODE_LEAD = 1, MODE_FOLL = 2, MODE_FULL_DEFER = 3 };
+enum : int {
+  MODE_FULL = 0, MODE_LEAD = 1, MODE_FOLL = 2, MODE_FULL_DEFER = 3,
+  MODE_FULL_LREM = 4,        // the whole table, the replica's remote slots in LDS (k_full_list)
+  MODE_FULL_LREM_DEFER = 5,  // ... and its sends deferred too
+};
 
 // Deferred message stores of the general step (MODE_FULL_DEFER, k_full_list):
 // send() keeps up to kLaneDefer messages of the lane in LDS and the step
@@ -487,7 +491,21 @@ constexpr u32 kLaneDefer = 6;
 // entries per batch of the general step's entry loops (Lane::copy_ring_to_arena,
 // on_replicate): loads of a batch are issued together, then its stores
 constexpr u32 kEntBatch = 8;
+// The replica's remote slots during a step of the general table in LDS
+// (MODE_FULL_LREM, k_full_list): loaded once before the step's first store,
+// written back at its end.  The handlers read and update them message by
+// message; in global memory each such read after the step's first store
+// waited for every store before it (vmcnt is in order), a round trip per
+// handler: C3's general step spent ~10 us per inbound message.
 #if defined(__HIPCC__) || defined(__HIP__)
+__device__ __forceinline__ RemoteMN (&lane_rem())[kMaxN][256] {
+  __shared__ RemoteMN s_rem[kMaxN][256];
+  return s_rem;
+}
+__device__ __forceinline__ u8 (&lane_rst())[kMaxN][256] {
+  __shared__ u8 s_rst[kMaxN][256];
+  return s_rst;
+}
 __device__ __forceinline__ Msg (&lane_defer_msgs())[kLaneDefer][256] {
   __shared__ Msg s_msgs[kLaneDefer][256];
   return s_msgs;
@@ -500,8 +518,14 @@ __device__ __forceinline__ u64 (&lane_defer_dst())[kLaneDefer][256] {
 
 template <int N, bool TRACE, int MODE>
 struct Lane {
-  static constexpr bool FULL = MODE == MODE_FULL || MODE == MODE_FULL_DEFER;  // the whole handler table
-  static constexpr bool DEFER = MODE == MODE_FULL_DEFER;  // sends kept in LDS until the end
+  static constexpr bool FULL = MODE == MODE_FULL || MODE == MODE_FULL_DEFER ||
+                               MODE == MODE_FULL_LREM || MODE == MODE_FULL_LREM_DEFER;  // the whole handler table
+  static constexpr bool DEFER = MODE == MODE_FULL_DEFER || MODE == MODE_FULL_LREM_DEFER;  // sends kept in LDS until the end
+#if defined(__HIP_DEVICE_COMPILE__)
+  static constexpr bool LREM = MODE == MODE_FULL_LREM || MODE == MODE_FULL_LREM_DEFER;  // remote slots in LDS
+#else
+  static constexpr bool LREM = false;  // host builds keep them in the planes
+#endif
   static constexpr bool LEAD = MODE == MODE_LEAD;  // steady-state leader subset
   static constexpr bool FOLL = MODE == MODE_FOLL;  // steady-state follower subset
   const Planes& P;
@@ -659,12 +683,21 @@ struct Lane {
   // slots in registers for the whole round (loaded by load(), written back by
   // store()); the selects over a compile-time N keep them out of scratch.
   // The other modes read and write the SoA planes directly.
+#if defined(__HIP_DEVICE_COMPILE__)
+  __device__ __forceinline__ RemoteMN& lrem(u32 s) const { return lane_rem()[s][threadIdx.x]; }
+  __device__ __forceinline__ u8& lrst(u32 s) const { return lane_rst()[s][threadIdx.x]; }
+#else
+  RemoteMN& lrem(u32 s) const { return P.rem[r * N + s]; }  // (not instantiated on the host)
+  u8& lrst(u32 s) const { return P.rem_st[r * N + s]; }
+#endif
   RBE_HD u64 rmatch(u32 s) const {
     if constexpr (LEAD) {
       u64 v = 0;
       for (u32 i = 0; i < N; i++)
         if (i == s) v = c_match[i];
       return v;
+    } else if constexpr (LREM) {
+      return lrem(s).match;
     } else {
       return P.rem[r * N + s].match;
     }
@@ -675,6 +708,8 @@ struct Lane {
       for (u32 i = 0; i < N; i++)
         if (i == s) v = c_next[i];
       return v;
+    } else if constexpr (LREM) {
+      return lrem(s).next;
     } else {
       return P.rem[r * N + s].next;
     }
@@ -685,6 +720,8 @@ struct Lane {
       for (u32 i = 0; i < N; i++)
         if (i == s) v = c_st[i];
       return v;
+    } else if constexpr (LREM) {
+      return lrst(s);
     } else {
       return P.rem_st[r * N + s];
     }
@@ -693,6 +730,8 @@ struct Lane {
     if constexpr (LEAD) {
       for (u32 i = 0; i < N; i++)
         if (i == s) c_match[i] = v;
+    } else if constexpr (LREM) {
+      lrem(s).match = v;
     } else {
       P.rem[r * N + s].match = v;
     }
@@ -701,6 +740,8 @@ struct Lane {
     if constexpr (LEAD) {
       for (u32 i = 0; i < N; i++)
         if (i == s) c_next[i] = v;
+    } else if constexpr (LREM) {
+      lrem(s).next = v;
     } else {
       P.rem[r * N + s].next = v;
     }
@@ -709,6 +750,8 @@ struct Lane {
     if constexpr (LEAD) {
       for (u32 i = 0; i < N; i++)
         if (i == s) c_st[i] = v;
+    } else if constexpr (LREM) {
+      lrst(s) = (u8)v;
     } else {
       P.rem_st[r * N + s] = (u8)v;
     }
@@ -2366,6 +2409,12 @@ struct Lane {
         P.rem_st[r * N + s] = (u8)c_st[s];
       }
     }
+    if constexpr (LREM) {
+      for (u32 s = 0; s < N; s++) {
+        P.rem[r * N + s] = lrem(s);
+        P.rem_st[r * N + s] = lrst(s);
+      }
+    }
   }
 
   // Steps the replica through one round.  The fast variant (FULL = false)
@@ -2382,6 +2431,12 @@ struct Lane {
         c_match[s] = x.match;
         c_next[s] = x.next;
         c_st[s] = P.rem_st[r * N + s];
+      }
+    }
+    if constexpr (LREM) {
+      for (u32 s = 0; s < N; s++) {
+        lrem(s) = P.rem[r * N + s];
+        lrst(s) = P.rem_st[r * N + s];
       }
     }
     fault = (flags & HF_FAULTED) ? P.upd[r].fault : 0u;
