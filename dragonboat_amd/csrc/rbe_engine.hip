@@ -153,28 +153,59 @@ __global__ __launch_bounds__(kBlock) void k_out_count(Planes P, Params C, u64 fi
     bsum[2 * blockIdx.x + 1] = tr;
   }
 }
-// one block: exclusive prefixes of the Q-tuples of block sums, totals in
-// pre[Q * nb ..].  Thread t owns a contiguous run of ceil(nb / 256) blocks:
-// its run totals are scanned across the block once, then the run is walked
-// (a loop over 256-block slices with two barriers each took 77 us at 11.7k
-// blocks, more than the count and write passes it sits between).
+// one block of 1024: exclusive prefixes of the Q-tuples of block sums, totals
+// in pre[Q * nb ..].  Thread t owns a contiguous run of ceil(nb / 1024)
+// blocks: the run totals are scanned across the block once, then the run is
+// walked (a loop over 256-block slices with two barriers each took 77 us at
+// 11.7k blocks, more than the count and write passes it sits between).
+constexpr u32 kScanThreads = 1024;
+__device__ __forceinline__ u32 block_excl_scan_1k(u32 v, u32* total) {
+  __shared__ u32 s_w[kScanThreads / 64];
+  const u32 lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  u32 x = v;
+#pragma unroll
+  for (u32 o = 1; o < 64; o <<= 1) {
+    const u32 t = __shfl_up(x, o, 64);
+    if (lane >= o) x += t;
+  }
+  __syncthreads();
+  if (lane == 63) s_w[w] = x;
+  __syncthreads();
+  u32 off = 0, tot = 0;
+#pragma unroll
+  for (u32 q = 0; q < kScanThreads / 64; q++) {
+    off += q < w ? s_w[q] : 0u;
+    tot += s_w[q];
+  }
+  *total = tot;
+  return off + x - v;
+}
 template <int Q>
-__global__ __launch_bounds__(kBlock) void k_scan_q(const u32* bsum, u32 nb, u64* pre) {
-  const u32 per = (nb + kBlock - 1) / kBlock;
+__global__ __launch_bounds__(kScanThreads) void k_scan_q(const u32* bsum, u32 nb, u64* pre) {
+  const u32 per = (nb + kScanThreads - 1) / kScanThreads;
   const u32 b0 = threadIdx.x * per < nb ? threadIdx.x * per : nb;
   const u32 b1 = b0 + per < nb ? b0 + per : nb;
+  u32 loc[Q];
+#pragma unroll
+  for (int q = 0; q < Q; q++) loc[q] = 0;
+#pragma unroll 4
+  for (u32 b = b0; b < b1; b++)
+#pragma unroll
+    for (int q = 0; q < Q; q++) loc[q] += bsum[Q * b + q];
+  u64 run[Q];
 #pragma unroll
   for (int q = 0; q < Q; q++) {
-    u32 loc = 0;
-    for (u32 b = b0; b < b1; b++) loc += bsum[Q * b + q];
     u32 tot;
-    u64 run = block_excl_scan(loc, &tot);
-    for (u32 b = b0; b < b1; b++) {
-      pre[Q * b + q] = run;
-      run += bsum[Q * b + q];
-    }
+    run[q] = block_excl_scan_1k(loc[q], &tot);
     if (threadIdx.x == 0) pre[(u64)Q * nb + q] = tot;
   }
+#pragma unroll 4
+  for (u32 b = b0; b < b1; b++)
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+      pre[Q * b + q] = run[q];
+      run[q] += bsum[Q * b + q];
+    }
 }
 __global__ __launch_bounds__(kBlock) void k_out_write(Planes P, Params C, u64 first, u64 count,
                                                       u32 round, const u64* pre, u64* moff,
@@ -219,6 +250,28 @@ __global__ __launch_bounds__(kBlock) void k_out_write(Planes P, Params C, u64 fi
   }
 }
 
+// upd_has on the device: the record's last 16-B chunk (fault, flags, events,
+// round, message and ReadyToRead counts) decides for a stale record — the
+// common case, a quiesced replica — and for a step without ranges; only a
+// step with ranges reads the rest (the collect passes test every replica)
+static_assert(offsetof(Upd, fault) == 48 && offsetof(Upd, flags) == 52 &&
+                  offsetof(Upd, round) == 56 && offsetof(Upd, n_msgs) == 60 &&
+                  offsetof(Upd, n_rtr) == 62,
+              "Upd chunk 3 layout (upd_has_dev)");
+__device__ __forceinline__ bool upd_has_dev(const Planes& P, u64 r, u32 round) {
+  const Upd* u = P.upd + r;
+  const uint4 c3 = reinterpret_cast<const uint4*>(u)[3];
+  const u32 flags = c3.y & 0xFFFFu, rnd = c3.z;
+  if (!(round > 0 && rnd == round - 1)) return false;
+  const u32 f = flags & ~(u32)UF_RANGES;
+  if ((f & (RBE_UF_STATE_CHANGED | RBE_UF_SENT_QUIESCE | RBE_UF_SNAPSHOT | RBE_UF_APPLIED |
+            RBE_UF_HAS_UPDATE)) ||
+      c3.w != 0u)  // n_msgs | n_rtr << 16
+    return true;
+  if (!(flags & UF_RANGES)) return false;
+  return upd_has(*u, round);
+}
+
 // ---- rbe_collect_step: Updates, their messages and ReadyToReads, one pass
 // whether replica r's message to slot d is returned (RBE_COLLECT_REMOTE_MSGS:
 // only to replicas another rank steps)
@@ -230,7 +283,7 @@ __device__ __forceinline__ bool out_msg_wanted(const Params& C, u64 g, u32 d, bo
 }
 __device__ __forceinline__ void step_out_counts(const Planes& P, const Params& C, u64 r, u32 round,
                                                 bool remote, u32* f, u32* nm, u32* nr) {
-  *f = upd_has(P.upd[r], round) ? 1u : 0u;
+  *f = upd_has_dev(P, r, round) ? 1u : 0u;
   *nm = *nr = 0;
   if (!*f) return;
   const u32 par = (round - 1u) & 1u, N = C.n;
@@ -313,7 +366,7 @@ __global__ __launch_bounds__(kBlock) void k_cs_write(Planes P, Params C, u64 fir
 __global__ __launch_bounds__(kBlock) void k_upd_count(Planes P, u64 first, u64 count, u32 round,
                                                       u32* bsum) {
   const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
-  const u32 f = i < count && upd_has(P.upd[first + i], round) ? 1u : 0u;
+  const u32 f = i < count && upd_has_dev(P, first + i, round) ? 1u : 0u;
   u32 t;
   block_excl_scan(f, &t);
   if (threadIdx.x == 0) {
@@ -324,7 +377,7 @@ __global__ __launch_bounds__(kBlock) void k_upd_count(Planes P, u64 first, u64 c
 __global__ __launch_bounds__(kBlock) void k_upd_write(Planes P, u64 first, u64 count, u32 round,
                                                       const u64* pre, u64* rep, rbe_update* ou) {
   const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
-  const u32 f = i < count && upd_has(P.upd[first + i], round) ? 1u : 0u;
+  const u32 f = i < count && upd_has_dev(P, first + i, round) ? 1u : 0u;
   u32 t;
   const u64 at = pre[2 * blockIdx.x] + block_excl_scan(f, &t);
   if (!f) return;
@@ -1870,7 +1923,7 @@ int rbe_collect_outputs(rbe_engine* e, uint64_t first, uint64_t count, rbe_outpu
   u64* pre = (u64*)(e->out_dev + o_pre);
   hipLaunchKernelGGL(k_out_count, dim3(nb), dim3(kBlock), 0, e->stream, e->P, e->C, (u64)first,
                      (u64)count, e->round, bsum);
-  hipLaunchKernelGGL(k_scan_q<2>, dim3(1), dim3(kBlock), 0, e->stream, bsum, nb, pre);
+  hipLaunchKernelGGL(k_scan_q<2>, dim3(1), dim3(kScanThreads), 0, e->stream, bsum, nb, pre);
   HIP_OK(hipGetLastError());
   u64 tot[2];
   HIP_OK(hipMemcpyAsync(tot, pre + 2ull * nb, sizeof(tot), hipMemcpyDeviceToHost, e->stream));
@@ -1926,7 +1979,7 @@ int rbe_collect_step(rbe_engine* e, uint64_t first, uint64_t count, uint32_t fla
   u64* pre = (u64*)(e->cs_dev + o_pre);
   hipLaunchKernelGGL(k_cs_count, dim3(nb), dim3(kBlock), 0, e->stream, e->P, e->C, (u64)first,
                      (u64)count, e->round, remote, (u32*)e->cs_dev);
-  hipLaunchKernelGGL(k_scan_q<3>, dim3(1), dim3(kBlock), 0, e->stream, (const u32*)e->cs_dev, nb,
+  hipLaunchKernelGGL(k_scan_q<3>, dim3(1), dim3(kScanThreads), 0, e->stream, (const u32*)e->cs_dev, nb,
                      pre);
   HIP_OK(hipGetLastError());
   u64 tot[3];
@@ -1985,7 +2038,7 @@ int rbe_collect_updates(rbe_engine* e, uint64_t first, uint64_t count, rbe_updat
   u64* pre = (u64*)(e->upd_dev + o_pre);
   hipLaunchKernelGGL(k_upd_count, dim3(nb), dim3(kBlock), 0, e->stream, e->P, (u64)first,
                      (u64)count, e->round, (u32*)e->upd_dev);
-  hipLaunchKernelGGL(k_scan_q<2>, dim3(1), dim3(kBlock), 0, e->stream, (const u32*)e->upd_dev, nb,
+  hipLaunchKernelGGL(k_scan_q<2>, dim3(1), dim3(kScanThreads), 0, e->stream, (const u32*)e->upd_dev, nb,
                      pre);
   HIP_OK(hipGetLastError());
   u64 tot[2];
