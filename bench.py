@@ -419,8 +419,8 @@ def run_host_driven(args, ws, rank, local, dist):
     leader_of = np.zeros(n_groups, dtype=np.uint64)  # leader slot + 1 per group, 0 = none
     cmd = np.frombuffer(rng.bytes(16 * len(active)), dtype=np.uint8).copy()
     ptr = lambda a, t: a.ctypes.data_as(C.POINTER(t))  # noqa: E731
-    stats = {"push": 0.0, "step": 0.0, "enqueue": 0.0, "out": 0.0, "reads": 0, "props": 0,
-             "msgs": 0, "rtr": 0, "upd": 0}
+    stats = {"push": 0.0, "push_abi": 0.0, "step": 0.0, "enqueue": 0.0, "out": 0.0, "reads": 0,
+             "props": 0, "msgs": 0, "rtr": 0, "upd": 0}
 
     def read_back():
         if not all_msgs:
@@ -458,6 +458,8 @@ def run_host_driven(args, ws, rank, local, dist):
         if len(rr):
             lo = (np.uint64(rnd + 1) << np.uint64(32)) | (rr + np.uint64(1))
             hi = rr.copy()
+        tc = time.perf_counter()
+        if len(rr):
             _check(L.rbe_push_read_index(h, len(rr), ptr(rr, C.c_uint64), ptr(lo, C.c_uint64),
                                          ptr(hi, C.c_uint64)), "rbe_push_read_index")
         if len(pr):
@@ -476,6 +478,7 @@ def run_host_driven(args, ws, rank, local, dist):
         t3 = time.perf_counter()
         if timed:
             stats["push"] += t1 - t0
+            stats["push_abi"] += t1 - tc
             stats["step"] += t2 - t1
             stats["enqueue"] += te - t1
             stats["out"] += t3 - t2
@@ -526,6 +529,8 @@ def run_host_driven(args, ws, rank, local, dist):
             "faulty_replicas": int(nf), "fault_bits_rank0": fo,
             "boundary": {
                 "push_ms_per_round": stats["push"] * 1e3 / K,
+                # of which the rbe_push_* calls (the rest: the bench's numpy batch assembly)
+                "push_abi_ms_per_round": stats["push_abi"] * 1e3 / K,
                 "step_ms_per_round": stats["step"] * 1e3 / K,
                 # host part of the step call: input upload staging + launches
                 "step_enqueue_ms_per_round": stats["enqueue"] * 1e3 / K,
