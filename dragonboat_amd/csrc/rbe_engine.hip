@@ -97,10 +97,11 @@ __device__ __forceinline__ bool upd_of(const Planes& P, u64 r, u32 round, rbe_up
   update_ids(*u, P.node_ids, P.ids_n, P.node_ids ? r / P.ids_n : 0);
   return (u->flags & RBE_UF_HAS_UPDATE) != 0;
 }
-__global__ __launch_bounds__(kBlock) void k_upd_count(Planes P, u64 first, u64 count, u32 round,
-                                                      u32* bsum);
-__global__ __launch_bounds__(kBlock) void k_upd_write(Planes P, u64 first, u64 count, u32 round,
-                                                      const u64* pre, u64* rep, rbe_update* ou);
+__global__ __launch_bounds__(kBlock) void k_upd_count(Planes P, u32 n, u64 first, u64 count,
+                                                      u32 round, u32* bsum);
+__global__ __launch_bounds__(kBlock) void k_upd_write(Planes P, u32 n, u64 first, u64 count,
+                                                      u32 round, const u64* pre, u64* rep,
+                                                      rbe_update* ou);
 
 // ---- batched outputs (rbe_collect_outputs): count → scan → write
 // Exclusive prefix of v over the 256 lanes of a block; *total = the sum.
@@ -153,12 +154,15 @@ __global__ __launch_bounds__(kBlock) void k_out_count(Planes P, Params C, u64 fi
     bsum[2 * blockIdx.x + 1] = tr;
   }
 }
-// one block of 1024: exclusive prefixes of the Q-tuples of block sums, totals
-// in pre[Q * nb ..].  Thread t owns a contiguous run of ceil(nb / 1024)
-// blocks: the run totals are scanned across the block once, then the run is
-// walked (a loop over 256-block slices with two barriers each took 77 us at
-// 11.7k blocks, more than the count and write passes it sits between).
+// Exclusive prefixes of the Q-tuples of block sums bsum[Q * nb] into
+// pre[Q * nb], totals in pre[Q * nb ..], in three launches (launch_scan): each
+// 1024-block tile scans itself (k_scan_up), one block scans the tile totals
+// (k_scan_top), the tiles add their offsets (k_scan_add).  pre holds
+// scan_words(Q, nb) words: the tile totals follow the grand totals.  (One
+// block walking all 11.7k block sums of a C4 engine took 54-77 us.)
 constexpr u32 kScanThreads = 1024;
+__host__ __device__ constexpr u64 scan_tiles(u64 nb) { return (nb + kScanThreads - 1) / kScanThreads; }
+__host__ __device__ constexpr u64 scan_words(u64 q, u64 nb) { return q * nb + q + q * scan_tiles(nb); }
 __device__ __forceinline__ u32 block_excl_scan_1k(u32 v, u32* total) {
   __shared__ u32 s_w[kScanThreads / 64];
   const u32 lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
@@ -181,31 +185,47 @@ __device__ __forceinline__ u32 block_excl_scan_1k(u32 v, u32* total) {
   return off + x - v;
 }
 template <int Q>
-__global__ __launch_bounds__(kScanThreads) void k_scan_q(const u32* bsum, u32 nb, u64* pre) {
-  const u32 per = (nb + kScanThreads - 1) / kScanThreads;
-  const u32 b0 = threadIdx.x * per < nb ? threadIdx.x * per : nb;
-  const u32 b1 = b0 + per < nb ? b0 + per : nb;
-  u32 loc[Q];
-#pragma unroll
-  for (int q = 0; q < Q; q++) loc[q] = 0;
-#pragma unroll 4
-  for (u32 b = b0; b < b1; b++)
-#pragma unroll
-    for (int q = 0; q < Q; q++) loc[q] += bsum[Q * b + q];
-  u64 run[Q];
+__global__ __launch_bounds__(kScanThreads) void k_scan_up(const u32* bsum, u32 nb, u64* pre) {
+  const u32 b = blockIdx.x * kScanThreads + threadIdx.x;
+  u64* tops = pre + (u64)Q * nb + Q;
 #pragma unroll
   for (int q = 0; q < Q; q++) {
+    const u32 v = b < nb ? bsum[(u64)Q * b + q] : 0u;
     u32 tot;
-    run[q] = block_excl_scan_1k(loc[q], &tot);
-    if (threadIdx.x == 0) pre[(u64)Q * nb + q] = tot;
+    const u32 ex = block_excl_scan_1k(v, &tot);
+    if (b < nb) pre[(u64)Q * b + q] = ex;
+    if (threadIdx.x == 0) tops[(u64)Q * blockIdx.x + q] = tot;
   }
-#pragma unroll 4
-  for (u32 b = b0; b < b1; b++)
+}
+template <int Q>
+__global__ __launch_bounds__(kScanThreads) void k_scan_top(u32 nb, u64* pre) {
+  const u32 nt = (u32)scan_tiles(nb), t = threadIdx.x;  // nt <= 1024 (launch_scan checks)
+  u64* tops = pre + (u64)Q * nb + Q;
 #pragma unroll
-    for (int q = 0; q < Q; q++) {
-      pre[Q * b + q] = run[q];
-      run[q] += bsum[Q * b + q];
-    }
+  for (int q = 0; q < Q; q++) {
+    const u32 v = t < nt ? (u32)tops[(u64)Q * t + q] : 0u;
+    u32 tot;
+    const u32 ex = block_excl_scan_1k(v, &tot);
+    if (t < nt) tops[(u64)Q * t + q] = ex;
+    if (t == 0) pre[(u64)Q * nb + q] = tot;
+  }
+}
+template <int Q>
+__global__ __launch_bounds__(kScanThreads) void k_scan_add(u32 nb, u64* pre) {
+  const u32 b = blockIdx.x * kScanThreads + threadIdx.x;
+  if (b >= nb || blockIdx.x == 0) return;
+  const u64* tops = pre + (u64)Q * nb + Q;
+#pragma unroll
+  for (int q = 0; q < Q; q++) pre[(u64)Q * b + q] += tops[(u64)Q * blockIdx.x + q];
+}
+template <int Q>
+static int launch_scan(hipStream_t st, const u32* bsum, u32 nb, u64* pre) {
+  const u32 nt = (u32)scan_tiles(nb);
+  if (nt > kScanThreads) return RBE_E_NOMEM;  // > 268M replicas in one call
+  hipLaunchKernelGGL(k_scan_up<Q>, dim3(nt), dim3(kScanThreads), 0, st, bsum, nb, pre);
+  hipLaunchKernelGGL(k_scan_top<Q>, dim3(1), dim3(kScanThreads), 0, st, nb, pre);
+  if (nt > 1) hipLaunchKernelGGL(k_scan_add<Q>, dim3(nt), dim3(kScanThreads), 0, st, nb, pre);
+  return hipGetLastError() == hipSuccess ? RBE_OK : RBE_E_HIP;
 }
 __global__ __launch_bounds__(kBlock) void k_out_write(Planes P, Params C, u64 first, u64 count,
                                                       u32 round, const u64* pre, u64* moff,
@@ -258,7 +278,10 @@ static_assert(offsetof(Upd, fault) == 48 && offsetof(Upd, flags) == 52 &&
                   offsetof(Upd, round) == 56 && offsetof(Upd, n_msgs) == 60 &&
                   offsetof(Upd, n_rtr) == 62,
               "Upd chunk 3 layout (upd_has_dev)");
-__device__ __forceinline__ bool upd_has_dev(const Planes& P, u64 r, u32 round) {
+__device__ __forceinline__ bool upd_has_dev(const Planes& P, u64 r, u32 n, u32 round) {
+  // a group asleep after the round slept through it or finished it lazily
+  // (group sleep, rbe_step.h group_transition): no replica of it has an Update
+  if (!(P.gwake[r / n] & GW_AWAKE)) return false;
   const Upd* u = P.upd + r;
   const uint4 c3 = reinterpret_cast<const uint4*>(u)[3];
   const u32 flags = c3.y & 0xFFFFu, rnd = c3.z;
@@ -283,7 +306,7 @@ __device__ __forceinline__ bool out_msg_wanted(const Params& C, u64 g, u32 d, bo
 }
 __device__ __forceinline__ void step_out_counts(const Planes& P, const Params& C, u64 r, u32 round,
                                                 bool remote, u32* f, u32* nm, u32* nr) {
-  *f = upd_has_dev(P, r, round) ? 1u : 0u;
+  *f = upd_has_dev(P, r, C.n, round) ? 1u : 0u;
   *nm = *nr = 0;
   if (!*f) return;
   const u32 par = (round - 1u) & 1u, N = C.n;
@@ -363,10 +386,10 @@ __global__ __launch_bounds__(kBlock) void k_cs_write(Planes P, Params C, u64 fir
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_upd_count(Planes P, u64 first, u64 count, u32 round,
-                                                      u32* bsum) {
+__global__ __launch_bounds__(kBlock) void k_upd_count(Planes P, u32 n, u64 first, u64 count,
+                                                      u32 round, u32* bsum) {
   const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
-  const u32 f = i < count && upd_has_dev(P, first + i, round) ? 1u : 0u;
+  const u32 f = i < count && upd_has_dev(P, first + i, n, round) ? 1u : 0u;
   u32 t;
   block_excl_scan(f, &t);
   if (threadIdx.x == 0) {
@@ -374,10 +397,11 @@ __global__ __launch_bounds__(kBlock) void k_upd_count(Planes P, u64 first, u64 c
     bsum[2 * blockIdx.x + 1] = 0;
   }
 }
-__global__ __launch_bounds__(kBlock) void k_upd_write(Planes P, u64 first, u64 count, u32 round,
-                                                      const u64* pre, u64* rep, rbe_update* ou) {
+__global__ __launch_bounds__(kBlock) void k_upd_write(Planes P, u32 n, u64 first, u64 count,
+                                                      u32 round, const u64* pre, u64* rep,
+                                                      rbe_update* ou) {
   const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
-  const u32 f = i < count && upd_has_dev(P, first + i, round) ? 1u : 0u;
+  const u32 f = i < count && upd_has_dev(P, first + i, n, round) ? 1u : 0u;
   u32 t;
   const u64 at = pre[2 * blockIdx.x] + block_excl_scan(f, &t);
   if (!f) return;
@@ -1914,7 +1938,7 @@ int rbe_collect_outputs(rbe_engine* e, uint64_t first, uint64_t count, rbe_outpu
   const u64 a8 = 256;
   auto al = [&](u64 x) { return (x + a8 - 1) & ~(a8 - 1); };
   // device scratch: block sums | block prefixes (+ totals) | offsets | records
-  const u64 o_pre = al(2ull * nb * sizeof(u32)), o_moff = o_pre + al((2ull * nb + 2) * sizeof(u64));
+  const u64 o_pre = al(2ull * nb * sizeof(u32)), o_moff = o_pre + al(scan_words(2, nb) * sizeof(u64));
   const u64 o_roff = o_moff + al((count + 1) * sizeof(u64));
   const u64 o_rec = o_roff + al((count + 1) * sizeof(u64));
   int rc = grow(&e->out_dev, &e->out_dev_bytes, o_rec, false);
@@ -1923,8 +1947,7 @@ int rbe_collect_outputs(rbe_engine* e, uint64_t first, uint64_t count, rbe_outpu
   u64* pre = (u64*)(e->out_dev + o_pre);
   hipLaunchKernelGGL(k_out_count, dim3(nb), dim3(kBlock), 0, e->stream, e->P, e->C, (u64)first,
                      (u64)count, e->round, bsum);
-  hipLaunchKernelGGL(k_scan_q<2>, dim3(1), dim3(kScanThreads), 0, e->stream, bsum, nb, pre);
-  HIP_OK(hipGetLastError());
+  if ((rc = launch_scan<2>(e->stream, bsum, nb, pre))) return rc;
   u64 tot[2];
   HIP_OK(hipMemcpyAsync(tot, pre + 2ull * nb, sizeof(tot), hipMemcpyDeviceToHost, e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
@@ -1973,15 +1996,13 @@ int rbe_collect_step(rbe_engine* e, uint64_t first, uint64_t count, uint32_t fla
   // device scratch: block sums (triples) | block prefixes (+ totals) | then the
   // records, laid out as the host copy: replicas | updates | msg offsets |
   // rtr offsets | messages | ReadyToReads
-  const u64 o_pre = al(3ull * nb * sizeof(u32)), o_rep = o_pre + al((3ull * nb + 3) * sizeof(u64));
+  const u64 o_pre = al(3ull * nb * sizeof(u32)), o_rep = o_pre + al(scan_words(3, nb) * sizeof(u64));
   int rc = grow(&e->cs_dev, &e->cs_dev_bytes, o_rep, false);
   if (rc) return rc;
   u64* pre = (u64*)(e->cs_dev + o_pre);
   hipLaunchKernelGGL(k_cs_count, dim3(nb), dim3(kBlock), 0, e->stream, e->P, e->C, (u64)first,
                      (u64)count, e->round, remote, (u32*)e->cs_dev);
-  hipLaunchKernelGGL(k_scan_q<3>, dim3(1), dim3(kScanThreads), 0, e->stream, (const u32*)e->cs_dev, nb,
-                     pre);
-  HIP_OK(hipGetLastError());
+  if ((rc = launch_scan<3>(e->stream, (const u32*)e->cs_dev, nb, pre))) return rc;
   u64 tot[3];
   HIP_OK(hipMemcpyAsync(tot, pre + 3ull * nb, sizeof(tot), hipMemcpyDeviceToHost, e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
@@ -2032,15 +2053,13 @@ int rbe_collect_updates(rbe_engine* e, uint64_t first, uint64_t count, rbe_updat
   const u32 nb = grid_for(count);
   auto al = [](u64 x) { return (x + 255) & ~255ull; };
   // device scratch: block sums (pairs) | block prefixes (+ totals) | replicas | records
-  const u64 o_pre = al(2ull * nb * sizeof(u32)), o_rep = o_pre + al((2ull * nb + 2) * sizeof(u64));
+  const u64 o_pre = al(2ull * nb * sizeof(u32)), o_rep = o_pre + al(scan_words(2, nb) * sizeof(u64));
   int rc = grow(&e->upd_dev, &e->upd_dev_bytes, o_rep, false);
   if (rc) return rc;
   u64* pre = (u64*)(e->upd_dev + o_pre);
-  hipLaunchKernelGGL(k_upd_count, dim3(nb), dim3(kBlock), 0, e->stream, e->P, (u64)first,
+  hipLaunchKernelGGL(k_upd_count, dim3(nb), dim3(kBlock), 0, e->stream, e->P, e->C.n, (u64)first,
                      (u64)count, e->round, (u32*)e->upd_dev);
-  hipLaunchKernelGGL(k_scan_q<2>, dim3(1), dim3(kScanThreads), 0, e->stream, (const u32*)e->upd_dev, nb,
-                     pre);
-  HIP_OK(hipGetLastError());
+  if ((rc = launch_scan<2>(e->stream, (const u32*)e->upd_dev, nb, pre))) return rc;
   u64 tot[2];
   HIP_OK(hipMemcpyAsync(tot, pre + 2ull * nb, sizeof(tot), hipMemcpyDeviceToHost, e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
@@ -2053,7 +2072,7 @@ int rbe_collect_updates(rbe_engine* e, uint64_t first, uint64_t count, rbe_updat
     HIP_OK(hipMemcpy(pre, keep.data(), keep.size() * sizeof(u64), hipMemcpyHostToDevice));
   }
   u8* d = e->upd_dev;
-  hipLaunchKernelGGL(k_upd_write, dim3(nb), dim3(kBlock), 0, e->stream, e->P, (u64)first,
+  hipLaunchKernelGGL(k_upd_write, dim3(nb), dim3(kBlock), 0, e->stream, e->P, e->C.n, (u64)first,
                      (u64)count, e->round, (const u64*)(d + o_pre), (u64*)(d + o_rep),
                      (rbe_update*)(d + o_rec));
   HIP_OK(hipGetLastError());

@@ -180,3 +180,26 @@ def test_gpu_collect_step_matches(gpu_available, name, kw, extra):
     if name == "C4":
         assert seen[2], seen
     eng.close()
+
+
+def test_gpu_collect_untraced_group_sleep(gpu_available):
+    """Untraced C4 (lazy quiesced ticks, group sleep): the collect passes skip
+    the groups asleep after the round, and still return exactly the replicas
+    whose rbe_get_updates record has an Update, round after round."""
+    from dragonboat_amd import engine as E
+    eng = E.Engine(device=0, trace=False, **dict(C4, n_groups=3000))
+    seen = 0
+    for rnd in range(300):
+        eng.step()
+        if rnd < 25:
+            continue
+        full = np.frombuffer(bytes(eng.updates()), E.UPDATE_DTYPE)
+        want = np.nonzero(full["flags"] & E.UF_HAS_UPDATE)[0]
+        rep, ups = eng.collect_updates()
+        assert np.array_equal(rep, want.astype(np.uint64)), rnd
+        assert ups.tobytes() == full[want].tobytes()
+        rep2, ups2, _, _, _, _ = eng.collect_step()
+        assert np.array_equal(rep2, rep) and ups2.tobytes() == ups.tobytes()
+        seen += len(rep)
+    assert seen > 1000
+    eng.close()
