@@ -6,8 +6,10 @@ cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 S=$(date +%s)
-for i in 1 2; do
-  for lib in dragonboat_amd/libdragonboat_amd.so build/full64.so; do
+timeout -k 10 300 python -u -m pytest tests/test_gpu_outputs.py -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/gpu_outputs.log 2>&1 || { tail -30 gpurun_out/gpu_outputs.log; exit 1; }
+tail -1 gpurun_out/gpu_outputs.log
+for i in 1; do
+  for lib in dragonboat_amd/libdragonboat_amd.so; do
     for w in c4 c3; do
       RBE_LIB=$PWD/$lib timeout -k 10 200 python bench.py --workload $w --no-cpu-baseline --also "" --steps 100 --warmup 10 > gpurun_out/ab.json 2>gpurun_out/ab.err || { tail -20 gpurun_out/ab.err; exit 1; }
       python3 scripts/summarize_bench.py gpurun_out/ab.json "$(basename $lib) $w" | head -5
