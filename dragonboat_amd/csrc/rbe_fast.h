@@ -108,6 +108,19 @@ RBE_HD void rbe_wait_all_loads() {
 #ifndef RBE_LDS_INBOX
 #define RBE_LDS_INBOX 1
 #endif
+// waves per SIMD of the fast kernels (launch bounds): groups of 3 at two;
+// wider groups (4..6) keep up to (N-1) x 5 inbound headers and N remote slots
+// per leader lane, which at two waves spill hundreds of bytes per lane to
+// scratch, so RBE_FAST_WAVES_WIDE may run them at one wave with the leader's
+// inbox in LDS (a whole CU's LDS for one block)
+#ifndef RBE_FAST_WAVES
+#define RBE_FAST_WAVES 2
+#endif
+#ifndef RBE_FAST_WAVES_WIDE
+#define RBE_FAST_WAVES_WIDE RBE_FAST_WAVES
+#endif
+template <int N>
+constexpr int kFastWaves = N <= 3 ? RBE_FAST_WAVES : RBE_FAST_WAVES_WIDE;
 template <int N>
 struct FastCaps {
   static constexpr u32 MAXM = N <= 3 ? RBE_LEAD_MAXM3 : 5;  // leader: per follower
@@ -753,7 +766,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   // registers fewer through the compute phase, so the compiler need not spill,
   // and an LDS read waits on lgkmcnt, never behind the lane's stores (vmcnt).
 #if defined(__HIP_DEVICE_COMPILE__) && RBE_LDS_INBOX
-  constexpr bool kLdsIn = N == 3;
+  constexpr bool kLdsIn = N == 3 || kFastWaves<N> == 1;
   constexpr u32 kLdsSlots = kLdsIn ? (N - 1) * Cap::MAXM : 1;
   constexpr u32 kLdsLanes = kLdsIn ? 256 : 1;
   __shared__ u32 s_in_w[kLdsSlots][kLdsLanes];

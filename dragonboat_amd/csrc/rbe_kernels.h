@@ -33,9 +33,7 @@ namespace rbe {
 static constexpr int kBlock = 256;
 // minimum waves per SIMD requested for the fast-step kernels (caps their VGPRs:
 // 2 -> 256, 3 -> 168, 4 -> 128; beyond the cap the compiler spills to scratch)
-#ifndef RBE_FAST_WAVES
-#define RBE_FAST_WAVES 2
-#endif
+
 #ifndef RBE_FAST_LDS_CTR
 #define RBE_FAST_LDS_CTR 1  // k_fast_both's event counters in LDS (LdsCounters)
 #endif
@@ -840,7 +838,7 @@ __device__ __forceinline__ void msg_stage_flush(Msg* out, u32 staged) {
 #define RBE_XCD_FAST 0  // measured slower (C4 k_fast_both 116.7-117.0 vs 110.5-110.9 us)
 #endif
 template <int N, bool TRACE>
-__global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_fast_both(Planes P, Params C,
+__global__ __launch_bounds__(kBlock, kFastWaves<N>) void k_fast_both(Planes P, Params C,
                                                                      RoundArg ra, Lists L) {
   __shared__ StageRow<N> s_rows[kBlock];
   const Clk ck = clk_of(ra);
