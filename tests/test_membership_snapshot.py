@@ -82,7 +82,7 @@ def test_membership_snapshot_parity(name, mode):
     assert diff > 0, "no replica restored a snapshot with a membership other than its own"
 
 
-@pytest.mark.parametrize("name", ["C2", "MIXED"])
+@pytest.mark.parametrize("name", ["C2", "C3_HOT", "MIXED"])
 def test_membership_snapshot_untraced(name):
     """The bench paths (untraced: lazy quiesced ticks, group sleep)."""
     kw, extra, rounds = CASES[name]
