@@ -1508,7 +1508,7 @@ extern "C" int rbe_debug_full_prof(rbe_engine* e, uint64_t* out, uint64_t cap, u
   HIP_OK(hipSetDevice(e->device));
   if (!e->P.prof) {
     HIP_OK(hipMalloc((void**)&e->P.prof, (4 + 4 * kFullProfCap) * sizeof(u64)));
-    HIP_OK(hipMemset(e->P.prof, 0, 4 * sizeof(u64)));
+    HIP_OK(hipMemset(e->P.prof, 0, 32 * sizeof(u64)));  // counter | phase sums (rbe_debug_phases)
     if (e->graph) {
       HIP_IGNORE(hipGraphExecDestroy(e->graph));
       e->graph = nullptr;
@@ -1526,17 +1526,19 @@ extern "C" int rbe_debug_full_prof(rbe_engine* e, uint64_t* out, uint64_t cap, u
   return RBE_OK;
 }
 
-#ifdef RBE_PHASE_TIMING
-// diagnostic build: read and clear the per-phase stamp sums (rbe_fast.h)
-int rbe_debug_phases(uint64_t* out24) {
-  unsigned long long h[24];
-  HIP_OK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)));
-  for (int i = 0; i < 24; i++) out24[i] = h[i];
-  memset(h, 0, sizeof(h));
-  HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), h, sizeof(h)));
+// Diagnostic: the per-phase stamp sums of an RBE_PHASE_TIMING build (24
+// words: leader, follower, k_triage x 8 phases; rbe_fast.h) since the last
+// call, and clear.  The first call allocates the buffer (Planes::prof).
+extern "C" int rbe_debug_phases(rbe_engine* e, uint64_t* out24) {
+  uint64_t n = 0;
+  if (!e || !out24) return RBE_E_INVALID;
+  if (!e->P.prof) return rbe_debug_full_prof(e, nullptr, 0, &n);
+  HIP_OK(hipSetDevice(e->device));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  HIP_OK(hipMemcpy(out24, e->P.prof + 8, 24 * sizeof(u64), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemset(e->P.prof + 8, 0, 24 * sizeof(u64)));
   return RBE_OK;
 }
-#endif
 
 int rbe_xchg_record_bytes(uint64_t* out3) {
   if (!out3) return RBE_E_INVALID;

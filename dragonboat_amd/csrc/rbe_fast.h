@@ -35,11 +35,10 @@
 
 namespace rbe {
 
-// Diagnostic build only (-DRBE_PHASE_TIMING, scripts/phase_timing.sh): per-wave
-// s_memtime stamps between the phases of the fast steps, summed per phase.
-#if defined(RBE_PHASE_TIMING) && (defined(__HIPCC__) || defined(__HIP__))
-__device__ unsigned long long g_phase[3][8];  // leader, follower, k_triage
-#endif
+// Diagnostic build only (-DRBE_PHASE_TIMING, scripts/phase_timing.py): per-wave
+// s_memtime stamps between the phases of the fast steps and k_triage, summed
+// per phase into Planes::prof[8 + 8 * role + phase] (role: leader, follower,
+// k_triage; rbe_debug_phases).
 #if defined(RBE_PHASE_TIMING) && defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ unsigned long long rbe_stamp() {
   unsigned long long t;
@@ -60,7 +59,8 @@ __device__ __forceinline__ unsigned long long rbe_rstamp() {
 #define RBE_PHASE_ADD(role, i, a, b)                                                   \
   do {                                                                                 \
     if ((threadIdx.x & 63) == (u32)(__ffsll((unsigned long long)__ballot(1)) - 1))     \
-      atomicAdd(&g_phase[role][i], (unsigned long long)((b) - (a)));                   \
+      if (P.prof) atomicAdd((unsigned long long*)&P.prof[8 + 8 * (role) + (i)],         \
+                            (unsigned long long)((b) - (a)));                           \
   } while (0)
 #else
 #define RBE_STAMP(var)

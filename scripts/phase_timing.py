@@ -1,9 +1,8 @@
 """Diagnostic: per-phase wave time of the fast steps (s_memtime stamps) from
 the RBE_PHASE_TIMING build (build/libdragonboat_amd_phase.so).
 
-    hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DRBE_PHASE_TIMING \
-        -DRBE_SINGLE_TU -o build/libdragonboat_amd_phase.so dragonboat_amd/csrc/rbe_engine.hip
-    RBE_MODE=split python scripts/phase_timing.py c4
+    scripts/build_variant.sh build/libdragonboat_amd_phase.so -DRBE_PHASE_TIMING
+    python scripts/phase_timing.py c4
 """
 import ctypes as C
 import os
@@ -16,7 +15,7 @@ from dragonboat_amd import engine as E  # noqa: E402
 
 lib = E.load_library(os.path.join(ROOT, "build", "libdragonboat_amd_phase.so"))
 E._lib = lib
-lib.rbe_debug_phases.argtypes = [C.POINTER(C.c_uint64)]
+lib.rbe_debug_phases.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
 w = sys.argv[1] if len(sys.argv) > 1 else "c4"
 kw, settle, _ = bench.WORKLOADS[w]
 kw = dict(kw)
@@ -26,10 +25,10 @@ eng = E.Engine(**kw)
 eng.run(settle)
 eng.sync()
 o = (C.c_uint64 * 24)()
-lib.rbe_debug_phases(o)
+lib.rbe_debug_phases(eng.h, o)
 rounds = 20
 ms = eng.profile_rounds(rounds)
-lib.rbe_debug_phases(o)
+lib.rbe_debug_phases(eng.h, o)
 names = {0: ["gather1", "gather2", "inbox+read", "tick+propose", "scatter+finish"],
          1: ["gather1", "gather2", "inbox", "-", "tick+finish"],
          2: ["groups", "loads", "classify+reserve", "lds-fill", "copy-out", "counters"]}
