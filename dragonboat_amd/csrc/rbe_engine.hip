@@ -49,6 +49,8 @@ RBE_EXTERN_ROUND(5, true)
 RBE_EXTERN_ROUND(5, false)
 RBE_EXTERN_ROUND(6, true)
 RBE_EXTERN_ROUND(6, false)
+RBE_EXTERN_ROUND(7, true)
+RBE_EXTERN_ROUND(7, false)
 #undef RBE_EXTERN_ROUND
 }  // namespace rbe
 #endif
@@ -132,9 +134,10 @@ __device__ __forceinline__ void out_counts(const Planes& P, const Params& C, u64
                                            u32* nm, u32* nr) {
   const u32 par = (round - 1u) & 1u;
   const CntRow row = P.cnt[par][r];
+  const u32 k = (u32)(r % C.n);
   u32 m = 0;
   for (u32 d = 0; d < C.n; d++) {
-    const u32 pc = row_word(row, d, round);
+    const u32 pc = row_word(row, d, k, round);
     m += (pc & 0x7Fu) + ((pc >> 7) & 0x7Fu);
   }
   *nm = m;
@@ -251,7 +254,7 @@ __global__ __launch_bounds__(kBlock) void k_out_write(Planes P, Params C, u64 fi
   const CntRow row = P.cnt[par][r];
   u64 at = bm;
   for (u32 d = 0; d < N; d++) {
-    const u32 pc = row_word(row, d, round), na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
+    const u32 pc = row_word(row, d, k, round), na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
     const Msg* lst = &P.msgs[par][((g * N + k) * N + d) * (u64)C.maxm];
     for (u32 j = 0; j < na + nb; j++, at++) {
       const Msg m = j < na ? lst[j] : lst[C.maxm - 1u - (j - na)];
@@ -312,9 +315,10 @@ __device__ __forceinline__ void step_out_counts(const Planes& P, const Params& C
   const u32 par = (round - 1u) & 1u, N = C.n;
   const CntRow row = P.cnt[par][r];
   const u64 g = r / N;
+  const u32 k = (u32)(r % N);
   u32 m = 0;
   for (u32 d = 0; d < N; d++) {
-    const u32 pc = row_word(row, d, round);
+    const u32 pc = row_word(row, d, k, round);
     if (out_msg_wanted(C, g, d, remote)) m += (pc & 0x7Fu) + ((pc >> 7) & 0x7Fu);
   }
   *nm = m;
@@ -367,7 +371,7 @@ __global__ __launch_bounds__(kBlock) void k_cs_write(Planes P, Params C, u64 fir
   u64 w = bm;
   for (u32 d = 0; d < N; d++) {
     if (!out_msg_wanted(C, g, d, remote)) continue;
-    const u32 pc = row_word(row, d, round), na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
+    const u32 pc = row_word(row, d, k, round), na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
     const Msg* lst = &P.msgs[par][((g * N + k) * N + d) * (u64)C.maxm];
     for (u32 j = 0; j < na + nb; j++, w++) {
       const Msg m = j < na ? lst[j] : lst[C.maxm - 1u - (j - na)];
@@ -1808,7 +1812,7 @@ int rbe_get_views(rbe_engine* e, uint64_t first, uint64_t count, rbe_replica_vie
     v.votes_granted = h.votes_granted;
     v.events = (e->round > 0 && upd[i].round == e->round - 1) ? upd[i].events : 0u;
     v.removed = c.members & MB_REMOVED;
-    if (c.members & MB_ROLES) {  // Planes::roles is only current while MB_ROLES is set
+    if (c.mflags & MB_ROLES) {  // Planes::roles is only current while MB_ROLES is set
       v.observers = roles[i] & 0xFFu;
       v.witnesses = roles[i] >> 8;
     }
@@ -1904,7 +1908,7 @@ int rbe_get_messages(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t
   HIP_OK(hipStreamSynchronize(e->stream));
   u32 n = 0;
   for (u32 d = 0; d < N; d++) {
-    const u32 pc = row_word(row, d, e->round), na = pc & 0x7F, nb = (pc >> 7) & 0x7F;
+    const u32 pc = row_word(row, d, k, e->round), na = pc & 0x7F, nb = (pc >> 7) & 0x7F;
     for (u32 i = 0; i < na + nb; i++) {
       const Msg& m = i < na ? lst[d * e->C.maxm + i] : lst[d * e->C.maxm + e->C.maxm - 1 - (i - na)];
       if (n < cap && out) msg_out(m, cid_of(e->C, g), e->hin.id_table(), N, g, out[n]);

@@ -676,7 +676,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   if (h.flags & HF_SNAP_WORK) return false;  // compaction / SnapshotStatus: full table
   // membership: a changed voter set, a ConfigChange in the log or to apply,
   // or one to propose this round (full handler table)
-  if (C.membership && ((c.members | c.cc_apply) != 0 ||
+  if (C.membership && ((c.members | c.cc_apply | c.mflags) != 0 ||
                        (C.cc_period && cc_selected(C, cid, round))))
     return false;
   // ext_commit: an Update whose unsaved entries left the in-memory log (Lane::run)
@@ -1416,7 +1416,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   u32 cdirty = 0;  // Core chunks an append or a new leader wrote (fast_finish)
   if (h.role != R_Follower) return false;
   if (h.flags & HF_SNAP_WORK) return false;  // compaction / SnapshotStatus: full table
-  if (C.membership && (c.members | c.cc_apply) != 0) return false;  // (lead_fast)
+  if (C.membership && (c.members | c.cc_apply | c.mflags) != 0) return false;  // (lead_fast)
   if (C.ext_commit && c.saved_to + 1 < P.imark[r]) return false;  // (lead_fast)
   if (h.flags & (HF_APPLY_PENDING | HF_IS_LTT)) return false;
   if (c.ltt != 0) return false;

@@ -38,6 +38,7 @@ inline auto with_n(u32 n, F&& f) -> decltype(f(std::integral_constant<int, 1>())
     case 4: return f(std::integral_constant<int, 4>());
     case 5: return f(std::integral_constant<int, 5>());
     case 6: return f(std::integral_constant<int, 6>());
+    case 7: return f(std::integral_constant<int, 7>());
     default: return f(std::integral_constant<int, 1>());
   }
 }
@@ -348,7 +349,7 @@ RBE_HD u64 heap_low_group(const Planes& P, const Params& C, u64 g, u32 round) {
     if (round == 0) continue;
     const CntRow row = P.cnt[par][r];
     for (u32 d = 0; d < N; d++) {
-      const u32 nb = (row_word(row, d, round) >> 7) & 0x7Fu;
+      const u32 nb = (row_word(row, d, k, round) >> 7) & 0x7Fu;
       const Msg* lst = &P.msgs[par][((g * N + k) * N + d) * (u64)C.maxm];
       for (u32 i = 0; i < nb; i++) {
         const Msg m = lst[C.maxm - 1u - i];

@@ -216,7 +216,8 @@ RBE_HD u32 ingest_sender(const Planes& P, const Params& C, u32 par, u32 round, c
     CntRow row;
     row.stamp = round;
     for (int q = 0; q < 6; q++) row.w[q] = 0;
-    for (int d = 0; d < N; d++) row.w[d] = (u16)words[d];
+    for (int d = 0; d < N; d++)
+      if ((u32)d != (u32)(sr % N)) row.w[cnt_widx((u32)d, (u32)(sr % N))] = (u16)words[d];
     P.cnt[par][sr] = row;
     P.gwake[sr / N] = GW_AWAKE;  // a message wakes the destination's group
   }

@@ -291,19 +291,25 @@ RBE_HD u32 idle_role(u8 ib) { return (ib >> IB_ROLE_SHIFT) & 7u; }
 // The count word of list (sender slot s → destination slot d) that a step of
 // round `round` reads: the sender's outbox header of the previous round's
 // parity, valid only if that round wrote it (CntRow::stamp == round).
-RBE_HD u32 row_word(const CntRow& row, u32 d, u32 round) {
-  return row.stamp == round ? (u32)row.w[d] : 0u;
+// the index in CntRow::w of destination slot d's word in sender slot k's row
+RBE_HD u32 cnt_widx(u32 d, u32 k) { return d < 6u ? d : k; }
+// the count word of destination slot d in sender slot k's row, read in `round`
+// (none to itself: in a group of 7 that index holds slot 6's word)
+RBE_HD u32 row_word(const CntRow& row, u32 d, u32 k, u32 round) {
+  return row.stamp == round && d != k ? (u32)row.w[cnt_widx(d, k)] : 0u;
 }
 template <int N>
 RBE_HD u32 in_word(const Planes& P, u64 g, u32 s, u32 d, u32 round) {
   if (round == 0) return 0u;
-  return row_word(P.cnt[(round & 1u) ^ 1u][g * N + s], d, round);
+  return row_word(P.cnt[(round & 1u) ^ 1u][g * N + s], d, s, round);
 }
 // This sender's outbox header of round `round` (one 16-B store).
 RBE_HD void put_row(const Planes& P, u64 r, u32 round, u32 n, const u32* w) {
   CntRow row;
   row.stamp = round + 1u;
-  for (u32 d = 0; d < 6; d++) row.w[d] = (u16)(d < n ? w[d] : 0u);
+  const u32 k = (u32)(r % n);
+  for (u32 d = 0; d < 6; d++) row.w[d] = (u16)(d < n && d != k ? w[d] : 0u);
+  if (n > 6 && k < 6) row.w[k] = (u16)w[6];  // slot 6's word in the sender's own place
   P.cnt[round & 1u][r] = row;
 }
 
@@ -550,6 +556,7 @@ struct Lane {
   u64 lead_start;  // leader: index of its no-op (Core::lead_start)
   u8 vote, leader, ltt, rq_head, rq_count;
   u8 members, cc_apply;  // Core::members / cc_apply (membership)
+  u8 mfl;                // Core::mflags (MB_ROLES | MB_CC_IN_LOG)
   u8 obs, wit;           // raft.observers / raft.witnesses (Planes::roles; membership)
   u8 roles0;             // MB_ROLES at load: Planes::roles holds something to rewrite
   u64 c_match[N], c_next[N];  // LEAD: remote slots held in registers
@@ -1311,7 +1318,7 @@ struct Lane {
       return;
     }
     if (((addr >> k) & 1u) && role == R_Observer) become_follower(term, leader);
-    members = (u8)((members & MB_CC_IN_LOG) | (~addr & MB_REMOVED & full));
+    members = (u8)(~addr & MB_REMOVED & full);
     obs = (u8)((ms >> 8) & full);
     wit = (u8)((ms >> 16) & full);
     for (u32 s = 0; s < N; s++) {
@@ -1324,7 +1331,7 @@ struct Lane {
   }
   // a log entry that is a ConfigChange: MB_CC_IN_LOG until it is applied
   RBE_HD void note_cc(u32 type) {
-    if (ent_type(type) == E_ConfigChange) members |= MB_CC_IN_LOG;
+    if (ent_type(type) == E_ConfigChange) mfl |= MB_CC_IN_LOG;
   }
 
   // ------------------------------------------------------------- commit (kernel 1)
@@ -2260,12 +2267,12 @@ struct Lane {
         ms_apply(sm_ms, t, nid, N);
       }
     }
-    if (members & MB_CC_IN_LOG) {
+    if (mfl & MB_CC_IN_LOG) {
       bool any = false;
       for (u64 i = processed + 1; i <= last && !any; i++)
         if (last - i < C.ring && ent_type(P.pay_ring[ring_slot(i)].type) == E_ConfigChange)
           any = true;
-      if (!any) members &= (u8)~MB_CC_IN_LOG;
+      if (!any) mfl &= (u8)~MB_CC_IN_LOG;
     }
   }
 
@@ -2356,7 +2363,8 @@ struct Lane {
     rq_count = c.rq_count;
     members = c.members;
     cc_apply = c.cc_apply;
-    roles0 = (u8)(members & MB_ROLES);
+    mfl = c.mflags;
+    roles0 = (u8)(mfl & MB_ROLES);
     obs = wit = 0;
     if (roles0) {
       const u16 x = P.roles[r];
@@ -2392,11 +2400,11 @@ struct Lane {
     c.rq_head = rq_head;
     c.rq_count = rq_count;
     // MB_ROLES: the replica has observers or witnesses (Planes::roles)
-    members = (u8)((members & ~MB_ROLES) | ((obs | wit) ? MB_ROLES : 0u));
+    mfl = (u8)((mfl & ~MB_ROLES) | ((obs | wit) ? MB_ROLES : 0u));
     if (C.membership && (roles0 || (obs | wit))) P.roles[r] = (u16)(obs | ((u16)wit << 8));
     c.members = members;
     c.cc_apply = cc_apply;
-    c.pad = 0;
+    c.mflags = mfl;
     c.t_last = t_last;
     c.lead_start = lead_start;
     P.core[r] = c;
@@ -3019,12 +3027,15 @@ RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   c.leader = 0;
   c.ltt = 0;
   c.rq_head = c.rq_count = 0;
-  c.members = c.cc_apply = c.pad = 0;
+  c.members = c.cc_apply = c.mflags = 0;
   c.t_last = boot ? 1 : 0;  // bootstrap entries are at term 1
   c.lead_start = 0;
   // the bootstrap ConfigChanges, applied in round 0; the slots outside the
   // replica's initial membership
-  if (C.membership) c.members = (u8)((boot ? MB_CC_IN_LOG : 0u) | boot_removed(C, k));
+  if (C.membership) {
+    c.members = (u8)boot_removed(C, k);
+    c.mflags = boot ? MB_CC_IN_LOG : 0u;
+  }
   P.core[r] = c;
   if (imark_on(C)) P.imark[r] = 1;  // inMemory.init(0), then bootstrap appends 1..V
   if (C.rl_max) {  // newRateLimiter; bootstrap's append is a merge that adds its entries
@@ -3143,7 +3154,7 @@ RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, 
   c.leader = 0;
   c.ltt = 0;
   c.rq_head = c.rq_count = 0;
-  c.members = c.cc_apply = c.pad = 0;
+  c.members = c.cc_apply = c.mflags = 0;
   c.t_last = n ? t[n - 1] : (last == marker ? marker_term : 0);
   c.lead_start = 0;
   // the restarted raft reads the group's members from the LogDB (NodeState:
@@ -3151,10 +3162,11 @@ RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, 
   // as oracle/harness.cpp harness_restart)
   if (C.membership) {
     const u16 roles = (u16)(((removed >> 8) & 0xFFu) | (((removed >> 16) & 0xFFu) << 8));
-    c.members = (u8)((removed & MB_REMOVED) | (roles ? MB_ROLES : 0u));
+    c.members = (u8)(removed & MB_REMOVED);
+    c.mflags = roles ? MB_ROLES : 0u;
     P.roles[r] = roles;
     for (u32 i = 0; i < n; i++)
-      if (ent_type(b[i].type) == E_ConfigChange) c.members |= MB_CC_IN_LOG;
+      if (ent_type(b[i].type) == E_ConfigChange) c.mflags |= MB_CC_IN_LOG;
   }
   P.core[r] = c;
   if (imark_on(C)) P.imark[r] = last + 1;  // inMemory.init(lastIndex), inmemory.go:46-57
@@ -3179,7 +3191,7 @@ RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, 
   // messages in flight: none from this replica, none to it
   P.cnt[ppar][r].stamp = 0;
   for (u32 s = 0; s < N; s++)
-    if (s != k) P.cnt[ppar][g * N + s].w[k] = 0;
+    if (s != k) P.cnt[ppar][g * N + s].w[cnt_widx(k, s)] = 0;
 }
 
 // ------------------------------------------------------------------ triage
@@ -3284,7 +3296,7 @@ RBE_HD void inbound_load(const Planes& P, u32 g, u32 k, u32 round, u16 (&w)[N]) 
   const CntRow* rows = &P.cnt[(round & 1u) ^ 1u][(u64)g * N];
   for (u32 s = 0; s < N; s++) {
     const CntRow row = rows[s];
-    w[s] = (u16)row_word(row, k, round);
+    w[s] = (u16)row_word(row, k, s, round);
   }
 }
 template <int N>

@@ -16,7 +16,7 @@ typedef uint16_t u16;
 typedef uint8_t u8;
 
 // the largest group size (voting slots per group) the engine is built for
-static constexpr u32 kMaxN = 6;
+static constexpr u32 kMaxN = 7;
 
 // raftpb MessageType, raft.pb.go:23-51
 enum : u32 {
@@ -89,11 +89,11 @@ enum : u8 {
                         // step (snapshot_entries > 0): triage sends it to k_full
 };
 
-// Core::members / Core::cc_apply bits
+// Core::members / Core::mflags / Core::cc_apply bits
 enum : u8 {
-  MB_REMOVED = 0x3F,   // slots that are not in raft.remotes (bit s = slot s, kMaxN = 6)
-  MB_ROLES = 0x40,     // some slot is an observer or a witness (Planes::roles)
-  MB_CC_IN_LOG = 0x80,
+  MB_REMOVED = 0x7F,   // members: slots that are not in raft.remotes (bit s = slot s, kMaxN = 7)
+  MB_ROLES = 0x01,     // mflags: some slot is an observer or a witness (Planes::roles)
+  MB_CC_IN_LOG = 0x02, // mflags: a ConfigChange entry may sit in (processed, last_index]
   CCA_VALID = 0x80, CCA_REJECT = 0x40,  // cc_apply: node id bits 0-2, ConfigChangeType bits 3-5
 };
 // pb.ConfigChangeType (raft.pb.go)
@@ -111,14 +111,15 @@ struct alignas(16) Core {
   u8 ltt;          // leaderTransferTarget
   u8 rq_head;      // readIndex queue ring head
   u8 rq_count;
-  // membership (cfg.membership; all zero otherwise): bits 0-4 the slots that
-  // are not voting members of this replica's raft.remotes (the group starts
-  // with every slot a voter), MB_CC_IN_LOG a ConfigChange entry may sit in
-  // (processed, last_index]; cc_apply a ConfigChange for the next step
-  // (CCA_* bits: the state machine applied one, or the host sent it)
+  // membership (cfg.membership; all zero otherwise): members has a bit per
+  // slot that is not a voting member of this replica's raft.remotes (the
+  // group starts with every slot a voter); mflags MB_CC_IN_LOG (a ConfigChange
+  // entry may sit in (processed, last_index]) and MB_ROLES; cc_apply a
+  // ConfigChange for the next step (CCA_* bits: the state machine applied
+  // one, or the host sent it)
   u8 members;
   u8 cc_apply;
-  u8 pad;
+  u8 mflags;       // MB_ROLES | MB_CC_IN_LOG (membership)
   u64 t_last;      // term of entry last_index (log-tail cache)
   u64 lead_start;  // leader: index of its no-op, the first entry of its term (raft.go:985);
                    // entries [lead_start, last_index] have term == term, earlier ones less
@@ -188,11 +189,14 @@ struct alignas(16) Msg {
 // rest, back of the list) << 7 | Quiesce notice << 15 — stamped with the round
 // that reads it (the writer's round + 1).  A sender that makes no step in a
 // round (a lazily skipped quiesced tick) writes no row, and the stale row of
-// that parity reads as empty, so nothing ever has to be cleared.
+// that parity reads as empty, so nothing ever has to be cleared.  Six words
+// serve groups of up to 7: a sender has no list to itself, so the word of
+// destination slot 6 takes the sender's own index (cnt_widx).
 struct alignas(16) CntRow {
   u32 stamp;
   u16 w[6];
 };
+
 
 // arena entry: 32 B (index implicit: log_index + 1 + i for Replicate)
 struct alignas(16) Ent {

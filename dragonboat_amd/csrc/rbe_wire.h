@@ -192,7 +192,7 @@ RBE_HD u32 wire_cell(const Planes& P, const Params& C, const u8* heap, u64 heap_
   const u32 par = (round - 1u) & 1u;
   const u64 r = g * N + k;
   const u64 cid = cid_of(C, g);
-  const u32 pc = row_word(P.cnt[par][r], d, round);
+  const u32 pc = row_word(P.cnt[par][r], d, k, round);
   const u32 na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
   u32 bytes = 0, nm = 0, ni = 0, bad = 0;
   // Message.To / From (and a RequestVote's / LeaderTransfer's Hint) as node ids

@@ -28,8 +28,8 @@ struct WireArgs {
   u64 heap_head;         // payload heap head at the last upload (lapped-record check)
   int32_t dst_rank;      // replica mode: receivers of this rank only (-1: every remote rank)
   u32 pad;
-  u32 alen[6];
-  u8 addr[6][48];        // source address of each slot
+  u32 alen[kMaxN];
+  u8 addr[kMaxN][48];        // source address of each slot
 };
 
 struct WireFrame {  // mirrors rbe_wire_frame (include/rbe.h)

@@ -99,7 +99,7 @@ RBE_HD void xchg_sender(const Planes& P, const Params& C, u64 r, u32 par, u32 ro
     if (peer == C.rep_rank) continue;
     const u64 gg = group_global(C, g);  // records carry global indexes
     const u64 key = (gg * N + s) * N + d;
-    const u32 word = row_word(row, d, round);
+    const u32 word = row_word(row, d, s, round);
     if (word == 0) continue;
     auto put = [&](u32 t) -> u8* {
       const u32 i = cnt[peer * XS_NUM + t]++;
@@ -228,7 +228,7 @@ int outbox_messages(const Params& C, u64 g, u32 k, const CntRow& row, u32 round,
     n++;
   };
   for (u32 d = 0; d < N; d++) {
-    const u32 pc = row_word(row, d, round), na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
+    const u32 pc = row_word(row, d, k, round), na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
     if (pc & 0x8000u) {
       Msg q = mk_msg(M_Quiesce, d + 1);
       emit(q, M_Quiesce, d + 1);
@@ -390,7 +390,7 @@ int messages_to_records(const Params& C, HostHeap& heap, u32 round, u64 n, const
         it = hdr.emplace(sr, oc.size()).first;
         oc.push_back(c);
       }
-      oc[it->second].row.w[d] = (u16)words[key];
+      oc[it->second].row.w[cnt_widx(d, (u32)(sr % N))] = (u16)words[key];
     }
     return RBE_OK;
   };

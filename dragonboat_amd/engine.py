@@ -14,7 +14,7 @@ import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libdragonboat_amd.so")
-RBE_ABI_VERSION = 7
+RBE_ABI_VERSION = 8
 
 COUNTER_NAMES = ["steps", "committed", "msg_in", "msg_out", "ent_in", "ent_out",
                  "reads_confirmed", "proposals", "reads", "quiesced_ticks", "active_ticks",
@@ -179,7 +179,7 @@ class RbeWireFrame(C.Structure):
 
 class RbeWireConfig(C.Structure):
     _fields_ = [("deployment_id", C.c_uint64), ("bin_ver", C.c_uint32),
-                ("groups_per_batch", C.c_uint32), ("source_address", C.c_char_p * 6),
+                ("groups_per_batch", C.c_uint32), ("source_address", C.c_char_p * 7),
                 ("dst_rank", C.c_int32), ("pad", C.c_uint32)]
 
 

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RBE_ABI_VERSION 7
+#define RBE_ABI_VERSION 8
 
 /* error codes */
 #define RBE_OK 0
@@ -94,7 +94,7 @@ typedef struct rbe_config {
   uint32_t abi_version;      /* RBE_ABI_VERSION */
   int32_t device;            /* HIP device ordinal */
   uint64_t n_groups;         /* groups owned by this engine */
-  uint32_t n_replicas;       /* replica slots per group, 1..6 (the group's largest size) */
+  uint32_t n_replicas;       /* replica slots per group, 1..7 (the group's largest size) */
   uint32_t election_rtt;     /* ticks, config.ElectionRTT */
   uint32_t heartbeat_rtt;    /* ticks, config.HeartbeatRTT */
   uint32_t check_quorum;     /* config.CheckQuorum */
@@ -543,7 +543,7 @@ typedef struct rbe_wire_config {
   uint64_t deployment_id;      /* MessageBatch.DeploymentId */
   uint32_t bin_ver;            /* MessageBatch.BinVer (raftio.RPCBinVersion) */
   uint32_t groups_per_batch;   /* 0 = every group in one batch per slot pair */
-  const char* source_address[6];  /* MessageBatch.SourceAddress per sender slot (< 48 B) */
+  const char* source_address[7];  /* MessageBatch.SourceAddress per sender slot (< 48 B) */
   /* replica mode (rep_world > 1): only the messages of the replicas stepped
    * here to replicas stepped by rank dst_rank (-1: by any other rank); the
    * stream for one remote engine, as a transport keeps one connection per

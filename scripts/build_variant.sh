@@ -10,7 +10,7 @@ mkdir -p "$obj"
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-parameter $*"
 /opt/rocm/bin/hipcc $F -c -o $obj/e.o dragonboat_amd/csrc/rbe_engine.hip &
 /opt/rocm/bin/hipcc $F -c -o $obj/s.o dragonboat_amd/csrc/rbe_sort.hip &
-for n in 1 2 3 4 5 6; do for t in 0 1; do
+for n in 1 2 3 4 5 6 7; do for t in 0 1; do
   /opt/rocm/bin/hipcc $F -DRBE_ROUND_N=$n -DRBE_ROUND_TRACE=$t -c -o $obj/r_${n}_$t.o dragonboat_amd/csrc/rbe_round.hip &
 done; done
 wait

@@ -242,7 +242,7 @@ class SoaCpu(NodeInputs):
     def wire_encode(self, deployment_id=0, bin_ver=0, groups_per_batch=0, source_address=(),
                     dst_rank=-1):
         """Host-build rbe_wire_encode + rbe_wire_fetch: (stream bytes, frames)."""
-        addrs = (C.c_char_p * 6)(*[a.encode() for a in source_address])
+        addrs = (C.c_char_p * 7)(*[a.encode() for a in source_address])
         n = self.cfg.n_replicas
         gpb = groups_per_batch or self.n_groups
         maxf = n * (n - 1) * ((self.n_groups + gpb - 1) // gpb)

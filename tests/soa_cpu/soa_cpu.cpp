@@ -831,7 +831,7 @@ void soa_views(void* h, rbe_replica_view* out) {
     v.votes_granted = hh.votes_granted;
     v.events = (e->round > 0 && e->P.upd[i].round == e->round - 1) ? e->P.upd[i].events : 0u;
     v.removed = c.members & MB_REMOVED;
-    if (c.members & MB_ROLES) {  // Planes::roles is only current while MB_ROLES is set
+    if (c.mflags & MB_ROLES) {  // Planes::roles is only current while MB_ROLES is set
       v.observers = e->P.roles[i] & 0xFFu;
       v.witnesses = e->P.roles[i] >> 8;
     }

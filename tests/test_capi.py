@@ -49,10 +49,10 @@ def test_footprint_and_validation():
     # config.Validate (config/config.go:173-208): ElectionRTT > 2 * HeartbeatRTT
     bad = E.make_config(n_groups=10, election_rtt=2, heartbeat_rtt=1)
     assert lib.rbe_footprint(C.byref(bad), C.byref(b)) == -1
-    for n in range(1, 7):  # group sizes 1..6
+    for n in range(1, 8):  # group sizes 1..7
         assert lib.rbe_footprint(C.byref(E.make_config(n_groups=10, n_replicas=n)),
                                  C.byref(b)) == 0
-    for n in (0, 7):
+    for n in (0, 8):
         assert lib.rbe_footprint(C.byref(E.make_config(n_groups=10, n_replicas=n)),
                                  C.byref(b)) == -1
     # spare slots (n_voters < n_replicas) need membership

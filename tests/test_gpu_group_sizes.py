@@ -1,4 +1,4 @@
-"""Every group size (N = 1..6) and spare slots on the HIP engine against the
+"""Every group size (N = 1..7) and spare slots on the HIP engine against the
 oracle harness, round by round; the CPU-tier twin is tests/test_group_sizes.py."""
 import pytest
 
@@ -25,7 +25,7 @@ def test_gpu_group_size_parity(gpu_available, n, shape):
     eng.close()
 
 
-@pytest.mark.parametrize("n", [2, 4, 6])
+@pytest.mark.parametrize("n", [2, 4, 6, 7])
 def test_gpu_group_size_untraced(gpu_available, n):
     from dragonboat_amd.engine import Engine
     kw, extra, rounds = shapes(n)["C4"]
@@ -35,7 +35,7 @@ def test_gpu_group_size_untraced(gpu_available, n):
     eng.close()
 
 
-@pytest.mark.parametrize("n,nv", [(5, 3), (4, 1), (6, 3)])
+@pytest.mark.parametrize("n,nv", [(5, 3), (4, 1), (6, 3), (7, 4)])
 def test_gpu_spare_slots_join(gpu_available, n, nv):
     from dragonboat_amd.engine import Engine
     kw = dict(C3, n_groups=12, n_replicas=n, n_voters=nv, **MEMB)

@@ -10,7 +10,7 @@ from test_replica_gloo import run_case
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name", ["C2_w2", "C4_w3", "N5_w4", "C3_iso_w2", "C3_iso_w4", "C2_w4c",
+@pytest.mark.parametrize("name", ["C2_w2", "C4_w3", "N5_w4", "N7_w3", "C3_iso_w2", "C3_iso_w4", "C2_w4c",
                                   "C3_iso_w4c"])
 def test_gpu_replica_per_rank_matches_oracle(gpu_available, name):
     run_case(name, gpu=True)

@@ -1,4 +1,4 @@
-"""Every group size the engine is built for (N = 1..6 voting slots; rbe_types.h
+"""Every group size the engine is built for (N = 1..7 voting slots; rbe_types.h
 kMaxN): the device step compiled for the host (tests/soa_cpu) against the
 oracle harness, round by round, on C2-shaped replication, C3-shaped leader
 isolation (elections, vote tally, conflicts and backtracking), C4-shaped
@@ -15,7 +15,7 @@ from parity_util import C2, C3, C4, counters_match, run_lockstep
 from soa_cpu.soa import SoaCpu
 from test_membership import CATCHUP, MEMB
 
-SIZES = [1, 2, 3, 4, 5, 6]
+SIZES = [1, 2, 3, 4, 5, 6, 7]
 
 
 def shapes(n):
@@ -43,7 +43,7 @@ def test_group_size_parity(n, shape):
         assert c["campaigns"] > kw["n_groups"], "the isolations forced no elections"
 
 
-@pytest.mark.parametrize("n", [2, 4, 6])
+@pytest.mark.parametrize("n", [2, 4, 6, 7])
 def test_group_size_untraced(n):
     """The bench paths (untraced: lazy quiesced ticks, group sleep)."""
     kw, extra, rounds = shapes(n)["C4"]
@@ -52,7 +52,7 @@ def test_group_size_untraced(n):
     assert run_lockstep(eng, ref, rounds, every=1, skip=("digest",)) is None
 
 
-@pytest.mark.parametrize("n", [4, 6])
+@pytest.mark.parametrize("n", [4, 6, 7])
 def test_group_size_membership(n):
     kw = dict(C3, n_groups=12, n_replicas=n, **MEMB)
     eng = SoaCpu(trace=True, **kw, **CATCHUP)
@@ -68,12 +68,12 @@ def test_group_size_membership(n):
 def test_group_size_limits():
     from dragonboat_amd.engine import Engine  # noqa: F401  (config builder only)
     with pytest.raises(Exception):
-        SoaCpu(trace=True, n_groups=2, n_replicas=7)
+        SoaCpu(trace=True, n_groups=2, n_replicas=8)
     with pytest.raises(Exception):
         SoaCpu(trace=True, n_groups=2, n_replicas=0)
 
 
-@pytest.mark.parametrize("n,nv", [(5, 3), (4, 1), (6, 3)])
+@pytest.mark.parametrize("n,nv", [(5, 3), (4, 1), (6, 3), (7, 4)])
 def test_spare_slots_join(n, nv):
     """Groups that start with nv voters and n - nv spare slots: nodes that join
     later (started with no peers and an empty log, node.go:280-292) and take

@@ -168,13 +168,14 @@ def deliver_ids(engs, n, n_rep, ids):
     return moved
 
 
+@pytest.mark.parametrize("n", [5, 7])
 @pytest.mark.parametrize("wire", [False, True])
-def test_node_ids_over_the_transport(wire):
+def test_node_ids_over_the_transport(wire, n):
     """W = 2 engines whose cross-engine traffic carries node ids: raftpb
     messages (rbe_get_outbox / rbe_push_messages) or wire frames
-    (rbe_wire_encode / rbe_wire_ingest)."""
+    (rbe_wire_encode / rbe_wire_ingest); groups of 5 and of 7."""
     from transport_util import deliver_wire
-    kw = dict(C3, n_groups=10, iso_mod=2, xfer_period=9, xfer_mod=2)
+    kw = dict(C3, n_groups=10, n_replicas=n, iso_mod=2, xfer_period=9, xfer_mod=2)
     n = kw["n_replicas"]
     ids = random_ids(10, n, seed=7)
     engs = []

@@ -39,6 +39,11 @@ CASES = {
     # the 3/4 of the groups it steps a replica of (W = 8: 3/8); n_groups not a
     # multiple of W leaves padding groups; the second case adds the isolation
     # schedule, whose leader bits are exchanged by global group
+    # a group of 7 over 3 ranks: slot 6's count word sits in the sender's own
+    # place of the 6-word outbox header (cnt_widx)
+    "N7_w3": (dict(n_groups=12, n_replicas=7, check_quorum=True, quiesce=True, wl_enabled=True,
+                   wl_start_round=25, wl_active_mod=2, wl_read_permille=500, iso_period=41,
+                   iso_len=20, iso_mod=2), 3, 300, dict(ring=128, rq_cap=64, maxm=24)),
     "C2_w4c": (dict(n_groups=22, n_replicas=3, wl_enabled=True, wl_start_round=30), 4, 200,
                dict(rep_compact=True)),
     "C3_iso_w4c": (dict(n_groups=22, n_replicas=3, check_quorum=True, wl_enabled=True,
