@@ -5,7 +5,7 @@ import pytest
 import oracle as O
 from parity_util import run_lockstep
 from test_membership import CATCHUP
-from test_observers_witnesses import OW_CASES
+from test_observers_witnesses import OW_CASES, SIZES
 
 pytestmark = pytest.mark.gpu
 
@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 def test_gpu_observer_witness_schedule(gpu_available, name):
     from dragonboat_amd.engine import Engine
     kw, rounds = OW_CASES[name]
-    eng = Engine(device=0, trace=True, **kw, **CATCHUP)
+    eng = Engine(device=0, trace=True, **kw, **SIZES.get(name, CATCHUP))
     ref = O.Harness(**kw)
     wit = 0
     for _ in range(rounds // 50):

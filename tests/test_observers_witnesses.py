@@ -41,7 +41,15 @@ OW_CASES = {
     # 4 voters, an observer and a witness, leaders isolated every epoch
     "N6": (dict(C3, n_groups=12, n_replicas=6, n_voters=4, observer_slots=0b010000,
                 witness_slots=0b100000, iso_mod=2, **MEMB), 400),
+    # groups of 7: 5 voters, an observer and a witness in slot 6 (the slot whose
+    # outbox word takes the sender's own place)
+    "N7": (dict(C3, n_groups=10, n_replicas=7, n_voters=5, observer_slots=0b0100000,
+                witness_slots=0b1000000, **MEMB), 400),
 }
+# engine sizes per case: in N7 the witness joins after ~370 rounds and catches up
+# from index 1 in one Replicate, so the ring and the round's arena hold all of it
+# (the default sizes fault it with F_ARENA, a capacity limit the reference lacks)
+SIZES = {"N7": dict(CATCHUP, ring=1024, ecap=1024)}
 
 
 def _roles_seen(ref):
@@ -54,13 +62,14 @@ def _roles_seen(ref):
 
 def run_ow(eng, ref, rounds, skip=()):
     obs = wit = promoted = 0
+    full = (1 << eng.cfg.n_replicas) - 1
     for _ in range(rounds // 50):
         d = run_lockstep(eng, ref, 50, every=1, skip=skip)
         assert d is None, f"first divergence {d}"
         o, w = _roles_seen(ref)
         obs |= o
         wit |= w
-        promoted = max(promoted, max(bin(~v.removed & ~v.observers & ~v.witnesses & 0x3F).count("1")
+        promoted = max(promoted, max(bin(~v.removed & ~v.observers & ~v.witnesses & full).count("1")
                                      for v in ref.views()))
     return obs, wit, promoted
 
@@ -68,7 +77,7 @@ def run_ow(eng, ref, rounds, skip=()):
 @pytest.mark.parametrize("name", list(OW_CASES))
 def test_observer_witness_schedule(name):
     kw, rounds = OW_CASES[name]
-    eng = SoaCpu(trace=True, **kw, **CATCHUP)
+    eng = SoaCpu(trace=True, **kw, **SIZES.get(name, CATCHUP))
     ref = O.Harness(**kw)
     obs, wit, _ = run_ow(eng, ref, rounds)
     assert eng.faults()[0] == 0
@@ -99,19 +108,21 @@ def test_observer_witness_full_table_only():
     assert run_lockstep(eng, ref, 300, every=1) is None
 
 
-def test_observer_witness_untraced():
-    kw, rounds = OW_CASES["N6"]
-    eng = SoaCpu(trace=False, **kw, **CATCHUP)
+@pytest.mark.parametrize("name", ["N6", "N7"])
+def test_observer_witness_untraced(name):
+    kw, rounds = OW_CASES[name]
+    eng = SoaCpu(trace=False, **kw, **SIZES.get(name, CATCHUP))
     ref = O.Harness(**kw)
-    assert run_lockstep(eng, ref, 300, every=1, skip=("digest",)) is None
+    assert run_lockstep(eng, ref, rounds, every=1, skip=("digest",)) is None
 
 
-def test_observer_witness_snapshots():
+@pytest.mark.parametrize("name", ["N5", "N7"])
+def test_observer_witness_snapshots(name):
     """Snapshots and compaction with observers / witnesses in the membership:
     a node snapshot records them, InstallSnapshot carries them (a witness gets
     a witness snapshot), RestoreRemotes restores them."""
     from test_membership_snapshot import run_memb_snap
-    kw = dict(OW_CASES["N5"][0], snapshot_entries=8, compaction_overhead=2, iso_mod=2)
+    kw = dict(OW_CASES[name][0], snapshot_entries=8, compaction_overhead=2, iso_mod=2)
     eng = SoaCpu(trace=True, **kw, **CATCHUP)
     ref = O.Harness(**kw)
     run_memb_snap(eng, ref, 400)
