@@ -11,7 +11,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("name", ["C3_SNAP", "C3_NOCQ_SNAP", "C3_R64_ISO100", "MIXED_SNAP",
-                                  "C4_SNAP"])
+                                  "C4_SNAP", "N7_SNAP"])
 def test_gpu_compaction_install_snapshot_parity(gpu_available, name):
     from dragonboat_amd.engine import Engine
     kw, extra, rounds = CASES[name]

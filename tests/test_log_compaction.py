@@ -32,6 +32,8 @@ CASES = {
     "MIXED_SNAP": (dict(MIXED, snapshot_entries=10, compaction_overhead=0),
                    dict(ring=128, rq_cap=64, maxm=24), 500),
     "C4_SNAP": (dict(C4, **SNAP), {}, 400),
+    # groups of 7 (slot 6's outbox word in the sender's own place), leaders isolated
+    "N7_SNAP": (dict(C3, n_groups=24, n_replicas=7, iso_mod=2, **SNAP), dict(ring=128), 400),
 }
 
 

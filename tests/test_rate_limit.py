@@ -21,6 +21,7 @@ CASES = {
     "MIXED": (MIXED, 500, 500),
     # InstallSnapshot restores (inMemory.restore: Set(0)) and LogDB compaction
     "C3_HOT_SNAP": (dict(C3_HOT, snapshot_entries=8, compaction_overhead=2), 400, 600),
+    "C3_HOT_N7": (dict(C3_HOT, n_groups=24, n_replicas=7), 400, 600),
 }
 
 
