@@ -18,10 +18,14 @@ DRIVEN = dict(maxm=40, ecap=64, rq_cap=32, ring=256)
 
 def _pair(kw):
     base = dict(kw, ext_inputs=True, ext_apply=True, ext_commit=True)
-    return SoaCpu(trace=True, **dict(base, **DRIVEN)), O.Harness(**base)
+    sizes = dict(DRIVEN)
+    if kw.get("n_replicas", 3) > 5:
+        sizes["ecap"] = 256  # a leader copies a range for each of its remotes in one round
+    return SoaCpu(trace=True, **dict(base, **sizes)), O.Harness(**base)
 
 
-@pytest.mark.parametrize("name,kw", [("C2", C2), ("C3", C3), ("C4", C4)])
+@pytest.mark.parametrize("name,kw", [("C2", C2), ("C3", C3), ("C4", C4),
+                                     ("C3_N7", dict(C3, n_groups=24, n_replicas=7))])
 def test_delayed_persist_parity(name, kw):
     eng, ref = _pair(dict(kw, n_groups=12))
     d, st = run_commit_driven(eng, ref, 160, seed=5)

@@ -15,11 +15,13 @@ pytestmark = pytest.mark.gpu
 DRIVEN = dict(maxm=40, ecap=64, rq_cap=32, ring=256)
 
 
-@pytest.mark.parametrize("name,kw", [("C2", C2), ("C3", C3), ("C4", C4)])
+@pytest.mark.parametrize("name,kw", [("C2", C2), ("C3", C3), ("C4", C4),
+                                     ("C3_N7", dict(C3, n_replicas=7))])
 def test_gpu_delayed_persist_parity(gpu_available, name, kw):
     from dragonboat_amd.engine import Engine
     base = dict(kw, n_groups=12, ext_inputs=True, ext_apply=True, ext_commit=True)
-    eng, ref = Engine(device=0, trace=True, **dict(base, **DRIVEN)), O.Harness(**base)
+    sizes = dict(DRIVEN, ecap=256) if base["n_replicas"] > 5 else DRIVEN  # tests/test_ext_commit.py
+    eng, ref = Engine(device=0, trace=True, **dict(base, **sizes)), O.Harness(**base)
     d, st = run_commit_driven(eng, ref, 160, seed=5)
     assert d is None, f"{name}: first divergence {d}"
     assert eng.fault_summary()[0] == 0

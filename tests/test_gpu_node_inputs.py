@@ -12,8 +12,10 @@ from parity_util import C2, C3, C4, MIXED, run_lockstep, counters_match
 
 pytestmark = pytest.mark.gpu
 
-EXTRA = {"C3": dict(ring=128), "MIXED": dict(ring=128, rq_cap=64, maxm=24)}
+EXTRA = {"C3": dict(ring=128), "C3_N7": dict(ring=128), "MIXED": dict(ring=128, rq_cap=64, maxm=24)}
 DRIVEN = dict(maxm=40, ecap=64, rq_cap=32)  # see tests/test_node_inputs.py
+DRIVEN_BY_NAME = {"C3_N7": dict(ecap=256)}
+N7 = ("C3_N7", dict(C3, n_groups=24, n_replicas=7))
 
 
 def _pair(kw, name="", trace=True, **more):
@@ -23,10 +25,11 @@ def _pair(kw, name="", trace=True, **more):
     eng_kw.update(EXTRA.get(name, {}))
     if kw.get("ext_inputs"):
         eng_kw.update(DRIVEN)
+        eng_kw.update(DRIVEN_BY_NAME.get(name, {}))
     return Engine(device=0, trace=trace, **eng_kw), O.Harness(**kw)
 
 
-@pytest.mark.parametrize("name,kw", [("C2", C2), ("C3", C3), ("C4", C4)])
+@pytest.mark.parametrize("name,kw", [("C2", C2), ("C3", C3), ("C4", C4), N7])
 def test_gpu_driven_inputs_parity(gpu_available, name, kw):
     kw = dict(kw, n_groups=min(kw["n_groups"], 16))
     eng, ref = _pair(kw, name, ext_inputs=True)
@@ -69,7 +72,7 @@ def test_gpu_rounds_without_tick(gpu_available, trace):
     eng.close()
 
 
-@pytest.mark.parametrize("name,kw", [("C2", C2), ("C3", C3), ("MIXED", MIXED)])
+@pytest.mark.parametrize("name,kw", [("C2", C2), ("C3", C3), ("MIXED", MIXED), N7])
 def test_gpu_leader_transfer_schedule_parity(gpu_available, name, kw):
     kw = dict(kw, xfer_period=23, xfer_mod=2)
     eng, ref = _pair(kw, name)

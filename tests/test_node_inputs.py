@@ -23,7 +23,7 @@ from input_util import run_driven
 from parity_util import C2, C3, C4, MIXED, run_lockstep
 from soa_cpu.soa import SoaCpu
 
-EXTRA = {"C3": dict(ring=128), "MIXED": dict(ring=128, rq_cap=64, maxm=24)}
+EXTRA = {"C3": dict(ring=128), "C3_N7": dict(ring=128), "MIXED": dict(ring=128, rq_cap=64, maxm=24)}
 
 
 # Host-driven rounds put more traffic on one (sender, destination) stream than
@@ -31,6 +31,8 @@ EXTRA = {"C3": dict(ring=128), "MIXED": dict(ring=128, rq_cap=64, maxm=24)}
 # broadcast, every forwarded proposal a Replicate): the per-round message and
 # entry capacities are raised so the test exercises the protocol, not F_OUTBOX.
 DRIVEN = dict(maxm=40, ecap=64, rq_cap=32)
+# a leader of 7 copies a range for each of six remotes in one round
+DRIVEN_BY_NAME = {"C3_N7": dict(ecap=256)}
 
 
 def _pair(kw, name="", **more):
@@ -39,10 +41,12 @@ def _pair(kw, name="", **more):
     eng_kw.update(EXTRA.get(name, {}))
     if kw.get("ext_inputs"):
         eng_kw.update(DRIVEN)
+        eng_kw.update(DRIVEN_BY_NAME.get(name, {}))
     return SoaCpu(trace=True, **eng_kw), O.Harness(**kw)
 
 
-@pytest.mark.parametrize("name,kw", [("C2", C2), ("C3", C3), ("C4", C4)])
+@pytest.mark.parametrize("name,kw", [("C2", C2), ("C3", C3), ("C4", C4),
+                                     ("C3_N7", dict(C3, n_groups=24, n_replicas=7))])
 def test_driven_inputs_parity(name, kw):
     kw = dict(kw, n_groups=min(kw["n_groups"], 16))
     eng, ref = _pair(kw, name, ext_inputs=True)
@@ -113,7 +117,8 @@ def test_rounds_without_tick(tick_every):
     assert d is None, f"untraced: first divergence {d}"
 
 
-@pytest.mark.parametrize("name,kw", [("C2", C2), ("C3", C3), ("MIXED", MIXED)])
+@pytest.mark.parametrize("name,kw", [("C2", C2), ("C3", C3), ("MIXED", MIXED),
+                                     ("C3_N7", dict(C3, n_groups=24, n_replicas=7))])
 def test_leader_transfer_schedule_parity(name, kw):
     """The seeded RequestLeaderTransfer schedule: transfers happen (TimeoutNow,
     a campaign with the transfer hint, a new leader) and every replica stays
