@@ -25,7 +25,7 @@ def test_gpu_membership_snapshot_parity(gpu_available, name):
     eng.close()
 
 
-@pytest.mark.parametrize("name", ["C2", "C3_HOT", "MIXED"])
+@pytest.mark.parametrize("name", ["C2", "C3_HOT", "MIXED", "C3_HOT_N7"])
 def test_gpu_membership_snapshot_untraced(gpu_available, name):
     from dragonboat_amd.engine import Engine
     kw, extra, rounds = CASES[name]

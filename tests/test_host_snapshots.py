@@ -24,6 +24,7 @@ DRIVE = dict(maxm=40, ecap=256, rq_cap=32, ring=128)
 CASES = {
     "C3": dict(C3, n_groups=16, **HOST_SNAP),
     "C3_HOT": dict(C3_HOT, n_groups=16, **HOST_SNAP),
+    "C3_N7": dict(C3, n_groups=12, n_replicas=7, **HOST_SNAP),
 }
 
 

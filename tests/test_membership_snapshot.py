@@ -36,6 +36,7 @@ CASES = {
     "C3_HOT": (dict(C3_HOT, n_groups=24, **MEMB, **SNAP), CATCHUP, 400),
     "MIXED": (dict(MIXED, **MEMB, snapshot_entries=10, compaction_overhead=0),
               dict(CATCHUP, rq_cap=64, maxm=24), 400),
+    "C3_HOT_N7": (dict(C3_HOT, n_groups=16, n_replicas=7, **MEMB, **SNAP), CATCHUP, 400),
 }
 
 
@@ -82,7 +83,7 @@ def test_membership_snapshot_parity(name, mode):
     assert diff > 0, "no replica restored a snapshot with a membership other than its own"
 
 
-@pytest.mark.parametrize("name", ["C2", "C3_HOT", "MIXED"])
+@pytest.mark.parametrize("name", ["C2", "C3_HOT", "MIXED", "C3_HOT_N7"])
 def test_membership_snapshot_untraced(name):
     """The bench paths (untraced: lazy quiesced ticks, group sleep)."""
     kw, extra, rounds = CASES[name]
