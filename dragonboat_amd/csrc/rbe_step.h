@@ -503,6 +503,10 @@ constexpr u32 kEntBatch = 8;
 // message; in global memory each such read after the step's first store
 // waited for every store before it (vmcnt is in order), a round trip per
 // handler: C3's general step spent ~10 us per inbound message.
+#ifndef RBE_FULL_INPF
+#define RBE_FULL_INPF 0
+#endif
+constexpr u32 kLaneInbox = RBE_FULL_INPF;
 #if defined(__HIPCC__) || defined(__HIP__)
 __device__ __forceinline__ RemoteMN (&lane_rem())[kMaxN][256] {
   __shared__ RemoteMN s_rem[kMaxN][256];
@@ -511,6 +515,20 @@ __device__ __forceinline__ RemoteMN (&lane_rem())[kMaxN][256] {
 __device__ __forceinline__ u8 (&lane_rst())[kMaxN][256] {
   __shared__ u8 s_rst[kMaxN][256];
   return s_rst;
+}
+// The first kLaneInbox inbound messages of a general step, and every sender's
+// count word, in LDS (RBE_FULL_INPF = kLaneInbox, k_full_list with LREM):
+// loaded with the remote slots before the step's first store, so the handlers
+// of those messages do not each wait for the stores of the ones before.
+// [message][16-B word][lane]: global_load_lds writes lane l's word at a
+// wave-uniform base + 16 * l
+__device__ __forceinline__ uint4 (&lane_inbox())[kLaneInbox ? kLaneInbox : 1][4][256] {
+  __shared__ uint4 s_inbox[kLaneInbox ? kLaneInbox : 1][4][256];
+  return s_inbox;
+}
+__device__ __forceinline__ u32 (&lane_inw())[kMaxN][256] {
+  __shared__ u32 s_inw[kMaxN][256];
+  return s_inw;
 }
 __device__ __forceinline__ Msg (&lane_defer_msgs())[kLaneDefer][256] {
   __shared__ Msg s_msgs[kLaneDefer][256];
@@ -532,6 +550,7 @@ struct Lane {
 #else
   static constexpr bool LREM = false;  // host builds keep them in the planes
 #endif
+  static constexpr bool INPF = LREM && kLaneInbox > 0;  // inbox head in LDS
   static constexpr bool LEAD = MODE == MODE_LEAD;  // steady-state leader subset
   static constexpr bool FOLL = MODE == MODE_FOLL;  // steady-state follower subset
   const Planes& P;
@@ -832,6 +851,63 @@ struct Lane {
   RBE_HD u64 msg_slot_base(u32 sender, u32 dest) const {
     return ((g * N + sender) * N + dest) * (u64)C.maxm;
   }
+#if defined(__HIP_DEVICE_COMPILE__)
+  // INPF: the count words of every sender, then the first kLaneInbox messages
+  // of the inbox in stream order (senders ascending, each sender's A list then
+  // its B list from the back), all loads issued before any is used and before
+  // the step's first store.  Positions past the inbox load the sender's first
+  // slot and are never read.
+  __device__ __forceinline__ void inbox_prefetch() {
+    if (round == 0) {
+      for (u32 s = 0; s < N; s++) lane_inw()[s][threadIdx.x] = 0u;
+      return;
+    }
+    u32 pcs[N];
+#pragma unroll
+    for (u32 s = 0; s < N; s++) pcs[s] = s == k ? 0u : in_word<N>(P, g, s, k, round);
+    const u32 ppar = par ^ 1u;
+    const Msg* src[kLaneInbox ? kLaneInbox : 1];
+#pragma unroll
+    for (u32 j = 0; j < kLaneInbox; j++) src[j] = &P.msgs[ppar][msg_slot_base(0, k)];
+    u32 before = 0;  // messages of the senders before s
+#pragma unroll
+    for (u32 s = 0; s < N; s++) {
+      const u32 na = pcs[s] & 0x7Fu, n = na + ((pcs[s] >> 7) & 0x7Fu);
+      const Msg* lst = &P.msgs[ppar][msg_slot_base(s, k)];
+#pragma unroll
+      for (u32 j = 0; j < kLaneInbox; j++) {
+        const u32 i = j - before;  // wraps when j < before: then i >= n
+        if (j >= before && i < n) src[j] = i < na ? &lst[i] : &lst[C.maxm - 1u - (i - na)];
+      }
+      before += n;
+    }
+    static_assert(sizeof(Msg) == 64, "a message is four 16-B words");
+#pragma unroll
+    for (u32 s = 0; s < N; s++) lane_inw()[s][threadIdx.x] = pcs[s];
+    // straight into LDS (no registers held), then one wait before the step's
+    // first store
+    const u32 wb = threadIdx.x & ~63u;
+#pragma unroll
+    for (u32 j = 0; j < kLaneInbox; j++)
+#pragma unroll
+      for (u32 c = 0; c < 4; c++)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)((const uint4*)src[j] + c),
+            (__attribute__((address_space(3))) void*)&lane_inbox()[j][c][wb], 16, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  }
+  __device__ __forceinline__ u32 inw_lds(u32 s) const { return lane_inw()[s][threadIdx.x]; }
+  __device__ __forceinline__ void inbox_lds(u32 j, Msg* m) const {
+    uint4 w[4];
+#pragma unroll
+    for (u32 c = 0; c < 4; c++) w[c] = lane_inbox()[j][c][threadIdx.x];
+    __builtin_memcpy(m, w, sizeof(Msg));
+  }
+#else
+  void inbox_prefetch() {}
+  u32 inw_lds(u32) const { return 0u; }
+  void inbox_lds(u32, Msg*) const {}
+#endif
   // raft.send + finalizeMessageTerm (raft.go:640-658) + the network: the
   // message joins Update.Messages (hashed here, in emission order) and is
   // written to the (self → dest) list, Replicate messages in front (node.go
@@ -2447,6 +2523,7 @@ struct Lane {
         lrst(s) = P.rem_st[r * N + s];
       }
     }
+    if constexpr (INPF) inbox_prefetch();
     fault = (flags & HF_FAULTED) ? P.upd[r].fault : 0u;
     const u64 digest0 = TRACE ? P.upd[r].digest : 0;
     snp_pend = snp_rej = 0;
@@ -2598,6 +2675,8 @@ struct Lane {
     //   handleLeaderTransferRequest (node.go:1069-1075) → Peer.RequestLeaderTransfer
     const u32 ppar = par ^ 1u;
     u32 cs = 0, ci = 0, cn = 0, cna = 0;  // inbox cursor: sender, index, count, #A
+    u32 n_taken = 0;                      // inbox messages taken (INPF: the first in LDS)
+    (void)n_taken;
     bool copen = false;
     const u32 phase0 = (unreach | snap_nodes) ? 0u : (round > 0 ? 1u : 2u);
     // calls the node makes under raftMu between two steps come first:
@@ -2670,7 +2749,9 @@ struct Lane {
               cs++;
               continue;
             }
-            const u32 pc = in_word<N>(P, g, cs, k, round);
+            u32 pc;
+            if constexpr (INPF) pc = inw_lds(cs);
+            else pc = in_word<N>(P, g, cs, k, round);
             if (pc & 0x8000u) {  // Quiesce first in the sender's stream (node.go:1207-1210)
               ctr.v[C_MSG_IN]++;
               q_try_enter();
@@ -2682,7 +2763,16 @@ struct Lane {
           }
           if (ci < cn) {
             const Msg* lst = &P.msgs[ppar][msg_slot_base(cs, k)];
-            m = ci < cna ? lst[ci] : lst[C.maxm - 1u - (ci - cna)];
+            if constexpr (INPF) {
+              if (n_taken < kLaneInbox) {
+                inbox_lds(n_taken, &m);
+              } else {
+                m = ci < cna ? lst[ci] : lst[C.maxm - 1u - (ci - cna)];
+              }
+              n_taken++;
+            } else {
+              m = ci < cna ? lst[ci] : lst[C.maxm - 1u - (ci - cna)];
+            }
             ents = &P.arena[ppar][(g * N + cs) * (u64)C.ecap + m.ent_off];
             ci++;
             kind = 1;
