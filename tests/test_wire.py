@@ -89,7 +89,8 @@ def test_message_batch_frame_round_trip():
 
 
 @pytest.mark.parametrize("name,kw,gpb", [("C2", C2, 16), ("C3", dict(C3, ring=128), 0),
-                                         ("C4", C4, 7)])
+                                         ("C4", C4, 7),
+                                         ("C3_N7", dict(C3, n_groups=20, n_replicas=7, ring=128), 5)])
 def test_host_build_frames_match_oracle(name, kw, gpb):
     eng = SoaCpu(trace=True, **kw)
     n, G = kw["n_replicas"], kw["n_groups"]

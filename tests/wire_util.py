@@ -6,7 +6,8 @@ import wire as W
 
 INSTALL_SNAPSHOT = W.INSTALL_SNAPSHOT
 ADDRS = ("node-1.example:26001", "node-2.example:26001", "node-3.example:26001",
-         "node-4.example:26001", "node-5.example:26001")
+         "node-4.example:26001", "node-5.example:26001", "node-6.example:26001",
+         "node-7.example:26001")
 
 
 def _msg_dict(m):
