@@ -542,8 +542,12 @@ struct rbe_engine {
   u32 tclk = 0;              // ticks before the next round (Clk::tclk)
   u32* d_clk = nullptr;      // device copy {round, tclk} read by graph replays
   std::vector<void*> allocs;
-  hipGraphExec_t graph = nullptr;
-  u32 graph_rounds = 0;
+  // captured K-round graphs, one per round count K (rbe_run; rbe_prepare_run
+  // captures ahead of a timed region), replaced round-robin
+  static constexpr int kGraphs = 4;
+  hipGraphExec_t graph[kGraphs] = {};
+  u32 graph_rounds[kGraphs] = {};
+  u32 graph_next = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   int mode = 3;              // RBE_MODE: 0 fused, 1 split (triage + 2 fast lists), 2 full,
                              // 3 both (default: triage + one merged fast launch)
@@ -595,6 +599,14 @@ struct rbe_engine {
   u64 wire_frames_off = 0;   // frame index inside wire_meta
 };
 
+static void drop_graphs(rbe_engine* e) {
+  for (int i = 0; i < rbe_engine::kGraphs; i++)
+    if (e->graph[i]) {
+      HIP_IGNORE(hipGraphExecDestroy(e->graph[i]));
+      e->graph[i] = nullptr;
+      e->graph_rounds[i] = 0;
+    }
+}
 
 // Copy `len` bytes at offset `off` of the heap record at absolute position
 // `pos`: still staged, from the host copy; else from the device after every
@@ -881,7 +893,7 @@ int rbe_destroy(rbe_engine* e) {
   if (!e) return RBE_OK;
   HIP_IGNORE(hipSetDevice(e->device));
   if (e->stream) HIP_IGNORE(hipStreamSynchronize(e->stream));
-  if (e->graph) HIP_IGNORE(hipGraphExecDestroy(e->graph));
+  drop_graphs(e);
   for (void* p : e->allocs) HIP_IGNORE(hipFree(p));
   if (e->d_clk) HIP_IGNORE(hipFree(e->d_clk));
   if (e->ev0) HIP_IGNORE(hipEventDestroy(e->ev0));
@@ -1189,13 +1201,21 @@ static int flush_inputs(rbe_engine* e) {
   if (!h.ents.empty())
     HIP_OK(hipMemcpyAsync(e->P.in_ents, h.ents.data(), h.ents.size() * sizeof(Ent),
                           hipMemcpyHostToDevice, e->stream));
-  const u64 m = std::max(std::max(n, ns), std::max(na, nc));
-  if (m) {  // (a flush of heap records alone, e.g. from rbe_push_messages, has none)
+  // three launches in the host build's order (input records and applied /
+  // ready pairs, then commits, then snapshot records): a replica may have one
+  // of each, and all three write its Hot flags, so no launch holds two lanes of
+  // one replica (a launch of heap records alone, from rbe_push_messages, has none)
+  const u64 m0 = std::max(n, na);
+  for (int ph = 0; ph < 3; ph++) {
+    const u64 pn = ph == 0 ? n : 0, pa = ph == 0 ? na : 0, pc = ph == 1 ? nc : 0,
+              ps = ph == 2 ? ns : 0;
+    const u64 m = ph == 0 ? m0 : (ph == 1 ? nc : ns);
+    if (!m) continue;
     hipLaunchKernelGGL(k_ext_scatter, dim3(grid_for(m)), dim3(kBlock), 0, e->stream, e->P,
-                       e->C.n, (const u64*)e->in_dev, (const ExtIn*)(e->in_dev + o_rec), n,
-                       (const u64*)(e->in_dev + o_ar), (const u64*)(e->in_dev + o_av), na,
-                       (const CommitRec*)(e->in_dev + o_cr), nc,
-                       (const SnapRec*)(e->in_dev + o_sr), ns, e->C, e->L, e->round & 1u);
+                       e->C.n, (const u64*)e->in_dev, (const ExtIn*)(e->in_dev + o_rec), pn,
+                       (const u64*)(e->in_dev + o_ar), (const u64*)(e->in_dev + o_av), pa,
+                       (const CommitRec*)(e->in_dev + o_cr), pc,
+                       (const SnapRec*)(e->in_dev + o_sr), ps, e->C, e->L, e->round & 1u);
     HIP_OK(hipGetLastError());
   }
   HIP_OK(hipEventRecord(e->in_ev, e->stream));
@@ -1232,45 +1252,73 @@ int rbe_step_ex(rbe_engine* e, uint32_t flags) {
 }
 
 // K rounds as one graph: K step launches reading the round from device memory,
-// then one advance of that counter.
-static int run_graph(rbe_engine* e, u32 rounds) {
-  if (e->graph && e->graph_rounds != rounds) {
-    HIP_IGNORE(hipGraphExecDestroy(e->graph));
-    e->graph = nullptr;
-  }
-  const u32 clk[2] = {e->round, e->tclk};
-  if (!e->graph) {
-    HIP_OK(hipMemcpyAsync(e->d_clk, clk, sizeof(clk), hipMemcpyHostToDevice, e->stream));
-    HIP_OK(hipStreamSynchronize(e->stream));
-    hipGraph_t g;
-    HIP_OK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
-    for (u32 i = 0; i < rounds; i++) {
-      int rc = launch_step(e, RoundArg{e->d_clk, i, i, 1u});
-      if (rc) {
-        HIP_IGNORE(hipStreamEndCapture(e->stream, &g));
-        return rc;
-      }
+// then one advance of that counter.  The graph does not depend on the round, so
+// one capture per K serves every later run of K rounds.
+static int graph_for(rbe_engine* e, u32 rounds, hipGraphExec_t* out) {
+  for (int i = 0; i < rbe_engine::kGraphs; i++)
+    if (e->graph[i] && e->graph_rounds[i] == rounds) {
+      *out = e->graph[i];
+      return RBE_OK;
     }
-    hipLaunchKernelGGL(k_advance, dim3(1), dim3(1), 0, e->stream, e->d_clk, rounds);
-    HIP_OK(hipStreamEndCapture(e->stream, &g));
-    HIP_OK(hipGraphInstantiate(&e->graph, g, nullptr, nullptr, 0));
-    HIP_IGNORE(hipGraphDestroy(g));
-    e->graph_rounds = rounds;
-  } else {
-    HIP_OK(hipMemcpyAsync(e->d_clk, clk, sizeof(clk), hipMemcpyHostToDevice, e->stream));
+  const int slot = (int)(e->graph_next++ % rbe_engine::kGraphs);
+  if (e->graph[slot]) {
+    HIP_IGNORE(hipGraphExecDestroy(e->graph[slot]));
+    e->graph[slot] = nullptr;
   }
-  HIP_OK(hipGraphLaunch(e->graph, e->stream));
+  // capture ends every queued round first; the clock copy before the replay
+  // (run_graph) gives the launches their round
+  HIP_OK(hipStreamSynchronize(e->stream));
+  hipGraph_t g;
+  HIP_OK(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+  for (u32 i = 0; i < rounds; i++) {
+    int rc = launch_step(e, RoundArg{e->d_clk, i, i, 1u});
+    if (rc) {
+      HIP_IGNORE(hipStreamEndCapture(e->stream, &g));
+      return rc;
+    }
+  }
+  hipLaunchKernelGGL(k_advance, dim3(1), dim3(1), 0, e->stream, e->d_clk, rounds);
+  HIP_OK(hipStreamEndCapture(e->stream, &g));
+  HIP_OK(hipGraphInstantiate(&e->graph[slot], g, nullptr, nullptr, 0));
+  HIP_IGNORE(hipGraphDestroy(g));
+  // the executable's first launch would otherwise upload it
+  HIP_OK(hipGraphUpload(e->graph[slot], e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  e->graph_rounds[slot] = rounds;
+  *out = e->graph[slot];
+  return RBE_OK;
+}
+
+static bool graphable(const rbe_engine* e, u32 rounds) {
+  return e->C.iso_period == 0 && !e->C.ext_inputs && rounds >= 2 &&
+         getenv("RBE_NO_GRAPH") == nullptr;
+}
+
+static int run_graph(rbe_engine* e, u32 rounds) {
+  hipGraphExec_t gx = nullptr;
+  int rc = graph_for(e, rounds, &gx);
+  if (rc) return rc;
+  const u32 clk[2] = {e->round, e->tclk};
+  HIP_OK(hipMemcpyAsync(e->d_clk, clk, sizeof(clk), hipMemcpyHostToDevice, e->stream));
+  HIP_OK(hipGraphLaunch(gx, e->stream));
   e->round += rounds;
   e->tclk += rounds;
   return RBE_OK;
+}
+
+int rbe_prepare_run(rbe_engine* e, uint32_t rounds) {
+  if (!e) return RBE_E_INVALID;
+  HIP_OK(hipSetDevice(e->device));
+  if (!graphable(e, rounds)) return RBE_OK;
+  hipGraphExec_t gx = nullptr;
+  return graph_for(e, rounds, &gx);
 }
 
 int rbe_run(rbe_engine* e, uint32_t rounds) {
   if (!e) return RBE_E_INVALID;
   if (rounds == 0) return RBE_OK;
   HIP_OK(hipSetDevice(e->device));
-  const bool graphable = e->C.iso_period == 0 && !e->C.ext_inputs && rounds >= 2;
-  if (graphable && getenv("RBE_NO_GRAPH") == nullptr) return run_graph(e, rounds);
+  if (graphable(e, rounds)) return run_graph(e, rounds);
   for (u32 i = 0; i < rounds; i++) {
     int rc = step_one(e);
     if (rc) return rc;
@@ -1280,7 +1328,8 @@ int rbe_run(rbe_engine* e, uint32_t rounds) {
 
 int rbe_run_timed(rbe_engine* e, uint32_t rounds, float* ms) {
   if (!e || !ms) return RBE_E_INVALID;
-  HIP_OK(hipSetDevice(e->device));
+  int rc0 = rbe_prepare_run(e, rounds);  // any capture before the first event
+  if (rc0) return rc0;
   HIP_OK(hipEventRecord(e->ev0, e->stream));
   int rc = rbe_run(e, rounds);
   if (rc) return rc;
@@ -1481,10 +1530,7 @@ int rbe_set_node_ids(rbe_engine* e, uint64_t first_group, uint64_t count, const 
   HIP_OK(hipMemcpyAsync((void*)e->P.node_ids, e->hin.ids.data(), bytes, hipMemcpyHostToDevice,
                         e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
-  if (e->graph) {  // kernels take the planes by value: a captured graph holds the old ones
-    HIP_OK(hipGraphExecDestroy(e->graph));
-    e->graph = nullptr;
-  }
+  drop_graphs(e);  // kernels take the planes by value: a captured graph holds the old ones
   return RBE_OK;
 }
 
@@ -1511,12 +1557,9 @@ extern "C" int rbe_debug_full_prof(rbe_engine* e, uint64_t* out, uint64_t cap, u
   if (!e || !n) return RBE_E_INVALID;
   HIP_OK(hipSetDevice(e->device));
   if (!e->P.prof) {
-    HIP_OK(hipMalloc((void**)&e->P.prof, (4 + 4 * kFullProfCap) * sizeof(u64)));
-    HIP_OK(hipMemset(e->P.prof, 0, 32 * sizeof(u64)));  // counter | phase sums (rbe_debug_phases)
-    if (e->graph) {
-      HIP_IGNORE(hipGraphExecDestroy(e->graph));
-      e->graph = nullptr;
-    }
+    HIP_OK(hipMalloc((void**)&e->P.prof, (kProfHdr + 4 * kFullProfCap) * sizeof(u64)));
+    HIP_OK(hipMemset(e->P.prof, 0, kProfHdr * sizeof(u64)));  // counter | phase sums (rbe_debug_phases)
+    drop_graphs(e);
     *n = 0;
     return RBE_OK;
   }
@@ -1524,7 +1567,7 @@ extern "C" int rbe_debug_full_prof(rbe_engine* e, uint64_t* out, uint64_t cap, u
   u64 cnt = 0;
   HIP_OK(hipMemcpy(&cnt, e->P.prof, sizeof(u64), hipMemcpyDeviceToHost));
   const u64 m = std::min<u64>(std::min<u64>(cnt, kFullProfCap), cap);
-  if (m && out) HIP_OK(hipMemcpy(out, e->P.prof + 4, m * 4 * sizeof(u64), hipMemcpyDeviceToHost));
+  if (m && out) HIP_OK(hipMemcpy(out, e->P.prof + kProfHdr, m * 4 * sizeof(u64), hipMemcpyDeviceToHost));
   *n = cnt;
   HIP_OK(hipMemset(e->P.prof, 0, sizeof(u64)));
   return RBE_OK;

@@ -478,6 +478,10 @@ struct HostInputs {
   // staged replica-value pairs: rbe_notify_applied values, and with bit 63 of
   // the replica word set, rbe_set_apply_ready flags (value 1 = ready)
   std::vector<u64> app_rep, app_val;
+  struct AppSlot {
+    u32 applied, ready;  // index into app_rep, ~0u = none staged
+  };
+  std::vector<AppSlot> app_slot;  // [n_rep]
   std::vector<u64> applied;  // [n_rep] host mirror of Planes::applied (the host is its only writer)
   std::vector<CommitRec> commits;  // rbe_commit records for the next step, in call order
   std::vector<u8> committing;      // [n_rep] a commit is staged (one per replica per step)
@@ -542,6 +546,7 @@ struct HostInputs {
     applied.assign(n_rep, 0);
     committing.assign(n_rep, 0);
     snap_slot.assign(n_rep, ~0u);
+    app_slot.assign(n_rep, AppSlot{~0u, ~0u});
   }
   bool empty() const {
     return reps.empty() && app_rep.empty() && heap.stage.empty() && commits.empty() &&
@@ -552,6 +557,7 @@ struct HostInputs {
     reps.clear();
     recs.clear();
     ents.clear();
+    for (u64 r : app_rep) app_slot[r & ~(1ull << 63)] = AppSlot{~0u, ~0u};
     app_rep.clear();
     app_val.clear();
     for (const CommitRec& c : commits) committing[c.r] = 0;
@@ -582,13 +588,18 @@ struct HostInputs {
         return RBE_E_INVALID;  // stepped by another engine
     }
     if (!flag) return RBE_OK;
+    return unique_replicas(cnt, replica, flag);
+  }
+  // RBE_E_STATE when a replica appears twice in the batch or already has
+  // `flag` staged (0: only the first check); O(cnt) with the epoch stamps
+  int unique_replicas(u64 cnt, const u64* replica, u32 flag) {
     if (++epoch == 0) {
       for (SlotMark& x : sm) x.mark = 0u;
       epoch = 1;
     }
     for (u64 i = 0; i < cnt; i++) {
       const u64 r = replica[i];
-      if (sm[r].mark == epoch || (staged_flags(r) & flag)) return RBE_E_STATE;
+      if (sm[r].mark == epoch || (flag && (staged_flags(r) & flag))) return RBE_E_STATE;
       sm[r].mark = epoch;
     }
     return RBE_OK;
@@ -773,8 +784,7 @@ struct HostInputs {
       if (value[i] < applied[replica[i]]) return RBE_E_INVALID;
     for (u64 i = 0; i < cnt; i++) {
       const u64 r = replica[i];
-      app_rep.push_back(r);
-      app_val.push_back(value[i]);
+      stage_pair(r, value[i], false);
       // a changed applied index is an event of the step (node.go:1033)
       if (value[i] != applied[r]) rec(r).flags |= EXT_APPLIED;
       applied[r] = value[i];
@@ -785,11 +795,20 @@ struct HostInputs {
     if (cnt && !ready) return RBE_E_INVALID;
     int rc = check_replicas(cnt, replica, 0);
     if (rc) return rc;
-    for (u64 i = 0; i < cnt; i++) {
-      app_rep.push_back(replica[i] | (1ull << 63));
-      app_val.push_back(ready[i] ? 1u : 0u);
-    }
+    for (u64 i = 0; i < cnt; i++) stage_pair(replica[i], ready[i] ? 1u : 0u, true);
     return RBE_OK;
+  }
+  // one staged pair per (replica, kind) between two steps, so no two lanes of
+  // the scatter write one replica's row: a later call overwrites the value
+  void stage_pair(u64 r, u64 v, bool ready) {
+    u32& slot = ready ? app_slot[r].ready : app_slot[r].applied;
+    if (slot == ~0u) {
+      slot = (u32)app_rep.size();
+      app_rep.push_back(ready ? (r | (1ull << 63)) : r);
+      app_val.push_back(v);
+    } else {
+      app_val[slot] = v;
+    }
   }
   // rbe_snapshot_saved / rbe_compact (snapshot_entries with ext_apply): one of
   // each per replica per step; a snapshot no newer than the state machine's
@@ -810,9 +829,8 @@ struct HostInputs {
       }
       const u32 s = snap_slot[replica[i]];
       if (s != ~0u && (snaps[s].kind & kind)) return RBE_E_STATE;
-      for (u64 j = 0; j < i; j++)
-        if (replica[j] == replica[i]) return RBE_E_STATE;
     }
+    if ((rc = unique_replicas(cnt, replica, 0))) return rc;
     for (u64 i = 0; i < cnt; i++) {
       const u64 r = replica[i];
       if (snap_slot[r] == ~0u) {
@@ -841,9 +859,7 @@ struct HostInputs {
       if (uc[i].stable_snapshot_to != 0) return RBE_E_INVALID;
     for (u64 i = 0; i < cnt; i++)
       if (committing[replica[i]]) return RBE_E_STATE;
-    for (u64 i = 0; i < cnt; i++)  // within the batch too
-      for (u64 j = 0; j < i; j++)
-        if (replica[j] == replica[i]) return RBE_E_STATE;
+    if ((rc = unique_replicas(cnt, replica, 0))) return rc;  // within the batch too
     for (u64 i = 0; i < cnt; i++) {
       committing[replica[i]] = 1;
       commits.push_back(CommitRec{replica[i], uc[i].stable_log_to, uc[i].stable_log_term,

@@ -964,6 +964,9 @@ __global__ __launch_bounds__(kBlock, kFastWaves<N>) void k_fast_both(Planes P, P
 }
 
 static constexpr u64 kFullProfCap = 1u << 20;  // wave records of RBE_FULL_PROF builds
+// Planes::prof header: [0] the record counter, [8, 32) the RBE_PHASE_TIMING
+// sums (rbe_fast.h); the wave records follow it
+static constexpr u64 kProfHdr = 32;
 
 // Pass 3: the whole handler table over the full list (persistent, grid-stride).
 template <int N, bool TRACE>
@@ -1064,7 +1067,7 @@ __global__ __launch_bounds__(kBlock) void k_full_list(Planes P, Params C, RoundA
     if ((threadIdx.x & 63u) == 0 && P.prof) {
       const u64 at = atomicAdd((unsigned long long*)&P.prof[0], 1ull);
       if (at < kFullProfCap) {
-        u64* rec = &P.prof[4 + at * 4];
+        u64* rec = &P.prof[kProfHdr + at * 4];
         rec[0] = t1 - t0;
         rec[1] = mlo;
         rec[2] = mhi;

@@ -210,7 +210,7 @@ RTR_DTYPE = _np_dtype(RbeReadyToRead)
 EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe_step", "rbe_step_ex", "rbe_run",
            "rbe_sync", "rbe_request_leader_transfer", "rbe_report_unreachable",
            "rbe_report_snapshot_status", "rbe_notify_applied",
-           "rbe_round", "rbe_run_timed", "rbe_push_proposals", "rbe_push_read_index",
+           "rbe_round", "rbe_run_timed", "rbe_prepare_run", "rbe_push_proposals", "rbe_push_read_index",
            "rbe_get_updates", "rbe_get_messages", "rbe_get_ready_to_reads", "rbe_get_entries",
            "rbe_get_views", "rbe_get_counters", "rbe_reset_counters", "rbe_fault_summary",
            "rbe_footprint", "rbe_profile_rounds", "rbe_get_kernel_counters", "rbe_kernel_name",
@@ -275,6 +275,7 @@ def load_library(path: Optional[str] = None):
         "rbe_sync": (i32, [vp]),
         "rbe_round": (i32, [vp, P(u32)]),
         "rbe_run_timed": (i32, [vp, u32, P(C.c_float)]),
+        "rbe_prepare_run": (i32, [vp, u32]),
         "rbe_push_proposals": (i32, [vp, u64, P(u64), P(u32), P(u32), P(u32), P(C.c_uint8)]),
         "rbe_propose_entries": (i32, [vp, u64, P(u64), P(u32), P(RbeEntry), P(C.c_uint8)]),
         "rbe_push_read_index": (i32, [vp, u64, P(u64), P(u64), P(u64)]),
@@ -689,6 +690,10 @@ class Engine(NodeInputs):
 
     def run(self, rounds: int):
         _check(self.lib.rbe_run(self.h, rounds), "rbe_run")
+
+    def prepare_run(self, rounds: int):
+        """Capture the replay graph of `rounds` rounds ahead of a timed run."""
+        _check(self.lib.rbe_prepare_run(self.h, rounds), "rbe_prepare_run")
 
     def run_timed(self, rounds: int) -> float:
         ms = C.c_float()

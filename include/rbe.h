@@ -179,7 +179,7 @@ typedef struct rbe_config {
    * every ticking replica on the full handler table. */
   uint64_t max_inmem_log_size;
   /* the slots beyond n_voters whose nodes start as observers (config.IsObserver)
-   * or witnesses (config.IsWitness), bit (id-1); they take part once an
+   * or witnesses (config.IsWitness), bit s = slot s; they take part once an
    * AddObserver / AddWitness for them is applied (raft.go:1159-1180).  Needs
    * cfg.membership. */
   uint32_t observer_slots;
@@ -195,8 +195,11 @@ typedef struct rbe_replica_view {
   uint64_t match[8], next[8];
   uint32_t rstate[8], ractive[8];
   uint32_t events;  /* RBE_EV_* of the last round's step (0 when it made no step) */
-  uint32_t removed; /* bit (id-1): not in this replica's raft.remotes (cfg.membership) */
-  uint32_t observers, witnesses; /* bit (id-1): raft.observers / raft.witnesses */
+  /* slot masks, bit s = slot s (the group's s-th node: node id s + 1, or the
+   * s-th id given to rbe_set_node_ids): not in this replica's raft.remotes
+   * (cfg.membership), and raft.observers / raft.witnesses */
+  uint32_t removed;
+  uint32_t observers, witnesses;
 } rbe_replica_view;
 
 /* Per-replica step result: the Update of peer.go:201-207 / raftpb Update
@@ -240,8 +243,10 @@ typedef struct rbe_message {
   uint64_t to, from, cluster_id, term, log_term, log_index, commit, hint, hint_high;
   uint32_t n_entries;
   /* InstallSnapshot: the snapshot's membership (Snapshot.Membership, raft.pb.go:
-   * 733-739) as the node ids it does not list as voters, bit (id-1) (its index
-   * and term are log_index / log_term); 0 for every other type */
+   * 733-739) in the packed slot-mask form of rbe_launch_state::removed: bits
+   * 0-7 the slots it does not list as voters (Addresses), 8-15 its Observers,
+   * 16-23 its Witnesses, bit s = slot s of the group (its index and term are
+   * log_index / log_term); 0 for every other type */
   uint32_t reserved;
 } rbe_message;
 
@@ -339,8 +344,13 @@ int rbe_run(rbe_engine* e, uint32_t rounds);
 int rbe_sync(rbe_engine* e);
 int rbe_round(const rbe_engine* e, uint32_t* round);
 
-/* Time `rounds` rounds with HIP events on the engine stream; *ms = elapsed. */
+/* Time `rounds` rounds with HIP events on the engine stream; *ms = elapsed.
+ * A graph for that round count is captured before the first event. */
 int rbe_run_timed(rbe_engine* e, uint32_t rounds, float* ms);
+/* Capture (and upload) the replay graph of `rounds` rounds now, so a later
+ * rbe_run / rbe_run_timed of that many rounds only launches it; a no-op when
+ * the configuration steps round by round.  Synchronizes the engine stream. */
+int rbe_prepare_run(rbe_engine* e, uint32_t rounds);
 
 /* Round-pipeline kernel slots (rbe_profile_rounds, rbe_get_kernel_counters,
  * rbe_kernel_name).  The default pipeline runs k_triage /
@@ -485,8 +495,10 @@ int rbe_get_entries(rbe_engine* e, uint64_t replica, uint64_t lo, uint64_t hi,
  * the latest snapshot's index and term (CreateSnapshot, or ApplySnapshot of one
  * received), the node's reqSnapshotIndex and pending compactLogTo (node.go
  * ss, 585-605 / 849-866), the latest snapshot's membership and the state
- * machine's current one, each as the node ids that are not voting members,
- * bit (id-1) (pb.Snapshot.Membership, raft.pb.go:733-739; a snapshot records
+ * machine's current one, each in the packed slot-mask form of
+ * rbe_launch_state::removed (bits 0-7 the slots that are not voters, 8-15
+ * observers, 16-23 witnesses, bit s = slot s; pb.Snapshot.Membership,
+ * raft.pb.go:733-739; a snapshot records
  * the state machine's membership at its index, and a node that restores one
  * sends it to raft with RestoreRemotes at its next step). */
 int rbe_get_snapshot_state(rbe_engine* e, uint64_t first, uint64_t count, uint64_t* out8);

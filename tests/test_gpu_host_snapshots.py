@@ -29,3 +29,17 @@ def test_gpu_host_driven_snapshots_untraced(gpu_available):
     run_host_snapshots(eng, ref, 200, skip=("digest",))
     assert eng.fault_summary()[0] == 0
     eng.close()
+
+
+def test_gpu_host_driven_snapshots_apply_queue(gpu_available):
+    """One step's input holds an applied index, apply-queue flags (twice for
+    some replicas), a snapshot and a compaction for the same replica: the
+    scatter writes each replica's Hot flags from one lane at a time."""
+    from dragonboat_amd.engine import Engine
+    kw = CASES["C3_HOT"]
+    eng = Engine(device=0, trace=True, **kw, **DRIVE)
+    ref = O.Harness(**kw)
+    saved, compacted, _ = run_host_snapshots(eng, ref, 200, ready=0.5)
+    assert eng.fault_summary()[0] == 0
+    assert saved > 10 and compacted > 5, (saved, compacted)
+    eng.close()

@@ -56,6 +56,28 @@ def test_graph_replay_matches_stepwise(gpu_available):
     assert a.counters() == b.counters()
 
 
+def test_graph_cache_across_round_counts(gpu_available):
+    """Graphs captured ahead (rbe_prepare_run) and cached per round count,
+    replayed interleaved and past the cache size, equal stepwise rounds."""
+    from dragonboat_amd.engine import Engine
+    kw = dict(C4_DENSE)
+    a = Engine(device=0, trace=True, **kw)
+    b = Engine(device=0, trace=True, **kw)
+    a.prepare_run(20)
+    a.prepare_run(7)
+    total = 0
+    for k in (20, 7, 20, 5, 3, 11, 7, 20, 2, 9):
+        if k == 9:
+            assert a.run_timed(k) >= 0.0
+        else:
+            a.run(k)
+        total += k
+    for _ in range(total):
+        b.step()
+    assert (a.digests() == b.digests()).all()
+    assert a.counters() == b.counters()
+
+
 def test_larger_groups_digest_parity(gpu_available):
     """Larger population, compared on digests every 25 rounds."""
     kw = dict(C4, n_groups=2000)

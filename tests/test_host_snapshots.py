@@ -28,12 +28,16 @@ CASES = {
 }
 
 
-def run_host_snapshots(eng, ref, rounds, seed=3, every=12, overhead=3, skip=(), density=0.15):
+def run_host_snapshots(eng, ref, rounds, seed=3, every=12, overhead=3, skip=(), density=0.15,
+                       ready=0.0):
     """Lockstep with host input and a snapshot worker: a replica whose applied
     index passed its last snapshot by `every` entries snapshots there (term from
     the oracle's log, the host's LogDB), and some rounds later asks for a
-    compaction to index - `overhead`.  Returns (snapshots saved, compactions,
-    snapshots restored from InstallSnapshot)."""
+    compaction to index - `overhead`.  With `ready` > 0 the apply queue fills
+    and drains too (rbe_set_apply_ready, sometimes twice for one replica in a
+    step: the last call wins), so one step's input can hold an applied index,
+    a ready flag, a snapshot and a compaction for the same replica.  Returns
+    (snapshots saved, compactions, snapshots restored from InstallSnapshot)."""
     rng = random.Random(seed)
     n = eng.cfg.n_replicas
     n_rep = eng.n_rep
@@ -43,7 +47,10 @@ def run_host_snapshots(eng, ref, rounds, seed=3, every=12, overhead=3, skip=(), 
     saved = compacted = restored = 0
     for rnd in range(rounds):
         views = ref.views()
-        ops = plan_round(rng, n_rep, n, rnd, views, True, density, applied)
+        ops = plan_round(rng, n_rep, n, rnd, views, True, density, applied, ready=ready)
+        if ready:  # a second, later apply-queue report for some replicas
+            ops += [("ready", r, rng.random() < 0.5) for kind, r, _ in list(ops)
+                    if kind == "ready" and rng.random() < 0.3]
         apply_engine(eng, ops)
         apply_oracle(ref, ops)
         if rnd >= 30:
@@ -99,6 +106,17 @@ def test_host_driven_snapshots_untraced():
     ref = O.Harness(**kw)
     run_host_snapshots(eng, ref, 200, skip=("digest",))
     assert eng.faults()[0] == 0
+
+
+def test_host_driven_snapshots_apply_queue():
+    """Applied indexes, apply-queue flags (twice for some replicas), snapshots
+    and compactions for the same replicas in one step's input."""
+    kw = CASES["C3_HOT"]
+    eng = SoaCpu(trace=True, **kw, **DRIVE)
+    ref = O.Harness(**kw)
+    saved, compacted, _ = run_host_snapshots(eng, ref, 200, ready=0.5)
+    assert eng.faults()[0] == 0
+    assert saved > 10 and compacted > 5, (saved, compacted)
 
 
 def test_host_snapshot_checks():
