@@ -88,7 +88,7 @@ __global__ __launch_bounds__(kBlock) void k_ext_scatter(Planes P, u32 nrep, cons
   // rbe_commit records (one per replica, so lanes never share a row)
   if (i < nc)
     commit_update(P, C, cr[i].r, cr[i].stable_log_to, cr[i].stable_log_term, cr[i].processed,
-                  cr[i].last_applied);
+                  cr[i].last_applied, cr[i].stable_snapshot_to);
   // rbe_snapshot_saved / rbe_compact records (one per replica)
   if (i < ns) snap_rec_apply(P, sr[i]);
 }
@@ -434,6 +434,24 @@ __global__ __launch_bounds__(kBlock) void k_relaunch(Planes P, Params C, const L
   P.gwake[x.replica / N] = GW_AWAKE;
 }
 
+// rbe_replace_node: whether slot (replica % N) is still referenced in its
+// group (rbe_step.h slot_referenced), then the new node in the slot
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_replace_check(Planes P, Params C, const u64* reps,
+                                                          u64 n, u32 round, u32* out) {
+  const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  out[i] = slot_referenced<N>(P, C, reps[i] / N, (u32)(reps[i] % N), round) ? 1u : 0u;
+}
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_join(Planes P, Params C, const u64* reps, u64 n,
+                                                 u32 ppar, u32 tclk) {
+  const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  join_replica<N>(P, C, reps[i], ppar, tclk);
+  P.gwake[reps[i] / N] = GW_AWAKE;
+}
+
 // the lowest live payload-heap position (rbe_host.h heap_low_group): one lane
 // per group, a wave minimum, one 64-bit atomicMin per wave
 template <int N>
@@ -736,11 +754,11 @@ static int make_params(const rbe_config* cfg, Params* out) {
   // engine's own (processed) only without ext_apply
   // With ext_apply the host's state machine is snapshotted by the host's
   // snapshot worker, which tells the engine (rbe_snapshot_saved, rbe_compact);
-  // the engine then never snapshots by itself.  Not with ext_commit (a
-  // snapshot's UpdateCommit.StableSnapshotTo is not carried).
+  // the engine then never snapshots by itself.  With ext_commit a restored
+  // snapshot stays in every Update until the host's UpdateCommit names it
+  // (StableSnapshotTo; SnapSt::upd_ss).
   C.snapshot_entries = cfg->snapshot_entries;
   C.compaction_overhead = cfg->compaction_overhead;
-  if (C.snapshot_entries && C.ext_commit) return RBE_E_INVALID;
   // the compaction of a snapshot at index i reads Term(i - CompactionOverhead),
   // which must still be in the in-memory window
   if (C.snapshot_entries && C.compaction_overhead >= C.ring) return RBE_E_INVALID;
@@ -1492,7 +1510,28 @@ int rbe_apply_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica,
                             const uint64_t* node_id, const uint32_t* type) {
   if (!e) return RBE_E_INVALID;
   if (!e->C.membership || !e->C.ext_apply) return RBE_E_STATE;
-  return e->hin.apply_config_change(n, replica, node_id, type, false);
+  // raft's membership of each replica now, for the check that no node lands
+  // in two of raft's maps (HostInputs::apply_config_change)
+  std::vector<u32> ms(n);
+  if (n && replica) {
+    for (u64 i = 0; i < n; i++)
+      if (replica[i] >= e->C.n_rep) return RBE_E_INVALID;
+    HIP_OK(hipSetDevice(e->device));
+    std::vector<Core> c(n);
+    std::vector<u16> ro(n);
+    for (u64 i = 0; i < n; i++) {
+      HIP_OK(hipMemcpyAsync(&c[i], e->P.core + replica[i], sizeof(Core), hipMemcpyDeviceToHost,
+                            e->stream));
+      HIP_OK(hipMemcpyAsync(&ro[i], e->P.roles + replica[i], sizeof(u16), hipMemcpyDeviceToHost,
+                            e->stream));
+    }
+    HIP_OK(hipStreamSynchronize(e->stream));
+    for (u64 i = 0; i < n; i++) {
+      const u32 x = (c[i].mflags & MB_ROLES) ? ro[i] : 0u;  // Planes::roles valid with MB_ROLES
+      ms[i] = pack_ms(c[i].members & MB_REMOVED, x & 0xFFu, x >> 8);
+    }
+  }
+  return e->hin.apply_config_change(n, replica, node_id, type, false, ms.data());
 }
 
 int rbe_reject_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica) {
@@ -1532,6 +1571,73 @@ int rbe_set_node_ids(rbe_engine* e, uint64_t first_group, uint64_t count, const 
   HIP_OK(hipStreamSynchronize(e->stream));
   drop_graphs(e);  // kernels take the planes by value: a captured graph holds the old ones
   return RBE_OK;
+}
+
+int rbe_replace_node(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint64_t* node_id) {
+  if (!e) return RBE_E_INVALID;
+  int rc = e->hin.replace_args(n, replica, node_id);
+  if (rc) return rc;
+  // the check reads every replica of the group: group-per-GPU only; and the
+  // seeded schedules name slots, not nodes
+  if (!e->C.membership || e->C.rep_world > 1 || e->C.cc_period || e->C.xfer_period)
+    return RBE_E_STATE;
+  if (n == 0) return RBE_OK;
+  HIP_OK(hipSetDevice(e->device));
+  u64* d = nullptr;
+  HIP_OK(hipMalloc((void**)&d, n * sizeof(u64) + n * sizeof(u32)));
+  u32* dref = (u32*)(d + n);
+  std::vector<u32> refd(n);
+  HIP_OK(hipMemcpyAsync(d, replica, n * sizeof(u64), hipMemcpyHostToDevice, e->stream));
+  rc = dispatch_n(e->C.n, [&](auto NN) {
+    constexpr int N = decltype(NN)::value;
+    hipLaunchKernelGGL(k_replace_check<N>, dim3(grid_for(n)), dim3(kBlock), 0, e->stream, e->P,
+                       e->C, (const u64*)d, (u64)n, e->round, dref);
+    HIP_OK(hipGetLastError());
+    return RBE_OK;
+  });
+  if (!rc) {
+    HIP_OK(hipMemcpyAsync(refd.data(), dref, n * sizeof(u32), hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    for (u64 i = 0; i < n && !rc; i++)
+      if (refd[i]) rc = RBE_E_STATE;
+  }
+  if (rc) {
+    HIP_IGNORE(hipFree(d));
+    return rc;
+  }
+  for (u64 i = 0; i < n; i++) e->hin.assign_node(e->C.n_groups, replica[i], node_id[i]);
+  const u64 bytes = e->hin.ids.size() * sizeof(u64);
+  if (!e->P.node_ids) {
+    u64* t = nullptr;
+    if (hipMalloc(&t, bytes) != hipSuccess) {
+      HIP_IGNORE(hipFree(d));
+      return RBE_E_NOMEM;
+    }
+    e->allocs.push_back(t);
+    e->P.node_ids = t;
+    drop_graphs(e);  // kernels take the planes by value
+    HIP_OK(hipMemcpyAsync((void*)e->P.node_ids, e->hin.ids.data(), bytes, hipMemcpyHostToDevice,
+                          e->stream));
+  } else {
+    for (u64 i = 0; i < n; i++)
+      HIP_OK(hipMemcpyAsync((void*)(e->P.node_ids + replica[i]), &e->hin.ids[replica[i]],
+                            sizeof(u64), hipMemcpyHostToDevice, e->stream));
+  }
+  const u32 ppar = (e->round & 1u) ^ 1u;
+  rc = dispatch_n(e->C.n, [&](auto NN) {
+    constexpr int N = decltype(NN)::value;
+    hipLaunchKernelGGL(k_join<N>, dim3(grid_for(n)), dim3(kBlock), 0, e->stream, e->P, e->C,
+                       (const u64*)d, (u64)n, ppar, e->tclk);
+    HIP_OK(hipGetLastError());
+    return RBE_OK;
+  });
+  // the next round scans every group (group sleep: the new node's group is awake)
+  e->scan_at = e->round;
+  HIP_OK(hipMemcpyAsync((void*)e->L.scan_round, &e->scan_at, sizeof(u32), hipMemcpyHostToDevice,
+                        e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  HIP_IGNORE(hipFree(d));
+  return rc;
 }
 
 int rbe_restore_remotes(rbe_engine* e, uint64_t n, const uint64_t* replica,
@@ -1898,8 +2004,10 @@ int rbe_get_update_commits(rbe_engine* e, uint64_t first, uint64_t count, rbe_up
   if (rc) return rc;
   std::vector<Core> core(count);
   std::vector<u64> app(count);
+  std::vector<SnapSt> snp(e->C.snapshot_entries ? count : 0);
   if (d2h(e, core.data(), e->P.core + first, count) || d2h(e, app.data(), e->P.applied + first, count))
     return RBE_E_HIP;
+  if (!snp.empty() && d2h(e, snp.data(), e->P.snp + first, count)) return RBE_E_HIP;
   HIP_OK(hipStreamSynchronize(e->stream));
   for (u64 i = 0; i < count; i++) {
     const u64 r = first + i;
@@ -1912,7 +2020,7 @@ int rbe_get_update_commits(rbe_engine* e, uint64_t first, uint64_t count, rbe_up
         trc = RBE_E_HIP;
       return t;
     };
-    update_commit_view(u[i], app[i], term_of, out[i]);
+    update_commit_view(u[i], app[i], snp.empty() ? 0 : snp[i].marker, term_of, out[i]);
     if (trc) return trc;
   }
   return RBE_OK;
@@ -1922,6 +2030,21 @@ int rbe_commit(rbe_engine* e, uint64_t n, const uint64_t* replica, const rbe_upd
   if (!e) return RBE_E_INVALID;
   if (!e->C.ext_commit) return RBE_E_STATE;
   return e->hin.commit(n, replica, uc);
+}
+
+int rbe_get_update_snapshots(rbe_engine* e, uint64_t first, uint64_t count, uint64_t* out4) {
+  if (!e || !out4 || first + count > e->C.n_rep || count == 0) return RBE_E_INVALID;
+  std::vector<rbe_update> u(count);
+  int rc = rbe_get_updates(e, first, count, u.data());
+  if (rc) return rc;
+  std::vector<SnapSt> snp(e->C.snapshot_entries ? count : 0);
+  if (!snp.empty()) {
+    if (d2h(e, snp.data(), e->P.snp + first, count)) return RBE_E_HIP;
+    HIP_OK(hipStreamSynchronize(e->stream));
+  }
+  for (u64 i = 0; i < count; i++)
+    update_snapshot_row(u[i], snp.empty() ? nullptr : &snp[i], out4 + 4 * i);
+  return RBE_OK;
 }
 
 int rbe_get_snapshot_state(rbe_engine* e, uint64_t first, uint64_t count, uint64_t* out8) {

@@ -554,7 +554,7 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, CT& ctr, FastOut<N, TR
                   (send_q ? UF_SENT_QUIESCE : 0u) | (ranges ? UF_RANGES : 0u));
   u.events = (u16)o.events;
   u.round = o.round_;
-  u.pad1 = 0;
+  u.cc_acc = 0;
 #ifndef RBE_DIAG_NO_STATE_STORES
   if constexpr ((STG & STG_OUT) != 0) sr->upd = u;
   else if (ranges) P.upd[r] = u;

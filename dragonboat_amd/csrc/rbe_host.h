@@ -293,16 +293,20 @@ RBE_HD void update_ids(rbe_update& u, const u64* ids, u32 n, u64 g) {
 // getUpdateCommit (peer.go:410-427) of an rbe_update: `applied` is the
 // applied index the step ran with (GetUpdate's lastApplied), `term_of(i)` the
 // term of log entry i (the last EntriesToSave entry)
+// `snap_index`: the index of the Update's Snapshot (RBE_UF_SNAPSHOT), else 0
 template <typename TermFn>
-inline void update_commit_view(const rbe_update& u, u64 applied, TermFn&& term_of,
+inline void update_commit_view(const rbe_update& u, u64 applied, u64 snap_index, TermFn&& term_of,
                                rbe_update_commit& o) {
   memset(&o, 0, sizeof(o));
   if (!(u.flags & RBE_UF_HAS_UPDATE)) return;
   o.ready_to_read = u.n_ready_to_read;
   o.last_applied = applied;
-  if (u.apply_lo <= u.apply_hi) o.processed = u.apply_hi;
-  if (u.save_lo <= u.save_hi) {
-    o.stable_log_to = u.save_hi;
+  u64 stable_log_to = 0;
+  update_commit(u.save_lo, u.save_hi, u.apply_lo, u.apply_hi,
+                (u.flags & RBE_UF_SNAPSHOT) ? snap_index : 0, &o.processed, &stable_log_to,
+                &o.stable_snapshot_to);
+  if (stable_log_to) {
+    o.stable_log_to = stable_log_to;
     o.stable_log_term = term_of(u.save_hi);
   }
 }
@@ -310,7 +314,7 @@ inline void update_commit_view(const rbe_update& u, u64 applied, TermFn&& term_o
 // One staged rbe_commit (Peer.Commit's log part, ext_commit mode); applied by
 // commit_update (rbe_step.h) in k_ext_scatter / HostInputs::apply_host.
 struct CommitRec {
-  u64 r, stable_log_to, stable_log_term, processed, last_applied;
+  u64 r, stable_log_to, stable_log_term, processed, last_applied, stable_snapshot_to;
 };
 
 // The lowest payload-heap position the replicas of group g that this engine
@@ -367,6 +371,16 @@ RBE_HD u64 heap_low_group(const Planes& P, const Params& C, u64 g, u32 round) {
 // rbe_get_snapshot_state row: marker, marker term, snapshot index, snapshot
 // term, reqSnapshotIndex, compactLogTo, the snapshot's and the state
 // machine's membership (removed masks)
+// The Snapshot of an Update (rbe_get_update_snapshots): index, term and packed
+// membership of the snapshot a replica restored and holds in memory (it sits
+// at the LogDB marker, SnapSt::upd_*), all zero when the Update carries none
+inline void update_snapshot_row(const rbe_update& u, const SnapSt* s, u64* o) {
+  o[0] = o[1] = o[2] = o[3] = 0;
+  if (!s || !(u.flags & RBE_UF_HAS_UPDATE) || !(u.flags & RBE_UF_SNAPSHOT)) return;
+  o[0] = s->marker;
+  o[1] = s->marker_term;
+  o[2] = pack_ms(s->upd_rem, s->upd_obs, s->upd_wit);
+}
 inline void snap_state_row(const SnapSt& s, u64* o) {
   o[0] = s.marker;
   o[1] = s.marker_term;
@@ -496,18 +510,53 @@ struct HostInputs {
 
   const u64* id_table() const { return ids.empty() ? nullptr : ids.data(); }
   // rbe_set_node_ids: groups [first, first + count), n ids each, non-zero and
-  // ascending within a group (the canonical node order is the slot order)
+  // distinct within a group.  The engine's canonical node order is the slot
+  // order: the reference visits its maps in Go's random order (raft.go:390-402,
+  // 803, 836), so any fixed order is one of its executions; per (sender,
+  // receiver) pair the message streams do not depend on it.
   int set_node_ids(u64 n_groups, u64 first, u64 count, const u64* v) {
     if (first > n_groups || count > n_groups - first || (count && !v)) return RBE_E_INVALID;
     for (u64 i = 0; i < count; i++)
-      for (u32 s = 0; s < n; s++)
-        if (v[i * n + s] == 0 || (s && v[i * n + s] <= v[i * n + s - 1])) return RBE_E_INVALID;
-    if (ids.empty()) {
-      ids.resize(n_groups * n);
-      for (u64 i = 0; i < n_groups * n; i++) ids[i] = i % n + 1;
-    }
+      for (u32 s = 0; s < n; s++) {
+        if (v[i * n + s] == 0) return RBE_E_INVALID;
+        for (u32 t = 0; t < s; t++)
+          if (v[i * n + t] == v[i * n + s]) return RBE_E_INVALID;
+      }
+    ensure_ids(n_groups);
     std::copy(v, v + count * n, ids.begin() + first * n);
     return RBE_OK;
+  }
+  void ensure_ids(u64 n_groups) {
+    if (!ids.empty()) return;
+    ids.resize(n_groups * n);
+    for (u64 i = 0; i < n_groups * n; i++) ids[i] = i % n + 1;
+  }
+  // rbe_replace_node's checks on the host: replica[i] in range, at most one
+  // per group, id[i] non-zero and not the id of another slot of the group, no
+  // input staged for any replica of the group (RBE_E_STATE)
+  int replace_args(u64 cnt, const u64* replica, const u64* id) const {
+    if (cnt && (!replica || !id)) return RBE_E_INVALID;
+    for (u64 i = 0; i < cnt; i++) {
+      if (replica[i] >= n_rep || id[i] == 0) return RBE_E_INVALID;
+      const u64 g = replica[i] / n;
+      for (u64 j = 0; j < i; j++)
+        if (replica[j] / n == g) return RBE_E_STATE;
+      for (u32 s = 0; s < n; s++) {
+        const u64 r = g * n + s;
+        if (r != replica[i] && (ids.empty() ? s + 1 : ids[r]) == id[i]) return RBE_E_INVALID;
+        if (sm[r].slot != ~0u || app_slot[r].applied != ~0u || app_slot[r].ready != ~0u ||
+            committing[r] || snap_slot[r] != ~0u)
+          return RBE_E_STATE;
+      }
+    }
+    return RBE_OK;
+  }
+  // the new node in replica r's slot: its id, and a state machine that has
+  // applied nothing (the host mirror of Planes::applied)
+  void assign_node(u64 n_groups, u64 r, u64 id) {
+    ensure_ids(n_groups);
+    ids[r] = id;
+    applied[r] = 0;
   }
   // node id → internal id (slot + 1) in replica r's group; 0 when no slot has it
   u64 in_id(u64 r, u64 id) const {
@@ -728,13 +777,26 @@ struct HostInputs {
     }
     return RBE_OK;
   }
+  // `ms_now[i]`: replica[i]'s raft membership now (packed, pack_ms), or null.
+  // An AddObserver / AddWitness of another node that is a voter or in the
+  // other set would put one node in two of raft's maps (raft.go:1159-1180
+  // only checks its own map), which a slot cannot hold: RBE_E_INVALID.
   int apply_config_change(u64 cnt, const u64* replica, const u64* node_id, const u32* type,
-                          bool reject) {
+                          bool reject, const u32* ms_now = nullptr) {
     if (cnt && !reject && (!type || !node_id)) return RBE_E_INVALID;
     std::vector<u64> nv(reject ? 0 : cnt);
     for (u64 i = 0; i < cnt && !reject; i++) {  // node id 0 = NoNode
       nv[i] = node_id[i] ? in_id(replica ? replica[i] : ~0ull, node_id[i]) : 0;
       if (type[i] > CC_AddWitness || (node_id[i] && !nv[i])) return RBE_E_INVALID;
+      if (ms_now && nv[i] && nv[i] != replica[i] % n + 1 &&
+          (type[i] == CC_AddObserver || type[i] == CC_AddWitness)) {
+        // the membership the step applies it to: after a staged RestoreRemotes
+        const u32 ms = (staged_flags(replica[i]) & EXT_RESTORE) ? (u32)recs[sm[replica[i]].slot].pad[2]
+                                                                : ms_now[i];
+        const u32 b = 1u << (nv[i] - 1);
+        const bool voter = !(ms & b), obs = (ms >> 8) & b, wit = (ms >> 16) & b;
+        if (voter || (type[i] == CC_AddObserver ? wit : obs)) return RBE_E_INVALID;
+      }
     }
     const u64* node = nv.data();
     int rc = check_replicas(cnt, replica, EXT_CC_APPLY);
@@ -856,14 +918,13 @@ struct HostInputs {
     int rc = check_replicas(cnt, replica, 0);
     if (rc) return rc;
     for (u64 i = 0; i < cnt; i++)
-      if (uc[i].stable_snapshot_to != 0) return RBE_E_INVALID;
-    for (u64 i = 0; i < cnt; i++)
       if (committing[replica[i]]) return RBE_E_STATE;
     if ((rc = unique_replicas(cnt, replica, 0))) return rc;  // within the batch too
     for (u64 i = 0; i < cnt; i++) {
       committing[replica[i]] = 1;
       commits.push_back(CommitRec{replica[i], uc[i].stable_log_to, uc[i].stable_log_term,
-                                  uc[i].processed, uc[i].last_applied});
+                                  uc[i].processed, uc[i].last_applied,
+                                  uc[i].stable_snapshot_to});
     }
     return RBE_OK;
   }
@@ -881,7 +942,8 @@ struct HostInputs {
     for (size_t i = 0; i < ents.size(); i++) P.in_ents[i] = ents[i];
     for (size_t i = 0; i < app_rep.size(); i++) apply_pair(P, app_rep[i], app_val[i]);
     for (const CommitRec& c : commits)
-      commit_update(P, C_, c.r, c.stable_log_to, c.stable_log_term, c.processed, c.last_applied);
+      commit_update(P, C_, c.r, c.stable_log_to, c.stable_log_term, c.processed, c.last_applied,
+                    c.stable_snapshot_to);
     for (const SnapRec& x : snaps) snap_rec_apply(P, x);
   }
 };

@@ -346,10 +346,13 @@ RBE_HD void update_commit(u64 save_lo, u64 save_hi, u64 apply_lo, u64 apply_hi, 
 // then inMemory.appliedLogTo (139-167).  `imark` is inMemory.markerIndex; the
 // in-memory log holds [imark, last_index] (empty when imark > last_index).
 // A reference panic sets F_PANIC in the sticky fault word and changes nothing
-// further.  stable_snapshot_to has nothing to clear: snapshots are not carried
-// with ext_commit.  Returns the fault bits raised.
+// further.  stable_snapshot_to clears the snapshot the Updates carry
+// (savedSnapshotTo, inmemory.go:168-176) when it names that snapshot; another
+// index only logs a warning in the reference and changes nothing here.
+// Returns the fault bits raised.
 RBE_HD u32 commit_update(const Planes& P, const Params& C, u64 r, u64 stable_log_to,
-                         u64 stable_log_term, u64 processed, u64 last_applied) {
+                         u64 stable_log_term, u64 processed, u64 last_applied,
+                         u64 stable_snapshot_to) {
   Core c = P.core[r];
   u64 mark = P.imark[r];
   u32 fault = 0;
@@ -361,6 +364,10 @@ RBE_HD u32 commit_update(const Planes& P, const Params& C, u64 r, u64 stable_log
       else t = P.term_ring[(stable_log_to & (u64)(C.ring - 1)) * C.n_rep + r];
     }
     if (!fault && t == stable_log_term) c.saved_to = stable_log_to;
+  }
+  if (!fault && stable_snapshot_to > 0 && C.snapshot_entries) {
+    SnapSt& sp = P.snp[r];
+    if (sp.upd_ss && sp.marker == stable_snapshot_to) sp.upd_ss = 0;
   }
   if (!fault && processed > 0) {
     if (processed < c.processed || processed > c.committed) fault |= F_PANIC;
@@ -575,6 +582,10 @@ struct Lane {
   u64 lead_start;  // leader: index of its no-op (Core::lead_start)
   u8 vote, leader, ltt, rq_head, rq_count;
   u8 members, cc_apply;  // Core::members / cc_apply (membership)
+  u32 cc_acc;            // ConfigChanges the state machine accepted this step (Upd::cc_acc)
+  u64 cc_i, cc_e;        // CCA_MULTI: the last step's apply range being handed to raft
+  u32 cc_bits, cc_n;     //   its accepted bits, ConfigChanges passed so far
+  bool cc_scan;
   u8 mfl;                // Core::mflags (MB_ROLES | MB_CC_IN_LOG)
   u8 obs, wit;           // raft.observers / raft.witnesses (Planes::roles; membership)
   u8 roles0;             // MB_ROLES at load: Planes::roles holds something to rewrite
@@ -1443,12 +1454,18 @@ struct Lane {
       // LogTerm, and the transport reports its outcome to the next step
       if (!ractive(slot)) return;
       const SnapSt& sp = P.snp[r];
-      const u64 si = sp.ss_index;
+      // entryLog.snapshot (logentry.go:248-253): the in-memory snapshot while
+      // the host has not committed it (ext_commit; it sits at the marker), else
+      // the LogDB's latest
+      const bool im = C.ext_commit && sp.upd_ss;
+      const u64 si = im ? marker : sp.ss_index;
       Msg m = mk(M_InstallSnapshot, (u8)(slot + 1));
       m.log_index = si;
-      m.log_term = sp.ss_term;
-      m.pad0 = sp.ss_rem;  // Snapshot.Membership: the slots not in Addresses,
-      m.pad1 = (u32)sp.ss_obs | ((u32)sp.ss_wit << 8);  // its Observers and Witnesses
+      m.log_term = im ? marker_term : sp.ss_term;
+      // Snapshot.Membership: the slots not in Addresses, its Observers and Witnesses
+      m.pad0 = im ? sp.upd_rem : sp.ss_rem;
+      m.pad1 = im ? ((u32)sp.upd_obs | ((u32)sp.upd_wit << 8))
+                  : ((u32)sp.ss_obs | ((u32)sp.ss_wit << 8));
       become_snapshot(slot, si);
       const u32 bit = 1u << slot;
       snp_pend |= (u8)bit;
@@ -1792,11 +1809,17 @@ struct Lane {
         sp.ss_rem = (u8)(m.pad0 & MB_REMOVED);  // and its membership
         sp.ss_obs = (u8)(m.pad1 & 0xFFu);
         sp.ss_wit = (u8)((m.pad1 >> 8) & 0xFFu);
-        if (rl_on()) {  // inMemory.restore (inmemory.go:236-246)
-          P.imark[r] = si + 1;
+        // inMemory.restore (inmemory.go:236-246): the in-memory log starts
+        // after the snapshot, which it holds until a Commit names it
+        if (imark_on(C)) P.imark[r] = si + 1;
+        if (rl_on()) {
           P.rl[r].new_ent = 1;
           P.rl[r].size = 0;
         }
+        sp.upd_ss = (u8)(C.ext_commit ? 1 : 0);
+        sp.upd_rem = sp.ss_rem;
+        sp.upd_obs = sp.ss_obs;
+        sp.upd_wit = sp.ss_wit;
         seg_len = mseg_len = 0;
         snap_restored = true;
         restored = true;
@@ -2314,34 +2337,55 @@ struct Lane {
   }
 
   // ------------------------------------------------------------- membership bookkeeping
+  // A ConfigChange entry of the stand-in form (cc_word) at ring body b: its
+  // type and node id, false when the engine cannot decode it
+  RBE_HD static bool cc_decode(const Body& b, u32* t, u64* nid) {
+    const u64 w = b.lo;
+    *t = (u32)((w >> 48) & 0xFFu);
+    *nid = w & 0xFFFFFFFFFFFFULL;
+    return !(ent_heap(b.type) || b.len != 8 || (w >> 56) != 0xCCu || *t > CC_AddWitness ||
+             *nid > N);
+  }
   // After the step's Update: without ext_apply the engine's state machine
-  // applies the CommittedEntries, and a ConfigChange among them goes back to
-  // raft at the node's next step (cc_apply; the last one of the range: raft
-  // allows one pending config change, and bootstrap's AddNodes are no-ops);
+  // applies the CommittedEntries, and each ConfigChange among them goes back
+  // to raft at the node's next step, in log order (the state machine calls
+  // node.ApplyConfigChange / ConfigChangeProcessed per entry under raftMu,
+  // node.go:217-277, rsm/statemachine.go:951): one in cc_apply, or with
+  // several (a node catching up, e.g. one that joins and replays the group's
+  // history) CCA_MULTI and the accepted ones as bits of Upd::cc_acc (the next
+  // step re-reads them from this range, which stays in the ring until then);
   // MB_CC_IN_LOG is dropped once (processed, last] holds no ConfigChange.
   RBE_HD void membership_after_update(const Upd& u) {
     if (!C.ext_apply && u.apply_hi >= u.apply_lo) {
       u32 ms = pack_ms(members & MB_REMOVED, obs, wit);  // raft's, as accepted changes go by
+      u32 ncc = 0;
       for (u64 i = u.apply_lo; i <= u.apply_hi; i++) {
         if (last - i >= C.ring) break;  // F_WINDOW already raised by the apply
         const Body b = P.pay_ring[ring_slot(i)];
         if (ent_type(b.type) != E_ConfigChange) continue;
-        const u64 w = b.lo;
-        const u32 t = (u32)((w >> 48) & 0xFFu);
-        const u64 nid = w & 0xFFFFFFFFFFFFULL;
-        if (ent_heap(b.type) || b.len != 8 || (w >> 56) != 0xCCu || t > CC_AddWitness || nid > N) {
+        u32 t;
+        u64 nid;
+        if (!cc_decode(b, &t, &nid)) {
           set_fault(F_UNSUPPORTED);  // not a ConfigChange the engine can decode
           continue;
         }
+        if (ncc == 32) {  // more than Upd::cc_acc holds
+          set_fault(F_UNSUPPORTED);
+          break;
+        }
         if (!cc_accepted(ms, t, nid, N)) {
           cc_apply = (u8)(CCA_VALID | CCA_REJECT);
+          ncc++;
           continue;
         }
         cc_apply = (u8)(CCA_VALID | (t << 3) | (u32)nid);
+        cc_acc |= 1u << ncc;
+        ncc++;
         ms_apply(ms, t, nid, N);
         // the state machine's own membership, which the next snapshot records
         ms_apply(sm_ms, t, nid, N);
       }
+      if (ncc > 1) cc_apply = (u8)(CCA_VALID | CCA_MULTI);
     }
     if (mfl & MB_CC_IN_LOG) {
       bool any = false;
@@ -2373,7 +2417,11 @@ struct Lane {
     sp.rr_pend = (u8)(snap_restored && C.membership && !C.ext_apply ? 1 : 0);
     sp.marker = marker;
     sp.marker_term = marker_term;
-    if (sp.compact_to) {
+    // (with ext_commit a compaction waits while the Updates carry a restored
+    // snapshot the host has not committed: the node runs compactLog before
+    // that Commit within one step, node.go:975-999, so the log's first index
+    // never moves past a snapshot it still holds in memory)
+    if (sp.compact_to && !sp.upd_ss) {
       // LogDB.Compact inside (marker, lastIndex], never past its snapshot
       const u64 c = sp.compact_to;
       if (c > marker && c <= last && c <= sp.ss_index) {
@@ -2405,7 +2453,7 @@ struct Lane {
     P.snp[r] = sp;
     marker = sp.marker;
     marker_term = sp.marker_term;
-    if (sp.compact_to || sp.pend || sp.rr_pend) flags |= HF_SNAP_WORK;
+    if (sp.compact_to || sp.pend || sp.rr_pend || sp.upd_ss) flags |= HF_SNAP_WORK;
     else flags &= (u8)~HF_SNAP_WORK;
   }
 
@@ -2439,6 +2487,8 @@ struct Lane {
     rq_count = c.rq_count;
     members = c.members;
     cc_apply = c.cc_apply;
+    cc_acc = 0;
+    cc_scan = false;
     mfl = c.mflags;
     roles0 = (u8)(mfl & MB_ROLES);
     obs = wit = 0;
@@ -2702,6 +2752,43 @@ struct Lane {
         m = mk(M_SnapshotReceived, self);
         m.hint = restore & 0xFFFFFFu;
         kind = 2;
+      } else if (phase == 8 && (cc_apply & CCA_MULTI)) {
+        // the ConfigChanges of the last step's apply range, one per pass, in
+        // log order: rejected, or applied (node id 0: only
+        // clearPendingConfigChange); the range is still in the ring
+        if (!cc_scan) {
+          const Upd pu = P.upd[r];
+          cc_i = pu.apply_lo;
+          cc_e = pu.apply_hi;
+          cc_bits = pu.cc_acc;
+          cc_n = 0;
+          cc_scan = true;
+        }
+#pragma unroll 1
+        while (kind == 0 && cc_i <= cc_e && last - cc_i < C.ring) {
+          const Body b = P.pay_ring[ring_slot(cc_i++)];
+          u32 t;
+          u64 nid;
+          if (ent_type(b.type) != E_ConfigChange || !cc_decode(b, &t, &nid)) continue;
+          const bool ok = (cc_bits >> cc_n) & 1u;
+          cc_n++;
+          if (ok && nid == 0) {
+            flags &= (u8)~HF_PENDING_CC;  // ApplyConfigChange(NoNode): clearPendingConfigChange
+            continue;
+          }
+          m = mk(M_ConfigChangeEvent, self);
+          if (ok) {
+            m.hint = nid;
+            m.hint_high = t;
+          } else {
+            m.reject = 1;
+          }
+          kind = 2;
+        }
+        if (kind == 0) {
+          cc_apply = 0;
+          phase = phase0;
+        }
       } else if (phase == 8) {
         phase = phase0;
         const u8 a = cc_apply;
@@ -2715,7 +2802,7 @@ struct Lane {
         } else {
           m = mk(M_ConfigChangeEvent, self);
           m.hint = a & 7u;
-          m.hint_high = (a >> 3) & 7u;
+          m.hint_high = (a >> 3) & 3u;
           kind = 2;
         }
       }
@@ -3026,13 +3113,17 @@ struct Lane {
     u.n_drop_ent = (u16)n_drop_ent;
     u.n_drop_ri = (u16)n_drop_ri;
     u.fault = fault;
+    // Update.Snapshot (peer.go:345-347): restored in this step, or still held
+    // in memory because the host has not committed it (ext_commit)
+    const bool snap_carried =
+        snap_restored || (C.ext_commit && C.snapshot_entries && P.snp[r].upd_ss);
     u.flags = (u16)((term != term0 || vote != vote0 || committed != committed0 ? UF_STATE_CHANGED
                                                                                 : 0u) |
-                    (send_q ? UF_SENT_QUIESCE : 0u) | (snap_restored ? UF_SNAPSHOT : 0u) |
+                    (send_q ? UF_SENT_QUIESCE : 0u) | (snap_carried ? UF_SNAPSHOT : 0u) |
                     (ext_applied ? UF_APPLIED : 0u) | UF_RANGES);
     u.events = (u16)(events | (leader != leader0 ? EV_LEADER_UPDATED : 0u));
     u.round = round;
-    u.pad1 = 0;
+    u.cc_acc = cc_acc;
     P.upd[r] = u;
     // this round's outbox header: the count word of every destination list
     {
@@ -3086,12 +3177,14 @@ RBE_HD u32 boot_removed(const Params& C, u32 k) {
 // (config.IsObserver / IsWitness: newRaft's becomeObserver / becomeWitness,
 // raft.go:274-281, and no becomeFollower(1), peer.go:71-73) stays at term 0
 // with its one randomized timeout.
+// `join`: the replica is a node that joins now whatever its slot (a node
+// replacing a removed one, rbe_replace_node).
 template <int N>
-RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
+RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r, bool join = false) {
   const u32 k = (u32)(r % N);
   const u64 cid = cid_of(C, r / N);
   const u64 self = k + 1;
-  const bool boot = k < C.n_voters;
+  const bool boot = k < C.n_voters && !join;
   const u32 V = boot ? C.n_voters : 0u;  // bootstrap entries in this replica's log
   const bool nv = ((C.obs_slots | C.wit_slots) >> k) & 1u;  // a non-voting start
   Hot h;
@@ -3122,9 +3215,11 @@ RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   c.lead_start = 0;
   // the bootstrap ConfigChanges, applied in round 0; the slots outside the
   // replica's initial membership
+  const u32 rem0 = boot ? boot_removed(C, k) : (1u << N) - 1u;
   if (C.membership) {
-    c.members = (u8)boot_removed(C, k);
+    c.members = (u8)rem0;
     c.mflags = boot ? MB_CC_IN_LOG : 0u;
+    P.roles[r] = 0;
   }
   P.core[r] = c;
   if (imark_on(C)) P.imark[r] = 1;  // inMemory.init(0), then bootstrap appends 1..V
@@ -3136,7 +3231,7 @@ RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   }
   if (C.snapshot_entries) {  // the LogDB's membership before any snapshot: the bootstrap's
     SnapSt sp = {};
-    sp.ss_rem = sp.sm_rem = (u8)boot_removed(C, k);
+    sp.ss_rem = sp.sm_rem = (u8)rem0;
     P.snp[r] = sp;
   }
   for (u32 s = 0; s < N; s++) {
@@ -3167,7 +3262,7 @@ RBE_HD void launch_replica(const Planes& P, const Params& C, u64 r) {
   u.flags = UF_RANGES;
   u.events = 0;
   u.round = ~0u;
-  u.pad1 = 0;
+  u.cc_acc = 0;
   P.upd[r] = u;
 }
 
@@ -3207,6 +3302,7 @@ RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, 
     sp.ss_obs = sp.sm_obs = (u8)((removed >> 8) & 0xFFu);
     sp.ss_wit = sp.sm_wit = (u8)((removed >> 16) & 0xFFu);
     sp.rr_pend = 0;
+    sp.upd_ss = 0;  // a new Peer's in-memory log holds no snapshot
     if (sp.compact_to || sp.pend) snap_flags |= HF_SNAP_WORK;
     if (ss_index && !C.ext_apply) snap_flags |= HF_APPLIED_NEW;  // recovered: confirmedIndex 0 lags it
     // Term(marker) for the steps' log lookups (the ring slot is free: the
@@ -3282,6 +3378,64 @@ RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, 
   P.cnt[ppar][r].stamp = 0;
   for (u32 s = 0; s < N; s++)
     if (s != k) P.cnt[ppar][g * N + s].w[cnt_widx(k, s)] = 0;
+}
+
+// A new node takes slot k of group g (rbe_replace_node): the node that held
+// the slot was removed from the group (raft.go:1212-1237 removeNode at every
+// replica) and another node id joins in its place, started as dragonboat starts
+// a node that joins a running cluster (node.go:280-292: no peers, an empty
+// LogDB, Launch with newNode, peer.go:64-86) in the slot's configured kind.
+// Its quiesce manager is fresh on the tick clock (as relaunch_replica), the
+// messages still addressed to the slot are dropped (none comes from it:
+// slot_referenced), and its Update record starts over.
+template <int N>
+RBE_HD void join_replica(const Planes& P, const Params& C, u64 r, u32 ppar, u32 tclk) {
+  launch_replica<N>(P, C, r, true);
+  Hot& h = P.hot[r];
+  const u32 q0 = C.quiesce ? tclk : 0u;
+  h.q_tick = h.q_no_activity_since = h.q_exit_quiesce_tick = q0;
+  h.q_quiesced_since = 0;
+  if (C.ext_apply) P.applied[r] = 0;
+  const u32 k = (u32)(r % N);
+  const u64 g = r / N;
+  P.cnt[ppar][r].stamp = 0;
+  for (u32 s = 0; s < N; s++)
+    if (s != k) P.cnt[ppar][g * N + s].w[cnt_widx(k, s)] = 0;
+}
+
+// Whether anything in group g other than slot s's own replica still refers to
+// the node in slot s, so a new node id there would not be a new node to the
+// others: a replica that holds it in raft.remotes / observers / witnesses, as
+// its vote, leader or leader-transfer target, in an ongoing vote tally, as the
+// sender or a confirmer of a queued ReadIndex or in the rate limiter's
+// follower reports; or a
+// message it sent in the last round (read by the round about to run).  Once
+// every replica applied the RemoveNode and the group moved on (a new term
+// clears votes and tallies), none does.
+template <int N>
+RBE_HD bool slot_referenced(const Planes& P, const Params& C, u64 g, u32 s, u32 round) {
+  const u8 id = (u8)(s + 1);
+  for (u32 j = 0; j < N; j++) {
+    if (j == s) continue;
+    const u64 r = g * N + j;
+    const Core c = P.core[r];
+    if (!((c.members >> s) & 1u)) return true;
+    if (C.membership && ((P.roles[r] >> s) & 0x101u)) return true;
+    if (c.vote == id || c.leader == id || c.ltt == id) return true;
+    const Hot h = P.hot[r];
+    if (((h.votes_resp | h.votes_granted) >> s) & 1u) return true;
+    for (u32 q = 0; q < c.rq_count; q++) {
+      const ReadReq& x = P.rq[r * C.rq_cap + (c.rq_head + q) % C.rq_cap];
+      if (x.from == id || ((x.confirmed >> s) & 1u)) return true;
+    }
+    if (rl_enabled(C.rl_max) && ((P.rl[r].fmask >> s) & 1u)) return true;
+  }
+  if (round > 0) {
+    const CntRow row = P.cnt[(round & 1u) ^ 1u][g * N + s];
+    for (u32 d = 0; d < N; d++)
+      if (d != s && row_word(row, d, s, round)) return true;
+  }
+  return false;
 }
 
 // ------------------------------------------------------------------ triage

@@ -94,7 +94,8 @@ enum : u8 {
   MB_REMOVED = 0x7F,   // members: slots that are not in raft.remotes (bit s = slot s, kMaxN = 7)
   MB_ROLES = 0x01,     // mflags: some slot is an observer or a witness (Planes::roles)
   MB_CC_IN_LOG = 0x02, // mflags: a ConfigChange entry may sit in (processed, last_index]
-  CCA_VALID = 0x80, CCA_REJECT = 0x40,  // cc_apply: node id bits 0-2, ConfigChangeType bits 3-5
+  CCA_VALID = 0x80, CCA_REJECT = 0x40,  // cc_apply: node id bits 0-2, ConfigChangeType bits 3-4
+  CCA_MULTI = 0x20,  // cc_apply: several ConfigChanges, in the last step's apply range (Upd::cc_acc)
 };
 // pb.ConfigChangeType (raft.pb.go)
 enum : u32 { CC_AddNode = 0, CC_RemoveNode = 1, CC_AddObserver = 2, CC_AddWitness = 3 };
@@ -149,7 +150,14 @@ struct alignas(16) SnapSt {
   // observers / witnesses of the snapshot's and the state machine's membership
   // (Membership.Observers / Witnesses, bit s = slot s)
   u8 ss_obs, ss_wit, sm_obs, sm_wit;
-  u8 pad[7];
+  // the snapshot restored from the last InstallSnapshot (inMemory.snapshot,
+  // inmemory.go:236-246): its membership, and with ext_commit upd_ss = the
+  // host has not yet committed an Update carrying it (savedSnapshotTo,
+  // inmemory.go:168-176), so every Update carries it again.  Its index and term
+  // are marker / marker_term: the LogDB took it (ApplySnapshot) and a
+  // compaction waits until the host has committed it (node_snapshot)
+  u8 upd_ss, upd_rem, upd_obs, upd_wit;
+  u8 pad[3];
 };
 
 // remote slot (remote.go:62-69): match/next; state|active<<2 lives in a u8 plane
@@ -221,7 +229,8 @@ struct alignas(16) Upd {
   u64 apply_hi;
   u16 n_drop_ent;   // DroppedEntries
   u16 n_drop_ri;    // DroppedReadIndexes
-  u32 pad1;
+  u32 cc_acc;       // membership: bit i = the i-th ConfigChange of the apply range was
+                    // accepted by the engine's state machine (Core::cc_apply CCA_MULTI)
   u32 fault;        // sticky F_* bits
   u16 flags;        // UF_* bits
   u16 events;       // EV_* bits: IRaftEventListener calls of the step
@@ -231,8 +240,9 @@ struct alignas(16) Upd {
 };
 enum : u32 {
   UF_STATE_CHANGED = 1, UF_SENT_QUIESCE = 2, UF_HAS_UPDATE = 4,
-  UF_SNAPSHOT = 0x20,  // the step restored a snapshot from InstallSnapshot: Update.Snapshot is
-                       // SnapSt::ss_index / ss_term (the state machine recovers from it);
+  UF_SNAPSHOT = 0x20,  // Update.Snapshot: the step restored a snapshot from InstallSnapshot
+                       // (or, with ext_commit, one the host has not committed yet): index /
+                       // term SnapSt::marker / marker_term, membership SnapSt::upd_*;
                        // the same bit as RBE_UF_SNAPSHOT
   UF_APPLIED = 0x40,   // ext_apply: the state machine's applied index changed for this step,
                        // so the node takes an Update even without other content (node.go:

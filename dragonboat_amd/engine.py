@@ -220,7 +220,7 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_xchg_chunk_bytes", "rbe_xchg_pack_fixed", "rbe_xchg_unpack_fixed",
            "rbe_xchg_status", "rbe_stream", "rbe_get_snapshot_state", "rbe_wire_encode",
            "rbe_wire_fetch", "rbe_wire_decode", "rbe_wire_ingest", "rbe_iso_leaders", "rbe_set_iso_leaders", "rbe_local_groups", "rbe_propose_entries", "rbe_commit",
-           "rbe_get_update_commits", "rbe_propose_config_change", "rbe_apply_config_change",
+           "rbe_get_update_commits", "rbe_get_update_snapshots", "rbe_replace_node", "rbe_propose_config_change", "rbe_apply_config_change",
            "rbe_reject_config_change", "rbe_rate_limited", "rbe_restore_remotes",
            "rbe_snapshot_saved", "rbe_compact", "rbe_set_node_ids", "rbe_collect_step"]
 KERNEL_SLOTS = 4
@@ -270,7 +270,9 @@ def load_library(path: Optional[str] = None):
         "rbe_snapshot_saved": (i32, [vp, u64, P(u64), P(u64), P(u64), P(u32)]),
         "rbe_compact": (i32, [vp, u64, P(u64), P(u64)]),
         "rbe_set_node_ids": (i32, [vp, u64, u64, P(u64)]),
+        "rbe_replace_node": (i32, [vp, u64, P(u64), P(u64)]),
         "rbe_get_update_commits": (i32, [vp, u64, u64, P(RbeUpdateCommit)]),
+        "rbe_get_update_snapshots": (i32, [vp, u64, u64, P(u64)]),
         "rbe_run": (i32, [vp, u32]),
         "rbe_sync": (i32, [vp]),
         "rbe_round": (i32, [vp, P(u32)]),
@@ -608,10 +610,16 @@ class NodeInputs:
 
     def set_node_ids(self, first_group, ids):
         """rbe_set_node_ids: the node ids of groups first_group.. (a list of
-        n_replicas-long ascending id lists), before the first step."""
+        n_replicas-long lists of distinct ids), before the first step."""
         flat = [x for row in ids for x in row]
         _check_input(self._input("set_node_ids", first_group, len(ids), _u64s(flat)),
                      "rbe_set_node_ids")
+
+    def replace_node(self, replicas, node_ids):
+        """rbe_replace_node: a new node (id node_ids[i]) joins in the slot of
+        replicas[i], whose old node the group has removed."""
+        _check_input(self._input("replace_node", len(replicas), _u64s(replicas), _u64s(node_ids)),
+                     "rbe_replace_node")
 
     def snapshot_saved(self, replicas, indexes, terms, removed=None):
         """The host's snapshot worker saved a snapshot of its state machine and the
@@ -925,6 +933,15 @@ class Engine(NodeInputs):
                "rbe_get_update_commits")
         return [tuple(getattr(arr[i], f) for f, _ in RbeUpdateCommit._fields_)
                 for i in range(count)]
+
+    def update_snapshots(self, first: int = 0, count: Optional[int] = None):
+        """The Snapshot of the last round's Updates (rbe_get_update_snapshots):
+        (index, term, packed membership, 0) per replica, zeros for none."""
+        count = self.n_rep - first if count is None else count
+        arr = (C.c_uint64 * (4 * max(1, count)))()
+        _check(self.lib.rbe_get_update_snapshots(self.h, first, count, arr),
+               "rbe_get_update_snapshots")
+        return [tuple(arr[4 * i:4 * i + 4]) for i in range(count)]
 
     def digests(self) -> np.ndarray:
         u = self.updates()

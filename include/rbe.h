@@ -313,14 +313,37 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out);
 int rbe_launch(rbe_engine* e, uint64_t n, const uint64_t* replica, const rbe_launch_state* st,
                const rbe_entry* ents, const uint8_t* cmd);
 /* The node ids of groups [first_group, first_group + count): n_replicas per
- * group in slot order, non-zero and strictly ascending within a group (the
- * engine's canonical order of a group's nodes — raft.go's map iterations,
- * SURVEY.md §8c — is ascending node id, which is then the slot order).  The
- * node ids of raft.Config.NodeID and pb.Message From/To (config.go, raft.pb.go)
- * that a dragonboat deployment assigns; a slot beyond the initial voters
- * (cfg.n_voters) is the id a joining node will have.  Only before the first
- * step (RBE_E_STATE after).  Without it slot s is node s + 1. */
+ * group in slot order, non-zero and distinct within a group.  The engine's
+ * canonical order of a group's nodes (raft.go's map iterations, SURVEY.md
+ * §8c) is the slot order: Go visits the maps in random order, so every fixed
+ * order is one of the reference's executions, and the per-(sender, receiver)
+ * message streams do not depend on it.  The node ids of raft.Config.NodeID
+ * and pb.Message From/To (config.go, raft.pb.go) that a dragonboat deployment
+ * assigns; a slot beyond the initial voters (cfg.n_voters) is the id a joining
+ * node will have.  Only before the first step (RBE_E_STATE after; later
+ * changes go through rbe_replace_node).  Without it slot s is node s + 1. */
 int rbe_set_node_ids(rbe_engine* e, uint64_t first_group, uint64_t count, const uint64_t* ids);
+/* A new node in a removed node's slot, between two rounds: replica[i]'s slot
+ * gets node id node_id[i] and its replica becomes that node, started as
+ * dragonboat starts a node that joins a running cluster (node.go:280-292: no
+ * peers, an empty LogDB, Launch with newNode; peer.go:64-86) in the slot's
+ * configured kind (voter, or cfg.observer_slots / witness_slots).  The host
+ * then adds it with a ConfigChange (AddNode / AddObserver / AddWitness of
+ * node_id[i], raft.go:1135-1180), which any replica of the group can take: a
+ * removed slot can host any number of new nodes over its life, as dragonboat
+ * gives every replacement a new node id (rsm membership refuses a removed id,
+ * membership.go:299-321).  Preconditions, checked whole before anything
+ * changes: cfg.membership, group-per-GPU (rep_world <= 1) and no seeded
+ * config-change / leader-transfer schedule (RBE_E_STATE); every replica[i]
+ * in range, at most one per group (RBE_E_STATE for two), node_id[i] non-zero
+ * and not the id of another slot of its group (RBE_E_INVALID); no input staged
+ * for any replica of the group; and nothing in the group still refers to the
+ * old node (RBE_E_STATE): every other replica has applied its RemoveNode (it
+ * is in none of raft.remotes / observers / witnesses), none has it as vote,
+ * leader or leader-transfer target, in a vote tally, as the sender or a
+ * confirmer of a queued ReadIndex or in the rate limiter's reports, and it sent no message
+ * in the last round.  Messages still addressed to the slot are dropped. */
+int rbe_replace_node(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint64_t* node_id);
 int rbe_destroy(rbe_engine* e);
 int rbe_abi_version(void);
 /* sizeof the ABI structs, in this order: rbe_config, rbe_replica_view,
@@ -513,7 +536,9 @@ typedef struct rbe_update_commit {
  * last_applied = the applied index the step ran with (rbe_notify_applied),
  * stable_log_to / stable_log_term = the last EntriesToSave entry,
  * ready_to_read = number of ReadyToReads; all zero for a replica whose step
- * made no Update (RBE_UF_HAS_UPDATE clear).  Needs cfg.ext_commit. */
+ * made no Update (RBE_UF_HAS_UPDATE clear); an Update carrying a Snapshot
+ * (RBE_UF_SNAPSHOT) gives stable_snapshot_to = its index and processed at
+ * least that index.  Needs cfg.ext_commit. */
 int rbe_get_update_commits(rbe_engine* e, uint64_t first, uint64_t count, rbe_update_commit* out);
 /* Peer.Commit's log part (peer.go:282-293 → entryLog.commitUpdate,
  * logentry.go:335-355; inMemory.savedLogTo / appliedLogTo, inmemory.go:
@@ -527,8 +552,22 @@ int rbe_get_update_commits(rbe_engine* e, uint64_t first, uint64_t count, rbe_up
  * step (RBE_E_STATE for a second).  A reference panic (processed below the
  * current value or above committed; last_applied above committed or
  * processed) sets RBE_FAULT_PANIC in the replica's fault word.  Needs
- * cfg.ext_commit (RBE_E_STATE); stable_snapshot_to must be 0 (no snapshots
- * with ext_commit, RBE_E_INVALID). */
+ * cfg.ext_commit (RBE_E_STATE).  A non-zero stable_snapshot_to equal to the
+ * index of the snapshot the replica restored (the Update's Snapshot) is
+ * savedSnapshotTo (inmemory.go:168-176): later Updates stop carrying it; any
+ * other value changes nothing (the reference only warns).  Until then every
+ * Update of the replica carries the snapshot again (peer.go:345-347) and a
+ * LogDB compaction (rbe_compact) waits.  With snapshots the engine's LogDB
+ * holds every entry up to the raft log's last, as a node's does: its
+ * UpdateCommit.LastApplied never passes the entries it has persisted (the
+ * node saves an Update before it applies it, node.go:975-994). */
+/* The Snapshot of the last round's Update of replicas [first, first + count)
+ * (pb.Update.Snapshot, peer.go:345-347): four words each — index, term,
+ * membership in the packed slot-mask form of rbe_launch_state::removed, 0 —
+ * all zero when the Update carries none (RBE_UF_SNAPSHOT clear).  This is what
+ * the node hands to LogReader.ApplySnapshot and the state machine
+ * (node.go:950-965). */
+int rbe_get_update_snapshots(rbe_engine* e, uint64_t first, uint64_t count, uint64_t* out4);
 int rbe_commit(rbe_engine* e, uint64_t n, const uint64_t* replica, const rbe_update_commit* uc);
 
 /* ---- Transport wire format ------------------------

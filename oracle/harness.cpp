@@ -101,11 +101,17 @@ struct Node {
   u64 ss_index = 0, ss_req = 0, compact_to = 0;
   u32 snap_pend = 0, snap_pend_reject = 0;  // SnapshotStatus of InstallSnapshots sent
   UpdateCommit uc;              // ext_commit: getUpdateCommit of the last step's Update
+  Snapshot ud_snap;             // the Snapshot of the last step's Update (empty: none)
   // a ConfigChange to apply to raft at the next step: applied by the state
   // machine (membership, a committed stand-in entry) or sent by the host
-  bool cc_pend = false, cc_reject = false;
-  int cc_type = 0;
-  u64 cc_node = 0;
+  // (each ConfigChange of an Update, in log order: node.ApplyConfigChange /
+  // ConfigChangeProcessed per entry, node.go:217-277)
+  struct CcApply {
+    bool reject;
+    int type;
+    u64 node;
+  };
+  std::vector<CcApply> cc_q;
   // the state machine's membership (rsm membership: the ConfigChanges it
   // applied, or the snapshot it recovered from), as the slots that are not
   // voters, bit k; a snapshot records it (pb.Snapshot.Membership)
@@ -369,6 +375,7 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
   const u32 n = cfg.n_replicas;
   nd->events = 0;
   nd->uc = UpdateCommit();
+  nd->ud_snap = Snapshot();
   // client input of this round: the workload goes to replicas that lead at
   // round start, host input (harness_push) to the replica it names
   const int wl = R->state == Leader ? wl_input(cfg, gr->cid, r) : 0;
@@ -408,7 +415,7 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
     // a round without a tick is a step only if handleEvents finds an event
     // (node.go:1030-1067)
     bool ev = do_read || do_prop || xfer || nd->x_unreach || nd->x_snap || nd->snap_pend ||
-              p->HasEntryToApply() || applied != nd->confirmedIndex || do_cc || nd->cc_pend ||
+              p->HasEntryToApply() || applied != nd->confirmedIndex || do_cc || !nd->cc_q.empty() ||
               nd->rr_pend || nd->x_rr;
     for (u32 s = 0; s < n; s++) ev = ev || !nd->in[s].empty();
     if (!ev) return;
@@ -431,11 +438,11 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
     nd->x_rr = nd->rr_pend = false;
     p->RestoreRemotes(ss);
   }
-  if (nd->cc_pend) {
-    nd->cc_pend = false;
-    if (nd->cc_reject) p->RejectConfigChange();
-    else p->ApplyConfigChange(nd->cc_node, nd->cc_type);
+  for (const Node::CcApply& a : nd->cc_q) {
+    if (a.reject) p->RejectConfigChange();
+    else p->ApplyConfigChange(a.node, a.type);
   }
+  nd->cc_q.clear();
   // handleEvents: updateBatchedLastApplied (node.go:1002-1006, 1032)
   p->NotifyRaftLastApplied(applied);
   // handleReadIndexRequests (node.go:1108-1118)
@@ -586,11 +593,9 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
           raft_ms = removed_of(m, n);
           have_ms = true;
         }
-        nd->cc_pend = true;
-        nd->cc_reject = !cc_accepted(raft_ms, t, nid, n);
-        nd->cc_type = t;
-        nd->cc_node = nid;
-        if (!nd->cc_reject) {
+        const bool rej = !cc_accepted(raft_ms, t, nid, n);
+        nd->cc_q.push_back(Node::CcApply{rej, t, nid});
+        if (!rej) {
           ms_apply(raft_ms, t, nid, n);
           // the state machine's membership (rsm membership.go)
           ms_apply(nd->sm_rem, t, nid, n);
@@ -628,8 +633,12 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
       if (m.type != Replicate) deliver(m);
     // a snapshot received through InstallSnapshot: the LogDB takes it and the
     // state machine recovers from it (node.go processSnapshot / rsm recover)
-    if (!isEmptySnapshot(ud.snapshot)) {
-      nd->db.ApplySnapshot(ud.snapshot);
+    // With ext_commit the Updates carry a restored snapshot until the host's
+    // UpdateCommit names it (StableSnapshotTo); the LogDB took it the first
+    // time (a later ApplySnapshot of it is ErrSnapshotOutOfDate, a soft
+    // error, node.go:950-965) and nothing else happens again.
+    nd->ud_snap = ud.snapshot;
+    if (!isEmptySnapshot(ud.snapshot) && nd->db.ApplySnapshot(ud.snapshot) == ErrOK) {
       if (!cfg.ext_apply) nd->smAppliedIndex = ud.snapshot.index;
       nd->ss_index = ud.snapshot.index;
       // the state machine takes the snapshot's membership, and the node
@@ -657,7 +666,11 @@ static void step_replica(const HarnessConfig& cfg, Group* gr, u32 k, u32 r, bool
     // compactSnapshot (node.go:585-605, 619-692) with the state machine's
     // applied index, done within the step (the lockstep definition of the
     // snapshot worker)
-    if (nd->compact_to) {
+    // With ext_commit a compaction waits while the raft log still holds a
+    // restored snapshot the host has not committed: the node runs compactLog
+    // before that Commit within one step (node.go:975-999), so the log's first
+    // index never moves past a snapshot it holds in memory.
+    if (nd->compact_to && !R->log.inmem.hasSnapshot) {
       // ErrCompacted / ErrUnavailable: nothing to do; never past the snapshot
       if (nd->compact_to <= nd->db.snapshot.index) nd->db.Compact(nd->compact_to);
       nd->compact_to = 0;
@@ -794,14 +807,10 @@ int harness_push(Harness* h, int kind, u64 replica, u64 a, u64 b, const Entry* e
       nd->x_cc_node = b;
       return 0;
     case PUSH_CC_APPLY:
-      nd->cc_pend = true;
-      nd->cc_reject = false;
-      nd->cc_node = a;
-      nd->cc_type = (int)b;
+      nd->cc_q.assign(1, Node::CcApply{false, (int)b, a});
       return 0;
     case PUSH_CC_REJECT:
-      nd->cc_pend = true;
-      nd->cc_reject = true;
+      nd->cc_q.assign(1, Node::CcApply{true, 0, 0});
       return 0;
     case PUSH_RESTORE:  // a: packed membership (pack_ms)
       if (((a & 0xFF) >> N) || (((a >> 8) & 0xFF) >> N) || (((a >> 16) & 0xFF) >> N) || (a >> 24))
@@ -917,6 +926,59 @@ void harness_restart(Harness* h, u64 replica) {
   for (u32 s = 0; s < N; s++) nd->in[s].clear();
   for (u32 j = 0; j < N; j++)
     if (j != k) gr->nodes[j]->in[k].clear();
+}
+
+// A new node in a removed node's slot (the engine's rbe_replace_node): -1
+// when another node of the group still refers to the slot's node (raft.go's
+// maps, vote, leader, leader-transfer target, vote tally, ReadIndex queue,
+// rate-limiter reports) or a message it sent last round is still to be
+// delivered; else the slot's node is a fresh one that joins the running
+// cluster (node.go:280-292: Launch with no peers and newNode over an empty
+// LogDB; the node around it is new too, its quiesce manager on the tick clock
+// as in harness_restart) and messages to the slot are dropped.  Inside the
+// harness the new node keeps the slot's node id: with nothing left that names
+// the old node, that is the reference run with a new id.
+int harness_replace(Harness* h, u64 replica) {
+  const HarnessConfig& cfg = h->cfg;
+  const u32 N = cfg.n_replicas;
+  if (replica >= h->groups.size() * N) return -1;
+  Group* gr = h->groups[replica / N];
+  const u32 k = (u32)(replica % N);
+  const u64 id = k + 1;
+  for (u32 j = 0; j < N; j++) {
+    if (j == k) continue;
+    const Node* o = gr->nodes[j];
+    const Raft* R = o->peer->raft;
+    if (R->remotes.count(id) || R->observers.count(id) || R->witnesses.count(id) ||
+        R->vote == id || R->leaderID == id || R->leaderTransferTarget == id || R->votes.count(id) ||
+        R->rl.followerSizes.count(id))
+      return -1;
+    for (const auto& kv : R->readIndex.pending)
+      if (kv.second.from == id || kv.second.confirmed.count(id)) return -1;
+    if (!o->in[k].empty()) return -1;
+  }
+  Node* old = gr->nodes[k];
+  const u64 t = old->q.tick;
+  Node* nd = new Node();
+  nd->peer = Peer::Launch(node_config(cfg, gr->cid, k), &nd->db, {}, false, true);
+  nd->sm_rem = (1u << N) - 1u;  // a joining node's state machine knows no members yet
+  nd->q.enabled = cfg.quiesce;
+  nd->q.electionTick = cfg.election_rtt * 2;  // node.go:165
+  nd->q.tick = nd->q.noActivitySince = nd->q.exitQuiesceTick = t;
+  gr->nodes[k] = nd;
+  delete old;
+  for (u32 j = 0; j < N; j++)
+    if (j != k) gr->nodes[j]->in[k].clear();
+  return 0;
+}
+
+void harness_update_snapshot(const Harness* h, u64 replica, u64 out4[4]) {
+  const u32 N = h->cfg.n_replicas;
+  const Snapshot& ss = h->groups[replica / N]->nodes[replica % N]->ud_snap;
+  out4[0] = ss.index;
+  out4[1] = ss.term;
+  out4[2] = isEmptySnapshot(ss) ? 0 : removed_of(ss.membership, N);
+  out4[3] = 0;
 }
 
 void harness_update_commit(const Harness* h, u64 replica, UpdateCommit* out) {

@@ -199,6 +199,11 @@ void harness_restart(Harness* h, u64 replica);
 // Update; getUpdateCommit, peer.go:410-427), and Peer.Commit's log part with a
 // host-chosen UpdateCommit (entryLog.commitUpdate, logentry.go:335-355)
 void harness_update_commit(const Harness* h, u64 replica, UpdateCommit* out);
+// a fresh node joins in the replica's slot (rbe_replace_node); -1 while the
+// group still refers to the slot's node
+int harness_replace(Harness* h, u64 replica);
+// the Snapshot of the replica's last Update: index, term, packed membership, 0
+void harness_update_snapshot(const Harness* h, u64 replica, u64 out4[4]);
 void harness_commit(Harness* h, u64 replica, const UpdateCommit& uc);
 // debugging: the messages replica `replica` receives from slot `sender` next
 // round (delivered by the last round), as 10 words each: type, from, to, term,

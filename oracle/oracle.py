@@ -199,6 +199,8 @@ def lib():
             "orc_harness_snapshot_saved": (i32, [vp, u64, u64, u64, u32]),
             "orc_harness_compact": (i32, [vp, u64, u64]),
             "orc_harness_update_commit": (None, [vp, u64, P(u64)]),
+            "orc_harness_update_snapshot": (None, [vp, u64, P(u64)]),
+            "orc_harness_replace": (C.c_int, [vp, u64]),
             "orc_harness_commit": (i32, [vp, u64, P(u64)]),
             "orc_harness_inbox": (u32, [vp, u64, u32, P(u64), u32]),
             "orc_view_size": (i32, []),
@@ -1011,6 +1013,21 @@ class Harness:
         stable_snapshot_to, ready_to_read); zeros when it made no Update."""
         o = (C.c_uint64 * 6)()
         lib().orc_harness_update_commit(self.h, replica, o)
+        return tuple(o)
+
+    def replace(self, replica):
+        """A fresh node joins in the replica's slot (rbe_replace_node); False
+        while the group still refers to the slot's node."""
+        rc = lib().orc_harness_replace(self.h, replica)
+        if rc == -2:
+            raise _err()
+        return rc == 0
+
+    def update_snapshot(self, replica):
+        """The Snapshot of the replica's last Update (peer.go:345-347): (index,
+        term, packed membership, 0); zeros when it carried none."""
+        o = (C.c_uint64 * 4)()
+        lib().orc_harness_update_snapshot(self.h, replica, o)
         return tuple(o)
 
     def commit(self, replica, uc):

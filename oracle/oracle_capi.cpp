@@ -939,6 +939,14 @@ void orc_harness_update_commit(void* h, uint64_t replica, uint64_t* out6) {
   out6[4] = u.stable_snapshot_to;
   out6[5] = u.ready_to_read;
 }
+int orc_harness_replace(void* h, uint64_t replica) {
+  GUARD_BEGIN
+  return harness_replace((Harness*)h, replica);
+  GUARD_END(-2)
+}
+void orc_harness_update_snapshot(void* h, uint64_t replica, uint64_t* out4) {
+  harness_update_snapshot((Harness*)h, replica, out4);
+}
 int orc_harness_commit(void* h, uint64_t replica, const uint64_t* uc6) {
   GUARD_BEGIN
   UpdateCommit u;

@@ -9,6 +9,8 @@
 //   F  C + Hot/Core/Upd/count row stored chunk-major ([chunk][replica] planes of
 //      16 B), so the adjacent lanes of a group write adjacent 16 B
 //   D  one lane per group, its N replicas' steps in sequence
+// each for the C4 workload's random 10% of the groups and for the first 100k
+// groups (an awake set compacted into adjacent rows: the bound of a dense slab)
 // Build: make -C scripts/microbench group_shape
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -151,22 +153,6 @@ __global__ __launch_bounds__(256, 2) void k_D(Planes P, const unsigned* groups, 
 
 int main(int argc, char** argv) {
   const unsigned G = 1u << 20, R = 3 * G, NG = 100000, MAXM = 12;
-  std::vector<unsigned> perm(G);
-  std::mt19937 rng(1);
-  for (unsigned i = 0; i < G; i++) perm[i] = i;
-  std::shuffle(perm.begin(), perm.end(), rng);
-  std::vector<unsigned> gs(perm.begin(), perm.begin() + NG);
-  std::sort(gs.begin(), gs.end());
-  std::vector<unsigned> list;
-  auto lead = [](unsigned g) {
-    unsigned x = g * 2654435761u;
-    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
-    return x % 3;
-  };
-  for (unsigned g : gs) list.push_back(g * 3 + lead(g));
-  for (unsigned g : gs)
-    for (unsigned k = 0; k < 3; k++)
-      if (k != lead(g)) list.push_back(g * 3 + k);
   Planes P;
   P.G = G;
   P.maxm = MAXM;
@@ -183,10 +169,8 @@ int main(int argc, char** argv) {
   hipMalloc(&P.mo, sizeof(Msg) * (size_t)G * 9 * MAXM);
   hipMemset(P.mi, 0, sizeof(Msg) * (size_t)G * 9 * MAXM);
   unsigned *dl, *dg;
-  hipMalloc(&dl, list.size() * 4);
+  hipMalloc(&dl, 3 * NG * 4);
   hipMalloc(&dg, NG * 4);
-  hipMemcpy(dl, list.data(), list.size() * 4, hipMemcpyHostToDevice);
-  hipMemcpy(dg, gs.data(), NG * 4, hipMemcpyHostToDevice);
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
@@ -198,27 +182,52 @@ int main(int argc, char** argv) {
     hipEventSynchronize(e1);
     float ms;
     hipEventElapsedTime(&ms, e0, e1);
-    printf("%-32s %8.2f us/launch\n", name, ms * 1000 / 20);
+    printf("%-40s %8.2f us/launch\n", name, ms * 1000 / 20);
   };
-  const unsigned nl = (unsigned)list.size();
-  const unsigned gA = (nl + 255) / 256, gB = ((NG + 20) / 21 + 3) / 4, gD = (NG + 255) / 256;
-  for (unsigned lds : {0u, 40u << 10, 52u << 10, 64u << 10}) {
-  printf("-- dynamic LDS %u KB per 256-thread block\n", lds >> 10);
-  for (unsigned wk : {0u, 1u}) {
-    char nm[64];
-    snprintf(nm, sizeof nm, "A role lists      work %u", wk);
-    t(nm, [&] { hipLaunchKernelGGL(k_A, dim3(gA), dim3(256), lds, 0, P, dl, nl, wk); });
-    snprintf(nm, sizeof nm, "B group lanes     work %u", wk);
-    t(nm, [&] { hipLaunchKernelGGL((k_B<false, false>), dim3(gB), dim3(256), lds, 0, P, dg, NG, wk); });
-    snprintf(nm, sizeof nm, "C B + mailbox     work %u", wk);
-    t(nm, [&] { hipLaunchKernelGGL((k_B<true, false>), dim3(gB), dim3(256), lds, 0, P, dg, NG, wk); });
-    snprintf(nm, sizeof nm, "F C + chunk-major work %u", wk);
-    t(nm, [&] { hipLaunchKernelGGL((k_B<true, true>), dim3(gB), dim3(256), lds, 0, P, dg, NG, wk); });
-    snprintf(nm, sizeof nm, "E B + chunk-major work %u", wk);
-    t(nm, [&] { hipLaunchKernelGGL((k_B<false, true>), dim3(gB), dim3(256), lds, 0, P, dg, NG, wk); });
-    snprintf(nm, sizeof nm, "D lane per group  work %u", wk);
-    t(nm, [&] { hipLaunchKernelGGL(k_D, dim3(gD), dim3(256), lds, 0, P, dg, NG, wk); });
-  }
+  auto lead = [](unsigned g) {
+    unsigned x = g * 2654435761u;
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x % 3;
+  };
+  // the active groups: a random 10% of the 1M (the C4 workload's hash), or
+  // the first 100k (an awake set compacted into adjacent rows)
+  for (int dense = 0; dense < 2; dense++) {
+    std::vector<unsigned> gs(NG);
+    if (dense) {
+      for (unsigned i = 0; i < NG; i++) gs[i] = i;
+    } else {
+      std::vector<unsigned> perm(G);
+      std::mt19937 rng(1);
+      for (unsigned i = 0; i < G; i++) perm[i] = i;
+      std::shuffle(perm.begin(), perm.end(), rng);
+      std::copy(perm.begin(), perm.begin() + NG, gs.begin());
+      std::sort(gs.begin(), gs.end());
+    }
+    std::vector<unsigned> list;
+    for (unsigned g : gs) list.push_back(g * 3 + lead(g));
+    for (unsigned g : gs)
+      for (unsigned k = 0; k < 3; k++)
+        if (k != lead(g)) list.push_back(g * 3 + k);
+    hipMemcpy(dl, list.data(), list.size() * 4, hipMemcpyHostToDevice);
+    hipMemcpy(dg, gs.data(), NG * 4, hipMemcpyHostToDevice);
+    const unsigned nl = (unsigned)list.size();
+    const unsigned gA = (nl + 255) / 256, gB = ((NG + 20) / 21 + 3) / 4, gD = (NG + 255) / 256;
+    const char* set = dense ? "dense " : "random";
+    for (unsigned wk : {0u, 1u}) {
+      char nm[80];
+      snprintf(nm, sizeof nm, "%s A role lists      work %u", set, wk);
+      t(nm, [&] { hipLaunchKernelGGL(k_A, dim3(gA), dim3(256), 0, 0, P, dl, nl, wk); });
+      snprintf(nm, sizeof nm, "%s B group lanes     work %u", set, wk);
+      t(nm, [&] { hipLaunchKernelGGL((k_B<false, false>), dim3(gB), dim3(256), 0, 0, P, dg, NG, wk); });
+      snprintf(nm, sizeof nm, "%s C B + mailbox     work %u", set, wk);
+      t(nm, [&] { hipLaunchKernelGGL((k_B<true, false>), dim3(gB), dim3(256), 0, 0, P, dg, NG, wk); });
+      snprintf(nm, sizeof nm, "%s E B + chunk-major work %u", set, wk);
+      t(nm, [&] { hipLaunchKernelGGL((k_B<false, true>), dim3(gB), dim3(256), 0, 0, P, dg, NG, wk); });
+      snprintf(nm, sizeof nm, "%s F C + chunk-major work %u", set, wk);
+      t(nm, [&] { hipLaunchKernelGGL((k_B<true, true>), dim3(gB), dim3(256), 0, 0, P, dg, NG, wk); });
+      snprintf(nm, sizeof nm, "%s D lane per group  work %u", set, wk);
+      t(nm, [&] { hipLaunchKernelGGL(k_D, dim3(gD), dim3(256), 0, 0, P, dg, NG, wk); });
+    }
   }
   hipDeviceSynchronize();
   printf("done\n");

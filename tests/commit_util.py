@@ -15,7 +15,9 @@ import random
 from input_util import run_driven
 
 
-def commit_hook(eng, ref, seed, p_commit=0.55, p_partial=0.25):
+def commit_hook(eng, ref, seed, p_commit=0.55, p_partial=0.25, tweak=None):
+    """`tweak(replica, uc)`, if given, may change each UpdateCommit before
+    both sides get it."""
     rng = random.Random(seed ^ 0xC0FFEE)
     n = eng.cfg.n_replicas
     pend = {}
@@ -42,6 +44,8 @@ def commit_hook(eng, ref, seed, p_commit=0.55, p_partial=0.25):
                 to = rng.randrange(v.saved_to + 1, uc[2])
                 uc[2], uc[3] = to, ref.log_term(r // n, r % n, to)
                 state["partial"] += 1
+            if tweak is not None:
+                uc = list(tweak(r, tuple(uc)))
             reps.append(r)
             ucs.append(tuple(uc))
         if reps:
@@ -56,4 +60,82 @@ def commit_hook(eng, ref, seed, p_commit=0.55, p_partial=0.25):
 def run_commit_driven(eng, ref, rounds, seed, **kw):
     hook, state = commit_hook(eng, ref, seed)
     d = run_driven(eng, ref, rounds, seed=seed, ext_apply=True, before_round=hook, **kw)
+    return d, state
+
+
+def run_commit_snapshots(eng, ref, rounds, seed, every=12, overhead=3, **kw):
+    """ext_commit with host-driven snapshots (cfg.snapshot_entries with
+    ext_apply): commit_hook's lagging persistence plus the node's snapshot
+    worker (rbe_snapshot_saved / rbe_compact, as tests/test_host_snapshots.py).
+    An Update that carries a restored snapshot keeps carrying it until a
+    commit names it (StableSnapshotTo, peer.go:410-427; inmemory.go:168-176;
+    a commit without it would leave a later Update's Processed at the
+    snapshot index, below raft's, which commitUpdate panics on, logentry.go:
+    337-342).  Every round the Updates' snapshots and the
+    node snapshot state must equal the oracle's too.  The host here is a
+    node's: its LastApplied never passes what it has persisted (the node
+    saves an Update before it applies it, node.go:975-994), so the LogDB it
+    compacts holds every entry up to the raft log's last (rbe.h, rbe_commit)."""
+    rng = random.Random(seed ^ 0x5A5A)
+    counts = {"snap_commits": 0}  # commits naming a carried snapshot
+
+    def tweak(r, uc):
+        saved = max(ref.views()[r].saved_to, uc[2])
+        if uc[1] > saved:
+            uc = (uc[0], saved) + uc[2:]
+        counts["snap_commits"] += uc[4] != 0
+        return uc
+
+    hook, state = commit_hook(eng, ref, seed, tweak=tweak)
+    n = eng.cfg.n_replicas
+    n_rep = eng.n_rep
+    applied = [0] * n_rep
+    last_ss = [0] * n_rep
+    pend = {}
+    state.update(carried=0, saved=0, compacted=0, restored=0)
+
+    def before_round(rnd):
+        hook(rnd)
+        if rnd == 0:
+            return
+        eus = eng.update_snapshots()
+        es = eng.snapshot_state()
+        for r in range(n_rep):
+            ous = ref.update_snapshot(r)
+            assert tuple(eus[r]) == ous, (rnd, r, "Update.Snapshot", eus[r], ous)
+            state["carried"] += ous[0] != 0
+            oss = ref.snapshot_state(r)
+            assert tuple(int(x) for x in es[r]) == tuple(oss), (rnd, r, "snapshot state",
+                                                                  tuple(es[r]), oss)
+            if oss[2] > last_ss[r]:  # a snapshot the host did not save: restored
+                state["restored"] += 1
+                last_ss[r] = oss[2]
+        if rnd < 30:
+            return
+        for r in range(n_rep):
+            if r in pend and rng.random() < 0.4:
+                to = pend.pop(r)
+                eng.compact([r], [to])
+                ref.compact(r, to)
+                state["compacted"] += 1
+            elif applied[r] > last_ss[r] + every and rng.random() < 0.5:
+                idx = applied[r]
+                term = ref.log_term(r // n, r % n, idx)
+                if term == 0:
+                    continue
+                eng.snapshot_saved([r], [idx], [term])
+                ref.snapshot_saved(r, idx, term)
+                last_ss[r] = idx
+                if idx > overhead:
+                    pend[r] = idx - overhead
+                state["saved"] += 1
+
+    def on_ops(ops):
+        for kind, r, a in ops:
+            if kind == "applied":
+                applied[r] = a
+
+    d = run_driven(eng, ref, rounds, seed=seed, ext_apply=True, before_round=before_round,
+                   on_ops=on_ops, **kw)
+    state.update(counts)
     return d, state

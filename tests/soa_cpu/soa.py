@@ -100,9 +100,11 @@ def lib():
                 "reject_config_change": [C.c_uint64, u64p],
                 "restore_remotes": [C.c_uint64, u64p, u32p, u64p],
                 "set_node_ids": [C.c_uint64, C.c_uint64, u64p],
+                "replace_node": [C.c_uint64, u64p, u64p],
                 "snapshot_saved": [C.c_uint64, u64p, u64p, u64p, u32p],
                 "compact": [C.c_uint64, u64p, u64p],
                 "get_update_commits": [C.c_uint64, C.c_uint64, P(RbeUpdateCommit)],
+                "get_update_snapshots": [C.c_uint64, C.c_uint64, u64p],
                 "launch": [C.c_uint64, u64p, C.c_void_p, C.c_void_p, C.c_void_p]}.items():
             fn = getattr(L, "soa_" + name)
             fn.restype = C.c_int
@@ -155,6 +157,14 @@ class SoaCpu(NodeInputs):
             raise RuntimeError(f"soa_get_update_commits rc={rc}")
         return [tuple(getattr(arr[i], f) for f, _ in RbeUpdateCommit._fields_)
                 for i in range(count)]
+
+    def update_snapshots(self, first=0, count=None):
+        count = self.n_rep - first if count is None else count
+        arr = (C.c_uint64 * (4 * max(1, count)))()
+        rc = lib().soa_get_update_snapshots(self.h, first, count, arr)
+        if rc:
+            raise RuntimeError(f"soa_get_update_snapshots rc={rc}")
+        return [tuple(arr[4 * i:4 * i + 4]) for i in range(count)]
 
     def entry_cmds(self, replica, lo, hi):
         return entry_cmds(lib().soa_get_entry_cmds, self.h, replica, lo, hi)

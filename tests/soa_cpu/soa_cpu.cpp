@@ -480,7 +480,14 @@ int soa_apply_config_change(void* h, uint64_t n, const uint64_t* replica, const 
                             const uint32_t* type) {
   SoaEngine* e = (SoaEngine*)h;
   if (!e->C.membership || !e->C.ext_apply) return RBE_E_STATE;
-  return e->hin.apply_config_change(n, replica, node, type, false);
+  std::vector<u32> ms(n);
+  for (u64 i = 0; i < n && replica; i++) {
+    if (replica[i] >= e->C.n_rep) return RBE_E_INVALID;
+    const Core& c = e->P.core[replica[i]];
+    const u32 x = (c.mflags & MB_ROLES) ? e->P.roles[replica[i]] : 0u;
+    ms[i] = pack_ms(c.members & MB_REMOVED, x & 0xFFu, x >> 8);
+  }
+  return e->hin.apply_config_change(n, replica, node, type, false, ms.data());
 }
 int soa_reject_config_change(void* h, uint64_t n, const uint64_t* replica) {
   SoaEngine* e = (SoaEngine*)h;
@@ -498,6 +505,36 @@ int soa_compact(void* h, uint64_t n, const uint64_t* replica, const uint64_t* to
   if (!e->C.snapshot_entries || !e->C.ext_apply) return RBE_E_STATE;
   return e->hin.snapshot_op(n, replica, SR_COMPACT, to, nullptr, nullptr, false);
 }
+// rbe_replace_node on the host build: the same checks (slot_referenced) and
+// the same new node (join_replica)
+int soa_replace_node(void* h, uint64_t n, const uint64_t* replica, const uint64_t* node_id) {
+  SoaEngine* e = (SoaEngine*)h;
+  int rc = e->hin.replace_args(n, replica, node_id);
+  if (rc) return rc;
+  if (!e->C.membership || e->C.rep_world > 1 || e->C.cc_period || e->C.xfer_period)
+    return RBE_E_STATE;
+  for (u64 i = 0; i < n; i++) {
+    bool refd = false;
+    with_n(e->C.n, [&](auto NN) {
+      constexpr int N = decltype(NN)::value;
+      refd = slot_referenced<N>(e->P, e->C, replica[i] / N, (u32)(replica[i] % N), e->round);
+    });
+    if (refd) return RBE_E_STATE;
+  }
+  const u32 ppar = (e->round & 1u) ^ 1u;
+  for (u64 i = 0; i < n; i++) {
+    e->hin.assign_node(e->C.n_groups, replica[i], node_id[i]);
+    with_n(e->C.n, [&](auto NN) {
+      constexpr int N = decltype(NN)::value;
+      join_replica<N>(e->P, e->C, replica[i], ppar, e->tclk);
+      e->P.gwake[replica[i] / N] = GW_AWAKE;
+    });
+  }
+  e->P.node_ids = e->hin.id_table();
+  e->scan_at = e->round;  // as rbe_launch: the next round scans every group
+  return RBE_OK;
+}
+
 int soa_set_node_ids(void* h, uint64_t first, uint64_t count, const uint64_t* ids) {
   SoaEngine* e = (SoaEngine*)h;
   if (e->round != 0) return RBE_E_STATE;
@@ -531,7 +568,20 @@ int soa_get_update_commits(void* h, uint64_t first, uint64_t count, rbe_update_c
       return idx == c.last_index ? c.t_last
                                  : e->P.term_ring[(idx & (u64)(e->C.ring - 1)) * e->C.n_rep + r];
     };
-    update_commit_view(u, e->P.applied[r], term_of, out[i]);
+    const u64 si = e->C.snapshot_entries ? e->P.snp[r].marker : 0;
+    update_commit_view(u, e->P.applied[r], si, term_of, out[i]);
+  }
+  return RBE_OK;
+}
+// rbe_get_update_snapshots on the host build
+int soa_get_update_snapshots(void* h, uint64_t first, uint64_t count, uint64_t* out4) {
+  SoaEngine* e = (SoaEngine*)h;
+  if (!out4 || first + count > e->C.n_rep) return RBE_E_INVALID;
+  for (u64 i = 0; i < count; i++) {
+    const u64 r = first + i;
+    rbe_update u;
+    update_view(e->P.upd[r], e->P.core[r], e->P.hot[r], e->round, u);
+    update_snapshot_row(u, e->C.snapshot_entries ? &e->P.snp[r] : nullptr, out4 + 4 * i);
   }
   return RBE_OK;
 }

@@ -70,12 +70,12 @@ def test_footprint_and_validation():
     assert lib.rbe_footprint(C.byref(E.make_config(n_groups=1000, snapshot_entries=16,
                                                    compaction_overhead=4)), C.byref(snap)) == 0
     assert snap.value >= b.value + 1000 * 3 * (64 + 3 * 8)
-    # host-driven snapshots (ext_apply) are fine; not with ext_commit
+    # host-driven snapshots (ext_apply), also with host-driven commits (ext_commit)
     assert lib.rbe_footprint(C.byref(E.make_config(n_groups=10, snapshot_entries=16, ext_inputs=True,
                                                    ext_apply=True)), C.byref(b)) == 0
     assert lib.rbe_footprint(C.byref(E.make_config(n_groups=10, snapshot_entries=16, ext_inputs=True,
                                                    ext_apply=True, ext_commit=True)),
-                             C.byref(b)) == -1
+                             C.byref(b)) == 0
 
 
 def test_null_handles_are_rejected():

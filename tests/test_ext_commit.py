@@ -8,9 +8,9 @@ unprocessed committed entries again (entriesToApply from processed + 1)."""
 import pytest
 
 import oracle as O
-from commit_util import run_commit_driven
-from dragonboat_amd.engine import InputError, RBE_E_INVALID, RBE_E_STATE
-from parity_util import C2, C3, C4
+from commit_util import run_commit_driven, run_commit_snapshots
+from dragonboat_amd.engine import InputError, RBE_E_STATE
+from parity_util import C2, C3, C3_HOT, C4
 from soa_cpu.soa import SoaCpu
 
 DRIVEN = dict(maxm=40, ecap=64, rq_cap=32, ring=256)
@@ -53,9 +53,6 @@ def test_commit_calls_refused():
     eng = SoaCpu(trace=True, n_groups=2, n_replicas=3, ext_inputs=True, ext_apply=True,
                  ext_commit=True)
     eng.step()
-    with pytest.raises(InputError) as ei:  # stable_snapshot_to: no snapshots with ext_commit
-        eng.commit([0], [(0, 0, 3, 1, 3, 0)])
-    assert ei.value.rc == RBE_E_INVALID
     with pytest.raises(InputError) as ei:  # the same replica twice in one batch
         eng.commit([1, 1], [(0, 0, 3, 1, 0, 0)] * 2)
     assert ei.value.rc == RBE_E_STATE
@@ -84,3 +81,23 @@ def test_commit_panics_fault_the_replica():
     eng.step()
     n, bits = eng.faults()
     assert n == 1 and bits & 0x20
+
+
+# ext_commit with snapshots: host-driven snapshots (rbe_snapshot_saved /
+# rbe_compact) and InstallSnapshot for the isolated replicas; the Update of a
+# restoring step carries the snapshot until a commit names it
+SNAP_COMMIT = dict(ext_inputs=True, ext_apply=True, ext_commit=True, snapshot_entries=1)
+SNAP_CASES = {"C3_HOT": dict(C3_HOT, n_groups=16), "C3_N7": dict(C3, n_groups=12, n_replicas=7)}
+SNAP_SIZES = dict(maxm=40, ecap=256, rq_cap=32, ring=128)
+
+
+@pytest.mark.parametrize("name", list(SNAP_CASES))
+def test_snapshots_with_delayed_persist(name):
+    base = dict(SNAP_CASES[name], **SNAP_COMMIT)
+    eng, ref = SoaCpu(trace=True, **dict(base, **SNAP_SIZES)), O.Harness(**base)
+    d, st = run_commit_snapshots(eng, ref, 300, seed=11)
+    assert d is None, f"{name}: first divergence {d}"
+    assert eng.faults()[0] == 0
+    assert st["saved"] > 20 and st["compacted"] > 10, st
+    assert st["restored"] > 0 and st["carried"] > st["restored"] and st["snap_commits"] > 0, st
+

@@ -7,8 +7,9 @@ tests/test_ext_commit.py."""
 import pytest
 
 import oracle as O
-from commit_util import run_commit_driven
+from commit_util import run_commit_driven, run_commit_snapshots
 from parity_util import C2, C3, C4
+from test_ext_commit import SNAP_CASES, SNAP_COMMIT, SNAP_SIZES
 
 pytestmark = pytest.mark.gpu
 
@@ -40,4 +41,19 @@ def test_gpu_commit_panic_faults(gpu_available):
     eng.step()
     n, bits = eng.fault_summary()
     assert n == 1 and bits & 0x20
+    eng.close()
+
+
+@pytest.mark.parametrize("name", list(SNAP_CASES))
+def test_gpu_snapshots_with_delayed_persist(gpu_available, name):
+    """ext_commit with host-driven snapshots and InstallSnapshot: the Updates'
+    snapshots, UpdateCommits (StableSnapshotTo), snapshot state, views and
+    digests equal the oracle's every round (CPU twin in test_ext_commit.py)."""
+    from dragonboat_amd.engine import Engine
+    base = dict(SNAP_CASES[name], **SNAP_COMMIT)
+    eng, ref = Engine(device=0, trace=True, **dict(base, **SNAP_SIZES)), O.Harness(**base)
+    d, st = run_commit_snapshots(eng, ref, 300, seed=11)
+    assert d is None, f"{name}: first divergence {d}"
+    assert eng.fault_summary()[0] == 0
+    assert st["saved"] > 20 and st["compacted"] > 10 and st["restored"] > 0, st
     eng.close()

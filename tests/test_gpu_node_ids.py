@@ -71,3 +71,30 @@ def test_gpu_node_ids_outputs(gpu_available):
     assert node_hints > 0, "no leader transfer carried a node id in its Hint"
     a.close()
     b.close()
+
+
+def test_gpu_replace_nodes_runtime_ids(gpu_available):
+    """rbe_replace_node on the HIP engine: remove node 3 and add node 9 in its
+    slot, remove node 1 and add node 4; the device check (slot_referenced)
+    allows it exactly when the oracle does, and every view equals the oracle's
+    every round (CPU twin: test_node_ids.py)."""
+    from dragonboat_amd.engine import Engine
+    from test_node_ids import REPL_CASE, REPL_PLAN, run_replacements
+    eng = Engine(device=0, trace=True, **REPL_CASE, **CATCHUP)
+    ref = O.Harness(**REPL_CASE)
+    stage, refused = run_replacements(eng, ref, 300)
+    assert eng.fault_summary()[0] == 0
+    assert all(s == len(REPL_PLAN) for s in stage) and refused > 0, (stage, refused)
+    eng.close()
+
+
+def test_gpu_node_ids_any_order(gpu_available):
+    from dragonboat_amd.engine import Engine
+    n = ID_CASE["n_replicas"]
+    ids = [list(reversed(row)) for row in random_ids(ID_CASE["n_groups"], n, seed=9)]
+    eng = Engine(device=0, trace=True, **ID_CASE, **CATCHUP)
+    eng.set_node_ids(0, ids)
+    ref = O.Harness(**ID_CASE)
+    lockstep_ids(eng, ref, ids, n, 150)
+    assert eng.fault_summary()[0] == 0
+    eng.close()

@@ -44,3 +44,28 @@ def test_gpu_observer_witness_snapshots(gpu_available):
     run_memb_snap(eng, ref, 400)
     assert eng.fault_summary()[0] == 0
     eng.close()
+
+
+def test_gpu_host_cannot_put_a_node_in_two_sets(gpu_available):
+    """rbe_apply_config_change reads the replicas' membership from the device
+    and refuses an AddObserver / AddWitness that would put a node in two of
+    raft's maps (CPU twin in test_observers_witnesses.py)."""
+    from dragonboat_amd.engine import Engine, InputError, RBE_E_INVALID
+    from parity_util import C2
+    kw = dict(C2, n_groups=2, n_replicas=5, n_voters=3, observer_slots=0b01000,
+              witness_slots=0b10000, ext_inputs=True, ext_apply=True, membership=True)
+    eng = Engine(device=0, trace=True, **dict(kw, maxm=40, ecap=256, rq_cap=32, ring=256))
+    eng.run(30)
+    eng.apply_config_change([0], [4], [O.CC_ADD_OBSERVER])
+    eng.step()
+    eng.apply_config_change([0], [5], [O.CC_ADD_WITNESS])
+    eng.step()
+    for node, t in ((2, O.CC_ADD_OBSERVER), (3, O.CC_ADD_WITNESS), (4, O.CC_ADD_WITNESS),
+                    (5, O.CC_ADD_OBSERVER)):
+        with pytest.raises(InputError) as ei:
+            eng.apply_config_change([0], [node], [t])
+        assert ei.value.rc == RBE_E_INVALID, (node, t)
+    v = eng.views()[0]
+    assert v.observers == 0b01000 and v.witnesses == 0b10000
+    assert eng.fault_summary()[0] == 0
+    eng.close()

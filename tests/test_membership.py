@@ -28,7 +28,7 @@ from soa_cpu.soa import SoaCpu
 # a voter added back is caught up from far behind in one Replicate: the entry
 # arena and the in-memory window hold that many entries (the reference has no
 # such capacities; the engine flags F_ARENA / F_WINDOW instead)
-CATCHUP = dict(ring=256, ecap=256, maxm=24, rq_cap=64)
+CATCHUP = dict(ring=512, ecap=1024, maxm=24, rq_cap=64)
 EXTRA = {"C3": CATCHUP, "MIXED": CATCHUP, "C2": CATCHUP}
 MEMB = dict(membership=True, cc_period=10, cc_mod=1)
 

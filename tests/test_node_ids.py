@@ -208,7 +208,7 @@ def test_node_ids_over_the_transport(wire, n):
 def test_node_id_checks():
     from dragonboat_amd.engine import InputError, RBE_E_INVALID, RBE_E_STATE
     e = SoaCpu(trace=True, n_groups=3, n_replicas=3, ext_inputs=True)
-    for bad in ([[5, 3, 9]], [[0, 4, 9]], [[4, 4, 9]]):  # not ascending, NoNode, repeated
+    for bad in ([[0, 4, 9]], [[4, 4, 9]], [[4, 9, 4]]):  # NoNode, repeated
         with pytest.raises(InputError) as ei:
             e.set_node_ids(0, bad)
         assert ei.value.rc == RBE_E_INVALID
@@ -224,3 +224,121 @@ def test_node_id_checks():
     with pytest.raises(InputError) as ei:  # only before the first step
         e.set_node_ids(0, [[7, 8, 9]])
     assert ei.value.rc == RBE_E_STATE
+
+
+# ---- runtime node ids (rbe_replace_node): a removed node's slot takes a new id
+REPL_CASE = dict(C2, n_groups=6, n_replicas=3, membership=True, ext_inputs=True)
+# per group: (slot, old id, new id) in order — remove node 3 and add node 9,
+# then remove node 1 (the first leader) and add node 4
+REPL_PLAN = ((2, 3, 9), (0, 1, 4))
+
+
+def run_replacements(eng, ref, rounds, plan=REPL_PLAN, n=3):
+    """Each group walks `plan`: propose RemoveNode(old) at its leader; once
+    every replica applied it and nothing refers to the old node, both sides
+    replace the slot (rbe_replace_node / Harness.replace must agree on when
+    that is allowed), then propose AddNode(new) and wait until the new node has
+    caught up.  Views (mapped through the current ids) equal the oracle's every
+    round.  Returns per group the steps completed."""
+    from dragonboat_amd.engine import InputError
+    ng = len(eng.views()) // n
+    ids = [[1, 2, 3] for _ in range(ng)]
+    stage = [0] * ng          # index into plan (x2: 0 = remove, 1 = replace/add)
+    phase = ["remove"] * ng   # remove -> wait_removed -> add -> wait_added
+    refused = 0
+    for rnd in range(rounds):
+        hv = ref.views()
+        for g in range(ng):
+            if stage[g] >= len(plan):
+                continue
+            slot, old, new = plan[stage[g]]
+            rows = [hv[g * n + k] for k in range(n)]
+            lead = [k for k in range(n) if rows[k].role == O.LEADER]
+            if phase[g] == "remove" and lead and rnd > 40:
+                L = lead[0]
+                eng.propose_config_change([g * n + L], [O.CC_REMOVE_NODE], [old])
+                ref.push(O.PUSH_CC_PROPOSE, g * n + L, O.CC_REMOVE_NODE, slot + 1)
+                phase[g] = "wait_removed"
+            elif phase[g] == "wait_removed":
+                ok_ref = ref.replace(g * n + slot)
+                try:
+                    eng.replace_node([g * n + slot], [new])
+                    ok_eng = True
+                except InputError:
+                    ok_eng = False
+                assert ok_eng == ok_ref, (rnd, g, "replace allowed", ok_eng, ok_ref)
+                if ok_ref:
+                    ids[g][slot] = new
+                    phase[g] = "add"
+                else:
+                    refused += 1
+            elif phase[g] == "add" and lead and lead[0] != slot:
+                L = lead[0]
+                eng.propose_config_change([g * n + L], [O.CC_ADD_NODE], [new])
+                ref.push(O.PUSH_CC_PROPOSE, g * n + L, O.CC_ADD_NODE, slot + 1)
+                phase[g] = "wait_added"
+            elif phase[g] == "wait_added" and lead:
+                lv = rows[lead[0]]
+                # the new node counts at the leader and follows it (one
+                # round behind on commits while proposals keep coming)
+                if rows[slot].committed + 2 >= lv.committed and not (lv.removed >> slot) & 1:
+                    stage[g] += 1
+                    phase[g] = "remove"
+        eng.step()
+        ref.step()
+        ev, hv = eng.views(), ref.views()
+        for i in range(len(hv)):
+            d = view_diff(ev[i], mapped(hv[i], ids[i // n]))
+            assert d is None, f"round {rnd} replica {i}: {d}"
+    return stage, refused
+
+
+def test_replace_nodes_runtime_ids():
+    """Remove node 3, add node 9 in its slot; remove node 1, add node 4: 300
+    rounds, every view field and digest equal to the oracle's every round."""
+    eng = SoaCpu(trace=True, **REPL_CASE, **CATCHUP)
+    ref = O.Harness(**REPL_CASE)
+    stage, refused = run_replacements(eng, ref, 300)
+    assert eng.faults()[0] == 0
+    assert all(s == len(REPL_PLAN) for s in stage), stage
+    assert refused > 0, "the replacement was never refused while the group still knew the node"
+    # the new ids are the nodes' ids at the boundary
+    assert {v.leader_id for v in eng.views()} <= {2, 3, 4, 9}
+
+
+def test_replace_node_checks():
+    from dragonboat_amd.engine import InputError, RBE_E_INVALID, RBE_E_STATE
+    eng = SoaCpu(trace=True, **REPL_CASE, **CATCHUP)
+    eng.run(40)
+    with pytest.raises(InputError) as ei:  # still a member everywhere
+        eng.replace_node([2], [9])
+    assert ei.value.rc == RBE_E_STATE
+    with pytest.raises(InputError) as ei:  # the id of another slot of the group
+        eng.replace_node([2], [1])
+    assert ei.value.rc == RBE_E_INVALID
+    with pytest.raises(InputError) as ei:  # node id 0
+        eng.replace_node([2], [0])
+    assert ei.value.rc == RBE_E_INVALID
+    with pytest.raises(InputError) as ei:  # two slots of one group at once
+        eng.replace_node([1, 2], [8, 9])
+    assert ei.value.rc == RBE_E_STATE
+    sched = SoaCpu(trace=True, **dict(REPL_CASE, **MEMB))
+    with pytest.raises(InputError) as ei:  # a seeded schedule names slots
+        sched.replace_node([2], [9])
+    assert ei.value.rc == RBE_E_STATE
+    plain = SoaCpu(trace=True, **C2)
+    with pytest.raises(InputError) as ei:  # no membership change at all
+        plain.replace_node([2], [9])
+    assert ei.value.rc == RBE_E_STATE
+
+
+def test_node_ids_any_order():
+    """Node ids need not ascend with the slots: the canonical order is the
+    slot order (any fixed order is one of the reference's map orders)."""
+    n = ID_CASE["n_replicas"]
+    ids = [list(reversed(row)) for row in random_ids(ID_CASE["n_groups"], n, seed=9)]
+    eng = SoaCpu(trace=True, **ID_CASE, **CATCHUP)
+    eng.set_node_ids(0, ids)
+    ref = O.Harness(**ID_CASE)
+    lockstep_ids(eng, ref, ids, n, 150)
+    assert eng.faults()[0] == 0

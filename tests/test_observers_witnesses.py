@@ -223,3 +223,33 @@ def test_host_applies_roles():
     assert applied > 20
     assert seen >> 8 and seen & 0xFF, "no observer or no witness joined"
     assert eng.faults()[0] == 0
+
+
+def test_host_cannot_put_a_node_in_two_sets():
+    """ext_apply: an AddObserver of a voter, an AddWitness of a voter or an
+    observer, an AddObserver of a witness would put one node in two of raft's
+    maps (raft.go:1159-1180 checks only its own map), which a slot cannot
+    hold: refused at the ABI with RBE_E_INVALID, nothing staged, no fault.
+    A no-op re-add (AddObserver of an observer) is accepted."""
+    from dragonboat_amd.engine import InputError, RBE_E_INVALID
+    kw = dict(C2, n_groups=2, n_replicas=5, n_voters=3, observer_slots=0b01000,
+              witness_slots=0b10000, ext_inputs=True, ext_apply=True, membership=True)
+    eng = SoaCpu(trace=True, **dict(kw, maxm=40, ecap=256, rq_cap=32, ring=256))
+    eng.run(30)
+    # node 4 (observer slot) becomes an observer at replica 0, node 5 a witness
+    eng.apply_config_change([0], [4], [O.CC_ADD_OBSERVER])
+    eng.step()
+    eng.apply_config_change([0], [5], [O.CC_ADD_WITNESS])
+    eng.step()
+    v = eng.views()[0]
+    assert v.observers == 0b01000 and v.witnesses == 0b10000, (v.observers, v.witnesses)
+    for node, t in ((2, O.CC_ADD_OBSERVER), (3, O.CC_ADD_WITNESS), (4, O.CC_ADD_WITNESS),
+                    (5, O.CC_ADD_OBSERVER)):
+        with pytest.raises(InputError) as ei:
+            eng.apply_config_change([0], [node], [t])
+        assert ei.value.rc == RBE_E_INVALID, (node, t)
+    eng.apply_config_change([0], [4], [O.CC_ADD_OBSERVER])  # already an observer: a no-op
+    eng.step()
+    v = eng.views()[0]
+    assert v.observers == 0b01000 and v.witnesses == 0b10000
+    assert eng.faults()[0] == 0
