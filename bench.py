@@ -85,12 +85,24 @@ WORKLOADS = {
 # engine capacities (per-replica window and per-round buffers) that the oracle
 # does not have: it keeps every entry and message in growable containers
 ENGINE_ONLY = ("ring", "ecap", "maxm", "rq_cap", "rtr_cap", "dri_cap")
+CAP_DEFAULT = {"ring": 64, "ecap": 32, "maxm": 12, "rq_cap": 8, "rtr_cap": 8, "dri_cap": 8}  # rbe.h
 
 # bounded CPU-baseline samples (groups for the T-thread run, groups for the
 # 1-thread run), sized for ~5-15 s of host time each on the GPU box
 CPU_SAMPLE = {"c4": (300_000, 30_000), "c2": (10_000, 10_000), "c2m": (100_000, 10_000),
               "c3": (50_000, 5_000), "c5": (100_000, 10_000), "c2s": (100_000, 10_000),
               "c3s": (50_000, 5_000)}
+
+
+def cfg_overrides(spec):
+    """--cfg a=1,b=2: engine capacities (ENGINE_ONLY keys) for A/B runs."""
+    out = {}
+    for kv in filter(None, spec.split(",")):
+        k, v = kv.split("=", 1)
+        if k not in ENGINE_ONLY:
+            raise SystemExit(f"--cfg: {k} is not an engine capacity ({', '.join(ENGINE_ONLY)})")
+        out[k] = int(v)
+    return out
 
 
 def dist_env():
@@ -393,9 +405,10 @@ def run_host_driven(args, ws, rank, local, dist):
     beside the device time (HIP events around the step)."""
     import ctypes as C
     import numpy as np
-    from dragonboat_amd.engine import (RBE_COLLECT_REMOTE_MSGS, UPDATE_DTYPE, Engine,
-                                       RbeOutputs, RbeStepOutputs, RbeUpdateList, _check,
-                                       footprint, make_config)
+    from dragonboat_amd.engine import (EV_LEADER_UPDATED, RBE_COLLECT_REMOTE_MSGS,
+                                       RBE_COLLECT_SKIP_LOCAL, UPDATE_DTYPE, Engine, RbeOutputs,
+                                       RbeStepOutputs, RbeUpdateList, _check, footprint,
+                                       make_config)
     from dragonboat_amd.shard import reduce_results, shard_params
 
     kw, settle, desc = WORKLOADS["c4h"]
@@ -413,28 +426,39 @@ def run_host_driven(args, ws, rank, local, dist):
     ul = RbeUpdateList()
     outs = RbeOutputs()
     so = RbeStepOutputs()
-    # --c4h-all-msgs: every message copied back as well (rbe_collect_updates +
-    # rbe_collect_outputs); default: rbe_collect_step with only the messages for
-    # other engines (none here: group-per-GPU, the engine delivers them itself)
+    # --c4h-all-msgs: every Update and every message copied back
+    # (rbe_collect_updates + rbe_collect_outputs); default: rbe_collect_step
+    # with only the messages for other engines (none here: group-per-GPU, the
+    # engine delivers them itself) and only the Updates that hold work for the
+    # node besides those messages (RBE_COLLECT_SKIP_LOCAL)
     all_msgs = args.c4h_all_msgs
+    cflags = RBE_COLLECT_REMOTE_MSGS | RBE_COLLECT_SKIP_LOCAL
     leader_of = np.zeros(n_groups, dtype=np.uint64)  # leader slot + 1 per group, 0 = none
     cmd = np.frombuffer(rng.bytes(16 * len(active)), dtype=np.uint8).copy()
     ptr = lambda a, t: a.ctypes.data_as(C.POINTER(t))  # noqa: E731
     stats = {"push": 0.0, "push_abi": 0.0, "step": 0.0, "enqueue": 0.0, "out": 0.0, "reads": 0,
              "props": 0, "msgs": 0, "rtr": 0, "upd": 0}
 
+    # the node layer learns a group's leader from the listener's LeaderUpdated
+    # (event.go:93-95), which the engine reports in Update.events
+    ev_leader = np.uint32(EV_LEADER_UPDATED)
+
+    def note_leaders(rep, ups):
+        chg = (ups["events"] & ev_leader) != 0
+        if chg.any():
+            lid = ups["leader_id"][chg]
+            known = lid != 0
+            leader_of[(rep[chg][known] // np.uint64(N)).astype(np.int64)] = lid[known]
+
     def read_back():
         if not all_msgs:
-            _check(L.rbe_collect_step(h, 0, n_rep, RBE_COLLECT_REMOTE_MSGS, C.byref(so)),
-                   "rbe_collect_step")
+            _check(L.rbe_collect_step(h, 0, n_rep, cflags, C.byref(so)), "rbe_collect_step")
             n = so.n
             if n:  # the engine's pinned buffer, read in place
                 rep = np.ctypeslib.as_array(so.replica, shape=(n,))
                 ups = np.frombuffer((C.c_uint8 * (n * UPDATE_DTYPE.itemsize)).from_address(
                     C.addressof(so.updates.contents)), dtype=UPDATE_DTYPE)
-                lid = ups["leader_id"]
-                known = lid != 0
-                leader_of[(rep[known] // np.uint64(N)).astype(np.int64)] = lid[known]
+                note_leaders(rep, ups)
             return so.n_messages, so.n_ready_to_reads, n
         _check(L.rbe_collect_updates(h, 0, n_rep, C.byref(ul)), "rbe_collect_updates")
         _check(L.rbe_collect_outputs(h, 0, n_rep, C.byref(outs)), "rbe_collect_outputs")
@@ -443,30 +467,38 @@ def run_host_driven(args, ws, rank, local, dist):
             rep = np.ctypeslib.as_array(ul.replica, shape=(n,))
             ups = np.frombuffer((C.c_uint8 * (n * UPDATE_DTYPE.itemsize)).from_address(
                 C.addressof(ul.updates.contents)), dtype=UPDATE_DTYPE)
-            lid = ups["leader_id"]
-            known = lid != 0
-            leader_of[(rep[known] // np.uint64(N)).astype(np.int64)] = lid[known]
+            note_leaders(rep, ups)
         return outs.n_messages, outs.n_ready_to_reads, n
+
+    # the client workload of every round, drawn before the timed region
+    # (synthetic requests, not node-layer work): which active groups get a
+    # ReadIndex (90%) and which a proposal
+    total_rounds = settle + max(1, args.warmup) + args.steps
+    read_mask = rng.random((total_rounds, len(active))) < 0.9
+    active_i = active.astype(np.int64)
+    active_n = active * np.uint64(N)
+    one = np.ones(len(active), dtype=np.uint32)
+    zero = np.zeros(len(active), dtype=np.uint32)
+    ln = np.full(len(active), 16, dtype=np.uint32)
 
     def one_round(rnd, timed):
         t0 = time.perf_counter()
-        lg = leader_of[active.astype(np.int64)]
-        has = lg != 0
-        g = active[has]
-        reps = g * np.uint64(N) + (lg[has] - np.uint64(1))
-        is_read = rng.random(len(reps)) < 0.9
-        rr, pr = reps[is_read].copy(), reps[~is_read].copy()
-        if len(rr):
-            lo = (np.uint64(rnd + 1) << np.uint64(32)) | (rr + np.uint64(1))
-            hi = rr.copy()
+        lg = leader_of[active_i]
+        is_read = read_mask[rnd]
+        if lg.all():
+            reps = active_n + (lg - np.uint64(1))
+        else:
+            has = lg != 0
+            reps = active_n[has] + (lg[has] - np.uint64(1))
+            is_read = is_read[has]
+        rr, pr = reps[is_read], reps[~is_read]
+        if len(rr):  # ctx.Low = round << 32 | replica + 1 (never 0), ctx.High = replica
+            lo = rr + np.uint64(((rnd + 1) << 32) + 1)
         tc = time.perf_counter()
         if len(rr):
             _check(L.rbe_push_read_index(h, len(rr), ptr(rr, C.c_uint64), ptr(lo, C.c_uint64),
-                                         ptr(hi, C.c_uint64)), "rbe_push_read_index")
+                                         ptr(rr, C.c_uint64)), "rbe_push_read_index")
         if len(pr):
-            one = np.ones(len(pr), dtype=np.uint32)
-            zero = np.zeros(len(pr), dtype=np.uint32)
-            ln = np.full(len(pr), 16, dtype=np.uint32)
             _check(L.rbe_push_proposals(h, len(pr), ptr(pr, C.c_uint64), ptr(one, C.c_uint32),
                                         ptr(zero, C.c_uint32), ptr(ln, C.c_uint32),
                                         ptr(cmd, C.c_uint8)), "rbe_push_proposals")
@@ -536,7 +568,8 @@ def run_host_driven(args, ws, rank, local, dist):
                 # host part of the step call: input upload staging + launches
                 "step_enqueue_ms_per_round": stats["enqueue"] * 1e3 / K,
                 "read_back": "rbe_collect_updates + rbe_collect_outputs (every message)"
-                if all_msgs else "rbe_collect_step (messages for other engines only)",
+                if all_msgs else ("rbe_collect_step (messages for other engines only; "
+                                  "RBE_COLLECT_SKIP_LOCAL: Updates with work for the node)"),
                 "outputs_ms_per_round": stats["out"] * 1e3 / K,
                 "boundary_share": (stats["push"] + stats["out"]) / max(1e-12, wall),
                 "reads_pushed_per_round": stats["reads"] / K,
@@ -557,6 +590,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
     ap.add_argument("--groups", type=int, default=0, help="override groups per GPU")
+    ap.add_argument("--cfg", default="",
+                    help="engine capacity overrides for A/B runs, e.g. maxm=4,ecap=16 "
+                         "(recorded in the line's config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-compact", action="store_true",
                     help="c5: allocate every group's planes on every rank")
@@ -609,6 +645,7 @@ def main():
     kw = dict(kw)
     if args.groups:
         kw["n_groups"] = args.groups
+    kw.update(cfg_overrides(args.cfg))
     # group-per-GPU sharding (dragonboat_amd/shard.py): rank r steps the
     # clusters with (cid - 1) % world == r, dragonboat's FixedPartitioner rule
     cid_base, cid_stride = shard_params(rank, ws)
@@ -688,6 +725,7 @@ def main():
                 "election_rtt": 10, "heartbeat_rtt": 1,
                 "settle_rounds": settle,
                 "device_bytes_per_gpu": footprint(cfg),
+                "capacities": {k: int(getattr(cfg, k)) or CAP_DEFAULT[k] for k in ENGINE_ONLY},
             },
             "committed_entries_per_s": committed / wall_max,
             "read_confirmations_per_s": reads / wall_max,

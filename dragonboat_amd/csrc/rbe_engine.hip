@@ -307,8 +307,24 @@ __device__ __forceinline__ bool out_msg_wanted(const Params& C, u64 g, u32 d, bo
   const u64 gg = group_global(C, g);
   return gg < C.n_groups_glob && (u32)((gg + d) % C.rep_world) != C.rep_rank;
 }
+// An Update with something for the node besides the messages it carries: a
+// State change, entries to save or apply, ReadyToReads, dropped requests, a
+// Snapshot, an applied index to confirm, listener events (RBE_COLLECT_SKIP_LOCAL)
+__device__ __forceinline__ bool upd_actionable_dev(const Planes& P, u64 r, u32 round) {
+  const Upd* u = P.upd + r;
+  const uint4 c3 = reinterpret_cast<const uint4*>(u)[3];
+  const u32 flags = c3.y & 0xFFFFu, events = c3.y >> 16;
+  if ((flags & (RBE_UF_STATE_CHANGED | RBE_UF_SENT_QUIESCE | RBE_UF_SNAPSHOT | RBE_UF_APPLIED |
+                RBE_UF_HAS_UPDATE)) ||
+      events || (c3.w >> 16) != 0u)  // n_rtr
+    return true;
+  if (!(flags & UF_RANGES)) return false;
+  const Upd d = *u;  // ranges and drops
+  return d.n_drop_ent || d.n_drop_ri || d.save_lo <= d.save_hi || d.apply_lo <= d.apply_hi;
+}
 __device__ __forceinline__ void step_out_counts(const Planes& P, const Params& C, u64 r, u32 round,
-                                                bool remote, u32* f, u32* nm, u32* nr) {
+                                                u32 cflags, u32* f, u32* nm, u32* nr) {
+  const bool remote = (cflags & RBE_COLLECT_REMOTE_MSGS) != 0;
   *f = upd_has_dev(P, r, C.n, round) ? 1u : 0u;
   *nm = *nr = 0;
   if (!*f) return;
@@ -322,14 +338,20 @@ __device__ __forceinline__ void step_out_counts(const Planes& P, const Params& C
     if (out_msg_wanted(C, g, d, remote)) m += (pc & 0x7Fu) + ((pc >> 7) & 0x7Fu);
   }
   *nm = m;
+  // RBE_COLLECT_SKIP_LOCAL: an Update whose only content is messages the
+  // engine delivers itself is left out (nothing to persist, apply or send)
+  if ((cflags & RBE_COLLECT_SKIP_LOCAL) && m == 0 && !upd_actionable_dev(P, r, round)) {
+    *f = 0;
+    return;
+  }
   const Upd& x = P.upd[r];
   *nr = x.round == round - 1u ? (x.n_rtr < C.rtr_cap ? x.n_rtr : C.rtr_cap) : 0u;
 }
 __global__ __launch_bounds__(kBlock) void k_cs_count(Planes P, Params C, u64 first, u64 count,
-                                                     u32 round, bool remote, u32* bsum) {
+                                                     u32 round, u32 cflags, u32* bsum) {
   const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
   u32 f = 0, nm = 0, nr = 0;
-  if (i < count) step_out_counts(P, C, first + i, round, remote, &f, &nm, &nr);
+  if (i < count) step_out_counts(P, C, first + i, round, cflags, &f, &nm, &nr);
   u32 tf, tm, tr;
   block_excl_scan(f, &tf);
   block_excl_scan(nm, &tm);
@@ -341,13 +363,14 @@ __global__ __launch_bounds__(kBlock) void k_cs_count(Planes P, Params C, u64 fir
   }
 }
 __global__ __launch_bounds__(kBlock) void k_cs_write(Planes P, Params C, u64 first, u64 count,
-                                                     u32 round, bool remote, const u64* pre,
+                                                     u32 round, u32 cflags, const u64* pre,
                                                      u64* rep, rbe_update* ou, u64* moff,
                                                      rbe_message* om, u64* roff,
                                                      rbe_ready_to_read* orr, u64 n_tot) {
   const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+  const bool remote = (cflags & RBE_COLLECT_REMOTE_MSGS) != 0;
   u32 f = 0, nm = 0, nr = 0;
-  if (i < count) step_out_counts(P, C, first + i, round, remote, &f, &nm, &nr);
+  if (i < count) step_out_counts(P, C, first + i, round, cflags, &f, &nm, &nr);
   u32 t;
   const u64 at = pre[3 * blockIdx.x] + block_excl_scan(f, &t);
   const u64 bm = pre[3 * blockIdx.x + 1] + block_excl_scan(nm, &t);
@@ -550,6 +573,28 @@ __global__ __launch_bounds__(kBlock) void k_xchg_put_ent(Planes P, Params C, u32
 }
 
 // ------------------------------------------------------------------ engine
+// Pinned host memory for the input staging vectors (HostInputsT): an upload
+// from them is a DMA with no host copy.  A failed allocation throws, as
+// std::allocator's does.
+template <class T>
+struct PinnedAlloc {
+  using value_type = T;
+  PinnedAlloc() = default;
+  template <class U>
+  PinnedAlloc(const PinnedAlloc<U>&) {}
+  T* allocate(size_t n) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, n * sizeof(T), hipHostMallocDefault) != hipSuccess || !p)
+      throw std::bad_alloc();
+    return (T*)p;
+  }
+  void deallocate(T* p, size_t) { HIP_IGNORE(hipHostFree(p)); }
+  template <class U>
+  bool operator==(const PinnedAlloc<U>&) const { return true; }
+  template <class U>
+  bool operator!=(const PinnedAlloc<U>&) const { return false; }
+};
+
 struct rbe_engine {
   rbe_config cfg;
   Params C;
@@ -571,12 +616,20 @@ struct rbe_engine {
                              // 3 both (default: triage + one merged fast launch)
   Lists L;                   // per-round work lists (triage → fast → full)
   u32* xcount = nullptr;     // replica-per-GPU pack counters [rep_world * XS_NUM]
-  HostInputs hin;            // rbe_push_* staged for the next step (rbe_host.h)
+  // rbe_push_* staged for the next step (rbe_host.h); its replica, record and
+  // entry vectors live in pinned memory and go to the device as they are,
+  // alternating with the `up_*` spares (flush_inputs)
+  HostInputsT<PinnedAlloc> hin;
+  HostInputsT<PinnedAlloc>::UpVec<u64> up_reps;
+  HostInputsT<PinnedAlloc>::UpVec<ExtIn> up_recs;
+  HostInputsT<PinnedAlloc>::UpVec<Ent> up_ents;
   u64 in_used = 0;
-  u8* in_pinned = nullptr;   // pinned upload buffer of the staged input
-  u8* in_dev = nullptr;      // its device copy (replicas, records, applied pairs)
-  u64 in_bytes = 0;          // capacity of both
-  hipEvent_t in_ev = nullptr;  // the last upload out of in_pinned has finished
+  u8* in_pinned[2] = {nullptr, nullptr};  // pinned staging of the small input parts, by
+  u64 in_pbytes[2] = {0, 0};              // flush parity, and their capacities
+  u8* in_dev = nullptr;      // the device copy (replicas, records, applied pairs, ...)
+  u64 in_bytes = 0;
+  hipEvent_t in_ev[2] = {nullptr, nullptr};  // the uploads of flush parity 0 / 1 have finished
+  u32 in_slot = 0;
   u8* heap = nullptr;        // payload heap (cfg.heap_bytes; positions in hin.heap)
   u64* heap_dev = nullptr;   // [0] heap head after the last upload (Planes::heap_head),
                              // [1] k_heap_low result
@@ -916,8 +969,10 @@ int rbe_destroy(rbe_engine* e) {
   if (e->d_clk) HIP_IGNORE(hipFree(e->d_clk));
   if (e->ev0) HIP_IGNORE(hipEventDestroy(e->ev0));
   if (e->ev1) HIP_IGNORE(hipEventDestroy(e->ev1));
-  if (e->in_ev) HIP_IGNORE(hipEventDestroy(e->in_ev));
-  if (e->in_pinned) HIP_IGNORE(hipHostFree(e->in_pinned));
+  for (int i = 0; i < 2; i++) {
+    if (e->in_ev[i]) HIP_IGNORE(hipEventDestroy(e->in_ev[i]));
+    if (e->in_pinned[i]) HIP_IGNORE(hipHostFree(e->in_pinned[i]));
+  }
   if (e->in_dev) HIP_IGNORE(hipFree(e->in_dev));
   if (e->out_dev) HIP_IGNORE(hipFree(e->out_dev));
   if (e->out_host) HIP_IGNORE(hipHostFree(e->out_host));
@@ -958,7 +1013,10 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   }
   HIP_IGNORE(hipEventCreate(&e->ev0));
   HIP_IGNORE(hipEventCreate(&e->ev1));
-  HIP_IGNORE(hipEventCreateWithFlags(&e->in_ev, hipEventDisableTiming));
+  for (int i = 0; i < 2; i++) {
+    HIP_IGNORE(hipEventCreateWithFlags(&e->in_ev[i], hipEventDisableTiming));
+    HIP_IGNORE(hipEventRecord(e->in_ev[i], e->stream));
+  }
   u64 parts[kPlaneAllocs];
   bytes_of(C, parts);
   void* ptrs[kPlaneAllocs];
@@ -1163,59 +1221,70 @@ static int launch_iso(rbe_engine* e) {
 // Upload the input staged since the last step (rbe_host.h) through the pinned
 // buffer in one copy and scatter it on device, ahead of the round's kernels.
 static int flush_inputs(rbe_engine* e) {
-  HostInputs& h = e->hin;
+  auto& h = e->hin;
   if (h.empty()) {
     h.heap.settle();
     return RBE_OK;
   }
+  const u32 sl = e->in_slot;
+  HIP_OK(hipEventSynchronize(e->in_ev[sl]));  // the upload two flushes back is out of slot sl
+  const u64 n = h.reps.size(), na = h.app_rep.size(), nc = h.commits.size(),
+            ns = h.snaps.size(), nh = h.heap.head - h.heap.flushed;
+  // device layout: replicas | records (16-B aligned) | applied replicas |
+  // applied values | commits | snapshot records; the first two come straight
+  // from the pinned staging vectors, the rest through in_pinned[sl], which
+  // also carries the payload-heap bytes of the staged proposals
+  const u64 o_rec = (n * sizeof(u64) + 15) & ~15ull;
+  const u64 o_ar = o_rec + n * sizeof(ExtIn), o_av = o_ar + na * sizeof(u64);
+  const u64 o_cr = o_av + na * sizeof(u64);
+  const u64 o_sr = o_cr + nc * sizeof(CommitRec);
+  const u64 total = o_sr + ns * sizeof(SnapRec);
+  const u64 small = total - o_ar, pneed = small + nh + 64;
+  if (total + 64 > e->in_bytes) {
+    if (e->in_dev) HIP_OK(hipFree(e->in_dev));
+    e->in_dev = nullptr;
+    e->in_bytes = 0;
+    const u64 cap = (total + 64) * 2;
+    HIP_OK(hipMalloc((void**)&e->in_dev, cap));
+    e->in_bytes = cap;
+  }
+  if (pneed > e->in_pbytes[sl]) {
+    if (e->in_pinned[sl]) HIP_OK(hipHostFree(e->in_pinned[sl]));
+    e->in_pinned[sl] = nullptr;
+    e->in_pbytes[sl] = 0;
+    HIP_OK(hipHostMalloc((void**)&e->in_pinned[sl], pneed * 2, hipHostMallocDefault));
+    e->in_pbytes[sl] = pneed * 2;
+  }
+  u8* b = e->in_pinned[sl];
   // payload heap bytes of the staged proposals: positions [flushed, head),
   // split where they cross the end of the ring
-  for (u64 p = h.heap.flushed; p < h.heap.head;) {
-    const u64 at = p % h.heap.cap, len = std::min(h.heap.head - p, h.heap.cap - at);
-    HIP_OK(hipMemcpyAsync(e->heap + at, h.heap.stage.data() + (p - h.heap.flushed), len,
-                          hipMemcpyHostToDevice, e->stream));
-    p += len;
+  if (nh) {
+    memcpy(b + small, h.heap.stage.data(), nh);
+    for (u64 p = h.heap.flushed; p < h.heap.head;) {
+      const u64 at = p % h.heap.cap, len = std::min(h.heap.head - p, h.heap.cap - at);
+      HIP_OK(hipMemcpyAsync(e->heap + at, b + small + (p - h.heap.flushed), len,
+                            hipMemcpyHostToDevice, e->stream));
+      p += len;
+    }
   }
   if (h.heap.head != e->heap_head_host) {  // Planes::heap_head for the lapped-record checks
     e->heap_head_host = h.heap.head;
     HIP_OK(hipMemcpyAsync(e->heap_dev, &e->heap_head_host, sizeof(u64), hipMemcpyHostToDevice,
                           e->stream));
   }
-  const u64 n = h.reps.size(), na = h.app_rep.size(), nc = h.commits.size(),
-            ns = h.snaps.size();
-  const u64 need = n * (sizeof(u64) + sizeof(ExtIn)) + na * 2 * sizeof(u64) +
-                   nc * sizeof(CommitRec) + ns * sizeof(SnapRec) + 64;
-  HIP_OK(hipEventSynchronize(e->in_ev));  // the previous upload is out of in_pinned
-  if (need > e->in_bytes) {
-    if (e->in_pinned) HIP_OK(hipHostFree(e->in_pinned));
-    if (e->in_dev) HIP_OK(hipFree(e->in_dev));
-    e->in_pinned = nullptr;
-    e->in_dev = nullptr;
-    e->in_bytes = 0;
-    const u64 cap = need * 2;
-    HIP_OK(hipHostMalloc((void**)&e->in_pinned, cap, hipHostMallocDefault));
-    HIP_OK(hipMalloc((void**)&e->in_dev, cap));
-    e->in_bytes = cap;
-  }
-  // layout: replicas | records (16-B aligned) | applied replicas | applied values | commits
-  // | snapshot records
-  u8* b = e->in_pinned;
-  const u64 o_rec = (n * sizeof(u64) + 15) & ~15ull;
-  const u64 o_ar = o_rec + n * sizeof(ExtIn), o_av = o_ar + na * sizeof(u64);
-  const u64 o_cr = o_av + na * sizeof(u64);
-  const u64 o_sr = o_cr + nc * sizeof(CommitRec);
-  const u64 total = o_sr + ns * sizeof(SnapRec);
   if (n) {
-    memcpy(b, h.reps.data(), n * sizeof(u64));
-    memcpy(b + o_rec, h.recs.data(), n * sizeof(ExtIn));
+    HIP_OK(hipMemcpyAsync(e->in_dev, h.reps.data(), n * sizeof(u64), hipMemcpyHostToDevice,
+                          e->stream));
+    HIP_OK(hipMemcpyAsync(e->in_dev + o_rec, h.recs.data(), n * sizeof(ExtIn),
+                          hipMemcpyHostToDevice, e->stream));
   }
   if (na) {
-    memcpy(b + o_ar, h.app_rep.data(), na * sizeof(u64));
-    memcpy(b + o_av, h.app_val.data(), na * sizeof(u64));
+    memcpy(b + (o_ar - o_ar), h.app_rep.data(), na * sizeof(u64));
+    memcpy(b + (o_av - o_ar), h.app_val.data(), na * sizeof(u64));
   }
-  if (nc) memcpy(b + o_cr, h.commits.data(), nc * sizeof(CommitRec));
-  if (ns) memcpy(b + o_sr, h.snaps.data(), ns * sizeof(SnapRec));
-  if (total) HIP_OK(hipMemcpyAsync(e->in_dev, b, total, hipMemcpyHostToDevice, e->stream));
+  if (nc) memcpy(b + (o_cr - o_ar), h.commits.data(), nc * sizeof(CommitRec));
+  if (ns) memcpy(b + (o_sr - o_ar), h.snaps.data(), ns * sizeof(SnapRec));
+  if (small) HIP_OK(hipMemcpyAsync(e->in_dev + o_ar, b, small, hipMemcpyHostToDevice, e->stream));
   if (!h.ents.empty())
     HIP_OK(hipMemcpyAsync(e->P.in_ents, h.ents.data(), h.ents.size() * sizeof(Ent),
                           hipMemcpyHostToDevice, e->stream));
@@ -1236,11 +1305,14 @@ static int flush_inputs(rbe_engine* e) {
                        (const SnapRec*)(e->in_dev + o_sr), ps, e->C, e->L, e->round & 1u);
     HIP_OK(hipGetLastError());
   }
-  HIP_OK(hipEventRecord(e->in_ev, e->stream));
-  // the entries and heap bytes came from pageable memory: wait for those
-  // copies before the vectors are reused (inputs are the host-driven path, not
-  // the bench path)
-  if (!h.ents.empty() || !h.heap.stage.empty()) HIP_OK(hipEventSynchronize(e->in_ev));
+  HIP_OK(hipEventRecord(e->in_ev[sl], e->stream));
+  // the staging vectors just uploaded become the spares; the spares, whose
+  // upload (the last flush, slot sl ^ 1) has long finished, take the next input
+  h.reps.swap(e->up_reps);
+  h.recs.swap(e->up_recs);
+  h.ents.swap(e->up_ents);
+  HIP_OK(hipEventSynchronize(e->in_ev[sl ^ 1u]));
+  e->in_slot = sl ^ 1u;
   h.clear();
   return RBE_OK;
 }
@@ -2155,14 +2227,13 @@ int rbe_collect_outputs(rbe_engine* e, uint64_t first, uint64_t count, rbe_outpu
 int rbe_collect_step(rbe_engine* e, uint64_t first, uint64_t count, uint32_t flags,
                      rbe_step_outputs* out) {
   if (!e || !out || count == 0 || first >= e->C.n_rep || count > e->C.n_rep - first ||
-      (flags & ~RBE_COLLECT_REMOTE_MSGS))
+      (flags & ~(RBE_COLLECT_REMOTE_MSGS | RBE_COLLECT_SKIP_LOCAL)))
     return RBE_E_INVALID;
   memset(out, 0, sizeof(*out));
   out->first = first;
   out->count = count;
   if (e->round == 0) return RBE_E_STATE;
   HIP_OK(hipSetDevice(e->device));
-  const bool remote = (flags & RBE_COLLECT_REMOTE_MSGS) != 0;
   const u32 nb = grid_for(count);
   auto al = [](u64 x) { return (x + 255) & ~255ull; };
   // device scratch: block sums (triples) | block prefixes (+ totals) | then the
@@ -2173,7 +2244,7 @@ int rbe_collect_step(rbe_engine* e, uint64_t first, uint64_t count, uint32_t fla
   if (rc) return rc;
   u64* pre = (u64*)(e->cs_dev + o_pre);
   hipLaunchKernelGGL(k_cs_count, dim3(nb), dim3(kBlock), 0, e->stream, e->P, e->C, (u64)first,
-                     (u64)count, e->round, remote, (u32*)e->cs_dev);
+                     (u64)count, e->round, flags, (u32*)e->cs_dev);
   if ((rc = launch_scan<3>(e->stream, (const u32*)e->cs_dev, nb, pre))) return rc;
   u64 tot[3];
   HIP_OK(hipMemcpyAsync(tot, pre + 3ull * nb, sizeof(tot), hipMemcpyDeviceToHost, e->stream));
@@ -2194,7 +2265,7 @@ int rbe_collect_step(rbe_engine* e, uint64_t first, uint64_t count, uint32_t fla
   }
   u8* d = e->cs_dev;
   hipLaunchKernelGGL(k_cs_write, dim3(nb), dim3(kBlock), 0, e->stream, e->P, e->C, (u64)first,
-                     (u64)count, e->round, remote, (const u64*)(d + o_pre), (u64*)(d + o_rep),
+                     (u64)count, e->round, flags, (const u64*)(d + o_pre), (u64*)(d + o_rep),
                      (rbe_update*)(d + o_upd), (u64*)(d + o_moff), (rbe_message*)(d + o_msg),
                      (u64*)(d + o_roff), (rbe_ready_to_read*)(d + o_rtr), n);
   HIP_OK(hipGetLastError());

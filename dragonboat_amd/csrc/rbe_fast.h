@@ -68,31 +68,6 @@ __device__ __forceinline__ unsigned long long rbe_rstamp() {
 #define RBE_PHASE_ADD(role, i, a, b)
 #endif
 
-// Outbound messages staged in LDS (k_fast_both, RBE_MSG_STAGE): send() puts
-// a message's 64 B in the lane's next LDS slot and its destination beside it,
-// and after the step the wave writes every staged message back cooperatively,
-// four lanes per message: one 64-B write request per message instead of four
-// scattered 16-B ones (messages are over half of the fast kernel's write
-// requests on C4).  LDS writes count in lgkmcnt, so staging never waits
-// behind the lane's stores.  A lane with more than kMsgStage messages in one
-// step writes the rest directly.  Device build only; the host build always
-// writes directly.
-#ifndef RBE_MSG_STAGE
-#define RBE_MSG_STAGE 0
-#endif
-constexpr u32 kMsgStage = 2;
-constexpr u32 kMsgStageLanes = 256;  // one slot row per thread of a 256-thread block
-#if defined(__HIPCC__) || defined(__HIP__)
-__device__ __forceinline__ Msg (&msg_stage_slots())[kMsgStage][kMsgStageLanes] {
-  __shared__ Msg s_slots[kMsgStage][kMsgStageLanes];
-  return s_slots;
-}
-__device__ __forceinline__ u32 (&msg_stage_dst())[kMsgStage][kMsgStageLanes] {
-  __shared__ u32 s_dst[kMsgStage][kMsgStageLanes];
-  return s_dst;
-}
-#endif
-
 // Wait until every outstanding load of the lane has returned (a no-op on the
 // host build).  Placed between the gather and the first store of a fast step.
 RBE_HD void rbe_wait_all_loads() {
@@ -101,66 +76,23 @@ RBE_HD void rbe_wait_all_loads() {
 #endif
 }
 
-// max inbound messages per sender held in registers
-#ifndef RBE_LEAD_MAXM3
-#define RBE_LEAD_MAXM3 4
-#endif
 #ifndef RBE_LDS_INBOX
 #define RBE_LDS_INBOX 1
 #endif
-// waves per SIMD of the fast kernels (launch bounds): groups of 3 at two;
-// wider groups (4..6) keep up to (N-1) x 5 inbound headers and N remote slots
-// per leader lane, which at two waves spill hundreds of bytes per lane to
-// scratch, so RBE_FAST_WAVES_WIDE may run them at one wave with the leader's
-// inbox in LDS (a whole CU's LDS for one block)
+// waves per SIMD of the fast kernels (launch bounds), every group size: two
+// (groups of 4-5 spill their wider remote state at two waves, and one wave
+// measured slower still: DESIGN.md §9)
 #ifndef RBE_FAST_WAVES
 #define RBE_FAST_WAVES 2
 #endif
-#ifndef RBE_FAST_WAVES_WIDE
-#define RBE_FAST_WAVES_WIDE RBE_FAST_WAVES
-#endif
 template <int N>
-constexpr int kFastWaves = N <= 3 ? RBE_FAST_WAVES : RBE_FAST_WAVES_WIDE;
+constexpr int kFastWaves = RBE_FAST_WAVES;
 template <int N>
 struct FastCaps {
-  static constexpr u32 MAXM = N <= 3 ? RBE_LEAD_MAXM3 : 5;  // leader: per follower
+  static constexpr u32 MAXM = N <= 3 ? 4 : 5;  // leader: inbound messages per follower
   static constexpr u32 FMAXM = 6;              // follower: from its leader
   static constexpr u32 RQ = 3;                 // readIndex queue entries in registers
 };
-
-// Wave-cooperative staging of a lane's state rows (k_fast_both).
-// Every lane writes its Hot/Core/Upd/remote rows whole at the end of a fast
-// step, each with 2-4 scattered 16-B stores, i.e. one L2 write request per
-// store and lane.  With STG_OUT the step writes those rows into its LDS row
-// instead and the whole wave writes them out afterwards, four lanes per 64-B
-// row (stage_out_wave), so one wave instruction makes 16 full-row requests
-// instead of 64 partial ones.  STG_IN also takes the step's Hot/Core/remote
-// reads from the row, loaded the same way before the step (measured slower:
-// it adds a dependent load level).  The host build stages one row at a time
-// (stage_row_in/out) so the CPU tier runs the same step code.
-enum : int { STG_OUT = 1, STG_IN = 2 };  // which side of a fast step uses the staged row
-template <int N>
-struct alignas(16) StageRow {
-  Core core;
-  Upd upd;
-  Hot hot;
-  RemoteMN rem[N];
-};
-template <int N>
-RBE_HD void stage_row_in(const Planes& P, u64 r, bool lead, StageRow<N>& s) {
-  s.core = P.core[r];
-  s.hot = P.hot[r];
-  if (lead)
-    for (u32 i = 0; i < N; i++) s.rem[i] = P.rem[r * N + i];
-}
-template <int N>
-RBE_HD void stage_row_out(const Planes& P, u64 r, bool lead, const StageRow<N>& s) {
-  P.core[r] = s.core;
-  P.hot[r] = s.hot;
-  P.upd[r] = s.upd;
-  if (lead)
-    for (u32 i = 0; i < N; i++) P.rem[r * N + i] = s.rem[i];
-}
 
 // one inbound message, the fields a steady-state handler reads
 struct InMsg {
@@ -224,8 +156,6 @@ struct FastOut {
   // bump, which puts the counter array in scratch memory — and a scratch
   // reload after the lane's first store waits for every store before it
   u32 fault0, n_out, n_drop_msg, n_ent_out;
-  u32 n_staged;  // messages staged in LDS this step (msg_stage)
-  bool msg_stage;
   u32 events;  // EV_* of the step (Upd::events)
 
   RBE_HD u32 get_pc(u32 d) const {
@@ -299,18 +229,7 @@ struct FastOut {
       add_pc(d, 1u << 7);
     }
 #ifndef RBE_DIAG_NO_MSG_STORES
-    const u64 at = ((g * N + k) * N + d) * (u64)C.maxm + slot;
-    Msg* to = &P.msgs[par][at];
-#if defined(__HIP_DEVICE_COMPILE__)
-    // one store path either way (a generic pointer into LDS or HBM): two
-    // store paths at every inlined send site cost registers and code
-    if (msg_stage && n_staged < kMsgStage) {  // `at` fits 32 bits (rbe_create checks)
-      msg_stage_dst()[n_staged][threadIdx.x] = (u32)at;
-      to = &msg_stage_slots()[n_staged][threadIdx.x];
-      n_staged++;
-    }
-#endif
-    *to = m;
+    P.msgs[par][((g * N + k) * N + d) * (u64)C.maxm + slot] = m;
 #endif
   }
   template <class CT>
@@ -437,11 +356,10 @@ RBE_HD void fast_node_snapshot(const Planes& P, const Params& C, CT& ctr,
 // Common epilogue: stepNode's quiesce send, getUpdate/Commit, the trace digest,
 // the Update record, this round's outbox counts, Hot/Core write-back.
 // Mirrors the tail of Lane::run().
-template <int N, bool TRACE, int STG = 0, class CT>
+template <int N, bool TRACE, class CT>
 RBE_HD void fast_finish(const Planes& P, const Params& C, CT& ctr, FastOut<N, TRACE>& o,
                         FastQ& q, u8 role, u8 flags, Hot h, Core c, u32 etick, u32 htick,
-                        u64 committed0, u64 digest0, StageRow<N>* sr = nullptr,
-                        u32 core_dirty = 0xFu) {
+                        u64 committed0, u64 digest0, u32 core_dirty = 0xFu) {
   const u64 r = o.r;
   // stepNode: sendEnterQuiesceMessages (node.go:873-886)
   const bool send_q = q.qnew;
@@ -548,16 +466,15 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, CT& ctr, FastOut<N, TR
   u.fault = o.fault;
   ctr.v[C_FAULTS] += popc8(o.fault & ~o.fault0 & 0xFFu);
   // chunks 0-2 only when they carry something (Upd, rbe_types.h)
-  const bool ranges = TRACE || (STG & STG_OUT) != 0 || u.save_lo <= u.save_hi ||
-                      u.apply_lo <= u.apply_hi || o.n_drop_ri != 0;
+  const bool ranges = TRACE || u.save_lo <= u.save_hi || u.apply_lo <= u.apply_hi ||
+                      o.n_drop_ri != 0;
   u.flags = (u16)((c.committed != committed0 ? UF_STATE_CHANGED : 0u) |
                   (send_q ? UF_SENT_QUIESCE : 0u) | (ranges ? UF_RANGES : 0u));
   u.events = (u16)o.events;
   u.round = o.round_;
   u.cc_acc = 0;
 #ifndef RBE_DIAG_NO_STATE_STORES
-  if constexpr ((STG & STG_OUT) != 0) sr->upd = u;
-  else if (ranges) P.upd[r] = u;
+  if (ranges) P.upd[r] = u;
   else __builtin_memcpy((char*)&P.upd[r] + 48, (const char*)&u + 48, 16);
   // this sender's outbox header: stamp + the N count words, one 16-B store
   {
@@ -573,16 +490,11 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, CT& ctr, FastOut<N, TR
   h.q_quiesced_since = q.qs;
   h.q_no_activity_since = q.nas;
   h.q_exit_quiesce_tick = q.eqt;
-  if constexpr ((STG & STG_OUT) != 0) {
-    sr->hot = h;
-    sr->core = c;
-  } else {
-    P.hot[r] = h;
+  P.hot[r] = h;
 #pragma unroll
-    for (u32 i = 0; i < 4; i++)
-      if (core_dirty & (1u << i))
-        __builtin_memcpy((char*)&P.core[r] + 16 * i, (const char*)&c + 16 * i, 16);
-  }
+  for (u32 i = 0; i < 4; i++)
+    if (core_dirty & (1u << i))
+      __builtin_memcpy((char*)&P.core[r] + 16 * i, (const char*)&c + 16 * i, 16);
   P.idle[r] = idle_byte(C, role, flags, q.qs);
 #endif
 }
@@ -593,9 +505,9 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, CT& ctr, FastOut<N, TR
 //   inbox (ascending sender; Quiesce marker, then the sender's messages) →
 //   local ReadIndex → tick → proposal, each followed by the deferred fan-out
 //   (Replicate sends in ascending slot order, heartbeats, readIndex confirm).
-template <int N, bool TRACE, int STG = 0, bool AUX = false, bool MSG = false, class CT>
+template <int N, bool TRACE, bool AUX = false, class CT>
 RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT& ctr,
-                      StageRow<N>* sr = nullptr, u32 aux = 0, u32* staged = nullptr) {
+                      u32 aux = 0) {
   const u32 round = ck.round;
   using Cap = FastCaps<N>;
   constexpr u32 Q = N / 2 + 1;
@@ -609,15 +521,8 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   // ---- gather, level 1: independent loads
   RBE_RSTAMP(rt0);
   RBE_STAMP(t0);
-  Hot h;
-  Core c;
-  if constexpr ((STG & STG_IN) != 0) {
-    h = materialize_hot(sr->hot, C, ck.tclk);
-    c = sr->core;
-  } else {
-    h = load_hot(P, C, r, ck.tclk);
-    c = P.core[r];
-  }
+  Hot h = load_hot(P, C, r, ck.tclk);
+  Core c = P.core[r];
   u64 match[N], next[N];
   u32 st[N];
   // remote slots whose (match, next, state) changed this round: the scatter
@@ -626,9 +531,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   u32 rdirty = 0;
 #pragma unroll
   for (u32 s = 0; s < N; s++) {
-    RemoteMN x;
-    if constexpr ((STG & STG_IN) != 0) x = sr->rem[s];
-    else x = P.rem[r * N + s];
+    const RemoteMN x = P.rem[r * N + s];
     match[s] = x.match;
     next[s] = x.next;
     st[s] = P.rem_st[r * N + s];
@@ -849,8 +752,6 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   o.g = g;
   o.k = k;
   o.par = par;
-  o.n_staged = 0;
-  o.msg_stage = MSG;
   o.self = k + 1;
   o.round_ = round;
   o.iso = round < until ? isom : (u8)0;
@@ -1306,10 +1207,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
     RemoteMN x;
     x.match = match[s];
     x.next = next[s];
-    if constexpr ((STG & STG_OUT) != 0) {
-      sr->rem[s] = x;
-      P.rem_st[r * N + s] = (u8)st[s];
-    } else if (rdirty & (1u << s)) {
+    if (rdirty & (1u << s)) {
       P.rem[r * N + s] = x;
       P.rem_st[r * N + s] = (u8)st[s];
     }
@@ -1332,9 +1230,8 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   if ((u8)rq_h != c.rq_head || (u8)rq_n != c.rq_count) cdirty |= 4u;
   c.rq_head = (u8)rq_h;
   c.rq_count = (u8)rq_n;
-  fast_finish<N, TRACE, STG>(P, C, ctr, o, q, R_Leader, flags, h, c, etick, htick, committed0,
-                                digest0, sr, cdirty);
-  if constexpr (MSG) *staged = o.n_staged;
+  fast_finish<N, TRACE>(P, C, ctr, o, q, R_Leader, flags, h, c, etick, htick, committed0,
+                        digest0, cdirty);
   RBE_STAMP(t5);
   RBE_RSTAMP(rt5);
   RBE_PHASE_ADD(0, 5, rt0, rt5);
@@ -1353,9 +1250,9 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
 // One steady-state follower round: inbox from the known leader only
 // (Replicate / Heartbeat / ReadIndexResp of the current term), no client
 // input, a tick that does not start an election.
-template <int N, bool TRACE, int STG = 0, bool AUX = false, bool MSG = false, class CT>
+template <int N, bool TRACE, bool AUX = false, class CT>
 RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT& ctr,
-                      StageRow<N>* sr = nullptr, u32 aux = 0, u32* staged = nullptr) {
+                      u32 aux = 0) {
   const u32 round = ck.round;
   using Cap = FastCaps<N>;
   if constexpr (!kFastN<N>) {
@@ -1367,15 +1264,8 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   // ---- gather, level 1
   RBE_RSTAMP(rt0);
   RBE_STAMP(t0);
-  Hot h;
-  Core c;
-  if constexpr ((STG & STG_IN) != 0) {
-    h = materialize_hot(sr->hot, C, ck.tclk);
-    c = sr->core;
-  } else {
-    h = load_hot(P, C, r, ck.tclk);
-    c = P.core[r];
-  }
+  Hot h = load_hot(P, C, r, ck.tclk);
+  Core c = P.core[r];
   u32 pcin[N];
   // With AUX the count words came with the work-list entry (inbound_aux):
   // the messages of the one sender that has any (the leader, checked below)
@@ -1536,8 +1426,6 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   o.g = g;
   o.k = k;
   o.par = par;
-  o.n_staged = 0;
-  o.msg_stage = MSG;
   o.self = k + 1;
   o.round_ = round;
   o.iso = round < until ? isom : (u8)0;
@@ -1679,9 +1567,8 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   cdirty |= lchg ? 4u : 0u;
   o.event_if(lchg, EV_LEADER_UPDATED);
   c.leader = n_in ? (u8)lid : c.leader;
-  fast_finish<N, TRACE, STG>(P, C, ctr, o, q, R_Follower, flags, h, c, etick, htick, committed0,
-                        digest0, sr, cdirty);
-  if constexpr (MSG) *staged = o.n_staged;
+  fast_finish<N, TRACE>(P, C, ctr, o, q, R_Follower, flags, h, c, etick, htick, committed0,
+                        digest0, cdirty);
   RBE_STAMP(t5);
   RBE_RSTAMP(rt5);
   RBE_PHASE_ADD(1, 5, rt0, rt5);
@@ -1696,12 +1583,11 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
 }
 
 // the fast step of one role (k_round, k_fast_list)
-template <int N, bool TRACE, int MODE, int STG = 0, bool AUX = false, bool MSG = false, class CT>
+template <int N, bool TRACE, int MODE, bool AUX = false, class CT>
 RBE_HD bool step_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT& ctr,
-                      StageRow<N>* sr = nullptr, u32 aux = 0, u32* staged = nullptr) {
-  if constexpr (MODE == MODE_LEAD)
-    return lead_fast<N, TRACE, STG, AUX, MSG>(P, C, r, ck, ctr, sr, aux, staged);
-  else return foll_fast<N, TRACE, STG, AUX, MSG>(P, C, r, ck, ctr, sr, aux, staged);
+                      u32 aux = 0) {
+  if constexpr (MODE == MODE_LEAD) return lead_fast<N, TRACE, AUX>(P, C, r, ck, ctr, aux);
+  else return foll_fast<N, TRACE, AUX>(P, C, r, ck, ctr, aux);
 }
 
 }  // namespace rbe

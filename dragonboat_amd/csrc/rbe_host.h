@@ -17,6 +17,7 @@
 #include <cstring>
 #include <functional>
 #include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "../../include/rbe.h"
@@ -474,26 +475,35 @@ inline int launch_rows(const Params& C, HostHeap& heap, u64 n, const u64* replic
   return RBE_OK;
 }
 
-struct HostInputs {
+// The input staged between two steps.  `Alloc` backs the three record
+// vectors the upload copies whole (replicas, records, entries): the HIP engine
+// gives them pinned host memory, so they go to the device without a host copy
+// (rbe_engine.hip flush_inputs), the host build plain heap memory.
+template <template <class> class Alloc>
+struct HostInputsT {
+  template <class T>
+  using UpVec = std::vector<T, Alloc<T>>;
   u64 n_rep = 0;
   u32 n = 0;
   u32 in_cap = 0;
-  // [n_rep] per replica: index into recs (~0u = nothing staged) and the
-  // duplicate-check stamp of the current call, side by side so a push touches
-  // one cache line per replica
+  // [n_rep] per replica: index into recs, valid when `gen` is the current
+  // staging generation (so clear() bumps the generation instead of visiting
+  // every staged replica), and the duplicate-check stamp of the current call,
+  // side by side so a push touches one cache line per replica
   struct SlotMark {
-    u32 slot, mark;
+    u32 slot, gen, mark;
   };
   std::vector<SlotMark> sm;
   u32 epoch = 0;
-  std::vector<u64> reps;    // staged replicas ...
-  std::vector<ExtIn> recs;  // ... and their input records
-  std::vector<Ent> ents;    // staged proposal entries (Planes::in_ents)
+  u32 gen = 1;
+  UpVec<u64> reps;    // staged replicas ...
+  UpVec<ExtIn> recs;  // ... and their input records
+  UpVec<Ent> ents;    // staged proposal entries (Planes::in_ents)
   // staged replica-value pairs: rbe_notify_applied values, and with bit 63 of
   // the replica word set, rbe_set_apply_ready flags (value 1 = ready)
   std::vector<u64> app_rep, app_val;
   struct AppSlot {
-    u32 applied, ready;  // index into app_rep, ~0u = none staged
+    u32 applied, ready, gen;  // index into app_rep (this generation), ~0u = none staged
   };
   std::vector<AppSlot> app_slot;  // [n_rep]
   std::vector<u64> applied;  // [n_rep] host mirror of Planes::applied (the host is its only writer)
@@ -544,7 +554,8 @@ struct HostInputs {
       for (u32 s = 0; s < n; s++) {
         const u64 r = g * n + s;
         if (r != replica[i] && (ids.empty() ? s + 1 : ids[r]) == id[i]) return RBE_E_INVALID;
-        if (sm[r].slot != ~0u || app_slot[r].applied != ~0u || app_slot[r].ready != ~0u ||
+        if (slot_of(r) != ~0u || (app_slot[r].gen == gen && (app_slot[r].applied != ~0u ||
+                                                              app_slot[r].ready != ~0u)) ||
             committing[r] || snap_slot[r] != ~0u)
           return RBE_E_STATE;
       }
@@ -591,22 +602,26 @@ struct HostInputs {
     n = n_;
     in_cap = in_cap_;
     heap.cap = heap_bytes;
-    sm.assign(n_rep, SlotMark{~0u, 0u});
+    sm.assign(n_rep, SlotMark{~0u, 0u, 0u});
     applied.assign(n_rep, 0);
     committing.assign(n_rep, 0);
     snap_slot.assign(n_rep, ~0u);
-    app_slot.assign(n_rep, AppSlot{~0u, ~0u});
+    app_slot.assign(n_rep, AppSlot{~0u, ~0u, 0u});
   }
   bool empty() const {
     return reps.empty() && app_rep.empty() && heap.stage.empty() && commits.empty() &&
            snaps.empty();
   }
   void clear() {
-    for (u64 r : reps) sm[r].slot = ~0u;
+    // a new generation: every slot of the last one reads as empty
+    if (++gen == 0) {
+      for (SlotMark& x : sm) x.gen = 0;
+      for (AppSlot& x : app_slot) x.gen = 0;
+      gen = 1;
+    }
     reps.clear();
     recs.clear();
     ents.clear();
-    for (u64 r : app_rep) app_slot[r & ~(1ull << 63)] = AppSlot{~0u, ~0u};
     app_rep.clear();
     app_val.clear();
     for (const CommitRec& c : commits) committing[c.r] = 0;
@@ -616,27 +631,27 @@ struct HostInputs {
     heap.stage.clear();
     heap.settle();
   }
+  u32 slot_of(u64 r) const { return sm[r].gen == gen ? sm[r].slot : ~0u; }
   ExtIn& rec(u64 r) {
-    if (sm[r].slot == ~0u) {
-      sm[r].slot = (u32)recs.size();
+    SlotMark& m = sm[r];
+    if (m.gen != gen) {
+      m.gen = gen;
+      m.slot = (u32)recs.size();
       reps.push_back(r);
-      ExtIn z;
-      memset(&z, 0, sizeof(z));
-      recs.push_back(z);
+      recs.emplace_back();
+      memset(&recs.back(), 0, sizeof(ExtIn));
     }
-    return recs[sm[r].slot];
+    return recs[m.slot];
   }
-  u32 staged_flags(u64 r) const { return sm[r].slot == ~0u ? 0u : recs[sm[r].slot].flags; }
+  u32 staged_flags(u64 r) const {
+    const u32 s = slot_of(r);
+    return s == ~0u ? 0u : recs[s].flags;
+  }
   // 0, or RBE_E_INVALID / RBE_E_STATE for the whole batch: every replica in
   // range, none twice in the batch, none with `flag` already staged
   int check_replicas(u64 cnt, const u64* replica, u32 flag) {
-    if (cnt && !replica) return RBE_E_INVALID;
-    for (u64 i = 0; i < cnt; i++) {
-      if (replica[i] >= n_rep) return RBE_E_INVALID;
-      if (owner && !owns_replica(*owner, replica[i] / n, (u32)(replica[i] % n)))
-        return RBE_E_INVALID;  // stepped by another engine
-    }
-    if (!flag) return RBE_OK;
+    int rc = check_range(cnt, replica);
+    if (rc || !flag) return rc;
     return unique_replicas(cnt, replica, flag);
   }
   // RBE_E_STATE when a replica appears twice in the batch or already has
@@ -696,8 +711,18 @@ struct HostInputs {
   int push_proposals(u64 cnt, const u64* replica, const u32* n_ents, const u32* type,
                      const u32* cmd_len, const u8* cmd) {
     if (cnt && (!n_ents || !type || !cmd_len)) return RBE_E_INVALID;
-    u64 total = 0;
-    for (u64 i = 0; i < cnt; i++) total += n_ents ? n_ents[i] : 0;
+    u64 total = 0, bytes = 0;
+    bool inline_only = true;
+    for (u64 i = 0; i < cnt; i++) {
+      if (n_ents[i] == 0 || n_ents[i] > 0xFFFFu) return RBE_E_INVALID;
+      total += n_ents[i];
+    }
+    for (u64 j = 0; j < total; j++) {
+      if (type[j] > E_Metadata || type[j] == E_ConfigChange) return RBE_E_INVALID;
+      inline_only = inline_only && cmd_len[j] <= 16;
+      bytes += cmd_len[j];
+    }
+    if (inline_only) return push_inline(cnt, replica, n_ents, type, cmd_len, cmd, total, bytes);
     std::vector<rbe_entry> pe(total);
     for (u64 j = 0; j < total; j++) {
       memset(&pe[j], 0, sizeof(rbe_entry));
@@ -710,16 +735,107 @@ struct HostInputs {
     if (cnt && (!lo || !hi)) return RBE_E_INVALID;
     for (u64 i = 0; i < cnt; i++)
       if (lo[i] == 0) return RBE_E_INVALID;  // ctx.Low is never 0 (requests.go:726)
-    int rc = check_replicas(cnt, replica, EXT_READ);
+    int rc = check_range(cnt, replica);
     if (rc) return rc;
-    for (u64 i = 0; i < cnt; i++) {
-      ExtIn& x = rec(replica[i]);
-      x.flags |= EXT_READ;
+    // one pass over the replicas: the duplicate checks and the staging
+    // together, undone whole when a check fails (all-or-nothing)
+    return stage_pass(cnt, replica, EXT_READ, [&](ExtIn& x, u64 i) {
       x.ctx_low = lo[i];
       x.ctx_high = hi[i];
+    });
+  }
+  // every replica in range (and, replica-per-GPU, stepped here)
+  int check_range(u64 cnt, const u64* replica) const {
+    if (cnt && !replica) return RBE_E_INVALID;
+    for (u64 i = 0; i < cnt; i++) {
+      if (replica[i] >= n_rep) return RBE_E_INVALID;
+      if (owner && !owns_replica(*owner, replica[i] / n, (u32)(replica[i] % n)))
+        return RBE_E_INVALID;  // stepped by another engine
     }
     return RBE_OK;
   }
+  // Stage `flag` for each replica (set(x, i) fills record x from input i) in
+  // one pass, with check_replicas' duplicate checks: RBE_E_STATE, and nothing
+  // staged, when a replica appears twice or already has `flag` staged
+  template <class Set>
+  int stage_pass(u64 cnt, const u64* replica, u32 flag, Set&& set) {
+    if (++epoch == 0) {
+      for (SlotMark& x : sm) x.mark = 0u;
+      epoch = 1;
+    }
+    const size_t n0 = recs.size();
+    recs.reserve(n0 + cnt);
+    reps.reserve(reps.size() + cnt);
+    undo.clear();
+    for (u64 i = 0; i < cnt; i++) {
+      const u64 r = replica[i];
+      if (i + 16 < cnt) __builtin_prefetch(&sm[replica[i + 16]], 1);
+      SlotMark& m = sm[r];
+      bool bad = m.mark == epoch;
+      m.mark = epoch;
+      if (!bad && m.gen == gen) {  // a record staged by another call: keep its old value
+        ExtIn& x = recs[m.slot];
+        bad = (x.flags & flag) != 0;
+        if (!bad) {
+          undo.push_back(std::make_pair(m.slot, x));
+          x.flags |= flag;
+          set(x, i);
+        }
+      } else if (!bad) {
+        m.gen = gen;
+        m.slot = (u32)recs.size();
+        reps.push_back(r);
+        recs.emplace_back();
+        ExtIn& x = recs.back();
+        memset(&x, 0, sizeof(ExtIn));
+        x.flags = flag;
+        set(x, i);
+      }
+      if (bad) {  // undo: the new records go, the old ones get their values back
+        for (size_t q = n0; q < recs.size(); q++) sm[reps[q]].gen = 0;
+        recs.resize(n0);
+        reps.resize(n0);
+        for (const auto& u : undo) recs[u.first] = u.second;
+        undo.clear();
+        return RBE_E_STATE;
+      }
+    }
+    return RBE_OK;
+  }
+  // push_proposals when every Cmd is inline (at most 16 bytes, no session
+  // fields): the entries go straight to ring form, in one pass with staging
+  int push_inline(u64 cnt, const u64* replica, const u32* n_ents, const u32* type,
+                  const u32* cmd_len, const u8* cmd, u64 total, u64 bytes) {
+    if (bytes && !cmd) return RBE_E_INVALID;
+    int rc = check_range(cnt, replica);
+    if (rc) return rc;
+    if (ents.size() + total > in_cap) return RBE_E_NOMEM;
+    const size_t e0 = ents.size();
+    ents.resize(e0 + total);
+    Ent* out = ents.data() + e0;
+    u64 j = 0, off = 0;
+    for (u64 i = 0; i < cnt; i++)
+      for (u32 t = 0; t < n_ents[i]; t++, j++) {
+        Ent& e = out[j];
+        e.term = 0;  // stamped by the leader (appendEntries, raft.go:909-920)
+        e.type = type[j];
+        e.len = cmd_len[j];
+        u8 b[16] = {0};
+        if (cmd_len[j]) memcpy(b, cmd + off, cmd_len[j]);
+        memcpy(&e.lo, b, 8);
+        memcpy(&e.hi, b + 8, 8);
+        off += cmd_len[j];
+      }
+    u64 first = e0;
+    rc = stage_pass(cnt, replica, EXT_PROPOSE, [&](ExtIn& x, u64 i) {
+      x.n_prop = n_ents[i];
+      x.prop_off = (u32)first;
+      first += n_ents[i];
+    });
+    if (rc) ents.resize(e0);
+    return rc;
+  }
+  std::vector<std::pair<u32, ExtIn>> undo;  // stage_pass: records to restore on failure
   int request_leader_transfer(u64 cnt, const u64* replica, const u64* target_id) {
     std::vector<u64> tv;  // NoNode panics (raft.go:1715), as does a node not in the group
     if (!map_ids(cnt, replica, target_id, tv)) return RBE_E_INVALID;
@@ -791,8 +907,9 @@ struct HostInputs {
       if (ms_now && nv[i] && nv[i] != replica[i] % n + 1 &&
           (type[i] == CC_AddObserver || type[i] == CC_AddWitness)) {
         // the membership the step applies it to: after a staged RestoreRemotes
-        const u32 ms = (staged_flags(replica[i]) & EXT_RESTORE) ? (u32)recs[sm[replica[i]].slot].pad[2]
-                                                                : ms_now[i];
+        const u32 ms = (staged_flags(replica[i]) & EXT_RESTORE)
+                           ? (u32)recs[slot_of(replica[i])].pad[2]
+                           : ms_now[i];
         const u32 b = 1u << (nv[i] - 1);
         const bool voter = !(ms & b), obs = (ms >> 8) & b, wit = (ms >> 16) & b;
         if (voter || (type[i] == CC_AddObserver ? wit : obs)) return RBE_E_INVALID;
@@ -863,7 +980,9 @@ struct HostInputs {
   // one staged pair per (replica, kind) between two steps, so no two lanes of
   // the scatter write one replica's row: a later call overwrites the value
   void stage_pair(u64 r, u64 v, bool ready) {
-    u32& slot = ready ? app_slot[r].ready : app_slot[r].applied;
+    AppSlot& a = app_slot[r];
+    if (a.gen != gen) a = AppSlot{~0u, ~0u, gen};
+    u32& slot = ready ? a.ready : a.applied;
     if (slot == ~0u) {
       slot = (u32)app_rep.size();
       app_rep.push_back(ready ? (r | (1ull << 63)) : r);
@@ -947,5 +1066,6 @@ struct HostInputs {
     for (const SnapRec& x : snaps) snap_rec_apply(P, x);
   }
 };
+using HostInputs = HostInputsT<std::allocator>;
 
 }  // namespace rbe

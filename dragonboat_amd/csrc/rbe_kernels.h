@@ -44,28 +44,8 @@ static constexpr int kBlock = 256;
 #ifndef RBE_LIST_AUX
 #define RBE_LIST_AUX 1
 #endif
-// how the fast steps of k_fast_both use wave-staged rows (StageRow, rbe_fast.h):
-// 0 = direct, 1 = STG_OUT (row writes staged), 3 = STG_OUT | STG_IN
-#ifndef RBE_FULL_SORT
-#define RBE_FULL_SORT 0  // measured: no change on C3 (263 vs 264 us)
-#endif
-#ifndef RBE_FULL_DEFER
-#define RBE_FULL_DEFER 0  // measured: 207 us without, 211 us with (C3)
-#endif
-#ifndef RBE_FULL_LREM
-#define RBE_FULL_LREM 1  // k_full_list keeps the replica's remote slots in LDS (MODE_FULL_LREM)
-#endif
-static constexpr int kFullMode = RBE_FULL_LREM ? (RBE_FULL_DEFER ? MODE_FULL_LREM_DEFER : MODE_FULL_LREM)
-                                               : (RBE_FULL_DEFER ? MODE_FULL_DEFER : MODE_FULL);
-#ifndef RBE_FAST_MIX
-#define RBE_FAST_MIX 0  // measured: C4 k_fast_both 138 vs 113 us, C3 399 vs 345 us
-#endif
-#ifndef RBE_STAGE_LEAD
-#define RBE_STAGE_LEAD 0
-#endif
-#ifndef RBE_STAGE_FOLL
-#define RBE_STAGE_FOLL 0
-#endif
+// k_full_list keeps the replica's remote slots in LDS for the step (MODE_FULL_LREM)
+static constexpr int kFullMode = MODE_FULL_LREM;
 static constexpr u32 kTriChunk = RBE_TRI_CHUNK;   // replicas per k_triage block (8 per lane)
 #ifndef RBE_SMALL_TRI_MAX
 #define RBE_SMALL_TRI_MAX (1u << 22)
@@ -710,137 +690,17 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Wave-cooperative row moves for the staged fast steps (StageRow, rbe_fast.h).
-// Load `it` of a plane with CH 16-B chunks per row serves chunk idx % CH of
-// row idx / CH, idx = it * 64 + lane: CH consecutive lanes cover one row, so a
-// wave instruction touches 64 / CH rows.  Row j belongs to lane j (its replica
-// index comes over by shuffle); bit j of `m` says whether lane j takes part.
-template <int N>
-__device__ __forceinline__ void stage_in_wave(const Planes& P, StageRow<N>* rows, u32 r,
-                                              u64 m_any, u64 m_lead) {
-  const int lane = threadIdx.x & 63;
-  constexpr int CC = sizeof(Core) / 16, CH = sizeof(Hot) / 16;
-  uint4 vc[CC], vh[CH], vr[N];
-#pragma unroll
-  for (int it = 0; it < CC; it++) {
-    const int idx = it * 64 + lane, j = idx / CC, q = idx % CC;
-    const u32 rj = __shfl(r, j, 64);
-    if ((m_any >> j) & 1ull) vc[it] = reinterpret_cast<const uint4*>(P.core + rj)[q];
-  }
-#pragma unroll
-  for (int it = 0; it < CH; it++) {
-    const int idx = it * 64 + lane, j = idx / CH, q = idx % CH;
-    const u32 rj = __shfl(r, j, 64);
-    if ((m_any >> j) & 1ull) vh[it] = reinterpret_cast<const uint4*>(P.hot + rj)[q];
-  }
-  if (m_lead) {
-#pragma unroll
-    for (int it = 0; it < N; it++) {
-      const int idx = it * 64 + lane, j = idx / N, q = idx % N;
-      const u32 rj = __shfl(r, j, 64);
-      if ((m_lead >> j) & 1ull) vr[it] = reinterpret_cast<const uint4*>(P.rem + (u64)rj * N)[q];
-    }
-  }
-#pragma unroll
-  for (int it = 0; it < CC; it++) {
-    const int idx = it * 64 + lane, j = idx / CC, q = idx % CC;
-    if ((m_any >> j) & 1ull) reinterpret_cast<uint4*>(&rows[j].core)[q] = vc[it];
-  }
-#pragma unroll
-  for (int it = 0; it < CH; it++) {
-    const int idx = it * 64 + lane, j = idx / CH, q = idx % CH;
-    if ((m_any >> j) & 1ull) reinterpret_cast<uint4*>(&rows[j].hot)[q] = vh[it];
-  }
-  if (m_lead) {
-#pragma unroll
-    for (int it = 0; it < N; it++) {
-      const int idx = it * 64 + lane, j = idx / N, q = idx % N;
-      if ((m_lead >> j) & 1ull) reinterpret_cast<uint4*>(&rows[j].rem[0])[q] = vr[it];
-    }
-  }
-}
-
-template <int N>
-__device__ __forceinline__ void stage_out_wave(const Planes& P, const StageRow<N>* rows, u32 r,
-                                               u64 m_done, u64 m_lead) {
-  const int lane = threadIdx.x & 63;
-  constexpr int CC = sizeof(Core) / 16, CU = sizeof(Upd) / 16, CH = sizeof(Hot) / 16;
-#pragma unroll
-  for (int it = 0; it < CC; it++) {
-    const int idx = it * 64 + lane, j = idx / CC, q = idx % CC;
-    const u32 rj = __shfl(r, j, 64);
-    if ((m_done >> j) & 1ull)
-      reinterpret_cast<uint4*>(P.core + rj)[q] = reinterpret_cast<const uint4*>(&rows[j].core)[q];
-  }
-#pragma unroll
-  for (int it = 0; it < CU; it++) {
-    const int idx = it * 64 + lane, j = idx / CU, q = idx % CU;
-    const u32 rj = __shfl(r, j, 64);
-    if ((m_done >> j) & 1ull)
-      reinterpret_cast<uint4*>(P.upd + rj)[q] = reinterpret_cast<const uint4*>(&rows[j].upd)[q];
-  }
-#pragma unroll
-  for (int it = 0; it < CH; it++) {
-    const int idx = it * 64 + lane, j = idx / CH, q = idx % CH;
-    const u32 rj = __shfl(r, j, 64);
-    if ((m_done >> j) & 1ull)
-      reinterpret_cast<uint4*>(P.hot + rj)[q] = reinterpret_cast<const uint4*>(&rows[j].hot)[q];
-  }
-  if (m_lead) {
-#pragma unroll
-    for (int it = 0; it < N; it++) {
-      const int idx = it * 64 + lane, j = idx / N, q = idx % N;
-      const u32 rj = __shfl(r, j, 64);
-      if ((m_lead >> j) & 1ull)
-        reinterpret_cast<uint4*>(P.rem + (u64)rj * N)[q] =
-            reinterpret_cast<const uint4*>(&rows[j].rem[0])[q];
-    }
-  }
-}
-
-// Write back the messages the wave's lanes staged in LDS (FastOut::send with
-// msg_stage): the wave lists its staged (lane, slot) pairs in lane order, then
-// four consecutive lanes move one 64-B message, 16 messages per instruction.
-__device__ __forceinline__ void msg_stage_flush(Msg* out, u32 staged) {
-  __shared__ u8 s_list[kMsgStageLanes * kMsgStage];
-  const u32 lane = threadIdx.x & 63u, w0 = threadIdx.x & ~63u;
-  const u64 below = (1ull << lane) - 1ull;
-  u32 pre = 0, tot = 0;
-#pragma unroll
-  for (u32 b = 0; (1u << b) <= kMsgStage; b++) {
-    const u64 m = __ballot((staged >> b) & 1u);
-    pre += (u32)__popcll(m & below) << b;
-    tot += (u32)__popcll(m) << b;
-  }
-  if (tot == 0) return;
-  u8* lst = &s_list[w0 * kMsgStage];
-  for (u32 j = 0; j < staged; j++) lst[pre + j] = (u8)(lane | (j << 6));
-  wave_lds_sync();
-  for (u32 b0 = 0; b0 < tot; b0 += 16) {
-    const u32 mi = b0 + (lane >> 2), q = lane & 3u;
-    if (mi < tot) {
-      const u32 e = lst[mi];
-      const u32 t = w0 + (e & 63u), j = e >> 6;
-      const uint4 v = reinterpret_cast<const uint4*>(&msg_stage_slots()[j][t])[q];
-      reinterpret_cast<uint4*>(out + msg_stage_dst()[j][t])[q] = v;
-    }
-  }
-  wave_lds_sync();  // the slots are free for the wave's next items
-}
-
 // Pass 2, merged (RBE_MODE=both, the default): the round's steady-state
 // leaders and followers in one launch, so the two roles' waves share the SIMDs
 // instead of running back to back; item i < n_lead is a leader, the rest
-// followers.  The rows a step reads and rewrites whole (Hot, Core, Upd, the
-// leader's remote slots) move between HBM and LDS wave-cooperatively
-// (stage_in_wave / stage_out_wave); the step works on its LDS row.
-#ifndef RBE_XCD_FAST
-#define RBE_XCD_FAST 0  // measured slower (C4 k_fast_both 116.7-117.0 vs 110.5-110.9 us)
-#endif
+// followers.  Block b takes chunks b, b + grid, ... of the item sequence
+// (fronts of every shard, then backs: seg_build / seg_find), one item a lane.
+// Measured and not kept: rows staged through LDS for wave-wide
+// stores, messages staged likewise, an XCD-aware chunk mapping, chunks that
+// alternate leaders and followers.
 template <int N, bool TRACE>
 __global__ __launch_bounds__(kBlock, kFastWaves<N>) void k_fast_both(Planes P, Params C,
                                                                      RoundArg ra, Lists L) {
-  __shared__ StageRow<N> s_rows[kBlock];
   const Clk ck = clk_of(ra);
   const u32 round = ck.round;
   const u32 par = round & 1u;
@@ -859,101 +719,29 @@ __global__ __launch_bounds__(kBlock, kFastWaves<N>) void k_fast_both(Planes P, P
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
 #endif
-  StageRow<N>* wrows = &s_rows[threadIdx.x & ~63u];
-  StageRow<N>* mine = &s_rows[threadIdx.x];
-  // XCD-aware item mapping (RBE_XCD_FAST): block b takes only the items of
-  // shard b % kShards, which k_triage blocks b' with b' % kShards == b %
-  // kShards wrote.  Blocks are dealt to the 8 XCDs round robin, so a group's
-  // leader and followers (one triage block, one shard) are stepped on the same
-  // XCD as each other and as its triage, and their partial-line writes to the
-  // group's rows meet in one L2 instead of being written back from several.
-  const bool xcd = RBE_XCD_FAST && gridDim.x >= kShards;
-  const u32 xsh = blockIdx.x % kShards;
-  u32 xcum[5] = {0, 0, 0, 0, 0};
-  if (xcd) {
-    for (u32 q = 0; q < 4; q++)
-      xcum[q + 1] = xcum[q] + (s_pre[q * kShards + xsh + 1] - s_pre[q * kShards + xsh]);
-  }
-  const u64 xn = xcum[4], xnl = xcum[2];
-  const u64 xblocks = (gridDim.x - xsh + kShards - 1) / kShards;
-  const u64 stride = xcd ? xblocks * kBlock : (u64)gridDim.x * kBlock;
-  const u64 lim = xcd ? xn : n;
-  // RBE_FAST_MIX: chunks of kBlock items alternate leader and follower work, so
-  // the blocks resident on a CU at once mix the two kinds of step (a leader
-  // step issues about twice the stores of a follower step) instead of the
-  // first blocks taking every leader
-  const u64 nlc = (nl + kBlock - 1) / kBlock, nfc = (n - nl + kBlock - 1) / kBlock;
-  const u64 mix = nlc < nfc ? nlc : nfc;
-  const bool mixed = RBE_FAST_MIX && !xcd;
   // a small engine spreads its items over twice the blocks (half of each
   // block's lanes take an item), so more CUs share the step's memory traffic
   // (a power of two: shifts, no 64-bit division in this kernel's registers)
   const u32 per = fast_items_per_block(C);
   const u32 per_log = per == 128u ? 7u : 8u;
-  const u64 nchunks = mixed ? nlc + nfc : (lim + per - 1) >> per_log;
-  const u64 cstride = xcd ? xblocks : gridDim.x;
-  (void)stride;
-  for (u64 ch = xcd ? blockIdx.x / kShards : blockIdx.x; ch < nchunks; ch += cstride) {
-    u64 i;
-    bool lead, any;
-    if (mixed) {
-      bool lc;
-      u64 k;
-      if (ch < 2 * mix) {
-        lc = (ch & 1u) == 0;
-        k = ch / 2;
-      } else {
-        lc = nlc > mix;
-        k = ch - mix;
-      }
-      i = (lc ? 0 : nl) + k * kBlock + threadIdx.x;
-      any = i < (lc ? (u64)nl : (u64)n);
-      lead = lc && any;
-    } else {
-      i = (ch << per_log) + threadIdx.x;
-      any = threadIdx.x < per && i < lim;
-      lead = any && (xcd ? i < xnl : i < nl);
-    }
+  const u64 nchunks = ((u64)n + per - 1) >> per_log;
+  for (u64 ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const u64 i = (ch << per_log) + threadIdx.x;
+    const bool any = threadIdx.x < per && i < n;
+    const bool lead = any && i < nl;
     u32 r = 0, aux = 0;
     if (any) {
-      u64 at;
-      if (xcd) {
-        const u32 q = (u32)(i >= xcum[1]) + (u32)(i >= xcum[2]) + (u32)(i >= xcum[3]);
-        at = list_pos(L, q / 2u, xsh, q & 1u, (u32)(i - xcum[q]));
-      } else {
-        const u32 sg = seg_find<4 * kShards>(s_pre, (u32)i);
-        at = list_pos(L, sg / (2 * kShards), sg % kShards, (sg / kShards) & 1u,
-                      (u32)i - s_pre[sg]);
-      }
+      const u32 sg = seg_find<4 * kShards>(s_pre, (u32)i);
+      const u64 at = list_pos(L, sg / (2 * kShards), sg % kShards, (sg / kShards) & 1u,
+                              (u32)i - s_pre[sg]);
       r = L.idx[at];
       if constexpr (kListAux<N>) aux = L.aux[at];
     }
-    const u64 m_any = __ballot(any), m_lead = __ballot(lead);
     bool ok = false;
-    if (m_any) {
-      constexpr int SL = RBE_STAGE_LEAD, SF = RBE_STAGE_FOLL;
-      const u64 m_in = ((SL & STG_IN) ? m_lead : 0ull) | ((SF & STG_IN) ? m_any & ~m_lead : 0ull);
-      const u64 m_out = (SL ? m_lead : 0ull) | (SF ? m_any & ~m_lead : 0ull);
-      if ((SL | SF) & STG_IN) {
-        stage_in_wave<N>(P, wrows, r, m_in, (SL & STG_IN) ? m_lead : 0ull);
-        wave_lds_sync();
-      }
-      u32 staged = 0;
-      constexpr bool ML = (RBE_MSG_STAGE & 2) != 0, MF = (RBE_MSG_STAGE & 1) != 0;
-      if (lead)
-        ok = step_fast<N, TRACE, MODE_LEAD, SL, kListAux<N>, ML>(P, C, r, ck, c, mine, aux,
-                                                                &staged);
-      else if (any)
-        ok = step_fast<N, TRACE, MODE_FOLL, SF, kListAux<N>, MF>(P, C, r, ck, c, mine, aux,
-                                                                &staged);
-      if constexpr (RBE_MSG_STAGE != 0) msg_stage_flush(P.msgs[par], staged);
-      if constexpr ((SL | SF) != 0) {
-        wave_lds_sync();
-        const u64 m_ok = __ballot(ok) & m_out;
-        stage_out_wave<N>(P, wrows, r, m_ok, SL ? m_ok & m_lead : 0ull);
-        wave_lds_sync();
-      }
-    }
+    if (lead)
+      ok = step_fast<N, TRACE, MODE_LEAD, kListAux<N>>(P, C, r, ck, c, aux);
+    else if (any)
+      ok = step_fast<N, TRACE, MODE_FOLL, kListAux<N>>(P, C, r, ck, c, aux);
     list_push(L, 2, par, any && !ok, r);
   }
 #if RBE_FAST_LDS_CTR
@@ -980,47 +768,7 @@ __global__ __launch_bounds__(kBlock) void k_full_list(Planes P, Params C, RoundA
   StepCounters c;
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
-#if RBE_FULL_SORT
-  // Block-local class sort: the general step's time is set by its slowest
-  // lanes, and a wave whose lanes take different handlers runs every handler's
-  // path in turn.  Each block takes 256 items, orders them by (role, any
-  // inbound message) with an LDS counting sort, and steps them in that order,
-  // so a wave mostly holds one kind of step (campaigns, vote tallies, replies).
-  __shared__ u32 s_hist[16], s_sorted[kBlock];
-  for (u64 b0 = (u64)blockIdx.x * kBlock; b0 < n; b0 += (u64)gridDim.x * kBlock) {
-    const u64 i = b0 + threadIdx.x;
-    u32 r = ~0u, cls = 15;
-    if (i < n) {
-      const u32 sg = seg_find<kShards>(s_pre, (u32)i);
-      r = L.idx[list_pos(L, 2, sg, false, (u32)i - s_pre[sg])];
-      const u64 g = r / N;
-      const u32 k = (u32)(r % N);
-      u32 inb = 0;
-#pragma unroll
-      for (u32 s = 0; s < N; s++)
-        if (s != k) inb |= in_word<N>(P, g, s, k, round);
-      cls = (idle_role(P.idle[r]) << 1) | (inb != 0 ? 1u : 0u);
-    }
-    if (threadIdx.x < 16) s_hist[threadIdx.x] = 0;
-    __syncthreads();
-    const u32 rank = atomicAdd(&s_hist[cls], 1u);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      u32 acc = 0;
-      for (u32 q = 0; q < 16; q++) {
-        const u32 v = s_hist[q];
-        s_hist[q] = acc;
-        acc += v;
-      }
-    }
-    __syncthreads();
-    s_sorted[s_hist[cls] + rank] = r;
-    __syncthreads();
-    const u32 rr = s_sorted[threadIdx.x];
-    if (rr != ~0u) step_replica<N, TRACE, kFullMode>(P, C, rr, ck, c);
-    __syncthreads();
-  }
-#elif defined(RBE_FULL_PROF)
+#if defined(RBE_FULL_PROF)
   // Diagnostic build: every wave iteration's s_memrealtime span, its active
   // lanes, the classes of its lanes (role before, role after, any inbound
   // message) and the most inbound / outbound messages of a lane, for

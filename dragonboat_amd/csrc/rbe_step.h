@@ -489,18 +489,9 @@ struct StepCounters {
 
 // ----------------------------------------------------------------- the lane
 enum : int {
-  MODE_FULL = 0, MODE_LEAD = 1, MODE_FOLL = 2, MODE_FULL_DEFER = 3,
-  MODE_FULL_LREM = 4,        // the whole table, the replica's remote slots in LDS (k_full_list)
-  MODE_FULL_LREM_DEFER = 5,  // ... and its sends deferred too
+  MODE_FULL = 0, MODE_LEAD = 1, MODE_FOLL = 2,
+  MODE_FULL_LREM = 4,  // the whole table, the replica's remote slots in LDS (k_full_list)
 };
-
-// Deferred message stores of the general step (MODE_FULL_DEFER, k_full_list):
-// send() keeps up to kLaneDefer messages of the lane in LDS and the step
-// writes them after everything else.  On CDNA vmcnt counts loads and stores
-// in order, so a load issued after a store also waits for that store: the
-// handler table interleaves sends with later inbox, ring and arena reads, and
-// every such read would otherwise pay for the messages sent before it.
-constexpr u32 kLaneDefer = 6;
 // entries per batch of the general step's entry loops (Lane::copy_ring_to_arena,
 // on_replicate): loads of a batch are issued together, then its stores
 constexpr u32 kEntBatch = 8;
@@ -510,10 +501,6 @@ constexpr u32 kEntBatch = 8;
 // message; in global memory each such read after the step's first store
 // waited for every store before it (vmcnt is in order), a round trip per
 // handler: C3's general step spent ~10 us per inbound message.
-#ifndef RBE_FULL_INPF
-#define RBE_FULL_INPF 0
-#endif
-constexpr u32 kLaneInbox = RBE_FULL_INPF;
 #if defined(__HIPCC__) || defined(__HIP__)
 __device__ __forceinline__ RemoteMN (&lane_rem())[kMaxN][256] {
   __shared__ RemoteMN s_rem[kMaxN][256];
@@ -523,41 +510,16 @@ __device__ __forceinline__ u8 (&lane_rst())[kMaxN][256] {
   __shared__ u8 s_rst[kMaxN][256];
   return s_rst;
 }
-// The first kLaneInbox inbound messages of a general step, and every sender's
-// count word, in LDS (RBE_FULL_INPF = kLaneInbox, k_full_list with LREM):
-// loaded with the remote slots before the step's first store, so the handlers
-// of those messages do not each wait for the stores of the ones before.
-// [message][16-B word][lane]: global_load_lds writes lane l's word at a
-// wave-uniform base + 16 * l
-__device__ __forceinline__ uint4 (&lane_inbox())[kLaneInbox ? kLaneInbox : 1][4][256] {
-  __shared__ uint4 s_inbox[kLaneInbox ? kLaneInbox : 1][4][256];
-  return s_inbox;
-}
-__device__ __forceinline__ u32 (&lane_inw())[kMaxN][256] {
-  __shared__ u32 s_inw[kMaxN][256];
-  return s_inw;
-}
-__device__ __forceinline__ Msg (&lane_defer_msgs())[kLaneDefer][256] {
-  __shared__ Msg s_msgs[kLaneDefer][256];
-  return s_msgs;
-}
-__device__ __forceinline__ u64 (&lane_defer_dst())[kLaneDefer][256] {
-  __shared__ u64 s_dst[kLaneDefer][256];
-  return s_dst;
-}
 #endif
 
 template <int N, bool TRACE, int MODE>
 struct Lane {
-  static constexpr bool FULL = MODE == MODE_FULL || MODE == MODE_FULL_DEFER ||
-                               MODE == MODE_FULL_LREM || MODE == MODE_FULL_LREM_DEFER;  // the whole handler table
-  static constexpr bool DEFER = MODE == MODE_FULL_DEFER || MODE == MODE_FULL_LREM_DEFER;  // sends kept in LDS until the end
+  static constexpr bool FULL = MODE == MODE_FULL || MODE == MODE_FULL_LREM;  // the whole handler table
 #if defined(__HIP_DEVICE_COMPILE__)
-  static constexpr bool LREM = MODE == MODE_FULL_LREM || MODE == MODE_FULL_LREM_DEFER;  // remote slots in LDS
+  static constexpr bool LREM = MODE == MODE_FULL_LREM;  // remote slots in LDS
 #else
   static constexpr bool LREM = false;  // host builds keep them in the planes
 #endif
-  static constexpr bool INPF = LREM && kLaneInbox > 0;  // inbox head in LDS
   static constexpr bool LEAD = MODE == MODE_LEAD;  // steady-state leader subset
   static constexpr bool FOLL = MODE == MODE_FOLL;  // steady-state follower subset
   const Planes& P;
@@ -567,7 +529,6 @@ struct Lane {
   const u32 k;      // slot; node id = k + 1
   const u32 round;
   const u32 par;    // round & 1: outbox buffer written this round
-  u32 n_defer = 0;  // sends held in LDS (DEFER)
   const Clk clk;    // round, ticks before it, whether it ticks
   const u64 cid;
   const u8 self;    // node id
@@ -862,63 +823,6 @@ struct Lane {
   RBE_HD u64 msg_slot_base(u32 sender, u32 dest) const {
     return ((g * N + sender) * N + dest) * (u64)C.maxm;
   }
-#if defined(__HIP_DEVICE_COMPILE__)
-  // INPF: the count words of every sender, then the first kLaneInbox messages
-  // of the inbox in stream order (senders ascending, each sender's A list then
-  // its B list from the back), all loads issued before any is used and before
-  // the step's first store.  Positions past the inbox load the sender's first
-  // slot and are never read.
-  __device__ __forceinline__ void inbox_prefetch() {
-    if (round == 0) {
-      for (u32 s = 0; s < N; s++) lane_inw()[s][threadIdx.x] = 0u;
-      return;
-    }
-    u32 pcs[N];
-#pragma unroll
-    for (u32 s = 0; s < N; s++) pcs[s] = s == k ? 0u : in_word<N>(P, g, s, k, round);
-    const u32 ppar = par ^ 1u;
-    const Msg* src[kLaneInbox ? kLaneInbox : 1];
-#pragma unroll
-    for (u32 j = 0; j < kLaneInbox; j++) src[j] = &P.msgs[ppar][msg_slot_base(0, k)];
-    u32 before = 0;  // messages of the senders before s
-#pragma unroll
-    for (u32 s = 0; s < N; s++) {
-      const u32 na = pcs[s] & 0x7Fu, n = na + ((pcs[s] >> 7) & 0x7Fu);
-      const Msg* lst = &P.msgs[ppar][msg_slot_base(s, k)];
-#pragma unroll
-      for (u32 j = 0; j < kLaneInbox; j++) {
-        const u32 i = j - before;  // wraps when j < before: then i >= n
-        if (j >= before && i < n) src[j] = i < na ? &lst[i] : &lst[C.maxm - 1u - (i - na)];
-      }
-      before += n;
-    }
-    static_assert(sizeof(Msg) == 64, "a message is four 16-B words");
-#pragma unroll
-    for (u32 s = 0; s < N; s++) lane_inw()[s][threadIdx.x] = pcs[s];
-    // straight into LDS (no registers held), then one wait before the step's
-    // first store
-    const u32 wb = threadIdx.x & ~63u;
-#pragma unroll
-    for (u32 j = 0; j < kLaneInbox; j++)
-#pragma unroll
-      for (u32 c = 0; c < 4; c++)
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)((const uint4*)src[j] + c),
-            (__attribute__((address_space(3))) void*)&lane_inbox()[j][c][wb], 16, 0, 0);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  }
-  __device__ __forceinline__ u32 inw_lds(u32 s) const { return lane_inw()[s][threadIdx.x]; }
-  __device__ __forceinline__ void inbox_lds(u32 j, Msg* m) const {
-    uint4 w[4];
-#pragma unroll
-    for (u32 c = 0; c < 4; c++) w[c] = lane_inbox()[j][c][threadIdx.x];
-    __builtin_memcpy(m, w, sizeof(Msg));
-  }
-#else
-  void inbox_prefetch() {}
-  u32 inw_lds(u32) const { return 0u; }
-  void inbox_lds(u32, Msg*) const {}
-#endif
   // raft.send + finalizeMessageTerm (raft.go:640-658) + the network: the
   // message joins Update.Messages (hashed here, in emission order) and is
   // written to the (self → dest) list, Replicate messages in front (node.go
@@ -978,27 +882,7 @@ struct Lane {
     const u64 at = msg_slot_base(k, d) + slot;
     ctr.v[C_MSG_OUT]++;
     ctr.v[C_ENT_OUT] += m.n_ent;
-#if defined(__HIP_DEVICE_COMPILE__)
-    if constexpr (DEFER) {
-      if (n_defer < kLaneDefer) {
-        lane_defer_msgs()[n_defer][threadIdx.x] = m;
-        lane_defer_dst()[n_defer][threadIdx.x] = at;
-        n_defer++;
-        return;
-      }
-    }
-#endif
     P.msgs[par][at] = m;
-  }
-  // the deferred sends, after every other access of the step
-  RBE_HD void flush_deferred() {
-#if defined(__HIP_DEVICE_COMPILE__)
-    if constexpr (DEFER) {
-      for (u32 j = 0; j < n_defer; j++)
-        P.msgs[par][lane_defer_dst()[j][threadIdx.x]] = lane_defer_msgs()[j][threadIdx.x];
-      n_defer = 0;
-    }
-#endif
   }
   RBE_HD Msg mk(u32 type, u8 to) const {
     Msg m;
@@ -2573,7 +2457,6 @@ struct Lane {
         lrst(s) = P.rem_st[r * N + s];
       }
     }
-    if constexpr (INPF) inbox_prefetch();
     fault = (flags & HF_FAULTED) ? P.upd[r].fault : 0u;
     const u64 digest0 = TRACE ? P.upd[r].digest : 0;
     snp_pend = snp_rej = 0;
@@ -2725,8 +2608,6 @@ struct Lane {
     //   handleLeaderTransferRequest (node.go:1069-1075) → Peer.RequestLeaderTransfer
     const u32 ppar = par ^ 1u;
     u32 cs = 0, ci = 0, cn = 0, cna = 0;  // inbox cursor: sender, index, count, #A
-    u32 n_taken = 0;                      // inbox messages taken (INPF: the first in LDS)
-    (void)n_taken;
     bool copen = false;
     const u32 phase0 = (unreach | snap_nodes) ? 0u : (round > 0 ? 1u : 2u);
     // calls the node makes under raftMu between two steps come first:
@@ -2836,9 +2717,7 @@ struct Lane {
               cs++;
               continue;
             }
-            u32 pc;
-            if constexpr (INPF) pc = inw_lds(cs);
-            else pc = in_word<N>(P, g, cs, k, round);
+            const u32 pc = in_word<N>(P, g, cs, k, round);
             if (pc & 0x8000u) {  // Quiesce first in the sender's stream (node.go:1207-1210)
               ctr.v[C_MSG_IN]++;
               q_try_enter();
@@ -2850,16 +2729,7 @@ struct Lane {
           }
           if (ci < cn) {
             const Msg* lst = &P.msgs[ppar][msg_slot_base(cs, k)];
-            if constexpr (INPF) {
-              if (n_taken < kLaneInbox) {
-                inbox_lds(n_taken, &m);
-              } else {
-                m = ci < cna ? lst[ci] : lst[C.maxm - 1u - (ci - cna)];
-              }
-              n_taken++;
-            } else {
-              m = ci < cna ? lst[ci] : lst[C.maxm - 1u - (ci - cna)];
-            }
+            m = ci < cna ? lst[ci] : lst[C.maxm - 1u - (ci - cna)];
             ents = &P.arena[ppar][(g * N + cs) * (u64)C.ecap + m.ent_off];
             ci++;
             kind = 1;
@@ -3149,7 +3019,6 @@ template <int N, bool TRACE, int MODE = MODE_FULL>
 RBE_HD void step_replica(const Planes& P, const Params& C, u64 r, Clk ck, StepCounters& ctr) {
   Lane<N, TRACE, MODE> lane(P, C, r, ck, ctr);
   lane.run();
-  lane.flush_deferred();
 }
 // the steady-state subset: returns false (nothing written) when the round
 // needs the full table

@@ -95,6 +95,7 @@ class RbeUpdate(C.Structure):
 
 # Update flags and listener events (include/rbe.h RBE_UF_* / RBE_EV_*)
 UF_STATE_CHANGED, UF_SENT_QUIESCE, UF_FAST_APPLY, UF_HAS_UPDATE, UF_SNAPSHOT = 1, 2, 8, 16, 32
+UF_APPLIED = 64
 EV_LEADER_UPDATED, EV_CAMPAIGN_LAUNCHED, EV_CAMPAIGN_SKIPPED, EV_SNAPSHOT_REJECTED = 1, 2, 4, 8
 EV_REPLICATION_REJECTED, EV_PROPOSAL_DROPPED, EV_READ_INDEX_DROPPED = 16, 32, 64
 
@@ -169,6 +170,7 @@ class RbeStepOutputs(C.Structure):
 
 
 RBE_COLLECT_REMOTE_MSGS = 1
+RBE_COLLECT_SKIP_LOCAL = 2
 
 
 class RbeWireFrame(C.Structure):
@@ -986,15 +988,16 @@ class Engine(NodeInputs):
         return (arr(o.msg_off, count + 1, u64), arr(o.messages, o.n_messages, MESSAGE_DTYPE),
                 arr(o.rtr_off, count + 1, u64), arr(o.ready_to_reads, o.n_ready_to_reads, RTR_DTYPE))
 
-    def collect_step(self, first: int = 0, count: Optional[int] = None, remote_only=False):
+    def collect_step(self, first: int = 0, count: Optional[int] = None, remote_only=False,
+                     skip_local=False):
         """rbe_collect_step: (replicas, Updates, msg_off, messages, rtr_off,
         ready_to_reads) of the replicas in [first, first + count) with an
-        Update, as numpy arrays (copies of the engine's pinned buffer)."""
+        Update, as numpy arrays (copies of the engine's pinned buffer).
+        skip_local: RBE_COLLECT_SKIP_LOCAL."""
         count = self.n_rep - first if count is None else count
         o = RbeStepOutputs()
-        _check(self.lib.rbe_collect_step(self.h, first, count,
-                                         RBE_COLLECT_REMOTE_MSGS if remote_only else 0,
-                                         C.byref(o)), "rbe_collect_step")
+        fl = (RBE_COLLECT_REMOTE_MSGS if remote_only else 0) | (RBE_COLLECT_SKIP_LOCAL if skip_local else 0)
+        _check(self.lib.rbe_collect_step(self.h, first, count, fl, C.byref(o)), "rbe_collect_step")
 
         def arr(ptr, n, dtype):
             if n == 0:

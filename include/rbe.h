@@ -692,9 +692,14 @@ int rbe_collect_updates(rbe_engine* e, uint64_t first, uint64_t count, rbe_updat
  * RBE_COLLECT_REMOTE_MSGS only the messages to replicas this engine does not
  * step are returned (rep_world > 1: the transport's share); the others the
  * engine delivers itself at the next step, so in group-per-GPU mode none is
- * copied.  Valid until the next rbe_collect_step, rbe_step/rbe_run or
- * rbe_destroy. */
+ * copied.  With RBE_COLLECT_SKIP_LOCAL an Update whose only content is
+ * messages the engine delivers itself (none returned under the flag above) is
+ * left out: the node would have nothing to persist, apply, send or report for
+ * it (no State change, entries, ReadyToReads, drops, Snapshot, applied index
+ * or listener event).  Valid until the next rbe_collect_step, rbe_step/rbe_run
+ * or rbe_destroy. */
 #define RBE_COLLECT_REMOTE_MSGS 1u
+#define RBE_COLLECT_SKIP_LOCAL 2u
 typedef struct rbe_step_outputs {
   uint64_t first, count, n, n_messages, n_ready_to_reads;
   const uint64_t* replica;                 /* n */

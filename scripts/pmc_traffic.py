@@ -3,9 +3,17 @@ per launch (profiles/traffic_<workload>.json, read by bench.py).
 
 Per /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE
 are in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide coalesced
-streaming reads, so the corrected read figure is 2 x FETCH_SIZE.  Both the raw
-and the corrected values are recorded.  Only the last LAST dispatches of each
-kernel are used (the bench's per-kernel profiled rounds, in steady state).
+streaming reads, and other access widths are to be calibrated on a known byte
+count.  The engine's kernels gather 16-B records scattered over the planes, so
+the calibration is the group_shape microbenchmark of the same shape
+(profiles/r05_calibration: 70.4 MB of known loads per launch read as FETCH_SIZE
+75.1 MB with the active groups adjacent, 93.8 MB with them scattered; doubled
+that would be 150-188 MB, more than the kernel can read): for these kernels
+FETCH_SIZE counts the bytes fetched, sector over-fetch included, without the
+factor 2.  `bytes_per_launch` is therefore FETCH_SIZE + WRITE_SIZE; the guide's
+2 x FETCH_SIZE + WRITE_SIZE is kept as `bytes_per_launch_fetch_x2`.  Only the
+last LAST dispatches of each kernel are used (the bench's per-kernel profiled
+rounds, in steady state).
 """
 import csv
 import glob
@@ -64,9 +72,12 @@ def main():
         sha = hashlib.sha256(f.read()).hexdigest()[:16]
     # bench.py reports this traffic only for the same library (content hash)
     res = {"workload": w, "unit": "bytes per launch", "dispatches_averaged": LAST,
-           "library_sha256_16": sha, "fetch_raw": fetch, "write": write, "bytes_per_launch": {}}
+           "library_sha256_16": sha, "fetch_raw": fetch, "write": write,
+           "fetch_calibration": "scattered 16-B gathers: FETCH_SIZE x 1 (profiles/r05_calibration)",
+           "bytes_per_launch": {}, "bytes_per_launch_fetch_x2": {}}
     for k in set(fetch) | set(write):
-        res["bytes_per_launch"][k] = 2.0 * fetch.get(k, 0.0) + write.get(k, 0.0)
+        res["bytes_per_launch"][k] = fetch.get(k, 0.0) + write.get(k, 0.0)
+        res["bytes_per_launch_fetch_x2"][k] = 2.0 * fetch.get(k, 0.0) + write.get(k, 0.0)
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     out = os.path.join(ROOT, "gpurun_out", f"traffic_{w}.json")
     with open(out, "w") as f:

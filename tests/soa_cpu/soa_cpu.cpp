@@ -29,7 +29,7 @@ struct SoaEngine {
   HostInputs hin;
   u64 counters[C_NUM] = {0};
   bool full_only = false;
-  int staged = 0;  // STG_* bits: fast steps on a staged row (StageRow); 4: counts from inbound_aux
+  int staged = 0;  // 4: the fast steps take the inbound counts from the summary word (inbound_aux)
   u64 slow_total = 0;
   std::vector<u8> heap;  // payload heap (cfg.heap_bytes), as on the device
   u64 heap_head = 0;     // Planes::heap_head
@@ -139,33 +139,12 @@ static void run_round(SoaEngine* e, bool tick = true) {
         const u32 aux = inbound_aux<N>(w, k, e->round);
         if (li == 0)
           ok = e->C.trace
-                   ? step_fast<N, true, MODE_LEAD, 0, true>(e->P, e->C, r, ck, c, nullptr, aux)
-                   : step_fast<N, false, MODE_LEAD, 0, true>(e->P, e->C, r, ck, c, nullptr, aux);
+                   ? step_fast<N, true, MODE_LEAD, true>(e->P, e->C, r, ck, c, aux)
+                   : step_fast<N, false, MODE_LEAD, true>(e->P, e->C, r, ck, c, aux);
         else
           ok = e->C.trace
-                   ? step_fast<N, true, MODE_FOLL, 0, true>(e->P, e->C, r, ck, c, nullptr, aux)
-                   : step_fast<N, false, MODE_FOLL, 0, true>(e->P, e->C, r, ck, c, nullptr, aux);
-      } else if (e->staged == (STG_OUT | STG_IN)) {
-        StageRow<N> row;
-        memset(&row, 0xA5, sizeof(row));  // nothing the step reads may come from here unset
-        stage_row_in<N>(e->P, r, li == 0, row);
-        if (li == 0)
-          ok = e->C.trace ? step_fast<N, true, MODE_LEAD, 3>(e->P, e->C, r, ck, c, &row)
-                          : step_fast<N, false, MODE_LEAD, 3>(e->P, e->C, r, ck, c, &row);
-        else
-          ok = e->C.trace ? step_fast<N, true, MODE_FOLL, 3>(e->P, e->C, r, ck, c, &row)
-                          : step_fast<N, false, MODE_FOLL, 3>(e->P, e->C, r, ck, c, &row);
-        if (ok) stage_row_out<N>(e->P, r, li == 0, row);
-      } else if (e->staged == STG_OUT) {
-        StageRow<N> row;
-        memset(&row, 0xA5, sizeof(row));
-        if (li == 0)
-          ok = e->C.trace ? step_fast<N, true, MODE_LEAD, 1>(e->P, e->C, r, ck, c, &row)
-                          : step_fast<N, false, MODE_LEAD, 1>(e->P, e->C, r, ck, c, &row);
-        else
-          ok = e->C.trace ? step_fast<N, true, MODE_FOLL, 1>(e->P, e->C, r, ck, c, &row)
-                          : step_fast<N, false, MODE_FOLL, 1>(e->P, e->C, r, ck, c, &row);
-        if (ok) stage_row_out<N>(e->P, r, li == 0, row);
+                   ? step_fast<N, true, MODE_FOLL, true>(e->P, e->C, r, ck, c, aux)
+                   : step_fast<N, false, MODE_FOLL, true>(e->P, e->C, r, ck, c, aux);
       } else if (li == 0) {
         ok = e->C.trace ? step_fast<N, true, MODE_LEAD>(e->P, e->C, r, ck, c)
                         : step_fast<N, false, MODE_LEAD>(e->P, e->C, r, ck, c);

@@ -151,7 +151,7 @@ def test_gpu_collect_step_matches(gpu_available, name, kw, extra):
     from dragonboat_amd.engine import Engine
     kw = dict(kw, n_groups=min(kw["n_groups"], 48))
     eng = Engine(device=0, trace=True, **dict(kw, **extra))
-    seen = [0, 0, 0]
+    seen = [0, 0, 0, 0]
     for rnd in range(120):
         eng.step()
         first, count = (0, eng.n_rep) if rnd % 3 else (5, eng.n_rep - 9)
@@ -173,13 +173,31 @@ def test_gpu_collect_step_matches(gpu_available, name, kw, extra):
         assert len(msgs) == len(allm) and len(rtrs) == len(allr)
         r2, u2, mo2, m2, ro2, t2 = eng.collect_step(first, count, remote_only=True)
         assert len(m2) == 0 and list(r2) == list(rep) and t2.tobytes() == rtrs.tobytes()
+        # RBE_COLLECT_SKIP_LOCAL: only the Updates with more than locally
+        # delivered messages, the same records and ReadyToReads
+        r3, u3, _, m3, ro3, t3 = eng.collect_step(first, count, remote_only=True, skip_local=True)
+        keep = [j for j in range(len(rep)) if _actionable(ups[j])]
+        assert list(r3) == [int(rep[j]) for j in keep], rnd
+        assert u3.tobytes() == ups[keep].tobytes() and len(m3) == 0
+        assert t3.tobytes() == rtrs.tobytes()  # every ReadyToRead is in a kept Update
+        seen[3] += len(rep) - len(r3)
         seen[0] += len(rep)
         seen[1] += len(msgs)
         seen[2] += len(rtrs)
-    assert seen[0] and seen[1], seen
+    assert seen[0] and seen[1] and seen[3], seen
     if name == "C4":
         assert seen[2], seen
     eng.close()
+
+
+def _actionable(u):
+    """An Update the node has work for besides its messages (RBE_COLLECT_SKIP_LOCAL)."""
+    from dragonboat_amd import engine as E
+    return bool(int(u["flags"]) & (E.UF_STATE_CHANGED | E.UF_SENT_QUIESCE | E.UF_SNAPSHOT |
+                                   E.UF_APPLIED)) or \
+        bool(u["events"] or u["n_ready_to_read"] or u["n_dropped_entries"] or
+             u["n_dropped_read_indexes"] or u["save_lo"] <= u["save_hi"] or
+             u["apply_lo"] <= u["apply_hi"])
 
 
 def test_gpu_collect_untraced_group_sleep(gpu_available):

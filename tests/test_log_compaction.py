@@ -155,12 +155,11 @@ def test_restart_after_compaction(name):
     assert not counters_match(eng.counters(), ref.counters())
 
 
-@pytest.mark.parametrize("mode", ["staged", "aux"])
-def test_compaction_fast_step_variants(mode):
-    """The fast steps' staged-row and summary-word variants (as k_fast_both runs
-    them) with node snapshots taken inside the fast epilogue."""
+def test_compaction_fast_step_aux():
+    """The fast steps' summary-word variant (as k_fast_both runs them) with
+    node snapshots taken inside the fast epilogue."""
     kw, extra, rounds = CASES["C3_SNAP"]
-    eng = SoaCpu(trace=True, staged={"staged": 3, "aux": 4}[mode], **kw, **extra)
+    eng = SoaCpu(trace=True, staged=4, **kw, **extra)
     ref = O.Harness(**kw)
     assert run_case(eng, ref, rounds) > 0
     assert eng.faults()[0] == 0

@@ -181,6 +181,20 @@ def test_push_batches_are_all_or_nothing():
         eng.notify_applied([0], [1])
     eng.step()
     eng.push_proposals([0], [[b"y"]])  # the next step takes a new batch
+    # a failed batch is undone whole: records it created go, records an
+    # earlier call staged keep their parts
+    eng.push_proposals([4], [[b"p"]])
+    with pytest.raises(InputError) as ei:
+        eng.push_read_index([3, 4, 5, 3], [(7, 0)] * 4)
+    assert ei.value.rc == RBE_E_STATE
+    eng.push_read_index([3, 4, 5], [(7, 0)] * 3)
+    with pytest.raises(InputError) as ei:
+        eng.push_proposals([2, 5, 2], [[b"a"], [b"b"], [b"c"]])
+    assert ei.value.rc == RBE_E_STATE
+    eng.push_proposals([2, 5], [[b"a"], [b"b"]])
+    with pytest.raises(InputError) as ei:
+        eng.push_proposals([4], [[b"q"]])
+    assert ei.value.rc == RBE_E_STATE
 
 
 @pytest.mark.parametrize("quiesce", [False, True])

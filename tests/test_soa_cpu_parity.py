@@ -16,15 +16,13 @@ CASES = {"C1": (C1, 400), "C2": (C2, 300), "C3": (C3, 400), "C3_HOT": (C3_HOT, 4
          "MIXED": (MIXED, 600)}
 
 
-@pytest.mark.parametrize("mode", ["pipeline", "full_table", "staged_out", "staged", "aux"])
+@pytest.mark.parametrize("mode", ["pipeline", "full_table", "aux"])
 @pytest.mark.parametrize("name", list(CASES))
 def test_soa_cpu_lockstep_parity(name, mode):
-    """`staged_out` / `staged`: the fast steps write (and read) a staged row
-    (StageRow, STG_OUT / STG_OUT | STG_IN); `aux`: they take their inbound
-    count words from the work-list summary word (inbound_aux), as k_fast_both
-    runs them."""
+    """`aux`: the fast steps take their inbound count words from the
+    work-list summary word (inbound_aux), as k_fast_both runs them."""
     kw, rounds = CASES[name]
-    staged = {"staged_out": 1, "staged": 3, "aux": 4}.get(mode, 0)
+    staged = {"aux": 4}.get(mode, 0)
     eng = SoaCpu(full_only=mode == "full_table", staged=staged, trace=True, **kw,
                  **ENGINE_EXTRA.get(name, {}))
     ref = O.Harness(**kw)
