@@ -433,7 +433,6 @@ def run_host_driven(args, ws, rank, local, dist):
     # node besides those messages (RBE_COLLECT_SKIP_LOCAL)
     all_msgs = args.c4h_all_msgs
     cflags = RBE_COLLECT_REMOTE_MSGS | RBE_COLLECT_SKIP_LOCAL
-    leader_of = np.zeros(n_groups, dtype=np.uint64)  # leader slot + 1 per group, 0 = none
     cmd = np.frombuffer(rng.bytes(16 * len(active)), dtype=np.uint8).copy()
     ptr = lambda a, t: a.ctypes.data_as(C.POINTER(t))  # noqa: E731
     stats = {"push": 0.0, "push_abi": 0.0, "step": 0.0, "enqueue": 0.0, "out": 0.0, "reads": 0,
@@ -443,12 +442,26 @@ def run_host_driven(args, ws, rank, local, dist):
     # (event.go:93-95), which the engine reports in Update.events
     ev_leader = np.uint32(EV_LEADER_UPDATED)
 
+    # the replica each active group's requests go to (its leader), kept
+    # current from the LeaderUpdated events; NONE while a group has no leader
+    NONE = np.uint64(np.iinfo(np.uint64).max)
+    active_i = active.astype(np.int64)
+    act_of = np.full(n_groups, -1, dtype=np.int64)
+    act_of[active_i] = np.arange(len(active))
+    lead_rep = np.full(len(active), NONE, dtype=np.uint64)
+
+    def set_leaders(g, lid):
+        a = act_of[g]
+        on = a >= 0
+        lead_rep[a[on]] = np.where(lid[on] != 0, g[on].astype(np.uint64) * np.uint64(N) +
+                                   lid[on] - np.uint64(1), NONE)
+
     def note_leaders(rep, ups):
         chg = (ups["events"] & ev_leader) != 0
         if chg.any():
             lid = ups["leader_id"][chg]
             known = lid != 0
-            leader_of[(rep[chg][known] // np.uint64(N)).astype(np.int64)] = lid[known]
+            set_leaders((rep[chg][known] // np.uint64(N)).astype(np.int64), lid[known])
 
     def read_back():
         if not all_msgs:
@@ -475,23 +488,17 @@ def run_host_driven(args, ws, rank, local, dist):
     # ReadIndex (90%) and which a proposal
     total_rounds = settle + max(1, args.warmup) + args.steps
     read_mask = rng.random((total_rounds, len(active))) < 0.9
-    active_i = active.astype(np.int64)
-    active_n = active * np.uint64(N)
+    read_at = [np.flatnonzero(m) for m in read_mask]
+    prop_at = [np.flatnonzero(~m) for m in read_mask]
     one = np.ones(len(active), dtype=np.uint32)
     zero = np.zeros(len(active), dtype=np.uint32)
     ln = np.full(len(active), 16, dtype=np.uint32)
 
     def one_round(rnd, timed):
         t0 = time.perf_counter()
-        lg = leader_of[active_i]
-        is_read = read_mask[rnd]
-        if lg.all():
-            reps = active_n + (lg - np.uint64(1))
-        else:
-            has = lg != 0
-            reps = active_n[has] + (lg[has] - np.uint64(1))
-            is_read = is_read[has]
-        rr, pr = reps[is_read], reps[~is_read]
+        rr, pr = lead_rep[read_at[rnd]], lead_rep[prop_at[rnd]]
+        if (len(rr) and rr.max() == NONE) or (len(pr) and pr.max() == NONE):
+            rr, pr = rr[rr != NONE], pr[pr != NONE]  # groups without a leader wait
         if len(rr):  # ctx.Low = round << 32 | replica + 1 (never 0), ctx.High = replica
             lo = rr + np.uint64(((rnd + 1) << 32) + 1)
         tc = time.perf_counter()
@@ -527,7 +534,7 @@ def run_host_driven(args, ws, rank, local, dist):
             if r == settle - 1:  # leaders of every group, quiesced ones included (untimed)
                 eng.sync()
                 lid = np.frombuffer(bytes(eng.updates()), UPDATE_DTYPE)["leader_id"]
-                leader_of[:] = lid.reshape(n_groups, N).max(axis=1)
+                set_leaders(np.arange(n_groups), lid.reshape(n_groups, N).max(axis=1))
                 read_back()
         else:
             one_round(r, False)

@@ -647,6 +647,9 @@ struct rbe_engine {
   // rbe_wire_ingest scratch (keys, indexes, heap offsets, sort temporary)
   u8* ing_dev = nullptr;
   u64 ing_dev_bytes = 0;
+  // capacities the no-read-back ingest launches for (messages, entries, Cmd
+  // bytes): the last call's counts + 25%; 0 until a call has measured them
+  u64 ing_cap[3] = {0, 0, 0};
   // rbe_collect_updates: the same for the compacted Updates
   u8* upd_dev = nullptr;
   u64 upd_dev_bytes = 0;
@@ -666,6 +669,16 @@ struct rbe_engine {
   u64 wire_rec_bytes = 0;
   u8* wire_in = nullptr;     // rbe_wire_decode: inbound bytes and per-frame scratch
   u64 wire_in_bytes = 0;
+  u8* wire_big_buf = nullptr;  // the chunked walk of big frames: exits, counts, chunk lists
+  u64 wire_big_bytes = 0;
+  // frames longer than this are walked by chunks (k_wire_chunk_exit / hop /
+  // emit), shorter ones by one block each (k_wire_bounds); RBE_WIRE_BIG sets it
+  u64 wire_big = 256u << 10;
+  // wire_front's piecewise upload: a copy stream, one event per piece and one
+  // for the engine stream's work before it
+  static constexpr u32 kCopyPieces = 8;
+  hipStream_t cp_stream = nullptr;
+  hipEvent_t cp_ev[kCopyPieces + 1] = {};
   u64 wire_totals[4] = {0, 0, 0, 0};
   u64 wire_frames_off = 0;   // frame index inside wire_meta
 };
@@ -987,6 +1000,13 @@ int rbe_destroy(rbe_engine* e) {
   if (e->wire_meta) HIP_IGNORE(hipFree(e->wire_meta));
   if (e->wire_rec) HIP_IGNORE(hipFree(e->wire_rec));
   if (e->wire_in) HIP_IGNORE(hipFree(e->wire_in));
+  if (e->wire_big_buf) HIP_IGNORE(hipFree(e->wire_big_buf));
+  if (e->cp_stream) {
+    HIP_IGNORE(hipStreamSynchronize(e->cp_stream));
+    for (auto& ev : e->cp_ev)
+      if (ev) HIP_IGNORE(hipEventDestroy(ev));
+    HIP_IGNORE(hipStreamDestroy(e->cp_stream));
+  }
   if (e->stream) HIP_IGNORE(hipStreamDestroy(e->stream));
   delete e;
   return RBE_OK;
@@ -1109,6 +1129,7 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
     return RBE_E_NOMEM;
   }
   HIP_IGNORE(hipMemsetAsync(e->d_clk, 0, 2 * sizeof(u32), e->stream));
+  if (const char* wb = getenv("RBE_WIRE_BIG")) e->wire_big = strtoull(wb, nullptr, 10);
   const char* mode = getenv("RBE_MODE");
   // default: k_triage → k_fast_both → k_full_list; RBE_MODE=split runs the two
   // roles as separate launches, RBE_MODE=fused k_round + k_full_list,
@@ -2561,14 +2582,24 @@ struct WireDecoded {
   u64 *ent0 = nullptr, *cmd0 = nullptr;
 };
 
-// rbe_wire_decode's device part: verify, find, count, scan and parse.  With
-// `caps` non-null (the caller's capacities: messages, entries, Cmd bytes) the
-// records are not parsed when one is short (RBE_E_NOMEM, counts reported).
-static int wire_decode_dev(rbe_engine* e, const void* data, uint64_t bytes, WireDecoded* o,
-                           const u64* caps) {
+// The front of a decode: the frame boundaries (magic + size of each header,
+// the receiver's reads, on the host), the stream and the frame table
+// uploaded, both crc32s verified, and every frame's requests found into its
+// single-pass slots (one block per frame; big frames by chunks).  Nothing is
+// read back.
+struct WireFront {
+  std::vector<WireIn> fr;
+  WireIn* dfr = nullptr;
+  WireMsgPos* spos = nullptr;
+  u64 big = 0, nch = 0;
+  u32 *ent = nullptr, *cbase = nullptr;
+  WireChunk* dch = nullptr;
+  u32 compact_y = 1;  // blocks per frame of k_wire_compact
+};
+static int wire_front(rbe_engine* e, const void* data, uint64_t bytes, WireFront* wf) {
+  std::vector<WireIn>& fr = wf->fr;
   // the frame boundaries: magic + size of each header (the receiver's reads)
   const u8* d = (const u8*)data;
-  std::vector<WireIn> fr;
   for (u64 i = 0; i < bytes;) {
     if (bytes - i < kWireHeader || d[i] != 0xAE || d[i + 1] != 0x7D) return RBE_E_CORRUPT;
     u64 size = 0;
@@ -2598,12 +2629,117 @@ static int wire_decode_dev(rbe_engine* e, const void* data, uint64_t bytes, Wire
   if (rc) return rc;
   WireIn* dfr = (WireIn*)(e->wire_in + o_fr);
   WireMsgPos* spos = (WireMsgPos*)(e->wire_in + o_sp);
-  HIP_OK(hipMemcpyAsync(e->wire_in, data, bytes, hipMemcpyHostToDevice, e->stream));
+  // big frames: their chunks and crc segments, in frame order (host lists,
+  // uploaded with the frames)
+  const u64 big = std::min<u64>(e->wire_big, 0xFFFFFF00ull);  // positions are u32
+  std::vector<WireChunk> chunks;
+  std::vector<WireSeg> segs;
+  std::vector<u32> bigf, chunk0;
+  for (u64 i = 0; i < nf; i++)
+    if (fr[i].size > big) {
+      bigf.push_back((u32)i);
+      chunk0.push_back((u32)chunks.size());
+      for (u64 c = 0; c < fr[i].size; c += kWireChunk) chunks.push_back(WireChunk{(u32)i, (u32)c});
+      for (u64 c = 0; c < fr[i].size; c += kWireCrcSeg) segs.push_back(WireSeg{(u32)i, (u32)c});
+    }
+  const u64 nch = chunks.size(), nbig = bigf.size(), nseg = segs.size();
+  u32 *exitv = nullptr, *ent = nullptr, *cbase = nullptr, *dbig = nullptr, *dch0 = nullptr;
+  u16* cntv = nullptr;
+  WireChunk* dch = nullptr;
+  WireSeg* dseg = nullptr;
+  if (nbig) {
+    const u64 o_c = al(bytes * 4), o_ent = o_c + al(bytes * 2), o_base = o_ent + al(nch * 4);
+    const u64 o_ch = o_base + al(nch * 4), o_bf = o_ch + al(nch * sizeof(WireChunk));
+    const u64 o_c0 = o_bf + al(nbig * 4), o_sg = o_c0 + al(nbig * 4);
+    const u64 need = o_sg + al(nseg * sizeof(WireSeg));
+    if ((rc = grow(&e->wire_big_buf, &e->wire_big_bytes, need, false))) return rc;
+    u8* b = e->wire_big_buf;
+    exitv = (u32*)b;
+    cntv = (u16*)(b + o_c);
+    ent = (u32*)(b + o_ent);
+    cbase = (u32*)(b + o_base);
+    dch = (WireChunk*)(b + o_ch);
+    dbig = (u32*)(b + o_bf);
+    dch0 = (u32*)(b + o_c0);
+    dseg = (WireSeg*)(b + o_sg);
+    HIP_OK(hipMemcpyAsync(dch, chunks.data(), nch * sizeof(WireChunk), hipMemcpyHostToDevice,
+                          e->stream));
+    HIP_OK(hipMemcpyAsync(dbig, bigf.data(), nbig * 4, hipMemcpyHostToDevice, e->stream));
+    HIP_OK(hipMemcpyAsync(dch0, chunk0.data(), nbig * 4, hipMemcpyHostToDevice, e->stream));
+    HIP_OK(hipMemcpyAsync(dseg, segs.data(), nseg * sizeof(WireSeg), hipMemcpyHostToDevice,
+                          e->stream));
+    HIP_OK(hipMemsetAsync(ent, 0xFF, nch * 4, e->stream));
+  }
   HIP_OK(hipMemcpyAsync(dfr, fr.data(), nf * sizeof(WireIn), hipMemcpyHostToDevice, e->stream));
-  hipLaunchKernelGGL(k_wire_verify, dim3((unsigned)nf), dim3(256), 0, e->stream, e->wire_in, dfr);
-  hipLaunchKernelGGL(k_wire_bounds, dim3((unsigned)nf), dim3(kWireWalkBlock), 0, e->stream,
-                     e->wire_in, dfr, 2, spos);
+  // The stream goes up in pieces of whole frames on the copy stream, and each
+  // piece's frames are verified and walked on the engine stream as soon as the
+  // piece has landed, so the copy of one piece overlaps the kernels of the last
+  // (the copy stream first waits for the engine stream: the previous call's
+  // kernels may still read wire_in).
+  if (!e->cp_stream) {
+    HIP_OK(hipStreamCreateWithFlags(&e->cp_stream, hipStreamNonBlocking));
+    for (auto& ev : e->cp_ev) HIP_OK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  }
+  constexpr u32 kPieces = rbe_engine::kCopyPieces;
+  HIP_OK(hipEventRecord(e->cp_ev[kPieces], e->stream));
+  HIP_OK(hipStreamWaitEvent(e->cp_stream, e->cp_ev[kPieces], 0));
+  const u64 target = std::max<u64>(bytes / kPieces + 1, 1u << 20);
+  const u8* src = (const u8*)data;
+  u32 piece = 0;
+  for (u64 f = 0; f < nf;) {
+    const u64 lo = fr[f].offset - kWireHeader;
+    u64 g = f + 1;
+    while (g < nf && (piece + 1 == kPieces || fr[g].offset + fr[g].size - lo <= target)) g++;
+    const u64 hi = fr[g - 1].offset + fr[g - 1].size;
+    HIP_OK(hipMemcpyAsync(e->wire_in + lo, src + lo, hi - lo, hipMemcpyHostToDevice, e->cp_stream));
+    HIP_OK(hipEventRecord(e->cp_ev[piece], e->cp_stream));
+    HIP_OK(hipStreamWaitEvent(e->stream, e->cp_ev[piece], 0));
+    hipLaunchKernelGGL(k_wire_verify, dim3((unsigned)(g - f)), dim3(256), 0, e->stream, e->wire_in,
+                       dfr, (u32)f, big);
+    hipLaunchKernelGGL(k_wire_bounds, dim3((unsigned)(g - f)), dim3(kWireWalkBlock), 0, e->stream,
+                       e->wire_in, dfr, 2, spos, big, (u32)f);
+    piece++;
+    f = g;
+  }
+  if (nbig) {
+    hipLaunchKernelGGL(k_wire_chunk_crc, dim3((unsigned)nseg), dim3(256), 0, e->stream, e->wire_in,
+                       dfr, dseg);
+    hipLaunchKernelGGL(k_wire_crc_check, dim3((unsigned)((nbig + 63) / 64)), dim3(64), 0,
+                       e->stream, dfr, dbig, (u32)nbig);
+    hipLaunchKernelGGL(k_wire_chunk_exit, dim3((unsigned)nch), dim3(256), 0, e->stream,
+                       e->wire_in, dfr, dch, exitv, cntv);
+    hipLaunchKernelGGL(k_wire_hop, dim3((unsigned)nbig), dim3(64), 0, e->stream, dfr, dbig, dch0,
+                       exitv, cntv, ent, cbase);
+    hipLaunchKernelGGL(k_wire_chunk_emit, dim3((unsigned)nch), dim3(64), 0, e->stream, e->wire_in,
+                       dfr, dch, ent, cbase, 2, spos);
+  }
   HIP_OK(hipGetLastError());
+  u32 ymax = 1;  // blocks per frame of k_wire_compact
+  for (const auto& w : fr) ymax = std::max<u32>(ymax, std::min<u32>(64, w.pos_cap / 4096 + 1));
+  wf->compact_y = ymax;
+  wf->dfr = dfr;
+  wf->spos = spos;
+  wf->big = big;
+  wf->nch = nch;
+  wf->ent = ent;
+  wf->cbase = cbase;
+  wf->dch = dch;
+  return RBE_OK;
+}
+
+// rbe_wire_decode's device part: verify, find, count, scan and parse.  With
+// `caps` non-null (the caller's capacities: messages, entries, Cmd bytes) the
+// records are not parsed when one is short (RBE_E_NOMEM, counts reported).
+static int wire_decode_dev(rbe_engine* e, const void* data, uint64_t bytes, WireDecoded* o,
+                           const u64* caps) {
+  WireFront wf;
+  int rc = wire_front(e, data, bytes, &wf);
+  if (rc || wf.fr.empty()) return rc;
+  std::vector<WireIn>& fr = wf.fr;
+  const u64 nf = fr.size(), nch = wf.nch, big = wf.big;
+  WireIn* dfr = wf.dfr;
+  WireMsgPos* spos = wf.spos;
+  auto al = [](u64 x) { return (x + 255) & ~255ull; };
   HIP_OK(hipMemcpyAsync(fr.data(), dfr, nf * sizeof(WireIn), hipMemcpyDeviceToHost, e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
   u64 tm = 0;
@@ -2633,12 +2769,15 @@ static int wire_decode_dev(rbe_engine* e, const void* data, uint64_t bytes, Wire
   u32* err = (u32*)(w + o_err);
   HIP_OK(hipMemcpyAsync(dfr, fr.data(), nf * sizeof(WireIn), hipMemcpyHostToDevice, e->stream));
   HIP_OK(hipMemsetAsync(err, 0, 4, e->stream));
-  if (refill)
+  if (refill) {
     hipLaunchKernelGGL(k_wire_bounds, dim3((unsigned)nf), dim3(kWireWalkBlock), 0, e->stream,
-                       e->wire_in, dfr, 1, pos);
-  else
-    hipLaunchKernelGGL(k_wire_compact, dim3((unsigned)nf), dim3(256), 0, e->stream, dfr, spos,
-                       pos);
+                       e->wire_in, dfr, 1, pos, big, 0u);
+    if (nch)
+      hipLaunchKernelGGL(k_wire_chunk_emit, dim3((unsigned)nch), dim3(64), 0, e->stream,
+                         e->wire_in, dfr, wf.dch, wf.ent, wf.cbase, 1, pos);
+  } else
+    hipLaunchKernelGGL(k_wire_compact, dim3((unsigned)nf, wf.compact_y), dim3(256), 0, e->stream,
+                       dfr, spos, pos, ~0ull);
   const unsigned gm = (unsigned)nbk;
   if (tm) {
     hipLaunchKernelGGL(k_wire_parse, dim3(gm), dim3(256), 0, e->stream, e->wire_in, pos, tm, 0,
@@ -2719,14 +2858,151 @@ int rbe_wire_decode(rbe_engine* e, const void* data, uint64_t bytes, rbe_message
   return RBE_OK;
 }
 
+static void note_ingest_caps(rbe_engine* e, u64 tm, u64 te, u64 tc) {
+  e->ing_cap[0] = tm + tm / 4 + 1024;
+  e->ing_cap[1] = te + te / 4 + 1024;
+  e->ing_cap[2] = tc + tc / 4 + 4096;
+}
+
+// The ingest with ONE read-back (no payload heap): decode and ingest kernels
+// launched back to back for the capacities of e->ing_cap, every count read on
+// the device, the writing walk gated on the device by every check before it.
+// *retry: a capacity was short, a frame needs the second walk or was refused —
+// nothing was written and the caller runs the exact path (rbe_wire_ingest),
+// which reports the same statuses as always.
+static int wire_ingest_fast(rbe_engine* e, const void* data, uint64_t bytes,
+                            rbe_wire_ingest_stats* st, bool* retry) {
+  *retry = false;
+  const Params& C = e->C;
+  WireFront wf;
+  int rc = wire_front(e, data, bytes, &wf);
+  if (rc || wf.fr.empty()) return rc;
+  const u64 nf = wf.fr.size();
+  const u64 cm = e->ing_cap[0], ce = e->ing_cap[1], cc = e->ing_cap[2];
+  const u64 nbk = (cm + 255) / 256;
+  auto al = [](u64 x) { return (x + 255) & ~255ull; };
+  // decode records: positions | entry counts | Cmd counts | their scan tops |
+  // message total | messages | entries | Cmd bytes
+  const u64 o_ec = al(cm * sizeof(WireMsgPos)), o_cc = o_ec + al(cm * 8), o_t1 = o_cc + al(cm * 8);
+  const u64 o_t2 = o_t1 + al((nbk + 1) * 8), o_tot = o_t2 + al((nbk + 1) * 8);
+  const u64 o_m = o_tot + 256, o_e = o_m + al(cm * sizeof(rbe_message));
+  const u64 o_c = o_e + al(ce * sizeof(rbe_entry)), need_rec = o_c + al(cc) + 256;
+  if ((rc = grow(&e->wire_rec, &e->wire_rec_bytes, need_rec, false))) return rc;
+  u8* w = e->wire_rec;
+  WireMsgPos* pos = (WireMsgPos*)w;
+  u64 *ec = (u64*)(w + o_ec), *ccn = (u64*)(w + o_cc), *t1 = (u64*)(w + o_t1), *t2 = (u64*)(w + o_t2);
+  u64* tot = (u64*)(w + o_tot);
+  rbe_message* dm = (rbe_message*)(w + o_m);
+  rbe_entry* de = (rbe_entry*)(w + o_e);
+  u8* dc = w + o_c;
+  // ingest scratch, as the exact path's, for cm messages
+  const u64 drop = (u64)C.n_rep * C.n;
+  int bits = 1;
+  while (bits < 64 && (drop >> bits)) bits++;
+  size_t tb = 0;
+  if (dev_sort_pairs(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, cm, bits, e->stream))
+    return RBE_E_HIP;
+  const u64 o_sk = al(cm * 8), o_hb = o_sk + al(cm * 8), o_hs = o_hb + al(cm * 8);
+  const u64 o_ix = o_hs + al(cm * 8), o_si = o_ix + al(cm * 4), o_top = o_si + al(cm * 4);
+  const u64 o_err = o_top + al((nbk + 1) * 8), o_tmp = o_err + 256;
+  if ((rc = grow(&e->ing_dev, &e->ing_dev_bytes, o_tmp + al(tb), false))) return rc;
+  u8* b = e->ing_dev;
+  u64 *key = (u64*)b, *skey = (u64*)(b + o_sk), *hb = (u64*)(b + o_hb), *hs = (u64*)(b + o_hs);
+  u32 *idx = (u32*)(b + o_ix), *sidx = (u32*)(b + o_si);
+  u64* top = (u64*)(b + o_top);
+  u32* err = (u32*)(b + o_err);     // [0] ingest checks (ING_*), [1] decode flags (WD_*)
+  u32* dfl = err + 1;
+  unsigned long long* ndrop = (unsigned long long*)(b + o_err + 8);
+  HIP_OK(hipMemsetAsync(b + o_err, 0, 16, e->stream));
+  const unsigned g = (unsigned)nbk;
+  hipLaunchKernelGGL(k_wire_frames_scan, dim3(1), dim3(256), 0, e->stream, wf.dfr, (u32)nf, cm,
+                     tot, dfl);
+  hipLaunchKernelGGL(k_wire_compact, dim3((unsigned)nf, wf.compact_y), dim3(256), 0, e->stream,
+                     wf.dfr, wf.spos, pos, cm);
+  hipLaunchKernelGGL(k_wire_parse, dim3(g), dim3(256), 0, e->stream, e->wire_in, pos, cm, 0, ec,
+                     ccn, nullptr, nullptr, nullptr, dfl, tot, nullptr, nullptr, 0ull, 0ull, dfl);
+  hipLaunchKernelGGL(k_scan_blocks, dim3(g), dim3(256), 0, e->stream, ec, cm, t1);
+  hipLaunchKernelGGL(k_scan_blocks, dim3(g), dim3(256), 0, e->stream, ccn, cm, t2);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, e->stream, t1, (u32)nbk);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, e->stream, t2, (u32)nbk);
+  hipLaunchKernelGGL(k_scan_add, dim3(g), dim3(256), 0, e->stream, ec, cm, t1);
+  hipLaunchKernelGGL(k_scan_add, dim3(g), dim3(256), 0, e->stream, ccn, cm, t2);
+  hipLaunchKernelGGL(k_wire_parse, dim3(g), dim3(256), 0, e->stream, e->wire_in, pos, cm, 1, ec,
+                     ccn, dm, de, dc, dfl, tot, t1 + nbk, t2 + nbk, ce, cc, dfl);
+  const u32 par = (e->round - 1) & 1u;
+  rc = dispatch_n(C.n, [&](auto NN) {
+    constexpr int N = decltype(NN)::value;
+    hipLaunchKernelGGL(k_ing_key<N>, dim3(g), dim3(256), 0, e->stream, C, (u64)C.heap_bytes, dm,
+                       (const rbe_entry*)de, (const u64*)ec, cm, key, idx, hb, err, ndrop,
+                       e->P.node_ids, (const u64*)tot, (const u32*)dfl);
+    return RBE_OK;
+  });
+  if (rc) return rc;
+  HIP_OK(hipGetLastError());
+  if (dev_sort_pairs(b + o_tmp, &tb, key, skey, idx, sidx, cm, bits, e->stream)) return RBE_E_HIP;
+  hipLaunchKernelGGL(k_ing_gather, dim3(g), dim3(256), 0, e->stream, (const u32*)sidx,
+                     (const u64*)hb, hs, cm);
+  hipLaunchKernelGGL(k_scan_blocks, dim3(g), dim3(256), 0, e->stream, hs, cm, top);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, e->stream, top, (u32)nbk);
+  hipLaunchKernelGGL(k_scan_add, dim3(g), dim3(256), 0, e->stream, hs, cm, (const u64*)top);
+  for (int wr = 0; wr < 2; wr++) {
+    rc = dispatch_n(C.n, [&](auto NN) {
+      constexpr int N = decltype(NN)::value;
+      if (wr)
+        hipLaunchKernelGGL((k_ing_walk<N, true>), dim3(g), dim3(256), 0, e->stream, e->P, C, par,
+                           e->round, (const u64*)skey, (const u32*)sidx, cm, (const rbe_message*)dm,
+                           (const rbe_entry*)de, (const u64*)ec, (const u64*)ccn, (const u8*)dc,
+                           e->heap, (u64)C.heap_bytes, 0ull, (const u64*)hs, err, (const u32*)err);
+      else
+        hipLaunchKernelGGL((k_ing_walk<N, false>), dim3(g), dim3(256), 0, e->stream, e->P, C, par,
+                           e->round, (const u64*)skey, (const u32*)sidx, cm, (const rbe_message*)dm,
+                           (const rbe_entry*)de, (const u64*)ec, (const u64*)ccn, (const u8*)dc,
+                           e->heap, (u64)C.heap_bytes, 0ull, (const u64*)hs, err, nullptr);
+      HIP_OK(hipGetLastError());
+      return RBE_OK;
+    });
+    if (rc) return rc;
+  }
+  u64 back[6];  // err | flags, drops, messages, entries, Cmd bytes, heap bytes
+  HIP_OK(hipMemcpyAsync(back, err, 16, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipMemcpyAsync(back + 2, tot, 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipMemcpyAsync(back + 3, t1 + nbk, 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipMemcpyAsync(back + 4, t2 + nbk, 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipMemcpyAsync(back + 5, top + nbk, 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  const u32 ferr = (u32)back[0], flags = (u32)(back[0] >> 32);
+  if (flags || back[5]) {  // nothing written: the exact path decides (and reports)
+    *retry = true;
+    return RBE_OK;
+  }
+  st->frames = nf;
+  st->messages = back[2];
+  st->entries = back[3];
+  st->cmd_bytes = back[4];
+  note_ingest_caps(e, back[2], back[3], back[4]);
+  if (ferr & ING_INVALID) return RBE_E_INVALID;
+  if (ferr & ING_NOMEM) return RBE_E_NOMEM;
+  st->dropped = back[1];
+  return RBE_OK;
+}
+
 // Device ingest of inbound frames (rbe_ingest.h): decode, check, sort by inbox
 // list, check capacities, one read-back, reserve heap room, write the lists.
+// Without a payload heap, and once a call has measured the traffic, the whole
+// pipeline runs with one read-back at its end (wire_ingest_fast); the exact
+// path below reads counts back between its stages.
 int rbe_wire_ingest(rbe_engine* e, const void* data, uint64_t bytes, rbe_wire_ingest_stats* st) {
   if (!e || (bytes && !data) || !st || e->round == 0) return RBE_E_INVALID;
   memset(st, 0, sizeof(*st));
   const Params& C = e->C;
   if (C.rep_world <= 1) return RBE_E_STATE;  // every sender is stepped here
   HIP_OK(hipSetDevice(e->device));
+  if (!C.heap_bytes && e->ing_cap[0] && !getenv("RBE_INGEST_EXACT")) {
+    bool retry = false;
+    const int rc = wire_ingest_fast(e, data, bytes, st, &retry);
+    if (!retry) return rc;
+    memset(st, 0, sizeof(*st));
+  }
   WireDecoded o;
   int rc = wire_decode_dev(e, data, bytes, &o, nullptr);
   st->frames = o.frames;
@@ -2734,6 +3010,7 @@ int rbe_wire_ingest(rbe_engine* e, const void* data, uint64_t bytes, rbe_wire_in
   st->entries = o.te;
   st->cmd_bytes = o.tc;
   if (rc) return rc;
+  note_ingest_caps(e, o.tm, o.te, o.tc);
   const u64 tm = o.tm;
   if (tm == 0) return RBE_OK;
   if (tm > 0x7FFFFFFFull) return RBE_E_NOMEM;

@@ -299,18 +299,23 @@ struct WireIn {  // one inbound frame
   u64 pos0;          // its first slot in the single-pass position area
   u64 pad0;
   u32 n_msgs, pos_cap;  // requests; slots reserved for them (single pass)
-  u64 pad1;
+  u32 crc_want, crc_acc;  // big frames: the header's payload crc; the XOR of the chunks' shifted crcs
   u32 status;  // 0 ok, 1 header crc, 2 payload crc, 3 malformed, 4 more requests than slots
   u32 pad;
 };
 
-__global__ __launch_bounds__(256) void k_wire_verify(const u8* data, WireIn* fr) {
+// One block per frame of [f0, f0 + grid): both crc32s.  A frame longer than
+// `big` has its header checked here and its payload crc left to
+// k_wire_chunk_crc (many blocks per frame) and k_wire_crc_check.
+__global__ __launch_bounds__(256) void k_wire_verify(const u8* data, WireIn* fr, u32 f0, u64 big) {
   __shared__ u32 s_table[1024], s_x2n[32], s_crc[256];
   crc_tables_lds(s_table);
   if (threadIdx.x < 32) s_x2n[threadIdx.x] = kCrcX2n.v[threadIdx.x];
   __syncthreads();
-  WireIn f = fr[blockIdx.x];
-  const u32 c = block_crc32(data + f.offset, f.size, s_table, s_x2n, s_crc);
+  const u32 fi = f0 + blockIdx.x;
+  WireIn f = fr[fi];
+  const bool chunked = f.size > big;
+  const u32 c = chunked ? 0u : block_crc32(data + f.offset, f.size, s_table, s_x2n, s_crc);
   if (threadIdx.x == 0) {
     const u8* h = data + f.offset - 18;
     u8 hb[18];
@@ -324,9 +329,45 @@ __global__ __launch_bounds__(256) void k_wire_verify(const u8* data, WireIn* fr)
     const u32 method = ((u32)hb[0] << 8) | hb[1];
     if (crc32_update(0, hb, 18, s_table) != inc) st = 1;
     else if (method != 100u) st = 3;
-    else if (pc != c) st = 2;
-    fr[blockIdx.x].status = st;
+    else if (!chunked && pc != c) st = 2;
+    fr[fi].status = st;
+    if (chunked) fr[fi].crc_want = pc;
   }
+}
+
+// A big frame's payload crc by 64 KiB segments, one block each: the
+// segment's crc shifted to the frame's end (crc32_combine is linear, as in
+// block_crc32) XORed into crc_acc; then one lane per frame compares.
+static constexpr u32 kWireCrcSeg = 65536;
+struct WireSeg {
+  u32 frame, start;
+};
+__global__ __launch_bounds__(256) void k_wire_chunk_crc(const u8* data, WireIn* fr,
+                                                        const WireSeg* seg) {
+  __shared__ u32 s_table[1024], s_x2n[32], s_crc[256];
+  crc_tables_lds(s_table);
+  if (threadIdx.x < 32) s_x2n[threadIdx.x] = kCrcX2n.v[threadIdx.x];
+  __syncthreads();
+  const WireSeg sg = seg[blockIdx.x];
+  const WireIn f = fr[sg.frame];
+  const u64 lo = sg.start, hi = f.size - lo < kWireCrcSeg ? f.size : lo + kWireCrcSeg;
+  u32 c = block_crc32(data + f.offset + lo, hi - lo, s_table, s_x2n, s_crc);
+  if (threadIdx.x == 0) {
+    u64 rest = f.size - hi;
+    if (c && rest) {
+      u32 sh = 1u << 31;  // x^(8 rest) mod P
+      for (u32 k = 3; rest; rest >>= 1, k++)
+        if (rest & 1u) sh = crc_multmodp(s_x2n[k & 31], sh);
+      c = crc_multmodp(sh, c);
+    }
+    if (c) atomicXor(&fr[sg.frame].crc_acc, c);
+  }
+}
+__global__ __launch_bounds__(64) void k_wire_crc_check(WireIn* fr, const u32* bigf, u32 nbig) {
+  const u32 i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= nbig) return;
+  WireIn& f = fr[bigf[i]];
+  if (f.status == 0 && f.crc_acc != f.crc_want) f.status = 2;
 }
 
 // Decode is parallel per message: one block per frame finds the top-level
@@ -354,12 +395,13 @@ __device__ __forceinline__ u64 uni64(u64 x) {
 static constexpr u32 kWireWin = 8192;
 static constexpr u32 kWireWalkBlock = 64;
 __global__ __launch_bounds__(kWireWalkBlock) void k_wire_bounds(const u8* data, WireIn* fr, int pass,
-                                                     WireMsgPos* pos) {
+                                                     WireMsgPos* pos, u64 big, u32 f0) {
   __shared__ __attribute__((aligned(16))) u8 s_buf[kWireWin + 16];
-  __shared__ u64 s_at, s_base, s_nm;
+  __shared__ u64 s_at, s_nm;
   __shared__ u32 s_state;  // 0 walking, 1 done, 2 bad
-  const WireIn f = fr[blockIdx.x];
-  if (f.status) return;
+  const u32 fi = f0 + blockIdx.x;
+  const WireIn f = fr[fi];
+  if (f.status || f.size > big) return;  // a big frame is walked by chunks (below)
   const u8* p = data + f.offset;
   const u64 n = uni64(f.size);
   if (threadIdx.x == 0) {
@@ -514,28 +556,288 @@ __global__ __launch_bounds__(kWireWalkBlock) void k_wire_bounds(const u8* data, 
   }
   if (threadIdx.x == 0) {
     if (s_state == 2) {
-      fr[blockIdx.x].status = 3;
+      fr[fi].status = 3;
     } else if (pass != 1) {
-      fr[blockIdx.x].n_msgs = (u32)s_nm;
-      if (pass == 2 && s_nm > f.pos_cap) fr[blockIdx.x].status = 4;
+      fr[fi].n_msgs = (u32)s_nm;
+      if (pass == 2 && s_nm > f.pos_cap) fr[fi].status = 4;
     }
   }
 }
 
-// a frame's single-pass positions to their place in request order
-__global__ __launch_bounds__(256) void k_wire_compact(const WireIn* fr, const WireMsgPos* pos,
-                                                      WireMsgPos* out) {
-  const WireIn f = fr[blockIdx.x];
-  for (u32 j = threadIdx.x; j < f.n_msgs; j += 256) out[f.msg0 + j] = pos[f.pos0 + j];
+// ------------------------------------------------- big frames, walked by chunks
+// A frame longer than the engine's walk threshold (rbe_engine.hip, wire_big) is
+// cut into kWireChunk-byte chunks and its top level walked in three launches,
+// so the walk no longer runs one field at a time across the whole frame:
+//   k_wire_chunk_exit  block per chunk: for EVERY byte position p of the
+//                      chunk, where the field walk started at p leaves the
+//                      chunk (its exit) and how many requests it passes —
+//                      each position's next field (wire_field_end) in LDS,
+//                      then pointer doubling over the chunk (log2 steps)
+//   k_wire_hop         lane per frame: the true walk from position 0, one
+//                      exit per chunk (a frame of 7 MB: ~900 hops, not ~130k
+//                      field headers); each chunk's entry and request base
+//   k_wire_chunk_emit  block per chunk: the walk from the chunk's entry to
+//                      its end, request positions written at their base
+// Same rules and the same results as k_wire_bounds (MessageBatch.Unmarshal,
+// raft_optimized.go:1051-1204; skipRaft for the trailer fields).
+static constexpr u32 kWireChunk = 8192;
+static constexpr u32 kWireNone = 0xFFFFFFFFu;  // exit of a malformed walk; entry of an unvisited chunk
+struct WireChunk {
+  u32 frame, start;  // the frame's index, the chunk's first payload byte
+};
+// One top-level field at payload position i (< n), bytes read through at(q):
+// its end, or ~0 when malformed (k_wire_bounds' rules); a request (field 1,
+// length-delimited) sets *req and its body start.
+template <class At>
+RBE_HD u64 wire_field_end(At at, u64 i, u64 n, u64* body, bool* req) {
+  u64 q = i, tag = 0;
+  bool ok = false;
+  for (u32 bs = 0; bs < 64 && q < n; bs += 7) {
+    const u8 b = at(q++);
+    tag |= (u64)(b & 0x7F) << bs;
+    if (b < 0x80) {
+      ok = true;
+      break;
+    }
+  }
+  if (!ok) return ~0ull;
+  const u32 wt = (u32)(tag & 7);
+  if (wt == 0 || wt == 2) {
+    u64 v = 0;
+    ok = false;
+    for (u32 bs = 0; bs < 64 && q < n; bs += 7) {
+      const u8 b = at(q++);
+      v |= (u64)(b & 0x7F) << bs;
+      if (b < 0x80) {
+        ok = true;
+        break;
+      }
+    }
+    if (!ok) return ~0ull;
+    if (wt == 2) {
+      if (v > n - q) return ~0ull;
+      *body = q;
+      *req = (tag >> 3) == 1;
+      q += v;
+    }
+    return q;
+  }
+  if (wt == 1 || wt == 5) {
+    q += wt == 1 ? 8 : 4;
+    return q > n ? ~0ull : q;
+  }
+  return ~0ull;
 }
 
-// pass 0: entries and Cmd bytes of each message; pass 1: the records
+__global__ __launch_bounds__(256) void k_wire_chunk_exit(const u8* data, const WireIn* fr,
+                                                         const WireChunk* ch, u32* exitv,
+                                                         u16* cntv) {
+  constexpr u32 kPer = kWireChunk / 256;
+  __shared__ __attribute__((aligned(16))) u8 s_b[kWireChunk + 32];
+  __shared__ u32 s_x[kWireChunk];
+  __shared__ u16 s_c[kWireChunk];
+  const WireChunk c = ch[blockIdx.x];
+  const WireIn f = fr[c.frame];
+  if (f.status) return;
+  const u64 n = f.size;
+  const u32 cb = c.start;
+  const u32 ce = (u32)(n - cb < kWireChunk ? n : cb + kWireChunk);
+  // bytes [cb, ce + 32) (or to the frame's end): a field header that starts
+  // in the chunk is at most 20 bytes
+  const u32 le = (u32)(n - ce < 32 ? n : ce + 32);
+  const u8* p = data + f.offset;
+  for (u32 j = threadIdx.x; j < le - cb; j += 256) s_b[j] = p[cb + j];
+  __syncthreads();
+  auto at = [&](u64 q) { return s_b[(u32)q - cb]; };
+#pragma unroll
+  for (u32 k = 0; k < kPer; k++) {
+    const u32 j = threadIdx.x + k * 256;
+    if (j < ce - cb) {
+      u64 body = 0;
+      bool req = false;
+      const u64 e = wire_field_end(at, cb + j, n, &body, &req);
+      s_x[j] = e == ~0ull ? kWireNone : (u32)e;
+      s_c[j] = req ? 1 : 0;
+    }
+  }
+  __syncthreads();
+  // pointer doubling: each pass composes every position's walk with the walk
+  // from where it stops, until every walk has left the chunk (or failed)
+  for (;;) {
+    u32 nx[kPer];
+    u32 nc[kPer];
+    bool chg = false;
+#pragma unroll
+    for (u32 k = 0; k < kPer; k++) {
+      const u32 j = threadIdx.x + k * 256;
+      nx[k] = kWireNone;
+      nc[k] = 0;
+      if (j < ce - cb) {
+        const u32 x = s_x[j];
+        nx[k] = x;
+        nc[k] = s_c[j];
+        if (x != kWireNone && x < ce) {
+          nx[k] = s_x[x - cb];
+          nc[k] += s_c[x - cb];
+          chg = true;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (u32 k = 0; k < kPer; k++) {
+      const u32 j = threadIdx.x + k * 256;
+      if (j < ce - cb) {
+        s_x[j] = nx[k];
+        s_c[j] = (u16)nc[k];
+      }
+    }
+    if (!__syncthreads_or(chg)) break;
+  }
+  for (u32 j = threadIdx.x; j < ce - cb; j += 256) {
+    exitv[f.offset + cb + j] = s_x[j];
+    cntv[f.offset + cb + j] = s_c[j];
+  }
+}
+
+// one lane per big frame (bigf: frame indexes, chunk0: each one's first chunk)
+__global__ __launch_bounds__(64) void k_wire_hop(WireIn* fr, const u32* bigf, const u32* chunk0,
+                                                 const u32* exitv, const u16* cntv, u32* ent,
+                                                 u32* base) {
+  if (threadIdx.x) return;
+  const u32 fi = bigf[blockIdx.x];
+  const WireIn f = fr[fi];
+  if (f.status) return;
+  const u32 c0 = chunk0[blockIdx.x];
+  u64 e = 0, run = 0;
+  bool bad = false;
+  while (e < f.size) {
+    const u32 c = c0 + (u32)(e / kWireChunk);
+    const u32 x = exitv[f.offset + e];
+    const u32 k = cntv[f.offset + e];
+    ent[c] = (u32)e;
+    base[c] = (u32)run;
+    if (x == kWireNone) {
+      bad = true;
+      break;
+    }
+    run += k;
+    e = x;
+  }
+  if (bad) {
+    fr[fi].status = 3;
+  } else {
+    fr[fi].n_msgs = (u32)run;
+    if (run > f.pos_cap) fr[fi].status = 4;
+  }
+}
+
+// pass 2: positions into the frame's single-pass slots; pass 1: at msg0
+__global__ __launch_bounds__(64) void k_wire_chunk_emit(const u8* data, const WireIn* fr,
+                                                        const WireChunk* ch, const u32* ent,
+                                                        const u32* base, int pass,
+                                                        WireMsgPos* pos) {
+  __shared__ __attribute__((aligned(16))) u8 s_b[kWireChunk + 32];
+  const WireChunk c = ch[blockIdx.x];
+  const WireIn f = fr[c.frame];
+  const u32 e0 = ent[blockIdx.x];
+  if (f.status || e0 == kWireNone) return;
+  const u64 n = f.size;
+  const u32 cb = c.start;
+  const u32 ce = (u32)(n - cb < kWireChunk ? n : cb + kWireChunk);
+  const u32 le = (u32)(n - ce < 32 ? n : ce + 32);
+  const u8* p = data + f.offset;
+  for (u32 j = threadIdx.x; j < le - cb; j += 64) s_b[j] = p[cb + j];
+  __syncthreads();
+  auto at = [&](u64 q) { return (u8)uni32(s_b[(u32)q - cb]); };
+  u64 i = e0;
+  u32 m = base[blockIdx.x];
+  while (i < ce) {  // every field here is well formed: k_wire_hop walked it
+    u64 body = 0;
+    bool req = false;
+    const u64 e = wire_field_end(at, i, n, &body, &req);
+    if (req) {
+      if (threadIdx.x == 0) {
+        if (pass == 1) pos[f.msg0 + m] = WireMsgPos{f.offset + body, e - body};
+        else if (m < f.pos_cap) pos[f.pos0 + m] = WireMsgPos{f.offset + body, e - body};
+      }
+      m++;
+    }
+    i = e;
+  }
+}
+
+// Decode without a read-back in the middle (rbe_wire_ingest): the kernels
+// after the walk are launched for capacities the host chose beforehand, read
+// the true counts from the device, and raise WD_RETRY in `flags` instead of
+// writing past a capacity (the host then decodes again with the counts it
+// reads back); WD_CORRUPT reports a frame the walk refused.
+enum : u32 { WD_CORRUPT = 1u, WD_RETRY = 2u };
+// One block: each frame's first request (msg0, an exclusive scan of n_msgs in
+// frame order), the total at tot[0], and the frames' statuses folded into flags.
+__global__ __launch_bounds__(256) void k_wire_frames_scan(WireIn* fr, u32 nf, u64 cap_m, u64* tot,
+                                                          u32* flags) {
+  __shared__ u64 s_tmp[4];
+  u64 carry = 0;
+  u32 fl = 0;
+  for (u32 b0 = 0; b0 < nf; b0 += 256) {
+    const u32 i = b0 + threadIdx.x;
+    u64 x = 0;
+    if (i < nf) {
+      const u32 st = fr[i].status;
+      if (st == 4) fl |= WD_RETRY;
+      else if (st) fl |= WD_CORRUPT;
+      x = st ? 0 : fr[i].n_msgs;
+    }
+    u64 t = 0;
+    const u64 pre = block_scan_u64(x, &t, s_tmp);
+    if (i < nf) fr[i].msg0 = carry + pre;
+    carry += t;
+  }
+  if (fl) atomicOr(flags, fl);
+  if (threadIdx.x == 0) {
+    tot[0] = carry;
+    if (carry > cap_m) atomicOr(flags, WD_RETRY);
+  }
+}
+
+// a frame's single-pass positions to their place in request order (at most
+// cap_m positions in all: past it the decode is retried)
+// (grid: frames x blocks per frame)
+__global__ __launch_bounds__(256) void k_wire_compact(const WireIn* fr, const WireMsgPos* pos,
+                                                      WireMsgPos* out, u64 cap_m) {
+  const WireIn f = fr[blockIdx.x];
+  if (f.status) return;
+  for (u32 j = blockIdx.y * 256 + threadIdx.x; j < f.n_msgs && f.msg0 + j < cap_m;
+       j += 256 * gridDim.y)
+    out[f.msg0 + j] = pos[f.pos0 + j];
+}
+
+// pass 0: entries and Cmd bytes of each message; pass 1: the records.  With
+// `dtm` (the no-read-back decode) nm is the launched capacity and *dtm the
+// messages: pass 0 zeroes the counts past *dtm (so the scans over nm stay
+// exact), pass 1 writes nothing when the scanned totals (*te, *tc) exceed the
+// record capacities cap_e / cap_c, and nothing after a refused frame.
 __global__ __launch_bounds__(256) void k_wire_parse(const u8* data, const WireMsgPos* pos,
                                                     u64 nm, int pass, u64* ecnt, u64* ccnt,
                                                     rbe_message* msgs, rbe_entry* ents, u8* cmd,
-                                                    u32* err) {
+                                                    u32* err, const u64* dtm = nullptr,
+                                                    const u64* te = nullptr, const u64* tc = nullptr,
+                                                    u64 cap_e = 0, u64 cap_c = 0,
+                                                    u32* flags = nullptr) {
   const u64 j = (u64)blockIdx.x * 256 + threadIdx.x;
   if (j >= nm) return;
+  if (dtm) {
+    if (*flags) return;
+    if (j >= *dtm) {
+      if (!pass) ecnt[j] = ccnt[j] = 0;
+      return;
+    }
+    if (pass && (*te > cap_e || *tc > cap_c)) {
+      if (j == 0) atomicOr(flags, WD_RETRY);
+      return;
+    }
+  }
   const WireMsgPos q = pos[j];
   WireRd rd{data, q.at + q.len, q.at, false};
   u64 cb = pass ? ccnt[j] : 0;
@@ -586,13 +888,23 @@ __global__ __launch_bounds__(256) void k_scan_add(u64* v, u64 n, const u64* top)
 // rbe_wire_ingest (rbe_ingest.h): decoded records → inbox plane slots.
 namespace rbe {
 
+// With `dtm` (the no-read-back decode) nm is the launched capacity: the
+// positions past *dtm become drop keys (sorted last, never listed or counted)
 template <int N>
 __global__ __launch_bounds__(256) void k_ing_key(Params C, u64 heap_cap, rbe_message* msgs,
                                                  const rbe_entry* ents, const u64* ent0, u64 nm,
                                                  u64* key, u32* idx, u64* hb, u32* err,
-                                                 unsigned long long* ndrop, const u64* ids) {
+                                                 unsigned long long* ndrop, const u64* ids,
+                                                 const u64* dtm = nullptr,
+                                                 const u32* flags = nullptr) {
   const u64 j = (u64)blockIdx.x * 256 + threadIdx.x;
   if (j >= nm) return;
+  if (dtm && (j >= *dtm || *flags)) {
+    key[j] = ing_drop_key(C);
+    idx[j] = (u32)j;
+    hb[j] = 0;
+    return;
+  }
   u32 e = 0;
   u64 h = 0;
   if (ids) {  // node ids → internal ids, in place for the walk that scatters them
@@ -620,9 +932,12 @@ __global__ __launch_bounds__(256) void k_ing_walk(Planes P, Params C, u32 par, u
                                                   const rbe_message* msgs, const rbe_entry* ents,
                                                   const u64* ent0, const u64* cmd0, const u8* cmd,
                                                   u8* heap, u64 heap_cap, u64 base, const u64* hs,
-                                                  u32* err) {
+                                                  u32* err, const u32* gate = nullptr) {
   const u64 p = (u64)blockIdx.x * 256 + threadIdx.x;
   if (p >= nm || !ingest_run_start(C, skey, p)) return;
+  // the writing walk of the no-read-back ingest: nothing at all when the
+  // checking walk or the decode found anything (all-or-nothing)
+  if (WRITE && gate && (gate[0] | gate[1])) return;
   const u64 q = ingest_run_end(C, skey, p, nm);
   const u32 e = ingest_sender<N, WRITE>(P, C, par, round, skey, sidx, p, q, msgs, ents, ent0, cmd0,
                                         cmd, heap, heap_cap, base, hs);

@@ -14,9 +14,10 @@ import argparse
 import ctypes as C
 import json
 import sys
+import os
 import time
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from dragonboat_amd.engine import (Engine, RbeWireIngestStats, _check,  # noqa: E402
                                    wire_config)

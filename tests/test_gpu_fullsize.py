@@ -1,6 +1,7 @@
 """Full-size runs of the HIP engine at the BASELINE configurations the bench
-quotes — C4 (1M groups x 3, Quiesce, 90% idle, 9:1 ReadIndex:propose) and C3
-(100k groups x 5, CheckQuorum, leader isolation) — in the bench's untraced
+quotes — C4 (1M groups x 3, Quiesce, 90% idle, 9:1 ReadIndex:propose), C3
+(100k groups x 5, CheckQuorum, leader isolation) and C2 (10k groups x 3, one
+proposal per group per round) — in the bench's untraced
 mode, checked through properties that hold at any size plus the oracle on a
 seeded sample of groups:
 
@@ -24,7 +25,9 @@ C4_FULL = dict(n_groups=1_000_000, n_replicas=3, quiesce=True, wl_enabled=True,
                wl_start_round=30, wl_active_mod=10, wl_read_permille=900)
 C3_FULL = dict(n_groups=100_000, n_replicas=5, check_quorum=True, wl_enabled=True,
                wl_start_round=40, iso_period=50, iso_len=30, iso_mod=10)
-ENGINE = {"C4": dict(ring=64), "C3": dict(ring=128, ecap=256)}
+C2_FULL = dict(n_groups=10_000, n_replicas=3, wl_enabled=True, wl_start_round=30)
+ENGINE = {"C4": dict(ring=64), "C3": dict(ring=128, ecap=256), "C2": dict(ring=64)}
+SAMPLE = {"C4": 48, "C3": 48, "C2": 160}
 FIELDS = [f for f in O.VIEW_FIELDS if f != "digest"]
 
 
@@ -72,7 +75,8 @@ def _sampled_oracle(eng, kw, rounds, groups):
 
 
 @pytest.mark.parametrize("name,kw,rounds,check_every",
-                         [("C4", C4_FULL, 400, 100), ("C3", C3_FULL, 300, 50)])
+                         [("C4", C4_FULL, 400, 100), ("C3", C3_FULL, 300, 50),
+                          ("C2", C2_FULL, 300, 50)])
 def test_fullsize_properties_and_sampled_oracle(gpu_available, name, kw, rounds, check_every):
     from dragonboat_amd.engine import Engine
     eng = Engine(device=0, trace=False, **kw, **ENGINE[name])
@@ -87,7 +91,11 @@ def test_fullsize_properties_and_sampled_oracle(gpu_available, name, kw, rounds,
         prev = _check_properties(_fields(eng), n, prev)
     c = eng.counters()
     assert c["committed"] > 0
+    if name == "C2":  # one proposal per group per round from round 30 on: every group
+        v = _fields(eng)  # commits (proposals before its first leader are dropped)
+        lead = v["committed"].reshape(-1, n).max(axis=1)
+        assert (lead >= (rounds - kw["wl_start_round"]) // 2).all(), int(lead.min())
     rng = np.random.RandomState(0x5EED)
-    sample = rng.choice(kw["n_groups"], 48, replace=False)
+    sample = rng.choice(kw["n_groups"], SAMPLE[name], replace=False)
     _sampled_oracle(eng, kw, rounds, sample)
     eng.close()
