@@ -678,6 +678,8 @@ struct rbe_engine {
   u64 wire_frames_off = 0;   // frame index inside wire_meta
 };
 
+unsigned rbe::g_fast_grid = rbe::kFastGrid;
+
 static void drop_graphs(rbe_engine* e) {
   for (int i = 0; i < rbe_engine::kGraphs; i++)
     if (e->graph[i]) {
@@ -1119,6 +1121,7 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   }
   HIP_IGNORE(hipMemsetAsync(e->d_clk, 0, 2 * sizeof(u32), e->stream));
   if (const char* wb = getenv("RBE_WIRE_BIG")) e->wire_big = strtoull(wb, nullptr, 10);
+  if (const char* fg = getenv("RBE_FAST_GRID")) g_fast_grid = (unsigned)strtoul(fg, nullptr, 10);
   const char* mode = getenv("RBE_MODE");
   // default: k_triage → k_fast_both → k_full_list; RBE_MODE=split runs the two
   // roles as separate launches, RBE_MODE=fused k_round + k_full_list,
@@ -1182,6 +1185,8 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
     e->L.al_on = C.quiesce && !C.trace && C.rep_world == 1 && (e->mode == 1 || e->mode == 3) &&
                  !(gl && strcmp(gl, "0") == 0);
   }
+  e->L.vgrid = 700u;
+  if (const char* vg = getenv("RBE_FAST_VGRID")) e->L.vgrid = (u32)strtoul(vg, nullptr, 10);
   // pack counters, then the sticky overflow flag of the fixed-layout exchange
   if (hipMalloc(&e->xcount, (kXchgMaxWorld * XS_NUM + 1) * sizeof(u32)) != hipSuccess) {
     rbe_destroy(e);

@@ -93,6 +93,9 @@ __device__ __forceinline__ u32 wave_sum(u32 v) {
 // Every thread of the block must call this (it synchronises the block).
 template <int KS>
 __device__ __forceinline__ void flush_counters(const Planes& P, const StepCounters& c) {
+#if defined(RBE_ABLATE_COUNTERS)  // diagnostic A/B builds only: the flush's cost
+  if (KS >= 0) return;
+#endif
   __shared__ u32 s_ctr[kBlock / 64][C_NUM];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
@@ -140,6 +143,9 @@ __device__ __forceinline__ void lds_counters_init(u32 (*slots)[kBlock]) {
 // Every thread of the block must call this (it synchronises the block).
 template <int KS>
 __device__ __forceinline__ void flush_lds_counters(const Planes& P, u32 (*slots)[kBlock]) {
+#if defined(RBE_ABLATE_COUNTERS)
+  if (KS >= 0) return;
+#endif
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   // wave w sums counters w, w + 4, ...: lane l adds slots l, l + 64, ...
@@ -198,6 +204,7 @@ struct Lists {
                          // [2 + 2p], [3 + 2p]: changes made in a round of parity p
   const u32* scan_round; // a round that must scan every group (launch, import)
   u32 al_on;             // list mode on (Quiesce, untraced, rep_world 1, a k_triage pipeline)
+  u32 vgrid;             // k_fast_both's blocks per 1000 chunks (700; RBE_FAST_VGRID for A/B)
 };
 // work-list entries carry their inbound summary word for N = 3 (14 bits; the
 // LDS compaction packs it with the 11-bit block position in one u32)
@@ -704,28 +711,38 @@ __global__ __launch_bounds__(kBlock, kFastWaves<N>) void k_fast_both(Planes P, P
   const Clk ck = clk_of(ra);
   const u32 round = ck.round;
   const u32 par = round & 1u;
-#if RBE_FAST_LDS_CTR
-  __shared__ u32 s_ctr_slots[C_NUM][kBlock];
-  lds_counters_init<KS_FAST_LEAD>(s_ctr_slots);
-  LdsCounters c{{&s_ctr_slots[0][threadIdx.x]}};
-#endif
   // segments: leader fronts, leader backs, follower fronts, follower backs
   __shared__ u32 s_pre[4 * kShards + 1];
   const u32 slots[4] = {0, 3, 1, 4};
   seg_build<4>(L, par, slots, s_pre);
   const u32 nl = s_pre[2 * kShards], n = s_pre[4 * kShards];
-#if !RBE_FAST_LDS_CTR
-  StepCounters c;
-#pragma unroll
-  for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
-#endif
   // a small engine spreads its items over twice the blocks (half of each
   // block's lanes take an item), so more CUs share the step's memory traffic
   // (a power of two: shifts, no 64-bit division in this kernel's registers)
   const u32 per = fast_items_per_block(C);
   const u32 per_log = per == 128u ? 7u : 8u;
   const u64 nchunks = ((u64)n + per - 1) >> per_log;
-  for (u64 ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+  // The grid is sized at capture for the worst case; the round's chunks are
+  // spread over g_eff = vgrid/1000 of their number (at least 256) blocks, the
+  // rest leaving at once (the whole block: no barrier follows for it), so ~30%
+  // of the blocks take a second chunk instead of waiting for a slot as a new
+  // block.  0.7 measured best on C4 (k_fast_both 111.7 → 102.4 µs; 500k / 2M
+  // groups 68.4 → 66.5 / 195 → 184 µs) and no worse on C3 / C2 (DESIGN.md §9,
+  // round 5); C2m's 11.7k chunks stay over the 2,048-block grid.
+  u64 g_eff = (nchunks * L.vgrid + 999) / 1000;
+  if (g_eff < 256) g_eff = nchunks < 256 ? nchunks : 256;
+  if (g_eff > gridDim.x) g_eff = gridDim.x;
+  if (blockIdx.x >= g_eff) return;
+#if RBE_FAST_LDS_CTR
+  __shared__ u32 s_ctr_slots[C_NUM][kBlock];
+  lds_counters_init<KS_FAST_LEAD>(s_ctr_slots);
+  LdsCounters c{{&s_ctr_slots[0][threadIdx.x]}};
+#else
+  StepCounters c;
+#pragma unroll
+  for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
+#endif
+  for (u64 ch = blockIdx.x; ch < nchunks; ch += g_eff) {
     const u64 i = (ch << per_log) + threadIdx.x;
     const bool any = threadIdx.x < per && i < n;
     const bool lead = any && i < nl;
@@ -865,6 +882,9 @@ __global__ __launch_bounds__(kBlock) void k_isolate(Planes P, Params C, u32 roun
 // applied indexes to the applied plane.
 
 static constexpr unsigned kFastGrid = 2048;  // persistent grid of k_fast_list
+// the fast launches' grid cap (kFastGrid; RBE_FAST_GRID overrides it for A/B
+// runs, read once at engine creation; defined in rbe_engine.hip)
+extern unsigned g_fast_grid;
 #ifndef RBE_FULL_GRID
 #define RBE_FULL_GRID 256
 #endif
@@ -916,7 +936,7 @@ int launch_round(const Planes& P, const Params& C, const Lists& L, hipStream_t s
                          ra, L);
     mark(1);
     const unsigned gfn = (unsigned)((C.n_rep + fast_items_per_block(C) - 1) / fast_items_per_block(C));
-    const unsigned gf = gfn < kFastGrid ? gfn : kFastGrid;
+    const unsigned gf = gfn < g_fast_grid ? gfn : g_fast_grid;
     hipLaunchKernelGGL((k_fast_both<N, TRACE>), dim3(gf), dim3(kBlock), 0, stream, P, C,
                        ra, L);
     mark(2);
@@ -938,7 +958,7 @@ int launch_round(const Planes& P, const Params& C, const Lists& L, hipStream_t s
                          ra, L);
     mark(1);
     const unsigned gfn = (unsigned)((C.n_rep + fast_items_per_block(C) - 1) / fast_items_per_block(C));
-    const unsigned gf = gfn < kFastGrid ? gfn : kFastGrid;
+    const unsigned gf = gfn < g_fast_grid ? gfn : g_fast_grid;
     hipLaunchKernelGGL((k_fast_list<N, TRACE, MODE_LEAD>), dim3(gf), dim3(kBlock), 0, stream,
                        P, C, ra, L);
     mark(2);
