@@ -91,12 +91,12 @@ __device__ __forceinline__ u32 wave_sum(u32 v) {
 // blockIdx % kCtrStripes: same-address atomics serialise in one L2 channel, so
 // one-atomic-per-wave into a single line was the round's bottleneck (r01 profile).
 // Every thread of the block must call this (it synchronises the block).
-template <int KS>
+template <int KS, int BS = kBlock>
 __device__ __forceinline__ void flush_counters(const Planes& P, const StepCounters& c) {
 #if defined(RBE_ABLATE_COUNTERS)  // diagnostic A/B builds only: the flush's cost
   if (KS >= 0) return;
 #endif
-  __shared__ u32 s_ctr[kBlock / 64][C_NUM];
+  __shared__ u32 s_ctr[BS / 64][C_NUM];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) {
@@ -108,7 +108,7 @@ __device__ __forceinline__ void flush_counters(const Planes& P, const StepCounte
   if (threadIdx.x < C_NUM) {
     u32 t = 0;
 #pragma unroll
-    for (int j = 0; j < kBlock / 64; j++) t += s_ctr[j][threadIdx.x];
+    for (int j = 0; j < BS / 64; j++) t += s_ctr[j][threadIdx.x];
     if (t)
       atomicAdd((unsigned long long*)&P.counters[((u64)KS * kCtrStripes + blockIdx.x % kCtrStripes) *
                                                      C_NUM + threadIdx.x],
@@ -773,9 +773,16 @@ static constexpr u64 kFullProfCap = 1u << 20;  // wave records of RBE_FULL_PROF 
 // sums (rbe_fast.h); the wave records follow it
 static constexpr u64 kProfHdr = 32;
 
-// Pass 3: the whole handler table over the full list (persistent, grid-stride).
+// Pass 3: the whole handler table over the full list (persistent, grid-stride),
+// in blocks of kFullBlock threads: one wave per block, so C3's ~8,000 general
+// steps spread over ~125 CUs instead of four waves on each of ~32 (C3
+// k_full_list 201 → 193 µs, C3s 121 → 113 µs against 256-thread blocks)
+#ifndef RBE_FULL_BLOCK
+#define RBE_FULL_BLOCK 64
+#endif
+static constexpr int kFullBlock = RBE_FULL_BLOCK;
 template <int N, bool TRACE>
-__global__ __launch_bounds__(kBlock) void k_full_list(Planes P, Params C, RoundArg ra, Lists L) {
+__global__ __launch_bounds__(kFullBlock) void k_full_list(Planes P, Params C, RoundArg ra, Lists L) {
   const Clk ck = clk_of(ra);
   const u32 round = ck.round;
   __shared__ u32 s_pre[kShards + 1];
@@ -790,7 +797,7 @@ __global__ __launch_bounds__(kBlock) void k_full_list(Planes P, Params C, RoundA
   // lanes, the classes of its lanes (role before, role after, any inbound
   // message) and the most inbound / outbound messages of a lane, for
   // scripts/full_prof.py: what the slowest waves of the general step hold.
-  for (u64 b0 = (u64)blockIdx.x * kBlock; b0 < n; b0 += (u64)gridDim.x * kBlock) {
+  for (u64 b0 = (u64)blockIdx.x * kFullBlock; b0 < n; b0 += (u64)gridDim.x * kFullBlock) {
     const u64 i = b0 + threadIdx.x;
     u32 r = 0, cls_b = 0, nin = 0;
     const bool on = i < n;
@@ -841,13 +848,14 @@ __global__ __launch_bounds__(kBlock) void k_full_list(Planes P, Params C, RoundA
     }
   }
 #else
-  for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock) {
+  for (u64 i = (u64)blockIdx.x * kFullBlock + threadIdx.x; i < n;
+       i += (u64)gridDim.x * kFullBlock) {
     const u32 sg = seg_find<kShards>(s_pre, (u32)i);
     step_replica<N, TRACE, kFullMode>(P, C, L.idx[list_pos(L, 2, sg, false, (u32)i - s_pre[sg])],
                                       ck, c);
   }
 #endif
-  flush_counters<KS_FULL>(P, c);
+  flush_counters<KS_FULL, kFullBlock>(P, c);
 }
 
 template <int N>
@@ -903,7 +911,7 @@ int launch_round(const Planes& P, const Params& C, const Lists& L, hipStream_t s
   };
   const unsigned gt = (unsigned)((C.n_rep + kTriChunk - 1) / kTriChunk);
   const unsigned gtg = (unsigned)((C.n_groups + kTriGroups<N> - 1) / kTriGroups<N>);
-  const unsigned gs = g < kFullGrid ? g : kFullGrid;
+  const unsigned gs = (g < kFullGrid ? g : kFullGrid) * (unsigned)(kBlock / kFullBlock);
   if (mode == 2) {
     mark(0);
     mark(1);
@@ -919,7 +927,7 @@ int launch_round(const Planes& P, const Params& C, const Lists& L, hipStream_t s
     mark(1);
     mark(2);
     mark(3);
-    hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kBlock), 0, stream, P, C,
+    hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kFullBlock), 0, stream, P, C,
                        ra, L);
     mark(4);
   } else if (mode == 3) {
@@ -941,7 +949,7 @@ int launch_round(const Planes& P, const Params& C, const Lists& L, hipStream_t s
                        ra, L);
     mark(2);
     mark(3);
-    hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kBlock), 0, stream, P, C,
+    hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kFullBlock), 0, stream, P, C,
                        ra, L);
     mark(4);
   } else {
@@ -965,7 +973,7 @@ int launch_round(const Planes& P, const Params& C, const Lists& L, hipStream_t s
     hipLaunchKernelGGL((k_fast_list<N, TRACE, MODE_FOLL>), dim3(gf), dim3(kBlock), 0, stream,
                        P, C, ra, L);
     mark(3);
-    hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kBlock), 0, stream, P, C,
+    hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kFullBlock), 0, stream, P, C,
                        ra, L);
     mark(4);
   }
