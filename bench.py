@@ -150,6 +150,29 @@ def _oracle_rate(name, groups, settle, rounds, threads):
             (c1["reads_confirmed"] - c0["reads_confirmed"]) / dt, dt)
 
 
+def _soa_rate(name, groups, settle, rounds, threads):
+    """The engine's own SoA step compiled for the host (tests/soa_cpu: the
+    device step built with RBE_HD for the CPU, -O2), T engines stepped on T
+    threads with the groups partitioned cid % T, as the GPU shards them: the
+    same algorithm and layout as the GPU path, on the host's cores."""
+    from concurrent.futures import ThreadPoolExecutor
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from soa_cpu.soa import SoaCpu
+    kw, _, _ = WORKLOADS[name]
+    per = max(1, groups // threads)
+    engs = [SoaCpu(trace=False, **dict(kw, n_groups=per, cid_base=1 + t, cid_stride=threads))
+            for t in range(threads)]
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(lambda e: e.run(settle), engs))
+        c0 = [e.counters() for e in engs]
+        t0 = time.perf_counter()
+        list(ex.map(lambda e: e.run(rounds), engs))
+        dt = time.perf_counter() - t0
+    c1 = [e.counters() for e in engs]
+    d = {k: sum(b[k] - a[k] for a, b in zip(c0, c1)) for k in ("steps", "committed", "reads_confirmed")}
+    return d["steps"] / dt, d["committed"] / dt, d["reads_confirmed"] / dt, dt, per * threads
+
+
 def cpu_baseline(name, groups, settle, rounds, threads, groups_1t, rounds_1t):
     """The oracle (C++ restatement of internal/raft, test infrastructure) on a
     bounded sample of the same workload, timed on this host's cores: T threads
@@ -159,6 +182,17 @@ def cpu_baseline(name, groups, settle, rounds, threads, groups_1t, rounds_1t):
     v1, ce1, rc1, dt1 = _oracle_rate(name, groups_1t, settle, rounds_1t, 1)
     _, aff = host_threads()
     kw, _, _ = WORKLOADS[name]
+    try:
+        srounds = max(rounds, 100)  # the SoA step is ~8x the oracle's speed: more timed rounds
+        sv, sce, src, sdt, sg = _soa_rate(name, groups, settle, srounds, threads)
+        soa = {"value": sv, "unit": "group-steps/s", "cores": threads,
+               "committed_entries_per_s": sce, "read_confirmations_per_s": src, "seconds": sdt,
+               "sample": (f"{sg} groups x {kw['n_replicas']} replicas, {srounds} timed rounds "
+                          f"after a {settle}-round settle; this engine's SoA step compiled for "
+                          f"the host (tests/soa_cpu), {threads} engines on {threads} threads, "
+                          f"groups partitioned cid % threads")}
+    except Exception as ex:  # a second baseline must not hide the first
+        soa = {"error": repr(ex)}
     return {
         "value": v,
         "unit": "group-steps/s",
@@ -178,6 +212,7 @@ def cpu_baseline(name, groups, settle, rounds, threads, groups_1t, rounds_1t):
                        "committed_entries_per_s": ce1, "read_confirmations_per_s": rc1,
                        "sample": f"{groups_1t} groups, {rounds_1t} timed rounds",
                        "seconds": dt1},
+        "soa_host": soa,
     }
 
 

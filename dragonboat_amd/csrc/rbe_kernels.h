@@ -848,6 +848,7 @@ __global__ __launch_bounds__(kFullBlock) void k_full_list(Planes P, Params C, Ro
     }
   }
 #else
+  if ((u64)blockIdx.x * kFullBlock >= n) return;  // the whole block: no item this round
   for (u64 i = (u64)blockIdx.x * kFullBlock + threadIdx.x; i < n;
        i += (u64)gridDim.x * kFullBlock) {
     const u32 sg = seg_find<kShards>(s_pre, (u32)i);
