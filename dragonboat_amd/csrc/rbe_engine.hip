@@ -1766,6 +1766,23 @@ extern "C" int rbe_debug_full_prof(rbe_engine* e, uint64_t* out, uint64_t cap, u
   return RBE_OK;
 }
 
+// Diagnostic: the general steps longer than 20 us of an RBE_FULL_ITEM_PROF
+// build since the last call (8 words each, rbe_step.h step_replica), at most
+// cap of them, and clear (the buffer comes from rbe_debug_full_prof).
+extern "C" int rbe_debug_full_items(rbe_engine* e, uint64_t* out, uint64_t cap, uint64_t* n) {
+  if (!e || !n) return RBE_E_INVALID;
+  if (!e->P.prof) return rbe_debug_full_prof(e, nullptr, 0, n);
+  HIP_OK(hipSetDevice(e->device));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  u64 cnt = 0;
+  HIP_OK(hipMemcpy(&cnt, e->P.prof + 1, sizeof(u64), hipMemcpyDeviceToHost));
+  const u64 m = std::min<u64>(std::min<u64>(cnt, kFullItemCap), cap);
+  if (m && out) HIP_OK(hipMemcpy(out, e->P.prof + kProfHdr, m * 8 * sizeof(u64), hipMemcpyDeviceToHost));
+  *n = cnt;
+  HIP_OK(hipMemset(e->P.prof + 1, 0, sizeof(u64)));
+  return RBE_OK;
+}
+
 // Diagnostic: the per-phase stamp sums of an RBE_PHASE_TIMING build (24
 // words: leader, follower, k_triage x 8 phases; rbe_fast.h) since the last
 // call, and clear.  The first call allocates the buffer (Planes::prof).

@@ -768,10 +768,6 @@ __global__ __launch_bounds__(kBlock, kFastWaves<N>) void k_fast_both(Planes P, P
 #endif
 }
 
-static constexpr u64 kFullProfCap = 1u << 20;  // wave records of RBE_FULL_PROF builds
-// Planes::prof header: [0] the record counter, [8, 32) the RBE_PHASE_TIMING
-// sums (rbe_fast.h); the wave records follow it
-static constexpr u64 kProfHdr = 32;
 
 // Pass 3: the whole handler table over the full list (persistent, grid-stride),
 // in blocks of kFullBlock threads: one wave per block, so C3's ~8,000 general
@@ -781,6 +777,7 @@ static constexpr u64 kProfHdr = 32;
 #define RBE_FULL_BLOCK 64
 #endif
 static constexpr int kFullBlock = RBE_FULL_BLOCK;
+static_assert(kFullBlock <= (int)kLaneCols, "k_full_list's LDS columns (rbe_step.h) hold one thread each");
 template <int N, bool TRACE>
 __global__ __launch_bounds__(kFullBlock) void k_full_list(Planes P, Params C, RoundArg ra, Lists L) {
   const Clk ck = clk_of(ra);

@@ -501,13 +501,19 @@ constexpr u32 kEntBatch = 8;
 // message; in global memory each such read after the step's first store
 // waited for every store before it (vmcnt is in order), a round trip per
 // handler: C3's general step spent ~10 us per inbound message.
+// threads per k_full_list block (rbe_kernels.h): the LDS arrays below hold
+// one column per thread of the block
+#ifndef RBE_FULL_BLOCK
+#define RBE_FULL_BLOCK 64
+#endif
+constexpr u32 kLaneCols = RBE_FULL_BLOCK;
 #if defined(__HIPCC__) || defined(__HIP__)
-__device__ __forceinline__ RemoteMN (&lane_rem())[kMaxN][256] {
-  __shared__ RemoteMN s_rem[kMaxN][256];
+__device__ __forceinline__ RemoteMN (&lane_rem())[kMaxN][kLaneCols] {
+  __shared__ RemoteMN s_rem[kMaxN][kLaneCols];
   return s_rem;
 }
-__device__ __forceinline__ u8 (&lane_rst())[kMaxN][256] {
-  __shared__ u8 s_rst[kMaxN][256];
+__device__ __forceinline__ u8 (&lane_rst())[kMaxN][kLaneCols] {
+  __shared__ u8 s_rst[kMaxN][kLaneCols];
   return s_rst;
 }
 #endif
@@ -575,6 +581,14 @@ struct Lane {
   u32 events;        // EV_* of this step (Upd::events)
   // deferred fan-out actions, executed in this order after each event
   u32 rep_mask;      // slots to sendReplicateMessage to
+#if defined(RBE_FULL_ITEM_PROF) && defined(__HIP_DEVICE_COMPILE__)
+  // diagnostic builds only: where a general step's wall time goes
+  // (s_memrealtime ticks): before the event loop, inbox messages, local
+  // events and ticks, the deferred fan-out after each event; the longest
+  // inbox message; inbox messages handled
+  u64 ip_t0 = 0, ip_pre = 0, ip_in = 0, ip_loc = 0, ip_fan = 0, ip_max = 0;
+  u32 ip_nin = 0, ip_maxtype = 0;
+#endif
   u8 tn_to;          // TimeoutNow target
   bool hb_pending;   // broadcastHeartbeatMessageWithHint(hb_lo, hb_hi)
   bool rq_pending;   // handleReadIndexLeaderConfirmation(rq_m)
@@ -2439,6 +2453,9 @@ struct Lane {
   // returns false without writing anything when the round needs the full
   // handler table; the caller then queues the replica for k_full.
   RBE_HD bool run() {
+#if defined(RBE_FULL_ITEM_PROF) && defined(__HIP_DEVICE_COMPILE__)
+    ip_t0 = wall_clock64();
+#endif
     load();
     if constexpr (!FULL) {
       if (!fast_eligible(role == R_Leader ? wl_input(C, cid, round) : 0u)) return false;
@@ -2623,8 +2640,14 @@ struct Lane {
     hb_pending = rq_pending = false;
     hb_lo = hb_hi = rq_lo = rq_hi = 0;
     rq_from = 0;
+#if defined(RBE_FULL_ITEM_PROF) && defined(__HIP_DEVICE_COMPILE__)
+    ip_pre = wall_clock64() - ip_t0;
+#endif
 #pragma unroll 1
     for (;;) {
+#if defined(RBE_FULL_ITEM_PROF) && defined(__HIP_DEVICE_COMPILE__)
+      const u64 ip_it = wall_clock64();
+#endif
       u32 kind = 0;  // 0 none, 1 inbox message, 2 local message, 3 tick
       Msg m;
       const Ent* ents = nullptr;
@@ -2837,6 +2860,19 @@ struct Lane {
         }
         if (deliver) handle(m, ents);
       }
+#if defined(RBE_FULL_ITEM_PROF) && defined(__HIP_DEVICE_COMPILE__)
+      const u64 ip_ev = wall_clock64();
+      if (kind == 1) {
+        ip_in += ip_ev - ip_it;
+        ip_nin++;
+        if (ip_ev - ip_it > ip_max) {
+          ip_max = ip_ev - ip_it;
+          ip_maxtype = m.type;
+        }
+      } else {
+        ip_loc += ip_ev - ip_it;
+      }
+#endif
       // deferred fan-out, in the reference's emission order
       // remotes, then observers, then witnesses, each ascending (raft.go:390-402 nodes())
 #pragma unroll 1
@@ -2870,6 +2906,9 @@ struct Lane {
         rq_pending = false;
         rq_confirm(rq_lo, rq_hi, rq_from, rq_lo, rq_hi);
       }
+#if defined(RBE_FULL_ITEM_PROF) && defined(__HIP_DEVICE_COMPILE__)
+      ip_fan += wall_clock64() - ip_ev;
+#endif
     }
     // stepNode: newQuiesceState → sendEnterQuiesceMessages (node.go:873-886)
     const bool send_q = q_new;
@@ -3018,7 +3057,30 @@ RBE_HD void Lane<N, TRACE, MODE>::raft_tick() {  // raft.go:551-564
 template <int N, bool TRACE, int MODE = MODE_FULL>
 RBE_HD void step_replica(const Planes& P, const Params& C, u64 r, Clk ck, StepCounters& ctr) {
   Lane<N, TRACE, MODE> lane(P, C, r, ck, ctr);
+#if defined(RBE_FULL_ITEM_PROF) && defined(__HIP_DEVICE_COMPILE__)
+  const u8 role0 = P.hot[r].role;
+#endif
   lane.run();
+#if defined(RBE_FULL_ITEM_PROF) && defined(__HIP_DEVICE_COMPILE__)
+  // a step longer than 20 us leaves a record (rbe_debug_full_items): total,
+  // before the loop, inbox, local, fan-out, longest message, counts, replica
+  const u64 tot = wall_clock64() - lane.ip_t0;
+  if (P.prof && tot > 2000) {
+    const u64 at = atomicAdd((unsigned long long*)&P.prof[1], 1ull);
+    if (at < kFullItemCap) {
+      u64* rec = &P.prof[kProfHdr + at * 8];
+      rec[0] = tot;
+      rec[1] = lane.ip_pre;
+      rec[2] = lane.ip_in;
+      rec[3] = lane.ip_loc;
+      rec[4] = lane.ip_fan;
+      rec[5] = lane.ip_max | ((u64)lane.ip_maxtype << 48);
+      rec[6] = (u64)lane.ip_nin | ((u64)lane.n_msgs << 16) | ((u64)role0 << 32) |
+               ((u64)P.hot[r].role << 40);
+      rec[7] = r;
+    }
+  }
+#endif
 }
 // the steady-state subset: returns false (nothing written) when the round
 // needs the full table

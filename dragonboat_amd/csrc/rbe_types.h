@@ -380,6 +380,13 @@ struct Clk {
 // Planes::gwake bit 0: the group is awake (rbe_step.h, group sleep)
 enum : u8 { GW_AWAKE = 1 };
 
+// Planes::prof (diagnostic builds): header [0] the wave-record counter
+// (RBE_FULL_PROF), [1] the item-record counter (RBE_FULL_ITEM_PROF), [8, 32)
+// the RBE_PHASE_TIMING sums (rbe_fast.h); the records follow the header
+static constexpr u64 kProfHdr = 32;
+static constexpr u64 kFullProfCap = 1u << 20;  // wave records (4 words each)
+static constexpr u64 kFullItemCap = 1u << 19;  // item records (8 words each)
+
 // device pointers of every plane
 struct Planes {
   Hot* hot;

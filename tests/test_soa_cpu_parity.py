@@ -42,7 +42,23 @@ def test_pipeline_takes_fast_paths():
     assert eng.slow_total() < 0.2 * eng.counters()["steps"]
 
 
-@pytest.mark.parametrize("name", ["C4", "C4_DENSE", "MIXED", "C2"])
+@pytest.mark.parametrize("name", list(CASES))
+def test_soa_cpu_untraced_full_table(name):
+    """Untraced, every replica-round on the general step: its Replicate sends
+    are deferred to the lane's send queue (rbe_step.h SendQ: flushed before a
+    ring write, a full queue and the step's end), and every protocol field of
+    every replica must still equal the oracle's, round by round."""
+    kw, rounds = CASES[name]
+    eng = SoaCpu(full_only=True, trace=False, **kw, **ENGINE_EXTRA.get(name, {}))
+    ref = O.Harness(**kw)
+    d = run_lockstep(eng, ref, rounds, every=1, skip=("digest",))
+    assert d is None, f"{name}: first divergence {d}"
+    assert eng.faults()[0] == 0
+    bad = counters_match(eng.counters(), ref.counters())
+    assert not bad, f"{name}: counters differ {bad}"
+
+
+@pytest.mark.parametrize("name", ["C4", "C4_DENSE", "MIXED", "C2", "C3", "C3_HOT"])
 def test_soa_cpu_untraced_state_parity(name):
     """Without trace the engine takes the bench paths (lazy quiesced ticks in
     triage, no digest); every protocol field must still match the oracle."""
