@@ -54,7 +54,7 @@ static constexpr u64 kSmallTriMax = RBE_SMALL_TRI_MAX;  // replicas up to which 
 #ifndef RBE_FAST_HALF_MAX
 #define RBE_FAST_HALF_MAX (1u << 17)  // below ~512 blocks of 256: C2 fast step 48.5 -> 45.6 us; C3 (500k) must not (352 -> 483 us)
 #endif
-// items per k_fast_both block chunk (and its grid: one block per chunk up to kFastGrid)
+// items per k_fast_both block chunk (its blocks: 0.7 x the chunks, up to the grid; L.vgrid)
 RBE_HD u32 fast_items_per_block(const Params& C) {
   return C.n_rep <= RBE_FAST_HALF_MAX ? 128u : 256u;
 }
@@ -894,7 +894,7 @@ extern unsigned g_fast_grid;
 #ifndef RBE_FULL_GRID
 #define RBE_FULL_GRID 256
 #endif
-static constexpr unsigned kFullGrid = RBE_FULL_GRID;  // persistent grid of k_full_list: its ~420 registers allow one wave per SIMD, so 256 blocks of 4 waves fill the chip once
+static constexpr unsigned kFullGrid = RBE_FULL_GRID;  // k_full_list's grid in 256-thread units: its ~490 registers allow one wave per SIMD, so 256 x 4 one-wave blocks fill the chip once
 static inline unsigned grid_for(u64 n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 // One round's launches.  With `ev` (KS_NUM + 1 events) an event is recorded
