@@ -258,12 +258,19 @@ class SoaCpu(NodeInputs):
         maxf = n * (n - 1) * ((self.n_groups + gpb - 1) // gpb)
         fr = (RbeWireFrame * max(1, maxf))()
         nf = C.c_uint32()
-        cap = 1 << 24
-        buf = C.create_string_buffer(cap)
-        got = lib().soa_wire_encode(self.h, deployment_id, bin_ver, groups_per_batch, addrs, buf,
-                                    cap, fr, C.byref(nf), dst_rank)
-        assert got >= 0
-        return buf.raw[:got], [fr[i] for i in range(nf.value)]
+        # one output buffer per engine, grown when a stream does not fit (-1);
+        # only the stream's bytes are copied out
+        while True:
+            buf = getattr(self, "_wire_buf", None)
+            if buf is None:
+                buf = self._wire_buf = C.create_string_buffer(1 << 20)
+            got = lib().soa_wire_encode(self.h, deployment_id, bin_ver, groups_per_batch, addrs,
+                                        buf, len(buf), fr, C.byref(nf), dst_rank)
+            if got >= 0:
+                break
+            assert got == -1, f"soa_wire_encode: {got}"
+            self._wire_buf = C.create_string_buffer(4 * len(buf))
+        return C.string_at(buf, got), [fr[i] for i in range(nf.value)]
 
     def snapshot_state(self):
         o = (C.c_uint64 * (8 * self.n_rep))()
