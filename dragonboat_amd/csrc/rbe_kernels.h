@@ -184,7 +184,8 @@ __global__ __launch_bounds__(kBlock) void k_step(Planes P, Params C, RoundArg ra
 // follower without a Replicate), the back the rest, so the waves of the fast
 // launch are mostly homogeneous and skip the code paths none of their lanes
 // take.  A consumer reads the regions as one sequence of segments (seg_build /
-// seg_find): fronts of every shard, then backs.
+// seg_find) in the slot order it names (k_fast_list: fronts of every shard,
+// then backs; k_fast_both: each role's backs first).
 static constexpr u32 kShards = 8;
 static constexpr u32 kSlots = 5;   // count slots: fronts of lists 0..2, backs of lists 0..1
 static constexpr u32 kCntPad = 64;  // u32 words from one count to the next (256 B)
@@ -700,8 +701,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 // Pass 2, merged (RBE_MODE=both, the default): the round's steady-state
 // leaders and followers in one launch, so the two roles' waves share the SIMDs
 // instead of running back to back; item i < n_lead is a leader, the rest
-// followers.  Block b takes chunks b, b + grid, ... of the item sequence
-// (fronts of every shard, then backs: seg_build / seg_find), one item a lane.
+// followers.  Block b takes chunks b, b + g_eff, ... of the item sequence
+// (per role the backs of every shard, then the fronts: seg_build / seg_find),
+// one item a lane.
 // Measured and not kept: rows staged through LDS for wave-wide
 // stores, messages staged likewise, an XCD-aware chunk mapping, chunks that
 // alternate leaders and followers.
@@ -711,9 +713,12 @@ __global__ __launch_bounds__(kBlock, kFastWaves<N>) void k_fast_both(Planes P, P
   const Clk ck = clk_of(ra);
   const u32 round = ck.round;
   const u32 par = round & 1u;
-  // segments: leader fronts, leader backs, follower fronts, follower backs
+  // segments: leader backs, leader fronts, follower backs, follower fronts
   __shared__ u32 s_pre[4 * kShards + 1];
-  const u32 slots[4] = {0, 3, 1, 4};
+  // each role's back segments first: a leader's proposal rounds and a
+  // follower's Replicate rounds are its longer steps, so they start first
+  // (C4 k_fast_both 99.7 → 97.7 µs, two runs each; C3 / C2 unchanged)
+  const u32 slots[4] = {3, 0, 4, 1};
   seg_build<4>(L, par, slots, s_pre);
   const u32 nl = s_pre[2 * kShards], n = s_pre[4 * kShards];
   // a small engine spreads its items over twice the blocks (half of each
@@ -749,7 +754,7 @@ __global__ __launch_bounds__(kBlock, kFastWaves<N>) void k_fast_both(Planes P, P
     u32 r = 0, aux = 0;
     if (any) {
       const u32 sg = seg_find<4 * kShards>(s_pre, (u32)i);
-      const u64 at = list_pos(L, sg / (2 * kShards), sg % kShards, (sg / kShards) & 1u,
+      const u64 at = list_pos(L, sg / (2 * kShards), sg % kShards, ((sg / kShards) & 1u) == 0u,
                               (u32)i - s_pre[sg]);
       r = L.idx[at];
       if constexpr (kListAux<N>) aux = L.aux[at];
