@@ -2536,7 +2536,19 @@ int rbe_wire_encode(rbe_engine* e, const rbe_wire_config* wc, uint64_t totals[4]
     return RBE_OK;
   });
   if (rc) return rc;
-  hipLaunchKernelGGL(k_wire_batch, dim3((unsigned)nbatch), dim3(256), 0, e->stream, C, A, B);
+  const u32 nseg = (u32)((gpb + kWireBatchSeg - 1) / kWireBatchSeg);  // segments per batch
+  if (nseg <= 1) {
+    hipLaunchKernelGGL(k_wire_batch, dim3((unsigned)nbatch), dim3(256), 0, e->stream, C, A, B);
+  } else {
+    if ((rc = grow(&e->wire_big_buf, &e->wire_big_bytes, nbatch * nseg * 16, false))) return rc;
+    u64* seg_tot = (u64*)e->wire_big_buf;
+    hipLaunchKernelGGL(k_wire_batch_part, dim3((unsigned)nbatch, nseg), dim3(256), 0, e->stream,
+                       C, A, B, seg_tot);
+    hipLaunchKernelGGL(k_wire_batch_fix, dim3((unsigned)nbatch), dim3(256), 0, e->stream, C, A,
+                       B, seg_tot, nseg);
+    hipLaunchKernelGGL(k_wire_batch_add, dim3((unsigned)nbatch, nseg), dim3(256), 0, e->stream,
+                       C, A, B, (const u64*)seg_tot);
+  }
   hipLaunchKernelGGL(k_wire_frames, dim3(1), dim3(256), 0, e->stream, C, A, B, (u32)nbatch);
   HIP_OK(hipGetLastError());
   u64 tot[5];
@@ -2556,8 +2568,40 @@ int rbe_wire_encode(rbe_engine* e, const rbe_wire_config* wc, uint64_t totals[4]
     if (rc) return rc;
     hipLaunchKernelGGL(k_wire_trailers, dim3((unsigned)((nbatch + 255) / 256)), dim3(256), 0,
                        e->stream, C, A, B, (u32)nbatch, e->wire_dev);
+    // frames over 256 KiB of payload (wire_big, as the decode's chunked walk)
+    // take their crc by 64 KiB segments over many blocks: their sizes come
+    // from the frame index (read only when the stream could hold one)
+    const u64 big = e->wire_big;
+    std::vector<WireEncSeg> segs;
+    std::vector<u32> bigf;
+    if (tot[0] > big + kWireHeader) {
+      std::vector<WireFrame> fr(tot[1]);
+      HIP_OK(hipMemcpy(fr.data(), B.frames, tot[1] * sizeof(WireFrame), hipMemcpyDeviceToHost));
+      for (u64 i = 0; i < tot[1]; i++) {
+        const u64 n = fr[i].bytes - kWireHeader;
+        if (n <= big) continue;
+        bigf.push_back((u32)i);
+        for (u64 o = 0; o < n; o += kWireEncSeg) segs.push_back(WireEncSeg{(u32)i, 0u, o});
+      }
+    }
     hipLaunchKernelGGL(k_wire_crc, dim3((unsigned)tot[1]), dim3(256), 0, e->stream, B,
-                       e->wire_dev);
+                       e->wire_dev, big);
+    if (!bigf.empty()) {
+      const u64 nb = bigf.size(), ns = segs.size();
+      const u64 o_acc = al(ns * sizeof(WireEncSeg)), o_bf = o_acc + al(tot[1] * 4);
+      if ((rc = grow(&e->wire_big_buf, &e->wire_big_bytes, o_bf + al(nb * 4), false))) return rc;
+      u8* b = e->wire_big_buf;
+      WireEncSeg* dseg = (WireEncSeg*)b;
+      u32 *acc = (u32*)(b + o_acc), *dbf = (u32*)(b + o_bf);
+      HIP_OK(hipMemcpyAsync(dseg, segs.data(), ns * sizeof(WireEncSeg), hipMemcpyHostToDevice,
+                            e->stream));
+      HIP_OK(hipMemcpyAsync(dbf, bigf.data(), nb * 4, hipMemcpyHostToDevice, e->stream));
+      HIP_OK(hipMemsetAsync(acc, 0, tot[1] * 4, e->stream));
+      hipLaunchKernelGGL(k_wire_crc_seg, dim3((unsigned)ns), dim3(256), 0, e->stream, B,
+                         (const WireEncSeg*)dseg, acc, (const u8*)e->wire_dev);
+      hipLaunchKernelGGL(k_wire_crc_fin, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0,
+                         e->stream, B, (const u32*)dbf, (u32)nb, (const u32*)acc, e->wire_dev);
+    }
     HIP_OK(hipGetLastError());
   }
   HIP_OK(hipStreamSynchronize(e->stream));

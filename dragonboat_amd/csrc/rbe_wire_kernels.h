@@ -134,6 +134,85 @@ __global__ __launch_bounds__(256) void k_wire_batch(Params C, WireArgs A, WireBu
   }
 }
 
+// Batches of more than kWireBatchSeg groups are scanned by segments, one
+// block each (k_wire_batch_part: offsets within the segment and its totals),
+// then per batch the segments' totals (k_wire_batch_fix) and the segment bases
+// added to the offsets (k_wire_batch_add), instead of one block walking the
+// whole batch
+static constexpr u32 kWireBatchSeg = 4096;
+__global__ __launch_bounds__(256) void k_wire_batch_part(Params C, WireArgs A, WireBufs B,
+                                                         u64* seg_tot) {
+  __shared__ u64 s_tmp[4];
+  const u32 bt = blockIdx.x, sgi = blockIdx.y;
+  const u32 p = bt / A.nchunks, ch = bt % A.nchunks;
+  const u64 b0 = (u64)ch * A.gpb;
+  const u64 b1 = b0 + A.gpb < C.n_groups ? b0 + A.gpb : C.n_groups;
+  const u64 g0 = b0 + (u64)sgi * kWireBatchSeg;
+  const u64 g1 = g0 + kWireBatchSeg < b1 ? g0 + kWireBatchSeg : b1;
+  const u64 base = (u64)p * C.n_groups;
+  u64 carry = 0, mi = 0;
+  for (u64 g = g0; g < g1; g += 256) {  // uniform over the block (empty past b1)
+    const u64 gi = g + threadIdx.x;
+    u64 v = 0;
+    u32 mm = 0;
+    if (gi < g1) {
+      v = B.cell_bytes[base + gi];
+      mm = B.cell_msgs[base + gi];
+    }
+    u64 tot = 0;
+    const u64 pre = block_scan_u64(v, &tot, s_tmp);
+    if (gi < g1) B.cell_off[base + gi] = (u32)(carry + pre);
+    carry += tot;
+    u64 t2 = 0;
+    block_scan_u64((u64)(mm & 0xFFFFu) | ((u64)(mm >> 16) << 32), &t2, s_tmp);
+    mi += t2;
+  }
+  if (threadIdx.x == 0) {
+    seg_tot[2 * ((u64)bt * gridDim.y + sgi)] = carry;
+    seg_tot[2 * ((u64)bt * gridDim.y + sgi) + 1] = mi;  // messages | InstallSnapshots << 32
+  }
+}
+__global__ __launch_bounds__(256) void k_wire_batch_fix(Params C, WireArgs A, WireBufs B,
+                                                        u64* seg_tot, u32 nseg) {
+  __shared__ u64 s_tmp[4];
+  const u32 bt = blockIdx.x;
+  u64 carry = 0, mi = 0;
+  for (u32 s0 = 0; s0 < nseg; s0 += 256) {
+    const u32 sgi = s0 + threadIdx.x;
+    u64* t = &seg_tot[2 * ((u64)bt * nseg + sgi)];
+    const u64 v = sgi < nseg ? t[0] : 0, m = sgi < nseg ? t[1] : 0;
+    u64 tot = 0, t2 = 0;
+    const u64 pre = block_scan_u64(v, &tot, s_tmp);
+    block_scan_u64(m, &t2, s_tmp);
+    if (sgi < nseg) t[0] = carry + pre;  // the segment's base within the batch
+    carry += tot;
+    mi += t2;
+  }
+  if (threadIdx.x == 0) {
+    const u64 msgs = mi & 0xFFFFFFFFull;
+    u32 k, d;
+    wire_pair(C.n, bt / A.nchunks, &k, &d);
+    B.batch_pay[bt] = msgs ? carry + wire_trailer(A.deployment_id, A.addr[k], A.alen[k], A.bin_ver,
+                                                  nullptr)
+                           : 0;
+    B.batch_msgs[bt] = (u32)msgs;
+    B.batch_is[bt] = (u32)(mi >> 32);
+  }
+}
+__global__ __launch_bounds__(256) void k_wire_batch_add(Params C, WireArgs A, WireBufs B,
+                                                        const u64* seg_tot) {
+  const u32 bt = blockIdx.x, sgi = blockIdx.y;
+  if (sgi == 0) return;
+  const u64 add = seg_tot[2 * ((u64)bt * gridDim.y + sgi)];
+  const u32 p = bt / A.nchunks, ch = bt % A.nchunks;
+  const u64 b0 = (u64)ch * A.gpb;
+  const u64 b1 = b0 + A.gpb < C.n_groups ? b0 + A.gpb : C.n_groups;
+  const u64 g0 = b0 + (u64)sgi * kWireBatchSeg;
+  const u64 g1 = g0 + kWireBatchSeg < b1 ? g0 + kWireBatchSeg : b1;
+  const u64 base = (u64)p * C.n_groups;
+  for (u64 gi = g0 + threadIdx.x; gi < g1; gi += 256) B.cell_off[base + gi] += (u32)add;
+}
+
 __global__ __launch_bounds__(256) void k_wire_frames(Params C, WireArgs A, WireBufs B,
                                                      u32 nbatch) {
   __shared__ u64 s_tmp[4];
@@ -280,16 +359,58 @@ __device__ u32 block_crc32(const u8* p, u64 n, const u32* table, const u32* x2n,
   return r;
 }
 
-__global__ __launch_bounds__(256) void k_wire_crc(WireBufs B, u8* out) {
+// one block per frame whose payload is at most `big` bytes: its crc32 and header
+__global__ __launch_bounds__(256) void k_wire_crc(WireBufs B, u8* out, u64 big) {
+  __shared__ u32 s_table[1024], s_x2n[32], s_crc[256];
+  const WireFrame f = B.frames[blockIdx.x];
+  const u64 n = f.bytes - kWireHeader;
+  if (n > big) return;  // (the whole block) k_wire_crc_seg / k_wire_crc_fin take it
+  crc_tables_lds(s_table);
+  if (threadIdx.x < 32) s_x2n[threadIdx.x] = kCrcX2n.v[threadIdx.x];
+  __syncthreads();
+  u8* fp = out + f.offset;
+  const u32 c = block_crc32(fp + kWireHeader, n, s_table, s_x2n, s_crc);
+  if (threadIdx.x == 0) wire_header_put(fp, n, c, s_table);
+}
+// A bigger frame's payload crc by 64 KiB segments, one block each, shifted to
+// the payload's end and XORed into acc[frame] (crc32_combine is linear, as in
+// block_crc32); then one lane per big frame writes its header.
+struct WireEncSeg {
+  u32 frame, pad;
+  u64 start;  // payload offset of the segment
+};
+static constexpr u64 kWireEncSeg = 65536;
+__global__ __launch_bounds__(256) void k_wire_crc_seg(WireBufs B, const WireEncSeg* seg, u32* acc,
+                                                      const u8* out) {
   __shared__ u32 s_table[1024], s_x2n[32], s_crc[256];
   crc_tables_lds(s_table);
   if (threadIdx.x < 32) s_x2n[threadIdx.x] = kCrcX2n.v[threadIdx.x];
   __syncthreads();
-  const WireFrame f = B.frames[blockIdx.x];
-  u8* fp = out + f.offset;
+  const WireEncSeg sg = seg[blockIdx.x];
+  const WireFrame f = B.frames[sg.frame];
   const u64 n = f.bytes - kWireHeader;
-  const u32 c = block_crc32(fp + kWireHeader, n, s_table, s_x2n, s_crc);
-  if (threadIdx.x == 0) wire_header_put(fp, n, c, s_table);
+  const u64 lo = sg.start, hi = n - lo < kWireEncSeg ? n : lo + kWireEncSeg;
+  u32 c = block_crc32(out + f.offset + kWireHeader + lo, hi - lo, s_table, s_x2n, s_crc);
+  if (threadIdx.x == 0) {
+    u64 rest = n - hi;
+    if (c && rest) {
+      u32 sh = 1u << 31;  // x^(8 rest) mod P
+      for (u32 k = 3; rest; rest >>= 1, k++)
+        if (rest & 1u) sh = crc_multmodp(s_x2n[k & 31], sh);
+      c = crc_multmodp(sh, c);
+    }
+    if (c) atomicXor(&acc[sg.frame], c);
+  }
+}
+__global__ __launch_bounds__(256) void k_wire_crc_fin(WireBufs B, const u32* bigf, u32 nbig,
+                                                      const u32* acc, u8* out) {
+  __shared__ u32 s_table[1024];
+  crc_tables_lds(s_table);
+  __syncthreads();
+  const u32 i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= nbig) return;
+  const WireFrame f = B.frames[bigf[i]];
+  wire_header_put(out + f.offset, f.bytes - kWireHeader, acc[bigf[i]], s_table);
 }
 
 // ---------------------------------------------------------------- decode

@@ -37,11 +37,13 @@ def _records(dec):
     return ([bytes(m) for m in msgs], [bytes(e) for e in ents], bytes(cmd))
 
 
-@pytest.mark.parametrize("big", [4096, 1 << 18])
-def test_gpu_wire_chunked_walk_equals_oracle(gpu_available, big):
-    """One frame per (sender, receiver) slot pair over 3,000 groups (gpb 0):
-    frames of ~100-400 KB, every one walked by chunks at threshold 4 KiB."""
-    kw = dict(C2, n_groups=3000)
+@pytest.mark.parametrize("big,groups", [(4096, 3000), (1 << 18, 3000), (1 << 18, 12000)])
+def test_gpu_wire_chunked_walk_equals_oracle(gpu_available, big, groups):
+    """One frame per (sender, receiver) slot pair (gpb 0): 3,000 groups give
+    frames of ~100-400 KB, every one walked by chunks at threshold 4 KiB;
+    12,000 groups give frames over 256 KiB whose batches are scanned by
+    segments and whose crc32s are taken by 64 KiB segments on encode."""
+    kw = dict(C2, n_groups=groups)
     eng = _engine(big=big, **kw)
     n, G = 3, kw["n_groups"]
     checked = 0
