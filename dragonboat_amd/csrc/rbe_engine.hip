@@ -138,11 +138,11 @@ __device__ __forceinline__ void out_counts(const Planes& P, const Params& C, u64
   u32 m = 0;
   for (u32 d = 0; d < C.n; d++) {
     const u32 pc = row_word(row, d, k, round);
-    m += (pc & 0x7Fu) + ((pc >> 7) & 0x7Fu);
+    m += list_len(P, C, par, r * C.n + d, pc);
   }
   *nm = m;
   const Upd& u = P.upd[r];
-  *nr = u.round == round - 1u ? (u.n_rtr < C.rtr_cap ? u.n_rtr : C.rtr_cap) : 0u;
+  *nr = u.round == round - 1u ? u.n_rtr : 0u;
 }
 __global__ __launch_bounds__(kBlock) void k_out_count(Planes P, Params C, u64 first, u64 count,
                                                       u32 round, u32* bsum) {
@@ -254,17 +254,17 @@ __global__ __launch_bounds__(kBlock) void k_out_write(Planes P, Params C, u64 fi
   const CntRow row = P.cnt[par][r];
   u64 at = bm;
   for (u32 d = 0; d < N; d++) {
-    const u32 pc = row_word(row, d, k, round), na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
-    const Msg* lst = &P.msgs[par][((g * N + k) * N + d) * (u64)C.maxm];
-    for (u32 j = 0; j < na + nb; j++, at++) {
-      const Msg m = j < na ? lst[j] : lst[C.maxm - 1u - (j - na)];
+    const ListView lv = list_view(P, C, par, r * N + d, row_word(row, d, k, round));
+    for (u32 j = 0; j < lv.n(); j++, at++) {
+      const Msg m = lv.at(j);
       rbe_message o;
       msg_out(m, cid_of(C, g), P.node_ids, N, g, o);
       om[at] = o;
     }
   }
+  const RTR* rl = rtr_list(P, C, r, nr, par);
   for (u32 j = 0; j < nr; j++) {
-    const RTR x = P.rtr[r * C.rtr_cap + j];
+    const RTR x = rl[j];
     rbe_ready_to_read o;
     o.index = x.index;
     o.ctx_low = x.low;
@@ -335,7 +335,7 @@ __device__ __forceinline__ void step_out_counts(const Planes& P, const Params& C
   u32 m = 0;
   for (u32 d = 0; d < N; d++) {
     const u32 pc = row_word(row, d, k, round);
-    if (out_msg_wanted(C, g, d, remote)) m += (pc & 0x7Fu) + ((pc >> 7) & 0x7Fu);
+    if (out_msg_wanted(C, g, d, remote)) m += list_len(P, C, par, r * N + d, pc);
   }
   *nm = m;
   // RBE_COLLECT_SKIP_LOCAL: an Update whose only content is messages the
@@ -345,7 +345,7 @@ __device__ __forceinline__ void step_out_counts(const Planes& P, const Params& C
     return;
   }
   const Upd& x = P.upd[r];
-  *nr = x.round == round - 1u ? (x.n_rtr < C.rtr_cap ? x.n_rtr : C.rtr_cap) : 0u;
+  *nr = x.round == round - 1u ? x.n_rtr : 0u;
 }
 __global__ __launch_bounds__(kBlock) void k_cs_count(Planes P, Params C, u64 first, u64 count,
                                                      u32 round, u32 cflags, u32* bsum) {
@@ -394,17 +394,17 @@ __global__ __launch_bounds__(kBlock) void k_cs_write(Planes P, Params C, u64 fir
   u64 w = bm;
   for (u32 d = 0; d < N; d++) {
     if (!out_msg_wanted(C, g, d, remote)) continue;
-    const u32 pc = row_word(row, d, k, round), na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
-    const Msg* lst = &P.msgs[par][((g * N + k) * N + d) * (u64)C.maxm];
-    for (u32 j = 0; j < na + nb; j++, w++) {
-      const Msg m = j < na ? lst[j] : lst[C.maxm - 1u - (j - na)];
+    const ListView lv = list_view(P, C, par, r * N + d, row_word(row, d, k, round));
+    for (u32 j = 0; j < lv.n(); j++, w++) {
+      const Msg m = lv.at(j);
       rbe_message o;
       msg_out(m, cid_of(C, g), P.node_ids, N, g, o);
       om[w] = o;
     }
   }
+  const RTR* rl = rtr_list(P, C, r, nr, par);
   for (u32 j = 0; j < nr; j++) {
-    const RTR x = P.rtr[r * C.rtr_cap + j];
+    const RTR x = rl[j];
     rbe_ready_to_read o;
     o.index = x.index;
     o.ctx_low = x.low;
@@ -487,6 +487,41 @@ __global__ __launch_bounds__(kBlock) void k_heap_low(Planes P, Params C, u32 rou
     lo = y < lo ? y : lo;
   }
   if ((threadIdx.x & 63u) == 0 && lo != ~0ull) atomicMin((unsigned long long*)out, lo);
+}
+
+// entries [lo, hi] of replica r's log (ring window and cold log, rbe_spill.h
+// log_ent_at) for the host getters; *miss counts the ones the replica does
+// not hold (compacted, or below what a launch handed over)
+__global__ __launch_bounds__(kBlock) void k_log_gather(Planes P, Params C, u64 r, u64 lo, u64 hi,
+                                                       Ent* out, u32* miss) {
+  const u64 last = P.core[r].last_index;
+  for (u64 i = lo + threadIdx.x; i <= hi; i += kBlock) {
+    Ent e;
+    if (!log_ent_at(P, C, r, last, i, &e)) {
+      atomicAdd(miss, 1u);
+      e.term = e.lo = e.hi = 0;
+      e.type = e.len = 0;
+    }
+    out[i - lo] = e;
+  }
+}
+
+// rbe_import_groups: replicas [r0, r0 + n) give back their cold log and
+// readIndex pages before the planes are overwritten, then rebuild them from
+// the snapshot's log section (rbe_snap.h; rec_off = each record's offset)
+__global__ __launch_bounds__(kBlock) void k_spill_release(Planes P, Params C, u64 r0, u64 n,
+                                                          u32 par) {
+  const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) spill_replica_release(P, C, r0 + i, par);
+}
+__global__ __launch_bounds__(kBlock) void k_snap_log_rebuild(Planes P, Params C, u64 r0, u64 n,
+                                                             const u8* sec, const u64* rec_off,
+                                                             u32 par, u32* fault) {
+  const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  u32 f = 0;
+  snap_log_rebuild(P, C, r0 + i, sec + rec_off[i], par, &f);
+  if (f) atomicOr(fault, f);
 }
 
 __global__ void k_advance(u32* clk, u32 k) {
@@ -638,6 +673,8 @@ struct rbe_engine {
   // rbe_collect_outputs: device scratch and the pinned host copy it returns
   u8* out_dev = nullptr;
   u64 out_dev_bytes = 0;
+  u8* gat_dev = nullptr;  // rbe_get_entries' gather buffer (k_log_gather)
+  u64 gat_dev_bytes = 0;
   u8* out_host = nullptr;
   u64 out_host_bytes = 0;
   // replica mode with the isolation schedule: every rank's leader bits, ORed
@@ -702,7 +739,12 @@ static int read_heap(rbe_engine* e, u64 pos, u64 off, u64 len, u8* dst) {
 }
 
 
-static constexpr int kPlaneAllocs = 25;
+static int read_window(rbe_engine* e, u64 replica, u64 lo, u64 hi, std::vector<u64>& t,
+                       std::vector<Body>& b);
+static int grow(u8** p, u64* have, u64 need, bool pinned);
+static int host_list(rbe_engine* e, u32 par, u64 li, u32 w, const Msg* pl, std::vector<Msg>& out);
+
+static constexpr int kPlaneAllocs = 30;
 static u64 bytes_of(const Params& C, u64* parts) {
   const u64 N = C.n, G = C.n_groups, R = C.n_rep;
   u64 p[kPlaneAllocs] = {
@@ -731,6 +773,13 @@ static u64 bytes_of(const Params& C, u64* parts) {
       (C.ext_commit || C.rl_max) ? R * sizeof(u64) : 0,
       C.rl_max ? R * sizeof(RlSt) : 0,
       C.membership ? R * sizeof(u16) : 0,
+      // spill tiers (rbe_spill.h): pool records, pool page links, cold-log refs,
+      // the round spill heap (both parities), the allocation words
+      (u64)C.pool_pages * kPageEnts * sizeof(Ent),
+      (u64)C.pool_pages * sizeof(PoolMeta),
+      R * sizeof(ColdRef),
+      2 * C.spill_units * 16,
+      sizeof(SpillCtl),
   };
   u64 t = 0;
   for (int i = 0; i < kPlaneAllocs; i++) {
@@ -758,7 +807,7 @@ static int make_params(const rbe_config* cfg, Params* out) {
   if (C.ring & (C.ring - 1)) return RBE_E_INVALID;
   if (C.ring < 8) return RBE_E_INVALID;
   C.rq_cap = cfg->rq_cap ? cfg->rq_cap : 8;
-  if (C.rq_cap > 255) return RBE_E_INVALID;
+  if (C.rq_cap >= kRqExt) return RBE_E_INVALID;  // (kRqExt marks a queue in pool pages)
   C.maxm = cfg->maxm ? cfg->maxm : 12;
   if (C.maxm > 127) return RBE_E_INVALID;
   C.ecap = cfg->ecap ? cfg->ecap : 32;
@@ -828,6 +877,7 @@ static int make_params(const rbe_config* cfg, Params* out) {
   // the payload heap holds host-pushed Cmds longer than 16 bytes
   C.heap_bytes = (cfg->heap_bytes + 255) & ~255ull;
   if (C.heap_bytes && !C.ext_inputs) return RBE_E_INVALID;
+  if (spill_sizes(cfg, &C)) return RBE_E_INVALID;
   *out = C;
   return RBE_OK;
 }
@@ -890,15 +940,104 @@ int rbe_snapshot_bytes(rbe_engine* e, uint64_t count, uint64_t* bytes) {
   return RBE_OK;
 }
 
+}  // extern "C"
+
+// The source side of a snapshot's log section (rbe_snap.h snap_log_write):
+// the range's cold log refs and Core rows copied once, pages and their meta
+// read as the chains are walked
+struct SnapLogDev {
+  rbe_engine* e;
+  u64 r0;
+  std::vector<ColdRef> cr;
+  std::vector<Core> co;
+  int rc = RBE_OK;
+  SnapLogDev(rbe_engine* en, u64 first_rep, u64 n) : e(en), r0(first_rep), cr(n), co(n) {
+    if (hipMemcpy(cr.data(), e->P.cold + r0, n * sizeof(ColdRef), hipMemcpyDeviceToHost) ||
+        hipMemcpy(co.data(), e->P.core + r0, n * sizeof(Core), hipMemcpyDeviceToHost))
+      rc = RBE_E_HIP;
+  }
+  ColdRef cold(u64 r) { return cr[r - r0]; }
+  Core core(u64 r) { return co[r - r0]; }
+  RqExt rq(u64 r) {
+    ReadReq d = {};
+    if (hipMemcpy(&d, e->P.rq + r * e->C.rq_cap, sizeof(d), hipMemcpyDeviceToHost)) rc = RBE_E_HIP;
+    RqExt x;
+    x.head = (u32)d.low;
+    x.tail = (u32)(d.low >> 32);
+    x.off = (u32)d.high;
+    x.n = (u32)(d.high >> 32);
+    return x;
+  }
+  PoolMeta meta(u32 p) {
+    PoolMeta m = {};
+    if (hipMemcpy(&m, e->P.pmeta + p, sizeof(m), hipMemcpyDeviceToHost)) rc = RBE_E_HIP;
+    return m;
+  }
+  void page(u32 p, Ent* out) {
+    if (hipMemcpy(out, e->P.pool + (u64)p * kPageEnts, kPageEnts * sizeof(Ent),
+                  hipMemcpyDeviceToHost))
+      rc = RBE_E_HIP;
+  }
+};
+
+// Whether the range's last step left round spill heap state a snapshot cannot
+// carry (rbe_snap.h snap_round_spilled)
+static int snap_range_spilled(rbe_engine* e, u64 first, u64 count, bool* out) {
+  const u32 N = e->C.n, par = (e->round - 1) & 1u;
+  const u64 r0 = first * N, n = count * N;
+  *out = false;
+  if (e->round == 0) return RBE_OK;
+  std::vector<CntRow> rows(n);
+  std::vector<Upd> upd(n);
+  std::vector<Msg> lst(n * N * e->C.maxm);
+  if (d2h(e, rows.data(), e->P.cnt[par] + r0, n) || d2h(e, upd.data(), e->P.upd + r0, n) ||
+      d2h(e, lst.data(), e->P.msgs[par] + r0 * N * e->C.maxm, lst.size()))
+    return RBE_E_HIP;
+  HIP_OK(hipStreamSynchronize(e->stream));
+  for (u64 i = 0; i < n && !*out; i++) {
+    u32 w[8];
+    for (u32 d = 0; d < N; d++) w[d] = row_word(rows[i], d, (u32)((r0 + i) % N), e->round);
+    *out = snap_round_spilled(e->C, w, &lst[i * N * e->C.maxm], upd[i]);
+  }
+  return RBE_OK;
+}
+
+extern "C" {
+
+int rbe_export_bytes(rbe_engine* e, uint64_t first, uint64_t count, uint64_t* bytes) {
+  if (!e || !bytes || count == 0 || first >= e->C.n_groups || count > e->C.n_groups - first)
+    return RBE_E_INVALID;
+  HIP_OK(hipSetDevice(e->device));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  SnapLogDev src(e, first * e->C.n, count * e->C.n);
+  const u64 lb = snap_log_write(e->C, first * e->C.n, count * e->C.n, src, nullptr);
+  if (src.rc) return src.rc;
+  *bytes = snap_log_at(snap_body_bytes(e->P, e->C, count)) + lb;
+  return RBE_OK;
+}
+
 int rbe_export_groups(rbe_engine* e, uint64_t first, uint64_t count, void* buf, uint64_t cap) {
   if (!e || !buf || count == 0 || first >= e->C.n_groups || count > e->C.n_groups - first)
     return RBE_E_INVALID;
   const u64 body = snap_body_bytes(e->P, e->C, count);
-  if (cap < sizeof(SnapHeader) + body) return RBE_E_NOMEM;
   HIP_OK(hipSetDevice(e->device));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  bool spilled = false;
+  int rc = snap_range_spilled(e, first, count, &spilled);
+  if (rc) return rc;
+  if (spilled) return RBE_E_STATE;
+  const u64 r0 = first * e->C.n, nr = count * e->C.n;
+  SnapLogDev src(e, r0, nr);
+  const u64 lb = snap_log_write(e->C, r0, nr, src, nullptr);
+  if (src.rc) return src.rc;
+  if (cap < snap_log_at(body) + lb) return RBE_E_NOMEM;
   SnapHeader h;
   snap_fill_header(e->C, RBE_ABI_VERSION, e->round, e->tclk, first, count, body, &h);
+  h.log_bytes = lb;
   memcpy(buf, &h, sizeof(h));
+  memset((u8*)buf + sizeof(h) + body, 0, snap_log_at(body) - sizeof(h) - body);
+  snap_log_write(e->C, r0, nr, src, (u8*)buf + snap_log_at(body));
+  if (src.rc) return src.rc;
   SnapPlane pl[kSnapPlanes];
   snap_planes(e->P, e->C, pl);
   u8* dst = (u8*)buf + sizeof(SnapHeader);
@@ -923,7 +1062,15 @@ int rbe_import_groups(rbe_engine* e, const void* buf, uint64_t bytes, uint32_t f
   const bool resume = (flags & RBE_IMPORT_RESUME) != 0;
   if (resume && (h.first != 0 || h.count != e->C.n_groups)) return RBE_E_INVALID;
   if (!resume && h.round != e->round) return RBE_E_STATE;
+  const u64 r0 = h.first * e->C.n, nr = h.count * e->C.n;
+  std::vector<u64> rec_off(nr);
+  if (snap_log_index(e->C, (const u8*)buf, nr, rec_off.data())) return RBE_E_INVALID;
   HIP_OK(hipSetDevice(e->device));
+  // the range's pages go back to the pool before its planes are replaced
+  const u32 spar = e->round & 1u;
+  hipLaunchKernelGGL(k_spill_release, dim3(grid_for(nr)), dim3(kBlock), 0, e->stream, e->P, e->C,
+                     r0, nr, spar);
+  HIP_OK(hipGetLastError());
   SnapPlane pl[kSnapPlanes];
   snap_planes(e->P, e->C, pl);
   const u8* src = (const u8*)buf + sizeof(SnapHeader);
@@ -932,6 +1079,26 @@ int rbe_import_groups(rbe_engine* e, const void* buf, uint64_t bytes, uint32_t f
     HIP_OK(hipMemcpy2DAsync(pl[i].base + h.first * pl[i].group_bytes, pl[i].pitch, src, w, w,
                             pl[i].rows, hipMemcpyHostToDevice, e->stream));
     src += w * pl[i].rows;
+  }
+  {  // the cold logs and pool-page readIndex queues of the log section
+    // device staging: fault word | record offsets | the section (16-B aligned)
+    const u64 lb = h.log_bytes, ob = (nr * sizeof(u64) + 15) & ~15ull;
+    const int rc = grow(&e->gat_dev, &e->gat_dev_bytes, 16 + ob + lb, false);
+    if (rc) return rc;
+    u32* fault = (u32*)e->gat_dev;
+    u64* d_off = (u64*)(e->gat_dev + 16);
+    u8* d_sec = e->gat_dev + 16 + ob;
+    HIP_OK(hipMemsetAsync(fault, 0, sizeof(u32), e->stream));
+    HIP_OK(hipMemcpyAsync(d_off, rec_off.data(), ob, hipMemcpyHostToDevice, e->stream));
+    HIP_OK(hipMemcpyAsync(d_sec, (const u8*)buf + snap_log_at(h.body_bytes), lb,
+                          hipMemcpyHostToDevice, e->stream));
+    hipLaunchKernelGGL(k_snap_log_rebuild, dim3(grid_for(nr)), dim3(kBlock), 0, e->stream, e->P,
+                       e->C, r0, nr, (const u8*)d_sec, (const u64*)d_off, spar ^ 1u, fault);
+    HIP_OK(hipGetLastError());
+    u32 f = 0;
+    HIP_OK(hipMemcpyAsync(&f, fault, sizeof(u32), hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    if (f) return RBE_E_NOMEM;
   }
   {  // the host mirror of the applied plane follows the imported rows
     std::vector<u64> app(h.count * e->C.n);
@@ -985,6 +1152,7 @@ int rbe_destroy(rbe_engine* e) {
   }
   if (e->in_dev) HIP_IGNORE(hipFree(e->in_dev));
   if (e->out_dev) HIP_IGNORE(hipFree(e->out_dev));
+  if (e->gat_dev) HIP_IGNORE(hipFree(e->gat_dev));
   if (e->out_host) HIP_IGNORE(hipHostFree(e->out_host));
   if (e->upd_dev) HIP_IGNORE(hipFree(e->upd_dev));
   if (e->ing_dev) HIP_IGNORE(hipFree(e->ing_dev));
@@ -1075,6 +1243,14 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   P.imark = (C.ext_commit || C.rl_max) ? (u64*)ptrs[22] : nullptr;
   P.rl = C.rl_max ? (RlSt*)ptrs[23] : nullptr;
   P.roles = C.membership ? (u16*)ptrs[24] : nullptr;
+  P.pool = (Ent*)ptrs[25];
+  P.pmeta = (PoolMeta*)ptrs[26];
+  P.cold = (ColdRef*)ptrs[27];
+  P.spill[0] = (u8*)ptrs[28];
+  P.spill[1] = P.spill[0] + C.spill_units * 16;
+  P.sctl = (SpillCtl*)ptrs[29];
+  // page 0 is the null page: the bump counter starts at 1
+  HIP_IGNORE(hipMemsetD32Async((hipDeviceptr_t)&P.sctl->bump, 1, 1, e->stream));
   P.node_ids = nullptr;  // slot s is node s + 1 until rbe_set_node_ids
   P.ids_n = C.n;
   HIP_IGNORE(hipMemsetAsync(P.gwake, GW_AWAKE, C.n_groups, e->stream));  // every group starts awake
@@ -1935,11 +2111,32 @@ int rbe_get_outbox(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t c
   HIP_OK(hipMemcpyAsync(arena.data(), e->P.arena[par] + replica * e->C.ecap,
                         arena.size() * sizeof(Ent), hipMemcpyDeviceToHost, e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
+  // the lists in reading order (spilled ones from the spill heap), and the
+  // entries of messages that carry theirs in the spill heap (rbe_spill.h)
+  std::vector<std::vector<Msg>> lists(N);
+  std::unordered_map<u64, std::vector<Ent>> xents;  // granule → entries
+  for (u32 d = 0; d < N; d++) {
+    int rc = host_list(e, par, replica * N + d, row_word(row, d, k, e->round), &lst[d * e->C.maxm],
+                       lists[d]);
+    if (rc) return rc;
+    for (const Msg& m : lists[d]) {
+      if (!(m.pad0 & kMsgXEnt) || xents.count(m.ent_off)) continue;
+      std::vector<Ent>& v = xents[m.ent_off];
+      v.resize(msg_nent(m));
+      HIP_OK(hipMemcpyAsync(v.data(), e->P.spill[par] + (u64)m.ent_off * 16, v.size() * sizeof(Ent),
+                            hipMemcpyDeviceToHost, e->stream));
+    }
+  }
+  HIP_OK(hipStreamSynchronize(e->stream));
+  auto list = [&](u32 d) -> const std::vector<Msg>& { return lists[d]; };
+  auto ent = [&](const Msg& m, u32 j) -> Ent {
+    return (m.pad0 & kMsgXEnt) ? xents[m.ent_off][j] : arena[m.ent_off + j];
+  };
   auto rd = [e](u64 pos, u64 off, u64 len, u8* dst) { return read_heap(e, pos, off, len, dst); };
   const int rc = dispatch_n(N, [&](auto NN) {
     constexpr int NC = decltype(NN)::value;
-    return outbox_messages<NC>(e->C, g, k, row, e->round, lst.data(), arena.data(), out, cap, ents,
-                               ent_cap, n_out, n_ents, cmd, cmd_cap, cmd_bytes, e->hin.id_table(), rd);
+    return outbox_messages<NC>(e->C, g, k, row, e->round, list, ent, out, cap, ents, ent_cap, n_out,
+                               n_ents, cmd, cmd_cap, cmd_bytes, e->hin.id_table(), rd);
   });
   HIP_OK(hipStreamSynchronize(e->stream));  // heap reads
   return rc;
@@ -2038,6 +2235,14 @@ int rbe_get_views(rbe_engine* e, uint64_t first, uint64_t count, rbe_replica_vie
       (e->C.membership && d2h(e, roles.data(), e->P.roles + first, count)))
     return RBE_E_HIP;
   HIP_OK(hipStreamSynchronize(e->stream));
+  // the length of a readIndex queue in pool pages (its descriptor in ring slot 0)
+  std::vector<u32> rqx_len(count, 0);
+  for (u64 i = 0; i < count; i++) {
+    if (core[i].rq_count != kRqExt) continue;
+    ReadReq d;
+    HIP_OK(hipMemcpy(&d, e->P.rq + (first + i) * e->C.rq_cap, sizeof(d), hipMemcpyDeviceToHost));
+    rqx_len[i] = (u32)(d.high >> 32);
+  }
   for (u64 i = 0; i < count; i++) {
     rbe_replica_view& v = out[i];
     memset(&v, 0, sizeof(v));
@@ -2060,7 +2265,7 @@ int rbe_get_views(rbe_engine* e, uint64_t first, uint64_t count, rbe_replica_vie
     v.q_no_activity_since = h.q_no_activity_since;
     v.q_exit_quiesce_tick = h.q_exit_quiesce_tick;
     v.raft_quiesce = (h.flags & HF_RAFT_QUIESCE) ? 1 : 0;
-    v.rq_count = c.rq_count;
+    v.rq_count = c.rq_count == kRqExt ? rqx_len[i] : c.rq_count;
     v.votes_resp = h.votes_resp;
     v.votes_granted = h.votes_granted;
     v.events = (e->round > 0 && upd[i].round == e->round - 1) ? upd[i].events : 0u;
@@ -2118,11 +2323,15 @@ int rbe_get_update_commits(rbe_engine* e, uint64_t first, uint64_t count, rbe_up
     int trc = RBE_OK;
     auto term_of = [&](u64 idx) -> u64 {
       if (idx == core[i].last_index) return core[i].t_last;
-      u64 t = 0;  // the log moved since the step (a relaunch): read the ring
-      if (hipMemcpy(&t, e->P.term_ring + (idx & (u64)(e->C.ring - 1)) * e->C.n_rep + r,
-                    sizeof(u64), hipMemcpyDeviceToHost) != hipSuccess)
-        trc = RBE_E_HIP;
-      return t;
+      // the log moved since the step (a relaunch): read the log
+      std::vector<u64> t;
+      std::vector<Body> b;
+      const int x = read_window(e, r, idx, idx, t, b);
+      if (x) {
+        trc = x;
+        return 0;
+      }
+      return t[0];
     };
     update_commit_view(u[i], app[i], snp.empty() ? 0 : snp[i].marker, term_of, out[i]);
     if (trc) return trc;
@@ -2162,6 +2371,30 @@ int rbe_get_snapshot_state(rbe_engine* e, uint64_t first, uint64_t count, uint64
   return RBE_OK;
 }
 
+// One message list in reading order, from its count word and the host copy of
+// its plane slots (`pl`); a spilled list is read from the round spill heap
+// (rbe_spill.h list_view)
+static int host_list(rbe_engine* e, u32 par, u64 li, u32 w, const Msg* pl, std::vector<Msg>& out) {
+  out.clear();
+  const Msg* base = pl;
+  u32 cap = e->C.maxm, na = w & 0x7Fu, nb = (w >> 7) & 0x7Fu;
+  std::vector<Msg> blk;
+  if (w & kCntSpill) {
+    const Msg h = pl[0];
+    cap = h.pad1;
+    na = (u32)h.log_index;
+    nb = (u32)h.commit;
+    blk.resize(cap);
+    HIP_OK(hipMemcpyAsync(blk.data(), e->P.spill[par] + h.hint * 16, (u64)cap * sizeof(Msg),
+                          hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    base = blk.data();
+  }
+  (void)li;
+  for (u32 i = 0; i < na + nb; i++) out.push_back(base[i < na ? i : cap - 1u - (i - na)]);
+  return RBE_OK;
+}
+
 int rbe_get_messages(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t cap,
                      uint32_t* n_out) {
   if (!e || !n_out || replica >= e->C.n_rep || e->round == 0) return RBE_E_INVALID;
@@ -2178,9 +2411,11 @@ int rbe_get_messages(rbe_engine* e, uint64_t replica, rbe_message* out, uint32_t
   HIP_OK(hipStreamSynchronize(e->stream));
   u32 n = 0;
   for (u32 d = 0; d < N; d++) {
-    const u32 pc = row_word(row, d, k, e->round), na = pc & 0x7F, nb = (pc >> 7) & 0x7F;
-    for (u32 i = 0; i < na + nb; i++) {
-      const Msg& m = i < na ? lst[d * e->C.maxm + i] : lst[d * e->C.maxm + e->C.maxm - 1 - (i - na)];
+    std::vector<Msg> ms;
+    const int rc = host_list(e, par, replica * N + d, row_word(row, d, k, e->round),
+                             &lst[d * e->C.maxm], ms);
+    if (rc) return rc;
+    for (const Msg& m : ms) {
       if (n < cap && out) msg_out(m, cid_of(e->C, g), e->hin.id_table(), N, g, out[n]);
       n++;
     }
@@ -2371,8 +2606,15 @@ int rbe_get_ready_to_reads(rbe_engine* e, uint64_t replica, rbe_ready_to_read* o
   HIP_OK(hipMemcpyAsync(v.data(), e->P.rtr + replica * e->C.rtr_cap, v.size() * sizeof(RTR),
                         hipMemcpyDeviceToHost, e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
-  u32 n = u.n_rtr < e->C.rtr_cap ? u.n_rtr : e->C.rtr_cap;
+  u32 n = u.n_rtr;
   if (e->round == 0 || u.round != e->round - 1) n = 0;
+  if (n > e->C.rtr_cap) {  // the list moved to the round spill heap (rbe_spill.h rtr_list)
+    const u64 gr = v[0].index;
+    v.resize(n);
+    HIP_OK(hipMemcpyAsync(v.data(), e->P.spill[u.round & 1u] + gr * 16, n * sizeof(RTR),
+                          hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+  }
   for (u32 i = 0; i < n && i < cap && out; i++) {
     out[i].index = v[i].index;
     out[i].ctx_low = v[i].low;
@@ -2391,17 +2633,31 @@ static int read_window(rbe_engine* e, u64 replica, u64 lo, u64 hi, std::vector<u
   Core c;
   HIP_OK(hipMemcpyAsync(&c, e->P.core + replica, sizeof(c), hipMemcpyDeviceToHost, e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
-  if (hi > c.last_index || c.last_index - lo >= e->C.ring) return RBE_E_INVALID;
-  t.resize(hi - lo + 1);
-  b.resize(hi - lo + 1);
-  for (u64 i = lo; i <= hi; i++) {
-    const u64 slot = (i & (u64)(e->C.ring - 1)) * e->C.n_rep + replica;
-    HIP_OK(hipMemcpyAsync(&t[i - lo], e->P.term_ring + slot, sizeof(u64), hipMemcpyDeviceToHost,
-                          e->stream));
-    HIP_OK(hipMemcpyAsync(&b[i - lo], e->P.pay_ring + slot, sizeof(Body), hipMemcpyDeviceToHost,
-                          e->stream));
-  }
+  if (hi > c.last_index) return RBE_E_INVALID;
+  // the ring window and the cold log below it (the LogDB's entries above its
+  // marker): one gather kernel, one copy
+  const u64 n = hi - lo + 1;
+  int rc = grow(&e->gat_dev, &e->gat_dev_bytes, n * sizeof(Ent) + 256, false);
+  if (rc) return rc;
+  u32* miss = (u32*)(e->gat_dev + n * sizeof(Ent));
+  HIP_OK(hipMemsetAsync(miss, 0, sizeof(u32), e->stream));
+  hipLaunchKernelGGL(k_log_gather, dim3(1), dim3(kBlock), 0, e->stream, e->P, e->C, replica, lo, hi,
+                     (Ent*)e->gat_dev, miss);
+  std::vector<Ent> en(n);
+  u32 nmiss = 0;
+  HIP_OK(hipMemcpyAsync(en.data(), e->gat_dev, n * sizeof(Ent), hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipMemcpyAsync(&nmiss, miss, sizeof(u32), hipMemcpyDeviceToHost, e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
+  if (nmiss) return RBE_E_STATE;  // compacted (ErrCompacted), or never handed over
+  t.resize(n);
+  b.resize(n);
+  for (u64 i = 0; i < n; i++) {
+    t[i] = en[i].term;
+    b[i].type = en[i].type;
+    b[i].len = en[i].len;
+    b[i].lo = en[i].lo;
+    b[i].hi = en[i].hi;
+  }
   return RBE_OK;
 }
 
@@ -2462,6 +2718,20 @@ int rbe_get_entry_cmds(rbe_engine* e, uint64_t replica, uint64_t lo, uint64_t hi
     }
   }
   HIP_OK(hipStreamSynchronize(e->stream));
+  return RBE_OK;
+}
+
+int rbe_spill_stats(rbe_engine* e, uint64_t* out) {
+  if (!e || !out) return RBE_E_INVALID;
+  HIP_OK(hipSetDevice(e->device));
+  SpillCtl s;
+  HIP_OK(hipMemcpyAsync(&s, e->P.sctl, sizeof(s), hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipStreamSynchronize(e->stream));
+  out[0] = s.live;
+  out[1] = e->C.pool_pages - 1;
+  out[2] = std::max(s.peak[0], s.peak[1]) * 16;
+  out[3] = e->C.spill_units * 16;
+  out[4] = s.oom;
   return RBE_OK;
 }
 

@@ -105,7 +105,9 @@ RBE_HD InMsg load_in(const Msg* p) {
   InMsg x;
   x.type = m.type;
   x.reject = m.reject;
-  x.n_ent = m.n_ent;
+  // entries in the round spill heap (rbe_spill.h kMsgXEnt): a count no fast
+  // step takes, so the round goes to the full handler table
+  x.n_ent = (m.pad0 & kMsgXEnt) ? 0xFFFFu : m.n_ent;
   x.ent_off = m.ent_off;
   x.term = m.term;
   x.log_term = m.log_term;
@@ -157,6 +159,8 @@ struct FastOut {
   // reload after the lane's first store waits for every store before it
   u32 fault0, n_out, n_drop_msg, n_ent_out;
   u32 events;  // EV_* of the step (Upd::events)
+  // messages past a full plane list (rbe_spill.h; relocated in fast_finish)
+  OutStash ost;
 
   RBE_HD u32 get_pc(u32 d) const {
     return d < 4 ? (u32)((pc >> (16 * d)) & 0xFFFFu) : (u32)((pc_hi >> (16 * (d - 4))) & 0xFFFFu);
@@ -214,12 +218,15 @@ struct FastOut {
     const u32 c = get_pc(d);
     const u32 a = c & 0x7Fu, b = (c >> 7) & 0x7Fu;
     const u32 full = drop ? 0u : (a + b >= C.maxm ? 1u : 0u);
-    fault_if(full != 0, F_OUTBOX);
-    const u32 ok = 1u - drop - full;
+    const u32 ok = 1u - drop;
     n_drop_msg += drop;
     n_out += ok;
     n_ent_out += ok ? (u32)m.n_ent : 0u;
     if (!ok) return;
+    if (full) {  // the list moves to the spill heap at the step's end
+      fault_if(!stash_put(P, C, par, ost, m), F_NOMEM);
+      return;
+    }
     u32 slot;
     if (m.type == M_Replicate) {
       slot = a;
@@ -235,8 +242,9 @@ struct FastOut {
   template <class CT>
   RBE_HD void dropped_read_index(const Planes& P, const Params& C, CT& ctr, u64 low,
                                  u64 high) {  // raft.go:1999-2012
+    // (the fast leader drops at most one ReadIndex a step, and dri_cap >= 1)
     const bool full = n_drop_ri >= C.dri_cap;
-    fault_if(full, F_DROPLIST);
+    fault_if(full, F_NOMEM);
     event_if(!full, EV_READ_INDEX_DROPPED);
     if (full) return;
     DropRI x;
@@ -252,8 +260,9 @@ struct FastOut {
   template <class CT>
   RBE_HD void ready_to_read(const Planes& P, const Params& C, CT& ctr, u64 index,
                             u64 low, u64 high) {  // raft.go:1624-1630
+    // (eligibility keeps a fast step's ReadyToReads within rtr_cap)
     const bool full = n_rtr >= C.rtr_cap;
-    fault_if(full, F_RTR);
+    fault_if(full, F_NOMEM);
     if (full) return;
     RTR x;
     x.index = index;
@@ -376,6 +385,12 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, CT& ctr, FastOut<N, TR
   ctr.v[C_MSG_OUT] += o.n_out;
   ctr.v[C_MSG_DROPPED] += o.n_drop_msg;
   ctr.v[C_ENT_OUT] += o.n_ent_out;
+  // this sender's outbox header: stamp + the N count words; lists with
+  // stashed messages move whole to the spill heap (rare: rbe_spill.h)
+  if (o.ost.n) o.fault |= outbox_relocate(P, C, o.par, r, N, o.ost, o.pc, o.pc_hi);
+  u32 ow[N];
+#pragma unroll
+  for (u32 dd = 0; dd < N; dd++) ow[dd] = o.get_pc(dd) & 0xFFFFu;
   Upd u;
   u.save_lo = c.saved_to + 1;
   u.save_hi = c.last_index;
@@ -464,7 +479,7 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, CT& ctr, FastOut<N, TR
   u.n_drop_ent = 0;
   u.n_drop_ri = (u16)o.n_drop_ri;
   u.fault = o.fault;
-  ctr.v[C_FAULTS] += popc8(o.fault & ~o.fault0 & 0xFFu);
+  ctr.v[C_FAULTS] += popc8(o.fault & ~o.fault0 & 0xFFu) + ((o.fault & ~o.fault0) >> 8 & 1u);
   // chunks 0-2 only when they carry something (Upd, rbe_types.h)
   const bool ranges = TRACE || u.save_lo <= u.save_hi || u.apply_lo <= u.apply_hi ||
                       o.n_drop_ri != 0;
@@ -476,13 +491,7 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, CT& ctr, FastOut<N, TR
 #ifndef RBE_DIAG_NO_STATE_STORES
   if (ranges) P.upd[r] = u;
   else __builtin_memcpy((char*)&P.upd[r] + 48, (const char*)&u + 48, 16);
-  // this sender's outbox header: stamp + the N count words, one 16-B store
-  {
-    u32 w[N];
-#pragma unroll
-    for (u32 dd = 0; dd < N; dd++) w[dd] = o.get_pc(dd) & 0xFFFFu;
-    put_row(P, r, o.round_, N, w);
-  }
+  put_row(P, r, o.round_, N, ow);  // one 16-B store
   h.flags = o.fault ? (u8)(flags | HF_FAULTED) : flags;
   h.election_tick = etick;
   h.heartbeat_tick = (u16)htick;
@@ -588,7 +597,14 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   if (c.ltt != 0) return false;
   if (!ck.tick) return false;
   if (C.xfer_period && xfer_input(C, cid, round, k)) return false;
-  if (c.rq_count >= Cap::RQ) return false;
+  // a queue past the register copy (or in pool pages: kRqExt), or one that
+  // this round's ReadIndex could overflow, takes the full table
+  if (c.rq_count >= Cap::RQ || c.rq_count >= C.rq_cap) return false;
+  // the step's outputs stay within the planes' lists: ReadyToReads of the
+  // queue (<= RQ), one dropped ReadIndex, two arena entries (rbe_spill.h)
+  if (C.rtr_cap < Cap::RQ || C.ecap < 2) return false;
+  // the apply range (< last + 2) stays in the ring window
+  if (c.last_index + 1 - c.processed > C.ring) return false;
   u32 inp = wl_input(C, cid, round);
   // Host input (rbe_push_read_index / rbe_push_proposals): one ReadIndex, or
   // one inline non-ConfigChange entry, takes the same path as the workload's
@@ -634,6 +650,27 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   // branch waits for its own loads (a wait inside each conditional block
   // would serialise the message loads).
   if constexpr (!AUX) load_inbox();
+  // the proposal's ring slot holds entry last + 1 - ring: it goes to the cold
+  // log (rbe_spill.h) unless compacted; its record and the cold-log ref now
+  const u64 lmark = C.snapshot_entries ? P.snp[r].marker : 0;
+  const u64 ev_idx = c.last_index + 1 > C.ring ? c.last_index + 1 - C.ring : 0;
+  const bool ev = inp == 1 && ev_idx > lmark;
+  Ent ev_e;
+  ColdRef ev_cr;
+  ev_e.term = ev_e.lo = ev_e.hi = 0;
+  ev_e.type = ev_e.len = 0;
+  ev_cr.head = ev_cr.tail = 0;
+  ev_cr.tail_pn = 0;
+  if (ev) {
+    const u64 es = (ev_idx & (u64)(C.ring - 1)) * C.n_rep + r;
+    const Body eb = P.pay_ring[es];
+    ev_e.term = P.term_ring[es];
+    ev_e.type = eb.type;
+    ev_e.len = eb.len;
+    ev_e.lo = eb.lo;
+    ev_e.hi = eb.hi;
+    ev_cr = P.cold[r];
+  }
   u64 rq_lo[Cap::RQ], rq_hi[Cap::RQ], rq_ix[Cap::RQ];
   u32 rq_fr[Cap::RQ], rq_cf[Cap::RQ];
   u32 rq_n = c.rq_count, rq_h = c.rq_head;
@@ -762,6 +799,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   o.fault0 = o.fault;
   o.msg_hash = o.rtr_hash = o.drop_hash = 0;
   o.events = 0;
+  stash_init(o.ost);
   o.term = c.term;
   u8 flags = h.flags;
   u32 etick = h.election_tick, htick = h.heartbeat_tick;
@@ -783,13 +821,12 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   // next[s] > last0, at an index >= lead_start (makeReplicateMessage), so
   // "lower" (0) is exact for every use.  The ring read the general Lane
   // performs is still counted and window-checked.
+  // (an index below the ring is in the cold log, and of a lower term too)
   auto log_term = [&](u64 idx) -> u64 {
     if (idx > c.last_index || idx == 0) return 0;
     if (idx == c.last_index) return c.t_last;
-    const bool miss = c.last_index - idx >= C.ring;
-    o.fault_if(miss, F_WINDOW);
-    ctr.v[C_RING_ACCESS] += miss ? 0u : 1u;
-    return !miss && idx >= c.lead_start ? c.term : 0;
+    ctr.v[C_RING_ACCESS]++;
+    return idx >= c.lead_start ? c.term : 0;
   };
   auto ent_at = [&](u64 idx) -> Ent {  // ring entry idx (registers when just proposed)
     // anything else is excluded by the eligibility rule next[s] > last0
@@ -1170,6 +1207,11 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
       }
       // appendEntries (raft.go:909-920)
       const u64 idx = c.last_index + 1;
+      if (ev) {  // the entry the slot held, into the cold log
+        const u32 t0 = ev_cr.tail;
+        o.fault_if(!cold_put(P, C, ev_cr, ev_idx, ev_e, par), F_NOMEM);
+        if (ev_cr.tail != t0) P.cold[r] = ev_cr;
+      }
       const u64 sl = (idx & (u64)(C.ring - 1)) * C.n_rep + r;
       P.term_ring[sl] = c.term;
       Body b;
@@ -1313,6 +1355,8 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   if (!ck.tick) return false;
   if (C.xfer_period && xfer_input(C, cid_of_n<N>(C, g), round, k)) return false;
   if (C.ext_inputs && P.ext[r].flags) return false;
+  // the step's ReadyToReads (one per ReadIndexResp) stay within the plane list
+  if (C.rtr_cap < Cap::FMAXM) return false;
   const u32 ls = (u32)c.leader - 1u;  // leader slot (0xFFFFFFFF when no leader)
   u32 n_in = 0;
 #pragma unroll
@@ -1342,6 +1386,29 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   } else {
     (void)ls_a;
   }
+  // a Replicate may append at last + 1, whose ring slot holds entry last + 1
+  // - ring: it goes to the cold log (rbe_spill.h) unless compacted; its
+  // record and the cold-log ref now, with the messages
+  const u64 lmark = C.snapshot_entries ? P.snp[r].marker : 0;
+  const u64 ev_idx = c.last_index + 1 > C.ring ? c.last_index + 1 - C.ring : 0;
+  const bool ev = na > 0 && ev_idx > lmark;
+  bool ev_app = false;
+  Ent ev_e;
+  ColdRef ev_cr;
+  ev_e.term = ev_e.lo = ev_e.hi = 0;
+  ev_e.type = ev_e.len = 0;
+  ev_cr.head = ev_cr.tail = 0;
+  ev_cr.tail_pn = 0;
+  if (ev) {
+    const u64 es = (ev_idx & (u64)(C.ring - 1)) * C.n_rep + r;
+    const Body eb = P.pay_ring[es];
+    ev_e.term = P.term_ring[es];
+    ev_e.type = eb.type;
+    ev_e.len = eb.len;
+    ev_e.lo = eb.lo;
+    ev_e.hi = eb.hi;
+    ev_cr = P.cold[r];
+  }
 #pragma unroll
   for (u32 i = 0; i < Cap::FMAXM; i++) {
     if (i < n_in) in[i] = load_in(&raw[i]);
@@ -1353,6 +1420,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
     const u32 t = in[i].type;
     if (in[i].term != c.term) return false;
     if (t != M_Replicate && t != M_Heartbeat && t != M_ReadIndexResp) return false;
+    if (in[i].n_ent == 0xFFFFu) return false;  // entries in the spill heap (load_in)
   }
   FastQ q;
   q.tick = h.q_tick;
@@ -1405,6 +1473,8 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
                 E_ConfigChange)
           return false;
         if (m.n_ent == 1) {                      // conflict at L + 1: append
+          // a second append past the ring would evict an entry not loaded above
+          if (L != c.last_index && L + 1 > C.ring) return false;
           T = i == 0 ? pre0.term : (i == 1 ? pre1.term : (i == 2 ? pre2.term : pre3.term));
           L = L + 1;
         }
@@ -1415,6 +1485,9 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
         if (m.commit > Cm && m.commit <= L) Cm = m.commit;
       }
     }
+    // the apply range stays in the ring window
+    if (L - c.processed > C.ring) return false;
+    ev_app = ev && L > c.last_index;  // the append at last + 1 happens
   }
   // ---- compute.  Every load above has completed before the first store
   // below (vmcnt counts loads and stores in order; see lead_fast).
@@ -1436,6 +1509,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   o.fault0 = o.fault;
   o.msg_hash = o.rtr_hash = o.drop_hash = 0;
   o.events = 0;
+  stash_init(o.ost);
   o.term = c.term;
   u8 flags = h.flags;
   u32 etick = h.election_tick;
@@ -1461,6 +1535,11 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
     c.committed = idx;
   };
   const u32 lid = ls + 1;
+  if (ev_app) {  // the append's ring slot held entry ev_idx: into the cold log
+    const u32 t0 = ev_cr.tail;
+    o.fault_if(!cold_put(P, C, ev_cr, ev_idx, ev_e, par), F_NOMEM);
+    if (ev_cr.tail != t0) P.cold[r] = ev_cr;
+  }
 #pragma unroll
   for (u32 s = 0; s < N; s++) {
     if (s == k) continue;
@@ -1511,7 +1590,8 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
               u64 tl = c.t_last;
               for (u32 e = ci; e < m.n_ent; e++) {
                 const Ent x = ent(e);
-                const u64 sl = ((m.log_index + 1 + e) & (u64)(C.ring - 1)) * C.n_rep + r;
+                const u64 ai = m.log_index + 1 + e;
+                const u64 sl = (ai & (u64)(C.ring - 1)) * C.n_rep + r;
                 P.term_ring[sl] = x.term;
                 Body b;
                 b.type = x.type;

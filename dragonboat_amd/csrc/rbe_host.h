@@ -44,6 +44,27 @@ inline auto with_n(u32 n, F&& f) -> decltype(f(std::integral_constant<int, 1>())
   }
 }
 
+// The spill tiers' sizes (rbe_spill.h): cfg.pool_bytes of page pool (0 = 8
+// KiB per replica, at least 64 MiB and at most 32 GiB: four pages, 256
+// entries of cold log, per replica on average) and cfg.spill_bytes of round
+// spill heap per round parity (0 = 128 B per replica, at least 16 MiB, at most
+// 4 GiB).  Shared with the test-only host build (tests/soa_cpu).
+inline int spill_sizes(const rbe_config* cfg, Params* C) {
+  const u64 R = C->n_rep, page = (u64)kPageEnts * sizeof(Ent);
+  u64 pb = cfg->pool_bytes;
+  if (!pb) pb = std::min(std::max(R * 8192ull, 64ull << 20), 32ull << 30);
+  u64 pages = pb / page;
+  if (pages < 2 || pages > 0xFFFFFFF0ull) return RBE_E_INVALID;
+  C->pool_pages = (u32)pages;
+  u64 sb = cfg->spill_bytes;
+  const u64 W = C->rep_world > 1 ? C->rep_world : 1;  // (a share per rank: spill_alloc)
+  if (!sb) sb = std::min(std::min(std::max(R * 128ull, 16ull << 20), 4ull << 30) * W, 0xFFFFFFF0ull * 16);
+  const u64 units = sb / 16;
+  if (units / W < 64 || units > 0xFFFFFFF0ull) return RBE_E_INVALID;  // granules are u32 in messages
+  C->spill_units = units;
+  return RBE_OK;
+}
+
 // Fingerprint of a Cmd longer than 16 bytes (Body/Ent lo when the bytes live in
 // the payload heap): 64 bits over the zero-padded 8-byte words and the length.
 // The trace digest folds it in place of the inline bytes, so the fingerprint
@@ -283,7 +304,7 @@ RBE_HD void msg_out(const Msg& m, u64 cid, const u64* ids, u32 n, u64 g, rbe_mes
   o.commit = m.commit;
   o.hint = hint_is_node(m.type) ? ext_id(ids, n, g, m.hint) : m.hint;
   o.hint_high = m.hint_high;
-  o.n_entries = m.n_ent;
+  o.n_entries = msg_nent(m);
   o.reserved = msg_reserved(m);
 }
 // an rbe_update's node ids (vote, leader) from the internal ids of group g
@@ -345,24 +366,22 @@ RBE_HD u64 heap_low_group(const Planes& P, const Params& C, u64 g, u32 round) {
     if (!owns_replica(C, g, k)) continue;
     const u64 r = g * N + k;
     const u64 last = P.core[r].last_index;
-    u64 from = last >= C.ring ? last - C.ring + 1 : 1;
-    if (mark + 1 > from) from = mark + 1;
-    for (u64 i = from; i <= last; i++) {
-      const Body b = P.pay_ring[(i & (u64)(C.ring - 1)) * C.n_rep + r];
-      if (ent_heap(b.type) && b.hi < lo) lo = b.hi;
+    u64 from = mark + 1;
+    if (C.snapshot_entries && P.snp[r].marker + 1 > from) from = P.snp[r].marker + 1;
+    for (u64 i = from; i <= last; i++) {  // the ring window and the cold log below it
+      Ent e;
+      if (log_ent_at(P, C, r, last, i, &e) && ent_heap(e.type) && e.hi < lo) lo = e.hi;
     }
     if (round == 0) continue;
     const CntRow row = P.cnt[par][r];
     for (u32 d = 0; d < N; d++) {
-      const u32 nb = (row_word(row, d, k, round) >> 7) & 0x7Fu;
-      const Msg* lst = &P.msgs[par][((g * N + k) * N + d) * (u64)C.maxm];
-      for (u32 i = 0; i < nb; i++) {
-        const Msg m = lst[C.maxm - 1u - i];
+      const ListView lv = list_view(P, C, par, r * N + d, row_word(row, d, k, round));
+      for (u32 i = 0; i < lv.n(); i++) {
+        const Msg m = lv.at(i);
         if (m.type != M_Propose) continue;
-        for (u32 j = 0; j < m.n_ent && m.ent_off + j < C.ecap; j++) {
-          const Ent e = P.arena[par][r * C.ecap + m.ent_off + j];
-          if (ent_heap(e.type) && e.hi < lo) lo = e.hi;
-        }
+        const Ent* es = msg_ents(P, C, par, r, m);
+        for (u32 j = 0; j < msg_nent(m); j++)
+          if (ent_heap(es[j].type) && es[j].hi < lo) lo = es[j].hi;
       }
     }
   }
@@ -434,10 +453,9 @@ inline int launch_rows(const Params& C, HostHeap& heap, u64 n, const u64* replic
     if (snap && !C.snapshot_entries) return RBE_E_INVALID;
     if (x.marker > x.last_index || x.n_entries > x.last_index - x.marker ||
         x.commit < x.marker || x.snapshot_index < x.marker || x.snapshot_index > x.last_index ||
-        (x.marker && !x.marker_term) || (x.snapshot_index && !x.snapshot_term) ||
-        (x.marker && x.last_index - x.marker >= C.ring))
+        (x.marker && !x.marker_term) || (x.snapshot_index && !x.snapshot_term))
       return RBE_E_INVALID;
-    if (replica[i] >= C.n_rep || x.n_entries > C.ring || x.n_entries > x.last_index ||
+    if (replica[i] >= C.n_rep || x.n_entries > x.last_index ||
         x.commit > x.last_index || x.vote > C.n || (x.last_index > x.marker && !x.n_entries))
       return RBE_E_INVALID;
     // the LogDB's membership (packed: slots not in Addresses | Observers << 8 |

@@ -166,6 +166,7 @@ template <int N, bool TRACE>
 __global__ __launch_bounds__(kBlock) void k_step(Planes P, Params C, RoundArg ra) {
   const Clk ck = clk_of(ra);
   const u64 r = (u64)blockIdx.x * kBlock + threadIdx.x;
+  if (r == 0) spill_clear_next(P, ck.round & 1u);
   StepCounters c;
 #pragma unroll
   for (int i = 0; i < C_NUM; i++) c.v[i] = 0;
@@ -311,6 +312,7 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
   const u32 round = ck.round;
   const u32 par = round & 1u;
   list_clear_next(L, par, kSlots);
+  if (blockIdx.x == 0 && threadIdx.x == 0) spill_clear_next(P, par);
   if (threadIdx.x < kSlots) s_n[threadIdx.x] = 0;
   if (threadIdx.x == 0) s_ng = s_nal = s_slp[0] = s_slp[1] = 0;
   __syncthreads();
@@ -617,6 +619,7 @@ __global__ __launch_bounds__(kBlock, RBE_FAST_WAVES) void k_round(Planes P, Para
   const u32 round = ck.round;
   const u32 par = round & 1u;
   list_clear_next(L, par, 3);  // slot 2: the full list
+  if (blockIdx.x == 0 && threadIdx.x == 0) spill_clear_next(P, par);
   if (threadIdx.x == 0) s_nl = s_nf = 0;
   __syncthreads();
   StepCounters c;

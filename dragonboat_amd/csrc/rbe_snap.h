@@ -18,7 +18,9 @@
 // order below, rows in order, each row `count * group_bytes` bytes.
 #pragma once
 
-#include "rbe_types.h"
+#include <cstring>
+
+#include "rbe_step.h"
 
 namespace rbe {
 
@@ -31,10 +33,13 @@ struct SnapHeader {
   u32 round, hdr_bytes;
   u64 first, count;
   u64 body_bytes;
-  u64 behavior;  // snap_behavior_hash of the writing configuration
-  u64 tclk;      // ticks before `round` (Clk::tclk)
+  u64 behavior;   // snap_behavior_hash of the writing configuration
+  u64 tclk;       // ticks before `round` (Clk::tclk)
+  u64 log_bytes;  // the log section after the planes (snap_log_*)
 };
-static_assert(sizeof(SnapHeader) == 88, "snapshot header layout");
+static_assert(sizeof(SnapHeader) == 96, "snapshot header layout");
+// where the log section starts (16-B aligned after the planes)
+inline u64 snap_log_at(u64 body_bytes) { return (sizeof(SnapHeader) + body_bytes + 15) & ~15ull; }
 
 struct SnapPlane {
   u8* base;          // plane start
@@ -140,8 +145,187 @@ inline int snap_check_header(const Params& C, u32 abi, const SnapHeader* h, u64 
     return -1;
   if (h->behavior != snap_behavior_hash(C)) return -1;
   if (h->count == 0 || h->first >= C.n_groups || h->count > C.n_groups - h->first) return -1;
-  if (buf_bytes < sizeof(SnapHeader) + h->body_bytes) return -1;
+  if (buf_bytes < snap_log_at(h->body_bytes) + h->log_bytes) return -1;
   return 0;
+}
+
+// ---------------------------------------------------------------- the log section
+// After the planes, 16-B aligned (snap_log_at): the spill-tier state that
+// lives across rounds (rbe_spill.h), replica by replica of the range, each a
+// SnapLogRec followed by its cold log's pages whole (SnapPage, in chain
+// order) and then, for a readIndex queue that moved into pool pages
+// (Core::rq_count == kRqExt), its requests in order.  The round spill heap
+// is not carried: an export whose next round would read a spilled list or
+// spilled entries, or whose last step's ReadyToReads / dropped ReadIndexes
+// went past their planes, is refused (snap_round_spilled).
+struct alignas(16) SnapLogRec {
+  u32 n_pages, n_rq;
+  u64 pad;
+};
+struct alignas(16) SnapPage {
+  u64 pn, pad;
+  Ent e[kPageEnts];
+};
+
+// The log section of replicas [r0, r0 + nr): its size, written at `out`
+// unless null.  The accessor reads the source engine: cold(r) / core(r) /
+// rq(r) (the queue descriptor) rows, meta(p) a page's PoolMeta, page(p, out)
+// its kPageEnts entries.
+template <class SRC>
+u64 snap_log_write(const Params& C, u64 r0, u64 nr, SRC& s, u8* out) {
+  u64 at = 0;
+  for (u64 r = r0; r < r0 + nr; r++) {
+    const ColdRef cr = s.cold(r);
+    const Core c = s.core(r);
+    SnapLogRec h = {};
+    const u64 hat = at;
+    at += sizeof(SnapLogRec);
+    for (u32 p = cr.head; p;) {
+      const PoolMeta m = s.meta(p);
+      if (out) {
+        SnapPage* sp = (SnapPage*)(out + at);
+        sp->pn = m.pn;
+        sp->pad = 0;
+        s.page(p, sp->e);
+      }
+      at += sizeof(SnapPage);
+      h.n_pages++;
+      p = p == cr.tail ? 0u : m.next;
+    }
+    if (c.rq_count == kRqExt) {
+      const RqExt x = s.rq(r);
+      h.n_rq = x.n;
+      u32 p = x.head, pos = x.off;
+      Ent pg[kPageEnts];
+      bool have = false;
+      for (u32 i = 0; i < x.n; i++, pos++) {
+        if (pos == kPageEnts) {
+          p = s.meta(p).next;
+          pos = 0;
+          have = false;
+        }
+        if (out) {
+          if (!have) s.page(p, pg);
+          have = true;
+          *(ReadReq*)(out + at) = *(const ReadReq*)&pg[pos];
+        }
+        at += sizeof(ReadReq);
+      }
+    }
+    if (out) *(SnapLogRec*)(out + hat) = h;
+  }
+  (void)C;
+  return at;
+}
+
+// A snapshot's log section checked against its planes before anything is
+// imported: the offset of each of its nr replica records into rec_off; -1
+// when a record runs past the section, or a replica's readIndex queue is in
+// pool pages (Core::rq_count == kRqExt in the snapshot's Core rows) without
+// requests in its record, or the other way round.
+inline int snap_log_index(const Params& C, const u8* snap, u64 nr, u64* rec_off) {
+  SnapHeader hd;
+  memcpy(&hd, snap, sizeof(hd));
+  const SnapHeader* h = &hd;
+  const u8* sec = snap + snap_log_at(h->body_bytes);
+  // the Core rows follow the Hot rows (snap_planes order)
+  const u8* core = snap + sizeof(SnapHeader) + nr * sizeof(Hot);
+  u64 at = 0;
+  for (u64 i = 0; i < nr; i++) {
+    if (at + sizeof(SnapLogRec) > h->log_bytes) return -1;
+    SnapLogRec rec;
+    memcpy(&rec, sec + at, sizeof(rec));
+    Core c;
+    memcpy(&c, core + i * sizeof(Core), sizeof(Core));
+    if ((c.rq_count == kRqExt) != (rec.n_rq != 0)) return -1;
+    const u64 sz = sizeof(SnapLogRec) + (u64)rec.n_pages * sizeof(SnapPage) +
+                   (u64)rec.n_rq * sizeof(ReadReq);
+    if (sz > h->log_bytes - at) return -1;
+    rec_off[i] = at;
+    at += sz;
+  }
+  (void)C;
+  return at == h->log_bytes ? 0 : -1;
+}
+
+// Replica r's record of a log section (16-B aligned, at `rec`): rebuilds its
+// cold log chain and its pool-page readIndex queue in this engine's pool
+// (page allocation as in a round of parity `par`), after the planes were
+// imported and r's old chains released (spill_replica_release).  Returns the
+// record's size, or 0 when the pool is exhausted (*fault = F_NOMEM).
+RBE_HD u64 snap_log_rebuild(const Planes& P, const Params& C, u64 r, const u8* rec, u32 par,
+                            u32* fault) {
+  const SnapLogRec h = *(const SnapLogRec*)rec;
+  u64 at = sizeof(SnapLogRec);
+  ColdRef cr;
+  cr.head = cr.tail = 0;
+  cr.tail_pn = 0;
+  for (u32 i = 0; i < h.n_pages; i++, at += sizeof(SnapPage)) {
+    const SnapPage* sp = (const SnapPage*)(rec + at);
+    const u32 p = pool_alloc(P, C, par);
+    if (!p) {
+      P.cold[r] = cr;
+      *fault = F_NOMEM;
+      return 0;
+    }
+    PoolMeta m;
+    m.pn = sp->pn;
+    m.prev = cr.tail;
+    m.next = 0;
+    P.pmeta[p] = m;
+    if (cr.tail) P.pmeta[cr.tail].next = p;
+    else cr.head = p;
+    cr.tail = p;
+    cr.tail_pn = sp->pn;
+    for (u32 j = 0; j < kPageEnts; j++) *pool_ent(P, p, j) = sp->e[j];
+  }
+  P.cold[r] = cr;
+  if (h.n_rq) {
+    RqExt x;
+    x.head = x.tail = 0;
+    x.off = 0;
+    x.n = 0;
+    for (u32 i = 0; i < h.n_rq; i++, at += sizeof(ReadReq)) {
+      if (i % kPageEnts == 0) {
+        const u32 p = pool_alloc(P, C, par);
+        if (!p) {
+          if (x.head) rq_ext_free(P, x, par);
+          P.core[r].rq_count = 0;
+          P.core[r].rq_head = 0;
+          *fault = F_NOMEM;
+          return 0;
+        }
+        P.pmeta[p].next = 0;
+        if (x.tail) P.pmeta[x.tail].next = p;
+        else x.head = p;
+        x.tail = p;
+      }
+      *(ReadReq*)pool_ent(P, x.tail, i % kPageEnts) = *(const ReadReq*)(rec + at);
+      x.n++;
+    }
+    rq_ext_store(P, C, r, x);
+  }
+  return at;
+}
+
+// Whether replica r's last step left state in the round spill heap that the
+// snapshot cannot carry: a list the next round reads (count word with
+// kCntSpill, stamp `round`), a message of those lists with entries in the
+// heap, ReadyToReads / dropped ReadIndexes past the planes.  w[d] = r's count
+// words for the next round (row_word of its outbox header of parity
+// (round - 1) & 1), `lists` its N * maxm slots, `u` its Upd.
+inline bool snap_round_spilled(const Params& C, const u32* w_in, const Msg* lists, const Upd& u) {
+  if (u.n_rtr > C.rtr_cap || u.n_drop_ri > C.dri_cap) return true;
+  for (u32 d = 0; d < C.n; d++) {
+    const u32 w = w_in[d];
+    if (w & kCntSpill) return true;
+    const u32 na = w & 0x7Fu, nb = (w >> 7) & 0x7Fu;
+    for (u32 i = 0; i < na + nb; i++) {
+      const Msg& m = lists[d * C.maxm + (i < na ? i : C.maxm - 1u - (i - na))];
+      if (m.pad0 & kMsgXEnt) return true;
+    }
+  }
+  return false;
 }
 
 }  // namespace rbe

@@ -133,6 +133,10 @@ RBE_HD u32 popc8(u32 x) {
   return (x + (x >> 4)) & 0x0Fu;
 }
 
+}  // namespace rbe
+#include "rbe_spill.h"
+namespace rbe {
+
 // ----------------------------------------------------------------- workload
 // DESIGN.md §Workload; restated independently in oracle/harness.cpp.
 RBE_HD u64 wl_payload_lo(u64 seed, u64 cid, u64 round) {
@@ -517,6 +521,24 @@ __device__ __forceinline__ u8 (&lane_rst())[kMaxN][kLaneCols] {
   return s_rst;
 }
 #endif
+// The spill-tier state of one step (rbe_spill.h): the cold log's ref (loaded
+// on first use), the outbox stash, the ReadyToRead / dropped-ReadIndex lists
+// moved to the spill heap (granule, capacity; capacity 0 = still in the
+// plane), the readIndex queue in pool pages (rqx, rqd)
+struct LaneX {
+  ColdRef cref;
+  OutStash ost;
+  u64 rtr_x, dri_x;
+  RqExt rqd;
+  u32 rtr_xcap, dri_xcap;
+  bool cref_ld, cref_dirty, rqx;
+};
+#if defined(__HIPCC__) || defined(__HIP__)
+__device__ __forceinline__ LaneX (&lane_x())[kLaneCols] {
+  __shared__ LaneX s_x[kLaneCols];
+  return s_x;
+}
+#endif
 
 template <int N, bool TRACE, int MODE>
 struct Lane {
@@ -559,6 +581,15 @@ struct Lane {
   u64 c_match[N], c_next[N];  // LEAD: remote slots held in registers
   u32 c_st[N];
   u8 iso;  // isolation mask of this group for this round
+  // spill-tier state of the step (LaneX): in LDS for k_full_list, whose
+  // lanes are at the register limit, else a member
+  mutable LaneX xm;
+  RBE_HD LaneX& X() const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (LREM) return lane_x()[threadIdx.x];
+#endif
+    return xm;
+  }
   // snapshot_entries > 0: the LogDB compaction marker (SnapSt), the
   // InstallSnapshots sent this step (SnapshotStatus for the next one) and a
   // snapshot restored from one received
@@ -575,6 +606,7 @@ struct Lane {
   u32 seg_off, seg_len;
   u64 mseg_lo;  // the last metadata copy for a witness (arena_meta_range)
   u32 mseg_off, mseg_len;
+  bool seg_x, mseg_x;  // the segment is in the round spill heap (offsets are granules)
   u64 msg_hash, rtr_hash, drop_hash;
   u32 n_msgs, n_rtr, n_drop_ent, n_drop_ri;
   u32 fault;
@@ -609,7 +641,46 @@ struct Lane {
   }
 
   // ------------------------------------------------------------- log (term ring)
+  // The in-memory window is the term / payload ring: entries [max(marker + 1,
+  // last - ring + 1), last] (the invariant every append and merge below keeps).
+  // Older entries above the LogDB marker are in the replica's cold log
+  // (rbe_spill.h), the ILogDB read path of logentry.go:144-161 / 186-246.
   RBE_HD u64 ring_slot(u64 idx) const { return (idx & (u64)(C.ring - 1)) * C.n_rep + r; }
+  RBE_HD ColdRef& cold() {
+    if (!X().cref_ld) {
+      X().cref = P.cold[r];
+      X().cref_ld = true;
+    }
+    return X().cref;
+  }
+  // entry idx (marker < idx <= last) from the ring or the cold log
+  RBE_HD Ent log_ent(u64 idx) {
+    Ent e;
+    if (last - idx < C.ring) {
+      const u64 s = ring_slot(idx);
+      const Body b = P.pay_ring[s];
+      e.term = P.term_ring[s];
+      e.type = b.type;
+      e.len = b.len;
+      e.lo = b.lo;
+      e.hi = b.hi;
+    } else if (!cold_get(P, cold(), idx, &e)) {
+      set_fault(F_WINDOW);  // the launch gave only the LogDB's tail
+      e.term = e.lo = e.hi = 0;
+      e.type = e.len = 0;
+    }
+    return e;
+  }
+  RBE_HD Body log_body(u64 idx) {
+    if (last - idx < C.ring) return P.pay_ring[ring_slot(idx)];
+    const Ent e = log_ent(idx);
+    Body b;
+    b.type = e.type;
+    b.len = e.len;
+    b.lo = e.lo;
+    b.hi = e.hi;
+    return b;
+  }
   // entryLog.term (logentry.go:142-161): 0 with no error outside
   // [firstIndex-1, lastIndex]; firstIndex - 1 is the LogDB's compaction marker
   // (0 without snapshot_entries), whose term the LogDB keeps (Term(marker)).
@@ -617,16 +688,14 @@ struct Lane {
     if (idx > last || idx == 0) return 0;
     if (idx == last) return t_last;
     if (C.snapshot_entries && idx <= marker) return idx == marker ? marker_term : 0;
-    if (last - idx >= C.ring) {
-      set_fault(F_WINDOW);
-      return 0;
-    }
     ctr.v[C_RING_ACCESS]++;
-    return P.term_ring[ring_slot(idx)];
+    if (last - idx < C.ring) return P.term_ring[ring_slot(idx)];
+    return log_ent(idx).term;
   }
   RBE_HD bool match_term(u64 idx, u64 t) { return log_term(idx) == t; }  // logentry.go:357-363
   // log_term split for batched lookups: the value without side effects (a
-  // prefetch that may run ahead of the loop that uses it), and the fault and
+  // prefetch that may run ahead of the loop that uses it; an index below the
+  // ring peeks 0 and is looked up by log_term_account's caller), and the
   // ring-access count log_term would have raised for it
   RBE_HD u64 log_term_peek(u64 idx) const {
     if (idx > last || idx == 0) return 0;
@@ -635,11 +704,35 @@ struct Lane {
     if (last - idx >= C.ring) return 0;
     return P.term_ring[ring_slot(idx)];
   }
+  RBE_HD bool log_term_cold(u64 idx) const {  // log_term(idx) reads the cold log
+    return idx < last && idx != 0 && !(C.snapshot_entries && idx <= marker) && last - idx >= C.ring;
+  }
   RBE_HD void log_term_account(u64 idx) {
     if (idx > last || idx == 0 || idx == last) return;
     if (C.snapshot_entries && idx <= marker) return;
-    if (last - idx >= C.ring) set_fault(F_WINDOW);
-    else ctr.v[C_RING_ACCESS]++;
+    ctr.v[C_RING_ACCESS]++;
+  }
+  // Evict entry j (its ring slot about to be overwritten) into the cold log
+  RBE_HD void evict(u64 j) {
+    const u64 s = ring_slot(j);
+    const Body b = P.pay_ring[s];
+    Ent e;
+    e.term = P.term_ring[s];
+    e.type = b.type;
+    e.len = b.len;
+    e.lo = b.lo;
+    e.hi = b.hi;
+    cold_store(j, e);
+  }
+  RBE_HD void cold_store(u64 j, const Ent& e) {
+    if (!cold_put(P, C, cold(), j, e, par)) set_fault(F_NOMEM);
+    X().cref_dirty = true;
+  }
+  // an append at idx = last + 1: the entry the ring slot held (idx - ring) goes
+  // to the cold log unless it is compacted
+  RBE_HD void log_append(u64 idx, u64 t, u32 type, u32 len, u64 lo, u64 hi) {
+    if (idx > C.ring && idx - C.ring > marker) evict(idx - C.ring);
+    ring_put(idx, t, type, len, lo, hi);
   }
   RBE_HD bool up_to_date(u64 idx, u64 t) {  // logentry.go:365-377
     u64 lt = log_term(last);
@@ -681,10 +774,10 @@ struct Lane {
   RBE_HD u64 limit_count(u64 lo, u64 hi) {
     u64 n = hi - lo + 1;
     if (!C.heap_bytes && n * (128 + 16) <= C.max_entry_size) return n;  // Cmd <= 16 B
-    u64 total = 128 + P.pay_ring[ring_slot(lo)].len;
+    u64 total = 128 + log_body(lo).len;
     u64 inc = 1;
     for (; inc < n; inc++) {
-      total += 128 + P.pay_ring[ring_slot(lo + inc)].len;
+      total += 128 + log_body(lo + inc).len;
       if (total > C.max_entry_size) break;
     }
     return inc;
@@ -848,9 +941,10 @@ struct Lane {
       else m.term = term;
     }
     n_msgs++;
+    const u32 ne = msg_nent(m);
     if (TRACE) {
       u64 h = msg_hash;
-      h = hfold(h, (u64)m.type | ((u64)m.reject << 8) | ((u64)m.n_ent << 16));
+      h = hfold(h, (u64)m.type | ((u64)m.reject << 8) | ((u64)ne << 16));
       h = hfold(h, m.to);
       h = hfold(h, m.from);
       h = hfold(h, m.term);
@@ -859,9 +953,9 @@ struct Lane {
       h = hfold(h, m.commit);
       h = hfold(h, m.hint);
       h = hfold(h, m.hint_high);
-      if (m.n_ent) {
-        const Ent* a = &P.arena[par][r * C.ecap + m.ent_off];
-        for (u32 i = 0; i < m.n_ent; i++) {
+      if (ne) {
+        const Ent* a = msg_ents(P, C, par, r, m);
+        for (u32 i = 0; i < ne; i++) {
           Ent e = a[i];
           u64 idx = m.type == M_Replicate ? m.log_index + 1 + i : 0;
           h = hfold(h, idx);
@@ -882,7 +976,14 @@ struct Lane {
     const u32 pc = get_pc(d);
     u32 a = pc & 0x7Fu, b = (pc >> 7) & 0x7Fu;
     if (a + b >= C.maxm) {
-      set_fault(F_OUTBOX);
+      // the plane list is full: the message joins the step's stash, and the
+      // list moves whole to the spill heap at the step's end (outbox_relocate)
+      if (stash_put(P, C, par, X().ost, m)) {
+        ctr.v[C_MSG_OUT]++;
+        ctr.v[C_ENT_OUT] += ne;
+      } else {
+        set_fault(F_NOMEM);
+      }
       return;
     }
     u32 slot;
@@ -895,7 +996,7 @@ struct Lane {
     }
     const u64 at = msg_slot_base(k, d) + slot;
     ctr.v[C_MSG_OUT]++;
-    ctr.v[C_ENT_OUT] += m.n_ent;
+    ctr.v[C_ENT_OUT] += ne;
     P.msgs[par][at] = m;
   }
   RBE_HD Msg mk(u32 type, u8 to) const {
@@ -911,8 +1012,8 @@ struct Lane {
     m.term = m.log_term = m.log_index = m.commit = m.hint = m.hint_high = 0;
     return m;
   }
-  // log entries [lo, lo + cnt) from the ring to `out`, kEntBatch at a time
-  // (every load of a batch before its stores)
+  // log entries [lo, lo + cnt) from the ring (or the cold log below it) to
+  // `out`, kEntBatch at a time (every load of a batch before its stores)
   RBE_HD void copy_ring_to_arena(u64 lo, u32 cnt, Ent* out) {
     for (u32 i0 = 0; i0 < cnt; i0 += kEntBatch) {
       Ent e[kEntBatch];
@@ -920,7 +1021,10 @@ struct Lane {
       for (u32 j = 0; j < kEntBatch; j++) {
         if (i0 + j >= cnt) continue;
         const u64 idx = lo + i0 + j;
-        if (last - idx >= C.ring) set_fault(F_WINDOW);
+        if (last - idx >= C.ring) {
+          e[j] = log_ent(idx);
+          continue;
+        }
         const u64 s = ring_slot(idx);
         const Body b = P.pay_ring[s];
         e[j].term = P.term_ring[s];
@@ -937,54 +1041,79 @@ struct Lane {
       }
     }
   }
+  // cnt entries of the round spill heap for a message whose entries do not
+  // fit the sender's arena (granule in *off), ~0 when the heap is full
+  RBE_HD Ent* spill_ents(u32 cnt, u32* off) {
+    const u64 g = spill_alloc(P, C, par, (u64)cnt * sizeof(Ent));
+    if (g == ~0ull) {
+      set_fault(F_NOMEM);
+      return nullptr;
+    }
+    *off = (u32)g;
+    return spill_at<Ent>(P, par, g);
+  }
   // copy log entries [lo, lo+cnt) into this round's arena (reusing the last
-  // copied segment when it already covers them); returns the arena offset
-  RBE_HD bool arena_log_range(u64 lo, u32 cnt, u32* off) {
+  // copied segment when it already covers them), or into the round spill heap
+  // when the arena cannot take them (*x): makeReplicateMessage's entries,
+  // limited only by MaxEntrySize (raft.go:709-740)
+  RBE_HD bool arena_log_range(u64 lo, u32 cnt, u32* off, bool* x) {
     if (seg_len && lo >= seg_lo && lo + cnt <= seg_lo + seg_len) {
-      *off = seg_off + (u32)(lo - seg_lo);
+      *off = seg_off + (u32)(lo - seg_lo) * (seg_x ? 2u : 1u);
+      *x = seg_x;
       return true;
     }
     Ent* a = &P.arena[par][r * C.ecap];
-    if (seg_len && lo >= seg_lo && lo <= seg_lo + seg_len && seg_off + seg_len == arena_used) {
+    if (!seg_x && seg_len && lo >= seg_lo && lo <= seg_lo + seg_len &&
+        seg_off + seg_len == arena_used) {
       u64 have_hi = seg_lo + seg_len;  // exclusive
       u32 extra = (u32)(lo + cnt - have_hi);
-      if (arena_used + extra > C.ecap) {
-        set_fault(F_ARENA);
-        return false;
+      if (arena_used + extra <= C.ecap) {
+        copy_ring_to_arena(have_hi, extra, a + arena_used);
+        ctr.v[C_RING_ACCESS] += extra;
+        arena_used += extra;
+        seg_len += extra;
+        *off = seg_off + (u32)(lo - seg_lo);
+        *x = false;
+        return true;
       }
-      copy_ring_to_arena(have_hi, extra, a + arena_used);
-      ctr.v[C_RING_ACCESS] += extra;
-      arena_used += extra;
-      seg_len += extra;
-      *off = seg_off + (u32)(lo - seg_lo);
-      return true;
     }
-    if (arena_used + cnt > C.ecap) {
-      set_fault(F_ARENA);
-      return false;
+    Ent* dst = nullptr;
+    u32 o = arena_used;
+    const bool sx = arena_used + cnt > C.ecap;
+    if (sx) {
+      if (!(dst = spill_ents(cnt, &o))) return false;
+    } else {
+      dst = a + arena_used;
+      arena_used += cnt;
     }
-    copy_ring_to_arena(lo, cnt, a + arena_used);
+    copy_ring_to_arena(lo, cnt, dst);
     ctr.v[C_RING_ACCESS] += cnt;
     seg_lo = lo;
-    seg_off = arena_used;
+    seg_off = o;
     seg_len = cnt;
-    *off = arena_used;
-    arena_used += cnt;
+    seg_x = sx;
+    *off = o;
+    *x = sx;
     return true;
   }
   // entries [lo, lo+cnt) for a witness (makeMetadataEntries, raft.go:742-756):
   // a copy of their own in the arena where every entry but a ConfigChange is a
   // MetadataEntry with only its index and term
-  RBE_HD bool arena_meta_range(u64 lo, u32 cnt, u32* off) {
+  RBE_HD bool arena_meta_range(u64 lo, u32 cnt, u32* off, bool* x) {
     if (mseg_len && lo >= mseg_lo && lo + cnt <= mseg_lo + mseg_len) {
-      *off = mseg_off + (u32)(lo - mseg_lo);
+      *off = mseg_off + (u32)(lo - mseg_lo) * (mseg_x ? 2u : 1u);
+      *x = mseg_x;
       return true;
     }
-    if (arena_used + cnt > C.ecap) {
-      set_fault(F_ARENA);
-      return false;
+    Ent* a = nullptr;
+    u32 o = arena_used;
+    const bool sx = arena_used + cnt > C.ecap;
+    if (sx) {
+      if (!(a = spill_ents(cnt, &o))) return false;
+    } else {
+      a = &P.arena[par][r * C.ecap + arena_used];
+      arena_used += cnt;
     }
-    Ent* a = &P.arena[par][r * C.ecap + arena_used];
     copy_ring_to_arena(lo, cnt, a);
     ctr.v[C_RING_ACCESS] += cnt;
     for (u32 i = 0; i < cnt; i++)
@@ -994,35 +1123,70 @@ struct Lane {
         a[i].lo = a[i].hi = 0;
       }
     mseg_lo = lo;
-    mseg_off = arena_used;
+    mseg_off = o;
     mseg_len = cnt;
-    *off = arena_used;
-    arena_used += cnt;
+    mseg_x = sx;
+    *off = o;
+    *x = sx;
     return true;
   }
-  RBE_HD bool arena_put(const Ent* src, u32 cnt, u32* off) {
-    if (arena_used + cnt > C.ecap) {
-      set_fault(F_ARENA);
-      return false;
+  // entries of a Propose this step sends or hands to its own handler; the
+  // pointer it can read them from (null when the spill heap is exhausted)
+  RBE_HD const Ent* arena_put(const Ent* src, u32 cnt, u32* off, bool* x) {
+    Ent* a = nullptr;
+    *x = arena_used + cnt > C.ecap;
+    if (*x) {
+      if (!(a = spill_ents(cnt, off))) return nullptr;
+    } else {
+      a = &P.arena[par][r * C.ecap + arena_used];
+      *off = arena_used;
+      arena_used += cnt;
     }
-    Ent* a = &P.arena[par][r * C.ecap];
-    for (u32 i = 0; i < cnt; i++) a[arena_used + i] = src[i];
-    *off = arena_used;
-    arena_used += cnt;
-    return true;
+    for (u32 i = 0; i < cnt; i++) a[i] = src[i];
+    return a;
+  }
+  // a message's entry reference: the arena offset, or the spill heap
+  RBE_HD static void set_ents(Msg& m, u32 cnt, u32 off, bool x) {
+    m.n_ent = (u16)(cnt > 0xFFFFu ? 0xFFFFu : cnt);
+    m.ent_off = off;
+    if (x) {
+      m.pad0 |= kMsgXEnt;
+      m.pad1 = cnt;
+    }
   }
 
   // ------------------------------------------------------------- outputs
-  RBE_HD void add_ready_to_read(u64 index, u64 low, u64 high) {  // raft.go:1624-1630
-    if (n_rtr >= C.rtr_cap) {
-      set_fault(F_RTR);
-      return;
+  // The step's ReadyToReads / dropped ReadIndexes: the plane list, then, past
+  // its capacity, the whole list in the round spill heap (rtr_x / dri_x, its
+  // granule; the plane's slot 0 names it at the step's end)
+  template <class T>
+  RBE_HD bool out_list_put(T* plane, u32 pcap, u32 n, u64& xg, u32& xcap, const T& v) {
+    if (n < pcap) {
+      plane[n] = v;
+      return true;
     }
+    if (n >= xcap) {  // (re)allocate at twice the size and copy what is there
+      const u32 cap = n * 2u;
+      const u64 g = spill_alloc(P, C, par, (u64)cap * sizeof(T));
+      if (g == ~0ull) return false;
+      T* nb = spill_at<T>(P, par, g);
+      const T* ob = xcap ? spill_at<T>(P, par, xg) : plane;
+      for (u32 i = 0; i < n; i++) nb[i] = ob[i];
+      xg = g;
+      xcap = cap;
+    }
+    spill_at<T>(P, par, xg)[n] = v;
+    return true;
+  }
+  RBE_HD void add_ready_to_read(u64 index, u64 low, u64 high) {  // raft.go:1624-1630
     RTR x;
     x.index = index;
     x.low = low;
     x.high = high;
-    P.rtr[r * C.rtr_cap + n_rtr] = x;
+    if (!out_list_put(&P.rtr[r * C.rtr_cap], C.rtr_cap, n_rtr, X().rtr_x, X().rtr_xcap, x)) {
+      set_fault(F_NOMEM);
+      return;
+    }
     n_rtr++;
     if (TRACE) {
       rtr_hash = hfold(rtr_hash, index);
@@ -1031,14 +1195,13 @@ struct Lane {
     }
   }
   RBE_HD void add_dropped_ri(u64 low, u64 high) {
-    if (n_drop_ri >= C.dri_cap) {
-      set_fault(F_DROPLIST);
-      return;
-    }
     DropRI x;
     x.low = low;
     x.high = high;
-    P.dri[r * C.dri_cap + n_drop_ri] = x;
+    if (!out_list_put(&P.dri[r * C.dri_cap], C.dri_cap, n_drop_ri, X().dri_x, X().dri_xcap, x)) {
+      set_fault(F_NOMEM);
+      return;
+    }
     n_drop_ri++;
   }
   RBE_HD void report_dropped_read_index(u64 low, u64 high) {  // raft.go:1999-2012
@@ -1081,7 +1244,7 @@ struct Lane {
     etick = 0;
     htick = 0;
     set_randomized_election_timeout();
-    rq_head = rq_count = 0;
+    rq_clear();
     flags &= (u8)~HF_PENDING_CC;
     ltt = 0;
     reset_remotes();
@@ -1111,13 +1274,8 @@ struct Lane {
     // preLeaderPromotionHandleConfigChange (raft.go:1010-1018): count config
     // change entries in (committed, last]
     u32 ncc = 0;
-    for (u64 i = committed + 1; i <= last; i++) {
-      if (last - i >= C.ring) {
-        set_fault(F_WINDOW);
-        break;
-      }
-      if (ent_type(P.pay_ring[ring_slot(i)].type) == E_ConfigChange) ncc++;
-    }
+    for (u64 i = committed + 1; i <= last; i++)
+      if (ent_type(log_body(i).type) == E_ConfigChange) ncc++;
     if (ncc > 1) set_fault(F_PANIC);
     else if (ncc == 1) flags |= HF_PENDING_CC;
     // p72 of the raft thesis: an empty entry at the new term
@@ -1128,7 +1286,7 @@ struct Lane {
   RBE_HD void append_entry(u32 type, u32 len, u64 lo, u64 hi) {
     u64 idx = last + 1;
     rl_grow(len);
-    ring_put(idx, term, type, len, lo, hi);
+    log_append(idx, term, type, len, lo, hi);
     last = idx;
     t_last = term;
     try_update(k, last);
@@ -1146,13 +1304,7 @@ struct Lane {
   // while last - i < ring; F_WINDOW otherwise)
   RBE_HD u64 rl_range(u64 lo, u64 hi, u64 base) {
     u64 s = 0;
-    for (u64 i = lo; i <= hi && i >= lo; i++) {
-      if (last - i >= C.ring) {
-        set_fault(F_WINDOW);
-        break;
-      }
-      s += base + P.pay_ring[ring_slot(i)].len;
-    }
+    for (u64 i = lo; i <= hi && i >= lo; i++) s += base + log_body(i).len;
     return s;
   }
   // inMemory.merge (inmemory.go:201-234) of entries from `first` on, before
@@ -1381,12 +1533,10 @@ struct Lane {
     if (next <= last) {
       u64 cnt = limit_count(next, last);
       u32 off = 0;
-      const bool ok = ((wit >> slot) & 1u) ? arena_meta_range(next, (u32)cnt, &off)
-                                           : arena_log_range(next, (u32)cnt, &off);
-      if (ok) {
-        m.n_ent = (u16)cnt;
-        m.ent_off = off;
-      }
+      bool x = false;
+      const bool ok = ((wit >> slot) & 1u) ? arena_meta_range(next, (u32)cnt, &off, &x)
+                                           : arena_log_range(next, (u32)cnt, &off, &x);
+      if (ok) set_ents(m, (u32)cnt, off, x);
       progress(slot, next + cnt - 1);
     }
     send(m);
@@ -1410,8 +1560,8 @@ struct Lane {
     hb_hi = high;
   }
   RBE_HD void broadcast_heartbeat() {  // raft.go:824-832
-    if (rq_count > 0) {
-      const ReadReq& q = *rq_at(rq_count - 1u);
+    if (rq_len() > 0) {
+      const ReadReq& q = *rq_at(rq_len() - 1u);
       broadcast_heartbeat_with_hint(q.low, q.high);
     } else {
       broadcast_heartbeat_with_hint(0, 0);
@@ -1419,18 +1569,94 @@ struct Lane {
   }
 
   // ------------------------------------------------------------- readIndex (kernel 4)
+  // The queue (readindex.go:24-34, unbounded) is the plane ring of rq_cap
+  // entries (rq_head, rq_count) until it would overflow; then it moves whole
+  // into pool pages (rqx, rqd; rbe_spill.h) and returns when it drains.
   RBE_HD u32 rq_wrap(u32 x) const { return x >= C.rq_cap ? x - C.rq_cap : x; }  // x < 2*cap
-  RBE_HD ReadReq* rq_at(u32 i) { return &P.rq[r * C.rq_cap + rq_wrap((u32)rq_head + i)]; }
-  RBE_HD void rq_add(u64 index, u64 low, u64 high, u8 from) {  // readindex.go:43-67
+  RBE_HD u32 rq_len() const { return X().rqx ? X().rqd.n : (u32)rq_count; }
+  RBE_HD ReadReq* rq_at(u32 i) {
+    if (X().rqx) return rq_ext_at(P, X().rqd, i);
+    return &P.rq[r * C.rq_cap + rq_wrap((u32)rq_head + i)];
+  }
+  // the queue of a full ring into pool pages; false when the pool is exhausted
+  RBE_HD bool rq_extend() {
+    RqExt x;
+    x.head = x.tail = pool_alloc(P, C, par);
+    if (!x.head) return false;
+    P.pmeta[x.head].next = 0;
+    x.off = 0;
+    x.n = 0;
     for (u32 i = 0; i < rq_count; i++) {
+      if (i > 0 && i % kPageEnts == 0) {
+        const u32 p = pool_alloc(P, C, par);
+        if (!p) {
+          rq_ext_free(P, x, par);
+          return false;
+        }
+        P.pmeta[p].next = 0;
+        P.pmeta[x.tail].next = p;
+        x.tail = p;
+      }
+      *(ReadReq*)pool_ent(P, x.tail, i % kPageEnts) = P.rq[r * C.rq_cap + rq_wrap((u32)rq_head + i)];
+      x.n++;
+    }
+    X().rqd = x;
+    X().rqx = true;
+    rq_head = 0;
+    return true;
+  }
+  RBE_HD bool rq_push(const ReadReq& q) {
+    if (!X().rqx && rq_count < C.rq_cap) {
+      *rq_at(rq_count) = q;
+      rq_count++;
+      return true;
+    }
+    if (!X().rqx && !rq_extend()) return false;
+    const u32 pos = X().rqd.off + X().rqd.n;
+    if (pos % kPageEnts == 0) {  // the tail page is full
+      const u32 p = pool_alloc(P, C, par);
+      if (!p) return false;
+      P.pmeta[p].next = 0;
+      P.pmeta[X().rqd.tail].next = p;
+      X().rqd.tail = p;
+    }
+    *(ReadReq*)pool_ent(P, X().rqd.tail, pos % kPageEnts) = q;
+    X().rqd.n++;
+    return true;
+  }
+  RBE_HD void rq_pop(u32 done) {
+    if (!X().rqx) {
+      rq_head = (u8)rq_wrap((u32)rq_head + done);
+      rq_count = (u8)(rq_count - done);
+      return;
+    }
+    X().rqd.n -= done;
+    X().rqd.off += done;
+    if (X().rqd.n == 0) {  // drained: back to the plane ring
+      rq_ext_free(P, X().rqd, par);
+      X().rqx = false;
+      rq_head = rq_count = 0;
+      return;
+    }
+    while (X().rqd.off >= kPageEnts) {
+      const u32 nx = P.pmeta[X().rqd.head].next;
+      pool_free(P, par, X().rqd.head);
+      X().rqd.head = nx;
+      X().rqd.off -= kPageEnts;
+    }
+  }
+  RBE_HD void rq_clear() {
+    if (X().rqx) rq_ext_free(P, X().rqd, par);
+    X().rqx = false;
+    rq_head = rq_count = 0;
+  }
+  RBE_HD void rq_add(u64 index, u64 low, u64 high, u8 from) {  // readindex.go:43-67
+    const u32 n = rq_len();
+    for (u32 i = 0; i < n; i++) {
       ReadReq* q = rq_at(i);
       if (q->low == low && q->high == high) return;
     }
-    if (rq_count > 0 && index < rq_at(rq_count - 1)->index) set_fault(F_PANIC);
-    if (rq_count >= C.rq_cap) {
-      set_fault(F_READQ);
-      return;
-    }
+    if (n > 0 && index < rq_at(n - 1)->index) set_fault(F_PANIC);
     ReadReq q;
     q.low = low;
     q.high = high;
@@ -1438,15 +1664,18 @@ struct Lane {
     q.from = from;
     q.confirmed = 0;
     for (int i = 0; i < 6; i++) q.pad[i] = 0;
-    *rq_at(rq_count) = q;
-    rq_count++;
+    if (!rq_push(q)) {
+      set_fault(F_NOMEM);
+      return;
+    }
     ctr.v[C_RQ_TOUCH]++;
   }
   // readIndex.confirm (readindex.go:77-116) + handleReadIndexLeaderConfirmation
   // (raft.go:1736-1756)
   RBE_HD void rq_confirm(u64 low, u64 high, u8 from, u64 m_hint, u64 m_hint_high) {
     int pos = -1;
-    for (u32 i = 0; i < rq_count; i++) {
+    const u32 n = rq_len();
+    for (u32 i = 0; i < n; i++) {
       ReadReq* q = rq_at(i);
       if (q->low == low && q->high == high) {
         pos = (int)i;
@@ -1474,8 +1703,7 @@ struct Lane {
       }
     }
     ctr.v[C_RQ_TOUCH] += done;
-    rq_head = (u8)rq_wrap((u32)rq_head + done);
-    rq_count = (u8)(rq_count - done);
+    rq_pop(done);
   }
 
   // ------------------------------------------------------------- leader handlers
@@ -1515,7 +1743,7 @@ struct Lane {
       }
       note_cc(e.type);
       rl_grow(e.len);
-      ring_put(idx, term, e.type, e.len, e.lo, e.hi);
+      log_append(idx, term, e.type, e.len, e.lo, e.hi);
       last = idx;
       t_last = term;
     }
@@ -1596,6 +1824,68 @@ struct Lane {
   }
 
   // ------------------------------------------------------------- follower side (kernel 2)
+  // inMemory.merge's log side (inmemory.go:201-234) for the entries src[0,
+  // cnt) at indexes [c, c + cnt), c <= last + 1: they replace everything from c
+  // on.  The ring invariant holds after it: the window entries the old tail
+  // had overwritten come back from the cold log, the old entries the new ones
+  // overwrite go to it, and new entries below the new window go straight there.
+  RBE_HD void log_merge(u64 c, const Ent* src, u32 cnt) {
+    const u64 L0 = last, nl = c + cnt - 1, R = C.ring;
+    const u64 wlo = nl >= R ? nl - R + 1 : 1;  // the new window (before the marker)
+    const u64 rs = c > wlo ? c : wlo;          // the first entry the ring takes
+    // 1. the old window's live entries below c that leave the window go to
+    // the cold log before the ring writes below overwrite their slots (the
+    // new entries of [rs, nl] cover the slots of every one of them)
+    {
+      u64 j = umax64(umax64(marker + 1, L0 >= R ? L0 - R + 1 : 1), 1);
+      const u64 je = umin64(umin64(L0, c - 1), wlo - 1);
+      for (; j <= je; j++) evict(j);
+    }
+    // 2. new entries below the new window
+    for (u64 i = c; i < rs; i++) {
+      if (i > marker) cold_store(i, src[i - c]);
+      note_cc(src[i - c].type);
+      ctr.v[C_RING_ACCESS]++;
+    }
+    // 3. the ring's entries, batched: a batch's entries are loaded before any
+    // ring store, so no load waits behind the stores of earlier entries (vmcnt
+    // is in order)
+    for (u64 i0 = rs; i0 <= nl; i0 += kEntBatch) {
+      Ent e[kEntBatch];
+#pragma unroll
+      for (u32 j = 0; j < kEntBatch; j++)
+        if (i0 + j <= nl) e[j] = src[i0 + j - c];
+#pragma unroll
+      for (u32 j = 0; j < kEntBatch; j++) {
+        if (i0 + j <= nl) {
+          ring_put(i0 + j, e[j].term, e[j].type, e[j].len, e[j].lo, e[j].hi);
+          note_cc(e[j].type);
+        }
+      }
+    }
+    // 4. the window below c: slots the old tail overwrote come back
+    if (L0 > R) {
+      u64 lo = umax64(umax64(marker + 1, wlo), 1);
+      const u64 hi = umin64(c - 1, L0 - R);
+      for (; lo <= hi; lo++) {
+        Ent e;
+        if (!cold_get(P, cold(), lo, &e)) {
+          set_fault(F_WINDOW);
+          continue;
+        }
+        const u64 s = ring_slot(lo);
+        P.term_ring[s] = e.term;
+        Body b;
+        b.type = e.type;
+        b.len = e.len;
+        b.lo = e.lo;
+        b.hi = e.hi;
+        P.pay_ring[s] = b;
+      }
+    }
+    last = nl;
+    t_last = src[cnt - 1].term;
+  }
   RBE_HD void on_replicate(const Msg& m, const Ent* ents) {  // raft.go:1339-1372
     Msg resp = mk(M_ReplicateResp, m.from);
     if (m.log_index < committed) {
@@ -1603,18 +1893,19 @@ struct Lane {
       send(resp);
       return;
     }
+    const u32 ne = msg_nent(m);
     if (match_term(m.log_index, m.log_term)) {
       // tryAppend (logentry.go:291-302) / getConflictIndex (315-322)
       // The lookups go in batches of kEntBatch: all loads of a batch are
       // issued before any is used, instead of one dependent round trip per entry
       u64 conflict = 0;
       u32 ci = 0;
-      for (u32 i0 = 0; i0 < m.n_ent && conflict == 0; i0 += kEntBatch) {
+      for (u32 i0 = 0; i0 < ne && conflict == 0; i0 += kEntBatch) {
         u64 et[kEntBatch], lt[kEntBatch];
 #pragma unroll
         for (u32 j = 0; j < kEntBatch; j++) {
           et[j] = lt[j] = 0;
-          if (i0 + j < m.n_ent) {
+          if (i0 + j < ne) {
             et[j] = ents[i0 + j].term;
             lt[j] = log_term_peek(m.log_index + 1 + i0 + j);
           }
@@ -1622,10 +1913,12 @@ struct Lane {
 #pragma unroll
         for (u32 j = 0; j < kEntBatch; j++) {
           const u32 i = i0 + j;
-          if (conflict == 0 && i < m.n_ent) {
+          if (conflict == 0 && i < ne) {
             const u64 idx = m.log_index + 1 + i;
             log_term_account(idx);
-            if (lt[j] != et[j]) {
+            // an entry below the ring: the cold log (the ILogDB read path)
+            const u64 t = log_term_cold(idx) ? log_ent(idx).term : lt[j];
+            if (t != et[j]) {
               conflict = idx;
               ci = i;
             }
@@ -1640,32 +1933,14 @@ struct Lane {
           // truncate-and-append; savedTo = min(savedTo, first-1)
           if (conflict - 1 >= 1 && conflict - 1 <= last && log_term(conflict - 1) > ents[ci].term)
             set_fault(F_PANIC);
-          if (rl_on()) rl_merge(conflict, ents + ci, m.n_ent - ci);
-          // batched: a batch's entries are loaded before any ring store, so no
-          // load waits behind the stores of earlier entries (vmcnt is in order)
-          u64 tl = 0;
-          for (u32 i0 = ci; i0 < m.n_ent; i0 += kEntBatch) {
-            Ent e[kEntBatch];
-#pragma unroll
-            for (u32 j = 0; j < kEntBatch; j++)
-              if (i0 + j < m.n_ent) e[j] = ents[i0 + j];
-#pragma unroll
-            for (u32 j = 0; j < kEntBatch; j++) {
-              if (i0 + j < m.n_ent) {
-                ring_put(m.log_index + 1 + i0 + j, e[j].term, e[j].type, e[j].len, e[j].lo, e[j].hi);
-                note_cc(e[j].type);
-                tl = e[j].term;
-              }
-            }
-          }
-          last = m.log_index + m.n_ent;
-          t_last = tl;
+          if (rl_on()) rl_merge(conflict, ents + ci, ne - ci);
+          log_merge(conflict, ents + ci, ne - ci);
           saved_to = umin64(saved_to, conflict - 1);
           if (imark_on(C) && conflict <= P.imark[r]) P.imark[r] = conflict;
           seg_len = mseg_len = 0;
         }
       }
-      u64 last_idx = m.log_index + m.n_ent;
+      u64 last_idx = m.log_index + ne;
       commit_to(umin64(last_idx, m.commit));
       resp.log_index = last_idx;
     } else {
@@ -1700,6 +1975,8 @@ struct Lane {
         committed = processed = saved_to = si;
         marker = si;
         marker_term = st;
+        cold_release(P, cold(), ~0ull, par);  // the log is the snapshot now
+        X().cref_dirty = true;
         P.term_ring[ring_slot(si)] = st;  // the fast steps read Term(marker) from the ring
         SnapSt& sp = P.snp[r];
         sp.ss_index = si;  // LogDB.ApplySnapshot (after the step's Update)
@@ -1940,12 +2217,14 @@ struct Lane {
         switch (m.type) {
           case M_Propose:  // raft.go:1841-1853
             if (leader == 0) {
-              report_dropped_proposal(ents, m.n_ent);
+              report_dropped_proposal(ents, msg_nent(m));
             } else {
               Msg f = m;
               f.to = leader;
               u32 off = 0;
-              if (m.n_ent && arena_put(ents, m.n_ent, &off)) f.ent_off = off;
+              bool x = false;
+              const u32 ne = msg_nent(m);
+              if (ne && arena_put(ents, ne, &off, &x)) set_ents(f, ne, off, x);
               send(f);
             }
             return;
@@ -1998,7 +2277,7 @@ struct Lane {
             become_follower(term, m.from);
             on_heartbeat(m);
             return;
-          case M_Propose: report_dropped_proposal(ents, m.n_ent); return;  // 1928-1931
+          case M_Propose: report_dropped_proposal(ents, msg_nent(m)); return;  // 1928-1931
           case M_ReadIndex:  // raft.go:1933-1941 (reported twice, as in the reference)
             report_dropped_read_index(m.hint, m.hint_high);
             add_dropped_ri(m.hint, m.hint_high);
@@ -2020,7 +2299,7 @@ struct Lane {
         }
       case R_Leader:
         switch (m.type) {
-          case M_Propose: on_leader_propose(ents, m.n_ent); return;
+          case M_Propose: on_leader_propose(ents, msg_nent(m)); return;
           case M_ReadIndex: on_leader_read_index(m.hint, m.hint_high, m.from); return;
           // lw (raft.go:2013-2035): the remote of m.From, or nothing when
           // it is not a member of this replica's view
@@ -2078,12 +2357,14 @@ struct Lane {
             return;
           case M_Propose:  // handleObserverPropose
             if (leader == 0) {
-              report_dropped_proposal(ents, m.n_ent);
+              report_dropped_proposal(ents, msg_nent(m));
             } else {
               Msg f = m;
               f.to = leader;
               u32 off = 0;
-              if (m.n_ent && arena_put(ents, m.n_ent, &off)) f.ent_off = off;
+              bool x = false;
+              const u32 ne = msg_nent(m);
+              if (ne && arena_put(ents, ne, &off, &x)) set_ents(f, ne, off, x);
               send(f);
             }
             return;
@@ -2165,7 +2446,7 @@ struct Lane {
     }
     if constexpr (LEAD) {
       switch (m.type) {
-        case M_Propose: on_leader_propose(ents, m.n_ent); return;
+        case M_Propose: on_leader_propose(ents, msg_nent(m)); return;
         case M_ReadIndex: on_leader_read_index(m.hint, m.hint_high, m.from); return;
         case M_ReplicateResp: on_replicate_resp(m, m.from - 1u); return;
         case M_HeartbeatResp: on_heartbeat_resp(m, m.from - 1u); return;
@@ -2192,11 +2473,12 @@ struct Lane {
       for (u32 s = 0; s < N; s++) {
         if (s == k) continue;
         const u32 pc = in_word<N>(P, g, s, k, round);
-        const u32 na = pc & 0x7Fu, n = na + ((pc >> 7) & 0x7Fu);
+        if (pc & kCntSpill) return false;  // a spilled list: the full handler table
+        const ListView lv = list_view(P, C, ppar, (g * N + s) * N + k, pc);
+        const u32 n = lv.n();
         n_in += n;
-        const Msg* lst = &P.msgs[ppar][msg_slot_base(s, k)];
         for (u32 i = 0; i < n; i++) {
-          const Msg* mp = i < na ? &lst[i] : &lst[C.maxm - 1u - (i - na)];
+          const Msg* mp = &lv.at(i);
           const u32 t = mp->type;
           const u64 mt = mp->term;
           if (role == R_Follower) {
@@ -2209,8 +2491,7 @@ struct Lane {
             } else if (t == M_Propose || t == M_ReadIndex) {
               if (mt != 0) return false;
               if (t == M_Propose &&
-                  ent_type(P.arena[ppar][(g * N + s) * (u64)C.ecap + mp->ent_off].type) ==
-                      E_ConfigChange)
+                  ent_type(msg_ents(P, C, ppar, g * N + s, *mp)->type) == E_ConfigChange)
                 return false;
             } else {
               return false;
@@ -2258,8 +2539,7 @@ struct Lane {
       u32 ms = pack_ms(members & MB_REMOVED, obs, wit);  // raft's, as accepted changes go by
       u32 ncc = 0;
       for (u64 i = u.apply_lo; i <= u.apply_hi; i++) {
-        if (last - i >= C.ring) break;  // F_WINDOW already raised by the apply
-        const Body b = P.pay_ring[ring_slot(i)];
+        const Body b = log_body(i);
         if (ent_type(b.type) != E_ConfigChange) continue;
         u32 t;
         u64 nid;
@@ -2288,8 +2568,7 @@ struct Lane {
     if (mfl & MB_CC_IN_LOG) {
       bool any = false;
       for (u64 i = processed + 1; i <= last && !any; i++)
-        if (last - i < C.ring && ent_type(P.pay_ring[ring_slot(i)].type) == E_ConfigChange)
-          any = true;
+        if (ent_type(log_body(i).type) == E_ConfigChange) any = true;
       if (!any) mfl &= (u8)~MB_CC_IN_LOG;
     }
   }
@@ -2325,6 +2604,8 @@ struct Lane {
       if (c > marker && c <= last && c <= sp.ss_index) {
         sp.marker_term = log_term(c);
         sp.marker = c;
+        cold_release(P, cold(), c, par);  // the cold log's pages at or below it
+        X().cref_dirty = true;
       }
       sp.compact_to = 0;
     }
@@ -2383,6 +2664,9 @@ struct Lane {
     ltt = c.ltt;
     rq_head = c.rq_head;
     rq_count = c.rq_count;
+    X().rqx = rq_count == kRqExt;  // the queue lives in pool pages (rbe_spill.h)
+    if (X().rqx) X().rqd = rq_ext_load(P, C, r);
+    X().cref_ld = X().cref_dirty = false;
     members = c.members;
     cc_apply = c.cc_apply;
     cc_acc = 0;
@@ -2422,7 +2706,9 @@ struct Lane {
     c.leader = leader;
     c.ltt = ltt;
     c.rq_head = rq_head;
-    c.rq_count = rq_count;
+    c.rq_count = X().rqx ? kRqExt : rq_count;
+    if (X().rqx) rq_ext_store(P, C, r, X().rqd);
+    if (X().cref_dirty) P.cold[r] = X().cref;
     // MB_ROLES: the replica has observers or witnesses (Planes::roles)
     mfl = (u8)((mfl & ~MB_ROLES) | ((obs | wit) ? MB_ROLES : 0u));
     if (C.membership && (roles0 || (obs | wit))) P.roles[r] = (u16)(obs | ((u16)wit << 8));
@@ -2504,6 +2790,10 @@ struct Lane {
     seg_off = seg_len = 0;
     mseg_lo = 0;
     mseg_off = mseg_len = 0;
+    seg_x = mseg_x = false;
+    stash_init(X().ost);
+    X().rtr_x = X().dri_x = 0;
+    X().rtr_xcap = X().dri_xcap = 0;
     msg_hash = rtr_hash = drop_hash = 0;
     n_msgs = n_rtr = n_drop_ent = n_drop_ri = 0;
     q_new = false;
@@ -2624,7 +2914,10 @@ struct Lane {
     //   handleProposals (node.go:1091-1106) → Peer.ProposeEntries
     //   handleLeaderTransferRequest (node.go:1069-1075) → Peer.RequestLeaderTransfer
     const u32 ppar = par ^ 1u;
-    u32 cs = 0, ci = 0, cn = 0, cna = 0;  // inbox cursor: sender, index, count, #A
+    u32 cs = 0, ci = 0, cn = 0;  // inbox cursor: sender, index, count
+    ListView cview;              // the sender's list (rbe_spill.h)
+    cview.base = nullptr;
+    cview.cap = cview.na = cview.nb = 0;
     bool copen = false;
     const u32 phase0 = (unreach | snap_nodes) ? 0u : (round > 0 ? 1u : 2u);
     // calls the node makes under raftMu between two steps come first:
@@ -2669,8 +2962,9 @@ struct Lane {
           cc_scan = true;
         }
 #pragma unroll 1
-        while (kind == 0 && cc_i <= cc_e && last - cc_i < C.ring) {
-          const Body b = P.pay_ring[ring_slot(cc_i++)];
+        // (membership_after_update evaluated at most 32 of them: Upd::cc_acc)
+        while (kind == 0 && cc_i <= cc_e && cc_i <= last && cc_n < 32) {
+          const Body b = log_body(cc_i++);
           u32 t;
           u64 nid;
           if (ent_type(b.type) != E_ConfigChange || !cc_decode(b, &t, &nid)) continue;
@@ -2745,15 +3039,14 @@ struct Lane {
               ctr.v[C_MSG_IN]++;
               q_try_enter();
             }
-            cna = pc & 0x7Fu;
-            cn = cna + ((pc >> 7) & 0x7Fu);
+            cview = list_view(P, C, ppar, (g * N + cs) * N + k, pc);
+            cn = cview.n();
             ci = 0;
             copen = true;
           }
           if (ci < cn) {
-            const Msg* lst = &P.msgs[ppar][msg_slot_base(cs, k)];
-            m = ci < cna ? lst[ci] : lst[C.maxm - 1u - (ci - cna)];
-            ents = &P.arena[ppar][(g * N + cs) * (u64)C.ecap + m.ent_off];
+            m = cview.at(ci);
+            ents = msg_ents(P, C, ppar, g * N + cs, m);
             ci++;
             kind = 1;
             break;
@@ -2788,11 +3081,12 @@ struct Lane {
         e.lo = cc_word(cc_type, cc_node);
         e.hi = 0;
         u32 off = 0;
-        if (arena_put(&e, 1, &off)) {
+        bool x = false;
+        if (const Ent* a = arena_put(&e, 1, &off, &x)) {
           m = mk(M_Propose, 0);
           m.from = self;
           m.n_ent = 1;
-          ents = &P.arena[par][r * (u64)C.ecap + off];
+          ents = a;
           kind = 2;
         }
       }
@@ -2809,8 +3103,9 @@ struct Lane {
             e.lo = wl_payload_lo(C.seed, cid, round);
             e.hi = mix64(e.lo);
             u32 off = 0;
-            if (arena_put(&e, 1, &off)) {
-              prop_ents = &P.arena[par][r * (u64)C.ecap + off];
+            bool x = false;
+            if (const Ent* a = arena_put(&e, 1, &off, &x)) {
+              prop_ents = a;
               prop_n = 1;
             }
           }
@@ -2848,7 +3143,7 @@ struct Lane {
         bool deliver = true;
         if (kind == 1) {
           ctr.v[C_MSG_IN]++;
-          ctr.v[C_ENT_IN] += m.n_ent;
+          ctr.v[C_ENT_IN] += msg_nent(m);
           // tryRecordNodeActivity (node.go:1161-1169)
           if ((m.type == M_Heartbeat || m.type == M_HeartbeatResp) && m.hint > 0)
             q_record_activity(M_ReadIndex);
@@ -2923,6 +3218,29 @@ struct Lane {
         ctr.v[C_MSG_OUT]++;
       }
     }
+    // this round's outbox header: the count word of every destination list;
+    // a list with stashed messages moves whole to the spill heap (rbe_spill.h)
+    if (X().ost.n) {
+      const u32 f = outbox_relocate(P, C, par, r, N, X().ost, pc_lo, pc_hi);
+      if (f) set_fault(f);
+    }
+    u32 ow[N];
+    for (u32 dd = 0; dd < N; dd++) ow[dd] = get_pc(dd);
+    // the ReadyToReads / dropped ReadIndexes that moved to the spill heap:
+    // the plane's slot 0 names their block
+    if (n_rtr > C.rtr_cap) {
+      RTR h;
+      h.index = X().rtr_x;
+      h.low = X().rtr_xcap;
+      h.high = 0;
+      P.rtr[r * C.rtr_cap] = h;
+    }
+    if (n_drop_ri > C.dri_cap) {
+      DropRI h;
+      h.low = X().dri_x;
+      h.high = X().dri_xcap;
+      P.dri[r * C.dri_cap] = h;
+    }
     // getUpdate / Commit (peer.go:201-293): the harness persists and applies
     // everything at once, so savedTo := lastIndex and processed := committed.
     Upd u;
@@ -2943,17 +3261,12 @@ struct Lane {
     u64 apply_hash = 0;
     if (C.trace && u.apply_hi >= u.apply_lo) {
       for (u64 i = u.apply_lo; i <= u.apply_hi; i++) {
-        if (last - i >= C.ring) {
-          set_fault(F_WINDOW);
-          break;
-        }
-        u64 s = ring_slot(i);
-        Body b = P.pay_ring[s];
+        const Ent e = log_ent(i);
         apply_hash = hfold(apply_hash, i);
-        apply_hash = hfold(apply_hash, P.term_ring[s]);
-        apply_hash = hfold(apply_hash, ent_word(b.type, b.len));
-        apply_hash = hfold(apply_hash, b.lo);
-        apply_hash = hfold(apply_hash, cmd_hi(b.type, b.hi));
+        apply_hash = hfold(apply_hash, e.term);
+        apply_hash = hfold(apply_hash, ent_word(e.type, e.len));
+        apply_hash = hfold(apply_hash, e.lo);
+        apply_hash = hfold(apply_hash, cmd_hi(e.type, e.hi));
       }
     }
     if (u.apply_hi >= u.apply_lo) ctr.v[C_ENT_APPLIED] += (u32)(u.apply_hi - u.apply_lo + 1);
@@ -2994,8 +3307,9 @@ struct Lane {
     u64 d = digest0;
     if (TRACE) {
       u64 dh = drop_hash;
+      const DropRI* dl = dri_list(P, C, r, n_drop_ri, par);
       for (u32 i = 0; i < n_drop_ri; i++) {
-        DropRI x = P.dri[r * C.dri_cap + i];
+        DropRI x = dl[i];
         dh = hfold(dh, x.low);
         dh = hfold(dh, x.high);
       }
@@ -3034,11 +3348,8 @@ struct Lane {
     u.round = round;
     u.cc_acc = cc_acc;
     P.upd[r] = u;
-    // this round's outbox header: the count word of every destination list
     {
-      u32 w[N];
-      for (u32 dd = 0; dd < N; dd++) w[dd] = get_pc(dd);
-      put_row(P, r, round, N, w);
+      put_row(P, r, round, N, ow);
     }
     store();
     return true;
@@ -3092,6 +3403,21 @@ RBE_HD bool step_replica_fast(const Planes& P, const Params& C, u64 r, Clk ck,
 }
 
 // ------------------------------------------------------------------ launch
+// A replica restarts or a new node takes its slot: its cold log and a
+// readIndex queue in pool pages go back to the pool (rbe_spill.h)
+RBE_HD void spill_replica_release(const Planes& P, const Params& C, u64 r, u32 par) {
+  ColdRef cr = P.cold[r];
+  if (cr.head) {
+    cold_release(P, cr, ~0ull, par);
+    P.cold[r] = cr;
+  }
+  Core& c = P.core[r];
+  if (c.rq_count == kRqExt) {
+    rq_ext_free(P, rq_ext_load(P, C, r), par);
+    c.rq_count = 0;
+    c.rq_head = 0;
+  }
+}
 // The voters a replica starts with, as the slots it does not count (removed
 // mask): the initial members for one of them, nobody for a slot that joins
 // later (Params::n_voters; the membership its LogDB reports before any snapshot)
@@ -3222,6 +3548,10 @@ RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, 
   const u64 self = k + 1;
   const bool faulted = P.upd[r].fault != 0;
   u8 snap_flags = 0;
+  // the old incarnation's cold log and readIndex queue pages go back to the pool
+  const u32 par = ppar ^ 1u;
+  spill_replica_release(P, C, r, par);
+  u32 sfault = 0;
   if (C.snapshot_entries) {
     SnapSt& sp = P.snp[r];
     sp.marker = marker;
@@ -3299,11 +3629,29 @@ RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, 
     P.rem[r * N + s] = x;
     P.rem_st[r * N + s] = 0;
   }
+  // the LogDB's entries: the in-memory window in the ring, the older ones in
+  // the cold log (rbe_spill.h)
+  ColdRef cr = P.cold[r];
   for (u32 i = 0; i < n; i++) {
     const u64 idx = last - n + 1 + i;
+    if (last - idx >= C.ring) {
+      Ent e;
+      e.term = t[i];
+      e.type = b[i].type;
+      e.len = b[i].len;
+      e.lo = b[i].lo;
+      e.hi = b[i].hi;
+      if (!cold_put(P, C, cr, idx, e, par)) sfault |= F_NOMEM;
+      continue;
+    }
     const u64 slot = (idx & (u64)(C.ring - 1)) * C.n_rep + r;
     P.term_ring[slot] = t[i];
     P.pay_ring[slot] = b[i];
+  }
+  P.cold[r] = cr;
+  if (sfault) {
+    P.upd[r].fault |= sfault;
+    P.hot[r].flags |= HF_FAULTED;
   }
   // messages in flight: none from this replica, none to it
   P.cnt[ppar][r].stamp = 0;
@@ -3321,6 +3669,7 @@ RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, 
 // slot_referenced), and its Update record starts over.
 template <int N>
 RBE_HD void join_replica(const Planes& P, const Params& C, u64 r, u32 ppar, u32 tclk) {
+  spill_replica_release(P, C, r, ppar ^ 1u);  // the removed node's pages
   launch_replica<N>(P, C, r, true);
   Hot& h = P.hot[r];
   const u32 q0 = C.quiesce ? tclk : 0u;
@@ -3355,8 +3704,9 @@ RBE_HD bool slot_referenced(const Planes& P, const Params& C, u64 g, u32 s, u32 
     if (c.vote == id || c.leader == id || c.ltt == id) return true;
     const Hot h = P.hot[r];
     if (((h.votes_resp | h.votes_granted) >> s) & 1u) return true;
-    for (u32 q = 0; q < c.rq_count; q++) {
-      const ReadReq& x = P.rq[r * C.rq_cap + (c.rq_head + q) % C.rq_cap];
+    const u32 nq = rq_length(P, C, r, c);
+    for (u32 q = 0; q < nq; q++) {
+      const ReadReq& x = *rq_entry(P, C, r, c, q);
       if (x.from == id || ((x.confirmed >> s) & 1u)) return true;
     }
     if (rl_enabled(C.rl_max) && ((P.rl[r].fmask >> s) & 1u)) return true;

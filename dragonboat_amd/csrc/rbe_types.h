@@ -47,15 +47,22 @@ static constexpr u32 kHeapHdr = 32;
 
 // sticky per-replica fault bits (the engine-side analog of plog.Panicf: the
 // replica stops being trustworthy, the engine keeps running, the host sees it)
+// Since round 6 no capacity of the planes is a fault: a full list, arena or
+// queue spills into the spill tiers (rbe_spill.h).  F_OUTBOX / F_ARENA /
+// F_READQ / F_RTR / F_DROPLIST are no longer raised; F_WINDOW means a log
+// entry the engine should hold is missing (an engine bug, or a launch that
+// handed over only the tail of a LogDB), and F_NOMEM that a spill tier
+// itself is exhausted (an engine resource: cfg.pool_bytes / spill_bytes).
 enum : u32 {
-  F_WINDOW = 1u << 0,       // term/payload ring miss (entry older than the ring window)
-  F_OUTBOX = 1u << 1,       // more than maxm messages to one destination in a round
-  F_ARENA = 1u << 2,        // per-round entry arena full
-  F_READQ = 1u << 3,        // readIndex queue full
-  F_RTR = 1u << 4,          // ReadyToRead output list full
+  F_WINDOW = 1u << 0,       // a log entry the replica holds is missing from the ring and the cold log
+  F_OUTBOX = 1u << 1,       // (unused since round 6: full lists spill)
+  F_ARENA = 1u << 2,        // (unused since round 6: full arenas spill)
+  F_READQ = 1u << 3,        // (unused since round 6: the readIndex queue grows into the pool)
+  F_RTR = 1u << 4,          // (unused since round 6: full ReadyToRead lists spill)
   F_PANIC = 1u << 5,        // a reference panic condition (e.g. commitTo > lastIndex)
   F_UNSUPPORTED = 1u << 6,  // a slow-path message/entry type reached the device
-  F_DROPLIST = 1u << 7,     // dropped-ReadIndex output list full
+  F_DROPLIST = 1u << 7,     // (unused since round 6: full dropped-ReadIndex lists spill)
+  F_NOMEM = 1u << 8,        // the page pool or the round spill heap is exhausted (engine resource)
 };
 
 // hot plane: everything a quiesced tick touches (32 B per replica)
@@ -350,6 +357,38 @@ struct Params {
   u64 n_groups_glob;  // global group count (= n_groups without compaction)
   u8 res[8];          // the n residues g % rep_world of the groups this rank touches, ascending
   u64 rl_max;         // config.MaxInMemLogSize (server.NewRateLimiter); 0 = limiter off
+  // spill tiers (rbe_spill.h)
+  u32 pool_pages;     // pages of the page pool (cold log, readIndex queue beyond rq_cap)
+  u64 spill_units;    // 16-B granules of the round spill heap, per round parity
+};
+
+// Spill tiers (rbe_spill.h).  Page pool: kPageEnts 32-B records a page (log
+// entries of the cold log, or ReadReq of a readIndex queue beyond rq_cap);
+// page 0 is the null page.  PoolMeta links a page into its owner's chain
+// (ascending page numbers), or into a free stack.
+static constexpr u32 kPageEnts = 64;
+struct alignas(16) PoolMeta {
+  u64 pn;         // cold log: the page's entries are [pn * kPageEnts, + kPageEnts)
+  u32 prev, next;
+};
+// A replica's cold log: the entries evicted from its term / payload ring, in
+// pages head .. tail (ascending pn); 0 = none
+struct alignas(16) ColdRef {
+  u32 head, tail;
+  u64 tail_pn;
+};
+// allocation words of the spill tiers, each on its own 256-B line
+struct alignas(256) SpillCtl {
+  u32 bump;          // next page never handed out (starts at 1)
+  u32 oom;           // sticky: bit 0 the page pool, bits 1-2 the round spill heap of parity 0 / 1
+  u32 live;          // pages in use
+  u32 pad0[61];
+  u32 free_head[2];  // free page stacks: a round of parity p frees into [p], takes from [p ^ 1]
+  u32 pad1[62];
+  u64 used[2];       // round spill heap granules handed out, by round parity
+  u64 pad2[30];
+  u64 peak[2];       // the largest `used` a round reached (diagnostics, rbe_spill_stats)
+  u64 pad3[30];
 };
 
 // The rate limiter of one replica (internal/server/rate.go:33-137, raft.go:204)
@@ -433,6 +472,12 @@ struct Planes {
   // diagnostic builds only (-DRBE_FULL_PROF): k_full_list's wave records
   // (rbe_debug_full_prof); null otherwise
   u64* prof;
+  // spill tiers (rbe_spill.h)
+  Ent* pool;          // [pool_pages * kPageEnts] page pool records
+  PoolMeta* pmeta;    // [pool_pages]
+  ColdRef* cold;      // [n_rep] each replica's cold log
+  u8* spill[2];       // [spill_units * 16] round spill heap, by round parity
+  SpillCtl* sctl;     // [1]
 };
 
 }  // namespace rbe

@@ -126,7 +126,7 @@ RBE_HD u32 wire_empty_snap_put(u8* o) {
 // refuses the whole encode then.
 RBE_HD u32 wire_message(const Msg& m, u32 type, u64 to, u64 from, u64 cid, const Ent* ents,
                         const u8* heap, u64 heap_cap, u64 heap_head, u8* out, u32* n_bad) {
-  const u32 ne = type == M_Replicate || type == M_Propose ? m.n_ent : 0u;
+  const u32 ne = type == M_Replicate || type == M_Propose ? msg_nent(m) : 0u;
   u32 body = 1 + wsov(type) + 1 + wsov(to) + 1 + wsov(from) + 1 + wsov(cid) + 1 + wsov(m.term) +
              1 + wsov(m.log_term) + 1 + wsov(m.log_index) + 1 + wsov(m.commit) + 2 + 1 +
              wsov(m.hint) + 1 + 1 + kWireEmptySnap + 1 + wsov(m.hint_high);
@@ -193,7 +193,6 @@ RBE_HD u32 wire_cell(const Planes& P, const Params& C, const u8* heap, u64 heap_
   const u64 r = g * N + k;
   const u64 cid = cid_of(C, g);
   const u32 pc = row_word(P.cnt[par][r], d, k, round);
-  const u32 na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
   u32 bytes = 0, nm = 0, ni = 0, bad = 0;
   // Message.To / From (and a RequestVote's / LeaderTransfer's Hint) as node ids
   const u64 to_id = ext_id(P.node_ids, N, g, d + 1), from_id = ext_id(P.node_ids, N, g, k + 1);
@@ -209,16 +208,17 @@ RBE_HD u32 wire_cell(const Planes& P, const Params& C, const u8* heap, u64 heap_
                           heap_head, out ? out + bytes : nullptr, &bad);
     nm++;
   }
-  const Msg* lst = &P.msgs[par][((g * N + k) * N + d) * (u64)C.maxm];
-  const Ent* arena = &P.arena[par][r * C.ecap];
-  for (u32 i = 0; i < na + nb; i++) {
-    Msg m = i < na ? lst[i] : lst[C.maxm - 1u - (i - na)];
+  // (the plane list or, past maxm, the spill heap's: rbe_spill.h)
+  const ListView lst = list_view(P, C, par, r * N + d, pc);
+  for (u32 i = 0; i < lst.n(); i++) {
+    Msg m = lst.at(i);
     if (m.type == M_InstallSnapshot) {
       ni++;
       continue;
     }
+    const Ent* ents = msg_ents(P, C, par, r, m);
     if (hint_is_node(m.type)) m.hint = ext_id(P.node_ids, N, g, m.hint);
-    bytes += wire_message(m, m.type, to_id, from_id, cid, arena + m.ent_off, heap, C.heap_bytes,
+    bytes += wire_message(m, m.type, to_id, from_id, cid, ents, heap, C.heap_bytes,
                           heap_head, out ? out + bytes : nullptr, &bad);
     nm++;
   }

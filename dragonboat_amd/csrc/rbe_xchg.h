@@ -40,6 +40,10 @@ struct alignas(16) XEnt {  // one arena entry of sender replica g * N + s
   Ent e;
 };
 constexpr u64 kXRecBytes[XS_NUM] = {sizeof(XCnt), sizeof(XMsg), sizeof(XEnt)};
+// XMsg::slot / XEnt::off of a record for the round spill heap (a list past
+// maxm, entries past ecap): the rest is its granule, which lies in the
+// sender rank's share of the heap (spill_alloc), free on every other rank
+constexpr u64 kXSpill = 1ull << 63;
 
 // rank that steps replica k of local group g (rep_world for a padding group
 // of a compacted engine: nobody)
@@ -118,27 +122,41 @@ RBE_HD void xchg_sender(const Planes& P, const Params& C, u64 r, u32 par, u32 ro
         *(XCnt*)p = x;
       }
     }
-    const u32 na = word & 0x7Fu, nb = (word >> 7) & 0x7Fu;
-    const Msg* lst = &P.msgs[par][((g * N + s) * N + d) * (u64)C.maxm];  // local list
-    for (u32 i = 0; i < na + nb; i++) {
-      const u32 slot = i < na ? i : C.maxm - 1u - (i - na);
-      const Msg m = lst[slot];
+    const u64 li = (g * N + s) * N + d;
+    const ListView lv = list_view(P, C, par, li, word);  // local list (or its spilled block)
+    const bool spl = (word & kCntSpill) != 0;
+    const u64 blk = spl ? P.msgs[par][li * C.maxm].hint : 0;
+    if (spl) {  // the plane slot 0 redirect record, as is
       if (u8* p = put(XS_MSG)) {
         XMsg x;
         x.key = key;
-        x.slot = slot;
+        x.slot = 0;
+        x.m = P.msgs[par][li * C.maxm];
+        *(XMsg*)p = x;
+      }
+    }
+    for (u32 i = 0; i < lv.n(); i++) {
+      const u32 bi = i < lv.na ? i : lv.cap - 1u - (i - lv.na);
+      const Msg m = lv.base[bi];
+      if (u8* p = put(XS_MSG)) {
+        XMsg x;
+        x.key = key;
+        x.slot = spl ? kXSpill | (blk + (u64)bi * (sizeof(Msg) / 16)) : bi;
         x.m = m;
         *(XMsg*)p = x;
       }
-      // the entries a Replicate carries live in the sender's arena
-      for (u32 e = 0; e < m.n_ent; e++) {
+      // the entries a Replicate carries live in the sender's arena, or past
+      // it in the spill heap (msg_ents)
+      const bool xe = (m.pad0 & kMsgXEnt) != 0;
+      const u32 ne = msg_nent(m);
+      for (u32 e = 0; e < ne; e++) {
         const u64 off = (u64)m.ent_off + e;
-        if (off >= C.ecap) break;
+        if (!xe && off >= C.ecap) break;
         if (u8* p = put(XS_ENT)) {
           XEnt x;
           x.key = gg * N + s;
-          x.off = off;
-          x.e = P.arena[par][r * C.ecap + off];
+          x.off = xe ? kXSpill | ((u64)m.ent_off + (u64)e * (sizeof(Ent) / 16)) : off;
+          x.e = xe ? spill_at<const Ent>(P, par, m.ent_off)[e] : P.arena[par][r * C.ecap + off];
           *(XEnt*)p = x;
         }
       }
@@ -162,12 +180,14 @@ RBE_HD void xchg_put_cnt(const Planes& P, const Params& C, u32 par, const XCnt& 
 RBE_HD void xchg_put_msg(const Planes& P, const Params& C, u32 par, const XMsg& x) {
   const u64 key = xchg_local_key(C, x.key, (u64)C.n * C.n);
   if (key == ~0ull) return;
-  P.msgs[par][key * (u64)C.maxm + x.slot] = x.m;
+  if (x.slot & kXSpill) *spill_at<Msg>(P, par, x.slot & ~kXSpill) = x.m;
+  else P.msgs[par][key * (u64)C.maxm + x.slot] = x.m;
 }
 RBE_HD void xchg_put_ent(const Planes& P, const Params& C, u32 par, const XEnt& x) {
   const u64 key = xchg_local_key(C, x.key, C.n);
   if (key == ~0ull) return;
-  P.arena[par][key * C.ecap + x.off] = x.e;
+  if (x.off & kXSpill) *spill_at<Ent>(P, par, x.off & ~kXSpill) = x.e;
+  else P.arena[par][key * C.ecap + x.off] = x.e;
 }
 // record i of stream t of source chunk p of a fixed-layout receive buffer, if
 // the chunk holds it (returns false past the chunk's count); *overflow gets
@@ -201,16 +221,17 @@ RBE_HD bool xchg_put_fixed(const Planes& P, const Params& C, u32 par, const u8* 
 // Replicate's with Index = LogIndex + 1 + i, a forwarded Propose's with Index
 // 0 as the client proposed them (raft.go:1841-1853); their whole Cmds go to
 // `cmd` back to back (when non-null).  row = the sender's outbox header of
-// that round's parity, `round` the round that reads it, lst = the N * maxm
-// message slots of (g, k, *), arena = the sender's ecap arena entries, all
-// host copies; `rd` reads payload-heap record bytes (rbe_host.h entry_out).
-// Counts beyond the capacities are reported in *n_msg / *n_ent / *n_cmd and
-// not written.  Returns RBE_OK or the reader's error (an overwritten record).
-template <int N, typename RD>
-int outbox_messages(const Params& C, u64 g, u32 k, const CntRow& row, u32 round, const Msg* lst,
-                    const Ent* arena, rbe_message* out, u32 cap, rbe_entry* ents, u32 ent_cap,
-                    u32* n_msg, u32* n_ent, u8* cmd, u64 cmd_cap, u64* n_cmd, const u64* ids,
-                    RD&& rd) {
+// that round's parity, `round` the round that reads it, list(d) = host copies
+// of the list to destination slot d in reading order (A, then B; a spilled
+// list's from its spill heap block), ent(m, j) = entry j of message m (its
+// sender's arena, or the spill heap: msg_ents); `rd` reads payload-heap record
+// bytes (rbe_host.h entry_out).  Counts beyond the capacities are reported in
+// *n_msg / *n_ent / *n_cmd and not written.  Returns RBE_OK or the reader's
+// error (an overwritten record).
+template <int N, typename LS, typename EA, typename RD>
+int outbox_messages(const Params& C, u64 g, u32 k, const CntRow& row, u32 round, LS&& list,
+                    EA&& ent, rbe_message* out, u32 cap, rbe_entry* ents, u32 ent_cap, u32* n_msg,
+                    u32* n_ent, u8* cmd, u64 cmd_cap, u64* n_cmd, const u64* ids, RD&& rd) {
   const u64 cid = cid_of(C, g);
   u32 n = 0, ne = 0;
   u64 nc = 0;
@@ -228,17 +249,18 @@ int outbox_messages(const Params& C, u64 g, u32 k, const CntRow& row, u32 round,
     n++;
   };
   for (u32 d = 0; d < N; d++) {
-    const u32 pc = row_word(row, d, k, round), na = pc & 0x7Fu, nb = (pc >> 7) & 0x7Fu;
+    const u32 pc = row_word(row, d, k, round);
     if (pc & 0x8000u) {
       Msg q = mk_msg(M_Quiesce, d + 1);
       emit(q, M_Quiesce, d + 1);
     }
-    for (u32 i = 0; i < na + nb; i++) {
-      const Msg& m = i < na ? lst[d * C.maxm + i] : lst[d * C.maxm + C.maxm - 1u - (i - na)];
+    if (!(pc & 0x7FFFu)) continue;
+    for (const Msg& m : list(d)) {
       emit(m, m.type, d + 1);
       if (m.type != M_Replicate && m.type != M_Propose) continue;
-      for (u32 j = 0; j < m.n_ent && m.ent_off + j < C.ecap; j++) {
-        const Ent& x = arena[m.ent_off + j];
+      const bool xe = (m.pad0 & kMsgXEnt) != 0;
+      for (u32 j = 0; j < msg_nent(m) && (xe || m.ent_off + j < C.ecap); j++) {
+        const Ent x = ent(m, j);
         const bool room_c = cmd && nc + x.len <= cmd_cap;
         if (ents && ne < ent_cap) {
           rbe_entry& e = ents[ne];

@@ -14,7 +14,7 @@ import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "libdragonboat_amd.so")
-RBE_ABI_VERSION = 8
+RBE_ABI_VERSION = 9
 
 COUNTER_NAMES = ["steps", "committed", "msg_in", "msg_out", "ent_in", "ent_out",
                  "reads_confirmed", "proposals", "reads", "quiesced_ticks", "active_ticks",
@@ -24,7 +24,7 @@ COUNTER_NAMES = ["steps", "committed", "msg_in", "msg_out", "ent_in", "ent_out",
 CTR_NUM = 24
 
 FAULT_NAMES = {0x01: "WINDOW", 0x02: "OUTBOX", 0x04: "ARENA", 0x08: "READQ", 0x10: "RTR",
-               0x20: "PANIC", 0x40: "UNSUPPORTED", 0x80: "DROPLIST"}
+               0x20: "PANIC", 0x40: "UNSUPPORTED", 0x80: "DROPLIST", 0x100: "NOMEM"}
 
 
 class RbeConfig(C.Structure):
@@ -48,7 +48,8 @@ class RbeConfig(C.Structure):
                 ("membership", C.c_uint32), ("cc_period", C.c_uint32), ("cc_mod", C.c_uint32),
                 ("rep_compact", C.c_uint32), ("n_voters", C.c_uint32),
                 ("max_inmem_log_size", C.c_uint64), ("observer_slots", C.c_uint32),
-                ("witness_slots", C.c_uint32)]
+                ("witness_slots", C.c_uint32), ("pool_bytes", C.c_uint64),
+                ("spill_bytes", C.c_uint64)]
 
 
 class RbeReplicaView(C.Structure):
@@ -215,9 +216,10 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_round", "rbe_run_timed", "rbe_prepare_run", "rbe_push_proposals", "rbe_push_read_index",
            "rbe_get_updates", "rbe_get_messages", "rbe_get_ready_to_reads", "rbe_get_entries",
            "rbe_get_views", "rbe_get_counters", "rbe_reset_counters", "rbe_fault_summary",
+           "rbe_spill_stats",
            "rbe_footprint", "rbe_profile_rounds", "rbe_get_kernel_counters", "rbe_kernel_name",
            "rbe_xchg_record_bytes", "rbe_xchg_pack", "rbe_xchg_unpack", "rbe_get_outbox",
-           "rbe_push_messages", "rbe_snapshot_bytes", "rbe_export_groups", "rbe_import_groups",
+           "rbe_push_messages", "rbe_snapshot_bytes", "rbe_export_bytes", "rbe_export_groups", "rbe_import_groups",
            "rbe_get_entry_cmds", "rbe_set_apply_ready", "rbe_collect_outputs", "rbe_collect_updates", "rbe_launch",
            "rbe_xchg_chunk_bytes", "rbe_xchg_pack_fixed", "rbe_xchg_unpack_fixed",
            "rbe_xchg_status", "rbe_stream", "rbe_get_snapshot_state", "rbe_wire_encode",
@@ -309,6 +311,7 @@ def load_library(path: Optional[str] = None):
         "rbe_get_counters": (i32, [vp, P(u64)]),
         "rbe_reset_counters": (i32, [vp]),
         "rbe_fault_summary": (i32, [vp, P(u64), P(u32)]),
+        "rbe_spill_stats": (i32, [vp, P(u64)]),
         "rbe_footprint": (i32, [P(RbeConfig), P(u64)]),
         "rbe_profile_rounds": (i32, [vp, u32, P(C.c_float)]),
         "rbe_get_kernel_counters": (i32, [vp, C.c_int32, P(u64)]),
@@ -322,6 +325,7 @@ def load_library(path: Optional[str] = None):
         "rbe_xchg_status": (i32, [vp, P(u32)]),
         "rbe_stream": (i32, [vp, P(vp)]),
         "rbe_snapshot_bytes": (i32, [vp, u64, P(u64)]),
+        "rbe_export_bytes": (i32, [vp, u64, u64, P(u64)]),
         "rbe_export_groups": (i32, [vp, u64, u64, vp, u64]),
         "rbe_import_groups": (i32, [vp, vp, u64, u32]),
     }
@@ -358,7 +362,7 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                 ext_commit: bool = False, membership: bool = False, cc_period: int = 0,
                 cc_mod: int = 1, rep_compact: bool = False,
                 max_inmem_log_size: int = 0, n_voters: int = 0, observer_slots: int = 0,
-                witness_slots: int = 0) -> RbeConfig:
+                witness_slots: int = 0, pool_bytes: int = 0, spill_bytes: int = 0) -> RbeConfig:
     return RbeConfig(abi_version=RBE_ABI_VERSION, device=device, n_groups=n_groups,
                      n_replicas=n_replicas, election_rtt=election_rtt,
                      heartbeat_rtt=heartbeat_rtt, check_quorum=int(check_quorum),
@@ -376,7 +380,8 @@ def make_config(n_groups: int, n_replicas: int = 3, device: int = 0, election_rt
                      membership=int(membership), cc_period=cc_period, cc_mod=cc_mod,
                      rep_compact=int(rep_compact), max_inmem_log_size=max_inmem_log_size,
                      n_voters=n_voters, observer_slots=observer_slots,
-                     witness_slots=witness_slots)
+                     witness_slots=witness_slots, pool_bytes=pool_bytes,
+                     spill_bytes=spill_bytes)
 
 
 class InputError(EngineError):
@@ -731,7 +736,12 @@ class Engine(NodeInputs):
         """The protocol state of groups [first, first + count) after the last
         queued round, as bytes (peer.go:64-87 / raft.go:283-330 restated)."""
         count = self.n_groups - first if count is None else count
-        n = self.snapshot_bytes(count) if cap is None else cap
+        if cap is None:
+            nb = C.c_uint64()
+            _check(self.lib.rbe_export_bytes(self.h, first, count, C.byref(nb)), "rbe_export_bytes")
+            n = nb.value
+        else:
+            n = cap
         buf = C.create_string_buffer(max(1, n))
         rc = self.lib.rbe_export_groups(self.h, first, count, buf, n)
         if rc != 0:
@@ -1010,12 +1020,13 @@ class Engine(NodeInputs):
                 arr(o.msg_off, o.n + 1, u64), arr(o.messages, o.n_messages, MESSAGE_DTYPE),
                 arr(o.rtr_off, o.n + 1, u64), arr(o.ready_to_reads, o.n_ready_to_reads, RTR_DTYPE))
 
-    def ready_to_reads(self, replica: int):
-        cap = 64
+    def ready_to_reads(self, replica: int, cap: int = 64):
         arr = (RbeReadyToRead * cap)()
         n = C.c_uint32()
         _check(self.lib.rbe_get_ready_to_reads(self.h, replica, arr, cap, C.byref(n)),
                "rbe_get_ready_to_reads")
+        if n.value > cap:  # a list that spilled past rtr_cap: never truncate silently
+            return self.ready_to_reads(replica, n.value)
         return [(arr[i].index, arr[i].ctx_low, arr[i].ctx_high) for i in range(n.value)]
 
     def entries(self, replica: int, lo: int, hi: int):
@@ -1034,6 +1045,15 @@ class Engine(NodeInputs):
 
     def entry_cmds(self, replica: int, lo: int, hi: int) -> List[bytes]:
         return entry_cmds(self.lib.rbe_get_entry_cmds, self.h, replica, lo, hi)
+
+    def spill_stats(self) -> Dict[str, int]:
+        """The spill tiers' use (rbe_spill_stats): pool pages in use / total,
+        the most round spill heap bytes a round used / its bytes per parity,
+        exhaustion flags."""
+        out = (C.c_uint64 * 5)()
+        _check(self.lib.rbe_spill_stats(self.h, out), "rbe_spill_stats")
+        return dict(pool_pages_used=out[0], pool_pages=out[1], spill_peak_bytes=out[2],
+                    spill_bytes=out[3], oom=out[4])
 
     def fault_summary(self):
         n = C.c_uint64()

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RBE_ABI_VERSION 8
+#define RBE_ABI_VERSION 9
 
 /* error codes */
 #define RBE_OK 0
@@ -56,6 +56,14 @@ extern "C" {
 #define RBE_FAULT_PANIC 0x20u
 #define RBE_FAULT_UNSUPPORTED 0x40u
 #define RBE_FAULT_DROPLIST 0x80u
+/* Since ABI 9 no per-replica capacity of the planes faults a replica: a full
+ * message list, entry arena, readIndex queue, ReadyToRead or dropped list and
+ * the log below the in-memory ring spill into the engine's spill tiers (a page
+ * pool and a round spill heap, cfg.pool_bytes / spill_bytes).  OUTBOX, ARENA,
+ * READQ, RTR and DROPLIST are no longer raised; WINDOW means a log entry the
+ * replica holds is missing (a launch that handed over only the LogDB's tail);
+ * NOMEM that a spill tier itself is exhausted (rbe_spill_stats). */
+#define RBE_FAULT_NOMEM 0x100u
 
 /* counter slots (rbe_get_counters) */
 enum rbe_counter {
@@ -184,6 +192,19 @@ typedef struct rbe_config {
    * cfg.membership. */
   uint32_t observer_slots;
   uint32_t witness_slots;
+  /* Spill tiers (dragonboat_amd/csrc/rbe_spill.h): everything a replica holds
+   * beyond the planes' fixed capacities.  pool_bytes: the page pool holding
+   * each replica's cold log (its entries below the in-memory ring: the ILogDB
+   * read path, logentry.go:144-161, 186-246; every entry above the LogDB
+   * marker is kept, as dragonboat's LogDB does) and readIndex queues longer
+   * than rq_cap; 0 = 8 KiB per replica, at least 64 MiB, at most 32 GiB.
+   * spill_bytes: the round spill heap per round parity (message lists past
+   * maxm, a message's entries past ecap — a catch-up Replicate sized by
+   * MaxEntrySize, raft.go:709-740 — ReadyToReads past rtr_cap, dropped
+   * ReadIndexes past dri_cap); 0 = 128 B per replica, at least 16 MiB, at most
+   * 4 GiB. */
+  uint64_t pool_bytes;
+  uint64_t spill_bytes;
 } rbe_config;
 
 /* Snapshot of one replica (tests, debugging, rbe_get_views). */
@@ -304,8 +325,10 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out);
  * (loadState panics below it, raft.go:429-437) and the entries lie above it.  The node around it restarts
  * too (fresh quiesce state and tick count), and the messages in flight to and
  * from a relaunched replica are lost.  replica[i] takes st[i] and the next
- * st[i].n_entries entries of `ents` (n_entries <= cfg.ring; an entry the
- * replica later needs below that window faults with RBE_FAULT_WINDOW).  The
+ * st[i].n_entries entries of `ents`: the LogDB's entries above its marker,
+ * up to last_index (the ring takes the newest cfg.ring of them, the cold log
+ * the rest; a LogDB handed over only in part faults with RBE_FAULT_WINDOW when
+ * the replica later needs an entry below what it was given).  The
  * entries' Cmds are concatenated in `cmd` (null: each is its rbe_entry.cmd,
  * at most 16 bytes); entries with longer Cmds or session fields go to the
  * payload heap.  Checked whole before anything changes (RBE_E_INVALID;
@@ -718,6 +741,12 @@ int rbe_reset_counters(rbe_engine* e);
 /* number of replicas whose sticky fault word holds a fault, and the OR of all
  * words */
 int rbe_fault_summary(rbe_engine* e, uint64_t* n_faulty, uint32_t* fault_or);
+/* The spill tiers' use (cfg.pool_bytes / spill_bytes; rbe_spill.h), after every
+ * round queued: out[0] pool pages in use, out[1] pool pages, out[2] the most
+ * round spill heap bytes one round used, out[3] its bytes per round parity,
+ * out[4] exhaustion flags (bit 0 the pool, bits 1-2 the heap of parity 0 / 1;
+ * sticky, the replicas concerned carry RBE_FAULT_NOMEM). */
+int rbe_spill_stats(rbe_engine* e, uint64_t* out /* 5 */);
 
 /* Replica-per-GPU mode (cfg.rep_world > 1).  The engine steps
  * only its own replicas; between rounds the host moves the messages of the
@@ -805,15 +834,25 @@ int rbe_push_messages(rbe_engine* e, uint64_t n, const uint64_t* group, const rb
  * Replaces what a restarted dragonboat node rebuilds from LogDB through Peer.Launch on
  * an existing log (peer.go:64-87, raft.go:283-330 loadState), and is the hand-off a
  * host slow path uses to run a rare handler on one group and put it back.
- *   rbe_snapshot_bytes: the buffer size `count` groups need;
+ *   rbe_snapshot_bytes: the size of `count` groups' header and planes (the fixed part);
+ *   rbe_export_bytes: the whole snapshot of [first, first + count) as the engine stands:
+ *     the fixed part, then the log section — every replica's log below its ring (the
+ *     cold log, in 64-entry pages) and a readIndex queue longer than cfg.rq_cap
+ *     (dragonboat_amd/csrc/rbe_spill.h) — so it grows with the logs it carries;
  *   rbe_export_groups: copies the range into `buf` (host memory, cap bytes; RBE_E_NOMEM
- *     when short), after every round already queued;
- *   rbe_import_groups: overwrites the snapshot's range.  The engine must be at the
- *     snapshot's round (RBE_E_STATE otherwise), unless flags has RBE_IMPORT_RESUME and
- *     the snapshot covers every group: then the engine resumes at that round.
- *     RBE_E_INVALID when the geometry (n, ring, capacities) differs. */
+ *     when short), after every round already queued.  RBE_E_STATE when the range's last
+ *     step left messages, entries, ReadyToReads or dropped ReadIndexes in the round
+ *     spill heap (lists past cfg.maxm, entries past cfg.ecap, outputs past cfg.rtr_cap /
+ *     cfg.dri_cap): step one more round and export then;
+ *   rbe_import_groups: overwrites the snapshot's range (its old cold logs go back to the
+ *     page pool first).  The engine must be at the snapshot's round (RBE_E_STATE
+ *     otherwise), unless flags has RBE_IMPORT_RESUME and the snapshot covers every
+ *     group: then the engine resumes at that round.  RBE_E_INVALID when the geometry
+ *     (n, ring, capacities) differs or the log section does not match the planes;
+ *     RBE_E_NOMEM when the page pool cannot take the log section. */
 #define RBE_IMPORT_RESUME 0x1u
 int rbe_snapshot_bytes(rbe_engine* e, uint64_t count, uint64_t* bytes);
+int rbe_export_bytes(rbe_engine* e, uint64_t first, uint64_t count, uint64_t* bytes);
 int rbe_export_groups(rbe_engine* e, uint64_t first, uint64_t count, void* buf, uint64_t cap);
 int rbe_import_groups(rbe_engine* e, const void* buf, uint64_t bytes, uint32_t flags);
 

@@ -8,12 +8,13 @@ and the tail of the log (its in-memory window)."""
 def restart(eng, ref, replicas, ring, snapshots=False):
     """`snapshots`: the LogDB may be compacted; the launch state carries its
     marker and latest snapshot (harness_snapshot_state) and the entries above
-    the marker."""
+    the marker.  `ring` None: the whole LogDB (the engine keeps what is below
+    its ring in the cold log), else only its last `ring` entries."""
     states, ents = [], []
     for r in replicas:
         term, vote, commit, last = ref.persisted(r)
         snap = ()
-        lo = max(1, last - ring + 1)
+        lo = 1 if ring is None else max(1, last - ring + 1)
         if snapshots:
             marker, mterm, ssi, sst = ref.snapshot_state(r)[:4]
             # the LogDB's membership (its snapshot's; all voters without one)

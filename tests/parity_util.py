@@ -21,11 +21,10 @@ MIXED = dict(n_groups=30, n_replicas=5, check_quorum=True, quiesce=True, wl_enab
              wl_start_round=25, wl_active_mod=2, wl_read_permille=500, iso_period=37,
              iso_len=20, iso_mod=2, seed=12345)
 
-# engine-only knobs (window/queue capacities) per config
-ENGINE_EXTRA = {
-    "C3": dict(ring=128), "C3_HOT": dict(ring=128),
-    "MIXED": dict(ring=128, rq_cap=64, maxm=24),
-}
+# engine-only knobs per config: none.  Every config runs with the engine's
+# default capacities (ring 64, rq_cap 8, maxm 12, ecap 32, rtr_cap / dri_cap 8);
+# what exceeds them goes to the spill tiers (dragonboat_amd/csrc/rbe_spill.h)
+ENGINE_EXTRA = {}
 
 
 def view_diff(a, b, skip=()):

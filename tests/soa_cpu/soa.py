@@ -45,6 +45,7 @@ def lib():
         L.soa_wire_ingest.restype = C.c_int
         L.soa_wire_ingest.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64,
                                       C.POINTER(RbeWireIngestStats)]
+        L.soa_spill_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         L.soa_set_full_only.argtypes = [C.c_void_p, C.c_int]
         L.soa_set_staged.argtypes = [C.c_void_p, C.c_int]
         L.soa_slow_total.restype = C.c_uint64
@@ -71,6 +72,8 @@ def lib():
                                       C.c_uint64, C.c_void_p, C.c_uint64]
         L.soa_snapshot_bytes.restype = C.c_uint64
         L.soa_snapshot_bytes.argtypes = [C.c_void_p, C.c_uint64]
+        L.soa_export_bytes.restype = C.c_uint64
+        L.soa_export_bytes.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64]
         L.soa_export_groups.restype = C.c_int
         L.soa_export_groups.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p,
                                         C.c_uint64]
@@ -134,6 +137,12 @@ class SoaCpu(NodeInputs):
         self.n_rep = self.n_groups * self.cfg.n_replicas
         lib().soa_set_full_only(self.h, int(full_only))
         lib().soa_set_staged(self.h, int(staged))
+
+    def spill_stats(self):
+        out = (C.c_uint64 * 5)()
+        lib().soa_spill_stats(self.h, out)
+        return dict(pool_pages_used=out[0], pool_pages=out[1], spill_peak_bytes=out[2],
+                    spill_bytes=out[3], oom=out[4])
 
     def slow_total(self):
         return lib().soa_slow_total(self.h)
@@ -214,7 +223,7 @@ class SoaCpu(NodeInputs):
     # group-range snapshots, same contract as Engine.export_groups / import_groups
     def export_groups(self, first=0, count=None, cap=None):
         count = self.n_groups - first if count is None else count
-        n = lib().soa_snapshot_bytes(self.h, count) if cap is None else cap
+        n = lib().soa_export_bytes(self.h, first, count) if cap is None else cap
         buf = C.create_string_buffer(max(1, n))
         rc = lib().soa_export_groups(self.h, first, count, buf, n)
         if rc != 0:

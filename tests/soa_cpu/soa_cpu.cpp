@@ -23,6 +23,10 @@ struct SoaEngine {
   Params C;
   Planes P;
   std::vector<std::vector<uint8_t>> bufs;
+  std::vector<void*> cbufs;  // calloc'd (the spill tiers: zero pages mapped on first touch)
+  ~SoaEngine() {
+    for (void* p : cbufs) free(p);
+  }
   u32 round = 0;
   u32 tclk = 0;
   u32 scan_at = 0;  // the host's last scan round (k_triage list mode: Lists::scan_round)
@@ -52,10 +56,17 @@ static T* alloc(SoaEngine* e, u64 n) {
   e->bufs.emplace_back(n * sizeof(T) + 64, 0);
   return (T*)e->bufs.back().data();
 }
+template <typename T>
+static T* calloc_t(SoaEngine* e, u64 n) {
+  void* p = calloc(n * sizeof(T) + 64, 1);
+  e->cbufs.push_back(p);
+  return (T*)p;
+}
 
 template <int N>
 static void run_round(SoaEngine* e, bool tick = true) {
   const Clk ck{e->round, e->tclk, tick ? 1u : 0u};
+  spill_clear_next(e->P, e->round & 1u);  // (k_triage's first thread on the device)
   if (!e->hin.empty()) {  // the HIP engine uploads and scatters the same records
     HostHeap& hp = e->hin.heap;
     for (u64 p = hp.flushed; p < hp.head; p++) e->heap[p % hp.cap] = hp.stage[p - hp.flushed];
@@ -257,6 +268,18 @@ void* soa_create(const rbe_config* cfg) {
   P.imark = (C.ext_commit || C.rl_max) ? alloc<u64>(e, R) : nullptr;
   P.rl = C.rl_max ? alloc<RlSt>(e, R) : nullptr;
   P.roles = C.membership ? alloc<u16>(e, R) : nullptr;
+  // spill tiers (rbe_spill.h), sized as the HIP engine sizes them
+  if (C.rq_cap >= kRqExt || spill_sizes(cfg, &C)) {
+    delete e;
+    return nullptr;
+  }
+  P.pool = calloc_t<Ent>(e, (u64)C.pool_pages * kPageEnts);
+  P.pmeta = calloc_t<PoolMeta>(e, C.pool_pages);
+  P.cold = alloc<ColdRef>(e, R);
+  P.spill[0] = calloc_t<u8>(e, 2 * C.spill_units * 16);
+  P.spill[1] = P.spill[0] + C.spill_units * 16;
+  P.sctl = calloc_t<SpillCtl>(e, 1);
+  P.sctl->bump = 1;
   C.heap_bytes = (cfg->heap_bytes + 255) & ~255ull;
   e->heap.assign(C.heap_bytes, 0);
   e->hin.init(R, C.n, C.in_cap, C.heap_bytes);
@@ -286,6 +309,17 @@ void* soa_create(const rbe_config* cfg) {
 
 void soa_destroy(void* h) { delete (SoaEngine*)h; }
 
+// rbe_spill_stats on the host build
+void soa_spill_stats(void* h, uint64_t* out) {
+  SoaEngine* e = (SoaEngine*)h;
+  const SpillCtl& s = *e->P.sctl;
+  out[0] = s.live;
+  out[1] = e->C.pool_pages - 1;
+  out[2] = std::max(s.peak[0], s.peak[1]) * 16;
+  out[3] = e->C.spill_units * 16;
+  out[4] = s.oom;
+}
+
 // rbe_get_entry_cmds: Cmd bytes of entries [lo, hi] of a replica, inline or
 // from the payload heap
 int soa_get_entry_cmds(void* h, uint64_t replica, uint64_t lo, uint64_t hi, uint8_t* buf,
@@ -294,16 +328,19 @@ int soa_get_entry_cmds(void* h, uint64_t replica, uint64_t lo, uint64_t hi, uint
   const Params& C = e->C;
   if (replica >= C.n_rep || lo == 0 || hi < lo) return RBE_E_INVALID;
   const Core& c = e->P.core[replica];
-  if (hi > c.last_index || c.last_index - lo >= C.ring) return RBE_E_INVALID;
+  if (hi > c.last_index) return RBE_E_INVALID;
+  std::vector<Ent> en(hi - lo + 1);
+  for (u64 i = lo; i <= hi; i++)  // the ring window and the cold log (rbe_spill.h)
+    if (!log_ent_at(e->P, C, replica, c.last_index, i, &en[i - lo])) return RBE_E_STATE;
   u64 off = 0;
   for (u64 i = lo; i <= hi; i++) {
     offsets[i - lo] = off;
-    off += e->P.pay_ring[(i & (C.ring - 1)) * C.n_rep + replica].len;
+    off += en[i - lo].len;
   }
   offsets[hi - lo + 1] = off;
   if (off > cap) return RBE_E_NOMEM;
   for (u64 i = lo; i <= hi; i++) {
-    const Body& b = e->P.pay_ring[(i & (C.ring - 1)) * C.n_rep + replica];
+    const Ent& b = en[i - lo];
     u8* d = buf + offsets[i - lo];
     if (!ent_heap(b.type)) {
       u8 w[16];
@@ -323,17 +360,11 @@ int soa_get_entries(void* h, uint64_t replica, uint64_t lo, uint64_t hi, rbe_ent
   const Params& C = e->C;
   if (replica >= C.n_rep || lo == 0 || hi < lo) return RBE_E_INVALID;
   const Core& c = e->P.core[replica];
-  if (hi > c.last_index || c.last_index - lo >= C.ring) return RBE_E_INVALID;
+  if (hi > c.last_index) return RBE_E_INVALID;
   auto rd = [e](u64 pos, u64 off, u64 len, u8* dst) { return soa_read_heap(e, pos, off, len, dst); };
   for (u64 i = lo; i <= hi; i++) {
-    const u64 sl = (i & (C.ring - 1)) * C.n_rep + replica;
-    const Body& b = e->P.pay_ring[sl];
-    Ent x;
-    x.term = e->P.term_ring[sl];
-    x.type = b.type;
-    x.len = b.len;
-    x.lo = b.lo;
-    x.hi = b.hi;
+    Ent x;  // the ring window and the cold log (rbe_spill.h)
+    if (!log_ent_at(e->P, C, replica, c.last_index, i, &x)) return RBE_E_STATE;
     rbe_entry& o = out[i - lo];
     memset(&o, 0, sizeof(o));
     const int rc = entry_out(x, &o, nullptr, rd);
@@ -544,8 +575,9 @@ int soa_get_update_commits(void* h, uint64_t first, uint64_t count, rbe_update_c
     update_view(e->P.upd[r], e->P.core[r], e->P.hot[r], e->round, u);
     auto term_of = [&](u64 idx) -> u64 {
       const Core& c = e->P.core[r];
-      return idx == c.last_index ? c.t_last
-                                 : e->P.term_ring[(idx & (u64)(e->C.ring - 1)) * e->C.n_rep + r];
+      if (idx == c.last_index) return c.t_last;
+      Ent x;
+      return log_ent_at(e->P, e->C, r, c.last_index, idx, &x) ? x.term : 0;
     };
     const u64 si = e->C.snapshot_entries ? e->P.snp[r].marker : 0;
     update_commit_view(u, e->P.applied[r], si, term_of, out[i]);
@@ -855,7 +887,7 @@ void soa_views(void* h, rbe_replica_view* out) {
     v.q_no_activity_since = hh.q_no_activity_since;
     v.q_exit_quiesce_tick = hh.q_exit_quiesce_tick;
     v.raft_quiesce = (hh.flags & HF_RAFT_QUIESCE) ? 1 : 0;
-    v.rq_count = c.rq_count;
+    v.rq_count = rq_length(e->P, e->C, i, c);
     v.votes_resp = hh.votes_resp;
     v.votes_granted = hh.votes_granted;
     v.events = (e->round > 0 && e->P.upd[i].round == e->round - 1) ? e->P.upd[i].events : 0u;
@@ -995,12 +1027,18 @@ extern "C" int soa_get_outbox(void* h, uint64_t replica, rbe_message* out, uint3
   const u64 g = replica / N;
   const u32 k = (u32)(replica % N);
   const CntRow& row = e->P.cnt[par][replica];
-  const Msg* lst = e->P.msgs[par] + (g * N + k) * N * (u64)e->C.maxm;
-  const Ent* arena = e->P.arena[par] + replica * e->C.ecap;
   const u32 rd = e->round;
+  std::vector<Msg> lv;
+  auto list = [&](u32 d) -> const std::vector<Msg>& {
+    const ListView v = list_view(e->P, e->C, par, replica * N + d, row_word(row, d, k, rd));
+    lv.clear();
+    for (u32 i = 0; i < v.n(); i++) lv.push_back(v.at(i));
+    return lv;
+  };
+  auto ent = [&](const Msg& m, u32 j) { return msg_ents(e->P, e->C, par, replica, m)[j]; };
   auto hr = [e](u64 pos, u64 off, u64 len, u8* dst) { return soa_read_heap(e, pos, off, len, dst); };
   return with_n(N, [&](auto NN) {
-    return outbox_messages<decltype(NN)::value>(e->C, g, k, row, rd, lst, arena, out, cap, ents,
+    return outbox_messages<decltype(NN)::value>(e->C, g, k, row, rd, list, ent, out, cap, ents,
                                                 ent_cap, n_out, n_ents, cmd, cmd_cap, cmd_bytes,
                                                 e->hin.id_table(), hr);
   });
@@ -1036,14 +1074,48 @@ extern "C" uint64_t soa_snapshot_bytes(void* h, uint64_t count) {
   return sizeof(SnapHeader) + snap_body_bytes(e->P, e->C, count);
 }
 
+// the log section's source (rbe_snap.h snap_log_write): the planes themselves
+struct SnapLogHost {
+  const Planes& P;
+  const Params& C;
+  ColdRef cold(u64 r) { return P.cold[r]; }
+  Core core(u64 r) { return P.core[r]; }
+  RqExt rq(u64 r) { return rq_ext_load(P, C, r); }
+  PoolMeta meta(u32 p) { return P.pmeta[p]; }
+  void page(u32 p, Ent* out) { memcpy(out, pool_ent(P, p, 0), kPageEnts * sizeof(Ent)); }
+};
+static bool soa_range_spilled(SoaEngine* e, u64 first, u64 count) {
+  if (e->round == 0) return false;
+  const u32 N = e->C.n, par = (e->round - 1) & 1u;
+  for (u64 r = first * N; r < (first + count) * N; r++) {
+    u32 w[8];
+    for (u32 d = 0; d < N; d++) w[d] = row_word(e->P.cnt[par][r], d, (u32)(r % N), e->round);
+    if (snap_round_spilled(e->C, w, e->P.msgs[par] + r * N * e->C.maxm, e->P.upd[r])) return true;
+  }
+  return false;
+}
+extern "C" uint64_t soa_export_bytes(void* h, uint64_t first, uint64_t count) {
+  SoaEngine* e = (SoaEngine*)h;
+  SnapLogHost src{e->P, e->C};
+  return snap_log_at(snap_body_bytes(e->P, e->C, count)) +
+         snap_log_write(e->C, first * e->C.n, count * e->C.n, src, nullptr);
+}
+
 extern "C" int soa_export_groups(void* h, uint64_t first, uint64_t count, void* buf, uint64_t cap) {
   SoaEngine* e = (SoaEngine*)h;
   if (count == 0 || first >= e->C.n_groups || count > e->C.n_groups - first) return RBE_E_INVALID;
+  if (soa_range_spilled(e, first, count)) return RBE_E_STATE;
   const u64 body = snap_body_bytes(e->P, e->C, count);
-  if (cap < sizeof(SnapHeader) + body) return RBE_E_NOMEM;
+  SnapLogHost src{e->P, e->C};
+  const u64 r0 = first * e->C.n, nr = count * e->C.n;
+  const u64 lb = snap_log_write(e->C, r0, nr, src, nullptr);
+  if (cap < snap_log_at(body) + lb) return RBE_E_NOMEM;
   SnapHeader hd;
   snap_fill_header(e->C, RBE_ABI_VERSION, e->round, e->tclk, first, count, body, &hd);
+  hd.log_bytes = lb;
   memcpy(buf, &hd, sizeof(hd));
+  memset((u8*)buf + sizeof(hd) + body, 0, snap_log_at(body) - sizeof(hd) - body);
+  snap_log_write(e->C, r0, nr, src, (u8*)buf + snap_log_at(body));
   SnapPlane pl[kSnapPlanes];
   snap_planes(e->P, e->C, pl);
   u8* dst = (u8*)buf + sizeof(SnapHeader);
@@ -1066,6 +1138,11 @@ extern "C" int soa_import_groups(void* h, const void* buf, uint64_t bytes, uint3
   const bool resume = (flags & RBE_IMPORT_RESUME) != 0;
   if (resume && (hd.first != 0 || hd.count != e->C.n_groups)) return RBE_E_INVALID;
   if (!resume && hd.round != e->round) return RBE_E_STATE;
+  const u64 r0 = hd.first * e->C.n, nr = hd.count * e->C.n;
+  std::vector<u64> rec_off(nr);
+  if (snap_log_index(e->C, (const u8*)buf, nr, rec_off.data())) return RBE_E_INVALID;
+  const u32 spar = e->round & 1u;  // (as rbe_import_groups)
+  for (u64 i = 0; i < nr; i++) spill_replica_release(e->P, e->C, r0 + i, spar);
   SnapPlane pl[kSnapPlanes];
   snap_planes(e->P, e->C, pl);
   const u8* src = (const u8*)buf + sizeof(SnapHeader);
@@ -1073,6 +1150,14 @@ extern "C" int soa_import_groups(void* h, const void* buf, uint64_t bytes, uint3
     const u64 w = hd.count * pl[i].group_bytes;
     for (u64 row = 0; row < pl[i].rows; row++, src += w)
       memcpy(pl[i].base + row * pl[i].pitch + hd.first * pl[i].group_bytes, src, w);
+  }
+  {  // the log section, 16-B aligned for the record reads
+    std::vector<u64> sec((hd.log_bytes + 15) / 8 + 2);
+    u8* s = (u8*)(((uintptr_t)sec.data() + 15) & ~(uintptr_t)15);
+    memcpy(s, (const u8*)buf + snap_log_at(hd.body_bytes), hd.log_bytes);
+    u32 f = 0;
+    for (u64 i = 0; i < nr; i++) snap_log_rebuild(e->P, e->C, r0 + i, s + rec_off[i], spar ^ 1u, &f);
+    if (f) return RBE_E_NOMEM;
   }
   e->hin.resync_applied(e->P.applied + hd.first * e->C.n, hd.first * e->C.n, hd.count * e->C.n);
   memset(e->P.gwake + hd.first, GW_AWAKE, hd.count);  // imported groups start awake
