@@ -309,14 +309,15 @@ __device__ __forceinline__ bool out_msg_wanted(const Params& C, u64 g, u32 d, bo
 }
 // An Update with something for the node besides the messages it carries: a
 // State change, entries to save or apply, ReadyToReads, dropped requests, a
-// Snapshot, an applied index to confirm, listener events (RBE_COLLECT_SKIP_LOCAL)
+// Snapshot, an applied index to confirm, listener events, a fault
+// (RBE_COLLECT_SKIP_LOCAL: a faulted replica's Update always reaches the host)
 __device__ __forceinline__ bool upd_actionable_dev(const Planes& P, u64 r, u32 round) {
   const Upd* u = P.upd + r;
   const uint4 c3 = reinterpret_cast<const uint4*>(u)[3];
   const u32 flags = c3.y & 0xFFFFu, events = c3.y >> 16;
   if ((flags & (RBE_UF_STATE_CHANGED | RBE_UF_SENT_QUIESCE | RBE_UF_SNAPSHOT | RBE_UF_APPLIED |
                 RBE_UF_HAS_UPDATE)) ||
-      events || (c3.w >> 16) != 0u)  // n_rtr
+      events || c3.x != 0u || (c3.w >> 16) != 0u)  // fault, n_rtr
     return true;
   if (!(flags & UF_RANGES)) return false;
   const Upd d = *u;  // ranges and drops
@@ -524,6 +525,17 @@ __global__ __launch_bounds__(kBlock) void k_snap_log_rebuild(Planes P, Params C,
   if (f) atomicOr(fault, f);
 }
 
+// rbe_apply_config_change: raft's membership of each listed replica now
+// (Planes::roles is valid with MB_ROLES)
+__global__ __launch_bounds__(kBlock) void k_ms_gather(Planes P, const u64* replica, u64 n,
+                                                      u32* ms) {
+  const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const Core& c = P.core[replica[i]];
+  const u32 x = (c.mflags & MB_ROLES) ? P.roles[replica[i]] : 0u;
+  ms[i] = pack_ms(c.members & MB_REMOVED, x & 0xFFu, x >> 8);
+}
+
 __global__ void k_advance(u32* clk, u32 k) {
   clk[0] += k;
   clk[1] += k;
@@ -618,8 +630,15 @@ struct PinnedAlloc {
   template <class U>
   PinnedAlloc(const PinnedAlloc<U>&) {}
   T* allocate(size_t n) {
+    // RBE_PINNED_LIMIT_BYTES: refuse larger allocations, as a host short of
+    // pinnable memory would (fault injection for the RBE_E_NOMEM path)
+    static const u64 limit = [] {
+      const char* v = getenv("RBE_PINNED_LIMIT_BYTES");
+      return v ? strtoull(v, nullptr, 10) : 0ull;
+    }();
     void* p = nullptr;
-    if (hipHostMalloc(&p, n * sizeof(T), hipHostMallocDefault) != hipSuccess || !p)
+    if ((limit && n * sizeof(T) > limit) ||
+        hipHostMalloc(&p, n * sizeof(T), hipHostMallocDefault) != hipSuccess || !p)
       throw std::bad_alloc();
     return (T*)p;
   }
@@ -629,6 +648,18 @@ struct PinnedAlloc {
   template <class U>
   bool operator!=(const PinnedAlloc<U>&) const { return false; }
 };
+
+// The C ABI never lets an exception out: a failed host allocation while
+// staging input (a pinned PinnedAlloc growth, or std::allocator's) is
+// RBE_E_NOMEM, and the staged input of the call is left as it was checked.
+template <class F>
+static int abi_nomem(F&& f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    return RBE_E_NOMEM;
+  }
+}
 
 struct rbe_engine {
   rbe_config cfg;
@@ -1181,6 +1212,16 @@ int rbe_create(const rbe_config* cfg, rbe_engine** out) {
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RBE_E_NODEV;
   if (cfg->device < 0 || cfg->device >= ndev) return RBE_E_NODEV;
   HIP_OK(hipSetDevice(cfg->device));
+  if (!cfg->pool_bytes) {
+    // the default page pool grows to an eighth of the free HBM (at most 32
+    // GiB): the cold logs keep every entry a LogDB without snapshots keeps, so
+    // a long run without compaction needs room in proportion to its rounds
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess) {
+      const u64 pages = std::min<u64>(fr / 8, 32ull << 30) / (kPageEnts * sizeof(Ent));
+      if (pages > C.pool_pages) C.pool_pages = (u32)std::min<u64>(pages, 0xFFFFFFF0ull);
+    }
+  }
   rbe_engine* e = new (std::nothrow) rbe_engine();
   if (!e) return RBE_E_NOMEM;
   e->cfg = *cfg;
@@ -1665,42 +1706,42 @@ int rbe_push_proposals(rbe_engine* e, uint64_t n, const uint64_t* replica, const
                        const uint32_t* type, const uint32_t* cmd_len, const uint8_t* cmd) {
   if (!e) return RBE_E_INVALID;
   if (!e->C.ext_inputs) return RBE_E_STATE;
-  return e->hin.push_proposals(n, replica, n_ents, type, cmd_len, cmd);
+  return abi_nomem([&] { return e->hin.push_proposals(n, replica, n_ents, type, cmd_len, cmd); });
 }
 
 int rbe_propose_entries(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint32_t* n_ents,
                         const rbe_entry* ents, const uint8_t* cmd) {
   if (!e) return RBE_E_INVALID;
   if (!e->C.ext_inputs) return RBE_E_STATE;
-  return e->hin.push_entries(n, replica, n_ents, ents, cmd);
+  return abi_nomem([&] { return e->hin.push_entries(n, replica, n_ents, ents, cmd); });
 }
 
 int rbe_push_read_index(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint64_t* lo,
                         const uint64_t* hi) {
   if (!e) return RBE_E_INVALID;
   if (!e->C.ext_inputs) return RBE_E_STATE;
-  return e->hin.push_read_index(n, replica, lo, hi);
+  return abi_nomem([&] { return e->hin.push_read_index(n, replica, lo, hi); });
 }
 
 int rbe_request_leader_transfer(rbe_engine* e, uint64_t n, const uint64_t* replica,
                                 const uint64_t* target) {
   if (!e) return RBE_E_INVALID;
   if (!e->C.ext_inputs) return RBE_E_STATE;
-  return e->hin.request_leader_transfer(n, replica, target);
+  return abi_nomem([&] { return e->hin.request_leader_transfer(n, replica, target); });
 }
 
 int rbe_report_unreachable(rbe_engine* e, uint64_t n, const uint64_t* replica,
                            const uint64_t* node_id) {
   if (!e) return RBE_E_INVALID;
   if (!e->C.ext_inputs) return RBE_E_STATE;
-  return e->hin.report_unreachable(n, replica, node_id);
+  return abi_nomem([&] { return e->hin.report_unreachable(n, replica, node_id); });
 }
 
 int rbe_report_snapshot_status(rbe_engine* e, uint64_t n, const uint64_t* replica,
                                const uint64_t* node_id, const uint8_t* reject) {
   if (!e) return RBE_E_INVALID;
   if (!e->C.ext_inputs) return RBE_E_STATE;
-  return e->hin.report_snapshot_status(n, replica, node_id, reject);
+  return abi_nomem([&] { return e->hin.report_snapshot_status(n, replica, node_id, reject); });
 }
 
 int rbe_launch(rbe_engine* e, uint64_t n, const uint64_t* replica, const rbe_launch_state* st_ids,
@@ -1730,8 +1771,9 @@ int rbe_launch(rbe_engine* e, uint64_t n, const uint64_t* replica, const rbe_lau
   }
   const u64 b_rec = n * sizeof(LaunchRec), b_t = terms.size() * sizeof(u64);
   const u64 bytes = b_rec + b_t + bodies.size() * sizeof(Body) + 64;
-  u8* d = nullptr;
-  HIP_OK(hipMalloc(&d, bytes));
+  rc = grow(&e->gat_dev, &e->gat_dev_bytes, bytes, false);  // (engine scratch, as rbe_replace_node)
+  if (rc) return rc;
+  u8* d = e->gat_dev;
   HIP_OK(hipMemcpyAsync(d, rec.data(), b_rec, hipMemcpyHostToDevice, e->stream));
   if (b_t) {
     HIP_OK(hipMemcpyAsync(d + b_rec, terms.data(), b_t, hipMemcpyHostToDevice, e->stream));
@@ -1752,21 +1794,20 @@ int rbe_launch(rbe_engine* e, uint64_t n, const uint64_t* replica, const rbe_lau
   HIP_OK(hipMemcpyAsync((void*)e->L.scan_round, &e->scan_at, sizeof(u32), hipMemcpyHostToDevice,
                         e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
-  HIP_IGNORE(hipFree(d));
   return rc;
 }
 
 int rbe_set_apply_ready(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint8_t* ready) {
   if (!e) return RBE_E_INVALID;
   if (!e->C.ext_inputs) return RBE_E_STATE;
-  return e->hin.set_apply_ready(n, replica, ready);
+  return abi_nomem([&] { return e->hin.set_apply_ready(n, replica, ready); });
 }
 
 int rbe_propose_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica,
                               const uint32_t* type, const uint64_t* node_id) {
   if (!e) return RBE_E_INVALID;
   if (!e->C.membership || !e->C.ext_inputs) return RBE_E_STATE;
-  return e->hin.propose_config_change(n, replica, type, node_id);
+  return abi_nomem([&] { return e->hin.propose_config_change(n, replica, type, node_id); });
 }
 
 int rbe_apply_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica,
@@ -1780,40 +1821,39 @@ int rbe_apply_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica,
     for (u64 i = 0; i < n; i++)
       if (replica[i] >= e->C.n_rep) return RBE_E_INVALID;
     HIP_OK(hipSetDevice(e->device));
-    std::vector<Core> c(n);
-    std::vector<u16> ro(n);
-    for (u64 i = 0; i < n; i++) {
-      HIP_OK(hipMemcpyAsync(&c[i], e->P.core + replica[i], sizeof(Core), hipMemcpyDeviceToHost,
-                            e->stream));
-      HIP_OK(hipMemcpyAsync(&ro[i], e->P.roles + replica[i], sizeof(u16), hipMemcpyDeviceToHost,
-                            e->stream));
-    }
+    // one gather kernel in the engine's scratch buffer: replicas in, packed
+    // memberships out, one copy each way
+    const u64 ob = (n * sizeof(u64) + 15) & ~15ull;
+    const int rc = grow(&e->gat_dev, &e->gat_dev_bytes, ob + n * sizeof(u32), false);
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(e->gat_dev, replica, n * sizeof(u64), hipMemcpyHostToDevice, e->stream));
+    hipLaunchKernelGGL(k_ms_gather, dim3(grid_for(n)), dim3(kBlock), 0, e->stream, e->P,
+                       (const u64*)e->gat_dev, (u64)n, (u32*)(e->gat_dev + ob));
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(ms.data(), e->gat_dev + ob, n * sizeof(u32), hipMemcpyDeviceToHost,
+                          e->stream));
     HIP_OK(hipStreamSynchronize(e->stream));
-    for (u64 i = 0; i < n; i++) {
-      const u32 x = (c[i].mflags & MB_ROLES) ? ro[i] : 0u;  // Planes::roles valid with MB_ROLES
-      ms[i] = pack_ms(c[i].members & MB_REMOVED, x & 0xFFu, x >> 8);
-    }
   }
-  return e->hin.apply_config_change(n, replica, node_id, type, false, ms.data());
+  return abi_nomem([&] { return e->hin.apply_config_change(n, replica, node_id, type, false, ms.data()); });
 }
 
 int rbe_reject_config_change(rbe_engine* e, uint64_t n, const uint64_t* replica) {
   if (!e) return RBE_E_INVALID;
   if (!e->C.membership || !e->C.ext_inputs) return RBE_E_STATE;
-  return e->hin.apply_config_change(n, replica, nullptr, nullptr, true);
+  return abi_nomem([&] { return e->hin.apply_config_change(n, replica, nullptr, nullptr, true); });
 }
 
 int rbe_snapshot_saved(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint64_t* index,
                        const uint64_t* term, const uint32_t* removed) {
   if (!e) return RBE_E_INVALID;
   if (!e->C.snapshot_entries || !e->C.ext_apply) return RBE_E_STATE;
-  return e->hin.snapshot_op(n, replica, SR_SAVE, index, term, removed, e->C.membership != 0);
+  return abi_nomem([&] { return e->hin.snapshot_op(n, replica, SR_SAVE, index, term, removed, e->C.membership != 0); });
 }
 
 int rbe_compact(rbe_engine* e, uint64_t n, const uint64_t* replica, const uint64_t* to) {
   if (!e) return RBE_E_INVALID;
   if (!e->C.snapshot_entries || !e->C.ext_apply) return RBE_E_STATE;
-  return e->hin.snapshot_op(n, replica, SR_COMPACT, to, nullptr, nullptr, false);
+  return abi_nomem([&] { return e->hin.snapshot_op(n, replica, SR_COMPACT, to, nullptr, nullptr, false); });
 }
 
 int rbe_set_node_ids(rbe_engine* e, uint64_t first_group, uint64_t count, const uint64_t* ids) {
@@ -1846,8 +1886,11 @@ int rbe_replace_node(rbe_engine* e, uint64_t n, const uint64_t* replica, const u
     return RBE_E_STATE;
   if (n == 0) return RBE_OK;
   HIP_OK(hipSetDevice(e->device));
-  u64* d = nullptr;
-  HIP_OK(hipMalloc((void**)&d, n * sizeof(u64) + n * sizeof(u32)));
+  // (the engine's scratch buffer: no allocation per call, nothing to free on
+  // an error path; every user synchronizes before it returns)
+  rc = grow(&e->gat_dev, &e->gat_dev_bytes, n * sizeof(u64) + n * sizeof(u32), false);
+  if (rc) return rc;
+  u64* d = (u64*)e->gat_dev;
   u32* dref = (u32*)(d + n);
   std::vector<u32> refd(n);
   HIP_OK(hipMemcpyAsync(d, replica, n * sizeof(u64), hipMemcpyHostToDevice, e->stream));
@@ -1864,18 +1907,12 @@ int rbe_replace_node(rbe_engine* e, uint64_t n, const uint64_t* replica, const u
     for (u64 i = 0; i < n && !rc; i++)
       if (refd[i]) rc = RBE_E_STATE;
   }
-  if (rc) {
-    HIP_IGNORE(hipFree(d));
-    return rc;
-  }
+  if (rc) return rc;
   for (u64 i = 0; i < n; i++) e->hin.assign_node(e->C.n_groups, replica[i], node_id[i]);
   const u64 bytes = e->hin.ids.size() * sizeof(u64);
   if (!e->P.node_ids) {
     u64* t = nullptr;
-    if (hipMalloc(&t, bytes) != hipSuccess) {
-      HIP_IGNORE(hipFree(d));
-      return RBE_E_NOMEM;
-    }
+    if (hipMalloc(&t, bytes) != hipSuccess) return RBE_E_NOMEM;
     e->allocs.push_back(t);
     e->P.node_ids = t;
     drop_graphs(e);  // kernels take the planes by value
@@ -1899,7 +1936,6 @@ int rbe_replace_node(rbe_engine* e, uint64_t n, const uint64_t* replica, const u
   HIP_OK(hipMemcpyAsync((void*)e->L.scan_round, &e->scan_at, sizeof(u32), hipMemcpyHostToDevice,
                         e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
-  HIP_IGNORE(hipFree(d));
   return rc;
 }
 
@@ -1907,14 +1943,14 @@ int rbe_restore_remotes(rbe_engine* e, uint64_t n, const uint64_t* replica,
                         const uint32_t* n_voters, const uint64_t* voter_ids) {
   if (!e) return RBE_E_INVALID;
   if (!e->C.membership || !e->C.ext_inputs) return RBE_E_STATE;
-  return e->hin.restore_remotes(n, replica, n_voters, voter_ids);
+  return abi_nomem([&] { return e->hin.restore_remotes(n, replica, n_voters, voter_ids); });
 }
 
 int rbe_notify_applied(rbe_engine* e, uint64_t n, const uint64_t* replica,
                        const uint64_t* applied) {
   if (!e) return RBE_E_INVALID;
   if (!e->C.ext_apply) return RBE_E_STATE;
-  return e->hin.notify_applied(n, replica, applied);
+  return abi_nomem([&] { return e->hin.notify_applied(n, replica, applied); });
 }
 
 // Diagnostic: the k_full_list wave records of an RBE_FULL_PROF build since
@@ -2342,7 +2378,7 @@ int rbe_get_update_commits(rbe_engine* e, uint64_t first, uint64_t count, rbe_up
 int rbe_commit(rbe_engine* e, uint64_t n, const uint64_t* replica, const rbe_update_commit* uc) {
   if (!e) return RBE_E_INVALID;
   if (!e->C.ext_commit) return RBE_E_STATE;
-  return e->hin.commit(n, replica, uc);
+  return abi_nomem([&] { return e->hin.commit(n, replica, uc); });
 }
 
 int rbe_get_update_snapshots(rbe_engine* e, uint64_t first, uint64_t count, uint64_t* out4) {

@@ -653,6 +653,10 @@ struct HostInputsT {
   ExtIn& rec(u64 r) {
     SlotMark& m = sm[r];
     if (m.gen != gen) {
+      // (both vectors grow before the slot is marked: a failed allocation
+      // leaves the staging as it was)
+      reps.reserve(reps.size() + 1);
+      recs.reserve(recs.size() + 1);
       m.gen = gen;
       m.slot = (u32)recs.size();
       reps.push_back(r);
@@ -710,6 +714,12 @@ struct HostInputsT {
     if ((rc = check_entries(heap, total, pe, cb, false, &need))) return rc;
     if (ents.size() + total > in_cap) return RBE_E_NOMEM;
     if (need && (rc = heap.room(need))) return rc;
+    // every allocation of the staging below happens here, before anything is
+    // staged (a failure is RBE_E_NOMEM at the ABI with nothing staged)
+    reps.reserve(reps.size() + cnt);
+    recs.reserve(recs.size() + cnt);
+    ents.reserve(ents.size() + total);
+    heap.stage.reserve(heap.stage.size() + need + 16 * total);
     u64 j = 0, off = 0;
     for (u64 i = 0; i < cnt; i++) {
       ExtIn& x = rec(replica[i]);
@@ -785,6 +795,7 @@ struct HostInputsT {
     recs.reserve(n0 + cnt);
     reps.reserve(reps.size() + cnt);
     undo.clear();
+    undo.reserve(cnt);
     for (u64 i = 0; i < cnt; i++) {
       const u64 r = replica[i];
       if (i + 16 < cnt) __builtin_prefetch(&sm[replica[i + 16]], 1);
@@ -845,11 +856,16 @@ struct HostInputsT {
         off += cmd_len[j];
       }
     u64 first = e0;
-    rc = stage_pass(cnt, replica, EXT_PROPOSE, [&](ExtIn& x, u64 i) {
-      x.n_prop = n_ents[i];
-      x.prop_off = (u32)first;
-      first += n_ents[i];
-    });
+    try {
+      rc = stage_pass(cnt, replica, EXT_PROPOSE, [&](ExtIn& x, u64 i) {
+        x.n_prop = n_ents[i];
+        x.prop_off = (u32)first;
+        first += n_ents[i];
+      });
+    } catch (...) {  // (stage_pass allocates before it stages anything)
+      ents.resize(e0);
+      throw;
+    }
     if (rc) ents.resize(e0);
     return rc;
   }

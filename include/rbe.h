@@ -197,12 +197,13 @@ typedef struct rbe_config {
    * each replica's cold log (its entries below the in-memory ring: the ILogDB
    * read path, logentry.go:144-161, 186-246; every entry above the LogDB
    * marker is kept, as dragonboat's LogDB does) and readIndex queues longer
-   * than rq_cap; 0 = 8 KiB per replica, at least 64 MiB, at most 32 GiB.
-   * spill_bytes: the round spill heap per round parity (message lists past
-   * maxm, a message's entries past ecap — a catch-up Replicate sized by
-   * MaxEntrySize, raft.go:709-740 — ReadyToReads past rtr_cap, dropped
-   * ReadIndexes past dri_cap); 0 = 128 B per replica, at least 16 MiB, at most
-   * 4 GiB. */
+   * than rq_cap; 0 = the larger of 8 KiB per replica (at least 64 MiB) and an
+   * eighth of the device's free HBM at rbe_create, at most 32 GiB (rbe_footprint
+   * counts the per-replica part).  spill_bytes: the round spill heap per round
+   * parity (message lists past maxm, a message's entries past ecap — a catch-up
+   * Replicate sized by MaxEntrySize, raft.go:709-740 — ReadyToReads past
+   * rtr_cap, dropped ReadIndexes past dri_cap); 0 = 128 B per replica, at least
+   * 16 MiB, at most 4 GiB (times rep_world: each rank allocates in its own share). */
   uint64_t pool_bytes;
   uint64_t spill_bytes;
 } rbe_config;
@@ -718,8 +719,9 @@ int rbe_collect_updates(rbe_engine* e, uint64_t first, uint64_t count, rbe_updat
  * copied.  With RBE_COLLECT_SKIP_LOCAL an Update whose only content is
  * messages the engine delivers itself (none returned under the flag above) is
  * left out: the node would have nothing to persist, apply, send or report for
- * it (no State change, entries, ReadyToReads, drops, Snapshot, applied index
- * or listener event).  Valid until the next rbe_collect_step, rbe_step/rbe_run
+ * it (no State change, entries, ReadyToReads, drops, Snapshot, applied index,
+ * listener event or fault: a faulted replica's Update is always returned).
+ * Valid until the next rbe_collect_step, rbe_step/rbe_run
  * or rbe_destroy. */
 #define RBE_COLLECT_REMOTE_MSGS 1u
 #define RBE_COLLECT_SKIP_LOCAL 2u

@@ -29,7 +29,7 @@ from parity_util import C2, view_diff
 from session_util import check_entry_records, check_outbox_decodes
 from transport_util import owner, run_transport
 
-DRIVEN = dict(maxm=40, ecap=64, rq_cap=32)
+DRIVEN = dict()
 
 
 def _pair(make, kw, heap_bytes=64 << 20, **eng_more):
@@ -140,7 +140,7 @@ def heap_never_laps(make):
     lives until it is saved and applied).  Once the state machine catches
     up, the heap takes proposals again."""
     kw = dict(C2, n_groups=2, ext_inputs=True, ext_apply=True)
-    eng, ref = _pair(make, kw, heap_bytes=96 << 10, ring=256)
+    eng, ref = _pair(make, kw, heap_bytes=96 << 10)
     rng = random.Random(3)
     leaders = []
     pushed, nomem = {}, 0

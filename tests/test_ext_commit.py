@@ -13,7 +13,7 @@ from dragonboat_amd.engine import InputError, RBE_E_STATE
 from parity_util import C2, C3, C3_HOT, C4
 from soa_cpu.soa import SoaCpu
 
-DRIVEN = dict(maxm=40, ecap=64, rq_cap=32, ring=256)
+DRIVEN = dict()
 
 
 def _pair(kw):
@@ -88,7 +88,7 @@ def test_commit_panics_fault_the_replica():
 # restoring step carries the snapshot until a commit names it
 SNAP_COMMIT = dict(ext_inputs=True, ext_apply=True, ext_commit=True, snapshot_entries=1)
 SNAP_CASES = {"C3_HOT": dict(C3_HOT, n_groups=16), "C3_N7": dict(C3, n_groups=12, n_replicas=7)}
-SNAP_SIZES = dict(maxm=40, ecap=256, rq_cap=32, ring=128)
+SNAP_SIZES = dict()
 
 
 @pytest.mark.parametrize("name", list(SNAP_CASES))

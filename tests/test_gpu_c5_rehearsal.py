@@ -23,7 +23,7 @@ pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 C5_KW = dict(n_groups=1_000_000, n_replicas=3, wl_enabled=True, wl_start_round=30)
-EXTRA = dict(ring=64, rep_compact=True)
+EXTRA = dict(rep_compact=True)
 ROUNDS, CHECKS, CAL_AT = 90, (60, 90), 45
 KEEP = ["role", "term", "committed", "processed", "last_index"]
 

@@ -13,7 +13,7 @@ from test_ext_commit import SNAP_CASES, SNAP_COMMIT, SNAP_SIZES
 
 pytestmark = pytest.mark.gpu
 
-DRIVEN = dict(maxm=40, ecap=64, rq_cap=32, ring=256)
+DRIVEN = dict()
 
 
 @pytest.mark.parametrize("name,kw", [("C2", C2), ("C3", C3), ("C4", C4),
@@ -21,7 +21,7 @@ DRIVEN = dict(maxm=40, ecap=64, rq_cap=32, ring=256)
 def test_gpu_delayed_persist_parity(gpu_available, name, kw):
     from dragonboat_amd.engine import Engine
     base = dict(kw, n_groups=12, ext_inputs=True, ext_apply=True, ext_commit=True)
-    sizes = dict(DRIVEN, ecap=256) if base["n_replicas"] > 5 else DRIVEN  # tests/test_ext_commit.py
+    sizes = dict(DRIVEN) if base["n_replicas"] > 5 else DRIVEN  # tests/test_ext_commit.py
     eng, ref = Engine(device=0, trace=True, **dict(base, **sizes)), O.Harness(**base)
     d, st = run_commit_driven(eng, ref, 160, seed=5)
     assert d is None, f"{name}: first divergence {d}"

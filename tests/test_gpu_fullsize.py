@@ -26,7 +26,7 @@ C4_FULL = dict(n_groups=1_000_000, n_replicas=3, quiesce=True, wl_enabled=True,
 C3_FULL = dict(n_groups=100_000, n_replicas=5, check_quorum=True, wl_enabled=True,
                wl_start_round=40, iso_period=50, iso_len=30, iso_mod=10)
 C2_FULL = dict(n_groups=10_000, n_replicas=3, wl_enabled=True, wl_start_round=30)
-ENGINE = {"C4": dict(ring=64), "C3": dict(ring=128, ecap=256), "C2": dict(ring=64)}
+ENGINE = {"C4": dict(), "C3": dict(), "C2": dict()}
 SAMPLE = {"C4": 48, "C3": 48, "C2": 160}
 FIELDS = [f for f in O.VIEW_FIELDS if f != "digest"]
 

@@ -11,7 +11,7 @@ from parity_util import C2, C3, C4, run_lockstep
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name,kw,extra", [("C2", C2, {}), ("C3", C3, dict(ring=128)),
+@pytest.mark.parametrize("name,kw,extra", [("C2", C2, {}), ("C3", C3, dict()),
                                            ("C4", C4, {})])
 def test_gpu_restart_continues_with_oracle(gpu_available, name, kw, extra):
     from dragonboat_amd.engine import Engine
@@ -44,7 +44,7 @@ def test_gpu_restart_untraced_group_sleep(gpu_available):
 def test_gpu_restart_with_lagging_applied(gpu_available):
     from dragonboat_amd.engine import Engine
     kw = dict(C2, n_groups=8, ext_inputs=True, ext_apply=True)
-    eng = Engine(device=0, trace=True, **dict(kw, maxm=40, ecap=64, rq_cap=32, ring=256))
+    eng = Engine(device=0, trace=True, **dict(kw))
     ref = O.Harness(**kw)
 
     def hook(rnd):

@@ -41,7 +41,7 @@ def test_gpu_membership_untraced(gpu_available):
 def test_gpu_host_config_changes(gpu_available):
     from dragonboat_amd.engine import Engine
     kw = dict(C2, n_groups=6, ext_inputs=True, ext_apply=True, membership=True)
-    eng = Engine(device=0, trace=True, **dict(kw, maxm=40, ecap=256, rq_cap=32, ring=256))
+    eng = Engine(device=0, trace=True, **dict(kw))
     ref = O.Harness(**kw)
     rng = random.Random(3)
     n = kw["n_replicas"]

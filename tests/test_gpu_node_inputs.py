@@ -12,9 +12,9 @@ from parity_util import C2, C3, C4, MIXED, run_lockstep, counters_match
 
 pytestmark = pytest.mark.gpu
 
-EXTRA = {"C3": dict(ring=128), "C3_N7": dict(ring=128), "MIXED": dict(ring=128, rq_cap=64, maxm=24)}
-DRIVEN = dict(maxm=40, ecap=64, rq_cap=32)  # see tests/test_node_inputs.py
-DRIVEN_BY_NAME = {"C3_N7": dict(ecap=256)}
+EXTRA = {"C3": dict(), "C3_N7": dict(), "MIXED": dict()}
+DRIVEN = dict()  # see tests/test_node_inputs.py
+DRIVEN_BY_NAME = {"C3_N7": dict()}
 N7 = ("C3_N7", dict(C3, n_groups=24, n_replicas=7))
 
 
@@ -54,7 +54,7 @@ def test_gpu_apply_ready_gate(gpu_available):
     from dragonboat_amd.engine import Engine
     kw = dict(C2, n_groups=12, ext_inputs=True, ext_apply=True)
     # a held replica's unapplied entries must stay in the device window
-    eng = Engine(device=0, trace=True, ring=256, **dict(kw, **dict(DRIVEN, ecap=256)))
+    eng = Engine(device=0, trace=True, **dict(kw, **dict(DRIVEN)))
     ref = O.Harness(**kw)
     d = run_driven(eng, ref, 200, seed=13, ext_apply=True, ready=0.2)
     assert d is None, f"first divergence {d}"

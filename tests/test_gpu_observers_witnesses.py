@@ -54,7 +54,7 @@ def test_gpu_host_cannot_put_a_node_in_two_sets(gpu_available):
     from parity_util import C2
     kw = dict(C2, n_groups=2, n_replicas=5, n_voters=3, observer_slots=0b01000,
               witness_slots=0b10000, ext_inputs=True, ext_apply=True, membership=True)
-    eng = Engine(device=0, trace=True, **dict(kw, maxm=40, ecap=256, rq_cap=32, ring=256))
+    eng = Engine(device=0, trace=True, **dict(kw))
     eng.run(30)
     eng.apply_config_change([0], [4], [O.CC_ADD_OBSERVER])
     eng.step()

@@ -31,7 +31,7 @@ def _check(eng, first, count):
     return len(msgs), len(rtrs)
 
 
-@pytest.mark.parametrize("name,kw,extra", [("C2", C2, {}), ("C3", C3, dict(ring=128)),
+@pytest.mark.parametrize("name,kw,extra", [("C2", C2, {}), ("C3", C3, dict()),
                                            ("C4", C4, {})])
 def test_gpu_collect_outputs_match_per_replica(gpu_available, name, kw, extra):
     from dragonboat_amd.engine import Engine
@@ -65,7 +65,7 @@ def test_gpu_collect_outputs_large(gpu_available):
     eng.close()
 
 
-@pytest.mark.parametrize("name,kw,extra", [("C3", C3, dict(ring=128)), ("C4", C4, {})])
+@pytest.mark.parametrize("name,kw,extra", [("C3", C3, dict()), ("C4", C4, {})])
 def test_gpu_collect_updates_match_per_replica(gpu_available, name, kw, extra):
     """rbe_collect_updates returns exactly the replicas whose rbe_get_updates
     record has RBE_UF_HAS_UPDATE, ascending, each with the same record."""
@@ -102,7 +102,7 @@ def test_gpu_collect_updates_large(gpu_available):
     eng.close()
 
 
-@pytest.mark.parametrize("name,kw,extra", [("C3", C3, dict(ring=128)), ("C4", C4, {})])
+@pytest.mark.parametrize("name,kw,extra", [("C3", C3, dict()), ("C4", C4, {})])
 def test_gpu_collect_outputs_match_oracle(gpu_available, name, kw, extra):
     """rbe_collect_outputs against the oracle harness itself, not the engine's
     own getters: every sender's messages of the round, per destination, equal
@@ -140,7 +140,7 @@ def test_gpu_collect_outputs_match_oracle(gpu_available, name, kw, extra):
     eng.close()
 
 
-@pytest.mark.parametrize("name,kw,extra", [("C2", C2, {}), ("C3", C3, dict(ring=128)),
+@pytest.mark.parametrize("name,kw,extra", [("C2", C2, {}), ("C3", C3, dict()),
                                            ("C4", C4, {})])
 def test_gpu_collect_step_matches(gpu_available, name, kw, extra):
     """rbe_collect_step: the Updates of rbe_collect_updates, and for exactly

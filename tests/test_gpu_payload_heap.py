@@ -15,7 +15,7 @@ from parity_util import C2, C3
 
 pytestmark = pytest.mark.gpu
 
-DRIVEN = dict(maxm=40, ecap=64, rq_cap=32)
+DRIVEN = dict()
 
 
 @pytest.mark.parametrize("name,kw,mes", [("C2", C2, 0), ("C2-small-batches", C2, 9000),

@@ -57,7 +57,7 @@ def test_gpu_rate_limiter_ext_commit(gpu_available):
     from parity_util import C3
     kw = dict(C3, n_groups=12, ext_inputs=True, ext_apply=True, ext_commit=True,
               max_inmem_log_size=400)
-    eng = Engine(device=0, trace=True, maxm=40, ecap=64, rq_cap=32, ring=256, **kw)
+    eng = Engine(device=0, trace=True, **kw)
     ref = O.Harness(**kw)
     d, st = run_commit_driven(eng, ref, 160, seed=5)
     assert d is None, f"first divergence {d}"

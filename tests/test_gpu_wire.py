@@ -19,10 +19,10 @@ def _engine(**kw):
 
 
 @pytest.mark.parametrize("name,kw,extra,gpb", [
-    ("C2", C2, {}, 16), ("C3", C3, dict(ring=128), 0), ("C4", C4, {}, 7),
+    ("C2", C2, {}, 16), ("C3", C3, dict(), 0), ("C4", C4, {}, 7),
     ("C3_SNAP", dict(C3, check_quorum=False, snapshot_entries=20, compaction_overhead=5),
-     dict(ring=128), 5),
-    ("C3_N7", dict(C3, n_groups=20, n_replicas=7), dict(ring=128), 5)])
+     dict(), 5),
+    ("C3_N7", dict(C3, n_groups=20, n_replicas=7), dict(), 5)])
 def test_gpu_wire_encode_decode(gpu_available, name, kw, extra, gpb):
     eng = _engine(**kw, **extra)
     n, G = kw["n_replicas"], kw["n_groups"]

@@ -21,7 +21,7 @@ SIZES = [1, 2, 3, 4, 5, 6, 7]
 def shapes(n):
     return {
         "C2": (dict(C2, n_groups=16, n_replicas=n), {}, 150),
-        "C3": (dict(C3, n_groups=16, n_replicas=n, iso_mod=2), dict(ring=128), 260),
+        "C3": (dict(C3, n_groups=16, n_replicas=n, iso_mod=2), dict(), 260),
         "C4": (dict(C4, n_groups=30, n_replicas=n, wl_active_mod=2), {}, 200),
     }
 

@@ -20,7 +20,7 @@ from parity_util import C3, C3_HOT, counters_match, view_diff
 from soa_cpu.soa import SoaCpu
 
 HOST_SNAP = dict(ext_inputs=True, ext_apply=True, snapshot_entries=1)
-DRIVE = dict(maxm=40, ecap=256, rq_cap=32, ring=128)
+DRIVE = dict()
 CASES = {
     "C3": dict(C3, n_groups=16, **HOST_SNAP),
     "C3_HOT": dict(C3_HOT, n_groups=16, **HOST_SNAP),

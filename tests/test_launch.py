@@ -19,7 +19,7 @@ def _leaders(views):
     return [i for i, v in enumerate(views) if v.role == O.LEADER]
 
 
-@pytest.mark.parametrize("name,kw,extra", [("C2", C2, {}), ("C3", C3, dict(ring=128))])
+@pytest.mark.parametrize("name,kw,extra", [("C2", C2, {}), ("C3", C3, dict())])
 def test_restart_continues_with_oracle(name, kw, extra):
     kw = dict(kw, n_groups=10)
     eng, ref = SoaCpu(trace=True, **dict(kw, **extra)), O.Harness(**kw)
@@ -39,7 +39,7 @@ def test_restart_with_lagging_applied():
     kw = dict(C2, n_groups=8, ext_inputs=True, ext_apply=True)
     # a restarted replica applies its log again from index 1 (processed =
     # firstIndex - 1): the window must still hold it
-    dr = dict(maxm=40, ecap=64, rq_cap=32, ring=256)
+    dr = dict()
     eng, ref = SoaCpu(trace=True, **dict(kw, **dr)), O.Harness(**kw)
 
     def hook(rnd):

@@ -21,19 +21,19 @@ from soa_cpu.soa import SoaCpu
 SNAP = dict(snapshot_entries=20, compaction_overhead=5)
 CASES = {
     # isolation epochs of 30 rounds leave the cut-off replica > 25 entries behind
-    "C3_SNAP": (dict(C3, **SNAP), dict(ring=128), 400),
+    "C3_SNAP": (dict(C3, **SNAP), dict(), 400),
     "C3_HOT_SNAP": (dict(C3, iso_mod=2, snapshot_entries=8, compaction_overhead=2),
-                    dict(ring=128), 400),
+                    dict(), 400),
     # no check-quorum: an isolated remote stays active, so the leader streams it
     # snapshots the transport fails (SnapshotStatus reject, clearPendingSnapshot)
-    "C3_NOCQ_SNAP": (dict(C3, check_quorum=False, **SNAP), dict(ring=128), 400),
+    "C3_NOCQ_SNAP": (dict(C3, check_quorum=False, **SNAP), dict(), 400),
     # a 64-entry window and 100-round partitions, fault-free
-    "C3_R64_ISO100": (dict(C3, iso_period=150, iso_len=100, **SNAP), dict(ring=64), 600),
+    "C3_R64_ISO100": (dict(C3, iso_period=150, iso_len=100, **SNAP), dict(), 600),
     "MIXED_SNAP": (dict(MIXED, snapshot_entries=10, compaction_overhead=0),
-                   dict(ring=128, rq_cap=64, maxm=24), 500),
+                   dict(), 500),
     "C4_SNAP": (dict(C4, **SNAP), {}, 400),
     # groups of 7 (slot 6's outbox word in the sender's own place), leaders isolated
-    "N7_SNAP": (dict(C3, n_groups=24, n_replicas=7, iso_mod=2, **SNAP), dict(ring=128), 400),
+    "N7_SNAP": (dict(C3, n_groups=24, n_replicas=7, iso_mod=2, **SNAP), dict(), 400),
 }
 
 
@@ -112,7 +112,7 @@ def test_compaction_launch_checks():
     commit lies below the marker (loadState panics, raft.go:429-437), when
     entries reach down to the marker, or when there is no snapshot plane."""
     from dragonboat_amd.engine import RBE_E_INVALID, InputError
-    eng = SoaCpu(trace=True, **dict(C3, **SNAP), ring=128)
+    eng = SoaCpu(trace=True, **dict(C3, **SNAP))
     eng.run(5)
     ents = [[(i, 2, 0, b"") for i in range(11, 21)]]
     with pytest.raises(InputError) as ei:  # commit below the marker
@@ -122,7 +122,7 @@ def test_compaction_launch_checks():
         eng.launch([0], [(2, 0, 12, 20, 10, 2, 10, 2)], [[(i, 2, 0, b"") for i in range(10, 21)]])
     with pytest.raises(InputError):  # a marker without its term
         eng.launch([0], [(2, 0, 12, 20, 10, 0, 10, 2)], ents)
-    plain = SoaCpu(trace=True, **C3, ring=128)
+    plain = SoaCpu(trace=True, **C3)
     with pytest.raises(InputError):  # no snapshots configured
         plain.launch([0], [(2, 0, 12, 20, 10, 2, 10, 2)], ents)
     eng.launch([0], [(2, 0, 12, 20, 10, 2, 10, 2)], ents)

@@ -28,7 +28,7 @@ from soa_cpu.soa import SoaCpu
 # a voter added back is caught up from far behind in one Replicate: the entry
 # arena and the in-memory window hold that many entries (the reference has no
 # such capacities; the engine flags F_ARENA / F_WINDOW instead)
-CATCHUP = dict(ring=512, ecap=1024, maxm=24, rq_cap=64)
+CATCHUP = dict()
 EXTRA = {"C3": CATCHUP, "MIXED": CATCHUP, "C2": CATCHUP}
 MEMB = dict(membership=True, cc_period=10, cc_mod=1)
 
@@ -74,7 +74,7 @@ def test_host_config_changes():
     rbe_reject_config_change), both sides driven identically."""
     import random
     kw = dict(C2, n_groups=6, ext_inputs=True, ext_apply=True, membership=True)
-    eng = SoaCpu(trace=True, **dict(kw, maxm=40, ecap=256, rq_cap=32, ring=256))
+    eng = SoaCpu(trace=True, **dict(kw))
     ref = O.Harness(**kw)
     rng = random.Random(3)
     n = kw["n_replicas"]

@@ -23,16 +23,16 @@ from input_util import run_driven
 from parity_util import C2, C3, C4, MIXED, run_lockstep
 from soa_cpu.soa import SoaCpu
 
-EXTRA = {"C3": dict(ring=128), "C3_N7": dict(ring=128), "MIXED": dict(ring=128, rq_cap=64, maxm=24)}
+EXTRA = {"C3": dict(), "C3_N7": dict(), "MIXED": dict()}
 
 
 # Host-driven rounds put more traffic on one (sender, destination) stream than
 # the lockstep workloads (a forwarded ReadIndex each triggers a heartbeat
 # broadcast, every forwarded proposal a Replicate): the per-round message and
 # entry capacities are raised so the test exercises the protocol, not F_OUTBOX.
-DRIVEN = dict(maxm=40, ecap=64, rq_cap=32)
+DRIVEN = dict()
 # a leader of 7 copies a range for each of six remotes in one round
-DRIVEN_BY_NAME = {"C3_N7": dict(ecap=256)}
+DRIVEN_BY_NAME = {"C3_N7": dict()}
 
 
 def _pair(kw, name="", **more):
@@ -74,7 +74,7 @@ def test_apply_ready_gate(name, kw):
     kw = dict(kw, n_groups=12)
     eng, ref = _pair(kw, name, ext_inputs=True, ext_apply=True)
     # a held replica's unapplied entries must stay in the device window
-    eng = SoaCpu(trace=True, **dict(kw, ext_inputs=True, ext_apply=True, **dict(DRIVEN, ecap=256), ring=256))
+    eng = SoaCpu(trace=True, **dict(kw, ext_inputs=True, ext_apply=True, **dict(DRIVEN)))
     d = run_driven(eng, ref, 200, seed=13, ext_apply=True, ready=0.2)
     assert d is None, f"{name}: first divergence {d}"
     assert eng.faults()[0] == 0

@@ -49,7 +49,7 @@ OW_CASES = {
 # engine sizes per case: in N7 the witness joins after ~370 rounds and catches up
 # from index 1 in one Replicate, so the ring and the round's arena hold all of it
 # (the default sizes fault it with F_ARENA, a capacity limit the reference lacks)
-SIZES = {"N7": dict(CATCHUP, ring=1024, ecap=1024)}
+SIZES = {"N7": dict(CATCHUP)}
 
 
 def _roles_seen(ref):
@@ -179,7 +179,7 @@ def test_host_applies_roles():
     from input_util import run_driven
     kw = dict(C2, n_groups=6, n_replicas=5, n_voters=3, observer_slots=0b01000,
               witness_slots=0b10000, ext_inputs=True, ext_apply=True, membership=True)
-    eng = SoaCpu(trace=True, **dict(kw, maxm=40, ecap=256, rq_cap=32, ring=256))
+    eng = SoaCpu(trace=True, **dict(kw))
     ref = O.Harness(**kw)
     rng = random.Random(8)
     n = kw["n_replicas"]
@@ -234,7 +234,7 @@ def test_host_cannot_put_a_node_in_two_sets():
     from dragonboat_amd.engine import InputError, RBE_E_INVALID
     kw = dict(C2, n_groups=2, n_replicas=5, n_voters=3, observer_slots=0b01000,
               witness_slots=0b10000, ext_inputs=True, ext_apply=True, membership=True)
-    eng = SoaCpu(trace=True, **dict(kw, maxm=40, ecap=256, rq_cap=32, ring=256))
+    eng = SoaCpu(trace=True, **dict(kw))
     eng.run(30)
     # node 4 (observer slot) becomes an observer at replica 0, node 5 a witness
     eng.apply_config_change([0], [4], [O.CC_ADD_OBSERVER])

@@ -18,7 +18,7 @@ from input_util import run_driven
 from parity_util import C2, C3
 from soa_cpu.soa import SoaCpu
 
-DRIVEN = dict(maxm=40, ecap=64, rq_cap=32)
+DRIVEN = dict()
 
 
 def _pair(kw, heap_bytes, **eng_more):

@@ -85,7 +85,7 @@ def test_rate_limiter_ext_commit(name):
     from parity_util import C3
     kw = dict({"C2": C2, "C3": C3}[name], n_groups=12, ext_inputs=True, ext_apply=True,
               ext_commit=True, max_inmem_log_size=400)
-    eng = SoaCpu(trace=True, maxm=40, ecap=64, rq_cap=32, ring=256, **kw)
+    eng = SoaCpu(trace=True, **kw)
     ref = O.Harness(**kw)
     # views and trace digests (RateLimit Hints) every round, the limiters at the end
     d, st = run_commit_driven(eng, ref, 160, seed=5)

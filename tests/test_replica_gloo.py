@@ -25,16 +25,16 @@ CASES = {
     # 5 replicas, check-quorum, elections from scratch, over 4 ranks
     "N5_w4": (dict(n_groups=16, n_replicas=5, check_quorum=True, quiesce=True, wl_enabled=True,
                    wl_start_round=25, wl_active_mod=2, wl_read_permille=500, seed=777), 4, 300,
-              dict(ring=128, rq_cap=64, maxm=24)),
+              dict()),
     # C3 with its isolation schedule (leaders cut off for 30 of every 50
     # rounds): each rank knows only its own replicas' roles, so the epoch's
     # leader bits are ORed over ranks before the step (ReplicaExchange.iso_sync)
     "C3_iso_w2": (dict(n_groups=20, n_replicas=5, check_quorum=True, wl_enabled=True,
                        wl_start_round=40, iso_period=50, iso_len=30, iso_mod=3), 2, 300,
-                  dict(ring=128)),
+                  dict()),
     "C3_iso_w4": (dict(n_groups=20, n_replicas=5, check_quorum=True, wl_enabled=True,
                        wl_start_round=40, iso_period=50, iso_len=30, iso_mod=3), 4, 300,
-                  dict(ring=128)),
+                  dict()),
     # compacted planes (rep_compact): 3 replicas over 4 ranks, each rank holds
     # the 3/4 of the groups it steps a replica of (W = 8: 3/8); n_groups not a
     # multiple of W leaves padding groups; the second case adds the isolation
@@ -43,12 +43,12 @@ CASES = {
     # place of the 6-word outbox header (cnt_widx)
     "N7_w3": (dict(n_groups=12, n_replicas=7, check_quorum=True, quiesce=True, wl_enabled=True,
                    wl_start_round=25, wl_active_mod=2, wl_read_permille=500, iso_period=41,
-                   iso_len=20, iso_mod=2), 3, 300, dict(ring=128, rq_cap=64, maxm=24)),
+                   iso_len=20, iso_mod=2), 3, 300, dict()),
     "C2_w4c": (dict(n_groups=22, n_replicas=3, wl_enabled=True, wl_start_round=30), 4, 200,
                dict(rep_compact=True)),
     "C3_iso_w4c": (dict(n_groups=22, n_replicas=3, check_quorum=True, wl_enabled=True,
                         wl_start_round=40, iso_period=50, iso_len=30, iso_mod=3), 4, 300,
-                   dict(ring=128, rep_compact=True)),
+                   dict(rep_compact=True)),
 }
 CHECK_EVERY = 50
 

@@ -43,8 +43,8 @@ def test_partial_import_overwrites_only_its_groups():
     proposals); importing A's groups [5, 17) into B makes exactly those groups
     equal A's, and leaves B's others alone."""
     kw = dict(C3, ext_inputs=True)
-    a = SoaCpu(trace=True, **kw, ring=128)
-    b = SoaCpu(trace=True, **kw, ring=128)
+    a = SoaCpu(trace=True, **kw)
+    b = SoaCpu(trace=True, **kw)
     a.run(89)
     b.run(88)
     # B diverges through host-pushed proposals at every replica of every group
@@ -114,7 +114,7 @@ def test_snapshot_errors():
         a.import_groups(snap, resume=True)
     assert ei.value.rc == RBE_E_INVALID
     # geometry mismatch (ring), truncation, corrupted magic
-    b = SoaCpu(trace=True, **C2, ring=128)
+    b = SoaCpu(trace=True, **C2, ring=128)  # (another geometry)
     b.run(10)
     for bad in (snap, snap[:-1], b"\0" * 8 + snap[8:]):
         with pytest.raises(SnapshotError) as ei:

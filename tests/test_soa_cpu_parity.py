@@ -101,7 +101,7 @@ def test_check_quorum_ticks_stay_on_fast_path():
     step takes it (rbe_fast.h), so a steady C3 group leaves the fast kernels
     only for its first election."""
     kw = dict(C3, iso_period=0)
-    eng = SoaCpu(trace=True, ring=128, **kw)
+    eng = SoaCpu(trace=True, **kw)
     ref = O.Harness(**kw)
     assert run_lockstep(eng, ref, 300, every=1) is None
     assert eng.slow_total() < 0.03 * eng.counters()["steps"]

@@ -20,11 +20,11 @@ CASES = {
     # which an engine stepping only some of them does not have)
     "N5_w4": (dict(n_groups=8, n_replicas=5, check_quorum=True, quiesce=True, wl_enabled=True,
                    wl_start_round=25, wl_active_mod=2, wl_read_permille=500, seed=777), 4, 300,
-              dict(ring=128, rq_cap=64, maxm=24)),
+              dict()),
     # the isolation schedule with every replica of a group on another engine
     "C3_iso_w3": (dict(n_groups=12, n_replicas=5, check_quorum=True, wl_enabled=True,
                        wl_start_round=40, iso_period=50, iso_len=30, iso_mod=3), 3, 250,
-                  dict(ring=128)),
+                  dict()),
 }
 
 

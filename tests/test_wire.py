@@ -88,9 +88,9 @@ def test_message_batch_frame_round_trip():
         W.frames_decode(bytes(bad))
 
 
-@pytest.mark.parametrize("name,kw,gpb", [("C2", C2, 16), ("C3", dict(C3, ring=128), 0),
+@pytest.mark.parametrize("name,kw,gpb", [("C2", C2, 16), ("C3", dict(C3), 0),
                                          ("C4", C4, 7),
-                                         ("C3_N7", dict(C3, n_groups=20, n_replicas=7, ring=128), 5)])
+                                         ("C3_N7", dict(C3, n_groups=20, n_replicas=7), 5)])
 def test_host_build_frames_match_oracle(name, kw, gpb):
     eng = SoaCpu(trace=True, **kw)
     n, G = kw["n_replicas"], kw["n_groups"]
@@ -113,7 +113,7 @@ def test_host_build_frames_with_snapshots_and_heap_cmds():
     from heap_util import mixed_cmd
     kw = dict(C3, check_quorum=False, snapshot_entries=20, compaction_overhead=5,
               n_groups=8, ext_inputs=True, wl_enabled=False)
-    eng = SoaCpu(trace=True, ring=128, heap_bytes=8 << 20, **kw)
+    eng = SoaCpu(trace=True, heap_bytes=8 << 20, **kw)
     n, G = kw["n_replicas"], kw["n_groups"]
     rng = random.Random(21)
     saw_is = saw_long = 0
