@@ -725,9 +725,11 @@ def main():
     round_bytes = alg_bytes(c) / args.steps
     round_gbs = round_bytes / ((ev_ms / 1e3) / args.steps) / 1e9
 
-    # per-kernel split: a further `prof_rounds` rounds, one at a time, with
-    # HIP events between the pipeline kernels on the engine stream and each
-    # kernel's own counters -> the dominant kernel's roofline
+    # per-kernel split: a further `prof_rounds` rounds, one at a time, each
+    # kernel launched with a start / stop HIP event pair its own dispatch
+    # stamps (hipExtLaunchKernel, on the engine stream: the kernel's execution
+    # as rocprofv3 times it) and each kernel's own counters -> the dominant
+    # kernel's roofline
     prof_rounds = max(1, min(args.steps, args.prof_rounds))
     eng.reset_counters()
     kms = eng.profile_rounds(prof_rounds)

@@ -1664,8 +1664,10 @@ int rbe_run_timed(rbe_engine* e, uint32_t rounds, float* ms) {
 int rbe_profile_rounds(rbe_engine* e, uint32_t rounds, float* ms_per_kernel) {
   if (!e || !ms_per_kernel || rounds == 0) return RBE_E_INVALID;
   HIP_OK(hipSetDevice(e->device));
-  hipEvent_t ev[KS_NUM + 1];
-  for (int i = 0; i <= KS_NUM; i++) HIP_OK(hipEventCreate(&ev[i]));
+  // a start / stop pair per kernel section, stamped by the kernel's own
+  // dispatch (hipExtLaunchKernel in launch_round): kernel time, not the gaps
+  hipEvent_t ev[2 * KS_NUM];
+  for (int i = 0; i < 2 * KS_NUM; i++) HIP_OK(hipEventCreate(&ev[i]));
   for (int i = 0; i < KS_NUM; i++) ms_per_kernel[i] = 0.f;
   int rc = RBE_OK;
   for (u32 k = 0; k < rounds && rc == RBE_OK; k++) {
@@ -1675,16 +1677,16 @@ int rbe_profile_rounds(rbe_engine* e, uint32_t rounds, float* ms_per_kernel) {
     if (rc) break;
     e->round++;
     e->tclk++;
-    if (hipEventSynchronize(ev[KS_NUM]) != hipSuccess) {
+    if (hipStreamSynchronize(e->stream) != hipSuccess) {
       rc = RBE_E_HIP;
       break;
     }
     for (int i = 0; i < KS_NUM; i++) {
       float ms = 0.f;
-      if (hipEventElapsedTime(&ms, ev[i], ev[i + 1]) == hipSuccess) ms_per_kernel[i] += ms;
+      if (hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]) == hipSuccess) ms_per_kernel[i] += ms;
     }
   }
-  for (int i = 0; i <= KS_NUM; i++) HIP_IGNORE(hipEventDestroy(ev[i]));
+  for (int i = 0; i < 2 * KS_NUM; i++) HIP_IGNORE(hipEventDestroy(ev[i]));
   return rc;
 }
 
@@ -2092,6 +2094,7 @@ int rbe_xchg_status(rbe_engine* e, uint32_t* overflow) {
   HIP_OK(hipSetDevice(e->device));
   HIP_OK(hipMemcpyAsync(overflow, e->xcount + kXchgMaxWorld * XS_NUM, sizeof(u32),
                         hipMemcpyDeviceToHost, e->stream));
+  HIP_OK(hipMemsetAsync(e->xcount + kXchgMaxWorld * XS_NUM, 0, sizeof(u32), e->stream));
   HIP_OK(hipStreamSynchronize(e->stream));
   return RBE_OK;
 }

@@ -654,7 +654,11 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   // log (rbe_spill.h) unless compacted; its record and the cold-log ref now
   const u64 lmark = C.snapshot_entries ? P.snp[r].marker : 0;
   const u64 ev_idx = c.last_index + 1 > C.ring ? c.last_index + 1 - C.ring : 0;
+#ifdef RBE_DIAG_NO_EVICT  // timing-only build: the evicted entry is dropped (wrong below the ring)
+  const bool ev = false;
+#else
   const bool ev = inp == 1 && ev_idx > lmark;
+#endif
   Ent ev_e;
   ColdRef ev_cr;
   ev_e.term = ev_e.lo = ev_e.hi = 0;
@@ -1391,7 +1395,11 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   // record and the cold-log ref now, with the messages
   const u64 lmark = C.snapshot_entries ? P.snp[r].marker : 0;
   const u64 ev_idx = c.last_index + 1 > C.ring ? c.last_index + 1 - C.ring : 0;
+#ifdef RBE_DIAG_NO_EVICT
+  const bool ev = false;
+#else
   const bool ev = na > 0 && ev_idx > lmark;
+#endif
   bool ev_app = false;
   Ent ev_e;
   ColdRef ev_cr;

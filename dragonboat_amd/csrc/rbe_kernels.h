@@ -6,6 +6,7 @@
 // instantiations of launch_round<N, TRACE>, so the heavy per-N kernel code
 // builds in parallel translation units.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -905,86 +906,66 @@ extern unsigned g_fast_grid;
 static constexpr unsigned kFullGrid = RBE_FULL_GRID;  // k_full_list's grid in 256-thread units: its ~490 registers allow one wave per SIMD, so 256 x 4 one-wave blocks fill the chip once
 static inline unsigned grid_for(u64 n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
-// One round's launches.  With `ev` (KS_NUM + 1 events) an event is recorded
-// on the engine stream before the first and after every pipeline kernel, so
-// ev[i]..ev[i+1] brackets kernel section i (rbe_profile_rounds).
+// One round's launches.  With `ev` (2 * KS_NUM events) every pipeline kernel
+// is launched with hipExtLaunchKernel, which stamps ev[2i] / ev[2i + 1] with
+// kernel section i's own start and end (the dispatch packet's timestamps, as
+// rocprofv3 reads them), so rbe_profile_rounds times the kernels without the
+// launch gaps between them; a section with no kernel in the mode gets both
+// events at one point (elapsed 0).
+#define RBE_LAUNCH(i, K, G, B, ...)                                                         \
+  do {                                                                                      \
+    if (ev)                                                                                 \
+      hipExtLaunchKernelGGL(K, G, B, 0, stream, ev[2 * (i)], ev[2 * (i) + 1], 0, __VA_ARGS__); \
+    else                                                                                    \
+      hipLaunchKernelGGL(K, G, B, 0, stream, __VA_ARGS__);                                  \
+  } while (0)
 template <int N, bool TRACE>
 int launch_round(const Planes& P, const Params& C, const Lists& L, hipStream_t stream, int mode,
                  RoundArg ra, hipEvent_t* ev) {
   const unsigned g = grid_for(C.n_rep);
-  auto mark = [&](int i) {
-    if (ev) HIP_IGNORE(hipEventRecord(ev[i], stream));
+  auto none = [&](int i) {  // an empty section
+    if (ev) {
+      HIP_IGNORE(hipEventRecord(ev[2 * i], stream));
+      HIP_IGNORE(hipEventRecord(ev[2 * i + 1], stream));
+    }
   };
   const unsigned gt = (unsigned)((C.n_rep + kTriChunk - 1) / kTriChunk);
   const unsigned gtg = (unsigned)((C.n_groups + kTriGroups<N> - 1) / kTriGroups<N>);
   const unsigned gs = (g < kFullGrid ? g : kFullGrid) * (unsigned)(kBlock / kFullBlock);
+  // Without group sleep (list mode needs Quiesce and no trace) the block to
+  // group mapping is free: 256 replicas per block instead of 2,048, so a
+  // small engine (C2: 10k groups) is triaged by 118 blocks, not 15
+  const bool small_tri = !(C.quiesce && !TRACE) && C.n_rep <= kSmallTriMax;
+  const unsigned gsm = (unsigned)((C.n_groups + kBlock / N - 1) / (kBlock / N));
+  const unsigned gfn = (unsigned)((C.n_rep + fast_items_per_block(C) - 1) / fast_items_per_block(C));
+  const unsigned gf = gfn < g_fast_grid ? gfn : g_fast_grid;
   if (mode == 2) {
-    mark(0);
-    mark(1);
-    mark(2);
-    mark(3);
-    hipLaunchKernelGGL((k_step<N, TRACE>), dim3(g), dim3(kBlock), 0, stream, P, C,
-                       ra);
-    mark(4);
+    none(0);
+    none(1);
+    none(2);
+    RBE_LAUNCH(3, (k_step<N, TRACE>), dim3(g), dim3(kBlock), P, C, ra);
   } else if (mode == 0) {
-    mark(0);
-    hipLaunchKernelGGL((k_round<N, TRACE>), dim3(gt), dim3(kBlock), 0, stream, P, C,
-                       ra, L);
-    mark(1);
-    mark(2);
-    mark(3);
-    hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kFullBlock), 0, stream, P, C,
-                       ra, L);
-    mark(4);
-  } else if (mode == 3) {
-    mark(0);
-    // Without group sleep (list mode needs Quiesce and no trace) the block to
-    // group mapping is free: 256 replicas per block instead of 2,048, so a
-    // small engine (C2: 10k groups) is triaged by 118 blocks, not 15
-    if (!(C.quiesce && !TRACE) && C.n_rep <= kSmallTriMax)
-      hipLaunchKernelGGL((k_triage<N, TRACE, kBlock>),
-                         dim3((unsigned)((C.n_groups + kBlock / N - 1) / (kBlock / N))),
-                         dim3(kBlock), 0, stream, P, C, ra, L);
-    else
-      hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(gtg), dim3(kBlock), 0, stream, P, C,
-                         ra, L);
-    mark(1);
-    const unsigned gfn = (unsigned)((C.n_rep + fast_items_per_block(C) - 1) / fast_items_per_block(C));
-    const unsigned gf = gfn < g_fast_grid ? gfn : g_fast_grid;
-    hipLaunchKernelGGL((k_fast_both<N, TRACE>), dim3(gf), dim3(kBlock), 0, stream, P, C,
-                       ra, L);
-    mark(2);
-    mark(3);
-    hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kFullBlock), 0, stream, P, C,
-                       ra, L);
-    mark(4);
+    RBE_LAUNCH(0, (k_round<N, TRACE>), dim3(gt), dim3(kBlock), P, C, ra, L);
+    none(1);
+    none(2);
+    RBE_LAUNCH(3, (k_full_list<N, TRACE>), dim3(gs), dim3(kFullBlock), P, C, ra, L);
   } else {
-    mark(0);
-    // Without group sleep (list mode needs Quiesce and no trace) the block to
-    // group mapping is free: 256 replicas per block instead of 2,048, so a
-    // small engine (C2: 10k groups) is triaged by 118 blocks, not 15
-    if (!(C.quiesce && !TRACE) && C.n_rep <= kSmallTriMax)
-      hipLaunchKernelGGL((k_triage<N, TRACE, kBlock>),
-                         dim3((unsigned)((C.n_groups + kBlock / N - 1) / (kBlock / N))),
-                         dim3(kBlock), 0, stream, P, C, ra, L);
+    if (small_tri)
+      RBE_LAUNCH(0, (k_triage<N, TRACE, kBlock>), dim3(gsm), dim3(kBlock), P, C, ra, L);
     else
-      hipLaunchKernelGGL((k_triage<N, TRACE>), dim3(gtg), dim3(kBlock), 0, stream, P, C,
-                         ra, L);
-    mark(1);
-    const unsigned gfn = (unsigned)((C.n_rep + fast_items_per_block(C) - 1) / fast_items_per_block(C));
-    const unsigned gf = gfn < g_fast_grid ? gfn : g_fast_grid;
-    hipLaunchKernelGGL((k_fast_list<N, TRACE, MODE_LEAD>), dim3(gf), dim3(kBlock), 0, stream,
-                       P, C, ra, L);
-    mark(2);
-    hipLaunchKernelGGL((k_fast_list<N, TRACE, MODE_FOLL>), dim3(gf), dim3(kBlock), 0, stream,
-                       P, C, ra, L);
-    mark(3);
-    hipLaunchKernelGGL((k_full_list<N, TRACE>), dim3(gs), dim3(kFullBlock), 0, stream, P, C,
-                       ra, L);
-    mark(4);
+      RBE_LAUNCH(0, (k_triage<N, TRACE>), dim3(gtg), dim3(kBlock), P, C, ra, L);
+    if (mode == 3) {
+      RBE_LAUNCH(1, (k_fast_both<N, TRACE>), dim3(gf), dim3(kBlock), P, C, ra, L);
+      none(2);
+    } else {
+      RBE_LAUNCH(1, (k_fast_list<N, TRACE, MODE_LEAD>), dim3(gf), dim3(kBlock), P, C, ra, L);
+      RBE_LAUNCH(2, (k_fast_list<N, TRACE, MODE_FOLL>), dim3(gf), dim3(kBlock), P, C, ra, L);
+    }
+    RBE_LAUNCH(3, (k_full_list<N, TRACE>), dim3(gs), dim3(kFullBlock), P, C, ra, L);
   }
   return hipGetLastError() == hipSuccess ? RBE_OK : RBE_E_HIP;
 }
+#undef RBE_LAUNCH
 
 
 }  // namespace rbe

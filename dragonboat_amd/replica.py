@@ -68,36 +68,53 @@ class ReplicaExchange:
                              f"rep_rank {self.rank} of rep_world {self.world}")
         self.rec = xchg_record_bytes()
         n = int(engine.cfg.n_replicas)
+        # caps: the fixed chunks' per-stream capacities (equal on every rank);
+        # ccaps: the counted exchange's regions (this rank's own, grown on demand)
         self.caps = list(caps) if caps else initial_caps(int(engine.cfg.n_groups) * n, n,
                                                          self.world)
+        self.ccaps = list(self.caps)
         self.buf_device = torch.device(buf_device)
         self.comm_device = torch.device(comm_device)
         self.bytes_sent = 0
         self.records_sent = [0] * STREAMS
         # fixed: equal chunks with a count header per peer, no host-side count
-        # read (rbe_xchg_pack_fixed); the capacities never grow, an overflow is
-        # reported by check()
+        # read (rbe_xchg_pack_fixed).  A round whose records did not fit its
+        # chunks (the headers say so on every rank) is repaired by a counted
+        # exchange of the same round (exchange_fixed): never invalid
         self.fixed = fixed
-        # per stream: the most records one (rank, peer) pair moved in a counted
-        # exchange since reset_peak (what to_fixed sizes the chunks by)
+        self.repaired = 0  # fixed rounds that took the counted second pass
+        # per stream, over the counted exchanges since reset_peak: the most
+        # records one (rank, peer) pair moved, and the sum / number of such
+        # counts (what to_fixed sizes the chunks by)
         self.peak = [0] * STREAMS
+        self.csum = [0] * STREAMS
+        self.cn = 0
+        self.cbuf = None
         self._alloc()
 
     # --- layout: per peer p, streams t = 0..2, cap[t] records each (rbe_xchg.h xchg_region)
-    def _per_peer(self) -> int:
-        return sum(c * b for c, b in zip(self.caps, self.rec))
+    def _per_peer(self, caps=None) -> int:
+        return sum(c * b for c, b in zip(self.caps if caps is None else caps, self.rec))
 
-    def _region(self, p: int, t: int) -> int:
-        return p * self._per_peer() + sum(self.caps[i] * self.rec[i] for i in range(t))
+    def _region(self, p: int, t: int) -> int:  # (the counted layout)
+        return p * self._per_peer(self.ccaps) + sum(self.ccaps[i] * self.rec[i] for i in range(t))
 
     def _alloc(self):
-        per = self._per_peer() + (XHDR_BYTES if self.fixed else 0)
+        """The fixed layout's send / receive chunks (fixed mode)."""
+        if not self.fixed:
+            return
+        per = self._per_peer() + XHDR_BYTES
         self.buf = self.torch.empty(self.world * per, dtype=self.torch.uint8,
                                     device=self.buf_device)
-        if self.fixed:
-            self.recv = self.torch.empty_like(self.buf, device=self.comm_device)
-            self.recv_buf = self.recv if self.comm_device == self.buf_device else \
-                self.torch.empty_like(self.buf)
+        self.recv = self.torch.empty_like(self.buf, device=self.comm_device)
+        self.recv_buf = self.recv if self.comm_device == self.buf_device else \
+            self.torch.empty_like(self.buf)
+
+    def _calloc(self):
+        """The counted layout's pack buffer (its regions grow on demand)."""
+        need = self.world * self._per_peer(self.ccaps)
+        if self.cbuf is None or self.cbuf.numel() < need:
+            self.cbuf = self.torch.empty(need, dtype=self.torch.uint8, device=self.buf_device)
 
     def exchange_fixed(self):
         """One round's exchange without reading counts on the host: pack into
@@ -120,35 +137,49 @@ class ReplicaExchange:
                 torch.cuda.current_stream(self.buf_device).synchronize()
         self.bytes_sent += self.buf.numel()
         self.eng.xchg_unpack_fixed(self.recv_buf.data_ptr(), self.caps)
+        # one 4-byte read (rbe_xchg_status, read-and-clear): set on every rank
+        # alike when any rank's records outgrew a chunk this round, because
+        # every chunk header reaches every rank.  The outboxes of the round
+        # are intact until the next step, so a counted exchange of the same
+        # round delivers every record again, each to its own slot (idempotent)
+        if self.eng.xchg_status():
+            self.repaired += 1
+            self.exchange(stats=False)
 
-    def check(self):
-        """Raise if a fixed-layout round overflowed a chunk (rbe_xchg_status)."""
-        if self.fixed and self.eng.xchg_status():
-            raise RuntimeError("replica exchange: a chunk overflowed its capacity; "
-                               "the rounds since are invalid (raise caps)")
+    def check(self) -> int:
+        """The number of fixed rounds repaired by a counted second pass."""
+        return self.repaired
 
     def reset_peak(self):
         self.peak = [0] * STREAMS
+        self.csum = [0] * STREAMS
+        self.cn = 0
 
     def to_fixed(self, margin: float = 1.25):
         """Switch to the fixed-capacity exchange with chunks sized from the
         counted rounds seen since reset_peak: every (peer, stream) capacity is
-        the largest count observed on any rank times `margin` (plus a small
-        floor), so the padding moved per round stays near `margin` times the
-        records instead of the worst-case bound of initial_caps.  Collective:
-        every rank calls it (the chunk size must agree).  An overflow in a
-        later round is reported by check()."""
-        t = self.torch.tensor(self.peak, dtype=self.torch.int64, device=self.comm_device)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
-        self.peak = [int(x) for x in t.tolist()]
-        self.caps = [int(p * margin) + 64 for p in self.peak]
+        `margin` times the MEAN count of one (rank, peer) pair over those
+        rounds and all ranks (plus a small floor), so the bytes moved per round
+        stay near `margin` times the records.  A round above that is repaired
+        by a counted second pass (exchange_fixed), so the chunks need not hold
+        the peak.  Collective: every rank calls it (the chunk size must agree)."""
+        t = self.torch.tensor(self.peak + self.csum + [self.cn], dtype=self.torch.int64,
+                              device=self.comm_device)
+        mx = t.clone()
+        self.dist.all_reduce(mx, op=self.dist.ReduceOp.MAX, group=self.group)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+        self.peak = [int(x) for x in mx[:STREAMS].tolist()]
+        tot, n = t[STREAMS:2 * STREAMS].tolist(), max(1, int(t[-1]))
+        self.mean = [x / n for x in tot]
+        self.caps = [int(m * margin) + 64 for m in self.mean]
         self.fixed = True
         self._alloc()
 
     def pad_ratio(self) -> float:
-        """Bytes of one fixed chunk (one peer) over the bytes of the largest
+        """Bytes of one fixed chunk (one peer) over the bytes of the mean
         counted round's records to one peer since reset_peak."""
-        rec = sum(p * b for p, b in zip(self.peak, self.rec))
+        mean = getattr(self, "mean", self.peak)
+        rec = sum(m * b for m, b in zip(mean, self.rec))
         return (self._per_peer() + XHDR_BYTES) / rec if rec else float("inf")
 
     def fixed_bytes_per_round(self) -> int:
@@ -157,22 +188,28 @@ class ReplicaExchange:
 
     def grow(self, counts: Sequence[int]):
         need = [max(counts[p * STREAMS + t] for p in range(self.world)) for t in range(STREAMS)]
-        self.caps = [max(c, n + n // 4 + 64) for c, n in zip(self.caps, need)]
-        self._alloc()
+        self.ccaps = [max(c, n + n // 4 + 64) for c, n in zip(self.ccaps, need)]
+        self._calloc()
 
-    def exchange(self):
-        """Move the last round's cross-rank records (call after every round)."""
+    def exchange(self, stats: bool = True):
+        """Move the last round's cross-rank records with their counts read on
+        the host (call after every round; exchange_fixed calls it for a round
+        its chunks could not hold, with stats=False)."""
         torch, dist = self.torch, self.dist
-        fits, counts = self.eng.xchg_pack(self.buf.data_ptr(), self.caps)
+        self._calloc()
+        fits, counts = self.eng.xchg_pack(self.cbuf.data_ptr(), self.ccaps)
         if not fits:
             self.grow(counts)
-            fits, counts = self.eng.xchg_pack(self.buf.data_ptr(), self.caps)
+            fits, counts = self.eng.xchg_pack(self.cbuf.data_ptr(), self.ccaps)
             if not fits:
                 raise RuntimeError("replica exchange: pack overflow after growing")
         W, S = self.world, STREAMS
-        for t in range(S):
-            self.peak[t] = max([self.peak[t]] + [counts[p * S + t] for p in range(W)
-                                                 if p != self.rank])
+        if stats:
+            self.cn += W - 1
+            for t in range(S):
+                c = [counts[p * S + t] for p in range(W) if p != self.rank]
+                self.peak[t] = max([self.peak[t]] + c)
+                self.csum[t] += sum(c)
         send_cnt = torch.tensor(counts, dtype=torch.int64, device=self.comm_device)
         recv_cnt = torch.empty_like(send_cnt)
         dist.all_to_all_single(recv_cnt, send_cnt, group=self.group)
@@ -185,7 +222,7 @@ class ReplicaExchange:
                 b = counts[p * S + t] * self.rec[t]
                 if b:
                     o = self._region(p, t)
-                    parts.append(self.buf[o:o + b])
+                    parts.append(self.cbuf[o:o + b])
                     nbytes += b
             out_split.append(nbytes)
         send = torch.cat(parts) if parts else torch.empty(0, dtype=torch.uint8,
@@ -197,8 +234,9 @@ class ReplicaExchange:
         dist.all_to_all_single(recv, send, output_split_sizes=in_split,
                                input_split_sizes=out_split, group=self.group)
         self.bytes_sent += sum(out_split)
-        for t in range(S):
-            self.records_sent[t] += sum(counts[p * S + t] for p in range(W))
+        if stats:
+            for t in range(S):
+                self.records_sent[t] += sum(counts[p * S + t] for p in range(W))
         # per stream: the records of every source rank, back to back
         streams: List[List] = [[] for _ in range(S)]
         at = 0

@@ -410,9 +410,10 @@ int rbe_prepare_run(rbe_engine* e, uint32_t rounds);
 /* Name of the kernel in `slot` for this engine's pipeline ("" if unused). */
 int rbe_kernel_name(const rbe_engine* e, int32_t slot, char* buf, uint32_t cap);
 
-/* Run `rounds` rounds one at a time with HIP events between the pipeline
- * kernels on the engine stream; ms_per_kernel[RBE_KERNEL_NUM] receives each
- * kernel's total elapsed time. */
+/* Run `rounds` rounds one at a time, each pipeline kernel launched with
+ * hipExtLaunchKernel and a start / stop event pair that its own dispatch
+ * stamps (the kernel's execution, not the launch gaps around it);
+ * ms_per_kernel[RBE_KERNEL_NUM] receives each kernel's total time. */
 int rbe_profile_rounds(rbe_engine* e, uint32_t rounds, float* ms_per_kernel);
 
 /* Host input for the next step (requires cfg.ext_inputs), the node-side events
@@ -770,8 +771,12 @@ int rbe_xchg_record_bytes(uint64_t* out3);
  *   rbe_xchg_pack_fixed: packs the last round's records into `buf` (rep_world
  *     chunks), enqueued on the engine stream, nothing read back;
  *   rbe_xchg_unpack_fixed: scatters a received buffer of the same layout;
- *   rbe_xchg_status: the sticky overflow flag (a chunk had more records than
- *     its capacity: those rounds are not valid; size cap3 up and rerun);
+ *   rbe_xchg_status: the overflow flag of the fixed exchanges since the last
+ *     call, cleared by the read: set when some rank's records outgrew a chunk
+ *     (every rank sees it, from the chunk headers it received).  The round's
+ *     outboxes are intact until the next step: a counted exchange of the same
+ *     round (rbe_xchg_pack / rbe_xchg_unpack) delivers every record again to
+ *     its slot, which repairs it (dragonboat_amd/replica.py exchange_fixed);
  *   rbe_stream: the engine's HIP stream (hipStream_t), so a collective can be
  *     enqueued between pack and unpack without a host wait. */
 int rbe_xchg_chunk_bytes(const uint64_t* cap3, uint64_t* bytes);

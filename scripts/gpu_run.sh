@@ -41,7 +41,7 @@ for step in "$@"; do
       python3 scripts/summarize_bench.py "$O/bench_default.json" default ;;
     prof)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/prof" \
-        -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --also "" \
+        -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --also "" \
         > "$GRAFT_REPO_ROOT/$O/bench_prof.json" 2> "$GRAFT_REPO_ROOT/$O/bench_prof.err") ;;
     pmc)
       timeout -k 10 600 bash scripts/pmc_traffic.sh ;;

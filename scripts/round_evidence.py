@@ -1,0 +1,97 @@
+"""Fold one GPU pass of `scripts/gpu_run.sh OUT ... prof` into profiles/<name>/:
+the bench line, the rocprofv3 stats, the round kernels' dispatch trace (only
+k_triage / k_fast_both / k_full_list, a few hundred KB) and summary.md, which
+averages the LAST `window` dispatches of each round kernel — the bench's timed
+and profiled rounds, not its settle and warmup — next to the bench's own
+HIP-event split of the same rounds, with the ratio of the two.
+
+    python3 scripts/round_evidence.py gpurun_out/r06x profiles/r06_final [window]
+
+window defaults to the bench's steps + prof_rounds (read from its JSON line)."""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+src, dst = sys.argv[1], sys.argv[2]
+os.makedirs(dst, exist_ok=True)
+ROUND = ("k_triage", "k_fast_both", "k_full_list")
+
+
+def last_json(p):
+    for line in reversed(open(p).read().strip().splitlines()):
+        if line.startswith("{"):
+            return json.loads(line)
+    raise SystemExit(f"no JSON line in {p}")
+
+
+bench_p = os.path.join(src, "bench_prof.json")
+b = last_json(bench_p)
+shutil.copy(bench_p, os.path.join(dst, "bench.json"))
+window = int(sys.argv[3]) if len(sys.argv) > 3 else \
+    int(b["steps"]) + int(b["roofline"].get("profiled_rounds", 0))
+prof = os.path.join(src, "prof")
+stats = os.path.join(prof, "run_kernel_stats.csv")
+if os.path.exists(stats):
+    shutil.copy(stats, os.path.join(dst, "rocprof_kernel_stats.csv"))
+elif os.path.exists(os.path.join(prof, "run_results.db")):  # (kept whole: 1 MB)
+    shutil.copy(os.path.join(prof, "run_results.db"), os.path.join(dst, "rocprof_results.db"))
+by = defaultdict(list)
+rows = []
+
+
+def dispatches():
+    """(start ns, kernel name, duration ns) in dispatch order: the CSV kernel
+    trace, or rocprofv3's rocpd database (its default output format)"""
+    tr = os.path.join(prof, "run_kernel_trace.csv")
+    if os.path.exists(tr):
+        with open(tr) as f:
+            for r in csv.DictReader(f):
+                yield (int(r["Start_Timestamp"]), r["Kernel_Name"],
+                       int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        return
+    import sqlite3
+    db = sqlite3.connect(os.path.join(prof, "run_results.db"))
+    yield from db.execute("select start, name, end - start from kernels order by start")
+
+
+for st, k, d in dispatches():
+    base = next((x for x in ROUND if x in k), None)
+    if base is None:
+        continue
+    by[base].append(d)
+    rows.append((st, base, d))
+with open(os.path.join(dst, "round_kernel_trace.csv"), "w") as f:
+    f.write("start_ns,kernel,duration_ns\n")
+    for s, k, d in rows:
+        f.write(f"{s},{k},{d}\n")
+hip = {k["kernel"]: k["avg_us"] for k in b["round"]["kernels"]}
+lines = [f"# {os.path.basename(dst)}: steady-state round kernels", "",
+         f"Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline --also \"\"` "
+         f"(C4, {b['steps']} timed + {b['roofline'].get('profiled_rounds', 0)} profiled rounds; "
+         f"library {b.get('library', {}).get('sha256_16', '?')}).", "",
+         f"rocprofv3 averages over the LAST {window} dispatches of each round kernel (the timed and "
+         "profiled rounds; the earlier ones are the 260 settle rounds with every group active and "
+         "the warmup), against the bench's HIP-event split of its profiled rounds:", "",
+         "| kernel | dispatches | rocprof avg µs (last window) | rocprof avg µs (all) | bench HIP-event µs | ratio |",
+         "|---|---|---|---|---|---|"]
+for k in ROUND:
+    v = by.get(k, [])
+    if not v:
+        continue
+    w = v[-window:]
+    a = sum(w) / len(w) / 1e3
+    h = hip.get(k)
+    ratio = f"{a / h:.3f}" if h else "-"
+    lines.append(f"| `{k}` | {len(v)} | {a:.1f} | {sum(v) / len(v) / 1e3:.1f} | "
+                 f"{h:.1f} | {ratio} |" if h else f"| `{k}` | {len(v)} | {a:.1f} | "
+                 f"{sum(v) / len(v) / 1e3:.1f} | - | - |")
+rf = b["roofline"]
+lines += ["", f"Roofline (dominant kernel `{rf['kernel']}`): {rf['alg_bytes_per_launch']:.0f} B "
+          f"algorithmic per launch / {rf['avg_launch_us']:.2f} µs = {rf['achieved']:.0f} GB/s, "
+          f"frac {rf['frac']:.4f} of {rf['peak']:.0f} GB/s; ms_per_step {b['ms_per_step']:.4f}.",
+          "", "Bench line:", "", "```json", json.dumps(b, indent=1), "```"]
+open(os.path.join(dst, "summary.md"), "w").write("\n".join(lines) + "\n")
+print("\n".join(lines[:16]))

@@ -994,11 +994,17 @@ extern "C" void soa_xchg_unpack_fixed(void* h, const uint8_t* recv, const uint64
     for (u32 p = 0; p < e->C.rep_world; p++)
       for (u64 i = 0; i < cap[t]; i++) {
         u32 ovf = 0;
-        if (!xchg_put_fixed(e->P, e->C, par, recv, cap, p, t, i, &ovf)) break;
+        const bool put = xchg_put_fixed(e->P, e->C, par, recv, cap, p, t, i, &ovf);
         if (ovf) e->xflag = 1;
+        if (!put) break;
       }
 }
-extern "C" uint32_t soa_xchg_status(void* h) { return ((SoaEngine*)h)->xflag; }
+extern "C" uint32_t soa_xchg_status(void* h) {  // read-and-clear, as rbe_xchg_status
+  SoaEngine* e = (SoaEngine*)h;
+  const u32 f = e->xflag;
+  e->xflag = 0;
+  return f;
+}
 
 extern "C" int soa_xchg_pack(void* h, uint8_t* buf, const uint64_t* cap, uint32_t* counts) {
   SoaEngine* e = (SoaEngine*)h;

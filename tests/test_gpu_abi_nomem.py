@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 
 CHILD = r"""
 import sys
-sys.path.insert(0, "tests")
+sys.path[:0] = ["oracle", "tests", "."]  # as tests/conftest.py
 import oracle as O
 from dragonboat_amd.engine import Engine, InputError, RBE_E_NOMEM
 from parity_util import run_lockstep

@@ -73,10 +73,13 @@ def _worker(rank, world, port, name, gpu, trace, q, fixed=False):
         # that never grow (initial_caps), counts travel in the chunk headers;
         # "cal": counted rounds first, then chunks sized from their peak counts
         # (to_fixed, as bench.py --xchg-fixed does)
-        cal = fixed == "cal"
+        # "ovf": fixed chunks of 4 records, so most rounds outgrow them and take
+        # the counted second pass (exchange_fixed's repair)
+        cal, ovf = fixed == "cal", fixed == "ovf"
         if cal:
             fixed = False
-        caps = None if (fixed or cal) else [8, 8, 8]
+        caps = [4, 4, 4] if ovf else None if (fixed or cal) else [8, 8, 8]
+        fixed = bool(fixed)
         if gpu:  # the HIP engine, records staged through host memory for gloo
             from dragonboat_amd.engine import Engine
             eng = Engine(device=0, trace=trace, rep_world=world, rep_rank=rank, **kw, **extra)
@@ -109,6 +112,8 @@ def _worker(rank, world, port, name, gpu, trace, q, fixed=False):
         nf = eng.fault_summary()[0] if gpu else eng.faults()[0]
         if cal:
             assert xch.fixed
+        if ovf:
+            assert xch.repaired > 0, "no round outgrew its chunks"
         q.put((rank, snaps, eng.counters(), nf,
                [xch.bytes_sent] * 3 if fixed else xch.records_sent))
     except Exception as ex:  # surface worker failures in the parent
@@ -181,8 +186,17 @@ def test_replica_fixed_exchange_matches_oracle(name):
     run_case(name, fixed=True)
 
 
+@pytest.mark.parametrize("name", ["C2_w2", "N5_w4"])
+def test_replica_fixed_exchange_overflow_repaired(name):
+    """Fixed chunks far too small for the rounds: every round that outgrows
+    them is repaired by a counted exchange of the same round (read-and-clear
+    rbe_xchg_status), bit-exact with the oracle; an overflow never
+    invalidates the run."""
+    run_case(name, fixed="ovf")
+
+
 def test_replica_calibrated_fixed_exchange():
     """Counted rounds, then the fixed exchange with chunks sized from the
-    counted rounds' largest counts (ReplicaExchange.to_fixed): still
-    bit-exact, no overflow."""
+    counted rounds' mean counts (ReplicaExchange.to_fixed): still bit-exact
+    (rounds above the mean take the counted second pass)."""
     run_case("C2_w2", fixed="cal")
