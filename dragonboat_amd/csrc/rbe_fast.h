@@ -139,6 +139,22 @@ RBE_HD LeadMsg load_lead(const Msg* p) {
   return x;
 }
 
+// A/B knobs (build variants): the evicted entry's cold-log store as the
+// step's first store, freeing its registers early; the outbox stash in LDS
+#ifndef RBE_FAST_EV_EARLY
+#define RBE_FAST_EV_EARLY 0
+#endif
+#ifndef RBE_FAST_STASH_LDS
+#define RBE_FAST_STASH_LDS 0
+#endif
+static constexpr u32 kFastStashLanes = 256;
+#if defined(__HIP_DEVICE_COMPILE__) && RBE_FAST_STASH_LDS
+__device__ __forceinline__ OutStash (&fast_stash())[kFastStashLanes] {
+  __shared__ OutStash s_ost[kFastStashLanes];
+  return s_ost;
+}
+#endif
+
 // Output side shared by both roles: message emission (raft.send +
 // finalizeMessageTerm, raft.go:640-658, then the network list), ReadyToRead,
 // counters, the running trace hashes.  Mirrors Lane::send exactly.
@@ -160,7 +176,12 @@ struct FastOut {
   u32 fault0, n_out, n_drop_msg, n_ent_out;
   u32 events;  // EV_* of the step (Upd::events)
   // messages past a full plane list (rbe_spill.h; relocated in fast_finish)
-  OutStash ost;
+#if defined(__HIP_DEVICE_COMPILE__) && RBE_FAST_STASH_LDS
+  RBE_HD OutStash& ost() const { return fast_stash()[threadIdx.x]; }
+#else
+  mutable OutStash ost_m;
+  RBE_HD OutStash& ost() const { return ost_m; }
+#endif
 
   RBE_HD u32 get_pc(u32 d) const {
     return d < 4 ? (u32)((pc >> (16 * d)) & 0xFFFFu) : (u32)((pc_hi >> (16 * (d - 4))) & 0xFFFFu);
@@ -224,7 +245,7 @@ struct FastOut {
     n_ent_out += ok ? (u32)m.n_ent : 0u;
     if (!ok) return;
     if (full) {  // the list moves to the spill heap at the step's end
-      fault_if(!stash_put(P, C, par, ost, m), F_NOMEM);
+      fault_if(!stash_put(P, C, par, ost(), m), F_NOMEM);
       return;
     }
     u32 slot;
@@ -387,7 +408,7 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, CT& ctr, FastOut<N, TR
   ctr.v[C_ENT_OUT] += o.n_ent_out;
   // this sender's outbox header: stamp + the N count words; lists with
   // stashed messages move whole to the spill heap (rare: rbe_spill.h)
-  if (o.ost.n) o.fault |= outbox_relocate(P, C, o.par, r, N, o.ost, o.pc, o.pc_hi);
+  if (o.ost().n) o.fault |= outbox_relocate(P, C, o.par, r, N, o.ost(), o.pc, o.pc_hi);
   u32 ow[N];
 #pragma unroll
   for (u32 dd = 0; dd < N; dd++) ow[dd] = o.get_pc(dd) & 0xFFFFu;
@@ -788,6 +809,17 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   asm volatile("" ::: "memory");
   rbe_wait_all_loads();
   RBE_STAMP(t2);
+  u32 ev_fault = 0;
+#if RBE_FAST_EV_EARLY
+  // the step's first store: entry ev_idx into the cold log (also when the
+  // proposal below does not append after all: a second copy of an entry the
+  // ring still holds is harmless), so its registers are free from here on
+  if (ev) {
+    const u32 t0 = ev_cr.tail;
+    ev_fault = cold_put(P, C, ev_cr, ev_idx, ev_e, par) ? 0u : F_NOMEM;
+    if (ev_cr.tail != t0) P.cold[r] = ev_cr;
+  }
+#endif
   FastOut<N, TRACE> o;
   o.r = r;
   o.g = g;
@@ -801,9 +833,10 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   o.n_msgs = o.n_rtr = o.n_drop_ri = 0;
   o.n_out = o.n_drop_msg = o.n_ent_out = 0;
   o.fault0 = o.fault;
+  o.fault |= ev_fault;
   o.msg_hash = o.rtr_hash = o.drop_hash = 0;
   o.events = 0;
-  stash_init(o.ost);
+  stash_init(o.ost());
   o.term = c.term;
   u8 flags = h.flags;
   u32 etick = h.election_tick, htick = h.heartbeat_tick;
@@ -1211,7 +1244,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
       }
       // appendEntries (raft.go:909-920)
       const u64 idx = c.last_index + 1;
-      if (ev) {  // the entry the slot held, into the cold log
+      if (!RBE_FAST_EV_EARLY && ev) {  // the entry the slot held, into the cold log
         const u32 t0 = ev_cr.tail;
         o.fault_if(!cold_put(P, C, ev_cr, ev_idx, ev_e, par), F_NOMEM);
         if (ev_cr.tail != t0) P.cold[r] = ev_cr;
@@ -1502,6 +1535,14 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   asm volatile("" ::: "memory");
   rbe_wait_all_loads();
   RBE_STAMP(t2);
+  u32 ev_fault = 0;
+#if RBE_FAST_EV_EARLY
+  if (ev_app) {  // the step's first store: the append's slot held entry ev_idx
+    const u32 t0 = ev_cr.tail;
+    ev_fault = cold_put(P, C, ev_cr, ev_idx, ev_e, par) ? 0u : F_NOMEM;
+    if (ev_cr.tail != t0) P.cold[r] = ev_cr;
+  }
+#endif
   FastOut<N, TRACE> o;
   o.r = r;
   o.g = g;
@@ -1515,9 +1556,10 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   o.n_msgs = o.n_rtr = o.n_drop_ri = 0;
   o.n_out = o.n_drop_msg = o.n_ent_out = 0;
   o.fault0 = o.fault;
+  o.fault |= ev_fault;
   o.msg_hash = o.rtr_hash = o.drop_hash = 0;
   o.events = 0;
-  stash_init(o.ost);
+  stash_init(o.ost());
   o.term = c.term;
   u8 flags = h.flags;
   u32 etick = h.election_tick;
@@ -1543,7 +1585,7 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
     c.committed = idx;
   };
   const u32 lid = ls + 1;
-  if (ev_app) {  // the append's ring slot held entry ev_idx: into the cold log
+  if (!RBE_FAST_EV_EARLY && ev_app) {  // the append's ring slot held entry ev_idx: into the cold log
     const u32 t0 = ev_cr.tail;
     o.fault_if(!cold_put(P, C, ev_cr, ev_idx, ev_e, par), F_NOMEM);
     if (ev_cr.tail != t0) P.cold[r] = ev_cr;

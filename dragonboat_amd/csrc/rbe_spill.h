@@ -76,11 +76,13 @@ RBE_HD void sp_atomic_max_u64(u64* p, u64 v) {
 }
 
 // ---------------------------------------------------------------- page pool
-RBE_HD Ent* pool_ent(const Planes& P, u32 page, u32 slot) {
+template <class PL>
+RBE_HD Ent* pool_ent(const PL& P, u32 page, u32 slot) {
   return &P.pool[(u64)page * kPageEnts + slot];
 }
 // a page for a step of round parity `par`; 0 when the pool is exhausted
-RBE_HD u32 pool_alloc(const Planes& P, const Params& C, u32 par) {
+template <class PL, class PA>
+RBE_HD u32 pool_alloc(const PL& P, const PA& C, u32 par) {
   SpillCtl* s = P.sctl;
   u32* fh = &s->free_head[par ^ 1u];
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -107,7 +109,8 @@ RBE_HD u32 pool_alloc(const Planes& P, const Params& C, u32 par) {
   sp_atomic_add_u32(&s->live, 1u);
   return p;
 }
-RBE_HD void pool_free(const Planes& P, u32 par, u32 page) {
+template <class PL>
+RBE_HD void pool_free(const PL& P, u32 par, u32 page) {
   sp_atomic_add_u32(&P.sctl->live, ~0u);  // - 1
   u32* fh = &P.sctl->free_head[par];
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -127,7 +130,8 @@ RBE_HD void pool_free(const Planes& P, u32 par, u32 page) {
 // ---------------------------------------------------------------- cold log
 // The page of `cr` holding page number pn, or 0: walked from the nearer end
 // (a catch-up reads just below the ring; a joining node from the bottom)
-RBE_HD u32 cold_find(const Planes& P, const ColdRef& cr, u64 pn) {
+template <class PL>
+RBE_HD u32 cold_find(const PL& P, const ColdRef& cr, u64 pn) {
   if (!cr.tail || pn > cr.tail_pn) return 0;
   if (cr.tail_pn - pn <= 8) {
     for (u32 p = cr.tail; p;) {
@@ -146,7 +150,8 @@ RBE_HD u32 cold_find(const Planes& P, const ColdRef& cr, u64 pn) {
   }
   return 0;
 }
-RBE_HD bool cold_get(const Planes& P, const ColdRef& cr, u64 idx, Ent* out) {
+template <class PL>
+RBE_HD bool cold_get(const PL& P, const ColdRef& cr, u64 idx, Ent* out) {
   const u32 p = cold_find(P, cr, idx / kPageEnts);
   if (!p) return false;
   *out = *pool_ent(P, p, (u32)(idx % kPageEnts));
@@ -155,7 +160,8 @@ RBE_HD bool cold_get(const Planes& P, const ColdRef& cr, u64 idx, Ent* out) {
 // Entry idx into the cold log (an eviction, or an entry written straight
 // there); false when the pool is exhausted.  Evictions come in index order, so
 // the common case is the tail page or a new one after it.
-RBE_HD bool cold_put(const Planes& P, const Params& C, ColdRef& cr, u64 idx, const Ent& e, u32 par) {
+template <class PL, class PA>
+RBE_HD bool cold_put(const PL& P, const PA& C, ColdRef& cr, u64 idx, const Ent& e, u32 par) {
   const u64 pn = idx / kPageEnts;
   u32 p = 0;
   if (cr.tail && pn == cr.tail_pn) {
@@ -195,7 +201,8 @@ RBE_HD bool cold_put(const Planes& P, const Params& C, ColdRef& cr, u64 idx, con
 }
 // Releases every page whose entries all lie at or below `upto` (LogDB.Compact
 // to a marker; ~0 releases the whole chain)
-RBE_HD void cold_release(const Planes& P, ColdRef& cr, u64 upto, u32 par) {
+template <class PL>
+RBE_HD void cold_release(const PL& P, ColdRef& cr, u64 upto, u32 par) {
   while (cr.head) {
     const PoolMeta m = P.pmeta[cr.head];
     if (upto != ~0ull && (m.pn + 1) * kPageEnts - 1 > upto) break;
@@ -234,10 +241,12 @@ RBE_HD bool log_ent_at(const Planes& P, const Params& C, u64 r, u64 last, u64 id
 // ~0 when the heap is exhausted.  With rep_world > 1 (rbe_xchg.h) each rank
 // allocates in its own 1/rep_world share, so the exchange can scatter a remote
 // sender's spilled lists and entries at the granules the sender chose.
-RBE_HD u64 spill_share(const Params& C) {
+template <class PA>
+RBE_HD u64 spill_share(const PA& C) {
   return C.rep_world > 1 ? C.spill_units / C.rep_world : C.spill_units;
 }
-RBE_HD u64 spill_alloc(const Planes& P, const Params& C, u32 par, u64 bytes) {
+template <class PL, class PA>
+RBE_HD u64 spill_alloc(const PL& P, const PA& C, u32 par, u64 bytes) {
   const u64 n = (bytes + 15) / 16;
   const u64 share = spill_share(C);
   const u64 at = sp_atomic_add_u64(&P.sctl->used[par], n);
@@ -248,8 +257,8 @@ RBE_HD u64 spill_alloc(const Planes& P, const Params& C, u32 par, u64 bytes) {
   sp_atomic_max_u64(&P.sctl->peak[par], at + n);
   return (C.rep_world > 1 ? share * C.rep_rank : 0) + at;
 }
-template <class T>
-RBE_HD T* spill_at(const Planes& P, u32 par, u64 granule) {
+template <class T, class PL>
+RBE_HD T* spill_at(const PL& P, u32 par, u64 granule) {
   return (T*)(P.spill[par] + granule * 16);
 }
 // The round of parity `par` starts: the next round's heap (the other parity,
@@ -325,7 +334,8 @@ RBE_HD void stash_init(OutStash& s) {
   s.head = s.cur = 0;
   s.n = s.mask = 0;
 }
-RBE_HD bool stash_put(const Planes& P, const Params& C, u32 par, OutStash& s, const Msg& m) {
+template <class PL, class PA>
+RBE_HD bool stash_put(const PL& P, const PA& C, u32 par, OutStash& s, const Msg& m) {
   const u32 i = s.n % (kStashChunk - 1u);
   if (i == 0) {
     const u64 g = spill_alloc(P, C, par, kStashChunk * sizeof(Msg));
@@ -346,8 +356,8 @@ RBE_HD bool stash_put(const Planes& P, const Params& C, u32 par, OutStash& s, co
   return true;
 }
 // The stashed messages in emission order: f(msg)
-template <class F>
-RBE_HD void stash_each(const Planes& P, u32 par, const OutStash& s, F&& f) {
+template <class PL, class F>
+RBE_HD void stash_each(const PL& P, u32 par, const OutStash& s, F&& f) {
   u64 c = s.head;
   for (u32 t = 0; t < s.n; t++) {
     const u32 i = t % (kStashChunk - 1u);
@@ -361,7 +371,8 @@ RBE_HD void stash_each(const Planes& P, u32 par, const OutStash& s, F&& f) {
 // 0-3) and w_hi (4-7), rewritten for the moved lists (packed, so no register
 // array is indexed at run time).  Returns F_NOMEM when the heap cannot take a
 // list (it keeps its plane part).
-RBE_HD u32 outbox_relocate(const Planes& P, const Params& C, u32 par, u64 rs, u32 n,
+template <class PL, class PA>
+RBE_HD u32 outbox_relocate(const PL& P, const PA& C, u32 par, u64 rs, u32 n,
                            const OutStash& s, u64& w_lo, u64& w_hi) {
   u32 fault = 0;
   for (u32 d = 0; d < n; d++) {
@@ -461,12 +472,162 @@ RBE_HD const ReadReq* rq_entry(const Planes& P, const Params& C, u64 r, const Co
 RBE_HD u32 rq_length(const Planes& P, const Params& C, u64 r, const Core& c) {
   return c.rq_count == kRqExt ? rq_ext_load(P, C, r).n : (u32)c.rq_count;
 }
-RBE_HD void rq_ext_free(const Planes& P, const RqExt& x, u32 par) {
+template <class PL>
+RBE_HD void rq_ext_free(const PL& P, const RqExt& x, u32 par) {
   for (u32 p = x.head; p;) {
     const u32 nx = p == x.tail ? 0u : P.pmeta[p].next;
     pool_free(P, par, p);
     p = nx;
   }
+}
+
+// ---------------------------------------------------------------- out of line
+// The general step (Lane, rbe_step.h) calls the tiers through these `_ol`
+// wrappers: each walk and allocation is compiled once there, as a real call
+// (RBE_COLD), instead of being inlined into every log read and send of the
+// handler table.  Inlined, the tiers doubled k_full_list's code and put it
+// into scratch spills (C3 k_full_list 238 → 208 µs outlined).  The calls take
+// values only (the tier pointers in a SpillRef, a ColdRef / OutStash / Msg by
+// value, results returned by value), so no caller object has its address
+// taken; inside, the templates above run on SpillP / SpillC, which hold just
+// the tiers' fields.  The fast steps keep the inline forms: a call in their
+// kernel costs more than the code it saves (measured: C4 k_fast_both +50%).
+#if defined(__HIPCC__) || defined(__HIP__)
+#define RBE_COLD __host__ __device__ inline __attribute__((noinline))
+#else
+#define RBE_COLD inline __attribute__((noinline))
+#endif
+// the tiers' fields of Planes / Params, for the templates above
+struct SpillP {
+  Ent* pool;
+  PoolMeta* pmeta;
+  SpillCtl* sctl;
+  u8* spill[2];
+  Msg* msgs[2];
+};
+struct SpillC {
+  u64 spill_units;
+  u32 pool_pages, rep_world, rep_rank, maxm;
+};
+struct SpillRef {
+  SpillP P;
+  SpillC C;
+};
+RBE_HD SpillRef spill_ref(const Planes& P, const Params& C) {
+  SpillRef s;
+  s.P.pool = P.pool;
+  s.P.pmeta = P.pmeta;
+  s.P.sctl = P.sctl;
+  s.P.spill[0] = P.spill[0];
+  s.P.spill[1] = P.spill[1];
+  s.P.msgs[0] = P.msgs[0];
+  s.P.msgs[1] = P.msgs[1];
+  s.C.spill_units = C.spill_units;
+  s.C.pool_pages = C.pool_pages;
+  s.C.rep_world = C.rep_world;
+  s.C.rep_rank = C.rep_rank;
+  s.C.maxm = C.maxm;
+  return s;
+}
+struct ColdGet {
+  Ent e;
+  u32 ok;
+};
+RBE_COLD ColdGet cold_get_o(SpillRef s, ColdRef cr, u64 idx) {
+  ColdGet g;
+  g.ok = cold_get(s.P, cr, idx, &g.e) ? 1u : 0u;
+  return g;
+}
+struct ColdPut {
+  ColdRef cr;
+  u32 ok;
+};
+RBE_COLD ColdPut cold_put_o(SpillRef s, ColdRef cr, u64 idx, Ent e, u32 par) {
+  ColdPut r;
+  r.ok = cold_put(s.P, s.C, cr, idx, e, par) ? 1u : 0u;
+  r.cr = cr;
+  return r;
+}
+RBE_COLD ColdRef cold_release_o(SpillRef s, ColdRef cr, u64 upto, u32 par) {
+  cold_release(s.P, cr, upto, par);
+  return cr;
+}
+RBE_COLD u64 spill_alloc_o(SpillRef s, u32 par, u64 bytes) {
+  return spill_alloc(s.P, s.C, par, bytes);
+}
+RBE_COLD u32 pool_alloc_o(SpillRef s, u32 par) {
+  return pool_alloc(s.P, s.C, par);
+}
+RBE_COLD void pool_free_o(SpillRef s, u32 par, u32 page) {
+  pool_free(s.P, par, page);
+}
+RBE_COLD void rq_ext_free_o(SpillRef s, RqExt q, u32 par) {
+  rq_ext_free(s.P, q, par);
+}
+struct StashPut {
+  OutStash st;
+  u32 ok;
+};
+RBE_COLD StashPut stash_put_o(SpillRef s, u32 par, OutStash st, Msg m) {
+  StashPut r;
+  r.ok = stash_put(s.P, s.C, par, st, m) ? 1u : 0u;
+  r.st = st;
+  return r;
+}
+struct Reloc {
+  u64 lo, hi;
+  u32 fault;
+};
+RBE_COLD Reloc outbox_relocate_o(SpillRef s, u32 par, u64 rs, u32 n, OutStash st, u64 w_lo,
+                                 u64 w_hi) {
+  Reloc r;
+  r.fault = outbox_relocate(s.P, s.C, par, rs, n, st, w_lo, w_hi);
+  r.lo = w_lo;
+  r.hi = w_hi;
+  return r;
+}
+// the call sites' forms (the inline functions' signatures)
+RBE_HD bool cold_get_ol(const Planes& P, const Params& C, const ColdRef& cr, u64 idx, Ent* out) {
+  const ColdGet g = cold_get_o(spill_ref(P, C), cr, idx);
+  *out = g.e;
+  return g.ok != 0;
+}
+RBE_HD bool cold_put_ol(const Planes& P, const Params& C, ColdRef& cr, u64 idx, const Ent& e,
+                        u32 par) {
+  if (cr.tail && idx / kPageEnts == cr.tail_pn) {  // the tail page: inline
+    P.pool[(u64)cr.tail * kPageEnts + idx % kPageEnts] = e;
+    return true;
+  }
+  const ColdPut r = cold_put_o(spill_ref(P, C), cr, idx, e, par);
+  cr = r.cr;
+  return r.ok != 0;
+}
+RBE_HD void cold_release_ol(const Planes& P, const Params& C, ColdRef& cr, u64 upto, u32 par) {
+  cr = cold_release_o(spill_ref(P, C), cr, upto, par);
+}
+RBE_HD u64 spill_alloc_ol(const Planes& P, const Params& C, u32 par, u64 bytes) {
+  return spill_alloc_o(spill_ref(P, C), par, bytes);
+}
+RBE_HD u32 pool_alloc_ol(const Planes& P, const Params& C, u32 par) {
+  return pool_alloc_o(spill_ref(P, C), par);
+}
+RBE_HD void pool_free_ol(const Planes& P, const Params& C, u32 par, u32 page) {
+  pool_free_o(spill_ref(P, C), par, page);
+}
+RBE_HD void rq_ext_free_ol(const Planes& P, const Params& C, const RqExt& q, u32 par) {
+  rq_ext_free_o(spill_ref(P, C), q, par);
+}
+RBE_HD bool stash_put_ol(const Planes& P, const Params& C, u32 par, OutStash& st, const Msg& m) {
+  const StashPut r = stash_put_o(spill_ref(P, C), par, st, m);
+  st = r.st;
+  return r.ok != 0;
+}
+RBE_HD u32 outbox_relocate_ol(const Planes& P, const Params& C, u32 par, u64 rs, u32 n,
+                              const OutStash& st, u64& w_lo, u64& w_hi) {
+  const Reloc r = outbox_relocate_o(spill_ref(P, C), par, rs, n, st, w_lo, w_hi);
+  w_lo = r.lo;
+  w_hi = r.hi;
+  return r.fault;
 }
 
 }  // namespace rbe

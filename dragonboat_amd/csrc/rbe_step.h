@@ -664,7 +664,7 @@ struct Lane {
       e.len = b.len;
       e.lo = b.lo;
       e.hi = b.hi;
-    } else if (!cold_get(P, cold(), idx, &e)) {
+    } else if (!cold_get_ol(P, C, cold(), idx, &e)) {
       set_fault(F_WINDOW);  // the launch gave only the LogDB's tail
       e.term = e.lo = e.hi = 0;
       e.type = e.len = 0;
@@ -725,7 +725,7 @@ struct Lane {
     cold_store(j, e);
   }
   RBE_HD void cold_store(u64 j, const Ent& e) {
-    if (!cold_put(P, C, cold(), j, e, par)) set_fault(F_NOMEM);
+    if (!cold_put_ol(P, C, cold(), j, e, par)) set_fault(F_NOMEM);
     X().cref_dirty = true;
   }
   // an append at idx = last + 1: the entry the ring slot held (idx - ring) goes
@@ -978,7 +978,7 @@ struct Lane {
     if (a + b >= C.maxm) {
       // the plane list is full: the message joins the step's stash, and the
       // list moves whole to the spill heap at the step's end (outbox_relocate)
-      if (stash_put(P, C, par, X().ost, m)) {
+      if (stash_put_ol(P, C, par, X().ost, m)) {
         ctr.v[C_MSG_OUT]++;
         ctr.v[C_ENT_OUT] += ne;
       } else {
@@ -1044,7 +1044,7 @@ struct Lane {
   // cnt entries of the round spill heap for a message whose entries do not
   // fit the sender's arena (granule in *off), ~0 when the heap is full
   RBE_HD Ent* spill_ents(u32 cnt, u32* off) {
-    const u64 g = spill_alloc(P, C, par, (u64)cnt * sizeof(Ent));
+    const u64 g = spill_alloc_ol(P, C, par, (u64)cnt * sizeof(Ent));
     if (g == ~0ull) {
       set_fault(F_NOMEM);
       return nullptr;
@@ -1167,7 +1167,7 @@ struct Lane {
     }
     if (n >= xcap) {  // (re)allocate at twice the size and copy what is there
       const u32 cap = n * 2u;
-      const u64 g = spill_alloc(P, C, par, (u64)cap * sizeof(T));
+      const u64 g = spill_alloc_ol(P, C, par, (u64)cap * sizeof(T));
       if (g == ~0ull) return false;
       T* nb = spill_at<T>(P, par, g);
       const T* ob = xcap ? spill_at<T>(P, par, xg) : plane;
@@ -1581,16 +1581,16 @@ struct Lane {
   // the queue of a full ring into pool pages; false when the pool is exhausted
   RBE_HD bool rq_extend() {
     RqExt x;
-    x.head = x.tail = pool_alloc(P, C, par);
+    x.head = x.tail = pool_alloc_ol(P, C, par);
     if (!x.head) return false;
     P.pmeta[x.head].next = 0;
     x.off = 0;
     x.n = 0;
     for (u32 i = 0; i < rq_count; i++) {
       if (i > 0 && i % kPageEnts == 0) {
-        const u32 p = pool_alloc(P, C, par);
+        const u32 p = pool_alloc_ol(P, C, par);
         if (!p) {
-          rq_ext_free(P, x, par);
+          rq_ext_free_ol(P, C, x, par);
           return false;
         }
         P.pmeta[p].next = 0;
@@ -1614,7 +1614,7 @@ struct Lane {
     if (!X().rqx && !rq_extend()) return false;
     const u32 pos = X().rqd.off + X().rqd.n;
     if (pos % kPageEnts == 0) {  // the tail page is full
-      const u32 p = pool_alloc(P, C, par);
+      const u32 p = pool_alloc_ol(P, C, par);
       if (!p) return false;
       P.pmeta[p].next = 0;
       P.pmeta[X().rqd.tail].next = p;
@@ -1633,20 +1633,20 @@ struct Lane {
     X().rqd.n -= done;
     X().rqd.off += done;
     if (X().rqd.n == 0) {  // drained: back to the plane ring
-      rq_ext_free(P, X().rqd, par);
+      rq_ext_free_ol(P, C, X().rqd, par);
       X().rqx = false;
       rq_head = rq_count = 0;
       return;
     }
     while (X().rqd.off >= kPageEnts) {
       const u32 nx = P.pmeta[X().rqd.head].next;
-      pool_free(P, par, X().rqd.head);
+      pool_free_ol(P, C, par, X().rqd.head);
       X().rqd.head = nx;
       X().rqd.off -= kPageEnts;
     }
   }
   RBE_HD void rq_clear() {
-    if (X().rqx) rq_ext_free(P, X().rqd, par);
+    if (X().rqx) rq_ext_free_ol(P, C, X().rqd, par);
     X().rqx = false;
     rq_head = rq_count = 0;
   }
@@ -1869,7 +1869,7 @@ struct Lane {
       const u64 hi = umin64(c - 1, L0 - R);
       for (; lo <= hi; lo++) {
         Ent e;
-        if (!cold_get(P, cold(), lo, &e)) {
+        if (!cold_get_ol(P, C, cold(), lo, &e)) {
           set_fault(F_WINDOW);
           continue;
         }
@@ -1975,7 +1975,7 @@ struct Lane {
         committed = processed = saved_to = si;
         marker = si;
         marker_term = st;
-        cold_release(P, cold(), ~0ull, par);  // the log is the snapshot now
+        cold_release_ol(P, C, cold(), ~0ull, par);  // the log is the snapshot now
         X().cref_dirty = true;
         P.term_ring[ring_slot(si)] = st;  // the fast steps read Term(marker) from the ring
         SnapSt& sp = P.snp[r];
@@ -2604,7 +2604,7 @@ struct Lane {
       if (c > marker && c <= last && c <= sp.ss_index) {
         sp.marker_term = log_term(c);
         sp.marker = c;
-        cold_release(P, cold(), c, par);  // the cold log's pages at or below it
+        cold_release_ol(P, C, cold(), c, par);  // the cold log's pages at or below it
         X().cref_dirty = true;
       }
       sp.compact_to = 0;
@@ -3221,7 +3221,7 @@ struct Lane {
     // this round's outbox header: the count word of every destination list;
     // a list with stashed messages moves whole to the spill heap (rbe_spill.h)
     if (X().ost.n) {
-      const u32 f = outbox_relocate(P, C, par, r, N, X().ost, pc_lo, pc_hi);
+      const u32 f = outbox_relocate_ol(P, C, par, r, N, X().ost, pc_lo, pc_hi);
       if (f) set_fault(f);
     }
     u32 ow[N];
@@ -3408,12 +3408,12 @@ RBE_HD bool step_replica_fast(const Planes& P, const Params& C, u64 r, Clk ck,
 RBE_HD void spill_replica_release(const Planes& P, const Params& C, u64 r, u32 par) {
   ColdRef cr = P.cold[r];
   if (cr.head) {
-    cold_release(P, cr, ~0ull, par);
+    cold_release_ol(P, C, cr, ~0ull, par);
     P.cold[r] = cr;
   }
   Core& c = P.core[r];
   if (c.rq_count == kRqExt) {
-    rq_ext_free(P, rq_ext_load(P, C, r), par);
+    rq_ext_free_ol(P, C, rq_ext_load(P, C, r), par);
     c.rq_count = 0;
     c.rq_head = 0;
   }
@@ -3641,7 +3641,7 @@ RBE_HD void relaunch_replica(const Planes& P, const Params& C, u64 r, u64 term, 
       e.len = b[i].len;
       e.lo = b[i].lo;
       e.hi = b[i].hi;
-      if (!cold_put(P, C, cr, idx, e, par)) sfault |= F_NOMEM;
+      if (!cold_put_ol(P, C, cr, idx, e, par)) sfault |= F_NOMEM;
       continue;
     }
     const u64 slot = (idx & (u64)(C.ring - 1)) * C.n_rep + r;

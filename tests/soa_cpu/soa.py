@@ -18,7 +18,8 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
-        p = os.path.join(_HERE, "libsoa_cpu.so")
+        # SOA_LIB: a variant build of the host tier (A/B knobs of the steps)
+        p = os.environ.get("SOA_LIB") or os.path.join(_HERE, "libsoa_cpu.so")
         if not os.path.exists(p):
             raise RuntimeError(f"{p} missing: run __graft_entry__.build()")
         L = C.CDLL(p)
