@@ -142,7 +142,7 @@ RBE_HD LeadMsg load_lead(const Msg* p) {
 // A/B knobs (build variants): the evicted entry's cold-log store as the
 // step's first store, freeing its registers early; the outbox stash in LDS
 #ifndef RBE_FAST_EV_EARLY
-#define RBE_FAST_EV_EARLY 0
+#define RBE_FAST_EV_EARLY 1
 #endif
 #ifndef RBE_FAST_STASH_LDS
 #define RBE_FAST_STASH_LDS 0
