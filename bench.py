@@ -468,10 +468,14 @@ def run_host_driven(args, ws, rank, local, dist):
     # node besides those messages (RBE_COLLECT_SKIP_LOCAL)
     all_msgs = args.c4h_all_msgs
     cflags = RBE_COLLECT_REMOTE_MSGS | RBE_COLLECT_SKIP_LOCAL
+    # default: rbe_collect_step_begin / _end with the next round's pushes in
+    # between (requests go to the leaders known through the round before);
+    # --c4h-serial: push, step, sync, collect, one after the other
+    pipelined = not all_msgs and not args.c4h_serial
     cmd = np.frombuffer(rng.bytes(16 * len(active)), dtype=np.uint8).copy()
     ptr = lambda a, t: a.ctypes.data_as(C.POINTER(t))  # noqa: E731
     stats = {"push": 0.0, "push_abi": 0.0, "step": 0.0, "enqueue": 0.0, "out": 0.0, "reads": 0,
-             "props": 0, "msgs": 0, "rtr": 0, "upd": 0}
+             "props": 0, "msgs": 0, "rtr": 0, "upd": 0, "push_next": 0.0}
 
     # the node layer learns a group's leader from the listener's LeaderUpdated
     # (event.go:93-95), which the engine reports in Update.events
@@ -529,8 +533,10 @@ def run_host_driven(args, ws, rank, local, dist):
     zero = np.zeros(len(active), dtype=np.uint32)
     ln = np.full(len(active), 16, dtype=np.uint32)
 
-    def one_round(rnd, timed):
-        t0 = time.perf_counter()
+    def push_round(rnd):
+        """The client requests of round rnd, staged at the leaders known so
+        far (rbe_push_read_index / rbe_push_proposals); returns (reads,
+        proposals, seconds in the ABI calls)."""
         rr, pr = lead_rep[read_at[rnd]], lead_rep[prop_at[rnd]]
         if (len(rr) and rr.max() == NONE) or (len(pr) and pr.max() == NONE):
             rr, pr = rr[rr != NONE], pr[pr != NONE]  # groups without a leader wait
@@ -544,21 +550,59 @@ def run_host_driven(args, ws, rank, local, dist):
             _check(L.rbe_push_proposals(h, len(pr), ptr(pr, C.c_uint64), ptr(one, C.c_uint32),
                                         ptr(zero, C.c_uint32), ptr(ln, C.c_uint32),
                                         ptr(cmd, C.c_uint8)), "rbe_push_proposals")
+        return len(rr), len(pr), time.perf_counter() - tc
+
+    def parse_step_outputs():
+        n = so.n
+        if n:  # the engine's mapped buffer, read in place
+            rep = np.ctypeslib.as_array(so.replica, shape=(n,))
+            ups = np.frombuffer((C.c_uint8 * (n * UPDATE_DTYPE.itemsize)).from_address(
+                C.addressof(so.updates.contents)), dtype=UPDATE_DTYPE)
+            note_leaders(rep, ups)
+        return so.n_messages, so.n_ready_to_reads, n
+
+    pending = {"pushed": None}  # round whose requests are staged already (pipelined)
+
+    def one_round(rnd, timed):
+        t0 = time.perf_counter()
+        if pending["pushed"] == rnd:
+            nrd, npr, tabi = pending["counts"]
+        else:
+            nrd, npr, tabi = push_round(rnd)
         t1 = time.perf_counter()
         eng.step()
         te = time.perf_counter()
-        eng.sync()
-        t2 = time.perf_counter()
-        nm, nr, nu = read_back()
-        t3 = time.perf_counter()
+        if pipelined:
+            # the collection of this round runs on the device while the host
+            # stages the next round's requests (leaders as known through the
+            # last round), then the outputs are read in place
+            _check(L.rbe_collect_step_begin(h, 0, n_rep, cflags), "rbe_collect_step_begin")
+            tq = time.perf_counter()
+            pending["counts"] = push_round(rnd + 1)
+            pending["pushed"] = rnd + 1
+            tn = time.perf_counter()
+            _check(L.rbe_collect_step_end(h, C.byref(so)), "rbe_collect_step_end")
+            t2 = t3 = time.perf_counter()
+            nm, nr, nu = parse_step_outputs()
+            t3 = time.perf_counter()
+        else:
+            eng.sync()
+            t2 = time.perf_counter()
+            nm, nr, nu = read_back()
+            t3 = time.perf_counter()
         if timed:
             stats["push"] += t1 - t0
-            stats["push_abi"] += t1 - tc
-            stats["step"] += t2 - t1
+            stats["push_abi"] += tabi
             stats["enqueue"] += te - t1
-            stats["out"] += t3 - t2
-            stats["reads"] += len(rr)
-            stats["props"] += len(pr)
+            if pipelined:
+                stats["push_next"] += tn - tq  # overlapped with the device
+                stats["step"] += t2 - t1 - (tn - tq)  # step + collection not hidden by it
+                stats["out"] += t3 - t2  # parsing the mapped records
+            else:
+                stats["step"] += t2 - t1
+                stats["out"] += t3 - t2
+            stats["reads"] += nrd
+            stats["props"] += npr
             stats["msgs"] += nm
             stats["rtr"] += nr
             stats["upd"] += nu
@@ -610,10 +654,17 @@ def run_host_driven(args, ws, rank, local, dist):
                 # host part of the step call: input upload staging + launches
                 "step_enqueue_ms_per_round": stats["enqueue"] * 1e3 / K,
                 "read_back": "rbe_collect_updates + rbe_collect_outputs (every message)"
-                if all_msgs else ("rbe_collect_step (messages for other engines only; "
-                                  "RBE_COLLECT_SKIP_LOCAL: Updates with work for the node)"),
+                if all_msgs else ((("rbe_collect_step_begin / _end, the next round's pushes "
+                                    "in between") if pipelined else "rbe_collect_step") +
+                                  " (messages for other engines only; RBE_COLLECT_SKIP_LOCAL: "
+                                  "Updates with work for the node)"),
                 "outputs_ms_per_round": stats["out"] * 1e3 / K,
-                "boundary_share": (stats["push"] + stats["out"]) / max(1e-12, wall),
+                "pipelined": pipelined,
+                # pipelined: the next round's pushes, made while the device
+                # steps and collects this one (inside step_ms when not)
+                "push_overlapped_ms_per_round": stats["push_next"] * 1e3 / K,
+                "boundary_share": (stats["push"] + stats["push_next"] + stats["out"]) /
+                max(1e-12, wall),
                 "reads_pushed_per_round": stats["reads"] / K,
                 "proposals_pushed_per_round": stats["props"] / K,
                 "messages_read_per_round": stats["msgs"] / K,
@@ -652,6 +703,9 @@ def main():
                     help="other workloads timed briefly in the same run (comma list, '' = none)")
     ap.add_argument("--c4h-all-msgs", action="store_true",
                     help="c4h: read every message back too (rbe_collect_outputs)")
+    ap.add_argument("--c4h-serial", action="store_true",
+                    help="c4h: push, step, sync and collect one after the other "
+                         "(default: rbe_collect_step_begin / _end around the next round's pushes)")
     ap.add_argument("--xchg-fixed", action="store_true",
                     help="c5: fixed-capacity exchange (count headers, no host-side count read)")
     args = ap.parse_args()

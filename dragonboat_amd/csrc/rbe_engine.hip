@@ -363,13 +363,30 @@ __global__ __launch_bounds__(kBlock) void k_cs_count(Planes P, Params C, u64 fir
     bsum[3 * blockIdx.x + 2] = tr;
   }
 }
+// the capacities of the regions k_cs_write fills (rbe_collect_step_begin:
+// engine-owned mapped host memory); hdr (when non-null) receives the three
+// totals and an overflow word, and nothing is written past a capacity
+struct CsCaps {
+  u64 n, m, r;
+  u64* hdr;
+};
 __global__ __launch_bounds__(kBlock) void k_cs_write(Planes P, Params C, u64 first, u64 count,
                                                      u32 round, u32 cflags, const u64* pre,
                                                      u64* rep, rbe_update* ou, u64* moff,
                                                      rbe_message* om, u64* roff,
-                                                     rbe_ready_to_read* orr, u64 n_tot) {
+                                                     rbe_ready_to_read* orr, CsCaps caps) {
   const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
   const bool remote = (cflags & RBE_COLLECT_REMOTE_MSGS) != 0;
+  const u64 n_tot = pre[3 * gridDim.x], m_tot = pre[3 * gridDim.x + 1],
+            r_tot = pre[3 * gridDim.x + 2];
+  const bool over = n_tot > caps.n || m_tot > caps.m || r_tot > caps.r;
+  if (caps.hdr && blockIdx.x == 0 && threadIdx.x == 0) {
+    caps.hdr[0] = n_tot;
+    caps.hdr[1] = m_tot;
+    caps.hdr[2] = r_tot;
+    caps.hdr[3] = over ? 1u : 0u;
+  }
+  if (over) return;
   u32 f = 0, nm = 0, nr = 0;
   if (i < count) step_out_counts(P, C, first + i, round, cflags, &f, &nm, &nr);
   u32 t;
@@ -728,6 +745,16 @@ struct rbe_engine {
   u64 cs_dev_bytes = 0;
   u8* cs_host = nullptr;
   u64 cs_host_bytes = 0;
+  // rbe_collect_step_begin / _end: mapped host memory the write kernel fills
+  // directly (header | replicas | updates | offsets | messages | ReadyToReads),
+  // its capacities, the pending call and its completion event
+  u8* csa_host = nullptr;
+  u64 csa_bytes = 0;
+  u64 csa_cap[3] = {0, 0, 0};
+  bool csa_pending = false;
+  u64 csa_first = 0, csa_count = 0;
+  u32 csa_flags = 0, csa_round = 0;
+  hipEvent_t csa_ev = nullptr;
   // rbe_wire_encode / rbe_wire_decode scratch
   u8* wire_dev = nullptr;    // the last rbe_wire_encode's frames (rbe_wire_fetch)
   u64 wire_dev_bytes = 0;
@@ -1192,6 +1219,8 @@ int rbe_destroy(rbe_engine* e) {
   if (e->cs_dev) HIP_IGNORE(hipFree(e->cs_dev));
   if (e->P.prof) HIP_IGNORE(hipFree(e->P.prof));
   if (e->cs_host) HIP_IGNORE(hipHostFree(e->cs_host));
+  if (e->csa_host) HIP_IGNORE(hipHostFree(e->csa_host));
+  if (e->csa_ev) HIP_IGNORE(hipEventDestroy(e->csa_ev));
   if (e->wire_dev) HIP_IGNORE(hipFree(e->wire_dev));
   if (e->wire_meta) HIP_IGNORE(hipFree(e->wire_meta));
   if (e->wire_rec) HIP_IGNORE(hipFree(e->wire_rec));
@@ -2573,7 +2602,8 @@ int rbe_collect_step(rbe_engine* e, uint64_t first, uint64_t count, uint32_t fla
   hipLaunchKernelGGL(k_cs_write, dim3(nb), dim3(kBlock), 0, e->stream, e->P, e->C, (u64)first,
                      (u64)count, e->round, flags, (const u64*)(d + o_pre), (u64*)(d + o_rep),
                      (rbe_update*)(d + o_upd), (u64*)(d + o_moff), (rbe_message*)(d + o_msg),
-                     (u64*)(d + o_roff), (rbe_ready_to_read*)(d + o_rtr), n);
+                     (u64*)(d + o_roff), (rbe_ready_to_read*)(d + o_rtr),
+                     CsCaps{n, tot[1], tot[2], nullptr});
   HIP_OK(hipGetLastError());
   if ((rc = grow(&e->cs_host, &e->cs_host_bytes, need - o_rep, true))) return rc;
   HIP_OK(hipMemcpyAsync(e->cs_host, d + o_rep, need - o_rep, hipMemcpyDeviceToHost, e->stream));
@@ -2588,6 +2618,100 @@ int rbe_collect_step(rbe_engine* e, uint64_t first, uint64_t count, uint32_t fla
   out->rtr_off = (const uint64_t*)(h + o_roff);
   out->messages = (const rbe_message*)(h + o_msg);
   out->ready_to_reads = (const rbe_ready_to_read*)(h + o_rtr);
+  return RBE_OK;
+}
+
+// rbe_collect_step in two halves (rbe.h): _begin enqueues the count, scan
+// and write kernels, the write kernel filling engine-owned mapped host memory
+// directly, and returns at once; _end waits for them and hands out the
+// records.  The host's own work of the next round (rbe_push_*) fits between.
+static u64 csa_layout(const u64* cap, u64* o) {  // region offsets in the mapped buffer
+  auto al = [](u64 x) { return (x + 255) & ~255ull; };
+  o[0] = 256;                                             // replicas (after the header)
+  o[1] = o[0] + al(cap[0] * sizeof(u64));                 // updates
+  o[2] = o[1] + al(cap[0] * sizeof(rbe_update));          // msg offsets
+  o[3] = o[2] + al((cap[0] + 1) * sizeof(u64));           // rtr offsets
+  o[4] = o[3] + al((cap[0] + 1) * sizeof(u64));           // messages
+  o[5] = o[4] + al(cap[1] * sizeof(rbe_message));         // ReadyToReads
+  return o[5] + al(cap[2] * sizeof(rbe_ready_to_read));  // total
+}
+int rbe_collect_step_begin(rbe_engine* e, uint64_t first, uint64_t count, uint32_t flags) {
+  if (!e || count == 0 || first >= e->C.n_rep || count > e->C.n_rep - first ||
+      (flags & ~(RBE_COLLECT_REMOTE_MSGS | RBE_COLLECT_SKIP_LOCAL)))
+    return RBE_E_INVALID;
+  if (e->round == 0 || e->csa_pending) return RBE_E_STATE;
+  HIP_OK(hipSetDevice(e->device));
+  // capacities: at least a quarter of the range's Updates and the last
+  // call's totals with room; a round past them is collected again by _end
+  const u64 floor_n = std::min<u64>(count, std::max<u64>(count / 4, 4096));
+  if (e->csa_cap[0] < floor_n) e->csa_cap[0] = floor_n;
+  if (e->csa_cap[2] < 4096) e->csa_cap[2] = 4096;
+  u64 o[6];
+  const u64 need = csa_layout(e->csa_cap, o);
+  if (need > e->csa_bytes) {
+    if (e->csa_host) HIP_OK(hipHostFree(e->csa_host));
+    e->csa_host = nullptr;
+    e->csa_bytes = 0;
+    HIP_OK(hipHostMalloc((void**)&e->csa_host, need, hipHostMallocMapped));
+    e->csa_bytes = need;
+  }
+  if (!e->csa_ev) HIP_OK(hipEventCreateWithFlags(&e->csa_ev, hipEventDisableTiming));
+  u8* d = nullptr;
+  HIP_OK(hipHostGetDevicePointer((void**)&d, e->csa_host, 0));
+  const u32 nb = grid_for(count);
+  auto al = [](u64 x) { return (x + 255) & ~255ull; };
+  const u64 o_pre = al(3ull * nb * sizeof(u32)), o_end = o_pre + al(scan_words(3, nb) * sizeof(u64));
+  int rc = grow(&e->cs_dev, &e->cs_dev_bytes, o_end, false);
+  if (rc) return rc;
+  const u64* pre = (const u64*)(e->cs_dev + o_pre);
+  hipLaunchKernelGGL(k_cs_count, dim3(nb), dim3(kBlock), 0, e->stream, e->P, e->C, (u64)first,
+                     (u64)count, e->round, flags, (u32*)e->cs_dev);
+  if ((rc = launch_scan<3>(e->stream, (const u32*)e->cs_dev, nb, (u64*)pre))) return rc;
+  hipLaunchKernelGGL(k_cs_write, dim3(nb), dim3(kBlock), 0, e->stream, e->P, e->C, (u64)first,
+                     (u64)count, e->round, flags, pre, (u64*)(d + o[0]), (rbe_update*)(d + o[1]),
+                     (u64*)(d + o[2]), (rbe_message*)(d + o[4]), (u64*)(d + o[3]),
+                     (rbe_ready_to_read*)(d + o[5]),
+                     CsCaps{e->csa_cap[0], e->csa_cap[1], e->csa_cap[2], (u64*)d});
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(e->csa_ev, e->stream));
+  e->csa_pending = true;
+  e->csa_first = first;
+  e->csa_count = count;
+  e->csa_flags = flags;
+  e->csa_round = e->round;
+  return RBE_OK;
+}
+
+int rbe_collect_step_end(rbe_engine* e, rbe_step_outputs* out) {
+  if (!e || !out) return RBE_E_INVALID;
+  if (!e->csa_pending) return RBE_E_STATE;
+  e->csa_pending = false;
+  if (e->round != e->csa_round) return RBE_E_STATE;  // a step ran in between: outputs gone
+  HIP_OK(hipSetDevice(e->device));
+  HIP_OK(hipEventSynchronize(e->csa_ev));
+  const volatile u64* hdr = (const volatile u64*)e->csa_host;
+  const u64 n = hdr[0], nm = hdr[1], nr = hdr[2];
+  if (hdr[3]) {  // past the capacities: grow them, collect synchronously this once
+    e->csa_cap[0] = std::max(e->csa_cap[0], n + n / 4);
+    e->csa_cap[1] = std::max(e->csa_cap[1], nm + nm / 4);
+    e->csa_cap[2] = std::max(e->csa_cap[2], nr + nr / 4);
+    return rbe_collect_step(e, e->csa_first, e->csa_count, e->csa_flags, out);
+  }
+  u64 o[6];
+  csa_layout(e->csa_cap, o);
+  memset(out, 0, sizeof(*out));
+  out->first = e->csa_first;
+  out->count = e->csa_count;
+  out->n = n;
+  out->n_messages = nm;
+  out->n_ready_to_reads = nr;
+  u8* h = e->csa_host;
+  out->replica = (const uint64_t*)(h + o[0]);
+  out->updates = (const rbe_update*)(h + o[1]);
+  out->msg_off = (const uint64_t*)(h + o[2]);
+  out->rtr_off = (const uint64_t*)(h + o[3]);
+  out->messages = (const rbe_message*)(h + o[4]);
+  out->ready_to_reads = (const rbe_ready_to_read*)(h + o[5]);
   return RBE_OK;
 }
 

@@ -226,7 +226,8 @@ EXPORTS = ["rbe_create", "rbe_destroy", "rbe_abi_version", "rbe_abi_sizes", "rbe
            "rbe_wire_fetch", "rbe_wire_decode", "rbe_wire_ingest", "rbe_iso_leaders", "rbe_set_iso_leaders", "rbe_local_groups", "rbe_propose_entries", "rbe_commit",
            "rbe_get_update_commits", "rbe_get_update_snapshots", "rbe_replace_node", "rbe_propose_config_change", "rbe_apply_config_change",
            "rbe_reject_config_change", "rbe_rate_limited", "rbe_restore_remotes",
-           "rbe_snapshot_saved", "rbe_compact", "rbe_set_node_ids", "rbe_collect_step"]
+           "rbe_snapshot_saved", "rbe_compact", "rbe_set_node_ids", "rbe_collect_step",
+           "rbe_collect_step_begin", "rbe_collect_step_end"]
 KERNEL_SLOTS = 4
 
 _lib = None
@@ -288,6 +289,8 @@ def load_library(path: Optional[str] = None):
         "rbe_get_updates": (i32, [vp, u64, u64, P(RbeUpdate)]),
         "rbe_collect_updates": (i32, [vp, u64, u64, P(RbeUpdateList)]),
         "rbe_collect_step": (i32, [vp, u64, u64, u32, P(RbeStepOutputs)]),
+        "rbe_collect_step_begin": (i32, [vp, u64, u64, u32]),
+        "rbe_collect_step_end": (i32, [vp, P(RbeStepOutputs)]),
         "rbe_get_messages": (i32, [vp, u64, P(RbeMessage), u32, P(u32)]),
         "rbe_get_outbox": (i32, [vp, u64, P(RbeMessage), u32, P(u32), P(RbeEntry), u32, P(u32),
                                  vp, u64, P(u64)]),
@@ -1008,7 +1011,23 @@ class Engine(NodeInputs):
         o = RbeStepOutputs()
         fl = (RBE_COLLECT_REMOTE_MSGS if remote_only else 0) | (RBE_COLLECT_SKIP_LOCAL if skip_local else 0)
         _check(self.lib.rbe_collect_step(self.h, first, count, fl, C.byref(o)), "rbe_collect_step")
+        return self._step_outputs(o)
 
+    def collect_step_begin(self, first: int = 0, count: Optional[int] = None, remote_only=False,
+                           skip_local=False):
+        """rbe_collect_step_begin: enqueue the collection of the last round's
+        outputs; collect_step_end() returns what collect_step would."""
+        count = self.n_rep - first if count is None else count
+        fl = (RBE_COLLECT_REMOTE_MSGS if remote_only else 0) | (RBE_COLLECT_SKIP_LOCAL if skip_local else 0)
+        _check(self.lib.rbe_collect_step_begin(self.h, first, count, fl), "rbe_collect_step_begin")
+
+    def collect_step_end(self):
+        o = RbeStepOutputs()
+        _check(self.lib.rbe_collect_step_end(self.h, C.byref(o)), "rbe_collect_step_end")
+        return self._step_outputs(o)
+
+    @staticmethod
+    def _step_outputs(o):
         def arr(ptr, n, dtype):
             if n == 0:
                 return np.zeros(0, dtype=dtype)

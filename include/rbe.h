@@ -737,6 +737,20 @@ typedef struct rbe_step_outputs {
 } rbe_step_outputs;
 int rbe_collect_step(rbe_engine* e, uint64_t first, uint64_t count, uint32_t flags,
                      rbe_step_outputs* out);
+/* rbe_collect_step in two halves, so the node layer's host work for the next
+ * round (rbe_push_*) runs while the device collects this one:
+ *   rbe_collect_step_begin enqueues the collection of the last round's
+ *     outputs (the same records and flags as rbe_collect_step) and returns at
+ *     once; the records go straight into engine-owned mapped host memory;
+ *   rbe_collect_step_end waits for it and fills *out exactly as
+ *     rbe_collect_step would.  When a round has more records than the buffer
+ *     the engine sized from the earlier rounds, _end collects that round again
+ *     synchronously (and grows the buffer).
+ * Between the two no step may run (rbe_step / rbe_run: _end then returns
+ * RBE_E_STATE); rbe_push_* and the other host-side calls may.  The records are
+ * valid until the next _begin or rbe_destroy. */
+int rbe_collect_step_begin(rbe_engine* e, uint64_t first, uint64_t count, uint32_t flags);
+int rbe_collect_step_end(rbe_engine* e, rbe_step_outputs* out);
 int rbe_get_counters(rbe_engine* e, uint64_t* out /* RBE_CTR_NUM */);
 /* the counters one pipeline kernel (RBE_KERNEL_*) contributed */
 int rbe_get_kernel_counters(rbe_engine* e, int32_t kernel, uint64_t* out /* RBE_CTR_NUM */);
