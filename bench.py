@@ -412,10 +412,13 @@ def run_replica_mode(args, ws, rank, local, dist, dev, gloo_staged):
             "exchange": {"bytes_per_round_all_ranks": sent_all / args.steps,
                          "ms_per_round_mean_rank": xms_mean,
                          "mode": "fixed" if (xch is not None and xch.fixed) else "counted",
-                         # one fixed chunk over the largest counted round's
+                         # one fixed chunk over the mean counted round's
                          # records to one peer (rank 0): the padding
                          "fixed_pad": xch.pad_ratio() if (xch is not None and xch.fixed)
-                         else None},
+                         else None,
+                         # fixed rounds whose records outgrew the chunks, repaired
+                         # by a counted second pass (rank 0; never invalid)
+                         "repaired_rounds": xch.repaired if xch is not None else 0},
             "roofline": {"bound": "hbm", "achieved": dom["achieved_gbs"], "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": dom["achieved_gbs"] / HBM_PEAK_GBS,
                          "traffic": None, "kernel": dom["kernel"],
@@ -525,7 +528,7 @@ def run_host_driven(args, ws, rank, local, dist):
     # the client workload of every round, drawn before the timed region
     # (synthetic requests, not node-layer work): which active groups get a
     # ReadIndex (90%) and which a proposal
-    total_rounds = settle + max(1, args.warmup) + args.steps
+    total_rounds = settle + max(1, args.warmup) + args.steps + 1  # (+1: the pipelined next push)
     read_mask = rng.random((total_rounds, len(active))) < 0.9
     read_at = [np.flatnonzero(m) for m in read_mask]
     prop_at = [np.flatnonzero(~m) for m in read_mask]
@@ -552,16 +555,20 @@ def run_host_driven(args, ws, rank, local, dist):
                                         ptr(cmd, C.c_uint8)), "rbe_push_proposals")
         return len(rr), len(pr), time.perf_counter() - tc
 
-    def parse_step_outputs():
-        n = so.n
+    def parse_step_outputs(o):
+        n = o.n
         if n:  # the engine's mapped buffer, read in place
-            rep = np.ctypeslib.as_array(so.replica, shape=(n,))
+            rep = np.ctypeslib.as_array(o.replica, shape=(n,))
             ups = np.frombuffer((C.c_uint8 * (n * UPDATE_DTYPE.itemsize)).from_address(
-                C.addressof(so.updates.contents)), dtype=UPDATE_DTYPE)
+                C.addressof(o.updates.contents)), dtype=UPDATE_DTYPE)
             note_leaders(rep, ups)
-        return so.n_messages, so.n_ready_to_reads, n
+        return o.n_messages, o.n_ready_to_reads, n
 
-    pending = {"pushed": None}  # round whose requests are staged already (pipelined)
+    # pipelined: the round whose requests are staged already, and the outputs
+    # of the last round (the engine's two mapped buffers, used in turn), read
+    # while the device runs the next step
+    pending = {"pushed": None, "outs": None}
+    so_pair = [RbeStepOutputs(), RbeStepOutputs()]
 
     def one_round(rnd, timed):
         t0 = time.perf_counter()
@@ -573,18 +580,24 @@ def run_host_driven(args, ws, rank, local, dist):
         eng.step()
         te = time.perf_counter()
         if pipelined:
-            # the collection of this round runs on the device while the host
-            # stages the next round's requests (leaders as known through the
-            # last round), then the outputs are read in place
+            # while the device runs this step: the last round's outputs are
+            # read in place; then this round's collection runs on the device
+            # while the host stages the next round's requests (at the leaders
+            # known through the round before the last)
+            nm = nr = nu = 0
+            if pending["outs"] is not None:
+                nm, nr, nu = parse_step_outputs(pending["outs"])
+                pending["outs"] = None
+            tp = time.perf_counter()
             _check(L.rbe_collect_step_begin(h, 0, n_rep, cflags), "rbe_collect_step_begin")
             tq = time.perf_counter()
             pending["counts"] = push_round(rnd + 1)
             pending["pushed"] = rnd + 1
             tn = time.perf_counter()
-            _check(L.rbe_collect_step_end(h, C.byref(so)), "rbe_collect_step_end")
+            o = so_pair[rnd & 1]
+            _check(L.rbe_collect_step_end(h, C.byref(o)), "rbe_collect_step_end")
+            pending["outs"] = o
             t2 = t3 = time.perf_counter()
-            nm, nr, nu = parse_step_outputs()
-            t3 = time.perf_counter()
         else:
             eng.sync()
             t2 = time.perf_counter()
@@ -596,8 +609,9 @@ def run_host_driven(args, ws, rank, local, dist):
             stats["enqueue"] += te - t1
             if pipelined:
                 stats["push_next"] += tn - tq  # overlapped with the device
-                stats["step"] += t2 - t1 - (tn - tq)  # step + collection not hidden by it
-                stats["out"] += t3 - t2  # parsing the mapped records
+                stats["out"] += tp - te  # the last round's records, read during this step
+                # step + collection not hidden by the two
+                stats["step"] += t2 - t1 - (tn - tq) - (tp - te)
             else:
                 stats["step"] += t2 - t1
                 stats["out"] += t3 - t2
@@ -621,9 +635,19 @@ def run_host_driven(args, ws, rank, local, dist):
     eng.reset_counters()
     if dist is not None:
         dist.barrier()
+    if pending["outs"] is not None:  # the warmup's last outputs
+        parse_step_outputs(pending["outs"])
+        pending["outs"] = None
     t0 = time.perf_counter()
     for r in range(args.steps):
         one_round(settle + args.warmup + r, True)
+    if pending["outs"] is not None:  # the last timed round's outputs
+        tl = time.perf_counter()
+        nm, nr, nu = parse_step_outputs(pending["outs"])
+        stats["out"] += time.perf_counter() - tl
+        stats["msgs"] += nm
+        stats["rtr"] += nr
+        stats["upd"] += nu
     eng.sync()
     if dist is not None:
         dist.barrier()

@@ -594,7 +594,8 @@ __global__ __launch_bounds__(kBlock) void k_xchg_pack(Planes P, Params C, u32 pa
 }
 // fixed layout: each peer's chunk header from the pack counts (one thread per
 // peer); an overflow also marks the engine's sticky flag
-__global__ void k_xchg_hdr(u8* buf, XchgCaps caps, const u32* gcount, u32 world, u32* flag) {
+__global__ void k_xchg_hdr(u8* buf, XchgCaps caps, const u32* gcount, u32 world, u32 self,
+                           u32* flag) {
   const u32 p = threadIdx.x;
   if (p >= world) return;
   XHdr h;
@@ -606,7 +607,7 @@ __global__ void k_xchg_hdr(u8* buf, XchgCaps caps, const u32* gcount, u32 world,
     if (n > caps.cap[t]) h.overflow = 1;
   }
   if (h.overflow) atomicOr(flag, 1u);
-  *(XHdr*)(buf + p * xchg_chunk_bytes(caps.cap, kXHdrBytes)) = h;
+  *(XHdr*)(buf + xchg_fixed_off(caps.cap, p, self)) = h;
 }
 // fixed layout, receive side: one lane per record slot of stream t of every
 // source chunk; slots past a chunk's count do nothing
@@ -748,8 +749,10 @@ struct rbe_engine {
   // rbe_collect_step_begin / _end: mapped host memory the write kernel fills
   // directly (header | replicas | updates | offsets | messages | ReadyToReads),
   // its capacities, the pending call and its completion event
-  u8* csa_host = nullptr;
-  u64 csa_bytes = 0;
+  u8* csa_buf[2] = {nullptr, nullptr};  // two, used in turn: a round's records
+  u64 csa_bytes[2] = {0, 0};              // outlive the next round's _begin
+  u32 csa_slot = 0;
+  u8* csa_host = nullptr;                 // the slot of the pending / last call
   u64 csa_cap[3] = {0, 0, 0};
   bool csa_pending = false;
   u64 csa_first = 0, csa_count = 0;
@@ -1219,7 +1222,8 @@ int rbe_destroy(rbe_engine* e) {
   if (e->cs_dev) HIP_IGNORE(hipFree(e->cs_dev));
   if (e->P.prof) HIP_IGNORE(hipFree(e->P.prof));
   if (e->cs_host) HIP_IGNORE(hipHostFree(e->cs_host));
-  if (e->csa_host) HIP_IGNORE(hipHostFree(e->csa_host));
+  for (int i = 0; i < 2; i++)
+    if (e->csa_buf[i]) HIP_IGNORE(hipHostFree(e->csa_buf[i]));
   if (e->csa_ev) HIP_IGNORE(hipEventDestroy(e->csa_ev));
   if (e->wire_dev) HIP_IGNORE(hipFree(e->wire_dev));
   if (e->wire_meta) HIP_IGNORE(hipFree(e->wire_meta));
@@ -2094,7 +2098,8 @@ int rbe_xchg_pack_fixed(rbe_engine* e, void* buf, const uint64_t* cap3) {
   });
   if (rc) return rc;
   hipLaunchKernelGGL(k_xchg_hdr, dim3(1), dim3(64), 0, e->stream, (u8*)buf, caps,
-                     (const u32*)e->xcount, e->C.rep_world, e->xcount + kXchgMaxWorld * XS_NUM);
+                     (const u32*)e->xcount, e->C.rep_world, e->C.rep_rank,
+                     e->xcount + kXchgMaxWorld * XS_NUM);
   HIP_OK(hipGetLastError());
   return RBE_OK;  // no host synchronisation: the counts travel in the chunk headers
 }
@@ -2648,13 +2653,16 @@ int rbe_collect_step_begin(rbe_engine* e, uint64_t first, uint64_t count, uint32
   if (e->csa_cap[2] < 4096) e->csa_cap[2] = 4096;
   u64 o[6];
   const u64 need = csa_layout(e->csa_cap, o);
-  if (need > e->csa_bytes) {
-    if (e->csa_host) HIP_OK(hipHostFree(e->csa_host));
-    e->csa_host = nullptr;
-    e->csa_bytes = 0;
-    HIP_OK(hipHostMalloc((void**)&e->csa_host, need, hipHostMallocMapped));
-    e->csa_bytes = need;
+  const u32 sl = e->csa_slot;
+  e->csa_slot ^= 1u;
+  if (need > e->csa_bytes[sl]) {
+    if (e->csa_buf[sl]) HIP_OK(hipHostFree(e->csa_buf[sl]));
+    e->csa_buf[sl] = nullptr;
+    e->csa_bytes[sl] = 0;
+    HIP_OK(hipHostMalloc((void**)&e->csa_buf[sl], need, hipHostMallocMapped));
+    e->csa_bytes[sl] = need;
   }
+  e->csa_host = e->csa_buf[sl];
   if (!e->csa_ev) HIP_OK(hipEventCreateWithFlags(&e->csa_ev, hipEventDisableTiming));
   u8* d = nullptr;
   HIP_OK(hipHostGetDevicePointer((void**)&d, e->csa_host, 0));

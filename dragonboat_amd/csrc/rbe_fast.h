@@ -144,6 +144,9 @@ RBE_HD LeadMsg load_lead(const Msg* p) {
 #ifndef RBE_FAST_EV_EARLY
 #define RBE_FAST_EV_EARLY 1
 #endif
+#ifndef RBE_FAST_PAUSED  // leaders with a paused remote behind take the fast step
+#define RBE_FAST_PAUSED 1
+#endif
 #ifndef RBE_FAST_STASH_LDS
 #define RBE_FAST_STASH_LDS 0
 #endif
@@ -773,8 +776,14 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
 #pragma unroll
   for (u32 s = 0; s < N; s++) {
     // every entry a Replicate of this round can carry is the one proposed
-    // this round (so no ring read is needed after the first store)
-    if (s != k && next[s] <= c.last_index) return false;
+    // this round (so no ring read is needed after the first store) — or the
+    // remote is paused (Wait / Snapshot: sendReplicateMessage sends nothing,
+    // raft.go:758-765) and nothing from it arrives this round to unpause it
+    // (the majority side's leader of a partitioned group)
+    if (s == k || next[s] > c.last_index) continue;
+    const u32 rs = st[s] & 3u;
+    const bool paused = RBE_FAST_PAUSED && (rs == RS_Wait || rs == RS_Snapshot);
+    if (!paused || (pcin[s] & 0x3FFFu) != 0) return false;
   }
   FastQ q;
   q.tick = h.q_tick;

@@ -65,7 +65,7 @@ RBE_HD bool owned(const Params& C, u64 r) {
 // chunks per round, capturable in a graph.
 struct alignas(16) XHdr {
   u32 cnt[XS_NUM];  // records of each stream in this chunk (at most its capacity)
-  u32 overflow;     // the sender had more than fit: the round is lost, the run is invalid
+  u32 overflow;     // the sender had more than fit: the round takes a counted second pass
   u32 pad[12];
 };
 constexpr u64 kXHdrBytes = sizeof(XHdr);
@@ -78,8 +78,15 @@ RBE_HD u64 xchg_chunk_bytes(const u64* cap, u64 hdr) {
   for (u32 i = 0; i < XS_NUM; i++) per_peer += cap[i] * kXRecBytes[i];
   return per_peer;
 }
-RBE_HD u64 xchg_region(const u64* cap, u32 p, u32 t, u64 hdr = 0) {
-  u64 off = p * xchg_chunk_bytes(cap, hdr) + hdr;
+// The fixed layout's chunk of peer p in a buffer of rank `self`: every other
+// peer's chunk is full size, the rank's own holds only its header (no record
+// goes to oneself), so the all-to-all moves nothing it does not need
+RBE_HD u64 xchg_fixed_off(const u64* cap, u32 p, u32 self) {
+  const u64 cb = xchg_chunk_bytes(cap, kXHdrBytes);
+  return p * cb - (p > self ? cb - kXHdrBytes : 0);
+}
+RBE_HD u64 xchg_region(const u64* cap, u32 p, u32 t, u64 hdr = 0, u32 self = 0) {
+  u64 off = (hdr ? xchg_fixed_off(cap, p, self) : p * xchg_chunk_bytes(cap, 0)) + hdr;
   for (u32 i = 0; i < t; i++) off += cap[i] * kXRecBytes[i];
   return off;
 }
@@ -110,7 +117,7 @@ RBE_HD void xchg_sender(const Planes& P, const Params& C, u64 r, u32 par, u32 ro
       if (!WRITE) return nullptr;
       const u32 at = base[peer * XS_NUM + t] + i;
       if (at >= cap[t]) return nullptr;
-      return buf + xchg_region(cap, peer, t, hdr) + (u64)at * kXRecBytes[t];
+      return buf + xchg_region(cap, peer, t, hdr, C.rep_rank) + (u64)at * kXRecBytes[t];
     };
     if (!((sent_to >> peer) & 1u)) {
       sent_to |= 1u << peer;
@@ -194,10 +201,10 @@ RBE_HD void xchg_put_ent(const Planes& P, const Params& C, u32 par, const XEnt& 
 // the chunk's overflow flag
 RBE_HD bool xchg_put_fixed(const Planes& P, const Params& C, u32 par, const u8* recv,
                            const u64* cap, u32 p, u32 t, u64 i, u32* overflow) {
-  const XHdr* h = (const XHdr*)(recv + p * xchg_chunk_bytes(cap, kXHdrBytes));
+  const XHdr* h = (const XHdr*)(recv + xchg_fixed_off(cap, p, C.rep_rank));
   *overflow = h->overflow;
   if (i >= h->cnt[t]) return false;
-  const u8* rec = recv + xchg_region(cap, p, t, kXHdrBytes) + i * kXRecBytes[t];
+  const u8* rec = recv + xchg_region(cap, p, t, kXHdrBytes, C.rep_rank) + i * kXRecBytes[t];
   if (t == XS_CNT) xchg_put_cnt(P, C, par, *(const XCnt*)rec);
   else if (t == XS_MSG) xchg_put_msg(P, C, par, *(const XMsg*)rec);
   else xchg_put_ent(P, C, par, *(const XEnt*)rec);

@@ -100,11 +100,14 @@ class ReplicaExchange:
         return p * self._per_peer(self.ccaps) + sum(self.ccaps[i] * self.rec[i] for i in range(t))
 
     def _alloc(self):
-        """The fixed layout's send / receive chunks (fixed mode)."""
+        """The fixed layout's send / receive chunks (fixed mode): a full chunk
+        per peer, a header-only one for this rank itself (rbe_xchg.h
+        xchg_fixed_off), so the all-to-all moves nothing it does not need."""
         if not self.fixed:
             return
         per = self._per_peer() + XHDR_BYTES
-        self.buf = self.torch.empty(self.world * per, dtype=self.torch.uint8,
+        self.splits = [XHDR_BYTES if p == self.rank else per for p in range(self.world)]
+        self.buf = self.torch.empty(sum(self.splits), dtype=self.torch.uint8,
                                     device=self.buf_device)
         self.recv = self.torch.empty_like(self.buf, device=self.comm_device)
         self.recv_buf = self.recv if self.comm_device == self.buf_device else \
@@ -126,16 +129,18 @@ class ReplicaExchange:
         if self.buf_device.type == "cuda" and self.comm_device == self.buf_device:
             s = torch.cuda.ExternalStream(self.eng.stream_handle(), device=self.buf_device)
             with torch.cuda.stream(s):
-                dist.all_to_all_single(self.recv, self.buf, group=self.group)
+                dist.all_to_all_single(self.recv, self.buf, output_split_sizes=self.splits,
+                                       input_split_sizes=self.splits, group=self.group)
         else:  # gloo: staged through host memory
             if self.buf_device.type == "cuda":
                 self.eng.sync()
             send = self.buf if self.buf.device == self.comm_device else self.buf.to(self.comm_device)
-            dist.all_to_all_single(self.recv, send, group=self.group)
+            dist.all_to_all_single(self.recv, send, output_split_sizes=self.splits,
+                                   input_split_sizes=self.splits, group=self.group)
             if self.recv_buf is not self.recv:
                 self.recv_buf.copy_(self.recv)
                 torch.cuda.current_stream(self.buf_device).synchronize()
-        self.bytes_sent += self.buf.numel()
+        self.bytes_sent += self.buf.numel() - XHDR_BYTES  # (the own header stays local)
         self.eng.xchg_unpack_fixed(self.recv_buf.data_ptr(), self.caps)
         # one 4-byte read (rbe_xchg_status, read-and-clear): set on every rank
         # alike when any rank's records outgrew a chunk this round, because
@@ -184,7 +189,7 @@ class ReplicaExchange:
 
     def fixed_bytes_per_round(self) -> int:
         """Bytes one fixed-layout exchange moves from this rank (all peers)."""
-        return self.world * (self._per_peer() + XHDR_BYTES)
+        return (self.world - 1) * (self._per_peer() + XHDR_BYTES)
 
     def grow(self, counts: Sequence[int]):
         need = [max(counts[p * STREAMS + t] for p in range(self.world)) for t in range(STREAMS)]

@@ -747,8 +747,10 @@ int rbe_collect_step(rbe_engine* e, uint64_t first, uint64_t count, uint32_t fla
  *     the engine sized from the earlier rounds, _end collects that round again
  *     synchronously (and grows the buffer).
  * Between the two no step may run (rbe_step / rbe_run: _end then returns
- * RBE_E_STATE); rbe_push_* and the other host-side calls may.  The records are
- * valid until the next _begin or rbe_destroy. */
+ * RBE_E_STATE); rbe_push_* and the other host-side calls may.  The records
+ * live in one of two buffers used in turn: they stay valid through the next
+ * _begin / _end pair (so the node can read them while the device runs the next
+ * round) until the one after it, or rbe_destroy. */
 int rbe_collect_step_begin(rbe_engine* e, uint64_t first, uint64_t count, uint32_t flags);
 int rbe_collect_step_end(rbe_engine* e, rbe_step_outputs* out);
 int rbe_get_counters(rbe_engine* e, uint64_t* out /* RBE_CTR_NUM */);

@@ -9,6 +9,8 @@
 #   suite      the whole -m gpu suite
 #   bench      bench.py as the driver runs it (20 steps), then the default run
 #   prof       rocprofv3 kernel trace + stats of the default bench (C4 only)
+#   c4h        the host-driven round, pipelined and serial
+#   c5         the replica-per-GPU rehearsal (2 ranks on the one GPU, gloo), counted and fixed
 #   pmc        HBM traffic counters of the default bench (scripts/pmc_traffic.sh)
 set -e
 cd "$GRAFT_REPO_ROOT"
@@ -43,6 +45,22 @@ for step in "$@"; do
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/prof" \
         -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --also "" \
         > "$GRAFT_REPO_ROOT/$O/bench_prof.json" 2> "$GRAFT_REPO_ROOT/$O/bench_prof.err") ;;
+    c4h)
+      timeout -k 10 400 python -u bench.py --workload c4h --steps 50 --warmup 5 --no-cpu-baseline \
+        > "$O/bench_c4h.json" 2> "$O/bench_c4h.err"
+      timeout -k 10 400 python -u bench.py --workload c4h --steps 50 --warmup 5 --no-cpu-baseline \
+        --c4h-serial > "$O/bench_c4h_serial.json" 2> "$O/bench_c4h_serial.err"
+      python3 scripts/c4h_pair.py "$O/bench_c4h.json" "$O/bench_c4h_serial.json" ;;
+    c5)
+      # two ranks sharing the box's one GPU, the exchange staged through gloo
+      for mode in "" "--xchg-fixed"; do
+        tag=${mode:+_fixed}
+        timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+          --master-addr 127.0.0.1 --master-port 29533 bench.py --workload c5 --xchg-gloo $mode \
+          --groups ${C5_GROUPS:-100000} --steps 30 --warmup 5 --prof-rounds 10 \
+          > "$O/bench_c5$tag.json" 2> "$O/bench_c5$tag.err" || { tail -30 "$O/bench_c5$tag.err"; exit 1; }
+        python3 scripts/summarize_bench.py "$O/bench_c5$tag.json" "c5$tag"
+      done ;;
     pmc)
       timeout -k 10 600 bash scripts/pmc_traffic.sh ;;
     *)

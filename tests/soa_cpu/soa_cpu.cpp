@@ -980,7 +980,7 @@ static void soa_xchg_pack_fixed_t(SoaEngine* e, uint8_t* buf, const uint64_t* ca
       if (n > cap[t]) hd.overflow = 1;
     }
     if (hd.overflow) e->xflag = 1;
-    memcpy(buf + p * xchg_chunk_bytes(cap, kXHdrBytes), &hd, sizeof(hd));
+    memcpy(buf + xchg_fixed_off(cap, p, e->C.rep_rank), &hd, sizeof(hd));
   }
 }
 extern "C" void soa_xchg_pack_fixed(void* h, uint8_t* buf, const uint64_t* cap) {
