@@ -248,7 +248,9 @@ def load_traffic(name, kernel, lib):
     if d.get("library_sha256_16") != lib.get("sha256_16"):
         return None, (f"PMC summary measured on library {d.get('library_sha256_16')}, "
                       f"not this one ({lib.get('sha256_16')})")
-    return d.get("bytes_per_launch", {}).get(kernel), "same library"
+    x2 = d.get("bytes_per_launch_fetch_x2", {}).get(kernel)
+    return d.get("bytes_per_launch", {}).get(kernel), "same library" + (
+        f"; with the guide's FETCH_SIZE x 2: {x2:.0f} B" if x2 else "")
 
 
 def side_line(name, local, steps, prof_rounds):

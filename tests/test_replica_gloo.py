@@ -49,6 +49,19 @@ CASES = {
     "C3_iso_w4c": (dict(n_groups=22, n_replicas=3, check_quorum=True, wl_enabled=True,
                         wl_start_round=40, iso_period=50, iso_len=30, iso_mod=3), 4, 300,
                    dict(rep_compact=True)),
+    # tiny plane capacities (rbe_spill.h): lists past maxm and entries past ecap
+    # cross ranks as spill-heap records, each landing at the granule its
+    # sender chose in the sender rank's share of the heap (kXSpill)
+    "MIXED_tiny_w2": (dict(n_groups=12, n_replicas=5, check_quorum=True, quiesce=True,
+                           wl_enabled=True, wl_start_round=25, wl_active_mod=2,
+                           wl_read_permille=500, iso_period=37, iso_len=20, iso_mod=2,
+                           seed=12345), 2, 300,
+                      dict(maxm=1, ecap=1, rtr_cap=1, dri_cap=1, rq_cap=1, ring=8)),
+    "MIXED_tiny_w3": (dict(n_groups=12, n_replicas=5, check_quorum=True, quiesce=True,
+                           wl_enabled=True, wl_start_round=25, wl_active_mod=2,
+                           wl_read_permille=500, iso_period=37, iso_len=20, iso_mod=2,
+                           seed=12345), 3, 300,
+                      dict(maxm=2, ecap=2, rq_cap=4, ring=8)),
 }
 CHECK_EVERY = 50
 
@@ -186,7 +199,7 @@ def test_replica_fixed_exchange_matches_oracle(name):
     run_case(name, fixed=True)
 
 
-@pytest.mark.parametrize("name", ["C2_w2", "N5_w4"])
+@pytest.mark.parametrize("name", ["C2_w2", "N5_w4", "MIXED_tiny_w2"])
 def test_replica_fixed_exchange_overflow_repaired(name):
     """Fixed chunks far too small for the rounds: every round that outgrows
     them is repaired by a counted exchange of the same round (read-and-clear
