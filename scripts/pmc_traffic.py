@@ -45,7 +45,7 @@ def kernel_key(name):
     return None
 
 
-def per_kernel(d, counter):
+def per_kernel(d, counter, scale=1024.0):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     vals = defaultdict(list)
     for f in files:
@@ -59,12 +59,13 @@ def per_kernel(d, counter):
     for k, v in vals.items():
         v.sort()
         last = [x for _, x in v[-LAST:]]
-        out[k] = sum(last) / len(last) * 1024.0  # KiB -> bytes
+        out[k] = sum(last) / len(last) * scale  # KiB -> bytes (sizes)
     return out
 
 
 def main():
     w, fdir, wdir = sys.argv[1:4]
+    rdir = sys.argv[4] if len(sys.argv) > 4 else None
     fetch = per_kernel(fdir, "FETCH_SIZE")
     write = per_kernel(wdir, "WRITE_SIZE")
     import hashlib
@@ -76,6 +77,9 @@ def main():
            "library_sha256_16": sha, "fetch_raw": fetch, "write": write,
            "fetch_calibration": "scattered 16-B gathers: FETCH_SIZE x 1 (profiles/r05_calibration)",
            "bytes_per_launch": {}, "bytes_per_launch_fetch_x2": {}}
+    if rdir:  # request counts per launch (not bytes)
+        res["tcp_tcc_write_req"] = per_kernel(rdir, "TCP_TCC_WRITE_REQ_sum", 1.0)
+        res["tcp_tcc_read_req"] = per_kernel(rdir, "TCP_TCC_READ_REQ_sum", 1.0)
     for k in set(fetch) | set(write):
         res["bytes_per_launch"][k] = fetch.get(k, 0.0) + write.get(k, 0.0)
         res["bytes_per_launch_fetch_x2"][k] = 2.0 * fetch.get(k, 0.0) + write.get(k, 0.0)
