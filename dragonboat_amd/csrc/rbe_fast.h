@@ -249,6 +249,7 @@ struct FastOut {
     if (!ok) return;
     if (full) {  // the list moves to the spill heap at the step's end
       fault_if(!stash_put(P, C, par, ost(), m), F_NOMEM);
+      RBE_AUDIT(AS_STASH, nullptr, sizeof(Msg));
       return;
     }
     u32 slot;
@@ -261,6 +262,8 @@ struct FastOut {
     }
 #ifndef RBE_DIAG_NO_MSG_STORES
     P.msgs[par][((g * N + k) * N + d) * (u64)C.maxm + slot] = m;
+    RBE_AUDIT(AS_MSG, &P.msgs[par][((g * N + k) * N + d) * (u64)C.maxm + slot],
+              sizeof(Msg) | (u64)m.type << 32);
 #endif
   }
   template <class CT>
@@ -275,6 +278,7 @@ struct FastOut {
     x.low = low;
     x.high = high;
     P.dri[r * C.dri_cap + n_drop_ri] = x;
+    RBE_AUDIT(AS_DRI, &P.dri[r * C.dri_cap + n_drop_ri], sizeof(x));
     n_drop_ri++;
     if (TRACE) {
       drop_hash = hfold(drop_hash, low);
@@ -293,6 +297,7 @@ struct FastOut {
     x.low = low;
     x.high = high;
     P.rtr[r * C.rtr_cap + n_rtr] = x;
+    RBE_AUDIT(AS_RTR, &P.rtr[r * C.rtr_cap + n_rtr], sizeof(x));
     n_rtr++;
     if (TRACE) {
       rtr_hash = hfold(rtr_hash, index);
@@ -367,6 +372,7 @@ RBE_HD void fast_node_snapshot(const Planes& P, const Params& C, CT& ctr,
   const u64 S = C.snapshot_entries;
   if (!(la > S + sp->ss_index && la > S + sp->ss_req)) return;
   sp->ss_req = la;
+  RBE_AUDIT(AS_SNAP, &sp->ss_req, 8);
   u64 t = t_last;
   if (la != last) {
     const bool miss = last - la >= C.ring;
@@ -383,6 +389,7 @@ RBE_HD void fast_node_snapshot(const Planes& P, const Params& C, CT& ctr,
   sp->ss_wit = sp->sm_wit;
   const u64 ct = la > C.compaction_overhead ? la - C.compaction_overhead : 0;
   sp->compact_to = ct;
+  RBE_AUDIT(AS_SNAP, &sp->ss_index, 8 * 3 + 3);
   if (ct) flags |= HF_SNAP_WORK;
 }
 
@@ -515,7 +522,10 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, CT& ctr, FastOut<N, TR
 #ifndef RBE_DIAG_NO_STATE_STORES
   if (ranges) P.upd[r] = u;
   else __builtin_memcpy((char*)&P.upd[r] + 48, (const char*)&u + 48, 16);
+  RBE_AUDIT(ranges ? AS_UPD : AS_UPD3, (char*)&P.upd[r] + (ranges ? 0 : 48),
+            ranges ? sizeof(Upd) : 16);
   put_row(P, r, o.round_, N, ow);  // one 16-B store
+  RBE_AUDIT(AS_CNT, &P.cnt[o.round_ & 1u][r], sizeof(CntRow));
   h.flags = o.fault ? (u8)(flags | HF_FAULTED) : flags;
   h.election_tick = etick;
   h.heartbeat_tick = (u16)htick;
@@ -524,11 +534,15 @@ RBE_HD void fast_finish(const Planes& P, const Params& C, CT& ctr, FastOut<N, TR
   h.q_no_activity_since = q.nas;
   h.q_exit_quiesce_tick = q.eqt;
   P.hot[r] = h;
+  RBE_AUDIT(AS_HOT, &P.hot[r], sizeof(Hot));
 #pragma unroll
   for (u32 i = 0; i < 4; i++)
-    if (core_dirty & (1u << i))
+    if (core_dirty & (1u << i)) {
       __builtin_memcpy((char*)&P.core[r] + 16 * i, (const char*)&c + 16 * i, 16);
+      RBE_AUDIT(AS_CORE, (char*)&P.core[r] + 16 * i, 16);
+    }
   P.idle[r] = idle_byte(C, role, flags, q.qs);
+  RBE_AUDIT(AS_IDLE, &P.idle[r], 1);
 #endif
 }
 
@@ -725,7 +739,10 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
     rq_fr[i] = rq_w[i] & 0xFFu;
     rq_cf[i] = (rq_w[i] >> 8) & 0xFFu;
   }
-  bool rq_dirty = false;
+  // queue entries (register index i, i.e. slot rq_h + i) this step wrote: only
+  // those are stored back (a pop moves the head; the entries behind it keep
+  // their slots)
+  u32 rq_dm = 0;
   // eligibility of the inbox, then only the fields the handlers read stay live
   LeadIn inc[N - 1][Cap::MAXM];
   // With RBE_LDS_INBOX (N = 3 on the device) the kept fields move to LDS, one
@@ -826,7 +843,10 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   if (ev) {
     const u32 t0 = ev_cr.tail;
     ev_fault = cold_put(P, C, ev_cr, ev_idx, ev_e, par) ? 0u : F_NOMEM;
-    if (ev_cr.tail != t0) P.cold[r] = ev_cr;
+    if (ev_cr.tail != t0) {
+      P.cold[r] = ev_cr;
+      RBE_AUDIT(AS_COLD_REF, &P.cold[r], sizeof(ColdRef));
+    }
   }
 #endif
   FastOut<N, TRACE> o;
@@ -1007,8 +1027,8 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
         rq_cf[i] |= 1u << (from - 1u);
         conf = rq_cf[i];
         sindex = rq_ix[i];
+        rq_dm |= 1u << i;
       }
-    rq_dirty = true;
     ctr.v[C_RQ_TOUCH]++;
     if ((int)popc8(conf) + 1 < (int)Q) return;
     const u32 done = (u32)pos + 1;
@@ -1050,6 +1070,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
     rq_h += done;
     if (rq_h >= C.rq_cap) rq_h -= C.rq_cap;
     rq_n -= done;
+    rq_dm >>= done;
   };
   auto fan_out = [&]() {
 #pragma unroll
@@ -1179,8 +1200,8 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
               rq_fr[i] = 0;
               rq_cf[i] = 0;
             }
+          rq_dm |= 1u << rq_n;
           rq_n++;
-          rq_dirty = true;
           ctr.v[C_RQ_TOUCH]++;
         }
       }
@@ -1256,16 +1277,21 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
       if (!RBE_FAST_EV_EARLY && ev) {  // the entry the slot held, into the cold log
         const u32 t0 = ev_cr.tail;
         o.fault_if(!cold_put(P, C, ev_cr, ev_idx, ev_e, par), F_NOMEM);
-        if (ev_cr.tail != t0) P.cold[r] = ev_cr;
+        if (ev_cr.tail != t0) {
+      P.cold[r] = ev_cr;
+      RBE_AUDIT(AS_COLD_REF, &P.cold[r], sizeof(ColdRef));
+    }
       }
       const u64 sl = (idx & (u64)(C.ring - 1)) * C.n_rep + r;
       P.term_ring[sl] = c.term;
+      RBE_AUDIT(AS_TERM, &P.term_ring[sl], 8);
       Body b;
       b.type = xtype;
       b.len = xlen;
       b.lo = lo;
       b.hi = hi;
       P.pay_ring[sl] = b;
+      RBE_AUDIT(AS_PAY, &P.pay_ring[sl], sizeof(Body));
       ctr.v[C_RING_ACCESS]++;
       c.last_index = idx;
       c.t_last = c.term;
@@ -1289,6 +1315,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   if (xin) {  // the host input is consumed (Lane::run clears the record)
     ExtIn z{};
     P.ext[r] = z;
+    RBE_AUDIT(AS_EXT, &P.ext[r], sizeof(ExtIn));
   }
 #pragma unroll
   for (u32 s = 0; s < N; s++) {
@@ -1298,12 +1325,14 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
     if (rdirty & (1u << s)) {
       P.rem[r * N + s] = x;
       P.rem_st[r * N + s] = (u8)st[s];
+      RBE_AUDIT(AS_REM, &P.rem[r * N + s], sizeof(RemoteMN));
+      RBE_AUDIT(AS_REM_ST, &P.rem_st[r * N + s], 1);
     }
   }
-  if (rq_dirty) {
+  if (rq_dm) {
 #pragma unroll
     for (u32 i = 0; i < Cap::RQ; i++) {
-      if (i < rq_n) {
+      if (i < rq_n && ((rq_dm >> i) & 1u)) {
         ReadReq x;
         x.low = rq_lo[i];
         x.high = rq_hi[i];
@@ -1312,6 +1341,7 @@ RBE_HD bool lead_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
         x.confirmed = (u8)rq_cf[i];
         for (int j = 0; j < 6; j++) x.pad[j] = 0;
         P.rq[rq_slot(i)] = x;
+        RBE_AUDIT(AS_RQ, &P.rq[rq_slot(i)], sizeof(ReadReq));
       }
     }
   }
@@ -1549,7 +1579,10 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   if (ev_app) {  // the step's first store: the append's slot held entry ev_idx
     const u32 t0 = ev_cr.tail;
     ev_fault = cold_put(P, C, ev_cr, ev_idx, ev_e, par) ? 0u : F_NOMEM;
-    if (ev_cr.tail != t0) P.cold[r] = ev_cr;
+    if (ev_cr.tail != t0) {
+      P.cold[r] = ev_cr;
+      RBE_AUDIT(AS_COLD_REF, &P.cold[r], sizeof(ColdRef));
+    }
   }
 #endif
   FastOut<N, TRACE> o;
@@ -1597,7 +1630,10 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
   if (!RBE_FAST_EV_EARLY && ev_app) {  // the append's ring slot held entry ev_idx: into the cold log
     const u32 t0 = ev_cr.tail;
     o.fault_if(!cold_put(P, C, ev_cr, ev_idx, ev_e, par), F_NOMEM);
-    if (ev_cr.tail != t0) P.cold[r] = ev_cr;
+    if (ev_cr.tail != t0) {
+      P.cold[r] = ev_cr;
+      RBE_AUDIT(AS_COLD_REF, &P.cold[r], sizeof(ColdRef));
+    }
   }
 #pragma unroll
   for (u32 s = 0; s < N; s++) {
@@ -1652,12 +1688,14 @@ RBE_HD bool foll_fast(const Planes& P, const Params& C, u64 r, const Clk& ck, CT
                 const u64 ai = m.log_index + 1 + e;
                 const u64 sl = (ai & (u64)(C.ring - 1)) * C.n_rep + r;
                 P.term_ring[sl] = x.term;
+                RBE_AUDIT(AS_TERM, &P.term_ring[sl], 8);
                 Body b;
                 b.type = x.type;
                 b.len = x.len;
                 b.lo = x.lo;
                 b.hi = x.hi;
                 P.pay_ring[sl] = b;
+                RBE_AUDIT(AS_PAY, &P.pay_ring[sl], sizeof(Body));
                 ctr.v[C_RING_ACCESS]++;
                 tl = x.term;
               }

@@ -174,6 +174,7 @@ RBE_HD bool cold_put(const PL& P, const PA& C, ColdRef& cr, u64 idx, const Ent& 
     m.prev = cr.tail;
     m.next = 0;
     P.pmeta[p] = m;
+    RBE_AUDIT(AS_COLD_META, &P.pmeta[p], sizeof(PoolMeta) + (cr.tail ? 4 : 0));
     if (cr.tail) P.pmeta[cr.tail].next = p;
     else cr.head = p;
     cr.tail = p;
@@ -197,6 +198,7 @@ RBE_HD bool cold_put(const PL& P, const PA& C, ColdRef& cr, u64 idx, const Ent& 
     }
   }
   *pool_ent(P, p, (u32)(idx % kPageEnts)) = e;
+  RBE_AUDIT(AS_COLD_ENT, pool_ent(P, p, (u32)(idx % kPageEnts)), sizeof(Ent));
   return true;
 }
 // Releases every page whose entries all lie at or below `upto` (LogDB.Compact

@@ -480,4 +480,30 @@ struct Planes {
   SpillCtl* sctl;     // [1]
 };
 
+// Store audit of the fast step (scripts/store_audit.py): a host
+// build of the step (tests/soa_cpu) with -DRBE_STORE_AUDIT counts every global
+// store a fast step makes, per site, while g_audit_on is set (bytes in the low
+// 32 bits of `bytes`; a message store puts its type above them).  Expands to
+// nothing in the device build and in every default build.
+enum : u32 {
+  AS_MSG, AS_DRI, AS_RTR, AS_SNAP, AS_UPD, AS_UPD3, AS_CNT, AS_HOT, AS_CORE, AS_IDLE,
+  AS_COLD_REF, AS_COLD_ENT, AS_COLD_META, AS_TERM, AS_PAY, AS_EXT, AS_REM, AS_REM_ST, AS_RQ,
+  AS_STASH, AS_NUM
+};
+#if defined(RBE_STORE_AUDIT) && !defined(__HIP_DEVICE_COMPILE__)
+extern bool g_audit_on;
+extern u64 g_store_audit[AS_NUM][2];
+void audit_store(u32 site, const void* at, u64 bytes);  // address trace (tests/soa_cpu)
+#define RBE_AUDIT(site, at, bytes)                                    \
+  do {                                                                \
+    if (::rbe::g_audit_on) {                                          \
+      ::rbe::g_store_audit[site][0]++;                                \
+      ::rbe::g_store_audit[site][1] += (::rbe::u64)(bytes)&0xFFFFFFFFu; \
+      ::rbe::audit_store(site, at, bytes);                            \
+    }                                                                 \
+  } while (0)
+#else
+#define RBE_AUDIT(site, at, bytes) ((void)0)
+#endif
+
 }  // namespace rbe

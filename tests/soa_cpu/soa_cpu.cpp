@@ -19,6 +19,49 @@
 
 using namespace rbe;
 
+#ifdef RBE_STORE_AUDIT
+namespace rbe {
+bool g_audit_on = false;
+u64 g_store_audit[AS_NUM][2];
+}  // namespace rbe
+static u64 g_audit_steps, g_audit_leads, g_audit_declined;
+// address trace: (item, site, address, bytes) per store while tracing, the
+// item being the step's position in the round's fast list (leaders first)
+static bool g_audit_tracing;
+static u64 g_audit_item;
+static std::vector<u64> g_audit_trace;
+namespace rbe {
+void audit_store(u32 site, const void* at, u64 bytes) {
+  if (!g_audit_tracing) return;
+  const u64 rec[4] = {g_audit_item, site, (u64)(uintptr_t)at, bytes};
+  g_audit_trace.insert(g_audit_trace.end(), rec, rec + 4);
+}
+}  // namespace rbe
+extern "C" void soa_audit_trace(int on) {
+  g_audit_tracing = on != 0;
+  if (on) g_audit_trace.clear();
+}
+extern "C" uint64_t soa_audit_trace_get(uint64_t* out, uint64_t max_recs) {
+  const u64 n = g_audit_trace.size() / 4;
+  if (out) memcpy(out, g_audit_trace.data(), 32 * (n < max_recs ? n : max_recs));
+  return n;
+}
+// out: AS_NUM (count, bytes) pairs, then fast steps, leader steps, declines
+extern "C" void soa_store_audit(uint64_t* out, int reset) {
+  for (u32 i = 0; i < AS_NUM; i++) {
+    out[2 * i] = g_store_audit[i][0];
+    out[2 * i + 1] = g_store_audit[i][1];
+  }
+  out[2 * AS_NUM] = g_audit_steps;
+  out[2 * AS_NUM + 1] = g_audit_leads;
+  out[2 * AS_NUM + 2] = g_audit_declined;
+  if (reset) {
+    for (u32 i = 0; i < AS_NUM; i++) g_store_audit[i][0] = g_store_audit[i][1] = 0;
+    g_audit_steps = g_audit_leads = g_audit_declined = 0;
+  }
+}
+#endif
+
 struct SoaEngine {
   Params C;
   Planes P;
@@ -139,6 +182,14 @@ static void run_round(SoaEngine* e, bool tick = true) {
       if (tr == GS_WAKE) e->P.gwake[g] = GW_AWAKE;
     }
   }
+#ifdef RBE_STORE_AUDIT
+  g_audit_on = true;
+  g_audit_steps += lists[0].size() + lists[1].size();
+  g_audit_leads += lists[0].size();
+#endif
+#ifdef RBE_STORE_AUDIT
+  g_audit_item = 0;
+#endif
   for (int li = 0; li < 2; li++) {
     for (u64 r : lists[li]) {
       memset(&c, 0, sizeof(c));
@@ -165,8 +216,15 @@ static void run_round(SoaEngine* e, bool tick = true) {
       }
       if (!ok) lists[2].push_back(r);
       for (int i = 0; i < C_NUM; i++) e->counters[i] += c.v[i];
+#ifdef RBE_STORE_AUDIT
+      g_audit_item++;
+#endif
     }
   }
+#ifdef RBE_STORE_AUDIT
+  g_audit_on = false;
+  g_audit_declined += lists[2].size();
+#endif
   std::vector<u64>& slow = lists[2];
   for (u64 r : slow) {
     memset(&c, 0, sizeof(c));
