@@ -149,6 +149,11 @@ def main():
           f" {tot['requests'] / max(steps * scale, 1):9.2f}")
     print("messages/launch by type:", res["messages_by_type"])
     if meas:
+        if meas.get("tcp_tcc_write_req"):
+            meas["model_over_measured_requests"] = tot["requests"] / meas["tcp_tcc_write_req"]
+            meas["algorithmic_over_write_size"] = tot["bytes"] / meas["write_bytes"]
+            with open(a.out, "w") as f:
+                json.dump(res, f, indent=1)
         print("measured:", meas)
 
 
