@@ -100,7 +100,10 @@ for k in ROUND:
 rf = (plain or b)["roofline"]
 lines += ["", "The bench's split times each kernel by a start / stop event pair its own dispatch "
           "stamps (hipExtLaunchKernel, rbe_profile_rounds); under rocprofv3 every dispatch is "
-          "slower, so the run without the profiler is the one the roofline below uses."]
+          "slower, so the run without the profiler is the one the roofline below uses.",
+          "", "A kernel whose rounds carry no item (C4's `k_full_list`: the full list is empty "
+          "in the steady state) is one dispatch of a few µs; its ratio measures the profiler's "
+          "per-dispatch cost (~1 µs), not work."]
 lines += ["", f"Roofline (dominant kernel `{rf['kernel']}`): {rf['alg_bytes_per_launch']:.0f} B "
           f"algorithmic per launch / {rf['avg_launch_us']:.2f} µs = {rf['achieved']:.0f} GB/s, "
           f"frac {rf['frac']:.4f} of {rf['peak']:.0f} GB/s; ms_per_step {(plain or b)['ms_per_step']:.4f}.",
