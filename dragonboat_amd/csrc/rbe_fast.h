@@ -87,9 +87,12 @@ RBE_HD void rbe_wait_all_loads() {
 #endif
 template <int N>
 constexpr int kFastWaves = RBE_FAST_WAVES;
+#ifndef RBE_FAST_MAXM_WIDE  // leader inbound messages per follower, N >= 4
+#define RBE_FAST_MAXM_WIDE 5
+#endif
 template <int N>
 struct FastCaps {
-  static constexpr u32 MAXM = N <= 3 ? 4 : 5;  // leader: inbound messages per follower
+  static constexpr u32 MAXM = N <= 3 ? 4 : RBE_FAST_MAXM_WIDE;  // leader: inbound messages per follower
   static constexpr u32 FMAXM = 6;              // follower: from its leader
   static constexpr u32 RQ = 3;                 // readIndex queue entries in registers
 };
