@@ -492,7 +492,11 @@ __global__ __launch_bounds__(kBlock) void k_triage(Planes P, Params C, RoundArg 
       base = __shfl(base, first, 64);
       if (want) pos = base + __popcll(mask & ((1ull << lane) - 1ull));
     }
-    (i < 4 ? sp_lo : sp_hi) |= (u64)(code | (pos << 3)) << (14 * (i % 4));
+    // (values selected, never a reference to one of the two words: a selected
+    // reference in this rolled loop puts both in scratch memory)
+    const u64 spv = (u64)(code | (pos << 3)) << (14 * (i % 4));
+    sp_lo |= i < 4 ? spv : 0ull;
+    sp_hi |= i < 4 ? 0ull : spv;
   }
   __syncthreads();
   const u32 sh = blockIdx.x % kShards;

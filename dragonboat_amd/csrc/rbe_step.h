@@ -299,8 +299,15 @@ RBE_HD u32 idle_role(u8 ib) { return (ib >> IB_ROLE_SHIFT) & 7u; }
 RBE_HD u32 cnt_widx(u32 d, u32 k) { return d < 6u ? d : k; }
 // the count word of destination slot d in sender slot k's row, read in `round`
 // (none to itself: in a group of 7 that index holds slot 6's word)
+// (the word is shifted out of the row's two 64-bit halves: indexing CntRow::w
+// with a run-time index puts the row in scratch memory, a store and two loads)
 RBE_HD u32 row_word(const CntRow& row, u32 d, u32 k, u32 round) {
-  return row.stamp == round && d != k ? (u32)row.w[cnt_widx(d, k)] : 0u;
+  u64 lo, hi;
+  __builtin_memcpy(&lo, &row, 8);
+  __builtin_memcpy(&hi, (const char*)&row + 8, 8);
+  const u32 i = cnt_widx(d, k);  // w[i] at byte 4 + 2i
+  const u64 x = i < 2u ? lo >> (32u + 16u * i) : hi >> (16u * (i - 2u));
+  return (u32)lo == round && d != k ? (u32)(x & 0xFFFFu) : 0u;
 }
 template <int N>
 RBE_HD u32 in_word(const Planes& P, u64 g, u32 s, u32 d, u32 round) {
